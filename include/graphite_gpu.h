@@ -1,0 +1,246 @@
+/*
+ * graphite_gpu.h — C ABI of the MI355X batch backend for Graphite's
+ * memory-subsystem hot path (private L1-D/L2 cache simulation and EMesh NoC
+ * packet latency).
+ *
+ * This is the drop-in boundary.  Every entry point below replaces one
+ * in-process C++ interface of the reference simulator (paths relative to
+ * nmtrmail/Graphite):
+ *
+ *   gg_cache_access_batch      batched Cache line access: the per-access state
+ *                              machine L1CacheCntlr::processMemOpFromCore
+ *                              (common/tile/memory_subsystem/
+ *                              pr_l1_pr_l2_dram_directory_msi/l1_cache_cntlr.cc:89-180)
+ *                              + L2CacheCntlr (l2_cache_cntlr.cc:74-527) driving
+ *                              Cache::accessCacheLine / insertCacheLine /
+ *                              getCacheLineInfo / setCacheLineInfo
+ *                              (common/tile/memory_subsystem/cache/cache.h:87-92),
+ *                              i.e. the "accessSingleLine" entry of the north star
+ *                              applied to a whole trace batch.
+ *   gg_cache_access_line       Cache::accessCacheLine            (cache.cc:84-112)
+ *   gg_cache_insert_line       Cache::insertCacheLine            (cache.cc:114-184)
+ *   gg_cache_get_line_info     Cache::getCacheLineInfo           (cache.cc:187-205)
+ *   gg_cache_set_line_info     Cache::setCacheLineInfo           (cache.cc:218-241)
+ *   gg_cache_get_counters      the counters printed by Cache::outputSummary
+ *                              (cache.cc:419-477)
+ *   gg_noc_route_batch         NetworkModel::__routePacket -> routePacket
+ *                              (common/network/network_model.cc:87-116,
+ *                              network_model.h:188) for every hop of each packet,
+ *                              plus NetworkModel::__processReceivedPacket
+ *                              (network_model.cc:118-150) at the receiver:
+ *                              emesh_hop_counter (models/network_model_emesh_hop_counter.cc:143-157)
+ *                              and emesh_hop_by_hop (models/network_model_emesh_hop_by_hop.cc:146-264)
+ *   gg_noc_get_counters        NetworkModel / RouterModel counters
+ *                              (network_model.cc:228-316, router_model.cc:120-145)
+ *   gg_queue_delay_batch       QueueModelHistoryTree::computeQueueDelay
+ *                              (common/shared_models/queue_models/queue_model_history_tree.cc:44-126)
+ *
+ * Conventions: every function returns a gg_status (0 = OK, negative = error);
+ * no exception crosses the ABI; pointers named *_dev are HIP device pointers,
+ * all others are host pointers owned by the caller; one host thread per
+ * context, one context per GPU.  The reference reports misuse with
+ * LOG_ASSERT_ERROR (aborting, common/misc/log.h:112-135); this ABI returns
+ * GG_ERR_* instead and records a message retrievable with gg_last_error().
+ */
+#ifndef GRAPHITE_GPU_H
+#define GRAPHITE_GPU_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GG_ABI_VERSION 1
+
+typedef int gg_status;
+enum {
+  GG_OK = 0,
+  GG_ERR_INVALID = -1,      /* bad argument / inconsistent config            */
+  GG_ERR_HIP = -2,          /* HIP runtime error                             */
+  GG_ERR_UNSUPPORTED = -3,  /* configuration outside what the backend builds */
+  GG_ERR_RANGE = -4,        /* address / time outside the encodable range    */
+  GG_ERR_STATE = -5         /* reference would LOG_ASSERT_ERROR here          */
+};
+
+/* Replacement policies: CacheReplacementPolicy::parse (cache_replacement_policy.cc:33-46) */
+enum { GG_POLICY_LRU = 0, GG_POLICY_ROUND_ROBIN = 1 };
+
+/* Network models: NetworkModel::parseNetworkType (network_model.cc:318-335) */
+enum { GG_NET_MAGIC = 0, GG_NET_EMESH_HOP_COUNTER = 1, GG_NET_EMESH_HOP_BY_HOP = 2 };
+
+/* Cache levels (pr_l1_pr_l2_dram_directory_msi/cache_level.h) */
+enum { GG_L1D = 0, GG_L2 = 1 };
+
+/* Cache line states, numerically identical to CacheState::Type (cache_state.h:11-21) */
+enum { GG_CSTATE_INVALID = 0, GG_CSTATE_SHARED = 1, GG_CSTATE_MODIFIED = 4 };
+
+/* Cached-location values of a private L2 line, MemComponent::Type subset
+ * (PrL2CacheLineInfo::_cached_loc, pr_l1_pr_l2_dram_directory_msi/cache_line_info.h) */
+enum { GG_LOC_INVALID = 0, GG_LOC_L1I = 2, GG_LOC_L1D = 3 };
+
+/* Access trace record metadata word (gg_trace.meta[i]):
+ *   bit 0      : 1 = WRITE (Core::WRITE), 0 = READ (Core::READ)
+ *   bits 1..30 : gap in core cycles before this access (coherent/timing modes;
+ *                ignored by the private-cache mode)
+ *   bit 31     : reserved, must be 0                                           */
+#define GG_META_WRITE 1u
+
+/* Per-access result word written by gg_cache_access_batch.                    */
+#define GG_RES_LEVEL_MASK      0x3u  /* where the access was served:            */
+#define GG_RES_L1_HIT          0x0u  /*   L1-D (operationPermissibleinL1Cache)  */
+#define GG_RES_L2_HIT          0x1u  /*   L2 hit (processShmemRequestFromL1Cache) */
+#define GG_RES_DIRECTORY       0x2u  /*   L2 miss -> SH_REQ/EX_REQ to the home  */
+#define GG_RES_UPGRADE         (1u << 2) /* WRITE to a SHARED L2 line: INV_REP + EX_REQ (l2:260-282) */
+#define GG_RES_L1_EVICT        (1u << 3) /* the L1-D insert evicted a line      */
+#define GG_RES_L2_EVICT        (1u << 4) /* the L2 insert evicted a line (l2:74-116) */
+#define GG_RES_L2_EVICT_DIRTY  (1u << 5) /* ... in MODIFIED: FLUSH_REP + data (else INV_REP) */
+#define GG_RES_L2_EVICT_INV_L1 (1u << 6) /* ... and invalidated its copy in L1-D */
+
+/* Cache counters, one vector per (tile, level).  Index = what Cache::outputSummary prints. */
+enum {
+  GG_CC_ACCESSES = 0, GG_CC_MISSES, GG_CC_READ_ACCESSES, GG_CC_READ_MISSES,
+  GG_CC_WRITE_ACCESSES, GG_CC_WRITE_MISSES, GG_CC_EVICTIONS, GG_CC_DIRTY_EVICTIONS,
+  GG_CC_TAG_READS, GG_CC_TAG_WRITES, GG_CC_DATA_READS, GG_CC_DATA_WRITES,
+  GG_NUM_CACHE_COUNTERS
+};
+
+/* Network counters per tile (NetworkModel::outputSummary + model event counters). */
+enum {
+  GG_NC_PACKETS_SENT = 0, GG_NC_FLITS_SENT, GG_NC_BITS_SENT,
+  GG_NC_PACKETS_RECEIVED, GG_NC_FLITS_RECEIVED, GG_NC_BITS_RECEIVED,
+  GG_NC_TOTAL_LATENCY_PS, GG_NC_TOTAL_CONTENTION_PS,
+  /* emesh_hop_counter: updateEventCounters (network_model_emesh_hop_counter.cc:120-127)
+   * emesh_hop_by_hop : mesh RouterModel event counters + link traversals    */
+  GG_NC_BUFFER_WRITES, GG_NC_BUFFER_READS, GG_NC_SWITCH_ALLOC, GG_NC_CROSSBAR,
+  GG_NC_LINK_TRAVERSALS,
+  GG_NC_ROUTER_CONTENTION_CYCLES, GG_NC_ROUTER_PACKETS, GG_NC_ANALYTICAL_REQUESTS,
+  GG_NUM_NET_COUNTERS
+};
+
+typedef struct gg_config {
+  uint32_t num_tiles;          /* application tiles (general/total_cores)          */
+  uint32_t line_size;          /* bytes, l1_dcache/T1/cache_line_size (64)          */
+  uint32_t l1d_size_kb;        /* l1_dcache/T1/cache_size (32)                      */
+  uint32_t l1d_assoc;          /* l1_dcache/T1/associativity (4)                    */
+  uint32_t l1d_policy;         /* GG_POLICY_*                                        */
+  uint32_t l2_size_kb;         /* l2_cache/T1/cache_size (512)                      */
+  uint32_t l2_assoc;           /* l2_cache/T1/associativity (8)                     */
+  uint32_t l2_policy;
+  uint32_t net_model;          /* GG_NET_* for network/memory                        */
+  uint32_t flit_width;         /* bits (64)                                          */
+  uint32_t router_delay;       /* cycles (1)                                         */
+  uint32_t link_delay;         /* cycles (1)                                         */
+  uint32_t queue_model_enabled;/* network/emesh_hop_by_hop/queue_model/enabled       */
+  uint32_t max_list_size;      /* queue_model/history_tree/max_list_size (100)      */
+  uint32_t analytical_enabled; /* queue_model/history_tree/analytical_model_enabled */
+  uint32_t total_tiles;        /* app tiles + MCP + spawners (config.cc:77-82); 0 = num_tiles+2 */
+  double   frequency_ghz;      /* single DVFS domain (carbon_sim.cfg:147-155)        */
+  int32_t  device;             /* HIP device ordinal                                 */
+  uint32_t reserved[7];
+} gg_config;
+
+/* Fill cfg with the reference defaults of carbon_sim.cfg for num_tiles tiles. */
+void gg_config_default(gg_config* cfg, uint32_t num_tiles);
+
+/* A batch of line accesses in tile-major program order (structure of arrays).
+ * Records of tile t are [tile_offsets[t], tile_offsets[t+1]).  addr[i] is the
+ * byte address of the accessed line (the low log2(line_size) bits are ignored,
+ * as Cache::getTag does, cache.cc:495-498).  Addresses must be < 2^48.        */
+typedef struct gg_trace {
+  const uint64_t* addr_dev;
+  const uint32_t* meta_dev;
+  const uint64_t* tile_offsets;   /* host, num_tiles + 1 entries */
+  uint64_t        num_records;
+} gg_trace;
+
+/* A batch of NoC packets.  Packet k: sender/receiver tile ids, modeled length
+ * in bits (NetworkModel::getModeledLength, network_model.cc:185-200) and its
+ * send time in picoseconds (NetPacket::time).                                 */
+typedef struct gg_packets {
+  const uint32_t* src_dev;
+  const uint32_t* dst_dev;
+  const uint32_t* length_bits_dev;
+  const uint64_t* time_ps_dev;
+  uint64_t        num_packets;
+} gg_packets;
+
+/* Per-packet result: time the packet is handed to the receiving tile
+ * (after serialization, network_model.cc:142-150) and the zero-load /
+ * contention split (Hop, network_model.cc:556-563).                            */
+typedef struct gg_packet_out {
+  uint64_t* arrival_ps_dev;
+  uint64_t* zero_load_ps_dev;
+  uint64_t* contention_ps_dev;
+} gg_packet_out;
+
+typedef struct gg_line_info {    /* CacheLineInfo / PrL2CacheLineInfo            */
+  uint64_t tag;                  /* line address (addr >> log2 line); ~0 = invalid */
+  uint32_t cstate;               /* GG_CSTATE_*                                   */
+  uint32_t cached_loc;           /* GG_LOC_* (L2 only)                            */
+} gg_line_info;
+
+typedef struct gg_ctx gg_ctx;
+
+int         gg_abi_version(void);
+const char* gg_last_error(void);
+
+/* Create a context on cfg->device: allocates the device-resident cache state of
+ * every tile (reset to the constructor state: all lines invalid, LRU ages =
+ * way index, lru_replacement_policy.cc:5-18) and the NoC router state.        */
+gg_ctx*   gg_create(const gg_config* cfg, gg_status* status);
+void      gg_destroy(gg_ctx* ctx);
+gg_status gg_reset(gg_ctx* ctx);
+
+/* Private (decoupled) cache replay of a trace batch, continuing from the
+ * context's cache state.  result_dev: one word per record (GG_RES_*), may be
+ * NULL.  evicted_dev: L2-evicted line byte address per record or ~0, may be
+ * NULL.  Asynchronous on stream (hipStream_t, NULL = default).  Counters
+ * accumulate in the context (gg_cache_get_counters).                          */
+gg_status gg_cache_access_batch(gg_ctx* ctx, const gg_trace* trace,
+                                uint32_t* result_dev, uint64_t* evicted_dev,
+                                void* stream);
+
+/* Counters: out has num_tiles * 2 * GG_NUM_CACHE_COUNTERS entries laid out
+ * [tile][level][counter].  Synchronizes the context's stream.                */
+gg_status gg_cache_get_counters(gg_ctx* ctx, uint64_t* out);
+
+/* The Cache quartet on one tile's device-resident cache (slow path, one line
+ * per call; used by the host mirror classes and the parity tests).           */
+gg_status gg_cache_get_line_info(gg_ctx* ctx, uint32_t tile, int level,
+                                 uint64_t addr, gg_line_info* out);
+gg_status gg_cache_set_line_info(gg_ctx* ctx, uint32_t tile, int level,
+                                 uint64_t addr, const gg_line_info* in);
+gg_status gg_cache_access_line(gg_ctx* ctx, uint32_t tile, int level,
+                               uint64_t addr, int is_store);
+gg_status gg_cache_insert_line(gg_ctx* ctx, uint32_t tile, int level,
+                               uint64_t addr, const gg_line_info* in,
+                               int* eviction, uint64_t* evicted_addr,
+                               gg_line_info* evicted_info);
+
+/* NoC: route every packet of the batch through the configured EMesh model in
+ * the canonical discrete-event order, continuing from the
+ * context's router queue state.  Asynchronous on stream.                      */
+gg_status gg_noc_route_batch(gg_ctx* ctx, const gg_packets* pk,
+                             const gg_packet_out* out, void* stream);
+/* out: num_tiles * GG_NUM_NET_COUNTERS, [tile][counter].                      */
+gg_status gg_noc_get_counters(gg_ctx* ctx, uint64_t* out);
+
+/* Stand-alone QueueModelHistoryTree(min_processing_time) over a sequence of
+ * (pkt_time, processing_time) requests; writes the queue delays.  Host
+ * pointers; used by the known-answer test (tests/unit/history_tree).         */
+gg_status gg_queue_delay_batch(gg_ctx* ctx, uint64_t min_processing_time,
+                               const uint64_t* pkt_time, const uint64_t* proc_time,
+                               uint64_t n, uint64_t* delay_out);
+
+/* Device time (ms) of the most recent launch of a named kernel
+ * ("cache_replay", "cache_shard", "noc_hop_counter", ...), measured with HIP
+ * events on the stream the kernel ran on; negative if not launched.           */
+float     gg_kernel_time_ms(gg_ctx* ctx, const char* kernel);
+void      gg_set_timing(gg_ctx* ctx, int enabled);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,951 @@
+/*
+ * gg_oracle.c — plain-C restatement of Graphite's memory-subsystem hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see gg_oracle.h).  The shipped backend
+ * (graphite_amd/) never links or calls this file; it is the checker for the
+ * HIP kernels and the CPU baseline timed by bench.py.
+ *
+ * Citations are path:line in the reference (nmtrmail/Graphite).
+ * Compile with -ffp-contract=off: the double/float arithmetic below must
+ * round exactly like the reference's (time_types.h:81-109,
+ * queue_model_m_g_1.cc:18-56).
+ */
+#include "gg_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ======================================================================== */
+/* misc/utils.cc:18-34                                                       */
+/* ======================================================================== */
+static int floor_log2(uint32_t n) { int p = -1; while (n) { n >>= 1; ++p; } return p; }
+static int ceil_log2(uint32_t n) { int p = floor_log2(n); return ((1u << p) == n) ? p : p + 1; }
+
+/* misc/time_types.h:81-109 */
+static uint64_t lat_to_ps(uint64_t cycles, double f) { return (uint64_t)ceil(((double)1000 * cycles) / (double)f); }
+static uint64_t time_to_cycles(uint64_t ps, double f) { return (uint64_t)ceil(((double)ps * (double)f) / (double)1.0e3); }
+
+/* ======================================================================== */
+/* Synthetic workloads        */
+/* ======================================================================== */
+static uint64_t mix64(uint64_t z)
+{
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+uint64_t oracle_splitmix64_at(uint64_t seed, uint64_t i)
+{
+  return mix64(seed + (i + 1) * 0x9E3779B97F4A7C15ull);
+}
+
+void oracle_gen_uniform(uint32_t tile, uint64_t first, uint64_t n, uint32_t lines_log2,
+                        uint32_t base_shift, uint64_t* addr, uint32_t* meta)
+{
+  const uint64_t seed = 0x9E3779B97F4A7C15ull ^ (uint64_t)tile;
+  const uint64_t mask = (1ull << lines_log2) - 1;
+  for (uint64_t k = 0; k < n; ++k) {
+    uint64_t z = oracle_splitmix64_at(seed, first + k);
+    addr[k] = ((uint64_t)tile << base_shift) + ((z & mask) << 6);
+    meta[k] = (((z >> 32) % 3) == 0) ? GG_META_WRITE : 0u;
+  }
+}
+
+/* Core::initiateMemoryAccess line split (common/tile/core/core.cc:167-201) */
+uint32_t oracle_split_lines(uint64_t addr, uint32_t size, uint32_t line, uint64_t* lines, uint32_t cap)
+{
+  if (size == 0) return 0;                          /* core.cc:145-155 */
+  uint64_t begin = addr, end = addr + size;
+  uint64_t ba = begin - (begin % line), ea = end - (end % line);
+  uint32_t cnt = 0;
+  for (uint64_t a = ba; a <= ea; a += line) {
+    uint32_t off = (a == ba) ? (uint32_t)(begin % line) : 0;
+    uint32_t sz;
+    if (a == ea) { sz = (uint32_t)(end % line) - off; if (sz == 0) continue; }
+    else sz = line - off;
+    (void)sz;
+    if (cnt < cap) lines[cnt] = a;
+    ++cnt;
+  }
+  return cnt;
+}
+
+/* ======================================================================== */
+/* Cache (common/tile/memory_subsystem/cache/)                               */
+/* ======================================================================== */
+#define O_INVALID_TAG (~0ull)                        /* cache_line_info.h:21-22 */
+enum { CS_I = GG_CSTATE_INVALID, CS_S = GG_CSTATE_SHARED, CS_M = GG_CSTATE_MODIFIED };
+
+typedef struct { uint64_t tag; uint32_t cstate; uint32_t loc; } o_line;
+
+typedef struct {
+  uint32_t sets, ways, log_line, policy, write_back;
+  o_line*   lines;     /* [sets][ways]   CacheSet::_cache_line_info_array     */
+  uint8_t*  lru;       /* [sets][ways]   LRUReplacementPolicy::_lru_bits_vec  */
+  uint32_t* rr;        /* [sets]         RoundRobin::_replacement_index_vec   */
+  uint64_t  c[GG_NUM_CACHE_COUNTERS];
+} o_cache;
+
+static void o_cache_init(o_cache* c, uint32_t size_kb, uint32_t assoc, uint32_t line,
+                         uint32_t policy, uint32_t write_back)
+{
+  memset(c, 0, sizeof(*c));
+  c->sets = size_kb * 1024u / (assoc * line);       /* cache.cc:44, cache_hash_fn.h:11 */
+  c->ways = assoc;
+  c->log_line = (uint32_t)floor_log2(line);
+  c->policy = policy;
+  c->write_back = write_back;
+  c->lines = (o_line*)malloc(sizeof(o_line) * c->sets * c->ways);
+  c->lru = (uint8_t*)malloc((size_t)c->sets * c->ways);
+  c->rr = (uint32_t*)malloc(sizeof(uint32_t) * c->sets);
+  for (uint32_t s = 0; s < c->sets; ++s) {
+    for (uint32_t w = 0; w < c->ways; ++w) {
+      o_line* l = &c->lines[(size_t)s * c->ways + w];
+      l->tag = O_INVALID_TAG; l->cstate = CS_I; l->loc = GG_LOC_INVALID;
+      c->lru[(size_t)s * c->ways + w] = (uint8_t)w;  /* lru_replacement_policy.cc:5-18 */
+    }
+    c->rr[s] = c->ways - 1;                         /* round_robin_replacement_policy.cc:4-9 */
+  }
+}
+
+static void o_cache_free(o_cache* c) { free(c->lines); free(c->lru); free(c->rr); }
+
+/* cache_hash_fn.h:17-18 and Cache::getTag (cache.cc:495-498) */
+static uint32_t o_set(const o_cache* c, uint64_t addr) { return (uint32_t)((addr >> c->log_line) & (c->sets - 1)); }
+static uint64_t o_tag(const o_cache* c, uint64_t addr) { return addr >> c->log_line; }
+
+/* CacheSet::find — scans ways from high to low (cache_set.cc:57-70) */
+static int o_find(const o_cache* c, uint32_t set, uint64_t tag)
+{
+  for (int w = (int)c->ways - 1; w >= 0; --w)
+    if (c->lines[(size_t)set * c->ways + w].tag == tag) return w;
+  return -1;
+}
+
+/* LRUReplacementPolicy::update (lru_replacement_policy.cc:40-50); RR update is a no-op */
+static void o_policy_update(o_cache* c, uint32_t set, uint32_t way)
+{
+  if (c->policy != GG_POLICY_LRU) return;
+  uint8_t* b = &c->lru[(size_t)set * c->ways];
+  uint8_t acc = b[way];
+  for (uint32_t i = 0; i < c->ways; ++i) if (b[i] < acc) b[i]++;
+  b[way] = 0;
+}
+
+/* getReplacementWay: LRU (lru_replacement_policy.cc:23-38), RR (round_robin_replacement_policy.cc:13-22) */
+static int o_victim(o_cache* c, uint32_t set)
+{
+  if (c->policy == GG_POLICY_LRU) {
+    const uint8_t* b = &c->lru[(size_t)set * c->ways];
+    uint32_t way = c->ways;
+    for (uint32_t i = 0; i < c->ways; ++i) {
+      if (c->lines[(size_t)set * c->ways + i].tag == O_INVALID_TAG) return (int)i;
+      else if (b[i] == c->ways - 1) way = i;
+    }
+    return (way < c->ways) ? (int)way : -1;          /* LOG_ASSERT_ERROR "Error Finding LRU bits" */
+  }
+  uint32_t cur = c->rr[set];
+  c->rr[set] = (c->rr[set] == 0) ? (c->ways - 1) : (c->rr[set] - 1);
+  return (int)cur;
+}
+
+/* Cache::updateMissCounters (cache.cc:321-360); track_miss_types=false (carbon_sim.cfg:228,239) */
+static void o_update_miss_counters(o_cache* c, int is_write, int miss)
+{
+  c->c[GG_CC_ACCESSES]++;
+  if (!is_write) c->c[GG_CC_READ_ACCESSES]++; else c->c[GG_CC_WRITE_ACCESSES]++;
+  if (miss) {
+    c->c[GG_CC_MISSES]++;
+    if (!is_write) c->c[GG_CC_READ_MISSES]++; else c->c[GG_CC_WRITE_MISSES]++;
+  }
+}
+
+/* Cache::accessCacheLine (cache.cc:84-112): find (must hit), read/write_line -> policy update */
+static int o_access_line(o_cache* c, uint64_t addr, int is_store)
+{
+  uint32_t s = o_set(c, addr);
+  int w = o_find(c, s, o_tag(c, addr));
+  if (w < 0) return GG_ERR_STATE;                    /* LOG_ASSERT_ERROR(cache_line_info) */
+  o_policy_update(c, s, (uint32_t)w);                /* cache_set.cc:31-55 */
+  c->c[is_store ? GG_CC_DATA_WRITES : GG_CC_DATA_READS]++;
+  return 0;
+}
+
+/* Cache::insertCacheLine (cache.cc:114-184) + CacheSet::insert (cache_set.cc:72-103) */
+static int o_insert_line(o_cache* c, uint64_t addr, const o_line* in, int* eviction,
+                         uint64_t* evicted_addr, o_line* evicted)
+{
+  uint32_t s = o_set(c, addr);
+  int w = o_victim(c, s);
+  if (w < 0 || (uint32_t)w >= c->ways) return GG_ERR_STATE;
+  o_line* l = &c->lines[(size_t)s * c->ways + w];
+  if (l->tag != O_INVALID_TAG) { *eviction = 1; *evicted = *l; }
+  else *eviction = 0;                                /* evicted keeps the caller's default */
+  *l = *in;
+  o_policy_update(c, s, (uint32_t)w);
+  *evicted_addr = evicted->tag << c->log_line;       /* getAddressFromTag (cache.cc:514-518) */
+  if (*eviction) {
+    c->c[GG_CC_TAG_READS]++; c->c[GG_CC_DATA_READS]++;
+    c->c[GG_CC_EVICTIONS]++;
+    if (c->write_back && (evicted->cstate == CS_M))  /* CacheState::dirty(): M/O/DIRTY */
+      c->c[GG_CC_DIRTY_EVICTIONS]++;
+  } else {
+    c->c[GG_CC_TAG_READS]++;
+  }
+  c->c[GG_CC_TAG_WRITES]++; c->c[GG_CC_DATA_WRITES]++;
+  return 0;
+}
+
+/* Cache::getCacheLineInfo (cache.cc:187-215): out keeps the caller's default when absent */
+static void o_get_line_info(o_cache* c, uint64_t addr, o_line* out)
+{
+  uint32_t s = o_set(c, addr);
+  int w = o_find(c, s, o_tag(c, addr));
+  if (w >= 0) *out = c->lines[(size_t)s * c->ways + w];
+  c->c[GG_CC_TAG_READS]++;
+}
+
+/* Cache::setCacheLineInfo (cache.cc:218-241) */
+static int o_set_line_info(o_cache* c, uint64_t addr, const o_line* in)
+{
+  uint32_t s = o_set(c, addr);
+  int w = o_find(c, s, o_tag(c, addr));
+  if (w < 0) return GG_ERR_STATE;
+  c->lines[(size_t)s * c->ways + w] = *in;
+  c->c[GG_CC_TAG_WRITES]++;
+  return 0;
+}
+
+static o_line o_default_line(void) { o_line l = { O_INVALID_TAG, CS_I, GG_LOC_INVALID }; return l; }
+static int cs_readable(uint32_t s) { return s == CS_M || s == 3 || s == 2 || s == CS_S; } /* cache_state.h:26-29 */
+static int cs_writable(uint32_t s) { return s == CS_M || s == 3; }                         /* cache_state.h:30-33 */
+
+/* ======================================================================== */
+/* pr_l1_pr_l2_dram_directory_msi controllers, private (decoupled) mode      */
+/* ======================================================================== */
+typedef struct { o_cache l1, l2; } o_tile;
+
+struct oracle_cache { gg_config cfg; uint32_t ntiles; o_tile* t; };
+
+oracle_cache* oracle_cache_create(const gg_config* cfg)
+{
+  oracle_cache* oc = (oracle_cache*)calloc(1, sizeof(*oc));
+  oc->cfg = *cfg;
+  oc->ntiles = cfg->num_tiles;
+  oc->t = (o_tile*)calloc(cfg->num_tiles, sizeof(o_tile));
+  for (uint32_t i = 0; i < cfg->num_tiles; ++i) {
+    /* L1-D is WRITE_THROUGH (l1_cache_cntlr.cc:55-71), L2 WRITE_BACK (l2_cache_cntlr.cc:31-46) */
+    o_cache_init(&oc->t[i].l1, cfg->l1d_size_kb, cfg->l1d_assoc, cfg->line_size, cfg->l1d_policy, 0);
+    o_cache_init(&oc->t[i].l2, cfg->l2_size_kb, cfg->l2_assoc, cfg->line_size, cfg->l2_policy, 1);
+  }
+  return oc;
+}
+
+void oracle_cache_destroy(oracle_cache* oc)
+{
+  if (!oc) return;
+  for (uint32_t i = 0; i < oc->ntiles; ++i) { o_cache_free(&oc->t[i].l1); o_cache_free(&oc->t[i].l2); }
+  free(oc->t); free(oc);
+}
+
+/* L1CacheCntlr::invalidateCacheLine (l1_cache_cntlr.cc:293-305); returns 1 if a valid line was invalidated */
+static int l1_invalidate(o_tile* T, uint64_t addr, int* err)
+{
+  o_line info = o_default_line();
+  o_get_line_info(&T->l1, addr, &info);
+  if (info.tag != O_INVALID_TAG) {
+    info.tag = O_INVALID_TAG; info.cstate = CS_I;     /* CacheLineInfo::invalidate (cache_line_info.cc:39-43) */
+    if (o_set_line_info(&T->l1, addr, &info)) *err = 1;
+    return 1;
+  }
+  return 0;
+}
+
+/* L1CacheCntlr::accessCache (l1_cache_cntlr.cc:182-205) incl. the write-through to L2 */
+static void l1_access_cache(o_tile* T, uint64_t addr, int is_write, int* err)
+{
+  if (o_access_line(&T->l1, addr, is_write)) *err = 1;
+  if (is_write && o_access_line(&T->l2, addr, 1)) *err = 1;   /* L2CacheCntlr::writeCacheLine (l2:66-70) */
+}
+
+/* L2CacheCntlr::insertCacheLineInL1 (l2_cache_cntlr.cc:133-165) */
+static void l2_insert_in_l1(o_tile* T, uint64_t addr, uint32_t cstate, uint32_t* res, int* err)
+{
+  o_line in = { o_tag(&T->l1, addr), cstate, GG_LOC_INVALID };   /* l1_cache_cntlr.cc:245-261 */
+  o_line ev = o_default_line();
+  int eviction = 0; uint64_t ev_addr = 0;
+  if (o_insert_line(&T->l1, addr, &in, &eviction, &ev_addr, &ev)) { *err = 1; return; }
+  if (eviction) {
+    *res |= GG_RES_L1_EVICT;
+    o_line l2i = o_default_line();
+    o_get_line_info(&T->l2, ev_addr, &l2i);
+    if (l2i.loc != GG_LOC_L1D) { *err = 1; return; }  /* LOG_ASSERT_ERROR: mem_component is L1-D */
+    l2i.loc = GG_LOC_INVALID;                          /* clearCachedLoc */
+    if (o_set_line_info(&T->l2, ev_addr, &l2i)) *err = 1;
+  }
+}
+
+/* L2CacheCntlr::insertCacheLine (l2_cache_cntlr.cc:74-116) */
+static void l2_insert(o_tile* T, uint64_t addr, uint32_t cstate, uint32_t* res, uint64_t* evicted_out, int* err)
+{
+  o_line in = { o_tag(&T->l2, addr), cstate, GG_LOC_L1D };
+  o_line ev = o_default_line();
+  int eviction = 0; uint64_t ev_addr = 0;
+  if (o_insert_line(&T->l2, addr, &in, &eviction, &ev_addr, &ev)) { *err = 1; return; }
+  if (eviction) {
+    *res |= GG_RES_L2_EVICT;
+    *evicted_out = ev_addr;
+    if (ev.loc != GG_LOC_INVALID)                      /* invalidateCacheLineInL1 (l2:124-131) */
+      if (l1_invalidate(T, ev_addr, err)) *res |= GG_RES_L2_EVICT_INV_L1;
+    if (ev.cstate == CS_M) *res |= GG_RES_L2_EVICT_DIRTY;       /* FLUSH_REP + data */
+    else if (ev.cstate != CS_S) *err = 1;                        /* LOG_ASSERT_ERROR(SHARED) -> INV_REP */
+  }
+}
+
+/*
+ * One line access of tile T in private mode: L1CacheCntlr::processMemOpFromCore
+ * (l1_cache_cntlr.cc:89-180) with the directory granting every request
+ * (DramDirectoryCntlr::processEx/ShReqFromL2Cache on an UNCACHED entry,
+ * dram_directory_cntlr.cc:238-380: EX_REQ -> EX_REP/MODIFIED, SH_REQ -> SH_REP/SHARED).
+ */
+static uint32_t modep_access(o_tile* T, uint64_t addr, int is_write, uint64_t* evicted_out, int* err)
+{
+  uint32_t res = 0;
+  *evicted_out = ~0ull;
+  for (int access_num = 1; access_num <= 2; ++access_num) {
+    /* operationPermissibleinL1Cache (l1:207-243) */
+    o_line info = o_default_line();
+    o_get_line_info(&T->l1, addr, &info);
+    int hit = is_write ? cs_writable(info.cstate) : cs_readable(info.cstate);
+    if (access_num == 1) o_update_miss_counters(&T->l1, is_write, !hit);
+    if (hit) { l1_access_cache(T, addr, is_write, err); return res; }
+    if (access_num == 2) { *err = 1; return res; }   /* LOG_ASSERT_ERROR(access_num == 1 || 2) */
+
+    l1_invalidate(T, addr, err);                       /* l1:135-137 */
+
+    /* L2CacheCntlr::processShmemRequestFromL1Cache (l2:180-224) */
+    o_line l2i = o_default_line();
+    o_get_line_info(&T->l2, addr, &l2i);
+    uint32_t cstate = l2i.cstate;
+    int l2hit = is_write ? cs_writable(cstate) : cs_readable(cstate);  /* l2:504-527 */
+    o_update_miss_counters(&T->l2, is_write, !l2hit);
+    if (l2hit) {
+      res |= GG_RES_L2_HIT;
+      if (o_access_line(&T->l2, addr, 0)) *err = 1;   /* readCacheLine */
+      l2_insert_in_l1(T, addr, cstate, &res, err);
+      l2i.loc = GG_LOC_L1D;                          /* setCachedLoc / setForcedCachedLoc */
+      if (o_set_line_info(&T->l2, addr, &l2i)) *err = 1;
+      l1_access_cache(T, addr, is_write, err);       /* l1:145-159 */
+      return res;
+    }
+
+    /* L2 miss: handleMsgFromL1Cache (l2:226-258) */
+    res |= GG_RES_DIRECTORY;
+    uint32_t new_state;
+    if (is_write) {                                  /* processExReqFromL1Cache (l2:260-282) */
+      o_line x = o_default_line();
+      o_get_line_info(&T->l2, addr, &x);
+      if (x.cstate == CS_S) {
+        x.tag = O_INVALID_TAG; x.cstate = CS_I; x.loc = GG_LOC_INVALID;  /* PrL2CacheLineInfo::invalidate */
+        if (o_set_line_info(&T->l2, addr, &x)) *err = 1;
+        res |= GG_RES_UPGRADE;                       /* INV_REP then EX_REQ to the home */
+      } else if (x.cstate != CS_I) *err = 1;
+      new_state = CS_M;                              /* EX_REP */
+    } else {
+      new_state = CS_S;                              /* processShReqFromL1Cache -> SH_REP */
+    }
+    /* insertCacheLineInHierarchy (l2:167-178) */
+    l2_insert(T, addr, new_state, &res, evicted_out, err);
+    l2_insert_in_l1(T, addr, new_state, &res, err);
+  }
+  return res;
+}
+
+int oracle_cache_run(oracle_cache* oc, const uint64_t* addr, const uint32_t* meta,
+                     const uint64_t* tile_offsets, uint32_t tile_begin, uint32_t tile_end,
+                     uint32_t* result, uint64_t* evicted)
+{
+  int err = 0;
+  const uint64_t line_mask = ~((uint64_t)oc->cfg.line_size - 1);
+  for (uint32_t t = tile_begin; t < tile_end && t < oc->ntiles; ++t) {
+    o_tile* T = &oc->t[t];
+    for (uint64_t i = tile_offsets[t]; i < tile_offsets[t + 1]; ++i) {
+      uint64_t ev = ~0ull;
+      uint32_t r = modep_access(T, addr[i] & line_mask, (int)(meta[i] & GG_META_WRITE), &ev, &err);
+      if (result) result[i] = r;
+      if (evicted) evicted[i] = ev;
+    }
+  }
+  return err ? GG_ERR_STATE : 0;
+}
+
+void oracle_cache_counters(const oracle_cache* oc, uint64_t* out)
+{
+  for (uint32_t t = 0; t < oc->ntiles; ++t) {
+    memcpy(out + ((size_t)t * 2 + 0) * GG_NUM_CACHE_COUNTERS, oc->t[t].l1.c, sizeof(uint64_t) * GG_NUM_CACHE_COUNTERS);
+    memcpy(out + ((size_t)t * 2 + 1) * GG_NUM_CACHE_COUNTERS, oc->t[t].l2.c, sizeof(uint64_t) * GG_NUM_CACHE_COUNTERS);
+  }
+}
+
+static o_cache* oc_level(oracle_cache* oc, uint32_t tile, int level)
+{
+  if (tile >= oc->ntiles) return NULL;
+  return level == GG_L1D ? &oc->t[tile].l1 : &oc->t[tile].l2;
+}
+
+int oracle_cache_get_line_info(oracle_cache* oc, uint32_t tile, int level, uint64_t addr, gg_line_info* out)
+{
+  o_cache* c = oc_level(oc, tile, level);
+  if (!c) return GG_ERR_INVALID;
+  o_line l = { out->tag, out->cstate, out->cached_loc };
+  o_get_line_info(c, addr, &l);
+  out->tag = l.tag; out->cstate = l.cstate; out->cached_loc = l.loc;
+  return 0;
+}
+
+int oracle_cache_set_line_info(oracle_cache* oc, uint32_t tile, int level, uint64_t addr, const gg_line_info* in)
+{
+  o_cache* c = oc_level(oc, tile, level);
+  if (!c) return GG_ERR_INVALID;
+  o_line l = { in->tag, in->cstate, level == GG_L2 ? in->cached_loc : GG_LOC_INVALID };
+  return o_set_line_info(c, addr, &l);
+}
+
+int oracle_cache_access_line(oracle_cache* oc, uint32_t tile, int level, uint64_t addr, int is_store)
+{
+  o_cache* c = oc_level(oc, tile, level);
+  if (!c) return GG_ERR_INVALID;
+  return o_access_line(c, addr, is_store);
+}
+
+int oracle_cache_insert_line(oracle_cache* oc, uint32_t tile, int level, uint64_t addr,
+                             const gg_line_info* in, int* eviction, uint64_t* evicted_addr,
+                             gg_line_info* evicted_info)
+{
+  o_cache* c = oc_level(oc, tile, level);
+  if (!c) return GG_ERR_INVALID;
+  o_line l = { in->tag, in->cstate, level == GG_L2 ? in->cached_loc : GG_LOC_INVALID };
+  o_line ev = { evicted_info->tag, evicted_info->cstate, evicted_info->cached_loc };
+  int rc = o_insert_line(c, addr, &l, eviction, evicted_addr, &ev);
+  evicted_info->tag = ev.tag; evicted_info->cstate = ev.cstate; evicted_info->cached_loc = ev.loc;
+  return rc;
+}
+
+/* ======================================================================== */
+/* IntervalTree (common/misc/interval_tree.cc:40-394)                        */
+/* ======================================================================== */
+typedef struct {
+  int parent, left, right;     /* node indices, -1 = NULL */
+  int32_t height;
+  uint64_t key, first, second; /* key == interval.first always */
+} it_node;
+
+typedef struct { it_node* n; int root; uint32_t size; } itree;
+
+static int32_t it_h(const itree* t, int x) { return x < 0 ? 0 : t->n[x].height; }
+
+/* updateChildPointer (interval_tree.cc:45-72): dir 0 = INVALID (by key), 1 = LEFT, 2 = RIGHT */
+static void it_upd_child(itree* t, int node, int child, int dir)
+{
+  if (node < 0) return;
+  if (dir == 0) {
+    if (t->n[node].key < t->n[child].key) t->n[node].right = child; else t->n[node].left = child;
+  } else if (dir == 1) t->n[node].left = child;
+  else t->n[node].right = child;
+}
+
+/* updateParentPointer (interval_tree.cc:74-81) */
+static void it_upd_parent(itree* t, int node, int parent)
+{
+  if (node >= 0) t->n[node].parent = parent;
+  if (parent < 0) t->root = node;
+}
+
+static int it_balanced(const itree* t, int x) { return abs(it_h(t, t->n[x].left) - it_h(t, t->n[x].right)) <= 1; }
+static void it_upd_height(itree* t, int x)
+{
+  int32_t a = it_h(t, t->n[x].left), b = it_h(t, t->n[x].right);
+  t->n[x].height = (a > b ? a : b) + 1;
+}
+
+/* performRotation (interval_tree.cc:103-140): cw = CLOCKWISE */
+static void it_rotate(itree* t, int y, int cw)
+{
+  int x;
+  if (cw) {
+    x = t->n[y].left;
+    it_upd_parent(t, x, t->n[y].parent);
+    it_upd_child(t, t->n[x].parent, x, 0);
+    t->n[y].left = t->n[x].right;
+    it_upd_parent(t, t->n[y].left, y);
+    t->n[x].right = y;
+    it_upd_parent(t, y, x);
+  } else {
+    x = t->n[y].right;
+    it_upd_parent(t, x, t->n[y].parent);
+    it_upd_child(t, t->n[x].parent, x, 0);
+    t->n[y].right = t->n[x].left;
+    it_upd_parent(t, t->n[y].right, y);
+    t->n[x].left = y;
+    it_upd_parent(t, y, x);
+  }
+  it_upd_height(t, y);
+  it_upd_height(t, x);
+}
+
+/* balanceHeight (interval_tree.cc:142-197) */
+static int it_balance(itree* t, int z)
+{
+  int zl = t->n[z].left, zr = t->n[z].right;
+  int y_left = it_h(t, zl) > it_h(t, zr);
+  int y = y_left ? zl : zr;
+  int yl = t->n[y].left, yr = t->n[y].right;
+  int x, x_left;
+  if (it_h(t, yl) != it_h(t, yr)) { x_left = it_h(t, yl) > it_h(t, yr); x = x_left ? yl : yr; }
+  else if (y_left) { x = yl; x_left = 1; }
+  else { x = yr; x_left = 0; }
+  if (y_left) {
+    if (!x_left) { it_rotate(t, y, 0); it_rotate(t, z, 1); return x; }
+    it_rotate(t, z, 1); return y;
+  } else {
+    if (x_left) { it_rotate(t, y, 1); it_rotate(t, z, 0); return x; }
+    it_rotate(t, z, 0); return y;
+  }
+}
+
+/* rebalanceAVLTree (interval_tree.cc:199-229) */
+static void it_rebalance(itree* t, int r)
+{
+  while (r >= 0) {
+    int32_t old = t->n[r].height;
+    int nr = r;
+    if (!it_balanced(t, r)) nr = it_balance(t, r);
+    else it_upd_height(t, r);
+    if (t->n[nr].height == old) return;
+    r = t->n[nr].parent;
+  }
+}
+
+/* insert / insertInTree (interval_tree.cc:250-290) */
+static int it_insert(itree* t, int node)
+{
+  t->size++;
+  int r = t->root;
+  for (;;) {
+    if (t->n[node].key < t->n[r].key) {
+      if (t->n[r].left >= 0) r = t->n[r].left;
+      else { t->n[r].left = node; t->n[node].parent = r; it_rebalance(t, r); return 0; }
+    } else if (t->n[node].key > t->n[r].key) {
+      if (t->n[r].right >= 0) r = t->n[r].right;
+      else { t->n[r].right = node; t->n[node].parent = r; it_rebalance(t, r); return 0; }
+    } else return GG_ERR_STATE;                   /* "Found 2 nodes with same key" */
+  }
+}
+
+/* findMinKeyNode (interval_tree.cc:241-248) */
+static int it_min(const itree* t, int r) { while (t->n[r].left >= 0) r = t->n[r].left; return r; }
+
+/* removeFromTree (interval_tree.cc:300-340): returns the node slot to release */
+static int it_remove_rec(itree* t, int node)
+{
+  it_node* n = &t->n[node];
+  if (n->left < 0) {
+    if (n->parent >= 0)
+      it_upd_child(t, n->parent, n->right, (t->n[n->parent].key < n->key) ? 2 : 1);
+    it_upd_parent(t, n->right, n->parent);
+    it_rebalance(t, n->parent);
+    return node;
+  } else if (n->right < 0) {
+    it_upd_child(t, n->parent, n->left, 0);
+    it_upd_parent(t, n->left, n->parent);
+    it_rebalance(t, n->parent);
+    return node;
+  } else {
+    int succ = it_min(t, n->right);
+    it_remove_rec(t, succ);
+    /* swap key/interval of node and successor (interval_tree.cc:231-239) */
+    it_node tmp = t->n[node];
+    t->n[node].key = t->n[succ].key; t->n[node].first = t->n[succ].first; t->n[node].second = t->n[succ].second;
+    t->n[succ].key = tmp.key; t->n[succ].first = tmp.first; t->n[succ].second = tmp.second;
+    return succ;
+  }
+}
+static int it_remove(itree* t, int node) { t->size--; return it_remove_rec(t, node); }
+
+/* searchTree (interval_tree.cc:349-377) */
+static int it_search(const itree* t, uint64_t a, uint64_t b, int r)
+{
+  while (r >= 0) {
+    const it_node* n = &t->n[r];
+    if (a >= n->first && b <= n->second) return r;
+    if (b < n->first) {
+      int f = it_search(t, a, b, n->left);
+      if (f >= 0) return f;
+    }
+    if (a < n->first && (n->second - n->first) >= (b - a)) return r;
+    r = n->right;
+  }
+  return -1;
+}
+
+/* ======================================================================== */
+/* QueueModelMG1 (shared_models/queue_models/queue_model_m_g_1.cc:18-56)     */
+/* ======================================================================== */
+typedef struct { double sig_sq, sig; uint64_t n, newest; } mg1;
+
+static double sq(double x) { return x * x; }
+static uint64_t mg1_delay(const mg1* m)
+{
+  if (m->n == 0) return 0;
+  double variance = (m->sig_sq / m->n) - sq(m->sig / m->n);
+  double service_rate = 1.0 / (m->sig / m->n);
+  double arrival_rate = ((double)m->n) / m->newest;
+  if (arrival_rate >= service_rate) arrival_rate = 0.999 * service_rate;
+  return (uint64_t)ceil(0.5 * service_rate * arrival_rate * ((1 / sq(service_rate)) + variance) /
+                        (service_rate - arrival_rate));
+}
+static void mg1_update(mg1* m, uint64_t t, uint64_t s, uint64_t w)
+{
+  m->sig_sq += sq((double)s);
+  m->sig += s;
+  m->n++;
+  uint64_t x = t + w + s;
+  m->newest = (m->newest > x) ? m->newest : x;
+}
+
+/* ======================================================================== */
+/* QueueModelHistoryTree (queue_model_history_tree.cc:14-167)                */
+/* ======================================================================== */
+struct oracle_htree {
+  uint64_t min_proc;
+  int max_size, analytical;
+  itree t;
+  int* free_list; int free_tail;                  /* allocateMemory (:129-137) */
+  mg1 m;
+  uint64_t analytical_requests;
+  uint64_t util_cycles, last_req, total_req;      /* queue_model.cc:41-55 */
+};
+
+static int ht_alloc(oracle_htree* h, uint64_t a, uint64_t b)    /* allocateNode (:146-157) */
+{
+  if (h->free_tail < 0) return -1;
+  int idx = h->free_list[h->free_tail--];
+  it_node* n = &h->t.n[idx];
+  n->parent = n->left = n->right = -1; n->height = 1; n->key = a; n->first = a; n->second = b;
+  return idx;
+}
+static void ht_release(oracle_htree* h, int idx) { h->free_list[++h->free_tail] = idx; } /* :159-167 */
+
+oracle_htree* oracle_htree_create(uint64_t min_proc, int max_list_size, int analytical)
+{
+  oracle_htree* h = (oracle_htree*)calloc(1, sizeof(*h));
+  h->min_proc = min_proc; h->max_size = max_list_size; h->analytical = analytical;
+  h->t.n = (it_node*)calloc((size_t)max_list_size, sizeof(it_node));
+  h->free_list = (int*)malloc(sizeof(int) * (size_t)max_list_size);
+  for (int i = 0; i < max_list_size; ++i) h->free_list[i] = i;
+  h->free_tail = max_list_size - 1;
+  h->t.root = ht_alloc(h, 0, UINT64_MAX);         /* PAIR(0, UINT64_MAX) (:30) */
+  h->t.size = 1;
+  return h;
+}
+
+void oracle_htree_destroy(oracle_htree* h) { if (h) { free(h->t.n); free(h->free_list); free(h); } }
+uint64_t oracle_htree_analytical_requests(const oracle_htree* h) { return h->analytical_requests; }
+uint32_t oracle_htree_size(const oracle_htree* h) { return h->t.size; }
+
+/* computeQueueDelay (queue_model_history_tree.cc:44-126) */
+uint64_t oracle_htree_delay(oracle_htree* h, uint64_t t, uint64_t p)
+{
+  uint64_t qd = UINT64_MAX;
+  itree* T = &h->t;
+  int min_node = it_search(T, 0, 1, T->root);
+  if (T->size >= (uint32_t)h->max_size) ht_release(h, it_remove(T, min_node));
+  min_node = it_search(T, 0, 1, T->root);
+  if (h->analytical && (T->n[min_node].first > (t + p))) {
+    h->analytical_requests++;
+    qd = mg1_delay(&h->m);
+  } else {
+    int node = it_search(T, t, t + p, T->root);
+    if (node < 0) return UINT64_MAX;              /* LOG_PRINT_ERROR("node = (NULL)") */
+    it_node* n = &T->n[node];
+    if (t >= n->first) {
+      qd = 0;
+      if ((t - n->first) >= h->min_proc) {
+        if ((n->second - (t + p)) >= h->min_proc) {
+          int nx = ht_alloc(h, t + p, n->second);
+          it_insert(T, nx);
+          n = &T->n[node];
+        }
+        n->second = t;
+      } else {
+        if ((n->second - (t + p)) >= h->min_proc) { n->first = t + p; n->key = n->first; }
+        else ht_release(h, it_remove(T, node));
+      }
+    } else {
+      qd = n->first - t;
+      if ((n->second - (n->first + p)) >= h->min_proc) { n->first = n->first + p; n->key = n->first; }
+      else ht_release(h, it_remove(T, node));
+    }
+  }
+  mg1_update(&h->m, t, p, qd);
+  h->util_cycles += p;                            /* updateQueueUtilizationCounters */
+  if (t + qd + p > h->last_req) h->last_req = t + qd + p;
+  h->total_req++;
+  return qd;
+}
+
+/* ======================================================================== */
+/* NoC: NetworkModel + emesh_hop_counter + emesh_hop_by_hop                  */
+/* ======================================================================== */
+enum { P_SELF = 0, P_LEFT, P_RIGHT, P_DOWN, P_UP, NPORTS };   /* network_model_emesh_hop_by_hop.h:41-48 */
+
+struct oracle_noc {
+  gg_config cfg;
+  uint32_t n, w, h, id_bits;
+  oracle_htree** inj;      /* [tile]            _injection_router queue (1 port)   */
+  oracle_htree** q;        /* [tile][NPORTS]    _mesh_router output-port queues     */
+  uint64_t* c;             /* [tile][GG_NUM_NET_COUNTERS]                           */
+};
+
+oracle_noc* oracle_noc_create(const gg_config* cfg)
+{
+  oracle_noc* on = (oracle_noc*)calloc(1, sizeof(*on));
+  on->cfg = *cfg;
+  on->n = cfg->num_tiles;
+  on->w = (uint32_t)floor(sqrt((double)cfg->num_tiles));        /* hop_counter.cc:18-19 */
+  on->h = (uint32_t)ceil(1.0 * cfg->num_tiles / on->w);
+  on->id_bits = (uint32_t)ceil_log2(cfg->num_tiles);            /* config.cc:149-152 */
+  on->c = (uint64_t*)calloc((size_t)on->n * GG_NUM_NET_COUNTERS, sizeof(uint64_t));
+  if (cfg->net_model == GG_NET_EMESH_HOP_BY_HOP && cfg->queue_model_enabled) {
+    on->inj = (oracle_htree**)calloc(on->n, sizeof(void*));
+    on->q = (oracle_htree**)calloc((size_t)on->n * NPORTS, sizeof(void*));
+    for (uint32_t i = 0; i < on->n; ++i) {
+      on->inj[i] = oracle_htree_create(1, (int)cfg->max_list_size, (int)cfg->analytical_enabled);
+      for (int p = 0; p < NPORTS; ++p)       /* QueueModel::create(type, 1) (router_model.cc:23-27) */
+        on->q[(size_t)i * NPORTS + p] = oracle_htree_create(1, (int)cfg->max_list_size, (int)cfg->analytical_enabled);
+    }
+  }
+  return on;
+}
+
+void oracle_noc_destroy(oracle_noc* on)
+{
+  if (!on) return;
+  if (on->inj) {
+    for (uint32_t i = 0; i < on->n; ++i) {
+      oracle_htree_destroy(on->inj[i]);
+      for (int p = 0; p < NPORTS; ++p) oracle_htree_destroy(on->q[(size_t)i * NPORTS + p]);
+    }
+    free(on->inj); free(on->q);
+  }
+  free(on->c); free(on);
+}
+
+void oracle_noc_counters(const oracle_noc* on, uint64_t* out)
+{
+  memcpy(out, on->c, sizeof(uint64_t) * on->n * GG_NUM_NET_COUNTERS);
+  if (on->q) {
+    for (uint32_t i = 0; i < on->n; ++i) {
+      uint64_t a = 0;
+      for (int p = 0; p < NPORTS; ++p) a += on->q[(size_t)i * NPORTS + p]->analytical_requests;
+      out[(size_t)i * GG_NUM_NET_COUNTERS + GG_NC_ANALYTICAL_REQUESTS] = a;
+    }
+  }
+}
+
+/* NetworkModel::computeNumFlits (network_model.cc:202-212) */
+static uint64_t n_flits(const oracle_noc* on, uint32_t bits)
+{
+  uint32_t fw = on->cfg.flit_width;
+  return (bits % fw == 0) ? bits / fw : bits / fw + 1;
+}
+
+static uint64_t* ncnt(oracle_noc* on, uint32_t tile) { return on->c + (size_t)tile * GG_NUM_NET_COUNTERS; }
+
+/* updateSendCounters (network_model.cc:228-251) */
+static void n_send_counters(oracle_noc* on, uint32_t src, uint32_t bits)
+{
+  uint64_t* c = ncnt(on, src);
+  c[GG_NC_PACKETS_SENT]++; c[GG_NC_FLITS_SENT] += n_flits(on, bits); c[GG_NC_BITS_SENT] += bits;
+}
+
+/* __processReceivedPacket -> processReceivedPacket + updateReceiveCounters (network_model.cc:118-150,253-272) */
+static void n_receive(oracle_noc* on, uint32_t dst, uint32_t bits, uint64_t* t, uint64_t* zl, uint64_t cont)
+{
+  uint64_t nf = n_flits(on, bits);
+  uint64_t ser = lat_to_ps(nf, on->cfg.frequency_ghz);
+  *t += ser; *zl += ser;
+  uint64_t* c = ncnt(on, dst);
+  c[GG_NC_PACKETS_RECEIVED]++; c[GG_NC_FLITS_RECEIVED] += nf; c[GG_NC_BITS_RECEIVED] += bits;
+  c[GG_NC_TOTAL_LATENCY_PS] += *zl + cont;
+  c[GG_NC_TOTAL_CONTENTION_PS] += cont;
+}
+
+/* binary min-heap of (time_ps, packet id) mesh-hop events */
+typedef struct { uint64_t t; uint64_t id; } n_ev;
+typedef struct { n_ev* a; uint64_t n, cap; } n_heap;
+static int ev_lt(n_ev x, n_ev y) { return x.t < y.t || (x.t == y.t && x.id < y.id); }
+static void heap_push(n_heap* h, n_ev e)
+{
+  if (h->n == h->cap) { h->cap = h->cap ? h->cap * 2 : 1024; h->a = (n_ev*)realloc(h->a, sizeof(n_ev) * h->cap); }
+  uint64_t i = h->n++;
+  while (i > 0) { uint64_t p = (i - 1) / 2; if (!ev_lt(e, h->a[p])) break; h->a[i] = h->a[p]; i = p; }
+  h->a[i] = e;
+}
+static n_ev heap_pop(n_heap* h)
+{
+  n_ev top = h->a[0], last = h->a[--h->n];
+  uint64_t i = 0;
+  for (;;) {
+    uint64_t l = 2 * i + 1, r = l + 1, m = i;
+    n_ev cand = last;
+    if (l < h->n && ev_lt(h->a[l], cand)) { m = l; cand = h->a[l]; }
+    if (r < h->n && ev_lt(h->a[r], cand)) { m = r; }
+    if (m == i) break;
+    h->a[i] = h->a[m]; i = m;
+  }
+  if (h->n) h->a[i] = last;
+  return top;
+}
+
+static int cmp_inj(const void* x, const void* y)
+{
+  const n_ev* a = (const n_ev*)x; const n_ev* b = (const n_ev*)y;
+  return ev_lt(*a, *b) ? -1 : (ev_lt(*b, *a) ? 1 : 0);
+}
+
+/*
+ * Route a batch.  emesh_hop_counter: one closed-form hop per packet
+ * (network_model_emesh_hop_counter.cc:143-157).  emesh_hop_by_hop: the
+ * canonical discrete-event order: the injection port of
+ * every tile serves its packets in (send time, packet index) order, then every
+ * mesh router output port serves the packets that reach it in (arrival time,
+ * packet index) order — exactly what a single global event queue keyed
+ * (time_ps, packet index) produces.
+ */
+int oracle_noc_route(oracle_noc* on, uint64_t n, const uint32_t* src, const uint32_t* dst,
+                     const uint32_t* len, const uint64_t* time_ps,
+                     uint64_t* arrival, uint64_t* zero_load, uint64_t* contention)
+{
+  const double f = on->cfg.frequency_ghz;
+  for (uint64_t k = 0; k < n; ++k)
+    if (src[k] >= on->n || dst[k] >= on->n) return GG_ERR_INVALID;
+
+  if (on->cfg.net_model == GG_NET_MAGIC) {
+    /* network_model_magic.cc:5-21: _flit_width = -1 (computeNumFlits -> 0 flits), one hop of 1 cycle */
+    for (uint64_t k = 0; k < n; ++k) {
+      uint64_t t = time_ps[k], zl = 0;
+      if (src[k] != dst[k]) {
+        uint64_t* cs = ncnt(on, src[k]);
+        cs[GG_NC_PACKETS_SENT]++; cs[GG_NC_BITS_SENT] += len[k];
+        uint64_t l1 = lat_to_ps(1, f);
+        t += l1; zl += l1;
+        uint64_t* cr = ncnt(on, dst[k]);
+        cr[GG_NC_PACKETS_RECEIVED]++; cr[GG_NC_BITS_RECEIVED] += len[k];
+        cr[GG_NC_TOTAL_LATENCY_PS] += zl;
+      }
+      arrival[k] = t; zero_load[k] = zl; contention[k] = 0;
+    }
+    return 0;
+  }
+
+  if (on->cfg.net_model == GG_NET_EMESH_HOP_COUNTER) {
+    const uint64_t hop_latency = (uint64_t)on->cfg.router_delay + on->cfg.link_delay;  /* :81 */
+    for (uint64_t k = 0; k < n; ++k) {
+      uint64_t t = time_ps[k], zl = 0;
+      if (src[k] != dst[k]) {                           /* processCornerCases (network_model.cc:413-424) */
+        n_send_counters(on, src[k], len[k]);
+        int sx = (int)(src[k] % on->w), sy = (int)(src[k] / on->w);
+        int dx = (int)(dst[k] % on->w), dy = (int)(dst[k] / on->w);
+        uint64_t hops = (uint64_t)(abs(sx - dx) + abs(sy - dy));
+        uint64_t lat = lat_to_ps(hops * hop_latency, f);
+        t += lat; zl += lat;                            /* Hop ctor (network_model.cc:556-563) */
+        uint64_t nf = n_flits(on, len[k]);              /* updateEventCounters (:120-127) */
+        uint64_t* c = ncnt(on, src[k]);
+        c[GG_NC_BUFFER_WRITES] += nf * hops; c[GG_NC_BUFFER_READS] += nf * hops;
+        c[GG_NC_SWITCH_ALLOC] += hops; c[GG_NC_CROSSBAR] += nf * hops; c[GG_NC_LINK_TRAVERSALS] += nf * hops;
+        n_receive(on, dst[k], len[k], &t, &zl, 0);
+      }
+      arrival[k] = t; zero_load[k] = zl; contention[k] = 0;
+    }
+    return 0;
+  }
+
+  if (on->cfg.net_model != GG_NET_EMESH_HOP_BY_HOP) return GG_ERR_UNSUPPORTED;
+  if (on->n != on->w * on->h) return GG_ERR_UNSUPPORTED;     /* hop_by_hop.cc:55-59 */
+  const int qm = on->cfg.queue_model_enabled != 0;
+
+  uint64_t* cur = (uint64_t*)malloc(sizeof(uint64_t) * (n ? n : 1));   /* current tile */
+  /* 1. injection ports (routePacket SEND_TILE, hop_by_hop.cc:151-159) */
+  n_ev* inj = (n_ev*)malloc(sizeof(n_ev) * (n ? n : 1));
+  uint64_t ninj = 0;
+  for (uint64_t k = 0; k < n; ++k) {
+    arrival[k] = time_ps[k]; zero_load[k] = 0; contention[k] = 0; cur[k] = src[k];
+    if (src[k] == dst[k]) continue;                  /* self: zero time, no counters */
+    inj[ninj].t = time_ps[k]; inj[ninj].id = k; ++ninj;
+  }
+  {
+    /* stable grouping by source: sort by (src, time, id) */
+    uint64_t* cnt = (uint64_t*)calloc(on->n + 1, sizeof(uint64_t));
+    for (uint64_t i = 0; i < ninj; ++i) cnt[src[inj[i].id] + 1]++;
+    for (uint32_t s = 0; s < on->n; ++s) cnt[s + 1] += cnt[s];
+    n_ev* by = (n_ev*)malloc(sizeof(n_ev) * (ninj ? ninj : 1));
+    uint64_t* pos = (uint64_t*)malloc(sizeof(uint64_t) * (on->n + 1));
+    memcpy(pos, cnt, sizeof(uint64_t) * (on->n + 1));
+    for (uint64_t i = 0; i < ninj; ++i) by[pos[src[inj[i].id]]++] = inj[i];
+    n_heap heap = { 0, 0, 0 };
+    for (uint32_t s = 0; s < on->n; ++s) {
+      uint64_t b = cnt[s], e = cnt[s + 1];
+      qsort(by + b, e - b, sizeof(n_ev), cmp_inj);
+      for (uint64_t i = b; i < e; ++i) {
+        uint64_t k = by[i].id;
+        n_send_counters(on, src[k], len[k]);
+        uint64_t qd = 0;
+        if (qm) qd = oracle_htree_delay(on->inj[s], time_to_cycles(arrival[k], f), n_flits(on, len[k]));
+        uint64_t cps = lat_to_ps(qd, f);
+        arrival[k] += lat_to_ps(0, f) + cps; contention[k] += cps;
+        n_ev ev = { arrival[k], k };
+        heap_push(&heap, ev);
+      }
+    }
+    free(cnt); free(by); free(pos);
+    /* 2. mesh hops in global (time, index) order (hop_by_hop.cc:223-256) */
+    while (heap.n) {
+      n_ev ev = heap_pop(&heap);
+      uint64_t k = ev.id;
+      uint32_t c = (uint32_t)cur[k];
+      int cx = (int)(c % on->w), cy = (int)(c / on->w);
+      int dx = (int)(dst[k] % on->w), dy = (int)(dst[k] / on->w);
+      int port; uint32_t next;
+      if (cx > dx)      { port = P_LEFT;  next = c - 1; }
+      else if (cx < dx) { port = P_RIGHT; next = c + 1; }
+      else if (cy > dy) { port = P_DOWN;  next = c - on->w; }
+      else if (cy < dy) { port = P_UP;    next = c + on->w; }
+      else              { port = P_SELF;  next = c; }
+      uint64_t nf = n_flits(on, len[k]);
+      uint64_t zlc = on->cfg.router_delay, qd = 0;   /* RouterModel::processPacket (router_model.cc:71-108) */
+      uint64_t* cc = ncnt(on, c);
+      if (qm) {
+        qd = oracle_htree_delay(on->q[(size_t)c * NPORTS + port], time_to_cycles(arrival[k], f), nf);
+        cc[GG_NC_ROUTER_CONTENTION_CYCLES] += qd; cc[GG_NC_ROUTER_PACKETS]++;
+      }
+      cc[GG_NC_BUFFER_WRITES] += nf; cc[GG_NC_BUFFER_READS] += nf; cc[GG_NC_SWITCH_ALLOC] += 1; cc[GG_NC_CROSSBAR] += nf;
+      zlc += on->cfg.link_delay;                      /* ElectricalLinkModel::processPacket (electrical_link_model.cc:31-45) */
+      cc[GG_NC_LINK_TRAVERSALS] += nf;
+      uint64_t zps = lat_to_ps(zlc, f), cps = lat_to_ps(qd, f);
+      arrival[k] += zps + cps; zero_load[k] += zps; contention[k] += cps;
+      if (port == P_SELF) {
+        n_receive(on, dst[k], len[k], &arrival[k], &zero_load[k], contention[k]);
+      } else {
+        cur[k] = next;
+        n_ev ne = { arrival[k], k };
+        heap_push(&heap, ne);
+      }
+    }
+    free(heap.a);
+  }
+  free(inj); free(cur);
+  return 0;
+}

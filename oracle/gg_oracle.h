@@ -1,0 +1,80 @@
+/*
+ * gg_oracle.h — CPU restatement of the reference algorithms on the hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in graphite_amd/ links, loads or calls
+ * this code: only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+ * leg use it, as the checker / the CPU baseline.  Every function names the
+ * reference file:line it restates (paths relative to nmtrmail/Graphite).
+ *
+ * Pinning: the history-tree queue model is pinned by the
+ * reference KAT (tests/unit/history_tree/history_tree.cc:9-20); the cache
+ * set / LRU / round-robin / line-info layer and the interval tree are pinned
+ * by fixtures produced by the reference's own code compiled from
+ * /root/reference (oracle/ref/, outputs in tests/golden/); the controller glue
+ * (L1/L2 MSI private path, NoC models) is a restatement checked by those
+ * fixtures where they reach and otherwise "parity unpinned" (cache.cc,
+ * l1/l2_cache_cntlr.cc and the network models need Boost/Pin headers absent
+ * from this image).
+ */
+#ifndef GG_ORACLE_H
+#define GG_ORACLE_H
+#include <stdint.h>
+#include "../include/graphite_gpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------- synthetic trace generators -------- */
+uint64_t oracle_splitmix64_at(uint64_t seed, uint64_t i);
+/* configs[1]: uniform private region of 2^lines_log2 lines per tile at
+ * byte base tile << base_shift, WRITE iff ((z >> 32) % 3) == 0.             */
+void oracle_gen_uniform(uint32_t tile, uint64_t first, uint64_t n,
+                        uint32_t lines_log2, uint32_t base_shift,
+                        uint64_t* addr, uint32_t* meta);
+
+/* ---------------- private cache replay (mode P) ---------------------------- */
+typedef struct oracle_cache oracle_cache;
+oracle_cache* oracle_cache_create(const gg_config* cfg);
+void          oracle_cache_destroy(oracle_cache* oc);
+/* Replays tiles [tile_begin, tile_end) of a tile-major trace; result/evicted
+ * may be NULL.  Returns 0 or GG_ERR_STATE where the reference would abort.  */
+int  oracle_cache_run(oracle_cache* oc, const uint64_t* addr, const uint32_t* meta,
+                      const uint64_t* tile_offsets, uint32_t tile_begin, uint32_t tile_end,
+                      uint32_t* result, uint64_t* evicted);
+void oracle_cache_counters(const oracle_cache* oc, uint64_t* out); /* [tile][2][12] */
+/* The Cache quartet (cache.cc:84-241) on one tile/level. */
+int  oracle_cache_get_line_info(oracle_cache* oc, uint32_t tile, int level, uint64_t addr, gg_line_info* out);
+int  oracle_cache_set_line_info(oracle_cache* oc, uint32_t tile, int level, uint64_t addr, const gg_line_info* in);
+int  oracle_cache_access_line(oracle_cache* oc, uint32_t tile, int level, uint64_t addr, int is_store);
+int  oracle_cache_insert_line(oracle_cache* oc, uint32_t tile, int level, uint64_t addr,
+                              const gg_line_info* in, int* eviction, uint64_t* evicted_addr,
+                              gg_line_info* evicted_info);
+
+/* ---------------- queue models ------------------------------------------- */
+typedef struct oracle_htree oracle_htree;
+oracle_htree* oracle_htree_create(uint64_t min_processing_time, int max_list_size, int analytical_enabled);
+void          oracle_htree_destroy(oracle_htree* h);
+uint64_t      oracle_htree_delay(oracle_htree* h, uint64_t pkt_time, uint64_t processing_time);
+uint64_t      oracle_htree_analytical_requests(const oracle_htree* h);
+uint32_t      oracle_htree_size(const oracle_htree* h);
+
+/* ---------------- NoC ------------------------------------------------------ */
+typedef struct oracle_noc oracle_noc;
+oracle_noc* oracle_noc_create(const gg_config* cfg);
+void        oracle_noc_destroy(oracle_noc* on);
+int  oracle_noc_route(oracle_noc* on, uint64_t n, const uint32_t* src, const uint32_t* dst,
+                      const uint32_t* length_bits, const uint64_t* time_ps,
+                      uint64_t* arrival_ps, uint64_t* zero_load_ps, uint64_t* contention_ps);
+void oracle_noc_counters(const oracle_noc* on, uint64_t* out); /* [tile][GG_NUM_NET_COUNTERS] */
+
+/* Network::netSend line split of Core::initiateMemoryAccess (core.cc:167-201):
+ * returns the number of line accesses [addr, addr+size) produces and writes
+ * their line-aligned addresses to lines (capacity cap).                    */
+uint32_t oracle_split_lines(uint64_t addr, uint32_t size, uint32_t line_size,
+                            uint64_t* lines, uint32_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,185 @@
+"""ctypes view of the C oracle (oracle/gg_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, as the checker.  The product (graphite_amd/)
+never imports it.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from graphite_amd.config import GGConfig, NUM_CACHE_COUNTERS, NUM_NET_COUNTERS
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+
+_u64p = np.ctypeslib.ndpointer(np.uint64, flags="C_CONTIGUOUS")
+_u32p = np.ctypeslib.ndpointer(np.uint32, flags="C_CONTIGUOUS")
+
+
+def build(force=False):
+    """Compile the oracle with gcc (plain C99, -ffp-contract=off)."""
+    src = os.path.join(HERE, "gg_oracle.c")
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", HERE, "liboracle.so"])
+    return LIB
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(LIB)
+        vp = ctypes.c_void_p
+        L.oracle_splitmix64_at.restype = ctypes.c_uint64
+        L.oracle_splitmix64_at.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
+        L.oracle_gen_uniform.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
+                                         ctypes.c_uint32, ctypes.c_uint32, _u64p, _u32p]
+        L.oracle_cache_create.restype = vp
+        L.oracle_cache_create.argtypes = [ctypes.POINTER(GGConfig)]
+        L.oracle_cache_destroy.argtypes = [vp]
+        L.oracle_cache_run.restype = ctypes.c_int
+        L.oracle_cache_run.argtypes = [vp, _u64p, _u32p, _u64p, ctypes.c_uint32, ctypes.c_uint32, vp, vp]
+        L.oracle_cache_counters.argtypes = [vp, _u64p]
+        L.oracle_cache_get_line_info.argtypes = [vp, ctypes.c_uint32, ctypes.c_int, ctypes.c_uint64, vp]
+        L.oracle_cache_set_line_info.argtypes = [vp, ctypes.c_uint32, ctypes.c_int, ctypes.c_uint64, vp]
+        L.oracle_cache_access_line.argtypes = [vp, ctypes.c_uint32, ctypes.c_int, ctypes.c_uint64, ctypes.c_int]
+        L.oracle_cache_insert_line.argtypes = [vp, ctypes.c_uint32, ctypes.c_int, ctypes.c_uint64, vp,
+                                               ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint64), vp]
+        L.oracle_htree_create.restype = vp
+        L.oracle_htree_create.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
+        L.oracle_htree_destroy.argtypes = [vp]
+        L.oracle_htree_delay.restype = ctypes.c_uint64
+        L.oracle_htree_delay.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64]
+        L.oracle_htree_analytical_requests.restype = ctypes.c_uint64
+        L.oracle_htree_analytical_requests.argtypes = [vp]
+        L.oracle_noc_create.restype = vp
+        L.oracle_noc_create.argtypes = [ctypes.POINTER(GGConfig)]
+        L.oracle_noc_destroy.argtypes = [vp]
+        L.oracle_noc_route.restype = ctypes.c_int
+        L.oracle_noc_route.argtypes = [vp, ctypes.c_uint64, _u32p, _u32p, _u32p, _u64p, _u64p, _u64p, _u64p]
+        L.oracle_noc_counters.argtypes = [vp, _u64p]
+        L.oracle_split_lines.restype = ctypes.c_uint32
+        L.oracle_split_lines.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _u64p, ctypes.c_uint32]
+        _lib = L
+    return _lib
+
+
+class LineInfo(ctypes.Structure):
+    _fields_ = [("tag", ctypes.c_uint64), ("cstate", ctypes.c_uint32), ("cached_loc", ctypes.c_uint32)]
+
+
+def gen_uniform(tile, first, n, lines_log2=15, base_shift=26):
+    addr = np.empty(n, np.uint64)
+    meta = np.empty(n, np.uint32)
+    lib().oracle_gen_uniform(tile, first, n, lines_log2, base_shift, addr, meta)
+    return addr, meta
+
+
+class OracleCache:
+    """Private-mode (decoupled) replay of L1-D/L2 per tile."""
+
+    def __init__(self, cfg):
+        self.cfg = cfg
+        self.h = lib().oracle_cache_create(ctypes.byref(cfg))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().oracle_cache_destroy(self.h)
+            self.h = None
+
+    def run(self, addr, meta, tile_offsets, tile_begin=0, tile_end=None, want_evicted=False):
+        n = len(addr)
+        addr = np.ascontiguousarray(addr, np.uint64)
+        meta = np.ascontiguousarray(meta, np.uint32)
+        offs = np.ascontiguousarray(tile_offsets, np.uint64)
+        res = np.zeros(n, np.uint32)
+        ev = np.zeros(n, np.uint64) if want_evicted else None
+        tile_end = self.cfg.num_tiles if tile_end is None else tile_end
+        rc = lib().oracle_cache_run(self.h, addr, meta, offs, tile_begin, tile_end,
+                                    res.ctypes.data, ev.ctypes.data if ev is not None else None)
+        if rc != 0:
+            raise RuntimeError("oracle: reference would abort (LOG_ASSERT_ERROR), rc=%d" % rc)
+        return (res, ev) if want_evicted else res
+
+    def counters(self):
+        out = np.zeros(self.cfg.num_tiles * 2 * NUM_CACHE_COUNTERS, np.uint64)
+        lib().oracle_cache_counters(self.h, out)
+        return out.reshape(self.cfg.num_tiles, 2, NUM_CACHE_COUNTERS)
+
+    def get_line_info(self, tile, level, addr, default=None):
+        li = default or LineInfo(0xFFFFFFFFFFFFFFFF, 0, 0)
+        rc = lib().oracle_cache_get_line_info(self.h, tile, level, addr, ctypes.addressof(li))
+        assert rc == 0
+        return li
+
+    def set_line_info(self, tile, level, addr, li):
+        return lib().oracle_cache_set_line_info(self.h, tile, level, addr, ctypes.addressof(li))
+
+    def access_line(self, tile, level, addr, is_store):
+        return lib().oracle_cache_access_line(self.h, tile, level, addr, int(is_store))
+
+    def insert_line(self, tile, level, addr, li):
+        ev = ctypes.c_int(0)
+        ea = ctypes.c_uint64(0)
+        evi = LineInfo(0xFFFFFFFFFFFFFFFF, 0, 0)
+        rc = lib().oracle_cache_insert_line(self.h, tile, level, addr, ctypes.addressof(li),
+                                            ctypes.byref(ev), ctypes.byref(ea), ctypes.addressof(evi))
+        return rc, ev.value, ea.value, evi
+
+
+class OracleHistoryTree:
+    def __init__(self, min_proc=1, max_list_size=100, analytical=True):
+        self.h = lib().oracle_htree_create(min_proc, max_list_size, int(analytical))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().oracle_htree_destroy(self.h)
+            self.h = None
+
+    def delay(self, t, p):
+        return lib().oracle_htree_delay(self.h, t, p)
+
+    @property
+    def analytical_requests(self):
+        return lib().oracle_htree_analytical_requests(self.h)
+
+
+class OracleNoc:
+    def __init__(self, cfg):
+        self.cfg = cfg
+        self.h = lib().oracle_noc_create(ctypes.byref(cfg))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().oracle_noc_destroy(self.h)
+            self.h = None
+
+    def route(self, src, dst, length_bits, time_ps):
+        n = len(src)
+        arr = np.zeros(n, np.uint64)
+        zl = np.zeros(n, np.uint64)
+        ct = np.zeros(n, np.uint64)
+        rc = lib().oracle_noc_route(self.h, n, np.ascontiguousarray(src, np.uint32),
+                                    np.ascontiguousarray(dst, np.uint32),
+                                    np.ascontiguousarray(length_bits, np.uint32),
+                                    np.ascontiguousarray(time_ps, np.uint64), arr, zl, ct)
+        if rc != 0:
+            raise RuntimeError("oracle noc rc=%d" % rc)
+        return arr, zl, ct
+
+    def counters(self):
+        out = np.zeros(self.cfg.num_tiles * NUM_NET_COUNTERS, np.uint64)
+        lib().oracle_noc_counters(self.h, out)
+        return out.reshape(self.cfg.num_tiles, NUM_NET_COUNTERS)
+
+
+def split_lines(addr, size, line=64):
+    buf = np.zeros(64, np.uint64)
+    n = lib().oracle_split_lines(addr, size, line, buf, 64)
+    return [int(x) for x in buf[:min(n, 64)]]

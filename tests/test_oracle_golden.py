@@ -1,0 +1,149 @@
+"""The CPU oracle (oracle/gg_oracle.c) pinned against the reference's own
+known-answer test and the fixtures produced by the reference's own code."""
+import numpy as np
+import pytest
+
+from graphite_amd import config as C
+from oracle import pyoracle as po
+from golden_util import manifest, load, POLICY
+
+M = manifest()
+
+# tests/unit/history_tree/history_tree.cc:9-20 (QueueModelHistoryTree(1), max_list_size 100, analytical on)
+KAT = [(10, 10, 0), (21, 10, 0), (32, 10, 0), (43, 10, 0), (0, 1, 0),
+       (0, 10, 53), (45, 10, 18), (60, 4, 13), (70, 8, 7), (75, 10, 10)]
+
+
+def test_history_tree_kat():
+    h = po.OracleHistoryTree(1, 100, True)
+    assert [h.delay(t, p) for t, p, _ in KAT] == [d for _, _, d in KAT]
+    assert M["htree_kat"]["rows"] == [list(r) for r in KAT]
+
+
+@pytest.mark.parametrize("name", [k for k, v in M.items() if v["kind"] == "htree"])
+def test_history_tree_reference_sequences(name):
+    e = M[name]
+    rows = load(e["file"], np.uint64).reshape(-1, 3)
+    h = po.OracleHistoryTree(1, e["max_list_size"], e["analytical"])
+    got = np.array([h.delay(int(t), int(p)) for t, p, _ in rows], np.uint64)
+    np.testing.assert_array_equal(got, rows[:, 2])
+    assert h.analytical_requests == e["analytical_requests"]
+
+
+@pytest.mark.parametrize("name", [k for k, v in M.items() if v["kind"] == "quartet"])
+def test_cache_quartet_reference_sequences(name):
+    e = M[name]
+    rows = load(e["file"], np.uint64).reshape(-1, 10)
+    level = e["level"]
+    kw = dict(line_size=64)
+    if level == 0:
+        kw.update(l1d_size_kb=e["size_kb"], l1d_assoc=e["assoc"], l1d_policy=POLICY[e["policy"]])
+    else:
+        kw.update(l2_size_kb=e["size_kb"], l2_assoc=e["assoc"], l2_policy=POLICY[e["policy"]])
+    oc = po.OracleCache(C.default_config(1, **kw))
+    INV = 0xFFFFFFFFFFFFFFFF
+    for r in rows:
+        op, addr, ins, loc, ok, otag, ost, oloc, ev, evaddr = (int(x) for x in r)
+        if op == 0:
+            li = oc.get_line_info(0, level, addr)
+            assert (li.tag, li.cstate, li.cached_loc) == (otag, ost, oloc)
+        elif op == 1:
+            tag = INV if ins == C.CSTATE_INVALID else addr >> 6
+            rc = oc.set_line_info(0, level, addr, po.LineInfo(tag, ins, loc if ins else 0))
+            assert (rc == 0) == bool(ok)
+        elif op in (2, 3):
+            rc = oc.access_line(0, level, addr, op == 3)
+            assert (rc == 0) == bool(ok)
+        else:
+            if not ok:
+                continue
+            rc, e_, ea, evi = oc.insert_line(0, level, addr, po.LineInfo(addr >> 6, ins, loc))
+            assert rc == 0
+            assert (e_, ea, evi.tag, evi.cstate, evi.cached_loc) == (ev, evaddr & 0xFFFFFFFFFFFFFFFF, otag, ost, oloc)
+    np.testing.assert_array_equal(oc.counters()[0, level], np.array(e["counters"], np.uint64))
+
+
+def modep_trace(e):
+    """The fixture's generator, restated (see ref_harness.cc gen_modep)."""
+    T, N, LL = e["tiles"], e["per_tile"], e["lines_log2"]
+    addrs, metas = [], []
+    for t in range(T):
+        seed = 0x9E3779B97F4A7C15 ^ t
+        i = np.arange(N, dtype=np.uint64)
+        z = _sm_vec(seed, i)
+        mask = np.uint64((1 << LL) - 1)
+        base = np.uint64(t << 26)
+        if e["gen"] == 0:
+            a = base + ((z & mask) << np.uint64(6))
+            w = ((z >> np.uint64(32)) % np.uint64(3)) == 0
+        else:
+            sel = (z >> np.uint64(60)) & np.uint64(3)
+            hot = base + (((z >> np.uint64(8)) & np.uint64(63)) << np.uint64(6))
+            stride = base + (((i * np.uint64(17)) & mask) << np.uint64(6))
+            uni = base + ((z & mask) << np.uint64(6))
+            a = np.where(sel == 0, hot, np.where(sel == 1, stride, uni))
+            w = ((z >> np.uint64(32)) & np.uint64(1)) == 0
+        addrs.append(a.astype(np.uint64))
+        metas.append(w.astype(np.uint32))
+    offs = np.arange(T + 1, dtype=np.uint64) * np.uint64(N)
+    return np.concatenate(addrs), np.concatenate(metas), offs
+
+
+def _sm_vec(seed, i):
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + (i + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def modep_config(e):
+    return C.default_config(e["tiles"], l1d_size_kb=e["l1d_size_kb"], l1d_assoc=e["l1d_assoc"],
+                            l1d_policy=POLICY[e["l1d_policy"]], l2_size_kb=e["l2_size_kb"],
+                            l2_assoc=e["l2_assoc"], l2_policy=POLICY[e["l2_policy"]])
+
+
+def test_vectorized_generator_matches_oracle():
+    a, m = po.gen_uniform(5, 100, 1000)
+    e = {"tiles": 6, "per_tile": 1100, "lines_log2": 15, "gen": 0}
+    A, Mt, offs = modep_trace(e)
+    np.testing.assert_array_equal(A[5 * 1100 + 100:5 * 1100 + 1100], a)
+    np.testing.assert_array_equal(Mt[5 * 1100 + 100:5 * 1100 + 1100], m)
+
+
+@pytest.mark.parametrize("name", [k for k, v in M.items() if v["kind"] == "modep"])
+def test_private_replay_reference_fixtures(name):
+    e = M[name]
+    addr, meta, offs = modep_trace(e)
+    oc = po.OracleCache(modep_config(e))
+    res, ev = oc.run(addr, meta, offs, want_evicted=True)
+    np.testing.assert_array_equal(res.astype(np.uint8), load(e["result_file"], np.uint8))
+    cnt = load(e["counters_file"], np.uint64).reshape(e["tiles"], 2, C.NUM_CACHE_COUNTERS)
+    np.testing.assert_array_equal(oc.counters(), cnt)
+    for t in range(e["tiles"]):
+        sl = slice(int(offs[t]), int(offs[t + 1]))
+        m = (res[sl] & C.RES_L2_EVICT) != 0
+        assert int(ev[sl][m].sum(dtype=np.uint64)) == e["evicted_sum"][t]
+
+
+def test_fixture_coverage():
+    """The fixtures reach every result flag the private path can produce."""
+    flags = 0
+    levels = set()
+    for k, e in M.items():
+        if e["kind"] == "modep":
+            r = load(e["result_file"], np.uint8)
+            levels |= set(np.unique(r & 3).tolist())
+            flags |= int(np.bitwise_or.reduce(r))
+    assert levels == {0, 1, 2}
+    for f in (C.RES_UPGRADE, C.RES_L1_EVICT, C.RES_L2_EVICT, C.RES_L2_EVICT_DIRTY, C.RES_L2_EVICT_INV_L1):
+        assert flags & f, hex(f)
+
+
+def test_split_lines():
+    # Core::initiateMemoryAccess (core.cc:167-201)
+    assert po.split_lines(0x1000, 4) == [0x1000]
+    assert po.split_lines(0x103E, 4) == [0x1000, 0x1040]
+    assert po.split_lines(0x1000, 64) == [0x1000]      # zero-size tail skipped
+    assert po.split_lines(0x1010, 128) == [0x1000, 0x1040, 0x1080]
+    assert po.split_lines(0x1000, 0) == []
