@@ -1,0 +1,222 @@
+"""Python binding of the C ABI (include/graphite_gpu.h) over ctypes.
+
+This is host plumbing only: every computation runs in libgraphite_gpu.so's
+HIP kernels.  There is no CPU fallback — if the library or a GPU is missing the
+calls raise.  Device buffers are torch tensors on the ROCm device (PyTorch is
+used for allocation and streams only).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from .config import GGConfig, NUM_CACHE_COUNTERS, NUM_NET_COUNTERS
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libgraphite_gpu.so")
+
+GG_OK = 0
+_ERR = {-1: "GG_ERR_INVALID", -2: "GG_ERR_HIP", -3: "GG_ERR_UNSUPPORTED", -4: "GG_ERR_RANGE", -5: "GG_ERR_STATE"}
+
+
+class GGError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s: %s" % (_ERR.get(code, code), msg))
+        self.code = code
+
+
+class LineInfo(ctypes.Structure):
+    _fields_ = [("tag", ctypes.c_uint64), ("cstate", ctypes.c_uint32), ("cached_loc", ctypes.c_uint32)]
+
+
+class _Trace(ctypes.Structure):
+    _fields_ = [("addr_dev", ctypes.c_void_p), ("meta_dev", ctypes.c_void_p),
+                ("tile_offsets", ctypes.POINTER(ctypes.c_uint64)), ("num_records", ctypes.c_uint64)]
+
+
+class _Packets(ctypes.Structure):
+    _fields_ = [("src_dev", ctypes.c_void_p), ("dst_dev", ctypes.c_void_p),
+                ("length_bits_dev", ctypes.c_void_p), ("time_ps_dev", ctypes.c_void_p),
+                ("num_packets", ctypes.c_uint64)]
+
+
+class _PacketOut(ctypes.Structure):
+    _fields_ = [("arrival_ps_dev", ctypes.c_void_p), ("zero_load_ps_dev", ctypes.c_void_p),
+                ("contention_ps_dev", ctypes.c_void_p)]
+
+
+# every symbol include/graphite_gpu.h declares (checked by tests/test_abi.py)
+EXPORTS = ["gg_abi_version", "gg_last_error", "gg_config_default", "gg_create", "gg_destroy", "gg_reset",
+           "gg_cache_access_batch", "gg_cache_get_counters", "gg_cache_get_line_info",
+           "gg_cache_set_line_info", "gg_cache_access_line", "gg_cache_insert_line",
+           "gg_noc_route_batch", "gg_noc_get_counters", "gg_queue_delay_batch",
+           "gg_gen_uniform_trace", "gg_kernel_time_ms", "gg_set_timing"]
+
+_lib = None
+
+
+def load():
+    """Load libgraphite_gpu.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("graphite_amd: %s is missing — run __graft_entry__.build() "
+                           "(make -C graphite_amd/csrc); there is no CPU fallback" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+    L.gg_abi_version.restype = i32
+    L.gg_last_error.restype = ctypes.c_char_p
+    L.gg_config_default.argtypes = [ctypes.POINTER(GGConfig), u32]
+    L.gg_create.restype = vp
+    L.gg_create.argtypes = [ctypes.POINTER(GGConfig), ctypes.POINTER(i32)]
+    L.gg_destroy.argtypes = [vp]
+    L.gg_reset.argtypes = [vp]
+    L.gg_cache_access_batch.argtypes = [vp, ctypes.POINTER(_Trace), vp, vp, vp]
+    L.gg_cache_get_counters.argtypes = [vp, vp]
+    L.gg_cache_get_line_info.argtypes = [vp, u32, i32, u64, ctypes.POINTER(LineInfo)]
+    L.gg_cache_set_line_info.argtypes = [vp, u32, i32, u64, ctypes.POINTER(LineInfo)]
+    L.gg_cache_access_line.argtypes = [vp, u32, i32, u64, i32]
+    L.gg_cache_insert_line.argtypes = [vp, u32, i32, u64, ctypes.POINTER(LineInfo), ctypes.POINTER(i32),
+                                       ctypes.POINTER(u64), ctypes.POINTER(LineInfo)]
+    L.gg_noc_route_batch.argtypes = [vp, ctypes.POINTER(_Packets), ctypes.POINTER(_PacketOut), vp]
+    L.gg_noc_get_counters.argtypes = [vp, vp]
+    L.gg_queue_delay_batch.argtypes = [vp, u64, vp, vp, u64, vp]
+    L.gg_gen_uniform_trace.argtypes = [vp, vp, u32, u32, u64, u64, u32, u32, vp]
+    L.gg_kernel_time_ms.restype = ctypes.c_float
+    L.gg_kernel_time_ms.argtypes = [vp, ctypes.c_char_p]
+    L.gg_set_timing.argtypes = [vp, i32]
+    for name in ["gg_reset", "gg_cache_access_batch", "gg_cache_get_counters", "gg_cache_get_line_info",
+                 "gg_cache_set_line_info", "gg_cache_access_line", "gg_cache_insert_line",
+                 "gg_noc_route_batch", "gg_noc_get_counters", "gg_queue_delay_batch", "gg_gen_uniform_trace"]:
+        getattr(L, name).restype = i32
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != GG_OK:
+        raise GGError(rc, load().gg_last_error().decode(errors="replace"))
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream(stream):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def _need_dev(t, dtype, n=None):
+    import torch
+    if not t.is_cuda:
+        raise ValueError("expected a device tensor")
+    if t.dtype != dtype or not t.is_contiguous():
+        raise ValueError("expected a contiguous %s device tensor" % dtype)
+    if n is not None and t.numel() != n:
+        raise ValueError("expected %d elements, got %d" % (n, t.numel()))
+
+
+class Backend:
+    """One context per GPU (gg_create): device-resident private caches of
+    every tile and the NoC router state."""
+
+    def __init__(self, cfg: GGConfig):
+        L = load()
+        st = ctypes.c_int(0)
+        self.cfg = cfg
+        self.h = L.gg_create(ctypes.byref(cfg), ctypes.byref(st))
+        if not self.h:
+            _check(st.value or -1)
+
+    def close(self):
+        if getattr(self, "h", None):
+            load().gg_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def reset(self):
+        _check(load().gg_reset(self.h))
+
+    def set_timing(self, on=True):
+        load().gg_set_timing(self.h, int(on))
+
+    def kernel_time_ms(self, name):
+        return load().gg_kernel_time_ms(self.h, name.encode())
+
+    # ---- cache ----------------------------------------------------------
+    def cache_access_batch(self, addr, meta, tile_offsets, result=None, evicted=None, stream=None):
+        """Replay a tile-major trace batch (device tensors addr: uint64 as
+        int64, meta: int32).  tile_offsets: host sequence of num_tiles+1."""
+        import torch
+        n = addr.numel()
+        _need_dev(addr, torch.int64, n)
+        _need_dev(meta, torch.int32, n)
+        if result is not None:
+            _need_dev(result, torch.int32, n)
+        if evicted is not None:
+            _need_dev(evicted, torch.int64, n)
+        offs = np.ascontiguousarray(tile_offsets, dtype=np.uint64)
+        if offs.size != self.cfg.num_tiles + 1:
+            raise ValueError("tile_offsets needs num_tiles + 1 entries")
+        tr = _Trace(addr.data_ptr(), meta.data_ptr(), offs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), n)
+        self._keep = offs
+        _check(load().gg_cache_access_batch(self.h, ctypes.byref(tr), _ptr(result), _ptr(evicted), _stream(stream)))
+
+    def cache_counters(self):
+        out = np.zeros(self.cfg.num_tiles * 2 * NUM_CACHE_COUNTERS, np.uint64)
+        _check(load().gg_cache_get_counters(self.h, out.ctypes.data_as(ctypes.c_void_p)))
+        return out.reshape(self.cfg.num_tiles, 2, NUM_CACHE_COUNTERS)
+
+    def get_line_info(self, tile, level, addr, default=None):
+        li = default or LineInfo(0xFFFFFFFFFFFFFFFF, 0, 0)
+        _check(load().gg_cache_get_line_info(self.h, tile, level, addr, ctypes.byref(li)))
+        return li
+
+    def set_line_info(self, tile, level, addr, li):
+        return load().gg_cache_set_line_info(self.h, tile, level, addr, ctypes.byref(li))
+
+    def access_line(self, tile, level, addr, is_store):
+        return load().gg_cache_access_line(self.h, tile, level, addr, int(is_store))
+
+    def insert_line(self, tile, level, addr, li):
+        ev = ctypes.c_int(0)
+        ea = ctypes.c_uint64(0)
+        evi = LineInfo(0xFFFFFFFFFFFFFFFF, 0, 0)
+        rc = load().gg_cache_insert_line(self.h, tile, level, addr, ctypes.byref(li), ctypes.byref(ev),
+                                         ctypes.byref(ea), ctypes.byref(evi))
+        return rc, ev.value, ea.value, evi
+
+    # ---- NoC ------------------------------------------------------------
+    def noc_route_batch(self, src, dst, length_bits, time_ps, arrival, zero_load, contention, stream=None):
+        import torch
+        n = src.numel()
+        for t, dt in ((src, torch.int32), (dst, torch.int32), (length_bits, torch.int32), (time_ps, torch.int64),
+                      (arrival, torch.int64), (zero_load, torch.int64), (contention, torch.int64)):
+            _need_dev(t, dt, n)
+        pk = _Packets(src.data_ptr(), dst.data_ptr(), length_bits.data_ptr(), time_ps.data_ptr(), n)
+        out = _PacketOut(arrival.data_ptr(), zero_load.data_ptr(), contention.data_ptr())
+        _check(load().gg_noc_route_batch(self.h, ctypes.byref(pk), ctypes.byref(out), _stream(stream)))
+
+    def noc_counters(self):
+        out = np.zeros(self.cfg.num_tiles * NUM_NET_COUNTERS, np.uint64)
+        _check(load().gg_noc_get_counters(self.h, out.ctypes.data_as(ctypes.c_void_p)))
+        return out.reshape(self.cfg.num_tiles, NUM_NET_COUNTERS)
+
+    def queue_delay_batch(self, pkt_time, proc_time, min_processing_time=1):
+        t = np.ascontiguousarray(pkt_time, np.uint64)
+        p = np.ascontiguousarray(proc_time, np.uint64)
+        d = np.zeros(t.size, np.uint64)
+        _check(load().gg_queue_delay_batch(self.h, min_processing_time, t.ctypes.data_as(ctypes.c_void_p),
+                                           p.ctypes.data_as(ctypes.c_void_p), t.size,
+                                           d.ctypes.data_as(ctypes.c_void_p)))
+        return d
+
+
+def gen_uniform_trace(addr, meta, tile_begin, tiles, per_tile, first=0, lines_log2=15, base_shift=26, stream=None):
+    """Fill device tensors with the configs[1] synthetic trace."""
+    _check(load().gg_gen_uniform_trace(_ptr(addr), _ptr(meta), tile_begin, tiles, per_tile, first,
+                                       lines_log2, base_shift, _stream(stream)))

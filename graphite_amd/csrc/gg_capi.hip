@@ -1,0 +1,290 @@
+// gg_capi.hip — the extern "C" boundary (include/graphite_gpu.h): context
+// lifetime, geometry, dispatch, error reporting and HIP-event kernel timing.
+#include "gg_internal.h"
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+
+namespace {
+thread_local std::string g_last_error;
+
+__global__ void k_gen_uniform(uint64_t* addr, uint32_t* meta, uint32_t tile_begin, uint32_t tiles,
+                              uint64_t per_tile, uint64_t first, uint32_t lines_log2, uint32_t base_shift)
+{
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (uint64_t)tiles * per_tile) return;
+  const uint32_t t = tile_begin + (uint32_t)(i / per_tile);
+  const uint64_t k = first + i % per_tile;
+  uint64_t z = (0x9E3779B97F4A7C15ull ^ (uint64_t)t) + (k + 1) * 0x9E3779B97F4A7C15ull;   // SplitMix64
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  addr[i] = ((uint64_t)t << base_shift) + ((z & ((1ull << lines_log2) - 1)) << 6);
+  meta[i] = (((z >> 32) % 3) == 0) ? GG_META_WRITE : 0u;
+}
+
+int floor_log2(uint64_t n) { int p = -1; while (n) { n >>= 1; ++p; } return p; }
+bool is_pow2(uint64_t n) { return n && !(n & (n - 1)); }
+}  // namespace
+
+gg_status gg_fail(gg_status code, const char* fmt, ...)
+{
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+gg_status gg_hip_check(hipError_t e, const char* what)
+{
+  return gg_fail(GG_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+void gg_timer_begin(gg_ctx* ctx, const char* name, hipStream_t s)
+{
+  if (!ctx->timing) return;
+  for (gg_timer& t : ctx->timers)
+    if (t.name == name) { hipEventRecord(t.start, s); t.valid = false; return; }
+  gg_timer t;
+  t.name = name;
+  hipEventCreate(&t.start);
+  hipEventCreate(&t.stop);
+  hipEventRecord(t.start, s);
+  ctx->timers.push_back(t);
+}
+
+void gg_timer_end(gg_ctx* ctx, const char* name, hipStream_t s)
+{
+  if (!ctx->timing) return;
+  for (gg_timer& t : ctx->timers)
+    if (t.name == name) { hipEventRecord(t.stop, s); t.valid = true; return; }
+}
+
+extern "C" {
+
+int gg_abi_version(void) { return GG_ABI_VERSION; }
+const char* gg_last_error(void) { return g_last_error.c_str(); }
+
+void gg_config_default(gg_config* c, uint32_t num_tiles)
+{
+  memset(c, 0, sizeof(*c));
+  c->num_tiles = num_tiles;
+  c->line_size = 64;
+  c->l1d_size_kb = 32; c->l1d_assoc = 4; c->l1d_policy = GG_POLICY_LRU;
+  c->l2_size_kb = 512; c->l2_assoc = 8; c->l2_policy = GG_POLICY_LRU;
+  c->net_model = GG_NET_EMESH_HOP_COUNTER;
+  c->flit_width = 64;
+  c->router_delay = 1;
+  c->link_delay = 1;
+  c->queue_model_enabled = 1;
+  c->max_list_size = 100;
+  c->analytical_enabled = 1;
+  c->frequency_ghz = 1.0;
+  c->device = 0;
+}
+
+gg_ctx* gg_create(const gg_config* cfg, gg_status* status)
+{
+  gg_status dummy;
+  if (!status) status = &dummy;
+  if (!cfg || cfg->num_tiles == 0) { *status = gg_fail(GG_ERR_INVALID, "config NULL or zero tiles"); return nullptr; }
+  const gg_config& c = *cfg;
+  if (!is_pow2(c.line_size)) { *status = gg_fail(GG_ERR_INVALID, "line size must be a power of two"); return nullptr; }
+  const uint64_t l1_sets = (uint64_t)c.l1d_size_kb * 1024 / ((uint64_t)c.l1d_assoc * c.line_size);
+  const uint64_t l2_sets = (uint64_t)c.l2_size_kb * 1024 / ((uint64_t)c.l2_assoc * c.line_size);
+  if (!is_pow2(l1_sets) || !is_pow2(l2_sets)) {
+    *status = gg_fail(GG_ERR_UNSUPPORTED, "set counts must be powers of two (cache_hash_fn.h masks the set index)");
+    return nullptr;
+  }
+  if (l2_sets < l1_sets) {
+    *status = gg_fail(GG_ERR_UNSUPPORTED, "private replay needs L2 sets >= L1-D sets (L2 sets nest in L1-D sets)");
+    return nullptr;
+  }
+  if (l1_sets > 1024) { *status = gg_fail(GG_ERR_UNSUPPORTED, "more than 1024 L1-D sets"); return nullptr; }
+  if (c.l1d_assoc > 8 || c.l2_assoc > 32) { *status = gg_fail(GG_ERR_UNSUPPORTED, "associativity beyond 8 (L1-D) / 32 (L2)"); return nullptr; }
+  if (c.l1d_policy > GG_POLICY_ROUND_ROBIN || c.l2_policy > GG_POLICY_ROUND_ROBIN) {
+    *status = gg_fail(GG_ERR_INVALID, "unknown replacement policy");
+    return nullptr;
+  }
+  if (c.frequency_ghz <= 0) { *status = gg_fail(GG_ERR_INVALID, "frequency must be positive"); return nullptr; }
+
+  hipError_t he = hipSetDevice(c.device);
+  if (he != hipSuccess) { *status = gg_hip_check(he, "hipSetDevice"); return nullptr; }
+
+  gg_ctx* ctx = new gg_ctx();
+  ctx->cfg = c;
+  ctx->device = c.device;
+  gg_geom& g = ctx->g;
+  g.tiles = c.num_tiles;
+  g.log_line = floor_log2(c.line_size);
+  g.u1 = (uint32_t)l1_sets;
+  g.log_u1 = floor_log2(l1_sets);
+  g.a1 = c.l1d_assoc;
+  g.l2_sets = (uint32_t)l2_sets;
+  g.log_l2 = floor_log2(l2_sets);
+  g.s2 = (uint32_t)(l2_sets / l1_sets);
+  g.a2 = c.l2_assoc;
+  g.mw = (c.l2_assoc + 7) / 8;
+  g.pol1 = c.l1d_policy;
+  g.pol2 = c.l2_policy;
+  g.units = (uint64_t)g.tiles * g.u1;
+  // L2 tags are stored as (line >> log2(L2 sets)) in 32 bits, 2^32-1 = invalid
+  const uint32_t lim_shift = 32 + g.log_l2 + g.log_line;
+  g.addr_limit = (lim_shift >= 64) ? ~0ull : ((0xFFFFFFFFull << (g.log_l2 + g.log_line)));
+
+  gg_status st = gg_cache_state_alloc(ctx);
+  if (st == GG_OK) st = gg_noc_alloc(ctx);
+  if (st == GG_OK) {
+    he = hipMalloc((void**)&ctx->err_dev, sizeof(uint32_t));
+    if (he != hipSuccess) st = gg_hip_check(he, "hipMalloc(err)");
+  }
+  if (st == GG_OK) st = gg_reset(ctx);
+  if (st != GG_OK) { gg_destroy(ctx); *status = st; return nullptr; }
+  *status = GG_OK;
+  return ctx;
+}
+
+void gg_destroy(gg_ctx* ctx)
+{
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  hipDeviceSynchronize();
+  gg_cache_state_free(ctx);
+  gg_noc_free(ctx);
+  if (ctx->err_dev) hipFree(ctx->err_dev);
+  for (gg_timer& t : ctx->timers) { hipEventDestroy(t.start); hipEventDestroy(t.stop); }
+  delete ctx;
+}
+
+gg_status gg_reset(gg_ctx* ctx)
+{
+  if (!ctx) return gg_fail(GG_ERR_INVALID, "ctx NULL");
+  hipSetDevice(ctx->device);
+  hipStream_t s = ctx->last_stream;
+  if (gg_status st = gg_cache_state_reset(ctx, s)) return st;
+  if (gg_status st = gg_noc_reset(ctx, s)) return st;
+  GG_HIP(hipMemsetAsync(ctx->err_dev, 0, sizeof(uint32_t), s));
+  GG_HIP(hipStreamSynchronize(s));
+  return GG_OK;
+}
+
+static gg_status check_device_errors(gg_ctx* ctx)
+{
+  uint32_t e = 0;
+  GG_HIP(hipMemcpy(&e, ctx->err_dev, sizeof(e), hipMemcpyDeviceToHost));
+  if (e & GG_DERR_RANGE) return gg_fail(GG_ERR_RANGE, "a trace address is beyond the compressed-tag range (%#llx)",
+                                        (unsigned long long)ctx->g.addr_limit);
+  if (e & GG_DERR_STATE) return gg_fail(GG_ERR_STATE, "cache state the reference would reject (LOG_ASSERT_ERROR)");
+  return GG_OK;
+}
+
+gg_status gg_cache_access_batch(gg_ctx* ctx, const gg_trace* trace, uint32_t* result_dev,
+                                uint64_t* evicted_dev, void* stream)
+{
+  if (!ctx) return gg_fail(GG_ERR_INVALID, "ctx NULL");
+  hipSetDevice(ctx->device);
+  hipStream_t s = (hipStream_t)stream;
+  ctx->last_stream = s;
+  return gg_cache_run_batch(ctx, trace, result_dev, evicted_dev, s);
+}
+
+gg_status gg_cache_get_counters(gg_ctx* ctx, uint64_t* out)
+{
+  if (!ctx || !out) return gg_fail(GG_ERR_INVALID, "NULL argument");
+  hipSetDevice(ctx->device);
+  GG_HIP(hipStreamSynchronize(ctx->last_stream));
+  GG_HIP(hipMemcpy(out, ctx->cs.counters, sizeof(uint64_t) * ctx->g.tiles * 2 * GG_NUM_CACHE_COUNTERS,
+                   hipMemcpyDeviceToHost));
+  return check_device_errors(ctx);
+}
+
+gg_status gg_cache_get_line_info(gg_ctx* ctx, uint32_t tile, int level, uint64_t addr, gg_line_info* out)
+{
+  if (!ctx || !out) return gg_fail(GG_ERR_INVALID, "NULL argument");
+  hipSetDevice(ctx->device);
+  return gg_cache_quartet(ctx, 0, tile, level, addr, nullptr, out, nullptr, nullptr);
+}
+
+gg_status gg_cache_set_line_info(gg_ctx* ctx, uint32_t tile, int level, uint64_t addr, const gg_line_info* in)
+{
+  if (!ctx || !in) return gg_fail(GG_ERR_INVALID, "NULL argument");
+  hipSetDevice(ctx->device);
+  return gg_cache_quartet(ctx, 1, tile, level, addr, in, nullptr, nullptr, nullptr);
+}
+
+gg_status gg_cache_access_line(gg_ctx* ctx, uint32_t tile, int level, uint64_t addr, int is_store)
+{
+  if (!ctx) return gg_fail(GG_ERR_INVALID, "NULL argument");
+  hipSetDevice(ctx->device);
+  return gg_cache_quartet(ctx, is_store ? 3 : 2, tile, level, addr, nullptr, nullptr, nullptr, nullptr);
+}
+
+gg_status gg_cache_insert_line(gg_ctx* ctx, uint32_t tile, int level, uint64_t addr, const gg_line_info* in,
+                               int* eviction, uint64_t* evicted_addr, gg_line_info* evicted_info)
+{
+  if (!ctx || !in || !eviction || !evicted_addr || !evicted_info) return gg_fail(GG_ERR_INVALID, "NULL argument");
+  hipSetDevice(ctx->device);
+  return gg_cache_quartet(ctx, 4, tile, level, addr, in, evicted_info, eviction, evicted_addr);
+}
+
+gg_status gg_noc_route_batch(gg_ctx* ctx, const gg_packets* pk, const gg_packet_out* out, void* stream)
+{
+  if (!ctx || !pk || !out) return gg_fail(GG_ERR_INVALID, "NULL argument");
+  hipSetDevice(ctx->device);
+  hipStream_t s = (hipStream_t)stream;
+  ctx->last_stream = s;
+  return gg_noc_run(ctx, pk, out, s);
+}
+
+gg_status gg_noc_get_counters(gg_ctx* ctx, uint64_t* out)
+{
+  if (!ctx || !out) return gg_fail(GG_ERR_INVALID, "NULL argument");
+  hipSetDevice(ctx->device);
+  GG_HIP(hipStreamSynchronize(ctx->last_stream));
+  if (gg_status st = gg_noc_counters(ctx, out)) return st;
+  return check_device_errors(ctx);
+}
+
+gg_status gg_queue_delay_batch(gg_ctx* ctx, uint64_t min_processing_time, const uint64_t* pkt_time,
+                               const uint64_t* proc_time, uint64_t n, uint64_t* delay_out)
+{
+  if (!ctx || (n && (!pkt_time || !proc_time || !delay_out))) return gg_fail(GG_ERR_INVALID, "NULL argument");
+  hipSetDevice(ctx->device);
+  return gg_htree_run(ctx, min_processing_time, pkt_time, proc_time, n, delay_out);
+}
+
+float gg_kernel_time_ms(gg_ctx* ctx, const char* kernel)
+{
+  if (!ctx || !kernel) return -1.0f;
+  for (gg_timer& t : ctx->timers) {
+    if (t.name == kernel && t.valid) {
+      if (hipEventSynchronize(t.stop) != hipSuccess) return -1.0f;
+      float ms = -1.0f;
+      if (hipEventElapsedTime(&ms, t.start, t.stop) != hipSuccess) return -1.0f;
+      return ms;
+    }
+  }
+  return -1.0f;
+}
+
+void gg_set_timing(gg_ctx* ctx, int enabled) { if (ctx) ctx->timing = enabled != 0; }
+
+gg_status gg_gen_uniform_trace(uint64_t* addr_dev, uint32_t* meta_dev, uint32_t tile_begin, uint32_t tiles,
+                               uint64_t per_tile, uint64_t first, uint32_t lines_log2, uint32_t base_shift, void* stream)
+{
+  if (!addr_dev || !meta_dev || lines_log2 > 40) return gg_fail(GG_ERR_INVALID, "bad generator arguments");
+  const uint64_t n = (uint64_t)tiles * per_tile;
+  if (n == 0) return GG_OK;
+  hipLaunchKernelGGL(k_gen_uniform, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     addr_dev, meta_dev, tile_begin, tiles, per_tile, first, lines_log2, base_shift);
+  GG_HIP(hipGetLastError());
+  return GG_OK;
+}
+
+}  // extern "C"

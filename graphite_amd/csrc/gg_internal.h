@@ -1,0 +1,118 @@
+// gg_internal.h — shared definitions of the MI355X backend (host + device).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include <vector>
+
+#include "../../include/graphite_gpu.h"
+
+#define GG_WAVE 64
+
+// Packed meta byte of one cache line in the device-resident state:
+//   bits 0-1 state (0 I, 1 S, 2 M), bit 2 cached_loc == L1-D (L2 only),
+//   bits 3-7 replacement age (LRUReplacementPolicy::_lru_bits_vec entry).
+#define GG_MS_I 0u
+#define GG_MS_S 1u
+#define GG_MS_M 2u
+#define GG_M_STATE(b) ((b) & 3u)
+#define GG_M_LOC(b) (((b) >> 2) & 1u)
+#define GG_M_AGE(b) ((b) >> 3)
+#define GG_M_MAKE(st, loc, age) ((uint32_t)(st) | ((uint32_t)(loc) << 2) | ((uint32_t)(age) << 3))
+
+#define GG_L1_INV_TAG (~0ull)     // CacheLineInfo invalid tag (cache_line_info.h:21-22)
+#define GG_L2_INV_TAG 0xFFFFFFFFu // compressed L2 tag (line >> log2(L2 sets)); 2^32-1 is out of range
+
+// Error bits of the device-side error word (ctx->err_dev).
+#define GG_DERR_RANGE 1u   // address beyond the compressed-tag range
+#define GG_DERR_STATE 2u   // the reference would LOG_ASSERT_ERROR on this state
+
+// Geometry derived from gg_config (cache.cc:44, cache_hash_fn.h:11).
+struct gg_geom {
+  uint32_t tiles;
+  uint32_t log_line;
+  uint32_t u1;        // L1-D sets = units per tile
+  uint32_t log_u1;
+  uint32_t a1;        // L1-D ways
+  uint32_t l2_sets;
+  uint32_t log_l2;
+  uint32_t s2;        // L2 sets per unit (l2_sets / u1)
+  uint32_t a2;        // L2 ways
+  uint32_t mw;        // u64 meta words per L2 set ((a2 + 7) / 8)
+  uint32_t pol1, pol2;
+  uint64_t units;     // tiles * u1
+  uint64_t addr_limit;  // first byte address whose L2 tag no longer fits 32 bits
+};
+
+// Device-resident cache state, structure of arrays indexed [field][unit] so a
+// wave of 64 consecutive units loads/stores it coalesced.
+struct gg_cache_state {
+  uint64_t* l1_tag;   // [a1][units]      line address or ~0
+  uint64_t* l1_meta;  // [units]          byte w = meta of way w
+  uint8_t*  l1_rr;    // [units]          RoundRobin index
+  uint32_t* l2_tag;   // [s2*a2][units]   line >> log2(l2_sets) or 2^32-1
+  uint64_t* l2_meta;  // [s2*mw][units]   byte (w%8) of word w/8
+  uint8_t*  l2_rr;    // [s2][units]
+  uint64_t* counters; // [tiles][2][GG_NUM_CACHE_COUNTERS]
+};
+
+struct gg_timer {
+  std::string name;
+  hipEvent_t start = nullptr, stop = nullptr;
+  bool valid = false;
+};
+
+struct gg_noc_state;
+
+struct gg_ctx {
+  gg_config cfg;
+  gg_geom g;
+  int device = 0;
+  hipStream_t last_stream = nullptr;
+  gg_cache_state cs{};
+  uint32_t* err_dev = nullptr;
+  // batch scratch (grown on demand)
+  uint64_t* sh_key = nullptr;    // sharded records: line address | write bit
+  uint32_t* sh_idx = nullptr;    // record index within its tile
+  uint64_t  sh_cap = 0;
+  uint32_t* chunk_cnt = nullptr; // [chunks][u1]
+  uint32_t* chunk_tile = nullptr;
+  uint64_t* chunk_start = nullptr;
+  uint32_t* chunk_len = nullptr;
+  uint64_t  chunk_cap = 0;
+  uint32_t* unit_len = nullptr;  // [units]
+  uint64_t* unit_base = nullptr; // [units]
+  uint64_t* tile_off_dev = nullptr; // [tiles+1]
+  std::vector<uint32_t> h_chunk_tile, h_chunk_len;
+  std::vector<uint64_t> h_chunk_start;
+  // NoC
+  gg_noc_state* noc = nullptr;
+  // timing
+  bool timing = false;
+  std::vector<gg_timer> timers;
+};
+
+// error reporting (gg_capi.hip)
+gg_status gg_fail(gg_status code, const char* fmt, ...);
+gg_status gg_hip_check(hipError_t e, const char* what);
+#define GG_HIP(x) do { hipError_t _e = (x); if (_e != hipSuccess) return gg_hip_check(_e, #x); } while (0)
+
+// timing helpers (gg_capi.hip)
+void gg_timer_begin(gg_ctx* ctx, const char* name, hipStream_t s);
+void gg_timer_end(gg_ctx* ctx, const char* name, hipStream_t s);
+
+// cache path (gg_cache.hip)
+gg_status gg_cache_state_alloc(gg_ctx* ctx);
+void      gg_cache_state_free(gg_ctx* ctx);
+gg_status gg_cache_state_reset(gg_ctx* ctx, hipStream_t s);
+gg_status gg_cache_run_batch(gg_ctx* ctx, const gg_trace* tr, uint32_t* result, uint64_t* evicted, hipStream_t s);
+gg_status gg_cache_quartet(gg_ctx* ctx, int op, uint32_t tile, int level, uint64_t addr,
+                           const gg_line_info* in, gg_line_info* out, int* eviction, uint64_t* ev_addr);
+
+// NoC path (gg_noc.hip)
+gg_status gg_noc_alloc(gg_ctx* ctx);
+void      gg_noc_free(gg_ctx* ctx);
+gg_status gg_noc_reset(gg_ctx* ctx, hipStream_t s);
+gg_status gg_noc_run(gg_ctx* ctx, const gg_packets* pk, const gg_packet_out* out, hipStream_t s);
+gg_status gg_noc_counters(gg_ctx* ctx, uint64_t* out);
+gg_status gg_htree_run(gg_ctx* ctx, uint64_t min_proc, const uint64_t* t, const uint64_t* p, uint64_t n, uint64_t* d);

@@ -1,0 +1,682 @@
+// gg_noc.hip — EMesh packet latency on MI355X (gfx950).
+//
+// emesh_hop_counter (network_model_emesh_hop_counter.cc:143-157): a closed
+// form per packet, one thread per packet.
+//
+// emesh_hop_by_hop (network_model_emesh_hop_by_hop.cc:146-264) with
+// RouterModel output-port contention through QueueModelHistoryTree
+// (queue_model_history_tree.cc:44-126, interval_tree.cc, queue_model_m_g_1.cc).
+// Canonical order: every queue serves its packets in
+// (arrival time, packet index) order.  XY routing makes the port graph a DAG
+// — injection port -> X chain of the source row (LEFT or RIGHT ports) -> Y
+// chain of the destination column (DOWN or UP ports) -> SELF port of the
+// destination — so each stage runs its chains independently, one thread per
+// chain with a private (time, index) event heap, which reproduces the order of
+// one global event queue exactly.
+#include "gg_internal.h"
+
+#include <algorithm>
+
+namespace {
+
+enum { P_SELF = 0, P_LEFT, P_RIGHT, P_DOWN, P_UP, NPORTS };   // network_model_emesh_hop_by_hop.h:41-48
+
+// ---------------------------------------------------------------------------
+// history tree (interval_tree.cc:40-394 + queue_model_history_tree.cc:44-167)
+// ---------------------------------------------------------------------------
+struct HNode { uint64_t first, second; int16_t parent, left, right, height; };
+struct HQueue {
+  int32_t root; uint32_t size; int32_t free_tail; uint32_t max_size;
+  double sig_sq, sig; uint64_t n, newest;          // QueueModelMG1
+  uint64_t analytical;                              // _total_requests_using_analytical_model
+  uint64_t util, last_req, total_req;               // QueueModel utilization counters
+};
+
+struct HTree {
+  HQueue* q; HNode* nd; int16_t* fl; uint64_t min_proc; bool analytical;
+
+  __device__ int32_t h(int x) const { return x < 0 ? 0 : nd[x].height; }
+  __device__ void upd_child(int node, int child, int dir)      // updateChildPointer
+  {
+    if (node < 0) return;
+    if (dir == 0) { if (nd[node].first < nd[child].first) nd[node].right = child; else nd[node].left = child; }
+    else if (dir == 1) nd[node].left = child;
+    else nd[node].right = child;
+  }
+  __device__ void upd_parent(int node, int parent)             // updateParentPointer
+  {
+    if (node >= 0) nd[node].parent = parent;
+    if (parent < 0) q->root = node;
+  }
+  __device__ bool balanced(int x) const { int d = h(nd[x].left) - h(nd[x].right); return d >= -1 && d <= 1; }
+  __device__ void upd_height(int x) { int a = h(nd[x].left), b = h(nd[x].right); nd[x].height = (int16_t)((a > b ? a : b) + 1); }
+  __device__ void rotate(int y, bool cw)                       // performRotation
+  {
+    int x;
+    if (cw) {
+      x = nd[y].left;
+      upd_parent(x, nd[y].parent); upd_child(nd[x].parent, x, 0);
+      nd[y].left = nd[x].right; upd_parent(nd[y].left, y);
+      nd[x].right = (int16_t)y; upd_parent(y, x);
+    } else {
+      x = nd[y].right;
+      upd_parent(x, nd[y].parent); upd_child(nd[x].parent, x, 0);
+      nd[y].right = nd[x].left; upd_parent(nd[y].right, y);
+      nd[x].left = (int16_t)y; upd_parent(y, x);
+    }
+    upd_height(y); upd_height(x);
+  }
+  __device__ int balance(int z)                                // balanceHeight
+  {
+    int zl = nd[z].left, zr = nd[z].right;
+    bool y_left = h(zl) > h(zr);
+    int y = y_left ? zl : zr;
+    int yl = nd[y].left, yr = nd[y].right;
+    int x; bool x_left;
+    if (h(yl) != h(yr)) { x_left = h(yl) > h(yr); x = x_left ? yl : yr; }
+    else if (y_left) { x = yl; x_left = true; }
+    else { x = yr; x_left = false; }
+    if (y_left) {
+      if (!x_left) { rotate(y, false); rotate(z, true); return x; }
+      rotate(z, true); return y;
+    } else {
+      if (x_left) { rotate(y, true); rotate(z, false); return x; }
+      rotate(z, false); return y;
+    }
+  }
+  __device__ void rebalance(int r)                             // rebalanceAVLTree
+  {
+    while (r >= 0) {
+      int old = nd[r].height, nr = r;
+      if (!balanced(r)) nr = balance(r); else upd_height(r);
+      if (nd[nr].height == old) return;
+      r = nd[nr].parent;
+    }
+  }
+  __device__ void insert(int node)                             // insert / insertInTree
+  {
+    q->size++;
+    int r = q->root;
+    for (;;) {
+      if (nd[node].first < nd[r].first) {
+        if (nd[r].left >= 0) r = nd[r].left;
+        else { nd[r].left = (int16_t)node; nd[node].parent = (int16_t)r; rebalance(r); return; }
+      } else if (nd[node].first > nd[r].first) {
+        if (nd[r].right >= 0) r = nd[r].right;
+        else { nd[r].right = (int16_t)node; nd[node].parent = (int16_t)r; rebalance(r); return; }
+      } else return;   // duplicate key: the reference aborts (LOG_PRINT_ERROR)
+    }
+  }
+  __device__ int remove_rec(int node)                          // removeFromTree
+  {
+    if (nd[node].left < 0) {
+      int p = nd[node].parent;
+      if (p >= 0) upd_child(p, nd[node].right, (nd[p].first < nd[node].first) ? 2 : 1);
+      upd_parent(nd[node].right, p);
+      rebalance(p);
+      return node;
+    } else if (nd[node].right < 0) {
+      int p = nd[node].parent;
+      upd_child(p, nd[node].left, 0);
+      upd_parent(nd[node].left, p);
+      rebalance(p);
+      return node;
+    }
+    int succ = nd[node].right;
+    while (nd[succ].left >= 0) succ = nd[succ].left;           // findMinKeyNode
+    remove_rec(succ);                                          // successor has no left child
+    uint64_t f = nd[node].first, s = nd[node].second;          // swap key/interval
+    nd[node].first = nd[succ].first; nd[node].second = nd[succ].second;
+    nd[succ].first = f; nd[succ].second = s;
+    return succ;
+  }
+  __device__ int remove(int node) { q->size--; return remove_rec(node); }
+  __device__ int search(uint64_t a, uint64_t b) const          // searchTree
+  {
+    int stack[40]; int sp = 0; int n = q->root;
+    for (;;) {
+      if (n < 0) {
+        if (sp == 0) return -1;
+        n = stack[--sp];
+        if (a < nd[n].first && (nd[n].second - nd[n].first) >= (b - a)) return n;
+        n = nd[n].right; continue;
+      }
+      if (a >= nd[n].first && b <= nd[n].second) return n;
+      if (b < nd[n].first) { if (sp < 40) { stack[sp++] = n; n = nd[n].left; continue; } return -1; }
+      if (a < nd[n].first && (nd[n].second - nd[n].first) >= (b - a)) return n;
+      n = nd[n].right;
+    }
+  }
+  __device__ int alloc(uint64_t a, uint64_t b)                 // allocateNode
+  {
+    if (q->free_tail < 0) return -1;
+    int i = fl[q->free_tail--];
+    nd[i].first = a; nd[i].second = b; nd[i].parent = nd[i].left = nd[i].right = -1; nd[i].height = 1;
+    return i;
+  }
+  __device__ void release(int i) { fl[++q->free_tail] = (int16_t)i; }
+  __device__ uint64_t mg1_delay() const                         // QueueModelMG1::computeQueueDelay
+  {
+    if (q->n == 0) return 0;
+    double variance = (q->sig_sq / q->n) - ((q->sig / q->n) * (q->sig / q->n));
+    double service_rate = 1.0 / (q->sig / q->n);
+    double arrival_rate = ((double)q->n) / q->newest;
+    if (arrival_rate >= service_rate) arrival_rate = 0.999 * service_rate;
+    return (uint64_t)ceil(0.5 * service_rate * arrival_rate * ((1 / (service_rate * service_rate)) + variance) /
+                          (service_rate - arrival_rate));
+  }
+  __device__ uint64_t delay(uint64_t t, uint64_t p, uint32_t* err)   // computeQueueDelay
+  {
+    uint64_t qd = ~0ull;
+    int mn = search(0, 1);
+    if (q->size >= q->max_size) release(remove(mn));
+    mn = search(0, 1);
+    if (analytical && nd[mn].first > (t + p)) {
+      q->analytical++;
+      qd = mg1_delay();
+    } else {
+      int node = search(t, t + p);
+      if (node < 0) { atomicOr(err, GG_DERR_STATE); return 0; }
+      if (t >= nd[node].first) {
+        qd = 0;
+        if ((t - nd[node].first) >= min_proc) {
+          if ((nd[node].second - (t + p)) >= min_proc) {
+            int nx = alloc(t + p, nd[node].second);
+            if (nx < 0) { atomicOr(err, GG_DERR_STATE); return 0; }
+            insert(nx);
+          }
+          nd[node].second = t;
+        } else {
+          if ((nd[node].second - (t + p)) >= min_proc) nd[node].first = t + p;
+          else release(remove(node));
+        }
+      } else {
+        qd = nd[node].first - t;
+        if ((nd[node].second - (nd[node].first + p)) >= min_proc) nd[node].first = nd[node].first + p;
+        else release(remove(node));
+      }
+    }
+    q->sig_sq += (double)p * (double)p;                          // QueueModelMG1::updateQueue
+    q->sig += (double)p;
+    q->n++;
+    { uint64_t x = t + qd + p; if (x > q->newest) q->newest = x; }
+    q->util += p;                                                // updateQueueUtilizationCounters
+    { uint64_t x = t + qd + p; if (x > q->last_req) q->last_req = x; }
+    q->total_req++;
+    return qd;
+  }
+};
+
+__device__ __forceinline__ uint64_t lat_to_ps(uint64_t cycles, double f) { return (uint64_t)ceil(((double)1000 * cycles) / f); }
+__device__ __forceinline__ uint64_t time_to_cycles(uint64_t ps, double f) { return (uint64_t)ceil(((double)ps * f) / 1.0e3); }
+
+struct NocParams {
+  uint32_t tiles, w, h, flit_width, router_delay, link_delay, qm, analytical, max_size, net_model;
+  double f;
+};
+
+__device__ __forceinline__ uint64_t nflits(const NocParams& P, uint32_t bits)
+{
+  return (bits % P.flit_width == 0) ? bits / P.flit_width : bits / P.flit_width + 1;   // computeNumFlits
+}
+
+__device__ __forceinline__ void cadd(uint64_t* c, uint32_t tile, int k, uint64_t v)
+{
+  if (v) atomicAdd((unsigned long long*)&c[(uint64_t)tile * GG_NUM_NET_COUNTERS + k], (unsigned long long)v);
+}
+
+// ---------------------------------------------------------------------------
+// hop counter / magic: one thread per packet
+// ---------------------------------------------------------------------------
+__global__ void k_hop_counter(NocParams P, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                              const uint32_t* __restrict__ len, const uint64_t* __restrict__ t0, uint64_t n,
+                              uint64_t* arrival, uint64_t* zero_load, uint64_t* contention, uint64_t* ctr)
+{
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t s = src[k], d = dst[k], bits = len[k];
+  uint64_t t = t0[k], zl = 0;
+  if (s != d) {                                   // processCornerCases: self-sends cost nothing
+    if (P.net_model == GG_NET_MAGIC) {            // network_model_magic.cc: 0 flits, 1 cycle
+      cadd(ctr, s, GG_NC_PACKETS_SENT, 1); cadd(ctr, s, GG_NC_BITS_SENT, bits);
+      const uint64_t l = lat_to_ps(1, P.f);
+      t += l; zl += l;
+      cadd(ctr, d, GG_NC_PACKETS_RECEIVED, 1); cadd(ctr, d, GG_NC_BITS_RECEIVED, bits);
+      cadd(ctr, d, GG_NC_TOTAL_LATENCY_PS, zl);
+    } else {
+      const uint64_t nf = nflits(P, bits);
+      cadd(ctr, s, GG_NC_PACKETS_SENT, 1); cadd(ctr, s, GG_NC_FLITS_SENT, nf); cadd(ctr, s, GG_NC_BITS_SENT, bits);
+      const int sx = (int)(s % P.w), sy = (int)(s / P.w), dx = (int)(d % P.w), dy = (int)(d / P.w);
+      const uint64_t hops = (uint64_t)(abs(sx - dx) + abs(sy - dy));
+      const uint64_t lat = lat_to_ps(hops * ((uint64_t)P.router_delay + P.link_delay), P.f);
+      t += lat; zl += lat;
+      cadd(ctr, s, GG_NC_BUFFER_WRITES, nf * hops); cadd(ctr, s, GG_NC_BUFFER_READS, nf * hops);
+      cadd(ctr, s, GG_NC_SWITCH_ALLOC, hops); cadd(ctr, s, GG_NC_CROSSBAR, nf * hops);
+      cadd(ctr, s, GG_NC_LINK_TRAVERSALS, nf * hops);
+      const uint64_t ser = lat_to_ps(nf, P.f);    // processReceivedPacket
+      t += ser; zl += ser;
+      cadd(ctr, d, GG_NC_PACKETS_RECEIVED, 1); cadd(ctr, d, GG_NC_FLITS_RECEIVED, nf);
+      cadd(ctr, d, GG_NC_BITS_RECEIVED, bits); cadd(ctr, d, GG_NC_TOTAL_LATENCY_PS, zl);
+    }
+  }
+  arrival[k] = t; zero_load[k] = zl; contention[k] = 0;
+}
+
+// ---------------------------------------------------------------------------
+// hop-by-hop
+// ---------------------------------------------------------------------------
+struct Ev { uint64_t t; uint32_t id; uint32_t pad; };
+__device__ __forceinline__ bool ev_lt(const Ev& a, const Ev& b) { return a.t < b.t || (a.t == b.t && a.id < b.id); }
+__device__ void heap_push(Ev* h, uint32_t& n, Ev e)
+{
+  uint32_t i = n++;
+  while (i > 0) { uint32_t p = (i - 1) / 2; if (!ev_lt(e, h[p])) break; h[i] = h[p]; i = p; }
+  h[i] = e;
+}
+__device__ Ev heap_pop(Ev* h, uint32_t& n)
+{
+  Ev top = h[0], last = h[--n];
+  uint32_t i = 0;
+  for (;;) {
+    uint32_t l = 2 * i + 1, r = l + 1, m = i;
+    Ev cand = last;
+    if (l < n && ev_lt(h[l], cand)) { m = l; cand = h[l]; }
+    if (r < n && ev_lt(h[r], cand)) m = r;
+    if (m == i) break;
+    h[i] = h[m]; i = m;
+  }
+  if (n) h[i] = last;
+  return top;
+}
+
+struct NocDev {
+  NocParams P;
+  HQueue* q; HNode* nd; int16_t* fl;   // queue (tile*6 + port): ports 0..4 mesh, 5 injection
+  uint64_t* ctr;
+  uint32_t* err;
+  __device__ HTree tree(uint32_t tile, int port) const
+  {
+    const uint64_t qi = (uint64_t)tile * 6 + port;
+    HTree t{q + qi, nd + qi * P.max_size, fl + qi * P.max_size, 1, P.analytical != 0};
+    return t;
+  }
+};
+
+struct PktState {   // per-packet working state of the current batch
+  uint64_t* t; uint64_t* zl; uint64_t* ct; uint32_t* cur;
+};
+
+// Stage ids of a packet's chains
+__device__ __forceinline__ uint32_t xchain_of(const NocParams& P, uint32_t s, uint32_t d)
+{
+  const uint32_t sx = s % P.w, sy = s / P.w, dx = d % P.w;
+  if (dx == sx) return ~0u;
+  return sy * 2 + (dx > sx ? 1u : 0u);        // [row][LEFT=0, RIGHT=1]
+}
+__device__ __forceinline__ uint32_t ychain_of(const NocParams& P, uint32_t s, uint32_t d)
+{
+  const uint32_t sy = s / P.w, dx = d % P.w, dy = d / P.w;
+  if (dy == sy) return ~0u;
+  return dx * 2 + (dy > sy ? 1u : 0u);        // [col][DOWN=0, UP=1]
+}
+
+// one mesh router hop (RouterModel::processPacket + ElectricalLinkModel::processPacket + Hop)
+__device__ void mesh_hop(const NocDev& D, uint32_t tile, int port, uint32_t bits, uint64_t& t, uint64_t& zl, uint64_t& ct)
+{
+  const NocParams& P = D.P;
+  const uint64_t nf = nflits(P, bits);
+  uint64_t zlc = P.router_delay, qd = 0;
+  if (P.qm) {
+    HTree tr = D.tree(tile, port);
+    qd = tr.delay(time_to_cycles(t, P.f), nf, D.err);
+    cadd(D.ctr, tile, GG_NC_ROUTER_CONTENTION_CYCLES, qd);
+    cadd(D.ctr, tile, GG_NC_ROUTER_PACKETS, 1);
+  }
+  cadd(D.ctr, tile, GG_NC_BUFFER_WRITES, nf); cadd(D.ctr, tile, GG_NC_BUFFER_READS, nf);
+  cadd(D.ctr, tile, GG_NC_SWITCH_ALLOC, 1); cadd(D.ctr, tile, GG_NC_CROSSBAR, nf);
+  zlc += P.link_delay;
+  cadd(D.ctr, tile, GG_NC_LINK_TRAVERSALS, nf);
+  const uint64_t zps = lat_to_ps(zlc, P.f), cps = lat_to_ps(qd, P.f);
+  t += zps + cps; zl += zps; ct += cps;
+}
+
+// Stage 0: injection port of each source tile, packets in (time, index) order.
+__global__ void k_inject(NocDev D, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                         const uint32_t* __restrict__ len, const uint64_t* __restrict__ bucket_off,
+                         const uint32_t* __restrict__ bucket_ids, Ev* heap, PktState S)
+{
+  const uint32_t tile = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tile >= D.P.tiles) return;
+  const uint64_t b = bucket_off[tile], e = bucket_off[tile + 1];
+  Ev* h = heap + b;
+  uint32_t n = 0;
+  for (uint64_t i = b; i < e; ++i) { uint32_t k = bucket_ids[i]; heap_push(h, n, Ev{S.t[k], k, 0}); }
+  HTree tr = D.tree(tile, 5);
+  while (n) {
+    Ev ev = heap_pop(h, n);
+    const uint32_t k = ev.id;
+    const uint64_t nf = nflits(D.P, len[k]);
+    cadd(D.ctr, tile, GG_NC_PACKETS_SENT, 1); cadd(D.ctr, tile, GG_NC_FLITS_SENT, nf);
+    cadd(D.ctr, tile, GG_NC_BITS_SENT, len[k]);
+    uint64_t qd = 0;
+    if (D.P.qm) qd = tr.delay(time_to_cycles(S.t[k], D.P.f), nf, D.err);   // injection router: delay 0
+    const uint64_t cps = lat_to_ps(qd, D.P.f);
+    S.t[k] += lat_to_ps(0, D.P.f) + cps;
+    S.ct[k] += cps;
+  }
+}
+
+// Stages X and Y: one thread per chain; ports along the chain in (time, index) order.
+__global__ void k_chain(NocDev D, int stage, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                        const uint32_t* __restrict__ len, const uint64_t* __restrict__ bucket_off,
+                        const uint32_t* __restrict__ bucket_ids, Ev* heap, PktState S, uint32_t nchains)
+{
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nchains) return;
+  const NocParams& P = D.P;
+  const uint64_t b = bucket_off[c], e = bucket_off[c + 1];
+  Ev* h = heap + b;
+  uint32_t n = 0;
+  for (uint64_t i = b; i < e; ++i) { uint32_t k = bucket_ids[i]; heap_push(h, n, Ev{S.t[k], k, 0}); }
+  while (n) {
+    Ev ev = heap_pop(h, n);
+    const uint32_t k = ev.id;
+    const uint32_t cur = S.cur[k], d = dst[k];
+    const uint32_t cx = cur % P.w, cy = cur / P.w, dx = d % P.w, dy = d / P.w;
+    int port; uint32_t next; bool done;
+    if (stage == 0) {                       // X: LEFT / RIGHT until the destination column
+      port = (cx > dx) ? P_LEFT : P_RIGHT;
+      next = (cx > dx) ? cur - 1 : cur + 1;
+      done = (next % P.w) == dx;
+    } else {                                // Y: DOWN / UP until the destination row
+      port = (cy > dy) ? P_DOWN : P_UP;
+      next = (cy > dy) ? cur - P.w : cur + P.w;
+      done = (next / P.w) == dy;
+    }
+    uint64_t t = S.t[k], zl = S.zl[k], ct = S.ct[k];
+    mesh_hop(D, cur, port, len[k], t, zl, ct);
+    S.t[k] = t; S.zl[k] = zl; S.ct[k] = ct; S.cur[k] = next;
+    if (!done) heap_push(h, n, Ev{t, k, 0});
+    (void)cx; (void)cy;
+  }
+}
+
+// Final stage: SELF port of each destination + receive (processReceivedPacket).
+__global__ void k_self(NocDev D, const uint32_t* __restrict__ dst, const uint32_t* __restrict__ len,
+                       const uint64_t* __restrict__ bucket_off, const uint32_t* __restrict__ bucket_ids,
+                       Ev* heap, PktState S)
+{
+  const uint32_t tile = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tile >= D.P.tiles) return;
+  const uint64_t b = bucket_off[tile], e = bucket_off[tile + 1];
+  Ev* h = heap + b;
+  uint32_t n = 0;
+  for (uint64_t i = b; i < e; ++i) { uint32_t k = bucket_ids[i]; heap_push(h, n, Ev{S.t[k], k, 0}); }
+  while (n) {
+    Ev ev = heap_pop(h, n);
+    const uint32_t k = ev.id;
+    uint64_t t = S.t[k], zl = S.zl[k], ct = S.ct[k];
+    mesh_hop(D, tile, P_SELF, len[k], t, zl, ct);
+    const uint64_t nf = nflits(D.P, len[k]);
+    const uint64_t ser = lat_to_ps(nf, D.P.f);
+    t += ser; zl += ser;
+    cadd(D.ctr, tile, GG_NC_PACKETS_RECEIVED, 1); cadd(D.ctr, tile, GG_NC_FLITS_RECEIVED, nf);
+    cadd(D.ctr, tile, GG_NC_BITS_RECEIVED, len[k]);
+    cadd(D.ctr, tile, GG_NC_TOTAL_LATENCY_PS, zl + ct); cadd(D.ctr, tile, GG_NC_TOTAL_CONTENTION_PS, ct);
+    S.t[k] = t; S.zl[k] = zl; S.ct[k] = ct;
+  }
+}
+
+// bucket keys: 0 = injection (src tile), 1 = X chain, 2 = Y chain, 3 = SELF (dst tile); ~0 = not in stage
+__global__ void k_keys(NocParams P, int stage, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                       uint64_t n, uint32_t* keys, uint32_t* counts, uint32_t* err)
+{
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t s = src[k], d = dst[k];
+  if (s >= P.tiles || d >= P.tiles) { atomicOr(err, GG_DERR_RANGE); keys[k] = ~0u; return; }
+  uint32_t key = ~0u;
+  if (s != d) {
+    if (stage == 0) key = s;
+    else if (stage == 1) key = xchain_of(P, s, d);
+    else if (stage == 2) key = ychain_of(P, s, d);
+    else key = d;
+  }
+  keys[k] = key;
+  if (key != ~0u) atomicAdd(&counts[key], 1u);
+}
+
+__global__ void k_scan_counts(const uint32_t* counts, uint32_t nb, uint64_t* off, uint32_t* cursor)
+{
+  // single block; nb is small (<= 2 * 4096)
+  __shared__ uint64_t part[1024];
+  const uint32_t t = threadIdx.x, per = (nb + blockDim.x - 1) / blockDim.x;
+  uint64_t s = 0;
+  for (uint32_t i = t * per; i < min(nb, (t + 1) * per); ++i) s += counts[i];
+  part[t] = s;
+  __syncthreads();
+  if (t == 0) { uint64_t a = 0; for (uint32_t i = 0; i < blockDim.x; ++i) { uint64_t v = part[i]; part[i] = a; a += v; } off[nb] = a; }
+  __syncthreads();
+  uint64_t a = part[t];
+  for (uint32_t i = t * per; i < min(nb, (t + 1) * per); ++i) { off[i] = a; cursor[i] = 0; a += counts[i]; }
+}
+
+__global__ void k_bucket(const uint32_t* __restrict__ keys, uint64_t n, const uint64_t* __restrict__ off,
+                         uint32_t* cursor, uint32_t* ids)
+{
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t key = keys[k];
+  if (key == ~0u) return;
+  ids[off[key] + atomicAdd(&cursor[key], 1u)] = (uint32_t)k;
+}
+
+__global__ void k_init_pkts(const uint32_t* __restrict__ src, const uint64_t* __restrict__ t0, uint64_t n, PktState S)
+{
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  S.t[k] = t0[k]; S.zl[k] = 0; S.ct[k] = 0; S.cur[k] = src[k];
+}
+
+__global__ void k_htree_reset(HQueue* q, HNode* nd, int16_t* fl, uint64_t nq, uint32_t max_size)
+{
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nq) return;
+  HQueue Q{};
+  Q.max_size = max_size;
+  int16_t* f = fl + i * max_size;
+  for (uint32_t j = 0; j < max_size; ++j) f[j] = (int16_t)j;        // allocateMemory
+  Q.free_tail = (int32_t)max_size - 1;
+  HNode* N = nd + i * max_size;
+  const int r = f[Q.free_tail--];                                   // allocateNode(PAIR(0, UINT64_MAX))
+  N[r].first = 0; N[r].second = ~0ull; N[r].parent = N[r].left = N[r].right = -1; N[r].height = 1;
+  Q.root = r; Q.size = 1;
+  q[i] = Q;
+}
+
+__global__ void k_htree_seq(HQueue* q, HNode* nd, int16_t* fl, uint64_t min_proc, uint32_t analytical,
+                            const uint64_t* t, const uint64_t* p, uint64_t n, uint64_t* d, uint32_t* err)
+{
+  HTree tr{q, nd, fl, min_proc, analytical != 0};
+  for (uint64_t i = 0; i < n; ++i) d[i] = tr.delay(t[i], p[i], err);
+}
+
+__global__ void k_analytical(const HQueue* q, uint32_t tiles, uint64_t* ctr)
+{
+  const uint32_t tile = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tile >= tiles) return;
+  uint64_t a = 0;
+  for (int p = 0; p < NPORTS; ++p) a += q[(uint64_t)tile * 6 + p].analytical;
+  ctr[(uint64_t)tile * GG_NUM_NET_COUNTERS + GG_NC_ANALYTICAL_REQUESTS] = a;
+}
+
+}  // namespace
+
+struct gg_noc_state {
+  NocParams P;
+  HQueue* q = nullptr; HNode* nd = nullptr; int16_t* fl = nullptr; uint64_t nq = 0;
+  uint64_t* ctr = nullptr;
+  // batch scratch
+  uint64_t cap = 0;
+  uint64_t *t = nullptr, *zl = nullptr, *ct = nullptr;
+  uint32_t *cur = nullptr, *keys = nullptr, *ids = nullptr;
+  Ev* heap = nullptr;
+  uint32_t* counts = nullptr; uint32_t* cursor = nullptr; uint64_t* off = nullptr; uint32_t nb_cap = 0;
+};
+
+gg_status gg_noc_alloc(gg_ctx* ctx)
+{
+  gg_noc_state* S = new gg_noc_state();
+  ctx->noc = S;
+  const gg_config& c = ctx->cfg;
+  NocParams& P = S->P;
+  P.tiles = c.num_tiles;
+  P.w = (uint32_t)floor(sqrt((double)c.num_tiles));               // hop_counter.cc:18-19
+  P.h = (uint32_t)ceil(1.0 * c.num_tiles / P.w);
+  P.flit_width = c.flit_width ? c.flit_width : 64;
+  P.router_delay = c.router_delay;
+  P.link_delay = c.link_delay;
+  P.qm = c.queue_model_enabled;
+  P.analytical = c.analytical_enabled;
+  P.max_size = c.max_list_size ? c.max_list_size : 100;
+  P.net_model = c.net_model;
+  P.f = c.frequency_ghz;
+  if (P.max_size > 32767) return gg_fail(GG_ERR_UNSUPPORTED, "max_list_size too large");
+  GG_HIP(hipMalloc((void**)&S->ctr, sizeof(uint64_t) * c.num_tiles * GG_NUM_NET_COUNTERS));
+  // one history tree per mesh output port (5) + the injection port, per tile; the
+  // stand-alone gg_queue_delay_batch queue lives at index tiles*6
+  S->nq = (uint64_t)c.num_tiles * 6 + 1;
+  GG_HIP(hipMalloc((void**)&S->q, sizeof(HQueue) * S->nq));
+  GG_HIP(hipMalloc((void**)&S->nd, sizeof(HNode) * S->nq * P.max_size));
+  GG_HIP(hipMalloc((void**)&S->fl, sizeof(int16_t) * S->nq * P.max_size));
+  return GG_OK;
+}
+
+void gg_noc_free(gg_ctx* ctx)
+{
+  gg_noc_state* S = ctx->noc;
+  if (!S) return;
+  void* ps[] = {S->q, S->nd, S->fl, S->ctr, S->t, S->zl, S->ct, S->cur, S->keys, S->ids, S->heap,
+                S->counts, S->cursor, S->off};
+  for (void* p : ps) if (p) hipFree(p);
+  delete S;
+  ctx->noc = nullptr;
+}
+
+gg_status gg_noc_reset(gg_ctx* ctx, hipStream_t s)
+{
+  gg_noc_state* S = ctx->noc;
+  GG_HIP(hipMemsetAsync(S->ctr, 0, sizeof(uint64_t) * S->P.tiles * GG_NUM_NET_COUNTERS, s));
+  hipLaunchKernelGGL(k_htree_reset, dim3((uint32_t)((S->nq + 255) / 256)), dim3(256), 0, s, S->q, S->nd, S->fl,
+                     S->nq, S->P.max_size);
+  GG_HIP(hipGetLastError());
+  return GG_OK;
+}
+
+static gg_status noc_grow(gg_noc_state* S, uint64_t n, uint32_t nb)
+{
+  if (n > S->cap) {
+    void* ps[] = {S->t, S->zl, S->ct, S->cur, S->keys, S->ids, S->heap};
+    for (void* p : ps) if (p) hipFree(p);
+    uint64_t c = n + n / 4 + 1024;
+    GG_HIP(hipMalloc((void**)&S->t, 8 * c)); GG_HIP(hipMalloc((void**)&S->zl, 8 * c));
+    GG_HIP(hipMalloc((void**)&S->ct, 8 * c)); GG_HIP(hipMalloc((void**)&S->cur, 4 * c));
+    GG_HIP(hipMalloc((void**)&S->keys, 4 * c)); GG_HIP(hipMalloc((void**)&S->ids, 4 * c));
+    GG_HIP(hipMalloc((void**)&S->heap, sizeof(Ev) * c));
+    S->cap = c;
+  }
+  if (nb > S->nb_cap) {
+    if (S->counts) { hipFree(S->counts); hipFree(S->cursor); hipFree(S->off); }
+    GG_HIP(hipMalloc((void**)&S->counts, 4 * (nb + 1)));
+    GG_HIP(hipMalloc((void**)&S->cursor, 4 * (nb + 1)));
+    GG_HIP(hipMalloc((void**)&S->off, 8 * (nb + 1)));
+    S->nb_cap = nb;
+  }
+  return GG_OK;
+}
+
+gg_status gg_noc_run(gg_ctx* ctx, const gg_packets* pk, const gg_packet_out* out, hipStream_t s)
+{
+  gg_noc_state* S = ctx->noc;
+  const NocParams& P = S->P;
+  const uint64_t n = pk->num_packets;
+  if (n == 0) return GG_OK;
+  if (!pk->src_dev || !pk->dst_dev || !pk->length_bits_dev || !pk->time_ps_dev ||
+      !out->arrival_ps_dev || !out->zero_load_ps_dev || !out->contention_ps_dev)
+    return gg_fail(GG_ERR_INVALID, "NULL packet or output pointer");
+  if (n >= (1ull << 32)) return gg_fail(GG_ERR_RANGE, "batch larger than 2^32 packets");
+  const uint32_t blocks = (uint32_t)((n + 255) / 256);
+  if (P.net_model == GG_NET_MAGIC || P.net_model == GG_NET_EMESH_HOP_COUNTER) {
+    gg_timer_begin(ctx, "noc_hop_counter", s);
+    hipLaunchKernelGGL(k_hop_counter, dim3(blocks), dim3(256), 0, s, P, pk->src_dev, pk->dst_dev,
+                       pk->length_bits_dev, pk->time_ps_dev, n, out->arrival_ps_dev, out->zero_load_ps_dev,
+                       out->contention_ps_dev, S->ctr);
+    GG_HIP(hipGetLastError());
+    gg_timer_end(ctx, "noc_hop_counter", s);
+    return GG_OK;
+  }
+  if (P.net_model != GG_NET_EMESH_HOP_BY_HOP) return gg_fail(GG_ERR_UNSUPPORTED, "network model %u", P.net_model);
+  if (P.w * P.h != P.tiles) return gg_fail(GG_ERR_UNSUPPORTED, "emesh_hop_by_hop needs a full W x H mesh (hop_by_hop.cc:55-59)");
+  const uint32_t nb_max = std::max(P.tiles, 2 * std::max(P.w, P.h));
+  if (gg_status st = noc_grow(S, n, nb_max)) return st;
+  NocDev D{P, S->q, S->nd, S->fl, S->ctr, ctx->err_dev};
+  PktState PS{S->t, S->zl, S->ct, S->cur};
+  gg_timer_begin(ctx, "noc_hop_by_hop", s);
+  hipLaunchKernelGGL(k_init_pkts, dim3(blocks), dim3(256), 0, s, pk->src_dev, pk->time_ps_dev, n, PS);
+  for (int stage = 0; stage < 4; ++stage) {
+    const uint32_t nb = (stage == 0 || stage == 3) ? P.tiles : (stage == 1 ? 2 * P.h : 2 * P.w);
+    GG_HIP(hipMemsetAsync(S->counts, 0, 4 * (nb + 1), s));
+    hipLaunchKernelGGL(k_keys, dim3(blocks), dim3(256), 0, s, P, stage, pk->src_dev, pk->dst_dev, n, S->keys,
+                       S->counts, ctx->err_dev);
+    hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, S->counts, nb, S->off, S->cursor);
+    hipLaunchKernelGGL(k_bucket, dim3(blocks), dim3(256), 0, s, S->keys, n, S->off, S->cursor, S->ids);
+    const uint32_t tb = (nb + 63) / 64;
+    if (stage == 0)
+      hipLaunchKernelGGL(k_inject, dim3(tb), dim3(64), 0, s, D, pk->src_dev, pk->dst_dev, pk->length_bits_dev,
+                         S->off, S->ids, S->heap, PS);
+    else if (stage == 3)
+      hipLaunchKernelGGL(k_self, dim3(tb), dim3(64), 0, s, D, pk->dst_dev, pk->length_bits_dev, S->off, S->ids,
+                         S->heap, PS);
+    else
+      hipLaunchKernelGGL(k_chain, dim3(tb), dim3(64), 0, s, D, stage - 1, pk->src_dev, pk->dst_dev,
+                         pk->length_bits_dev, S->off, S->ids, S->heap, PS, nb);
+    GG_HIP(hipGetLastError());
+  }
+  gg_timer_end(ctx, "noc_hop_by_hop", s);
+  GG_HIP(hipMemcpyAsync(out->arrival_ps_dev, S->t, 8 * n, hipMemcpyDeviceToDevice, s));
+  GG_HIP(hipMemcpyAsync(out->zero_load_ps_dev, S->zl, 8 * n, hipMemcpyDeviceToDevice, s));
+  GG_HIP(hipMemcpyAsync(out->contention_ps_dev, S->ct, 8 * n, hipMemcpyDeviceToDevice, s));
+  return GG_OK;
+}
+
+gg_status gg_noc_counters(gg_ctx* ctx, uint64_t* out)
+{
+  gg_noc_state* S = ctx->noc;
+  if (S->P.net_model == GG_NET_EMESH_HOP_BY_HOP && S->P.qm) {
+    hipLaunchKernelGGL(k_analytical, dim3((S->P.tiles + 63) / 64), dim3(64), 0, ctx->last_stream, S->q, S->P.tiles, S->ctr);
+    GG_HIP(hipGetLastError());
+    GG_HIP(hipStreamSynchronize(ctx->last_stream));
+  }
+  GG_HIP(hipMemcpy(out, S->ctr, sizeof(uint64_t) * S->P.tiles * GG_NUM_NET_COUNTERS, hipMemcpyDeviceToHost));
+  return GG_OK;
+}
+
+gg_status gg_htree_run(gg_ctx* ctx, uint64_t min_proc, const uint64_t* t, const uint64_t* p, uint64_t n, uint64_t* d)
+{
+  gg_noc_state* S = ctx->noc;
+  hipStream_t s = ctx->last_stream;
+  const uint64_t qi = (uint64_t)S->P.tiles * 6;   // the stand-alone queue
+  hipLaunchKernelGGL(k_htree_reset, dim3(1), dim3(1), 0, s, S->q + qi, S->nd + qi * S->P.max_size,
+                     S->fl + qi * S->P.max_size, 1ull, S->P.max_size);
+  uint64_t* buf = nullptr;
+  GG_HIP(hipMalloc((void**)&buf, 24 * (n ? n : 1)));
+  GG_HIP(hipMemcpyAsync(buf, t, 8 * n, hipMemcpyHostToDevice, s));
+  GG_HIP(hipMemcpyAsync(buf + n, p, 8 * n, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_htree_seq, dim3(1), dim3(1), 0, s, S->q + qi, S->nd + qi * S->P.max_size,
+                     S->fl + qi * S->P.max_size, min_proc, S->P.analytical, buf, buf + n, n, buf + 2 * n, ctx->err_dev);
+  GG_HIP(hipGetLastError());
+  GG_HIP(hipMemcpyAsync(d, buf + 2 * n, 8 * n, hipMemcpyDeviceToHost, s));
+  GG_HIP(hipStreamSynchronize(s));
+  hipFree(buf);
+  return GG_OK;
+}

@@ -234,6 +234,16 @@ gg_status gg_queue_delay_batch(gg_ctx* ctx, uint64_t min_processing_time,
                                const uint64_t* pkt_time, const uint64_t* proc_time,
                                uint64_t n, uint64_t* delay_out);
 
+/* Synthetic workload generator (not part of the reference boundary; the
+ * reference has no trace capture): fills a tile-major trace of
+ * `per_tile` records for tiles [tile_begin, tile_begin + tiles) with the
+ * configs[1] generator of DESIGN.md §Workloads — record i of tile t is
+ * z = SplitMix64(0x9E3779B97F4A7C15 ^ t) step first+i+1, line = z mod 2^lines_log2
+ * at byte base t << base_shift, WRITE iff (z >> 32) % 3 == 0.                */
+gg_status gg_gen_uniform_trace(uint64_t* addr_dev, uint32_t* meta_dev, uint32_t tile_begin,
+                               uint32_t tiles, uint64_t per_tile, uint64_t first,
+                               uint32_t lines_log2, uint32_t base_shift, void* stream);
+
 /* Device time (ms) of the most recent launch of a named kernel
  * ("cache_replay", "cache_shard", "noc_hop_counter", ...), measured with HIP
  * events on the stream the kernel ran on; negative if not launched.           */

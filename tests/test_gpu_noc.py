@@ -1,0 +1,111 @@
+"""Parity of the HIP NoC models and the history-tree queue model with the
+reference KAT / fixtures and the CPU oracle.  Bit-exact."""
+import numpy as np
+import pytest
+
+from graphite_amd import config as C
+from graphite_amd import backend as B
+from oracle import pyoracle as po
+from golden_util import manifest, load
+from gpu_util import torch_dev, to_dev, to_np
+from test_oracle_golden import KAT
+
+pytestmark = pytest.mark.gpu
+M = manifest()
+
+
+def test_history_tree_kat_on_gpu():
+    torch_dev()
+    be = B.Backend(C.default_config(4))
+    d = be.queue_delay_batch([t for t, _, _ in KAT], [p for _, p, _ in KAT])
+    assert d.tolist() == [x for _, _, x in KAT]
+
+
+@pytest.mark.parametrize("name", [k for k, v in M.items() if v["kind"] == "htree"])
+def test_history_tree_fixtures_on_gpu(name):
+    torch_dev()
+    e = M[name]
+    rows = load(e["file"], np.uint64).reshape(-1, 3)
+    be = B.Backend(C.default_config(4, max_list_size=e["max_list_size"], analytical_enabled=int(e["analytical"])))
+    np.testing.assert_array_equal(be.queue_delay_batch(rows[:, 0], rows[:, 1]), rows[:, 2])
+
+
+def packets(T, n, seed, span_ps, self_frac=0.05):
+    rng = np.random.default_rng(seed)
+    src = rng.integers(0, T, n).astype(np.uint32)
+    dst = rng.integers(0, T, n).astype(np.uint32)
+    self_m = rng.random(n) < self_frac
+    dst[self_m] = src[self_m]
+    bits = np.where(rng.random(n) < 0.5, C.shmem_modeled_bits(T, False),
+                    C.shmem_modeled_bits(T, True)).astype(np.uint32)
+    t = np.sort(rng.integers(0, span_ps, n)).astype(np.uint64)
+    t[rng.random(n) < 0.1] += np.uint64(7)                          # some out-of-order times
+    return src, dst, bits, t
+
+
+def run_noc(torch, cfg, src, dst, bits, t, batches=1):
+    be = B.Backend(cfg)
+    n = len(src)
+    outs = [np.zeros(n, np.uint64) for _ in range(3)]
+    cuts = [n * k // batches for k in range(batches + 1)]
+    for k in range(batches):
+        sl = slice(cuts[k], cuts[k + 1])
+        m = cuts[k + 1] - cuts[k]
+        dev = [to_dev(torch, src[sl], torch.int32), to_dev(torch, dst[sl], torch.int32),
+               to_dev(torch, bits[sl], torch.int32), to_dev(torch, t[sl], torch.int64)]
+        o = [torch.zeros(m, dtype=torch.int64, device="cuda") for _ in range(3)]
+        be.noc_route_batch(*dev, *o)
+        torch.cuda.synchronize()
+        for i in range(3):
+            outs[i][sl] = to_np(o[i], np.uint64)
+    return be, outs
+
+
+def oracle_noc(cfg, src, dst, bits, t, batches=1):
+    on = po.OracleNoc(cfg)
+    n = len(src)
+    outs = [np.zeros(n, np.uint64) for _ in range(3)]
+    cuts = [n * k // batches for k in range(batches + 1)]
+    for k in range(batches):
+        sl = slice(cuts[k], cuts[k + 1])
+        r = on.route(src[sl], dst[sl], bits[sl], t[sl])
+        for i in range(3):
+            outs[i][sl] = r[i]
+    return on, outs
+
+
+@pytest.mark.parametrize("T", [16, 64, 1024])
+def test_hop_counter_matches_oracle(T):
+    torch = torch_dev()
+    cfg = C.default_config(T, net_model=C.NET_EMESH_HOP_COUNTER)
+    src, dst, bits, t = packets(T, 50000, T, 10 ** 9)
+    be, got = run_noc(torch, cfg, src, dst, bits, t)
+    on, ref = oracle_noc(cfg, src, dst, bits, t)
+    for g, r in zip(got, ref):
+        np.testing.assert_array_equal(g, r)
+    np.testing.assert_array_equal(be.noc_counters(), on.counters())
+
+
+@pytest.mark.parametrize("T,n,span,batches", [(16, 4000, 200000, 1), (64, 20000, 2000000, 2),
+                                              (256, 30000, 1000000, 1), (64, 30000, 100000, 3)])
+def test_hop_by_hop_matches_oracle(T, n, span, batches):
+    torch = torch_dev()
+    cfg = C.default_config(T, net_model=C.NET_EMESH_HOP_BY_HOP)
+    src, dst, bits, t = packets(T, n, T + n, span)
+    be, got = run_noc(torch, cfg, src, dst, bits, t, batches)
+    on, ref = oracle_noc(cfg, src, dst, bits, t, batches)
+    for g, r in zip(got, ref):
+        np.testing.assert_array_equal(g, r)
+    np.testing.assert_array_equal(be.noc_counters(), on.counters())
+    assert int(ref[2].sum()) > 0                                   # contention was exercised
+
+
+def test_hop_by_hop_without_queue_model():
+    torch = torch_dev()
+    cfg = C.default_config(64, net_model=C.NET_EMESH_HOP_BY_HOP, queue_model_enabled=0)
+    src, dst, bits, t = packets(64, 5000, 3, 100000)
+    be, got = run_noc(torch, cfg, src, dst, bits, t)
+    on, ref = oracle_noc(cfg, src, dst, bits, t)
+    for g, r in zip(got, ref):
+        np.testing.assert_array_equal(g, r)
+    assert int(ref[2].sum()) == 0
