@@ -106,21 +106,6 @@ __device__ __forceinline__ uint32_t ms_to_cstate(uint32_t st) { return st == GG_
 // Storage views of the L2 sets of one unit: LDS (replay) or HBM (quartet).
 // ---------------------------------------------------------------------------
 template <int A2>
-struct L2Lds {
-  static constexpr int MW = (A2 + 7) / 8;
-  uint32_t* T;   // [s*A2 + w][64]
-  uint64_t* M;   // [(s*64 + lane)*MW + k]
-  uint8_t*  R;   // [s][64]
-  uint32_t lane;
-  __device__ uint32_t tag(uint32_t s, uint32_t w) const { return T[(s * A2 + w) * GG_WAVE + lane]; }
-  __device__ void set_tag(uint32_t s, uint32_t w, uint32_t v) { T[(s * A2 + w) * GG_WAVE + lane] = v; }
-  __device__ uint64_t meta(uint32_t s, uint32_t k) const { return M[(s * GG_WAVE + lane) * MW + k]; }
-  __device__ void set_meta(uint32_t s, uint32_t k, uint64_t v) { M[(s * GG_WAVE + lane) * MW + k] = v; }
-  __device__ uint32_t rr(uint32_t s) const { return R[s * GG_WAVE + lane]; }
-  __device__ void set_rr(uint32_t s, uint32_t v) { R[s * GG_WAVE + lane] = (uint8_t)v; }
-};
-
-template <int A2>
 struct L2Hbm {
   static constexpr int MW = (A2 + 7) / 8;
   gg_cache_state cs; uint64_t units, u;
@@ -130,249 +115,6 @@ struct L2Hbm {
   __device__ void set_meta(uint32_t s, uint32_t k, uint64_t v) { cs.l2_meta[(uint64_t)(s * MW + k) * units + u] = v; }
   __device__ uint32_t rr(uint32_t s) const { return cs.l2_rr[(uint64_t)s * units + u]; }
   __device__ void set_rr(uint32_t s, uint32_t v) { cs.l2_rr[(uint64_t)s * units + u] = (uint8_t)v; }
-};
-
-// ---------------------------------------------------------------------------
-// One unit (tile, L1-D set): L1-D set in registers + its L2 sets in a store.
-// ---------------------------------------------------------------------------
-template <int A1, int A2, class Store>
-struct Unit {
-  static constexpr int MW = (A2 + 7) / 8;
-  uint64_t t1[A1];        // L1-D line numbers (~0 = invalid)
-  uint64_t m1;            // L1-D meta bytes
-  uint32_t rr1;           // L1-D round-robin index
-  uint32_t c1[NC], c2[NC];
-  uint32_t err;
-  Store st;
-  uint32_t l1set, log_u1, s2, log_l2, pol1, pol2;
-
-  // ---- L1-D (Cache "L1-D", WRITE_THROUGH: l1_cache_cntlr.cc:55-71) ----
-  __device__ int l1_find(uint64_t line) const
-  {
-    int w1 = -1;   // CacheSet::find scans high -> low; tags are unique
-#pragma unroll
-    for (int w = 0; w < A1; ++w) if (t1[w] == line) w1 = w;
-    return w1;
-  }
-  __device__ void l1_policy_update(uint32_t way) { if (pol1 == GG_POLICY_LRU) lru_update<1>(&m1, way); }
-
-  // L1CacheCntlr::invalidateCacheLine (l1_cache_cntlr.cc:293-305)
-  __device__ bool l1_invalidate(uint64_t line)
-  {
-    c1[TR]++;
-    const int w = l1_find(line);
-    if (w < 0) return false;
-#pragma unroll
-    for (int k = 0; k < A1; ++k) if (k == w) t1[k] = GG_L1_INV_TAG;
-    uint64_t mw = m1; meta_set_byte(&mw, (uint32_t)w, meta_byte(&mw, (uint32_t)w) & ~7u); m1 = mw;
-    c1[TW]++;
-    return true;
-  }
-
-  // ---- L2 (Cache "L2", WRITE_BACK) ----
-  __device__ uint32_t l2_set_of(uint64_t line) const { return (uint32_t)(line >> log_u1) & (s2 - 1); }
-  __device__ uint32_t l2_tag_of(uint64_t line) const { return (uint32_t)(line >> log_l2); }
-  __device__ uint64_t l2_line_of(uint32_t s, uint32_t tag) const
-  {
-    return ((uint64_t)tag << log_l2) | ((uint64_t)s << log_u1) | l1set;
-  }
-  __device__ int l2_find(uint32_t s, uint32_t tag) const
-  {
-    int w2 = -1;
-#pragma unroll
-    for (int w = 0; w < A2; ++w) if (st.tag(s, w) == tag) w2 = w;
-    return w2;
-  }
-  __device__ void l2_policy_update(uint32_t s, uint32_t way)
-  {
-    if (pol2 != GG_POLICY_LRU) return;
-    uint64_t mw[MW];
-#pragma unroll
-    for (int k = 0; k < MW; ++k) mw[k] = st.meta(s, k);
-    lru_update<MW>(mw, way);
-#pragma unroll
-    for (int k = 0; k < MW; ++k) st.set_meta(s, k, mw[k]);
-  }
-  // Cache::accessCacheLine on L2 (cache.cc:84-112)
-  __device__ void l2_access(uint64_t line, bool store)
-  {
-    const uint32_t s = l2_set_of(line);
-    const int w = l2_find(s, l2_tag_of(line));
-    if (w < 0) { err |= GG_DERR_STATE; return; }
-    l2_policy_update(s, (uint32_t)w);
-    c2[DW] += store ? 1u : 0u; c2[DR] += store ? 0u : 1u;
-  }
-  __device__ void l2_set_meta_byte(uint32_t s, uint32_t w, uint32_t b)
-  {
-    uint64_t v = st.meta(s, w >> 3);
-    const uint32_t sh = 8 * (w & 7);
-    v = (v & ~(0xFFull << sh)) | ((uint64_t)b << sh);
-    st.set_meta(s, w >> 3, v);
-  }
-  __device__ uint32_t l2_meta_byte(uint32_t s, uint32_t w) const { return (uint32_t)(st.meta(s, w >> 3) >> (8 * (w & 7))) & 0xFFu; }
-
-  // L2CacheCntlr::insertCacheLineInL1 (l2_cache_cntlr.cc:133-165)
-  __device__ void insert_in_l1(uint64_t line, uint32_t ms, uint32_t& res, int& way_out)
-  {
-    int v;
-    if (pol1 == GG_POLICY_LRU) {
-      uint32_t inv = 0;
-#pragma unroll
-      for (int w = 0; w < A1; ++w) inv |= (t1[w] == GG_L1_INV_TAG ? 1u : 0u) << w;
-      v = lru_victim<A1, 1>(inv, &m1);
-    } else {
-      v = (int)rr1;
-      rr1 = (rr1 == 0) ? (A1 - 1) : (rr1 - 1);
-    }
-    if (v < 0) { err |= GG_DERR_STATE; v = 0; }
-    uint64_t ev_line = GG_L1_INV_TAG;
-#pragma unroll
-    for (int w = 0; w < A1; ++w) if (w == v) { ev_line = t1[w]; t1[w] = line; }
-    uint64_t mw = m1;
-    const uint32_t old = meta_byte(&mw, (uint32_t)v);
-    meta_set_byte(&mw, (uint32_t)v, (old & ~7u) | ms);
-    m1 = mw;
-    l1_policy_update((uint32_t)v);
-    // Cache::insertCacheLine counters (cache.cc:151-180), WRITE_THROUGH: no dirty evictions
-    if (ev_line != GG_L1_INV_TAG) { c1[TR]++; c1[DR]++; c1[EV]++; }
-    else c1[TR]++;
-    c1[TW]++; c1[DW]++;
-    way_out = v;
-    if (ev_line != GG_L1_INV_TAG) {
-      res |= GG_RES_L1_EVICT;
-      // clear the L2 line's cached_loc (getCacheLineInfo + setCacheLineInfo)
-      const uint32_t s = l2_set_of(ev_line);
-      c2[TR]++;
-      const int w = l2_find(s, l2_tag_of(ev_line));
-      if (w < 0) { err |= GG_DERR_STATE; return; }
-      const uint32_t b = l2_meta_byte(s, (uint32_t)w);
-      if (!GG_M_LOC(b)) err |= GG_DERR_STATE;   // LOG_ASSERT_ERROR (l2_cache_cntlr.cc:152-157)
-      l2_set_meta_byte(s, (uint32_t)w, b & ~4u);
-      c2[TW]++;
-    }
-  }
-
-  // Cache::updateMissCounters (cache.cc:321-360)
-  __device__ static void miss_counters(uint32_t* c, bool wr, bool miss)
-  {
-    const uint32_t w = wr ? 1u : 0u, r = 1u - w, m = miss ? 1u : 0u;
-    c[ACC]++; c[WACC] += w; c[RACC] += r;
-    c[MISS] += m; c[WMISS] += m & w; c[RMISS] += m & r;
-  }
-
-  // L1CacheCntlr::processMemOpFromCore, private mode.  Returns GG_RES_* flags;
-  // *ev = byte address of the L2 victim (or ~0).
-  __device__ uint32_t access(uint64_t line, bool wr, uint64_t* ev_line)
-  {
-    uint32_t res = 0;
-    *ev_line = ~0ull;
-    // access_num == 1: operationPermissibleinL1Cache (l1:207-243)
-    c1[TR]++;
-    int w1 = l1_find(line);
-    const uint32_t s1 = (w1 >= 0) ? GG_M_STATE(meta_byte(&m1, (uint32_t)w1)) : GG_MS_I;
-    const bool hit1 = wr ? (s1 == GG_MS_M) : (s1 != GG_MS_I);
-    miss_counters(c1, wr, !hit1);
-    if (hit1) {
-      l1_policy_update((uint32_t)w1);          // accessCache -> accessCacheLine
-      c1[DW] += wr ? 1u : 0u; c1[DR] += wr ? 0u : 1u;
-      if (wr) l2_access(line, true);           // write-through (L2CacheCntlr::writeCacheLine)
-      return res;
-    }
-    l1_invalidate(line);                       // l1:135-137
-
-    // L2CacheCntlr::processShmemRequestFromL1Cache (l2:180-224)
-    const uint32_t s = l2_set_of(line), tag2 = l2_tag_of(line);
-    uint32_t tags[A2];
-#pragma unroll
-    for (int w = 0; w < A2; ++w) tags[w] = st.tag(s, w);
-    uint64_t mw[MW];
-#pragma unroll
-    for (int k = 0; k < MW; ++k) mw[k] = st.meta(s, k);
-    int w2 = -1;
-#pragma unroll
-    for (int w = 0; w < A2; ++w) if (tags[w] == tag2) w2 = w;
-    c2[TR]++;
-    const uint32_t b2 = (w2 >= 0) ? meta_byte_t<MW>(mw, (uint32_t)w2) : 0u;
-    const uint32_t s2st = GG_M_STATE(b2);
-    const bool hit2 = wr ? (s2st == GG_MS_M) : (s2st != GG_MS_I);
-    miss_counters(c2, wr, !hit2);
-
-    if (hit2) {
-      res |= GG_RES_L2_HIT;
-      if (pol2 == GG_POLICY_LRU) lru_update<MW>(mw, (uint32_t)w2);   // readCacheLine
-      c2[DR]++;
-#pragma unroll
-      for (int k = 0; k < MW; ++k) st.set_meta(s, k, mw[k]);
-      int v1;
-      insert_in_l1(line, s2st, res, v1);
-      // setCachedLoc / setForcedCachedLoc(L1_DCACHE) + setCacheLineInfo
-      l2_set_meta_byte(s, (uint32_t)w2, l2_meta_byte(s, (uint32_t)w2) | 4u);
-      c2[TW]++;
-      l1_policy_update((uint32_t)v1);          // accessCache (l1:145-159)
-      c1[DW] += wr ? 1u : 0u; c1[DR] += wr ? 0u : 1u;
-      if (wr) l2_access(line, true);
-      return res;
-    }
-
-    // L2 miss -> directory (handleMsgFromL1Cache, l2:226-258)
-    res |= GG_RES_DIRECTORY;
-    uint32_t ns;
-    uint32_t inv = 0;
-#pragma unroll
-    for (int w = 0; w < A2; ++w) inv |= (tags[w] == GG_L2_INV_TAG ? 1u : 0u) << w;
-    if (wr) {                                  // processExReqFromL1Cache (l2:260-282)
-      c2[TR]++;
-      if (s2st == GG_MS_S) {
-        // PrL2CacheLineInfo::invalidate + setCacheLineInfo: tag ~0, state I, loc I; age kept
-#pragma unroll
-        for (int w = 0; w < A2; ++w) if (w == w2) tags[w] = GG_L2_INV_TAG;
-        st.set_tag(s, (uint32_t)w2, GG_L2_INV_TAG);
-        meta_set_byte_t<MW>(mw, (uint32_t)w2, b2 & ~7u);
-        inv |= 1u << w2;
-        c2[TW]++;
-        res |= GG_RES_UPGRADE;
-      } else if (s2st != GG_MS_I) err |= GG_DERR_STATE;
-      ns = GG_MS_M;
-    } else {
-      ns = GG_MS_S;
-    }
-    // insertCacheLineInHierarchy (l2:167-178) -> L2CacheCntlr::insertCacheLine (l2:74-116)
-    int v2;
-    if (pol2 == GG_POLICY_LRU) v2 = lru_victim<A2, MW>(inv, mw);
-    else { v2 = (int)st.rr(s); st.set_rr(s, v2 == 0 ? (A2 - 1) : (v2 - 1)); }
-    if (v2 < 0) { err |= GG_DERR_STATE; v2 = 0; }
-    uint32_t vt = 0;
-#pragma unroll
-    for (int w = 0; w < A2; ++w) if (w == v2) vt = tags[w];
-    const uint32_t vb = meta_byte_t<MW>(mw, (uint32_t)v2);
-    if (vt != GG_L2_INV_TAG) {
-      const uint64_t e = l2_line_of(s, vt);
-      *ev_line = e;
-      c2[TR]++; c2[DR]++; c2[EV]++;
-      res |= GG_RES_L2_EVICT;
-      if (GG_M_STATE(vb) == GG_MS_M) { c2[DEV]++; res |= GG_RES_L2_EVICT_DIRTY; }   // FLUSH_REP
-      else if (GG_M_STATE(vb) != GG_MS_S) err |= GG_DERR_STATE;                       // INV_REP
-      if (GG_M_LOC(vb)) {                      // invalidateCacheLineInL1 (l2:124-131)
-        if (l1_invalidate(e)) res |= GG_RES_L2_EVICT_INV_L1;
-      }
-    } else {
-      c2[TR]++;
-    }
-    c2[TW]++; c2[DW]++;
-    st.set_tag(s, (uint32_t)v2, tag2);
-    meta_set_byte_t<MW>(mw, (uint32_t)v2, (vb & ~7u) | ns | 4u);   // state, cached_loc = L1-D
-    if (pol2 == GG_POLICY_LRU) lru_update<MW>(mw, (uint32_t)v2);
-#pragma unroll
-    for (int k = 0; k < MW; ++k) st.set_meta(s, k, mw[k]);
-    int v1;
-    insert_in_l1(line, ns, res, v1);           // insertCacheLineInL1
-    // access_num == 2: the retry hits (no miss counters)
-    c1[TR]++;
-    l1_policy_update((uint32_t)v1);
-    c1[DW] += wr ? 1u : 0u; c1[DR] += wr ? 0u : 1u;
-    if (wr) l2_access(line, true);
-    return res;
-  }
 };
 
 // ---------------------------------------------------------------------------
@@ -499,8 +241,79 @@ __global__ __launch_bounds__(64) void k_shard_scatter(const uint64_t* __restrict
   }
 }
 
-// Replay: one lane per unit, 64 units per workgroup (one wave).
-template <int A1, int A2>
+// ---------------------------------------------------------------------------
+// Replay kernel.  One lane per unit (tile, L1-D set), 64 units per wave.
+//
+// Every access runs the same straight-line, select-based sequence (no
+// divergent control flow): L1-D lookup in VGPRs, one LDS read of the accessed
+// L2 set (tags [s][lane][A2] via ds_read_b128, meta [s][lane] via
+// ds_read_b64), the hit / L2-hit / directory paths of
+// L1CacheCntlr::processMemOpFromCore folded into predicated updates, one LDS
+// write-back.  Two facts of the private path keep it to ONE L2 set per access:
+//   * PrL2CacheLineInfo::_cached_loc == L1-D  <=>  the L1-D holds the line
+//     (it is set on every L1-D insert, l2_cache_cntlr.cc:98/160-163, and
+//     cleared on every L1-D eviction, :145-164; the only other L1-D
+//     invalidation, l1_cache_cntlr.cc:137, precedes an upgrade that
+//     invalidates the L2 line too).  So the L1-D eviction's
+//     getCacheLineInfo/setCacheLineInfo pair on the victim's L2 set changes
+//     only counters, and invalidateCacheLineInL1 fires exactly when the L1-D
+//     holds the L2 victim.  The kernel checks the invariant on entry and
+//     writes the cached_loc bits back on exit, so the persisted state is the
+//     reference's.
+//   * every counter of Cache::outputSummary is a linear function of 11
+//     per-access indicator sums (see kCounterMap below).
+// ---------------------------------------------------------------------------
+enum { I_WR = 0, I_NH1, I_NH1W, I_M2, I_M2W, I_W1V, I_L1EV, I_L2EV, I_DIRTY, I_INVL1, I_UPG, NI };
+
+template <int A1>
+__device__ __forceinline__ int match_u64(const uint64_t (&t)[A1], uint64_t x)
+{
+  int w1 = -1;
+#pragma unroll
+  for (int w = 0; w < A1; ++w) w1 = (t[w] == x) ? w : w1;
+  return w1;
+}
+
+template <int A2>
+__device__ __forceinline__ int match_u32(const uint32_t (&t)[A2], uint32_t x)
+{
+  int w2 = -1;
+#pragma unroll
+  for (int w = 0; w < A2; ++w) w2 = (t[w] == x) ? w : w2;
+  return w2;
+}
+
+template <int A>
+__device__ __forceinline__ uint32_t inv_mask_u64(const uint64_t (&t)[A])
+{
+  uint32_t m = 0;
+#pragma unroll
+  for (int w = 0; w < A; ++w) m |= (t[w] == GG_L1_INV_TAG ? 1u : 0u) << w;
+  return m;
+}
+
+template <int A>
+__device__ __forceinline__ uint32_t inv_mask_u32(const uint32_t (&t)[A])
+{
+  uint32_t m = 0;
+#pragma unroll
+  for (int w = 0; w < A; ++w) m |= (t[w] == GG_L2_INV_TAG ? 1u : 0u) << w;
+  return m;
+}
+
+// LRU update of way `way` applied only when `cond`
+template <int MW>
+__device__ __forceinline__ void lru_update_if(uint64_t* mw, uint32_t way, bool cond)
+{
+  uint64_t nw[MW];
+#pragma unroll
+  for (int k = 0; k < MW; ++k) nw[k] = mw[k];
+  lru_update<MW>(nw, way);
+#pragma unroll
+  for (int k = 0; k < MW; ++k) mw[k] = cond ? nw[k] : mw[k];
+}
+
+template <int A1, int A2, bool LRU1, bool LRU2>
 __global__ __launch_bounds__(64) void k_cache_replay(gg_cache_state cs, gg_geom g,
     const uint64_t* __restrict__ sh_key, const uint32_t* __restrict__ sh_idx,
     const uint32_t* __restrict__ unit_len, const uint64_t* __restrict__ unit_base,
@@ -508,36 +321,57 @@ __global__ __launch_bounds__(64) void k_cache_replay(gg_cache_state cs, gg_geom 
     uint64_t* __restrict__ evicted, uint32_t* err)
 {
   constexpr int MW = (A2 + 7) / 8;
+  constexpr int TQ = (A2 + 3) / 4;                 // uint4 quads of tags per set
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t lane = threadIdx.x;
   const uint64_t u = (uint64_t)blockIdx.x * GG_WAVE + lane;
   const bool active = u < g.units;
   const uint64_t uu = active ? u : 0;
   const uint32_t S2 = g.s2;
+  const uint32_t l1set = (uint32_t)(uu & (g.u1 - 1));
+  uint32_t errv = 0;
 
-  Unit<A1, A2, L2Lds<A2>> U;
-  U.st.T = reinterpret_cast<uint32_t*>(smem);
-  U.st.M = reinterpret_cast<uint64_t*>(smem + (size_t)S2 * A2 * GG_WAVE * 4);
-  U.st.R = reinterpret_cast<uint8_t*>(smem + (size_t)S2 * A2 * GG_WAVE * 4 + (size_t)S2 * GG_WAVE * MW * 8);
-  U.st.lane = lane;
-  U.l1set = (uint32_t)(uu & (g.u1 - 1));
-  U.log_u1 = g.log_u1; U.s2 = S2; U.log_l2 = g.log_l2; U.pol1 = g.pol1; U.pol2 = g.pol2;
-  U.err = 0;
-#pragma unroll
-  for (int k = 0; k < NC; ++k) { U.c1[k] = 0; U.c2[k] = 0; }
+  // LDS carve: tags [s][lane][TQ*4] u32 | meta [s][lane][MW] u64 | rr [s][lane] u8
+  uint32_t* T = reinterpret_cast<uint32_t*>(smem);
+  uint64_t* Mv = reinterpret_cast<uint64_t*>(smem + (size_t)S2 * GG_WAVE * TQ * 16);
+  uint8_t* R = reinterpret_cast<uint8_t*>(smem + (size_t)S2 * GG_WAVE * TQ * 16 + (size_t)S2 * GG_WAVE * MW * 8);
+  auto tq = [&](uint32_t s, int q) -> uint4* { return reinterpret_cast<uint4*>(T) + ((size_t)s * GG_WAVE + lane) * TQ + q; };
+  auto mp = [&](uint32_t s, int k) -> uint64_t* { return Mv + ((size_t)s * GG_WAVE + lane) * MW + k; };
 
-  // load state (coalesced: [field][unit])
+  // ---- load state (coalesced [field][unit] -> LDS / VGPRs) ----
+  uint64_t t1[A1];
 #pragma unroll
-  for (int w = 0; w < A1; ++w) U.t1[w] = cs.l1_tag[(uint64_t)w * g.units + uu];
-  U.m1 = cs.l1_meta[uu];
-  U.rr1 = cs.l1_rr[uu];
+  for (int w = 0; w < A1; ++w) t1[w] = cs.l1_tag[(uint64_t)w * g.units + uu];
+  uint64_t m1 = cs.l1_meta[uu];
+  uint32_t rr1 = cs.l1_rr[uu];
+  uint32_t nloc = 0, nl1 = 0;
   for (uint32_t s = 0; s < S2; ++s) {
+    uint32_t tg[TQ * 4];
 #pragma unroll
-    for (int w = 0; w < A2; ++w) U.st.set_tag(s, w, cs.l2_tag[(uint64_t)(s * A2 + w) * g.units + uu]);
+    for (int w = 0; w < TQ * 4; ++w)
+      tg[w] = (w < A2) ? cs.l2_tag[(uint64_t)(s * A2 + w) * g.units + uu] : GG_L2_INV_TAG;
 #pragma unroll
-    for (int k = 0; k < MW; ++k) U.st.set_meta(s, k, cs.l2_meta[(uint64_t)(s * MW + k) * g.units + uu]);
-    if (g.pol2 != GG_POLICY_LRU) U.st.set_rr(s, cs.l2_rr[(uint64_t)s * g.units + uu]);
+    for (int q = 0; q < TQ; ++q) *tq(s, q) = make_uint4(tg[4 * q], tg[4 * q + 1], tg[4 * q + 2], tg[4 * q + 3]);
+    uint64_t mw[MW];
+#pragma unroll
+    for (int k = 0; k < MW; ++k) mw[k] = cs.l2_meta[(uint64_t)(s * MW + k) * g.units + uu];
+    // cached_loc invariant check: loc bit <=> the L1-D holds the line
+#pragma unroll
+    for (int w = 0; w < A2; ++w) {
+      const uint64_t ln = ((uint64_t)tg[w] << g.log_l2) | ((uint64_t)s << g.log_u1) | l1set;
+      const bool held = tg[w] != GG_L2_INV_TAG && match_u64<A1>(t1, ln) >= 0;
+      const bool loc = GG_M_LOC(meta_byte_t<MW>(mw, w)) != 0;
+      nloc += loc ? 1u : 0u;
+      errv |= (loc != held) ? GG_DERR_STATE : 0u;
+      meta_set_byte_t<MW>(mw, w, meta_byte_t<MW>(mw, w) & ~4u);   // loc is implicit during the replay
+    }
+#pragma unroll
+    for (int k = 0; k < MW; ++k) *mp(s, k) = mw[k];
+    if (!LRU2) R[s * GG_WAVE + lane] = cs.l2_rr[(uint64_t)s * g.units + uu];
   }
+#pragma unroll
+  for (int w = 0; w < A1; ++w) nl1 += (t1[w] != GG_L1_INV_TAG) ? 1u : 0u;
+  if (active && nl1 != nloc) errv |= GG_DERR_STATE;                 // an L1-D line missing from L2
 
   const uint32_t len = active ? unit_len[uu] : 0;
   const uint64_t base = active ? unit_base[uu] : 0;
@@ -546,53 +380,208 @@ __global__ __launch_bounds__(64) void k_cache_replay(gg_cache_state cs, gg_geom 
   uint32_t maxlen = len;
   for (int o = 32; o > 0; o >>= 1) maxlen = max(maxlen, (uint32_t)__shfl_xor((int)maxlen, o));
 
-  uint64_t key = (len > 0) ? sh_key[base] : 0;
-  uint32_t idx = (len > 0) ? sh_idx[base] : 0;
+  uint32_t cnt[NI];
+#pragma unroll
+  for (int k = 0; k < NI; ++k) cnt[k] = 0;
+
+  // prefetch ring of the lane's record stream (distance 4)
+  constexpr int PD = 4;
+  uint64_t kr[PD]; uint32_t ir[PD];
+#pragma unroll
+  for (int d = 0; d < PD; ++d) {
+    kr[d] = (d < (int)len) ? sh_key[base + d] : 0;
+    ir[d] = (d < (int)len) ? sh_idx[base + d] : 0;
+  }
+  const uint64_t lmask = (g.s2 - 1);
+
   for (uint32_t j = 0; j < maxlen; ++j) {
     const bool live = j < len;
-    const bool more = j + 1 < len;
-    const uint64_t nkey = more ? sh_key[base + j + 1] : 0;
-    const uint32_t nidx = more ? sh_idx[base + j + 1] : 0;
-    if (live) {
-      uint64_t ev;
-      const uint32_t r = U.access(key >> g.log_line, (key & 1u) != 0, &ev);
-      if (result) result[rbase + idx] = r;
-      if (evicted) evicted[rbase + idx] = (ev == ~0ull) ? ~0ull : (ev << g.log_line);
+    const uint64_t key = kr[0];
+    const uint32_t idx = ir[0];
+#pragma unroll
+    for (int d = 0; d < PD - 1; ++d) { kr[d] = kr[d + 1]; ir[d] = ir[d + 1]; }
+    const bool more = j + PD < len;
+    kr[PD - 1] = more ? sh_key[base + j + PD] : 0;
+    ir[PD - 1] = more ? sh_idx[base + j + PD] : 0;
+    if (!live) continue;
+
+    const uint64_t line = key >> g.log_line;
+    const bool wr = (key & 1u) != 0;
+    const uint32_t s = (uint32_t)((line >> g.log_u1) & lmask);
+    const uint32_t tag2 = (uint32_t)(line >> g.log_l2);
+
+    // -- L2 set s (one LDS round trip) --
+    uint32_t tg[TQ * 4];
+#pragma unroll
+    for (int q = 0; q < TQ; ++q) {
+      const uint4 v = *tq(s, q);
+      tg[4 * q] = v.x; tg[4 * q + 1] = v.y; tg[4 * q + 2] = v.z; tg[4 * q + 3] = v.w;
     }
-    key = nkey; idx = nidx;
+    uint64_t mw[MW];
+#pragma unroll
+    for (int k = 0; k < MW; ++k) mw[k] = *mp(s, k);
+    uint32_t rr2 = LRU2 ? 0u : R[s * GG_WAVE + lane];
+
+    // -- operationPermissibleinL1Cache (l1:207-243) --
+    const int w1 = match_u64<A1>(t1, line);
+    const uint32_t s1 = (w1 >= 0) ? GG_M_STATE(meta_byte(&m1, (uint32_t)w1)) : GG_MS_I;
+    const bool hit1 = wr ? (s1 == GG_MS_M) : (s1 != GG_MS_I);
+
+    // -- processShmemRequestFromL1Cache (l2:180-224) --
+    uint32_t tga[A2];
+#pragma unroll
+    for (int w = 0; w < A2; ++w) tga[w] = tg[w];
+    const int w2 = match_u32<A2>(tga, tag2);
+    const uint32_t b2 = (w2 >= 0) ? meta_byte_t<MW>(mw, (uint32_t)w2) : 0u;
+    const uint32_t s2 = GG_M_STATE(b2);
+    const bool hit2 = !hit1 && (wr ? (s2 == GG_MS_M) : (s2 != GG_MS_I));
+    const bool miss2 = !hit1 && !hit2;
+    const bool upg = miss2 && wr && (s2 == GG_MS_S);                 // processExReqFromL1Cache (l2:260-282)
+    const bool w1v = !hit1 && (w1 >= 0);
+    errv |= (hit1 && wr && w2 < 0) ? GG_DERR_STATE : 0u;             // write-through needs the L2 copy
+
+    // L1CacheCntlr::invalidateCacheLine of the missing line (l1:135-137)
+#pragma unroll
+    for (int w = 0; w < A1; ++w) t1[w] = (w1v && w == w1) ? GG_L1_INV_TAG : t1[w];
+    if (w1v) m1 &= ~(7ull << (8 * w1));
+    // upgrade: PrL2CacheLineInfo::invalidate + setCacheLineInfo (tag, state, loc; age kept)
+#pragma unroll
+    for (int w = 0; w < A2; ++w) tga[w] = (upg && w == w2) ? GG_L2_INV_TAG : tga[w];
+    if (upg) meta_set_byte_t<MW>(mw, (uint32_t)w2, b2 & ~7u);
+
+    // -- L2CacheCntlr::insertCacheLine (l2:74-116): victim, eviction, install --
+    int v2;
+    if (LRU2) v2 = lru_victim<A2, MW>(inv_mask_u32<A2>(tga), mw);
+    else v2 = (int)rr2;
+    errv |= (miss2 && v2 < 0) ? GG_DERR_STATE : 0u;
+    v2 = v2 < 0 ? 0 : v2;
+    uint32_t vt = GG_L2_INV_TAG;
+#pragma unroll
+    for (int w = 0; w < A2; ++w) vt = (w == v2) ? tga[w] : vt;
+    const uint32_t vb = meta_byte_t<MW>(mw, (uint32_t)v2);
+    const bool l2ev = miss2 && vt != GG_L2_INV_TAG;
+    const bool dirty = l2ev && GG_M_STATE(vb) == GG_MS_M;            // FLUSH_REP (else INV_REP)
+    errv |= (l2ev && GG_M_STATE(vb) == GG_MS_I) ? GG_DERR_STATE : 0u;
+    const uint64_t e2 = ((uint64_t)vt << g.log_l2) | ((uint64_t)s << g.log_u1) | l1set;
+    // invalidateCacheLineInL1: fires iff the L1-D holds the victim (cached_loc invariant)
+    const int we = match_u64<A1>(t1, e2);
+    const bool invl1 = l2ev && we >= 0;
+#pragma unroll
+    for (int w = 0; w < A1; ++w) t1[w] = (invl1 && w == we) ? GG_L1_INV_TAG : t1[w];
+    if (invl1) m1 &= ~(7ull << (8 * we));
+    const uint32_t ns = wr ? GG_MS_M : GG_MS_S;                      // EX_REP / SH_REP
+#pragma unroll
+    for (int w = 0; w < A2; ++w) tga[w] = (miss2 && w == v2) ? tag2 : tga[w];
+    if (miss2) meta_set_byte_t<MW>(mw, (uint32_t)v2, (vb & ~7u) | ns);
+    if (!LRU2 && miss2) rr2 = (rr2 == 0) ? (A2 - 1) : (rr2 - 1);
+    // L2 replacement update: readCacheLine (hit2), install (miss2), write-through (hit1 && wr)
+    if (LRU2) lru_update_if<MW>(mw, (uint32_t)(miss2 ? v2 : (w2 < 0 ? 0 : w2)), (!hit1 || wr) && (miss2 || w2 >= 0));
+
+    // -- insertCacheLineInL1 (l2:133-165): victim after both invalidations --
+    int v1;
+    if (LRU1) v1 = lru_victim<A1, 1>(inv_mask_u64<A1>(t1), &m1);
+    else v1 = (int)rr1;
+    errv |= (!hit1 && v1 < 0) ? GG_DERR_STATE : 0u;
+    v1 = v1 < 0 ? 0 : v1;
+    uint64_t et = GG_L1_INV_TAG;
+#pragma unroll
+    for (int w = 0; w < A1; ++w) et = (w == v1) ? t1[w] : et;
+    const bool l1ev = !hit1 && et != GG_L1_INV_TAG;
+    const uint32_t ins = hit2 ? s2 : ns;
+#pragma unroll
+    for (int w = 0; w < A1; ++w) t1[w] = (!hit1 && w == v1) ? line : t1[w];
+    if (!hit1) meta_set_byte(&m1, (uint32_t)v1, (meta_byte(&m1, (uint32_t)v1) & ~7u) | ins);
+    if (!LRU1 && !hit1) rr1 = (rr1 == 0) ? (A1 - 1) : (rr1 - 1);
+    // L1-D replacement update: accessCache on the hit way or the inserted way
+    if (LRU1) lru_update<1>(&m1, (uint32_t)(hit1 ? w1 : v1));
+
+    // -- write the L2 set back --
+#pragma unroll
+    for (int w = A2; w < TQ * 4; ++w) tg[w] = GG_L2_INV_TAG;
+#pragma unroll
+    for (int w = 0; w < A2; ++w) tg[w] = tga[w];
+#pragma unroll
+    for (int q = 0; q < TQ; ++q) *tq(s, q) = make_uint4(tg[4 * q], tg[4 * q + 1], tg[4 * q + 2], tg[4 * q + 3]);
+#pragma unroll
+    for (int k = 0; k < MW; ++k) *mp(s, k) = mw[k];
+    if (!LRU2 && miss2) R[s * GG_WAVE + lane] = (uint8_t)rr2;
+
+    // -- indicator sums and outputs --
+    cnt[I_WR] += wr; cnt[I_NH1] += !hit1; cnt[I_NH1W] += (!hit1 && wr); cnt[I_M2] += miss2;
+    cnt[I_M2W] += (miss2 && wr); cnt[I_W1V] += w1v; cnt[I_L1EV] += l1ev; cnt[I_L2EV] += l2ev;
+    cnt[I_DIRTY] += dirty; cnt[I_INVL1] += invl1; cnt[I_UPG] += upg;
+    const uint32_t res = (hit1 ? GG_RES_L1_HIT : (hit2 ? GG_RES_L2_HIT : GG_RES_DIRECTORY)) |
+                         (upg ? GG_RES_UPGRADE : 0u) | (l1ev ? GG_RES_L1_EVICT : 0u) |
+                         (l2ev ? GG_RES_L2_EVICT : 0u) | (dirty ? GG_RES_L2_EVICT_DIRTY : 0u) |
+                         (invl1 ? GG_RES_L2_EVICT_INV_L1 : 0u);
+    if (result) result[rbase + idx] = res;
+    if (evicted) evicted[rbase + idx] = l2ev ? (e2 << g.log_line) : ~0ull;
   }
 
-  // store state back
+  // ---- store state back, with cached_loc materialised from the L1-D ----
   if (active) {
 #pragma unroll
-    for (int w = 0; w < A1; ++w) cs.l1_tag[(uint64_t)w * g.units + u] = U.t1[w];
-    cs.l1_meta[u] = U.m1;
-    cs.l1_rr[u] = (uint8_t)U.rr1;
+    for (int w = 0; w < A1; ++w) cs.l1_tag[(uint64_t)w * g.units + u] = t1[w];
+    cs.l1_meta[u] = m1;
+    cs.l1_rr[u] = (uint8_t)rr1;
     for (uint32_t s = 0; s < S2; ++s) {
+      uint32_t tg[TQ * 4];
 #pragma unroll
-      for (int w = 0; w < A2; ++w) cs.l2_tag[(uint64_t)(s * A2 + w) * g.units + u] = U.st.tag(s, w);
+      for (int q = 0; q < TQ; ++q) {
+        const uint4 v = *tq(s, q);
+        tg[4 * q] = v.x; tg[4 * q + 1] = v.y; tg[4 * q + 2] = v.z; tg[4 * q + 3] = v.w;
+      }
+      uint64_t mw[MW];
 #pragma unroll
-      for (int k = 0; k < MW; ++k) cs.l2_meta[(uint64_t)(s * MW + k) * g.units + u] = U.st.meta(s, k);
-      if (g.pol2 != GG_POLICY_LRU) cs.l2_rr[(uint64_t)s * g.units + u] = (uint8_t)U.st.rr(s);
+      for (int k = 0; k < MW; ++k) mw[k] = *mp(s, k);
+#pragma unroll
+      for (int w = 0; w < A2; ++w) {
+        const uint64_t ln = ((uint64_t)tg[w] << g.log_l2) | ((uint64_t)s << g.log_u1) | l1set;
+        const bool held = tg[w] != GG_L2_INV_TAG && match_u64<A1>(t1, ln) >= 0;
+        meta_set_byte_t<MW>(mw, w, (meta_byte_t<MW>(mw, w) & ~4u) | (held ? 4u : 0u));
+        cs.l2_tag[(uint64_t)(s * A2 + w) * g.units + u] = tg[w];
+      }
+#pragma unroll
+      for (int k = 0; k < MW; ++k) cs.l2_meta[(uint64_t)(s * MW + k) * g.units + u] = mw[k];
+      if (!LRU2) cs.l2_rr[(uint64_t)s * g.units + u] = R[s * GG_WAVE + lane];
     }
   }
-  if (U.err) atomicOr(err, U.err);
+  if (!active) errv = 0;
+  if (errv) atomicOr(err, errv);
 
-  // counters: all 64 lanes of the wave belong to one tile when u1 % 64 == 0
+  // ---- counters: Cache::outputSummary fields from the indicator sums ----
+  const uint32_t n = len;
+  const uint32_t nwr = cnt[I_WR], nh1 = cnt[I_NH1], nh1w = cnt[I_NH1W], m2 = cnt[I_M2], m2w = cnt[I_M2W];
+  const uint32_t w1v = cnt[I_W1V], l1ev = cnt[I_L1EV], l2ev = cnt[I_L2EV], drt = cnt[I_DIRTY];
+  const uint32_t invl1 = cnt[I_INVL1], upg = cnt[I_UPG], h2 = nh1 - m2;
+  uint32_t c[2 * NC];
+  // L1-D
+  c[ACC] = n; c[WACC] = nwr; c[RACC] = n - nwr; c[MISS] = nh1; c[WMISS] = nh1w; c[RMISS] = nh1 - nh1w;
+  c[EV] = l1ev; c[DEV] = 0;
+  c[TR] = n + 2 * nh1 + m2 + invl1;           // probe, invalidate probe + insert, retry probe, L2-evict probe
+  c[TW] = w1v + nh1 + invl1;                  // invalidate, insert, L2-evict invalidation
+  c[DR] = (n - nwr) + l1ev;                   // load access, eviction
+  c[DW] = nwr + nh1;                          // store access, insert
+  // L2
+  c[NC + ACC] = nh1; c[NC + WACC] = nh1w; c[NC + RACC] = nh1 - nh1w;
+  c[NC + MISS] = m2; c[NC + WMISS] = m2w; c[NC + RMISS] = m2 - m2w;
+  c[NC + EV] = l2ev; c[NC + DEV] = drt;
+  c[NC + TR] = nh1 + m2w + m2 + l1ev;         // probe, EX_REQ probe, insert, L1-D-eviction probe
+  c[NC + TW] = upg + m2 + l1ev + h2;          // upgrade, insert, cached_loc clear, cached_loc set
+  c[NC + DR] = h2 + l2ev;                     // readCacheLine, eviction
+  c[NC + DW] = nwr + m2;                      // write-through, insert
   uint64_t* ctr = cs.counters + (uint64_t)tile * 2 * NC;
   if ((g.u1 & (GG_WAVE - 1)) == 0) {
 #pragma unroll
-    for (int k = 0; k < NC; ++k) {
-      uint32_t a = U.c1[k], b = U.c2[k];
-      for (int o = 32; o > 0; o >>= 1) { a += __shfl_xor(a, o); b += __shfl_xor(b, o); }
-      if (lane == 0) { if (a) atomicAdd((unsigned long long*)&ctr[k], a); if (b) atomicAdd((unsigned long long*)&ctr[NC + k], b); }
+    for (int k = 0; k < 2 * NC; ++k) {
+      uint32_t a = active ? c[k] : 0u;
+      for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+      if (lane == 0 && a) atomicAdd((unsigned long long*)&ctr[k], (unsigned long long)a);
     }
   } else if (active) {
 #pragma unroll
-    for (int k = 0; k < NC; ++k) {
-      if (U.c1[k]) atomicAdd((unsigned long long*)&ctr[k], U.c1[k]);
-      if (U.c2[k]) atomicAdd((unsigned long long*)&ctr[NC + k], U.c2[k]);
-    }
+    for (int k = 0; k < 2 * NC; ++k)
+      if (c[k]) atomicAdd((unsigned long long*)&ctr[k], (unsigned long long)c[k]);
   }
 }
 
@@ -761,25 +750,31 @@ typedef void (*replay_fn)(gg_cache_state, gg_geom, const uint64_t*, const uint32
                           const uint64_t*, const uint64_t*, uint32_t*, uint64_t*, uint32_t*);
 typedef void (*quartet_fn)(gg_cache_state, gg_geom, QuartetIO*);
 
-struct Kern { int a1, a2; replay_fn replay; quartet_fn quartet; };
+struct Kern { int a1, a2; int lru1, lru2; replay_fn replay; quartet_fn quartet; };
 
-#define GG_KERN(A1, A2) { A1, A2, k_cache_replay<A1, A2>, k_quartet<A1, A2> }
+// Replay instantiations: every geometry with LRU (the carbon_sim.cfg default),
+// all four policy combinations for the reference geometries.
+#define GG_KERN(A1, A2, P1, P2) { A1, A2, P1, P2, k_cache_replay<A1, A2, P1, P2>, k_quartet<A1, A2> }
 const Kern kKernels[] = {
-  GG_KERN(4, 8), GG_KERN(4, 16), GG_KERN(4, 4),
-  GG_KERN(2, 4), GG_KERN(2, 8), GG_KERN(2, 16),
-  GG_KERN(8, 8), GG_KERN(8, 16), GG_KERN(8, 4),
-  GG_KERN(1, 8), GG_KERN(4, 2), GG_KERN(4, 32),
+  GG_KERN(4, 8, 1, 1), GG_KERN(4, 8, 0, 0), GG_KERN(4, 8, 1, 0), GG_KERN(4, 8, 0, 1),
+  GG_KERN(4, 16, 1, 1), GG_KERN(4, 16, 0, 0), GG_KERN(4, 16, 1, 0), GG_KERN(4, 16, 0, 1),
+  GG_KERN(4, 4, 1, 1), GG_KERN(2, 4, 1, 1), GG_KERN(2, 8, 1, 1), GG_KERN(2, 16, 1, 1),
+  GG_KERN(8, 8, 1, 1), GG_KERN(8, 16, 1, 1), GG_KERN(8, 4, 1, 1), GG_KERN(1, 8, 1, 1),
+  GG_KERN(4, 2, 1, 1), GG_KERN(4, 32, 1, 1),
 };
 
-const Kern* find_kernel(uint32_t a1, uint32_t a2)
+const Kern* find_kernel(uint32_t a1, uint32_t a2, uint32_t pol1, uint32_t pol2)
 {
-  for (const Kern& k : kKernels) if ((uint32_t)k.a1 == a1 && (uint32_t)k.a2 == a2) return &k;
+  const int l1 = pol1 == GG_POLICY_LRU, l2 = pol2 == GG_POLICY_LRU;
+  for (const Kern& k : kKernels)
+    if ((uint32_t)k.a1 == a1 && (uint32_t)k.a2 == a2 && k.lru1 == l1 && k.lru2 == l2) return &k;
   return nullptr;
 }
 
 size_t replay_lds_bytes(const gg_geom& g)
 {
-  return (size_t)g.s2 * g.a2 * GG_WAVE * 4 + (size_t)g.s2 * GG_WAVE * g.mw * 8 +
+  const size_t tq = (g.a2 + 3) / 4;
+  return (size_t)g.s2 * GG_WAVE * tq * 16 + (size_t)g.s2 * GG_WAVE * g.mw * 8 +
          (g.pol2 == GG_POLICY_LRU ? 0 : (size_t)g.s2 * GG_WAVE);
 }
 
@@ -800,8 +795,9 @@ gg_status gg_cache_state_alloc(gg_ctx* ctx)
 {
   gg_geom& g = ctx->g;
   gg_cache_state& cs = ctx->cs;
-  if (!find_kernel(g.a1, g.a2))
-    return gg_fail(GG_ERR_UNSUPPORTED, "no replay kernel instantiated for L1-D assoc %u / L2 assoc %u", g.a1, g.a2);
+  if (!find_kernel(g.a1, g.a2, g.pol1, g.pol2))
+    return gg_fail(GG_ERR_UNSUPPORTED, "no replay kernel instantiated for L1-D assoc %u / L2 assoc %u / policies %u,%u",
+                   g.a1, g.a2, g.pol1, g.pol2);
   if (replay_lds_bytes(g) > 64 * 1024)
     return gg_fail(GG_ERR_UNSUPPORTED, "L2 lines per L1-D set (%u) too large for the LDS-resident replay", g.s2 * g.a2);
   GG_HIP(hipMalloc((void**)&cs.l1_tag, sizeof(uint64_t) * g.a1 * g.units));
@@ -899,7 +895,7 @@ gg_status gg_cache_run_batch(gg_ctx* ctx, const gg_trace* tr, uint32_t* result, 
     GG_HIP(hipGetLastError());
     gg_timer_end(ctx, "cache_shard", s);
   }
-  const Kern* k = find_kernel(g.a1, g.a2);
+  const Kern* k = find_kernel(g.a1, g.a2, g.pol1, g.pol2);
   const uint32_t groups = (uint32_t)((g.units + GG_WAVE - 1) / GG_WAVE);
   gg_timer_begin(ctx, "cache_replay", s);
   hipLaunchKernelGGL(k->replay, dim3(groups), dim3(GG_WAVE), replay_lds_bytes(g), s, ctx->cs, g,
@@ -924,7 +920,7 @@ gg_status gg_cache_quartet(gg_ctx* ctx, int op, uint32_t tile, int level, uint64
   GG_HIP(hipMalloc((void**)&d, sizeof(QuartetIO)));
   hipStream_t s = ctx->last_stream;
   GG_HIP(hipMemcpyAsync(d, &q, sizeof(q), hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(find_kernel(g.a1, g.a2)->quartet, dim3(1), dim3(1), 0, s, ctx->cs, g, d);
+  hipLaunchKernelGGL(find_kernel(g.a1, g.a2, g.pol1, g.pol2)->quartet, dim3(1), dim3(1), 0, s, ctx->cs, g, d);
   GG_HIP(hipGetLastError());
   GG_HIP(hipMemcpyAsync(&q, d, sizeof(q), hipMemcpyDeviceToHost, s));
   GG_HIP(hipStreamSynchronize(s));
