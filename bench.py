@@ -47,6 +47,7 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu count)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--replay-kernel", type=int, default=0, help="0 = fastest instantiated, 1 = generic")
     return p.parse_args()
 
 
@@ -96,7 +97,7 @@ def main():
     torch.cuda.set_device(dev)
 
     T, N = args.tiles, args.per_tile
-    cfg = C.default_config(T, device=local)
+    cfg = C.default_config(T, device=local, replay_kernel=args.replay_kernel)
     be = B.Backend(cfg)
     be.set_timing(True)
     stream = torch.cuda.current_stream(dev)

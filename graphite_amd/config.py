@@ -67,7 +67,8 @@ class GGConfig(ctypes.Structure):
         ("total_tiles", ctypes.c_uint32),
         ("frequency_ghz", ctypes.c_double),
         ("device", ctypes.c_int32),
-        ("reserved", ctypes.c_uint32 * 7),
+        ("replay_kernel", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32 * 6),
     ]
 
 
@@ -88,6 +89,7 @@ def default_config(num_tiles, **overrides):
     c.total_tiles = 0
     c.frequency_ghz = 1.0
     c.device = 0
+    c.replay_kernel = 0
     for k, v in overrides.items():
         if not hasattr(c, k):
             raise KeyError(k)

@@ -313,6 +313,46 @@ __device__ __forceinline__ void lru_update_if(uint64_t* mw, uint32_t way, bool c
   for (int k = 0; k < MW; ++k) mw[k] = cond ? nw[k] : mw[k];
 }
 
+// Cache::outputSummary counters of one unit from its indicator sums, reduced
+// over the wave and added to the tile's counters.
+__device__ void replay_counters(const gg_cache_state& cs, const gg_geom& g, const uint32_t (&cnt)[NI],
+                                uint32_t len, uint32_t tile, uint32_t lane, bool active)
+{
+  const uint32_t n = len;
+  const uint32_t nwr = cnt[I_WR], nh1 = cnt[I_NH1], nh1w = cnt[I_NH1W], m2 = cnt[I_M2], m2w = cnt[I_M2W];
+  const uint32_t w1v = cnt[I_W1V], l1ev = cnt[I_L1EV], l2ev = cnt[I_L2EV], drt = cnt[I_DIRTY];
+  const uint32_t invl1 = cnt[I_INVL1], upg = cnt[I_UPG], h2 = nh1 - m2;
+  uint32_t c[2 * NC];
+  // L1-D
+  c[ACC] = n; c[WACC] = nwr; c[RACC] = n - nwr; c[MISS] = nh1; c[WMISS] = nh1w; c[RMISS] = nh1 - nh1w;
+  c[EV] = l1ev; c[DEV] = 0;
+  c[TR] = n + 2 * nh1 + m2 + invl1;           // probe, invalidate probe + insert, retry probe, L2-evict probe
+  c[TW] = w1v + nh1 + invl1;                  // invalidate, insert, L2-evict invalidation
+  c[DR] = (n - nwr) + l1ev;                   // load access, eviction
+  c[DW] = nwr + nh1;                          // store access, insert
+  // L2
+  c[NC + ACC] = nh1; c[NC + WACC] = nh1w; c[NC + RACC] = nh1 - nh1w;
+  c[NC + MISS] = m2; c[NC + WMISS] = m2w; c[NC + RMISS] = m2 - m2w;
+  c[NC + EV] = l2ev; c[NC + DEV] = drt;
+  c[NC + TR] = nh1 + m2w + m2 + l1ev;         // probe, EX_REQ probe, insert, L1-D-eviction probe
+  c[NC + TW] = upg + m2 + l1ev + h2;          // upgrade, insert, cached_loc clear, cached_loc set
+  c[NC + DR] = h2 + l2ev;                     // readCacheLine, eviction
+  c[NC + DW] = nwr + m2;                      // write-through, insert
+  uint64_t* ctr = cs.counters + (uint64_t)tile * 2 * NC;
+  if ((g.u1 & (GG_WAVE - 1)) == 0) {
+#pragma unroll
+    for (int k = 0; k < 2 * NC; ++k) {
+      uint32_t a = active ? c[k] : 0u;
+      for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+      if (lane == 0 && a) atomicAdd((unsigned long long*)&ctr[k], (unsigned long long)a);
+    }
+  } else if (active) {
+#pragma unroll
+    for (int k = 0; k < 2 * NC; ++k)
+      if (c[k]) atomicAdd((unsigned long long*)&ctr[k], (unsigned long long)c[k]);
+  }
+}
+
 template <int A1, int A2, bool LRU1, bool LRU2>
 __global__ __launch_bounds__(64) void k_cache_replay(gg_cache_state cs, gg_geom g,
     const uint64_t* __restrict__ sh_key, const uint32_t* __restrict__ sh_idx,
@@ -549,40 +589,298 @@ __global__ __launch_bounds__(64) void k_cache_replay(gg_cache_state cs, gg_geom 
   if (!active) errv = 0;
   if (errv) atomicOr(err, errv);
 
-  // ---- counters: Cache::outputSummary fields from the indicator sums ----
-  const uint32_t n = len;
-  const uint32_t nwr = cnt[I_WR], nh1 = cnt[I_NH1], nh1w = cnt[I_NH1W], m2 = cnt[I_M2], m2w = cnt[I_M2W];
-  const uint32_t w1v = cnt[I_W1V], l1ev = cnt[I_L1EV], l2ev = cnt[I_L2EV], drt = cnt[I_DIRTY];
-  const uint32_t invl1 = cnt[I_INVL1], upg = cnt[I_UPG], h2 = nh1 - m2;
-  uint32_t c[2 * NC];
-  // L1-D
-  c[ACC] = n; c[WACC] = nwr; c[RACC] = n - nwr; c[MISS] = nh1; c[WMISS] = nh1w; c[RMISS] = nh1 - nh1w;
-  c[EV] = l1ev; c[DEV] = 0;
-  c[TR] = n + 2 * nh1 + m2 + invl1;           // probe, invalidate probe + insert, retry probe, L2-evict probe
-  c[TW] = w1v + nh1 + invl1;                  // invalidate, insert, L2-evict invalidation
-  c[DR] = (n - nwr) + l1ev;                   // load access, eviction
-  c[DW] = nwr + nh1;                          // store access, insert
-  // L2
-  c[NC + ACC] = nh1; c[NC + WACC] = nh1w; c[NC + RACC] = nh1 - nh1w;
-  c[NC + MISS] = m2; c[NC + WMISS] = m2w; c[NC + RMISS] = m2 - m2w;
-  c[NC + EV] = l2ev; c[NC + DEV] = drt;
-  c[NC + TR] = nh1 + m2w + m2 + l1ev;         // probe, EX_REQ probe, insert, L1-D-eviction probe
-  c[NC + TW] = upg + m2 + l1ev + h2;          // upgrade, insert, cached_loc clear, cached_loc set
-  c[NC + DR] = h2 + l2ev;                     // readCacheLine, eviction
-  c[NC + DW] = nwr + m2;                      // write-through, insert
-  uint64_t* ctr = cs.counters + (uint64_t)tile * 2 * NC;
-  if ((g.u1 & (GG_WAVE - 1)) == 0) {
+  replay_counters(cs, g, cnt, len, tile, lane, active);
+}
+
+// ---------------------------------------------------------------------------
+// Lean replay for the reference geometries (L1-D assoc <= 4, L2 assoc <= 8).
+// Same semantics as k_cache_replay; per-unit state re-packed for fewer
+// instructions per access:
+//   L1-D: t1[] line numbers (stale when the way is invalid), st1 = 2-bit
+//         states, a1 = 4-bit LRU ages, pos1 = per-way byte "L2 slot"
+//         (s * A2 + way of the line's L2 copy; 0xFF = none).  The slot code
+//         turns "does the L1-D hold the L2 victim" into one SWAR byte match.
+//   L2:   tags [s][lane][4*TQ] u32 in LDS (canonical: ~0 = invalid, updated by
+//         predicated ds_write_b32), meta [s][lane] = {ages u32, states u16 | rr}.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t zero_nibbles(uint32_t x)
+{
+  return ~(((x & 0x77777777u) + 0x77777777u) | x | 0x77777777u) & 0x88888888u;
+}
+__device__ __forceinline__ uint32_t zero_bytes32(uint32_t x)
+{
+  return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu) & 0x80808080u;
+}
+// LRUReplacementPolicy::update on nibble-packed ages (ages < 8; unused = 0xF)
+__device__ __forceinline__ uint32_t lru_nib(uint32_t ages, uint32_t way)
+{
+  const uint32_t sh = 4 * way;
+  const uint32_t acc = (ages >> sh) & 0xFu;
+  const uint32_t x = (ages | 0x88888888u) - acc * 0x11111111u;   // bit 3 of a nibble: age >= acc
+  const uint32_t lt = ~x & 0x88888888u;
+  return (ages + (lt >> 3)) & ~(0xFu << sh);
+}
+// getReplacementWay: first invalid way (2-bit state == 0) else the last way with age A-1
+template <int A>
+__device__ __forceinline__ int victim_nib(uint32_t states, uint32_t ages)
+{
+  constexpr uint32_t PAIRS = (A >= 16) ? 0x55555555u : ((1u << (2 * A)) - 1) & 0x55555555u;
+  const uint32_t ip = ~(states | (states >> 1)) & PAIRS;
+  const int fi = (int)(__builtin_ctz(ip | 0x80000000u) >> 1);
+  const uint32_t zn = zero_nibbles(ages ^ ((uint32_t)(A - 1) * 0x11111111u));
+  const int lw = zn ? (int)((31 - __builtin_clz(zn)) >> 2) : -1;
+  return ip ? fi : lw;
+}
+
+template <int A1, int A2, bool LRU1, bool LRU2>
+__global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_geom g,
+    const uint64_t* __restrict__ sh_key, const uint32_t* __restrict__ sh_idx,
+    const uint32_t* __restrict__ unit_len, const uint64_t* __restrict__ unit_base,
+    const uint64_t* __restrict__ tile_off, uint32_t* __restrict__ result,
+    uint64_t* __restrict__ evicted, uint32_t* err)
+{
+  static_assert(A1 <= 4 && A2 <= 8, "lean replay covers L1-D assoc <= 4, L2 assoc <= 8");
+  constexpr int TQ = (A2 + 3) / 4;
+  constexpr int MW = 1;                            // HBM meta words per L2 set (A2 <= 8)
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t lane = threadIdx.x;
+  const uint64_t u = (uint64_t)blockIdx.x * GG_WAVE + lane;
+  const bool active = u < g.units;
+  const uint64_t uu = active ? u : 0;
+  const uint32_t S2 = g.s2;
+  const uint32_t l1set = (uint32_t)(uu & (g.u1 - 1));
+  uint32_t errv = 0;
+
+  uint32_t* T = reinterpret_cast<uint32_t*>(smem);                                   // [s][lane][4*TQ]
+  uint2* Mt = reinterpret_cast<uint2*>(smem + (size_t)S2 * GG_WAVE * TQ * 16);        // [s][lane]
+  auto tptr = [&](uint32_t s) -> uint32_t* { return T + ((size_t)s * GG_WAVE + lane) * (4 * TQ); };
+
+  // ---- load + re-pack state ----
+  uint64_t t1[A1];
+  uint32_t st1 = 0, a1 = 0xFFFFFFFFu, pos1 = 0xFFFFFFFFu;
+  {
+    const uint64_t m1 = cs.l1_meta[uu];
 #pragma unroll
-    for (int k = 0; k < 2 * NC; ++k) {
-      uint32_t a = active ? c[k] : 0u;
-      for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
-      if (lane == 0 && a) atomicAdd((unsigned long long*)&ctr[k], (unsigned long long)a);
+    for (int w = 0; w < A1; ++w) {
+      t1[w] = cs.l1_tag[(uint64_t)w * g.units + uu];
+      const uint32_t b = (uint32_t)(m1 >> (8 * w)) & 0xFFu;
+      const uint32_t st = (t1[w] == GG_L1_INV_TAG) ? 0u : GG_M_STATE(b);
+      errv |= (t1[w] != GG_L1_INV_TAG && st == GG_MS_I) ? GG_DERR_STATE : 0u;   // valid tag, INVALID state
+      st1 |= st << (2 * w);
+      a1 = (a1 & ~(0xFu << (4 * w))) | ((GG_M_AGE(b) & 0xFu) << (4 * w));
     }
-  } else if (active) {
-#pragma unroll
-    for (int k = 0; k < 2 * NC; ++k)
-      if (c[k]) atomicAdd((unsigned long long*)&ctr[k], (unsigned long long)c[k]);
   }
+  uint32_t rr1 = cs.l1_rr[uu];
+  uint32_t nloc = 0, nheld = 0;
+  for (uint32_t s = 0; s < S2; ++s) {
+    uint32_t tg[4 * TQ];
+#pragma unroll
+    for (int w = 0; w < 4 * TQ; ++w)
+      tg[w] = (w < A2) ? cs.l2_tag[(uint64_t)(s * A2 + w) * g.units + uu] : GG_L2_INV_TAG;
+    const uint64_t mw = cs.l2_meta[(uint64_t)(s * MW) * g.units + uu];
+    uint32_t ages = 0xFFFFFFFFu, st = 0;
+#pragma unroll
+    for (int w = 0; w < A2; ++w) {
+      const uint32_t b = (uint32_t)(mw >> (8 * w)) & 0xFFu;
+      const bool valid = tg[w] != GG_L2_INV_TAG;
+      errv |= (valid != (GG_M_STATE(b) != GG_MS_I)) ? GG_DERR_STATE : 0u;
+      st |= (valid ? GG_M_STATE(b) : 0u) << (2 * w);
+      ages = (ages & ~(0xFu << (4 * w))) | ((GG_M_AGE(b) & 0xFu) << (4 * w));
+      // cached_loc invariant + the L1-D way holding this line
+      const uint64_t ln = ((uint64_t)tg[w] << g.log_l2) | ((uint64_t)s << g.log_u1) | l1set;
+      int hw = -1;
+#pragma unroll
+      for (int k = 0; k < A1; ++k) hw = (valid && ((st1 >> (2 * k)) & 3u) && t1[k] == ln) ? k : hw;
+      const bool loc = GG_M_LOC(b) != 0;
+      nloc += loc ? 1u : 0u;
+      nheld += (hw >= 0) ? 1u : 0u;
+      errv |= (loc != (hw >= 0)) ? GG_DERR_STATE : 0u;
+      if (hw >= 0) pos1 = (pos1 & ~(0xFFu << (8 * hw))) | ((s * A2 + w) << (8 * hw));
+    }
+    uint32_t* tp = tptr(s);
+#pragma unroll
+    for (int q = 0; q < TQ; ++q)
+      *reinterpret_cast<uint4*>(tp + 4 * q) = make_uint4(tg[4 * q], tg[4 * q + 1], tg[4 * q + 2], tg[4 * q + 3]);
+    const uint32_t rr = LRU2 ? 0u : cs.l2_rr[(uint64_t)s * g.units + uu];
+    Mt[s * GG_WAVE + lane] = make_uint2(ages, st | (rr << 16));
+  }
+  {
+    uint32_t nvalid = 0;
+#pragma unroll
+    for (int k = 0; k < A1; ++k) nvalid += ((st1 >> (2 * k)) & 3u) ? 1u : 0u;
+    if (active && nvalid != nheld) errv |= GG_DERR_STATE;          // an L1-D line without its L2 copy
+  }
+
+  const uint32_t len = active ? unit_len[uu] : 0;
+  const uint64_t base = active ? unit_base[uu] : 0;
+  const uint32_t tile = (uint32_t)(uu >> g.log_u1);
+  const uint64_t rbase = tile_off[tile];
+  uint32_t maxlen = len;
+  for (int o = 32; o > 0; o >>= 1) maxlen = max(maxlen, (uint32_t)__shfl_xor((int)maxlen, o));
+
+  uint32_t cnt[NI];
+#pragma unroll
+  for (int k = 0; k < NI; ++k) cnt[k] = 0;
+  constexpr int PD = 2;
+  uint64_t kr[PD]; uint32_t ir[PD];
+#pragma unroll
+  for (int d = 0; d < PD; ++d) {
+    kr[d] = (d < (int)len) ? sh_key[base + d] : 0;
+    ir[d] = (d < (int)len) ? sh_idx[base + d] : 0;
+  }
+  const uint32_t s2m = S2 - 1;
+  const uint32_t log_line = g.log_line, log_u1 = g.log_u1, log_l2 = g.log_l2;
+
+  for (uint32_t j = 0; j < maxlen; ++j) {
+    const bool live = j < len;
+    const uint64_t key = kr[0];
+    const uint32_t idx = ir[0];
+#pragma unroll
+    for (int d = 0; d < PD - 1; ++d) { kr[d] = kr[d + 1]; ir[d] = ir[d + 1]; }
+    const bool more = j + PD < len;
+    kr[PD - 1] = more ? sh_key[base + j + PD] : 0;
+    ir[PD - 1] = more ? sh_idx[base + j + PD] : 0;
+    if (!live) continue;
+
+    const uint64_t line = key >> log_line;
+    const uint32_t wr = (uint32_t)key & 1u;
+    const uint32_t s = (uint32_t)(line >> log_u1) & s2m;
+    const uint32_t tag2 = (uint32_t)(line >> log_l2);
+    uint32_t* tp = tptr(s);
+    uint32_t tg[4 * TQ];
+#pragma unroll
+    for (int q = 0; q < TQ; ++q) {
+      const uint4 v = *reinterpret_cast<const uint4*>(tp + 4 * q);
+      tg[4 * q] = v.x; tg[4 * q + 1] = v.y; tg[4 * q + 2] = v.z; tg[4 * q + 3] = v.w;
+    }
+    const uint2 mt = Mt[s * GG_WAVE + lane];
+    uint32_t ages2 = mt.x, st2 = mt.y & 0xFFFFu, rr2 = (mt.y >> 16) & 0xFFu;
+
+    // L1-D lookup among valid ways (operationPermissibleinL1Cache)
+    uint32_t mm = 0;
+#pragma unroll
+    for (int w = 0; w < A1; ++w) mm |= (t1[w] == line) ? (1u << (2 * w)) : 0u;
+    mm &= (st1 | (st1 >> 1)) & 0x55u;
+    const int w1 = mm ? (int)(__builtin_ctz(mm) >> 1) : -1;
+    const uint32_t s1 = (st1 >> ((2 * w1) & 31)) & 3u;                // 0 when w1 < 0
+    const bool hit1 = s1 > wr;                                         // READ: readable, WRITE: writable
+    // L2 lookup (processShmemRequestFromL1Cache)
+    int w2 = -1;
+#pragma unroll
+    for (int w = 0; w < A2; ++w) w2 = (tg[w] == tag2) ? w : w2;
+    const uint32_t s2 = (st2 >> ((2 * w2) & 31)) & 3u;
+    const bool hit2n = s2 > wr;
+    const bool hit2 = !hit1 && hit2n;
+    const bool miss2 = !hit1 && !hit2n;
+    const bool upg = miss2 && wr && s2 == GG_MS_S;
+    const bool w1v = !hit1 && w1 >= 0;
+    errv |= (hit1 && wr && w2 < 0) ? GG_DERR_STATE : 0u;
+
+    // invalidate the L1-D copy before going to L2 (l1:135-137)
+    const uint32_t m1 = 3u << ((2 * w1) & 31);
+    st1 = w1v ? (st1 & ~m1) : st1;
+    pos1 = w1v ? (pos1 | (0xFFu << ((8 * w1) & 31))) : pos1;
+    // upgrade: invalidate the SHARED L2 line (l2:260-282)
+    if (upg) tp[w2] = GG_L2_INV_TAG;
+    st2 = upg ? (st2 & ~(3u << (2 * w2))) : st2;
+    // L2 victim / eviction (l2:74-116)
+    int v2 = LRU2 ? victim_nib<A2>(st2, ages2) : (int)rr2;
+    errv |= (miss2 && v2 < 0) ? GG_DERR_STATE : 0u;
+    v2 &= 7;
+    const uint32_t sv = (st2 >> (2 * v2)) & 3u;
+    const bool l2ev = miss2 && sv != 0;
+    const bool dirty = l2ev && sv == GG_MS_M;
+    uint32_t vt = 0;
+    if (evicted) {
+#pragma unroll
+      for (int w = 0; w < A2; ++w) vt = (w == v2) ? tg[w] : vt;
+    }
+    // invalidateCacheLineInL1: does the L1-D hold L2 slot (s, v2)?
+    const uint32_t zb = zero_bytes32(pos1 ^ ((s * A2 + v2) * 0x01010101u));
+    const bool invl1 = l2ev && zb != 0;
+    const uint32_t we = zb ? (uint32_t)(__builtin_ctz(zb) >> 3) : 0u;
+    st1 = invl1 ? (st1 & ~(3u << (2 * we))) : st1;
+    pos1 = invl1 ? (pos1 | (0xFFu << (8 * we))) : pos1;
+    // install (EX_REP -> MODIFIED, SH_REP -> SHARED)
+    const uint32_t ns = 1u + wr;
+    if (miss2) tp[v2] = tag2;
+    st2 = miss2 ? ((st2 & ~(3u << (2 * v2))) | (ns << (2 * v2))) : st2;
+    if (!LRU2 && miss2) rr2 = rr2 ? rr2 - 1 : (A2 - 1);
+    // L2 LRU: readCacheLine (hit2) / insert (miss2) / write-through (hit1 && wr)
+    if (LRU2) {
+      const uint32_t x2 = miss2 ? (uint32_t)v2 : (uint32_t)(w2 & 7);
+      const uint32_t nb = lru_nib(ages2, x2);
+      ages2 = (!hit1 || wr) ? nb : ages2;
+    }
+    // L1-D insert (insertCacheLineInL1) after both invalidations
+    int v1 = LRU1 ? victim_nib<A1>(st1, a1) : (int)rr1;
+    errv |= (!hit1 && v1 < 0) ? GG_DERR_STATE : 0u;
+    v1 &= 3;
+    const bool l1ev = !hit1 && ((st1 >> (2 * v1)) & 3u) != 0;
+    const uint32_t ins = hit2 ? s2 : ns;
+#pragma unroll
+    for (int w = 0; w < A1; ++w) t1[w] = (!hit1 && w == v1) ? line : t1[w];
+    const uint32_t slot = s * A2 + (uint32_t)(hit2 ? (w2 & 7) : v2);
+    st1 = !hit1 ? ((st1 & ~(3u << (2 * v1))) | (ins << (2 * v1))) : st1;
+    pos1 = !hit1 ? ((pos1 & ~(0xFFu << (8 * v1))) | (slot << (8 * v1))) : pos1;
+    if (!LRU1 && !hit1) rr1 = rr1 ? rr1 - 1 : (A1 - 1);
+    // L1-D LRU: accessCache on the hit way or the inserted way
+    if (LRU1) a1 = lru_nib(a1, hit1 ? (uint32_t)(w1 & 3) : (uint32_t)v1);
+
+    Mt[s * GG_WAVE + lane] = make_uint2(ages2, st2 | (rr2 << 16));
+
+    cnt[I_WR] += wr; cnt[I_NH1] += !hit1; cnt[I_NH1W] += (!hit1 && wr); cnt[I_M2] += miss2;
+    cnt[I_M2W] += (miss2 && wr); cnt[I_W1V] += w1v; cnt[I_L1EV] += l1ev; cnt[I_L2EV] += l2ev;
+    cnt[I_DIRTY] += dirty; cnt[I_INVL1] += invl1; cnt[I_UPG] += upg;
+    const uint32_t res = (hit1 ? GG_RES_L1_HIT : (hit2 ? GG_RES_L2_HIT : GG_RES_DIRECTORY)) |
+                         (upg ? GG_RES_UPGRADE : 0u) | (l1ev ? GG_RES_L1_EVICT : 0u) |
+                         (l2ev ? GG_RES_L2_EVICT : 0u) | (dirty ? GG_RES_L2_EVICT_DIRTY : 0u) |
+                         (invl1 ? GG_RES_L2_EVICT_INV_L1 : 0u);
+    if (result) result[rbase + idx] = res;
+    if (evicted) {
+      const uint64_t e2 = ((uint64_t)vt << log_l2) | ((uint64_t)s << log_u1) | l1set;
+      evicted[rbase + idx] = l2ev ? (e2 << log_line) : ~0ull;
+    }
+  }
+
+  // ---- store state back in the HBM format (canonical tags, byte meta, cached_loc) ----
+  if (active) {
+    uint64_t m1 = 0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      if (w < A1) {
+        const uint32_t st = (st1 >> (2 * w)) & 3u;
+        cs.l1_tag[(uint64_t)w * g.units + u] = st ? t1[w] : GG_L1_INV_TAG;
+        m1 |= (uint64_t)GG_M_MAKE(st, 0, (a1 >> (4 * w)) & 0xFu) << (8 * w);
+      } else {
+        m1 |= 0xF8ull << (8 * w);
+      }
+    }
+    cs.l1_meta[u] = m1;
+    cs.l1_rr[u] = (uint8_t)rr1;
+    for (uint32_t s = 0; s < S2; ++s) {
+      const uint32_t* tp = tptr(s);
+      const uint2 mt = Mt[s * GG_WAVE + lane];
+      uint64_t mw = 0;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        if (w < A2) {
+          const uint32_t st = (mt.y >> (2 * w)) & 3u;
+          // cached_loc: does an L1-D way name this slot?
+          const uint32_t zb = zero_bytes32(pos1 ^ ((s * A2 + w) * 0x01010101u));
+          mw |= (uint64_t)GG_M_MAKE(st, (zb != 0) ? 1u : 0u, (mt.x >> (4 * w)) & 0xFu) << (8 * w);
+          cs.l2_tag[(uint64_t)(s * A2 + w) * g.units + u] = tp[w];
+        } else {
+          mw |= 0xF8ull << (8 * w);
+        }
+      }
+      cs.l2_meta[(uint64_t)s * g.units + u] = mw;
+      if (!LRU2) cs.l2_rr[(uint64_t)s * g.units + u] = (uint8_t)((mt.y >> 16) & 0xFFu);
+    }
+  }
+  if (!active) errv = 0;
+  if (errv) atomicOr(err, errv);
+  replay_counters(cs, g, cnt, len, tile, lane, active);
 }
 
 // ---------------------------------------------------------------------------
@@ -763,6 +1061,20 @@ const Kern kKernels[] = {
   GG_KERN(4, 2, 1, 1), GG_KERN(4, 32, 1, 1),
 };
 
+#define GG_LEAN(A1, A2, P1, P2) { A1, A2, P1, P2, k_cache_replay_lean<A1, A2, P1, P2>, k_quartet<A1, A2> }
+const Kern kLean[] = {
+  GG_LEAN(4, 8, 1, 1), GG_LEAN(4, 8, 0, 0), GG_LEAN(4, 8, 1, 0), GG_LEAN(4, 8, 0, 1),
+  GG_LEAN(4, 4, 1, 1), GG_LEAN(2, 4, 1, 1), GG_LEAN(2, 8, 1, 1), GG_LEAN(4, 2, 1, 1),
+};
+
+const Kern* find_lean(uint32_t a1, uint32_t a2, uint32_t pol1, uint32_t pol2)
+{
+  const int l1 = pol1 == GG_POLICY_LRU, l2 = pol2 == GG_POLICY_LRU;
+  for (const Kern& k : kLean)
+    if ((uint32_t)k.a1 == a1 && (uint32_t)k.a2 == a2 && k.lru1 == l1 && k.lru2 == l2) return &k;
+  return nullptr;
+}
+
 const Kern* find_kernel(uint32_t a1, uint32_t a2, uint32_t pol1, uint32_t pol2)
 {
   const int l1 = pol1 == GG_POLICY_LRU, l2 = pol2 == GG_POLICY_LRU;
@@ -771,8 +1083,9 @@ const Kern* find_kernel(uint32_t a1, uint32_t a2, uint32_t pol1, uint32_t pol2)
   return nullptr;
 }
 
-size_t replay_lds_bytes(const gg_geom& g)
+size_t replay_lds_bytes(const gg_geom& g, bool lean)
 {
+  if (lean) return (size_t)g.s2 * GG_WAVE * ((g.a2 + 3) / 4) * 16 + (size_t)g.s2 * GG_WAVE * 8;
   const size_t tq = (g.a2 + 3) / 4;
   return (size_t)g.s2 * GG_WAVE * tq * 16 + (size_t)g.s2 * GG_WAVE * g.mw * 8 +
          (g.pol2 == GG_POLICY_LRU ? 0 : (size_t)g.s2 * GG_WAVE);
@@ -798,7 +1111,7 @@ gg_status gg_cache_state_alloc(gg_ctx* ctx)
   if (!find_kernel(g.a1, g.a2, g.pol1, g.pol2))
     return gg_fail(GG_ERR_UNSUPPORTED, "no replay kernel instantiated for L1-D assoc %u / L2 assoc %u / policies %u,%u",
                    g.a1, g.a2, g.pol1, g.pol2);
-  if (replay_lds_bytes(g) > 64 * 1024)
+  if (replay_lds_bytes(g, false) > 64 * 1024)
     return gg_fail(GG_ERR_UNSUPPORTED, "L2 lines per L1-D set (%u) too large for the LDS-resident replay", g.s2 * g.a2);
   GG_HIP(hipMalloc((void**)&cs.l1_tag, sizeof(uint64_t) * g.a1 * g.units));
   GG_HIP(hipMalloc((void**)&cs.l1_meta, sizeof(uint64_t) * g.units));
@@ -895,10 +1208,11 @@ gg_status gg_cache_run_batch(gg_ctx* ctx, const gg_trace* tr, uint32_t* result, 
     GG_HIP(hipGetLastError());
     gg_timer_end(ctx, "cache_shard", s);
   }
-  const Kern* k = find_kernel(g.a1, g.a2, g.pol1, g.pol2);
+  const Kern* k = (ctx->replay_variant != 1) ? find_lean(g.a1, g.a2, g.pol1, g.pol2) : nullptr;
+  if (!k) k = find_kernel(g.a1, g.a2, g.pol1, g.pol2);
   const uint32_t groups = (uint32_t)((g.units + GG_WAVE - 1) / GG_WAVE);
   gg_timer_begin(ctx, "cache_replay", s);
-  hipLaunchKernelGGL(k->replay, dim3(groups), dim3(GG_WAVE), replay_lds_bytes(g), s, ctx->cs, g,
+  hipLaunchKernelGGL(k->replay, dim3(groups), dim3(GG_WAVE), replay_lds_bytes(g, k == find_lean(g.a1, g.a2, g.pol1, g.pol2)), s, ctx->cs, g,
                      (const uint64_t*)ctx->sh_key, (const uint32_t*)ctx->sh_idx, (const uint32_t*)ctx->unit_len,
                      (const uint64_t*)ctx->unit_base, (const uint64_t*)ctx->tile_off_dev, result, evicted, ctx->err_dev);
   GG_HIP(hipGetLastError());

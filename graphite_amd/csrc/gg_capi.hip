@@ -120,6 +120,7 @@ gg_ctx* gg_create(const gg_config* cfg, gg_status* status)
   gg_ctx* ctx = new gg_ctx();
   ctx->cfg = c;
   ctx->device = c.device;
+  ctx->replay_variant = (int)c.replay_kernel;
   gg_geom& g = ctx->g;
   g.tiles = c.num_tiles;
   g.log_line = floor_log2(c.line_size);

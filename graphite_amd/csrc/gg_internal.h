@@ -87,6 +87,8 @@ struct gg_ctx {
   std::vector<uint64_t> h_chunk_start;
   // NoC
   gg_noc_state* noc = nullptr;
+  // replay kernel choice: 0 = lean when instantiated (default), 1 = generic
+  int replay_variant = 0;
   // timing
   bool timing = false;
   std::vector<gg_timer> timers;

@@ -138,7 +138,8 @@ typedef struct gg_config {
   uint32_t total_tiles;        /* app tiles + MCP + spawners (config.cc:77-82); 0 = num_tiles+2 */
   double   frequency_ghz;      /* single DVFS domain (carbon_sim.cfg:147-155)        */
   int32_t  device;             /* HIP device ordinal                                 */
-  uint32_t reserved[7];
+  uint32_t replay_kernel;      /* 0 = fastest instantiated replay kernel, 1 = generic */
+  uint32_t reserved[6];
 } gg_config;
 
 /* Fill cfg with the reference defaults of carbon_sim.cfg for num_tiles tiles. */

@@ -42,11 +42,14 @@ def run_gpu(cfg, addr, meta, offs, torch, chunks=1, want_ev=True):
 
 @pytest.mark.parametrize("name", [k for k, v in M.items() if v["kind"] == "modep"])
 @pytest.mark.parametrize("chunks", [1, 3])
-def test_replay_matches_reference_fixtures(name, chunks):
+@pytest.mark.parametrize("kern", [0, 1])          # 0 = lean replay where instantiated, 1 = generic
+def test_replay_matches_reference_fixtures(name, chunks, kern):
     torch = torch_dev()
     e = M[name]
     addr, meta, offs = modep_trace(e)
-    be, res, ev = run_gpu(modep_config(e), addr, meta, offs, torch, chunks=chunks)
+    cfg = modep_config(e)
+    cfg.replay_kernel = kern
+    be, res, ev = run_gpu(cfg, addr, meta, offs, torch, chunks=chunks)
     np.testing.assert_array_equal(res.astype(np.uint8), load(e["result_file"], np.uint8))
     cnt = load(e["counters_file"], np.uint64).reshape(e["tiles"], 2, C.NUM_CACHE_COUNTERS)
     np.testing.assert_array_equal(be.cache_counters(), cnt)
@@ -77,11 +80,12 @@ def ragged_trace(T, seed, lines_log2, max_len):
     dict(l1d_policy=C.POLICY_ROUND_ROBIN, l2_policy=C.POLICY_ROUND_ROBIN),
     dict(l1d_size_kb=16, l1d_assoc=8, l2_size_kb=256, l2_assoc=8),
 ])
-def test_replay_matches_oracle_ragged(geom):
+@pytest.mark.parametrize("kern", [0, 1])
+def test_replay_matches_oracle_ragged(geom, kern):
     torch = torch_dev()
     T = 24
     addr, meta, offs = ragged_trace(T, 7, 12, 20000)
-    cfg = C.default_config(T, **geom)
+    cfg = C.default_config(T, replay_kernel=kern, **geom)
     oc = po.OracleCache(cfg)
     ref, ref_ev = oc.run(addr, meta, offs, want_evicted=True)
     be, res, ev = run_gpu(cfg, addr, meta, offs, torch, chunks=2)
