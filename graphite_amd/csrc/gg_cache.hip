@@ -166,33 +166,57 @@ __global__ __launch_bounds__(256) void k_shard_hist(const uint64_t* __restrict__
   for (uint32_t s = threadIdx.x; s < g.u1; s += blockDim.x) cnt[(uint64_t)c * g.u1 + s] = h[s];
 }
 
-// Pass 2: per tile, exclusive scan over its chunks per set (in place), unit
-// lengths, and unit bases = tile offset + exclusive scan over sets.
+// Pass 2: per tile, exclusive scan over its chunks per set (in place) and the
+// unit lengths.
 __global__ void k_shard_scan(uint32_t* __restrict__ cnt, const uint32_t* __restrict__ tile_chunk0,
-                             const uint64_t* __restrict__ tile_off, uint32_t* __restrict__ unit_len,
-                             uint64_t* __restrict__ unit_base, gg_geom g)
+                             uint32_t* __restrict__ unit_len, gg_geom g)
 {
-  __shared__ uint64_t sc[1024];
   const uint32_t t = blockIdx.x, s = threadIdx.x;
+  if (s >= g.u1) return;
   uint64_t acc = 0;
-  if (s < g.u1) {
-    for (uint32_t c = tile_chunk0[t]; c < tile_chunk0[t + 1]; ++c) {
-      uint32_t* p = &cnt[(uint64_t)c * g.u1 + s];
-      const uint32_t v = *p;
-      *p = (uint32_t)acc;
-      acc += v;
-    }
-    unit_len[(uint64_t)t * g.u1 + s] = (uint32_t)acc;
+  for (uint32_t c = tile_chunk0[t]; c < tile_chunk0[t + 1]; ++c) {
+    uint32_t* p = &cnt[(uint64_t)c * g.u1 + s];
+    const uint32_t v = *p;
+    *p = (uint32_t)acc;
+    acc += v;
   }
-  sc[s] = (s < g.u1) ? acc : 0;
+  unit_len[(uint64_t)t * g.u1 + s] = (uint32_t)acc;
+}
+
+// Pass 2b: interleaved sharded layout.  The 64 units of a replay wave form a
+// group; record j of unit u lives at unit_base[u] + 64*j, unit_base[u] =
+// group base + (u % 64), group bases = exclusive scan of 64 * (longest unit of
+// the group).  One block; writes the total slot count to *total.
+__global__ __launch_bounds__(1024) void k_group_scan(const uint32_t* __restrict__ unit_len, uint64_t units,
+                                                     uint64_t* __restrict__ unit_base, uint64_t* __restrict__ total)
+{
+  __shared__ uint64_t part[1024];
+  const uint32_t t = threadIdx.x;
+  const uint64_t groups = (units + GG_WAVE - 1) / GG_WAVE;
+  const uint64_t per = (groups + blockDim.x - 1) / blockDim.x;
+  const uint64_t g0 = t * per, g1 = min(groups, g0 + per);
+  uint64_t sum = 0;
+  for (uint64_t gi = g0; gi < g1; ++gi) {
+    uint32_t m = 0;
+    for (uint32_t l = 0; l < GG_WAVE; ++l) { const uint64_t u = gi * GG_WAVE + l; if (u < units) m = max(m, unit_len[u]); }
+    sum += (uint64_t)m * GG_WAVE;
+  }
+  part[t] = sum;
   __syncthreads();
   for (uint32_t o = 1; o < blockDim.x; o <<= 1) {
-    const uint64_t v = (s >= o) ? sc[s - o] : 0;
+    const uint64_t v = (t >= o) ? part[t - o] : 0;
     __syncthreads();
-    sc[s] += v;
+    part[t] += v;
     __syncthreads();
   }
-  if (s < g.u1) unit_base[(uint64_t)t * g.u1 + s] = tile_off[t] + sc[s] - acc;
+  uint64_t base = part[t] - sum;
+  if (t == blockDim.x - 1) *total = part[t];
+  for (uint64_t gi = g0; gi < g1; ++gi) {
+    uint32_t m = 0;
+    for (uint32_t l = 0; l < GG_WAVE; ++l) { const uint64_t u = gi * GG_WAVE + l; if (u < units) m = max(m, unit_len[u]); }
+    for (uint32_t l = 0; l < GG_WAVE; ++l) { const uint64_t u = gi * GG_WAVE + l; if (u < units) unit_base[u] = base + l; }
+    base += (uint64_t)m * GG_WAVE;
+  }
 }
 
 // Pass 3: one wave per chunk, 64 records per step in program order; lanes
@@ -205,11 +229,14 @@ __global__ __launch_bounds__(64) void k_shard_scatter(const uint64_t* __restrict
     const uint64_t* __restrict__ tile_off, uint64_t* __restrict__ sh_key,
     uint32_t* __restrict__ sh_idx, gg_geom g)
 {
-  __shared__ uint64_t base[1024];
+  __shared__ uint64_t ubase[1024];
+  __shared__ uint32_t rank0[1024];
   const uint32_t c = blockIdx.x, lane = threadIdx.x;
   const uint32_t t = chunk_tile[c];
-  for (uint32_t s = lane; s < g.u1; s += GG_WAVE)
-    base[s] = unit_base[(uint64_t)t * g.u1 + s] + cnt[(uint64_t)c * g.u1 + s];
+  for (uint32_t s = lane; s < g.u1; s += GG_WAVE) {
+    ubase[s] = unit_base[(uint64_t)t * g.u1 + s];
+    rank0[s] = cnt[(uint64_t)c * g.u1 + s];
+  }
   __syncthreads();
   const uint64_t start = chunk_start[c];
   const uint32_t len = chunk_len[c];
@@ -229,12 +256,12 @@ __global__ __launch_bounds__(64) void k_shard_scatter(const uint64_t* __restrict
       peers &= bit ? bb : ~bb;
     }
     const uint32_t rank = __popcll(peers & lt_mask);
-    const uint64_t b0 = valid ? base[s] : 0;
+    const uint32_t r0 = valid ? rank0[s] : 0;
     __builtin_amdgcn_wave_barrier();
-    if (valid && rank == 0) base[s] = b0 + __popcll(peers);
+    if (valid && rank == 0) rank0[s] = r0 + (uint32_t)__popcll(peers);
     __builtin_amdgcn_wave_barrier();
     if (valid) {
-      const uint64_t pos = b0 + rank;
+      const uint64_t pos = ubase[s] + (uint64_t)(r0 + rank) * GG_WAVE;
       sh_key[pos] = (a & line_mask) | (m & GG_META_WRITE);
       sh_idx[pos] = rel0 + i;
     }
@@ -429,8 +456,8 @@ __global__ __launch_bounds__(64) void k_cache_replay(gg_cache_state cs, gg_geom 
   uint64_t kr[PD]; uint32_t ir[PD];
 #pragma unroll
   for (int d = 0; d < PD; ++d) {
-    kr[d] = (d < (int)len) ? sh_key[base + d] : 0;
-    ir[d] = (d < (int)len) ? sh_idx[base + d] : 0;
+    kr[d] = (d < (int)len) ? sh_key[base + (uint64_t)d * GG_WAVE] : 0;
+    ir[d] = (d < (int)len) ? sh_idx[base + (uint64_t)d * GG_WAVE] : 0;
   }
   const uint64_t lmask = (g.s2 - 1);
 
@@ -441,8 +468,8 @@ __global__ __launch_bounds__(64) void k_cache_replay(gg_cache_state cs, gg_geom 
 #pragma unroll
     for (int d = 0; d < PD - 1; ++d) { kr[d] = kr[d + 1]; ir[d] = ir[d + 1]; }
     const bool more = j + PD < len;
-    kr[PD - 1] = more ? sh_key[base + j + PD] : 0;
-    ir[PD - 1] = more ? sh_idx[base + j + PD] : 0;
+    kr[PD - 1] = more ? sh_key[base + (uint64_t)(j + PD) * GG_WAVE] : 0;
+    ir[PD - 1] = more ? sh_idx[base + (uint64_t)(j + PD) * GG_WAVE] : 0;
     if (!live) continue;
 
     const uint64_t line = key >> g.log_line;
@@ -725,8 +752,8 @@ __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_
   uint64_t kr[PD]; uint32_t ir[PD];
 #pragma unroll
   for (int d = 0; d < PD; ++d) {
-    kr[d] = (d < (int)len) ? sh_key[base + d] : 0;
-    ir[d] = (d < (int)len) ? sh_idx[base + d] : 0;
+    kr[d] = (d < (int)len) ? sh_key[base + (uint64_t)d * GG_WAVE] : 0;
+    ir[d] = (d < (int)len) ? sh_idx[base + (uint64_t)d * GG_WAVE] : 0;
   }
   const uint32_t s2m = S2 - 1;
   const uint32_t log_line = g.log_line, log_u1 = g.log_u1, log_l2 = g.log_l2;
@@ -738,8 +765,8 @@ __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_
 #pragma unroll
     for (int d = 0; d < PD - 1; ++d) { kr[d] = kr[d + 1]; ir[d] = ir[d + 1]; }
     const bool more = j + PD < len;
-    kr[PD - 1] = more ? sh_key[base + j + PD] : 0;
-    ir[PD - 1] = more ? sh_idx[base + j + PD] : 0;
+    kr[PD - 1] = more ? sh_key[base + (uint64_t)(j + PD) * GG_WAVE] : 0;
+    ir[PD - 1] = more ? sh_idx[base + (uint64_t)(j + PD) * GG_WAVE] : 0;
     if (!live) continue;
 
     const uint64_t line = key >> log_line;
@@ -1122,6 +1149,7 @@ gg_status gg_cache_state_alloc(gg_ctx* ctx)
   GG_HIP(hipMalloc((void**)&cs.counters, sizeof(uint64_t) * g.tiles * 2 * GG_NUM_CACHE_COUNTERS));
   GG_HIP(hipMalloc((void**)&ctx->unit_len, sizeof(uint32_t) * g.units));
   GG_HIP(hipMalloc((void**)&ctx->unit_base, sizeof(uint64_t) * g.units));
+  GG_HIP(hipMalloc((void**)&ctx->total_dev, sizeof(uint64_t)));
   GG_HIP(hipMalloc((void**)&ctx->tile_off_dev, sizeof(uint64_t) * (g.tiles + 1)));
   return GG_OK;
 }
@@ -1131,7 +1159,7 @@ void gg_cache_state_free(gg_ctx* ctx)
   gg_cache_state& cs = ctx->cs;
   void* ps[] = {cs.l1_tag, cs.l1_meta, cs.l1_rr, cs.l2_tag, cs.l2_meta, cs.l2_rr, cs.counters,
                 ctx->sh_key, ctx->sh_idx, ctx->chunk_cnt, ctx->chunk_tile, ctx->chunk_start,
-                ctx->chunk_len, ctx->unit_len, ctx->unit_base, ctx->tile_off_dev};
+                ctx->chunk_len, ctx->unit_len, ctx->unit_base, ctx->tile_off_dev, ctx->total_dev};
   for (void* p : ps) if (p) hipFree(p);
 }
 
@@ -1178,11 +1206,6 @@ gg_status gg_cache_run_batch(gg_ctx* ctx, const gg_trace* tr, uint32_t* result, 
     GG_HIP(hipMalloc((void**)&ctx->chunk_len, sizeof(uint32_t) * cap));
     ctx->chunk_cap = cap;
   }
-  uint64_t cap_key = ctx->sh_cap, cap_idx = ctx->sh_cap;
-  if (gg_status st = grow(&ctx->sh_key, &cap_key, n)) return st;
-  if (gg_status st = grow(&ctx->sh_idx, &cap_idx, n)) return st;
-  ctx->sh_cap = std::min(cap_key, cap_idx);
-
   // upload tables (chunk_tile doubles as storage for tile_chunk0 after the chunk entries)
   GG_HIP(hipMemcpyAsync(ctx->chunk_tile, ctx->h_chunk_tile.data(), sizeof(uint32_t) * nchunks, hipMemcpyHostToDevice, s));
   GG_HIP(hipMemcpyAsync(ctx->chunk_tile + nchunks, tile_chunk0.data(), sizeof(uint32_t) * (g.tiles + 1), hipMemcpyHostToDevice, s));
@@ -1199,8 +1222,20 @@ gg_status gg_cache_run_batch(gg_ctx* ctx, const gg_trace* tr, uint32_t* result, 
   uint32_t scan_threads = 64;
   while (scan_threads < g.u1) scan_threads <<= 1;
   hipLaunchKernelGGL(k_shard_scan, dim3(g.tiles), dim3(scan_threads), 0, s, ctx->chunk_cnt,
-                     ctx->chunk_tile + nchunks, ctx->tile_off_dev, ctx->unit_len, ctx->unit_base, g);
+                     ctx->chunk_tile + nchunks, ctx->unit_len, g);
   GG_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_group_scan, dim3(1), dim3(1024), 0, s, ctx->unit_len, g.units, ctx->unit_base, ctx->total_dev);
+  GG_HIP(hipGetLastError());
+  // size the interleaved record buffers (one small device->host read per batch)
+  uint64_t total = 0;
+  GG_HIP(hipMemcpyAsync(&total, ctx->total_dev, sizeof(total), hipMemcpyDeviceToHost, s));
+  GG_HIP(hipStreamSynchronize(s));
+  {
+    uint64_t cap_key = ctx->sh_cap, cap_idx = ctx->sh_cap;
+    if (gg_status st = grow(&ctx->sh_key, &cap_key, total)) return st;
+    if (gg_status st = grow(&ctx->sh_idx, &cap_idx, total)) return st;
+    ctx->sh_cap = std::min(cap_key, cap_idx);
+  }
   if (nchunks) {
     hipLaunchKernelGGL(k_shard_scatter, dim3((uint32_t)nchunks), dim3(64), 0, s, tr->addr_dev, tr->meta_dev,
                        ctx->chunk_tile, ctx->chunk_start, ctx->chunk_len, ctx->chunk_cnt, ctx->unit_base,

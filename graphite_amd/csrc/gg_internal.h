@@ -81,7 +81,8 @@ struct gg_ctx {
   uint32_t* chunk_len = nullptr;
   uint64_t  chunk_cap = 0;
   uint32_t* unit_len = nullptr;  // [units]
-  uint64_t* unit_base = nullptr; // [units]
+  uint64_t* unit_base = nullptr; // [units] slot of record 0; record j at +64*j
+  uint64_t* total_dev = nullptr; // slots of the interleaved layout
   uint64_t* tile_off_dev = nullptr; // [tiles+1]
   std::vector<uint32_t> h_chunk_tile, h_chunk_len;
   std::vector<uint64_t> h_chunk_start;

@@ -1,0 +1,338 @@
+// graphite_host.hpp — C++ host side above the C ABI, mirroring the reference's
+// in-process interfaces so a Graphite-style caller reads the same:
+//
+//   graphite_amd::Cache          Cache::accessCacheLine / insertCacheLine /
+//                                getCacheLineInfo / setCacheLineInfo and
+//                                outputSummary (common/tile/memory_subsystem/cache/cache.h:87-92,
+//                                cache.cc:419-477), one (tile, level) of a context
+//   graphite_amd::TraceReplayer  the per-access loop of Core::initiateMemoryAccess
+//                                (common/tile/core/core.cc:139-266: line split,
+//                                miss count) batched through gg_cache_access_batch
+//   graphite_amd::NetworkModel   NetworkModel::routePacket (common/network/network_model.h:188)
+//                                + __processReceivedPacket, batched through
+//                                gg_noc_route_batch; Hop carries the same fields
+//                                (network_model.h:45-63)
+//
+// Errors: the reference aborts through LOG_ASSERT_ERROR (common/misc/log.h:112-135);
+// the mirror throws graphite_amd::Error carrying the ABI status and message.
+// Only host memory crosses this header's API; device buffers are internal.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <iomanip>
+#include <ostream>
+#include <queue>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/graphite_gpu.h"
+
+namespace graphite_amd {
+
+typedef uint64_t IntPtr;
+typedef uint8_t Byte;
+
+struct Error : std::runtime_error {
+  gg_status status;
+  Error(gg_status s, const std::string& m) : std::runtime_error(m), status(s) {}
+};
+
+inline void check(gg_status s, const char* what)
+{
+  if (s != GG_OK) throw Error(s, std::string(what) + ": " + gg_last_error());
+}
+inline void hip_check(hipError_t e, const char* what)
+{
+  if (e != hipSuccess) throw Error(GG_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// CacheState::Type values of the MSI protocol (cache_state.h:11-21)
+struct CacheState { enum Type { INVALID = 0, SHARED = 1, MODIFIED = 4 }; };
+// MemComponent::Type values (mem_component.h:9-18)
+struct MemComponent { enum Type { INVALID = 0, L1_DCACHE = 3 }; };
+
+// PrL2CacheLineInfo (pr_l1_pr_l2_dram_directory_msi/cache_line_info.h)
+class CacheLineInfo {
+ public:
+  explicit CacheLineInfo(IntPtr tag = ~(IntPtr)0, CacheState::Type cstate = CacheState::INVALID,
+                         MemComponent::Type loc = MemComponent::INVALID)
+  { _i.tag = tag; _i.cstate = cstate; _i.cached_loc = loc; }
+  bool isValid() const { return _i.tag != ~(IntPtr)0; }
+  IntPtr getTag() const { return _i.tag; }
+  CacheState::Type getCState() const { return (CacheState::Type)_i.cstate; }
+  MemComponent::Type getCachedLoc() const { return (MemComponent::Type)_i.cached_loc; }
+  void setTag(IntPtr t) { _i.tag = t; }
+  void setCState(CacheState::Type c) { _i.cstate = c; }
+  void setCachedLoc(MemComponent::Type l) { _i.cached_loc = l; }
+  void invalidate() { _i.tag = ~(IntPtr)0; _i.cstate = CacheState::INVALID; _i.cached_loc = MemComponent::INVALID; }
+  gg_line_info* raw() { return &_i; }
+ private:
+  gg_line_info _i;
+};
+
+// RAII owner of one gg_ctx (one per GPU)
+class Backend {
+ public:
+  explicit Backend(const gg_config& cfg) : _cfg(cfg)
+  {
+    gg_status st = GG_OK;
+    _ctx = gg_create(&cfg, &st);
+    if (!_ctx) check(st ? st : GG_ERR_INVALID, "gg_create");
+  }
+  ~Backend() { gg_destroy(_ctx); }
+  Backend(const Backend&) = delete;
+  Backend& operator=(const Backend&) = delete;
+  gg_ctx* ctx() const { return _ctx; }
+  const gg_config& config() const { return _cfg; }
+  void reset() { check(gg_reset(_ctx), "gg_reset"); }
+  std::vector<uint64_t> cacheCounters() const
+  {
+    std::vector<uint64_t> c((size_t)_cfg.num_tiles * 2 * GG_NUM_CACHE_COUNTERS);
+    check(gg_cache_get_counters(_ctx, c.data()), "gg_cache_get_counters");
+    return c;
+  }
+ private:
+  gg_config _cfg;
+  gg_ctx* _ctx = nullptr;
+};
+
+// Cache::outputSummary (cache.cc:419-477) for one cache's counters.  The empty
+// write-miss-rate line keeps the reference's 4-space indent (cache.cc:445); the
+// asynchronous-communication block is empty in a single DVFS domain.
+inline void writeCacheSummary(std::ostream& out, const std::string& name, const uint64_t* c,
+                              bool write_back, bool instruction_cache = false)
+{
+  out << "  Cache " << name << ": " << std::endl;
+  out << "    Cache Accesses: " << c[GG_CC_ACCESSES] << std::endl;
+  out << "    Cache Misses: " << c[GG_CC_MISSES] << std::endl;
+  if (c[GG_CC_ACCESSES] > 0)
+    out << "    Miss Rate (%): " << 100.0 * c[GG_CC_MISSES] / c[GG_CC_ACCESSES] << std::endl;
+  else
+    out << "    Miss Rate (%): " << std::endl;
+  if (!instruction_cache) {
+    out << "      Read Accesses: " << c[GG_CC_READ_ACCESSES] << std::endl;
+    out << "      Read Misses: " << c[GG_CC_READ_MISSES] << std::endl;
+    if (c[GG_CC_READ_ACCESSES] > 0)
+      out << "      Read Miss Rate (%): " << 100.0 * c[GG_CC_READ_MISSES] / c[GG_CC_READ_ACCESSES] << std::endl;
+    else
+      out << "      Read Miss Rate (%): " << std::endl;
+    out << "      Write Accesses: " << c[GG_CC_WRITE_ACCESSES] << std::endl;
+    out << "      Write Misses: " << c[GG_CC_WRITE_MISSES] << std::endl;
+    if (c[GG_CC_WRITE_ACCESSES] > 0)
+      out << "      Write Miss Rate (%): " << 100.0 * c[GG_CC_WRITE_MISSES] / c[GG_CC_WRITE_ACCESSES] << std::endl;
+    else
+      out << "    Write Miss Rate (%): " << std::endl;
+  }
+  out << "    Evictions: " << c[GG_CC_EVICTIONS] << std::endl;
+  if (write_back) out << "    Dirty Evictions: " << c[GG_CC_DIRTY_EVICTIONS] << std::endl;
+  out << "    Event Counters:" << std::endl;
+  out << "      Tag Array Reads: " << c[GG_CC_TAG_READS] << std::endl;
+  out << "      Tag Array Writes: " << c[GG_CC_TAG_WRITES] << std::endl;
+  out << "      Data Array Reads: " << c[GG_CC_DATA_READS] << std::endl;
+  out << "      Data Array Writes: " << c[GG_CC_DATA_WRITES] << std::endl;
+}
+
+// One cache (tile, level) of a Backend with the reference Cache API.
+class Cache {
+ public:
+  enum AccessType { LOAD = 0, STORE };
+  Cache(Backend& be, uint32_t tile, int level) : _be(be), _tile(tile), _level(level) {}
+
+  void accessCacheLine(IntPtr address, AccessType access_type, Byte* /*buf*/ = nullptr, uint32_t /*num_bytes*/ = 0)
+  {
+    check(gg_cache_access_line(_be.ctx(), _tile, _level, address, access_type == STORE), "Cache::accessCacheLine");
+  }
+  void insertCacheLine(IntPtr inserted_address, CacheLineInfo* inserted, Byte* /*fill_buf*/, bool* eviction,
+                       IntPtr* evicted_address, CacheLineInfo* evicted, Byte* /*writeback_buf*/)
+  {
+    int ev = 0;
+    check(gg_cache_insert_line(_be.ctx(), _tile, _level, inserted_address, inserted->raw(), &ev, evicted_address,
+                               evicted->raw()), "Cache::insertCacheLine");
+    *eviction = ev != 0;
+  }
+  void getCacheLineInfo(IntPtr address, CacheLineInfo* info)
+  {
+    check(gg_cache_get_line_info(_be.ctx(), _tile, _level, address, info->raw()), "Cache::getCacheLineInfo");
+  }
+  void setCacheLineInfo(IntPtr address, CacheLineInfo* info)
+  {
+    check(gg_cache_set_line_info(_be.ctx(), _tile, _level, address, info->raw()), "Cache::setCacheLineInfo");
+  }
+  void outputSummary(std::ostream& out) const
+  {
+    std::vector<uint64_t> c = _be.cacheCounters();
+    writeCacheSummary(out, _level == GG_L1D ? "L1-D" : "L2",
+                      &c[((size_t)_tile * 2 + _level) * GG_NUM_CACHE_COUNTERS], _level == GG_L2);
+  }
+ private:
+  Backend& _be;
+  uint32_t _tile;
+  int _level;
+};
+
+// Device buffer helper
+template <class T>
+struct DeviceBuffer {
+  T* p = nullptr;
+  size_t n = 0;
+  void resize(size_t want)
+  {
+    if (want <= n && p) return;
+    if (p) hipFree(p);
+    hip_check(hipMalloc((void**)&p, sizeof(T) * (want ? want : 1)), "hipMalloc");
+    n = want;
+  }
+  ~DeviceBuffer() { if (p) hipFree(p); }
+};
+
+// Core::initiateMemoryAccess line split (core.cc:167-201): the line-aligned
+// addresses touched by [address, address + size), zero-size tail skipped.
+inline void splitIntoLines(IntPtr address, uint32_t size, uint32_t line, std::vector<IntPtr>& out)
+{
+  if (size == 0) return;
+  const IntPtr begin = address, end = address + size;
+  const IntPtr ba = begin - (begin % line), ea = end - (end % line);
+  for (IntPtr a = ba; a <= ea; a += line) {
+    const uint32_t off = (a == ba) ? (uint32_t)(begin % line) : 0;
+    if (a == ea && (uint32_t)(end % line) - off == 0) continue;
+    out.push_back(a);
+  }
+}
+
+// Per-tile line-access trace, replayed in batches through the private-cache
+// backend (the batched accessSingleLine of the north star).
+class TraceReplayer {
+ public:
+  explicit TraceReplayer(Backend& be) : _be(be), _lines(be.config().num_tiles), _meta(be.config().num_tiles) {}
+
+  // Core::initiateMemoryAccess(L1_DCACHE, ..., READ/WRITE, address, size): queue its line accesses
+  void initiateMemoryAccess(uint32_t tile, bool is_write, IntPtr address, uint32_t size)
+  {
+    const size_t before = _lines.at(tile).size();
+    splitIntoLines(address, size, _be.config().line_size, _lines[tile]);
+    _meta[tile].resize(_lines[tile].size(), is_write ? GG_META_WRITE : 0u);
+    (void)before;
+  }
+  void accessSingleLine(uint32_t tile, bool is_write, IntPtr line_address)
+  {
+    _lines.at(tile).push_back(line_address);
+    _meta[tile].push_back(is_write ? GG_META_WRITE : 0u);
+  }
+  size_t pending() const { size_t n = 0; for (auto& v : _lines) n += v.size(); return n; }
+
+  // Replay everything queued; returns the per-access GG_RES_* words in
+  // tile-major order of the queued accesses.
+  std::vector<uint32_t> flush(hipStream_t stream = nullptr)
+  {
+    const uint32_t T = _be.config().num_tiles;
+    std::vector<uint64_t> offs(T + 1, 0), addr;
+    std::vector<uint32_t> meta;
+    for (uint32_t t = 0; t < T; ++t) {
+      offs[t + 1] = offs[t] + _lines[t].size();
+      addr.insert(addr.end(), _lines[t].begin(), _lines[t].end());
+      meta.insert(meta.end(), _meta[t].begin(), _meta[t].end());
+      _lines[t].clear();
+      _meta[t].clear();
+    }
+    const size_t n = addr.size();
+    std::vector<uint32_t> res(n);
+    _addr.resize(n); _m.resize(n); _res.resize(n);
+    if (n) {
+      hip_check(hipMemcpyAsync(_addr.p, addr.data(), 8 * n, hipMemcpyHostToDevice, stream), "copy addr");
+      hip_check(hipMemcpyAsync(_m.p, meta.data(), 4 * n, hipMemcpyHostToDevice, stream), "copy meta");
+    }
+    gg_trace tr{_addr.p, _m.p, offs.data(), n};
+    check(gg_cache_access_batch(_be.ctx(), &tr, _res.p, nullptr, stream), "gg_cache_access_batch");
+    if (n) hip_check(hipMemcpyAsync(res.data(), _res.p, 4 * n, hipMemcpyDeviceToHost, stream), "copy result");
+    hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
+    return res;
+  }
+
+  // "Cache Summary:" block of every tile (MemoryManager::outputSummary,
+  // pr_l1_pr_l2_dram_directory_msi/memory_manager.cc:415-430, L1-D and L2 only)
+  void outputSummary(std::ostream& out) const
+  {
+    std::vector<uint64_t> c = _be.cacheCounters();
+    for (uint32_t t = 0; t < _be.config().num_tiles; ++t) {
+      out << "Tile " << t << " Cache Summary:" << std::endl;
+      writeCacheSummary(out, "L1-D", &c[((size_t)t * 2 + 0) * GG_NUM_CACHE_COUNTERS], false);
+      writeCacheSummary(out, "L2", &c[((size_t)t * 2 + 1) * GG_NUM_CACHE_COUNTERS], true);
+    }
+  }
+
+ private:
+  Backend& _be;
+  std::vector<std::vector<IntPtr>> _lines;
+  std::vector<std::vector<uint32_t>> _meta;
+  DeviceBuffer<uint64_t> _addr;
+  DeviceBuffer<uint32_t> _m, _res;
+};
+
+// NetworkModel::routePacket mirror.  NetPacket/Hop keep the reference fields
+// that carry timing (network.h:27-55, network_model.h:45-63).
+struct NetPacket {
+  uint64_t time_ps = 0;         // NetPacket::time
+  uint32_t sender = 0, receiver = 0;
+  uint32_t modeled_length_bits = 0;   // NetworkModel::getModeledLength
+  uint64_t zero_load_delay_ps = 0, contention_delay_ps = 0;
+};
+struct Hop {
+  uint32_t next_tile_id;
+  int32_t next_node_type;       // RECEIVE_TILE
+  uint64_t time_ps, zero_load_delay_ps, contention_delay_ps;
+};
+enum { RECEIVE_TILE = 2 };
+
+class NetworkModel {
+ public:
+  explicit NetworkModel(Backend& be) : _be(be) {}
+  // Routes every packet of the batch to its receiver (all hops, in the
+  // canonical order of DESIGN.md §NoC) and returns one RECEIVE_TILE hop per
+  // packet, after the receiver's serialization delay.
+  void routePackets(const std::vector<NetPacket>& pkts, std::vector<Hop>& hops, hipStream_t stream = nullptr)
+  {
+    const size_t n = pkts.size();
+    std::vector<uint32_t> src(n), dst(n), len(n);
+    std::vector<uint64_t> t(n), arr(n), zl(n), ct(n);
+    for (size_t k = 0; k < n; ++k) {
+      src[k] = pkts[k].sender; dst[k] = pkts[k].receiver;
+      len[k] = pkts[k].modeled_length_bits; t[k] = pkts[k].time_ps;
+    }
+    _s.resize(n); _d.resize(n); _l.resize(n); _t.resize(n); _a.resize(n); _z.resize(n); _c.resize(n);
+    if (n) {
+      hip_check(hipMemcpyAsync(_s.p, src.data(), 4 * n, hipMemcpyHostToDevice, stream), "copy");
+      hip_check(hipMemcpyAsync(_d.p, dst.data(), 4 * n, hipMemcpyHostToDevice, stream), "copy");
+      hip_check(hipMemcpyAsync(_l.p, len.data(), 4 * n, hipMemcpyHostToDevice, stream), "copy");
+      hip_check(hipMemcpyAsync(_t.p, t.data(), 8 * n, hipMemcpyHostToDevice, stream), "copy");
+    }
+    gg_packets pk{_s.p, _d.p, _l.p, _t.p, n};
+    gg_packet_out out{_a.p, _z.p, _c.p};
+    check(gg_noc_route_batch(_be.ctx(), &pk, &out, stream), "gg_noc_route_batch");
+    if (n) {
+      hip_check(hipMemcpyAsync(arr.data(), _a.p, 8 * n, hipMemcpyDeviceToHost, stream), "copy");
+      hip_check(hipMemcpyAsync(zl.data(), _z.p, 8 * n, hipMemcpyDeviceToHost, stream), "copy");
+      hip_check(hipMemcpyAsync(ct.data(), _c.p, 8 * n, hipMemcpyDeviceToHost, stream), "copy");
+    }
+    hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
+    hops.resize(n);
+    for (size_t k = 0; k < n; ++k)
+      hops[k] = Hop{dst[k], RECEIVE_TILE, arr[k], zl[k], ct[k]};
+  }
+  // The single-packet form of the reference: pushes the packet's delivery hop.
+  void routePacket(const NetPacket& pkt, std::queue<Hop>& next_hops)
+  {
+    std::vector<Hop> h;
+    routePackets(std::vector<NetPacket>(1, pkt), h);
+    next_hops.push(h[0]);
+  }
+ private:
+  Backend& _be;
+  DeviceBuffer<uint32_t> _s, _d, _l;
+  DeviceBuffer<uint64_t> _t, _a, _z, _c;
+};
+
+}  // namespace graphite_amd

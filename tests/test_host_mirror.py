@@ -1,0 +1,87 @@
+"""The C++ host mirror (graphite_amd/host/graphite_host.hpp): its sim.out-style
+cache summary matches the reference's Cache::outputSummary text
+(cache.cc:419-477), and its TraceReplayer drives the GPU backend to the
+oracle's counters."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from graphite_amd import config as C
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPLAY = os.path.join(ROOT, "graphite_amd", "host", "gg_replay")
+
+
+def reference_summary(name, c, write_back):
+    """Cache::outputSummary (cache.cc:419-477), restated; float formatting is
+    the default std::ostream one (6 significant digits, like %g)."""
+    L = ["  Cache %s: " % name, "    Cache Accesses: %d" % c[0], "    Cache Misses: %d" % c[1]]
+    L.append("    Miss Rate (%%): %s" % ("%g" % (100.0 * c[1] / c[0]) if c[0] else ""))
+    L.append("      Read Accesses: %d" % c[2])
+    L.append("      Read Misses: %d" % c[3])
+    L.append("      Read Miss Rate (%%): %s" % ("%g" % (100.0 * c[3] / c[2]) if c[2] else ""))
+    L.append("      Write Accesses: %d" % c[4])
+    L.append("      Write Misses: %d" % c[5])
+    if c[4]:
+        L.append("      Write Miss Rate (%%): %g" % (100.0 * c[5] / c[4]))
+    else:
+        L.append("    Write Miss Rate (%): ")                 # the reference's 4-space quirk (cache.cc:445)
+    L.append("    Evictions: %d" % c[6])
+    if write_back:
+        L.append("    Dirty Evictions: %d" % c[7])
+    L += ["    Event Counters:", "      Tag Array Reads: %d" % c[8], "      Tag Array Writes: %d" % c[9],
+          "      Data Array Reads: %d" % c[10], "      Data Array Writes: %d" % c[11]]
+    return L
+
+
+def test_summary_format_matches_reference():
+    if not os.path.exists(REPLAY):
+        pytest.skip("gg_replay not built")
+    out = subprocess.run([REPLAY, "--summary-selftest"], capture_output=True, text=True, check=True).stdout
+    c1 = [1000, 250, 700, 150, 300, 100, 240, 0, 2600, 900, 760, 1250]
+    c2 = [250, 180, 150, 110, 100, 70, 120, 45, 700, 600, 190, 480]
+    exp = reference_summary("L1-D", c1, False) + reference_summary("L2", c2, True) + \
+        reference_summary("L2", [0] * 12, True)
+    assert out.splitlines() == exp
+
+
+def parse_summaries(text):
+    tiles = {}
+    cur = None
+    keys = {"Cache Accesses": 0, "Cache Misses": 1, "Read Accesses": 2, "Read Misses": 3, "Write Accesses": 4,
+            "Write Misses": 5, "Evictions": 6, "Dirty Evictions": 7, "Tag Array Reads": 8,
+            "Tag Array Writes": 9, "Data Array Reads": 10, "Data Array Writes": 11}
+    for line in text.splitlines():
+        s = line.strip()
+        if s.startswith("Tile ") and s.endswith("Cache Summary:"):
+            t = int(s.split()[1])
+            tiles[t] = np.zeros((2, 12), np.uint64)
+        elif s.startswith("Cache L1-D"):
+            cur = 0
+        elif s.startswith("Cache L2"):
+            cur = 1
+        elif ":" in s:
+            k, v = s.split(":", 1)
+            if k in keys and v.strip():
+                tiles[t][cur, keys[k]] = int(v)
+    return tiles
+
+
+@pytest.mark.gpu
+def test_trace_replayer_matches_oracle():
+    from gpu_util import torch_dev
+    torch_dev()
+    from oracle import pyoracle as po
+    T, N = 6, 30000
+    out = subprocess.run([REPLAY, "--tiles", str(T), "--per-tile", str(N), "--lines-log2", "12", "--batches", "3"],
+                         capture_output=True, text=True, check=True).stdout
+    got = parse_summaries(out)
+    a = np.concatenate([po.gen_uniform(t, 0, N, lines_log2=12)[0] for t in range(T)])
+    m = np.concatenate([po.gen_uniform(t, 0, N, lines_log2=12)[1] for t in range(T)])
+    oc = po.OracleCache(C.default_config(T))
+    oc.run(a, m, np.arange(T + 1, dtype=np.uint64) * np.uint64(N))
+    ref = oc.counters()
+    for t in range(T):
+        np.testing.assert_array_equal(got[t], ref[t])
