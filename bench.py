@@ -2,17 +2,20 @@
 """bench.py — simulated memory accesses per second of the MI355X backend.
 
 Metric (BASELINE.json): "simulated mem accesses/sec (node) ... bit-exact stats".
-Workload (round 1): BASELINE.json configs[1] — uniform-random private trace,
-64 tiles per GPU, 32 KB/4-way L1-D + 512 KB/8-way L2 (carbon_sim.cfg
-defaults), 2^22 line accesses per tile, private-cache (decoupled) mode.  One
-step = one full replay of the batch from the constructor cache state: the
-stable (tile, L1-D set) partition kernels + the replay kernel
-(graphite_amd/csrc/gg_cache.hip), inputs resident in HBM.
+Workload (round 1): the metric's scale — 1024 tiles per GPU (BASELINE.json
+configs[3] tile count), 2^20 line accesses per tile (configs[3] length) — with
+the configs[1] uniform-random private generator, 32 KB/4-way L1-D + 512 KB/8-way
+L2 (carbon_sim.cfg defaults), private-cache (decoupled) mode.  The coherent
+MSI + hop-by-hop mode of configs[3] is not built yet.
+`--tiles 64 --per-tile 4194304` runs configs[1] exactly.  One step = one full
+replay of the batch from the constructor cache state: the stable (tile,
+L1-D set) partition kernels + the replay kernel (graphite_amd/csrc/gg_cache.hip),
+inputs resident in HBM.
 
-Multi-GPU: one process per GPU (torchrun); rank r simulates its own 64 tiles
-(global tiles r*64 .. r*64+63) — units are independent in private mode, so
+Multi-GPU: one process per GPU (torchrun); rank r simulates its own tiles
+(global tiles r*T .. r*T+T-1) — units are independent in private mode, so
 there is no collective on the data path ("weak" scaling); only the timing is
-max-reduced over ranks.
+max-reduced over ranks (graphite_amd/dist.py).
 
 Also reported: the replay kernel's roofline (algorithmic 16 B/access: 8 B
 address + 4 B metadata in, 4 B result out) from HIP
@@ -41,9 +44,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--tiles", type=int, default=64, help="tiles per GPU")
-    p.add_argument("--per-tile", type=int, default=1 << 22, help="line accesses per tile")
-    p.add_argument("--cpu-sample-tiles", type=int, default=16)
+    p.add_argument("--tiles", type=int, default=1024, help="tiles per GPU")
+    p.add_argument("--per-tile", type=int, default=1 << 20, help="line accesses per tile")
+    p.add_argument("--cpu-sample-tiles", type=int, default=480, help="tile replays in the CPU baseline sample")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu count)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
@@ -52,10 +55,12 @@ def parse():
 
 
 def cpu_baseline(tiles, per_tile, threads):
-    """Oracle (oracle/gg_oracle.c, -O3, 1 thread per tile stream) on a bounded sample."""
+    """Oracle (oracle/gg_oracle.c, -O3) on a bounded sample: `tiles` tile
+    replays (fresh cache state each) cycling over 16 pre-generated tiles of
+    the same workload, one tile per thread at a time."""
     from graphite_amd import config as C
     from oracle import pyoracle as po
-    traces = [po.gen_uniform(t, 0, per_tile) for t in range(tiles)]
+    traces = [po.gen_uniform(t, 0, per_tile) for t in range(min(16, tiles))]
     offs = np.array([0, per_tile], np.uint64)
     todo = list(range(tiles))
     lock = threading.Lock()
@@ -67,8 +72,9 @@ def cpu_baseline(tiles, per_tile, threads):
                     return
                 t = todo.pop()
             oc = po.OracleCache(C.default_config(1))
-            a, m = traces[t]
-            oc.run(a - np.uint64(t << 26), m, offs)   # tile t's private region, replayed as tile 0
+            k = t % len(traces)
+            a, m = traces[k]
+            oc.run(a - np.uint64(k << 26), m, offs)   # tile k's private region, replayed as tile 0
 
     ths = [threading.Thread(target=worker) for _ in range(threads)]
     t0 = time.perf_counter()
@@ -87,12 +93,10 @@ def main():
     from graphite_amd import config as C
     from graphite_amd import backend as B
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+    from graphite_amd import dist as D
+    world, rank, local = D.env()
+    torch.cuda.set_device(local)
+    D.init("nccl")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -117,8 +121,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    D.barrier()
     torch.cuda.synchronize()
     replay_ms, shard_ms = [], []
     t0 = time.perf_counter()
@@ -127,24 +130,19 @@ def main():
         replay_ms.append(be.kernel_time_ms("cache_replay"))
         shard_ms.append(be.kernel_time_ms("cache_shard"))
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    D.barrier()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = D.max_over_ranks(time.perf_counter() - t0)
 
     # bit-exact check of this run (rank 0): one tile's results + counters vs the oracle
     verified = None
     if not args.no_verify and rank == 0:
         from oracle import pyoracle as po
         cnt = be.cache_counters()
-        t = T - 1
-        a, m = po.gen_uniform(t, 0, N)
+        t = T - 1                                   # last local tile = global tile rank*T + T-1
+        a, m = po.gen_uniform(rank * T + t, 0, N)
         oc = po.OracleCache(C.default_config(1))
-        ref = oc.run(a - np.uint64(t << 26), m, np.array([0, N], np.uint64))
+        ref = oc.run(a - np.uint64((rank * T + t) << 26), m, np.array([0, N], np.uint64))
         got = result[t * N:(t + 1) * N].cpu().numpy().view(np.uint32)
         verified = bool(np.array_equal(got, ref) and np.array_equal(cnt[t], oc.counters()[0]))
         if not verified:
@@ -169,13 +167,15 @@ def main():
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic (configs[1] SplitMix64 uniform-random private trace, generated on device)",
-            "config": {"workload": "configs[1]: uniform-random private trace, %d tiles/GPU, 32KB/4w L1-D + 512KB/8w L2, "
-                                   "private-cache mode" % T,
+            "config": {"workload": ("configs[1] exactly (64 tiles x 2^22)" if (T, N) == (64, 1 << 22) else
+                                    "%d tiles/GPU x %d accesses/tile (configs[3] scale) with the configs[1] "
+                                    "uniform-random private generator" % (T, N)) +
+                                   "; 32KB/4w L1-D + 512KB/8w L2, private-cache mode",
                        "tiles_per_gpu": T, "accesses_per_tile": N, "mode": "private",
                        "parallelism": "tiles sharded over %d rank(s), no data-path collective" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "k_cache_replay", "kernel_ms": rep, "shard_ms": shd,
+                         "kernel": "k_cache_replay_lean", "kernel_ms": rep, "shard_ms": shd,
                          "bytes_per_access": ALGO_BYTES_PER_ACCESS},
             "bit_exact_checked": verified,
         }
@@ -187,7 +187,7 @@ def main():
                                              "-O3, one tile per thread, %.1f s" % (args.cpu_sample_tiles, N, cdt)}
         print(json.dumps(out))
     if world > 1:
-        dist.barrier()
+        D.barrier()
         dist.destroy_process_group()
 
 

@@ -23,7 +23,8 @@
 
 namespace {
 
-constexpr uint32_t kChunk = 4096;        // records per shard chunk (one wave)
+constexpr uint32_t kChunk = 2048;        // records per shard chunk (one wave, staged in LDS)
+constexpr uint32_t kPerLane = kChunk / 64;
 constexpr uint64_t kB7 = 0x8080808080808080ull;
 constexpr uint64_t k7F = 0x7F7F7F7F7F7F7F7Full;
 constexpr uint64_t k1F = 0x1F1F1F1F1F1F1F1Full;
@@ -183,24 +184,19 @@ __global__ void k_shard_scan(uint32_t* __restrict__ cnt, const uint32_t* __restr
   unit_len[(uint64_t)t * g.u1 + s] = (uint32_t)acc;
 }
 
-// Pass 2b: interleaved sharded layout.  The 64 units of a replay wave form a
-// group; record j of unit u lives at unit_base[u] + 64*j, unit_base[u] =
-// group base + (u % 64), group bases = exclusive scan of 64 * (longest unit of
-// the group).  One block; writes the total slot count to *total.
-__global__ __launch_bounds__(1024) void k_group_scan(const uint32_t* __restrict__ unit_len, uint64_t units,
-                                                     uint64_t* __restrict__ unit_base, uint64_t* __restrict__ total)
+// Pass 2b: unit-contiguous sharded layout.  Unit u's records are stored
+// contiguously from unit_base[u], each unit padded to a multiple of 8 records
+// so a lane streams its records in 64-byte blocks.  One block; writes the
+// total slot count to *total.
+__global__ __launch_bounds__(1024) void k_unit_scan(const uint32_t* __restrict__ unit_len, uint64_t units,
+                                                    uint64_t* __restrict__ unit_base, uint64_t* __restrict__ total)
 {
   __shared__ uint64_t part[1024];
   const uint32_t t = threadIdx.x;
-  const uint64_t groups = (units + GG_WAVE - 1) / GG_WAVE;
-  const uint64_t per = (groups + blockDim.x - 1) / blockDim.x;
-  const uint64_t g0 = t * per, g1 = min(groups, g0 + per);
+  const uint64_t per = (units + blockDim.x - 1) / blockDim.x;
+  const uint64_t u0 = t * per, u1 = min(units, u0 + per);
   uint64_t sum = 0;
-  for (uint64_t gi = g0; gi < g1; ++gi) {
-    uint32_t m = 0;
-    for (uint32_t l = 0; l < GG_WAVE; ++l) { const uint64_t u = gi * GG_WAVE + l; if (u < units) m = max(m, unit_len[u]); }
-    sum += (uint64_t)m * GG_WAVE;
-  }
+  for (uint64_t u = u0; u < u1; ++u) sum += (unit_len[u] + 7u) & ~7u;
   part[t] = sum;
   __syncthreads();
   for (uint32_t o = 1; o < blockDim.x; o <<= 1) {
@@ -211,17 +207,14 @@ __global__ __launch_bounds__(1024) void k_group_scan(const uint32_t* __restrict_
   }
   uint64_t base = part[t] - sum;
   if (t == blockDim.x - 1) *total = part[t];
-  for (uint64_t gi = g0; gi < g1; ++gi) {
-    uint32_t m = 0;
-    for (uint32_t l = 0; l < GG_WAVE; ++l) { const uint64_t u = gi * GG_WAVE + l; if (u < units) m = max(m, unit_len[u]); }
-    for (uint32_t l = 0; l < GG_WAVE; ++l) { const uint64_t u = gi * GG_WAVE + l; if (u < units) unit_base[u] = base + l; }
-    base += (uint64_t)m * GG_WAVE;
-  }
+  for (uint64_t u = u0; u < u1; ++u) { unit_base[u] = base; base += (unit_len[u] + 7u) & ~7u; }
 }
 
-// Pass 3: one wave per chunk, 64 records per step in program order; lanes
-// with the same set are matched with log2(u1) ballots so the rank of each
-// record inside its unit is stable (program order is kept per unit).
+// Pass 3: one wave per chunk of kChunk records.  The chunk is held in VGPRs,
+// counted per L1-D set with LDS atomics, ranked in program order (lanes with
+// the same set matched by log2(u1) ballots, so each unit keeps program order),
+// staged in LDS sorted by set, then written out per set as contiguous runs
+// (consecutive lanes -> consecutive addresses: whole cache lines per run).
 __global__ __launch_bounds__(64) void k_shard_scatter(const uint64_t* __restrict__ addr,
     const uint32_t* __restrict__ meta, const uint32_t* __restrict__ chunk_tile,
     const uint64_t* __restrict__ chunk_start, const uint32_t* __restrict__ chunk_len,
@@ -229,26 +222,59 @@ __global__ __launch_bounds__(64) void k_shard_scatter(const uint64_t* __restrict
     const uint64_t* __restrict__ tile_off, uint64_t* __restrict__ sh_key,
     uint32_t* __restrict__ sh_idx, gg_geom g)
 {
-  __shared__ uint64_t ubase[1024];
-  __shared__ uint32_t rank0[1024];
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint64_t* skey = reinterpret_cast<uint64_t*>(smem);                      // [kChunk]
+  uint32_t* sidx = reinterpret_cast<uint32_t*>(skey + kChunk);             // [kChunk]
+  uint16_t* sset = reinterpret_cast<uint16_t*>(sidx + kChunk);             // [kChunk]
+  uint64_t* dbase = reinterpret_cast<uint64_t*>(sset + kChunk);            // [u1] dest - local offset
+  uint32_t* lcnt = reinterpret_cast<uint32_t*>(dbase + g.u1);             // [u1] count, then running rank
+  uint32_t* loff = lcnt + g.u1;                                            // [u1] exclusive prefix
   const uint32_t c = blockIdx.x, lane = threadIdx.x;
   const uint32_t t = chunk_tile[c];
-  for (uint32_t s = lane; s < g.u1; s += GG_WAVE) {
-    ubase[s] = unit_base[(uint64_t)t * g.u1 + s];
-    rank0[s] = cnt[(uint64_t)c * g.u1 + s];
-  }
-  __syncthreads();
   const uint64_t start = chunk_start[c];
   const uint32_t len = chunk_len[c];
   const uint32_t rel0 = (uint32_t)(start - tile_off[t]);
-  const uint64_t lt_mask = (1ull << lane) - 1;
   const uint64_t line_mask = ~((1ull << g.log_line) - 1);
-  for (uint32_t i0 = 0; i0 < len; i0 += GG_WAVE) {
-    const uint32_t i = i0 + lane;
+  const uint32_t smask = g.u1 - 1;
+  for (uint32_t s = lane; s < g.u1; s += GG_WAVE) lcnt[s] = 0;
+  __syncthreads();
+  uint64_t key[kPerLane];
+#pragma unroll
+  for (uint32_t k = 0; k < kPerLane; ++k) {
+    const uint32_t i = k * GG_WAVE + lane;
     const bool valid = i < len;
     const uint64_t a = valid ? addr[start + i] : 0;
     const uint32_t m = valid ? meta[start + i] : 0;
-    const uint32_t s = (uint32_t)(a >> g.log_line) & (g.u1 - 1);
+    key[k] = (a & line_mask) | (m & GG_META_WRITE);
+    if (valid) atomicAdd(&lcnt[(uint32_t)(a >> g.log_line) & smask], 1u);
+  }
+  __syncthreads();
+  // exclusive prefix of the per-set counts (lane-strided blocks + wave scan)
+  {
+    const uint32_t per = (g.u1 + GG_WAVE - 1) / GG_WAVE;
+    uint32_t sum = 0;
+    for (uint32_t k = 0; k < per; ++k) { const uint32_t s = lane * per + k; if (s < g.u1) sum += lcnt[s]; }
+    uint32_t incl = sum;
+    for (int o = 1; o < GG_WAVE; o <<= 1) { const uint32_t v = __shfl_up(incl, o); if ((int)lane >= o) incl += v; }
+    uint32_t run = incl - sum;
+    for (uint32_t k = 0; k < per; ++k) {
+      const uint32_t s = lane * per + k;
+      if (s < g.u1) {
+        loff[s] = run;
+        dbase[s] = unit_base[(uint64_t)t * g.u1 + s] + cnt[(uint64_t)c * g.u1 + s] - run;
+        run += lcnt[s];
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t s = lane; s < g.u1; s += GG_WAVE) lcnt[s] = 0;
+  __syncthreads();
+  const uint64_t lt_mask = (1ull << lane) - 1;
+#pragma unroll
+  for (uint32_t k = 0; k < kPerLane; ++k) {
+    const uint32_t i = k * GG_WAVE + lane;
+    const bool valid = i < len;
+    const uint32_t s = (uint32_t)(key[k] >> g.log_line) & smask;
     uint64_t peers = __ballot(valid);
     for (uint32_t b = 0; b < g.log_u1; ++b) {
       const bool bit = (s >> b) & 1u;
@@ -256,17 +282,26 @@ __global__ __launch_bounds__(64) void k_shard_scatter(const uint64_t* __restrict
       peers &= bit ? bb : ~bb;
     }
     const uint32_t rank = __popcll(peers & lt_mask);
-    const uint32_t r0 = valid ? rank0[s] : 0;
+    const uint32_t r0 = valid ? lcnt[s] : 0;
     __builtin_amdgcn_wave_barrier();
-    if (valid && rank == 0) rank0[s] = r0 + (uint32_t)__popcll(peers);
+    if (valid && rank == 0) lcnt[s] = r0 + (uint32_t)__popcll(peers);
     __builtin_amdgcn_wave_barrier();
     if (valid) {
-      const uint64_t pos = ubase[s] + (uint64_t)(r0 + rank) * GG_WAVE;
-      sh_key[pos] = (a & line_mask) | (m & GG_META_WRITE);
-      sh_idx[pos] = rel0 + i;
+      const uint32_t q = loff[s] + r0 + rank;
+      skey[q] = key[k];
+      sidx[q] = rel0 + i;
+      sset[q] = (uint16_t)s;
     }
   }
+  __syncthreads();
+  for (uint32_t q = lane; q < len; q += GG_WAVE) {
+    const uint64_t dst = dbase[sset[q]] + q;
+    sh_key[dst] = skey[q];
+    sh_idx[dst] = sidx[q];
+  }
 }
+
+size_t scatter_lds_bytes(const gg_geom& g) { return (size_t)kChunk * (8 + 4 + 2) + (size_t)g.u1 * (8 + 4 + 4); }
 
 // ---------------------------------------------------------------------------
 // Replay kernel.  One lane per unit (tile, L1-D set), 64 units per wave.
@@ -456,8 +491,8 @@ __global__ __launch_bounds__(64) void k_cache_replay(gg_cache_state cs, gg_geom 
   uint64_t kr[PD]; uint32_t ir[PD];
 #pragma unroll
   for (int d = 0; d < PD; ++d) {
-    kr[d] = (d < (int)len) ? sh_key[base + (uint64_t)d * GG_WAVE] : 0;
-    ir[d] = (d < (int)len) ? sh_idx[base + (uint64_t)d * GG_WAVE] : 0;
+    kr[d] = (d < (int)len) ? sh_key[base + d] : 0;
+    ir[d] = (d < (int)len) ? sh_idx[base + d] : 0;
   }
   const uint64_t lmask = (g.s2 - 1);
 
@@ -468,8 +503,8 @@ __global__ __launch_bounds__(64) void k_cache_replay(gg_cache_state cs, gg_geom 
 #pragma unroll
     for (int d = 0; d < PD - 1; ++d) { kr[d] = kr[d + 1]; ir[d] = ir[d + 1]; }
     const bool more = j + PD < len;
-    kr[PD - 1] = more ? sh_key[base + (uint64_t)(j + PD) * GG_WAVE] : 0;
-    ir[PD - 1] = more ? sh_idx[base + (uint64_t)(j + PD) * GG_WAVE] : 0;
+    kr[PD - 1] = more ? sh_key[base + j + PD] : 0;
+    ir[PD - 1] = more ? sh_idx[base + j + PD] : 0;
     if (!live) continue;
 
     const uint64_t line = key >> g.log_line;
@@ -748,27 +783,11 @@ __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_
   uint32_t cnt[NI];
 #pragma unroll
   for (int k = 0; k < NI; ++k) cnt[k] = 0;
-  constexpr int PD = 2;
-  uint64_t kr[PD]; uint32_t ir[PD];
-#pragma unroll
-  for (int d = 0; d < PD; ++d) {
-    kr[d] = (d < (int)len) ? sh_key[base + (uint64_t)d * GG_WAVE] : 0;
-    ir[d] = (d < (int)len) ? sh_idx[base + (uint64_t)d * GG_WAVE] : 0;
-  }
   const uint32_t s2m = S2 - 1;
   const uint32_t log_line = g.log_line, log_u1 = g.log_u1, log_l2 = g.log_l2;
 
-  for (uint32_t j = 0; j < maxlen; ++j) {
-    const bool live = j < len;
-    const uint64_t key = kr[0];
-    const uint32_t idx = ir[0];
-#pragma unroll
-    for (int d = 0; d < PD - 1; ++d) { kr[d] = kr[d + 1]; ir[d] = ir[d + 1]; }
-    const bool more = j + PD < len;
-    kr[PD - 1] = more ? sh_key[base + (uint64_t)(j + PD) * GG_WAVE] : 0;
-    ir[PD - 1] = more ? sh_idx[base + (uint64_t)(j + PD) * GG_WAVE] : 0;
-    if (!live) continue;
-
+  // One access of this lane's unit (the body of processMemOpFromCore).
+  auto step = [&](const uint64_t key, const uint32_t idx) {
     const uint64_t line = key >> log_line;
     const uint32_t wr = (uint32_t)key & 1u;
     const uint32_t s = (uint32_t)(line >> log_u1) & s2m;
@@ -867,6 +886,48 @@ __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_
     if (evicted) {
       const uint64_t e2 = ((uint64_t)vt << log_l2) | ((uint64_t)s << log_u1) | l1set;
       evicted[rbase + idx] = l2ev ? (e2 << log_line) : ~0ull;
+    }
+    };
+
+  // The unit's records are contiguous from `base` (8-record aligned): stream
+  // them in 8-record blocks (4 + 2 dwordx4 loads), next block in flight while
+  // the current one is replayed from registers.
+  constexpr int KB = 8;
+  const uint4* kp = reinterpret_cast<const uint4*>(sh_key + base);
+  const uint4* ip = reinterpret_cast<const uint4*>(sh_idx + base);
+  uint4 kb[KB / 2], ib[KB / 4];
+  if (len > 0) {
+#pragma unroll
+    for (int q = 0; q < KB / 2; ++q) kb[q] = kp[q];
+#pragma unroll
+    for (int q = 0; q < KB / 4; ++q) ib[q] = ip[q];
+  }
+  for (uint32_t j0 = 0; j0 < maxlen; j0 += KB) {
+    uint4 nkb[KB / 2], nib[KB / 4];
+    const bool more = j0 + KB < len;
+    if (more) {
+#pragma unroll
+      for (int q = 0; q < KB / 2; ++q) nkb[q] = kp[(j0 + KB) / 2 + q];
+#pragma unroll
+      for (int q = 0; q < KB / 4; ++q) nib[q] = ip[(j0 + KB) / 4 + q];
+    }
+    if (j0 < len) {
+#pragma unroll
+      for (int d = 0; d < KB; ++d) {
+        if (j0 + d < len) {
+          const uint4 kv = kb[d / 2];
+          const uint64_t key = (d & 1) ? (((uint64_t)kv.w << 32) | kv.z) : (((uint64_t)kv.y << 32) | kv.x);
+          const uint4 iv = ib[d / 4];
+          const uint32_t idx = (d & 3) == 0 ? iv.x : ((d & 3) == 1 ? iv.y : ((d & 3) == 2 ? iv.z : iv.w));
+          step(key, idx);
+        }
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int q = 0; q < KB / 2; ++q) kb[q] = nkb[q];
+#pragma unroll
+      for (int q = 0; q < KB / 4; ++q) ib[q] = nib[q];
     }
   }
 
@@ -1224,7 +1285,7 @@ gg_status gg_cache_run_batch(gg_ctx* ctx, const gg_trace* tr, uint32_t* result, 
   hipLaunchKernelGGL(k_shard_scan, dim3(g.tiles), dim3(scan_threads), 0, s, ctx->chunk_cnt,
                      ctx->chunk_tile + nchunks, ctx->unit_len, g);
   GG_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_group_scan, dim3(1), dim3(1024), 0, s, ctx->unit_len, g.units, ctx->unit_base, ctx->total_dev);
+  hipLaunchKernelGGL(k_unit_scan, dim3(1), dim3(1024), 0, s, ctx->unit_len, g.units, ctx->unit_base, ctx->total_dev);
   GG_HIP(hipGetLastError());
   // size the interleaved record buffers (one small device->host read per batch)
   uint64_t total = 0;
@@ -1237,7 +1298,7 @@ gg_status gg_cache_run_batch(gg_ctx* ctx, const gg_trace* tr, uint32_t* result, 
     ctx->sh_cap = std::min(cap_key, cap_idx);
   }
   if (nchunks) {
-    hipLaunchKernelGGL(k_shard_scatter, dim3((uint32_t)nchunks), dim3(64), 0, s, tr->addr_dev, tr->meta_dev,
+    hipLaunchKernelGGL(k_shard_scatter, dim3((uint32_t)nchunks), dim3(64), scatter_lds_bytes(g), s, tr->addr_dev, tr->meta_dev,
                        ctx->chunk_tile, ctx->chunk_start, ctx->chunk_len, ctx->chunk_cnt, ctx->unit_base,
                        ctx->tile_off_dev, ctx->sh_key, ctx->sh_idx, g);
     GG_HIP(hipGetLastError());
