@@ -210,30 +210,38 @@ __global__ __launch_bounds__(1024) void k_unit_scan(const uint32_t* __restrict__
   for (uint64_t u = u0; u < u1; ++u) { unit_base[u] = base; base += (unit_len[u] + 7u) & ~7u; }
 }
 
-// Pass 3: one wave per chunk of kChunk records.  The chunk is held in VGPRs,
-// counted per L1-D set with LDS atomics, ranked in program order (lanes with
-// the same set matched by log2(u1) ballots, so each unit keeps program order),
-// staged in LDS sorted by set, then written out per set as contiguous runs
-// (consecutive lanes -> consecutive addresses: whole cache lines per run).
+// Workgroup -> chunk map that gives each XCD a contiguous range of chunks.
+// Workgroups are dealt round-robin to the 8 XCDs (blockIdx % 8); mapping
+// XCD x to chunks [x*q + min(x,r), ...) keeps adjacent chunks of a tile on the
+// same XCD, so the partial cache lines at the ends of their per-set runs
+// merge in that XCD's L2 instead of being written back half-filled.
+__device__ __forceinline__ uint32_t xcd_chunk(uint32_t b, uint32_t n)
+{
+  const uint32_t q = n / GG_NUM_XCD, r = n % GG_NUM_XCD, x = b % GG_NUM_XCD, k = b / GG_NUM_XCD;
+  return x * q + min(x, r) + k;
+}
+
+// Pass 3: one wave per chunk of kChunk records.  The chunk's keys are held in
+// VGPRs, counted per L1-D set with LDS atomics, ranked in program order (lanes
+// with the same set matched by log2(u1) ballots, so each unit keeps program
+// order), staged in LDS sorted by set, then written out per set as contiguous
+// runs (consecutive lanes -> consecutive addresses).  Each record's slot goes
+// to rec_slot[] in program order (coalesced), for k_unshard.
 __global__ __launch_bounds__(64) void k_shard_scatter(const uint64_t* __restrict__ addr,
     const uint32_t* __restrict__ meta, const uint32_t* __restrict__ chunk_tile,
     const uint64_t* __restrict__ chunk_start, const uint32_t* __restrict__ chunk_len,
     const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ unit_base,
-    const uint64_t* __restrict__ tile_off, uint64_t* __restrict__ sh_key,
-    uint32_t* __restrict__ sh_idx, gg_geom g)
+    uint64_t* __restrict__ sh_key, uint32_t* __restrict__ rec_slot, gg_geom g, uint32_t nchunks)
 {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint64_t* skey = reinterpret_cast<uint64_t*>(smem);                      // [kChunk]
-  uint32_t* sidx = reinterpret_cast<uint32_t*>(skey + kChunk);             // [kChunk]
-  uint16_t* sset = reinterpret_cast<uint16_t*>(sidx + kChunk);             // [kChunk]
-  uint64_t* dbase = reinterpret_cast<uint64_t*>(sset + kChunk);            // [u1] dest - local offset
+  uint64_t* dbase = skey + kChunk;                                         // [u1] dest - local offset
   uint32_t* lcnt = reinterpret_cast<uint32_t*>(dbase + g.u1);             // [u1] count, then running rank
   uint32_t* loff = lcnt + g.u1;                                            // [u1] exclusive prefix
-  const uint32_t c = blockIdx.x, lane = threadIdx.x;
+  const uint32_t c = xcd_chunk(blockIdx.x, nchunks), lane = threadIdx.x;
   const uint32_t t = chunk_tile[c];
   const uint64_t start = chunk_start[c];
   const uint32_t len = chunk_len[c];
-  const uint32_t rel0 = (uint32_t)(start - tile_off[t]);
   const uint64_t line_mask = ~((1ull << g.log_line) - 1);
   const uint32_t smask = g.u1 - 1;
   for (uint32_t s = lane; s < g.u1; s += GG_WAVE) lcnt[s] = 0;
@@ -289,19 +297,46 @@ __global__ __launch_bounds__(64) void k_shard_scatter(const uint64_t* __restrict
     if (valid) {
       const uint32_t q = loff[s] + r0 + rank;
       skey[q] = key[k];
-      sidx[q] = rel0 + i;
-      sset[q] = (uint16_t)s;
+      rec_slot[start + i] = (uint32_t)(dbase[s] + q);
     }
   }
   __syncthreads();
   for (uint32_t q = lane; q < len; q += GG_WAVE) {
-    const uint64_t dst = dbase[sset[q]] + q;
-    sh_key[dst] = skey[q];
-    sh_idx[dst] = sidx[q];
+    const uint64_t k = skey[q];
+    sh_key[dbase[(uint32_t)(k >> g.log_line) & smask] + q] = k;
   }
 }
 
-size_t scatter_lds_bytes(const gg_geom& g) { return (size_t)kChunk * (8 + 4 + 2) + (size_t)g.u1 * (8 + 4 + 4); }
+size_t scatter_lds_bytes(const gg_geom& g) { return (size_t)kChunk * 8 + (size_t)g.u1 * (8 + 4 + 4); }
+
+// Pass 5: program-order results.  result[i] = sh_res[rec_slot[i]]; the reads
+// of one workgroup fall in the per-set runs of one or two chunks (local).
+__global__ __launch_bounds__(256) void k_unshard(const uint32_t* __restrict__ rec_slot,
+    const uint32_t* __restrict__ sh_res, const uint64_t* __restrict__ sh_ev, uint32_t* __restrict__ result,
+    uint64_t* __restrict__ evicted, uint64_t n)
+{
+  const uint64_t nb = (n + 1023) / 1024;
+  for (uint64_t b = xcd_chunk(blockIdx.x, gridDim.x); b < nb; b += gridDim.x) {
+    const uint64_t i0 = b * 1024 + threadIdx.x;
+    uint32_t sl[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sl[k] = (i0 + 256 * k < n) ? rec_slot[i0 + 256 * k] : 0u;
+    if (result) {
+      uint32_t r[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) r[k] = (i0 + 256 * k < n) ? sh_res[sl[k]] : 0u;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) if (i0 + 256 * k < n) result[i0 + 256 * k] = r[k];
+    }
+    if (evicted) {
+      uint64_t e[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) e[k] = (i0 + 256 * k < n) ? sh_ev[sl[k]] : 0ull;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) if (i0 + 256 * k < n) evicted[i0 + 256 * k] = e[k];
+    }
+  }
+}
 
 // ---------------------------------------------------------------------------
 // Replay kernel.  One lane per unit (tile, L1-D set), 64 units per wave.
@@ -417,10 +452,9 @@ __device__ void replay_counters(const gg_cache_state& cs, const gg_geom& g, cons
 
 template <int A1, int A2, bool LRU1, bool LRU2>
 __global__ __launch_bounds__(64) void k_cache_replay(gg_cache_state cs, gg_geom g,
-    const uint64_t* __restrict__ sh_key, const uint32_t* __restrict__ sh_idx,
-    const uint32_t* __restrict__ unit_len, const uint64_t* __restrict__ unit_base,
-    const uint64_t* __restrict__ tile_off, uint32_t* __restrict__ result,
-    uint64_t* __restrict__ evicted, uint32_t* err)
+    const uint64_t* __restrict__ sh_key, const uint32_t* __restrict__ unit_len,
+    const uint64_t* __restrict__ unit_base, uint32_t* __restrict__ sh_res,
+    uint64_t* __restrict__ sh_ev, uint32_t* err)
 {
   constexpr int MW = (A2 + 7) / 8;
   constexpr int TQ = (A2 + 3) / 4;                 // uint4 quads of tags per set
@@ -478,7 +512,6 @@ __global__ __launch_bounds__(64) void k_cache_replay(gg_cache_state cs, gg_geom 
   const uint32_t len = active ? unit_len[uu] : 0;
   const uint64_t base = active ? unit_base[uu] : 0;
   const uint32_t tile = (uint32_t)(uu >> g.log_u1);
-  const uint64_t rbase = tile_off[tile];
   uint32_t maxlen = len;
   for (int o = 32; o > 0; o >>= 1) maxlen = max(maxlen, (uint32_t)__shfl_xor((int)maxlen, o));
 
@@ -488,23 +521,18 @@ __global__ __launch_bounds__(64) void k_cache_replay(gg_cache_state cs, gg_geom 
 
   // prefetch ring of the lane's record stream (distance 4)
   constexpr int PD = 4;
-  uint64_t kr[PD]; uint32_t ir[PD];
+  uint64_t kr[PD];
 #pragma unroll
-  for (int d = 0; d < PD; ++d) {
-    kr[d] = (d < (int)len) ? sh_key[base + d] : 0;
-    ir[d] = (d < (int)len) ? sh_idx[base + d] : 0;
-  }
+  for (int d = 0; d < PD; ++d) kr[d] = (d < (int)len) ? sh_key[base + d] : 0;
   const uint64_t lmask = (g.s2 - 1);
 
   for (uint32_t j = 0; j < maxlen; ++j) {
     const bool live = j < len;
     const uint64_t key = kr[0];
-    const uint32_t idx = ir[0];
 #pragma unroll
-    for (int d = 0; d < PD - 1; ++d) { kr[d] = kr[d + 1]; ir[d] = ir[d + 1]; }
+    for (int d = 0; d < PD - 1; ++d) kr[d] = kr[d + 1];
     const bool more = j + PD < len;
     kr[PD - 1] = more ? sh_key[base + j + PD] : 0;
-    ir[PD - 1] = more ? sh_idx[base + j + PD] : 0;
     if (!live) continue;
 
     const uint64_t line = key >> g.log_line;
@@ -616,8 +644,8 @@ __global__ __launch_bounds__(64) void k_cache_replay(gg_cache_state cs, gg_geom 
                          (upg ? GG_RES_UPGRADE : 0u) | (l1ev ? GG_RES_L1_EVICT : 0u) |
                          (l2ev ? GG_RES_L2_EVICT : 0u) | (dirty ? GG_RES_L2_EVICT_DIRTY : 0u) |
                          (invl1 ? GG_RES_L2_EVICT_INV_L1 : 0u);
-    if (result) result[rbase + idx] = res;
-    if (evicted) evicted[rbase + idx] = l2ev ? (e2 << g.log_line) : ~0ull;
+    if (sh_res) sh_res[base + j] = res;
+    if (sh_ev) sh_ev[base + j] = l2ev ? (e2 << g.log_line) : ~0ull;
   }
 
   // ---- store state back, with cached_loc materialised from the L1-D ----
@@ -696,10 +724,9 @@ __device__ __forceinline__ int victim_nib(uint32_t states, uint32_t ages)
 
 template <int A1, int A2, bool LRU1, bool LRU2>
 __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_geom g,
-    const uint64_t* __restrict__ sh_key, const uint32_t* __restrict__ sh_idx,
-    const uint32_t* __restrict__ unit_len, const uint64_t* __restrict__ unit_base,
-    const uint64_t* __restrict__ tile_off, uint32_t* __restrict__ result,
-    uint64_t* __restrict__ evicted, uint32_t* err)
+    const uint64_t* __restrict__ sh_key, const uint32_t* __restrict__ unit_len,
+    const uint64_t* __restrict__ unit_base, uint32_t* __restrict__ sh_res,
+    uint64_t* __restrict__ sh_ev, uint32_t* err)
 {
   static_assert(A1 <= 4 && A2 <= 8, "lean replay covers L1-D assoc <= 4, L2 assoc <= 8");
   constexpr int TQ = (A2 + 3) / 4;
@@ -733,7 +760,7 @@ __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_
     }
   }
   uint32_t rr1 = cs.l1_rr[uu];
-  uint32_t nloc = 0, nheld = 0;
+  uint32_t nheld = 0;
   for (uint32_t s = 0; s < S2; ++s) {
     uint32_t tg[4 * TQ];
 #pragma unroll
@@ -754,7 +781,6 @@ __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_
 #pragma unroll
       for (int k = 0; k < A1; ++k) hw = (valid && ((st1 >> (2 * k)) & 3u) && t1[k] == ln) ? k : hw;
       const bool loc = GG_M_LOC(b) != 0;
-      nloc += loc ? 1u : 0u;
       nheld += (hw >= 0) ? 1u : 0u;
       errv |= (loc != (hw >= 0)) ? GG_DERR_STATE : 0u;
       if (hw >= 0) pos1 = (pos1 & ~(0xFFu << (8 * hw))) | ((s * A2 + w) << (8 * hw));
@@ -776,7 +802,6 @@ __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_
   const uint32_t len = active ? unit_len[uu] : 0;
   const uint64_t base = active ? unit_base[uu] : 0;
   const uint32_t tile = (uint32_t)(uu >> g.log_u1);
-  const uint64_t rbase = tile_off[tile];
   uint32_t maxlen = len;
   for (int o = 32; o > 0; o >>= 1) maxlen = max(maxlen, (uint32_t)__shfl_xor((int)maxlen, o));
 
@@ -786,8 +811,9 @@ __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_
   const uint32_t s2m = S2 - 1;
   const uint32_t log_line = g.log_line, log_u1 = g.log_u1, log_l2 = g.log_l2;
 
-  // One access of this lane's unit (the body of processMemOpFromCore).
-  auto step = [&](const uint64_t key, const uint32_t idx) {
+  // One access of this lane's unit (the body of processMemOpFromCore); returns
+  // the result word, and the evicted L2 line address through *ev.
+  auto step = [&](const uint64_t key, uint64_t* ev) -> uint32_t {
     const uint64_t line = key >> log_line;
     const uint32_t wr = (uint32_t)key & 1u;
     const uint32_t s = (uint32_t)(line >> log_u1) & s2m;
@@ -837,7 +863,7 @@ __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_
     const bool l2ev = miss2 && sv != 0;
     const bool dirty = l2ev && sv == GG_MS_M;
     uint32_t vt = 0;
-    if (evicted) {
+    if (sh_ev) {
 #pragma unroll
       for (int w = 0; w < A2; ++w) vt = (w == v2) ? tg[w] : vt;
     }
@@ -882,52 +908,59 @@ __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_
                          (upg ? GG_RES_UPGRADE : 0u) | (l1ev ? GG_RES_L1_EVICT : 0u) |
                          (l2ev ? GG_RES_L2_EVICT : 0u) | (dirty ? GG_RES_L2_EVICT_DIRTY : 0u) |
                          (invl1 ? GG_RES_L2_EVICT_INV_L1 : 0u);
-    if (result) result[rbase + idx] = res;
-    if (evicted) {
+    if (sh_ev) {
       const uint64_t e2 = ((uint64_t)vt << log_l2) | ((uint64_t)s << log_u1) | l1set;
-      evicted[rbase + idx] = l2ev ? (e2 << log_line) : ~0ull;
+      *ev = l2ev ? (e2 << log_line) : ~0ull;
     }
-    };
+    return res;
+  };
 
   // The unit's records are contiguous from `base` (8-record aligned): stream
-  // them in 8-record blocks (4 + 2 dwordx4 loads), next block in flight while
-  // the current one is replayed from registers.
+  // them in 8-record blocks (4 dwordx4 loads), next block in flight while the
+  // current one is replayed from registers; the block's 8 results go out as
+  // 2 dwordx4 stores to the same slots of sh_res (padding slots included).
   constexpr int KB = 8;
   const uint4* kp = reinterpret_cast<const uint4*>(sh_key + base);
-  const uint4* ip = reinterpret_cast<const uint4*>(sh_idx + base);
-  uint4 kb[KB / 2], ib[KB / 4];
+  uint4* rp = reinterpret_cast<uint4*>(sh_res + base);
+  uint4* ep = reinterpret_cast<uint4*>(sh_ev + base);
+  uint4 kb[KB / 2];
   if (len > 0) {
 #pragma unroll
     for (int q = 0; q < KB / 2; ++q) kb[q] = kp[q];
-#pragma unroll
-    for (int q = 0; q < KB / 4; ++q) ib[q] = ip[q];
   }
   for (uint32_t j0 = 0; j0 < maxlen; j0 += KB) {
-    uint4 nkb[KB / 2], nib[KB / 4];
+    uint4 nkb[KB / 2];
     const bool more = j0 + KB < len;
     if (more) {
 #pragma unroll
       for (int q = 0; q < KB / 2; ++q) nkb[q] = kp[(j0 + KB) / 2 + q];
-#pragma unroll
-      for (int q = 0; q < KB / 4; ++q) nib[q] = ip[(j0 + KB) / 4 + q];
     }
     if (j0 < len) {
+      uint32_t rv[KB];
+      uint64_t ev[KB];
 #pragma unroll
       for (int d = 0; d < KB; ++d) {
+        rv[d] = 0; ev[d] = ~0ull;
         if (j0 + d < len) {
           const uint4 kv = kb[d / 2];
           const uint64_t key = (d & 1) ? (((uint64_t)kv.w << 32) | kv.z) : (((uint64_t)kv.y << 32) | kv.x);
-          const uint4 iv = ib[d / 4];
-          const uint32_t idx = (d & 3) == 0 ? iv.x : ((d & 3) == 1 ? iv.y : ((d & 3) == 2 ? iv.z : iv.w));
-          step(key, idx);
+          rv[d] = step(key, &ev[d]);
         }
+      }
+      if (sh_res) {
+        rp[j0 / 4] = make_uint4(rv[0], rv[1], rv[2], rv[3]);
+        rp[j0 / 4 + 1] = make_uint4(rv[4], rv[5], rv[6], rv[7]);
+      }
+      if (sh_ev) {
+#pragma unroll
+        for (int q = 0; q < KB / 2; ++q)
+          ep[j0 / 2 + q] = make_uint4((uint32_t)ev[2 * q], (uint32_t)(ev[2 * q] >> 32),
+                                      (uint32_t)ev[2 * q + 1], (uint32_t)(ev[2 * q + 1] >> 32));
       }
     }
     if (more) {
 #pragma unroll
       for (int q = 0; q < KB / 2; ++q) kb[q] = nkb[q];
-#pragma unroll
-      for (int q = 0; q < KB / 4; ++q) ib[q] = nib[q];
     }
   }
 
@@ -1132,8 +1165,8 @@ __global__ void k_quartet(gg_cache_state cs, gg_geom g, QuartetIO* io)
 // ---------------------------------------------------------------------------
 // dispatch over the instantiated geometries
 // ---------------------------------------------------------------------------
-typedef void (*replay_fn)(gg_cache_state, gg_geom, const uint64_t*, const uint32_t*, const uint32_t*,
-                          const uint64_t*, const uint64_t*, uint32_t*, uint64_t*, uint32_t*);
+typedef void (*replay_fn)(gg_cache_state, gg_geom, const uint64_t*, const uint32_t*, const uint64_t*,
+                          uint32_t*, uint64_t*, uint32_t*);
 typedef void (*quartet_fn)(gg_cache_state, gg_geom, QuartetIO*);
 
 struct Kern { int a1, a2; int lru1, lru2; replay_fn replay; quartet_fn quartet; };
@@ -1219,7 +1252,7 @@ void gg_cache_state_free(gg_ctx* ctx)
 {
   gg_cache_state& cs = ctx->cs;
   void* ps[] = {cs.l1_tag, cs.l1_meta, cs.l1_rr, cs.l2_tag, cs.l2_meta, cs.l2_rr, cs.counters,
-                ctx->sh_key, ctx->sh_idx, ctx->chunk_cnt, ctx->chunk_tile, ctx->chunk_start,
+                ctx->sh_key, ctx->sh_res, ctx->sh_ev, ctx->rec_slot, ctx->chunk_cnt, ctx->chunk_tile, ctx->chunk_start,
                 ctx->chunk_len, ctx->unit_len, ctx->unit_base, ctx->tile_off_dev, ctx->total_dev};
   for (void* p : ps) if (p) hipFree(p);
 }
@@ -1275,7 +1308,7 @@ gg_status gg_cache_run_batch(gg_ctx* ctx, const gg_trace* tr, uint32_t* result, 
   GG_HIP(hipMemcpyAsync(ctx->tile_off_dev, tr->tile_offsets, sizeof(uint64_t) * (g.tiles + 1), hipMemcpyHostToDevice, s));
 
   if (nchunks) {
-    gg_timer_begin(ctx, "cache_shard", s);
+    gg_timer_begin(ctx, "cache_hist", s);
     hipLaunchKernelGGL(k_shard_hist, dim3((uint32_t)nchunks), dim3(256), 0, s, tr->addr_dev, ctx->chunk_tile,
                        ctx->chunk_start, ctx->chunk_len, ctx->chunk_cnt, g, ctx->err_dev);
     GG_HIP(hipGetLastError());
@@ -1287,32 +1320,42 @@ gg_status gg_cache_run_batch(gg_ctx* ctx, const gg_trace* tr, uint32_t* result, 
   GG_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_unit_scan, dim3(1), dim3(1024), 0, s, ctx->unit_len, g.units, ctx->unit_base, ctx->total_dev);
   GG_HIP(hipGetLastError());
-  // size the interleaved record buffers (one small device->host read per batch)
+  if (nchunks) gg_timer_end(ctx, "cache_hist", s);
+  // size the sharded record buffers (one small device->host read per batch)
   uint64_t total = 0;
   GG_HIP(hipMemcpyAsync(&total, ctx->total_dev, sizeof(total), hipMemcpyDeviceToHost, s));
   GG_HIP(hipStreamSynchronize(s));
-  {
-    uint64_t cap_key = ctx->sh_cap, cap_idx = ctx->sh_cap;
-    if (gg_status st = grow(&ctx->sh_key, &cap_key, total)) return st;
-    if (gg_status st = grow(&ctx->sh_idx, &cap_idx, total)) return st;
-    ctx->sh_cap = std::min(cap_key, cap_idx);
-  }
+  if (total >= (1ull << 32)) return gg_fail(GG_ERR_RANGE, "batch needs %llu record slots (limit 2^32)", (unsigned long long)total);
+  if (gg_status st = grow(&ctx->sh_key, &ctx->sh_cap, total)) return st;
+  if (gg_status st = grow(&ctx->rec_slot, &ctx->rec_cap, n)) return st;
+  if (result) { if (gg_status st = grow(&ctx->sh_res, &ctx->sh_res_cap, total)) return st; }
+  if (evicted) { if (gg_status st = grow(&ctx->sh_ev, &ctx->sh_ev_cap, total)) return st; }
   if (nchunks) {
+    gg_timer_begin(ctx, "cache_scatter", s);
     hipLaunchKernelGGL(k_shard_scatter, dim3((uint32_t)nchunks), dim3(64), scatter_lds_bytes(g), s, tr->addr_dev, tr->meta_dev,
                        ctx->chunk_tile, ctx->chunk_start, ctx->chunk_len, ctx->chunk_cnt, ctx->unit_base,
-                       ctx->tile_off_dev, ctx->sh_key, ctx->sh_idx, g);
+                       ctx->sh_key, ctx->rec_slot, g, (uint32_t)nchunks);
     GG_HIP(hipGetLastError());
-    gg_timer_end(ctx, "cache_shard", s);
+    gg_timer_end(ctx, "cache_scatter", s);
   }
-  const Kern* k = (ctx->replay_variant != 1) ? find_lean(g.a1, g.a2, g.pol1, g.pol2) : nullptr;
-  if (!k) k = find_kernel(g.a1, g.a2, g.pol1, g.pol2);
+  const Kern* lean = find_lean(g.a1, g.a2, g.pol1, g.pol2);
+  const Kern* k = (ctx->replay_variant != 1 && lean) ? lean : find_kernel(g.a1, g.a2, g.pol1, g.pol2);
   const uint32_t groups = (uint32_t)((g.units + GG_WAVE - 1) / GG_WAVE);
   gg_timer_begin(ctx, "cache_replay", s);
-  hipLaunchKernelGGL(k->replay, dim3(groups), dim3(GG_WAVE), replay_lds_bytes(g, k == find_lean(g.a1, g.a2, g.pol1, g.pol2)), s, ctx->cs, g,
-                     (const uint64_t*)ctx->sh_key, (const uint32_t*)ctx->sh_idx, (const uint32_t*)ctx->unit_len,
-                     (const uint64_t*)ctx->unit_base, (const uint64_t*)ctx->tile_off_dev, result, evicted, ctx->err_dev);
+  hipLaunchKernelGGL(k->replay, dim3(groups), dim3(GG_WAVE), replay_lds_bytes(g, k == lean), s, ctx->cs, g,
+                     (const uint64_t*)ctx->sh_key, (const uint32_t*)ctx->unit_len, (const uint64_t*)ctx->unit_base,
+                     result ? ctx->sh_res : nullptr, evicted ? ctx->sh_ev : nullptr, ctx->err_dev);
   GG_HIP(hipGetLastError());
   gg_timer_end(ctx, "cache_replay", s);
+  if (n && (result || evicted)) {
+    const uint64_t nb = (n + 1023) / 1024;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(nb, 256ull * 64);
+    gg_timer_begin(ctx, "cache_unshard", s);
+    hipLaunchKernelGGL(k_unshard, dim3(grid), dim3(256), 0, s, (const uint32_t*)ctx->rec_slot,
+                       (const uint32_t*)ctx->sh_res, (const uint64_t*)ctx->sh_ev, result, evicted, n);
+    GG_HIP(hipGetLastError());
+    gg_timer_end(ctx, "cache_unshard", s);
+  }
   return GG_OK;
 }
 

@@ -8,6 +8,7 @@
 #include "../../include/graphite_gpu.h"
 
 #define GG_WAVE 64
+#define GG_NUM_XCD 8          // MI355X: 8 XCDs, workgroups dealt round-robin by blockIdx
 
 // Packed meta byte of one cache line in the device-resident state:
 //   bits 0-1 state (0 I, 1 S, 2 M), bit 2 cached_loc == L1-D (L2 only),
@@ -72,17 +73,20 @@ struct gg_ctx {
   gg_cache_state cs{};
   uint32_t* err_dev = nullptr;
   // batch scratch (grown on demand)
-  uint64_t* sh_key = nullptr;    // sharded records: line address | write bit
-  uint32_t* sh_idx = nullptr;    // record index within its tile
-  uint64_t  sh_cap = 0;
+  uint64_t* sh_key = nullptr;    // sharded records (slot order): line address | write bit
+  uint32_t* sh_res = nullptr;    // replay results in slot order
+  uint64_t* sh_ev = nullptr;     // evicted L2 line addresses in slot order (only when requested)
+  uint64_t  sh_cap = 0, sh_res_cap = 0, sh_ev_cap = 0;
+  uint32_t* rec_slot = nullptr;  // [records] slot of each program-order record (written by the scatter)
+  uint64_t  rec_cap = 0;
   uint32_t* chunk_cnt = nullptr; // [chunks][u1]
   uint32_t* chunk_tile = nullptr;
   uint64_t* chunk_start = nullptr;
   uint32_t* chunk_len = nullptr;
   uint64_t  chunk_cap = 0;
   uint32_t* unit_len = nullptr;  // [units]
-  uint64_t* unit_base = nullptr; // [units] slot of record 0; record j at +64*j
-  uint64_t* total_dev = nullptr; // slots of the interleaved layout
+  uint64_t* unit_base = nullptr; // [units] slot of the unit's record 0 (records contiguous, padded to 8)
+  uint64_t* total_dev = nullptr; // slots of the sharded layout
   uint64_t* tile_off_dev = nullptr; // [tiles+1]
   std::vector<uint32_t> h_chunk_tile, h_chunk_len;
   std::vector<uint64_t> h_chunk_start;

@@ -246,7 +246,8 @@ gg_status gg_gen_uniform_trace(uint64_t* addr_dev, uint32_t* meta_dev, uint32_t 
                                uint32_t lines_log2, uint32_t base_shift, void* stream);
 
 /* Device time (ms) of the most recent launch of a named kernel
- * ("cache_replay", "cache_shard", "noc_hop_counter", ...), measured with HIP
+ * ("cache_hist", "cache_scatter", "cache_replay", "cache_unshard",
+ * "noc_hop_counter", ...), measured with HIP
  * events on the stream the kernel ran on; negative if not launched.           */
 float     gg_kernel_time_ms(gg_ctx* ctx, const char* kernel);
 void      gg_set_timing(gg_ctx* ctx, int enabled);
