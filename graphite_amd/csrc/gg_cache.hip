@@ -19,11 +19,12 @@
 #include "gg_internal.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 namespace {
 
-constexpr uint32_t kChunk = 2048;        // records per shard chunk (one wave, staged in LDS)
+constexpr uint32_t kChunk = 1024;        // records per shard chunk (one wave, staged in LDS)
 constexpr uint32_t kPerLane = kChunk / 64;
 constexpr uint64_t kB7 = 0x8080808080808080ull;
 constexpr uint64_t k7F = 0x7F7F7F7F7F7F7F7Full;
@@ -227,6 +228,13 @@ __device__ __forceinline__ uint32_t xcd_chunk(uint32_t b, uint32_t n)
 // order), staged in LDS sorted by set, then written out per set as contiguous
 // runs (consecutive lanes -> consecutive addresses).  Each record's slot goes
 // to rec_slot[] in program order (coalesced), for k_unshard.
+//
+// Persistent: workgroup b walks chunks b, b+G, b+2G, ... (G = gridDim.x, a
+// multiple of 8, so every chunk of a workgroup lies in its XCD's range), and
+// the next chunk's addr/meta loads are in flight while the current chunk is
+// ranked and written.  The workgroup is one wave, so LDS hand-offs between
+// phases need only a wave barrier (LDS instructions of a wave execute in order).
+template <int PER, bool PERSIST>    // PER = L1-D sets per lane: max(1, u1 / 64)
 __global__ __launch_bounds__(64) void k_shard_scatter(const uint64_t* __restrict__ addr,
     const uint32_t* __restrict__ meta, const uint32_t* __restrict__ chunk_tile,
     const uint64_t* __restrict__ chunk_start, const uint32_t* __restrict__ chunk_len,
@@ -238,102 +246,152 @@ __global__ __launch_bounds__(64) void k_shard_scatter(const uint64_t* __restrict
   uint64_t* dbase = skey + kChunk;                                         // [u1] dest - local offset
   uint32_t* lcnt = reinterpret_cast<uint32_t*>(dbase + g.u1);             // [u1] count, then running rank
   uint32_t* loff = lcnt + g.u1;                                            // [u1] exclusive prefix
-  const uint32_t c = xcd_chunk(blockIdx.x, nchunks), lane = threadIdx.x;
-  const uint32_t t = chunk_tile[c];
-  const uint64_t start = chunk_start[c];
-  const uint32_t len = chunk_len[c];
+  const uint32_t lane = threadIdx.x, G = gridDim.x;
   const uint64_t line_mask = ~((1ull << g.log_line) - 1);
   const uint32_t smask = g.u1 - 1;
-  for (uint32_t s = lane; s < g.u1; s += GG_WAVE) lcnt[s] = 0;
-  __syncthreads();
-  uint64_t key[kPerLane];
+  const uint64_t lt_mask = (1ull << lane) - 1;
+  auto wave_sync = [] { __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); };
+
+  uint32_t i = blockIdx.x;
+  if (i >= nchunks) return;
+  uint32_t c = xcd_chunk(i, nchunks);
+  uint64_t pa[kPerLane];
+  uint32_t pm[kPerLane];
+  auto issue = [&](uint32_t cc) {
+    const uint64_t st = chunk_start[cc];
+    const uint32_t ln = chunk_len[cc];
 #pragma unroll
-  for (uint32_t k = 0; k < kPerLane; ++k) {
-    const uint32_t i = k * GG_WAVE + lane;
-    const bool valid = i < len;
-    const uint64_t a = valid ? addr[start + i] : 0;
-    const uint32_t m = valid ? meta[start + i] : 0;
-    key[k] = (a & line_mask) | (m & GG_META_WRITE);
-    if (valid) atomicAdd(&lcnt[(uint32_t)(a >> g.log_line) & smask], 1u);
-  }
-  __syncthreads();
-  // exclusive prefix of the per-set counts (lane-strided blocks + wave scan)
-  {
-    const uint32_t per = (g.u1 + GG_WAVE - 1) / GG_WAVE;
-    uint32_t sum = 0;
-    for (uint32_t k = 0; k < per; ++k) { const uint32_t s = lane * per + k; if (s < g.u1) sum += lcnt[s]; }
-    uint32_t incl = sum;
-    for (int o = 1; o < GG_WAVE; o <<= 1) { const uint32_t v = __shfl_up(incl, o); if ((int)lane >= o) incl += v; }
-    uint32_t run = incl - sum;
-    for (uint32_t k = 0; k < per; ++k) {
-      const uint32_t s = lane * per + k;
-      if (s < g.u1) {
-        loff[s] = run;
-        dbase[s] = unit_base[(uint64_t)t * g.u1 + s] + cnt[(uint64_t)c * g.u1 + s] - run;
-        run += lcnt[s];
+    for (uint32_t k = 0; k < kPerLane; ++k) {
+      const uint32_t j = k * GG_WAVE + lane;
+      pa[k] = (j < ln) ? addr[st + j] : 0;
+      pm[k] = (j < ln) ? meta[st + j] : 0;
+    }
+  };
+  issue(c);
+  for (;;) {
+    const uint32_t t = chunk_tile[c];
+    const uint64_t start = chunk_start[c];
+    const uint32_t len = chunk_len[c];
+    // this chunk's per-set bases (issued before the next chunk's prefetch)
+    uint64_t ub[PER];
+    uint32_t cb[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const uint32_t s = lane * PER + k;
+      ub[k] = (s < g.u1) ? unit_base[(uint64_t)t * g.u1 + s] : 0;
+      cb[k] = (s < g.u1) ? cnt[(uint64_t)c * g.u1 + s] : 0;
+    }
+    uint64_t key[kPerLane];
+#pragma unroll
+    for (uint32_t k = 0; k < kPerLane; ++k) key[k] = (pa[k] & line_mask) | (pm[k] & GG_META_WRITE);
+    const uint32_t inext = i + G;
+    const bool more = PERSIST && inext < nchunks;
+    const uint32_t cn = more ? xcd_chunk(inext, nchunks) : c;
+    if (more) issue(cn);
+
+    for (uint32_t s = lane; s < g.u1; s += GG_WAVE) lcnt[s] = 0;
+    wave_sync();
+#pragma unroll
+    for (uint32_t k = 0; k < kPerLane; ++k)
+      if (k * GG_WAVE + lane < len) atomicAdd(&lcnt[(uint32_t)(key[k] >> g.log_line) & smask], 1u);
+    wave_sync();
+    // exclusive prefix of the per-set counts (lane-blocked + wave scan)
+    {
+      uint32_t lc[PER];
+      uint32_t sum = 0;
+#pragma unroll
+      for (int k = 0; k < PER; ++k) { const uint32_t s = lane * PER + k; lc[k] = (s < g.u1) ? lcnt[s] : 0; sum += lc[k]; }
+      uint32_t incl = sum;
+      for (int o = 1; o < GG_WAVE; o <<= 1) { const uint32_t v = __shfl_up(incl, o); if ((int)lane >= o) incl += v; }
+      uint32_t run = incl - sum;
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const uint32_t s = lane * PER + k;
+        if (s < g.u1) { loff[s] = run; dbase[s] = ub[k] + cb[k] - run; lcnt[s] = 0; }
+        run += lc[k];
       }
     }
-  }
-  __syncthreads();
-  for (uint32_t s = lane; s < g.u1; s += GG_WAVE) lcnt[s] = 0;
-  __syncthreads();
-  const uint64_t lt_mask = (1ull << lane) - 1;
+    wave_sync();
 #pragma unroll
-  for (uint32_t k = 0; k < kPerLane; ++k) {
-    const uint32_t i = k * GG_WAVE + lane;
-    const bool valid = i < len;
-    const uint32_t s = (uint32_t)(key[k] >> g.log_line) & smask;
-    uint64_t peers = __ballot(valid);
-    for (uint32_t b = 0; b < g.log_u1; ++b) {
-      const bool bit = (s >> b) & 1u;
-      const uint64_t bb = __ballot(bit);
-      peers &= bit ? bb : ~bb;
+    for (uint32_t k = 0; k < kPerLane; ++k) {
+      const uint32_t j = k * GG_WAVE + lane;
+      const bool valid = j < len;
+      const uint32_t s = (uint32_t)(key[k] >> g.log_line) & smask;
+      uint64_t peers = __ballot(valid);
+      for (uint32_t b = 0; b < g.log_u1; ++b) {
+        const bool bit = (s >> b) & 1u;
+        const uint64_t bb = __ballot(bit);
+        peers &= bit ? bb : ~bb;
+      }
+      const uint32_t rank = __popcll(peers & lt_mask);
+      const uint32_t r0 = valid ? lcnt[s] : 0;
+      wave_sync();
+      if (valid && rank == 0) lcnt[s] = r0 + (uint32_t)__popcll(peers);
+      wave_sync();
+      if (valid) {
+        const uint32_t q = loff[s] + r0 + rank;
+        skey[q] = key[k];
+        rec_slot[start + j] = (uint32_t)(dbase[s] + q);
+      }
     }
-    const uint32_t rank = __popcll(peers & lt_mask);
-    const uint32_t r0 = valid ? lcnt[s] : 0;
-    __builtin_amdgcn_wave_barrier();
-    if (valid && rank == 0) lcnt[s] = r0 + (uint32_t)__popcll(peers);
-    __builtin_amdgcn_wave_barrier();
-    if (valid) {
-      const uint32_t q = loff[s] + r0 + rank;
-      skey[q] = key[k];
-      rec_slot[start + i] = (uint32_t)(dbase[s] + q);
+    wave_sync();
+    for (uint32_t q = lane; q < len; q += GG_WAVE) {
+      const uint64_t k = skey[q];
+      sh_key[dbase[(uint32_t)(k >> g.log_line) & smask] + q] = k;
     }
-  }
-  __syncthreads();
-  for (uint32_t q = lane; q < len; q += GG_WAVE) {
-    const uint64_t k = skey[q];
-    sh_key[dbase[(uint32_t)(k >> g.log_line) & smask] + q] = k;
+    wave_sync();
+    if (!more) break;
+    i = inext;
+    c = cn;
   }
 }
 
 size_t scatter_lds_bytes(const gg_geom& g) { return (size_t)kChunk * 8 + (size_t)g.u1 * (8 + 4 + 4); }
 
-// Pass 5: program-order results.  result[i] = sh_res[rec_slot[i]]; the reads
-// of one workgroup fall in the per-set runs of one or two chunks (local).
+// Pass 5: program-order results.  result[i] = sh_res[rec_slot[i]]: each lane
+// takes 4 consecutive records (dwordx4 slot load and result store) and issues
+// its 4 gathers together; 4 such groups per lane are in flight per iteration.
+// The gathers of one workgroup fall in the per-set runs of a few chunks.
+constexpr uint32_t kUnshardPer = 16;                   // records per lane per iteration
 __global__ __launch_bounds__(256) void k_unshard(const uint32_t* __restrict__ rec_slot,
     const uint32_t* __restrict__ sh_res, const uint64_t* __restrict__ sh_ev, uint32_t* __restrict__ result,
     uint64_t* __restrict__ evicted, uint64_t n)
 {
-  const uint64_t nb = (n + 1023) / 1024;
-  for (uint64_t b = xcd_chunk(blockIdx.x, gridDim.x); b < nb; b += gridDim.x) {
-    const uint64_t i0 = b * 1024 + threadIdx.x;
-    uint32_t sl[4];
+  constexpr uint32_t G = kUnshardPer / 4;
+  const uint64_t per_block = 256ull * kUnshardPer;
+  const uint64_t nb = (n + per_block - 1) / per_block;
+  const bool vec = (((uintptr_t)result | (uintptr_t)evicted) & 15) == 0;
+  for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    const uint64_t base = b * per_block;
+    if (vec && base + per_block <= n) {
+      uint4 sl[G];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) sl[k] = (i0 + 256 * k < n) ? rec_slot[i0 + 256 * k] : 0u;
-    if (result) {
-      uint32_t r[4];
+      for (uint32_t k = 0; k < G; ++k)
+        sl[k] = *reinterpret_cast<const uint4*>(rec_slot + base + (k * 256 + threadIdx.x) * 4);
+      if (result) {
+        uint4 r[G];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) r[k] = (i0 + 256 * k < n) ? sh_res[sl[k]] : 0u;
+        for (uint32_t k = 0; k < G; ++k)
+          r[k] = make_uint4(sh_res[sl[k].x], sh_res[sl[k].y], sh_res[sl[k].z], sh_res[sl[k].w]);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) if (i0 + 256 * k < n) result[i0 + 256 * k] = r[k];
-    }
-    if (evicted) {
-      uint64_t e[4];
+        for (uint32_t k = 0; k < G; ++k)
+          *reinterpret_cast<uint4*>(result + base + (k * 256 + threadIdx.x) * 4) = r[k];
+      }
+      if (evicted) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) e[k] = (i0 + 256 * k < n) ? sh_ev[sl[k]] : 0ull;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) if (i0 + 256 * k < n) evicted[i0 + 256 * k] = e[k];
+        for (uint32_t k = 0; k < G; ++k) {
+          const uint64_t i = base + (k * 256 + threadIdx.x) * 4;
+          const uint64_t e0 = sh_ev[sl[k].x], e1 = sh_ev[sl[k].y], e2 = sh_ev[sl[k].z], e3 = sh_ev[sl[k].w];
+          reinterpret_cast<uint4*>(evicted + i)[0] = make_uint4((uint32_t)e0, (uint32_t)(e0 >> 32), (uint32_t)e1, (uint32_t)(e1 >> 32));
+          reinterpret_cast<uint4*>(evicted + i)[1] = make_uint4((uint32_t)e2, (uint32_t)(e2 >> 32), (uint32_t)e3, (uint32_t)(e3 >> 32));
+        }
+      }
+    } else {
+      for (uint64_t i = base + threadIdx.x; i < min(n, base + per_block); i += 256) {
+        const uint32_t sl = rec_slot[i];
+        if (result) result[i] = sh_res[sl];
+        if (evicted) evicted[i] = sh_ev[sl];
+      }
     }
   }
 }
@@ -1332,7 +1390,18 @@ gg_status gg_cache_run_batch(gg_ctx* ctx, const gg_trace* tr, uint32_t* result, 
   if (evicted) { if (gg_status st = grow(&ctx->sh_ev, &ctx->sh_ev_cap, total)) return st; }
   if (nchunks) {
     gg_timer_begin(ctx, "cache_scatter", s);
-    hipLaunchKernelGGL(k_shard_scatter, dim3((uint32_t)nchunks), dim3(64), scatter_lds_bytes(g), s, tr->addr_dev, tr->meta_dev,
+    // persistent (default): 8 one-wave workgroups per CU, a multiple of 8;
+    // GG_SCATTER_MODE=1 (A/B knob): one chunk per workgroup
+    static const int mode = getenv("GG_SCATTER_MODE") ? atoi(getenv("GG_SCATTER_MODE")) : 0;
+    const bool persist = mode != 1;
+    const uint32_t grid = persist ? (uint32_t)std::min<uint64_t>((nchunks + 7) & ~7ull, (uint64_t)ctx->num_cus * 8)
+                                  : (uint32_t)nchunks;
+    const uint32_t per = std::max<uint32_t>(1, g.u1 / GG_WAVE);
+    auto* fn = persist ? (per == 1 ? k_shard_scatter<1, true> : per == 2 ? k_shard_scatter<2, true> : per == 4 ? k_shard_scatter<4, true>
+                          : per == 8 ? k_shard_scatter<8, true> : k_shard_scatter<16, true>)
+                       : (per == 1 ? k_shard_scatter<1, false> : per == 2 ? k_shard_scatter<2, false> : per == 4 ? k_shard_scatter<4, false>
+                          : per == 8 ? k_shard_scatter<8, false> : k_shard_scatter<16, false>);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(64), scatter_lds_bytes(g), s, tr->addr_dev, tr->meta_dev,
                        ctx->chunk_tile, ctx->chunk_start, ctx->chunk_len, ctx->chunk_cnt, ctx->unit_base,
                        ctx->sh_key, ctx->rec_slot, g, (uint32_t)nchunks);
     GG_HIP(hipGetLastError());
@@ -1348,8 +1417,8 @@ gg_status gg_cache_run_batch(gg_ctx* ctx, const gg_trace* tr, uint32_t* result, 
   GG_HIP(hipGetLastError());
   gg_timer_end(ctx, "cache_replay", s);
   if (n && (result || evicted)) {
-    const uint64_t nb = (n + 1023) / 1024;
-    const uint32_t grid = (uint32_t)std::min<uint64_t>(nb, 256ull * 64);
+    const uint64_t nb = (n + 256 * kUnshardPer - 1) / (256 * kUnshardPer);
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(nb, 256ull * 16);
     gg_timer_begin(ctx, "cache_unshard", s);
     hipLaunchKernelGGL(k_unshard, dim3(grid), dim3(256), 0, s, (const uint32_t*)ctx->rec_slot,
                        (const uint32_t*)ctx->sh_res, (const uint64_t*)ctx->sh_ev, result, evicted, n);

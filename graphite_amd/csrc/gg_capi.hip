@@ -120,6 +120,8 @@ gg_ctx* gg_create(const gg_config* cfg, gg_status* status)
   gg_ctx* ctx = new gg_ctx();
   ctx->cfg = c;
   ctx->device = c.device;
+  if (hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, c.device) != hipSuccess || ctx->num_cus <= 0)
+    ctx->num_cus = 256;
   ctx->replay_variant = (int)c.replay_kernel;
   gg_geom& g = ctx->g;
   g.tiles = c.num_tiles;

@@ -69,6 +69,7 @@ struct gg_ctx {
   gg_config cfg;
   gg_geom g;
   int device = 0;
+  int num_cus = 256;
   hipStream_t last_stream = nullptr;
   gg_cache_state cs{};
   uint32_t* err_dev = nullptr;
