@@ -25,15 +25,14 @@ LOC_L1D = 3
 
 META_WRITE = 1
 
-RES_LEVEL_MASK = 0x3
-RES_L1_HIT = 0x0
-RES_L2_HIT = 0x1
-RES_DIRECTORY = 0x2
-RES_UPGRADE = 1 << 2
-RES_L1_EVICT = 1 << 3
-RES_L2_EVICT = 1 << 4
-RES_L2_EVICT_DIRTY = 1 << 5
-RES_L2_EVICT_INV_L1 = 1 << 6
+RES_L1_MISS = 1 << 0
+RES_L2_MISS = 1 << 4
+RES_L1_INVAL = 1 << 8
+RES_L1_EVICT = 1 << 12
+RES_L2_EVICT = 1 << 16
+RES_L2_EVICT_DIRTY = 1 << 20
+RES_L2_EVICT_INV_L1 = 1 << 24
+RES_UPGRADE = 1 << 28
 
 CACHE_COUNTERS = ["accesses", "misses", "read_accesses", "read_misses",
                   "write_accesses", "write_misses", "evictions", "dirty_evictions",

@@ -211,6 +211,21 @@ __global__ __launch_bounds__(1024) void k_unit_scan(const uint32_t* __restrict__
   for (uint64_t u = u0; u < u1; ++u) { unit_base[u] = base; base += (unit_len[u] + 7u) & ~7u; }
 }
 
+// Sharded record ("replay key"), built once by the scatter so the replay
+// decodes nothing wider than 32 bits:
+//   bits 63..32  L2 tag (line >> log2 L2 sets, < 2^32 by gg_geom::addr_limit)
+//   bits 16..25  L1-D set (line mod u1; used by the scatter's write-out only)
+//   bits  1..15  L2 set within the unit ((line >> log2 u1) mod S2)
+//   bit   0      WRITE
+__device__ __forceinline__ uint64_t replay_key(uint64_t a, uint32_t m, const gg_geom& g)
+{
+  const uint64_t line = a >> g.log_line;
+  const uint32_t lo = (m & GG_META_WRITE) | (((uint32_t)(line >> g.log_u1) & (g.s2 - 1)) << 1) |
+                      (((uint32_t)line & (g.u1 - 1)) << 16);
+  return ((uint64_t)(uint32_t)(line >> g.log_l2) << 32) | lo;
+}
+__device__ __forceinline__ uint32_t key_l1set(uint64_t k, uint32_t smask) { return ((uint32_t)k >> 16) & smask; }
+
 // Workgroup -> chunk map that gives each XCD a contiguous range of chunks.
 // Workgroups are dealt round-robin to the 8 XCDs (blockIdx % 8); mapping
 // XCD x to chunks [x*q + min(x,r), ...) keeps adjacent chunks of a tile on the
@@ -247,7 +262,6 @@ __global__ __launch_bounds__(64) void k_shard_scatter(const uint64_t* __restrict
   uint32_t* lcnt = reinterpret_cast<uint32_t*>(dbase + g.u1);             // [u1] count, then running rank
   uint32_t* loff = lcnt + g.u1;                                            // [u1] exclusive prefix
   const uint32_t lane = threadIdx.x, G = gridDim.x;
-  const uint64_t line_mask = ~((1ull << g.log_line) - 1);
   const uint32_t smask = g.u1 - 1;
   const uint64_t lt_mask = (1ull << lane) - 1;
   auto wave_sync = [] { __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); };
@@ -283,7 +297,7 @@ __global__ __launch_bounds__(64) void k_shard_scatter(const uint64_t* __restrict
     }
     uint64_t key[kPerLane];
 #pragma unroll
-    for (uint32_t k = 0; k < kPerLane; ++k) key[k] = (pa[k] & line_mask) | (pm[k] & GG_META_WRITE);
+    for (uint32_t k = 0; k < kPerLane; ++k) key[k] = replay_key(pa[k], pm[k], g);
     const uint32_t inext = i + G;
     const bool more = PERSIST && inext < nchunks;
     const uint32_t cn = more ? xcd_chunk(inext, nchunks) : c;
@@ -293,7 +307,7 @@ __global__ __launch_bounds__(64) void k_shard_scatter(const uint64_t* __restrict
     wave_sync();
 #pragma unroll
     for (uint32_t k = 0; k < kPerLane; ++k)
-      if (k * GG_WAVE + lane < len) atomicAdd(&lcnt[(uint32_t)(key[k] >> g.log_line) & smask], 1u);
+      if (k * GG_WAVE + lane < len) atomicAdd(&lcnt[key_l1set(key[k], smask)], 1u);
     wave_sync();
     // exclusive prefix of the per-set counts (lane-blocked + wave scan)
     {
@@ -316,7 +330,7 @@ __global__ __launch_bounds__(64) void k_shard_scatter(const uint64_t* __restrict
     for (uint32_t k = 0; k < kPerLane; ++k) {
       const uint32_t j = k * GG_WAVE + lane;
       const bool valid = j < len;
-      const uint32_t s = (uint32_t)(key[k] >> g.log_line) & smask;
+      const uint32_t s = key_l1set(key[k], smask);
       uint64_t peers = __ballot(valid);
       for (uint32_t b = 0; b < g.log_u1; ++b) {
         const bool bit = (s >> b) & 1u;
@@ -337,7 +351,7 @@ __global__ __launch_bounds__(64) void k_shard_scatter(const uint64_t* __restrict
     wave_sync();
     for (uint32_t q = lane; q < len; q += GG_WAVE) {
       const uint64_t k = skey[q];
-      sh_key[dbase[(uint32_t)(k >> g.log_line) & smask] + q] = k;
+      sh_key[dbase[key_l1set(k, smask)] + q] = k;
     }
     wave_sync();
     if (!more) break;
@@ -593,10 +607,10 @@ __global__ __launch_bounds__(64) void k_cache_replay(gg_cache_state cs, gg_geom 
     kr[PD - 1] = more ? sh_key[base + j + PD] : 0;
     if (!live) continue;
 
-    const uint64_t line = key >> g.log_line;
     const bool wr = (key & 1u) != 0;
-    const uint32_t s = (uint32_t)((line >> g.log_u1) & lmask);
-    const uint32_t tag2 = (uint32_t)(line >> g.log_l2);
+    const uint32_t s = ((uint32_t)key >> 1) & (uint32_t)lmask;
+    const uint32_t tag2 = (uint32_t)(key >> 32);
+    const uint64_t line = ((uint64_t)tag2 << g.log_l2) | ((uint64_t)s << g.log_u1) | l1set;
 
     // -- L2 set s (one LDS round trip) --
     uint32_t tg[TQ * 4];
@@ -698,7 +712,7 @@ __global__ __launch_bounds__(64) void k_cache_replay(gg_cache_state cs, gg_geom 
     cnt[I_WR] += wr; cnt[I_NH1] += !hit1; cnt[I_NH1W] += (!hit1 && wr); cnt[I_M2] += miss2;
     cnt[I_M2W] += (miss2 && wr); cnt[I_W1V] += w1v; cnt[I_L1EV] += l1ev; cnt[I_L2EV] += l2ev;
     cnt[I_DIRTY] += dirty; cnt[I_INVL1] += invl1; cnt[I_UPG] += upg;
-    const uint32_t res = (hit1 ? GG_RES_L1_HIT : (hit2 ? GG_RES_L2_HIT : GG_RES_DIRECTORY)) |
+    const uint32_t res = (hit1 ? 0u : GG_RES_L1_MISS) | (miss2 ? GG_RES_L2_MISS : 0u) | (w1v ? GG_RES_L1_INVAL : 0u) |
                          (upg ? GG_RES_UPGRADE : 0u) | (l1ev ? GG_RES_L1_EVICT : 0u) |
                          (l2ev ? GG_RES_L2_EVICT : 0u) | (dirty ? GG_RES_L2_EVICT_DIRTY : 0u) |
                          (invl1 ? GG_RES_L2_EVICT_INV_L1 : 0u);
@@ -744,12 +758,18 @@ __global__ __launch_bounds__(64) void k_cache_replay(gg_cache_state cs, gg_geom 
 // Lean replay for the reference geometries (L1-D assoc <= 4, L2 assoc <= 8).
 // Same semantics as k_cache_replay; per-unit state re-packed for fewer
 // instructions per access:
-//   L1-D: t1[] line numbers (stale when the way is invalid), st1 = 2-bit
-//         states, a1 = 4-bit LRU ages, pos1 = per-way byte "L2 slot"
-//         (s * A2 + way of the line's L2 copy; 0xFF = none).  The slot code
-//         turns "does the L1-D hold the L2 victim" into one SWAR byte match.
+//   L1-D: no tags.  The private L1-D is inclusive in the L2 (every L1-D line
+//         has its L2 copy, cached_loc invariant above), so an L1-D way is
+//         named by the L2 slot of its line: pos1 = per-way byte s * A2 + way
+//         (0xFF = invalid way).  "Does the L1-D hold the line" and "does the
+//         L1-D hold the L2 victim" are one SWAR byte match each; tags are
+//         rebuilt from the L2 at exit.  st1 = 2-bit states, a1 = 4-bit ages.
 //   L2:   tags [s][lane][4*TQ] u32 in LDS (canonical: ~0 = invalid, updated by
 //         predicated ds_write_b32), meta [s][lane] = {ages u32, states u16 | rr}.
+//   Counters: the result word has one flag per 4-bit field, so the 8 result
+//         words of a block are summed field-wise (3 add3) and folded into
+//         byte-wide accumulators (flushed every 31 blocks) instead of 11
+//         per-access counter increments.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t zero_nibbles(uint32_t x)
 {
@@ -788,7 +808,6 @@ __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_
 {
   static_assert(A1 <= 4 && A2 <= 8, "lean replay covers L1-D assoc <= 4, L2 assoc <= 8");
   constexpr int TQ = (A2 + 3) / 4;
-  constexpr int MW = 1;                            // HBM meta words per L2 set (A2 <= 8)
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t lane = threadIdx.x;
   const uint64_t u = (uint64_t)blockIdx.x * GG_WAVE + lane;
@@ -803,8 +822,8 @@ __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_
   auto tptr = [&](uint32_t s) -> uint32_t* { return T + ((size_t)s * GG_WAVE + lane) * (4 * TQ); };
 
   // ---- load + re-pack state ----
-  uint64_t t1[A1];
   uint32_t st1 = 0, a1 = 0xFFFFFFFFu, pos1 = 0xFFFFFFFFu;
+  uint64_t t1[A1];
   {
     const uint64_t m1 = cs.l1_meta[uu];
 #pragma unroll
@@ -824,7 +843,7 @@ __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_
 #pragma unroll
     for (int w = 0; w < 4 * TQ; ++w)
       tg[w] = (w < A2) ? cs.l2_tag[(uint64_t)(s * A2 + w) * g.units + uu] : GG_L2_INV_TAG;
-    const uint64_t mw = cs.l2_meta[(uint64_t)(s * MW) * g.units + uu];
+    const uint64_t mw = cs.l2_meta[(uint64_t)s * g.units + uu];
     uint32_t ages = 0xFFFFFFFFu, st = 0;
 #pragma unroll
     for (int w = 0; w < A2; ++w) {
@@ -863,19 +882,14 @@ __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_
   uint32_t maxlen = len;
   for (int o = 32; o > 0; o >>= 1) maxlen = max(maxlen, (uint32_t)__shfl_xor((int)maxlen, o));
 
-  uint32_t cnt[NI];
-#pragma unroll
-  for (int k = 0; k < NI; ++k) cnt[k] = 0;
-  const uint32_t s2m = S2 - 1;
+  const uint32_t log_s2 = (uint32_t)__builtin_ctz(S2);
   const uint32_t log_line = g.log_line, log_u1 = g.log_u1, log_l2 = g.log_l2;
 
   // One access of this lane's unit (the body of processMemOpFromCore); returns
   // the result word, and the evicted L2 line address through *ev.
-  auto step = [&](const uint64_t key, uint64_t* ev) -> uint32_t {
-    const uint64_t line = key >> log_line;
-    const uint32_t wr = (uint32_t)key & 1u;
-    const uint32_t s = (uint32_t)(line >> log_u1) & s2m;
-    const uint32_t tag2 = (uint32_t)(line >> log_l2);
+  auto step = [&](const uint32_t klo, const uint32_t tag2, uint64_t* ev) -> uint32_t {
+    const uint32_t wr = klo & 1u;
+    const uint32_t s = __builtin_amdgcn_ubfe(klo, 1, log_s2);
     uint32_t* tp = tptr(s);
     uint32_t tg[4 * TQ];
 #pragma unroll
@@ -886,30 +900,28 @@ __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_
     const uint2 mt = Mt[s * GG_WAVE + lane];
     uint32_t ages2 = mt.x, st2 = mt.y & 0xFFFFu, rr2 = (mt.y >> 16) & 0xFFu;
 
-    // L1-D lookup among valid ways (operationPermissibleinL1Cache)
-    uint32_t mm = 0;
+    // L2 lookup (processShmemRequestFromL1Cache): valid tags are unique in a
+    // set and the invalid tag never matches, so at most one way hits
+    uint32_t mm2 = 0;
 #pragma unroll
-    for (int w = 0; w < A1; ++w) mm |= (t1[w] == line) ? (1u << (2 * w)) : 0u;
-    mm &= (st1 | (st1 >> 1)) & 0x55u;
-    const int w1 = mm ? (int)(__builtin_ctz(mm) >> 1) : -1;
-    const uint32_t s1 = (st1 >> ((2 * w1) & 31)) & 3u;                // 0 when w1 < 0
+    for (int w = 0; w < A2; ++w) mm2 |= (tg[w] == tag2) ? (1u << w) : 0u;
+    const uint32_t w2 = (uint32_t)__builtin_ctz(mm2 | (1u << A2));     // A2 when absent
+    const uint32_t s2 = (st2 >> (2 * w2)) & 3u;                        // 0 when absent
+    // L1-D lookup (operationPermissibleinL1Cache): the L1-D holds the line
+    // iff one of its ways names the line's L2 slot
+    const uint32_t zb1 = mm2 ? zero_bytes32(pos1 ^ ((s * A2 + w2) * 0x01010101u)) : 0u;
+    const uint32_t w1 = (uint32_t)__builtin_ctz(zb1 | 0x80000000u) >> 3;
+    const uint32_t s1 = zb1 ? (st1 >> (2 * w1)) & 3u : 0u;
     const bool hit1 = s1 > wr;                                         // READ: readable, WRITE: writable
-    // L2 lookup (processShmemRequestFromL1Cache)
-    int w2 = -1;
-#pragma unroll
-    for (int w = 0; w < A2; ++w) w2 = (tg[w] == tag2) ? w : w2;
-    const uint32_t s2 = (st2 >> ((2 * w2) & 31)) & 3u;
     const bool hit2n = s2 > wr;
     const bool hit2 = !hit1 && hit2n;
     const bool miss2 = !hit1 && !hit2n;
     const bool upg = miss2 && wr && s2 == GG_MS_S;
-    const bool w1v = !hit1 && w1 >= 0;
-    errv |= (hit1 && wr && w2 < 0) ? GG_DERR_STATE : 0u;
+    const bool w1v = !hit1 && zb1 != 0;
 
     // invalidate the L1-D copy before going to L2 (l1:135-137)
-    const uint32_t m1 = 3u << ((2 * w1) & 31);
-    st1 = w1v ? (st1 & ~m1) : st1;
-    pos1 = w1v ? (pos1 | (0xFFu << ((8 * w1) & 31))) : pos1;
+    st1 = w1v ? (st1 & ~(3u << (2 * w1))) : st1;
+    pos1 = w1v ? (pos1 | (0xFFu << (8 * w1))) : pos1;
     // upgrade: invalidate the SHARED L2 line (l2:260-282)
     if (upg) tp[w2] = GG_L2_INV_TAG;
     st2 = upg ? (st2 & ~(3u << (2 * w2))) : st2;
@@ -928,7 +940,7 @@ __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_
     // invalidateCacheLineInL1: does the L1-D hold L2 slot (s, v2)?
     const uint32_t zb = zero_bytes32(pos1 ^ ((s * A2 + v2) * 0x01010101u));
     const bool invl1 = l2ev && zb != 0;
-    const uint32_t we = zb ? (uint32_t)(__builtin_ctz(zb) >> 3) : 0u;
+    const uint32_t we = (uint32_t)__builtin_ctz(zb | 0x80000000u) >> 3;
     st1 = invl1 ? (st1 & ~(3u << (2 * we))) : st1;
     pos1 = invl1 ? (pos1 | (0xFFu << (8 * we))) : pos1;
     // install (EX_REP -> MODIFIED, SH_REP -> SHARED)
@@ -938,7 +950,7 @@ __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_
     if (!LRU2 && miss2) rr2 = rr2 ? rr2 - 1 : (A2 - 1);
     // L2 LRU: readCacheLine (hit2) / insert (miss2) / write-through (hit1 && wr)
     if (LRU2) {
-      const uint32_t x2 = miss2 ? (uint32_t)v2 : (uint32_t)(w2 & 7);
+      const uint32_t x2 = miss2 ? (uint32_t)v2 : (w2 & 7u);
       const uint32_t nb = lru_nib(ages2, x2);
       ages2 = (!hit1 || wr) ? nb : ages2;
     }
@@ -948,29 +960,40 @@ __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_
     v1 &= 3;
     const bool l1ev = !hit1 && ((st1 >> (2 * v1)) & 3u) != 0;
     const uint32_t ins = hit2 ? s2 : ns;
-#pragma unroll
-    for (int w = 0; w < A1; ++w) t1[w] = (!hit1 && w == v1) ? line : t1[w];
-    const uint32_t slot = s * A2 + (uint32_t)(hit2 ? (w2 & 7) : v2);
+    const uint32_t slot = s * A2 + (hit2 ? w2 : (uint32_t)v2);
     st1 = !hit1 ? ((st1 & ~(3u << (2 * v1))) | (ins << (2 * v1))) : st1;
     pos1 = !hit1 ? ((pos1 & ~(0xFFu << (8 * v1))) | (slot << (8 * v1))) : pos1;
     if (!LRU1 && !hit1) rr1 = rr1 ? rr1 - 1 : (A1 - 1);
     // L1-D LRU: accessCache on the hit way or the inserted way
-    if (LRU1) a1 = lru_nib(a1, hit1 ? (uint32_t)(w1 & 3) : (uint32_t)v1);
+    if (LRU1) a1 = lru_nib(a1, hit1 ? (w1 & 3u) : (uint32_t)v1);
 
     Mt[s * GG_WAVE + lane] = make_uint2(ages2, st2 | (rr2 << 16));
-
-    cnt[I_WR] += wr; cnt[I_NH1] += !hit1; cnt[I_NH1W] += (!hit1 && wr); cnt[I_M2] += miss2;
-    cnt[I_M2W] += (miss2 && wr); cnt[I_W1V] += w1v; cnt[I_L1EV] += l1ev; cnt[I_L2EV] += l2ev;
-    cnt[I_DIRTY] += dirty; cnt[I_INVL1] += invl1; cnt[I_UPG] += upg;
-    const uint32_t res = (hit1 ? GG_RES_L1_HIT : (hit2 ? GG_RES_L2_HIT : GG_RES_DIRECTORY)) |
-                         (upg ? GG_RES_UPGRADE : 0u) | (l1ev ? GG_RES_L1_EVICT : 0u) |
-                         (l2ev ? GG_RES_L2_EVICT : 0u) | (dirty ? GG_RES_L2_EVICT_DIRTY : 0u) |
-                         (invl1 ? GG_RES_L2_EVICT_INV_L1 : 0u);
     if (sh_ev) {
       const uint64_t e2 = ((uint64_t)vt << log_l2) | ((uint64_t)s << log_u1) | l1set;
       *ev = l2ev ? (e2 << log_line) : ~0ull;
     }
-    return res;
+    return (hit1 ? 0u : GG_RES_L1_MISS) | (miss2 ? GG_RES_L2_MISS : 0u) | (w1v ? GG_RES_L1_INVAL : 0u) |
+           (l1ev ? GG_RES_L1_EVICT : 0u) | (l2ev ? GG_RES_L2_EVICT : 0u) | (dirty ? GG_RES_L2_EVICT_DIRTY : 0u) |
+           (invl1 ? GG_RES_L2_EVICT_INV_L1 : 0u) | (upg ? GG_RES_UPGRADE : 0u);
+  };
+
+  // Counter fields, in result-word nibble order: 0 L1 miss, 1 L2 miss,
+  // 2 L1 inval, 3 L1 evict, 4 L2 evict, 5 dirty, 6 inv-L1, 7 upgrade.
+  uint32_t f8[8], fw[2], nwr = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) f8[k] = 0;
+  fw[0] = fw[1] = 0;
+  uint32_t acc_lo = 0, acc_hi = 0, acc_w = 0, nblk = 0;
+  auto flush = [&]() {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f8[2 * k] += (acc_lo >> (8 * k)) & 0xFFu;
+      f8[2 * k + 1] += (acc_hi >> (8 * k)) & 0xFFu;
+    }
+    fw[0] += acc_w & 0xFFFFu;
+    fw[1] += acc_w >> 16;
+    acc_lo = acc_hi = acc_w = 0;
+    nblk = 0;
   };
 
   // The unit's records are contiguous from `base` (8-record aligned): stream
@@ -993,18 +1016,19 @@ __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_
 #pragma unroll
       for (int q = 0; q < KB / 2; ++q) nkb[q] = kp[(j0 + KB) / 2 + q];
     }
-    if (j0 < len) {
-      uint32_t rv[KB];
-      uint64_t ev[KB];
+    uint32_t rv[KB], wm[KB];
+    uint64_t ev[KB];
 #pragma unroll
-      for (int d = 0; d < KB; ++d) {
-        rv[d] = 0; ev[d] = ~0ull;
-        if (j0 + d < len) {
-          const uint4 kv = kb[d / 2];
-          const uint64_t key = (d & 1) ? (((uint64_t)kv.w << 32) | kv.z) : (((uint64_t)kv.y << 32) | kv.x);
-          rv[d] = step(key, &ev[d]);
-        }
+    for (int d = 0; d < KB; ++d) {
+      rv[d] = 0; wm[d] = 0; ev[d] = ~0ull;
+      if (j0 + d < len) {
+        const uint4 kv = kb[d / 2];
+        const uint32_t klo = (d & 1) ? kv.z : kv.x, tag2 = (d & 1) ? kv.w : kv.y;
+        rv[d] = step(klo, tag2, &ev[d]);
+        wm[d] = klo & 1u;
       }
+    }
+    if (j0 < len) {
       if (sh_res) {
         rp[j0 / 4] = make_uint4(rv[0], rv[1], rv[2], rv[3]);
         rp[j0 / 4 + 1] = make_uint4(rv[4], rv[5], rv[6], rv[7]);
@@ -1016,11 +1040,22 @@ __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_
                                       (uint32_t)ev[2 * q + 1], (uint32_t)(ev[2 * q + 1] >> 32));
       }
     }
+    // field-wise sums of the block's result words (each field <= 8)
+    const uint32_t sum = rv[0] + rv[1] + rv[2] + rv[3] + rv[4] + rv[5] + rv[6] + rv[7];
+    uint32_t sw = 0, nw = 0;
+#pragma unroll
+    for (int d = 0; d < KB; ++d) { sw += rv[d] & (wm[d] * 0x11u); nw += wm[d]; }
+    acc_lo += sum & 0x0F0F0F0Fu;
+    acc_hi += (sum >> 4) & 0x0F0F0F0Fu;
+    acc_w += (sw & 0xFu) | ((sw & 0xF0u) << 12);
+    nwr += nw;
+    if (++nblk == 31) flush();
     if (more) {
 #pragma unroll
       for (int q = 0; q < KB / 2; ++q) kb[q] = nkb[q];
     }
   }
+  flush();
 
   // ---- store state back in the HBM format (canonical tags, byte meta, cached_loc) ----
   if (active) {
@@ -1029,7 +1064,13 @@ __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_
     for (int w = 0; w < 8; ++w) {
       if (w < A1) {
         const uint32_t st = (st1 >> (2 * w)) & 3u;
-        cs.l1_tag[(uint64_t)w * g.units + u] = st ? t1[w] : GG_L1_INV_TAG;
+        uint64_t tag1 = GG_L1_INV_TAG;
+        if (st) {                                     // rebuild the line from its L2 slot
+          const uint32_t slot = (pos1 >> (8 * w)) & 0xFFu;
+          const uint32_t ss = slot / A2, ww = slot % A2;
+          tag1 = ((uint64_t)tptr(ss)[ww] << g.log_l2) | ((uint64_t)ss << g.log_u1) | l1set;
+        }
+        cs.l1_tag[(uint64_t)w * g.units + u] = tag1;
         m1 |= (uint64_t)GG_M_MAKE(st, 0, (a1 >> (4 * w)) & 0xFu) << (8 * w);
       } else {
         m1 |= 0xF8ull << (8 * w);
@@ -1059,6 +1100,10 @@ __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_
   }
   if (!active) errv = 0;
   if (errv) atomicOr(err, errv);
+  uint32_t cnt[NI];
+  cnt[I_WR] = nwr; cnt[I_NH1] = f8[0]; cnt[I_NH1W] = fw[0]; cnt[I_M2] = f8[1]; cnt[I_M2W] = fw[1];
+  cnt[I_W1V] = f8[2]; cnt[I_L1EV] = f8[3]; cnt[I_L2EV] = f8[4]; cnt[I_DIRTY] = f8[5]; cnt[I_INVL1] = f8[6];
+  cnt[I_UPG] = f8[7];
   replay_counters(cs, g, cnt, len, tile, lane, active);
 }
 

@@ -84,7 +84,7 @@ int main(int argc, char** argv)
         for (size_t i = lo; i < hi; ++i)
           rep.accessSingleLine(t, (recs[t][i].second & GG_META_WRITE) != 0, recs[t][i].first);
       }
-      for (uint32_t r : rep.flush()) misses += (r & GG_RES_LEVEL_MASK) != GG_RES_L1_HIT;
+      for (uint32_t r : rep.flush()) misses += (r & GG_RES_L1_MISS) != 0;
     }
     rep.outputSummary(std::cout);
     std::cout << "L1-D misses reported per access: " << misses << std::endl;

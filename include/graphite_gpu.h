@@ -87,16 +87,18 @@ enum { GG_LOC_INVALID = 0, GG_LOC_L1I = 2, GG_LOC_L1D = 3 };
  *   bit 31     : reserved, must be 0                                           */
 #define GG_META_WRITE 1u
 
-/* Per-access result word written by gg_cache_access_batch.                    */
-#define GG_RES_LEVEL_MASK      0x3u  /* where the access was served:            */
-#define GG_RES_L1_HIT          0x0u  /*   L1-D (operationPermissibleinL1Cache)  */
-#define GG_RES_L2_HIT          0x1u  /*   L2 hit (processShmemRequestFromL1Cache) */
-#define GG_RES_DIRECTORY       0x2u  /*   L2 miss -> SH_REQ/EX_REQ to the home  */
-#define GG_RES_UPGRADE         (1u << 2) /* WRITE to a SHARED L2 line: INV_REP + EX_REQ (l2:260-282) */
-#define GG_RES_L1_EVICT        (1u << 3) /* the L1-D insert evicted a line      */
-#define GG_RES_L2_EVICT        (1u << 4) /* the L2 insert evicted a line (l2:74-116) */
-#define GG_RES_L2_EVICT_DIRTY  (1u << 5) /* ... in MODIFIED: FLUSH_REP + data (else INV_REP) */
-#define GG_RES_L2_EVICT_INV_L1 (1u << 6) /* ... and invalidated its copy in L1-D */
+/* Per-access result word written by gg_cache_access_batch: one flag per 4-bit
+ * field, so result words of up to 15 accesses can be summed field-wise (the
+ * replay kernel derives its counters that way).  Where the access was served:
+ * L1-D hit = !L1_MISS; L2 hit = L1_MISS && !L2_MISS; directory = L2_MISS.   */
+#define GG_RES_L1_MISS         (1u << 0)  /* not an L1-D hit (operationPermissibleinL1Cache, l1:207-243): request to the L2 */
+#define GG_RES_L2_MISS         (1u << 4)  /* not an L2 hit either (l2:180-224): SH_REQ / EX_REQ to the home directory */
+#define GG_RES_L1_INVAL        (1u << 8)  /* the L1-D held the line without the needed permission: invalidated first (l1:135-137) */
+#define GG_RES_L1_EVICT        (1u << 12) /* the L1-D insert evicted a line (insertCacheLineInL1, l2:133-165) */
+#define GG_RES_L2_EVICT        (1u << 16) /* the L2 insert evicted a line (l2:74-116) */
+#define GG_RES_L2_EVICT_DIRTY  (1u << 20) /* ... in MODIFIED: FLUSH_REP + data (else INV_REP) */
+#define GG_RES_L2_EVICT_INV_L1 (1u << 24) /* ... and invalidated its copy in L1-D (invalidateCacheLineInL1, l2:124-131) */
+#define GG_RES_UPGRADE         (1u << 28) /* WRITE to a SHARED L2 line: INV_REP + EX_REQ (l2:260-282) */
 
 /* Cache counters, one vector per (tile, level).  Index = what Cache::outputSummary prints. */
 enum {

@@ -322,8 +322,9 @@ static uint32_t modep_access(o_tile* T, uint64_t addr, int is_write, uint64_t* e
     if (access_num == 1) o_update_miss_counters(&T->l1, is_write, !hit);
     if (hit) { l1_access_cache(T, addr, is_write, err); return res; }
     if (access_num == 2) { *err = 1; return res; }   /* LOG_ASSERT_ERROR(access_num == 1 || 2) */
+    res |= GG_RES_L1_MISS;
 
-    l1_invalidate(T, addr, err);                       /* l1:135-137 */
+    if (l1_invalidate(T, addr, err)) res |= GG_RES_L1_INVAL;   /* l1:135-137 */
 
     /* L2CacheCntlr::processShmemRequestFromL1Cache (l2:180-224) */
     o_line l2i = o_default_line();
@@ -332,7 +333,6 @@ static uint32_t modep_access(o_tile* T, uint64_t addr, int is_write, uint64_t* e
     int l2hit = is_write ? cs_writable(cstate) : cs_readable(cstate);  /* l2:504-527 */
     o_update_miss_counters(&T->l2, is_write, !l2hit);
     if (l2hit) {
-      res |= GG_RES_L2_HIT;
       if (o_access_line(&T->l2, addr, 0)) *err = 1;   /* readCacheLine */
       l2_insert_in_l1(T, addr, cstate, &res, err);
       l2i.loc = GG_LOC_L1D;                          /* setCachedLoc / setForcedCachedLoc */
@@ -342,7 +342,7 @@ static uint32_t modep_access(o_tile* T, uint64_t addr, int is_write, uint64_t* e
     }
 
     /* L2 miss: handleMsgFromL1Cache (l2:226-258) */
-    res |= GG_RES_DIRECTORY;
+    res |= GG_RES_L2_MISS;
     uint32_t new_state;
     if (is_write) {                                  /* processExReqFromL1Cache (l2:260-282) */
       o_line x = o_default_line();

@@ -6,7 +6,7 @@ import pytest
 from graphite_amd import config as C
 from graphite_amd import backend as B
 from oracle import pyoracle as po
-from golden_util import manifest, load, POLICY
+from golden_util import manifest, load, POLICY, compact_code
 from gpu_util import torch_dev, to_dev, to_np
 from test_oracle_golden import modep_trace, modep_config
 
@@ -50,7 +50,7 @@ def test_replay_matches_reference_fixtures(name, chunks, kern):
     cfg = modep_config(e)
     cfg.replay_kernel = kern
     be, res, ev = run_gpu(cfg, addr, meta, offs, torch, chunks=chunks)
-    np.testing.assert_array_equal(res.astype(np.uint8), load(e["result_file"], np.uint8))
+    np.testing.assert_array_equal(compact_code(res), load(e["result_file"], np.uint8))
     cnt = load(e["counters_file"], np.uint64).reshape(e["tiles"], 2, C.NUM_CACHE_COUNTERS)
     np.testing.assert_array_equal(be.cache_counters(), cnt)
     for t in range(e["tiles"]):
@@ -167,6 +167,7 @@ def test_full_size_config2_subset_and_properties():
     assert np.all(l2[:, 0] == l1[:, 1])                            # L1-D misses go to L2
     assert np.all(l1[:, 2] + l1[:, 4] == l1[:, 0])
     r = to_np(res, np.uint32)
-    assert int(((r & 3) == 2).sum()) == int(l2[:, 1].sum())        # directory requests = L2 misses
+    assert int(((r & C.RES_L2_MISS) != 0).sum()) == int(l2[:, 1].sum())   # directory requests = L2 misses
+    assert int(((r & C.RES_L1_MISS) != 0).sum()) == int(l1[:, 1].sum())
     assert int(((r & C.RES_L2_EVICT) != 0).sum()) == int(l2[:, 6].sum())
     assert int(((r & C.RES_L2_EVICT_DIRTY) != 0).sum()) == int(l2[:, 7].sum())
