@@ -16,8 +16,8 @@ import sys
 
 
 def short(name):
-    n = name.split("(")[0]
-    return n.replace("void ", "").replace("(anonymous namespace)::", "").strip()
+    n = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    return n.split("(")[0].strip()
 
 
 def main():
