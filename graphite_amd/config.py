@@ -43,6 +43,21 @@ NET_COUNTERS = ["packets_sent", "flits_sent", "bits_sent", "packets_received",
                 "switch_alloc", "crossbar", "link_traversals",
                 "router_contention_cycles", "router_packets", "analytical_requests"]
 NUM_CACHE_COUNTERS = len(CACHE_COUNTERS)
+
+# coherent mode (include/graphite_gpu.h)
+MSG_TYPES = ["EX_REQ", "SH_REQ", "INV_REQ", "FLUSH_REQ", "WB_REQ", "EX_REP", "SH_REP",
+             "UPGRADE_REP", "INV_REP", "FLUSH_REP", "WB_REP"]
+MSG = {n: i + 1 for i, n in enumerate(MSG_TYPES)}
+LVL_L1, LVL_L2, LVL_DIR = 0, 1, 2
+TILE_STATS = ["clock_ps", "accesses", "l1_hits", "l2_hits", "l2_misses", "latency_ps",
+              "dir_accesses", "dir_evictions", "dir_back_invalidations",
+              "dram_accesses", "dram_latency_ns", "dram_queue_delay_ns",
+              "dram_queue_requests", "dram_queue_analytical", "msgs_sent", "msgs_received"] + \
+             ["sent_" + n.lower() for n in MSG_TYPES]
+NUM_TILE_STATS = 32
+RUN_INFO = ["quanta", "steps", "net_msgs", "self_msgs", "boundary_msgs", "final_quantum"]
+NUM_RUN_INFO = 8
+CMSG_DTYPE = None  # filled below (numpy view of gg_cmsg)
 NUM_NET_COUNTERS = len(NET_COUNTERS)
 
 
@@ -67,7 +82,21 @@ class GGConfig(ctypes.Structure):
         ("frequency_ghz", ctypes.c_double),
         ("device", ctypes.c_int32),
         ("replay_kernel", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32 * 6),
+        ("l1d_data_cycles", ctypes.c_uint32),
+        ("l1d_tags_cycles", ctypes.c_uint32),
+        ("l2_data_cycles", ctypes.c_uint32),
+        ("l2_tags_cycles", ctypes.c_uint32),
+        ("dir_assoc", ctypes.c_uint32),
+        ("dir_total_entries", ctypes.c_uint32),
+        ("dir_access_cycles", ctypes.c_uint32),
+        ("dram_latency_ns", ctypes.c_uint32),
+        ("dram_bandwidth", ctypes.c_float),
+        ("dram_queue_model_enabled", ctypes.c_uint32),
+        ("quantum_ns", ctypes.c_uint32),
+        ("num_shards", ctypes.c_uint32),
+        ("shard_begin", ctypes.c_uint32),
+        ("shard_end", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32 * 4),
     ]
 
 
@@ -89,6 +118,14 @@ def default_config(num_tiles, **overrides):
     c.frequency_ghz = 1.0
     c.device = 0
     c.replay_kernel = 0
+    # coherent mode (carbon_sim.cfg:97, 219-273)
+    c.l1d_data_cycles, c.l1d_tags_cycles = 1, 1
+    c.l2_data_cycles, c.l2_tags_cycles = 8, 3
+    c.dir_assoc, c.dir_total_entries, c.dir_access_cycles = 16, 0, 0
+    c.dram_latency_ns, c.dram_bandwidth, c.dram_queue_model_enabled = 100, 5.0, 1
+    c.quantum_ns = 1000
+    c.num_shards = 1
+    c.shard_begin, c.shard_end = 0, 0
     for k, v in overrides.items():
         if not hasattr(c, k):
             raise KeyError(k)
@@ -106,3 +143,18 @@ def shmem_modeled_bits(num_tiles, with_data):
     (network_model.cc:185-200) + 4 msg-type + 48 address bits (+ 64 B of data)
     (pr_l1_pr_l2_dram_directory_msi/shmem_msg.cc:100-125, shmem_msg.h:81)."""
     return 2 * tile_id_bits(num_tiles) + 4 + 48 + (512 if with_data else 0)
+
+
+def _cmsg_dtype():
+    import numpy as np
+    return np.dtype([("addr", "<u8"), ("send_ps", "<u8"), ("arrival_ps", "<u8"), ("src", "<u4"),
+                     ("dst", "<u4"), ("requester", "<u4"), ("seq", "<u4"), ("type", "<u4"),
+                     ("link", "<u4")])
+
+
+CMSG_DTYPE = _cmsg_dtype()
+
+
+def shard_of_tile(tile, num_tiles, num_shards):
+    """Logical shard of a tile: contiguous tile ranges."""
+    return (tile * num_shards) // num_tiles

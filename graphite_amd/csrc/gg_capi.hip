@@ -87,6 +87,12 @@ void gg_config_default(gg_config* c, uint32_t num_tiles)
   c->analytical_enabled = 1;
   c->frequency_ghz = 1.0;
   c->device = 0;
+  c->l1d_data_cycles = 1; c->l1d_tags_cycles = 1;       /* carbon_sim.cfg:219-228 */
+  c->l2_data_cycles = 8; c->l2_tags_cycles = 3;         /* carbon_sim.cfg:230-239 */
+  c->dir_assoc = 16; c->dir_total_entries = 0; c->dir_access_cycles = 0;   /* :253-258 ("auto") */
+  c->dram_latency_ns = 100; c->dram_bandwidth = 5.0f; c->dram_queue_model_enabled = 1;  /* :265-273 */
+  c->quantum_ns = 1000;                                 /* :97 */
+  c->num_shards = 1;
 }
 
 gg_ctx* gg_create(const gg_config* cfg, gg_status* status)

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define GG_ABI_VERSION 1
+#define GG_ABI_VERSION 2
 
 typedef int gg_status;
 enum {
@@ -141,7 +141,22 @@ typedef struct gg_config {
   double   frequency_ghz;      /* single DVFS domain (carbon_sim.cfg:147-155)        */
   int32_t  device;             /* HIP device ordinal                                 */
   uint32_t replay_kernel;      /* 0 = fastest instantiated replay kernel, 1 = generic */
-  uint32_t reserved[6];
+  /* ---- coherent mode (pr_l1_pr_l2_dram_directory_msi with directory, DRAM, NoC) ---- */
+  uint32_t l1d_data_cycles;    /* l1_dcache/T1/data_access_time (1)                 */
+  uint32_t l1d_tags_cycles;    /* l1_dcache/T1/tags_access_time (1)                 */
+  uint32_t l2_data_cycles;     /* l2_cache/T1/data_access_time (8)                  */
+  uint32_t l2_tags_cycles;     /* l2_cache/T1/tags_access_time (3)                  */
+  uint32_t dir_assoc;          /* dram_directory/associativity (16)                 */
+  uint32_t dir_total_entries;  /* dram_directory/total_entries, 0 = "auto"          */
+  uint32_t dir_access_cycles;  /* dram_directory/access_time, 0 = "auto"            */
+  uint32_t dram_latency_ns;    /* dram/latency (100)                                */
+  float    dram_bandwidth;     /* dram/per_controller_bandwidth, GB/s (5.0)         */
+  uint32_t dram_queue_model_enabled; /* dram/queue_model/enabled (history_tree)     */
+  uint32_t quantum_ns;         /* clock_skew_management/lax_barrier/quantum (1000)  */
+  uint32_t num_shards;         /* logical shards (canonical schedule); 0 = 1 */
+  uint32_t shard_begin;        /* shards owned by this context: [shard_begin, shard_end) */
+  uint32_t shard_end;          /* 0 = all                                            */
+  uint32_t reserved[4];
 } gg_config;
 
 /* Fill cfg with the reference defaults of carbon_sim.cfg for num_tiles tiles. */
@@ -183,6 +198,75 @@ typedef struct gg_line_info {    /* CacheLineInfo / PrL2CacheLineInfo           
   uint32_t cstate;               /* GG_CSTATE_*                                   */
   uint32_t cached_loc;           /* GG_LOC_* (L2 only)                            */
 } gg_line_info;
+
+/* ------------------------------------------------------------------------
+ * Coherent mode ("Mode C"): the full pr_l1_pr_l2_dram_directory_msi protocol —
+ * L1CacheCntlr / L2CacheCntlr (l1_cache_cntlr.cc, l2_cache_cntlr.cc),
+ * DramDirectoryCntlr with DirectoryCache + full-map entries
+ * (dram_directory_cntlr.cc, cache/directory_cache.cc,
+ * directory_schemes/directory_entry_full_map.cc), DramCntlr + DramPerfModel
+ * (dram_cntlr.cc, performance_models/dram_perf_model.cc), the ShmemPerfModel
+ * clock (performance_models/shmem_perf_model.cc), the memory network
+ * (NetworkModel::routePacket) and the lax-barrier quantum
+ * (clock_skew_management_schemes/lax_barrier_sync_*.cc) — driven in the
+ * canonical schedule of DESIGN.md §Mode C.
+ * ------------------------------------------------------------------------ */
+
+/* ShmemMsg::Type (pr_l1_pr_l2_dram_directory_msi/shmem_msg.h:12-30) */
+enum {
+  GG_MSG_EX_REQ = 1, GG_MSG_SH_REQ, GG_MSG_INV_REQ, GG_MSG_FLUSH_REQ, GG_MSG_WB_REQ,
+  GG_MSG_EX_REP, GG_MSG_SH_REP, GG_MSG_UPGRADE_REP, GG_MSG_INV_REP, GG_MSG_FLUSH_REP,
+  GG_MSG_WB_REP, GG_MSG_NULLIFY_REQ
+};
+
+/* One ShmemMsg in flight (48 bytes).  The per-sender sequence number keeps
+ * the per-channel FIFO order of the reference transports
+ * (socktransport.cc:225,366).                                                */
+typedef struct gg_cmsg {
+  uint64_t addr;         /* line byte address                                   */
+  uint64_t send_ps;      /* NetPacket::time when sent (MemoryManager::sendMsg)  */
+  uint64_t arrival_ps;   /* time handed to the receiver, after the network      */
+  uint32_t src, dst;     /* sender / receiver tile                              */
+  uint32_t requester;    /* ShmemMsg::_requester                                */
+  uint32_t seq;          /* per-sender sequence number                          */
+  uint32_t type;         /* GG_MSG_*                                            */
+  uint32_t link;         /* backend-private (ignored on import)                 */
+} gg_cmsg;
+
+/* Per-access output word of the coherent mode: (latency_ps << 2) | level,
+ * latency = Core::initiateMemoryAccess final - initial time (core.cc:245-251). */
+enum { GG_LVL_L1 = 0, GG_LVL_L2 = 1, GG_LVL_DIR = 2 };
+
+/* Per-tile statistics of the coherent mode, [tile][GG_NUM_TILE_STATS]. */
+enum {
+  GG_CT_CLOCK_PS = 0,        /* core clock after the tile's last access              */
+  GG_CT_ACCESSES, GG_CT_L1_HITS, GG_CT_L2_HITS, GG_CT_L2_MISSES, GG_CT_LATENCY_PS,
+  GG_CT_DIR_ACCESSES,        /* DirectoryCache::_total_directory_accesses (directory_cache.cc:97-100) */
+  GG_CT_DIR_EVICTIONS,       /* _total_evictions                                      */
+  GG_CT_DIR_BACK_INVALIDATIONS,
+  GG_CT_DRAM_ACCESSES,       /* DramPerfModel::m_num_accesses (dram_perf_model.cc:110)  */
+  GG_CT_DRAM_LATENCY_NS,     /* m_total_access_latency                                */
+  GG_CT_DRAM_QUEUE_DELAY_NS, /* m_total_queueing_delay                                */
+  GG_CT_DRAM_QUEUE_REQUESTS, /* QueueModel::_total_requests of the DRAM queue          */
+  GG_CT_DRAM_QUEUE_ANALYTICAL,
+  GG_CT_MSGS_SENT,           /* ShmemMsgs sent over the network (self-sends included)  */
+  GG_CT_MSGS_RECEIVED,
+  GG_CT_SENT_BY_TYPE,        /* + (type - 1), 11 entries                               */
+  GG_NUM_TILE_STATS = 32
+};
+
+/* Whole-run information, [GG_NUM_RUN_INFO]. */
+enum { GG_RI_QUANTA = 0, GG_RI_STEPS, GG_RI_NET_MSGS, GG_RI_SELF_MSGS, GG_RI_BOUNDARY_MSGS,
+       GG_RI_FINAL_QUANTUM, GG_NUM_RUN_INFO = 8 };
+
+/* Result of one quantum on the shards a context owns. */
+typedef struct gg_coherent_status {
+  uint64_t steps;           /* steps run                                                */
+  uint64_t boundary_msgs;   /* cross-shard messages waiting for the quantum boundary     */
+  uint64_t min_next_ps;     /* earliest next-access start of a gated owned tile, ~0 if none */
+  uint32_t active_tiles;    /* owned tiles whose trace is not finished                  */
+  uint32_t blocked_tiles;   /* owned tiles waiting for EX_REP / SH_REP                  */
+} gg_coherent_status;
 
 typedef struct gg_ctx gg_ctx;
 
@@ -236,6 +320,26 @@ gg_status gg_noc_get_counters(gg_ctx* ctx, uint64_t* out);
 gg_status gg_queue_delay_batch(gg_ctx* ctx, uint64_t min_processing_time,
                                const uint64_t* pkt_time, const uint64_t* proc_time,
                                uint64_t n, uint64_t* delay_out);
+
+/* Coherent mode.  gg_coherent_begin resets the coherent state and binds a
+ * tile-major trace of ALL tiles (meta bits 1..30 = gap cycles before the
+ * access); only the owned shards' tiles replay.  access_out_dev receives one
+ * word per record (GG_LVL_*), may be NULL.  gg_coherent_quantum runs quantum
+ * q (lax barrier at (q+1) * quantum_ns) on the owned shards until no owned
+ * tile can progress.  gg_coherent_export moves the cross-shard messages of the
+ * quantum into out_dev (device, grouped by destination shard, ascending;
+ * counts per shard into per_shard_counts, host, num_shards entries);
+ * gg_coherent_import delivers messages for owned tiles (device pointer).
+ * gg_coherent_run does the whole run on a context that owns every shard.   */
+gg_status gg_coherent_begin(gg_ctx* ctx, const gg_trace* trace, uint64_t* access_out_dev, void* stream);
+gg_status gg_coherent_quantum(gg_ctx* ctx, uint64_t q, gg_coherent_status* st);
+gg_status gg_coherent_export(gg_ctx* ctx, gg_cmsg* out_dev, uint64_t cap, uint64_t* per_shard_counts);
+gg_status gg_coherent_import(gg_ctx* ctx, const gg_cmsg* in_dev, uint64_t n);
+gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* trace, uint64_t* access_out_dev, void* stream);
+/* tile_stats: [tiles][GG_NUM_TILE_STATS]; cache: [tiles][2][GG_NUM_CACHE_COUNTERS]
+ * (either may be NULL); run_info: [GG_NUM_RUN_INFO] (may be NULL).  Tiles a
+ * context does not own read 0.  Network counters: gg_noc_get_counters.      */
+gg_status gg_coherent_get_stats(gg_ctx* ctx, uint64_t* tile_stats, uint64_t* cache, uint64_t* run_info);
 
 /* Synthetic workload generator (not part of the reference boundary; the
  * reference has no trace capture): fills a tile-major trace of

@@ -53,6 +53,30 @@ void oracle_gen_uniform(uint32_t tile, uint64_t first, uint64_t n, uint32_t line
   }
 }
 
+/* configs[2..4] hotspot generator: record i of tile t,
+ * z = SplitMix64(0x9E3779B97F4A7C15 ^ t) step first+i+1;
+ *   hot     iff ((z >> 40) & 0xFF) < hot_frac256  -> line (z & 0xFFFFFFFF) % hot_lines of the
+ *                                                   shared region at 1 << 44
+ *   private otherwise                            -> line z & (2^lines_log2 - 1) at t << base_shift
+ *   WRITE   iff ((z >> 32) & 0xFF) % 3 == 0
+ *   gap     = ctz(((z >> 48) & 0xFF) | 0x100) + ctz(((z >> 56) & 0xFF) | 0x100) cycles (mean ~2) */
+void oracle_gen_hotspot(uint32_t tile, uint64_t first, uint64_t n, uint32_t lines_log2,
+                        uint32_t base_shift, uint32_t hot_lines, uint32_t hot_frac256,
+                        uint64_t* addr, uint32_t* meta)
+{
+  const uint64_t seed = 0x9E3779B97F4A7C15ull ^ (uint64_t)tile;
+  const uint64_t mask = (1ull << lines_log2) - 1;
+  for (uint64_t k = 0; k < n; ++k) {
+    uint64_t z = oracle_splitmix64_at(seed, first + k);
+    int hot = hot_lines && (((z >> 40) & 0xFF) < hot_frac256);
+    if (hot) addr[k] = (1ull << 44) + ((z & 0xFFFFFFFFull) % hot_lines) * 64ull;
+    else addr[k] = ((uint64_t)tile << base_shift) + ((z & mask) << 6);
+    uint32_t gap = (uint32_t)__builtin_ctz((uint32_t)(((z >> 48) & 0xFF) | 0x100)) +
+                   (uint32_t)__builtin_ctz((uint32_t)(((z >> 56) & 0xFF) | 0x100));
+    meta[k] = ((((z >> 32) & 0xFF) % 3) == 0 ? GG_META_WRITE : 0u) | (gap << 1);
+  }
+}
+
 /* Core::initiateMemoryAccess line split (common/tile/core/core.cc:167-201) */
 uint32_t oracle_split_lines(uint64_t addr, uint32_t size, uint32_t line, uint64_t* lines, uint32_t cap)
 {
@@ -949,3 +973,4 @@ int oracle_noc_route(oracle_noc* on, uint64_t n, const uint32_t* src, const uint
   free(inj); free(cur);
   return 0;
 }
+#include "gg_coherent.inc"

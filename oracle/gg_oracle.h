@@ -33,6 +33,11 @@ void oracle_gen_uniform(uint32_t tile, uint64_t first, uint64_t n,
                         uint32_t lines_log2, uint32_t base_shift,
                         uint64_t* addr, uint32_t* meta);
 
+/* configs[2..4]: hotspot / shared-line trace with core-cycle gaps (meta bits 1..30). */
+void oracle_gen_hotspot(uint32_t tile, uint64_t first, uint64_t n, uint32_t lines_log2,
+                        uint32_t base_shift, uint32_t hot_lines, uint32_t hot_frac256,
+                        uint64_t* addr, uint32_t* meta);
+
 /* ---------------- private cache replay (mode P) ---------------------------- */
 typedef struct oracle_cache oracle_cache;
 oracle_cache* oracle_cache_create(const gg_config* cfg);
@@ -67,6 +72,26 @@ int  oracle_noc_route(oracle_noc* on, uint64_t n, const uint32_t* src, const uin
                       const uint32_t* length_bits, const uint64_t* time_ps,
                       uint64_t* arrival_ps, uint64_t* zero_load_ps, uint64_t* contention_ps);
 void oracle_noc_counters(const oracle_noc* on, uint64_t* out); /* [tile][GG_NUM_NET_COUNTERS] */
+
+/* ---------------- coherent mode (Mode C) ----------------
+ * pr_l1_pr_l2_dram_directory_msi with directory, DRAM, NoC and lax-barrier
+ * quanta in the canonical schedule (oracle/gg_coherent.inc).  The context
+ * owns shards [cfg.shard_begin, cfg.shard_end) of cfg.num_shards.          */
+typedef struct oracle_coh oracle_coh;
+oracle_coh* oracle_coh_create(const gg_config* cfg);
+void        oracle_coh_destroy(oracle_coh* C);
+int  oracle_coh_begin(oracle_coh* C, const uint64_t* addr, const uint32_t* meta,
+                      const uint64_t* tile_offsets, uint64_t* access_out);
+/* status: steps, held boundary messages, min next-access start, active tiles, blocked tiles */
+int  oracle_coh_quantum(oracle_coh* C, uint64_t q, uint64_t* status);
+uint64_t oracle_coh_export(oracle_coh* C, gg_cmsg* out, uint64_t cap);
+int  oracle_coh_import(oracle_coh* C, const gg_cmsg* in, uint64_t n);
+int  oracle_coh_run(oracle_coh* C, const uint64_t* addr, const uint32_t* meta,
+                    const uint64_t* tile_offsets, uint64_t* access_out);
+void oracle_coh_tile_stats(const oracle_coh* C, uint64_t* out);      /* [tile][GG_NUM_TILE_STATS] */
+void oracle_coh_cache_counters(const oracle_coh* C, uint64_t* out);  /* [tile][2][12] */
+void oracle_coh_net_counters(const oracle_coh* C, uint64_t* out);    /* [tile][GG_NUM_NET_COUNTERS] */
+void oracle_coh_run_info(const oracle_coh* C, uint64_t* out);        /* [GG_NUM_RUN_INFO] */
 
 /* Network::netSend line split of Core::initiateMemoryAccess (core.cc:167-201):
  * returns the number of line accesses [addr, addr+size) produces and writes

@@ -10,7 +10,8 @@ import subprocess
 
 import numpy as np
 
-from graphite_amd.config import GGConfig, NUM_CACHE_COUNTERS, NUM_NET_COUNTERS
+from graphite_amd.config import (GGConfig, NUM_CACHE_COUNTERS, NUM_NET_COUNTERS, NUM_TILE_STATS,
+                                 NUM_RUN_INFO, CMSG_DTYPE)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "liboracle.so")
@@ -66,6 +67,24 @@ def lib():
         L.oracle_noc_counters.argtypes = [vp, _u64p]
         L.oracle_split_lines.restype = ctypes.c_uint32
         L.oracle_split_lines.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _u64p, ctypes.c_uint32]
+        L.oracle_gen_hotspot.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                         ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u64p, _u32p]
+        L.oracle_coh_create.restype = vp
+        L.oracle_coh_create.argtypes = [ctypes.POINTER(GGConfig)]
+        L.oracle_coh_destroy.argtypes = [vp]
+        L.oracle_coh_begin.restype = ctypes.c_int
+        L.oracle_coh_begin.argtypes = [vp, _u64p, _u32p, _u64p, vp]
+        L.oracle_coh_quantum.restype = ctypes.c_int
+        L.oracle_coh_quantum.argtypes = [vp, ctypes.c_uint64, _u64p]
+        L.oracle_coh_export.restype = ctypes.c_uint64
+        L.oracle_coh_export.argtypes = [vp, vp, ctypes.c_uint64]
+        L.oracle_coh_import.restype = ctypes.c_int
+        L.oracle_coh_import.argtypes = [vp, vp, ctypes.c_uint64]
+        L.oracle_coh_run.restype = ctypes.c_int
+        L.oracle_coh_run.argtypes = [vp, _u64p, _u32p, _u64p, vp]
+        for n in ("oracle_coh_tile_stats", "oracle_coh_cache_counters", "oracle_coh_net_counters",
+                  "oracle_coh_run_info"):
+            getattr(L, n).argtypes = [vp, _u64p]
         _lib = L
     return _lib
 
@@ -79,6 +98,95 @@ def gen_uniform(tile, first, n, lines_log2=15, base_shift=26):
     meta = np.empty(n, np.uint32)
     lib().oracle_gen_uniform(tile, first, n, lines_log2, base_shift, addr, meta)
     return addr, meta
+
+
+def gen_hotspot(tile, first, n, lines_log2=15, base_shift=26, hot_lines=64, hot_frac256=51):
+    addr = np.empty(n, np.uint64)
+    meta = np.empty(n, np.uint32)
+    lib().oracle_gen_hotspot(tile, first, n, lines_log2, base_shift, hot_lines, hot_frac256, addr, meta)
+    return addr, meta
+
+
+def gen_trace(tiles, per_tile, **kw):
+    """Tile-major hotspot trace of `tiles` tiles x `per_tile` records + offsets."""
+    parts = [gen_hotspot(t, 0, per_tile, **kw) for t in range(tiles)]
+    addr = np.concatenate([p[0] for p in parts]) if parts else np.zeros(0, np.uint64)
+    meta = np.concatenate([p[1] for p in parts]) if parts else np.zeros(0, np.uint32)
+    offs = np.arange(tiles + 1, dtype=np.uint64) * np.uint64(per_tile)
+    return addr, meta, offs
+
+
+class OracleCoherent:
+    """Coherent (Mode C) run: MSI directory + DRAM + NoC + lax-barrier quanta,
+    canonical schedule (oracle/gg_coherent.inc)."""
+
+    def __init__(self, cfg):
+        self.cfg = cfg
+        self.h = lib().oracle_coh_create(ctypes.byref(cfg))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().oracle_coh_destroy(self.h)
+            self.h = None
+
+    def run(self, addr, meta, tile_offsets):
+        """Whole run (context owns every shard); returns the per-access words."""
+        self._keep = (np.ascontiguousarray(addr, np.uint64), np.ascontiguousarray(meta, np.uint32),
+                      np.ascontiguousarray(tile_offsets, np.uint64))
+        out = np.zeros(len(addr), np.uint64)
+        self._out = out
+        rc = lib().oracle_coh_run(self.h, *self._keep, out.ctypes.data)
+        if rc != 0:
+            raise RuntimeError("coherent oracle rc=%d (the reference would abort / deadlock)" % rc)
+        return out
+
+    # -- sharded (multi-rank) driving ------------------------------------
+    def begin(self, addr, meta, tile_offsets):
+        self._keep = (np.ascontiguousarray(addr, np.uint64), np.ascontiguousarray(meta, np.uint32),
+                      np.ascontiguousarray(tile_offsets, np.uint64))
+        self._out = np.zeros(len(addr), np.uint64)
+        rc = lib().oracle_coh_begin(self.h, *self._keep, self._out.ctypes.data)
+        if rc != 0:
+            raise RuntimeError("coherent oracle begin rc=%d" % rc)
+        return self._out
+
+    def quantum(self, q):
+        st = np.zeros(5, np.uint64)
+        rc = lib().oracle_coh_quantum(self.h, q, st)
+        if rc != 0:
+            raise RuntimeError("coherent oracle quantum rc=%d" % rc)
+        return {"steps": int(st[0]), "boundary_msgs": int(st[1]), "min_next_ps": int(st[2]),
+                "active_tiles": int(st[3]), "blocked_tiles": int(st[4])}
+
+    def export(self, cap):
+        buf = np.zeros(cap, CMSG_DTYPE)
+        n = lib().oracle_coh_export(self.h, buf.ctypes.data, cap)
+        if n == 0xFFFFFFFFFFFFFFFF:
+            raise RuntimeError("export buffer too small")
+        return buf[:n]
+
+    def import_(self, msgs):
+        msgs = np.ascontiguousarray(msgs, CMSG_DTYPE)
+        rc = lib().oracle_coh_import(self.h, msgs.ctypes.data, len(msgs))
+        if rc != 0:
+            raise RuntimeError("coherent oracle import rc=%d" % rc)
+
+    def _get(self, fn, shape):
+        out = np.zeros(int(np.prod(shape)), np.uint64)
+        getattr(lib(), fn)(self.h, out)
+        return out.reshape(shape)
+
+    def tile_stats(self):
+        return self._get("oracle_coh_tile_stats", (self.cfg.num_tiles, NUM_TILE_STATS))
+
+    def cache_counters(self):
+        return self._get("oracle_coh_cache_counters", (self.cfg.num_tiles, 2, NUM_CACHE_COUNTERS))
+
+    def net_counters(self):
+        return self._get("oracle_coh_net_counters", (self.cfg.num_tiles, NUM_NET_COUNTERS))
+
+    def run_info(self):
+        return self._get("oracle_coh_run_info", (NUM_RUN_INFO,))
 
 
 class OracleCache:
