@@ -10,7 +10,8 @@ import os
 
 import numpy as np
 
-from .config import GGConfig, NUM_CACHE_COUNTERS, NUM_NET_COUNTERS
+from .config import (GGConfig, NUM_CACHE_COUNTERS, NUM_NET_COUNTERS, NUM_TILE_STATS, NUM_RUN_INFO,
+                     CMSG_DTYPE)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libgraphite_gpu.so")
@@ -50,7 +51,14 @@ EXPORTS = ["gg_abi_version", "gg_last_error", "gg_config_default", "gg_create", 
            "gg_cache_access_batch", "gg_cache_get_counters", "gg_cache_get_line_info",
            "gg_cache_set_line_info", "gg_cache_access_line", "gg_cache_insert_line",
            "gg_noc_route_batch", "gg_noc_get_counters", "gg_queue_delay_batch",
-           "gg_gen_uniform_trace", "gg_kernel_time_ms", "gg_set_timing"]
+           "gg_gen_uniform_trace", "gg_kernel_time_ms", "gg_set_timing",
+           "gg_coherent_begin", "gg_coherent_quantum", "gg_coherent_export", "gg_coherent_import",
+           "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace"]
+
+
+class _CStatus(ctypes.Structure):
+    _fields_ = [("steps", ctypes.c_uint64), ("boundary_msgs", ctypes.c_uint64), ("min_next_ps", ctypes.c_uint64),
+                ("active_tiles", ctypes.c_uint32), ("blocked_tiles", ctypes.c_uint32)]
 
 _lib = None
 
@@ -86,6 +94,16 @@ def load():
     L.gg_kernel_time_ms.restype = ctypes.c_float
     L.gg_kernel_time_ms.argtypes = [vp, ctypes.c_char_p]
     L.gg_set_timing.argtypes = [vp, i32]
+    L.gg_coherent_begin.argtypes = [vp, ctypes.POINTER(_Trace), vp, vp]
+    L.gg_coherent_quantum.argtypes = [vp, u64, ctypes.POINTER(_CStatus)]
+    L.gg_coherent_export.argtypes = [vp, vp, u64, vp]
+    L.gg_coherent_import.argtypes = [vp, vp, u64]
+    L.gg_coherent_run.argtypes = [vp, ctypes.POINTER(_Trace), vp, vp]
+    L.gg_coherent_get_stats.argtypes = [vp, vp, vp, vp]
+    L.gg_gen_hotspot_trace.argtypes = [vp, vp, u32, u32, u64, u64, u32, u32, u32, u32, vp]
+    for name in ["gg_coherent_begin", "gg_coherent_quantum", "gg_coherent_export", "gg_coherent_import",
+                 "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace"]:
+        getattr(L, name).restype = i32
     for name in ["gg_reset", "gg_cache_access_batch", "gg_cache_get_counters", "gg_cache_get_line_info",
                  "gg_cache_set_line_info", "gg_cache_access_line", "gg_cache_insert_line",
                  "gg_noc_route_batch", "gg_noc_get_counters", "gg_queue_delay_batch", "gg_gen_uniform_trace"]:
@@ -206,6 +224,60 @@ class Backend:
         _check(load().gg_noc_get_counters(self.h, out.ctypes.data_as(ctypes.c_void_p)))
         return out.reshape(self.cfg.num_tiles, NUM_NET_COUNTERS)
 
+    # ---- coherent mode (Mode C) ----------------------------------------
+    def _trace(self, addr, meta, tile_offsets):
+        import torch
+        n = addr.numel()
+        _need_dev(addr, torch.int64, n)
+        _need_dev(meta, torch.int32, n)
+        offs = np.ascontiguousarray(tile_offsets, dtype=np.uint64)
+        if offs.size != self.cfg.num_tiles + 1:
+            raise ValueError("tile_offsets needs num_tiles + 1 entries")
+        self._keep = offs
+        return _Trace(addr.data_ptr(), meta.data_ptr(), offs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), n)
+
+    def coherent_run(self, addr, meta, tile_offsets, out=None, stream=None):
+        """Whole coherent run (the context must own every shard).  out: int64
+        device tensor, one word per record ((latency_ps << 2) | level)."""
+        import torch
+        if out is not None:
+            _need_dev(out, torch.int64, addr.numel())
+        tr = self._trace(addr, meta, tile_offsets)
+        _check(load().gg_coherent_run(self.h, ctypes.byref(tr), _ptr(out), _stream(stream)))
+
+    def coherent_begin(self, addr, meta, tile_offsets, out=None, stream=None):
+        import torch
+        if out is not None:
+            _need_dev(out, torch.int64, addr.numel())
+        tr = self._trace(addr, meta, tile_offsets)
+        _check(load().gg_coherent_begin(self.h, ctypes.byref(tr), _ptr(out), _stream(stream)))
+
+    def coherent_quantum(self, q):
+        st = _CStatus()
+        _check(load().gg_coherent_quantum(self.h, q, ctypes.byref(st)))
+        return {"steps": st.steps, "boundary_msgs": st.boundary_msgs, "min_next_ps": st.min_next_ps,
+                "active_tiles": st.active_tiles, "blocked_tiles": st.blocked_tiles}
+
+    def coherent_export(self, out_buf, cap):
+        """Held cross-shard messages -> out_buf (uint8 device tensor of cap*48
+        bytes), grouped by destination shard; returns per-shard counts."""
+        K = self.cfg.num_shards or 1
+        counts = np.zeros(K, np.uint64)
+        _check(load().gg_coherent_export(self.h, _ptr(out_buf), cap, counts.ctypes.data_as(ctypes.c_void_p)))
+        return counts
+
+    def coherent_import(self, buf, n):
+        _check(load().gg_coherent_import(self.h, _ptr(buf), n))
+
+    def coherent_stats(self):
+        T = self.cfg.num_tiles
+        st = np.zeros(T * NUM_TILE_STATS, np.uint64)
+        cc = np.zeros(T * 2 * NUM_CACHE_COUNTERS, np.uint64)
+        ri = np.zeros(NUM_RUN_INFO, np.uint64)
+        _check(load().gg_coherent_get_stats(self.h, st.ctypes.data_as(ctypes.c_void_p),
+                                            cc.ctypes.data_as(ctypes.c_void_p), ri.ctypes.data_as(ctypes.c_void_p)))
+        return st.reshape(T, NUM_TILE_STATS), cc.reshape(T, 2, NUM_CACHE_COUNTERS), ri
+
     def queue_delay_batch(self, pkt_time, proc_time, min_processing_time=1):
         t = np.ascontiguousarray(pkt_time, np.uint64)
         p = np.ascontiguousarray(proc_time, np.uint64)
@@ -220,3 +292,36 @@ def gen_uniform_trace(addr, meta, tile_begin, tiles, per_tile, first=0, lines_lo
     """Fill device tensors with the configs[1] synthetic trace."""
     _check(load().gg_gen_uniform_trace(_ptr(addr), _ptr(meta), tile_begin, tiles, per_tile, first,
                                        lines_log2, base_shift, _stream(stream)))
+
+
+def gen_hotspot_trace(addr, meta, tile_begin, tiles, per_tile, first=0, lines_log2=15, base_shift=26,
+                      hot_lines=64, hot_frac256=51, stream=None):
+    """Fill device tensors with the configs[2..4] hotspot trace."""
+    _check(load().gg_gen_hotspot_trace(_ptr(addr), _ptr(meta), tile_begin, tiles, per_tile, first, lines_log2,
+                                       base_shift, hot_lines, hot_frac256, _stream(stream)))
+
+
+class CoherentEngine:
+    """A Backend context behind the engine surface of graphite_amd.coherent.run
+    (one rank: the shards [cfg.shard_begin, cfg.shard_end))."""
+
+    def __init__(self, backend, addr, meta, tile_offsets, out=None):
+        import torch
+        self.be = backend
+        self.dev = addr.device
+        backend.coherent_begin(addr, meta, tile_offsets, out)
+        self.cap = 64 * backend.cfg.num_tiles + 65536
+        self.buf = torch.empty(self.cap * 48, dtype=torch.uint8, device=self.dev)
+
+    def quantum(self, q):
+        return self.be.coherent_quantum(q)
+
+    def export(self):
+        counts = self.be.coherent_export(self.buf, self.cap)
+        n = int(counts.sum())
+        return self.buf[:n * 48], counts
+
+    def import_(self, buf):
+        n = buf.numel() // 48
+        if n:
+            self.be.coherent_import(buf.contiguous(), n)

@@ -85,3 +85,35 @@ def run(engine, quantum_ps, num_shards, world=1, rank=0, backend=None, device="c
         if nq is None:
             return quanta
         q = nq
+
+
+def run_local(engines, quantum_ps, num_shards):
+    """Several engines in one process (each owning an equal block of shards,
+    in rank order), exchanging at the quantum boundary by direct copies —
+    the same schedule as `run` over ranks.  Returns the number of quanta."""
+    import torch
+    world = len(engines)
+    per = num_shards // world
+    q, quanta = 0, 0
+    while True:
+        sts = [e.quantum(q) for e in engines]
+        quanta += 1
+        outs = [e.export() for e in engines]
+        for r, e in enumerate(engines):
+            parts = []
+            for buf, counts in outs:
+                counts = np.asarray(counts, np.int64)
+                off = int(counts[:r * per].sum()) * CMSG_BYTES
+                n = int(counts[r * per:(r + 1) * per].sum()) * CMSG_BYTES
+                if n:
+                    parts.append(buf[off:off + n].to(e.dev if hasattr(e, "dev") else "cpu"))
+            if parts:
+                e.import_(torch.cat(parts))
+        msgs = sum(int(np.asarray(c, np.int64).sum()) for _, c in outs)
+        active = sum(s["active_tiles"] for s in sts)
+        blocked = sum(s["blocked_tiles"] for s in sts)
+        mn = min(s["min_next_ps"] for s in sts)
+        nq = next_quantum(q, quantum_ps, msgs, active, blocked, mn)
+        if nq is None:
+            return quanta
+        q = nq

@@ -26,6 +26,28 @@ __global__ void k_gen_uniform(uint64_t* addr, uint32_t* meta, uint32_t tile_begi
   meta[i] = (((z >> 32) % 3) == 0) ? GG_META_WRITE : 0u;
 }
 
+// configs[2..4] hotspot generator (the same bit recipe as
+// oracle_gen_hotspot, the checker)
+__global__ void k_gen_hotspot(uint64_t* addr, uint32_t* meta, uint32_t tile_begin, uint32_t tiles, uint64_t per_tile,
+                              uint64_t first, uint32_t lines_log2, uint32_t base_shift, uint32_t hot_lines,
+                              uint32_t hot_frac256)
+{
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (uint64_t)tiles * per_tile) return;
+  const uint32_t t = tile_begin + (uint32_t)(i / per_tile);
+  const uint64_t k = first + i % per_tile;
+  uint64_t z = (0x9E3779B97F4A7C15ull ^ (uint64_t)t) + (k + 1) * 0x9E3779B97F4A7C15ull;   // SplitMix64
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  const bool hot = hot_lines && (((z >> 40) & 0xFF) < hot_frac256);
+  addr[i] = hot ? (1ull << 44) + ((z & 0xFFFFFFFFull) % hot_lines) * 64ull
+                : ((uint64_t)t << base_shift) + ((z & ((1ull << lines_log2) - 1)) << 6);
+  const uint32_t gap = (uint32_t)__builtin_ctz((uint32_t)(((z >> 48) & 0xFF) | 0x100)) +
+                       (uint32_t)__builtin_ctz((uint32_t)(((z >> 56) & 0xFF) | 0x100));
+  meta[i] = ((((z >> 32) & 0xFF) % 3) == 0 ? GG_META_WRITE : 0u) | (gap << 1);
+}
+
 int floor_log2(uint64_t n) { int p = -1; while (n) { n >>= 1; ++p; } return p; }
 bool is_pow2(uint64_t n) { return n && !(n & (n - 1)); }
 }  // namespace
@@ -166,6 +188,7 @@ void gg_destroy(gg_ctx* ctx)
   hipDeviceSynchronize();
   gg_cache_state_free(ctx);
   gg_noc_free(ctx);
+  gg_coh_free(ctx);
   if (ctx->err_dev) hipFree(ctx->err_dev);
   for (gg_timer& t : ctx->timers) { hipEventDestroy(t.start); hipEventDestroy(t.stop); }
   delete ctx;
@@ -292,6 +315,21 @@ gg_status gg_gen_uniform_trace(uint64_t* addr_dev, uint32_t* meta_dev, uint32_t 
   if (n == 0) return GG_OK;
   hipLaunchKernelGGL(k_gen_uniform, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      addr_dev, meta_dev, tile_begin, tiles, per_tile, first, lines_log2, base_shift);
+  GG_HIP(hipGetLastError());
+  return GG_OK;
+}
+
+gg_status gg_gen_hotspot_trace(uint64_t* addr_dev, uint32_t* meta_dev, uint32_t tile_begin, uint32_t tiles,
+                               uint64_t per_tile, uint64_t first, uint32_t lines_log2, uint32_t base_shift,
+                               uint32_t hot_lines, uint32_t hot_frac256, void* stream)
+{
+  if (!addr_dev || !meta_dev || lines_log2 > 31 || hot_frac256 > 256 || (uint64_t)tile_begin + tiles > (1ull << 17))
+    return gg_fail(GG_ERR_INVALID, "bad generator arguments");
+  const uint64_t n = (uint64_t)tiles * per_tile;
+  if (n == 0) return GG_OK;
+  hipLaunchKernelGGL(k_gen_hotspot, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     addr_dev, meta_dev, tile_begin, tiles, per_tile, first, lines_log2, base_shift, hot_lines,
+                     hot_frac256);
   GG_HIP(hipGetLastError());
   return GG_OK;
 }

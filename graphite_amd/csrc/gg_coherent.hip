@@ -1,0 +1,1187 @@
+// gg_coherent.hip — the coherent ("Mode C") path on MI355X (gfx950):
+// pr_l1_pr_l2_dram_directory_msi with the DRAM directory, DRAM controller,
+// ShmemPerfModel clock, memory network and lax-barrier quanta, in the
+// canonical step schedule of DESIGN.md §Mode C.
+//
+// Reference (nmtrmail/Graphite, common/tile/memory_subsystem/):
+//   pr_l1_pr_l2_dram_directory_msi/l1_cache_cntlr.cc:89-305   L1 state machine
+//   pr_l1_pr_l2_dram_directory_msi/l2_cache_cntlr.cc:74-527   L2 state machine
+//   pr_l1_pr_l2_dram_directory_msi/dram_directory_cntlr.cc:43-550  MSI directory
+//   cache/directory_cache.cc:102-348                          DirectoryCache
+//   directory_schemes/directory_entry_full_map.cc:18-86       full-map sharers
+//   dram_cntlr.cc:37-74, performance_models/dram_perf_model.cc:75-116  DRAM
+//   performance_models/shmem_perf_model.cc:16-45              per-tile clock
+//   network: gg_dev.h route_closed_form (emesh_hop_counter / magic)
+//
+// Layout: one lane = one tile (the tile's controllers are sequential by
+// construction: a per-tile lock in the reference, memory_manager.cc:78-120).
+// Every tile owns its state in HBM, indexed by local tile (tile - first owned):
+// L1-D / L2 sets (u64 line tags + one meta byte per way: state, cached_loc,
+// LRU age), the directory slice (16-byte entries + full-map sharer words), the
+// replaced-entry pool, the per-address request FIFO and the DRAM history tree.
+// A step is two launches: k_c_tiles (lane per tile: inbox, then trace) and
+// k_c_route (thread per message: network latency, delivery into per-tile
+// linked lists of the next step or into the quantum-boundary buffer).  Steps
+// are launched in batches; a step that sends nothing sets `quiet`, and the
+// launches after it return at once, so one host sync per batch suffices.
+#include "gg_dev.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+namespace {
+using namespace gg;
+
+enum { M_EX_REQ = GG_MSG_EX_REQ, M_SH_REQ = GG_MSG_SH_REQ, M_INV_REQ = GG_MSG_INV_REQ,
+       M_FLUSH_REQ = GG_MSG_FLUSH_REQ, M_WB_REQ = GG_MSG_WB_REQ, M_EX_REP = GG_MSG_EX_REP,
+       M_SH_REP = GG_MSG_SH_REP, M_INV_REP = GG_MSG_INV_REP, M_FLUSH_REP = GG_MSG_FLUSH_REP,
+       M_WB_REP = GG_MSG_WB_REP, M_NULLIFY_REQ = GG_MSG_NULLIFY_REQ };
+enum { DS_UNCACHED = 0, DS_SHARED = 1, DS_MODIFIED = 2 };
+enum { ST_I = 0, ST_S = 1, ST_M = 2 };           // meta byte bits 0-1
+#define INV_ADDR (~0ull)
+#define NO_ENT (-0x7fffffff)
+
+__device__ __forceinline__ bool to_directory(uint32_t t)
+{
+  return t == M_EX_REQ || t == M_SH_REQ || t == M_INV_REP || t == M_FLUSH_REP || t == M_WB_REP;
+}
+__device__ __forceinline__ bool has_data(uint32_t t)
+{
+  return t == M_EX_REP || t == M_SH_REP || t == M_FLUSH_REP || t == M_WB_REP;
+}
+
+struct DEnt { uint64_t addr; int32_t owner; uint16_t dstate; uint16_t nsh; };   // 16 B
+struct CReq { uint64_t addr, time; uint32_t type, requester; };                 // 24 B
+
+struct CP {
+  uint32_t T, K, tb, lt;                 // tiles, shards, first owned tile, owned tiles
+  uint32_t s1, a1, s2, a2, log_line, pol1, pol2;
+  uint32_t E, dassoc, log_dsets, log_slices, W, R, QC, IC;
+  uint32_t bits_req, bits_data, max_list, analytical, dram_qm;
+  uint64_t lat_l1d, lat_l1t, lat_l2d, lat_l2t, lat_dir, gap_ps, dram_proc, dram_cost;
+  uint64_t msg_cap;
+  NocParams np;
+};
+
+struct CS {
+  uint64_t* l1_tag; uint8_t* l1_meta; uint8_t* l1_rr;
+  uint64_t* l2_tag; uint8_t* l2_meta; uint8_t* l2_rr;
+  uint64_t* cc;                          // [lt][2][12]
+  uint64_t* st;                          // [lt][GG_NUM_TILE_STATS]
+  uint64_t *rec, *rec_end, *clk, *pend_start, *out_addr, *out_time;
+  uint32_t *blocked, *seq;
+  DEnt* dir; uint64_t* dsh;              // [lt][E], [lt][E][W]
+  DEnt* rep; uint64_t* rsh; uint32_t* nrep;   // [lt][R], [lt][R][W]
+  CReq* rq; uint32_t* nrq;               // [lt][QC]
+  HQueue* dq; HNode* dnd; int16_t* dfl;  // DRAM queue per tile
+  const uint64_t* addr; const uint32_t* meta; uint64_t* out;
+  gg_cmsg* buf0; gg_cmsg* buf1; uint32_t* cnt;   // cnt[2]
+  int32_t* head0; int32_t* head1;                // [lt]
+  gg_cmsg* bnd; uint32_t* bnd_cnt;
+  uint32_t* scratch;                     // [lt][IC]
+  uint32_t* quiet; uint64_t* ri;
+  uint64_t* ctr;                         // NoC counters [T][GG_NUM_NET_COUNTERS]
+  uint32_t* err;
+};
+
+__device__ __forceinline__ gg_cmsg* bufp(const CS& S, int p) { return p ? S.buf1 : S.buf0; }
+__device__ __forceinline__ int32_t* headp(const CS& S, int p) { return p ? S.head1 : S.head0; }
+
+// ---------------------------------------------------------------------------
+// one private cache (Cache + CacheSet + replacement policy, cache.cc / cache_set.cc)
+// ---------------------------------------------------------------------------
+struct Cache {
+  uint64_t* tag; uint8_t* meta; uint8_t* rr; uint64_t* c;
+  uint32_t sets, ways, log_line, pol, wb;
+
+  __device__ uint32_t set_of(uint64_t a) const { return (uint32_t)((a >> log_line) & (sets - 1)); }   // cache_hash_fn.h:17
+  __device__ uint64_t tag_of(uint64_t a) const { return a >> log_line; }                             // cache.cc:495
+  __device__ int find(uint32_t s, uint64_t t) const                                                   // cache_set.cc:57-70
+  {
+    for (int w = (int)ways - 1; w >= 0; --w) if (tag[(size_t)s * ways + w] == t) return w;
+    return -1;
+  }
+  __device__ void touch(uint32_t s, uint32_t w)                                                        // lru:40-50
+  {
+    if (pol != GG_POLICY_LRU) return;
+    uint8_t* m = meta + (size_t)s * ways;
+    const uint32_t acc = m[w] >> 3;
+    for (uint32_t i = 0; i < ways; ++i) { uint32_t a = m[i] >> 3; if (a < acc) m[i] = (uint8_t)((m[i] & 7u) | ((a + 1) << 3)); }
+    m[w] = (uint8_t)(m[w] & 7u);
+  }
+  __device__ int victim(uint32_t s)                                                                    // lru:23-38, rr:13-22
+  {
+    if (pol == GG_POLICY_LRU) {
+      const uint8_t* m = meta + (size_t)s * ways;
+      int way = -1;
+      for (uint32_t i = 0; i < ways; ++i) {
+        if (tag[(size_t)s * ways + i] == INV_ADDR) return (int)i;
+        else if ((uint32_t)(m[i] >> 3) == ways - 1) way = (int)i;
+      }
+      return way;
+    }
+    const uint32_t cur = rr[s];
+    rr[s] = (uint8_t)(cur == 0 ? ways - 1 : cur - 1);
+    return (int)cur;
+  }
+  __device__ void miss_counters(bool wr, bool miss)                                                   // cache.cc:321-360
+  {
+    c[GG_CC_ACCESSES]++;
+    c[wr ? GG_CC_WRITE_ACCESSES : GG_CC_READ_ACCESSES]++;
+    if (miss) { c[GG_CC_MISSES]++; c[wr ? GG_CC_WRITE_MISSES : GG_CC_READ_MISSES]++; }
+  }
+  // getCacheLineInfo (cache.cc:187-215): state / loc of the line, I / 0 when absent
+  __device__ void get(uint64_t a, uint32_t& st, uint32_t& loc)
+  {
+    const uint32_t s = set_of(a);
+    const int w = find(s, tag_of(a));
+    c[GG_CC_TAG_READS]++;
+    if (w >= 0) { const uint8_t m = meta[(size_t)s * ways + w]; st = m & 3u; loc = (m >> 2) & 1u; }
+    else { st = ST_I; loc = 0; }
+  }
+  // setCacheLineInfo (cache.cc:218-241): st == I writes the invalid tag (CacheLineInfo::invalidate)
+  __device__ bool set(uint64_t a, uint32_t st, uint32_t loc)
+  {
+    const uint32_t s = set_of(a);
+    const int w = find(s, tag_of(a));
+    if (w < 0) return false;
+    uint8_t& m = meta[(size_t)s * ways + w];
+    m = (uint8_t)((m & 0xF8u) | st | (loc << 2));
+    if (st == ST_I) tag[(size_t)s * ways + w] = INV_ADDR;
+    c[GG_CC_TAG_WRITES]++;
+    return true;
+  }
+  // accessCacheLine (cache.cc:84-112)
+  __device__ bool access(uint64_t a, bool store)
+  {
+    const uint32_t s = set_of(a);
+    const int w = find(s, tag_of(a));
+    if (w < 0) return false;
+    touch(s, (uint32_t)w);
+    c[store ? GG_CC_DATA_WRITES : GG_CC_DATA_READS]++;
+    return true;
+  }
+  // insertCacheLine (cache.cc:114-184); returns false on a policy error
+  __device__ bool insert(uint64_t a, uint32_t st, uint32_t loc, bool& ev, uint64_t& ev_addr, uint32_t& ev_st,
+                         uint32_t& ev_loc)
+  {
+    const uint32_t s = set_of(a);
+    const int w = victim(s);
+    if (w < 0 || (uint32_t)w >= ways) return false;
+    const size_t i = (size_t)s * ways + w;
+    ev = tag[i] != INV_ADDR;
+    if (ev) { ev_addr = tag[i] << log_line; ev_st = meta[i] & 3u; ev_loc = (meta[i] >> 2) & 1u; }
+    tag[i] = tag_of(a);
+    meta[i] = (uint8_t)((meta[i] & 0xF8u) | st | (loc << 2));
+    touch(s, (uint32_t)w);
+    c[GG_CC_TAG_READS]++;
+    if (ev) {
+      c[GG_CC_DATA_READS]++;
+      c[GG_CC_EVICTIONS]++;
+      if (wb && ev_st == ST_M) c[GG_CC_DIRTY_EVICTIONS]++;
+    }
+    c[GG_CC_TAG_WRITES]++; c[GG_CC_DATA_WRITES]++;
+    return true;
+  }
+};
+
+// work items of the directory controller's call chains (recursion in the
+// reference, an explicit continuation stack here)
+enum { W_NONE = 0, W_PROC, W_CONT, W_NEXT, W_NULLIFY };
+struct Work { uint64_t addr; uint32_t kind, type, requester, cached; int32_t h; };
+#define WSTACK 32
+
+// ---------------------------------------------------------------------------
+// one tile's controllers
+// ---------------------------------------------------------------------------
+struct Tile {
+  const CP& P; const CS& S;
+  uint32_t lt, tile; int po;
+  Cache L1, L2;
+  uint64_t* st;
+
+  __device__ Tile(const CP& p, const CS& s, uint32_t l, int out_parity) : P(p), S(s), lt(l), tile(p.tb + l), po(out_parity)
+  {
+    L1 = Cache{S.l1_tag + (size_t)lt * P.s1 * P.a1, S.l1_meta + (size_t)lt * P.s1 * P.a1, S.l1_rr + (size_t)lt * P.s1,
+               S.cc + (size_t)lt * 2 * GG_NUM_CACHE_COUNTERS, P.s1, P.a1, P.log_line, P.pol1, 0};
+    L2 = Cache{S.l2_tag + (size_t)lt * P.s2 * P.a2, S.l2_meta + (size_t)lt * P.s2 * P.a2, S.l2_rr + (size_t)lt * P.s2,
+               S.cc + ((size_t)lt * 2 + 1) * GG_NUM_CACHE_COUNTERS, P.s2, P.a2, P.log_line, P.pol2, 1};
+    st = S.st + (size_t)lt * GG_NUM_TILE_STATS;
+  }
+  __device__ void fail(uint32_t e = GG_DERR_STATE) const { atomicOr(S.err, e); }
+
+  // MemoryManager::sendMsg (…msi/memory_manager.cc:306-332)
+  __device__ void send(uint32_t dst, uint32_t type, uint32_t requester, uint64_t addr, uint64_t t)
+  {
+    const uint32_t i = atomicAdd(&S.cnt[po], 1u);
+    if (i >= P.msg_cap) { fail(GG_DERR_CAP); return; }
+    gg_cmsg m;
+    m.addr = addr; m.send_ps = t; m.arrival_ps = t; m.src = tile; m.dst = dst; m.requester = requester;
+    m.seq = S.seq[lt]++; m.type = type; m.link = 0xFFFFFFFFu;
+    bufp(S, po)[i] = m;
+    st[GG_CT_MSGS_SENT]++;
+    st[GG_CT_SENT_BY_TYPE + type - 1]++;
+  }
+  __device__ uint32_t home(uint64_t a) const { return (uint32_t)((a >> 6) % P.T); }   // address_home_lookup.cc:19-26
+
+  // ---- directory (DirectoryCache + DirectoryEntryFullMap) ------------------
+  __device__ DEnt* ent(int32_t h) const
+  {
+    return h >= 0 ? S.dir + (size_t)lt * P.E + h : S.rep + (size_t)lt * P.R + (-h - 1);
+  }
+  __device__ uint64_t* shw(int32_t h) const
+  {
+    return h >= 0 ? S.dsh + ((size_t)lt * P.E + h) * P.W : S.rsh + ((size_t)lt * P.R + (-h - 1)) * P.W;
+  }
+  __device__ bool has(int32_t h, uint32_t s) const { return (shw(h)[s >> 6] >> (s & 63)) & 1ull; }
+  __device__ void add_sharer(int32_t h, uint32_t s)                 // addSharer (full_map.cc:27-33)
+  {
+    if (has(h, s)) fail();
+    shw(h)[s >> 6] |= 1ull << (s & 63); ent(h)->nsh++;
+  }
+  __device__ void remove_sharer(int32_t h, uint32_t s)              // removeSharer (:35-41)
+  {
+    if (!has(h, s)) { fail(); return; }
+    shw(h)[s >> 6] &= ~(1ull << (s & 63)); ent(h)->nsh--;
+  }
+  __device__ void set_owner(int32_t h, int32_t o)                   // DirectoryEntry::setOwner
+  {
+    if (o >= 0 && !has(h, (uint32_t)o)) fail();
+    ent(h)->owner = o;
+  }
+  __device__ uint32_t dset(uint64_t a) const                        // computeSetIndex (directory_cache.cc:332-348)
+  {
+    uint64_t s = 0;
+    const uint64_t mask = (1ull << P.log_dsets) - 1;
+    for (uint32_t i = P.log_line + P.log_slices; i + P.log_dsets <= 64; i += P.log_dsets) s ^= (a >> i) & mask;
+    return (uint32_t)s;
+  }
+  // getDirectoryEntry (directory_cache.cc:102-145)
+  __device__ int32_t dget(uint64_t a, uint64_t& t)
+  {
+    t += P.lat_dir;
+    st[GG_CT_DIR_ACCESSES]++;
+    const uint32_t base = dset(a) * P.dassoc;
+    DEnt* d = S.dir + (size_t)lt * P.E;
+    for (uint32_t i = 0; i < P.dassoc; ++i) if (d[base + i].addr == a) return (int32_t)(base + i);
+    for (uint32_t i = 0; i < P.dassoc; ++i) if (d[base + i].addr == INV_ADDR) { d[base + i].addr = a; return (int32_t)(base + i); }
+    const uint32_t nr = S.nrep[lt];
+    for (uint32_t r = 0; r < nr; ++r) if (ent(-(int32_t)r - 1)->addr == a) return -(int32_t)r - 1;
+    return NO_ENT;
+  }
+  // replaceDirectoryEntry (directory_cache.cc:163-213): the slot gets a fresh
+  // entry, the old one moves to the replaced list
+  __device__ int32_t dreplace(uint64_t replaced, uint64_t a, uint64_t& t)
+  {
+    const uint32_t base = dset(replaced) * P.dassoc;
+    DEnt* d = S.dir + (size_t)lt * P.E;
+    int32_t slot = -1;
+    for (uint32_t i = 0; i < P.dassoc; ++i) if (d[base + i].addr == replaced) { slot = (int32_t)(base + i); break; }
+    if (slot < 0) { fail(); return NO_ENT; }
+    const uint32_t r = S.nrep[lt];
+    if (r >= P.R) { fail(GG_DERR_CAP); return NO_ENT; }
+    S.nrep[lt] = r + 1;
+    *ent(-(int32_t)r - 1) = d[slot];
+    uint64_t* so = shw(slot); uint64_t* sr = shw(-(int32_t)r - 1);
+    for (uint32_t w = 0; w < P.W; ++w) { sr[w] = so[w]; so[w] = 0; }
+    d[slot] = DEnt{a, -1, DS_UNCACHED, 0};
+    t += P.lat_dir;
+    st[GG_CT_DIR_ACCESSES]++;
+    st[GG_CT_DIR_EVICTIONS]++;
+    if (ent(-(int32_t)r - 1)->dstate != DS_UNCACHED) st[GG_CT_DIR_BACK_INVALIDATIONS]++;
+    return slot;
+  }
+  // invalidateDirectoryEntry (directory_cache.cc:215-231): erase from the replaced list
+  __device__ void dinvalidate(uint64_t a)
+  {
+    const uint32_t nr = S.nrep[lt];
+    for (uint32_t r = 0; r < nr; ++r) {
+      if (ent(-(int32_t)r - 1)->addr != a) continue;
+      for (uint32_t k = r; k + 1 < nr; ++k) {
+        *ent(-(int32_t)k - 1) = *ent(-(int32_t)k - 2);
+        uint64_t* dst = shw(-(int32_t)k - 1); const uint64_t* src = shw(-(int32_t)k - 2);
+        for (uint32_t w = 0; w < P.W; ++w) dst[w] = src[w];
+      }
+      S.nrep[lt] = nr - 1;
+      return;
+    }
+    fail();
+  }
+
+  // ---- per-address request FIFO (HashMapList<IntPtr, ShmemReq*>) -----------
+  __device__ CReq* q() const { return S.rq + (size_t)lt * P.QC; }
+  __device__ uint32_t qcount(uint64_t a) const
+  {
+    const uint32_t n = S.nrq[lt]; uint32_t c = 0;
+    for (uint32_t i = 0; i < n; ++i) c += (q()[i].addr == a);
+    return c;
+  }
+  __device__ int32_t qfront(uint64_t a) const
+  {
+    const uint32_t n = S.nrq[lt];
+    for (uint32_t i = 0; i < n; ++i) if (q()[i].addr == a) return (int32_t)i;
+    return -1;
+  }
+  __device__ void qpush(uint64_t a, uint64_t t, uint32_t type, uint32_t req)
+  {
+    const uint32_t n = S.nrq[lt];
+    if (n >= P.QC) { fail(GG_DERR_CAP); return; }
+    q()[n] = CReq{a, t, type, req};
+    S.nrq[lt] = n + 1;
+  }
+  __device__ void qpop(uint64_t a)
+  {
+    const uint32_t n = S.nrq[lt];
+    for (uint32_t i = 0; i < n; ++i) {
+      if (q()[i].addr != a) continue;
+      for (uint32_t k = i; k + 1 < n; ++k) q()[k] = q()[k + 1];
+      S.nrq[lt] = n - 1;
+      return;
+    }
+  }
+  __device__ static void front_time(CReq& r, uint64_t& t)   // ShmemReq::updateTime + updateCurrTime
+  {
+    if (r.time < t) r.time = t;
+    if (t < r.time) t = r.time;
+  }
+
+  // ---- DramCntlr / DramPerfModel --------------------------------------------
+  __device__ uint64_t dram_ps(uint64_t t)
+  {
+    const uint64_t pkt_ns = (uint64_t)ceil(t / 1000.0);
+    uint64_t qd = 0;
+    if (P.dram_qm) {
+      HTree tr{S.dq + lt, S.dnd + (size_t)lt * P.max_list, S.dfl + (size_t)lt * P.max_list, P.dram_proc,
+               P.analytical != 0};
+      qd = tr.delay(pkt_ns, P.dram_proc, S.err);
+      st[GG_CT_DRAM_QUEUE_REQUESTS]++;
+    }
+    const uint64_t lat = qd + P.dram_proc + P.dram_cost;
+    st[GG_CT_DRAM_ACCESSES]++;
+    st[GG_CT_DRAM_LATENCY_NS] += lat;
+    st[GG_CT_DRAM_QUEUE_DELAY_NS] += qd;
+    return lat_to_ps(lat, 1.0);
+  }
+
+  // ---- DramDirectoryCntlr: the call chains as a work loop -------------------
+  __device__ void directory_run(Work w, uint64_t& t)
+  {
+    Work stack[WSTACK];
+    int sp = 0;
+    for (;;) {
+      switch (w.kind) {
+      case W_PROC: {                     // processEx/ShReqFromL2Cache (:238-380): entry lookup
+        int32_t h = dget(w.addr, t);
+        if (h == NO_ENT) {               // processDirectoryEntryAllocationReq (:126-170)
+          const uint64_t msg_time = t;
+          if (dget(w.addr, t) != NO_ENT) fail();   // the assert in getReplacementCandidates (directory_cache.cc:161)
+          const uint32_t base = dset(w.addr) * P.dassoc;
+          const DEnt* d = S.dir + (size_t)lt * P.E;
+          int32_t cand = -1;
+          for (uint32_t i = 0; i < P.dassoc; ++i) {
+            const DEnt& it = d[base + i];
+            if ((cand < 0 || d[cand].nsh > it.nsh) && qcount(it.addr) == 0) cand = (int32_t)(base + i);
+          }
+          if (cand < 0) { fail(); return; }
+          const uint64_t replaced = d[cand].addr;
+          h = dreplace(replaced, w.addr, t);
+          if (h == NO_ENT) return;
+          qpush(replaced, msg_time, M_NULLIFY_REQ, w.requester);
+          if (qcount(replaced) != 1) fail();
+          if (sp >= WSTACK) { fail(GG_DERR_CAP); return; }
+          Work c = w; c.kind = W_CONT; c.h = h;
+          stack[sp++] = c;
+          w = Work{replaced, W_NULLIFY, 0, w.requester, 0, 0};
+          continue;
+        }
+        w.kind = W_CONT; w.h = h;
+        continue;
+      }
+      case W_CONT: {                     // the directory-state switch
+        DEnt* e = ent(w.h);
+        if (w.type == M_EX_REQ) {
+          if (e->dstate == DS_MODIFIED) {
+            if (w.cached) fail();
+            send((uint32_t)e->owner, M_FLUSH_REQ, w.requester, w.addr, t);
+            w.kind = W_NONE;
+          } else if (e->dstate == DS_SHARED) {
+            if (w.cached) fail();
+            const uint64_t* sh = shw(w.h);
+            for (uint32_t k = 0; k < P.W; ++k) {                     // getSharersList: ascending
+              uint64_t bits = sh[k];
+              while (bits) {
+                const uint32_t b = __builtin_ctzll(bits); bits &= bits - 1;
+                send(k * 64 + b, M_INV_REQ, w.requester, w.addr, t);
+              }
+            }
+            w.kind = W_NONE;
+          } else {
+            add_sharer(w.h, w.requester);
+            set_owner(w.h, (int32_t)w.requester);
+            ent(w.h)->dstate = DS_MODIFIED;
+            if (!w.cached) t += dram_ps(t);                         // retrieveDataAndSendToL2Cache (:382-408)
+            send(w.requester, M_EX_REP, w.requester, w.addr, t);
+            w.kind = W_NEXT;
+          }
+        } else {
+          if (e->dstate == DS_MODIFIED) {
+            if (w.cached) fail();
+            send((uint32_t)e->owner, M_WB_REQ, w.requester, w.addr, t);
+            w.kind = W_NONE;
+          } else {
+            add_sharer(w.h, w.requester);
+            ent(w.h)->dstate = DS_SHARED;
+            if (!w.cached) t += dram_ps(t);
+            send(w.requester, M_SH_REP, w.requester, w.addr, t);
+            w.kind = W_NEXT;
+          }
+        }
+        continue;
+      }
+      case W_NEXT: {                     // processNextReqFromL2Cache (:98-124)
+        if (qcount(w.addr) < 1) { fail(); return; }
+        qpop(w.addr);
+        const int32_t f = qfront(w.addr);
+        if (f < 0) { w.kind = W_NONE; continue; }
+        CReq& r = q()[f];
+        front_time(r, t);
+        if (r.type != M_EX_REQ && r.type != M_SH_REQ) { fail(); return; }
+        w = Work{w.addr, W_PROC, r.type, r.requester, 0, 0};
+        continue;
+      }
+      case W_NULLIFY: {                  // processNullifyReq (:172-236)
+        const int32_t h = dget(w.addr, t);
+        if (h == NO_ENT) { fail(); return; }
+        DEnt* e = ent(h);
+        if (e->dstate == DS_MODIFIED) {
+          send((uint32_t)e->owner, M_FLUSH_REQ, w.requester, w.addr, t);
+          w.kind = W_NONE;
+        } else if (e->dstate == DS_SHARED) {
+          const uint64_t* sh = shw(h);
+          for (uint32_t k = 0; k < P.W; ++k) {
+            uint64_t bits = sh[k];
+            while (bits) {
+              const uint32_t b = __builtin_ctzll(bits); bits &= bits - 1;
+              send(k * 64 + b, M_INV_REQ, w.requester, w.addr, t);
+            }
+          }
+          w.kind = W_NONE;
+        } else {
+          dinvalidate(w.addr);
+          w.kind = W_NEXT;
+        }
+        continue;
+      }
+      default:
+        if (sp == 0) return;
+        w = stack[--sp];
+        continue;
+      }
+    }
+  }
+
+  // handleMsgFromL2Cache (:43-96) + processInv/Flush/WbRepFromL2Cache (:410-543)
+  __device__ void directory_msg(const gg_cmsg& m)
+  {
+    uint64_t t = m.arrival_ps;           // __handleMsgFromNetwork: setCurrTime(packet.time)
+    const uint64_t a = m.addr;
+    if (m.type == M_EX_REQ || m.type == M_SH_REQ) {
+      qpush(a, t, m.type, m.requester);
+      if (qcount(a) == 1) directory_run(Work{a, W_PROC, m.type, m.requester, 0, 0}, t);
+      return;
+    }
+    const int32_t h = dget(a, t);
+    if (h == NO_ENT) { fail(); return; }
+    DEnt* e = ent(h);
+    if (m.type == M_INV_REP) {
+      if (e->dstate != DS_SHARED) { fail(); return; }
+      remove_sharer(h, m.src);
+      if (e->nsh == 0) e->dstate = DS_UNCACHED;
+      const int32_t f = qfront(a);
+      if (f < 0) return;
+      CReq& r = q()[f];
+      front_time(r, t);
+      if (r.type == M_EX_REQ) { if (e->dstate == DS_UNCACHED) directory_run(Work{a, W_PROC, M_EX_REQ, r.requester, 0, 0}, t); }
+      else if (r.type == M_SH_REQ) directory_run(Work{a, W_PROC, M_SH_REQ, r.requester, 0, 0}, t);
+      else { if (e->dstate == DS_UNCACHED) directory_run(Work{a, W_NULLIFY, 0, r.requester, 0, 0}, t); }
+    } else if (m.type == M_FLUSH_REP) {
+      if (e->dstate != DS_MODIFIED) { fail(); return; }
+      remove_sharer(h, m.src);
+      set_owner(h, -1);
+      e->dstate = DS_UNCACHED;
+      const int32_t f = qfront(a);
+      if (f < 0) { (void)dram_ps(t); return; }                      // putDataToDram: queue model, no latency
+      CReq& r = q()[f];
+      front_time(r, t);
+      if (r.type == M_EX_REQ) directory_run(Work{a, W_PROC, M_EX_REQ, r.requester, 1, 0}, t);
+      else if (r.type == M_SH_REQ) { (void)dram_ps(t); directory_run(Work{a, W_PROC, M_SH_REQ, r.requester, 1, 0}, t); }
+      else { (void)dram_ps(t); directory_run(Work{a, W_NULLIFY, 0, r.requester, 0, 0}, t); }
+    } else if (m.type == M_WB_REP) {
+      if (e->dstate != DS_MODIFIED || !has(h, m.src)) { fail(); return; }
+      set_owner(h, -1);
+      e->dstate = DS_SHARED;
+      const int32_t f = qfront(a);
+      if (f < 0) { fail(); return; }
+      CReq& r = q()[f];
+      front_time(r, t);
+      (void)dram_ps(t);
+      if (r.type != M_SH_REQ) { fail(); return; }
+      directory_run(Work{a, W_PROC, M_SH_REQ, r.requester, 1, 0}, t);
+    } else {
+      fail();
+    }
+  }
+
+  // ---- L1 / L2 controllers ---------------------------------------------------
+  __device__ void l1_invalidate(uint64_t a)                          // l1_cache_cntlr.cc:293-305
+  {
+    uint32_t s, l;
+    L1.get(a, s, l);
+    if (s != ST_I && !L1.set(a, ST_I, 0)) fail();
+  }
+  __device__ void l1_access(uint64_t a, bool wr)                    // l1:182-205 (+ write-through, l2:66-70)
+  {
+    if (!L1.access(a, wr)) fail();
+    if (wr && !L2.access(a, true)) fail();
+  }
+  __device__ void insert_in_l1(uint64_t a, uint32_t cs)             // l2_cache_cntlr.cc:133-165
+  {
+    bool ev; uint64_t ea = 0; uint32_t es = 0, el = 0;
+    if (!L1.insert(a, cs, 0, ev, ea, es, el)) { fail(); return; }
+    if (ev) {
+      uint32_t s2, l2;
+      L2.get(ea, s2, l2);
+      if (l2 != 1) { fail(); return; }                               // cached_loc must be L1-D
+      if (!L2.set(ea, s2, 0)) fail();                                // clearCachedLoc
+    }
+  }
+  __device__ void l2_insert(uint64_t a, uint32_t cs, uint64_t t)    // l2_cache_cntlr.cc:74-116
+  {
+    bool ev; uint64_t ea = 0; uint32_t es = 0, el = 0;
+    if (!L2.insert(a, cs, 1, ev, ea, es, el)) { fail(); return; }
+    if (ev) {
+      if (el) l1_invalidate(ea);
+      if (es == ST_M) send(home(ea), M_FLUSH_REP, tile, ea, t);
+      else if (es == ST_S) send(home(ea), M_INV_REP, tile, ea, t);
+      else fail();
+    }
+  }
+  __device__ void finish(uint64_t start, uint64_t end, uint32_t level)
+  {
+    const uint64_t r = S.rec[lt];
+    const uint64_t lat = end - start;
+    if (S.out) S.out[r] = (lat << 2) | level;
+    st[GG_CT_ACCESSES]++;
+    st[GG_CT_LATENCY_PS] += lat;
+    st[level == GG_LVL_L1 ? GG_CT_L1_HITS : level == GG_LVL_L2 ? GG_CT_L2_HITS : GG_CT_L2_MISSES]++;
+    S.clk[lt] = end;
+    st[GG_CT_CLOCK_PS] = end;
+    S.rec[lt] = r + 1;
+  }
+  // Core::initiateMemoryAccess -> L1CacheCntlr::processMemOpFromCore, first attempt (l1:89-180)
+  __device__ void app_access(uint64_t a, bool wr, uint64_t s)
+  {
+    uint64_t t = s;
+    uint32_t cs, loc;
+    L1.get(a, cs, loc);
+    const bool hit = wr ? cs == ST_M : cs != ST_I;
+    L1.miss_counters(wr, !hit);
+    if (hit) { t += P.lat_l1d; l1_access(a, wr); finish(s, t, GG_LVL_L1); return; }
+    t += P.lat_l1t;
+    l1_invalidate(a);
+    uint32_t c2, l2;                                                 // processShmemRequestFromL1Cache (l2:180-224)
+    L2.get(a, c2, l2);
+    const bool hit2 = wr ? c2 == ST_M : c2 != ST_I;
+    L2.miss_counters(wr, !hit2);
+    if (hit2) {
+      if (!L2.access(a, false)) fail();
+      insert_in_l1(a, c2);
+      if (!L2.set(a, c2, 1)) fail();                                 // set(Forced)CachedLoc(L1-D)
+      t += P.lat_l2d; t += P.lat_l1d;
+      l1_access(a, wr);
+      finish(s, t, GG_LVL_L2);
+      return;
+    }
+    t += P.lat_l2t;
+    if (S.out_addr[lt] != INV_ADDR) fail();                          // handleMsgFromL1Cache (l2:226-258)
+    S.out_addr[lt] = a; S.out_time[lt] = t;
+    const uint32_t h = home(a);
+    if (wr) {                                                        // processExReqFromL1Cache (l2:260-282)
+      uint32_t x, xl;
+      L2.get(a, x, xl);
+      if (x == ST_S) { if (!L2.set(a, ST_I, 0)) fail(); send(h, M_INV_REP, tile, a, t); }
+      else if (x != ST_I) fail();
+      send(h, M_EX_REQ, tile, a, t);
+    } else {
+      send(h, M_SH_REQ, tile, a, t);
+    }
+    S.blocked[lt] = 1;
+    S.pend_start[lt] = s;
+  }
+  // L2CacheCntlr::handleMsgFromDramDirectory (l2:294-502) + the core's second attempt
+  __device__ void l2_msg(const gg_cmsg& m)
+  {
+    uint64_t t = m.arrival_ps;
+    const uint64_t a = m.addr;
+    if (m.type == M_EX_REP || m.type == M_SH_REP) {
+      const uint32_t cs = m.type == M_EX_REP ? ST_M : ST_S;
+      if (!S.blocked[lt] || S.out_addr[lt] != a) { fail(); return; }
+      l2_insert(a, cs, t);
+      insert_in_l1(a, cs);
+      if (S.out_time[lt] > t) fail();
+      t += P.lat_l2d;
+      S.out_addr[lt] = INV_ADDR;
+      const bool wr = (S.meta[S.rec[lt]] & GG_META_WRITE) != 0;     // access_num == 2 (l1:106-126)
+      uint32_t c1, l1;
+      L1.get(a, c1, l1);
+      const bool hit = wr ? c1 == ST_M : c1 != ST_I;
+      if (!hit) { fail(); return; }
+      t += P.lat_l1d;
+      l1_access(a, wr);
+      S.blocked[lt] = 0;
+      finish(S.pend_start[lt], t, GG_LVL_DIR);
+      return;
+    }
+    uint32_t c2, loc;
+    L2.get(a, c2, loc);
+    if (c2 == ST_I) { t += P.lat_l2t; return; }                      // line already gone: tags only, no reply
+    if (m.type == M_INV_REQ) {                                       // l2:369-410
+      if (c2 != ST_S) { fail(); return; }
+      t += P.lat_l2t;
+      if (loc) { t += P.lat_l1t; l1_invalidate(a); }
+      if (!L2.set(a, ST_I, 0)) fail();
+      send(m.src, M_INV_REP, m.requester, a, t);
+    } else if (m.type == M_FLUSH_REQ) {                              // l2:412-455
+      if (c2 != ST_M) { fail(); return; }
+      t += P.lat_l2d;
+      if (loc) { t += P.lat_l1t; l1_invalidate(a); }
+      if (!L2.access(a, false)) fail();
+      if (!L2.set(a, ST_I, 0)) fail();
+      send(m.src, M_FLUSH_REP, m.requester, a, t);
+    } else if (m.type == M_WB_REQ) {                                 // l2:457-502
+      if (c2 != ST_M) { fail(); return; }
+      t += P.lat_l2d;
+      if (loc) {
+        t += P.lat_l1t;
+        uint32_t c1, l1;                                             // setCacheLineState (l1:278-291)
+        L1.get(a, c1, l1);
+        if (c1 == ST_I) fail();
+        if (!L1.set(a, ST_S, 0)) fail();
+      }
+      if (!L2.access(a, false)) fail();
+      if (!L2.set(a, ST_S, loc)) fail();
+      send(m.src, M_WB_REP, m.requester, a, t);
+    } else {
+      fail();
+    }
+  }
+};
+
+__device__ __forceinline__ bool chan_lt(const gg_cmsg& a, const gg_cmsg& b)
+{
+  return a.src < b.src || (a.src == b.src && a.seq < b.seq);
+}
+
+// A step, lane per owned tile: the inbox (per-channel FIFO, channels merged by
+// (arrival, sender)), then the trace up to the barrier or the next miss.
+__global__ void __launch_bounds__(64) k_c_tiles(CP P, CS S, int p, uint64_t barrier)
+{
+  if (*(volatile uint32_t*)S.quiet) return;
+  const uint32_t lt = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lt >= P.lt) return;
+  Tile T(P, S, lt, 1 - p);
+  // 1. gather the inbox list
+  int32_t* head = headp(S, p);
+  const gg_cmsg* in = bufp(S, p);
+  uint32_t* idx = S.scratch + (size_t)lt * P.IC;
+  uint32_t n = 0;
+  for (int32_t i = head[lt]; i >= 0; i = (int32_t)in[i].link) {
+    if (n >= P.IC) { T.fail(GG_DERR_CAP); return; }
+    idx[n++] = (uint32_t)i;
+  }
+  head[lt] = -1;
+  // insertion sort by (sender, sequence)
+  for (uint32_t i = 1; i < n; ++i) {
+    const uint32_t v = idx[i];
+    const gg_cmsg& mv = in[v];
+    uint32_t j = i;
+    while (j > 0 && chan_lt(mv, in[idx[j - 1]])) { idx[j] = idx[j - 1]; --j; }
+    idx[j] = v;
+  }
+  // merge the channels: repeatedly the channel head with the least (arrival, sender)
+  for (uint32_t k = 0; k < n; ++k) {
+    uint32_t best = ~0u, prev_src = ~0u;
+    for (uint32_t i = 0; i < n; ++i) {
+      if (idx[i] == ~0u) continue;
+      const gg_cmsg& m = in[idx[i]];
+      if (m.src == prev_src) continue;               // not the head of its channel
+      prev_src = m.src;
+      if (best == ~0u) { best = i; continue; }
+      const gg_cmsg& b = in[idx[best]];
+      if (m.arrival_ps < b.arrival_ps || (m.arrival_ps == b.arrival_ps && m.src < b.src)) best = i;
+    }
+    const gg_cmsg m = in[idx[best]];
+    idx[best] = ~0u;
+    T.st[GG_CT_MSGS_RECEIVED]++;
+    if (to_directory(m.type)) T.directory_msg(m); else T.l2_msg(m);
+  }
+  // 2. the trace
+  const uint64_t line_mask = ~((1ull << P.log_line) - 1);
+  while (!S.blocked[lt]) {
+    const uint64_t r = S.rec[lt];
+    if (r >= S.rec_end[lt]) break;
+    const uint32_t meta = S.meta[r];
+    const uint64_t s = S.clk[lt] + (uint64_t)((meta & 0x7FFFFFFFu) >> 1) * P.gap_ps;
+    if (s >= barrier) break;
+    T.app_access(S.addr[r] & line_mask, (meta & GG_META_WRITE) != 0, s);
+  }
+}
+
+// A step's messages: network latency, then delivery (same shard: the next
+// step's inbox list; otherwise the quantum-boundary buffer).
+__global__ void k_c_route(CP P, CS S, int p)
+{
+  if (*(volatile uint32_t*)S.quiet) return;
+  const int po = 1 - p;
+  const uint32_t n = min(S.cnt[po], (uint32_t)P.msg_cap);
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid == 0) {
+    if (n == 0) *S.quiet = 1;
+    S.cnt[p] = 0;                                  // the outbox of the next step
+  }
+  gg_cmsg* B = bufp(S, po);
+  int32_t* head = headp(S, po);
+  for (uint32_t i = gid; i < n; i += gridDim.x * blockDim.x) {
+    gg_cmsg m = B[i];
+    uint64_t zl;
+    m.arrival_ps = route_closed_form(P.np, m.src, m.dst, has_data(m.type) ? P.bits_data : P.bits_req,
+                                     m.send_ps, zl, S.ctr);
+    atomicAdd((unsigned long long*)&S.ri[m.src == m.dst ? GG_RI_SELF_MSGS : GG_RI_NET_MSGS], 1ull);
+    const uint32_t ss = (uint32_t)(((uint64_t)m.src * P.K) / P.T), ds = (uint32_t)(((uint64_t)m.dst * P.K) / P.T);
+    if (ss == ds) {
+      m.link = (uint32_t)atomicExch(&head[m.dst - P.tb], (int32_t)i);
+      B[i] = m;
+    } else {
+      const uint32_t j = atomicAdd(S.bnd_cnt, 1u);
+      if (j >= P.msg_cap) { atomicOr(S.err, GG_DERR_CAP); continue; }
+      S.bnd[j] = m;
+      atomicAdd((unsigned long long*)&S.ri[GG_RI_BOUNDARY_MSGS], 1ull);
+    }
+  }
+}
+
+__global__ void k_c_count_step(CS S) { if (!*(volatile uint32_t*)S.quiet) S.ri[GG_RI_STEPS]++; }
+
+// Deliver imported (boundary) messages into the inbox of the quantum's first step.
+__global__ void k_c_import(CP P, CS S, const gg_cmsg* in, uint32_t n)
+{
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  gg_cmsg m = in[i];
+  if (m.dst < P.tb || m.dst >= P.tb + P.lt) { atomicOr(S.err, GG_DERR_STATE); return; }
+  m.link = (uint32_t)atomicExch(&S.head0[m.dst - P.tb], (int32_t)i);
+  S.buf0[i] = m;
+}
+
+// Status after a quantum: active / blocked tiles, least next-access start.
+__global__ void k_c_status(CP P, CS S, uint64_t* out /* [active, blocked, min_next] */)
+{
+  const uint32_t lt = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lt >= P.lt) return;
+  const uint64_t r = S.rec[lt];
+  if (r >= S.rec_end[lt]) return;
+  atomicAdd((unsigned long long*)&out[0], 1ull);
+  if (S.blocked[lt]) { atomicAdd((unsigned long long*)&out[1], 1ull); return; }
+  const uint64_t s = S.clk[lt] + (uint64_t)((S.meta[r] & 0x7FFFFFFFu) >> 1) * P.gap_ps;
+  atomicMin((unsigned long long*)&out[2], (unsigned long long)s);
+}
+
+__global__ void k_c_reset(CP P, CS S, const uint64_t* offs)
+{
+  const uint32_t lt = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lt >= P.lt) return;
+  for (uint32_t i = 0; i < P.s1 * P.a1; ++i) { S.l1_tag[(size_t)lt * P.s1 * P.a1 + i] = INV_ADDR;
+                                               S.l1_meta[(size_t)lt * P.s1 * P.a1 + i] = (uint8_t)((i % P.a1) << 3); }
+  for (uint32_t i = 0; i < P.s1; ++i) S.l1_rr[(size_t)lt * P.s1 + i] = (uint8_t)(P.a1 - 1);
+  for (uint32_t i = 0; i < P.s2 * P.a2; ++i) { S.l2_tag[(size_t)lt * P.s2 * P.a2 + i] = INV_ADDR;
+                                               S.l2_meta[(size_t)lt * P.s2 * P.a2 + i] = (uint8_t)((i % P.a2) << 3); }
+  for (uint32_t i = 0; i < P.s2; ++i) S.l2_rr[(size_t)lt * P.s2 + i] = (uint8_t)(P.a2 - 1);
+  for (uint32_t i = 0; i < 2 * GG_NUM_CACHE_COUNTERS; ++i) S.cc[(size_t)lt * 2 * GG_NUM_CACHE_COUNTERS + i] = 0;
+  for (uint32_t i = 0; i < GG_NUM_TILE_STATS; ++i) S.st[(size_t)lt * GG_NUM_TILE_STATS + i] = 0;
+  for (uint32_t i = 0; i < P.E; ++i) S.dir[(size_t)lt * P.E + i] = DEnt{INV_ADDR, -1, DS_UNCACHED, 0};
+  for (uint64_t i = 0; i < (uint64_t)P.E * P.W; ++i) S.dsh[(size_t)lt * P.E * P.W + i] = 0;
+  S.nrep[lt] = 0; S.nrq[lt] = 0;
+  const uint32_t tile = P.tb + lt;
+  S.rec[lt] = offs[tile]; S.rec_end[lt] = offs[tile + 1];
+  S.clk[lt] = 0; S.pend_start[lt] = 0; S.out_addr[lt] = INV_ADDR; S.out_time[lt] = 0;
+  S.blocked[lt] = 0; S.seq[lt] = 0;
+  S.head0[lt] = -1; S.head1[lt] = -1;
+  if (P.dram_qm) {                                   // QueueModelHistoryTree(min_processing_time)
+    HQueue Q{};
+    Q.max_size = P.max_list;
+    int16_t* f = S.dfl + (size_t)lt * P.max_list;
+    for (uint32_t j = 0; j < P.max_list; ++j) f[j] = (int16_t)j;
+    Q.free_tail = (int32_t)P.max_list - 1;
+    HNode* N = S.dnd + (size_t)lt * P.max_list;
+    const int r = f[Q.free_tail--];
+    N[r].first = 0; N[r].second = ~0ull; N[r].parent = N[r].left = N[r].right = -1; N[r].height = 1;
+    Q.root = r; Q.size = 1;
+    S.dq[lt] = Q;
+  }
+}
+
+__global__ void k_c_final_stats(CP P, CS S)
+{
+  const uint32_t lt = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lt >= P.lt || !P.dram_qm) return;
+  S.st[(size_t)lt * GG_NUM_TILE_STATS + GG_CT_DRAM_QUEUE_ANALYTICAL] = S.dq[lt].analytical;
+}
+
+// export: group the boundary messages by destination shard
+__global__ void k_c_export_count(CP P, const gg_cmsg* b, uint32_t n, uint32_t* counts)
+{
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  atomicAdd(&counts[((uint64_t)b[i].dst * P.K) / P.T], 1u);
+}
+__global__ void k_c_export_scatter(CP P, const gg_cmsg* b, uint32_t n, const uint32_t* base, uint32_t* cursor,
+                                   gg_cmsg* out)
+{
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t k = (uint32_t)(((uint64_t)b[i].dst * P.K) / P.T);
+  out[base[k] + atomicAdd(&cursor[k], 1u)] = b[i];
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+struct gg_coh_state {
+  CP P{};
+  CS S{};
+  std::vector<void*> allocs;
+  uint64_t* status_dev = nullptr;
+  uint32_t* ecount_dev = nullptr;    // export counts + cursors
+  uint64_t* offs_dev = nullptr;
+  uint64_t n_records = 0;
+  bool begun = false;
+};
+
+static int ilog2(uint64_t v) { int p = -1; while (v) { v >>= 1; ++p; } return p; }
+static int clog2(uint64_t v) { int p = ilog2(v); return ((1ull << p) == v) ? p : p + 1; }
+static uint64_t lat_ps_host(uint64_t cycles, double f) { return (uint64_t)ceil(((double)1000 * cycles) / f); }
+
+template <class T> static gg_status dalloc(gg_coh_state* C, T** p, uint64_t n)
+{
+  hipError_t e = hipMalloc((void**)p, sizeof(T) * (n ? n : 1));
+  if (e != hipSuccess) return gg_hip_check(e, "hipMalloc(coherent state)");
+  C->allocs.push_back((void*)*p);
+  return GG_OK;
+}
+
+void gg_coh_free(gg_ctx* ctx)
+{
+  gg_coh_state* C = ctx->coh;
+  if (!C) return;
+  for (void* p : C->allocs) hipFree(p);
+  delete C;
+  ctx->coh = nullptr;
+}
+
+static gg_status coh_alloc(gg_ctx* ctx)
+{
+  if (ctx->coh) return GG_OK;
+  const gg_config& c = ctx->cfg;
+  gg_coh_state* C = new gg_coh_state();
+  ctx->coh = C;
+  CP& P = C->P;
+  P.T = c.num_tiles;
+  P.K = c.num_shards ? c.num_shards : 1;
+  const uint32_t k0 = c.shard_begin, k1 = c.shard_end ? c.shard_end : P.K;
+  if (k0 >= k1 || k1 > P.K || P.K > P.T) return gg_fail(GG_ERR_INVALID, "bad shard range [%u, %u) of %u", k0, k1, P.K);
+  // tiles of shard k: { t : t*K/T == k } = [ceil(k*T/K), ceil((k+1)*T/K))
+  P.tb = (uint32_t)(((uint64_t)k0 * P.T + P.K - 1) / P.K);
+  const uint32_t te = (uint32_t)(((uint64_t)k1 * P.T + P.K - 1) / P.K);
+  P.lt = te - P.tb;
+  if (c.net_model == GG_NET_EMESH_HOP_BY_HOP)
+    return gg_fail(GG_ERR_UNSUPPORTED, "coherent mode: emesh_hop_by_hop is not built on the GPU yet");
+  if (c.l1d_assoc > 31 || c.l2_assoc > 31) return gg_fail(GG_ERR_UNSUPPORTED, "coherent mode: associativity above 31");
+  P.log_line = (uint32_t)ilog2(c.line_size);
+  P.s1 = c.l1d_size_kb * 1024u / (c.l1d_assoc * c.line_size); P.a1 = c.l1d_assoc; P.pol1 = c.l1d_policy;
+  P.s2 = c.l2_size_kb * 1024u / (c.l2_assoc * c.line_size); P.a2 = c.l2_assoc; P.pol2 = c.l2_policy;
+  const double f = c.frequency_ghz;
+  P.lat_l1d = lat_ps_host(c.l1d_data_cycles, f); P.lat_l1t = lat_ps_host(c.l1d_tags_cycles, f);
+  P.lat_l2d = lat_ps_host(c.l2_data_cycles, f); P.lat_l2t = lat_ps_host(c.l2_tags_cycles, f);
+  P.gap_ps = lat_ps_host(1, f);
+  // DirectoryCache sizing and access time (directory_cache.cc:46-90, 243-322)
+  P.dassoc = c.dir_assoc;
+  const uint32_t slices = P.T;
+  uint32_t entries;
+  if (c.dir_total_entries == 0) {
+    uint32_t sets = (uint32_t)ceil(2.0 * c.l2_size_kb * 1024 * P.T / (64.0 * c.dir_assoc * slices));
+    sets = 1u << clog2(sets);
+    entries = sets * c.dir_assoc;
+  } else entries = c.dir_total_entries;
+  P.E = entries;
+  const uint32_t dsets = entries / c.dir_assoc;
+  if (dsets == 0 || (dsets & (dsets - 1))) return gg_fail(GG_ERR_UNSUPPORTED, "directory sets must be a power of two");
+  P.log_dsets = (uint32_t)ilog2(dsets);
+  P.log_slices = (uint32_t)clog2(slices);
+  const uint64_t dir_size = (uint64_t)entries * (uint64_t)ceil(1.0 * P.T / 8);
+  uint64_t cyc = c.dir_access_cycles;
+  if (cyc == 0) {
+    const uint32_t kb = (uint32_t)ceil(1.0 * dir_size / 1024);
+    cyc = kb <= 16 ? 1 : kb <= 32 ? 2 : kb <= 64 ? 4 : kb <= 128 ? 6 : kb <= 256 ? 8 :
+          kb <= 512 ? 10 : kb <= 1024 ? 13 : kb <= 2048 ? 16 : 20;
+  }
+  P.lat_dir = lat_ps_host(cyc, f);
+  P.W = (P.T + 63) / 64;
+  P.R = 64;
+  P.QC = P.T + P.R + 8;
+  P.IC = 2 * P.T + 256;
+  const uint32_t idb = P.T > 1 ? (uint32_t)clog2(P.T) : 0;
+  P.bits_req = 2 * idb + 4 + 48;
+  P.bits_data = P.bits_req + 8 * c.line_size;
+  P.dram_qm = c.dram_queue_model_enabled;
+  P.max_list = c.max_list_size ? c.max_list_size : 100;
+  P.analytical = c.analytical_enabled;
+  P.dram_proc = (uint64_t)((float)c.line_size / c.dram_bandwidth) + 1;
+  P.dram_cost = (uint64_t)(float)c.dram_latency_ns;
+  P.msg_cap = (uint64_t)64 * P.T + 65536;
+  P.np = gg_noc_params(ctx);
+  const uint64_t L = P.lt;
+  CS& S = C->S;
+  gg_status st = GG_OK;
+#define A(ptr, n) if (st == GG_OK) st = dalloc(C, &S.ptr, (n))
+  A(l1_tag, L * P.s1 * P.a1); A(l1_meta, L * P.s1 * P.a1); A(l1_rr, L * P.s1);
+  A(l2_tag, L * P.s2 * P.a2); A(l2_meta, L * P.s2 * P.a2); A(l2_rr, L * P.s2);
+  A(cc, L * 2 * GG_NUM_CACHE_COUNTERS); A(st, L * GG_NUM_TILE_STATS);
+  A(rec, L); A(rec_end, L); A(clk, L); A(pend_start, L); A(out_addr, L); A(out_time, L);
+  A(blocked, L); A(seq, L);
+  A(dir, L * P.E); A(dsh, L * P.E * P.W);
+  A(rep, L * P.R); A(rsh, L * P.R * P.W); A(nrep, L);
+  A(rq, L * P.QC); A(nrq, L);
+  A(dq, L); A(dnd, L * P.max_list); A(dfl, L * P.max_list);
+  A(buf0, P.msg_cap); A(buf1, P.msg_cap); A(cnt, 2);
+  A(head0, L); A(head1, L);
+  A(bnd, P.msg_cap); A(bnd_cnt, 1);
+  A(scratch, L * P.IC);
+  A(quiet, 1); A(ri, GG_NUM_RUN_INFO);
+#undef A
+  if (st == GG_OK) st = dalloc(C, &C->status_dev, 4);
+  if (st == GG_OK) st = dalloc(C, &C->ecount_dev, 2 * (uint64_t)P.K + 2);
+  if (st == GG_OK) st = dalloc(C, &C->offs_dev, (uint64_t)P.T + 1);
+  S.ctr = gg_noc_ctr(ctx);
+  S.err = ctx->err_dev;
+  return st;
+}
+
+static gg_status coh_check(gg_ctx* ctx)
+{
+  uint32_t e = 0;
+  GG_HIP(hipMemcpy(&e, ctx->err_dev, sizeof(e), hipMemcpyDeviceToHost));
+  if (e & GG_DERR_CAP) return gg_fail(GG_ERR_UNSUPPORTED, "coherent mode: a device capacity (messages / inbox / "
+                                      "request queue / replaced entries / call chain) was exceeded");
+  if (e & GG_DERR_STATE) return gg_fail(GG_ERR_STATE, "coherent mode: a state the reference would reject "
+                                        "(LOG_ASSERT_ERROR / assert)");
+  return GG_OK;
+}
+
+gg_status gg_coherent_begin(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_dev, void* stream)
+{
+  if (!ctx || !tr || !tr->tile_offsets) return gg_fail(GG_ERR_INVALID, "NULL argument");
+  hipSetDevice(ctx->device);
+  hipStream_t s = (hipStream_t)stream;
+  ctx->last_stream = s;
+  if (gg_status st = coh_alloc(ctx)) return st;
+  gg_coh_state* C = ctx->coh;
+  const CP& P = C->P;
+  if (tr->tile_offsets[P.T] != tr->num_records) return gg_fail(GG_ERR_INVALID, "tile_offsets[num_tiles] != num_records");
+  for (uint32_t t = 0; t < P.T; ++t)
+    if (tr->tile_offsets[t] > tr->tile_offsets[t + 1]) return gg_fail(GG_ERR_INVALID, "tile_offsets not monotone");
+  if (tr->num_records && (!tr->addr_dev || !tr->meta_dev)) return gg_fail(GG_ERR_INVALID, "NULL trace pointers");
+  C->S.addr = tr->addr_dev; C->S.meta = tr->meta_dev; C->S.out = access_out_dev;
+  C->n_records = tr->num_records;
+  GG_HIP(hipMemcpyAsync(C->offs_dev, tr->tile_offsets, sizeof(uint64_t) * (P.T + 1), hipMemcpyHostToDevice, s));
+  if (gg_status st = gg_noc_reset(ctx, s)) return st;
+  GG_HIP(hipMemsetAsync(ctx->err_dev, 0, sizeof(uint32_t), s));
+  GG_HIP(hipMemsetAsync(C->S.ri, 0, sizeof(uint64_t) * GG_NUM_RUN_INFO, s));
+  GG_HIP(hipMemsetAsync(C->S.cnt, 0, sizeof(uint32_t) * 2, s));
+  GG_HIP(hipMemsetAsync(C->S.bnd_cnt, 0, sizeof(uint32_t), s));
+  hipLaunchKernelGGL(k_c_reset, dim3((P.lt + 63) / 64), dim3(64), 0, s, P, C->S, (const uint64_t*)C->offs_dev);
+  GG_HIP(hipGetLastError());
+  GG_HIP(hipStreamSynchronize(s));
+  C->begun = true;
+  return coh_check(ctx);
+}
+
+gg_status gg_coherent_quantum(gg_ctx* ctx, uint64_t q, gg_coherent_status* out)
+{
+  if (!ctx || !out) return gg_fail(GG_ERR_INVALID, "NULL argument");
+  gg_coh_state* C = ctx->coh;
+  if (!C || !C->begun) return gg_fail(GG_ERR_INVALID, "gg_coherent_begin first");
+  hipSetDevice(ctx->device);
+  hipStream_t s = ctx->last_stream;
+  const CP& P = C->P;
+  const uint64_t quantum_ps = (uint64_t)ctx->cfg.quantum_ns * 1000ull;
+  const uint64_t barrier = (q + 1) * quantum_ps;
+  GG_HIP(hipMemsetAsync(C->S.quiet, 0, sizeof(uint32_t), s));
+  const uint32_t tb = (P.lt + 63) / 64;
+  const uint32_t rb = (uint32_t)std::min<uint64_t>((P.msg_cap + 255) / 256, 1024);
+  uint64_t steps = 0;
+  uint32_t batch = 8;
+  for (;;) {
+    for (uint32_t k = 0; k < batch; ++k) {
+      const int p = (int)((steps + k) & 1);
+      hipLaunchKernelGGL(k_c_count_step, dim3(1), dim3(1), 0, s, C->S);
+      hipLaunchKernelGGL(k_c_tiles, dim3(tb), dim3(64), 0, s, P, C->S, p, barrier);
+      hipLaunchKernelGGL(k_c_route, dim3(rb), dim3(256), 0, s, P, C->S, p);
+    }
+    GG_HIP(hipGetLastError());
+    steps += batch;
+    uint32_t quiet = 0, err = 0;
+    GG_HIP(hipMemcpyAsync(&quiet, C->S.quiet, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    GG_HIP(hipMemcpyAsync(&err, ctx->err_dev, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    GG_HIP(hipStreamSynchronize(s));
+    if (err) return coh_check(ctx);
+    if (quiet) break;
+    if (batch < 64) batch *= 2;
+  }
+  uint64_t init[4] = {0, 0, ~0ull, 0};
+  GG_HIP(hipMemcpyAsync(C->status_dev, init, sizeof(init), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_c_status, dim3(tb), dim3(64), 0, s, P, C->S, C->status_dev);
+  GG_HIP(hipGetLastError());
+  uint64_t res[4];
+  uint32_t nb = 0;
+  uint64_t ri[GG_NUM_RUN_INFO];
+  GG_HIP(hipMemcpyAsync(res, C->status_dev, sizeof(res), hipMemcpyDeviceToHost, s));
+  GG_HIP(hipMemcpyAsync(&nb, C->S.bnd_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  GG_HIP(hipMemcpyAsync(ri, C->S.ri, sizeof(ri), hipMemcpyDeviceToHost, s));
+  GG_HIP(hipStreamSynchronize(s));
+  ri[GG_RI_QUANTA]++;
+  ri[GG_RI_FINAL_QUANTUM] = q;
+  GG_HIP(hipMemcpyAsync(C->S.ri, ri, sizeof(ri), hipMemcpyHostToDevice, s));
+  out->steps = 0;
+  out->boundary_msgs = nb;
+  out->min_next_ps = res[2];
+  out->active_tiles = (uint32_t)res[0];
+  out->blocked_tiles = (uint32_t)res[1];
+  return coh_check(ctx);
+}
+
+gg_status gg_coherent_export(gg_ctx* ctx, gg_cmsg* out_dev, uint64_t cap, uint64_t* per_shard_counts)
+{
+  if (!ctx || !per_shard_counts) return gg_fail(GG_ERR_INVALID, "NULL argument");
+  gg_coh_state* C = ctx->coh;
+  if (!C || !C->begun) return gg_fail(GG_ERR_INVALID, "gg_coherent_begin first");
+  hipSetDevice(ctx->device);
+  hipStream_t s = ctx->last_stream;
+  const CP& P = C->P;
+  uint32_t nb = 0;
+  GG_HIP(hipMemcpy(&nb, C->S.bnd_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (nb > cap) return gg_fail(GG_ERR_RANGE, "export buffer holds %llu messages, %u waiting",
+                               (unsigned long long)cap, nb);
+  if (nb && !out_dev) return gg_fail(GG_ERR_INVALID, "NULL export buffer");
+  std::vector<uint32_t> counts(P.K, 0), base(P.K, 0);
+  if (nb) {
+    GG_HIP(hipMemsetAsync(C->ecount_dev, 0, sizeof(uint32_t) * 2 * P.K, s));
+    hipLaunchKernelGGL(k_c_export_count, dim3((nb + 255) / 256), dim3(256), 0, s, P, C->S.bnd, nb, C->ecount_dev);
+    GG_HIP(hipMemcpyAsync(counts.data(), C->ecount_dev, sizeof(uint32_t) * P.K, hipMemcpyDeviceToHost, s));
+    GG_HIP(hipStreamSynchronize(s));
+    uint32_t a = 0;
+    for (uint32_t k = 0; k < P.K; ++k) { base[k] = a; a += counts[k]; }
+    GG_HIP(hipMemcpyAsync(C->ecount_dev, base.data(), sizeof(uint32_t) * P.K, hipMemcpyHostToDevice, s));
+    GG_HIP(hipMemsetAsync(C->ecount_dev + P.K, 0, sizeof(uint32_t) * P.K, s));
+    hipLaunchKernelGGL(k_c_export_scatter, dim3((nb + 255) / 256), dim3(256), 0, s, P, C->S.bnd, nb,
+                       C->ecount_dev, C->ecount_dev + P.K, out_dev);
+    GG_HIP(hipGetLastError());
+  }
+  GG_HIP(hipMemsetAsync(C->S.bnd_cnt, 0, sizeof(uint32_t), s));
+  GG_HIP(hipStreamSynchronize(s));
+  for (uint32_t k = 0; k < P.K; ++k) per_shard_counts[k] = counts[k];
+  return GG_OK;
+}
+
+gg_status gg_coherent_import(gg_ctx* ctx, const gg_cmsg* in_dev, uint64_t n)
+{
+  if (!ctx) return gg_fail(GG_ERR_INVALID, "NULL argument");
+  gg_coh_state* C = ctx->coh;
+  if (!C || !C->begun) return gg_fail(GG_ERR_INVALID, "gg_coherent_begin first");
+  if (n == 0) return GG_OK;
+  if (!in_dev) return gg_fail(GG_ERR_INVALID, "NULL import buffer");
+  if (n > C->P.msg_cap) return gg_fail(GG_ERR_UNSUPPORTED, "import of %llu messages beyond the step buffer",
+                                       (unsigned long long)n);
+  hipSetDevice(ctx->device);
+  hipStream_t s = ctx->last_stream;
+  // the quantum's first step reads buffer 0; its outbox (buffer 1) starts empty
+  GG_HIP(hipMemsetAsync(C->S.cnt + 1, 0, sizeof(uint32_t), s));
+  hipLaunchKernelGGL(k_c_import, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, C->P, C->S, in_dev, (uint32_t)n);
+  GG_HIP(hipGetLastError());
+  GG_HIP(hipStreamSynchronize(s));
+  return coh_check(ctx);
+}
+
+gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_dev, void* stream)
+{
+  if (!ctx) return gg_fail(GG_ERR_INVALID, "NULL argument");
+  const gg_config& c = ctx->cfg;
+  const uint32_t K = c.num_shards ? c.num_shards : 1;
+  if (c.shard_begin != 0 || (c.shard_end != 0 && c.shard_end != K))
+    return gg_fail(GG_ERR_INVALID, "gg_coherent_run needs a context that owns every shard");
+  if (gg_status st = gg_coherent_begin(ctx, tr, access_out_dev, stream)) return st;
+  gg_coh_state* C = ctx->coh;
+  hipStream_t s = ctx->last_stream;
+  const uint64_t quantum_ps = (uint64_t)c.quantum_ns * 1000ull;
+  gg_timer_begin(ctx, "coherent_run", s);
+  uint64_t q = 0;
+  for (;;) {
+    gg_coherent_status st;
+    if (gg_status e = gg_coherent_quantum(ctx, q, &st)) return e;
+    const uint64_t nb = st.boundary_msgs;
+    if (nb) {                                          // the boundary: held messages -> next inboxes
+      GG_HIP(hipMemcpyAsync(C->S.buf1, C->S.bnd, sizeof(gg_cmsg) * nb, hipMemcpyDeviceToDevice, s));
+      GG_HIP(hipMemsetAsync(C->S.bnd_cnt, 0, sizeof(uint32_t), s));
+      if (gg_status e = gg_coherent_import(ctx, C->S.buf1, nb)) return e;
+    }
+    if (st.active_tiles == 0 && nb == 0) break;
+    if (nb == 0 && st.blocked_tiles == 0) {
+      const uint64_t nq = st.min_next_ps / quantum_ps;
+      q = nq > q + 1 ? nq : q + 1;
+    } else if (nb == 0) {
+      return gg_fail(GG_ERR_STATE, "coherent run deadlocked: tiles blocked with no message in flight");
+    } else {
+      q = q + 1;
+    }
+  }
+  gg_timer_end(ctx, "coherent_run", s);
+  GG_HIP(hipStreamSynchronize(s));
+  return coh_check(ctx);
+}
+
+gg_status gg_coherent_get_stats(gg_ctx* ctx, uint64_t* tile_stats, uint64_t* cache, uint64_t* run_info)
+{
+  if (!ctx) return gg_fail(GG_ERR_INVALID, "NULL argument");
+  gg_coh_state* C = ctx->coh;
+  if (!C) return gg_fail(GG_ERR_INVALID, "no coherent run on this context");
+  hipSetDevice(ctx->device);
+  hipStream_t s = ctx->last_stream;
+  const CP& P = C->P;
+  hipLaunchKernelGGL(k_c_final_stats, dim3((P.lt + 63) / 64), dim3(64), 0, s, P, C->S);
+  GG_HIP(hipGetLastError());
+  GG_HIP(hipStreamSynchronize(s));
+  if (tile_stats) {
+    std::memset(tile_stats, 0, sizeof(uint64_t) * P.T * GG_NUM_TILE_STATS);
+    GG_HIP(hipMemcpy(tile_stats + (size_t)P.tb * GG_NUM_TILE_STATS, C->S.st,
+                     sizeof(uint64_t) * P.lt * GG_NUM_TILE_STATS, hipMemcpyDeviceToHost));
+  }
+  if (cache) {
+    std::memset(cache, 0, sizeof(uint64_t) * P.T * 2 * GG_NUM_CACHE_COUNTERS);
+    GG_HIP(hipMemcpy(cache + (size_t)P.tb * 2 * GG_NUM_CACHE_COUNTERS, C->S.cc,
+                     sizeof(uint64_t) * P.lt * 2 * GG_NUM_CACHE_COUNTERS, hipMemcpyDeviceToHost));
+  }
+  if (run_info) GG_HIP(hipMemcpy(run_info, C->S.ri, sizeof(uint64_t) * GG_NUM_RUN_INFO, hipMemcpyDeviceToHost));
+  return coh_check(ctx);
+}

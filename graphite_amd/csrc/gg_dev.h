@@ -1,0 +1,251 @@
+// gg_dev.h — device-side building blocks shared by the NoC (gg_noc.hip) and
+// coherent (gg_coherent.hip) paths: the QueueModelHistoryTree restatement,
+// the time conversions and the closed-form EMesh routes.
+#pragma once
+#include "gg_internal.h"
+
+namespace gg {
+
+// ---------------------------------------------------------------------------
+// history tree (interval_tree.cc:40-394 + queue_model_history_tree.cc:44-167)
+// ---------------------------------------------------------------------------
+struct HNode { uint64_t first, second; int16_t parent, left, right, height; };
+struct HQueue {
+  int32_t root; uint32_t size; int32_t free_tail; uint32_t max_size;
+  double sig_sq, sig; uint64_t n, newest;          // QueueModelMG1
+  uint64_t analytical;                              // _total_requests_using_analytical_model
+  uint64_t util, last_req, total_req;               // QueueModel utilization counters
+};
+
+struct HTree {
+  HQueue* q; HNode* nd; int16_t* fl; uint64_t min_proc; bool analytical;
+
+  __device__ int32_t h(int x) const { return x < 0 ? 0 : nd[x].height; }
+  __device__ void upd_child(int node, int child, int dir)      // updateChildPointer
+  {
+    if (node < 0) return;
+    if (dir == 0) { if (nd[node].first < nd[child].first) nd[node].right = child; else nd[node].left = child; }
+    else if (dir == 1) nd[node].left = child;
+    else nd[node].right = child;
+  }
+  __device__ void upd_parent(int node, int parent)             // updateParentPointer
+  {
+    if (node >= 0) nd[node].parent = parent;
+    if (parent < 0) q->root = node;
+  }
+  __device__ bool balanced(int x) const { int d = h(nd[x].left) - h(nd[x].right); return d >= -1 && d <= 1; }
+  __device__ void upd_height(int x) { int a = h(nd[x].left), b = h(nd[x].right); nd[x].height = (int16_t)((a > b ? a : b) + 1); }
+  __device__ void rotate(int y, bool cw)                       // performRotation
+  {
+    int x;
+    if (cw) {
+      x = nd[y].left;
+      upd_parent(x, nd[y].parent); upd_child(nd[x].parent, x, 0);
+      nd[y].left = nd[x].right; upd_parent(nd[y].left, y);
+      nd[x].right = (int16_t)y; upd_parent(y, x);
+    } else {
+      x = nd[y].right;
+      upd_parent(x, nd[y].parent); upd_child(nd[x].parent, x, 0);
+      nd[y].right = nd[x].left; upd_parent(nd[y].right, y);
+      nd[x].left = (int16_t)y; upd_parent(y, x);
+    }
+    upd_height(y); upd_height(x);
+  }
+  __device__ int balance(int z)                                // balanceHeight
+  {
+    int zl = nd[z].left, zr = nd[z].right;
+    bool y_left = h(zl) > h(zr);
+    int y = y_left ? zl : zr;
+    int yl = nd[y].left, yr = nd[y].right;
+    int x; bool x_left;
+    if (h(yl) != h(yr)) { x_left = h(yl) > h(yr); x = x_left ? yl : yr; }
+    else if (y_left) { x = yl; x_left = true; }
+    else { x = yr; x_left = false; }
+    if (y_left) {
+      if (!x_left) { rotate(y, false); rotate(z, true); return x; }
+      rotate(z, true); return y;
+    } else {
+      if (x_left) { rotate(y, true); rotate(z, false); return x; }
+      rotate(z, false); return y;
+    }
+  }
+  __device__ void rebalance(int r)                             // rebalanceAVLTree
+  {
+    while (r >= 0) {
+      int old = nd[r].height, nr = r;
+      if (!balanced(r)) nr = balance(r); else upd_height(r);
+      if (nd[nr].height == old) return;
+      r = nd[nr].parent;
+    }
+  }
+  __device__ void insert(int node)                             // insert / insertInTree
+  {
+    q->size++;
+    int r = q->root;
+    for (;;) {
+      if (nd[node].first < nd[r].first) {
+        if (nd[r].left >= 0) r = nd[r].left;
+        else { nd[r].left = (int16_t)node; nd[node].parent = (int16_t)r; rebalance(r); return; }
+      } else if (nd[node].first > nd[r].first) {
+        if (nd[r].right >= 0) r = nd[r].right;
+        else { nd[r].right = (int16_t)node; nd[node].parent = (int16_t)r; rebalance(r); return; }
+      } else return;   // duplicate key: the reference aborts (LOG_PRINT_ERROR)
+    }
+  }
+  __device__ int remove_rec(int node)                          // removeFromTree
+  {
+    if (nd[node].left < 0) {
+      int p = nd[node].parent;
+      if (p >= 0) upd_child(p, nd[node].right, (nd[p].first < nd[node].first) ? 2 : 1);
+      upd_parent(nd[node].right, p);
+      rebalance(p);
+      return node;
+    } else if (nd[node].right < 0) {
+      int p = nd[node].parent;
+      upd_child(p, nd[node].left, 0);
+      upd_parent(nd[node].left, p);
+      rebalance(p);
+      return node;
+    }
+    int succ = nd[node].right;
+    while (nd[succ].left >= 0) succ = nd[succ].left;           // findMinKeyNode
+    remove_rec(succ);                                          // successor has no left child
+    uint64_t f = nd[node].first, s = nd[node].second;          // swap key/interval
+    nd[node].first = nd[succ].first; nd[node].second = nd[succ].second;
+    nd[succ].first = f; nd[succ].second = s;
+    return succ;
+  }
+  __device__ int remove(int node) { q->size--; return remove_rec(node); }
+  __device__ int search(uint64_t a, uint64_t b) const          // searchTree
+  {
+    int stack[40]; int sp = 0; int n = q->root;
+    for (;;) {
+      if (n < 0) {
+        if (sp == 0) return -1;
+        n = stack[--sp];
+        if (a < nd[n].first && (nd[n].second - nd[n].first) >= (b - a)) return n;
+        n = nd[n].right; continue;
+      }
+      if (a >= nd[n].first && b <= nd[n].second) return n;
+      if (b < nd[n].first) { if (sp < 40) { stack[sp++] = n; n = nd[n].left; continue; } return -1; }
+      if (a < nd[n].first && (nd[n].second - nd[n].first) >= (b - a)) return n;
+      n = nd[n].right;
+    }
+  }
+  __device__ int alloc(uint64_t a, uint64_t b)                 // allocateNode
+  {
+    if (q->free_tail < 0) return -1;
+    int i = fl[q->free_tail--];
+    nd[i].first = a; nd[i].second = b; nd[i].parent = nd[i].left = nd[i].right = -1; nd[i].height = 1;
+    return i;
+  }
+  __device__ void release(int i) { fl[++q->free_tail] = (int16_t)i; }
+  __device__ uint64_t mg1_delay() const                         // QueueModelMG1::computeQueueDelay
+  {
+    if (q->n == 0) return 0;
+    double variance = (q->sig_sq / q->n) - ((q->sig / q->n) * (q->sig / q->n));
+    double service_rate = 1.0 / (q->sig / q->n);
+    double arrival_rate = ((double)q->n) / q->newest;
+    if (arrival_rate >= service_rate) arrival_rate = 0.999 * service_rate;
+    return (uint64_t)ceil(0.5 * service_rate * arrival_rate * ((1 / (service_rate * service_rate)) + variance) /
+                          (service_rate - arrival_rate));
+  }
+  __device__ uint64_t delay(uint64_t t, uint64_t p, uint32_t* err)   // computeQueueDelay
+  {
+    uint64_t qd = ~0ull;
+    int mn = search(0, 1);
+    if (q->size >= q->max_size) release(remove(mn));
+    mn = search(0, 1);
+    if (analytical && nd[mn].first > (t + p)) {
+      q->analytical++;
+      qd = mg1_delay();
+    } else {
+      int node = search(t, t + p);
+      if (node < 0) { atomicOr(err, GG_DERR_STATE); return 0; }
+      if (t >= nd[node].first) {
+        qd = 0;
+        if ((t - nd[node].first) >= min_proc) {
+          if ((nd[node].second - (t + p)) >= min_proc) {
+            int nx = alloc(t + p, nd[node].second);
+            if (nx < 0) { atomicOr(err, GG_DERR_STATE); return 0; }
+            insert(nx);
+          }
+          nd[node].second = t;
+        } else {
+          if ((nd[node].second - (t + p)) >= min_proc) nd[node].first = t + p;
+          else release(remove(node));
+        }
+      } else {
+        qd = nd[node].first - t;
+        if ((nd[node].second - (nd[node].first + p)) >= min_proc) nd[node].first = nd[node].first + p;
+        else release(remove(node));
+      }
+    }
+    q->sig_sq += (double)p * (double)p;                          // QueueModelMG1::updateQueue
+    q->sig += (double)p;
+    q->n++;
+    { uint64_t x = t + qd + p; if (x > q->newest) q->newest = x; }
+    q->util += p;                                                // updateQueueUtilizationCounters
+    { uint64_t x = t + qd + p; if (x > q->last_req) q->last_req = x; }
+    q->total_req++;
+    return qd;
+  }
+};
+
+__device__ __forceinline__ uint64_t lat_to_ps(uint64_t cycles, double f) { return (uint64_t)ceil(((double)1000 * cycles) / f); }
+__device__ __forceinline__ uint64_t time_to_cycles(uint64_t ps, double f) { return (uint64_t)ceil(((double)ps * f) / 1.0e3); }
+
+struct NocParams {
+  uint32_t tiles, w, h, flit_width, router_delay, link_delay, qm, analytical, max_size, net_model;
+  double f;
+};
+
+__device__ __forceinline__ uint64_t nflits(const NocParams& P, uint32_t bits)
+{
+  return (bits % P.flit_width == 0) ? bits / P.flit_width : bits / P.flit_width + 1;   // computeNumFlits
+}
+
+__device__ __forceinline__ void cadd(uint64_t* c, uint32_t tile, int k, uint64_t v)
+{
+  if (v) atomicAdd((unsigned long long*)&c[(uint64_t)tile * GG_NUM_NET_COUNTERS + k], (unsigned long long)v);
+}
+
+
+// emesh_hop_counter (network_model_emesh_hop_counter.cc:143-157) / magic
+// (network_model_magic.cc:5-21) for one packet, with the sender / receiver
+// counters and processReceivedPacket's serialization (network_model.cc:142-150).
+// Returns the time the packet is handed to the receiver; zl = zero-load part.
+__device__ __forceinline__ uint64_t route_closed_form(const NocParams& P, uint32_t s, uint32_t d, uint32_t bits,
+                                                      uint64_t t, uint64_t& zl, uint64_t* ctr)
+{
+  zl = 0;
+  if (s == d) return t;                           // processCornerCases: self-sends cost nothing
+  if (P.net_model == GG_NET_MAGIC) {
+    cadd(ctr, s, GG_NC_PACKETS_SENT, 1); cadd(ctr, s, GG_NC_BITS_SENT, bits);
+    const uint64_t l = lat_to_ps(1, P.f);
+    t += l; zl += l;
+    cadd(ctr, d, GG_NC_PACKETS_RECEIVED, 1); cadd(ctr, d, GG_NC_BITS_RECEIVED, bits);
+    cadd(ctr, d, GG_NC_TOTAL_LATENCY_PS, zl);
+    return t;
+  }
+  const uint64_t nf = nflits(P, bits);
+  cadd(ctr, s, GG_NC_PACKETS_SENT, 1); cadd(ctr, s, GG_NC_FLITS_SENT, nf); cadd(ctr, s, GG_NC_BITS_SENT, bits);
+  const int sx = (int)(s % P.w), sy = (int)(s / P.w), dx = (int)(d % P.w), dy = (int)(d / P.w);
+  const uint64_t hops = (uint64_t)(abs(sx - dx) + abs(sy - dy));
+  const uint64_t lat = lat_to_ps(hops * ((uint64_t)P.router_delay + P.link_delay), P.f);
+  t += lat; zl += lat;
+  cadd(ctr, s, GG_NC_BUFFER_WRITES, nf * hops); cadd(ctr, s, GG_NC_BUFFER_READS, nf * hops);
+  cadd(ctr, s, GG_NC_SWITCH_ALLOC, hops); cadd(ctr, s, GG_NC_CROSSBAR, nf * hops);
+  cadd(ctr, s, GG_NC_LINK_TRAVERSALS, nf * hops);
+  const uint64_t ser = lat_to_ps(nf, P.f);
+  t += ser; zl += ser;
+  cadd(ctr, d, GG_NC_PACKETS_RECEIVED, 1); cadd(ctr, d, GG_NC_FLITS_RECEIVED, nf);
+  cadd(ctr, d, GG_NC_BITS_RECEIVED, bits); cadd(ctr, d, GG_NC_TOTAL_LATENCY_PS, zl);
+  return t;
+}
+
+}  // namespace gg
+
+// accessors of the NoC state (gg_noc.hip) for the coherent path
+gg::NocParams gg_noc_params(gg_ctx* ctx);
+uint64_t* gg_noc_ctr(gg_ctx* ctx);

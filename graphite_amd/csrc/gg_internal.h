@@ -27,6 +27,7 @@
 // Error bits of the device-side error word (ctx->err_dev).
 #define GG_DERR_RANGE 1u   // address beyond the compressed-tag range
 #define GG_DERR_STATE 2u   // the reference would LOG_ASSERT_ERROR on this state
+#define GG_DERR_CAP 4u     // a device-side capacity (messages, queues, inbox) was exceeded
 
 // Geometry derived from gg_config (cache.cc:44, cache_hash_fn.h:11).
 struct gg_geom {
@@ -64,6 +65,7 @@ struct gg_timer {
 };
 
 struct gg_noc_state;
+struct gg_coh_state;
 
 struct gg_ctx {
   gg_config cfg;
@@ -93,6 +95,8 @@ struct gg_ctx {
   std::vector<uint64_t> h_chunk_start;
   // NoC
   gg_noc_state* noc = nullptr;
+  // coherent mode (gg_coherent.hip), allocated on first use
+  gg_coh_state* coh = nullptr;
   // replay kernel choice: 0 = lean when instantiated (default), 1 = generic
   int replay_variant = 0;
   // timing
@@ -123,4 +127,6 @@ void      gg_noc_free(gg_ctx* ctx);
 gg_status gg_noc_reset(gg_ctx* ctx, hipStream_t s);
 gg_status gg_noc_run(gg_ctx* ctx, const gg_packets* pk, const gg_packet_out* out, hipStream_t s);
 gg_status gg_noc_counters(gg_ctx* ctx, uint64_t* out);
+// coherent path (gg_coherent.hip)
+void      gg_coh_free(gg_ctx* ctx);
 gg_status gg_htree_run(gg_ctx* ctx, uint64_t min_proc, const uint64_t* t, const uint64_t* p, uint64_t n, uint64_t* d);

@@ -351,6 +351,16 @@ gg_status gg_gen_uniform_trace(uint64_t* addr_dev, uint32_t* meta_dev, uint32_t 
                                uint32_t tiles, uint64_t per_tile, uint64_t first,
                                uint32_t lines_log2, uint32_t base_shift, void* stream);
 
+/* configs[2..4] hotspot generator: record i of tile t,
+ * z = SplitMix64(0x9E3779B97F4A7C15 ^ t) step first+i+1; hot iff
+ * ((z >> 40) & 0xFF) < hot_frac256 -> line (z & 0xFFFFFFFF) % hot_lines at byte
+ * 1 << 44, else line z mod 2^lines_log2 at t << base_shift; WRITE iff
+ * ((z >> 32) & 0xFF) % 3 == 0; gap = ctz(((z>>48)&0xFF)|0x100) +
+ * ctz(((z>>56)&0xFF)|0x100) core cycles in meta bits 1..30.                 */
+gg_status gg_gen_hotspot_trace(uint64_t* addr_dev, uint32_t* meta_dev, uint32_t tile_begin, uint32_t tiles,
+                               uint64_t per_tile, uint64_t first, uint32_t lines_log2, uint32_t base_shift,
+                               uint32_t hot_lines, uint32_t hot_frac256, void* stream);
+
 /* Device time (ms) of the most recent launch of a named kernel
  * ("cache_hist", "cache_scatter", "cache_replay", "cache_unshard",
  * "noc_hop_counter", ...), measured with HIP

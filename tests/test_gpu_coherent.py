@@ -1,0 +1,136 @@
+"""GPU parity of the coherent mode (Mode C) through the C ABI: the HIP path
+(graphite_amd/csrc/gg_coherent.hip) against the C oracle
+(oracle/gg_coherent.inc) on the same seeded traces — per-access level and
+latency, per-tile statistics, L1-D/L2 counters and NoC counters, bit-exact."""
+import numpy as np
+import pytest
+
+from graphite_amd import config as C
+from tests.coherent_util import check_invariants
+from tests.gpu_util import torch_dev, to_dev, to_np
+
+pytestmark = pytest.mark.gpu
+
+
+def _gpu_run(cfg, a, m, o):
+    torch = torch_dev()
+    from graphite_amd import backend as B
+    be = B.Backend(cfg)
+    addr, meta = to_dev(torch, a, torch.int64), to_dev(torch, m, torch.int32)
+    out = torch.zeros(len(a), dtype=torch.int64, device="cuda")
+    be.coherent_run(addr, meta, o, out)
+    torch.cuda.synchronize()
+    st, cc, ri = be.coherent_stats()
+    return to_np(out, np.uint64), st, cc, be.noc_counters(), ri
+
+
+def _oracle_run(cfg, a, m, o):
+    from oracle import pyoracle as po
+    oc = po.OracleCoherent(cfg)
+    out = oc.run(a, m, o)
+    return out, oc.tile_stats(), oc.cache_counters(), oc.net_counters(), oc.run_info()
+
+
+def _compare(cfg, a, m, o):
+    g = _gpu_run(cfg, a, m, o)
+    r = _oracle_run(cfg, a, m, o)
+    for name, x, y in zip(("access words", "tile stats", "cache counters", "noc counters"), g[:4], r[:4]):
+        if not np.array_equal(x, y):
+            d = np.argwhere(np.asarray(x) != np.asarray(y))
+            raise AssertionError("%s differ at %d places, first %s: gpu %s oracle %s"
+                                 % (name, len(d), d[0], np.asarray(x)[tuple(d[0])], np.asarray(y)[tuple(d[0])]))
+    for k in ("steps", "net_msgs", "self_msgs", "boundary_msgs"):
+        i = C.RUN_INFO.index(k)
+        assert g[4][i] == r[4][i], (k, g[4][i], r[4][i])
+    check_invariants(g[1], g[2], g[0], o, per_tile_expected=int(o[1] - o[0]))
+    return g
+
+
+@pytest.mark.parametrize("T,N,hot,K,net", [
+    (16, 3000, 0, 1, C.NET_EMESH_HOP_COUNTER),      # private: no sharing
+    (16, 2500, 64, 1, C.NET_EMESH_HOP_COUNTER),     # configs[2]-style hotspot, 16 tiles
+    (16, 2000, 8, 1, C.NET_MAGIC),
+    (64, 1200, 64, 1, C.NET_EMESH_HOP_COUNTER),
+    (64, 1000, 32, 8, C.NET_EMESH_HOP_COUNTER),     # 8 logical shards, quantum-boundary delivery
+    (256, 300, 64, 4, C.NET_EMESH_HOP_COUNTER),
+])
+def test_coherent_matches_oracle(T, N, hot, K, net):
+    from oracle import pyoracle as po
+    cfg = C.default_config(T, num_shards=K, net_model=net)
+    a, m, o = po.gen_trace(T, N, hot_lines=hot)
+    _compare(cfg, a, m, o)
+
+
+def test_coherent_directory_replacements():
+    """A small directory: DirectoryCache replacement, NULLIFY, back-invalidations."""
+    from oracle import pyoracle as po
+    cfg = C.default_config(16, dir_total_entries=64, dir_assoc=4)
+    a, m, o = po.gen_trace(16, 1500, hot_lines=32)
+    g = _compare(cfg, a, m, o)
+    assert g[1][:, C.TILE_STATS.index("dir_back_invalidations")].sum() > 0
+
+
+def test_coherent_ragged_and_empty_tiles():
+    from oracle import pyoracle as po
+    T = 16
+    parts = [po.gen_hotspot(t, 0, [0, 7, 1500, 31][t % 4], hot_lines=16) for t in range(T)]
+    a = np.concatenate([p[0] for p in parts])
+    m = np.concatenate([p[1] for p in parts])
+    o = np.zeros(T + 1, np.uint64)
+    o[1:] = np.cumsum([len(p[0]) for p in parts])
+    cfg = C.default_config(T)
+    g = _gpu_run(cfg, a, m, o)
+    r = _oracle_run(cfg, a, m, o)
+    np.testing.assert_array_equal(g[0], r[0])
+    np.testing.assert_array_equal(g[1], r[1])
+
+
+def test_coherent_two_contexts_exchange():
+    """Two contexts on one GPU, each owning half of 4 logical shards, exchanging
+    the cross-shard messages at every quantum boundary == one context owning all."""
+    torch = torch_dev()
+    from graphite_amd import backend as B
+    from graphite_amd import coherent as CO
+    from oracle import pyoracle as po
+    T, N, K = 64, 800, 4
+    a, m, o = po.gen_trace(T, N, hot_lines=32)
+    addr, meta = to_dev(torch, a, torch.int64), to_dev(torch, m, torch.int32)
+    outs, engines, bes = [], [], []
+    for r in range(2):
+        k0, k1 = CO.shard_range(r, 2, K)
+        be = B.Backend(C.default_config(T, num_shards=K, shard_begin=k0, shard_end=k1))
+        out = torch.zeros(len(a), dtype=torch.int64, device="cuda")
+        engines.append(B.CoherentEngine(be, addr, meta, o, out))
+        outs.append(out); bes.append(be)
+    CO.run_local(engines, 1000 * 1000, K)
+    torch.cuda.synchronize()
+    got = to_np(outs[0], np.uint64) + to_np(outs[1], np.uint64)
+    st = sum(be.coherent_stats()[0] for be in bes)
+    ref = _oracle_run(C.default_config(T, num_shards=K), a, m, o)
+    np.testing.assert_array_equal(got, ref[0])
+    np.testing.assert_array_equal(st, ref[1])
+
+
+def test_gpu_hotspot_generator_matches_oracle():
+    torch = torch_dev()
+    from graphite_amd import backend as B
+    from oracle import pyoracle as po
+    T, N = 8, 5000
+    addr = torch.empty(T * N, dtype=torch.int64, device="cuda")
+    meta = torch.empty(T * N, dtype=torch.int32, device="cuda")
+    B.gen_hotspot_trace(addr, meta, 3, T, N, first=11, hot_lines=64)
+    a = np.concatenate([po.gen_hotspot(t, 11, N, hot_lines=64)[0] for t in range(3, 3 + T)])
+    m = np.concatenate([po.gen_hotspot(t, 11, N, hot_lines=64)[1] for t in range(3, 3 + T)])
+    np.testing.assert_array_equal(to_np(addr, np.uint64), a)
+    np.testing.assert_array_equal(to_np(meta, np.uint32), m)
+
+
+def test_coherent_rejects_unbuilt_config():
+    torch = torch_dev()
+    from graphite_amd import backend as B
+    from oracle import pyoracle as po
+    cfg = C.default_config(16, net_model=C.NET_EMESH_HOP_BY_HOP)
+    a, m, o = po.gen_trace(16, 10)
+    be = B.Backend(cfg)
+    with pytest.raises(B.GGError):
+        be.coherent_run(to_dev(torch, a, torch.int64), to_dev(torch, m, torch.int32), o)
