@@ -36,3 +36,30 @@ def compact_code(res):
                    (32, C.RES_L2_EVICT_DIRTY), (64, C.RES_L2_EVICT_INV_L1)):
         out |= np.where(r & f, bit, 0).astype(np.uint8)
     return out
+
+
+def coh_manifest():
+    with open(os.path.join(GOLDEN, "coh_manifest.json")) as f:
+        return json.load(f)
+
+
+def coh_case(name, m):
+    """(cfg, addr, meta, offsets, expected dict) of a coherent-mode fixture written
+    by oracle/ref/coh_harness.cc (the reference's MSI controllers)."""
+    from graphite_amd import config as C
+    from oracle import pyoracle as po
+    T, N = m["tiles"], m["per_tile"]
+    kw = dict(num_shards=m["num_shards"], net_model=C.NET_EMESH_HOP_COUNTER if m["net"] == 1 else C.NET_MAGIC)
+    if m["dir_entries"]:
+        kw.update(dir_total_entries=m["dir_entries"], dir_assoc=m["dir_assoc"])
+    cfg = C.default_config(T, **kw)
+    a, meta, o = po.gen_trace(T, N, hot_lines=m["hot_lines"])
+    exp = {"out": load("coh_%s_out.u64" % name, np.uint64),
+           "stats": load("coh_%s_stats.u64" % name, np.uint64).reshape(T, 32),
+           "cache": load("coh_%s_cache.u64" % name, np.uint64).reshape(T, 2, 12),
+           "net": load("coh_%s_net.u64" % name, np.uint64).reshape(T, 3),
+           "quanta": m["quanta"], "steps": m["steps"]}
+    return cfg, a, meta, o, exp
+
+
+NET3 = ["packets_sent", "packets_received", "total_latency_ps"]

@@ -134,3 +134,18 @@ def test_coherent_rejects_unbuilt_config():
     be = B.Backend(cfg)
     with pytest.raises(B.GGError):
         be.coherent_run(to_dev(torch, a, torch.int64), to_dev(torch, m, torch.int32), o)
+
+
+@pytest.mark.parametrize("name", sorted(__import__("golden_util").coh_manifest()))
+def test_coherent_matches_reference_fixtures(name):
+    """The HIP path against the fixtures of the reference's own MSI controllers
+    (oracle/ref/coh_harness.cc, tests/golden/coh_*)."""
+    import golden_util as G
+    cfg, a, m, o, exp = G.coh_case(name, G.coh_manifest()[name])
+    out, st, cc, nc, ri = _gpu_run(cfg, a, m, o)
+    np.testing.assert_array_equal(out, exp["out"])
+    np.testing.assert_array_equal(st, exp["stats"])
+    np.testing.assert_array_equal(cc, exp["cache"])
+    np.testing.assert_array_equal(nc[:, [C.NET_COUNTERS.index(k) for k in G.NET3]], exp["net"])
+    assert ri[C.RUN_INFO.index("quanta")] == exp["quanta"]
+    assert ri[C.RUN_INFO.index("steps")] == exp["steps"]

@@ -6,6 +6,7 @@ import pytest
 from graphite_amd import config as C
 from oracle import pyoracle as po
 from golden_util import manifest, load, POLICY, compact_code
+import golden_util as G
 
 M = manifest()
 
@@ -161,3 +162,24 @@ def test_split_lines():
     assert po.split_lines(0x1000, 64) == [0x1000]      # zero-size tail skipped
     assert po.split_lines(0x1010, 128) == [0x1000, 0x1040, 0x1080]
     assert po.split_lines(0x1000, 0) == []
+
+
+# ---- coherent mode: pinned by the reference's own MSI controllers ----------
+@pytest.mark.parametrize("name", sorted(G.coh_manifest()))
+def test_coherent_oracle_matches_reference_controllers(name):
+    """oracle/gg_coherent.inc == L1CacheCntlr / L2CacheCntlr / DramDirectoryCntlr
+    compiled from /root/reference and driven in the same canonical schedule
+    (oracle/ref/coh_harness.cc): every access word, tile statistic, L1-D/L2
+    counter and NoC counter, and the quantum / step counts."""
+    from graphite_amd import config as C
+    cfg, a, m, o, exp = G.coh_case(name, G.coh_manifest()[name])
+    oc = po.OracleCoherent(cfg)
+    out = oc.run(a, m, o)
+    np.testing.assert_array_equal(out, exp["out"])
+    np.testing.assert_array_equal(oc.tile_stats(), exp["stats"])
+    np.testing.assert_array_equal(oc.cache_counters(), exp["cache"])
+    nc = oc.net_counters()[:, [C.NET_COUNTERS.index(k) for k in G.NET3]]
+    np.testing.assert_array_equal(nc, exp["net"])
+    ri = oc.run_info()
+    assert ri[C.RUN_INFO.index("quanta")] == exp["quanta"]
+    assert ri[C.RUN_INFO.index("steps")] == exp["steps"]
