@@ -150,8 +150,8 @@ class Backend:
             _check(st.value or -1)
 
     def close(self):
-        if getattr(self, "h", None):
-            load().gg_destroy(self.h)
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.gg_destroy(self.h)
             self.h = None
 
     __del__ = close

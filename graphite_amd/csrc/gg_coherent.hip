@@ -29,6 +29,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <cstdlib>
 
 namespace {
 using namespace gg;
@@ -61,6 +62,7 @@ struct CP {
   uint32_t bits_req, bits_data, max_list, analytical, dram_qm;
   uint64_t lat_l1d, lat_l1t, lat_l2d, lat_l2t, lat_dir, gap_ps, dram_proc, dram_cost;
   uint64_t msg_cap;
+  uint32_t tiles_per_block;              // 64: a lane per tile; 1: a wave per tile (lane 0)
   NocParams np;
 };
 
@@ -91,89 +93,145 @@ __device__ __forceinline__ int32_t* headp(const CS& S, int p) { return p ? S.hea
 // ---------------------------------------------------------------------------
 // one private cache (Cache + CacheSet + replacement policy, cache.cc / cache_set.cc)
 // ---------------------------------------------------------------------------
+#define CMAXW 16   // ways held in registers at once (larger associativities take the serial path)
 struct Cache {
-  uint64_t* tag; uint8_t* meta; uint8_t* rr; uint64_t* c;
+  uint64_t* tag; uint8_t* meta; uint8_t* rr; uint64_t* cg;
   uint32_t sets, ways, log_line, pol, wb;
+  uint32_t c[GG_NUM_CACHE_COUNTERS];   // this step's counter increments (registers), flushed to cg
 
-  __device__ uint32_t set_of(uint64_t a) const { return (uint32_t)((a >> log_line) & (sets - 1)); }   // cache_hash_fn.h:17
-  __device__ uint64_t tag_of(uint64_t a) const { return a >> log_line; }                             // cache.cc:495
-  __device__ int find(uint32_t s, uint64_t t) const                                                   // cache_set.cc:57-70
+  __device__ __forceinline__ uint32_t set_of(uint64_t a) const { return (uint32_t)((a >> log_line) & (sets - 1)); }   // cache_hash_fn.h:17
+  __device__ __forceinline__ uint64_t tag_of(uint64_t a) const { return a >> log_line; }                             // cache.cc:495
+  // the set's tags and meta bytes, every way's load in flight at once
+  __device__ __forceinline__ void load_set(uint32_t s, uint64_t (&tv)[CMAXW], uint8_t (&mv)[CMAXW]) const
   {
-    for (int w = (int)ways - 1; w >= 0; --w) if (tag[(size_t)s * ways + w] == t) return w;
+    const uint64_t* p = tag + (size_t)s * ways;
+    const uint8_t* m = meta + (size_t)s * ways;
+#pragma unroll
+    for (int w = 0; w < CMAXW; ++w) { tv[w] = INV_ADDR; mv[w] = 0; if (w < (int)ways) { tv[w] = p[w]; mv[w] = m[w]; } }
+  }
+  // CacheSet::find (cache_set.cc:57-70); tags are unique, so any match is the match
+  __device__ __forceinline__ int find(uint32_t s, uint64_t t, uint8_t& mb) const
+  {
+    if (ways <= CMAXW) {
+      uint64_t tv[CMAXW]; uint8_t mv[CMAXW];
+      load_set(s, tv, mv);
+      int f = -1; mb = 0;
+#pragma unroll
+      for (int w = 0; w < CMAXW; ++w) if (w < (int)ways && tv[w] == t) { f = w; mb = mv[w]; }
+      return f;
+    }
+    for (int w = (int)ways - 1; w >= 0; --w)
+      if (tag[(size_t)s * ways + w] == t) { mb = meta[(size_t)s * ways + w]; return w; }
     return -1;
   }
-  __device__ void touch(uint32_t s, uint32_t w)                                                        // lru:40-50
+  __device__ __forceinline__ void touch(uint32_t s, uint32_t w)                                                        // lru:40-50
   {
     if (pol != GG_POLICY_LRU) return;
     uint8_t* m = meta + (size_t)s * ways;
+    if (ways <= CMAXW) {
+      uint8_t v[CMAXW];
+#pragma unroll
+      for (int i = 0; i < CMAXW; ++i) { v[i] = 0; if (i < (int)ways) v[i] = m[i]; }
+      uint32_t acc = 0;
+#pragma unroll
+      for (int i = 0; i < CMAXW; ++i) if (i == (int)w) acc = v[i] >> 3;
+#pragma unroll
+      for (int i = 0; i < CMAXW; ++i) {
+        if (i >= (int)ways) continue;
+        const uint32_t a = v[i] >> 3;
+        const uint8_t nv = (i == (int)w) ? (uint8_t)(v[i] & 7u) : (a < acc ? (uint8_t)((v[i] & 7u) | ((a + 1) << 3)) : v[i]);
+        if (nv != v[i]) m[i] = nv;
+      }
+      return;
+    }
     const uint32_t acc = m[w] >> 3;
     for (uint32_t i = 0; i < ways; ++i) { uint32_t a = m[i] >> 3; if (a < acc) m[i] = (uint8_t)((m[i] & 7u) | ((a + 1) << 3)); }
     m[w] = (uint8_t)(m[w] & 7u);
   }
-  __device__ int victim(uint32_t s)                                                                    // lru:23-38, rr:13-22
+  // getReplacementWay: LRU (lru:23-38) = first invalid way, else the (last) way of age assoc-1;
+  // round robin (rr:13-22).  Returns the way and its current tag / meta byte.
+  __device__ __forceinline__ int victim(uint32_t s, uint64_t& vt, uint8_t& vm)
   {
     if (pol == GG_POLICY_LRU) {
+      if (ways <= CMAXW) {
+        uint64_t tv[CMAXW]; uint8_t mv[CMAXW];
+        load_set(s, tv, mv);
+        int inv = -1, way = -1;
+#pragma unroll
+        for (int i = CMAXW - 1; i >= 0; --i) if (i < (int)ways && tv[i] == INV_ADDR) inv = i;
+#pragma unroll
+        for (int i = 0; i < CMAXW; ++i) if (i < (int)ways && tv[i] != INV_ADDR && (uint32_t)(mv[i] >> 3) == ways - 1) way = i;
+        const int r = inv >= 0 ? inv : way;
+        vt = INV_ADDR; vm = 0;
+#pragma unroll
+        for (int i = 0; i < CMAXW; ++i) if (i == r) { vt = tv[i]; vm = mv[i]; }
+        return r;
+      }
       const uint8_t* m = meta + (size_t)s * ways;
       int way = -1;
       for (uint32_t i = 0; i < ways; ++i) {
-        if (tag[(size_t)s * ways + i] == INV_ADDR) return (int)i;
+        if (tag[(size_t)s * ways + i] == INV_ADDR) { vt = INV_ADDR; vm = m[i]; return (int)i; }
         else if ((uint32_t)(m[i] >> 3) == ways - 1) way = (int)i;
       }
+      if (way >= 0) { vt = tag[(size_t)s * ways + way]; vm = m[way]; }
       return way;
     }
     const uint32_t cur = rr[s];
     rr[s] = (uint8_t)(cur == 0 ? ways - 1 : cur - 1);
+    vt = tag[(size_t)s * ways + cur]; vm = meta[(size_t)s * ways + cur];
     return (int)cur;
   }
-  __device__ void miss_counters(bool wr, bool miss)                                                   // cache.cc:321-360
+  __device__ __forceinline__ void miss_counters(bool wr, bool miss)                                                   // cache.cc:321-360
   {
     c[GG_CC_ACCESSES]++;
-    c[wr ? GG_CC_WRITE_ACCESSES : GG_CC_READ_ACCESSES]++;
-    if (miss) { c[GG_CC_MISSES]++; c[wr ? GG_CC_WRITE_MISSES : GG_CC_READ_MISSES]++; }
+    if (wr) c[GG_CC_WRITE_ACCESSES]++; else c[GG_CC_READ_ACCESSES]++;
+    if (miss) { c[GG_CC_MISSES]++; if (wr) c[GG_CC_WRITE_MISSES]++; else c[GG_CC_READ_MISSES]++; }
   }
   // getCacheLineInfo (cache.cc:187-215): state / loc of the line, I / 0 when absent
-  __device__ void get(uint64_t a, uint32_t& st, uint32_t& loc)
+  __device__ __forceinline__ void get(uint64_t a, uint32_t& st, uint32_t& loc)
   {
-    const uint32_t s = set_of(a);
-    const int w = find(s, tag_of(a));
+    uint8_t m;
+    const int w = find(set_of(a), tag_of(a), m);
     c[GG_CC_TAG_READS]++;
-    if (w >= 0) { const uint8_t m = meta[(size_t)s * ways + w]; st = m & 3u; loc = (m >> 2) & 1u; }
+    if (w >= 0) { st = m & 3u; loc = (m >> 2) & 1u; }
     else { st = ST_I; loc = 0; }
   }
   // setCacheLineInfo (cache.cc:218-241): st == I writes the invalid tag (CacheLineInfo::invalidate)
-  __device__ bool set(uint64_t a, uint32_t st, uint32_t loc)
+  __device__ __forceinline__ bool set(uint64_t a, uint32_t st, uint32_t loc)
   {
     const uint32_t s = set_of(a);
-    const int w = find(s, tag_of(a));
+    uint8_t m;
+    const int w = find(s, tag_of(a), m);
     if (w < 0) return false;
-    uint8_t& m = meta[(size_t)s * ways + w];
-    m = (uint8_t)((m & 0xF8u) | st | (loc << 2));
+    meta[(size_t)s * ways + w] = (uint8_t)((m & 0xF8u) | st | (loc << 2));
     if (st == ST_I) tag[(size_t)s * ways + w] = INV_ADDR;
     c[GG_CC_TAG_WRITES]++;
     return true;
   }
   // accessCacheLine (cache.cc:84-112)
-  __device__ bool access(uint64_t a, bool store)
+  __device__ __forceinline__ bool access(uint64_t a, bool store)
   {
     const uint32_t s = set_of(a);
-    const int w = find(s, tag_of(a));
+    uint8_t m;
+    const int w = find(s, tag_of(a), m);
     if (w < 0) return false;
     touch(s, (uint32_t)w);
-    c[store ? GG_CC_DATA_WRITES : GG_CC_DATA_READS]++;
+    if (store) c[GG_CC_DATA_WRITES]++; else c[GG_CC_DATA_READS]++;
     return true;
   }
   // insertCacheLine (cache.cc:114-184); returns false on a policy error
-  __device__ bool insert(uint64_t a, uint32_t st, uint32_t loc, bool& ev, uint64_t& ev_addr, uint32_t& ev_st,
+  __device__ __forceinline__ bool insert(uint64_t a, uint32_t st, uint32_t loc, bool& ev, uint64_t& ev_addr, uint32_t& ev_st,
                          uint32_t& ev_loc)
   {
     const uint32_t s = set_of(a);
-    const int w = victim(s);
+    uint64_t vt; uint8_t vm;
+    const int w = victim(s, vt, vm);
     if (w < 0 || (uint32_t)w >= ways) return false;
     const size_t i = (size_t)s * ways + w;
-    ev = tag[i] != INV_ADDR;
-    if (ev) { ev_addr = tag[i] << log_line; ev_st = meta[i] & 3u; ev_loc = (meta[i] >> 2) & 1u; }
+    ev = vt != INV_ADDR;
+    if (ev) { ev_addr = vt << log_line; ev_st = vm & 3u; ev_loc = (vm >> 2) & 1u; }
     tag[i] = tag_of(a);
-    meta[i] = (uint8_t)((meta[i] & 0xF8u) | st | (loc << 2));
+    meta[i] = (uint8_t)((vm & 0xF8u) | st | (loc << 2));
     touch(s, (uint32_t)w);
     c[GG_CC_TAG_READS]++;
     if (ev) {
@@ -183,6 +241,11 @@ struct Cache {
     }
     c[GG_CC_TAG_WRITES]++; c[GG_CC_DATA_WRITES]++;
     return true;
+  }
+  __device__ __forceinline__ void flush()
+  {
+#pragma unroll
+    for (int k = 0; k < GG_NUM_CACHE_COUNTERS; ++k) if (c[k]) cg[k] += c[k];
   }
 };
 
@@ -199,58 +262,78 @@ struct Tile {
   const CP& P; const CS& S;
   uint32_t lt, tile; int po;
   Cache L1, L2;
-  uint64_t* st;
+  uint64_t* stg;
+  uint64_t st[GG_NUM_TILE_STATS];       // this step's statistics increments (registers)
+  // the tile's scalars, in registers for the step (written back by flush)
+  uint64_t rec, rec_end, clk, pend_start, out_addr, out_time;
+  uint32_t blocked, seq, nrep, nrq;
 
-  __device__ Tile(const CP& p, const CS& s, uint32_t l, int out_parity) : P(p), S(s), lt(l), tile(p.tb + l), po(out_parity)
+  __device__ __forceinline__ Tile(const CP& p, const CS& s, uint32_t l, int out_parity) : P(p), S(s), lt(l), tile(p.tb + l), po(out_parity)
   {
     L1 = Cache{S.l1_tag + (size_t)lt * P.s1 * P.a1, S.l1_meta + (size_t)lt * P.s1 * P.a1, S.l1_rr + (size_t)lt * P.s1,
-               S.cc + (size_t)lt * 2 * GG_NUM_CACHE_COUNTERS, P.s1, P.a1, P.log_line, P.pol1, 0};
+               S.cc + (size_t)lt * 2 * GG_NUM_CACHE_COUNTERS, P.s1, P.a1, P.log_line, P.pol1, 0, {}};
     L2 = Cache{S.l2_tag + (size_t)lt * P.s2 * P.a2, S.l2_meta + (size_t)lt * P.s2 * P.a2, S.l2_rr + (size_t)lt * P.s2,
-               S.cc + ((size_t)lt * 2 + 1) * GG_NUM_CACHE_COUNTERS, P.s2, P.a2, P.log_line, P.pol2, 1};
-    st = S.st + (size_t)lt * GG_NUM_TILE_STATS;
+               S.cc + ((size_t)lt * 2 + 1) * GG_NUM_CACHE_COUNTERS, P.s2, P.a2, P.log_line, P.pol2, 1, {}};
+    stg = S.st + (size_t)lt * GG_NUM_TILE_STATS;
+#pragma unroll
+    for (int k = 0; k < GG_NUM_TILE_STATS; ++k) st[k] = 0;
+    rec = S.rec[lt]; rec_end = S.rec_end[lt]; clk = S.clk[lt]; pend_start = S.pend_start[lt];
+    out_addr = S.out_addr[lt]; out_time = S.out_time[lt];
+    blocked = S.blocked[lt]; seq = S.seq[lt]; nrep = S.nrep[lt]; nrq = S.nrq[lt];
   }
-  __device__ void fail(uint32_t e = GG_DERR_STATE) const { atomicOr(S.err, e); }
+  __device__ __forceinline__ void flush()
+  {
+    L1.flush(); L2.flush();
+#pragma unroll
+    for (int k = 0; k < GG_NUM_TILE_STATS; ++k) if (k != GG_CT_CLOCK_PS && st[k]) stg[k] += st[k];
+    stg[GG_CT_CLOCK_PS] = clk;
+    S.rec[lt] = rec; S.clk[lt] = clk; S.pend_start[lt] = pend_start;
+    S.out_addr[lt] = out_addr; S.out_time[lt] = out_time;
+    S.blocked[lt] = blocked; S.seq[lt] = seq; S.nrep[lt] = nrep; S.nrq[lt] = nrq;
+  }
+  __device__ __forceinline__ void fail(uint32_t e = GG_DERR_STATE) const { atomicOr(S.err, e); }
 
   // MemoryManager::sendMsg (…msi/memory_manager.cc:306-332)
-  __device__ void send(uint32_t dst, uint32_t type, uint32_t requester, uint64_t addr, uint64_t t)
+  __device__ __forceinline__ void send(uint32_t dst, uint32_t type, uint32_t requester, uint64_t addr, uint64_t t)
   {
     const uint32_t i = atomicAdd(&S.cnt[po], 1u);
     if (i >= P.msg_cap) { fail(GG_DERR_CAP); return; }
     gg_cmsg m;
     m.addr = addr; m.send_ps = t; m.arrival_ps = t; m.src = tile; m.dst = dst; m.requester = requester;
-    m.seq = S.seq[lt]++; m.type = type; m.link = 0xFFFFFFFFu;
+    m.seq = seq++; m.type = type; m.link = 0xFFFFFFFFu;
     bufp(S, po)[i] = m;
     st[GG_CT_MSGS_SENT]++;
-    st[GG_CT_SENT_BY_TYPE + type - 1]++;
+#pragma unroll
+    for (int k = 0; k < 11; ++k) if (type == (uint32_t)k + 1) st[GG_CT_SENT_BY_TYPE + k]++;
   }
-  __device__ uint32_t home(uint64_t a) const { return (uint32_t)((a >> 6) % P.T); }   // address_home_lookup.cc:19-26
+  __device__ __forceinline__ uint32_t home(uint64_t a) const { return (uint32_t)((a >> 6) % P.T); }   // address_home_lookup.cc:19-26
 
   // ---- directory (DirectoryCache + DirectoryEntryFullMap) ------------------
-  __device__ DEnt* ent(int32_t h) const
+  __device__ __forceinline__ DEnt* ent(int32_t h) const
   {
     return h >= 0 ? S.dir + (size_t)lt * P.E + h : S.rep + (size_t)lt * P.R + (-h - 1);
   }
-  __device__ uint64_t* shw(int32_t h) const
+  __device__ __forceinline__ uint64_t* shw(int32_t h) const
   {
     return h >= 0 ? S.dsh + ((size_t)lt * P.E + h) * P.W : S.rsh + ((size_t)lt * P.R + (-h - 1)) * P.W;
   }
-  __device__ bool has(int32_t h, uint32_t s) const { return (shw(h)[s >> 6] >> (s & 63)) & 1ull; }
-  __device__ void add_sharer(int32_t h, uint32_t s)                 // addSharer (full_map.cc:27-33)
+  __device__ __forceinline__ bool has(int32_t h, uint32_t s) const { return (shw(h)[s >> 6] >> (s & 63)) & 1ull; }
+  __device__ __forceinline__ void add_sharer(int32_t h, uint32_t s)                 // addSharer (full_map.cc:27-33)
   {
     if (has(h, s)) fail();
     shw(h)[s >> 6] |= 1ull << (s & 63); ent(h)->nsh++;
   }
-  __device__ void remove_sharer(int32_t h, uint32_t s)              // removeSharer (:35-41)
+  __device__ __forceinline__ void remove_sharer(int32_t h, uint32_t s)              // removeSharer (:35-41)
   {
     if (!has(h, s)) { fail(); return; }
     shw(h)[s >> 6] &= ~(1ull << (s & 63)); ent(h)->nsh--;
   }
-  __device__ void set_owner(int32_t h, int32_t o)                   // DirectoryEntry::setOwner
+  __device__ __forceinline__ void set_owner(int32_t h, int32_t o)                   // DirectoryEntry::setOwner
   {
     if (o >= 0 && !has(h, (uint32_t)o)) fail();
     ent(h)->owner = o;
   }
-  __device__ uint32_t dset(uint64_t a) const                        // computeSetIndex (directory_cache.cc:332-348)
+  __device__ __forceinline__ uint32_t dset(uint64_t a) const                        // computeSetIndex (directory_cache.cc:332-348)
   {
     uint64_t s = 0;
     const uint64_t mask = (1ull << P.log_dsets) - 1;
@@ -258,30 +341,41 @@ struct Tile {
     return (uint32_t)s;
   }
   // getDirectoryEntry (directory_cache.cc:102-145)
-  __device__ int32_t dget(uint64_t a, uint64_t& t)
+  __device__ __forceinline__ int32_t dget(uint64_t a, uint64_t& t)
   {
     t += P.lat_dir;
     st[GG_CT_DIR_ACCESSES]++;
     const uint32_t base = dset(a) * P.dassoc;
     DEnt* d = S.dir + (size_t)lt * P.E;
-    for (uint32_t i = 0; i < P.dassoc; ++i) if (d[base + i].addr == a) return (int32_t)(base + i);
-    for (uint32_t i = 0; i < P.dassoc; ++i) if (d[base + i].addr == INV_ADDR) { d[base + i].addr = a; return (int32_t)(base + i); }
-    const uint32_t nr = S.nrep[lt];
+    if (P.dassoc <= 16) {                           // every way's address in flight at once
+      uint64_t v[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { v[i] = 0; if (i < (int)P.dassoc) v[i] = d[base + i].addr; }
+      int hit = -1, fr = -1;
+#pragma unroll
+      for (int i = 15; i >= 0; --i) if (i < (int)P.dassoc) { if (v[i] == a) hit = i; if (v[i] == INV_ADDR) fr = i; }
+      if (hit >= 0) return (int32_t)(base + hit);
+      if (fr >= 0) { d[base + fr].addr = a; return (int32_t)(base + fr); }
+    } else {
+      for (uint32_t i = 0; i < P.dassoc; ++i) if (d[base + i].addr == a) return (int32_t)(base + i);
+      for (uint32_t i = 0; i < P.dassoc; ++i) if (d[base + i].addr == INV_ADDR) { d[base + i].addr = a; return (int32_t)(base + i); }
+    }
+    const uint32_t nr = nrep;
     for (uint32_t r = 0; r < nr; ++r) if (ent(-(int32_t)r - 1)->addr == a) return -(int32_t)r - 1;
     return NO_ENT;
   }
   // replaceDirectoryEntry (directory_cache.cc:163-213): the slot gets a fresh
   // entry, the old one moves to the replaced list
-  __device__ int32_t dreplace(uint64_t replaced, uint64_t a, uint64_t& t)
+  __device__ __forceinline__ int32_t dreplace(uint64_t replaced, uint64_t a, uint64_t& t)
   {
     const uint32_t base = dset(replaced) * P.dassoc;
     DEnt* d = S.dir + (size_t)lt * P.E;
     int32_t slot = -1;
     for (uint32_t i = 0; i < P.dassoc; ++i) if (d[base + i].addr == replaced) { slot = (int32_t)(base + i); break; }
     if (slot < 0) { fail(); return NO_ENT; }
-    const uint32_t r = S.nrep[lt];
+    const uint32_t r = nrep;
     if (r >= P.R) { fail(GG_DERR_CAP); return NO_ENT; }
-    S.nrep[lt] = r + 1;
+    nrep = r + 1;
     *ent(-(int32_t)r - 1) = d[slot];
     uint64_t* so = shw(slot); uint64_t* sr = shw(-(int32_t)r - 1);
     for (uint32_t w = 0; w < P.W; ++w) { sr[w] = so[w]; so[w] = 0; }
@@ -293,9 +387,9 @@ struct Tile {
     return slot;
   }
   // invalidateDirectoryEntry (directory_cache.cc:215-231): erase from the replaced list
-  __device__ void dinvalidate(uint64_t a)
+  __device__ __forceinline__ void dinvalidate(uint64_t a)
   {
-    const uint32_t nr = S.nrep[lt];
+    const uint32_t nr = nrep;
     for (uint32_t r = 0; r < nr; ++r) {
       if (ent(-(int32_t)r - 1)->addr != a) continue;
       for (uint32_t k = r; k + 1 < nr; ++k) {
@@ -303,51 +397,51 @@ struct Tile {
         uint64_t* dst = shw(-(int32_t)k - 1); const uint64_t* src = shw(-(int32_t)k - 2);
         for (uint32_t w = 0; w < P.W; ++w) dst[w] = src[w];
       }
-      S.nrep[lt] = nr - 1;
+      nrep = nr - 1;
       return;
     }
     fail();
   }
 
   // ---- per-address request FIFO (HashMapList<IntPtr, ShmemReq*>) -----------
-  __device__ CReq* q() const { return S.rq + (size_t)lt * P.QC; }
-  __device__ uint32_t qcount(uint64_t a) const
+  __device__ __forceinline__ CReq* q() const { return S.rq + (size_t)lt * P.QC; }
+  __device__ __forceinline__ uint32_t qcount(uint64_t a) const
   {
-    const uint32_t n = S.nrq[lt]; uint32_t c = 0;
+    const uint32_t n = nrq; uint32_t c = 0;
     for (uint32_t i = 0; i < n; ++i) c += (q()[i].addr == a);
     return c;
   }
-  __device__ int32_t qfront(uint64_t a) const
+  __device__ __forceinline__ int32_t qfront(uint64_t a) const
   {
-    const uint32_t n = S.nrq[lt];
+    const uint32_t n = nrq;
     for (uint32_t i = 0; i < n; ++i) if (q()[i].addr == a) return (int32_t)i;
     return -1;
   }
-  __device__ void qpush(uint64_t a, uint64_t t, uint32_t type, uint32_t req)
+  __device__ __forceinline__ void qpush(uint64_t a, uint64_t t, uint32_t type, uint32_t req)
   {
-    const uint32_t n = S.nrq[lt];
+    const uint32_t n = nrq;
     if (n >= P.QC) { fail(GG_DERR_CAP); return; }
     q()[n] = CReq{a, t, type, req};
-    S.nrq[lt] = n + 1;
+    nrq = n + 1;
   }
-  __device__ void qpop(uint64_t a)
+  __device__ __forceinline__ void qpop(uint64_t a)
   {
-    const uint32_t n = S.nrq[lt];
+    const uint32_t n = nrq;
     for (uint32_t i = 0; i < n; ++i) {
       if (q()[i].addr != a) continue;
       for (uint32_t k = i; k + 1 < n; ++k) q()[k] = q()[k + 1];
-      S.nrq[lt] = n - 1;
+      nrq = n - 1;
       return;
     }
   }
-  __device__ static void front_time(CReq& r, uint64_t& t)   // ShmemReq::updateTime + updateCurrTime
+  __device__ __forceinline__ static void front_time(CReq& r, uint64_t& t)   // ShmemReq::updateTime + updateCurrTime
   {
     if (r.time < t) r.time = t;
     if (t < r.time) t = r.time;
   }
 
   // ---- DramCntlr / DramPerfModel --------------------------------------------
-  __device__ uint64_t dram_ps(uint64_t t)
+  __device__ __forceinline__ uint64_t dram_ps(uint64_t t)
   {
     const uint64_t pkt_ns = (uint64_t)ceil(t / 1000.0);
     uint64_t qd = 0;
@@ -365,7 +459,7 @@ struct Tile {
   }
 
   // ---- DramDirectoryCntlr: the call chains as a work loop -------------------
-  __device__ void directory_run(Work w, uint64_t& t)
+  __device__ __forceinline__ void directory_run(Work w, uint64_t& t)
   {
     Work stack[WSTACK];
     int sp = 0;
@@ -481,71 +575,79 @@ struct Tile {
     }
   }
 
-  // handleMsgFromL2Cache (:43-96) + processInv/Flush/WbRepFromL2Cache (:410-543)
-  __device__ void directory_msg(const gg_cmsg& m)
+  // handleMsgFromL2Cache (:43-96) + processInv/Flush/WbRepFromL2Cache (:410-543); every
+  // path ends in at most one directory call chain (one call site keeps the lane's
+  // state in registers)
+  __device__ __forceinline__ void directory_msg(const gg_cmsg& m)
   {
     uint64_t t = m.arrival_ps;           // __handleMsgFromNetwork: setCurrTime(packet.time)
     const uint64_t a = m.addr;
+    Work w{a, W_NONE, 0, 0, 0, 0};
     if (m.type == M_EX_REQ || m.type == M_SH_REQ) {
       qpush(a, t, m.type, m.requester);
-      if (qcount(a) == 1) directory_run(Work{a, W_PROC, m.type, m.requester, 0, 0}, t);
-      return;
-    }
-    const int32_t h = dget(a, t);
-    if (h == NO_ENT) { fail(); return; }
-    DEnt* e = ent(h);
-    if (m.type == M_INV_REP) {
-      if (e->dstate != DS_SHARED) { fail(); return; }
-      remove_sharer(h, m.src);
-      if (e->nsh == 0) e->dstate = DS_UNCACHED;
-      const int32_t f = qfront(a);
-      if (f < 0) return;
-      CReq& r = q()[f];
-      front_time(r, t);
-      if (r.type == M_EX_REQ) { if (e->dstate == DS_UNCACHED) directory_run(Work{a, W_PROC, M_EX_REQ, r.requester, 0, 0}, t); }
-      else if (r.type == M_SH_REQ) directory_run(Work{a, W_PROC, M_SH_REQ, r.requester, 0, 0}, t);
-      else { if (e->dstate == DS_UNCACHED) directory_run(Work{a, W_NULLIFY, 0, r.requester, 0, 0}, t); }
-    } else if (m.type == M_FLUSH_REP) {
-      if (e->dstate != DS_MODIFIED) { fail(); return; }
-      remove_sharer(h, m.src);
-      set_owner(h, -1);
-      e->dstate = DS_UNCACHED;
-      const int32_t f = qfront(a);
-      if (f < 0) { (void)dram_ps(t); return; }                      // putDataToDram: queue model, no latency
-      CReq& r = q()[f];
-      front_time(r, t);
-      if (r.type == M_EX_REQ) directory_run(Work{a, W_PROC, M_EX_REQ, r.requester, 1, 0}, t);
-      else if (r.type == M_SH_REQ) { (void)dram_ps(t); directory_run(Work{a, W_PROC, M_SH_REQ, r.requester, 1, 0}, t); }
-      else { (void)dram_ps(t); directory_run(Work{a, W_NULLIFY, 0, r.requester, 0, 0}, t); }
-    } else if (m.type == M_WB_REP) {
-      if (e->dstate != DS_MODIFIED || !has(h, m.src)) { fail(); return; }
-      set_owner(h, -1);
-      e->dstate = DS_SHARED;
-      const int32_t f = qfront(a);
-      if (f < 0) { fail(); return; }
-      CReq& r = q()[f];
-      front_time(r, t);
-      (void)dram_ps(t);
-      if (r.type != M_SH_REQ) { fail(); return; }
-      directory_run(Work{a, W_PROC, M_SH_REQ, r.requester, 1, 0}, t);
+      if (qcount(a) == 1) w = Work{a, W_PROC, m.type, m.requester, 0, 0};
     } else {
-      fail();
+      const int32_t h = dget(a, t);
+      if (h == NO_ENT) { fail(); return; }
+      DEnt* e = ent(h);
+      const uint32_t ds = e->dstate;
+      if (m.type == M_INV_REP) {
+        if (ds != DS_SHARED) { fail(); return; }
+        remove_sharer(h, m.src);
+        const bool unc = e->nsh == 0;
+        if (unc) e->dstate = DS_UNCACHED;
+        const int32_t f = qfront(a);
+        if (f >= 0) {
+          CReq& r = q()[f];
+          front_time(r, t);
+          if (r.type == M_EX_REQ) { if (unc) w = Work{a, W_PROC, M_EX_REQ, r.requester, 0, 0}; }
+          else if (r.type == M_SH_REQ) w = Work{a, W_PROC, M_SH_REQ, r.requester, 0, 0};
+          else { if (unc) w = Work{a, W_NULLIFY, 0, r.requester, 0, 0}; }
+        }
+      } else if (m.type == M_FLUSH_REP) {
+        if (ds != DS_MODIFIED) { fail(); return; }
+        remove_sharer(h, m.src);
+        set_owner(h, -1);
+        e->dstate = DS_UNCACHED;
+        const int32_t f = qfront(a);
+        if (f < 0) { (void)dram_ps(t); return; }                    // putDataToDram: queue model, no latency
+        CReq& r = q()[f];
+        front_time(r, t);
+        if (r.type == M_EX_REQ) w = Work{a, W_PROC, M_EX_REQ, r.requester, 1, 0};
+        else if (r.type == M_SH_REQ) { (void)dram_ps(t); w = Work{a, W_PROC, M_SH_REQ, r.requester, 1, 0}; }
+        else { (void)dram_ps(t); w = Work{a, W_NULLIFY, 0, r.requester, 0, 0}; }
+      } else if (m.type == M_WB_REP) {
+        if (ds != DS_MODIFIED || !has(h, m.src)) { fail(); return; }
+        set_owner(h, -1);
+        e->dstate = DS_SHARED;
+        const int32_t f = qfront(a);
+        if (f < 0) { fail(); return; }
+        CReq& r = q()[f];
+        front_time(r, t);
+        (void)dram_ps(t);
+        if (r.type != M_SH_REQ) { fail(); return; }
+        w = Work{a, W_PROC, M_SH_REQ, r.requester, 1, 0};
+      } else {
+        fail();
+        return;
+      }
     }
+    if (w.kind != W_NONE) directory_run(w, t);
   }
 
   // ---- L1 / L2 controllers ---------------------------------------------------
-  __device__ void l1_invalidate(uint64_t a)                          // l1_cache_cntlr.cc:293-305
+  __device__ __forceinline__ void l1_invalidate(uint64_t a)                          // l1_cache_cntlr.cc:293-305
   {
     uint32_t s, l;
     L1.get(a, s, l);
     if (s != ST_I && !L1.set(a, ST_I, 0)) fail();
   }
-  __device__ void l1_access(uint64_t a, bool wr)                    // l1:182-205 (+ write-through, l2:66-70)
+  __device__ __forceinline__ void l1_access(uint64_t a, bool wr)                    // l1:182-205 (+ write-through, l2:66-70)
   {
     if (!L1.access(a, wr)) fail();
     if (wr && !L2.access(a, true)) fail();
   }
-  __device__ void insert_in_l1(uint64_t a, uint32_t cs)             // l2_cache_cntlr.cc:133-165
+  __device__ __forceinline__ void insert_in_l1(uint64_t a, uint32_t cs)             // l2_cache_cntlr.cc:133-165
   {
     bool ev; uint64_t ea = 0; uint32_t es = 0, el = 0;
     if (!L1.insert(a, cs, 0, ev, ea, es, el)) { fail(); return; }
@@ -556,7 +658,7 @@ struct Tile {
       if (!L2.set(ea, s2, 0)) fail();                                // clearCachedLoc
     }
   }
-  __device__ void l2_insert(uint64_t a, uint32_t cs, uint64_t t)    // l2_cache_cntlr.cc:74-116
+  __device__ __forceinline__ void l2_insert(uint64_t a, uint32_t cs, uint64_t t)    // l2_cache_cntlr.cc:74-116
   {
     bool ev; uint64_t ea = 0; uint32_t es = 0, el = 0;
     if (!L2.insert(a, cs, 1, ev, ea, es, el)) { fail(); return; }
@@ -567,20 +669,19 @@ struct Tile {
       else fail();
     }
   }
-  __device__ void finish(uint64_t start, uint64_t end, uint32_t level)
+  __device__ __forceinline__ void finish(uint64_t start, uint64_t end, uint32_t level)
   {
-    const uint64_t r = S.rec[lt];
+    const uint64_t r = rec;
     const uint64_t lat = end - start;
     if (S.out) S.out[r] = (lat << 2) | level;
     st[GG_CT_ACCESSES]++;
     st[GG_CT_LATENCY_PS] += lat;
-    st[level == GG_LVL_L1 ? GG_CT_L1_HITS : level == GG_LVL_L2 ? GG_CT_L2_HITS : GG_CT_L2_MISSES]++;
-    S.clk[lt] = end;
-    st[GG_CT_CLOCK_PS] = end;
-    S.rec[lt] = r + 1;
+    if (level == GG_LVL_L1) st[GG_CT_L1_HITS]++; else if (level == GG_LVL_L2) st[GG_CT_L2_HITS]++; else st[GG_CT_L2_MISSES]++;
+    clk = end;
+    rec = r + 1;
   }
   // Core::initiateMemoryAccess -> L1CacheCntlr::processMemOpFromCore, first attempt (l1:89-180)
-  __device__ void app_access(uint64_t a, bool wr, uint64_t s)
+  __device__ __forceinline__ void app_access(uint64_t a, bool wr, uint64_t s)
   {
     uint64_t t = s;
     uint32_t cs, loc;
@@ -604,8 +705,8 @@ struct Tile {
       return;
     }
     t += P.lat_l2t;
-    if (S.out_addr[lt] != INV_ADDR) fail();                          // handleMsgFromL1Cache (l2:226-258)
-    S.out_addr[lt] = a; S.out_time[lt] = t;
+    if (out_addr != INV_ADDR) fail();                          // handleMsgFromL1Cache (l2:226-258)
+    out_addr = a; out_time = t;
     const uint32_t h = home(a);
     if (wr) {                                                        // processExReqFromL1Cache (l2:260-282)
       uint32_t x, xl;
@@ -616,31 +717,31 @@ struct Tile {
     } else {
       send(h, M_SH_REQ, tile, a, t);
     }
-    S.blocked[lt] = 1;
-    S.pend_start[lt] = s;
+    blocked = 1;
+    pend_start = s;
   }
   // L2CacheCntlr::handleMsgFromDramDirectory (l2:294-502) + the core's second attempt
-  __device__ void l2_msg(const gg_cmsg& m)
+  __device__ __forceinline__ void l2_msg(const gg_cmsg& m)
   {
     uint64_t t = m.arrival_ps;
     const uint64_t a = m.addr;
     if (m.type == M_EX_REP || m.type == M_SH_REP) {
       const uint32_t cs = m.type == M_EX_REP ? ST_M : ST_S;
-      if (!S.blocked[lt] || S.out_addr[lt] != a) { fail(); return; }
+      if (!blocked || out_addr != a) { fail(); return; }
       l2_insert(a, cs, t);
       insert_in_l1(a, cs);
-      if (S.out_time[lt] > t) fail();
+      if (out_time > t) fail();
       t += P.lat_l2d;
-      S.out_addr[lt] = INV_ADDR;
-      const bool wr = (S.meta[S.rec[lt]] & GG_META_WRITE) != 0;     // access_num == 2 (l1:106-126)
+      out_addr = INV_ADDR;
+      const bool wr = (S.meta[rec] & GG_META_WRITE) != 0;     // access_num == 2 (l1:106-126)
       uint32_t c1, l1;
       L1.get(a, c1, l1);
       const bool hit = wr ? c1 == ST_M : c1 != ST_I;
       if (!hit) { fail(); return; }
       t += P.lat_l1d;
       l1_access(a, wr);
-      S.blocked[lt] = 0;
-      finish(S.pend_start[lt], t, GG_LVL_DIR);
+      blocked = 0;
+      finish(pend_start, t, GG_LVL_DIR);
       return;
     }
     uint32_t c2, loc;
@@ -685,10 +786,15 @@ __device__ __forceinline__ bool chan_lt(const gg_cmsg& a, const gg_cmsg& b)
 
 // A step, lane per owned tile: the inbox (per-channel FIFO, channels merged by
 // (arrival, sender)), then the trace up to the barrier or the next miss.
+// One tile per wave (a one-lane workgroup): the tiles' controller paths diverge
+// completely, so packing 64 tiles into one wave would serialize the union of
+// their paths; one wave per tile costs issue slots the chip has to spare.
 __global__ void __launch_bounds__(64) k_c_tiles(CP P, CS S, int p, uint64_t barrier)
 {
   if (*(volatile uint32_t*)S.quiet) return;
-  const uint32_t lt = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lt = P.tiles_per_block == 1 ? blockIdx.x : blockIdx.x * blockDim.x + threadIdx.x;
+  if (P.tiles_per_block == 1 && threadIdx.x != 0) return;
+  if (lt == 0) S.ri[GG_RI_STEPS]++;
   if (lt >= P.lt) return;
   Tile T(P, S, lt, 1 - p);
   // 1. gather the inbox list
@@ -728,14 +834,15 @@ __global__ void __launch_bounds__(64) k_c_tiles(CP P, CS S, int p, uint64_t barr
   }
   // 2. the trace
   const uint64_t line_mask = ~((1ull << P.log_line) - 1);
-  while (!S.blocked[lt]) {
-    const uint64_t r = S.rec[lt];
-    if (r >= S.rec_end[lt]) break;
+  while (!T.blocked) {
+    const uint64_t r = T.rec;
+    if (r >= T.rec_end) break;
     const uint32_t meta = S.meta[r];
-    const uint64_t s = S.clk[lt] + (uint64_t)((meta & 0x7FFFFFFFu) >> 1) * P.gap_ps;
+    const uint64_t s = T.clk + (uint64_t)((meta & 0x7FFFFFFFu) >> 1) * P.gap_ps;
     if (s >= barrier) break;
     T.app_access(S.addr[r] & line_mask, (meta & GG_META_WRITE) != 0, s);
   }
+  T.flush();
 }
 
 // A step's messages: network latency, then delivery (same shard: the next
@@ -771,7 +878,6 @@ __global__ void k_c_route(CP P, CS S, int p)
   }
 }
 
-__global__ void k_c_count_step(CS S) { if (!*(volatile uint32_t*)S.quiet) S.ri[GG_RI_STEPS]++; }
 
 // Deliver imported (boundary) messages into the inbox of the quantum's first step.
 __global__ void k_c_import(CP P, CS S, const gg_cmsg* in, uint32_t n)
@@ -951,6 +1057,8 @@ static gg_status coh_alloc(gg_ctx* ctx)
   P.dram_proc = (uint64_t)((float)c.line_size / c.dram_bandwidth) + 1;
   P.dram_cost = (uint64_t)(float)c.dram_latency_ns;
   P.msg_cap = (uint64_t)64 * P.T + 65536;
+  // a wave per tile (default; GG_COH_TILES_PER_BLOCK=64 packs a lane per tile, for A/B runs)
+  { const char* e = getenv("GG_COH_TILES_PER_BLOCK"); P.tiles_per_block = (e && atoi(e) == 64) ? 64 : 1; }
   P.np = gg_noc_params(ctx);
   const uint64_t L = P.lt;
   CS& S = C->S;
@@ -1036,8 +1144,10 @@ gg_status gg_coherent_quantum(gg_ctx* ctx, uint64_t q, gg_coherent_status* out)
   for (;;) {
     for (uint32_t k = 0; k < batch; ++k) {
       const int p = (int)((steps + k) & 1);
-      hipLaunchKernelGGL(k_c_count_step, dim3(1), dim3(1), 0, s, C->S);
-      hipLaunchKernelGGL(k_c_tiles, dim3(tb), dim3(64), 0, s, P, C->S, p, barrier);
+      if (P.tiles_per_block == 1)
+        hipLaunchKernelGGL(k_c_tiles, dim3(P.lt), dim3(64), 0, s, P, C->S, p, barrier);
+      else
+        hipLaunchKernelGGL(k_c_tiles, dim3(tb), dim3(64), 0, s, P, C->S, p, barrier);
       hipLaunchKernelGGL(k_c_route, dim3(rb), dim3(256), 0, s, P, C->S, p);
     }
     GG_HIP(hipGetLastError());

@@ -92,24 +92,28 @@ struct HTree {
       } else return;   // duplicate key: the reference aborts (LOG_PRINT_ERROR)
     }
   }
-  __device__ int remove_rec(int node)                          // removeFromTree
+  // removeFromTree (interval_tree.cc:322-356) without recursion: the successor
+  // of a two-child node has no left child, so its removal is the one-child case
+  __device__ void remove_leafish(int node)
   {
     if (nd[node].left < 0) {
       int p = nd[node].parent;
       if (p >= 0) upd_child(p, nd[node].right, (nd[p].first < nd[node].first) ? 2 : 1);
       upd_parent(nd[node].right, p);
       rebalance(p);
-      return node;
-    } else if (nd[node].right < 0) {
+    } else {
       int p = nd[node].parent;
       upd_child(p, nd[node].left, 0);
       upd_parent(nd[node].left, p);
       rebalance(p);
-      return node;
     }
+  }
+  __device__ int remove_rec(int node)
+  {
+    if (nd[node].left < 0 || nd[node].right < 0) { remove_leafish(node); return node; }
     int succ = nd[node].right;
     while (nd[succ].left >= 0) succ = nd[succ].left;           // findMinKeyNode
-    remove_rec(succ);                                          // successor has no left child
+    remove_leafish(succ);                                      // successor has no left child
     uint64_t f = nd[node].first, s = nd[node].second;          // swap key/interval
     nd[node].first = nd[succ].first; nd[node].second = nd[succ].second;
     nd[succ].first = f; nd[succ].second = s;
