@@ -48,6 +48,26 @@ KERNEL_SYMBOL = {"cache_hist": "k_shard_hist", "cache_scatter": "k_shard_scatter
                  "cache_replay": "k_cache_replay_lean", "cache_unshard": "k_unshard"}
 
 
+def pmc_traffic(kernel, tiles, per_tile):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    of this workload (profiles/<round>/summary.json: FETCH_SIZE x2 (16-B loads,
+    MI355X_MICROARCH.md) + WRITE_SIZE, separate passes; tools/gpu_pmc.sh)."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "summary.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("workload", {}).get("tiles") not in (None, tiles) or \
+           d.get("workload", {}).get("per_tile") not in (None, per_tile):
+            continue
+        for k, v in d.get("kernels", {}).items():
+            if k.split("<")[0] == kernel and "hbm_bytes" in v:
+                best = {"bytes": v["hbm_bytes"], "source": os.path.relpath(f, ROOT)}
+    return best
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -60,7 +80,75 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--replay-kernel", type=int, default=0, help="0 = fastest instantiated, 1 = generic")
+    p.add_argument("--coherent-tiles", type=int, default=256,
+                   help="coherent-mode (Mode C) section: total tiles (0 = skip); configs[2] = 256")
+    p.add_argument("--coherent-per-tile", type=int, default=4096, help="coherent-mode accesses per tile")
+    p.add_argument("--coherent-shards", type=int, default=0, help="logical shards (0 = 1, or 8 with --gpus > 1)")
+    p.add_argument("--coherent", action="store_true",
+                   help="run the coherent section on N > 1 ranks too (RCCL all-to-all per quantum)")
     return p.parse_args()
+
+
+def coherent_section(args, world, rank, dev, backend_name):
+    """Mode C: the full MSI protocol (directory, DRAM, NoC, lax-barrier quanta)
+    on the configs[2..4] hotspot trace, tiles sharded over the ranks by logical
+    shard, cross-shard messages exchanged once per quantum (RCCL all-to-all on
+    N > 1).  Timed once (the run is deterministic), checked bit-exact against
+    the C oracle on rank 0 at N = 1, whose run is also the CPU baseline."""
+    import torch
+    from graphite_amd import config as C
+    from graphite_amd import backend as B
+    from graphite_amd import coherent as CO
+    from graphite_amd import dist as D
+    T, N = args.coherent_tiles, args.coherent_per_tile
+    K = args.coherent_shards or (8 if world > 1 else 1)
+    k0, k1 = CO.shard_range(rank, world, K)
+    cfg = C.default_config(T, num_shards=K, shard_begin=k0, shard_end=k1)
+    be = B.Backend(cfg)
+    addr = torch.empty(T * N, dtype=torch.int64, device=dev)
+    meta = torch.empty(T * N, dtype=torch.int32, device=dev)
+    out = torch.zeros(T * N, dtype=torch.int64, device=dev)
+    B.gen_hotspot_trace(addr, meta, 0, T, N, hot_lines=64)
+    offs = np.arange(T + 1, dtype=np.uint64) * np.uint64(N)
+    torch.cuda.synchronize()
+    D.barrier()
+    t0 = time.perf_counter()
+    if world == 1 and K == 1:
+        be.coherent_run(addr, meta, offs, out)
+        quanta = None
+    else:
+        eng = B.CoherentEngine(be, addr, meta, offs, out)
+        quanta = CO.run(eng, cfg.quantum_ns * 1000, K, world, rank, backend_name,
+                        str(dev) if backend_name == "nccl" else "cpu")
+    torch.cuda.synchronize()
+    D.barrier()
+    elapsed = D.max_over_ranks(time.perf_counter() - t0)
+    st, cc, ri = be.coherent_stats()
+    res = {"workload": "configs[2]-style hotspot trace: %d tiles x %d accesses (20%% to 64 shared lines, "
+                       "WRITE 1/3, gap ~2 cycles), MSI full-map directory + DRAM history tree + "
+                       "emesh_hop_counter, quantum 1000 ns, %d logical shard(s)" % (T, N, K),
+           "value": T * N / elapsed, "unit": "accesses/s", "seconds": elapsed,
+           "quanta": int(ri[C.RUN_INFO.index("quanta")]) if quanta is None else quanta,
+           "steps": int(ri[C.RUN_INFO.index("steps")]),
+           "messages": int(ri[C.RUN_INFO.index("net_msgs")] + ri[C.RUN_INFO.index("self_msgs")]),
+           "simulated_ns": int(st[:, 0].max()) // 1000}
+    if rank == 0 and world == 1 and not args.no_verify:
+        from oracle import pyoracle as po
+        a, m, o = po.gen_trace(T, N, hot_lines=64)
+        oc = po.OracleCoherent(C.default_config(T, num_shards=K))
+        c0 = time.perf_counter()
+        ref = oc.run(a, m, o)
+        cdt = time.perf_counter() - c0
+        res["bit_exact_checked"] = bool(np.array_equal(out.cpu().numpy().view(np.uint64), ref) and
+                                        np.array_equal(st, oc.tile_stats()) and
+                                        np.array_equal(cc, oc.cache_counters()))
+        if not res["bit_exact_checked"]:
+            print("bench.py: COHERENT BIT-EXACT CHECK FAILED", file=sys.stderr)
+        res["cpu_baseline"] = {"value": T * N / cdt, "unit": "accesses/s", "cores": 1, "kind": "port",
+                               "sample": "the whole coherent workload, oracle/gg_coherent.inc -O3, 1 thread, "
+                                         "%.2f s" % cdt}
+    be.close()
+    return res
 
 
 def cpu_baseline(tiles, per_tile, threads):
@@ -195,12 +283,21 @@ def main():
                          "path_GB_s": n * ALGO_BYTES_PER_ACCESS / (elapsed / args.steps) / 1e9},
             "bit_exact_checked": verified,
         }
+        prof = pmc_traffic(out["roofline"]["kernel"], T, N)
+        if prof:
+            out["roofline"]["traffic"] = prof["bytes"]
+            out["roofline"]["traffic_source"] = prof["source"]
         if not args.no_cpu_baseline:
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)
             cps, cdt = cpu_baseline(args.cpu_sample_tiles, N, threads)
             out["cpu_baseline"] = {"value": cps, "unit": "accesses/s", "cores": threads, "kind": "port",
                                    "sample": "%d tiles x %d accesses of the same workload, oracle/gg_oracle.c "
                                              "-O3, one tile per thread, %.1f s" % (args.cpu_sample_tiles, N, cdt)}
+    if args.coherent_tiles and (world == 1 or args.coherent):
+        coh = coherent_section(args, world, rank, dev, "nccl")
+        if rank == 0:
+            out["coherent"] = coh
+    if rank == 0:
         print(json.dumps(out))
     if world > 1:
         D.barrier()

@@ -68,11 +68,13 @@ def run(engine, quantum_ps, num_shards, world=1, rank=0, backend=None, device="c
             rcv = torch.empty(world, dtype=torch.int64, device=device)
             dist.all_to_all_single(rcv, cnt)
             recv_counts = [int(x) for x in rcv.cpu().tolist()]
+            home = buf.device
+            send = buf if str(home) == str(torch.device(device)) else buf.to(device)   # gloo: stage through host
             out = torch.empty(sum(recv_counts) * CMSG_BYTES, dtype=torch.uint8, device=device)
-            dist.all_to_all_single(out, buf, [c * CMSG_BYTES for c in recv_counts],
+            dist.all_to_all_single(out, send, [c * CMSG_BYTES for c in recv_counts],
                                    [c * CMSG_BYTES for c in send_counts])
             if len(out):
-                engine.import_(out)
+                engine.import_(out if out.device == home else out.to(home))
             tot = torch.tensor([int(per_shard.sum()), st["active_tiles"], st["blocked_tiles"]],
                                dtype=torch.int64, device=device)
             dist.all_reduce(tot)

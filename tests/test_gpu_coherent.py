@@ -149,3 +149,54 @@ def test_coherent_matches_reference_fixtures(name):
     np.testing.assert_array_equal(nc[:, [C.NET_COUNTERS.index(k) for k in G.NET3]], exp["net"])
     assert ri[C.RUN_INFO.index("quanta")] == exp["quanta"]
     assert ri[C.RUN_INFO.index("steps")] == exp["steps"]
+
+
+def _rank_worker(rank, world, port, T, N, K, outdir):
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch
+    import torch.distributed as dist
+    from graphite_amd import backend as B
+    from graphite_amd import coherent as CO
+    from oracle import pyoracle as po
+    dist.init_process_group("gloo")
+    k0, k1 = CO.shard_range(rank, world, K)
+    cfg = C.default_config(T, num_shards=K, shard_begin=k0, shard_end=k1)
+    a, m, o = po.gen_trace(T, N, hot_lines=32)
+    addr = torch.from_numpy(a.view(np.int64)).cuda()
+    meta = torch.from_numpy(m.view(np.int32)).cuda()
+    out = torch.zeros(len(a), dtype=torch.int64, device="cuda")
+    be = B.Backend(cfg)
+    eng = B.CoherentEngine(be, addr, meta, o, out)
+    CO.run(eng, cfg.quantum_ns * 1000, K, world, rank, "gloo", "cpu")
+    torch.cuda.synchronize()
+    st = be.coherent_stats()[0]
+    res = torch.from_numpy(out.cpu().numpy().copy())
+    sts = torch.from_numpy(st.view(np.int64).copy())
+    dist.all_reduce(res)
+    dist.all_reduce(sts)
+    if rank == 0:
+        np.save(os.path.join(outdir, "out.npy"), res.numpy().view(np.uint64))
+        np.save(os.path.join(outdir, "stats.npy"), sts.numpy().view(np.uint64))
+    dist.destroy_process_group()
+
+
+def test_coherent_two_ranks_one_gpu(tmp_path):
+    """The multi-rank path with the real GPU engines: 2 processes on cuda:0,
+    2 of 4 logical shards each, the cross-shard ShmemMsgs exchanged by
+    all_to_all (gloo, staged through the host) at every quantum boundary
+    (graphite_amd/coherent.run) == the oracle owning all 4 shards."""
+    torch_dev()
+    import socket
+    import torch.multiprocessing as mp
+    from oracle import pyoracle as po
+    s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
+    T, N, K = 32, 600, 4
+    mp.spawn(_rank_worker, args=(2, port, T, N, K, str(tmp_path)), nprocs=2, join=True)
+    a, m, o = po.gen_trace(T, N, hot_lines=32)
+    ref = _oracle_run(C.default_config(T, num_shards=K), a, m, o)
+    np.testing.assert_array_equal(np.load(tmp_path / "out.npy"), ref[0])
+    np.testing.assert_array_equal(np.load(tmp_path / "stats.npy"), ref[1])

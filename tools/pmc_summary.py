@@ -7,7 +7,7 @@ FETCH_SIZE reports half the bytes of 16-B-per-lane loads
 (MI355X_MICROARCH.md §HBM), which is the load width of every kernel on the
 path (dwordx4 record blocks, dwordx4 slot loads); it is doubled here.
 
-usage: pmc_summary.py STATS_CSV PMC_DIR OUT_JSON [label]
+usage: pmc_summary.py STATS_CSV PMC_DIR OUT_JSON [label [tiles per_tile]]
 """
 import csv
 import collections
@@ -43,7 +43,10 @@ def main():
             d["hbm_read_bytes"] = per["FETCH_SIZE"] * 1024 * 2
             d["hbm_write_bytes"] = per["WRITE_SIZE"] * 1024
             d["hbm_bytes"] = d["hbm_read_bytes"] + d["hbm_write_bytes"]
-    json.dump({"label": label, "fetch_size_correction": 2.0, "kernels": kern}, open(out, "w"), indent=1)
+    res = {"label": label, "fetch_size_correction": 2.0, "kernels": kern}
+    if len(sys.argv) > 6:
+        res["workload"] = {"tiles": int(sys.argv[5]), "per_tile": int(sys.argv[6])}
+    json.dump(res, open(out, "w"), indent=1)
 
 
 if __name__ == "__main__":
