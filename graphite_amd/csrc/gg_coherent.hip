@@ -83,6 +83,8 @@ struct CS {
   gg_cmsg* bnd; uint32_t* bnd_cnt;
   uint32_t* scratch;                     // [lt][IC]
   uint32_t* quiet; uint64_t* ri;
+  // hop-by-hop: the step's messages as packet arrays (gg_noc_hbh)
+  uint32_t *pk_src, *pk_dst, *pk_len; uint64_t *pk_t0, *pk_khi, *pk_klo;
   uint64_t* ctr;                         // NoC counters [T][GG_NUM_NET_COUNTERS]
   uint32_t* err;
 };
@@ -845,9 +847,10 @@ __global__ void __launch_bounds__(64) k_c_tiles(CP P, CS S, int p, uint64_t barr
   T.flush();
 }
 
-// A step's messages: network latency, then delivery (same shard: the next
-// step's inbox list; otherwise the quantum-boundary buffer).
-__global__ void k_c_route(CP P, CS S, int p)
+// A step's messages: network latency (closed form, or the arrival the
+// hop-by-hop pipeline computed), then delivery (same shard: the next step's
+// inbox list; otherwise the quantum-boundary buffer).
+__global__ void k_c_route(CP P, CS S, int p, const uint64_t* hbh_arrival)
 {
   if (*(volatile uint32_t*)S.quiet) return;
   const int po = 1 - p;
@@ -861,9 +864,13 @@ __global__ void k_c_route(CP P, CS S, int p)
   int32_t* head = headp(S, po);
   for (uint32_t i = gid; i < n; i += gridDim.x * blockDim.x) {
     gg_cmsg m = B[i];
-    uint64_t zl;
-    m.arrival_ps = route_closed_form(P.np, m.src, m.dst, has_data(m.type) ? P.bits_data : P.bits_req,
-                                     m.send_ps, zl, S.ctr);
+    if (hbh_arrival) {
+      m.arrival_ps = hbh_arrival[i];
+    } else {
+      uint64_t zl;
+      m.arrival_ps = route_closed_form(P.np, m.src, m.dst, has_data(m.type) ? P.bits_data : P.bits_req,
+                                       m.send_ps, zl, S.ctr);
+    }
     atomicAdd((unsigned long long*)&S.ri[m.src == m.dst ? GG_RI_SELF_MSGS : GG_RI_NET_MSGS], 1ull);
     const uint32_t ss = (uint32_t)(((uint64_t)m.src * P.K) / P.T), ds = (uint32_t)(((uint64_t)m.dst * P.K) / P.T);
     if (ss == ds) {
@@ -878,6 +885,21 @@ __global__ void k_c_route(CP P, CS S, int p)
   }
 }
 
+// hop-by-hop: the step's messages as packets, keyed (send time, sender, sequence)
+// — the order the oracle routes a step's batch in (oracle/gg_coherent.inc c_route_step)
+__global__ void k_c_packets(CP P, CS S, int p)
+{
+  if (*(volatile uint32_t*)S.quiet) return;
+  const int po = 1 - p;
+  const uint32_t n = min(S.cnt[po], (uint32_t)P.msg_cap);
+  const gg_cmsg* B = bufp(S, po);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const gg_cmsg m = B[i];
+    S.pk_src[i] = m.src; S.pk_dst[i] = m.dst;
+    S.pk_len[i] = has_data(m.type) ? P.bits_data : P.bits_req;
+    S.pk_t0[i] = m.send_ps; S.pk_khi[i] = m.send_ps; S.pk_klo[i] = ((uint64_t)m.src << 32) | m.seq;
+  }
+}
 
 // Deliver imported (boundary) messages into the inbox of the quantum's first step.
 __global__ void k_c_import(CP P, CS S, const gg_cmsg* in, uint32_t n)
@@ -1012,8 +1034,9 @@ static gg_status coh_alloc(gg_ctx* ctx)
   P.tb = (uint32_t)(((uint64_t)k0 * P.T + P.K - 1) / P.K);
   const uint32_t te = (uint32_t)(((uint64_t)k1 * P.T + P.K - 1) / P.K);
   P.lt = te - P.tb;
-  if (c.net_model == GG_NET_EMESH_HOP_BY_HOP)
-    return gg_fail(GG_ERR_UNSUPPORTED, "coherent mode: emesh_hop_by_hop is not built on the GPU yet");
+  if (c.net_model == GG_NET_EMESH_HOP_BY_HOP && P.K > 1)
+    return gg_fail(GG_ERR_UNSUPPORTED, "coherent mode: emesh_hop_by_hop with more than one logical shard "
+                   "(router queues split by shard) is not built yet");
   if (c.l1d_assoc > 31 || c.l2_assoc > 31) return gg_fail(GG_ERR_UNSUPPORTED, "coherent mode: associativity above 31");
   P.log_line = (uint32_t)ilog2(c.line_size);
   P.s1 = c.l1d_size_kb * 1024u / (c.l1d_assoc * c.line_size); P.a1 = c.l1d_assoc; P.pol1 = c.l1d_policy;
@@ -1078,6 +1101,8 @@ static gg_status coh_alloc(gg_ctx* ctx)
   A(bnd, P.msg_cap); A(bnd_cnt, 1);
   A(scratch, L * P.IC);
   A(quiet, 1); A(ri, GG_NUM_RUN_INFO);
+  const uint64_t pk = (c.net_model == GG_NET_EMESH_HOP_BY_HOP) ? P.msg_cap : 1;
+  A(pk_src, pk); A(pk_dst, pk); A(pk_len, pk); A(pk_t0, pk); A(pk_khi, pk); A(pk_klo, pk);
 #undef A
   if (st == GG_OK) st = dalloc(C, &C->status_dev, 4);
   if (st == GG_OK) st = dalloc(C, &C->ecount_dev, 2 * (uint64_t)P.K + 2);
@@ -1148,7 +1173,15 @@ gg_status gg_coherent_quantum(gg_ctx* ctx, uint64_t q, gg_coherent_status* out)
         hipLaunchKernelGGL(k_c_tiles, dim3(P.lt), dim3(64), 0, s, P, C->S, p, barrier);
       else
         hipLaunchKernelGGL(k_c_tiles, dim3(tb), dim3(64), 0, s, P, C->S, p, barrier);
-      hipLaunchKernelGGL(k_c_route, dim3(rb), dim3(256), 0, s, P, C->S, p);
+      if (ctx->cfg.net_model == GG_NET_EMESH_HOP_BY_HOP) {
+        hipLaunchKernelGGL(k_c_packets, dim3(rb), dim3(256), 0, s, P, C->S, p);
+        if (gg_status e = gg_noc_hbh(ctx, C->S.pk_src, C->S.pk_dst, C->S.pk_len, C->S.pk_t0, C->S.pk_khi,
+                                     C->S.pk_klo, P.msg_cap, C->S.cnt + (1 - p), s))
+          return e;
+        hipLaunchKernelGGL(k_c_route, dim3(rb), dim3(256), 0, s, P, C->S, p, gg_noc_packet_times(ctx));
+      } else {
+        hipLaunchKernelGGL(k_c_route, dim3(rb), dim3(256), 0, s, P, C->S, p, (const uint64_t*)nullptr);
+      }
     }
     GG_HIP(hipGetLastError());
     steps += batch;

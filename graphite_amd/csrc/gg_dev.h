@@ -253,3 +253,8 @@ __device__ __forceinline__ uint64_t route_closed_form(const NocParams& P, uint32
 // accessors of the NoC state (gg_noc.hip) for the coherent path
 gg::NocParams gg_noc_params(gg_ctx* ctx);
 uint64_t* gg_noc_ctr(gg_ctx* ctx);
+// hop-by-hop stage pipeline over up to `cap` packets (*n_dev of them when given);
+// khi / klo: canonical tie-break keys (NULL: the packet index)
+gg_status gg_noc_hbh(gg_ctx* ctx, const uint32_t* src, const uint32_t* dst, const uint32_t* len, const uint64_t* t0,
+                     const uint64_t* khi, const uint64_t* klo, uint64_t cap, const uint32_t* n_dev, hipStream_t s);
+const uint64_t* gg_noc_packet_times(gg_ctx* ctx);   // arrival times of the last pipeline run

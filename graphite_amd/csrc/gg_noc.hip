@@ -39,8 +39,14 @@ __global__ void k_hop_counter(NocParams P, const uint32_t* __restrict__ src, con
 // ---------------------------------------------------------------------------
 // hop-by-hop
 // ---------------------------------------------------------------------------
-struct Ev { uint64_t t; uint32_t id; uint32_t pad; };
-__device__ __forceinline__ bool ev_lt(const Ev& a, const Ev& b) { return a.t < b.t || (a.t == b.t && a.id < b.id); }
+// (time, canonical key, packet): the batch API keys packets by index; the
+// coherent path keys a step's messages by (send time, sender, sequence), the
+// order the oracle sorts its batch into, so no global sort is needed.
+struct Ev { uint64_t t; uint64_t khi; uint64_t klo; uint32_t id; uint32_t pad; };
+__device__ __forceinline__ bool ev_lt(const Ev& a, const Ev& b)
+{
+  return a.t < b.t || (a.t == b.t && (a.khi < b.khi || (a.khi == b.khi && a.klo < b.klo)));
+}
 __device__ void heap_push(Ev* h, uint32_t& n, Ev e)
 {
   uint32_t i = n++;
@@ -78,7 +84,12 @@ struct NocDev {
 
 struct PktState {   // per-packet working state of the current batch
   uint64_t* t; uint64_t* zl; uint64_t* ct; uint32_t* cur;
+  const uint64_t* khi; const uint64_t* klo;   // canonical keys, or NULL (key = packet index)
 };
+__device__ __forceinline__ Ev mkev(const PktState& S, uint64_t t, uint32_t k)
+{
+  return Ev{t, S.khi ? S.khi[k] : 0ull, S.klo ? S.klo[k] : (uint64_t)k, k, 0};
+}
 
 // Stage ids of a packet's chains
 __device__ __forceinline__ uint32_t xchain_of(const NocParams& P, uint32_t s, uint32_t d)
@@ -124,7 +135,7 @@ __global__ void k_inject(NocDev D, const uint32_t* __restrict__ src, const uint3
   const uint64_t b = bucket_off[tile], e = bucket_off[tile + 1];
   Ev* h = heap + b;
   uint32_t n = 0;
-  for (uint64_t i = b; i < e; ++i) { uint32_t k = bucket_ids[i]; heap_push(h, n, Ev{S.t[k], k, 0}); }
+  for (uint64_t i = b; i < e; ++i) { uint32_t k = bucket_ids[i]; heap_push(h, n, mkev(S, S.t[k], k)); }
   HTree tr = D.tree(tile, 5);
   while (n) {
     Ev ev = heap_pop(h, n);
@@ -151,7 +162,7 @@ __global__ void k_chain(NocDev D, int stage, const uint32_t* __restrict__ src, c
   const uint64_t b = bucket_off[c], e = bucket_off[c + 1];
   Ev* h = heap + b;
   uint32_t n = 0;
-  for (uint64_t i = b; i < e; ++i) { uint32_t k = bucket_ids[i]; heap_push(h, n, Ev{S.t[k], k, 0}); }
+  for (uint64_t i = b; i < e; ++i) { uint32_t k = bucket_ids[i]; heap_push(h, n, mkev(S, S.t[k], k)); }
   while (n) {
     Ev ev = heap_pop(h, n);
     const uint32_t k = ev.id;
@@ -170,7 +181,7 @@ __global__ void k_chain(NocDev D, int stage, const uint32_t* __restrict__ src, c
     uint64_t t = S.t[k], zl = S.zl[k], ct = S.ct[k];
     mesh_hop(D, cur, port, len[k], t, zl, ct);
     S.t[k] = t; S.zl[k] = zl; S.ct[k] = ct; S.cur[k] = next;
-    if (!done) heap_push(h, n, Ev{t, k, 0});
+    if (!done) heap_push(h, n, mkev(S, t, k));
     (void)cx; (void)cy;
   }
 }
@@ -185,7 +196,7 @@ __global__ void k_self(NocDev D, const uint32_t* __restrict__ dst, const uint32_
   const uint64_t b = bucket_off[tile], e = bucket_off[tile + 1];
   Ev* h = heap + b;
   uint32_t n = 0;
-  for (uint64_t i = b; i < e; ++i) { uint32_t k = bucket_ids[i]; heap_push(h, n, Ev{S.t[k], k, 0}); }
+  for (uint64_t i = b; i < e; ++i) { uint32_t k = bucket_ids[i]; heap_push(h, n, mkev(S, S.t[k], k)); }
   while (n) {
     Ev ev = heap_pop(h, n);
     const uint32_t k = ev.id;
@@ -202,9 +213,12 @@ __global__ void k_self(NocDev D, const uint32_t* __restrict__ dst, const uint32_
 }
 
 // bucket keys: 0 = injection (src tile), 1 = X chain, 2 = Y chain, 3 = SELF (dst tile); ~0 = not in stage
+__device__ __forceinline__ uint64_t batch_n(uint64_t n, const uint32_t* n_dev) { return n_dev ? min((uint64_t)*n_dev, n) : n; }
+
 __global__ void k_keys(NocParams P, int stage, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
-                       uint64_t n, uint32_t* keys, uint32_t* counts, uint32_t* err)
+                       uint64_t cap, const uint32_t* n_dev, uint32_t* keys, uint32_t* counts, uint32_t* err)
 {
+  const uint64_t n = batch_n(cap, n_dev);
   const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
   const uint32_t s = src[k], d = dst[k];
@@ -235,9 +249,10 @@ __global__ void k_scan_counts(const uint32_t* counts, uint32_t nb, uint64_t* off
   for (uint32_t i = t * per; i < min(nb, (t + 1) * per); ++i) { off[i] = a; cursor[i] = 0; a += counts[i]; }
 }
 
-__global__ void k_bucket(const uint32_t* __restrict__ keys, uint64_t n, const uint64_t* __restrict__ off,
-                         uint32_t* cursor, uint32_t* ids)
+__global__ void k_bucket(const uint32_t* __restrict__ keys, uint64_t cap, const uint32_t* n_dev,
+                         const uint64_t* __restrict__ off, uint32_t* cursor, uint32_t* ids)
 {
+  const uint64_t n = batch_n(cap, n_dev);
   const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
   const uint32_t key = keys[k];
@@ -245,8 +260,10 @@ __global__ void k_bucket(const uint32_t* __restrict__ keys, uint64_t n, const ui
   ids[off[key] + atomicAdd(&cursor[key], 1u)] = (uint32_t)k;
 }
 
-__global__ void k_init_pkts(const uint32_t* __restrict__ src, const uint64_t* __restrict__ t0, uint64_t n, PktState S)
+__global__ void k_init_pkts(const uint32_t* __restrict__ src, const uint64_t* __restrict__ t0, uint64_t cap,
+                            const uint32_t* n_dev, PktState S)
 {
+  const uint64_t n = batch_n(cap, n_dev);
   const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
   S.t[k] = t0[k]; S.zl[k] = 0; S.ct[k] = 0; S.cur[k] = src[k];
@@ -391,37 +408,56 @@ gg_status gg_noc_run(gg_ctx* ctx, const gg_packets* pk, const gg_packet_out* out
   }
   if (P.net_model != GG_NET_EMESH_HOP_BY_HOP) return gg_fail(GG_ERR_UNSUPPORTED, "network model %u", P.net_model);
   if (P.w * P.h != P.tiles) return gg_fail(GG_ERR_UNSUPPORTED, "emesh_hop_by_hop needs a full W x H mesh (hop_by_hop.cc:55-59)");
-  const uint32_t nb_max = std::max(P.tiles, 2 * std::max(P.w, P.h));
-  if (gg_status st = noc_grow(S, n, nb_max)) return st;
-  NocDev D{P, S->q, S->nd, S->fl, S->ctr, ctx->err_dev};
-  PktState PS{S->t, S->zl, S->ct, S->cur};
-  gg_timer_begin(ctx, "noc_hop_by_hop", s);
-  hipLaunchKernelGGL(k_init_pkts, dim3(blocks), dim3(256), 0, s, pk->src_dev, pk->time_ps_dev, n, PS);
-  for (int stage = 0; stage < 4; ++stage) {
-    const uint32_t nb = (stage == 0 || stage == 3) ? P.tiles : (stage == 1 ? 2 * P.h : 2 * P.w);
-    GG_HIP(hipMemsetAsync(S->counts, 0, 4 * (nb + 1), s));
-    hipLaunchKernelGGL(k_keys, dim3(blocks), dim3(256), 0, s, P, stage, pk->src_dev, pk->dst_dev, n, S->keys,
-                       S->counts, ctx->err_dev);
-    hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, S->counts, nb, S->off, S->cursor);
-    hipLaunchKernelGGL(k_bucket, dim3(blocks), dim3(256), 0, s, S->keys, n, S->off, S->cursor, S->ids);
-    const uint32_t tb = (nb + 63) / 64;
-    if (stage == 0)
-      hipLaunchKernelGGL(k_inject, dim3(tb), dim3(64), 0, s, D, pk->src_dev, pk->dst_dev, pk->length_bits_dev,
-                         S->off, S->ids, S->heap, PS);
-    else if (stage == 3)
-      hipLaunchKernelGGL(k_self, dim3(tb), dim3(64), 0, s, D, pk->dst_dev, pk->length_bits_dev, S->off, S->ids,
-                         S->heap, PS);
-    else
-      hipLaunchKernelGGL(k_chain, dim3(tb), dim3(64), 0, s, D, stage - 1, pk->src_dev, pk->dst_dev,
-                         pk->length_bits_dev, S->off, S->ids, S->heap, PS, nb);
-    GG_HIP(hipGetLastError());
-  }
-  gg_timer_end(ctx, "noc_hop_by_hop", s);
+  if (gg_status st = gg_noc_hbh(ctx, pk->src_dev, pk->dst_dev, pk->length_bits_dev, pk->time_ps_dev, nullptr, nullptr,
+                                n, nullptr, s))
+    return st;
   GG_HIP(hipMemcpyAsync(out->arrival_ps_dev, S->t, 8 * n, hipMemcpyDeviceToDevice, s));
   GG_HIP(hipMemcpyAsync(out->zero_load_ps_dev, S->zl, 8 * n, hipMemcpyDeviceToDevice, s));
   GG_HIP(hipMemcpyAsync(out->contention_ps_dev, S->ct, 8 * n, hipMemcpyDeviceToDevice, s));
   return GG_OK;
 }
+
+// The hop-by-hop stage pipeline over up to `cap` packets; the packet count is
+// `cap` or, when n_dev is given, *n_dev read on the device (the coherent path
+// launches whole batches of steps without a host sync).  Arrival / zero-load /
+// contention land in the NoC state's packet arrays (gg_noc_packet_times).
+gg_status gg_noc_hbh(gg_ctx* ctx, const uint32_t* src, const uint32_t* dst, const uint32_t* len, const uint64_t* t0,
+                     const uint64_t* khi, const uint64_t* klo, uint64_t cap, const uint32_t* n_dev, hipStream_t s)
+{
+  gg_noc_state* S = ctx->noc;
+  const NocParams& P = S->P;
+  if (P.net_model != GG_NET_EMESH_HOP_BY_HOP) return gg_fail(GG_ERR_UNSUPPORTED, "network model %u", P.net_model);
+  if (P.w * P.h != P.tiles) return gg_fail(GG_ERR_UNSUPPORTED, "emesh_hop_by_hop needs a full W x H mesh (hop_by_hop.cc:55-59)");
+  if (cap >= (1ull << 32)) return gg_fail(GG_ERR_RANGE, "batch larger than 2^32 packets");
+  const uint32_t nb_max = std::max(P.tiles, 2 * std::max(P.w, P.h));
+  if (gg_status st = noc_grow(S, cap, nb_max)) return st;
+  NocDev D{P, S->q, S->nd, S->fl, S->ctr, ctx->err_dev};
+  PktState PS{S->t, S->zl, S->ct, S->cur, khi, klo};
+  const uint32_t blocks = (uint32_t)((cap + 255) / 256);
+  gg_timer_begin(ctx, "noc_hop_by_hop", s);
+  hipLaunchKernelGGL(k_init_pkts, dim3(blocks), dim3(256), 0, s, src, t0, cap, n_dev, PS);
+  for (int stage = 0; stage < 4; ++stage) {
+    const uint32_t nb = (stage == 0 || stage == 3) ? P.tiles : (stage == 1 ? 2 * P.h : 2 * P.w);
+    GG_HIP(hipMemsetAsync(S->counts, 0, 4 * (nb + 1), s));
+    hipLaunchKernelGGL(k_keys, dim3(blocks), dim3(256), 0, s, P, stage, src, dst, cap, n_dev, S->keys,
+                       S->counts, ctx->err_dev);
+    hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, S->counts, nb, S->off, S->cursor);
+    hipLaunchKernelGGL(k_bucket, dim3(blocks), dim3(256), 0, s, S->keys, cap, n_dev, S->off, S->cursor, S->ids);
+    const uint32_t tb = (nb + 63) / 64;
+    if (stage == 0)
+      hipLaunchKernelGGL(k_inject, dim3(tb), dim3(64), 0, s, D, src, dst, len, S->off, S->ids, S->heap, PS);
+    else if (stage == 3)
+      hipLaunchKernelGGL(k_self, dim3(tb), dim3(64), 0, s, D, dst, len, S->off, S->ids, S->heap, PS);
+    else
+      hipLaunchKernelGGL(k_chain, dim3(tb), dim3(64), 0, s, D, stage - 1, src, dst, len, S->off, S->ids, S->heap,
+                         PS, nb);
+    GG_HIP(hipGetLastError());
+  }
+  gg_timer_end(ctx, "noc_hop_by_hop", s);
+  return GG_OK;
+}
+
+const uint64_t* gg_noc_packet_times(gg_ctx* ctx) { return ctx->noc->t; }
 
 gg_status gg_noc_counters(gg_ctx* ctx, uint64_t* out)
 {

@@ -53,6 +53,9 @@ def _compare(cfg, a, m, o):
     (64, 1200, 64, 1, C.NET_EMESH_HOP_COUNTER),
     (64, 1000, 32, 8, C.NET_EMESH_HOP_COUNTER),     # 8 logical shards, quantum-boundary delivery
     (256, 300, 64, 4, C.NET_EMESH_HOP_COUNTER),
+    (16, 1500, 8, 1, C.NET_EMESH_HOP_BY_HOP),      # configs[2]: router / link contention
+    (64, 700, 64, 1, C.NET_EMESH_HOP_BY_HOP),
+    (256, 200, 64, 1, C.NET_EMESH_HOP_BY_HOP),
 ])
 def test_coherent_matches_oracle(T, N, hot, K, net):
     from oracle import pyoracle as po
@@ -129,7 +132,7 @@ def test_coherent_rejects_unbuilt_config():
     torch = torch_dev()
     from graphite_amd import backend as B
     from oracle import pyoracle as po
-    cfg = C.default_config(16, net_model=C.NET_EMESH_HOP_BY_HOP)
+    cfg = C.default_config(16, net_model=C.NET_EMESH_HOP_BY_HOP, num_shards=2)   # router queues split by shard: not built
     a, m, o = po.gen_trace(16, 10)
     be = B.Backend(cfg)
     with pytest.raises(B.GGError):
