@@ -8,16 +8,16 @@ the configs[1] uniform-random private generator, 32 KB/4-way L1-D + 512 KB/8-way
 L2 (carbon_sim.cfg defaults), private-cache (decoupled) mode.  The coherent
 MSI + hop-by-hop mode of configs[3] is not built yet.
 `--tiles 64 --per-tile 4194304` runs configs[1] exactly.  One step = one full
-replay of the batch from the constructor cache state: the stable (tile,
-L1-D set) partition kernels + the replay kernel (graphite_amd/csrc/gg_cache.hip),
-inputs resident in HBM.
+replay of the batch from the constructor cache state: the single-pass
+streaming replay kernel k_cache_stream (graphite_amd/csrc/gg_cache.hip; one
+workgroup per tile), inputs resident in HBM.
 
 Multi-GPU: one process per GPU (torchrun); rank r simulates its own tiles
 (global tiles r*T .. r*T+T-1) — units are independent in private mode, so
 there is no collective on the data path ("weak" scaling); only the timing is
 max-reduced over ranks (graphite_amd/dist.py).
 
-Also reported: the replay kernel's roofline (algorithmic 16 B/access: 8 B
+Also reported: the dominant kernel's roofline (algorithmic 16 B/access: 8 B
 address + 4 B metadata in, 4 B result out) from HIP
 events on its own stream, and the CPU baseline (the C oracle, a bounded sample,
 threads = cores used).  Bit-exactness is checked in the same run: one tile's
@@ -39,12 +39,13 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 ALGO_BYTES_PER_ACCESS = 16     # whole path: 8 B addr + 4 B meta in, 4 B result out
 # Algorithmic bytes per access of each kernel of the path
 KERNEL_BYTES = {
+    "cache_stream": 16,    # single pass (default): read addr (8) + meta (4), write result (4); state < 1%
     "cache_hist": 8,       # read addr (+ per-chunk set counts, scans: < 1%)
     "cache_scatter": 24,   # read addr + meta (12), write key (8) + record slot (4)
     "cache_replay": 12,    # read key (8), write result in slot order (4); state load/store < 1%
     "cache_unshard": 12,   # read slot (4) + result (4), write program-order result (4)
 }
-KERNEL_SYMBOL = {"cache_hist": "k_shard_hist", "cache_scatter": "k_shard_scatter",
+KERNEL_SYMBOL = {"cache_stream": "k_cache_stream", "cache_hist": "k_shard_hist", "cache_scatter": "k_shard_scatter",
                  "cache_replay": "k_cache_replay_lean", "cache_unshard": "k_unshard"}
 
 
@@ -79,7 +80,8 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu count)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
-    p.add_argument("--replay-kernel", type=int, default=0, help="0 = fastest instantiated, 1 = generic")
+    p.add_argument("--replay-kernel", type=int, default=0,
+                   help="0 = single-pass streaming replay, 1 = sharded generic, 2 = sharded lean")
     p.add_argument("--coherent-tiles", type=int, default=256,
                    help="coherent-mode (Mode C) section: total tiles (0 = skip); configs[2] = 256")
     p.add_argument("--coherent-per-tile", type=int, default=4096, help="coherent-mode accesses per tile")
@@ -250,6 +252,9 @@ def main():
         value = total / elapsed
         kern = {}
         for k, v in kms.items():
+            v = [x for x in v if x >= 0]          # kernels of this path only (negative = not launched)
+            if not v:
+                continue
             ms = float(np.mean(v[1:] if len(v) > 1 else v))
             kern[k] = {"ms": ms, "bytes_per_access": KERNEL_BYTES[k],
                        "GB_s": n * KERNEL_BYTES[k] / (ms * 1e-3) / 1e9}

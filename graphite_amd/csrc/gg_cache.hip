@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <cstdio>
 
 namespace {
 
@@ -784,7 +785,8 @@ __device__ __forceinline__ uint32_t lru_nib(uint32_t ages, uint32_t way)
 {
   const uint32_t sh = 4 * way;
   const uint32_t acc = (ages >> sh) & 0xFu;
-  const uint32_t x = (ages | 0x88888888u) - acc * 0x11111111u;   // bit 3 of a nibble: age >= acc
+  // acc in every nibble (v_perm byte broadcast instead of a 32-bit multiply)
+  const uint32_t x = (ages | 0x88888888u) - __builtin_amdgcn_perm(0u, acc | (acc << 4), 0u);  // bit 3: age >= acc
   const uint32_t lt = ~x & 0x88888888u;
   return (ages + (lt >> 3)) & ~(0xFu << sh);
 }
@@ -1108,6 +1110,534 @@ __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_
 }
 
 // ---------------------------------------------------------------------------
+// Streaming replay (the default batch path): ONE kernel, one workgroup per
+// tile, reading the caller's program-order trace once and writing each
+// result once (16 B of HBM per access: 8 addr + 4 meta in, 4 result out).
+//
+//   * NCW consumer waves = the tile's u1 units (lane = L1-D set), each
+//     running the access step of k_cache_replay_lean on its unit.  The tile's
+//     L2 sets stay in LDS for the whole batch ([s][q][u] uint4, 16-B lane
+//     stride: conflict-free ds_read_b128), the L1-D set in VGPRs.
+//   * one producer wave streams the tile's records (4 rounds of 64 coalesced
+//     8-B + 4-B loads in flight while the previous 4 are distributed) and
+//     appends each to its unit's LDS ring (kRing records per unit).  Records
+//     of one round that name the same unit are ranked by lane (log2 u1
+//     ballots), so every unit receives its records in program order — the
+//     only order the reference's per-set state depends on.
+//   * hand-off: the producer writes ring slots, waits for them
+//     (lgkmcnt), then publishes the unit's tail; a consumer reads the tail
+//     before the slot (volatile, so in issue order; one CU's LDS serves a
+//     wave's instructions in order).  A consumer publishes its head after
+//     each access; the producer waits for ring space on it.  Both waits are
+//     bounded: consumers always drain a published record, and the producer
+//     publishes at most kRing records of a unit per sub-round.
+//   * ring entry: high word = the 32-bit L2 tag; low word = WRITE (bit 0),
+//     L2 set within the unit (bits 1..log2 S2), the record's index within the
+//     tile above that; the consumer stores its result word straight to
+//     result[tile base + index] (scattered dword stores that fill whole lines
+//     in L2 while the tile's window is in flight).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kRing = 32;
+constexpr int kMaskRounds = 4;              // producer rounds matched at once (LDS peer masks)
+constexpr uint32_t kSpinLimit = 1u << 22;   // s_sleep(1) polls (~64 cycles each) before giving up
+constexpr uint16_t kLgkm0 = 0xC07F;         // s_waitcnt lgkmcnt(0) (vmcnt/expcnt fields at their maxima)
+
+size_t stream_lds_bytes(uint32_t u1, uint32_t s2, uint32_t a2)
+{
+  const size_t tq = (a2 + 3) / 4;
+  return (size_t)s2 * u1 * (tq * 16 + 8) + (size_t)kRing * u1 * 8 + (size_t)u1 * 12 + 16 + (size_t)kMaskRounds * u1 * 8 + (size_t)u1 * 4;
+}
+
+template <int A1, int A2, bool LRU1, bool LRU2, int NCW, bool EV>
+__global__ __launch_bounds__((NCW + 1) * GG_WAVE) void k_cache_stream(gg_cache_state cs, gg_geom g,
+    const uint64_t* __restrict__ addr, const uint32_t* __restrict__ meta, const uint64_t* __restrict__ tile_off,
+    uint32_t* __restrict__ result, uint64_t* __restrict__ evicted, uint32_t* err, unsigned long long* dbg)
+{
+  static_assert(A1 <= 4 && A2 <= 8, "streaming replay covers L1-D assoc <= 4, L2 assoc <= 8");
+  constexpr uint32_t U1 = NCW * GG_WAVE;   // == g.u1 (host-checked)
+  constexpr int TQ = (A2 + 3) / 4;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t S2 = g.s2;
+  uint4* T = reinterpret_cast<uint4*>(smem);                                            // [s][q][u]
+  uint2* Mt = reinterpret_cast<uint2*>(smem + (size_t)S2 * U1 * TQ * 16);                // [s][u]
+  uint64_t* ring = reinterpret_cast<uint64_t*>(smem + (size_t)S2 * U1 * (TQ * 16 + 8));  // [kRing][u]
+  uint32_t* tailp = reinterpret_cast<uint32_t*>(ring + kRing * U1);                      // [u]
+  uint32_t* headp = tailp + U1;                                                          // [u]
+  uint32_t* resv = headp + U1;                                                           // [u] producer-private
+  uint32_t* donep = resv + U1;
+  uint64_t* pmask = reinterpret_cast<uint64_t*>(donep + 4);                              // [kMaskRounds][u]
+  uint32_t* dummy = reinterpret_cast<uint32_t*>(pmask + kMaskRounds * U1);               // [u] sink of masked-off writes
+  // Cross-wave LDS words go through relaxed workgroup-scope atomics: they stay
+  // ds_* instructions (a volatile generic pointer would become a flat access)
+  // and keep their program order.
+  auto ld32 = [](uint32_t* q) { return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+  auto ld64 = [](uint64_t* q) { return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+  auto st32 = [](uint32_t* q, uint32_t v) { __hip_atomic_store(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+  auto st64 = [](uint64_t* q, uint64_t v) { __hip_atomic_store(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+
+  const uint32_t tile = blockIdx.x;
+  const uint64_t base = tile_off[tile];
+  const uint32_t n = (uint32_t)(tile_off[tile + 1] - base);
+  const uint32_t wave = threadIdx.x / GG_WAVE, lane = threadIdx.x % GG_WAVE;
+  const uint32_t log_s2 = (uint32_t)__builtin_ctz(S2);
+  const bool producer = wave == NCW;
+
+  // ---- consumer: load + re-pack the unit's state (as k_cache_replay_lean) ----
+  const uint32_t u = producer ? 0u : threadIdx.x;
+  const uint64_t gu = (uint64_t)tile * U1 + u;
+  const uint32_t l1set = u;
+  uint32_t errv = 0;
+  uint32_t st1 = 0, a1 = 0xFFFFFFFFu, pos1 = 0xFFFFFFFFu, rr1 = 0;
+  auto tag_at = [&](uint32_t s, uint32_t w) -> uint32_t& {
+    return reinterpret_cast<uint32_t*>(&T[((size_t)s * TQ + w / 4) * U1 + u])[w % 4];
+  };
+  if (!producer) {
+    uint64_t t1[A1];
+    const uint64_t m1 = cs.l1_meta[gu];
+#pragma unroll
+    for (int w = 0; w < A1; ++w) {
+      t1[w] = cs.l1_tag[(uint64_t)w * g.units + gu];
+      const uint32_t b = (uint32_t)(m1 >> (8 * w)) & 0xFFu;
+      const uint32_t st = (t1[w] == GG_L1_INV_TAG) ? 0u : GG_M_STATE(b);
+      errv |= (t1[w] != GG_L1_INV_TAG && st == GG_MS_I) ? GG_DERR_STATE : 0u;
+      st1 |= st << (2 * w);
+      a1 = (a1 & ~(0xFu << (4 * w))) | ((GG_M_AGE(b) & 0xFu) << (4 * w));
+    }
+    rr1 = cs.l1_rr[gu];
+    uint32_t nheld = 0;
+    for (uint32_t s = 0; s < S2; ++s) {
+      uint32_t tg[4 * TQ];
+#pragma unroll
+      for (int w = 0; w < 4 * TQ; ++w)
+        tg[w] = (w < A2) ? cs.l2_tag[(uint64_t)(s * A2 + w) * g.units + gu] : GG_L2_INV_TAG;
+      const uint64_t mw = cs.l2_meta[(uint64_t)s * g.units + gu];
+      uint32_t ages = 0xFFFFFFFFu, st = 0;
+#pragma unroll
+      for (int w = 0; w < A2; ++w) {
+        const uint32_t b = (uint32_t)(mw >> (8 * w)) & 0xFFu;
+        const bool valid = tg[w] != GG_L2_INV_TAG;
+        errv |= (valid != (GG_M_STATE(b) != GG_MS_I)) ? GG_DERR_STATE : 0u;
+        st |= (valid ? GG_M_STATE(b) : 0u) << (2 * w);
+        ages = (ages & ~(0xFu << (4 * w))) | ((GG_M_AGE(b) & 0xFu) << (4 * w));
+        const uint64_t ln = ((uint64_t)tg[w] << g.log_l2) | ((uint64_t)s << g.log_u1) | l1set;
+        int hw = -1;
+#pragma unroll
+        for (int k = 0; k < A1; ++k) hw = (valid && ((st1 >> (2 * k)) & 3u) && t1[k] == ln) ? k : hw;
+        nheld += (hw >= 0) ? 1u : 0u;
+        errv |= ((GG_M_LOC(b) != 0) != (hw >= 0)) ? GG_DERR_STATE : 0u;
+        if (hw >= 0) pos1 = (pos1 & ~(0xFFu << (8 * hw))) | ((s * A2 + w) << (8 * hw));
+      }
+#pragma unroll
+      for (int q = 0; q < TQ; ++q)
+        T[((size_t)s * TQ + q) * U1 + u] = make_uint4(tg[4 * q], tg[4 * q + 1], tg[4 * q + 2], tg[4 * q + 3]);
+      const uint32_t rr = LRU2 ? 0u : cs.l2_rr[(uint64_t)s * g.units + gu];
+      Mt[s * U1 + u] = make_uint2(ages, st | (rr << 16));
+    }
+    uint32_t nvalid = 0;
+#pragma unroll
+    for (int k = 0; k < A1; ++k) nvalid += ((st1 >> (2 * k)) & 3u) ? 1u : 0u;
+    if (nvalid != nheld) errv |= GG_DERR_STATE;
+  } else {
+    for (uint32_t k = lane; k < U1; k += GG_WAVE) { tailp[k] = 0; headp[k] = 0; resv[k] = 0; }
+    for (uint32_t k = lane; k < kMaskRounds * U1; k += GG_WAVE) pmask[k] = 0;
+    if (lane == 0) *donep = 0;
+  }
+  __syncthreads();
+
+  if (producer) {
+    // ---------------- producer: program-order trace -> per-unit rings ----------------
+    // Batches of K rounds x 64 records; the next batch's loads are in flight
+    // while this one is classified, reserved (one ds_add_rtn per (round, unit)
+    // on resv[], all rounds at once), checked for ring space and written.
+    constexpr int K = 8;
+    const uint64_t* ap = addr + base;
+    const uint32_t* mp = meta + base;
+    const uint64_t lt_mask = (1ull << lane) - 1;
+    // three batches in registers: this one, and the next two in flight
+    uint64_t pa[K], na[K], qa[K];
+    uint32_t pm[K], nm[K], qm[K];
+    uint32_t bad = 0;
+    bool hung = false;
+    uint32_t d_batch = 0, d_slow = 0, d_spin = 0;
+    // unconditional loads (index clamped to the tile's last record): no
+    // branches around them, so the waits stay per-register
+    auto load = [&](uint32_t c0, uint64_t (&a)[K], uint32_t (&m)[K]) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const uint32_t j = min(c0 + k * GG_WAVE + lane, n - 1);
+        a[k] = __builtin_nontemporal_load(ap + j);
+        m[k] = __builtin_nontemporal_load(mp + j);
+      }
+    };
+    // one batch: classify, reserve, check space, write, publish
+    auto batch = [&](const uint32_t c, const uint64_t (&pa)[K], const uint32_t (&pm)[K]) {
+      // classify and rank (lanes of a round naming the same unit, in lane order);
+      // per round one packed word: unit (9 bits, U1 = no record), rank (7),
+      // count (7), first lane of the unit (6)
+      uint64_t key[K];
+      uint32_t inf[K], p[K];
+      constexpr int KM = kMaskRounds;
+      auto f_set = [](uint32_t w) { return w & 0x1FFu; };
+      auto f_rank = [](uint32_t w) { return (w >> 9) & 0x7Fu; };
+      auto f_cnt = [](uint32_t w) { return (w >> 16) & 0x7Fu; };
+      auto f_lead = [](uint32_t w) { return w >> 23; };
+      // unit of each record (U1 = no record) and its ring entry
+      uint32_t set[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const uint32_t j = c + k * GG_WAVE + lane;
+        const bool valid = j < n;
+        bad |= (valid && pa[k] >= g.addr_limit) ? 1u : 0u;
+        const uint64_t line = pa[k] >> g.log_line;
+        set[k] = valid ? (uint32_t)line & (U1 - 1) : U1;
+        key[k] = ((uint64_t)(uint32_t)(line >> g.log_l2) << 32) | (j << (1 + log_s2)) |
+                 ((((uint32_t)line >> g.log_u1) & (S2 - 1)) << 1) | (pm[k] & GG_META_WRITE);
+      }
+      // lanes of a round naming the same unit: OR the lane bits into a per-unit
+      // LDS mask (commutative, so deterministic), read it back, clear it
+#pragma unroll
+      for (int h = 0; h < K; h += KM) {
+#pragma unroll
+        for (int k = h; k < h + KM; ++k)
+          if (set[k] < U1)
+            __hip_atomic_fetch_or(&pmask[(k - h) * U1 + set[k]], 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        uint64_t peers[KM];
+#pragma unroll
+        for (int k = h; k < h + KM; ++k) peers[k - h] = set[k] < U1 ? ld64(&pmask[(k - h) * U1 + set[k]]) : 0ull;
+#pragma unroll
+        for (int k = h; k < h + KM; ++k)
+          if (set[k] < U1) st64(&pmask[(k - h) * U1 + set[k]], 0ull);
+#pragma unroll
+        for (int k = h; k < h + KM; ++k) {
+          const uint64_t pr = peers[k - h];
+          const uint32_t lead = pr ? (uint32_t)__builtin_ctzll(pr) : lane;
+          inf[k] = set[k] | ((uint32_t)__popcll(pr & lt_mask) << 9) | ((uint32_t)__popcll(pr) << 16) | (lead << 23);
+        }
+      }
+      // reserve ring positions: the round's first lane of each unit adds the
+      // round's count (atomics of one wave execute in issue order)
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        p[k] = (f_set(inf[k]) < U1 && f_rank(inf[k]) == 0)
+                   ? __hip_atomic_fetch_add(&resv[f_set(inf[k])], f_cnt(inf[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+                   : 0u;
+#pragma unroll
+      for (int k = 0; k < K; ++k) p[k] = (uint32_t)__shfl((int)p[k], (int)f_lead(inf[k])) + f_rank(inf[k]);
+      // fast path: every record of the batch fits within kRing of its unit's
+      // published tail (so waiting for consumer heads terminates)
+      bool fits = true;
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        fits = fits && (f_set(inf[k]) == U1 || p[k] - ld32(&tailp[f_set(inf[k])]) < kRing);
+      ++d_batch;
+      if (__ballot(!fits) == 0) {
+        for (uint32_t spin = 0;; ++spin, ++d_spin) {
+          bool ok = true;
+#pragma unroll
+          for (int k = 0; k < K; ++k) ok = ok && (f_set(inf[k]) == U1 || p[k] - ld32(&headp[f_set(inf[k])]) < kRing);
+          if (__ballot(!ok) == 0) break;
+          if (spin == kSpinLimit) { hung = true; break; }
+          __builtin_amdgcn_s_sleep(1);
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+          if (f_set(inf[k]) < U1) st64(&ring[(p[k] % kRing) * U1 + f_set(inf[k])], key[k]);
+        __builtin_amdgcn_s_waitcnt(kLgkm0);                // slots written before the tails move
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+          if (f_set(inf[k]) < U1 && f_rank(inf[k]) == f_cnt(inf[k]) - 1) st32(&tailp[f_set(inf[k])], p[k] + 1);
+      } else {
+        // slow path (a unit with >= kRing records in flight): round by round,
+        // at most kRing records of a unit per publication
+        ++d_slow;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const uint32_t set = f_set(inf[k]), rank = f_rank(inf[k]), cnt = f_cnt(inf[k]);
+          for (uint32_t r0 = 0;; r0 += kRing) {
+            const bool act = set < U1 && rank >= r0 && rank < r0 + kRing;
+            if (!__ballot(act)) break;
+            for (uint32_t spin = 0;; ++spin) {
+              const bool ok = !act || (p[k] - ld32(&headp[set]) < kRing);
+              if (__ballot(!ok) == 0) break;
+              if (spin == kSpinLimit) { hung = true; break; }
+              __builtin_amdgcn_s_sleep(1);
+            }
+            if (act) st64(&ring[(p[k] % kRing) * U1 + set], key[k]);
+            __builtin_amdgcn_s_waitcnt(kLgkm0);
+            if (act && rank == min(cnt, r0 + kRing) - 1) st32(&tailp[set], p[k] + 1);
+          }
+        }
+      }
+    };
+    // the loop is unrolled by three so the buffers rotate roles without
+    // register moves (a move would wait for the load it copies)
+    constexpr uint32_t B = K * GG_WAVE;
+    if (n) {
+      load(0, pa, pm);
+      load(B, na, nm);
+    }
+    for (uint32_t c = 0; c < n; c += 3 * B) {
+      load(c + 2 * B, qa, qm);
+      batch(c, pa, pm);
+      if (c + B >= n) break;
+      load(c + 3 * B, pa, pm);
+      batch(c + B, na, nm);
+      if (c + 2 * B >= n) break;
+      load(c + 4 * B, na, nm);
+      batch(c + 2 * B, qa, qm);
+    }
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
+    if (lane == 0) st32(donep, 1u);
+    if (__ballot(bad) && lane == 0) atomicOr(err, GG_DERR_RANGE);
+    if (hung && lane == 0) atomicOr(err, GG_DERR_CAP);
+    if (dbg && lane == 0) {
+      atomicAdd(&dbg[0], (unsigned long long)d_batch);
+      atomicAdd(&dbg[1], (unsigned long long)d_slow);
+      atomicAdd(&dbg[2], (unsigned long long)d_spin);
+    }
+    return;
+  }
+
+  // ---------------- consumers: one unit per lane ----------------
+  // The L1-D set lives in four VGPRs: pos1 (byte w = L2 slot s*A2+w of the
+  // line L1-D way w holds, 0xFF = invalid; the L1-D only holds lines its L2
+  // holds, checked on entry), mbyt (0x80 in byte w iff way w is MODIFIED),
+  // a1 (LRU age nibbles), rr1.  Every per-access decision is a lane mask; the
+  // step has no divergent branch: the two possible L2 tag writes go to the
+  // real slot or to the lane's dummy word.
+  uint32_t mbyt = 0;
+#pragma unroll
+  for (int w = 0; w < A1; ++w) mbyt |= (((st1 >> (2 * w)) & 3u) == GG_MS_M) ? (0x80u << (8 * w)) : 0u;
+  const uint32_t log_line = g.log_line, log_u1 = g.log_u1, log_l2 = g.log_l2;
+  uint32_t* res_out = result ? result + base : nullptr;
+  uint64_t* ev_out = EV ? evicted + base : nullptr;
+  uint32_t* tag0 = reinterpret_cast<uint32_t*>(T) + 4 * u;        // tag (s, w) = tag0[(s*TQ + w/4)*4*U1 + w%4]
+  uint32_t* my_dummy = dummy + u;
+  // 0x80 flags of a byte mask -> 0xFF bytes
+  auto bytes_of = [](uint32_t m) { return m | (m - (m >> 7)); };
+
+  // counters: the result word's eight 1-bit nibble fields summed into byte
+  // fields (even / odd nibbles), folded into u32 totals every 128 iterations
+  // (wave-uniform, so <= 128 per byte); WRITE splits of the two miss fields in
+  // two 16-bit halves.
+  uint32_t f8[8], c_wr = 0, c_nh1w = 0, c_m2w = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) f8[k] = 0;
+  uint32_t acc_lo = 0, acc_hi = 0, acc_w = 0;
+  auto flush = [&]() {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f8[2 * k] += (acc_lo >> (8 * k)) & 0xFFu;
+      f8[2 * k + 1] += (acc_hi >> (8 * k)) & 0xFFu;
+    }
+    c_nh1w += acc_w & 0xFFFFu;
+    c_m2w += acc_w >> 16;
+    acc_lo = acc_hi = acc_w = 0;
+  };
+
+  // One access; returns the result word (GG_RES_*), the evicted line through *ev.
+  auto step = [&](const uint32_t kl, const uint32_t tag2, uint64_t* ev) -> uint32_t {
+    const uint32_t wr = kl & 1u;
+    const uint32_t s = __builtin_amdgcn_ubfe(kl, 1, log_s2);
+    const uint32_t tq0 = s * TQ * 4 * U1;
+    uint32_t tg[4 * TQ];
+#pragma unroll
+    for (int q = 0; q < TQ; ++q) {
+      const uint4 v = *reinterpret_cast<const uint4*>(tag0 + tq0 + q * 4 * U1);
+      tg[4 * q] = v.x; tg[4 * q + 1] = v.y; tg[4 * q + 2] = v.z; tg[4 * q + 3] = v.w;
+    }
+    const uint2 mt = Mt[s * U1 + u];
+    uint32_t ages2 = mt.x, st2 = mt.y & 0xFFFFu, rr2 = mt.y >> 16;
+    // L2 lookup (valid tags are unique in a set; invalid ways hold the invalid tag)
+    bool eq[A2];
+#pragma unroll
+    for (int w = 0; w < A2; ++w) eq[w] = tg[w] == tag2;
+    uint32_t w2 = A2;
+#pragma unroll
+    for (int w = A2 - 1; w >= 0; --w) w2 = eq[w] ? (uint32_t)w : w2;
+    const uint32_t has2m = w2 < A2 ? 0xFFFFFFFFu : 0u;
+    const uint32_t s2 = __builtin_amdgcn_ubfe(st2, 2 * w2, 2);            // 0 when absent
+    // L1-D lookup: the way naming the line's L2 slot; hit = readable (READ) or MODIFIED (WRITE)
+    const uint32_t slot = s * A2 + w2;
+    const uint32_t zb1 = zero_bytes32(pos1 ^ __builtin_amdgcn_perm(0u, slot, 0u)) & has2m;
+    const uint32_t wrm = 0u - wr;
+    const uint32_t hitb = zb1 & (~wrm | mbyt);
+    const bool hit1 = hitb != 0;
+    // no permission: invalidate the L1-D copy first (l1_cache_cntlr.cc:135-137)
+    const uint32_t inv1 = hit1 ? 0u : zb1;
+    {
+      const uint32_t f = bytes_of(inv1);
+      pos1 |= f;
+      mbyt &= ~f;
+    }
+    const bool hit2n = s2 > wr;
+    const bool hit2 = !hit1 && hit2n;
+    const bool miss2 = !hit1 && !hit2n;
+    const bool upg = miss2 && wr && s2 == GG_MS_S;
+    // upgrade: invalidate the SHARED L2 line (l2_cache_cntlr.cc:260-282)
+    st2 = upg ? (st2 & ~(3u << (2 * w2))) : st2;
+    *(upg ? tag0 + tq0 + (w2 / 4) * 4 * U1 + (w2 % 4) : my_dummy) = GG_L2_INV_TAG;
+    // L2 victim (l2_cache_cntlr.cc:74-116)
+    int v2 = LRU2 ? victim_nib<A2>(st2, ages2) : (int)rr2;
+    errv |= (miss2 && v2 < 0) ? GG_DERR_STATE : 0u;
+    const uint32_t vw = (uint32_t)v2 & (A2 - 1);
+    const uint32_t sv = __builtin_amdgcn_ubfe(st2, 2 * vw, 2);
+    const bool l2ev = miss2 && sv != 0;
+    const bool dirty = l2ev && sv == GG_MS_M;
+    uint32_t vt = 0;
+    if (EV) {
+#pragma unroll
+      for (int w = 0; w < A2; ++w) vt = (w == (int)vw) ? tg[w] : vt;
+    }
+    // invalidateCacheLineInL1 (l2_cache_cntlr.cc:124-131) when the L1-D holds the victim
+    const uint32_t zbv = zero_bytes32(pos1 ^ __builtin_amdgcn_perm(0u, s * A2 + vw, 0u)) & (l2ev ? 0xFFFFFFFFu : 0u);
+    {
+      const uint32_t f = bytes_of(zbv);
+      pos1 |= f;
+      mbyt &= ~f;
+    }
+    // install (EX_REP -> MODIFIED, SH_REP -> SHARED)
+    const uint32_t ns = 1u + wr;
+    st2 = miss2 ? ((st2 & ~(3u << (2 * vw))) | (ns << (2 * vw))) : st2;
+    *(miss2 ? tag0 + tq0 + (vw / 4) * 4 * U1 + (vw % 4) : my_dummy) = tag2;
+    if (!LRU2) rr2 = miss2 ? (rr2 ? rr2 - 1 : (A2 - 1)) : rr2;
+    if (LRU2) {
+      const uint32_t nb = lru_nib(ages2, miss2 ? vw : (w2 & (A2 - 1)));
+      ages2 = (!hit1 || wr) ? nb : ages2;
+    }
+    Mt[s * U1 + u] = make_uint2(ages2, st2 | (rr2 << 16));
+    // L1-D insert (insertCacheLineInL1, l2_cache_cntlr.cc:133-165) after both invalidations
+    uint32_t v1;
+    bool l1ev;
+    if (LRU1) {
+      constexpr uint32_t WM1 = (A1 >= 4) ? 0xFFFFFFFFu : ((1u << (8 * A1)) - 1);
+      constexpr uint32_t NM1 = (A1 >= 8) ? 0xFFFFFFFFu : ((1u << (4 * A1)) - 1);
+      const uint32_t invb = zero_bytes32(~pos1) & WM1;                     // invalid ways
+      const uint32_t zn = zero_nibbles(a1 ^ ((uint32_t)(A1 - 1) * 0x11111111u)) & NM1;
+      v1 = invb ? ((uint32_t)__builtin_ctz(invb) >> 3) : ((uint32_t)__builtin_ctz(zn | 0x80000000u) >> 2);
+      errv |= (!hit1 && !invb && !zn) ? GG_DERR_STATE : 0u;
+      l1ev = !hit1 && invb == 0;
+    } else {
+      v1 = rr1;
+      l1ev = !hit1 && ((pos1 >> (8 * v1)) & 0xFFu) != 0xFFu;
+    }
+    v1 &= A1 - 1;
+    {
+      const uint32_t sh = 8 * v1;
+      const uint32_t islot = s * A2 + (hit2 ? w2 : vw);
+      const uint32_t npos = (pos1 & ~(0xFFu << sh)) | (islot << sh);
+      const uint32_t nm = (mbyt & ~(0x80u << sh)) | (((hit2 ? s2 : ns) == GG_MS_M) ? (0x80u << sh) : 0u);
+      pos1 = hit1 ? pos1 : npos;
+      mbyt = hit1 ? mbyt : nm;
+    }
+    if (!LRU1) rr1 = !hit1 ? (rr1 ? rr1 - 1 : (A1 - 1)) : rr1;
+    if (LRU1) a1 = lru_nib(a1, hit1 ? ((uint32_t)__builtin_ctz(hitb) >> 3) : v1);
+    if (EV) {
+      const uint64_t e2 = ((uint64_t)vt << log_l2) | ((uint64_t)s << log_u1) | l1set;
+      *ev = l2ev ? (e2 << log_line) : ~0ull;
+    }
+    const uint32_t rv = (hit1 ? 0u : GG_RES_L1_MISS) | (miss2 ? GG_RES_L2_MISS : 0u) | (inv1 ? GG_RES_L1_INVAL : 0u) |
+                        (l1ev ? GG_RES_L1_EVICT : 0u) | (l2ev ? GG_RES_L2_EVICT : 0u) | (dirty ? GG_RES_L2_EVICT_DIRTY : 0u) |
+                        (zbv ? GG_RES_L2_EVICT_INV_L1 : 0u) | (upg ? GG_RES_UPGRADE : 0u);
+    acc_lo += rv & 0x0F0F0F0Fu;
+    acc_hi += (rv >> 4) & 0x0F0F0F0Fu;
+    const uint32_t x = rv & (wrm & 0x11u);
+    acc_w += (x & 1u) + ((x & 0x10u) << 12);
+    c_wr += wr;
+    return rv;
+  };
+
+  uint32_t h = 0, idle = 0, d_iter = 0, d_sleep = 0;
+  uint32_t t = ld32(&tailp[u]);
+  uint64_t kn = ld64(&ring[u]);
+  for (uint32_t it = 1;; ++it) {
+    bool have = h < t;
+    if (!__ballot(have)) {
+      const uint32_t d = ld32(donep);                    // before the tails: final once set
+      t = ld32(&tailp[u]);
+      kn = ld64(&ring[(h % kRing) * U1 + u]);
+      have = h < t;
+      if (!__ballot(have)) {
+        if (d) break;
+        if (++idle == kSpinLimit) { errv |= GG_DERR_CAP; break; }
+        ++d_sleep;
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+    }
+    idle = 0;
+    ++d_iter;
+    const uint64_t key = kn;
+    const uint32_t hn = h + (have ? 1u : 0u);
+    t = ld32(&tailp[u]);                                 // next record's tail, then its slot
+    kn = ld64(&ring[(hn % kRing) * U1 + u]);
+    if (have) {
+      const uint32_t kl = (uint32_t)key;
+      const uint32_t idx = kl >> (1 + log_s2);
+      uint64_t ev = 0;
+      const uint32_t rv = step(kl, (uint32_t)(key >> 32), &ev);
+      st32(&headp[u], hn);
+      if (res_out) res_out[idx] = rv;
+      if (EV) ev_out[idx] = ev;
+    }
+    h = hn;
+    if ((it & 127u) == 0) flush();
+  }
+  flush();
+  if (dbg && lane == 0) {
+    atomicAdd(&dbg[3], (unsigned long long)d_iter);
+    atomicAdd(&dbg[4], (unsigned long long)d_sleep);
+  }
+  if (dbg) atomicAdd(&dbg[5], (unsigned long long)h);
+
+  // ---- store state back in the HBM format ----
+  {
+    uint64_t m1 = 0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      if (w < A1) {
+        const uint32_t slot = (pos1 >> (8 * w)) & 0xFFu;
+        const uint32_t st = slot == 0xFFu ? GG_MS_I : (((mbyt >> (8 * w + 7)) & 1u) ? GG_MS_M : GG_MS_S);
+        uint64_t tag1 = GG_L1_INV_TAG;
+        if (st) {
+          const uint32_t ss = slot / A2, ww = slot % A2;
+          tag1 = ((uint64_t)tag_at(ss, ww) << g.log_l2) | ((uint64_t)ss << g.log_u1) | l1set;
+        }
+        cs.l1_tag[(uint64_t)w * g.units + gu] = tag1;
+        m1 |= (uint64_t)GG_M_MAKE(st, 0, (a1 >> (4 * w)) & 0xFu) << (8 * w);
+      } else {
+        m1 |= 0xF8ull << (8 * w);
+      }
+    }
+    cs.l1_meta[gu] = m1;
+    cs.l1_rr[gu] = (uint8_t)rr1;
+    for (uint32_t s = 0; s < S2; ++s) {
+      const uint2 mt = Mt[s * U1 + u];
+      uint64_t mw = 0;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        if (w < A2) {
+          const uint32_t st = (mt.y >> (2 * w)) & 3u;
+          const uint32_t zb = zero_bytes32(pos1 ^ ((s * A2 + w) * 0x01010101u));
+          mw |= (uint64_t)GG_M_MAKE(st, (zb != 0) ? 1u : 0u, (mt.x >> (4 * w)) & 0xFu) << (8 * w);
+          cs.l2_tag[(uint64_t)(s * A2 + w) * g.units + gu] = tag_at(s, w);
+        } else {
+          mw |= 0xF8ull << (8 * w);
+        }
+      }
+      cs.l2_meta[(uint64_t)s * g.units + gu] = mw;
+      if (!LRU2) cs.l2_rr[(uint64_t)s * g.units + gu] = (uint8_t)((mt.y >> 16) & 0xFFu);
+    }
+  }
+  if (errv) atomicOr(err, errv);
+  uint32_t cnt[NI];
+  cnt[I_WR] = c_wr; cnt[I_NH1] = f8[0]; cnt[I_NH1W] = c_nh1w; cnt[I_M2] = f8[1]; cnt[I_M2W] = c_m2w;
+  cnt[I_W1V] = f8[2]; cnt[I_L1EV] = f8[3]; cnt[I_L2EV] = f8[4]; cnt[I_DIRTY] = f8[5]; cnt[I_INVL1] = f8[6];
+  cnt[I_UPG] = f8[7];
+  replay_counters(cs, g, cnt, h, tile, lane, true);
+}
+
+// ---------------------------------------------------------------------------
 // Quartet (Cache::{get,set}CacheLineInfo, accessCacheLine, insertCacheLine)
 // on one tile's HBM-resident state.  Single thread; slow path.
 // ---------------------------------------------------------------------------
@@ -1291,6 +1821,27 @@ const Kern kLean[] = {
   GG_LEAN(4, 4, 1, 1), GG_LEAN(2, 4, 1, 1), GG_LEAN(2, 8, 1, 1), GG_LEAN(4, 2, 1, 1),
 };
 
+using stream_fn = void (*)(gg_cache_state, gg_geom, const uint64_t*, const uint32_t*, const uint64_t*,
+                           uint32_t*, uint64_t*, uint32_t*, unsigned long long*);
+struct StreamKern { int a1, a2, lru1, lru2, ncw; stream_fn plain, ev; };
+#define GG_STREAM(A1, A2, P1, P2, W) \
+  { A1, A2, P1, P2, W, k_cache_stream<A1, A2, P1, P2, W, false>, k_cache_stream<A1, A2, P1, P2, W, true> }
+const StreamKern kStream[] = {
+  GG_STREAM(4, 8, 1, 1, 2), GG_STREAM(4, 8, 0, 0, 2), GG_STREAM(4, 8, 1, 0, 2), GG_STREAM(4, 8, 0, 1, 2),
+  GG_STREAM(4, 4, 1, 1, 2), GG_STREAM(2, 4, 1, 1, 2), GG_STREAM(2, 8, 1, 1, 2), GG_STREAM(4, 2, 1, 1, 2),
+  GG_STREAM(4, 8, 1, 1, 1), GG_STREAM(4, 8, 1, 1, 4),
+};
+
+const StreamKern* find_stream(const gg_geom& g)
+{
+  const int l1 = g.pol1 == GG_POLICY_LRU, l2 = g.pol2 == GG_POLICY_LRU;
+  for (const StreamKern& k : kStream)
+    if ((uint32_t)k.a1 == g.a1 && (uint32_t)k.a2 == g.a2 && k.lru1 == l1 && k.lru2 == l2 &&
+        (uint32_t)k.ncw * GG_WAVE == g.u1)
+      return &k;
+  return nullptr;
+}
+
 const Kern* find_lean(uint32_t a1, uint32_t a2, uint32_t pol1, uint32_t pol2)
 {
   const int l1 = pol1 == GG_POLICY_LRU, l2 = pol2 == GG_POLICY_LRU;
@@ -1377,6 +1928,44 @@ gg_status gg_cache_run_batch(gg_ctx* ctx, const gg_trace* tr, uint32_t* result, 
   if (tr->tile_offsets[0] != 0 || tr->tile_offsets[g.tiles] != tr->num_records)
     return gg_fail(GG_ERR_INVALID, "tile_offsets must run from 0 to num_records");
   if (tr->num_records && (!tr->addr_dev || !tr->meta_dev)) return gg_fail(GG_ERR_INVALID, "addr/meta device pointers are NULL");
+  // ---- default: the single-pass streaming replay ----
+  if (ctx->replay_variant == 0) {
+    const StreamKern* sk = find_stream(g);
+    const size_t lds = stream_lds_bytes(g.u1, g.s2, g.a2);
+    uint64_t max_len = 0;
+    for (uint32_t t = 0; t < g.tiles; ++t) {
+      if (tr->tile_offsets[t + 1] < tr->tile_offsets[t]) return gg_fail(GG_ERR_INVALID, "tile_offsets not monotonic at tile %u", t);
+      max_len = std::max<uint64_t>(max_len, tr->tile_offsets[t + 1] - tr->tile_offsets[t]);
+    }
+    const uint32_t log_s2 = (uint32_t)__builtin_ctz(g.s2);
+    if (sk && lds <= 160 * 1024 && g.s2 * g.a2 < 255 && max_len < (1ull << (31 - log_s2))) {
+      GG_HIP(hipMemcpyAsync(ctx->tile_off_dev, tr->tile_offsets, sizeof(uint64_t) * (g.tiles + 1), hipMemcpyHostToDevice, s));
+      stream_fn fn = evicted ? sk->ev : sk->plain;
+      GG_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      gg_timer_begin(ctx, "cache_stream", s);
+      // GG_STREAM_DEBUG=1: hand-off counters of the launch on stderr (diagnostics)
+      static const bool dbg_on = getenv("GG_STREAM_DEBUG") && atoi(getenv("GG_STREAM_DEBUG"));
+      unsigned long long* dbg = nullptr;
+      if (dbg_on) {
+        GG_HIP(hipMalloc((void**)&dbg, 8 * sizeof(unsigned long long)));
+        GG_HIP(hipMemsetAsync(dbg, 0, 8 * sizeof(unsigned long long), s));
+      }
+      hipLaunchKernelGGL(fn, dim3(g.tiles), dim3((sk->ncw + 1) * GG_WAVE), lds, s, ctx->cs, g, tr->addr_dev,
+                         tr->meta_dev, (const uint64_t*)ctx->tile_off_dev, result, evicted, ctx->err_dev, dbg);
+      GG_HIP(hipGetLastError());
+      gg_timer_end(ctx, "cache_stream", s);
+      if (dbg) {
+        unsigned long long h[8];
+        GG_HIP(hipMemcpyAsync(h, dbg, sizeof(h), hipMemcpyDeviceToHost, s));
+        GG_HIP(hipStreamSynchronize(s));
+        hipFree(dbg);
+        fprintf(stderr, "[gg_stream] batches %llu slow %llu producer-spins %llu | consumer wave-iters %llu "
+                "idle-sleeps %llu records %llu (lane util %.3f)\n", h[0], h[1], h[2], h[3], h[4], h[5],
+                h[3] ? (double)h[5] / (64.0 * h[3]) : 0.0);
+      }
+      return GG_OK;
+    }
+  }
   // chunk table (host) — chunks never straddle tiles
   ctx->h_chunk_tile.clear(); ctx->h_chunk_start.clear(); ctx->h_chunk_len.clear();
   std::vector<uint32_t> tile_chunk0(g.tiles + 1);

@@ -213,6 +213,7 @@ static gg_status check_device_errors(gg_ctx* ctx)
   if (e & GG_DERR_RANGE) return gg_fail(GG_ERR_RANGE, "a trace address is beyond the compressed-tag range (%#llx)",
                                         (unsigned long long)ctx->g.addr_limit);
   if (e & GG_DERR_STATE) return gg_fail(GG_ERR_STATE, "cache state the reference would reject (LOG_ASSERT_ERROR)");
+  if (e & GG_DERR_CAP) return gg_fail(GG_ERR_HIP, "a device-side capacity or hand-off bound was exceeded");
   return GG_OK;
 }
 

@@ -140,7 +140,8 @@ typedef struct gg_config {
   uint32_t total_tiles;        /* app tiles + MCP + spawners (config.cc:77-82); 0 = num_tiles+2 */
   double   frequency_ghz;      /* single DVFS domain (carbon_sim.cfg:147-155)        */
   int32_t  device;             /* HIP device ordinal                                 */
-  uint32_t replay_kernel;      /* 0 = fastest instantiated replay kernel, 1 = generic */
+  uint32_t replay_kernel;      /* 0 = single-pass streaming replay where instantiated (else 2),
+                                  1 = sharded generic replay, 2 = sharded lean replay */
   /* ---- coherent mode (pr_l1_pr_l2_dram_directory_msi with directory, DRAM, NoC) ---- */
   uint32_t l1d_data_cycles;    /* l1_dcache/T1/data_access_time (1)                 */
   uint32_t l1d_tags_cycles;    /* l1_dcache/T1/tags_access_time (1)                 */

@@ -42,7 +42,7 @@ def run_gpu(cfg, addr, meta, offs, torch, chunks=1, want_ev=True):
 
 @pytest.mark.parametrize("name", [k for k, v in M.items() if v["kind"] == "modep"])
 @pytest.mark.parametrize("chunks", [1, 3])
-@pytest.mark.parametrize("kern", [0, 1])          # 0 = lean replay where instantiated, 1 = generic
+@pytest.mark.parametrize("kern", [0, 1, 2])       # 0 = streaming (else lean), 1 = sharded generic, 2 = sharded lean
 def test_replay_matches_reference_fixtures(name, chunks, kern):
     torch = torch_dev()
     e = M[name]
@@ -80,7 +80,7 @@ def ragged_trace(T, seed, lines_log2, max_len):
     dict(l1d_policy=C.POLICY_ROUND_ROBIN, l2_policy=C.POLICY_ROUND_ROBIN),
     dict(l1d_size_kb=16, l1d_assoc=8, l2_size_kb=256, l2_assoc=8),
 ])
-@pytest.mark.parametrize("kern", [0, 1])
+@pytest.mark.parametrize("kern", [0, 1, 2])
 def test_replay_matches_oracle_ragged(geom, kern):
     torch = torch_dev()
     T = 24
