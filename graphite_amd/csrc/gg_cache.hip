@@ -1138,14 +1138,13 @@ __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_
 //     in L2 while the tile's window is in flight).
 // ---------------------------------------------------------------------------
 constexpr uint32_t kRing = 32;
-constexpr int kMaskRounds = 4;              // producer rounds matched at once (LDS peer masks)
 constexpr uint32_t kSpinLimit = 1u << 22;   // s_sleep(1) polls (~64 cycles each) before giving up
 constexpr uint16_t kLgkm0 = 0xC07F;         // s_waitcnt lgkmcnt(0) (vmcnt/expcnt fields at their maxima)
 
 size_t stream_lds_bytes(uint32_t u1, uint32_t s2, uint32_t a2)
 {
   const size_t tq = (a2 + 3) / 4;
-  return (size_t)s2 * u1 * (tq * 16 + 8) + (size_t)kRing * u1 * 8 + (size_t)u1 * 12 + 16 + (size_t)kMaskRounds * u1 * 8 + (size_t)u1 * 4;
+  return (size_t)s2 * u1 * (tq * 16 + 8) + (size_t)kRing * u1 * 8 + (size_t)u1 * 12 + 16 + (size_t)u1 * 8 + (size_t)u1 * 4;
 }
 
 template <int A1, int A2, bool LRU1, bool LRU2, int NCW, bool EV>
@@ -1165,8 +1164,8 @@ __global__ __launch_bounds__((NCW + 1) * GG_WAVE) void k_cache_stream(gg_cache_s
   uint32_t* headp = tailp + U1;                                                          // [u]
   uint32_t* resv = headp + U1;                                                           // [u] producer-private
   uint32_t* donep = resv + U1;
-  uint64_t* pmask = reinterpret_cast<uint64_t*>(donep + 4);                              // [kMaskRounds][u]
-  uint32_t* dummy = reinterpret_cast<uint32_t*>(pmask + kMaskRounds * U1);               // [u] sink of masked-off writes
+  uint64_t* pmask = reinterpret_cast<uint64_t*>(donep + 4);                              // [u] producer peer masks
+  uint32_t* dummy = reinterpret_cast<uint32_t*>(pmask + U1);                             // [u] sink of masked-off writes
   // Cross-wave LDS words go through relaxed workgroup-scope atomics: they stay
   // ds_* instructions (a volatile generic pointer would become a flat access)
   // and keep their program order.
@@ -1239,21 +1238,26 @@ __global__ __launch_bounds__((NCW + 1) * GG_WAVE) void k_cache_stream(gg_cache_s
     if (nvalid != nheld) errv |= GG_DERR_STATE;
   } else {
     for (uint32_t k = lane; k < U1; k += GG_WAVE) { tailp[k] = 0; headp[k] = 0; resv[k] = 0; }
-    for (uint32_t k = lane; k < kMaskRounds * U1; k += GG_WAVE) pmask[k] = 0;
+    for (uint32_t k = lane; k < U1; k += GG_WAVE) pmask[k] = 0;
     if (lane == 0) *donep = 0;
   }
   __syncthreads();
 
   if (producer) {
     // ---------------- producer: program-order trace -> per-unit rings ----------------
-    // Batches of K rounds x 64 records; the next batch's loads are in flight
-    // while this one is classified, reserved (one ds_add_rtn per (round, unit)
-    // on resv[], all rounds at once), checked for ring space and written.
+    // Batches of K rounds x 64 records, the next two batches' loads in flight.
+    // Per round, five LDS operations issued back to back (no waits between
+    // rounds; one wave's LDS operations execute in order):
+    //   ds_or   pmask[unit] |= lane bit      -> after the round: lanes of the unit
+    //   ds_read pmask[unit]; ds_write pmask[unit] = 0
+    //   ds_read resv[unit]                    -> ring position base of the round
+    //   ds_add  resv[unit] += 1               -> += the round's count of the unit
+    // position = base + lanes of the unit below this lane (program order).
+    // Space and publication are checked per unit (lane l owns units l + 64 i).
     constexpr int K = 8;
     const uint64_t* ap = addr + base;
     const uint32_t* mp = meta + base;
     const uint64_t lt_mask = (1ull << lane) - 1;
-    // three batches in registers: this one, and the next two in flight
     uint64_t pa[K], na[K], qa[K];
     uint32_t pm[K], nm[K], qm[K];
     uint32_t bad = 0;
@@ -1269,102 +1273,77 @@ __global__ __launch_bounds__((NCW + 1) * GG_WAVE) void k_cache_stream(gg_cache_s
         m[k] = __builtin_nontemporal_load(mp + j);
       }
     };
-    // one batch: classify, reserve, check space, write, publish
     auto batch = [&](const uint32_t c, const uint64_t (&pa)[K], const uint32_t (&pm)[K]) {
-      // classify and rank (lanes of a round naming the same unit, in lane order);
-      // per round one packed word: unit (9 bits, U1 = no record), rank (7),
-      // count (7), first lane of the unit (6)
-      uint64_t key[K];
-      uint32_t inf[K], p[K];
-      constexpr int KM = kMaskRounds;
-      auto f_set = [](uint32_t w) { return w & 0x1FFu; };
-      auto f_rank = [](uint32_t w) { return (w >> 9) & 0x7Fu; };
-      auto f_cnt = [](uint32_t w) { return (w >> 16) & 0x7Fu; };
-      auto f_lead = [](uint32_t w) { return w >> 23; };
-      // unit of each record (U1 = no record) and its ring entry
-      uint32_t set[K];
+      uint64_t key[K], msk[K];
+      uint32_t set[K], p[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         const uint32_t j = c + k * GG_WAVE + lane;
         const bool valid = j < n;
         bad |= (valid && pa[k] >= g.addr_limit) ? 1u : 0u;
         const uint64_t line = pa[k] >> g.log_line;
-        set[k] = valid ? (uint32_t)line & (U1 - 1) : U1;
+        set[k] = valid ? (uint32_t)line & (U1 - 1) : U1;             // U1 = no record
         key[k] = ((uint64_t)(uint32_t)(line >> g.log_l2) << 32) | (j << (1 + log_s2)) |
                  ((((uint32_t)line >> g.log_u1) & (S2 - 1)) << 1) | (pm[k] & GG_META_WRITE);
       }
-      // lanes of a round naming the same unit: OR the lane bits into a per-unit
-      // LDS mask (commutative, so deterministic), read it back, clear it
 #pragma unroll
-      for (int h = 0; h < K; h += KM) {
-#pragma unroll
-        for (int k = h; k < h + KM; ++k)
-          if (set[k] < U1)
-            __hip_atomic_fetch_or(&pmask[(k - h) * U1 + set[k]], 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        uint64_t peers[KM];
-#pragma unroll
-        for (int k = h; k < h + KM; ++k) peers[k - h] = set[k] < U1 ? ld64(&pmask[(k - h) * U1 + set[k]]) : 0ull;
-#pragma unroll
-        for (int k = h; k < h + KM; ++k)
-          if (set[k] < U1) st64(&pmask[(k - h) * U1 + set[k]], 0ull);
-#pragma unroll
-        for (int k = h; k < h + KM; ++k) {
-          const uint64_t pr = peers[k - h];
-          const uint32_t lead = pr ? (uint32_t)__builtin_ctzll(pr) : lane;
-          inf[k] = set[k] | ((uint32_t)__popcll(pr & lt_mask) << 9) | ((uint32_t)__popcll(pr) << 16) | (lead << 23);
+      for (int k = 0; k < K; ++k) {
+        msk[k] = 0;
+        p[k] = 0;
+        if (set[k] < U1) {
+          __hip_atomic_fetch_or(&pmask[set[k]], 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          msk[k] = ld64(&pmask[set[k]]);
+          st64(&pmask[set[k]], 0ull);
+          p[k] = ld32(&resv[set[k]]);
+          __hip_atomic_fetch_add(&resv[set[k]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
       }
-      // reserve ring positions: the round's first lane of each unit adds the
-      // round's count (atomics of one wave execute in issue order)
 #pragma unroll
-      for (int k = 0; k < K; ++k)
-        p[k] = (f_set(inf[k]) < U1 && f_rank(inf[k]) == 0)
-                   ? __hip_atomic_fetch_add(&resv[f_set(inf[k])], f_cnt(inf[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
-                   : 0u;
-#pragma unroll
-      for (int k = 0; k < K; ++k) p[k] = (uint32_t)__shfl((int)p[k], (int)f_lead(inf[k])) + f_rank(inf[k]);
-      // fast path: every record of the batch fits within kRing of its unit's
-      // published tail (so waiting for consumer heads terminates)
+      for (int k = 0; k < K; ++k) p[k] += (uint32_t)__popcll(msk[k] & lt_mask);
+      // per unit: reserved end vs published tail (no deadlock) and consumer head (space)
+      uint32_t rn[NCW];
       bool fits = true;
 #pragma unroll
-      for (int k = 0; k < K; ++k)
-        fits = fits && (f_set(inf[k]) == U1 || p[k] - ld32(&tailp[f_set(inf[k])]) < kRing);
+      for (int i = 0; i < NCW; ++i) {
+        rn[i] = ld32(&resv[lane + GG_WAVE * i]);
+        fits = fits && rn[i] - ld32(&tailp[lane + GG_WAVE * i]) <= kRing;
+      }
       ++d_batch;
       if (__ballot(!fits) == 0) {
         for (uint32_t spin = 0;; ++spin, ++d_spin) {
           bool ok = true;
 #pragma unroll
-          for (int k = 0; k < K; ++k) ok = ok && (f_set(inf[k]) == U1 || p[k] - ld32(&headp[f_set(inf[k])]) < kRing);
+          for (int i = 0; i < NCW; ++i) ok = ok && rn[i] - ld32(&headp[lane + GG_WAVE * i]) <= kRing;
           if (__ballot(!ok) == 0) break;
           if (spin == kSpinLimit) { hung = true; break; }
           __builtin_amdgcn_s_sleep(1);
         }
 #pragma unroll
         for (int k = 0; k < K; ++k)
-          if (f_set(inf[k]) < U1) st64(&ring[(p[k] % kRing) * U1 + f_set(inf[k])], key[k]);
+          if (set[k] < U1) st64(&ring[(p[k] % kRing) * U1 + set[k]], key[k]);
         __builtin_amdgcn_s_waitcnt(kLgkm0);                // slots written before the tails move
 #pragma unroll
-        for (int k = 0; k < K; ++k)
-          if (f_set(inf[k]) < U1 && f_rank(inf[k]) == f_cnt(inf[k]) - 1) st32(&tailp[f_set(inf[k])], p[k] + 1);
+        for (int i = 0; i < NCW; ++i) st32(&tailp[lane + GG_WAVE * i], rn[i]);
       } else {
-        // slow path (a unit with >= kRing records in flight): round by round,
-        // at most kRing records of a unit per publication
+        // slow path (a unit with > kRing records in this batch): round by
+        // round, at most kRing records of a unit per publication
         ++d_slow;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-          const uint32_t set = f_set(inf[k]), rank = f_rank(inf[k]), cnt = f_cnt(inf[k]);
+          const uint32_t st = set[k];
+          const uint32_t rank = (uint32_t)__popcll(msk[k] & lt_mask), cnt = (uint32_t)__popcll(msk[k]);
           for (uint32_t r0 = 0;; r0 += kRing) {
-            const bool act = set < U1 && rank >= r0 && rank < r0 + kRing;
+            const bool act = st < U1 && rank >= r0 && rank < r0 + kRing;
             if (!__ballot(act)) break;
             for (uint32_t spin = 0;; ++spin) {
-              const bool ok = !act || (p[k] - ld32(&headp[set]) < kRing);
+              const bool ok = !act || (p[k] - ld32(&headp[st]) < kRing);
               if (__ballot(!ok) == 0) break;
               if (spin == kSpinLimit) { hung = true; break; }
               __builtin_amdgcn_s_sleep(1);
             }
-            if (act) st64(&ring[(p[k] % kRing) * U1 + set], key[k]);
+            if (act) st64(&ring[(p[k] % kRing) * U1 + st], key[k]);
             __builtin_amdgcn_s_waitcnt(kLgkm0);
-            if (act && rank == min(cnt, r0 + kRing) - 1) st32(&tailp[set], p[k] + 1);
+            if (act && rank == min(cnt, r0 + kRing) - 1) st32(&tailp[st], p[k] + 1);
           }
         }
       }
@@ -1539,14 +1518,17 @@ __global__ __launch_bounds__((NCW + 1) * GG_WAVE) void k_cache_stream(gg_cache_s
     const uint32_t rv = (hit1 ? 0u : GG_RES_L1_MISS) | (miss2 ? GG_RES_L2_MISS : 0u) | (inv1 ? GG_RES_L1_INVAL : 0u) |
                         (l1ev ? GG_RES_L1_EVICT : 0u) | (l2ev ? GG_RES_L2_EVICT : 0u) | (dirty ? GG_RES_L2_EVICT_DIRTY : 0u) |
                         (zbv ? GG_RES_L2_EVICT_INV_L1 : 0u) | (upg ? GG_RES_UPGRADE : 0u);
-    acc_lo += rv & 0x0F0F0F0Fu;
-    acc_hi += (rv >> 4) & 0x0F0F0F0Fu;
-    const uint32_t x = rv & (wrm & 0x11u);
-    acc_w += (x & 1u) + ((x & 0x10u) << 12);
-    c_wr += wr;
     return rv;
   };
+  auto count = [&](const uint32_t rv, const uint32_t wr) {
+    acc_lo += rv & 0x0F0F0F0Fu;
+    acc_hi += (rv >> 4) & 0x0F0F0F0Fu;
+    const uint32_t x = rv & ((0u - wr) & 0x11u);
+    acc_w += (x & 1u) + ((x & 0x10u) << 12);
+    c_wr += wr;
+  };
 
+  const bool nostep = dbg && dbg[7] == 1;               // diagnostics: hand-off machinery alone
   uint32_t h = 0, idle = 0, d_iter = 0, d_sleep = 0;
   uint32_t t = ld32(&tailp[u]);
   uint64_t kn = ld64(&ring[u]);
@@ -1575,10 +1557,11 @@ __global__ __launch_bounds__((NCW + 1) * GG_WAVE) void k_cache_stream(gg_cache_s
       const uint32_t kl = (uint32_t)key;
       const uint32_t idx = kl >> (1 + log_s2);
       uint64_t ev = 0;
-      const uint32_t rv = step(kl, (uint32_t)(key >> 32), &ev);
+      const uint32_t rv = nostep ? kl : step(kl, (uint32_t)(key >> 32), &ev);
       st32(&headp[u], hn);
       if (res_out) res_out[idx] = rv;
       if (EV) ev_out[idx] = ev;
+      count(rv, kl & 1u);
     }
     h = hn;
     if ((it & 127u) == 0) flush();
@@ -1944,14 +1927,18 @@ gg_status gg_cache_run_batch(gg_ctx* ctx, const gg_trace* tr, uint32_t* result, 
       GG_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       gg_timer_begin(ctx, "cache_stream", s);
       // GG_STREAM_DEBUG=1: hand-off counters of the launch on stderr (diagnostics)
-      static const bool dbg_on = getenv("GG_STREAM_DEBUG") && atoi(getenv("GG_STREAM_DEBUG"));
+      static const int dbg_on = getenv("GG_STREAM_DEBUG") ? atoi(getenv("GG_STREAM_DEBUG")) : 0;
       unsigned long long* dbg = nullptr;
       if (dbg_on) {
         GG_HIP(hipMalloc((void**)&dbg, 8 * sizeof(unsigned long long)));
         GG_HIP(hipMemsetAsync(dbg, 0, 8 * sizeof(unsigned long long), s));
+        if (dbg_on == 2) GG_HIP(hipMemsetAsync(dbg + 7, 1, 1, s));   // GG_STREAM_DEBUG=2: skip the cache step
       }
+      // GG_STREAM_NORES=1 (diagnostics only): drop the result stores
+      static const bool nores = getenv("GG_STREAM_NORES") && atoi(getenv("GG_STREAM_NORES"));
       hipLaunchKernelGGL(fn, dim3(g.tiles), dim3((sk->ncw + 1) * GG_WAVE), lds, s, ctx->cs, g, tr->addr_dev,
-                         tr->meta_dev, (const uint64_t*)ctx->tile_off_dev, result, evicted, ctx->err_dev, dbg);
+                         tr->meta_dev, (const uint64_t*)ctx->tile_off_dev, nores ? nullptr : result, evicted,
+                         ctx->err_dev, dbg);
       GG_HIP(hipGetLastError());
       gg_timer_end(ctx, "cache_stream", s);
       if (dbg) {
