@@ -22,5 +22,13 @@ pass write WRITE_SIZE &&
 pass sq SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU &&
 pass sq2 SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE
 rc=$?
+[ $rc -ne 0 ] && exit $rc
+# counter calibration: known byte counts at the access widths of the path
+CAL="$GRAFT_REPO_ROOT/tools/calib/calib_traffic"
+for c in FETCH_SIZE:calib_fetch WRITE_SIZE:calib_write; do
+  timeout -k 10 120 rocprofv3 --pmc ${c%%:*} -d "$OUT/${c##*:}" -o run --output-format csv -- "$CAL" 2048 \
+    > "$OUT/${c##*:}.json" 2> "$OUT/${c##*:}.log" || exit $?
+  echo "calibration ${c##*:} rc=0"
+done
 find "$OUT" -name "*counter_collection*" | head -20
-exit $rc
+exit 0
