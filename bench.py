@@ -88,6 +88,8 @@ def parse():
     p.add_argument("--coherent-shards", type=int, default=0, help="logical shards (0 = 1, or 8 with --gpus > 1)")
     p.add_argument("--coherent", action="store_true",
                    help="run the coherent section on N > 1 ranks too (RCCL all-to-all per quantum)")
+    p.add_argument("--fft-m", type=int, default=14,
+                   help="configs[0] section: captured FFT of 2^m points on 16 tiles (0 = skip; configs[0] is m=20)")
     return p.parse_args()
 
 
@@ -149,6 +151,50 @@ def coherent_section(args, world, rank, dev, backend_name):
         res["cpu_baseline"] = {"value": T * N / cdt, "unit": "accesses/s", "cores": 1, "kind": "port",
                                "sample": "the whole coherent workload, oracle/gg_coherent.inc -O3, 1 thread, "
                                          "%.2f s" % cdt}
+    be.close()
+    return res
+
+
+def fft_section(args, dev):
+    """configs[0]: the SPLASH-2-style FFT (-p16) captured by the source-level
+    front end (graphite_amd.capture), simulated in Mode C (MSI directory +
+    emesh_hop_counter, 16 tiles) on the GPU; bit-exact against the C oracle,
+    whose run is the CPU baseline."""
+    import torch
+    from graphite_amd import config as C
+    from graphite_amd import backend as B
+    from graphite_amd import capture as cp
+    m, p = args.fft_m, 16
+    a, meta, offs, X = cp.capture_fft(m, p)
+    fft_ok = bool(np.abs(X - np.fft.fft(cp.fft_input(m))).max() <= 1e-9 * np.abs(X).max())
+    cfg = C.default_config(p, net_model=C.NET_EMESH_HOP_COUNTER)
+    be = B.Backend(cfg)
+    addr = torch.from_numpy(a.view(np.int64)).to(dev)
+    mt = torch.from_numpy(meta.view(np.int32)).to(dev)
+    out = torch.zeros(len(a), dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    be.coherent_run(addr, mt, offs, out)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    st, cc, ri = be.coherent_stats()
+    res = {"workload": "configs[0]: captured six-step FFT of 2^%d points, %d threads = %d tiles, %d accesses, "
+                       "pr_l1_pr_l2_dram_directory_msi + emesh_hop_counter" % (m, p, p, len(a)),
+           "value": len(a) / dt, "unit": "accesses/s", "seconds": dt, "fft_correct": fft_ok,
+           "steps": int(ri[C.RUN_INFO.index("steps")]), "simulated_ns": int(st[:, 0].max()) // 1000}
+    if not args.no_verify:
+        from oracle import pyoracle as po
+        oc = po.OracleCoherent(cfg)
+        c0 = time.perf_counter()
+        ref = oc.run(a, meta, offs)
+        cdt = time.perf_counter() - c0
+        res["bit_exact_checked"] = bool(np.array_equal(out.cpu().numpy().view(np.uint64), ref) and
+                                        np.array_equal(st, oc.tile_stats()) and
+                                        np.array_equal(cc, oc.cache_counters()))
+        if not res["bit_exact_checked"]:
+            print("bench.py: FFT BIT-EXACT CHECK FAILED", file=sys.stderr)
+        res["cpu_baseline"] = {"value": len(a) / cdt, "unit": "accesses/s", "cores": 1, "kind": "port",
+                               "sample": "the whole FFT trace, oracle/gg_coherent.inc -O3, 1 thread, %.2f s" % cdt}
     be.close()
     return res
 
@@ -302,6 +348,8 @@ def main():
         coh = coherent_section(args, world, rank, dev, "nccl")
         if rank == 0:
             out["coherent"] = coh
+    if args.fft_m and world == 1:
+        out["fft"] = fft_section(args, dev)
     if rank == 0:
         print(json.dumps(out))
     if world > 1:

@@ -87,6 +87,9 @@ struct CS {
   uint32_t *pk_src, *pk_dst, *pk_len; uint64_t *pk_t0, *pk_khi, *pk_klo;
   uint64_t* ctr;                         // NoC counters [T][GG_NUM_NET_COUNTERS]
   uint32_t* err;
+  // GG_COH_PROFILE=1 (diagnostics): shader-clock cycles per step phase
+  unsigned long long* prof;              // [0..3] phase sums over tiles and steps, [8 + step] max tile total
+  uint32_t prof_steps;
 };
 
 __device__ __forceinline__ gg_cmsg* bufp(const CS& S, int p) { return p ? S.buf1 : S.buf0; }
@@ -244,10 +247,14 @@ struct Cache {
     c[GG_CC_TAG_WRITES]++; c[GG_CC_DATA_WRITES]++;
     return true;
   }
+  // all loads in flight, then all stores (no load waits behind a store)
   __device__ __forceinline__ void flush()
   {
+    uint64_t v[GG_NUM_CACHE_COUNTERS];
 #pragma unroll
-    for (int k = 0; k < GG_NUM_CACHE_COUNTERS; ++k) if (c[k]) cg[k] += c[k];
+    for (int k = 0; k < GG_NUM_CACHE_COUNTERS; ++k) v[k] = cg[k];
+#pragma unroll
+    for (int k = 0; k < GG_NUM_CACHE_COUNTERS; ++k) cg[k] = v[k] + c[k];
   }
 };
 
@@ -269,6 +276,8 @@ struct Tile {
   // the tile's scalars, in registers for the step (written back by flush)
   uint64_t rec, rec_end, clk, pend_start, out_addr, out_time;
   uint32_t blocked, seq, nrep, nrq;
+  // the tile's DRAM queue (history tree): global memory, or the step's LDS copy
+  HQueue* dq; HNode* dnd; int16_t* dfl;
 
   __device__ __forceinline__ Tile(const CP& p, const CS& s, uint32_t l, int out_parity) : P(p), S(s), lt(l), tile(p.tb + l), po(out_parity)
   {
@@ -282,13 +291,16 @@ struct Tile {
     rec = S.rec[lt]; rec_end = S.rec_end[lt]; clk = S.clk[lt]; pend_start = S.pend_start[lt];
     out_addr = S.out_addr[lt]; out_time = S.out_time[lt];
     blocked = S.blocked[lt]; seq = S.seq[lt]; nrep = S.nrep[lt]; nrq = S.nrq[lt];
+    dq = S.dq + lt; dnd = S.dnd + (size_t)lt * P.max_list; dfl = S.dfl + (size_t)lt * P.max_list;
   }
   __device__ __forceinline__ void flush()
   {
     L1.flush(); L2.flush();
+    uint64_t v[GG_NUM_TILE_STATS];
 #pragma unroll
-    for (int k = 0; k < GG_NUM_TILE_STATS; ++k) if (k != GG_CT_CLOCK_PS && st[k]) stg[k] += st[k];
-    stg[GG_CT_CLOCK_PS] = clk;
+    for (int k = 0; k < GG_NUM_TILE_STATS; ++k) v[k] = stg[k];
+#pragma unroll
+    for (int k = 0; k < GG_NUM_TILE_STATS; ++k) stg[k] = (k == GG_CT_CLOCK_PS) ? clk : v[k] + st[k];
     S.rec[lt] = rec; S.clk[lt] = clk; S.pend_start[lt] = pend_start;
     S.out_addr[lt] = out_addr; S.out_time[lt] = out_time;
     S.blocked[lt] = blocked; S.seq[lt] = seq; S.nrep[lt] = nrep; S.nrq[lt] = nrq;
@@ -448,8 +460,7 @@ struct Tile {
     const uint64_t pkt_ns = (uint64_t)ceil(t / 1000.0);
     uint64_t qd = 0;
     if (P.dram_qm) {
-      HTree tr{S.dq + lt, S.dnd + (size_t)lt * P.max_list, S.dfl + (size_t)lt * P.max_list, P.dram_proc,
-               P.analytical != 0};
+      HTree tr{dq, dnd, dfl, P.dram_proc, P.analytical != 0};
       qd = tr.delay(pkt_ns, P.dram_proc, S.err);
       st[GG_CT_DRAM_QUEUE_REQUESTS]++;
     }
@@ -791,14 +802,58 @@ __device__ __forceinline__ bool chan_lt(const gg_cmsg& a, const gg_cmsg& b)
 // One tile per wave (a one-lane workgroup): the tiles' controller paths diverge
 // completely, so packing 64 tiles into one wave would serialize the union of
 // their paths; one wave per tile costs issue slots the chip has to spare.
+// The DRAM history tree of a wave-per-tile step lives in LDS for the step: the
+// wave copies it in (HQueue + max_list nodes + free list, 16 B per lane per
+// load) before lane 0 runs the tile, and back after.  Its AVL operations are
+// chains of dependent node accesses, each an HBM/MALL round trip otherwise.
+constexpr uint32_t kTreeLds = 128;           // largest max_list_size staged (carbon_sim.cfg: 100)
+struct TreeLds {
+  HQueue q;
+  HNode nd[kTreeLds];
+  int16_t fl[kTreeLds];
+};
+
+__device__ __forceinline__ void copy_words(uint32_t* dst, const uint32_t* src, uint32_t words, uint32_t lane)
+{
+  for (uint32_t i = lane; i < words; i += GG_WAVE) dst[i] = src[i];
+}
+
+__device__ void c_tile_step(const CP& P, const CS& S, int p, uint64_t barrier, uint32_t lt, TreeLds* tl);
+
 __global__ void __launch_bounds__(64) k_c_tiles(CP P, CS S, int p, uint64_t barrier)
 {
   if (*(volatile uint32_t*)S.quiet) return;
-  const uint32_t lt = P.tiles_per_block == 1 ? blockIdx.x : blockIdx.x * blockDim.x + threadIdx.x;
-  if (P.tiles_per_block == 1 && threadIdx.x != 0) return;
-  if (lt == 0) S.ri[GG_RI_STEPS]++;
-  if (lt >= P.lt) return;
+  if (P.tiles_per_block != 1) {
+    const uint32_t lt = blockIdx.x * blockDim.x + threadIdx.x;
+    if (lt == 0) S.ri[GG_RI_STEPS]++;
+    if (lt < P.lt) c_tile_step(P, S, p, barrier, lt, nullptr);
+    return;
+  }
+  const uint32_t lt = blockIdx.x, lane = threadIdx.x;
+  if (lt == 0 && lane == 0) S.ri[GG_RI_STEPS]++;
+  __shared__ TreeLds tl;
+  const bool stage = P.dram_qm && P.max_list <= kTreeLds && (P.max_list % 2) == 0;
+  const uint32_t qw = sizeof(HQueue) / 4, nw = P.max_list * sizeof(HNode) / 4, fw = (P.max_list + 1) / 2;
+  if (stage) {
+    copy_words((uint32_t*)&tl.q, (const uint32_t*)(S.dq + lt), qw, lane);
+    copy_words((uint32_t*)tl.nd, (const uint32_t*)(S.dnd + (size_t)lt * P.max_list), nw, lane);
+    copy_words((uint32_t*)tl.fl, (const uint32_t*)(S.dfl + (size_t)lt * P.max_list), fw, lane);
+    __syncthreads();
+  }
+  if (lane == 0) c_tile_step(P, S, p, barrier, lt, stage ? &tl : nullptr);
+  if (stage) {
+    __syncthreads();
+    copy_words((uint32_t*)(S.dq + lt), (const uint32_t*)&tl.q, qw, lane);
+    copy_words((uint32_t*)(S.dnd + (size_t)lt * P.max_list), (const uint32_t*)tl.nd, nw, lane);
+    copy_words((uint32_t*)(S.dfl + (size_t)lt * P.max_list), (const uint32_t*)tl.fl, fw, lane);
+  }
+}
+
+__device__ void c_tile_step(const CP& P, const CS& S, int p, uint64_t barrier, uint32_t lt, TreeLds* tl)
+{
+  const uint64_t c0 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
   Tile T(P, S, lt, 1 - p);
+  if (tl) { T.dq = &tl->q; T.dnd = tl->nd; T.dfl = tl->fl; }
   // 1. gather the inbox list
   int32_t* head = headp(S, p);
   const gg_cmsg* in = bufp(S, p);
@@ -817,6 +872,7 @@ __global__ void __launch_bounds__(64) k_c_tiles(CP P, CS S, int p, uint64_t barr
     while (j > 0 && chan_lt(mv, in[idx[j - 1]])) { idx[j] = idx[j - 1]; --j; }
     idx[j] = v;
   }
+  const uint64_t c1 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
   // merge the channels: repeatedly the channel head with the least (arrival, sender)
   for (uint32_t k = 0; k < n; ++k) {
     uint32_t best = ~0u, prev_src = ~0u;
@@ -832,8 +888,11 @@ __global__ void __launch_bounds__(64) k_c_tiles(CP P, CS S, int p, uint64_t barr
     const gg_cmsg m = in[idx[best]];
     idx[best] = ~0u;
     T.st[GG_CT_MSGS_RECEIVED]++;
+    const uint64_t h0 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
     if (to_directory(m.type)) T.directory_msg(m); else T.l2_msg(m);
+    if (S.prof) atomicAdd(&S.prof[to_directory(m.type) ? 5 : 6], (unsigned long long)(__builtin_amdgcn_s_memtime() - h0));
   }
+  const uint64_t c2 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
   // 2. the trace
   const uint64_t line_mask = ~((1ull << P.log_line) - 1);
   while (!T.blocked) {
@@ -844,7 +903,18 @@ __global__ void __launch_bounds__(64) k_c_tiles(CP P, CS S, int p, uint64_t barr
     if (s >= barrier) break;
     T.app_access(S.addr[r] & line_mask, (meta & GG_META_WRITE) != 0, s);
   }
+  const uint64_t c3 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
   T.flush();
+  if (S.prof) {
+    const uint64_t c4 = __builtin_amdgcn_s_memtime();
+    atomicAdd(&S.prof[0], (unsigned long long)(c1 - c0));     // tile load + inbox gather + sort
+    atomicAdd(&S.prof[1], (unsigned long long)(c2 - c1));     // message handlers
+    atomicAdd(&S.prof[2], (unsigned long long)(c3 - c2));     // trace
+    atomicAdd(&S.prof[3], (unsigned long long)(c4 - c3));     // flush
+    atomicAdd(&S.prof[4], (unsigned long long)n);
+    const uint32_t st = (uint32_t)S.ri[GG_RI_STEPS];
+    if (st < S.prof_steps) atomicMax(&S.prof[8 + st], (unsigned long long)(c4 - c0));
+  }
 }
 
 // A step's messages: network latency (closed form, or the arrival the
@@ -1082,6 +1152,11 @@ static gg_status coh_alloc(gg_ctx* ctx)
   P.msg_cap = (uint64_t)64 * P.T + 65536;
   // a wave per tile (default; GG_COH_TILES_PER_BLOCK=64 packs a lane per tile, for A/B runs)
   { const char* e = getenv("GG_COH_TILES_PER_BLOCK"); P.tiles_per_block = (e && atoi(e) == 64) ? 64 : 1; }
+  if (getenv("GG_COH_PROFILE") && atoi(getenv("GG_COH_PROFILE"))) {
+    C->S.prof_steps = 1u << 16;
+    if (gg_status st = dalloc(C, &C->S.prof, 8 + C->S.prof_steps)) return st;
+    GG_HIP(hipMemset(C->S.prof, 0, sizeof(unsigned long long) * (8 + C->S.prof_steps)));
+  }
   P.np = gg_noc_params(ctx);
   const uint64_t L = P.lt;
   CS& S = C->S;
@@ -1301,6 +1376,15 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
   }
   gg_timer_end(ctx, "coherent_run", s);
   GG_HIP(hipStreamSynchronize(s));
+  if (C->S.prof) {
+    std::vector<unsigned long long> h(8 + C->S.prof_steps);
+    GG_HIP(hipMemcpy(h.data(), C->S.prof, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
+    unsigned long long crit = 0, nst = 0;
+    for (uint32_t i = 0; i < C->S.prof_steps; ++i) { crit += h[8 + i]; nst += h[8 + i] ? 1 : 0; }
+    fprintf(stderr, "[gg_coh] tile-step cycles summed over tiles: gather+sort %llu handlers %llu (directory %llu, L2 %llu)"
+            " trace %llu flush %llu | msgs %llu | critical path (max tile per step, %llu steps) %llu cycles\n",
+            h[0], h[1], h[5], h[6], h[2], h[3], h[4], nst, crit);
+  }
   return coh_check(ctx);
 }
 
