@@ -63,6 +63,7 @@ struct CP {
   uint64_t lat_l1d, lat_l1t, lat_l2d, lat_l2t, lat_dir, gap_ps, dram_proc, dram_cost;
   uint64_t msg_cap;
   uint32_t tiles_per_block;              // 64: a lane per tile; 1: a wave per tile (lane 0)
+  uint32_t stage_rq;                     // wave per tile: directory request FIFO staged in LDS per step
   NocParams np;
 };
 
@@ -276,8 +277,10 @@ struct Tile {
   // the tile's scalars, in registers for the step (written back by flush)
   uint64_t rec, rec_end, clk, pend_start, out_addr, out_time;
   uint32_t blocked, seq, nrep, nrq;
-  // the tile's DRAM queue (history tree): global memory, or the step's LDS copy
+  // the tile's DRAM queue (history tree) and directory request FIFO: global
+  // memory, or the step's LDS copies
   HQueue* dq; HNode* dnd; int16_t* dfl;
+  CReq* rqp;
 
   __device__ __forceinline__ Tile(const CP& p, const CS& s, uint32_t l, int out_parity) : P(p), S(s), lt(l), tile(p.tb + l), po(out_parity)
   {
@@ -292,6 +295,7 @@ struct Tile {
     out_addr = S.out_addr[lt]; out_time = S.out_time[lt];
     blocked = S.blocked[lt]; seq = S.seq[lt]; nrep = S.nrep[lt]; nrq = S.nrq[lt];
     dq = S.dq + lt; dnd = S.dnd + (size_t)lt * P.max_list; dfl = S.dfl + (size_t)lt * P.max_list;
+    rqp = S.rq + (size_t)lt * P.QC;
   }
   __device__ __forceinline__ void flush()
   {
@@ -309,6 +313,12 @@ struct Tile {
 
   // MemoryManager::sendMsg (…msi/memory_manager.cc:306-332)
   __device__ __forceinline__ void send(uint32_t dst, uint32_t type, uint32_t requester, uint64_t addr, uint64_t t)
+  {
+    const uint64_t p0 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
+    send_(dst, type, requester, addr, t);
+    if (S.prof) atomicAdd(&S.prof[11], (unsigned long long)(__builtin_amdgcn_s_memtime() - p0));
+  }
+  __device__ __forceinline__ void send_(uint32_t dst, uint32_t type, uint32_t requester, uint64_t addr, uint64_t t)
   {
     const uint32_t i = atomicAdd(&S.cnt[po], 1u);
     if (i >= P.msg_cap) { fail(GG_DERR_CAP); return; }
@@ -356,6 +366,13 @@ struct Tile {
   }
   // getDirectoryEntry (directory_cache.cc:102-145)
   __device__ __forceinline__ int32_t dget(uint64_t a, uint64_t& t)
+  {
+    const uint64_t p0 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
+    const int32_t r = dget_(a, t);
+    if (S.prof) atomicAdd(&S.prof[9], (unsigned long long)(__builtin_amdgcn_s_memtime() - p0));
+    return r;
+  }
+  __device__ __forceinline__ int32_t dget_(uint64_t a, uint64_t& t)
   {
     t += P.lat_dir;
     st[GG_CT_DIR_ACCESSES]++;
@@ -418,7 +435,7 @@ struct Tile {
   }
 
   // ---- per-address request FIFO (HashMapList<IntPtr, ShmemReq*>) -----------
-  __device__ __forceinline__ CReq* q() const { return S.rq + (size_t)lt * P.QC; }
+  __device__ __forceinline__ CReq* q() const { return rqp; }
   __device__ __forceinline__ uint32_t qcount(uint64_t a) const
   {
     const uint32_t n = nrq; uint32_t c = 0;
@@ -456,6 +473,13 @@ struct Tile {
 
   // ---- DramCntlr / DramPerfModel --------------------------------------------
   __device__ __forceinline__ uint64_t dram_ps(uint64_t t)
+  {
+    const uint64_t p0 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
+    const uint64_t r = dram_ps_(t);
+    if (S.prof) atomicAdd(&S.prof[10], (unsigned long long)(__builtin_amdgcn_s_memtime() - p0));
+    return r;
+  }
+  __device__ __forceinline__ uint64_t dram_ps_(uint64_t t)
   {
     const uint64_t pkt_ns = (uint64_t)ceil(t / 1000.0);
     uint64_t qd = 0;
@@ -817,8 +841,20 @@ __device__ __forceinline__ void copy_words(uint32_t* dst, const uint32_t* src, u
 {
   for (uint32_t i = lane; i < words; i += GG_WAVE) dst[i] = src[i];
 }
+// bytes (multiple of 4) between 16-B aligned buffers where possible
+__device__ __forceinline__ void copy_bytes(void* dst, const void* src, uint32_t bytes, uint32_t lane)
+{
+  if ((((uintptr_t)dst | (uintptr_t)src | bytes) & 15) == 0) {
+    uint4* d = (uint4*)dst; const uint4* q = (const uint4*)src;
+    for (uint32_t i = lane; i < bytes / 16; i += GG_WAVE) d[i] = q[i];
+  } else {
+    copy_words((uint32_t*)dst, (const uint32_t*)src, bytes / 4, lane);
+  }
+}
 
-__device__ void c_tile_step(const CP& P, const CS& S, int p, uint64_t barrier, uint32_t lt, TreeLds* tl);
+struct StepLds { TreeLds* tree; CReq* rq; uint32_t* nrq_out; };
+
+__device__ __forceinline__ void c_tile_step(const CP& P, const CS& S, int p, uint64_t barrier, uint32_t lt, const StepLds* sl);
 
 __global__ void __launch_bounds__(64) k_c_tiles(CP P, CS S, int p, uint64_t barrier)
 {
@@ -832,28 +868,43 @@ __global__ void __launch_bounds__(64) k_c_tiles(CP P, CS S, int p, uint64_t barr
   const uint32_t lt = blockIdx.x, lane = threadIdx.x;
   if (lt == 0 && lane == 0) S.ri[GG_RI_STEPS]++;
   __shared__ TreeLds tl;
-  const bool stage = P.dram_qm && P.max_list <= kTreeLds && (P.max_list % 2) == 0;
+  extern __shared__ __attribute__((aligned(16))) uint8_t csm[];
+  StepLds sl{};
+  const bool tree = P.dram_qm && P.max_list <= kTreeLds && (P.max_list % 2) == 0;
   const uint32_t qw = sizeof(HQueue) / 4, nw = P.max_list * sizeof(HNode) / 4, fw = (P.max_list + 1) / 2;
-  if (stage) {
+  sl.tree = tree ? &tl : nullptr;
+  if (tree) {
     copy_words((uint32_t*)&tl.q, (const uint32_t*)(S.dq + lt), qw, lane);
     copy_words((uint32_t*)tl.nd, (const uint32_t*)(S.dnd + (size_t)lt * P.max_list), nw, lane);
     copy_words((uint32_t*)tl.fl, (const uint32_t*)(S.dfl + (size_t)lt * P.max_list), fw, lane);
-    __syncthreads();
   }
-  if (lane == 0) c_tile_step(P, S, p, barrier, lt, stage ? &tl : nullptr);
-  if (stage) {
-    __syncthreads();
+  // the directory request FIFO (HashMapList of dram_directory_cntlr.h:46): its
+  // scans are loops of dependent loads; staged when QC entries fit
+  __shared__ uint32_t nrq_out;
+  CReq* grq = S.rq + (size_t)lt * P.QC;
+  if (P.stage_rq) {
+    sl.rq = (CReq*)csm;
+    sl.nrq_out = &nrq_out;
+    copy_words((uint32_t*)sl.rq, (const uint32_t*)grq, S.nrq[lt] * (sizeof(CReq) / 4), lane);
+  }
+  __syncthreads();
+  if (lane == 0) c_tile_step(P, S, p, barrier, lt, &sl);
+  __syncthreads();
+  if (P.stage_rq) copy_words((uint32_t*)grq, (const uint32_t*)sl.rq, nrq_out * (sizeof(CReq) / 4), lane);
+  if (tree) {
     copy_words((uint32_t*)(S.dq + lt), (const uint32_t*)&tl.q, qw, lane);
     copy_words((uint32_t*)(S.dnd + (size_t)lt * P.max_list), (const uint32_t*)tl.nd, nw, lane);
     copy_words((uint32_t*)(S.dfl + (size_t)lt * P.max_list), (const uint32_t*)tl.fl, fw, lane);
   }
 }
 
-__device__ void c_tile_step(const CP& P, const CS& S, int p, uint64_t barrier, uint32_t lt, TreeLds* tl)
+__device__ __forceinline__ void c_tile_step(const CP& P, const CS& S, int p, uint64_t barrier, uint32_t lt, const StepLds* sl)
 {
   const uint64_t c0 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
+  const uint64_t r0 = S.prof ? __builtin_amdgcn_s_memrealtime() : 0;
   Tile T(P, S, lt, 1 - p);
-  if (tl) { T.dq = &tl->q; T.dnd = tl->nd; T.dfl = tl->fl; }
+  if (sl && sl->tree) { T.dq = &sl->tree->q; T.dnd = sl->tree->nd; T.dfl = sl->tree->fl; }
+  if (sl && sl->rq) T.rqp = sl->rq;
   // 1. gather the inbox list
   int32_t* head = headp(S, p);
   const gg_cmsg* in = bufp(S, p);
@@ -905,6 +956,7 @@ __device__ void c_tile_step(const CP& P, const CS& S, int p, uint64_t barrier, u
   }
   const uint64_t c3 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
   T.flush();
+  if (sl && sl->nrq_out) *sl->nrq_out = T.nrq;
   if (S.prof) {
     const uint64_t c4 = __builtin_amdgcn_s_memtime();
     atomicAdd(&S.prof[0], (unsigned long long)(c1 - c0));     // tile load + inbox gather + sort
@@ -912,8 +964,9 @@ __device__ void c_tile_step(const CP& P, const CS& S, int p, uint64_t barrier, u
     atomicAdd(&S.prof[2], (unsigned long long)(c3 - c2));     // trace
     atomicAdd(&S.prof[3], (unsigned long long)(c4 - c3));     // flush
     atomicAdd(&S.prof[4], (unsigned long long)n);
+    atomicAdd(&S.prof[7], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - r0));   // 100 MHz ticks
     const uint32_t st = (uint32_t)S.ri[GG_RI_STEPS];
-    if (st < S.prof_steps) atomicMax(&S.prof[8 + st], (unsigned long long)(c4 - c0));
+    if (st < S.prof_steps) atomicMax(&S.prof[16 + st], (unsigned long long)(c4 - c0));
   }
 }
 
@@ -1152,10 +1205,15 @@ static gg_status coh_alloc(gg_ctx* ctx)
   P.msg_cap = (uint64_t)64 * P.T + 65536;
   // a wave per tile (default; GG_COH_TILES_PER_BLOCK=64 packs a lane per tile, for A/B runs)
   { const char* e = getenv("GG_COH_TILES_PER_BLOCK"); P.tiles_per_block = (e && atoi(e) == 64) ? 64 : 1; }
+  {
+    const uint64_t rq = (uint64_t)P.QC * sizeof(CReq);
+    const char* r = getenv("GG_COH_STAGE_RQ");
+    P.stage_rq = (P.tiles_per_block == 1 && rq <= 48 * 1024 && !(r && atoi(r) == 0)) ? 1 : 0;
+  }
   if (getenv("GG_COH_PROFILE") && atoi(getenv("GG_COH_PROFILE"))) {
     C->S.prof_steps = 1u << 16;
-    if (gg_status st = dalloc(C, &C->S.prof, 8 + C->S.prof_steps)) return st;
-    GG_HIP(hipMemset(C->S.prof, 0, sizeof(unsigned long long) * (8 + C->S.prof_steps)));
+    if (gg_status st = dalloc(C, &C->S.prof, 16 + C->S.prof_steps)) return st;
+    GG_HIP(hipMemset(C->S.prof, 0, sizeof(unsigned long long) * (16 + C->S.prof_steps)));
   }
   P.np = gg_noc_params(ctx);
   const uint64_t L = P.lt;
@@ -1239,13 +1297,17 @@ gg_status gg_coherent_quantum(gg_ctx* ctx, uint64_t q, gg_coherent_status* out)
   GG_HIP(hipMemsetAsync(C->S.quiet, 0, sizeof(uint32_t), s));
   const uint32_t tb = (P.lt + 63) / 64;
   const uint32_t rb = (uint32_t)std::min<uint64_t>((P.msg_cap + 255) / 256, 1024);
+  const uint32_t dyn_lds = P.stage_rq ? P.QC * (uint32_t)sizeof(CReq) : 0u;
+  if (dyn_lds)
+    GG_HIP(hipFuncSetAttribute((const void*)k_c_tiles, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)(dyn_lds + sizeof(TreeLds) + 16)));
   uint64_t steps = 0;
   uint32_t batch = 8;
   for (;;) {
     for (uint32_t k = 0; k < batch; ++k) {
       const int p = (int)((steps + k) & 1);
       if (P.tiles_per_block == 1)
-        hipLaunchKernelGGL(k_c_tiles, dim3(P.lt), dim3(64), 0, s, P, C->S, p, barrier);
+        hipLaunchKernelGGL(k_c_tiles, dim3(P.lt), dim3(64), dyn_lds, s, P, C->S, p, barrier);
       else
         hipLaunchKernelGGL(k_c_tiles, dim3(tb), dim3(64), 0, s, P, C->S, p, barrier);
       if (ctx->cfg.net_model == GG_NET_EMESH_HOP_BY_HOP) {
@@ -1377,13 +1439,15 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
   gg_timer_end(ctx, "coherent_run", s);
   GG_HIP(hipStreamSynchronize(s));
   if (C->S.prof) {
-    std::vector<unsigned long long> h(8 + C->S.prof_steps);
+    std::vector<unsigned long long> h(16 + C->S.prof_steps);
     GG_HIP(hipMemcpy(h.data(), C->S.prof, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
     unsigned long long crit = 0, nst = 0;
-    for (uint32_t i = 0; i < C->S.prof_steps; ++i) { crit += h[8 + i]; nst += h[8 + i] ? 1 : 0; }
+    for (uint32_t i = 0; i < C->S.prof_steps; ++i) { crit += h[16 + i]; nst += h[16 + i] ? 1 : 0; }
     fprintf(stderr, "[gg_coh] tile-step cycles summed over tiles: gather+sort %llu handlers %llu (directory %llu, L2 %llu)"
-            " trace %llu flush %llu | msgs %llu | critical path (max tile per step, %llu steps) %llu cycles\n",
-            h[0], h[1], h[5], h[6], h[2], h[3], h[4], nst, crit);
+            " trace %llu flush %llu | msgs %llu | critical path (max tile per step, %llu steps) %llu cycles"
+            " | memtime/memrealtime %.1f MHz | dget %llu dram %llu send %llu\n",
+            h[0], h[1], h[5], h[6], h[2], h[3], h[4], nst, crit,
+            h[7] ? 100.0 * (double)(h[0] + h[1] + h[2] + h[3]) / (double)h[7] : 0.0, h[9], h[10], h[11]);
   }
   return coh_check(ctx);
 }

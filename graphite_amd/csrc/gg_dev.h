@@ -120,20 +120,40 @@ struct HTree {
     return succ;
   }
   __device__ int remove(int node) { q->size--; return remove_rec(node); }
-  __device__ int search(uint64_t a, uint64_t b) const          // searchTree
+  // searchTree (interval_tree.cc:366-394).  The recursion comes back to a
+  // node only after searching its LEFT subtree (it descends left only when
+  // b < first), so the pending nodes are exactly the ancestors entered through
+  // their left child: falling off the tree right after a left descent resumes
+  // that node; otherwise the walk climbs parent pointers to the nearest
+  // ancestor whose left subtree it is leaving.  No explicit stack (a
+  // dynamically indexed array would live in scratch memory).
+  __device__ int search(uint64_t a, uint64_t b) const
   {
-    int stack[40]; int sp = 0; int n = q->root;
+    int n = q->root, last = -1;
+    bool went_left = false;
     for (;;) {
       if (n < 0) {
-        if (sp == 0) return -1;
-        n = stack[--sp];
-        if (a < nd[n].first && (nd[n].second - nd[n].first) >= (b - a)) return n;
-        n = nd[n].right; continue;
+        int p;
+        if (went_left) {
+          p = last;
+        } else {
+          int c = last;
+          for (;;) {
+            if (c < 0) return -1;
+            p = nd[c].parent;
+            if (p < 0) return -1;
+            if (nd[p].left == c) break;
+            c = p;
+          }
+        }
+        if (a < nd[p].first && (nd[p].second - nd[p].first) >= (b - a)) return p;
+        last = p; went_left = false; n = nd[p].right;
+        continue;
       }
       if (a >= nd[n].first && b <= nd[n].second) return n;
-      if (b < nd[n].first) { if (sp < 40) { stack[sp++] = n; n = nd[n].left; continue; } return -1; }
+      if (b < nd[n].first) { last = n; went_left = true; n = nd[n].left; continue; }
       if (a < nd[n].first && (nd[n].second - nd[n].first) >= (b - a)) return n;
-      n = nd[n].right;
+      last = n; went_left = false; n = nd[n].right;
     }
   }
   __device__ int alloc(uint64_t a, uint64_t b)                 // allocateNode
