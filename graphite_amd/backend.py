@@ -14,7 +14,8 @@ from .config import (GGConfig, NUM_CACHE_COUNTERS, NUM_NET_COUNTERS, NUM_TILE_ST
                      CMSG_DTYPE)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libgraphite_gpu.so")
+# GG_LIB (diagnostics only): load an alternative in-tree build for A/B kernel runs
+LIB_PATH = os.environ.get("GG_LIB") or os.path.join(HERE, "libgraphite_gpu.so")
 
 GG_OK = 0
 _ERR = {-1: "GG_ERR_INVALID", -2: "GG_ERR_HIP", -3: "GG_ERR_UNSUPPORTED", -4: "GG_ERR_RANGE", -5: "GG_ERR_STATE"}

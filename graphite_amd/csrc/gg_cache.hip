@@ -1378,6 +1378,9 @@ __global__ __launch_bounds__((NCW + 1) * GG_WAVE) void k_cache_stream(gg_cache_s
   }
 
   // ---------------- consumers: one unit per lane ----------------
+#ifdef GG_CONS_PRIO
+  __builtin_amdgcn_s_setprio(GG_CONS_PRIO);
+#endif
   // The L1-D set lives in four VGPRs: pos1 (byte w = L2 slot s*A2+w of the
   // line L1-D way w holds, 0xFF = invalid; the L1-D only holds lines its L2
   // holds, checked on entry), mbyt (0x80 in byte w iff way w is MODIFIED),
@@ -1396,8 +1399,8 @@ __global__ __launch_bounds__((NCW + 1) * GG_WAVE) void k_cache_stream(gg_cache_s
   auto bytes_of = [](uint32_t m) { return m | (m - (m >> 7)); };
 
   // counters: the result word's eight 1-bit nibble fields summed into byte
-  // fields (even / odd nibbles), folded into u32 totals every 128 iterations
-  // (wave-uniform, so <= 128 per byte); WRITE splits of the two miss fields in
+  // fields (even / odd nibbles), folded into u32 totals every 128 stepping
+  // passes (wave-uniform, so <= 128 per byte); WRITE splits of the two miss fields in
   // two 16-bit halves.
   uint32_t f8[8], c_wr = 0, c_nh1w = 0, c_m2w = 0;
 #pragma unroll
@@ -1532,7 +1535,7 @@ __global__ __launch_bounds__((NCW + 1) * GG_WAVE) void k_cache_stream(gg_cache_s
   uint32_t h = 0, idle = 0, d_iter = 0, d_sleep = 0;
   uint32_t t = ld32(&tailp[u]);
   uint64_t kn = ld64(&ring[u]);
-  for (uint32_t it = 1;; ++it) {
+  for (;;) {
     bool have = h < t;
     if (!__ballot(have)) {
       const uint32_t d = ld32(donep);                    // before the tails: final once set
@@ -1564,7 +1567,9 @@ __global__ __launch_bounds__((NCW + 1) * GG_WAVE) void k_cache_stream(gg_cache_s
       count(rv, kl & 1u);
     }
     h = hn;
-    if ((it & 127u) == 0) flush();
+    // fold the byte fields after every 128 passes that reached here (each adds
+    // at most 1 per field); idle passes `continue` above and add nothing
+    if ((d_iter & 127u) == 0) flush();
   }
   flush();
   if (dbg && lane == 0) {

@@ -171,3 +171,32 @@ def test_full_size_config2_subset_and_properties():
     assert int(((r & C.RES_L1_MISS) != 0).sum()) == int(l1[:, 1].sum())
     assert int(((r & C.RES_L2_EVICT) != 0).sum()) == int(l2[:, 6].sum())
     assert int(((r & C.RES_L2_EVICT_DIRTY) != 0).sum()) == int(l2[:, 7].sum())
+
+
+def test_stream_idle_waves_alternating_bursts():
+    """Streaming replay with consumer waves that go idle for long stretches:
+    records come in bursts that name only the L1-D sets of one consumer wave
+    (sets 0..63, then 64..127, ...), so the other wave polls an empty ring while
+    it keeps its counters in byte fields.  Results and counters bit-exact vs the
+    oracle (guards the counter-folding cadence against idle passes)."""
+    torch = torch_dev()
+    T, N = 16, 400000
+    rng = np.random.default_rng(11)
+    addrs, metas = [], []
+    for t in range(T):
+        a, m = po.gen_uniform(t, 0, N, lines_log2=16)
+        line = a >> np.uint64(6)
+        burst = np.cumsum(rng.integers(1500, 4000, N // 1500 + 1))
+        half = (np.searchsorted(burst, np.arange(N), side="right") & 1).astype(np.uint64)
+        s = (line & np.uint64(63)) | (half << np.uint64(6))
+        line = (line & ~np.uint64(127)) | s
+        addrs.append(line << np.uint64(6))
+        metas.append(m)
+    addr, meta = np.concatenate(addrs), np.concatenate(metas)
+    offs = np.arange(T + 1, dtype=np.uint64) * np.uint64(N)
+    cfg = C.default_config(T)
+    oc = po.OracleCache(cfg)
+    ref = oc.run(addr, meta, offs)
+    be, res, _ = run_gpu(cfg, addr, meta, offs, torch, want_ev=False)
+    np.testing.assert_array_equal(res, ref)
+    np.testing.assert_array_equal(be.cache_counters(), oc.counters())
