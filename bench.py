@@ -86,6 +86,8 @@ def parse():
                    help="coherent-mode (Mode C) section: total tiles (0 = skip); configs[2] = 256")
     p.add_argument("--coherent-per-tile", type=int, default=4096, help="coherent-mode accesses per tile")
     p.add_argument("--coherent-shards", type=int, default=0, help="logical shards (0 = 1, or 8 with --gpus > 1)")
+    p.add_argument("--coherent-net", default="hop_counter", choices=["hop_counter", "hop_by_hop", "magic"],
+                   help="memory-network model of the coherent section (hop_by_hop needs one logical shard)")
     p.add_argument("--coherent", action="store_true",
                    help="run the coherent section on N > 1 ranks too (RCCL all-to-all per quantum)")
     p.add_argument("--fft-m", type=int, default=14,
@@ -107,7 +109,8 @@ def coherent_section(args, world, rank, dev, backend_name):
     T, N = args.coherent_tiles, args.coherent_per_tile
     K = args.coherent_shards or (8 if world > 1 else 1)
     k0, k1 = CO.shard_range(rank, world, K)
-    cfg = C.default_config(T, num_shards=K, shard_begin=k0, shard_end=k1)
+    net = {"hop_counter": C.NET_EMESH_HOP_COUNTER, "hop_by_hop": C.NET_EMESH_HOP_BY_HOP, "magic": C.NET_MAGIC}[args.coherent_net]
+    cfg = C.default_config(T, num_shards=K, shard_begin=k0, shard_end=k1, net_model=net)
     be = B.Backend(cfg)
     addr = torch.empty(T * N, dtype=torch.int64, device=dev)
     meta = torch.empty(T * N, dtype=torch.int32, device=dev)
@@ -130,7 +133,7 @@ def coherent_section(args, world, rank, dev, backend_name):
     st, cc, ri = be.coherent_stats()
     res = {"workload": "configs[2]-style hotspot trace: %d tiles x %d accesses (20%% to 64 shared lines, "
                        "WRITE 1/3, gap ~2 cycles), MSI full-map directory + DRAM history tree + "
-                       "emesh_hop_counter, quantum 1000 ns, %d logical shard(s)" % (T, N, K),
+                       "%s, quantum 1000 ns, %d logical shard(s)" % (T, N, "magic" if args.coherent_net == "magic" else "emesh_" + args.coherent_net, K),
            "value": T * N / elapsed, "unit": "accesses/s", "seconds": elapsed,
            "quanta": int(ri[C.RUN_INFO.index("quanta")]) if quanta is None else quanta,
            "steps": int(ri[C.RUN_INFO.index("steps")]),
@@ -139,7 +142,7 @@ def coherent_section(args, world, rank, dev, backend_name):
     if rank == 0 and world == 1 and not args.no_verify:
         from oracle import pyoracle as po
         a, m, o = po.gen_trace(T, N, hot_lines=64)
-        oc = po.OracleCoherent(C.default_config(T, num_shards=K))
+        oc = po.OracleCoherent(C.default_config(T, num_shards=K, net_model=net))
         c0 = time.perf_counter()
         ref = oc.run(a, m, o)
         cdt = time.perf_counter() - c0

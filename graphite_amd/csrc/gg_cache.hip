@@ -1137,7 +1137,13 @@ __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_
 //     result[tile base + index] (scattered dword stores that fill whole lines
 //     in L2 while the tile's window is in flight).
 // ---------------------------------------------------------------------------
-constexpr uint32_t kRing = 32;
+#ifndef GG_RING
+#define GG_RING 32
+#endif
+#ifndef GG_PK
+#define GG_PK 4
+#endif
+constexpr uint32_t kRing = GG_RING;
 constexpr uint32_t kSpinLimit = 1u << 22;   // s_sleep(1) polls (~64 cycles each) before giving up
 constexpr uint16_t kLgkm0 = 0xC07F;         // s_waitcnt lgkmcnt(0) (vmcnt/expcnt fields at their maxima)
 
@@ -1254,7 +1260,10 @@ __global__ __launch_bounds__((NCW + 1) * GG_WAVE) void k_cache_stream(gg_cache_s
     //   ds_add  resv[unit] += 1               -> += the round's count of the unit
     // position = base + lanes of the unit below this lane (program order).
     // Space and publication are checked per unit (lane l owns units l + 64 i).
-    constexpr int K = 8;
+#ifdef GG_PROD_PRIO
+    __builtin_amdgcn_s_setprio(GG_PROD_PRIO);
+#endif
+    constexpr int K = GG_PK;
     const uint64_t* ap = addr + base;
     const uint32_t* mp = meta + base;
     const uint64_t lt_mask = (1ull << lane) - 1;
@@ -1531,7 +1540,11 @@ __global__ __launch_bounds__((NCW + 1) * GG_WAVE) void k_cache_stream(gg_cache_s
     c_wr += wr;
   };
 
-  const bool nostep = dbg && dbg[7] == 1;               // diagnostics: hand-off machinery alone
+#ifdef GG_STREAM_NOSTEP
+  const bool nostep = dbg && dbg[7] == 1;               // diagnostics build: hand-off machinery alone
+#else
+  constexpr bool nostep = false;
+#endif
   uint32_t h = 0, idle = 0, d_iter = 0, d_sleep = 0;
   uint32_t t = ld32(&tailp[u]);
   uint64_t kn = ld64(&ring[u]);
@@ -1937,7 +1950,7 @@ gg_status gg_cache_run_batch(gg_ctx* ctx, const gg_trace* tr, uint32_t* result, 
       if (dbg_on) {
         GG_HIP(hipMalloc((void**)&dbg, 8 * sizeof(unsigned long long)));
         GG_HIP(hipMemsetAsync(dbg, 0, 8 * sizeof(unsigned long long), s));
-        if (dbg_on == 2) GG_HIP(hipMemsetAsync(dbg + 7, 1, 1, s));   // GG_STREAM_DEBUG=2: skip the cache step
+        if (dbg_on == 2) GG_HIP(hipMemsetAsync(dbg + 7, 1, 1, s));   // GG_STREAM_DEBUG=2: skip the cache step (builds with -DGG_STREAM_NOSTEP)
       }
       // GG_STREAM_NORES=1 (diagnostics only): drop the result stores
       static const bool nores = getenv("GG_STREAM_NORES") && atoi(getenv("GG_STREAM_NORES"));

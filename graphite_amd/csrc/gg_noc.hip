@@ -106,23 +106,70 @@ __device__ __forceinline__ uint32_t ychain_of(const NocParams& P, uint32_t s, ui
 }
 
 // one mesh router hop (RouterModel::processPacket + ElectricalLinkModel::processPacket + Hop)
-__device__ void mesh_hop(const NocDev& D, uint32_t tile, int port, uint32_t bits, uint64_t& t, uint64_t& zl, uint64_t& ct)
+// through the output-port queue `tr` of `tile`
+__device__ void mesh_hop_q(const NocDev& D, uint32_t tile, HTree& tr, uint32_t bits, uint64_t& t, uint64_t& zl, uint64_t& ct,
+                           uint64_t* lc = nullptr)
 {
+  // counters: straight to HBM, or to the workgroup's LDS block of this tile (lc, flushed at the end)
+  auto add = [&](int k, uint64_t v) { if (lc) lc[k] += v; else cadd(D.ctr, tile, k, v); };
   const NocParams& P = D.P;
   const uint64_t nf = nflits(P, bits);
   uint64_t zlc = P.router_delay, qd = 0;
   if (P.qm) {
-    HTree tr = D.tree(tile, port);
     qd = tr.delay(time_to_cycles(t, P.f), nf, D.err);
-    cadd(D.ctr, tile, GG_NC_ROUTER_CONTENTION_CYCLES, qd);
-    cadd(D.ctr, tile, GG_NC_ROUTER_PACKETS, 1);
+    add(GG_NC_ROUTER_CONTENTION_CYCLES, qd);
+    add(GG_NC_ROUTER_PACKETS, 1);
   }
-  cadd(D.ctr, tile, GG_NC_BUFFER_WRITES, nf); cadd(D.ctr, tile, GG_NC_BUFFER_READS, nf);
-  cadd(D.ctr, tile, GG_NC_SWITCH_ALLOC, 1); cadd(D.ctr, tile, GG_NC_CROSSBAR, nf);
+  add(GG_NC_BUFFER_WRITES, nf); add(GG_NC_BUFFER_READS, nf);
+  add(GG_NC_SWITCH_ALLOC, 1); add(GG_NC_CROSSBAR, nf);
   zlc += P.link_delay;
-  cadd(D.ctr, tile, GG_NC_LINK_TRAVERSALS, nf);
+  add(GG_NC_LINK_TRAVERSALS, nf);
   const uint64_t zps = lat_to_ps(zlc, P.f), cps = lat_to_ps(qd, P.f);
   t += zps + cps; zl += zps; ct += cps;
+}
+__device__ void mesh_hop(const NocDev& D, uint32_t tile, int port, uint32_t bits, uint64_t& t, uint64_t& zl, uint64_t& ct)
+{
+  HTree tr = D.tree(tile, port);
+  mesh_hop_q(D, tile, tr, bits, t, zl, ct);
+}
+
+// ---------------------------------------------------------------------------
+// LDS-staged queues.  A stage walks its packets in event order and every
+// queue operation is a chain of dependent node accesses (AVL search, insert,
+// rebalance); from HBM/L2 each costs a memory round trip.  The staged
+// kernels copy the queues a workgroup owns (a chain's w or h ports, or 16
+// tiles' injection / SELF ports) into LDS once per launch, run the same code
+// on the LDS image and write it back.  Image = HQueue | max_size HNode |
+// max_size int16 free list.
+// ---------------------------------------------------------------------------
+__host__ __device__ inline uint32_t qimg_bytes(uint32_t ms)
+{
+  return (uint32_t)((sizeof(HQueue) + ms * sizeof(HNode) + ms * sizeof(int16_t) + 15) & ~15u);
+}
+__device__ inline HTree qimg_tree(uint8_t* img, uint32_t ms, bool analytical)
+{
+  HTree t{reinterpret_cast<HQueue*>(img), reinterpret_cast<HNode*>(img + sizeof(HQueue)),
+          reinterpret_cast<int16_t*>(img + sizeof(HQueue) + ms * sizeof(HNode)), 1, analytical};
+  return t;
+}
+// cooperative copy of queue qi between HBM and its LDS image (all threads of the block)
+__device__ void qimg_copy(const NocDev& D, uint64_t qi, uint8_t* img, bool to_lds)
+{
+  static_assert(sizeof(HQueue) % 8 == 0 && sizeof(HNode) % 8 == 0, "8-byte images");
+  const uint32_t ms = D.P.max_size, tid = threadIdx.x, nt = blockDim.x;
+  uint64_t* gq = reinterpret_cast<uint64_t*>(D.q + qi);
+  uint64_t* gn = reinterpret_cast<uint64_t*>(D.nd + qi * ms);
+  int16_t* gf = D.fl + qi * ms;
+  uint64_t* lq = reinterpret_cast<uint64_t*>(img);
+  uint64_t* ln = reinterpret_cast<uint64_t*>(img + sizeof(HQueue));
+  int16_t* lf = reinterpret_cast<int16_t*>(img + sizeof(HQueue) + ms * sizeof(HNode));
+  constexpr uint32_t QW = sizeof(HQueue) / 8;
+  const uint32_t NW = ms * (uint32_t)(sizeof(HNode) / 8);
+  for (uint32_t i = tid; i < QW + NW + ms; i += nt) {
+    if (i < QW) { if (to_lds) lq[i] = gq[i]; else gq[i] = lq[i]; }
+    else if (i < QW + NW) { const uint32_t j = i - QW; if (to_lds) ln[j] = gn[j]; else gn[j] = ln[j]; }
+    else { const uint32_t j = i - QW - NW; if (to_lds) lf[j] = gf[j]; else gf[j] = lf[j]; }
+  }
 }
 
 // Stage 0: injection port of each source tile, packets in (time, index) order.
@@ -210,6 +257,206 @@ __global__ void k_self(NocDev D, const uint32_t* __restrict__ dst, const uint32_
     cadd(D.ctr, tile, GG_NC_TOTAL_LATENCY_PS, zl + ct); cadd(D.ctr, tile, GG_NC_TOTAL_CONTENTION_PS, ct);
     S.t[k] = t; S.zl[k] = zl; S.ct[k] = ct;
   }
+}
+
+// Staged packets: a workgroup's packets (a contiguous bucket range [B, E))
+// gathered into LDS next to its queues — the event heap, the working times
+// and the canonical keys — so the serial event walk touches no HBM; written
+// back at the end.  Used when they fit (kPktLdsBytes per packet), else the
+// walk keeps its heap and packet state in HBM.
+constexpr uint32_t kPortTiles = 16;
+constexpr size_t kStageLdsMax = 160 * 1024;
+constexpr uint32_t kPktLdsBytes = sizeof(Ev) + 5 * 8 + 4 * 4;
+constexpr uint32_t kCtrBytes = GG_NUM_NET_COUNTERS * 8;   // a tile's counter block in LDS
+__device__ void lctr_zero(uint64_t* lc, uint32_t ntiles)
+{
+  for (uint32_t i = threadIdx.x; i < ntiles * GG_NUM_NET_COUNTERS; i += blockDim.x) lc[i] = 0;
+}
+template <class TileAt>
+__device__ void lctr_flush(const NocDev& D, const uint64_t* lc, uint32_t ntiles, TileAt tile_at)
+{
+  for (uint32_t i = threadIdx.x; i < ntiles * GG_NUM_NET_COUNTERS; i += blockDim.x)
+    if (lc[i]) cadd(D.ctr, tile_at(i / GG_NUM_NET_COUNTERS), (int)(i % GG_NUM_NET_COUNTERS), lc[i]);
+}
+struct LPk {
+  Ev* heap; uint64_t *t, *zl, *ct, *khi, *klo; uint32_t *cur, *dst, *len, *gid;
+  __device__ LPk(uint8_t* base, uint32_t np)
+  {
+    heap = reinterpret_cast<Ev*>(base);
+    t = reinterpret_cast<uint64_t*>(heap + np); zl = t + np; ct = zl + np; khi = ct + np; klo = khi + np;
+    cur = reinterpret_cast<uint32_t*>(klo + np); dst = cur + np; len = dst + np; gid = len + np;
+  }
+  __device__ Ev ev(uint32_t i) const { return Ev{t[i], khi[i], klo[i], i, 0}; }
+};
+__device__ void lpk_load(LPk& L, uint64_t B, uint32_t np, const uint32_t* bucket_ids, const PktState& S,
+                         const uint32_t* dst, const uint32_t* len)
+{
+  for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) {
+    const uint32_t k = bucket_ids[B + i];
+    L.gid[i] = k; L.t[i] = S.t[k]; L.zl[i] = S.zl[k]; L.ct[i] = S.ct[k]; L.cur[i] = S.cur[k];
+    L.dst[i] = dst[k]; L.len[i] = len[k];
+    L.khi[i] = S.khi ? S.khi[k] : 0ull; L.klo[i] = S.klo ? S.klo[k] : (uint64_t)k;
+  }
+}
+__device__ void lpk_store(const LPk& L, uint32_t np, const PktState& S)
+{
+  for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) {
+    const uint32_t k = L.gid[i];
+    S.t[k] = L.t[i]; S.zl[k] = L.zl[i]; S.ct[k] = L.ct[i]; S.cur[k] = L.cur[i];
+  }
+}
+
+// Staged stage 0 / 3: kPortTiles tiles per workgroup, one thread per tile,
+// their injection (port 5) or SELF (port 0) queues in LDS.
+template <bool SELF>
+__global__ __launch_bounds__(64) void k_port_staged(NocDev D, const uint32_t* __restrict__ dst,
+    const uint32_t* __restrict__ len, const uint64_t* __restrict__ bucket_off,
+    const uint32_t* __restrict__ bucket_ids, Ev* heap, PktState S)
+{
+  extern __shared__ __attribute__((aligned(16))) uint8_t qlds[];
+  const uint32_t ms = D.P.max_size, qb = qimg_bytes(ms);
+  const uint32_t t0 = blockIdx.x * kPortTiles;
+  const uint32_t nt = min(kPortTiles, D.P.tiles - t0);
+  const uint64_t B = bucket_off[t0], E = bucket_off[t0 + nt];
+  if (B == E) return;                                                // no packet in these tiles
+  const uint32_t np = (uint32_t)(E - B);
+  const bool lp = (size_t)nt * (qb + kCtrBytes) + (size_t)np * kPktLdsBytes <= kStageLdsMax;
+  uint64_t* lcb = reinterpret_cast<uint64_t*>(qlds + nt * qb);
+  LPk L(qlds + nt * (qb + kCtrBytes), lp ? np : 0u);
+  const int port = SELF ? P_SELF : 5;
+  for (uint32_t i = 0; i < nt; ++i) qimg_copy(D, (uint64_t)(t0 + i) * 6 + port, qlds + i * qb, true);
+  if (lp) lpk_load(L, B, np, bucket_ids, S, dst, len);
+  if (lp) lctr_zero(lcb, nt);
+  __syncthreads();
+  if (threadIdx.x < nt) {
+    const uint32_t tile = t0 + threadIdx.x;
+    uint64_t* lc = lcb + threadIdx.x * GG_NUM_NET_COUNTERS;
+    const uint64_t b = bucket_off[tile], e = bucket_off[tile + 1];
+    HTree tr = qimg_tree(qlds + threadIdx.x * qb, ms, D.P.analytical != 0);
+    if (lp) {
+      Ev* h = L.heap + (b - B);
+      uint32_t n = 0;
+      for (uint32_t i = (uint32_t)(b - B); i < (uint32_t)(e - B); ++i) heap_push(h, n, L.ev(i));
+      while (n) {
+        const uint32_t i = heap_pop(h, n).id;
+        const uint64_t nf = nflits(D.P, L.len[i]);
+        if (!SELF) {                                  // k_inject
+          lc[GG_NC_PACKETS_SENT] += 1; lc[GG_NC_FLITS_SENT] += nf;
+          lc[GG_NC_BITS_SENT] += L.len[i];
+          uint64_t qd = 0;
+          if (D.P.qm) qd = tr.delay(time_to_cycles(L.t[i], D.P.f), nf, D.err);
+          const uint64_t cps = lat_to_ps(qd, D.P.f);
+          L.t[i] += lat_to_ps(0, D.P.f) + cps;
+          L.ct[i] += cps;
+        } else {                                      // k_self
+          uint64_t t = L.t[i], zl = L.zl[i], ct = L.ct[i];
+          mesh_hop_q(D, tile, tr, L.len[i], t, zl, ct, lc);
+          const uint64_t ser = lat_to_ps(nf, D.P.f);
+          t += ser; zl += ser;
+          lc[GG_NC_PACKETS_RECEIVED] += 1; lc[GG_NC_FLITS_RECEIVED] += nf;
+          lc[GG_NC_BITS_RECEIVED] += L.len[i];
+          lc[GG_NC_TOTAL_LATENCY_PS] += zl + ct; lc[GG_NC_TOTAL_CONTENTION_PS] += ct;
+          L.t[i] = t; L.zl[i] = zl; L.ct[i] = ct;
+        }
+      }
+    } else {
+      Ev* h = heap + b;
+      uint32_t n = 0;
+      for (uint64_t i = b; i < e; ++i) { uint32_t k = bucket_ids[i]; heap_push(h, n, mkev(S, S.t[k], k)); }
+      while (n) {
+        const uint32_t k = heap_pop(h, n).id;
+        const uint64_t nf = nflits(D.P, len[k]);
+        if (!SELF) {
+          cadd(D.ctr, tile, GG_NC_PACKETS_SENT, 1); cadd(D.ctr, tile, GG_NC_FLITS_SENT, nf);
+          cadd(D.ctr, tile, GG_NC_BITS_SENT, len[k]);
+          uint64_t qd = 0;
+          if (D.P.qm) qd = tr.delay(time_to_cycles(S.t[k], D.P.f), nf, D.err);
+          const uint64_t cps = lat_to_ps(qd, D.P.f);
+          S.t[k] += lat_to_ps(0, D.P.f) + cps;
+          S.ct[k] += cps;
+        } else {
+          uint64_t t = S.t[k], zl = S.zl[k], ct = S.ct[k];
+          mesh_hop_q(D, tile, tr, len[k], t, zl, ct);
+          const uint64_t ser = lat_to_ps(nf, D.P.f);
+          t += ser; zl += ser;
+          cadd(D.ctr, tile, GG_NC_PACKETS_RECEIVED, 1); cadd(D.ctr, tile, GG_NC_FLITS_RECEIVED, nf);
+          cadd(D.ctr, tile, GG_NC_BITS_RECEIVED, len[k]);
+          cadd(D.ctr, tile, GG_NC_TOTAL_LATENCY_PS, zl + ct); cadd(D.ctr, tile, GG_NC_TOTAL_CONTENTION_PS, ct);
+          S.t[k] = t; S.zl[k] = zl; S.ct[k] = ct;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (lp) lpk_store(L, np, S);
+  if (lp) lctr_flush(D, lcb, nt, [&](uint32_t i) { return t0 + i; });
+  for (uint32_t i = 0; i < nt; ++i) qimg_copy(D, (uint64_t)(t0 + i) * 6 + port, qlds + i * qb, false);
+}
+
+// Staged stages X / Y: one workgroup per chain (row or column, direction),
+// the chain's w (or h) output-port queues in LDS; thread 0 walks the events.
+__global__ __launch_bounds__(64) void k_chain_staged(NocDev D, int stage, const uint32_t* __restrict__ dst,
+    const uint32_t* __restrict__ len, const uint64_t* __restrict__ bucket_off,
+    const uint32_t* __restrict__ bucket_ids, Ev* heap, PktState S)
+{
+  extern __shared__ __attribute__((aligned(16))) uint8_t qlds[];
+  const NocParams& P = D.P;
+  const uint32_t c = blockIdx.x, line = c / 2, dir = c % 2;
+  const uint64_t b = bucket_off[c], e = bucket_off[c + 1];
+  if (b == e) return;
+  const uint32_t ms = P.max_size, qb = qimg_bytes(ms);
+  const uint32_t Lq = stage == 0 ? P.w : P.h;
+  const uint32_t np = (uint32_t)(e - b);
+  const bool lp = (size_t)Lq * (qb + kCtrBytes) + (size_t)np * kPktLdsBytes <= kStageLdsMax;
+  uint64_t* lcb = reinterpret_cast<uint64_t*>(qlds + Lq * qb);
+  LPk L(qlds + Lq * (qb + kCtrBytes), lp ? np : 0u);
+  const int port = stage == 0 ? (dir ? P_RIGHT : P_LEFT) : (dir ? P_UP : P_DOWN);   // xchain_of / ychain_of
+  auto tile_at = [&](uint32_t i) -> uint32_t { return stage == 0 ? line * P.w + i : i * P.w + line; };
+  for (uint32_t i = 0; i < Lq; ++i) qimg_copy(D, (uint64_t)tile_at(i) * 6 + port, qlds + i * qb, true);
+  if (lp) lpk_load(L, b, np, bucket_ids, S, dst, len);
+  if (lp) lctr_zero(lcb, Lq);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    // one hop of packet (cur, d) along the chain; returns whether it left the chain
+    auto hop = [&](uint32_t cur, uint32_t d, uint32_t bits, uint64_t& t, uint64_t& zl, uint64_t& ct,
+                   uint32_t& next) -> bool {
+      uint32_t pos;
+      bool done;
+      if (stage == 0) { next = dir ? cur + 1 : cur - 1; done = (next % P.w) == d % P.w; pos = cur % P.w; }
+      else { next = dir ? cur + P.w : cur - P.w; done = (next / P.w) == d / P.w; pos = cur / P.w; }
+      HTree tr = qimg_tree(qlds + pos * qb, ms, P.analytical != 0);
+      mesh_hop_q(D, cur, tr, bits, t, zl, ct, lp ? lcb + pos * GG_NUM_NET_COUNTERS : nullptr);
+      return done;
+    };
+    uint32_t n = 0;
+    if (lp) {
+      Ev* h = L.heap;
+      for (uint32_t i = 0; i < np; ++i) heap_push(h, n, L.ev(i));
+      while (n) {
+        const uint32_t i = heap_pop(h, n).id;
+        uint32_t next;
+        uint64_t t = L.t[i], zl = L.zl[i], ct = L.ct[i];
+        const bool done = hop(L.cur[i], L.dst[i], L.len[i], t, zl, ct, next);
+        L.t[i] = t; L.zl[i] = zl; L.ct[i] = ct; L.cur[i] = next;
+        if (!done) heap_push(h, n, L.ev(i));
+      }
+    } else {
+      Ev* h = heap + b;
+      for (uint64_t i = b; i < e; ++i) { uint32_t k = bucket_ids[i]; heap_push(h, n, mkev(S, S.t[k], k)); }
+      while (n) {
+        const uint32_t k = heap_pop(h, n).id;
+        uint32_t next;
+        uint64_t t = S.t[k], zl = S.zl[k], ct = S.ct[k];
+        const bool done = hop(S.cur[k], dst[k], len[k], t, zl, ct, next);
+        S.t[k] = t; S.zl[k] = zl; S.ct[k] = ct; S.cur[k] = next;
+        if (!done) heap_push(h, n, mkev(S, t, k));
+      }
+    }
+  }
+  __syncthreads();
+  if (lp) lpk_store(L, np, S);
+  if (lp) lctr_flush(D, lcb, Lq, tile_at);
+  for (uint32_t i = 0; i < Lq; ++i) qimg_copy(D, (uint64_t)tile_at(i) * 6 + port, qlds + i * qb, false);
 }
 
 // bucket keys: 0 = injection (src tile), 1 = X chain, 2 = Y chain, 3 = SELF (dst tile); ~0 = not in stage
@@ -313,6 +560,7 @@ struct gg_noc_state {
   uint32_t *cur = nullptr, *keys = nullptr, *ids = nullptr;
   Ev* heap = nullptr;
   uint32_t* counts = nullptr; uint32_t* cursor = nullptr; uint64_t* off = nullptr; uint32_t nb_cap = 0;
+  bool staged = true;   // LDS-staged stage kernels where the queues fit (GG_NOC_STAGED=0: HBM-resident, A/B)
 };
 
 gg_status gg_noc_alloc(gg_ctx* ctx)
@@ -333,6 +581,10 @@ gg_status gg_noc_alloc(gg_ctx* ctx)
   P.net_model = c.net_model;
   P.f = c.frequency_ghz;
   if (P.max_size > 32767) return gg_fail(GG_ERR_UNSUPPORTED, "max_list_size too large");
+  S->staged = !(getenv("GG_NOC_STAGED") && atoi(getenv("GG_NOC_STAGED")) == 0);
+  GG_HIP(hipFuncSetAttribute((const void*)k_port_staged<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
+  GG_HIP(hipFuncSetAttribute((const void*)k_port_staged<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
+  GG_HIP(hipFuncSetAttribute((const void*)k_chain_staged, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
   GG_HIP(hipMalloc((void**)&S->ctr, sizeof(uint64_t) * c.num_tiles * GG_NUM_NET_COUNTERS));
   // one history tree per mesh output port (5) + the injection port, per tile; the
   // stand-alone gg_queue_delay_batch queue lives at index tiles*6
@@ -444,7 +696,20 @@ gg_status gg_noc_hbh(gg_ctx* ctx, const uint32_t* src, const uint32_t* dst, cons
     hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, S->counts, nb, S->off, S->cursor);
     hipLaunchKernelGGL(k_bucket, dim3(blocks), dim3(256), 0, s, S->keys, cap, n_dev, S->off, S->cursor, S->ids);
     const uint32_t tb = (nb + 63) / 64;
-    if (stage == 0)
+    const size_t qb = qimg_bytes(P.max_size);
+    const size_t port_lds = kPortTiles * qb, chain_lds = (stage == 1 ? P.w : P.h) * qb;
+    const bool staged = S->staged && ((stage == 0 || stage == 3) ? port_lds : chain_lds) <= kStageLdsMax;
+    if (staged && (stage == 0 || stage == 3)) {
+      const uint32_t pb = (P.tiles + kPortTiles - 1) / kPortTiles;
+      // the whole LDS budget: the packet count of a workgroup is known on the device only
+      if (stage == 0)
+        hipLaunchKernelGGL(k_port_staged<false>, dim3(pb), dim3(64), kStageLdsMax, s, D, dst, len, S->off, S->ids, S->heap, PS);
+      else
+        hipLaunchKernelGGL(k_port_staged<true>, dim3(pb), dim3(64), kStageLdsMax, s, D, dst, len, S->off, S->ids, S->heap, PS);
+    } else if (staged) {
+      hipLaunchKernelGGL(k_chain_staged, dim3(nb), dim3(64), kStageLdsMax, s, D, stage - 1, dst, len, S->off, S->ids,
+                         S->heap, PS);
+    } else if (stage == 0)
       hipLaunchKernelGGL(k_inject, dim3(tb), dim3(64), 0, s, D, src, dst, len, S->off, S->ids, S->heap, PS);
     else if (stage == 3)
       hipLaunchKernelGGL(k_self, dim3(tb), dim3(64), 0, s, D, dst, len, S->off, S->ids, S->heap, PS);
