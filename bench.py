@@ -86,6 +86,8 @@ def parse():
                    help="coherent-mode (Mode C) section: total tiles (0 = skip); configs[2] = 256")
     p.add_argument("--coherent-per-tile", type=int, default=4096, help="coherent-mode accesses per tile")
     p.add_argument("--coherent-shards", type=int, default=0, help="logical shards (0 = 1, or 8 with --gpus > 1)")
+    p.add_argument("--noc-packets", type=int, default=1 << 18, help="NoC section batch size (0 = skip)")
+    p.add_argument("--noc-tiles", type=int, default=1024)
     p.add_argument("--coherent-net", default="hop_counter", choices=["hop_counter", "hop_by_hop", "magic"],
                    help="memory-network model of the coherent section (hop_by_hop needs one logical shard)")
     p.add_argument("--coherent", action="store_true",
@@ -199,6 +201,59 @@ def fft_section(args, dev):
         res["cpu_baseline"] = {"value": len(a) / cdt, "unit": "accesses/s", "cores": 1, "kind": "port",
                                "sample": "the whole FFT trace, oracle/gg_coherent.inc -O3, 1 thread, %.2f s" % cdt}
     be.close()
+    return res
+
+
+def noc_section(args, dev):
+    """NetworkModel::routePacket batches (gg_noc_route_batch): uniform-random
+    (src, dst) packets at configs[3]'s 1024-tile mesh, data-length messages
+    (shmem EX_REP, 584 bits), injection times sorted, under emesh_hop_counter
+    and emesh_hop_by_hop with history-tree router contention.  One batch per
+    model, routed from fresh router queues, HIP-event timed, bit-exact
+    against the C oracle (arrival, zero-load, contention and the per-tile
+    counters), whose 1-thread run is the CPU baseline."""
+    import torch
+    from graphite_amd import config as C
+    from graphite_amd import backend as B
+    from oracle import pyoracle as po
+    T = args.noc_tiles
+    d = lambda x: torch.from_numpy(x.view(np.int64 if x.dtype == np.uint64 else np.int32)).to(dev)
+    res = {"workload": "uniform-random packets of %d bits on the %d-tile mesh (configs[3]), one batch per model, "
+                       "injection times ~50 ps apart" % (C.shmem_modeled_bits(T, True), T),
+           "bytes_per_packet": 44}
+    # the closed-form model is one thread per packet: a large batch; the hop-by-hop walk is serial per chain
+    for name, model, n in (("hop_counter", C.NET_EMESH_HOP_COUNTER, 64 * args.noc_packets),
+                           ("hop_by_hop", C.NET_EMESH_HOP_BY_HOP, args.noc_packets)):
+        rng = np.random.default_rng(7)
+        src = rng.integers(0, T, n).astype(np.uint32)
+        dst = rng.integers(0, T, n).astype(np.uint32)
+        bits = np.full(n, C.shmem_modeled_bits(T, True), np.uint32)
+        t = np.sort(rng.integers(0, 50 * n, n)).astype(np.uint64)
+        be = B.Backend(C.default_config(T, net_model=model))
+        ins = [d(src), d(dst), d(bits), d(t)]
+        outs = [torch.zeros(n, dtype=torch.int64, device=dev) for _ in range(3)]
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        be.noc_route_batch(*ins, *outs)
+        e1.record()
+        torch.cuda.synchronize()
+        dt = e0.elapsed_time(e1) / 1e3
+        r = {"packets": n, "value": n / dt, "unit": "packets/s", "seconds": dt, "GB_s": 44 * n / dt / 1e9}
+        if not args.no_verify:
+            on = po.OracleNoc(C.default_config(T, net_model=model))
+            c0 = time.perf_counter()
+            ref = on.route(src, dst, bits, t)
+            cdt = time.perf_counter() - c0
+            r["bit_exact_checked"] = bool(all(np.array_equal(o.cpu().numpy().view(np.uint64), x)
+                                              for o, x in zip(outs, ref)) and
+                                          np.array_equal(be.noc_counters(), on.counters()))
+            if not r["bit_exact_checked"]:
+                print("bench.py: NOC %s BIT-EXACT CHECK FAILED" % name, file=sys.stderr)
+            r["cpu_baseline"] = {"value": n / cdt, "unit": "packets/s", "cores": 1, "kind": "port",
+                                 "sample": "the whole batch, oracle/gg_oracle.c -O3, 1 thread, %.2f s" % cdt}
+        res[name] = r
+        be.close()
     return res
 
 
@@ -353,6 +408,8 @@ def main():
             out["coherent"] = coh
     if args.fft_m and world == 1:
         out["fft"] = fft_section(args, dev)
+    if args.noc_packets and world == 1:
+        out["noc"] = noc_section(args, dev)
     if rank == 0:
         print(json.dumps(out))
     if world > 1:
