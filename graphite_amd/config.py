@@ -13,6 +13,14 @@ POLICY_ROUND_ROBIN = 1
 NET_MAGIC = 0
 NET_EMESH_HOP_COUNTER = 1
 NET_EMESH_HOP_BY_HOP = 2
+# queue model types (QueueModel::create, queue_model.cc:19-39) and queue_model/basic moving averages
+QM_HISTORY_TREE = 0
+QM_HISTORY_LIST = 1
+QM_BASIC = 2
+MAVG_ARITHMETIC_MEAN = 0
+MAVG_MEDIAN = 1
+MAVG_NONE = 2
+MAVG_GEOMETRIC_MEAN = 3
 
 L1D = 0
 L2 = 1
@@ -96,7 +104,10 @@ class GGConfig(ctypes.Structure):
         ("num_shards", ctypes.c_uint32),
         ("shard_begin", ctypes.c_uint32),
         ("shard_end", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32 * 4),
+        ("queue_model_type", ctypes.c_uint32),
+        ("dram_queue_model_type", ctypes.c_uint32),
+        ("basic_moving_avg", ctypes.c_uint32),
+        ("history_list_no_interleaving", ctypes.c_uint32),
     ]
 
 

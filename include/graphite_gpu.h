@@ -121,6 +121,14 @@ enum {
   GG_NUM_NET_COUNTERS
 };
 
+/* Queue model types (the type strings of QueueModel::create) and the
+ * moving averages of queue_model/basic (MovingAverage::createAvgType,
+ * common/misc/moving_average.h).  history_list uses max_list_size and
+ * analytical_enabled below (queue_model/history_list, same defaults).    */
+enum { GG_QM_HISTORY_TREE = 0, GG_QM_HISTORY_LIST = 1, GG_QM_BASIC = 2 };
+enum { GG_MAVG_ARITHMETIC_MEAN = 0, GG_MAVG_MEDIAN = 1, GG_MAVG_NONE = 2 /* moving_avg_enabled = false */,
+       GG_MAVG_GEOMETRIC_MEAN = 3 /* not supported: GG_ERR_UNSUPPORTED */ };
+
 typedef struct gg_config {
   uint32_t num_tiles;          /* application tiles (general/total_cores)          */
   uint32_t line_size;          /* bytes, l1_dcache/T1/cache_line_size (64)          */
@@ -157,7 +165,12 @@ typedef struct gg_config {
   uint32_t num_shards;         /* logical shards (canonical schedule); 0 = 1 */
   uint32_t shard_begin;        /* shards owned by this context: [shard_begin, shard_end) */
   uint32_t shard_end;          /* 0 = all                                            */
-  uint32_t reserved[4];
+  /* ---- queue models (QueueModel::create, shared_models/queue_model.cc:19-39) ---- */
+  uint32_t queue_model_type;   /* network/emesh_hop_by_hop/queue_model/type: GG_QM_* (0 = history_tree) */
+  uint32_t dram_queue_model_type; /* dram/queue_model/type: GG_QM_*                 */
+  uint32_t basic_moving_avg;   /* queue_model/basic: moving_avg_window_size in bits 0..15
+                                  (0 = 64) | GG_MAVG_* << 16 (0 = arithmetic_mean)  */
+  uint32_t history_list_no_interleaving; /* queue_model/history_list/interleaving_enabled = false */
 } gg_config;
 
 /* Fill cfg with the reference defaults of carbon_sim.cfg for num_tiles tiles. */

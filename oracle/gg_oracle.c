@@ -650,6 +650,18 @@ struct oracle_htree {
   mg1 m;
   uint64_t analytical_requests;
   uint64_t util_cycles, last_req, total_req;      /* queue_model.cc:41-55 */
+  /* QueueModel::create (queue_model.cc:19-39) picks the model by type */
+  uint32_t type;                                  /* GG_QM_* */
+  /* history_list (queue_model_history_list.cc): the free-interval std::list
+   * as an array in list order, room for max_list_size + 1 entries (the list
+   * overgrows by one before its front is dropped, :128-131) */
+  uint64_t (*lst)[2]; uint32_t lsize; int interleaving;
+  /* basic (queue_model_basic.cc) with MovingAverage<UInt64> (moving_average.h) */
+  uint64_t queue_time;
+  int avg;                                        /* GG_MAVG_* */
+  uint32_t win_max, front, back;                  /* ModuloNum(window + 1) */
+  uint64_t* win;
+  double mean;
 };
 
 static int ht_alloc(oracle_htree* h, uint64_t a, uint64_t b)    /* allocateNode (:146-157) */
@@ -675,14 +687,151 @@ oracle_htree* oracle_htree_create(uint64_t min_proc, int max_list_size, int anal
   return h;
 }
 
-void oracle_htree_destroy(oracle_htree* h) { if (h) { free(h->t.n); free(h->free_list); free(h); } }
+/* QueueModelHistoryList(min_processing_time) (queue_model_history_list.cc:9-28) */
+static oracle_htree* qm_list_create(uint64_t min_proc, int max_list_size, int analytical, int interleaving)
+{
+  oracle_htree* h = (oracle_htree*)calloc(1, sizeof(*h));
+  h->type = GG_QM_HISTORY_LIST;
+  h->min_proc = min_proc; h->max_size = max_list_size; h->analytical = analytical;
+  h->interleaving = interleaving;
+  h->lst = (uint64_t(*)[2])calloc((size_t)max_list_size + 2, sizeof(*h->lst));
+  h->lst[0][0] = 0; h->lst[0][1] = UINT64_MAX;    /* push_back(make_pair(0, UINT64_MAX)) (:26) */
+  h->lsize = 1;
+  return h;
+}
+
+/* QueueModelBasic (queue_model_basic.cc:7-28): moving_avg_window_size / _type */
+static oracle_htree* qm_basic_create(uint32_t window, int avg)
+{
+  oracle_htree* h = (oracle_htree*)calloc(1, sizeof(*h));
+  h->type = GG_QM_BASIC;
+  h->avg = avg;
+  h->win_max = window;
+  h->win = (uint64_t*)calloc((size_t)window + 1, sizeof(uint64_t));   /* _num_list.resize(max + 1) */
+  return h;
+}
+
+oracle_htree* oracle_qmodel_create(uint32_t type, uint32_t aux, uint64_t min_proc, int max_list_size, int analytical)
+{
+  if (type == GG_QM_HISTORY_LIST) return qm_list_create(min_proc, max_list_size, analytical, aux == 0);
+  if (type == GG_QM_BASIC) {
+    const uint32_t w = (aux & 0xFFFFu) ? (aux & 0xFFFFu) : 64u;
+    return qm_basic_create(w, (int)(aux >> 16));
+  }
+  return oracle_htree_create(min_proc, max_list_size, analytical);
+}
+
+void oracle_htree_destroy(oracle_htree* h) { if (h) { free(h->t.n); free(h->free_list); free(h->lst); free(h->win); free(h); } }
 uint64_t oracle_htree_analytical_requests(const oracle_htree* h) { return h->analytical_requests; }
 uint32_t oracle_htree_size(const oracle_htree* h) { return h->t.size; }
 
-/* computeQueueDelay (queue_model_history_tree.cc:44-126) */
+/* ---- history list: std::list operations on the array (index = iterator) ---- */
+static void lst_erase(oracle_htree* h, uint32_t i)
+{
+  memmove(&h->lst[i], &h->lst[i + 1], sizeof(*h->lst) * (h->lsize - i - 1));
+  h->lsize--;
+}
+static void lst_insert(oracle_htree* h, uint32_t i, uint64_t a, uint64_t b)   /* insert before i */
+{
+  memmove(&h->lst[i + 1], &h->lst[i], sizeof(*h->lst) * (h->lsize - i));
+  h->lst[i][0] = a; h->lst[i][1] = b;
+  h->lsize++;
+}
+
+/* computeUsingHistoryList (queue_model_history_list.cc:68-134) */
+static uint64_t list_delay(oracle_htree* h, uint64_t t, uint64_t p)
+{
+  uint64_t qd = 0;
+  const uint64_t mp = h->min_proc;
+  for (uint32_t it = 0; it < h->lsize; ++it) {
+    const uint64_t a = h->lst[it][0], b = h->lst[it][1];
+    if (t >= a && (t + p) <= b) {                 /* fits: no additional delay */
+      lst_erase(h, it);
+      if ((t - a) >= mp) lst_insert(h, it++, a, t);
+      if ((b - (t + p)) >= mp) lst_insert(h, it++, t + p, b);
+      break;
+    } else if (t < a && (a + p) <= b) {           /* starts at the interval */
+      qd += a - t;
+      lst_erase(h, it);
+      if ((b - (a + p)) >= mp) lst_insert(h, it, a + p, b);
+      break;
+    } else if (h->interleaving) {
+      if (t >= a && t < b) {
+        lst_erase(h, it);
+        if ((t - a) >= mp) lst_insert(h, it++, a, t);
+        it--;                                     /* the loop's ++ lands after the erased interval */
+        t = b;
+        p -= (b - t);                             /* the reference subtracts after moving pkt_time: 0 */
+      } else if (t < a) {
+        lst_erase(h, it);
+        it--;
+        qd += a - t;
+        t = b;
+        p -= (b - a);
+      }
+    }
+  }
+  if (h->lsize > (uint32_t)h->max_size) lst_erase(h, 0);
+  return qd;
+}
+
+/* MovingAverage<UInt64>::compute (moving_average.h): arithmetic mean / median */
+static uint64_t mavg(oracle_htree* h, uint64_t x)
+{
+  const uint32_t M = h->win_max + 1;
+  const uint32_t cws = (h->back >= h->front) ? h->back - h->front : h->back + M - h->front;
+  uint64_t r;
+  if (h->avg == GG_MAVG_MEDIAN) {
+    h->win[h->back] = x;                          /* addToWindow */
+    h->back = (h->back + 1) % M;
+    if (h->back == h->front) h->front = (h->front + 1) % M;
+    const uint32_t c2 = (h->back >= h->front) ? h->back - h->front : h->back + M - h->front;
+    r = h->win[(h->front + (c2 / 2) % M) % M];
+  } else {                                        /* MovingArithmeticMean */
+    if (cws == h->win_max) {
+      const uint64_t old = h->win[h->front];
+      h->mean += (((double)x / cws) - ((double)old / cws));
+    } else {
+      h->mean = (h->mean * cws + x) / (cws + 1);
+    }
+    h->win[h->back] = x;
+    h->back = (h->back + 1) % M;
+    if (h->back == h->front) h->front = (h->front + 1) % M;
+    r = (uint64_t)h->mean;
+  }
+  return r;
+}
+
+/* QueueModelBasic::computeQueueDelay (queue_model_basic.cc:34-61) */
+static uint64_t basic_delay(oracle_htree* h, uint64_t t, uint64_t p)
+{
+  const uint64_t ref = (h->avg == GG_MAVG_NONE) ? t : mavg(h, t);
+  const uint64_t qd = (h->queue_time > ref) ? (h->queue_time - ref) : 0;
+  h->queue_time = ((h->queue_time > ref) ? h->queue_time : ref) + p;
+  h->util_cycles += p;
+  if (ref + qd + p > h->last_req) h->last_req = ref + qd + p;
+  h->total_req++;
+  return qd;
+}
+
+/* computeQueueDelay (queue_model_history_tree.cc:44-126; history_list: queue_model_history_list.cc:40-66) */
 uint64_t oracle_htree_delay(oracle_htree* h, uint64_t t, uint64_t p)
 {
   uint64_t qd = UINT64_MAX;
+  if (h->type == GG_QM_BASIC) return basic_delay(h, t, p);
+  if (h->type == GG_QM_HISTORY_LIST) {
+    if (h->analytical && ((t + p) < h->lst[0][0])) {
+      h->analytical_requests++;
+      qd = mg1_delay(&h->m);
+    } else {
+      qd = list_delay(h, t, p);
+    }
+    mg1_update(&h->m, t, p, qd);
+    h->util_cycles += p;
+    if (t + qd + p > h->last_req) h->last_req = t + qd + p;
+    h->total_req++;
+    return qd;
+  }
   itree* T = &h->t;
   int min_node = it_search(T, 0, 1, T->root);
   if (T->size >= (uint32_t)h->max_size) ht_release(h, it_remove(T, min_node));
@@ -725,6 +874,13 @@ uint64_t oracle_htree_delay(oracle_htree* h, uint64_t t, uint64_t p)
 /* ======================================================================== */
 enum { P_SELF = 0, P_LEFT, P_RIGHT, P_DOWN, P_UP, NPORTS };   /* network_model_emesh_hop_by_hop.h:41-48 */
 
+/* the model-specific parameter of oracle_qmodel_create for the router queues */
+static uint32_t qm_aux_of(const gg_config* c, uint32_t type)
+{
+  return type == GG_QM_BASIC ? c->basic_moving_avg : c->history_list_no_interleaving;
+}
+static uint32_t qm_aux(const gg_config* c) { return qm_aux_of(c, c->queue_model_type); }
+
 struct oracle_noc {
   gg_config cfg;
   uint32_t n, w, h, id_bits;
@@ -746,9 +902,10 @@ oracle_noc* oracle_noc_create(const gg_config* cfg)
     on->inj = (oracle_htree**)calloc(on->n, sizeof(void*));
     on->q = (oracle_htree**)calloc((size_t)on->n * NPORTS, sizeof(void*));
     for (uint32_t i = 0; i < on->n; ++i) {
-      on->inj[i] = oracle_htree_create(1, (int)cfg->max_list_size, (int)cfg->analytical_enabled);
+      on->inj[i] = oracle_qmodel_create(cfg->queue_model_type, qm_aux(cfg), 1, (int)cfg->max_list_size, (int)cfg->analytical_enabled);
       for (int p = 0; p < NPORTS; ++p)       /* QueueModel::create(type, 1) (router_model.cc:23-27) */
-        on->q[(size_t)i * NPORTS + p] = oracle_htree_create(1, (int)cfg->max_list_size, (int)cfg->analytical_enabled);
+        on->q[(size_t)i * NPORTS + p] = oracle_qmodel_create(cfg->queue_model_type, qm_aux(cfg), 1, (int)cfg->max_list_size,
+                                                           (int)cfg->analytical_enabled);
     }
   }
   return on;

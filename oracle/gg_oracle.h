@@ -59,6 +59,10 @@ int  oracle_cache_insert_line(oracle_cache* oc, uint32_t tile, int level, uint64
 /* ---------------- queue models ------------------------------------------- */
 typedef struct oracle_htree oracle_htree;
 oracle_htree* oracle_htree_create(uint64_t min_processing_time, int max_list_size, int analytical_enabled);
+/* any QueueModel::create type (GG_QM_*); aux = history_list_no_interleaving
+ * for history_list, basic_moving_avg for basic (gg_config fields)          */
+oracle_htree* oracle_qmodel_create(uint32_t type, uint32_t aux, uint64_t min_processing_time,
+                                   int max_list_size, int analytical_enabled);
 void          oracle_htree_destroy(oracle_htree* h);
 uint64_t      oracle_htree_delay(oracle_htree* h, uint64_t pkt_time, uint64_t processing_time);
 uint64_t      oracle_htree_analytical_requests(const oracle_htree* h);

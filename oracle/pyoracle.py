@@ -55,6 +55,8 @@ def lib():
         L.oracle_htree_create.restype = vp
         L.oracle_htree_create.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
         L.oracle_htree_destroy.argtypes = [vp]
+        L.oracle_qmodel_create.restype = vp
+        L.oracle_qmodel_create.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
         L.oracle_htree_delay.restype = ctypes.c_uint64
         L.oracle_htree_delay.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64]
         L.oracle_htree_analytical_requests.restype = ctypes.c_uint64
@@ -256,6 +258,14 @@ class OracleHistoryTree:
     @property
     def analytical_requests(self):
         return lib().oracle_htree_analytical_requests(self.h)
+
+
+class OracleQueueModel(OracleHistoryTree):
+    """Any QueueModel::create type (queue_model.cc:19-39): qtype = QM_*; aux =
+    history_list_no_interleaving (history_list) or basic_moving_avg (basic)."""
+
+    def __init__(self, qtype, aux=0, min_proc=1, max_list_size=100, analytical=True):
+        self.h = lib().oracle_qmodel_create(qtype, aux, min_proc, max_list_size, int(analytical))
 
 
 class OracleNoc:

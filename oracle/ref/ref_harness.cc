@@ -279,6 +279,47 @@ static void gen_htree(const char* name, uint64_t seed, int n, UInt64 span, UInt6
   manifest(m);
 }
 
+// The same arrival process through the other two queue models of
+// QueueModel::create (queue_model.cc:19-39).  kind "qlist": history_list
+// (aux = no-interleaving flag), "qbasic": basic (aux = GG basic_moving_avg).
+static void gen_qlist(const char* name, uint64_t seed, int n, UInt64 span, UInt64 maxp, int max_size, bool an, bool il) {
+  RefHistoryList h(1, (UInt32)max_size, an, il);
+  vector<UInt64> rows;
+  UInt64 base = 0;
+  for (int i = 0; i < n; ++i) {
+    uint64_t z = sm_at(seed, (uint64_t)i);
+    base += (z & 7);
+    UInt64 t = ((z >> 8) % 4 == 0 && base > span) ? base - ((z >> 16) % span) : base;
+    UInt64 p = 1 + ((z >> 32) % maxp);
+    rows.push_back(t); rows.push_back(p); rows.push_back(h.delay(t, p));
+  }
+  char file[256]; snprintf(file, sizeof file, "%s.u64", name);
+  write_bin(file, rows.data(), rows.size() * 8);
+  char m[512];
+  snprintf(m, sizeof m, "\"%s\": {\"file\": \"%s\", \"kind\": \"qlist\", \"rows\": %d, \"cols\": [\"pkt_time\", \"proc_time\", \"delay\"], "
+           "\"max_list_size\": %d, \"analytical\": %s, \"aux\": %d, \"analytical_requests\": %llu}",
+           name, file, n, max_size, an ? "true" : "false", il ? 0 : 1, (unsigned long long)h.analytical_requests);
+  manifest(m);
+}
+static void gen_qbasic(const char* name, uint64_t seed, int n, UInt64 span, UInt64 maxp, const char* avg, int gg_avg, UInt32 window) {
+  RefBasic h(avg, window);
+  vector<UInt64> rows;
+  UInt64 base = 0;
+  for (int i = 0; i < n; ++i) {
+    uint64_t z = sm_at(seed, (uint64_t)i);
+    base += (z & 7);
+    UInt64 t = ((z >> 8) % 4 == 0 && base > span) ? base - ((z >> 16) % span) : base;
+    UInt64 p = 1 + ((z >> 32) % maxp);
+    rows.push_back(t); rows.push_back(p); rows.push_back(h.delay(t, p));
+  }
+  char file[256]; snprintf(file, sizeof file, "%s.u64", name);
+  write_bin(file, rows.data(), rows.size() * 8);
+  char m[512];
+  snprintf(m, sizeof m, "\"%s\": {\"file\": \"%s\", \"kind\": \"qbasic\", \"rows\": %d, \"cols\": [\"pkt_time\", \"proc_time\", \"delay\"], "
+           "\"aux\": %u}", name, file, n, (unsigned)(window | ((UInt32)gg_avg << 16)));
+  manifest(m);
+}
+
 // Random quartet-op sequences on one RefCache.  op codes: 0 get, 1 set, 2 access(load), 3 access(store), 4 insert
 // Info is PrL1CacheLineInfo for L1 and PrL2CacheLineInfo for L2 (their assign() must see matching types).
 template <class Info>
@@ -408,6 +449,16 @@ int main(int argc, char** argv) {
   gen_htree("htree_rand_b", 2, 4000, 300, 3, 100, true);
   gen_htree("htree_rand_c", 3, 3000, 40, 12, 16, true);
   gen_htree("htree_rand_noan", 4, 3000, 64, 9, 100, false);
+  // 2b. history_list and basic queue models on the same arrival process
+  gen_qlist("qlist_rand_a", 1, 4000, 64, 9, 100, true, true);
+  gen_qlist("qlist_rand_b", 2, 4000, 300, 3, 100, true, true);
+  gen_qlist("qlist_rand_c", 3, 3000, 40, 12, 16, true, true);
+  gen_qlist("qlist_noil", 5, 3000, 64, 9, 100, true, false);
+  gen_qlist("qlist_noan", 4, 3000, 64, 9, 24, false, true);
+  gen_qbasic("qbasic_mean", 6, 3000, 64, 9, "arithmetic_mean", 0, 64);
+  gen_qbasic("qbasic_mean7", 7, 3000, 300, 12, "arithmetic_mean", 0, 7);
+  gen_qbasic("qbasic_median", 8, 3000, 64, 9, "median", 1, 16);
+  gen_qbasic("qbasic_none", 9, 3000, 64, 9, "", 2, 64);
   // 3. Cache quartet sequences, L1 (write-through) and L2 (write-back), LRU and round robin
   gen_quartet("quartet_l1_lru", 11, 3000, 2, 4, "lru", 0);
   gen_quartet("quartet_l2_lru", 12, 3000, 4, 8, "lru", 1);

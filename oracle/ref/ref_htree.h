@@ -69,3 +69,86 @@ struct RefHistoryTree {
   }
 };
 
+
+// --------------------------------------------------------------------------
+// QueueModelHistoryList::computeQueueDelay (queue_model_history_list.cc:40-134)
+// on std::list — the container the reference uses, with its iterator
+// semantics (erase returns the next node, insert goes before it, -- on
+// begin() wraps to the sentinel) — and the reference QueueModelMG1.  The
+// reference file reads its parameters through Sim()->getCfg() (Boost), so
+// the glue is restated here.
+// --------------------------------------------------------------------------
+#include <list>
+struct RefHistoryList {
+  typedef std::list<std::pair<UInt64, UInt64> > L;
+  UInt64 min_proc; UInt32 max_size; bool analytical, interleaving;
+  L fl; QueueModelMG1 mg1; UInt64 analytical_requests;
+
+  RefHistoryList(UInt64 mp, UInt32 ms, bool an, bool il)
+      : min_proc(mp), max_size(ms), analytical(an), interleaving(il), analytical_requests(0) {
+    fl.push_back(std::make_pair((UInt64)0, (UInt64)UINT64_MAX));
+  }
+  UInt64 scan(UInt64 t, UInt64 p) {
+    CHECK(fl.size() <= max_size);
+    UInt64 qd = 0;
+    for (L::iterator it = fl.begin(); it != fl.end(); ++it) {
+      const UInt64 a = it->first, b = it->second;
+      if (t >= a && t + p <= b) {
+        it = fl.erase(it);
+        if (t - a >= min_proc) fl.insert(it, std::make_pair(a, t));
+        if (b - (t + p) >= min_proc) fl.insert(it, std::make_pair(t + p, b));
+        break;
+      }
+      if (t < a && a + p <= b) {
+        qd += a - t;
+        it = fl.erase(it);
+        if (b - (a + p) >= min_proc) fl.insert(it, std::make_pair(a + p, b));
+        break;
+      }
+      if (!interleaving) continue;
+      if (t >= a && t < b) {
+        it = fl.erase(it);
+        if (t - a >= min_proc) fl.insert(it, std::make_pair(a, t));
+        --it;
+        t = b;
+        p -= (b - t);          // as the reference: after t moved, this subtracts 0
+      } else if (t < a) {
+        it = fl.erase(it);
+        --it;
+        qd += a - t;
+        t = b;
+        p -= (b - a);
+      }
+    }
+    if (fl.size() > max_size) fl.erase(fl.begin());
+    return qd;
+  }
+  UInt64 delay(UInt64 t, UInt64 p) {
+    CHECK(fl.size() >= 1);
+    UInt64 qd;
+    if (analytical && (t + p) < fl.front().first) { analytical_requests++; qd = mg1.computeQueueDelay(t, p); }
+    else qd = scan(t, p);
+    mg1.updateQueue(t, p, qd);
+    return qd;
+  }
+};
+
+// --------------------------------------------------------------------------
+// QueueModelBasic::computeQueueDelay (queue_model_basic.cc:34-61) on the
+// reference's own MovingAverage<UInt64> (common/misc/moving_average.h +
+// modulo_num.cc); avg = "arithmetic_mean" / "median" / "" (disabled).
+// --------------------------------------------------------------------------
+#include "moving_average.h"
+struct RefBasic {
+  UInt64 queue_time; MovingAverage<UInt64>* ma;
+  RefBasic(const char* avg, UInt32 window) : queue_time(0), ma(NULL) {
+    if (avg[0]) { ma = MovingAverage<UInt64>::createAvgType(avg, window); CHECK(ma); }
+  }
+  ~RefBasic() { delete ma; }
+  UInt64 delay(UInt64 t, UInt64 p) {
+    const UInt64 ref = ma ? ma->compute(t) : t;
+    const UInt64 qd = queue_time > ref ? queue_time - ref : 0;
+    queue_time = std::max(queue_time, ref) + p;
+    return qd;
+  }
+};

@@ -31,6 +31,22 @@ def test_history_tree_reference_sequences(name):
     assert h.analytical_requests == e["analytical_requests"]
 
 
+@pytest.mark.parametrize("name", [k for k, v in M.items() if v["kind"] in ("qlist", "qbasic")])
+def test_other_queue_models_reference_sequences(name):
+    """history_list (std::list restatement + reference QueueModelMG1) and basic
+    (reference MovingAverage) fixtures from oracle/ref/ref_harness.cc."""
+    e = M[name]
+    rows = load(e["file"], np.uint64).reshape(-1, 3)
+    if e["kind"] == "qlist":
+        h = po.OracleQueueModel(C.QM_HISTORY_LIST, e["aux"], 1, e["max_list_size"], e["analytical"])
+    else:
+        h = po.OracleQueueModel(C.QM_BASIC, e["aux"])
+    got = np.array([h.delay(int(t), int(p)) for t, p, _ in rows], np.uint64)
+    np.testing.assert_array_equal(got, rows[:, 2])
+    if e["kind"] == "qlist":
+        assert h.analytical_requests == e["analytical_requests"]
+
+
 @pytest.mark.parametrize("name", [k for k, v in M.items() if v["kind"] == "quartet"])
 def test_cache_quartet_reference_sequences(name):
     e = M[name]
