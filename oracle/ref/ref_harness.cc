@@ -455,6 +455,7 @@ int main(int argc, char** argv) {
   gen_qlist("qlist_rand_c", 3, 3000, 40, 12, 16, true, true);
   gen_qlist("qlist_noil", 5, 3000, 64, 9, 100, true, false);
   gen_qlist("qlist_noan", 4, 3000, 64, 9, 24, false, true);
+  gen_qlist("qlist_small", 10, 3000, 300, 2, 3, true, true);
   gen_qbasic("qbasic_mean", 6, 3000, 64, 9, "arithmetic_mean", 0, 64);
   gen_qbasic("qbasic_mean7", 7, 3000, 300, 12, "arithmetic_mean", 0, 7);
   gen_qbasic("qbasic_median", 8, 3000, 64, 9, "median", 1, 16);
