@@ -60,6 +60,7 @@ struct CP {
   uint32_t s1, a1, s2, a2, log_line, pol1, pol2;
   uint32_t E, dassoc, log_dsets, log_slices, W, R, QC, IC;
   uint32_t bits_req, bits_data, max_list, analytical, dram_qm;
+  uint32_t dram_qtype, dram_qaux;          // dram/queue_model/type (GG_QM_*) and its hq_aux parameter
   uint64_t lat_l1d, lat_l1t, lat_l2d, lat_l2t, lat_dir, gap_ps, dram_proc, dram_cost;
   uint64_t msg_cap;
   uint32_t tiles_per_block;              // 64: a lane per tile; 1: a wave per tile (lane 0)
@@ -1068,18 +1069,9 @@ __global__ void k_c_reset(CP P, CS S, const uint64_t* offs)
   S.clk[lt] = 0; S.pend_start[lt] = 0; S.out_addr[lt] = INV_ADDR; S.out_time[lt] = 0;
   S.blocked[lt] = 0; S.seq[lt] = 0;
   S.head0[lt] = -1; S.head1[lt] = -1;
-  if (P.dram_qm) {                                   // QueueModelHistoryTree(min_processing_time)
-    HQueue Q{};
-    Q.max_size = P.max_list;
-    int16_t* f = S.dfl + (size_t)lt * P.max_list;
-    for (uint32_t j = 0; j < P.max_list; ++j) f[j] = (int16_t)j;
-    Q.free_tail = (int32_t)P.max_list - 1;
-    HNode* N = S.dnd + (size_t)lt * P.max_list;
-    const int r = f[Q.free_tail--];
-    N[r].first = 0; N[r].second = ~0ull; N[r].parent = N[r].left = N[r].right = -1; N[r].height = 1;
-    Q.root = r; Q.size = 1;
-    S.dq[lt] = Q;
-  }
+  if (P.dram_qm)                                     // QueueModel::create(dram/queue_model/type, min_processing_time)
+    hq_init(S.dq + lt, S.dnd + (size_t)lt * P.max_list, S.dfl + (size_t)lt * P.max_list, P.max_list, P.dram_qtype,
+            P.dram_qaux);
 }
 
 __global__ void k_c_final_stats(CP P, CS S)
@@ -1198,6 +1190,10 @@ static gg_status coh_alloc(gg_ctx* ctx)
   P.bits_req = 2 * idb + 4 + 48;
   P.bits_data = P.bits_req + 8 * c.line_size;
   P.dram_qm = c.dram_queue_model_enabled;
+  P.dram_qtype = c.dram_queue_model_type;
+  P.dram_qaux = hq_aux(c.dram_queue_model_type, c.basic_moving_avg, c.history_list_no_interleaving);
+  if (P.dram_qm)
+    if (gg_status e = gg_check_queue_model(P.dram_qtype, P.dram_qaux, c.max_list_size ? c.max_list_size : 100)) return e;
   P.max_list = c.max_list_size ? c.max_list_size : 100;
   P.analytical = c.analytical_enabled;
   P.dram_proc = (uint64_t)((float)c.line_size / c.dram_bandwidth) + 1;

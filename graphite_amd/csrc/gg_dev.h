@@ -7,7 +7,14 @@
 namespace gg {
 
 // ---------------------------------------------------------------------------
-// history tree (interval_tree.cc:40-394 + queue_model_history_tree.cc:44-167)
+// Queue models (QueueModel::create, queue_model.cc:19-39).  One storage
+// layout for all three: HQueue + max_size HNode + max_size int16 free list.
+//   history_tree (interval_tree.cc:40-394 + queue_model_history_tree.cc:44-167):
+//     AVL nodes + free list;
+//   history_list (queue_model_history_list.cc:40-134): the free-interval
+//     list as nd[0..size) in list order (first/second);
+//   basic (queue_model_basic.cc:34-61): the MovingAverage window
+//     (moving_average.h, window + 1 slots) as raw u64 words over nd[].
 // ---------------------------------------------------------------------------
 struct HNode { uint64_t first, second; int16_t parent, left, right, height; };
 struct HQueue {
@@ -15,7 +22,54 @@ struct HQueue {
   double sig_sq, sig; uint64_t n, newest;          // QueueModelMG1
   uint64_t analytical;                              // _total_requests_using_analytical_model
   uint64_t util, last_req, total_req;               // QueueModel utilization counters
+  uint32_t type, aux;                               // GG_QM_*; list: no-interleaving flag; basic: basic_moving_avg
+  uint32_t front, back;                             // basic: ModuloNum window ends (modulo window + 1)
+  double mean;                                      // basic: MovingArithmeticMean::_arithmetic_mean
+  uint64_t qtime;                                   // basic: QueueModelBasic::_queue_time
 };
+
+// the model-specific parameter of a queue of type `type` (gg_config fields)
+__host__ __device__ inline uint32_t hq_aux(uint32_t type, uint32_t basic_moving_avg, uint32_t list_no_interleaving)
+{
+  return type == GG_QM_BASIC ? basic_moving_avg : list_no_interleaving;
+}
+__host__ __device__ inline uint32_t hq_window(uint32_t aux) { return (aux & 0xFFFFu) ? (aux & 0xFFFFu) : 64u; }
+
+// host-side validation of a queue model configuration
+inline gg_status gg_check_queue_model(uint32_t type, uint32_t aux, uint32_t max_size)
+{
+  if (type > GG_QM_BASIC) return gg_fail(GG_ERR_INVALID, "unknown queue model type");
+  if (type == GG_QM_BASIC) {
+    if ((aux >> 16) == GG_MAVG_GEOMETRIC_MEAN) return gg_fail(GG_ERR_UNSUPPORTED, "geometric_mean moving average");
+    if ((aux >> 16) > GG_MAVG_GEOMETRIC_MEAN) return gg_fail(GG_ERR_INVALID, "unknown moving average type");
+    if (hq_window(aux) + 1 > 3 * max_size)
+      return gg_fail(GG_ERR_UNSUPPORTED, "moving_avg_window_size + 1 exceeds 3 * max_list_size queue words");
+  }
+  return GG_OK;
+}
+
+// QueueModel{HistoryTree,HistoryList,Basic} constructors on one queue's storage
+__device__ inline void hq_init(HQueue* q, HNode* N, int16_t* f, uint32_t max_size, uint32_t type, uint32_t aux)
+{
+  HQueue Q{};
+  Q.max_size = max_size;
+  Q.type = type;
+  Q.aux = aux;
+  if (type == GG_QM_HISTORY_LIST) {
+    N[0].first = 0; N[0].second = ~0ull;            // push_back(make_pair(0, UINT64_MAX))
+    Q.size = 1;
+  } else if (type == GG_QM_BASIC) {
+    uint64_t* w = reinterpret_cast<uint64_t*>(N);
+    for (uint32_t j = 0; j <= hq_window(aux); ++j) w[j] = 0;   // _num_list.resize(window + 1)
+  } else {
+    for (uint32_t j = 0; j < max_size; ++j) f[j] = (int16_t)j;  // allocateMemory
+    Q.free_tail = (int32_t)max_size - 1;
+    const int r = f[Q.free_tail--];                             // allocateNode(PAIR(0, UINT64_MAX))
+    N[r].first = 0; N[r].second = ~0ull; N[r].parent = N[r].left = N[r].right = -1; N[r].height = 1;
+    Q.root = r; Q.size = 1;
+  }
+  *q = Q;
+}
 
 struct HTree {
   HQueue* q; HNode* nd; int16_t* fl; uint64_t min_proc; bool analytical;
@@ -174,9 +228,101 @@ struct HTree {
     return (uint64_t)ceil(0.5 * service_rate * arrival_rate * ((1 / (service_rate * service_rate)) + variance) /
                           (service_rate - arrival_rate));
   }
+  // ---- history_list: nd[0..size) in list order ----
+  __device__ void l_erase(uint32_t i)
+  {
+    for (uint32_t j = i + 1; j < q->size; ++j) { nd[j - 1].first = nd[j].first; nd[j - 1].second = nd[j].second; }
+    q->size--;
+  }
+  // replace interval i by up to two intervals (in list order).  The list may
+  // overgrow by one only here, and then loses its front (the size check after
+  // the scan, queue_model_history_list.cc:128-131): done in place.
+  __device__ void l_replace(uint32_t i, bool k1, uint64_t a1, uint64_t b1, bool k2, uint64_t a2, uint64_t b2)
+  {
+    if (k1 && !k2) { nd[i].first = a1; nd[i].second = b1; return; }
+    if (!k1 && k2) { nd[i].first = a2; nd[i].second = b2; return; }
+    if (!k1) { l_erase(i); return; }
+    if (q->size < q->max_size) {
+      for (uint32_t j = q->size; j > i + 1; --j) { nd[j].first = nd[j - 1].first; nd[j].second = nd[j - 1].second; }
+      nd[i].first = a1; nd[i].second = b1; nd[i + 1].first = a2; nd[i + 1].second = b2;
+      q->size++;
+    } else if (i == 0) {                        // the first new interval is the front that goes
+      nd[0].first = a2; nd[0].second = b2;
+    } else {                                    // drop the front: [1, i) moves down by one
+      for (uint32_t j = 1; j < i; ++j) { nd[j - 1].first = nd[j].first; nd[j - 1].second = nd[j].second; }
+      nd[i - 1].first = a1; nd[i - 1].second = b1; nd[i].first = a2; nd[i].second = b2;
+    }
+  }
+  __device__ uint64_t list_scan(uint64_t t, uint64_t p)       // computeUsingHistoryList
+  {
+    uint64_t qd = 0;
+    const bool inter = q->aux == 0;
+    uint32_t i = 0;
+    while (i < q->size) {
+      const uint64_t a = nd[i].first, b = nd[i].second;
+      if (t >= a && t + p <= b) {
+        l_replace(i, t - a >= min_proc, a, t, b - (t + p) >= min_proc, t + p, b);
+        return qd;
+      }
+      if (t < a && a + p <= b) {
+        qd += a - t;
+        l_replace(i, false, 0, 0, b - (a + p) >= min_proc, a + p, b);
+        return qd;
+      }
+      if (inter && t >= a && t < b) {           // pkt_time moves to b, processing_time -= 0 (as the reference)
+        if (t - a >= min_proc) { nd[i].second = t; ++i; } else l_erase(i);
+        t = b;
+      } else if (inter && t < a) {
+        l_erase(i);
+        qd += a - t;
+        p -= b - a;
+        t = b;
+      } else {
+        ++i;
+      }
+    }
+    return qd;
+  }
+  // ---- basic: MovingAverage<UInt64>::compute over the window words ----
+  __device__ uint64_t mavg(uint64_t x)
+  {
+    uint64_t* w = reinterpret_cast<uint64_t*>(nd);
+    const uint32_t W = hq_window(q->aux), M = W + 1, avg = q->aux >> 16;
+    const uint32_t cws = q->back >= q->front ? q->back - q->front : q->back + M - q->front;
+    if (avg != GG_MAVG_MEDIAN) {
+      if (cws == W) q->mean += (((double)x / cws) - ((double)w[q->front] / cws));
+      else q->mean = (q->mean * cws + (double)x) / (double)(cws + 1);
+    }
+    w[q->back] = x;                             // addToWindow
+    q->back = (q->back + 1) % M;
+    if (q->back == q->front) q->front = (q->front + 1) % M;
+    if (avg == GG_MAVG_MEDIAN) {
+      const uint32_t c2 = q->back >= q->front ? q->back - q->front : q->back + M - q->front;
+      return w[(q->front + (c2 / 2) % M) % M];
+    }
+    return (uint64_t)q->mean;
+  }
+  __device__ uint64_t basic_delay(uint64_t t, uint64_t p)
+  {
+    const uint64_t ref = ((q->aux >> 16) == GG_MAVG_NONE) ? t : mavg(t);
+    const uint64_t qd = q->qtime > ref ? q->qtime - ref : 0;
+    q->qtime = (q->qtime > ref ? q->qtime : ref) + p;
+    q->util += p;
+    { uint64_t x = ref + qd + p; if (x > q->last_req) q->last_req = x; }
+    q->total_req++;
+    return qd;
+  }
+
   __device__ uint64_t delay(uint64_t t, uint64_t p, uint32_t* err)   // computeQueueDelay
   {
+    if (q->type == GG_QM_BASIC) return basic_delay(t, p);
     uint64_t qd = ~0ull;
+    if (q->type == GG_QM_HISTORY_LIST) {
+      if (analytical && (t + p) < nd[0].first) { q->analytical++; qd = mg1_delay(); }
+      else qd = list_scan(t, p);
+      mg1_update(t, p, qd);
+      return qd;
+    }
     int mn = search(0, 1);
     if (q->size >= q->max_size) release(remove(mn));
     mn = search(0, 1);
@@ -205,6 +351,11 @@ struct HTree {
         else release(remove(node));
       }
     }
+    mg1_update(t, p, qd);
+    return qd;
+  }
+  __device__ void mg1_update(uint64_t t, uint64_t p, uint64_t qd)
+  {
     q->sig_sq += (double)p * (double)p;                          // QueueModelMG1::updateQueue
     q->sig += (double)p;
     q->n++;
@@ -212,7 +363,6 @@ struct HTree {
     q->util += p;                                                // updateQueueUtilizationCounters
     { uint64_t x = t + qd + p; if (x > q->last_req) q->last_req = x; }
     q->total_req++;
-    return qd;
   }
 };
 
@@ -221,6 +371,7 @@ __device__ __forceinline__ uint64_t time_to_cycles(uint64_t ps, double f) { retu
 
 struct NocParams {
   uint32_t tiles, w, h, flit_width, router_delay, link_delay, qm, analytical, max_size, net_model;
+  uint32_t qtype, qaux;                 // router queue model (GG_QM_*) and its hq_aux parameter
   double f;
 };
 

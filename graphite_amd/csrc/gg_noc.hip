@@ -516,20 +516,12 @@ __global__ void k_init_pkts(const uint32_t* __restrict__ src, const uint64_t* __
   S.t[k] = t0[k]; S.zl[k] = 0; S.ct[k] = 0; S.cur[k] = src[k];
 }
 
-__global__ void k_htree_reset(HQueue* q, HNode* nd, int16_t* fl, uint64_t nq, uint32_t max_size)
+__global__ void k_htree_reset(HQueue* q, HNode* nd, int16_t* fl, uint64_t nq, uint32_t max_size, uint32_t type,
+                              uint32_t aux)
 {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nq) return;
-  HQueue Q{};
-  Q.max_size = max_size;
-  int16_t* f = fl + i * max_size;
-  for (uint32_t j = 0; j < max_size; ++j) f[j] = (int16_t)j;        // allocateMemory
-  Q.free_tail = (int32_t)max_size - 1;
-  HNode* N = nd + i * max_size;
-  const int r = f[Q.free_tail--];                                   // allocateNode(PAIR(0, UINT64_MAX))
-  N[r].first = 0; N[r].second = ~0ull; N[r].parent = N[r].left = N[r].right = -1; N[r].height = 1;
-  Q.root = r; Q.size = 1;
-  q[i] = Q;
+  hq_init(q + i, nd + i * max_size, fl + i * max_size, max_size, type, aux);
 }
 
 __global__ void k_htree_seq(HQueue* q, HNode* nd, int16_t* fl, uint64_t min_proc, uint32_t analytical,
@@ -581,6 +573,9 @@ gg_status gg_noc_alloc(gg_ctx* ctx)
   P.net_model = c.net_model;
   P.f = c.frequency_ghz;
   if (P.max_size > 32767) return gg_fail(GG_ERR_UNSUPPORTED, "max_list_size too large");
+  P.qtype = c.queue_model_type;
+  P.qaux = hq_aux(c.queue_model_type, c.basic_moving_avg, c.history_list_no_interleaving);
+  if (gg_status e = gg_check_queue_model(c.queue_model_type, P.qaux, P.max_size)) return e;
   S->staged = !(getenv("GG_NOC_STAGED") && atoi(getenv("GG_NOC_STAGED")) == 0);
   GG_HIP(hipFuncSetAttribute((const void*)k_port_staged<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
   GG_HIP(hipFuncSetAttribute((const void*)k_port_staged<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
@@ -611,7 +606,7 @@ gg_status gg_noc_reset(gg_ctx* ctx, hipStream_t s)
   gg_noc_state* S = ctx->noc;
   GG_HIP(hipMemsetAsync(S->ctr, 0, sizeof(uint64_t) * S->P.tiles * GG_NUM_NET_COUNTERS, s));
   hipLaunchKernelGGL(k_htree_reset, dim3((uint32_t)((S->nq + 255) / 256)), dim3(256), 0, s, S->q, S->nd, S->fl,
-                     S->nq, S->P.max_size);
+                     S->nq, S->P.max_size, S->P.qtype, S->P.qaux);
   GG_HIP(hipGetLastError());
   return GG_OK;
 }
@@ -742,7 +737,7 @@ gg_status gg_htree_run(gg_ctx* ctx, uint64_t min_proc, const uint64_t* t, const 
   hipStream_t s = ctx->last_stream;
   const uint64_t qi = (uint64_t)S->P.tiles * 6;   // the stand-alone queue
   hipLaunchKernelGGL(k_htree_reset, dim3(1), dim3(1), 0, s, S->q + qi, S->nd + qi * S->P.max_size,
-                     S->fl + qi * S->P.max_size, 1ull, S->P.max_size);
+                     S->fl + qi * S->P.max_size, 1ull, S->P.max_size, S->P.qtype, S->P.qaux);
   uint64_t* buf = nullptr;
   GG_HIP(hipMalloc((void**)&buf, 24 * (n ? n : 1)));
   GG_HIP(hipMemcpyAsync(buf, t, 8 * n, hipMemcpyHostToDevice, s));

@@ -287,6 +287,50 @@ struct Hop {
 };
 enum { RECEIVE_TILE = 2 };
 
+// QueueModel::create (shared_models/queue_model.cc:19-39): the type string of
+// network/emesh_hop_by_hop/queue_model/type or dram/queue_model/type ->
+// gg_config.queue_model_type / dram_queue_model_type.  Unknown types are an
+// error, as LOG_PRINT_ERROR("Unrecognized Queue Model Type") in the reference.
+inline uint32_t queueModelType(const std::string& type)
+{
+  if (type == "history_tree") return GG_QM_HISTORY_TREE;
+  if (type == "history_list") return GG_QM_HISTORY_LIST;
+  if (type == "basic") return GG_QM_BASIC;
+  throw std::invalid_argument("Unrecognized Queue Model Type(" + type + ")");
+}
+// MovingAverage::createAvgType (common/misc/moving_average.h) for
+// queue_model/basic: packs moving_avg_{enabled,type,window_size} into
+// gg_config.basic_moving_avg.
+inline uint32_t basicMovingAverage(bool enabled, const std::string& type, uint32_t window)
+{
+  uint32_t avg;
+  if (!enabled) avg = GG_MAVG_NONE;
+  else if (type == "arithmetic_mean") avg = GG_MAVG_ARITHMETIC_MEAN;
+  else if (type == "median") avg = GG_MAVG_MEDIAN;
+  else if (type == "geometric_mean") avg = GG_MAVG_GEOMETRIC_MEAN;   // rejected by gg_create
+  else throw std::invalid_argument("Unsupported Average Type: " + type);
+  if (window == 0 || window > 0xFFFF) throw std::invalid_argument("moving_avg_window_size");
+  return window | (avg << 16);
+}
+
+// The configured queue model (cfg.queue_model_type) over a sequence of
+// requests from its constructor state: computeQueueDelay per request.
+class QueueModel {
+ public:
+  QueueModel(Backend& be, uint64_t min_processing_time) : _be(be), _min(min_processing_time) {}
+  std::vector<uint64_t> computeQueueDelays(const std::vector<uint64_t>& pkt_time, const std::vector<uint64_t>& proc_time)
+  {
+    if (pkt_time.size() != proc_time.size()) throw std::invalid_argument("computeQueueDelays: size mismatch");
+    std::vector<uint64_t> d(pkt_time.size());
+    check(gg_queue_delay_batch(_be.ctx(), _min, pkt_time.data(), proc_time.data(), pkt_time.size(), d.data()),
+          "gg_queue_delay_batch");
+    return d;
+  }
+ private:
+  Backend& _be;
+  uint64_t _min;
+};
+
 class NetworkModel {
  public:
   explicit NetworkModel(Backend& be) : _be(be) {}

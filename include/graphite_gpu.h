@@ -328,9 +328,11 @@ gg_status gg_noc_route_batch(gg_ctx* ctx, const gg_packets* pk,
 /* out: num_tiles * GG_NUM_NET_COUNTERS, [tile][counter].                      */
 gg_status gg_noc_get_counters(gg_ctx* ctx, uint64_t* out);
 
-/* Stand-alone QueueModelHistoryTree(min_processing_time) over a sequence of
- * (pkt_time, processing_time) requests; writes the queue delays.  Host
- * pointers; used by the known-answer test (tests/unit/history_tree).         */
+/* Stand-alone queue model of cfg.queue_model_type (QueueModel::create(type,
+ * min_processing_time), queue_model.cc:19-39: history_tree by default,
+ * history_list, basic) over a sequence of (pkt_time, processing_time)
+ * requests; writes the queue delays.  Host pointers; used by the known-answer
+ * test (tests/unit/history_tree) and the reference-harness fixtures.         */
 gg_status gg_queue_delay_batch(gg_ctx* ctx, uint64_t min_processing_time,
                                const uint64_t* pkt_time, const uint64_t* proc_time,
                                uint64_t n, uint64_t* delay_out);

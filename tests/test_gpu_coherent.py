@@ -214,3 +214,17 @@ def test_coherent_fft_capture_matches_oracle(m, p, net):
     cfg = C.default_config(p, net_model=net)
     g = _compare(cfg, a, meta, offs)
     assert g[1][:, C.TILE_STATS.index("l2_misses")].sum() > 0
+
+
+@pytest.mark.parametrize("qtype,aux,net", [
+    (C.QM_HISTORY_LIST, 0, C.NET_EMESH_HOP_COUNTER),
+    (C.QM_BASIC, 0, C.NET_EMESH_HOP_COUNTER),
+    (C.QM_HISTORY_LIST, 0, C.NET_EMESH_HOP_BY_HOP),       # list in the DRAM queue and the routers
+])
+def test_coherent_other_queue_models(qtype, aux, net):
+    """dram/queue_model/type (and the router queues) = history_list / basic."""
+    from oracle import pyoracle as po
+    cfg = C.default_config(16, net_model=net, dram_queue_model_type=qtype, queue_model_type=qtype,
+                           basic_moving_avg=aux)
+    a, m, o = po.gen_trace(16, 1500, hot_lines=16)
+    _compare(cfg, a, m, o)

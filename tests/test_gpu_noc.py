@@ -109,3 +109,49 @@ def test_hop_by_hop_without_queue_model():
     for g, r in zip(got, ref):
         np.testing.assert_array_equal(g, r)
     assert int(ref[2].sum()) == 0
+
+
+# ---- history_list / basic queue models (QueueModel::create, queue_model.cc:19-39) ----
+def _qcfg(e, T=4):
+    if e["kind"] == "qlist":
+        return C.default_config(T, queue_model_type=C.QM_HISTORY_LIST, max_list_size=e["max_list_size"],
+                                analytical_enabled=int(e["analytical"]), history_list_no_interleaving=e["aux"])
+    return C.default_config(T, queue_model_type=C.QM_BASIC, basic_moving_avg=e["aux"])
+
+
+@pytest.mark.parametrize("name", [k for k, v in M.items() if v["kind"] in ("qlist", "qbasic")])
+def test_other_queue_model_fixtures_on_gpu(name):
+    torch_dev()
+    e = M[name]
+    rows = load(e["file"], np.uint64).reshape(-1, 3)
+    be = B.Backend(_qcfg(e))
+    np.testing.assert_array_equal(be.queue_delay_batch(rows[:, 0], rows[:, 1]), rows[:, 2])
+
+
+@pytest.mark.parametrize("qtype,aux,T,n,span", [
+    (C.QM_HISTORY_LIST, 0, 16, 4000, 200000),
+    (C.QM_HISTORY_LIST, 1, 64, 20000, 500000),             # interleaving disabled
+    (C.QM_BASIC, 0, 64, 20000, 500000),                    # arithmetic mean over 64
+    (C.QM_BASIC, C.MAVG_MEDIAN << 16 | 16, 16, 4000, 200000),
+    (C.QM_BASIC, C.MAVG_NONE << 16, 256, 30000, 1000000),
+])
+def test_hop_by_hop_other_queue_models_match_oracle(qtype, aux, T, n, span):
+    """Router output-port contention through network/emesh_hop_by_hop/queue_model/type
+    = history_list / basic, bit-exact vs the oracle."""
+    torch = torch_dev()
+    kw = dict(basic_moving_avg=aux) if qtype == C.QM_BASIC else dict(history_list_no_interleaving=aux)
+    cfg = C.default_config(T, net_model=C.NET_EMESH_HOP_BY_HOP, queue_model_type=qtype, **kw)
+    src, dst, bits, t = packets(T, n, T + n + qtype, span)
+    be, got = run_noc(torch, cfg, src, dst, bits, t)
+    on, ref = oracle_noc(cfg, src, dst, bits, t)
+    for g, r in zip(got, ref):
+        np.testing.assert_array_equal(g, r)
+    np.testing.assert_array_equal(be.noc_counters(), on.counters())
+    assert int(ref[2].sum()) > 0
+
+
+def test_unsupported_queue_model_is_rejected():
+    torch_dev()
+    with pytest.raises(Exception):
+        B.Backend(C.default_config(16, net_model=C.NET_EMESH_HOP_BY_HOP, queue_model_type=C.QM_BASIC,
+                                   basic_moving_avg=C.MAVG_GEOMETRIC_MEAN << 16))
