@@ -50,6 +50,18 @@ int main(int argc, char** argv)
       writeCacheSummary(std::cout, "L2", c2, true);
       writeCacheSummary(std::cout, "L2", z, true);
       return 0;
+    } else if (a == "--net-summary-selftest") {
+      uint64_t nc[GG_NUM_NET_COUNTERS] = {0};
+      nc[GG_NC_PACKETS_SENT] = 70; nc[GG_NC_FLITS_SENT] = 430; nc[GG_NC_BITS_SENT] = 24530;
+      nc[GG_NC_PACKETS_RECEIVED] = 66; nc[GG_NC_FLITS_RECEIVED] = 400; nc[GG_NC_BITS_RECEIVED] = 23000;
+      nc[GG_NC_TOTAL_LATENCY_PS] = 1234567; nc[GG_NC_TOTAL_CONTENTION_PS] = 45001;
+      nc[GG_NC_BUFFER_WRITES] = 1720; nc[GG_NC_BUFFER_READS] = 1720; nc[GG_NC_SWITCH_ALLOC] = 280;
+      nc[GG_NC_CROSSBAR] = 1720; nc[GG_NC_LINK_TRAVERSALS] = 1720;
+      const uint64_t z[GG_NUM_NET_COUNTERS] = {0};
+      writeNetworkSummary(std::cout, nc, 1.0, GG_NET_EMESH_HOP_COUNTER);
+      writeNetworkSummary(std::cout, nc, 2.5, GG_NET_EMESH_HOP_BY_HOP);
+      writeNetworkSummary(std::cout, z, 1.0, GG_NET_MAGIC);
+      return 0;
     } else { std::fprintf(stderr, "unknown option %s\n", a.c_str()); return 2; }
   }
   try {

@@ -20,6 +20,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <iomanip>
@@ -134,6 +135,49 @@ inline void writeCacheSummary(std::ostream& out, const std::string& name, const 
   out << "      Tag Array Writes: " << c[GG_CC_TAG_WRITES] << std::endl;
   out << "      Data Array Reads: " << c[GG_CC_DATA_READS] << std::endl;
   out << "      Data Array Writes: " << c[GG_CC_DATA_WRITES] << std::endl;
+}
+
+// NetworkModel::outputSummary (network/network_model.cc:274-316) for one tile's
+// GG_NC_* counters, followed for emesh_hop_counter by its event counters
+// (network_model_emesh_hop_counter.cc:160-165,226-236).  Time::toCycles /
+// toNanosec (misc/time_types.h:104-114) on the picosecond sums; averages are
+// float, printed with the default ostream format.  No broadcasts are modeled
+// (full_map never broadcasts), so the broadcast lines read 0.  The
+// asynchronous-communication block is empty in a single DVFS domain.
+inline void writeNetworkSummary(std::ostream& out, const uint64_t* nc, double frequency_ghz, uint32_t net_model)
+{
+  auto to_cycles = [&](uint64_t ps) { return (uint64_t)ceil(((double)ps * frequency_ghz) / double(1.0e3)); };
+  auto to_ns = [](uint64_t ps) { return (uint64_t)ceil(((double)ps) / double(1.0e3)); };
+  out << "    Total Packets Sent: " << nc[GG_NC_PACKETS_SENT] << std::endl;
+  out << "    Total Flits Sent: " << nc[GG_NC_FLITS_SENT] << std::endl;
+  out << "    Total Bits Sent: " << nc[GG_NC_BITS_SENT] << std::endl;
+  out << "    Total Packets Broadcasted: " << 0 << std::endl;
+  out << "    Total Flits Broadcasted: " << 0 << std::endl;
+  out << "    Total Bits Broadcasted: " << 0 << std::endl;
+  out << "    Total Packets Received: " << nc[GG_NC_PACKETS_RECEIVED] << std::endl;
+  out << "    Total Flits Received: " << nc[GG_NC_FLITS_RECEIVED] << std::endl;
+  out << "    Total Bits Received: " << nc[GG_NC_BITS_RECEIVED] << std::endl;
+  const uint64_t n = nc[GG_NC_PACKETS_RECEIVED];
+  if (n > 0) {
+    const uint64_t lat = nc[GG_NC_TOTAL_LATENCY_PS], con = nc[GG_NC_TOTAL_CONTENTION_PS];
+    out << "    Average Packet Latency (in clock cycles): " << ((float)to_cycles(lat)) / n << std::endl;
+    out << "    Average Packet Latency (in nanoseconds): " << ((float)to_ns(lat)) / n << std::endl;
+    out << "    Average Contention Delay (in clock cycles): " << ((float)to_cycles(con)) / n << std::endl;
+    out << "    Average Contention Delay (in nanoseconds): " << ((float)to_ns(con)) / n << std::endl;
+  } else {
+    out << "    Average Packet Latency (in clock cycles): 0" << std::endl;
+    out << "    Average Packet Latency (in nanoseconds): 0" << std::endl;
+    out << "    Average Contention Delay (in clock cycles): 0" << std::endl;
+    out << "    Average Contention Delay (in nanoseconds): 0" << std::endl;
+  }
+  if (net_model == GG_NET_EMESH_HOP_COUNTER) {
+    out << "    Event Counters:" << std::endl;
+    out << "      Buffer Writes: " << nc[GG_NC_BUFFER_WRITES] << std::endl;
+    out << "      Buffer Reads: " << nc[GG_NC_BUFFER_READS] << std::endl;
+    out << "      Switch Allocator Traversals: " << nc[GG_NC_SWITCH_ALLOC] << std::endl;
+    out << "      Crossbar Traversals: " << nc[GG_NC_CROSSBAR] << std::endl;
+    out << "      Link Traversals: " << nc[GG_NC_LINK_TRAVERSALS] << std::endl;
+  }
 }
 
 // One cache (tile, level) of a Backend with the reference Cache API.

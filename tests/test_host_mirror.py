@@ -85,3 +85,45 @@ def test_trace_replayer_matches_oracle():
     ref = oc.counters()
     for t in range(T):
         np.testing.assert_array_equal(got[t], ref[t])
+
+
+def reference_net_summary(nc, f, hop_counter):
+    """NetworkModel::outputSummary (network_model.cc:274-316) + the hop counter's
+    event counters (network_model_emesh_hop_counter.cc:226-236), restated;
+    averages are float32 printed like %g."""
+    import math
+    f32 = lambda x: float(np.float32(x))
+    L = ["    Total Packets Sent: %d" % nc["ps"], "    Total Flits Sent: %d" % nc["fs"],
+         "    Total Bits Sent: %d" % nc["bs"], "    Total Packets Broadcasted: 0",
+         "    Total Flits Broadcasted: 0", "    Total Bits Broadcasted: 0",
+         "    Total Packets Received: %d" % nc["pr"], "    Total Flits Received: %d" % nc["fr"],
+         "    Total Bits Received: %d" % nc["br"]]
+    n = nc["pr"]
+    if n:
+        cyc = lambda ps: math.ceil(ps * f / 1.0e3)
+        ns = lambda ps: math.ceil(ps / 1.0e3)
+        avg = lambda v: "%g" % f32(f32(v) / np.float32(n))
+        L += ["    Average Packet Latency (in clock cycles): " + avg(cyc(nc["lat"])),
+              "    Average Packet Latency (in nanoseconds): " + avg(ns(nc["lat"])),
+              "    Average Contention Delay (in clock cycles): " + avg(cyc(nc["con"])),
+              "    Average Contention Delay (in nanoseconds): " + avg(ns(nc["con"]))]
+    else:
+        L += ["    Average Packet Latency (in clock cycles): 0", "    Average Packet Latency (in nanoseconds): 0",
+              "    Average Contention Delay (in clock cycles): 0", "    Average Contention Delay (in nanoseconds): 0"]
+    if hop_counter:
+        L += ["    Event Counters:", "      Buffer Writes: %d" % nc["bw"], "      Buffer Reads: %d" % nc["brd"],
+              "      Switch Allocator Traversals: %d" % nc["sa"], "      Crossbar Traversals: %d" % nc["xb"],
+              "      Link Traversals: %d" % nc["lt"]]
+    return L
+
+
+def test_network_summary_format_matches_reference():
+    if not os.path.exists(REPLAY):
+        pytest.skip("gg_replay not built")
+    out = subprocess.run([REPLAY, "--net-summary-selftest"], capture_output=True, text=True, check=True).stdout
+    nc = dict(ps=70, fs=430, bs=24530, pr=66, fr=400, br=23000, lat=1234567, con=45001,
+              bw=1720, brd=1720, sa=280, xb=1720, lt=1720)
+    z = {k: 0 for k in nc}
+    exp = reference_net_summary(nc, 1.0, True) + reference_net_summary(nc, 2.5, False) + \
+        reference_net_summary(z, 1.0, False)
+    assert out.splitlines() == exp
