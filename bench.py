@@ -82,6 +82,9 @@ def parse():
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--replay-kernel", type=int, default=0,
                    help="0 = single-pass streaming replay, 1 = sharded generic, 2 = sharded lean")
+    p.add_argument("--stress-tiles", type=int, default=4096,
+                   help="configs[4] private-part section: tiles (0 = skip)")
+    p.add_argument("--stress-per-tile", type=int, default=1 << 18)
     p.add_argument("--coherent-tiles", type=int, default=256,
                    help="coherent-mode (Mode C) section: total tiles (0 = skip); configs[2] = 256")
     p.add_argument("--coherent-per-tile", type=int, default=4096, help="coherent-mode accesses per tile")
@@ -257,6 +260,72 @@ def noc_section(args, dev):
     return res
 
 
+def stress_section(args, dev):
+    """configs[4] geometry in Mode P (its private part): 4096 tiles,
+    32KB/4w L1-D + 512KB/16w L2 (512 sets), 2^18 accesses per tile from the
+    configs[1] uniform-random private generator (WRITE p = 1/3).  16-way L2
+    sets do not fit the streaming kernel's LDS budget, so the batch runs the
+    sharded path (shard scatter -> lean replay -> unshard).  HIP-event timed
+    whole batch; one tile checked bit-exact against the oracle; the oracle on
+    4 tiles, 1 thread, is the CPU baseline."""
+    import torch
+    from graphite_amd import config as C
+    from graphite_amd import backend as B
+    from oracle import pyoracle as po
+    T, N = args.stress_tiles, args.stress_per_tile
+    cfg = C.default_config(T, l2_assoc=16)
+    be = B.Backend(cfg)
+    be.set_timing(True)
+    n = T * N
+    addr = torch.empty(n, dtype=torch.int64, device=dev)
+    meta = torch.empty(n, dtype=torch.int32, device=dev)
+    result = torch.empty(n, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    B.gen_uniform_trace(addr, meta, 0, T, N, stream=stream)
+    offs = np.arange(T + 1, dtype=np.uint64) * np.uint64(N)
+    times = []
+    for it in range(2):                       # first launch warms up
+        be.reset()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        be.cache_access_batch(addr, meta, offs, result, None, stream)
+        e1.record()
+        torch.cuda.synchronize()
+        times.append(e0.elapsed_time(e1) / 1e3)
+    dt = times[-1]
+    kern = {k: be.kernel_time_ms(k) for k in KERNEL_BYTES}
+    kern = {k: round(v, 4) for k, v in kern.items() if v >= 0}
+    res = {"workload": "configs[4] private part: %d tiles x %d accesses, 32KB/4w L1-D + 512KB/16w L2, "
+                       "configs[1] uniform-random private generator (WRITE p=1/3), Mode P" % (T, N),
+           "value": n / dt, "unit": "accesses/s", "seconds": dt, "kernels_ms": kern,
+           "path_GB_s": n * ALGO_BYTES_PER_ACCESS / dt / 1e9}
+    if not args.no_verify:
+        t = T - 1
+        a, m = po.gen_uniform(t, 0, N)
+        oc = po.OracleCache(C.default_config(1, l2_assoc=16))
+        ref = oc.run(a - np.uint64(t << 26), m, np.array([0, N], np.uint64))
+        got = result[t * N:(t + 1) * N].cpu().numpy().view(np.uint32)
+        res["bit_exact_checked"] = bool(np.array_equal(got, ref) and
+                                        np.array_equal(be.cache_counters()[t], oc.counters()[0]))
+        if not res["bit_exact_checked"]:
+            print("bench.py: STRESS BIT-EXACT CHECK FAILED", file=sys.stderr)
+        if not args.no_cpu_baseline:
+            c0 = time.perf_counter()
+            for k in range(4):
+                a, m = po.gen_uniform(k, 0, N)
+                po.OracleCache(C.default_config(1, l2_assoc=16)).run(a - np.uint64(k << 26), m,
+                                                                       np.array([0, N], np.uint64))
+            cdt = time.perf_counter() - c0
+            res["cpu_baseline"] = {"value": 4 * N / cdt, "unit": "accesses/s", "cores": 1, "kind": "port",
+                                   "sample": "4 tiles x %d accesses, oracle/gg_oracle.c -O3, 1 thread, %.2f s"
+                                             % (N, cdt)}
+    be.close()
+    del addr, meta, result
+    torch.cuda.empty_cache()
+    return res
+
+
 def cpu_baseline(tiles, per_tile, threads):
     """Oracle (oracle/gg_oracle.c, -O3) on a bounded sample: `tiles` tile
     replays (fresh cache state each) cycling over 16 pre-generated tiles of
@@ -410,6 +479,8 @@ def main():
         out["fft"] = fft_section(args, dev)
     if args.noc_packets and world == 1:
         out["noc"] = noc_section(args, dev)
+    if args.stress_tiles and world == 1:
+        out["stress"] = stress_section(args, dev)
     if rank == 0:
         print(json.dumps(out))
     if world > 1:
