@@ -61,7 +61,7 @@ TILE_STATS = ["clock_ps", "accesses", "l1_hits", "l2_hits", "l2_misses", "latenc
               "dir_accesses", "dir_evictions", "dir_back_invalidations",
               "dram_accesses", "dram_latency_ns", "dram_queue_delay_ns",
               "dram_queue_requests", "dram_queue_analytical", "msgs_sent", "msgs_received"] + \
-             ["sent_" + n.lower() for n in MSG_TYPES]
+             ["sent_" + n.lower() for n in MSG_TYPES] + ["dram_queue_utilized_ns", "dram_queue_last_ns"]
 NUM_TILE_STATS = 32
 RUN_INFO = ["quanta", "steps", "net_msgs", "self_msgs", "boundary_msgs", "final_quantum"]
 NUM_RUN_INFO = 8

@@ -1079,6 +1079,8 @@ __global__ void k_c_final_stats(CP P, CS S)
   const uint32_t lt = blockIdx.x * blockDim.x + threadIdx.x;
   if (lt >= P.lt || !P.dram_qm) return;
   S.st[(size_t)lt * GG_NUM_TILE_STATS + GG_CT_DRAM_QUEUE_ANALYTICAL] = S.dq[lt].analytical;
+  S.st[(size_t)lt * GG_NUM_TILE_STATS + GG_CT_DRAM_QUEUE_UTILIZED_NS] = S.dq[lt].util;
+  S.st[(size_t)lt * GG_NUM_TILE_STATS + GG_CT_DRAM_QUEUE_LAST_NS] = S.dq[lt].last_req;
 }
 
 // export: group the boundary messages by destination shard

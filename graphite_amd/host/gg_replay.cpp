@@ -62,6 +62,27 @@ int main(int argc, char** argv)
       writeNetworkSummary(std::cout, nc, 2.5, GG_NET_EMESH_HOP_BY_HOP);
       writeNetworkSummary(std::cout, z, 1.0, GG_NET_MAGIC);
       return 0;
+    } else if (a == "--mem-summary-selftest") {
+      uint64_t st[GG_NUM_TILE_STATS] = {0};
+      st[GG_CT_DIR_ACCESSES] = 5123; st[GG_CT_DIR_EVICTIONS] = 17; st[GG_CT_DIR_BACK_INVALIDATIONS] = 9;
+      st[GG_CT_DRAM_ACCESSES] = 321; st[GG_CT_DRAM_LATENCY_NS] = 40417; st[GG_CT_DRAM_QUEUE_DELAY_NS] = 1537;
+      st[GG_CT_DRAM_QUEUE_REQUESTS] = 321; st[GG_CT_DRAM_QUEUE_ANALYTICAL] = 7;
+      st[GG_CT_DRAM_QUEUE_UTILIZED_NS] = 4173; st[GG_CT_DRAM_QUEUE_LAST_NS] = 90211;
+      uint64_t cc[2 * GG_NUM_CACHE_COUNTERS] = {1000, 250, 700, 150, 300, 100, 240, 0, 2600, 900, 760, 1250,
+                                                250, 180, 150, 110, 100, 70, 120, 45, 700, 600, 190, 480};
+      const uint64_t z[GG_NUM_TILE_STATS] = {0};
+      gg_config c;
+      gg_config_default(&c, 64);
+      writeMemorySummary(std::cout, c, st, cc);                       // auto sizing, history_tree
+      gg_config_default(&c, 1024);
+      c.dram_queue_model_type = GG_QM_HISTORY_LIST;
+      writeDramSummary(std::cout, st, true, c.dram_queue_model_type);
+      writeDirectorySummary(std::cout, z, directorySizing(c));
+      c.dir_total_entries = 4096; c.dir_access_cycles = 3;
+      writeDramSummary(std::cout, z, false, GG_QM_HISTORY_TREE);       // 0 accesses, no queue block
+      writeDirectorySummary(std::cout, st, directorySizing(c));
+      writeDramSummary(std::cout, st, true, GG_QM_BASIC);
+      return 0;
     } else { std::fprintf(stderr, "unknown option %s\n", a.c_str()); return 2; }
   }
   try {

@@ -180,6 +180,88 @@ inline void writeNetworkSummary(std::ostream& out, const uint64_t* nc, double fr
   }
 }
 
+// DramPerfModel::outputSummary (performance_models/dram_perf_model.cc:131-164)
+// for one tile's GG_CT_* stats of the coherent mode.  The averages are double
+// sums divided by the access count, printed as float (0 accesses print the
+// x86 default NaN, "-nan", as the reference does); the queue block exists for
+// history_list / history_tree only and reads QueueModel::getQueueUtilization
+// (queue_model.cc:57-62) and the analytical-request fraction, both float.
+inline void writeDramSummary(std::ostream& out, const uint64_t* st, bool queue_model_enabled, uint32_t queue_type)
+{
+  const uint64_t n = st[GG_CT_DRAM_ACCESSES];
+  const double lat = (double)st[GG_CT_DRAM_LATENCY_NS], qd = (double)st[GG_CT_DRAM_QUEUE_DELAY_NS];
+  out << "Dram Performance Model Summary: " << std::endl;
+  out << "    Total Dram Accesses: " << n << std::endl;
+  out << "    Average Dram Access Latency (in nanoseconds): " << (float)(lat / n) << std::endl;
+  out << "    Average Dram Contention Delay (in nanoseconds): " << (float)(qd / n) << std::endl;
+  if (queue_model_enabled && (queue_type == GG_QM_HISTORY_LIST || queue_type == GG_QM_HISTORY_TREE)) {
+    const uint64_t total_cycles = st[GG_CT_DRAM_QUEUE_LAST_NS];
+    const float util = total_cycles > 0 ? ((float)st[GG_CT_DRAM_QUEUE_UTILIZED_NS]) / total_cycles : 0.0f;
+    const float frac = ((float)st[GG_CT_DRAM_QUEUE_ANALYTICAL]) / st[GG_CT_DRAM_QUEUE_REQUESTS];
+    out << "    Queue Model:" << std::endl;
+    out << "      Queue Utilization(%): " << util * 100 << std::endl;
+    out << "      Analytical Model Used(%): " << frac * 100 << std::endl;
+  }
+}
+
+// DirectoryCache sizing of a coherent configuration (directory_cache.cc:46-59,
+// 243-322): auto total entries from the L2 size, full-map entry bytes =
+// ceil(application tiles / 8) (DirectoryEntry::getSize, directory_entry.cc:75-92),
+// auto access cycles from the directory size.
+struct DirectorySizing {
+  uint32_t total_entries, size_kb;
+  uint64_t access_cycles;
+  bool auto_entries, auto_cycles;
+};
+inline DirectorySizing directorySizing(const gg_config& c)
+{
+  DirectorySizing d;
+  d.auto_entries = c.dir_total_entries == 0;
+  d.auto_cycles = c.dir_access_cycles == 0;
+  if (d.auto_entries) {
+    uint32_t sets = (uint32_t)ceil(2.0 * c.l2_size_kb * 1024 * c.num_tiles / (1.0 * c.line_size * c.dir_assoc * c.num_tiles));
+    uint32_t lg = 0;
+    while ((1u << lg) < sets) ++lg;
+    d.total_entries = (1u << lg) * c.dir_assoc;
+  } else d.total_entries = c.dir_total_entries;
+  const uint64_t size = (uint64_t)d.total_entries * (uint64_t)ceil(1.0 * c.num_tiles / 8);
+  d.size_kb = (uint32_t)ceil(1.0 * size / 1024);
+  const uint32_t kb = d.size_kb;
+  d.access_cycles = !d.auto_cycles ? c.dir_access_cycles
+                  : kb <= 16 ? 1 : kb <= 32 ? 2 : kb <= 64 ? 4 : kb <= 128 ? 6 : kb <= 256 ? 8
+                  : kb <= 512 ? 10 : kb <= 1024 ? 13 : kb <= 2048 ? 16 : 20;
+  return d;
+}
+
+// "Dram Directory Summary:" (MemoryManager::outputSummary, msi/memory_manager.cc:427-428)
+// + DirectoryCache::outputSummary (directory_cache.cc:350-369, 385-398).  The
+// asynchronous-communication block is empty in a single DVFS domain.
+inline void writeDirectorySummary(std::ostream& out, const uint64_t* st, const DirectorySizing& d)
+{
+  out << "Dram Directory Summary:\n";
+  if (d.auto_entries) {
+    out << "    Total Entries [auto-generated]: " << d.total_entries << std::endl;
+    out << "    Size (in KB) [auto-generated]: " << d.size_kb << std::endl;
+  }
+  if (d.auto_cycles) out << "    Access Time (in clock cycles) [auto-generated]: " << d.access_cycles << std::endl;
+  out << "    Total Accesses: " << st[GG_CT_DIR_ACCESSES] << std::endl;
+  out << "    Total Evictions: " << st[GG_CT_DIR_EVICTIONS] << std::endl;
+  out << "    Total Back-Invalidations: " << st[GG_CT_DIR_BACK_INVALIDATIONS] << std::endl;
+}
+
+// The memory part of one tile's sim.out block in the coherent mode
+// (msi/memory_manager.cc:415-430): Cache Summary (L1-D, L2; no L1-I is
+// modeled), then the DRAM and directory summaries.
+inline void writeMemorySummary(std::ostream& out, const gg_config& c, const uint64_t* tile_stats,
+                               const uint64_t* cache_counters)
+{
+  out << "Cache Summary:\n";
+  writeCacheSummary(out, "L1-D", cache_counters, false);
+  writeCacheSummary(out, "L2", cache_counters + GG_NUM_CACHE_COUNTERS, true);
+  writeDramSummary(out, tile_stats, c.dram_queue_model_enabled != 0, c.dram_queue_model_type);
+  writeDirectorySummary(out, tile_stats, directorySizing(c));
+}
+
 // One cache (tile, level) of a Backend with the reference Cache API.
 class Cache {
  public:

@@ -266,6 +266,10 @@ enum {
   GG_CT_MSGS_SENT,           /* ShmemMsgs sent over the network (self-sends included)  */
   GG_CT_MSGS_RECEIVED,
   GG_CT_SENT_BY_TYPE,        /* + (type - 1), 11 entries                               */
+  /* QueueModel utilization counters of the DRAM queue (queue_model.cc:49-55),
+   * for DramPerfModel::outputSummary's "Queue Utilization" (dram_perf_model.cc:141-163) */
+  GG_CT_DRAM_QUEUE_UTILIZED_NS = GG_CT_SENT_BY_TYPE + 11, /* _total_utilized_cycles */
+  GG_CT_DRAM_QUEUE_LAST_NS,                               /* _last_request_time     */
   GG_NUM_TILE_STATS = 32
 };
 

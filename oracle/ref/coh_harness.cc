@@ -70,7 +70,7 @@ static HCfg H;
 
 enum { NC_PS = 0, NC_PR, NC_LAT, NC_N };        // packets sent, received, total latency (ps)
 enum { S_CLOCK = 0, S_ACC, S_L1H, S_L2H, S_MISS, S_LAT, S_DACC, S_DEV, S_DBI, S_DRAM, S_DRAMLAT, S_DRAMQD,
-       S_DRAMQR, S_DRAMQA, S_SENT, S_RECV, S_BYTYPE, S_N = 32 };
+       S_DRAMQR, S_DRAMQA, S_SENT, S_RECV, S_BYTYPE, S_DRAMQU = S_BYTYPE + 11, S_DRAMQL, S_N = 32 };
 
 struct HMsg {
   UInt32 src, dst, seq, type;
@@ -790,6 +790,7 @@ static void run_case(FILE* man, bool first, const char* name, UInt32 T, UInt32 N
     HDram& d = g_dram[X.mm->getDramCntlr()];
     s[S_DRAM] = d.n; s[S_DRAMLAT] = d.lat; s[S_DRAMQD] = d.qd; s[S_DRAMQR] = d.qreq;
     s[S_DRAMQA] = d.q ? d.q->analytical_requests : 0;
+    s[S_DRAMQU] = d.q ? d.q->util : 0; s[S_DRAMQL] = d.q ? d.q->last_req : 0;
     memcpy(&cc[((size_t)t * 2 + 0) * CC_N], ccount(X.mm->getL1DCache()), sizeof(UInt64) * CC_N);
     memcpy(&cc[((size_t)t * 2 + 1) * CC_N], ccount(X.mm->getL2Cache()), sizeof(UInt64) * CC_N);
   }

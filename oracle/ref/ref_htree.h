@@ -5,6 +5,7 @@
 #pragma once
 #include <vector>
 #include <utility>
+#include <algorithm>
 #include "interval_tree.h"
 #include "queue_model_m_g_1.h"
 
@@ -19,8 +20,10 @@ struct RefHistoryTree {
   UInt64 min_proc; SInt32 max_size; bool analytical;
   IntervalTree::Node* blocks; vector<SInt32> free_list; SInt32 tail;
   IntervalTree* tree; QueueModelMG1 mg1; UInt64 analytical_requests;
+  UInt64 util, last_req;                      // QueueModel utilization counters (queue_model.cc:41-55)
 
-  RefHistoryTree(UInt64 mp, SInt32 ms, bool an) : min_proc(mp), max_size(ms), analytical(an), analytical_requests(0) {
+  RefHistoryTree(UInt64 mp, SInt32 ms, bool an)
+      : min_proc(mp), max_size(ms), analytical(an), analytical_requests(0), util(0), last_req(0) {
     blocks = new IntervalTree::Node[ms];                          // allocateMemory (:129-137)
     free_list.resize(ms); for (SInt32 i = 0; i < ms; ++i) free_list[i] = i;
     tail = ms - 1;
@@ -65,6 +68,8 @@ struct RefHistoryTree {
     }
     CHECK(qd != UINT64_MAX);
     mg1.updateQueue(t, p, qd);
+    util += p;                                  // updateQueueUtilizationCounters (queue_model.cc:49-55)
+    last_req = std::max<UInt64>(last_req, t + qd + p);
     return qd;
   }
 };

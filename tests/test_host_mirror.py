@@ -127,3 +127,53 @@ def test_network_summary_format_matches_reference():
     exp = reference_net_summary(nc, 1.0, True) + reference_net_summary(nc, 2.5, False) + \
         reference_net_summary(z, 1.0, False)
     assert out.splitlines() == exp
+
+
+def reference_dram_summary(st, queue_block):
+    """DramPerfModel::outputSummary (dram_perf_model.cc:131-164), restated:
+    double sums / count printed as float (0 accesses: x86 default NaN, "-nan");
+    QueueModel::getQueueUtilization (queue_model.cc:57-62) and the analytical
+    fraction in float."""
+    f32 = np.float32
+    g = lambda x: "-nan" if np.isnan(x) else "%g" % float(x)
+    n = st["dram"]
+    avg = lambda s: g(f32(s / n) if n else float("nan"))
+    L = ["Dram Performance Model Summary: ", "    Total Dram Accesses: %d" % n,
+         "    Average Dram Access Latency (in nanoseconds): " + avg(st["lat"]),
+         "    Average Dram Contention Delay (in nanoseconds): " + avg(st["qd"])]
+    if queue_block:
+        util = f32(f32(st["util"]) / f32(st["last"])) if st["last"] else f32(0)
+        frac = f32(f32(st["an"]) / f32(st["qreq"]))
+        L += ["    Queue Model:", "      Queue Utilization(%%): %s" % g(f32(util * f32(100))),
+              "      Analytical Model Used(%%): %s" % g(f32(frac * f32(100)))]
+    return L
+
+
+def reference_directory_summary(st, auto):
+    """"Dram Directory Summary:" + DirectoryCache::outputSummary
+    (memory_manager.cc:427-428, directory_cache.cc:350-369,385-398); auto =
+    (entries, size KB, access cycles) when "auto", else None."""
+    L = ["Dram Directory Summary:"]
+    if auto:
+        L += ["    Total Entries [auto-generated]: %d" % auto[0], "    Size (in KB) [auto-generated]: %d" % auto[1],
+              "    Access Time (in clock cycles) [auto-generated]: %d" % auto[2]]
+    return L + ["    Total Accesses: %d" % st["dacc"], "    Total Evictions: %d" % st["dev"],
+                "    Total Back-Invalidations: %d" % st["dbi"]]
+
+
+def test_memory_summary_format_matches_reference():
+    if not os.path.exists(REPLAY):
+        pytest.skip("gg_replay not built")
+    out = subprocess.run([REPLAY, "--mem-summary-selftest"], capture_output=True, text=True, check=True).stdout
+    st = dict(dacc=5123, dev=17, dbi=9, dram=321, lat=40417, qd=1537, qreq=321, an=7, util=4173, last=90211)
+    z = {k: 0 for k in st}
+    c1 = [1000, 250, 700, 150, 300, 100, 240, 0, 2600, 900, 760, 1250]
+    c2 = [250, 180, 150, 110, 100, 70, 120, 45, 700, 600, 190, 480]
+    # SURVEY.md §8 derived constants: 64 tiles -> 1024x16 entries, 128 KB, 6 cycles;
+    # 1024 tiles -> 2 MB, 16 cycles
+    exp = ["Cache Summary:"] + reference_summary("L1-D", c1, False) + reference_summary("L2", c2, True) + \
+        reference_dram_summary(st, True) + reference_directory_summary(st, (16384, 128, 6)) + \
+        reference_dram_summary(st, True) + reference_directory_summary(z, (16384, 2048, 16)) + \
+        reference_dram_summary(z, False) + reference_directory_summary(st, None) + \
+        reference_dram_summary(st, False)
+    assert out.splitlines() == exp
