@@ -85,9 +85,11 @@ def parse():
     p.add_argument("--stress-tiles", type=int, default=4096,
                    help="configs[4] private-part section: tiles (0 = skip)")
     p.add_argument("--stress-per-tile", type=int, default=1 << 18)
-    p.add_argument("--coherent-tiles", type=int, default=256,
-                   help="coherent-mode (Mode C) section: total tiles (0 = skip); configs[2] = 256")
-    p.add_argument("--coherent-per-tile", type=int, default=4096, help="coherent-mode accesses per tile")
+    p.add_argument("--coherent-tiles", type=int, default=1024,
+                   help="coherent-mode (Mode C) section: total tiles (0 = skip); configs[2] = 256, configs[3] = 1024")
+    p.add_argument("--coherent-per-tile", type=int, default=2048, help="coherent-mode accesses per tile")
+    p.add_argument("--coherent-hot-lines", type=int, default=0,
+                   help="shared hot lines of the hotspot trace (0 = 64 up to 256 tiles (configs[2]), else 256 (configs[3]))")
     p.add_argument("--coherent-shards", type=int, default=0, help="logical shards (0 = 1, or 8 with --gpus > 1)")
     p.add_argument("--noc-packets", type=int, default=1 << 18, help="NoC section batch size (0 = skip)")
     p.add_argument("--noc-tiles", type=int, default=1024)
@@ -112,6 +114,7 @@ def coherent_section(args, world, rank, dev, backend_name):
     from graphite_amd import coherent as CO
     from graphite_amd import dist as D
     T, N = args.coherent_tiles, args.coherent_per_tile
+    H = args.coherent_hot_lines or (64 if T <= 256 else 256)
     K = args.coherent_shards or (8 if world > 1 else 1)
     k0, k1 = CO.shard_range(rank, world, K)
     net = {"hop_counter": C.NET_EMESH_HOP_COUNTER, "hop_by_hop": C.NET_EMESH_HOP_BY_HOP, "magic": C.NET_MAGIC}[args.coherent_net]
@@ -120,7 +123,7 @@ def coherent_section(args, world, rank, dev, backend_name):
     addr = torch.empty(T * N, dtype=torch.int64, device=dev)
     meta = torch.empty(T * N, dtype=torch.int32, device=dev)
     out = torch.zeros(T * N, dtype=torch.int64, device=dev)
-    B.gen_hotspot_trace(addr, meta, 0, T, N, hot_lines=64)
+    B.gen_hotspot_trace(addr, meta, 0, T, N, hot_lines=H)
     offs = np.arange(T + 1, dtype=np.uint64) * np.uint64(N)
     torch.cuda.synchronize()
     D.barrier()
@@ -136,9 +139,9 @@ def coherent_section(args, world, rank, dev, backend_name):
     D.barrier()
     elapsed = D.max_over_ranks(time.perf_counter() - t0)
     st, cc, ri = be.coherent_stats()
-    res = {"workload": "configs[2]-style hotspot trace: %d tiles x %d accesses (20%% to 64 shared lines, "
+    res = {"workload": "configs[2..3]-style hotspot trace: %d tiles x %d accesses (20%% to %d shared lines, "
                        "WRITE 1/3, gap ~2 cycles), MSI full-map directory + DRAM history tree + "
-                       "%s, quantum 1000 ns, %d logical shard(s)" % (T, N, "magic" if args.coherent_net == "magic" else "emesh_" + args.coherent_net, K),
+                       "%s, quantum 1000 ns, %d logical shard(s)" % (T, N, H, "magic" if args.coherent_net == "magic" else "emesh_" + args.coherent_net, K),
            "value": T * N / elapsed, "unit": "accesses/s", "seconds": elapsed,
            "quanta": int(ri[C.RUN_INFO.index("quanta")]) if quanta is None else quanta,
            "steps": int(ri[C.RUN_INFO.index("steps")]),
@@ -146,7 +149,7 @@ def coherent_section(args, world, rank, dev, backend_name):
            "simulated_ns": int(st[:, 0].max()) // 1000}
     if rank == 0 and world == 1 and not args.no_verify:
         from oracle import pyoracle as po
-        a, m, o = po.gen_trace(T, N, hot_lines=64)
+        a, m, o = po.gen_trace(T, N, hot_lines=H)
         oc = po.OracleCoherent(C.default_config(T, num_shards=K, net_model=net))
         c0 = time.perf_counter()
         ref = oc.run(a, m, o)
