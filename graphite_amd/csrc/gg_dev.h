@@ -74,22 +74,22 @@ __device__ inline void hq_init(HQueue* q, HNode* N, int16_t* f, uint32_t max_siz
 struct HTree {
   HQueue* q; HNode* nd; int16_t* fl; uint64_t min_proc; bool analytical;
 
-  __device__ int32_t h(int x) const { return x < 0 ? 0 : nd[x].height; }
-  __device__ void upd_child(int node, int child, int dir)      // updateChildPointer
+  __device__ __forceinline__ int32_t h(int x) const { return x < 0 ? 0 : nd[x].height; }
+  __device__ __forceinline__ void upd_child(int node, int child, int dir)      // updateChildPointer
   {
     if (node < 0) return;
     if (dir == 0) { if (nd[node].first < nd[child].first) nd[node].right = child; else nd[node].left = child; }
     else if (dir == 1) nd[node].left = child;
     else nd[node].right = child;
   }
-  __device__ void upd_parent(int node, int parent)             // updateParentPointer
+  __device__ __forceinline__ void upd_parent(int node, int parent)             // updateParentPointer
   {
     if (node >= 0) nd[node].parent = parent;
     if (parent < 0) q->root = node;
   }
-  __device__ bool balanced(int x) const { int d = h(nd[x].left) - h(nd[x].right); return d >= -1 && d <= 1; }
-  __device__ void upd_height(int x) { int a = h(nd[x].left), b = h(nd[x].right); nd[x].height = (int16_t)((a > b ? a : b) + 1); }
-  __device__ void rotate(int y, bool cw)                       // performRotation
+  __device__ __forceinline__ bool balanced(int x) const { int d = h(nd[x].left) - h(nd[x].right); return d >= -1 && d <= 1; }
+  __device__ __forceinline__ void upd_height(int x) { int a = h(nd[x].left), b = h(nd[x].right); nd[x].height = (int16_t)((a > b ? a : b) + 1); }
+  __device__ __forceinline__ void rotate(int y, bool cw)                       // performRotation
   {
     int x;
     if (cw) {
@@ -105,7 +105,7 @@ struct HTree {
     }
     upd_height(y); upd_height(x);
   }
-  __device__ int balance(int z)                                // balanceHeight
+  __device__ __forceinline__ int balance(int z)                                // balanceHeight
   {
     int zl = nd[z].left, zr = nd[z].right;
     bool y_left = h(zl) > h(zr);
@@ -123,7 +123,7 @@ struct HTree {
       rotate(z, false); return y;
     }
   }
-  __device__ void rebalance(int r)                             // rebalanceAVLTree
+  __device__ __forceinline__ void rebalance(int r)                             // rebalanceAVLTree
   {
     while (r >= 0) {
       int old = nd[r].height, nr = r;
@@ -132,7 +132,7 @@ struct HTree {
       r = nd[nr].parent;
     }
   }
-  __device__ void insert(int node)                             // insert / insertInTree
+  __device__ __forceinline__ void insert(int node)                             // insert / insertInTree
   {
     q->size++;
     int r = q->root;
@@ -148,7 +148,7 @@ struct HTree {
   }
   // removeFromTree (interval_tree.cc:322-356) without recursion: the successor
   // of a two-child node has no left child, so its removal is the one-child case
-  __device__ void remove_leafish(int node)
+  __device__ __forceinline__ void remove_leafish(int node)
   {
     if (nd[node].left < 0) {
       int p = nd[node].parent;
@@ -162,7 +162,7 @@ struct HTree {
       rebalance(p);
     }
   }
-  __device__ int remove_rec(int node)
+  __device__ __forceinline__ int remove_rec(int node)
   {
     if (nd[node].left < 0 || nd[node].right < 0) { remove_leafish(node); return node; }
     int succ = nd[node].right;
@@ -173,7 +173,7 @@ struct HTree {
     nd[succ].first = f; nd[succ].second = s;
     return succ;
   }
-  __device__ int remove(int node) { q->size--; return remove_rec(node); }
+  __device__ __forceinline__ int remove(int node) { q->size--; return remove_rec(node); }
   // searchTree (interval_tree.cc:366-394).  The recursion comes back to a
   // node only after searching its LEFT subtree (it descends left only when
   // b < first), so the pending nodes are exactly the ancestors entered through
@@ -181,7 +181,7 @@ struct HTree {
   // that node; otherwise the walk climbs parent pointers to the nearest
   // ancestor whose left subtree it is leaving.  No explicit stack (a
   // dynamically indexed array would live in scratch memory).
-  __device__ int search(uint64_t a, uint64_t b) const
+  __device__ __forceinline__ int search(uint64_t a, uint64_t b) const
   {
     int n = q->root, last = -1;
     bool went_left = false;
@@ -210,15 +210,15 @@ struct HTree {
       last = n; went_left = false; n = nd[n].right;
     }
   }
-  __device__ int alloc(uint64_t a, uint64_t b)                 // allocateNode
+  __device__ __forceinline__ int alloc(uint64_t a, uint64_t b)                 // allocateNode
   {
     if (q->free_tail < 0) return -1;
     int i = fl[q->free_tail--];
     nd[i].first = a; nd[i].second = b; nd[i].parent = nd[i].left = nd[i].right = -1; nd[i].height = 1;
     return i;
   }
-  __device__ void release(int i) { fl[++q->free_tail] = (int16_t)i; }
-  __device__ uint64_t mg1_delay() const                         // QueueModelMG1::computeQueueDelay
+  __device__ __forceinline__ void release(int i) { fl[++q->free_tail] = (int16_t)i; }
+  __device__ __forceinline__ uint64_t mg1_delay() const                         // QueueModelMG1::computeQueueDelay
   {
     if (q->n == 0) return 0;
     double variance = (q->sig_sq / q->n) - ((q->sig / q->n) * (q->sig / q->n));
@@ -229,7 +229,7 @@ struct HTree {
                           (service_rate - arrival_rate));
   }
   // ---- history_list: nd[0..size) in list order ----
-  __device__ void l_erase(uint32_t i)
+  __device__ __forceinline__ void l_erase(uint32_t i)
   {
     for (uint32_t j = i + 1; j < q->size; ++j) { nd[j - 1].first = nd[j].first; nd[j - 1].second = nd[j].second; }
     q->size--;
@@ -237,7 +237,7 @@ struct HTree {
   // replace interval i by up to two intervals (in list order).  The list may
   // overgrow by one only here, and then loses its front (the size check after
   // the scan, queue_model_history_list.cc:128-131): done in place.
-  __device__ void l_replace(uint32_t i, bool k1, uint64_t a1, uint64_t b1, bool k2, uint64_t a2, uint64_t b2)
+  __device__ __forceinline__ void l_replace(uint32_t i, bool k1, uint64_t a1, uint64_t b1, bool k2, uint64_t a2, uint64_t b2)
   {
     if (k1 && !k2) { nd[i].first = a1; nd[i].second = b1; return; }
     if (!k1 && k2) { nd[i].first = a2; nd[i].second = b2; return; }
@@ -253,7 +253,7 @@ struct HTree {
       nd[i - 1].first = a1; nd[i - 1].second = b1; nd[i].first = a2; nd[i].second = b2;
     }
   }
-  __device__ uint64_t list_scan(uint64_t t, uint64_t p)       // computeUsingHistoryList
+  __device__ __forceinline__ uint64_t list_scan(uint64_t t, uint64_t p)       // computeUsingHistoryList
   {
     uint64_t qd = 0;
     const bool inter = q->aux == 0;
@@ -284,7 +284,7 @@ struct HTree {
     return qd;
   }
   // ---- basic: MovingAverage<UInt64>::compute over the window words ----
-  __device__ uint64_t mavg(uint64_t x)
+  __device__ __forceinline__ uint64_t mavg(uint64_t x)
   {
     uint64_t* w = reinterpret_cast<uint64_t*>(nd);
     const uint32_t W = hq_window(q->aux), M = W + 1, avg = q->aux >> 16;
@@ -302,7 +302,7 @@ struct HTree {
     }
     return (uint64_t)q->mean;
   }
-  __device__ uint64_t basic_delay(uint64_t t, uint64_t p)
+  __device__ __forceinline__ uint64_t basic_delay(uint64_t t, uint64_t p)
   {
     const uint64_t ref = ((q->aux >> 16) == GG_MAVG_NONE) ? t : mavg(t);
     const uint64_t qd = q->qtime > ref ? q->qtime - ref : 0;
@@ -313,7 +313,7 @@ struct HTree {
     return qd;
   }
 
-  __device__ uint64_t delay(uint64_t t, uint64_t p, uint32_t* err)   // computeQueueDelay
+  __device__ __forceinline__ uint64_t delay(uint64_t t, uint64_t p, uint32_t* err)   // computeQueueDelay
   {
     if (q->type == GG_QM_BASIC) return basic_delay(t, p);
     uint64_t qd = ~0ull;
@@ -354,7 +354,7 @@ struct HTree {
     mg1_update(t, p, qd);
     return qd;
   }
-  __device__ void mg1_update(uint64_t t, uint64_t p, uint64_t qd)
+  __device__ __forceinline__ void mg1_update(uint64_t t, uint64_t p, uint64_t qd)
   {
     q->sig_sq += (double)p * (double)p;                          // QueueModelMG1::updateQueue
     q->sig += (double)p;

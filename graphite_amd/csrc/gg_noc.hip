@@ -47,13 +47,13 @@ __device__ __forceinline__ bool ev_lt(const Ev& a, const Ev& b)
 {
   return a.t < b.t || (a.t == b.t && (a.khi < b.khi || (a.khi == b.khi && a.klo < b.klo)));
 }
-__device__ void heap_push(Ev* h, uint32_t& n, Ev e)
+__device__ __forceinline__ void heap_push(Ev* h, uint32_t& n, Ev e)
 {
   uint32_t i = n++;
   while (i > 0) { uint32_t p = (i - 1) / 2; if (!ev_lt(e, h[p])) break; h[i] = h[p]; i = p; }
   h[i] = e;
 }
-__device__ Ev heap_pop(Ev* h, uint32_t& n)
+__device__ __forceinline__ Ev heap_pop(Ev* h, uint32_t& n)
 {
   Ev top = h[0], last = h[--n];
   uint32_t i = 0;
@@ -107,7 +107,7 @@ __device__ __forceinline__ uint32_t ychain_of(const NocParams& P, uint32_t s, ui
 
 // one mesh router hop (RouterModel::processPacket + ElectricalLinkModel::processPacket + Hop)
 // through the output-port queue `tr` of `tile`
-__device__ void mesh_hop_q(const NocDev& D, uint32_t tile, HTree& tr, uint32_t bits, uint64_t& t, uint64_t& zl, uint64_t& ct,
+__device__ __forceinline__ void mesh_hop_q(const NocDev& D, uint32_t tile, HTree& tr, uint32_t bits, uint64_t& t, uint64_t& zl, uint64_t& ct,
                            uint64_t* lc = nullptr)
 {
   // counters: straight to HBM, or to the workgroup's LDS block of this tile (lc, flushed at the end)
@@ -152,23 +152,62 @@ __device__ inline HTree qimg_tree(uint8_t* img, uint32_t ms, bool analytical)
           reinterpret_cast<int16_t*>(img + sizeof(HQueue) + ms * sizeof(HNode)), 1, analytical};
   return t;
 }
-// cooperative copy of queue qi between HBM and its LDS image (all threads of the block)
-__device__ void qimg_copy(const NocDev& D, uint64_t qi, uint8_t* img, bool to_lds)
+static_assert(sizeof(HQueue) % 8 == 0 && sizeof(HNode) % 8 == 0, "8-byte images");
+// Cooperative copy (all threads of the block) between HBM and the LDS images
+// of n queues (image slot s <- queue qid(s)), slots with skip(s) left alone.
+// One flat index space over all images, 8 independent loads in flight per
+// thread before their stores (a per-queue word loop waits one memory round
+// trip per 8-byte word, which dominated the short per-step launches of the
+// coherent hop-by-hop path).
+template <bool TO_LDS, class Qid, class Skip>
+__device__ void qimg_copy_set(const NocDev& D, uint32_t n, Qid qid, Skip skip, uint8_t* base, uint32_t qb)
 {
-  static_assert(sizeof(HQueue) % 8 == 0 && sizeof(HNode) % 8 == 0, "8-byte images");
   const uint32_t ms = D.P.max_size, tid = threadIdx.x, nt = blockDim.x;
-  uint64_t* gq = reinterpret_cast<uint64_t*>(D.q + qi);
-  uint64_t* gn = reinterpret_cast<uint64_t*>(D.nd + qi * ms);
-  int16_t* gf = D.fl + qi * ms;
-  uint64_t* lq = reinterpret_cast<uint64_t*>(img);
-  uint64_t* ln = reinterpret_cast<uint64_t*>(img + sizeof(HQueue));
-  int16_t* lf = reinterpret_cast<int16_t*>(img + sizeof(HQueue) + ms * sizeof(HNode));
   constexpr uint32_t QW = sizeof(HQueue) / 8;
   const uint32_t NW = ms * (uint32_t)(sizeof(HNode) / 8);
-  for (uint32_t i = tid; i < QW + NW + ms; i += nt) {
-    if (i < QW) { if (to_lds) lq[i] = gq[i]; else gq[i] = lq[i]; }
-    else if (i < QW + NW) { const uint32_t j = i - QW; if (to_lds) ln[j] = gn[j]; else gn[j] = ln[j]; }
-    else { const uint32_t j = i - QW - NW; if (to_lds) lf[j] = gf[j]; else gf[j] = lf[j]; }
+  const uint32_t per = QW + NW + ms;               // 8-byte words of queue + nodes, int16 free-list entries
+  const uint32_t total = n * per;
+  constexpr uint32_t U = 8;
+  for (uint32_t i0 = tid; i0 < total; i0 += U * nt) {
+    uint64_t v[U];
+    #pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t i = i0 + u * nt;
+      if (i >= total) break;
+      const uint32_t s = i / per, w = i % per;
+      if (skip(s)) continue;
+      const uint64_t qi = qid(s);
+      uint8_t* img = base + (size_t)s * qb;
+      if (w < QW) v[u] = TO_LDS ? reinterpret_cast<const uint64_t*>(D.q + qi)[w] : reinterpret_cast<uint64_t*>(img)[w];
+      else if (w < QW + NW) {
+        const uint32_t j = w - QW;
+        v[u] = TO_LDS ? reinterpret_cast<const uint64_t*>(D.nd + qi * ms)[j]
+                      : reinterpret_cast<uint64_t*>(img + sizeof(HQueue))[j];
+      } else {
+        const uint32_t j = w - QW - NW;
+        v[u] = (uint16_t)(TO_LDS ? D.fl[qi * ms + j] : reinterpret_cast<int16_t*>(img + sizeof(HQueue) + ms * sizeof(HNode))[j]);
+      }
+    }
+    #pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t i = i0 + u * nt;
+      if (i >= total) break;
+      const uint32_t s = i / per, w = i % per;
+      if (skip(s)) continue;
+      const uint64_t qi = qid(s);
+      uint8_t* img = base + (size_t)s * qb;
+      if (w < QW) {
+        if (TO_LDS) reinterpret_cast<uint64_t*>(img)[w] = v[u]; else reinterpret_cast<uint64_t*>(D.q + qi)[w] = v[u];
+      } else if (w < QW + NW) {
+        const uint32_t j = w - QW;
+        if (TO_LDS) reinterpret_cast<uint64_t*>(img + sizeof(HQueue))[j] = v[u];
+        else reinterpret_cast<uint64_t*>(D.nd + qi * ms)[j] = v[u];
+      } else {
+        const uint32_t j = w - QW - NW;
+        if (TO_LDS) reinterpret_cast<int16_t*>(img + sizeof(HQueue) + ms * sizeof(HNode))[j] = (int16_t)(uint16_t)v[u];
+        else D.fl[qi * ms + j] = (int16_t)(uint16_t)v[u];
+      }
+    }
   }
 }
 
@@ -265,7 +304,7 @@ __global__ void k_self(NocDev D, const uint32_t* __restrict__ dst, const uint32_
 // back at the end.  Used when they fit (kPktLdsBytes per packet), else the
 // walk keeps its heap and packet state in HBM.
 constexpr uint32_t kPortTiles = 16;
-constexpr size_t kStageLdsMax = 160 * 1024;
+constexpr size_t kStageLdsMax = 160 * 1024 - 64;   // leaves room for k_chain_staged's static position range
 constexpr uint32_t kPktLdsBytes = sizeof(Ev) + 5 * 8 + 4 * 4;
 constexpr uint32_t kCtrBytes = GG_NUM_NET_COUNTERS * 8;   // a tile's counter block in LDS
 __device__ void lctr_zero(uint64_t* lc, uint32_t ntiles)
@@ -324,7 +363,11 @@ __global__ __launch_bounds__(64) void k_port_staged(NocDev D, const uint32_t* __
   uint64_t* lcb = reinterpret_cast<uint64_t*>(qlds + nt * qb);
   LPk L(qlds + nt * (qb + kCtrBytes), lp ? np : 0u);
   const int port = SELF ? P_SELF : 5;
-  for (uint32_t i = 0; i < nt; ++i) qimg_copy(D, (uint64_t)(t0 + i) * 6 + port, qlds + i * qb, true);
+  uint32_t empty = 0;                                 // tiles of this workgroup without packets: queues untouched
+  for (uint32_t i = 0; i < nt; ++i) empty |= (bucket_off[t0 + i] == bucket_off[t0 + i + 1]) ? (1u << i) : 0u;
+  auto pq = [&](uint32_t i) { return (uint64_t)(t0 + i) * 6 + port; };
+  auto pskip = [&](uint32_t i) { return ((empty >> i) & 1u) != 0; };
+  qimg_copy_set<true>(D, nt, pq, pskip, qlds, qb);
   if (lp) lpk_load(L, B, np, bucket_ids, S, dst, len);
   if (lp) lctr_zero(lcb, nt);
   __syncthreads();
@@ -390,7 +433,7 @@ __global__ __launch_bounds__(64) void k_port_staged(NocDev D, const uint32_t* __
   __syncthreads();
   if (lp) lpk_store(L, np, S);
   if (lp) lctr_flush(D, lcb, nt, [&](uint32_t i) { return t0 + i; });
-  for (uint32_t i = 0; i < nt; ++i) qimg_copy(D, (uint64_t)(t0 + i) * 6 + port, qlds + i * qb, false);
+  qimg_copy_set<false>(D, nt, pq, pskip, qlds, qb);
 }
 
 // Staged stages X / Y: one workgroup per chain (row or column, direction),
@@ -412,9 +455,29 @@ __global__ __launch_bounds__(64) void k_chain_staged(NocDev D, int stage, const 
   LPk L(qlds + Lq * (qb + kCtrBytes), lp ? np : 0u);
   const int port = stage == 0 ? (dir ? P_RIGHT : P_LEFT) : (dir ? P_UP : P_DOWN);   // xchain_of / ychain_of
   auto tile_at = [&](uint32_t i) -> uint32_t { return stage == 0 ? line * P.w + i : i * P.w + line; };
-  for (uint32_t i = 0; i < Lq; ++i) qimg_copy(D, (uint64_t)tile_at(i) * 6 + port, qlds + i * qb, true);
+  // only the ports between a packet's current and destination position can be
+  // visited: stage the chain's queues in that position range
+  __shared__ uint32_t s_lo, s_hi;
+  if (threadIdx.x == 0) { s_lo = ~0u; s_hi = 0; }
   if (lp) lpk_load(L, b, np, bucket_ids, S, dst, len);
   if (lp) lctr_zero(lcb, Lq);
+  __syncthreads();
+  {
+    auto pos_of = [&](uint32_t tile) { return stage == 0 ? tile % P.w : tile / P.w; };
+    uint32_t lo = ~0u, hi = 0;
+    for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) {
+      const uint32_t cur = lp ? L.cur[i] : S.cur[bucket_ids[b + i]];
+      const uint32_t d = lp ? L.dst[i] : dst[bucket_ids[b + i]];
+      const uint32_t a = pos_of(cur), z = pos_of(d);
+      lo = min(lo, min(a, z)); hi = max(hi, max(a, z));
+    }
+    if (lo <= hi) { atomicMin(&s_lo, lo); atomicMax(&s_hi, hi); }
+  }
+  __syncthreads();
+  const uint32_t plo = s_lo, phi = s_hi;
+  auto cq = [&](uint32_t i) { return (uint64_t)tile_at(i) * 6 + port; };
+  auto cskip = [&](uint32_t i) { return i < plo || i > phi; };
+  qimg_copy_set<true>(D, Lq, cq, cskip, qlds, qb);
   __syncthreads();
   if (threadIdx.x == 0) {
     // one hop of packet (cur, d) along the chain; returns whether it left the chain
@@ -456,7 +519,7 @@ __global__ __launch_bounds__(64) void k_chain_staged(NocDev D, int stage, const 
   __syncthreads();
   if (lp) lpk_store(L, np, S);
   if (lp) lctr_flush(D, lcb, Lq, tile_at);
-  for (uint32_t i = 0; i < Lq; ++i) qimg_copy(D, (uint64_t)tile_at(i) * 6 + port, qlds + i * qb, false);
+  qimg_copy_set<false>(D, Lq, cq, cskip, qlds, qb);
 }
 
 // bucket keys: 0 = injection (src tile), 1 = X chain, 2 = Y chain, 3 = SELF (dst tile); ~0 = not in stage
