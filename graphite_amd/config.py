@@ -49,7 +49,8 @@ NET_COUNTERS = ["packets_sent", "flits_sent", "bits_sent", "packets_received",
                 "flits_received", "bits_received", "total_latency_ps",
                 "total_contention_ps", "buffer_writes", "buffer_reads",
                 "switch_alloc", "crossbar", "link_traversals",
-                "router_contention_cycles", "router_packets", "analytical_requests"]
+                "router_contention_cycles", "router_packets", "analytical_requests"] + \
+               ["port%d_utilized_cycles" % p for p in range(5)] + ["port%d_last_cycles" % p for p in range(5)]
 NUM_CACHE_COUNTERS = len(CACHE_COUNTERS)
 
 # coherent mode (include/graphite_gpu.h)

@@ -601,6 +601,10 @@ __global__ void k_analytical(const HQueue* q, uint32_t tiles, uint64_t* ctr)
   uint64_t a = 0;
   for (int p = 0; p < NPORTS; ++p) a += q[(uint64_t)tile * 6 + p].analytical;
   ctr[(uint64_t)tile * GG_NUM_NET_COUNTERS + GG_NC_ANALYTICAL_REQUESTS] = a;
+  for (int p = 0; p < NPORTS; ++p) {
+    ctr[(uint64_t)tile * GG_NUM_NET_COUNTERS + GG_NC_PORT_UTILIZED_CYCLES + p] = q[(uint64_t)tile * 6 + p].util;
+    ctr[(uint64_t)tile * GG_NUM_NET_COUNTERS + GG_NC_PORT_LAST_CYCLES + p] = q[(uint64_t)tile * 6 + p].last_req;
+  }
 }
 
 }  // namespace

@@ -60,6 +60,10 @@ int main(int argc, char** argv)
       const uint64_t z[GG_NUM_NET_COUNTERS] = {0};
       writeNetworkSummary(std::cout, nc, 1.0, GG_NET_EMESH_HOP_COUNTER);
       writeNetworkSummary(std::cout, nc, 2.5, GG_NET_EMESH_HOP_BY_HOP);
+      nc[GG_NC_ROUTER_CONTENTION_CYCLES] = 913; nc[GG_NC_ROUTER_PACKETS] = 280; nc[GG_NC_ANALYTICAL_REQUESTS] = 3;
+      const uint64_t util[5] = {120, 0, 450, 77, 1000}, last[5] = {9000, 0, 12345, 8000, 40001};
+      for (int p = 0; p < 5; ++p) { nc[GG_NC_PORT_UTILIZED_CYCLES + p] = util[p]; nc[GG_NC_PORT_LAST_CYCLES + p] = last[p]; }
+      writeNetworkSummary(std::cout, nc, 1.0, GG_NET_EMESH_HOP_BY_HOP, true);
       writeNetworkSummary(std::cout, z, 1.0, GG_NET_MAGIC);
       return 0;
     } else if (a == "--mem-summary-selftest") {

@@ -144,7 +144,8 @@ inline void writeCacheSummary(std::ostream& out, const std::string& name, const 
 // float, printed with the default ostream format.  No broadcasts are modeled
 // (full_map never broadcasts), so the broadcast lines read 0.  The
 // asynchronous-communication block is empty in a single DVFS domain.
-inline void writeNetworkSummary(std::ostream& out, const uint64_t* nc, double frequency_ghz, uint32_t net_model)
+inline void writeNetworkSummary(std::ostream& out, const uint64_t* nc, double frequency_ghz, uint32_t net_model,
+                                bool contention_model_enabled = false)
 {
   auto to_cycles = [&](uint64_t ps) { return (uint64_t)ceil(((double)ps * frequency_ghz) / double(1.0e3)); };
   auto to_ns = [](uint64_t ps) { return (uint64_t)ceil(((double)ps) / double(1.0e3)); };
@@ -177,6 +178,35 @@ inline void writeNetworkSummary(std::ostream& out, const uint64_t* nc, double fr
     out << "      Switch Allocator Traversals: " << nc[GG_NC_SWITCH_ALLOC] << std::endl;
     out << "      Crossbar Traversals: " << nc[GG_NC_CROSSBAR] << std::endl;
     out << "      Link Traversals: " << nc[GG_NC_LINK_TRAVERSALS] << std::endl;
+  }
+  if (net_model == GG_NET_EMESH_HOP_BY_HOP) {
+    // outputEventCountSummary (network_model_emesh_hop_by_hop.cc:436-462): unicast
+    // only (full_map never broadcasts), so every crossbar traversal is Crossbar[1]
+    out << "    Event Counters:" << std::endl;
+    out << "      Buffer Writes: " << nc[GG_NC_BUFFER_WRITES] << std::endl;
+    out << "      Buffer Reads: " << nc[GG_NC_BUFFER_READS] << std::endl;
+    out << "      Switch Allocator Requests: " << nc[GG_NC_SWITCH_ALLOC] << std::endl;
+    for (int i = 1; i <= 5; ++i)
+      out << "      Crossbar[" << i << "] Traversals: " << (i == 1 ? nc[GG_NC_CROSSBAR] : 0) << std::endl;
+    out << "      Link Traversals: " << nc[GG_NC_LINK_TRAVERSALS] << std::endl;
+    if (contention_model_enabled) {
+      // outputContentionModelsSummary (:464-486) over mesh ports 0..4 with
+      // RouterModel::getAverageContentionDelay / getAverageLinkUtilization /
+      // getPercentAnalyticalModelsUsed (router_model.cc:145-215), all float
+      const uint64_t pk = nc[GG_NC_ROUTER_PACKETS];
+      const float avg_delay = pk > 0 ? ((float)nc[GG_NC_ROUTER_CONTENTION_CYCLES]) / pk : 0.0f;
+      float util = 0.0f;
+      for (int p = 0; p < 5; ++p) {
+        const uint64_t last = nc[GG_NC_PORT_LAST_CYCLES + p];
+        util += last > 0 ? ((float)nc[GG_NC_PORT_UTILIZED_CYCLES + p]) / last : 0.0f;   // QueueModel::getQueueUtilization
+      }
+      util = util / 5;
+      const float an = pk > 0 ? ((float)nc[GG_NC_ANALYTICAL_REQUESTS] * 100) / pk : 0.0f;
+      out << "    Contention Counters:" << std::endl;
+      out << "      Average EMesh Router Contention Delay: " << avg_delay << std::endl;
+      out << "      Average EMesh Router Link Utilization: " << util << std::endl;
+      out << "      Analytical Models Used (%): " << an << std::endl;
+    }
   }
 }
 

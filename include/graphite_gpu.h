@@ -118,7 +118,12 @@ enum {
   GG_NC_BUFFER_WRITES, GG_NC_BUFFER_READS, GG_NC_SWITCH_ALLOC, GG_NC_CROSSBAR,
   GG_NC_LINK_TRAVERSALS,
   GG_NC_ROUTER_CONTENTION_CYCLES, GG_NC_ROUTER_PACKETS, GG_NC_ANALYTICAL_REQUESTS,
-  GG_NUM_NET_COUNTERS
+  /* emesh_hop_by_hop with contention: QueueModel utilization counters of the 5
+   * mesh output-port queues (queue_model.cc:49-55), + port (SELF, LEFT, RIGHT,
+   * DOWN, UP), for RouterModel::getAverageLinkUtilization (router_model.cc:168-182) */
+  GG_NC_PORT_UTILIZED_CYCLES,
+  GG_NC_PORT_LAST_CYCLES = GG_NC_PORT_UTILIZED_CYCLES + 5,
+  GG_NUM_NET_COUNTERS = GG_NC_PORT_LAST_CYCLES + 5
 };
 
 /* Queue model types (the type strings of QueueModel::create) and the

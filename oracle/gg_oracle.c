@@ -932,6 +932,10 @@ void oracle_noc_counters(const oracle_noc* on, uint64_t* out)
       uint64_t a = 0;
       for (int p = 0; p < NPORTS; ++p) a += on->q[(size_t)i * NPORTS + p]->analytical_requests;
       out[(size_t)i * GG_NUM_NET_COUNTERS + GG_NC_ANALYTICAL_REQUESTS] = a;
+      for (int p = 0; p < 5; ++p) {                /* mesh output ports: queue_model.cc:49-55 */
+        out[(size_t)i * GG_NUM_NET_COUNTERS + GG_NC_PORT_UTILIZED_CYCLES + p] = on->q[(size_t)i * NPORTS + p]->util_cycles;
+        out[(size_t)i * GG_NUM_NET_COUNTERS + GG_NC_PORT_LAST_CYCLES + p] = on->q[(size_t)i * NPORTS + p]->last_req;
+      }
     }
   }
 }

@@ -87,7 +87,7 @@ def test_trace_replayer_matches_oracle():
         np.testing.assert_array_equal(got[t], ref[t])
 
 
-def reference_net_summary(nc, f, hop_counter):
+def reference_net_summary(nc, f, hop_counter, hop_by_hop=False, contention=False):
     """NetworkModel::outputSummary (network_model.cc:274-316) + the hop counter's
     event counters (network_model_emesh_hop_counter.cc:226-236), restated;
     averages are float32 printed like %g."""
@@ -114,6 +114,22 @@ def reference_net_summary(nc, f, hop_counter):
         L += ["    Event Counters:", "      Buffer Writes: %d" % nc["bw"], "      Buffer Reads: %d" % nc["brd"],
               "      Switch Allocator Traversals: %d" % nc["sa"], "      Crossbar Traversals: %d" % nc["xb"],
               "      Link Traversals: %d" % nc["lt"]]
+    if hop_by_hop:   # outputEventCountSummary / outputContentionModelsSummary (hop_by_hop.cc:436-486)
+        L += ["    Event Counters:", "      Buffer Writes: %d" % nc["bw"], "      Buffer Reads: %d" % nc["brd"],
+              "      Switch Allocator Requests: %d" % nc["sa"]] + \
+             ["      Crossbar[%d] Traversals: %d" % (i, nc["xb"] if i == 1 else 0) for i in range(1, 6)] + \
+             ["      Link Traversals: %d" % nc["lt"]]
+        if contention:   # RouterModel averages over ports 0..4 (router_model.cc:145-215), float
+            f32 = np.float32
+            pk = nc["rpk"]
+            d = f32(f32(nc["rcc"]) / f32(pk)) if pk else f32(0)
+            u = f32(0)
+            for a, b in zip(nc["util"], nc["last"]):
+                u = f32(u + (f32(f32(a) / f32(b)) if b else f32(0)))
+            u = f32(u / f32(5))
+            an = f32(f32(f32(nc["an"]) * f32(100)) / f32(pk)) if pk else f32(0)
+            L += ["    Contention Counters:", "      Average EMesh Router Contention Delay: %g" % d,
+                  "      Average EMesh Router Link Utilization: %g" % u, "      Analytical Models Used (%%): %g" % an]
     return L
 
 
@@ -124,7 +140,9 @@ def test_network_summary_format_matches_reference():
     nc = dict(ps=70, fs=430, bs=24530, pr=66, fr=400, br=23000, lat=1234567, con=45001,
               bw=1720, brd=1720, sa=280, xb=1720, lt=1720)
     z = {k: 0 for k in nc}
-    exp = reference_net_summary(nc, 1.0, True) + reference_net_summary(nc, 2.5, False) + \
+    nc2 = dict(nc, rcc=913, rpk=280, an=3, util=[120, 0, 450, 77, 1000], last=[9000, 0, 12345, 8000, 40001])
+    exp = reference_net_summary(nc, 1.0, True) + reference_net_summary(nc, 2.5, False, hop_by_hop=True) + \
+        reference_net_summary(nc2, 1.0, False, hop_by_hop=True, contention=True) + \
         reference_net_summary(z, 1.0, False)
     assert out.splitlines() == exp
 
