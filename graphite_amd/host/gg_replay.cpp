@@ -6,6 +6,11 @@
 //       synthetic configs[1] trace, generated on the host
 //   gg_replay --tiles T --trace FILE [--batches B]
 //       FILE: little-endian records {u32 tile, u32 meta, u64 byte address}
+//   gg_replay --coherent --tiles T --per-tile N [--hot-lines H] [--net hop_counter|hop_by_hop|magic]
+//       coherent mode (MSI directory + DRAM + NoC, gg_coherent_run) on the
+//       configs[2..4] hotspot trace generated on the device; prints every
+//       tile's memory block (MemoryManager::outputSummary) and memory-network
+//       block (Network::outputSummary, network.cc:79-89, the Memory network)
 //   gg_replay --summary-selftest
 //       prints writeCacheSummary() for fixed counters (no GPU needed)
 #include <cstdio>
@@ -30,7 +35,8 @@ static uint64_t splitmix_at(uint64_t seed, uint64_t i)
 
 int main(int argc, char** argv)
 {
-  uint32_t tiles = 4, lines_log2 = 15, batches = 1, l2_assoc = 8;
+  uint32_t tiles = 4, lines_log2 = 15, batches = 1, l2_assoc = 8, hot_lines = 64, net = GG_NET_EMESH_HOP_COUNTER;
+  bool coherent = false;
   uint64_t per_tile = 100000;
   std::string trace;
   for (int i = 1; i < argc; ++i) {
@@ -42,6 +48,15 @@ int main(int argc, char** argv)
     else if (a == "--batches") batches = (uint32_t)std::strtoul(next(), nullptr, 0);
     else if (a == "--l2-assoc") l2_assoc = (uint32_t)std::strtoul(next(), nullptr, 0);
     else if (a == "--trace") trace = next();
+    else if (a == "--coherent") coherent = true;
+    else if (a == "--hot-lines") hot_lines = (uint32_t)std::strtoul(next(), nullptr, 0);
+    else if (a == "--net") {
+      const std::string n = next();
+      if (n == "hop_counter") net = GG_NET_EMESH_HOP_COUNTER;
+      else if (n == "hop_by_hop") net = GG_NET_EMESH_HOP_BY_HOP;
+      else if (n == "magic") net = GG_NET_MAGIC;
+      else { std::fprintf(stderr, "unknown network %s\n", n.c_str()); return 2; }
+    }
     else if (a == "--summary-selftest") {
       const uint64_t c1[GG_NUM_CACHE_COUNTERS] = {1000, 250, 700, 150, 300, 100, 240, 0, 2600, 900, 760, 1250};
       const uint64_t c2[GG_NUM_CACHE_COUNTERS] = {250, 180, 150, 110, 100, 70, 120, 45, 700, 600, 190, 480};
@@ -88,6 +103,41 @@ int main(int argc, char** argv)
       writeDramSummary(std::cout, st, true, GG_QM_BASIC);
       return 0;
     } else { std::fprintf(stderr, "unknown option %s\n", a.c_str()); return 2; }
+  }
+  if (coherent) {
+    try {
+      gg_config cfg;
+      gg_config_default(&cfg, tiles);
+      cfg.l2_assoc = l2_assoc;
+      cfg.net_model = net;
+      Backend be(cfg);
+      const uint64_t n = (uint64_t)tiles * per_tile;
+      DeviceBuffer<uint64_t> addr;
+      DeviceBuffer<uint32_t> meta;
+      addr.resize(n); meta.resize(n);
+      check(gg_gen_hotspot_trace(addr.p, meta.p, 0, tiles, per_tile, 0, lines_log2, 26, hot_lines, 51, nullptr),
+            "gg_gen_hotspot_trace");
+      std::vector<uint64_t> offs(tiles + 1);
+      for (uint32_t t = 0; t <= tiles; ++t) offs[t] = (uint64_t)t * per_tile;
+      gg_trace tr{addr.p, meta.p, offs.data(), n};
+      check(gg_coherent_run(be.ctx(), &tr, nullptr, nullptr), "gg_coherent_run");
+      std::vector<uint64_t> st((size_t)tiles * GG_NUM_TILE_STATS), cc((size_t)tiles * 2 * GG_NUM_CACHE_COUNTERS),
+          nc((size_t)tiles * GG_NUM_NET_COUNTERS);
+      check(gg_coherent_get_stats(be.ctx(), st.data(), cc.data(), nullptr), "gg_coherent_get_stats");
+      check(gg_noc_get_counters(be.ctx(), nc.data()), "gg_noc_get_counters");
+      for (uint32_t t = 0; t < tiles; ++t) {
+        std::cout << "Tile " << t << " Summary:" << std::endl;
+        writeMemorySummary(std::cout, cfg, &st[(size_t)t * GG_NUM_TILE_STATS],
+                           &cc[(size_t)t * 2 * GG_NUM_CACHE_COUNTERS]);
+        std::cout << "Network Summary: " << std::endl << "  Network (Memory): " << std::endl;
+        writeNetworkSummary(std::cout, &nc[(size_t)t * GG_NUM_NET_COUNTERS], cfg.frequency_ghz, cfg.net_model,
+                            cfg.queue_model_enabled != 0);
+      }
+    } catch (const Error& e) {
+      std::fprintf(stderr, "gg_replay: %s\n", e.what());
+      return 1;
+    }
+    return 0;
   }
   try {
     gg_config cfg;

@@ -1,0 +1,70 @@
+"""GPU: the host mirror's sim.out writers on a real coherent run.  gg_replay
+--coherent runs the MSI coherent mode through the C ABI (gg_coherent_run) and
+prints every tile's memory block (MemoryManager::outputSummary,
+msi/memory_manager.cc:415-430) and memory-network block (Network::outputSummary,
+network.cc:79-89); the expected text is the reference's format restated in
+tests/test_host_mirror.py, filled with the C oracle's statistics of the same
+seeded trace."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from graphite_amd import config as C
+from tests.test_host_mirror import (REPLAY, reference_summary, reference_dram_summary,
+                                    reference_directory_summary, reference_net_summary)
+
+pytestmark = pytest.mark.gpu
+
+
+def _expected(T, N, net, hop_by_hop):
+    from oracle import pyoracle as po
+    cfg = C.default_config(T, net_model=net)
+    a, m, o = po.gen_trace(T, N, hot_lines=64)
+    oc = po.OracleCoherent(cfg)
+    oc.run(a, m, o)
+    st, cc, nc = oc.tile_stats(), oc.cache_counters(), oc.net_counters()
+    S = {n: i for i, n in enumerate(C.TILE_STATS)}
+    K = {n: i for i, n in enumerate(C.NET_COUNTERS)}
+    # DirectoryCache auto sizing (SURVEY.md §8 derived constants): 16 tiles -> 16384 entries, 32 KB, 2 cycles
+    auto = {16: (16384, 32, 2), 64: (16384, 128, 6)}[T]
+    L = []
+    for t in range(T):
+        s = st[t]
+        d = dict(dacc=s[S["dir_accesses"]], dev=s[S["dir_evictions"]], dbi=s[S["dir_back_invalidations"]],
+                 dram=s[S["dram_accesses"]], lat=s[S["dram_latency_ns"]], qd=s[S["dram_queue_delay_ns"]],
+                 qreq=s[S["dram_queue_requests"]], an=s[S["dram_queue_analytical"]],
+                 util=s[S["dram_queue_utilized_ns"]], last=s[S["dram_queue_last_ns"]])
+        d = {k: int(v) for k, v in d.items()}
+        n = nc[t]
+        g = lambda k: int(n[K[k]])
+        nd = dict(ps=g("packets_sent"), fs=g("flits_sent"), bs=g("bits_sent"), pr=g("packets_received"),
+                  fr=g("flits_received"), br=g("bits_received"), lat=g("total_latency_ps"),
+                  con=g("total_contention_ps"), bw=g("buffer_writes"), brd=g("buffer_reads"), sa=g("switch_alloc"),
+                  xb=g("crossbar"), lt=g("link_traversals"), rcc=g("router_contention_cycles"),
+                  rpk=g("router_packets"), an=g("analytical_requests"),
+                  util=[g("port%d_utilized_cycles" % p) for p in range(5)],
+                  last=[g("port%d_last_cycles" % p) for p in range(5)])
+        L += ["Tile %d Summary:" % t, "Cache Summary:"]
+        L += reference_summary("L1-D", [int(x) for x in cc[t, 0]], False)
+        L += reference_summary("L2", [int(x) for x in cc[t, 1]], True)
+        L += reference_dram_summary(d, True) + reference_directory_summary(d, auto)
+        L += ["Network Summary: ", "  Network (Memory): "]
+        L += reference_net_summary(nd, cfg.frequency_ghz, net == C.NET_EMESH_HOP_COUNTER,
+                                   hop_by_hop=hop_by_hop, contention=hop_by_hop and bool(cfg.queue_model_enabled))
+    return L
+
+
+@pytest.mark.parametrize("T,N,net", [(16, 400, "hop_by_hop"), (16, 600, "hop_counter"), (64, 150, "hop_by_hop")])
+def test_coherent_sim_out_matches_oracle(T, N, net):
+    if not os.path.exists(REPLAY):
+        pytest.skip("gg_replay not built")
+    out = subprocess.run([REPLAY, "--coherent", "--tiles", str(T), "--per-tile", str(N), "--hot-lines", "64",
+                          "--net", net], capture_output=True, text=True, check=True, timeout=120).stdout
+    netid = C.NET_EMESH_HOP_BY_HOP if net == "hop_by_hop" else C.NET_EMESH_HOP_COUNTER
+    exp = _expected(T, N, netid, net == "hop_by_hop")
+    got = out.splitlines()
+    assert len(got) == len(exp)
+    for i, (x, y) in enumerate(zip(got, exp)):
+        assert x == y, "line %d: %r != %r" % (i, x, y)
