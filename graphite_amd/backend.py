@@ -13,6 +13,8 @@ import numpy as np
 from .config import (GGConfig, NUM_CACHE_COUNTERS, NUM_NET_COUNTERS, NUM_TILE_STATS, NUM_RUN_INFO,
                      CMSG_DTYPE)
 
+CMSG_BYTES = CMSG_DTYPE.itemsize
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 # GG_LIB (diagnostics only): load an alternative in-tree build for A/B kernel runs
 LIB_PATH = os.environ.get("GG_LIB") or os.path.join(HERE, "libgraphite_gpu.so")
@@ -54,7 +56,7 @@ EXPORTS = ["gg_abi_version", "gg_last_error", "gg_config_default", "gg_create", 
            "gg_noc_route_batch", "gg_noc_get_counters", "gg_queue_delay_batch",
            "gg_gen_uniform_trace", "gg_kernel_time_ms", "gg_set_timing",
            "gg_coherent_begin", "gg_coherent_quantum", "gg_coherent_export", "gg_coherent_import",
-           "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace"]
+           "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace", "gg_shard_map"]
 
 
 class _CStatus(ctypes.Structure):
@@ -102,8 +104,9 @@ def load():
     L.gg_coherent_run.argtypes = [vp, ctypes.POINTER(_Trace), vp, vp]
     L.gg_coherent_get_stats.argtypes = [vp, vp, vp, vp]
     L.gg_gen_hotspot_trace.argtypes = [vp, vp, u32, u32, u64, u64, u32, u32, u32, u32, vp]
-    for name in ["gg_coherent_begin", "gg_coherent_quantum", "gg_coherent_export", "gg_coherent_import",
-                 "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace"]:
+    L.gg_shard_map.argtypes = [u32, u32, vp]
+    for name in ["gg_shard_map", "gg_coherent_begin", "gg_coherent_quantum", "gg_coherent_export", "gg_coherent_import",
+                 "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace", "gg_shard_map"]:
         getattr(L, name).restype = i32
     for name in ["gg_reset", "gg_cache_access_batch", "gg_cache_get_counters", "gg_cache_get_line_info",
                  "gg_cache_set_line_info", "gg_cache_access_line", "gg_cache_insert_line",
@@ -260,7 +263,7 @@ class Backend:
                 "active_tiles": st.active_tiles, "blocked_tiles": st.blocked_tiles}
 
     def coherent_export(self, out_buf, cap):
-        """Held cross-shard messages -> out_buf (uint8 device tensor of cap*48
+        """Held cross-shard records -> out_buf (uint8 device tensor of cap*CMSG_BYTES
         bytes), grouped by destination shard; returns per-shard counts."""
         K = self.cfg.num_shards or 1
         counts = np.zeros(K, np.uint64)
@@ -289,6 +292,13 @@ class Backend:
         return d
 
 
+def shard_map(num_tiles, num_shards):
+    """tile -> logical shard through the ABI (gg_shard_map)."""
+    out = np.zeros(num_tiles, np.uint32)
+    _check(load().gg_shard_map(num_tiles, num_shards, out.ctypes.data_as(ctypes.c_void_p)))
+    return out
+
+
 def gen_uniform_trace(addr, meta, tile_begin, tiles, per_tile, first=0, lines_log2=15, base_shift=26, stream=None):
     """Fill device tensors with the configs[1] synthetic trace."""
     _check(load().gg_gen_uniform_trace(_ptr(addr), _ptr(meta), tile_begin, tiles, per_tile, first,
@@ -312,7 +322,7 @@ class CoherentEngine:
         self.dev = addr.device
         backend.coherent_begin(addr, meta, tile_offsets, out)
         self.cap = 64 * backend.cfg.num_tiles + 65536
-        self.buf = torch.empty(self.cap * 48, dtype=torch.uint8, device=self.dev)
+        self.buf = torch.empty(self.cap * CMSG_BYTES, dtype=torch.uint8, device=self.dev)
 
     def quantum(self, q):
         return self.be.coherent_quantum(q)
@@ -320,9 +330,9 @@ class CoherentEngine:
     def export(self):
         counts = self.be.coherent_export(self.buf, self.cap)
         n = int(counts.sum())
-        return self.buf[:n * 48], counts
+        return self.buf[:n * CMSG_BYTES], counts
 
     def import_(self, buf):
-        n = buf.numel() // 48
+        n = buf.numel() // CMSG_BYTES
         if n:
             self.be.coherent_import(buf.contiguous(), n)

@@ -6,22 +6,24 @@ over its TCP transport in real time (common/transport/socktransport.cc) and
 synchronise clocks at a lax barrier every quantum
 (common/system/clock_skew_management_schemes/lax_barrier_sync_client.cc:31-69,
 lax_barrier_sync_server.cc:57-160).  Here the tiles are split into logical
-shards (contiguous tile ranges, a fixed part of the configuration); messages
-that stay inside a shard are delivered step by step on the device, messages
-that cross shards are held until the quantum boundary and exchanged there with
-one all-to-all (RCCL over xGMI on GPUs, gloo on CPU).  The schedule — and so
+shards (the reference's 2-D process blocks of the mesh, config.shard_map, a
+fixed part of the configuration); messages that stay inside a shard are
+delivered step by step on the device, records that cross shards (messages, and
+emesh_hop_by_hop packets at the edge of a shard's routers) are held until the
+quantum boundary and exchanged there with one all-to-all (RCCL over xGMI on
+GPUs, gloo on CPU).  The schedule — and so
 every statistic — depends on the shard count, never on how many ranks hold the
 shards.
 
 `engine` is anything with the gg_coherent_* surface (graphite_amd.backend's
 CoherentRun on a GPU; the oracle in the CPU tests):
   quantum(q) -> {"boundary_msgs", "min_next_ps", "active_tiles", "blocked_tiles", ...}
-  export()   -> (uint8 tensor [n*48] on the engine's device, per-shard counts [num_shards])
-  import_(uint8 tensor [m*48])
+  export()   -> (uint8 tensor [n*64] on the engine's device, per-shard counts [num_shards])
+  import_(uint8 tensor [m*64])
 """
 import numpy as np
 
-CMSG_BYTES = 48
+CMSG_BYTES = 64
 NO_TIME = (1 << 64) - 1
 
 

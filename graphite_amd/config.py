@@ -159,14 +159,58 @@ def shmem_modeled_bits(num_tiles, with_data):
 
 def _cmsg_dtype():
     import numpy as np
-    return np.dtype([("addr", "<u8"), ("send_ps", "<u8"), ("arrival_ps", "<u8"), ("src", "<u4"),
-                     ("dst", "<u4"), ("requester", "<u4"), ("seq", "<u4"), ("type", "<u4"),
-                     ("link", "<u4")])
+    return np.dtype([("addr", "<u8"), ("send_ps", "<u8"), ("arrival_ps", "<u8"), ("zero_load_ps", "<u8"),
+                     ("src", "<u4"), ("dst", "<u4"), ("requester", "<u4"), ("seq", "<u4"), ("type", "<u4"),
+                     ("link", "<u4"), ("hop", "<u4"), ("pad", "<u4")])
 
 
 CMSG_DTYPE = _cmsg_dtype()
 
 
+HOP_NONE = 0xFFFFFFFF
+
+
+def shard_map(num_tiles, num_shards):
+    """Logical shard of every tile: on a full W x H mesh
+    the 2-D block the reference gives process k of num_shards under
+    emesh_hop_by_hop (NetworkModelEMeshHopByHop::computeProcessToTileMapping,
+    network_model_emesh_hop_by_hop.cc:367-433); contiguous tile ranges
+    otherwise.  Same rule as the ABI's gg_shard_map."""
+    import numpy as np
+    T, K = int(num_tiles), int(num_shards or 1)
+    if K < 1 or K > T:
+        raise ValueError("num_shards must be in [1, num_tiles]")
+    W = int(math.floor(math.sqrt(T)))
+    H = int(math.ceil(T / W))
+    if W * H != T:
+        return (np.arange(T, dtype=np.int64) * K // T).astype(np.uint32)
+    out = np.full(T, 0xFFFFFFFF, np.uint32)
+    pw = int(math.floor(math.sqrt(K)))
+    ph = int(math.floor(K / pw))
+    mhl = int((1.0 * H * pw * ph) / K)
+    for i in range(pw):
+        for j in range(ph):
+            sx, sy = W // pw, mhl // ph
+            bx, by = i * sx, j * sy
+            if i == pw - 1:
+                sx = W - (pw - 1) * sx
+            if j == ph - 1:
+                sy = mhl - (ph - 1) * sy
+            for jj in range(sy):
+                out[(by + jj) * W + bx:(by + jj) * W + bx + sx] = i + j * pw
+    left = K - pw * ph
+    for i in range(pw * ph, K):
+        sx = W // left
+        sy, bx, by = H - mhl, (i - pw * ph) * sx, mhl
+        if i == K - 1:
+            sx = W - (left - 1) * sx
+        for jj in range(sy):
+            out[(by + jj) * W + bx:(by + jj) * W + bx + sx] = i
+    if (out >= K).any() or len(np.unique(out)) != K:
+        raise ValueError("no shard map for %d tiles in %d shards" % (T, K))
+    return out
+
+
 def shard_of_tile(tile, num_tiles, num_shards):
-    """Logical shard of a tile: contiguous tile ranges."""
-    return (tile * num_shards) // num_tiles
+    """Logical shard of a tile (shard_map)."""
+    return int(shard_map(num_tiles, num_shards)[tile])

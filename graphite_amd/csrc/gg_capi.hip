@@ -288,8 +288,59 @@ gg_status gg_queue_delay_batch(gg_ctx* ctx, uint64_t min_processing_time, const 
                                const uint64_t* proc_time, uint64_t n, uint64_t* delay_out)
 {
   if (!ctx || (n && (!pkt_time || !proc_time || !delay_out))) return gg_fail(GG_ERR_INVALID, "NULL argument");
+  // every reference queue has min_processing_time >= 1 and processing times
+  // >= 1 (router_model.cc:23-27, dram_perf_model.cc:48,92): the interval
+  // representation of gg_dev.h relies on it
+  if (min_processing_time == 0) return gg_fail(GG_ERR_UNSUPPORTED, "min_processing_time 0");
   hipSetDevice(ctx->device);
-  return gg_htree_run(ctx, min_processing_time, pkt_time, proc_time, n, delay_out);
+  GG_HIP(hipMemset(ctx->err_dev, 0, sizeof(uint32_t)));
+  if (gg_status st = gg_htree_run(ctx, min_processing_time, pkt_time, proc_time, n, delay_out)) return st;
+  uint32_t e = 0;
+  GG_HIP(hipMemcpy(&e, ctx->err_dev, sizeof(e), hipMemcpyDeviceToHost));
+  if (e & GG_DERR_RANGE) return gg_fail(GG_ERR_UNSUPPORTED, "processing time 0");
+  return check_device_errors(ctx);
+}
+
+gg_status gg_shard_map(uint32_t num_tiles, uint32_t num_shards, uint32_t* tile_shard)
+{
+  if (!tile_shard) return gg_fail(GG_ERR_INVALID, "NULL argument");
+  if (num_shards == 0 || num_shards > num_tiles) return gg_fail(GG_ERR_INVALID, "num_shards %u for %u tiles", num_shards, num_tiles);
+  const int T = (int)num_tiles, K = (int)num_shards;
+  const int W = (int)floor(sqrt((double)T)), H = (int)ceil(1.0 * T / W);
+  if (W * H != T) {                                   // not a mesh: contiguous tile ranges
+    for (int t = 0; t < T; ++t) tile_shard[t] = (uint32_t)(((uint64_t)t * K) / T);
+    return GG_OK;
+  }
+  // NetworkModelEMeshHopByHop::computeProcessToTileMapping (hop_by_hop.cc:367-433):
+  // a pw x ph grid of blocks over the first mesh_height_l rows, the remaining
+  // processes side by side in the rows below
+  std::vector<uint32_t> m((size_t)T, ~0u);
+  const int pw = (int)floor(sqrt((double)K)), ph = (int)floor(1.0 * K / pw);
+  const int hl = (int)((1.0 * H * pw * ph) / K);
+  auto fill = [&](int bx, int by, int sx, int sy, uint32_t k) {
+    for (int y = by; y < by + sy; ++y)
+      for (int x = bx; x < bx + sx; ++x) m[(size_t)y * W + x] = k;
+  };
+  for (int i = 0; i < pw; ++i)
+    for (int j = 0; j < ph; ++j) {
+      const int bsx = W / pw, bsy = hl / ph;
+      fill(i * bsx, j * bsy, i == pw - 1 ? W - (pw - 1) * bsx : bsx, j == ph - 1 ? hl - (ph - 1) * bsy : bsy,
+           (uint32_t)(i + j * pw));
+    }
+  const int left = K - pw * ph;
+  for (int i = pw * ph; i < K; ++i) {
+    const int bsx = W / left;
+    fill((i - pw * ph) * bsx, hl, i == K - 1 ? W - (left - 1) * bsx : bsx, H - hl, (uint32_t)i);
+  }
+  std::vector<char> seen((size_t)K, 0);
+  for (int t = 0; t < T; ++t) {
+    if (m[t] >= (uint32_t)K) return gg_fail(GG_ERR_INVALID, "no shard map for %u tiles in %u shards", num_tiles, num_shards);
+    seen[m[t]] = 1;
+  }
+  for (int k = 0; k < K; ++k)
+    if (!seen[k]) return gg_fail(GG_ERR_INVALID, "shard %d of %u is empty", k, num_shards);
+  std::memcpy(tile_shard, m.data(), sizeof(uint32_t) * T);
+  return GG_OK;
 }
 
 float gg_kernel_time_ms(gg_ctx* ctx, const char* kernel)

@@ -1,7 +1,7 @@
 // gg_coherent.hip — the coherent ("Mode C") path on MI355X (gfx950):
 // pr_l1_pr_l2_dram_directory_msi with the DRAM directory, DRAM controller,
 // ShmemPerfModel clock, memory network and lax-barrier quanta, in the
-// canonical step schedule of DESIGN.md §Mode C.
+// canonical step schedule of DESIGN.md §4.
 //
 // Reference (nmtrmail/Graphite, common/tile/memory_subsystem/):
 //   pr_l1_pr_l2_dram_directory_msi/l1_cache_cntlr.cc:89-305   L1 state machine
@@ -11,25 +11,49 @@
 //   directory_schemes/directory_entry_full_map.cc:18-86       full-map sharers
 //   dram_cntlr.cc:37-74, performance_models/dram_perf_model.cc:75-116  DRAM
 //   performance_models/shmem_perf_model.cc:16-45              per-tile clock
-//   network: gg_dev.h route_closed_form (emesh_hop_counter / magic)
+//   common/network/models/network_model_emesh_hop_by_hop.cc:146-264  hop-by-hop
+//   common/network/components/router/router_model.cc:52-108    output ports
 //
-// Layout: one lane = one tile (the tile's controllers are sequential by
-// construction: a per-tile lock in the reference, memory_manager.cc:78-120).
-// Every tile owns its state in HBM, indexed by local tile (tile - first owned):
-// L1-D / L2 sets (u64 line tags + one meta byte per way: state, cached_loc,
-// LRU age), the directory slice (16-byte entries + full-map sharer words), the
-// replaced-entry pool, the per-address request FIFO and the DRAM history tree.
-// A step is two launches: k_c_tiles (lane per tile: inbox, then trace) and
-// k_c_route (thread per message: network latency, delivery into per-tile
-// linked lists of the next step or into the quantum-boundary buffer).  Steps
-// are launched in batches; a step that sends nothing sets `quiet`, and the
-// launches after it return at once, so one host sync per batch suffices.
+// Execution model.  ONE WAVE PER TILE.  A tile's controllers are sequential
+// by construction (the per-tile lock of memory_manager.cc:78-120), so the
+// whole wave runs the tile's control flow in lockstep with identical values
+// on every lane; the lanes split the work wherever the data is wide:
+//   * a cache set: lane w holds way w (tag + meta byte); the hit is a ballot,
+//     the LRU victim a ballot + ffs, the age update lane-parallel;
+//   * a directory set: lane i checks way i; the replacement candidate is a
+//     wave min over (sharers, way) of the ways with no queued request;
+//   * a full-map sharer vector: lane k holds word k; an INV_REQ fan-out is a
+//     popcount prefix scan and every lane writes its word's messages;
+//   * the request FIFO (LDS) and the DRAM / router queues (LDS images of the
+//     flat interval list of gg_dev.h): lane-parallel scans and shifts;
+//   * the inbox: keys in LDS, channel prefix-max and ranks lane-parallel.
+// Plain stores in the uniform parts are made by every lane (same address,
+// same value), so each lane reads back its own writes; lane-parallel stores
+// touch only data the same lane reads again, or are followed by a
+// workgroup barrier (one wave = one workgroup) before other lanes read them.
+//
+// Step: k_c_step, one launch, wave per owned tile:
+//   (hop-by-hop) the SELF output port + receive of the packets that reached
+//   the tile in the previous step, in (time, key) order;
+//   the inbox in the reference's per-channel FIFO order, channels merged by
+//   (arrival, sender);  the trace up to the lax barrier or the next miss;
+//   publish: hop counter / magic route every record (closed form) into its
+//   receiver's inbox list or the quantum-boundary buffer; hop-by-hop sends
+//   the tile's packets through its injection port in (time, key) order and
+//   onto the list of the X (or Y) chain segment they enter.
+// Hop-by-hop adds k_c_walk for the X segments, then for the Y segments: one
+// wave per run of one row (column) inside one logical shard walks that
+// run's packets in (time, key) order through the output-port queues (LDS
+// images), hands packets that finish the run to the next segment list or to
+// their destination's SELF list, and holds packets whose next router lies in
+// another logical shard for the quantum boundary (gg_cmsg.hop).
 #include "gg_dev.h"
 
 #include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <cstdlib>
+#include <vector>
 
 namespace {
 using namespace gg;
@@ -40,6 +64,7 @@ enum { M_EX_REQ = GG_MSG_EX_REQ, M_SH_REQ = GG_MSG_SH_REQ, M_INV_REQ = GG_MSG_IN
        M_WB_REP = GG_MSG_WB_REP, M_NULLIFY_REQ = GG_MSG_NULLIFY_REQ };
 enum { DS_UNCACHED = 0, DS_SHARED = 1, DS_MODIFIED = 2 };
 enum { ST_I = 0, ST_S = 1, ST_M = 2 };           // meta byte bits 0-1
+enum { P_SELF = 0, P_LEFT, P_RIGHT, P_DOWN, P_UP, P_INJ };   // network_model_emesh_hop_by_hop.h:41-48 (+ injection)
 #define INV_ADDR (~0ull)
 #define NO_ENT (-0x7fffffff)
 
@@ -54,141 +79,132 @@ __device__ __forceinline__ bool has_data(uint32_t t)
 
 struct DEnt { uint64_t addr; int32_t owner; uint16_t dstate; uint16_t nsh; };   // 16 B
 struct CReq { uint64_t addr, time; uint32_t type, requester; };                 // 24 B
+struct Seg { uint32_t line, lo, hi, pad; };       // a run of row (X) / column (Y) `line`: positions [lo, hi]
+
+constexpr uint32_t kInLds = 512;       // inbox / port batch entries ordered in LDS (more: global scratch)
+constexpr uint32_t kRqLds = 512;       // directory request FIFO entries staged in LDS
+constexpr uint32_t kChunks = 128;      // record chunks per tile step
+constexpr uint32_t kChunk = 16;        // records per chunk
+constexpr uint32_t kQMax = 128;        // largest max_list_size of a queue staged in LDS (wave ops: 2 per lane)
+constexpr uint32_t kNetCtr = 7;        // router / link counters a walker accumulates per position
+constexpr size_t kWalkLdsMax = 160 * 1024;
+constexpr uint32_t kWalkPkBytes = 5 * 8 + 4 * 4;   // t, khi, klo, zl, (pad) | idx, pos, dpos, nf/status
 
 struct CP {
-  uint32_t T, K, tb, lt;                 // tiles, shards, first owned tile, owned tiles
+  uint32_t T, K, L;                      // tiles, logical shards, owned tiles
   uint32_t s1, a1, s2, a2, log_line, pol1, pol2;
   uint32_t E, dassoc, log_dsets, log_slices, W, R, QC, IC;
-  uint32_t bits_req, bits_data, max_list, analytical, dram_qm;
-  uint32_t dram_qtype, dram_qaux;          // dram/queue_model/type (GG_QM_*) and its hq_aux parameter
+  uint32_t bits_req, bits_data, max_list, analytical, dram_qm, dram_qtype, dram_qaux;
+  uint32_t net, nsx, nsy, mw, mh, qimg;  // network model; X / Y segments; mesh; bytes of a queue image
+  uint32_t msg_cap, seg_cap, walk_pk;    // pool records per parity; entries per segment list; walker LDS packets
   uint64_t lat_l1d, lat_l1t, lat_l2d, lat_l2t, lat_dir, gap_ps, dram_proc, dram_cost;
-  uint64_t msg_cap;
-  uint32_t tiles_per_block;              // 64: a lane per tile; 1: a wave per tile (lane 0)
-  uint32_t stage_rq;                     // wave per tile: directory request FIFO staged in LDS per step
   NocParams np;
 };
 
 struct CS {
   uint64_t* l1_tag; uint8_t* l1_meta; uint8_t* l1_rr;
   uint64_t* l2_tag; uint8_t* l2_meta; uint8_t* l2_rr;
-  uint64_t* cc;                          // [lt][2][12]
-  uint64_t* st;                          // [lt][GG_NUM_TILE_STATS]
+  uint64_t* cc;                          // [L][2][12]
+  uint64_t* st;                          // [L][GG_NUM_TILE_STATS]
   uint64_t *rec, *rec_end, *clk, *pend_start, *out_addr, *out_time;
   uint32_t *blocked, *seq;
-  DEnt* dir; uint64_t* dsh;              // [lt][E], [lt][E][W]
-  DEnt* rep; uint64_t* rsh; uint32_t* nrep;   // [lt][R], [lt][R][W]
-  CReq* rq; uint32_t* nrq;               // [lt][QC]
-  HQueue* dq; HNode* dnd; int16_t* dfl;  // DRAM queue per tile
+  DEnt* dir; uint64_t* dsh;              // [L][E], [L][E][W]
+  DEnt* rep; uint64_t* rsh; uint32_t* nrep;   // [L][R], [L][R][W]
+  CReq* rq; uint32_t* nrq;               // [L][QC]
+  HQueue* dq; HNode* dnd;                // DRAM queue per tile
+  const uint32_t* gtile; const int32_t* ltile; const uint32_t* shard;   // local -> tile, tile -> local (-1), tile -> shard
   const uint64_t* addr; const uint32_t* meta; uint64_t* out;
-  gg_cmsg* buf0; gg_cmsg* buf1; uint32_t* cnt;   // cnt[2]
-  int32_t* head0; int32_t* head1;                // [lt]
-  gg_cmsg* bnd; uint32_t* bnd_cnt;
-  uint32_t* scratch;                     // [lt][IC]
-  uint32_t* quiet; uint64_t* ri;
-  // hop-by-hop: the step's messages as packet arrays (gg_noc_hbh)
-  uint32_t *pk_src, *pk_dst, *pk_len; uint64_t *pk_t0, *pk_khi, *pk_klo;
+  gg_cmsg* pool0; gg_cmsg* pool1; uint32_t* npool;    // records of even / odd steps, alloc counters [2]
+  uint32_t* inb0; uint32_t* inb1; uint32_t* ninb0; uint32_t* ninb1;   // inbox record lists [L][IC], [L]
+  uint32_t* arv0; uint32_t* arv1; uint32_t* narv0; uint32_t* narv1;   // hop-by-hop SELF lists
+  uint32_t* xl; uint32_t* nxl; uint32_t* yl; uint32_t* nyl;           // segment lists [n][seg_cap], [n]
+  const Seg* segx; const Seg* segy;
+  const uint32_t* tseg;                  // [T][2]: X run, Y run of a tile (~0 if not owned)
+  gg_cmsg* bnd; uint32_t* bnd_cnt;       // held for the quantum boundary
+  uint32_t* ring; uint32_t* quiet;       // records sent per step (mod 4); quiet flag of the quantum
+  uint64_t* ri; uint32_t* err;
+  HQueue* nq; HNode* nnd;                // router queues [tile * 6 + port]
   uint64_t* ctr;                         // NoC counters [T][GG_NUM_NET_COUNTERS]
-  uint32_t* err;
-  // GG_COH_PROFILE=1 (diagnostics): shader-clock cycles per step phase
-  unsigned long long* prof;              // [0..3] phase sums over tiles and steps, [8 + step] max tile total
-  uint32_t prof_steps;
+  uint64_t* gscr;                        // [L][5 * IC] ordering scratch beyond kInLds
 };
 
-__device__ __forceinline__ gg_cmsg* bufp(const CS& S, int p) { return p ? S.buf1 : S.buf0; }
-__device__ __forceinline__ int32_t* headp(const CS& S, int p) { return p ? S.head1 : S.head0; }
+__device__ __forceinline__ gg_cmsg* pool(const CS& S, uint32_t p) { return p ? S.pool1 : S.pool0; }
+__device__ __forceinline__ uint32_t* inb(const CS& S, uint32_t p) { return p ? S.inb1 : S.inb0; }
+__device__ __forceinline__ uint32_t* ninb(const CS& S, uint32_t p) { return p ? S.ninb1 : S.ninb0; }
+__device__ __forceinline__ uint32_t* arv(const CS& S, uint32_t p) { return p ? S.arv1 : S.arv0; }
+__device__ __forceinline__ uint32_t* narv(const CS& S, uint32_t p) { return p ? S.narv1 : S.narv0; }
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) { return (uint64_t)__shfl((long long)v, src); }
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
+{
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_min(uint32_t v)
+{
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t ln)
+{
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) { const uint32_t y = __shfl_up(x, o); if (ln >= (uint32_t)o) x += y; }
+  return x - v;
+}
+// pick the element of a per-thread register array selected by a lane-varying index
+template <int N> __device__ __forceinline__ uint64_t pick(const uint64_t (&a)[N], uint32_t i)
+{
+  uint64_t v = 0;
+#pragma unroll
+  for (int k = 0; k < N; ++k) if (i == (uint32_t)k) v = a[k];
+  return v;
+}
+template <int N> __device__ __forceinline__ uint32_t pick(const uint32_t (&a)[N], uint32_t i)
+{
+  uint32_t v = 0;
+#pragma unroll
+  for (int k = 0; k < N; ++k) if (i == (uint32_t)k) v = a[k];
+  return v;
+}
 
 // ---------------------------------------------------------------------------
-// one private cache (Cache + CacheSet + replacement policy, cache.cc / cache_set.cc)
+// one private cache (Cache + CacheSet + replacement policy, cache.cc / cache_set.cc):
+// lane w handles way w of the set an operation touches
 // ---------------------------------------------------------------------------
-#define CMAXW 16   // ways held in registers at once (larger associativities take the serial path)
 struct Cache {
   uint64_t* tag; uint8_t* meta; uint8_t* rr; uint64_t* cg;
-  uint32_t sets, ways, log_line, pol, wb;
-  uint32_t c[GG_NUM_CACHE_COUNTERS];   // this step's counter increments (registers), flushed to cg
+  uint32_t sets, ways, log_line, pol, wb, ln;
+  uint32_t c[GG_NUM_CACHE_COUNTERS];   // this step's counter increments, flushed to cg
 
   __device__ __forceinline__ uint32_t set_of(uint64_t a) const { return (uint32_t)((a >> log_line) & (sets - 1)); }   // cache_hash_fn.h:17
   __device__ __forceinline__ uint64_t tag_of(uint64_t a) const { return a >> log_line; }                             // cache.cc:495
-  // the set's tags and meta bytes, every way's load in flight at once
-  __device__ __forceinline__ void load_set(uint32_t s, uint64_t (&tv)[CMAXW], uint8_t (&mv)[CMAXW]) const
+  __device__ __forceinline__ void ld(uint32_t s, uint64_t& tv, uint32_t& mv) const
   {
-    const uint64_t* p = tag + (size_t)s * ways;
-    const uint8_t* m = meta + (size_t)s * ways;
-#pragma unroll
-    for (int w = 0; w < CMAXW; ++w) { tv[w] = INV_ADDR; mv[w] = 0; if (w < (int)ways) { tv[w] = p[w]; mv[w] = m[w]; } }
+    tv = INV_ADDR; mv = 0;
+    if (ln < ways) { tv = tag[(size_t)s * ways + ln]; mv = meta[(size_t)s * ways + ln]; }
   }
-  // CacheSet::find (cache_set.cc:57-70); tags are unique, so any match is the match
-  __device__ __forceinline__ int find(uint32_t s, uint64_t t, uint8_t& mb) const
+  // CacheSet::find (cache_set.cc:57-70): tags are unique, so any matching lane is the way
+  __device__ __forceinline__ int way_of(uint64_t tv, uint64_t t) const
   {
-    if (ways <= CMAXW) {
-      uint64_t tv[CMAXW]; uint8_t mv[CMAXW];
-      load_set(s, tv, mv);
-      int f = -1; mb = 0;
-#pragma unroll
-      for (int w = 0; w < CMAXW; ++w) if (w < (int)ways && tv[w] == t) { f = w; mb = mv[w]; }
-      return f;
-    }
-    for (int w = (int)ways - 1; w >= 0; --w)
-      if (tag[(size_t)s * ways + w] == t) { mb = meta[(size_t)s * ways + w]; return w; }
-    return -1;
+    const uint64_t m = __ballot(ln < ways && tv == t);
+    return m ? (int)__builtin_ctzll(m) : -1;
   }
-  __device__ __forceinline__ void touch(uint32_t s, uint32_t w)                                                        // lru:40-50
+  __device__ __forceinline__ void touch(uint32_t s, int w, uint32_t mv)                                           // lru:40-50
   {
     if (pol != GG_POLICY_LRU) return;
-    uint8_t* m = meta + (size_t)s * ways;
-    if (ways <= CMAXW) {
-      uint8_t v[CMAXW];
-#pragma unroll
-      for (int i = 0; i < CMAXW; ++i) { v[i] = 0; if (i < (int)ways) v[i] = m[i]; }
-      uint32_t acc = 0;
-#pragma unroll
-      for (int i = 0; i < CMAXW; ++i) if (i == (int)w) acc = v[i] >> 3;
-#pragma unroll
-      for (int i = 0; i < CMAXW; ++i) {
-        if (i >= (int)ways) continue;
-        const uint32_t a = v[i] >> 3;
-        const uint8_t nv = (i == (int)w) ? (uint8_t)(v[i] & 7u) : (a < acc ? (uint8_t)((v[i] & 7u) | ((a + 1) << 3)) : v[i]);
-        if (nv != v[i]) m[i] = nv;
-      }
-      return;
+    const uint32_t acc = (uint32_t)__shfl((int)mv, w) >> 3;
+    if (ln < ways) {
+      const uint32_t a = mv >> 3;
+      uint32_t nv = mv;
+      if ((int)ln == w) nv = mv & 7u;
+      else if (a < acc) nv = (mv & 7u) | ((a + 1) << 3);
+      if (nv != mv) meta[(size_t)s * ways + ln] = (uint8_t)nv;
     }
-    const uint32_t acc = m[w] >> 3;
-    for (uint32_t i = 0; i < ways; ++i) { uint32_t a = m[i] >> 3; if (a < acc) m[i] = (uint8_t)((m[i] & 7u) | ((a + 1) << 3)); }
-    m[w] = (uint8_t)(m[w] & 7u);
   }
-  // getReplacementWay: LRU (lru:23-38) = first invalid way, else the (last) way of age assoc-1;
-  // round robin (rr:13-22).  Returns the way and its current tag / meta byte.
-  __device__ __forceinline__ int victim(uint32_t s, uint64_t& vt, uint8_t& vm)
-  {
-    if (pol == GG_POLICY_LRU) {
-      if (ways <= CMAXW) {
-        uint64_t tv[CMAXW]; uint8_t mv[CMAXW];
-        load_set(s, tv, mv);
-        int inv = -1, way = -1;
-#pragma unroll
-        for (int i = CMAXW - 1; i >= 0; --i) if (i < (int)ways && tv[i] == INV_ADDR) inv = i;
-#pragma unroll
-        for (int i = 0; i < CMAXW; ++i) if (i < (int)ways && tv[i] != INV_ADDR && (uint32_t)(mv[i] >> 3) == ways - 1) way = i;
-        const int r = inv >= 0 ? inv : way;
-        vt = INV_ADDR; vm = 0;
-#pragma unroll
-        for (int i = 0; i < CMAXW; ++i) if (i == r) { vt = tv[i]; vm = mv[i]; }
-        return r;
-      }
-      const uint8_t* m = meta + (size_t)s * ways;
-      int way = -1;
-      for (uint32_t i = 0; i < ways; ++i) {
-        if (tag[(size_t)s * ways + i] == INV_ADDR) { vt = INV_ADDR; vm = m[i]; return (int)i; }
-        else if ((uint32_t)(m[i] >> 3) == ways - 1) way = (int)i;
-      }
-      if (way >= 0) { vt = tag[(size_t)s * ways + way]; vm = m[way]; }
-      return way;
-    }
-    const uint32_t cur = rr[s];
-    rr[s] = (uint8_t)(cur == 0 ? ways - 1 : cur - 1);
-    vt = tag[(size_t)s * ways + cur]; vm = meta[(size_t)s * ways + cur];
-    return (int)cur;
-  }
-  __device__ __forceinline__ void miss_counters(bool wr, bool miss)                                                   // cache.cc:321-360
+  __device__ __forceinline__ void miss_counters(bool wr, bool miss)                                               // cache.cc:321-360
   {
     c[GG_CC_ACCESSES]++;
     if (wr) c[GG_CC_WRITE_ACCESSES]++; else c[GG_CC_READ_ACCESSES]++;
@@ -197,21 +213,25 @@ struct Cache {
   // getCacheLineInfo (cache.cc:187-215): state / loc of the line, I / 0 when absent
   __device__ __forceinline__ void get(uint64_t a, uint32_t& st, uint32_t& loc)
   {
-    uint8_t m;
-    const int w = find(set_of(a), tag_of(a), m);
+    uint64_t tv; uint32_t mv;
+    ld(set_of(a), tv, mv);
+    const int w = way_of(tv, tag_of(a));
     c[GG_CC_TAG_READS]++;
-    if (w >= 0) { st = m & 3u; loc = (m >> 2) & 1u; }
+    if (w >= 0) { const uint32_t m = (uint32_t)__shfl((int)mv, w); st = m & 3u; loc = (m >> 2) & 1u; }
     else { st = ST_I; loc = 0; }
   }
   // setCacheLineInfo (cache.cc:218-241): st == I writes the invalid tag (CacheLineInfo::invalidate)
   __device__ __forceinline__ bool set(uint64_t a, uint32_t st, uint32_t loc)
   {
     const uint32_t s = set_of(a);
-    uint8_t m;
-    const int w = find(s, tag_of(a), m);
+    uint64_t tv; uint32_t mv;
+    ld(s, tv, mv);
+    const int w = way_of(tv, tag_of(a));
     if (w < 0) return false;
-    meta[(size_t)s * ways + w] = (uint8_t)((m & 0xF8u) | st | (loc << 2));
-    if (st == ST_I) tag[(size_t)s * ways + w] = INV_ADDR;
+    if ((int)ln == w) {
+      meta[(size_t)s * ways + ln] = (uint8_t)((mv & 0xF8u) | st | (loc << 2));
+      if (st == ST_I) tag[(size_t)s * ways + ln] = INV_ADDR;
+    }
     c[GG_CC_TAG_WRITES]++;
     return true;
   }
@@ -219,27 +239,44 @@ struct Cache {
   __device__ __forceinline__ bool access(uint64_t a, bool store)
   {
     const uint32_t s = set_of(a);
-    uint8_t m;
-    const int w = find(s, tag_of(a), m);
+    uint64_t tv; uint32_t mv;
+    ld(s, tv, mv);
+    const int w = way_of(tv, tag_of(a));
     if (w < 0) return false;
-    touch(s, (uint32_t)w);
+    touch(s, w, mv);
     if (store) c[GG_CC_DATA_WRITES]++; else c[GG_CC_DATA_READS]++;
     return true;
   }
-  // insertCacheLine (cache.cc:114-184); returns false on a policy error
-  __device__ __forceinline__ bool insert(uint64_t a, uint32_t st, uint32_t loc, bool& ev, uint64_t& ev_addr, uint32_t& ev_st,
-                         uint32_t& ev_loc)
+  // insertCacheLine (cache.cc:114-184) with getReplacementWay: LRU (lru:23-38) = first
+  // invalid way, else the way of age assoc-1; round robin (rr:13-22)
+  __device__ __forceinline__ bool insert(uint64_t a, uint32_t st, uint32_t loc, bool& ev, uint64_t& ev_addr,
+                                         uint32_t& ev_st, uint32_t& ev_loc)
   {
     const uint32_t s = set_of(a);
-    uint64_t vt; uint8_t vm;
-    const int w = victim(s, vt, vm);
+    uint64_t tv; uint32_t mv;
+    ld(s, tv, mv);
+    int w;
+    if (pol == GG_POLICY_LRU) {
+      const uint64_t inv = __ballot(ln < ways && tv == INV_ADDR);
+      const uint64_t old = __ballot(ln < ways && tv != INV_ADDR && (mv >> 3) == ways - 1);
+      w = inv ? (int)__builtin_ctzll(inv) : (old ? (int)__builtin_ctzll(old) : -1);
+    } else {
+      const uint32_t cur = rr[s];
+      rr[s] = (uint8_t)(cur == 0 ? ways - 1 : cur - 1);
+      w = (int)cur;
+    }
     if (w < 0 || (uint32_t)w >= ways) return false;
-    const size_t i = (size_t)s * ways + w;
+    const uint64_t vt = shfl64(tv, w);
+    const uint32_t vm = (uint32_t)__shfl((int)mv, w);
     ev = vt != INV_ADDR;
     if (ev) { ev_addr = vt << log_line; ev_st = vm & 3u; ev_loc = (vm >> 2) & 1u; }
-    tag[i] = tag_of(a);
-    meta[i] = (uint8_t)((vm & 0xF8u) | st | (loc << 2));
-    touch(s, (uint32_t)w);
+    if ((int)ln == w) {
+      const uint32_t nm = (vm & 0xF8u) | st | (loc << 2);
+      tag[(size_t)s * ways + ln] = tag_of(a);
+      meta[(size_t)s * ways + ln] = (uint8_t)nm;
+      mv = nm;
+    }
+    touch(s, w, mv);
     c[GG_CC_TAG_READS]++;
     if (ev) {
       c[GG_CC_DATA_READS]++;
@@ -249,14 +286,10 @@ struct Cache {
     c[GG_CC_TAG_WRITES]++; c[GG_CC_DATA_WRITES]++;
     return true;
   }
-  // all loads in flight, then all stores (no load waits behind a store)
   __device__ __forceinline__ void flush()
   {
-    uint64_t v[GG_NUM_CACHE_COUNTERS];
-#pragma unroll
-    for (int k = 0; k < GG_NUM_CACHE_COUNTERS; ++k) v[k] = cg[k];
-#pragma unroll
-    for (int k = 0; k < GG_NUM_CACHE_COUNTERS; ++k) cg[k] = v[k] + c[k];
+    const uint32_t v = pick(c, ln);
+    if (ln < GG_NUM_CACHE_COUNTERS && v) cg[ln] += v;
   }
 };
 
@@ -266,70 +299,94 @@ enum { W_NONE = 0, W_PROC, W_CONT, W_NEXT, W_NULLIFY };
 struct Work { uint64_t addr; uint32_t kind, type, requester, cached; int32_t h; };
 #define WSTACK 32
 
+// LDS of one tile step
+struct StepLds {
+  CReq rq[kRqLds];
+  uint8_t dimg[sizeof(HQueue) + kQMax * sizeof(HNode)];   // DRAM queue image
+  uint8_t pimg[sizeof(HQueue) + kQMax * sizeof(HNode)];   // SELF / injection port image
+  uint64_t x1[kInLds], x2[kInLds], x3[kInLds];
+  uint32_t i1[kInLds], i2[kInLds];
+  uint32_t ch[2 * kChunks];                               // record chunks: base, used
+};
+
 // ---------------------------------------------------------------------------
-// one tile's controllers
+// one tile's controllers (every lane, identical values)
 // ---------------------------------------------------------------------------
 struct Tile {
   const CP& P; const CS& S;
-  uint32_t lt, tile; int po;
+  uint32_t lt, tile, ln, p;             // local index, tile id, lane, step parity
+  StepLds& sl;
   Cache L1, L2;
-  uint64_t* stg;
-  uint64_t st[GG_NUM_TILE_STATS];       // this step's statistics increments (registers)
-  // the tile's scalars, in registers for the step (written back by flush)
+  uint64_t st[GG_NUM_TILE_STATS];       // this step's statistics increments
   uint64_t rec, rec_end, clk, pend_start, out_addr, out_time;
   uint32_t blocked, seq, nrep, nrq;
-  // the tile's DRAM queue (history tree) and directory request FIFO: global
-  // memory, or the step's LDS copies
-  HQueue* dq; HNode* dnd; int16_t* dfl;
-  CReq* rqp;
+  HQueue* dq; HNode* dnd; bool dq_lds;
+  CReq* rqp; bool rq_lds;
+  uint32_t nch, cbase, cused, ccap, nsent;
+  bool failed;
 
-  __device__ __forceinline__ Tile(const CP& p, const CS& s, uint32_t l, int out_parity) : P(p), S(s), lt(l), tile(p.tb + l), po(out_parity)
+  __device__ __forceinline__ Tile(const CP& P_, const CS& S_, uint32_t l, uint32_t par, StepLds& s_)
+      : P(P_), S(S_), lt(l), tile(S_.gtile[l]), ln(lane_id()), p(par), sl(s_)
   {
     L1 = Cache{S.l1_tag + (size_t)lt * P.s1 * P.a1, S.l1_meta + (size_t)lt * P.s1 * P.a1, S.l1_rr + (size_t)lt * P.s1,
-               S.cc + (size_t)lt * 2 * GG_NUM_CACHE_COUNTERS, P.s1, P.a1, P.log_line, P.pol1, 0, {}};
+               S.cc + (size_t)lt * 2 * GG_NUM_CACHE_COUNTERS, P.s1, P.a1, P.log_line, P.pol1, 0, ln, {}};
     L2 = Cache{S.l2_tag + (size_t)lt * P.s2 * P.a2, S.l2_meta + (size_t)lt * P.s2 * P.a2, S.l2_rr + (size_t)lt * P.s2,
-               S.cc + ((size_t)lt * 2 + 1) * GG_NUM_CACHE_COUNTERS, P.s2, P.a2, P.log_line, P.pol2, 1, {}};
-    stg = S.st + (size_t)lt * GG_NUM_TILE_STATS;
+               S.cc + ((size_t)lt * 2 + 1) * GG_NUM_CACHE_COUNTERS, P.s2, P.a2, P.log_line, P.pol2, 1, ln, {}};
 #pragma unroll
     for (int k = 0; k < GG_NUM_TILE_STATS; ++k) st[k] = 0;
     rec = S.rec[lt]; rec_end = S.rec_end[lt]; clk = S.clk[lt]; pend_start = S.pend_start[lt];
     out_addr = S.out_addr[lt]; out_time = S.out_time[lt];
     blocked = S.blocked[lt]; seq = S.seq[lt]; nrep = S.nrep[lt]; nrq = S.nrq[lt];
-    dq = S.dq + lt; dnd = S.dnd + (size_t)lt * P.max_list; dfl = S.dfl + (size_t)lt * P.max_list;
-    rqp = S.rq + (size_t)lt * P.QC;
+    dq = S.dq + lt; dnd = S.dnd + (size_t)lt * P.max_list; dq_lds = false;
+    rqp = S.rq + (size_t)lt * P.QC; rq_lds = false;
+    nch = 0; cbase = 0; cused = 0; ccap = 0; nsent = 0; failed = false;
   }
-  __device__ __forceinline__ void flush()
+  __device__ __forceinline__ void fail(uint32_t e = GG_DERR_STATE)
   {
-    L1.flush(); L2.flush();
-    uint64_t v[GG_NUM_TILE_STATS];
-#pragma unroll
-    for (int k = 0; k < GG_NUM_TILE_STATS; ++k) v[k] = stg[k];
-#pragma unroll
-    for (int k = 0; k < GG_NUM_TILE_STATS; ++k) stg[k] = (k == GG_CT_CLOCK_PS) ? clk : v[k] + st[k];
-    S.rec[lt] = rec; S.clk[lt] = clk; S.pend_start[lt] = pend_start;
-    S.out_addr[lt] = out_addr; S.out_time[lt] = out_time;
-    S.blocked[lt] = blocked; S.seq[lt] = seq; S.nrep[lt] = nrep; S.nrq[lt] = nrq;
+    failed = true;
+    if (ln == 0) atomicOr(S.err, e);
   }
-  __device__ __forceinline__ void fail(uint32_t e = GG_DERR_STATE) const { atomicOr(S.err, e); }
 
-  // MemoryManager::sendMsg (…msi/memory_manager.cc:306-332)
+  // ---- records (MemoryManager::sendMsg, …msi/memory_manager.cc:306-332) ------
+  // n contiguous record slots of this step's pool, from the tile's current chunk
+  __device__ __forceinline__ uint32_t alloc(uint32_t n)
+  {
+    if (failed) return ~0u;
+    if (cused + n > ccap) {
+      if (nch) sl.ch[2 * (nch - 1) + 1] = cused;
+      const uint32_t want = n > kChunk ? n : kChunk;
+      uint32_t b = 0;
+      if (ln == 0) b = atomicAdd(&S.npool[p], want);
+      b = (uint32_t)__shfl((int)b, 0);
+      if ((uint64_t)b + want > P.msg_cap || nch >= kChunks) { fail(GG_DERR_CAP); return ~0u; }
+      sl.ch[2 * nch] = b; sl.ch[2 * nch + 1] = 0;
+      ++nch; cbase = b; ccap = want; cused = 0;
+    }
+    const uint32_t i = cbase + cused;
+    cused += n; nsent += n;
+    return i;
+  }
+  __device__ __forceinline__ void put(uint32_t i, uint32_t dst, uint32_t type, uint32_t requester, uint64_t addr,
+                                      uint64_t t, uint32_t sq)
+  {
+    gg_cmsg m;
+    m.addr = addr; m.send_ps = t; m.arrival_ps = t; m.zero_load_ps = 0;
+    m.src = tile; m.dst = dst; m.requester = requester; m.seq = sq; m.type = type; m.link = 0;
+    m.hop = GG_HOP_NONE; m.pad = 0;
+    pool(S, p)[i] = m;
+  }
+  __device__ __forceinline__ void count_sent(uint32_t type, uint64_t n)
+  {
+    st[GG_CT_MSGS_SENT] += n;
+#pragma unroll
+    for (int k = 0; k < 11; ++k) if (type == (uint32_t)k + 1) st[GG_CT_SENT_BY_TYPE + k] += n;
+  }
   __device__ __forceinline__ void send(uint32_t dst, uint32_t type, uint32_t requester, uint64_t addr, uint64_t t)
   {
-    const uint64_t p0 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
-    send_(dst, type, requester, addr, t);
-    if (S.prof) atomicAdd(&S.prof[11], (unsigned long long)(__builtin_amdgcn_s_memtime() - p0));
-  }
-  __device__ __forceinline__ void send_(uint32_t dst, uint32_t type, uint32_t requester, uint64_t addr, uint64_t t)
-  {
-    const uint32_t i = atomicAdd(&S.cnt[po], 1u);
-    if (i >= P.msg_cap) { fail(GG_DERR_CAP); return; }
-    gg_cmsg m;
-    m.addr = addr; m.send_ps = t; m.arrival_ps = t; m.src = tile; m.dst = dst; m.requester = requester;
-    m.seq = seq++; m.type = type; m.link = 0xFFFFFFFFu;
-    bufp(S, po)[i] = m;
-    st[GG_CT_MSGS_SENT]++;
-#pragma unroll
-    for (int k = 0; k < 11; ++k) if (type == (uint32_t)k + 1) st[GG_CT_SENT_BY_TYPE + k]++;
+    const uint32_t i = alloc(1);
+    if (i == ~0u) return;
+    put(i, dst, type, requester, addr, t, seq++);
+    count_sent(type, 1);
   }
   __device__ __forceinline__ uint32_t home(uint64_t a) const { return (uint32_t)((a >> 6) % P.T); }   // address_home_lookup.cc:19-26
 
@@ -345,13 +402,19 @@ struct Tile {
   __device__ __forceinline__ bool has(int32_t h, uint32_t s) const { return (shw(h)[s >> 6] >> (s & 63)) & 1ull; }
   __device__ __forceinline__ void add_sharer(int32_t h, uint32_t s)                 // addSharer (full_map.cc:27-33)
   {
-    if (has(h, s)) fail();
-    shw(h)[s >> 6] |= 1ull << (s & 63); ent(h)->nsh++;
+    uint64_t* w = shw(h) + (s >> 6);
+    const uint64_t v = *w;
+    if ((v >> (s & 63)) & 1ull) fail();
+    *w = v | (1ull << (s & 63));
+    ent(h)->nsh++;
   }
   __device__ __forceinline__ void remove_sharer(int32_t h, uint32_t s)              // removeSharer (:35-41)
   {
-    if (!has(h, s)) { fail(); return; }
-    shw(h)[s >> 6] &= ~(1ull << (s & 63)); ent(h)->nsh--;
+    uint64_t* w = shw(h) + (s >> 6);
+    const uint64_t v = *w;
+    if (!((v >> (s & 63)) & 1ull)) { fail(); return; }
+    *w = v & ~(1ull << (s & 63));
+    ent(h)->nsh--;
   }
   __device__ __forceinline__ void set_owner(int32_t h, int32_t o)                   // DirectoryEntry::setOwner
   {
@@ -365,35 +428,21 @@ struct Tile {
     for (uint32_t i = P.log_line + P.log_slices; i + P.log_dsets <= 64; i += P.log_dsets) s ^= (a >> i) & mask;
     return (uint32_t)s;
   }
-  // getDirectoryEntry (directory_cache.cc:102-145)
+  // getDirectoryEntry (directory_cache.cc:102-145): lane i checks way i, then replaced entry i
   __device__ __forceinline__ int32_t dget(uint64_t a, uint64_t& t)
-  {
-    const uint64_t p0 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
-    const int32_t r = dget_(a, t);
-    if (S.prof) atomicAdd(&S.prof[9], (unsigned long long)(__builtin_amdgcn_s_memtime() - p0));
-    return r;
-  }
-  __device__ __forceinline__ int32_t dget_(uint64_t a, uint64_t& t)
   {
     t += P.lat_dir;
     st[GG_CT_DIR_ACCESSES]++;
     const uint32_t base = dset(a) * P.dassoc;
     DEnt* d = S.dir + (size_t)lt * P.E;
-    if (P.dassoc <= 16) {                           // every way's address in flight at once
-      uint64_t v[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) { v[i] = 0; if (i < (int)P.dassoc) v[i] = d[base + i].addr; }
-      int hit = -1, fr = -1;
-#pragma unroll
-      for (int i = 15; i >= 0; --i) if (i < (int)P.dassoc) { if (v[i] == a) hit = i; if (v[i] == INV_ADDR) fr = i; }
-      if (hit >= 0) return (int32_t)(base + hit);
-      if (fr >= 0) { d[base + fr].addr = a; return (int32_t)(base + fr); }
-    } else {
-      for (uint32_t i = 0; i < P.dassoc; ++i) if (d[base + i].addr == a) return (int32_t)(base + i);
-      for (uint32_t i = 0; i < P.dassoc; ++i) if (d[base + i].addr == INV_ADDR) { d[base + i].addr = a; return (int32_t)(base + i); }
-    }
-    const uint32_t nr = nrep;
-    for (uint32_t r = 0; r < nr; ++r) if (ent(-(int32_t)r - 1)->addr == a) return -(int32_t)r - 1;
+    const uint64_t v = ln < P.dassoc ? d[base + ln].addr : 0;
+    const uint64_t hit = __ballot(ln < P.dassoc && v == a);
+    if (hit) return (int32_t)(base + __builtin_ctzll(hit));
+    const uint64_t fr = __ballot(ln < P.dassoc && v == INV_ADDR);
+    if (fr) { const uint32_t i = base + (uint32_t)__builtin_ctzll(fr); d[i].addr = a; return (int32_t)i; }
+    const uint64_t rv = ln < nrep ? ent(-(int32_t)ln - 1)->addr : 0;
+    const uint64_t rh = __ballot(ln < nrep && rv == a);
+    if (rh) return -(int32_t)__builtin_ctzll(rh) - 1;
     return NO_ENT;
   }
   // replaceDirectoryEntry (directory_cache.cc:163-213): the slot gets a fresh
@@ -402,9 +451,10 @@ struct Tile {
   {
     const uint32_t base = dset(replaced) * P.dassoc;
     DEnt* d = S.dir + (size_t)lt * P.E;
-    int32_t slot = -1;
-    for (uint32_t i = 0; i < P.dassoc; ++i) if (d[base + i].addr == replaced) { slot = (int32_t)(base + i); break; }
-    if (slot < 0) { fail(); return NO_ENT; }
+    const uint64_t v = ln < P.dassoc ? d[base + ln].addr : 0;
+    const uint64_t m = __ballot(ln < P.dassoc && v == replaced);
+    if (!m) { fail(); return NO_ENT; }
+    const int32_t slot = (int32_t)(base + __builtin_ctzll(m));
     const uint32_t r = nrep;
     if (r >= P.R) { fail(GG_DERR_CAP); return NO_ENT; }
     nrep = r + 1;
@@ -422,71 +472,101 @@ struct Tile {
   __device__ __forceinline__ void dinvalidate(uint64_t a)
   {
     const uint32_t nr = nrep;
-    for (uint32_t r = 0; r < nr; ++r) {
-      if (ent(-(int32_t)r - 1)->addr != a) continue;
-      for (uint32_t k = r; k + 1 < nr; ++k) {
-        *ent(-(int32_t)k - 1) = *ent(-(int32_t)k - 2);
-        uint64_t* dst = shw(-(int32_t)k - 1); const uint64_t* src = shw(-(int32_t)k - 2);
-        for (uint32_t w = 0; w < P.W; ++w) dst[w] = src[w];
-      }
-      nrep = nr - 1;
-      return;
+    const uint64_t rv = ln < nr ? ent(-(int32_t)ln - 1)->addr : 0;
+    const uint64_t rh = __ballot(ln < nr && rv == a);
+    if (!rh) { fail(); return; }
+    for (uint32_t k = (uint32_t)__builtin_ctzll(rh); k + 1 < nr; ++k) {
+      *ent(-(int32_t)k - 1) = *ent(-(int32_t)k - 2);
+      uint64_t* dst = shw(-(int32_t)k - 1); const uint64_t* src = shw(-(int32_t)k - 2);
+      for (uint32_t w = 0; w < P.W; ++w) dst[w] = src[w];
     }
-    fail();
+    nrep = nr - 1;
+  }
+  // getSharersList (ascending, full_map.cc:48-66): one message per sharer,
+  // lane k writes the messages of sharer word k
+  __device__ __forceinline__ void send_sharers(int32_t h, uint32_t type, uint32_t requester, uint64_t a, uint64_t t)
+  {
+    uint64_t bits = ln < P.W ? shw(h)[ln] : 0;
+    const uint32_t c = (uint32_t)__builtin_popcountll(bits);
+    const uint32_t pre = wave_excl_scan(c, ln);
+    const uint32_t tot = wave_sum(c);
+    if (!tot) return;
+    const uint32_t base = alloc(tot);
+    if (base == ~0u) return;
+    uint32_t k = pre;
+    while (bits) {
+      const uint32_t b = (uint32_t)__builtin_ctzll(bits); bits &= bits - 1;
+      put(base + k, ln * 64 + b, type, requester, a, t, seq + k);
+      ++k;
+    }
+    seq += tot;
+    count_sent(type, tot);
   }
 
   // ---- per-address request FIFO (HashMapList<IntPtr, ShmemReq*>) -----------
-  __device__ __forceinline__ CReq* q() const { return rqp; }
   __device__ __forceinline__ uint32_t qcount(uint64_t a) const
   {
-    const uint32_t n = nrq; uint32_t c = 0;
-    for (uint32_t i = 0; i < n; ++i) c += (q()[i].addr == a);
-    return c;
+    uint32_t c = 0;
+    for (uint32_t i = ln; i < nrq; i += 64) c += (rqp[i].addr == a);
+    return wave_sum(c);
   }
   __device__ __forceinline__ int32_t qfront(uint64_t a) const
   {
-    const uint32_t n = nrq;
-    for (uint32_t i = 0; i < n; ++i) if (q()[i].addr == a) return (int32_t)i;
+    for (uint32_t b = 0; b < nrq; b += 64) {
+      const uint32_t i = b + ln;
+      const uint64_t m = __ballot(i < nrq && rqp[i].addr == a);
+      if (m) return (int32_t)(b + __builtin_ctzll(m));
+    }
     return -1;
   }
   __device__ __forceinline__ void qpush(uint64_t a, uint64_t t, uint32_t type, uint32_t req)
   {
-    const uint32_t n = nrq;
-    if (n >= P.QC) { fail(GG_DERR_CAP); return; }
-    q()[n] = CReq{a, t, type, req};
-    nrq = n + 1;
+    if (nrq >= (rq_lds ? kRqLds : P.QC)) { fail(GG_DERR_CAP); return; }
+    rqp[nrq] = CReq{a, t, type, req};
+    if (rq_lds) wave_sync();
+    ++nrq;
   }
   __device__ __forceinline__ void qpop(uint64_t a)
   {
-    const uint32_t n = nrq;
-    for (uint32_t i = 0; i < n; ++i) {
-      if (q()[i].addr != a) continue;
-      for (uint32_t k = i; k + 1 < n; ++k) q()[k] = q()[k + 1];
-      nrq = n - 1;
-      return;
+    const int32_t f = qfront(a);
+    if (f < 0) return;
+    if (rq_lds) {                                   // shift down in LDS, lane-parallel
+      for (uint32_t b = (uint32_t)f + 1; b < nrq; b += 64) {
+        const uint32_t i = b + ln;
+        CReq v{};
+        if (i < nrq) v = rqp[i];
+        wave_sync();
+        if (i < nrq) rqp[i - 1] = v;
+        wave_sync();
+      }
+    } else {
+      for (uint32_t k = (uint32_t)f; k + 1 < nrq; ++k) rqp[k] = rqp[k + 1];
     }
+    --nrq;
   }
   __device__ __forceinline__ static void front_time(CReq& r, uint64_t& t)   // ShmemReq::updateTime + updateCurrTime
   {
     if (r.time < t) r.time = t;
     if (t < r.time) t = r.time;
   }
+  __device__ __forceinline__ void front_update(int32_t f, uint64_t& t, uint32_t& type, uint32_t& requester)
+  {
+    CReq r = rqp[f];
+    front_time(r, t);
+    if (rq_lds) wave_sync();
+    rqp[f].time = r.time;
+    if (rq_lds) wave_sync();
+    type = r.type; requester = r.requester;
+  }
 
   // ---- DramCntlr / DramPerfModel --------------------------------------------
   __device__ __forceinline__ uint64_t dram_ps(uint64_t t)
   {
-    const uint64_t p0 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
-    const uint64_t r = dram_ps_(t);
-    if (S.prof) atomicAdd(&S.prof[10], (unsigned long long)(__builtin_amdgcn_s_memtime() - p0));
-    return r;
-  }
-  __device__ __forceinline__ uint64_t dram_ps_(uint64_t t)
-  {
     const uint64_t pkt_ns = (uint64_t)ceil(t / 1000.0);
     uint64_t qd = 0;
     if (P.dram_qm) {
-      HTree tr{dq, dnd, dfl, P.dram_proc, P.analytical != 0};
-      qd = tr.delay(pkt_ns, P.dram_proc, S.err);
+      HTree tr{dq, dnd, P.dram_proc, P.analytical != 0};
+      qd = dq_lds ? tr.delay_wave(pkt_ns, P.dram_proc, S.err, ln) : tr.delay(pkt_ns, P.dram_proc, S.err);
       st[GG_CT_DRAM_QUEUE_REQUESTS]++;
     }
     const uint64_t lat = qd + P.dram_proc + P.dram_cost;
@@ -502,6 +582,7 @@ struct Tile {
     Work stack[WSTACK];
     int sp = 0;
     for (;;) {
+      if (failed) return;
       switch (w.kind) {
       case W_PROC: {                     // processEx/ShReqFromL2Cache (:238-380): entry lookup
         int32_t h = dget(w.addr, t);
@@ -510,13 +591,17 @@ struct Tile {
           if (dget(w.addr, t) != NO_ENT) fail();   // the assert in getReplacementCandidates (directory_cache.cc:161)
           const uint32_t base = dset(w.addr) * P.dassoc;
           const DEnt* d = S.dir + (size_t)lt * P.E;
-          int32_t cand = -1;
-          for (uint32_t i = 0; i < P.dassoc; ++i) {
-            const DEnt& it = d[base + i];
-            if ((cand < 0 || d[cand].nsh > it.nsh) && qcount(it.addr) == 0) cand = (int32_t)(base + i);
+          // candidate (:138-149): fewest sharers among ways with no queued request, first wins
+          uint32_t key = ~0u;
+          if (ln < P.dassoc) {
+            const DEnt e = d[base + ln];
+            uint32_t qc = 0;
+            for (uint32_t i = 0; i < nrq; ++i) qc += (rqp[i].addr == e.addr);
+            if (qc == 0) key = ((uint32_t)e.nsh << 8) | ln;
           }
-          if (cand < 0) { fail(); return; }
-          const uint64_t replaced = d[cand].addr;
+          key = wave_min(key);
+          if (key == ~0u) { fail(); return; }
+          const uint64_t replaced = d[base + (key & 0xFFu)].addr;
           h = dreplace(replaced, w.addr, t);
           if (h == NO_ENT) return;
           qpush(replaced, msg_time, M_NULLIFY_REQ, w.requester);
@@ -532,21 +617,15 @@ struct Tile {
       }
       case W_CONT: {                     // the directory-state switch
         DEnt* e = ent(w.h);
+        const uint32_t ds = e->dstate;
         if (w.type == M_EX_REQ) {
-          if (e->dstate == DS_MODIFIED) {
+          if (ds == DS_MODIFIED) {
             if (w.cached) fail();
             send((uint32_t)e->owner, M_FLUSH_REQ, w.requester, w.addr, t);
             w.kind = W_NONE;
-          } else if (e->dstate == DS_SHARED) {
+          } else if (ds == DS_SHARED) {
             if (w.cached) fail();
-            const uint64_t* sh = shw(w.h);
-            for (uint32_t k = 0; k < P.W; ++k) {                     // getSharersList: ascending
-              uint64_t bits = sh[k];
-              while (bits) {
-                const uint32_t b = __builtin_ctzll(bits); bits &= bits - 1;
-                send(k * 64 + b, M_INV_REQ, w.requester, w.addr, t);
-              }
-            }
+            send_sharers(w.h, M_INV_REQ, w.requester, w.addr, t);
             w.kind = W_NONE;
           } else {
             add_sharer(w.h, w.requester);
@@ -557,7 +636,7 @@ struct Tile {
             w.kind = W_NEXT;
           }
         } else {
-          if (e->dstate == DS_MODIFIED) {
+          if (ds == DS_MODIFIED) {
             if (w.cached) fail();
             send((uint32_t)e->owner, M_WB_REQ, w.requester, w.addr, t);
             w.kind = W_NONE;
@@ -576,28 +655,22 @@ struct Tile {
         qpop(w.addr);
         const int32_t f = qfront(w.addr);
         if (f < 0) { w.kind = W_NONE; continue; }
-        CReq& r = q()[f];
-        front_time(r, t);
-        if (r.type != M_EX_REQ && r.type != M_SH_REQ) { fail(); return; }
-        w = Work{w.addr, W_PROC, r.type, r.requester, 0, 0};
+        uint32_t type, req;
+        front_update(f, t, type, req);
+        if (type != M_EX_REQ && type != M_SH_REQ) { fail(); return; }
+        w = Work{w.addr, W_PROC, type, req, 0, 0};
         continue;
       }
       case W_NULLIFY: {                  // processNullifyReq (:172-236)
         const int32_t h = dget(w.addr, t);
         if (h == NO_ENT) { fail(); return; }
         DEnt* e = ent(h);
-        if (e->dstate == DS_MODIFIED) {
+        const uint32_t ds = e->dstate;
+        if (ds == DS_MODIFIED) {
           send((uint32_t)e->owner, M_FLUSH_REQ, w.requester, w.addr, t);
           w.kind = W_NONE;
-        } else if (e->dstate == DS_SHARED) {
-          const uint64_t* sh = shw(h);
-          for (uint32_t k = 0; k < P.W; ++k) {
-            uint64_t bits = sh[k];
-            while (bits) {
-              const uint32_t b = __builtin_ctzll(bits); bits &= bits - 1;
-              send(k * 64 + b, M_INV_REQ, w.requester, w.addr, t);
-            }
-          }
+        } else if (ds == DS_SHARED) {
+          send_sharers(h, M_INV_REQ, w.requester, w.addr, t);
           w.kind = W_NONE;
         } else {
           dinvalidate(w.addr);
@@ -613,9 +686,7 @@ struct Tile {
     }
   }
 
-  // handleMsgFromL2Cache (:43-96) + processInv/Flush/WbRepFromL2Cache (:410-543); every
-  // path ends in at most one directory call chain (one call site keeps the lane's
-  // state in registers)
+  // handleMsgFromL2Cache (:43-96) + processInv/Flush/WbRepFromL2Cache (:410-543)
   __device__ __forceinline__ void directory_msg(const gg_cmsg& m)
   {
     uint64_t t = m.arrival_ps;           // __handleMsgFromNetwork: setCurrTime(packet.time)
@@ -636,11 +707,11 @@ struct Tile {
         if (unc) e->dstate = DS_UNCACHED;
         const int32_t f = qfront(a);
         if (f >= 0) {
-          CReq& r = q()[f];
-          front_time(r, t);
-          if (r.type == M_EX_REQ) { if (unc) w = Work{a, W_PROC, M_EX_REQ, r.requester, 0, 0}; }
-          else if (r.type == M_SH_REQ) w = Work{a, W_PROC, M_SH_REQ, r.requester, 0, 0};
-          else { if (unc) w = Work{a, W_NULLIFY, 0, r.requester, 0, 0}; }
+          uint32_t type, req;
+          front_update(f, t, type, req);
+          if (type == M_EX_REQ) { if (unc) w = Work{a, W_PROC, M_EX_REQ, req, 0, 0}; }
+          else if (type == M_SH_REQ) w = Work{a, W_PROC, M_SH_REQ, req, 0, 0};
+          else { if (unc) w = Work{a, W_NULLIFY, 0, req, 0, 0}; }
         }
       } else if (m.type == M_FLUSH_REP) {
         if (ds != DS_MODIFIED) { fail(); return; }
@@ -649,22 +720,22 @@ struct Tile {
         e->dstate = DS_UNCACHED;
         const int32_t f = qfront(a);
         if (f < 0) { (void)dram_ps(t); return; }                    // putDataToDram: queue model, no latency
-        CReq& r = q()[f];
-        front_time(r, t);
-        if (r.type == M_EX_REQ) w = Work{a, W_PROC, M_EX_REQ, r.requester, 1, 0};
-        else if (r.type == M_SH_REQ) { (void)dram_ps(t); w = Work{a, W_PROC, M_SH_REQ, r.requester, 1, 0}; }
-        else { (void)dram_ps(t); w = Work{a, W_NULLIFY, 0, r.requester, 0, 0}; }
+        uint32_t type, req;
+        front_update(f, t, type, req);
+        if (type == M_EX_REQ) w = Work{a, W_PROC, M_EX_REQ, req, 1, 0};
+        else if (type == M_SH_REQ) { (void)dram_ps(t); w = Work{a, W_PROC, M_SH_REQ, req, 1, 0}; }
+        else { (void)dram_ps(t); w = Work{a, W_NULLIFY, 0, req, 0, 0}; }
       } else if (m.type == M_WB_REP) {
         if (ds != DS_MODIFIED || !has(h, m.src)) { fail(); return; }
         set_owner(h, -1);
         e->dstate = DS_SHARED;
         const int32_t f = qfront(a);
         if (f < 0) { fail(); return; }
-        CReq& r = q()[f];
-        front_time(r, t);
+        uint32_t type, req;
+        front_update(f, t, type, req);
         (void)dram_ps(t);
-        if (r.type != M_SH_REQ) { fail(); return; }
-        w = Work{a, W_PROC, M_SH_REQ, r.requester, 1, 0};
+        if (type != M_SH_REQ) { fail(); return; }
+        w = Work{a, W_PROC, M_SH_REQ, req, 1, 0};
       } else {
         fail();
         return;
@@ -743,7 +814,7 @@ struct Tile {
       return;
     }
     t += P.lat_l2t;
-    if (out_addr != INV_ADDR) fail();                          // handleMsgFromL1Cache (l2:226-258)
+    if (out_addr != INV_ADDR) fail();                                // handleMsgFromL1Cache (l2:226-258)
     out_addr = a; out_time = t;
     const uint32_t h = home(a);
     if (wr) {                                                        // processExReqFromL1Cache (l2:260-282)
@@ -815,232 +886,571 @@ struct Tile {
       fail();
     }
   }
-};
 
-__device__ __forceinline__ bool chan_lt(const gg_cmsg& a, const gg_cmsg& b)
-{
-  return a.src < b.src || (a.src == b.src && a.seq < b.seq);
-}
-
-// A step, lane per owned tile: the inbox (per-channel FIFO, channels merged by
-// (arrival, sender)), then the trace up to the barrier or the next miss.
-// One tile per wave (a one-lane workgroup): the tiles' controller paths diverge
-// completely, so packing 64 tiles into one wave would serialize the union of
-// their paths; one wave per tile costs issue slots the chip has to spare.
-// The DRAM history tree of a wave-per-tile step lives in LDS for the step: the
-// wave copies it in (HQueue + max_list nodes + free list, 16 B per lane per
-// load) before lane 0 runs the tile, and back after.  Its AVL operations are
-// chains of dependent node accesses, each an HBM/MALL round trip otherwise.
-constexpr uint32_t kTreeLds = 128;           // largest max_list_size staged (carbon_sim.cfg: 100)
-struct TreeLds {
-  HQueue q;
-  HNode nd[kTreeLds];
-  int16_t fl[kTreeLds];
-};
-
-__device__ __forceinline__ void copy_words(uint32_t* dst, const uint32_t* src, uint32_t words, uint32_t lane)
-{
-  for (uint32_t i = lane; i < words; i += GG_WAVE) dst[i] = src[i];
-}
-// bytes (multiple of 4) between 16-B aligned buffers where possible
-__device__ __forceinline__ void copy_bytes(void* dst, const void* src, uint32_t bytes, uint32_t lane)
-{
-  if ((((uintptr_t)dst | (uintptr_t)src | bytes) & 15) == 0) {
-    uint4* d = (uint4*)dst; const uint4* q = (const uint4*)src;
-    for (uint32_t i = lane; i < bytes / 16; i += GG_WAVE) d[i] = q[i];
-  } else {
-    copy_words((uint32_t*)dst, (const uint32_t*)src, bytes / 4, lane);
-  }
-}
-
-struct StepLds { TreeLds* tree; CReq* rq; uint32_t* nrq_out; };
-
-__device__ __forceinline__ void c_tile_step(const CP& P, const CS& S, int p, uint64_t barrier, uint32_t lt, const StepLds* sl);
-
-__global__ void __launch_bounds__(64) k_c_tiles(CP P, CS S, int p, uint64_t barrier)
-{
-  if (*(volatile uint32_t*)S.quiet) return;
-  if (P.tiles_per_block != 1) {
-    const uint32_t lt = blockIdx.x * blockDim.x + threadIdx.x;
-    if (lt == 0) S.ri[GG_RI_STEPS]++;
-    if (lt < P.lt) c_tile_step(P, S, p, barrier, lt, nullptr);
-    return;
-  }
-  const uint32_t lt = blockIdx.x, lane = threadIdx.x;
-  if (lt == 0 && lane == 0) S.ri[GG_RI_STEPS]++;
-  __shared__ TreeLds tl;
-  extern __shared__ __attribute__((aligned(16))) uint8_t csm[];
-  StepLds sl{};
-  const bool tree = P.dram_qm && P.max_list <= kTreeLds && (P.max_list % 2) == 0;
-  const uint32_t qw = sizeof(HQueue) / 4, nw = P.max_list * sizeof(HNode) / 4, fw = (P.max_list + 1) / 2;
-  sl.tree = tree ? &tl : nullptr;
-  if (tree) {
-    copy_words((uint32_t*)&tl.q, (const uint32_t*)(S.dq + lt), qw, lane);
-    copy_words((uint32_t*)tl.nd, (const uint32_t*)(S.dnd + (size_t)lt * P.max_list), nw, lane);
-    copy_words((uint32_t*)tl.fl, (const uint32_t*)(S.dfl + (size_t)lt * P.max_list), fw, lane);
-  }
-  // the directory request FIFO (HashMapList of dram_directory_cntlr.h:46): its
-  // scans are loops of dependent loads; staged when QC entries fit
-  __shared__ uint32_t nrq_out;
-  CReq* grq = S.rq + (size_t)lt * P.QC;
-  if (P.stage_rq) {
-    sl.rq = (CReq*)csm;
-    sl.nrq_out = &nrq_out;
-    copy_words((uint32_t*)sl.rq, (const uint32_t*)grq, S.nrq[lt] * (sizeof(CReq) / 4), lane);
-  }
-  __syncthreads();
-  if (lane == 0) c_tile_step(P, S, p, barrier, lt, &sl);
-  __syncthreads();
-  if (P.stage_rq) copy_words((uint32_t*)grq, (const uint32_t*)sl.rq, nrq_out * (sizeof(CReq) / 4), lane);
-  if (tree) {
-    copy_words((uint32_t*)(S.dq + lt), (const uint32_t*)&tl.q, qw, lane);
-    copy_words((uint32_t*)(S.dnd + (size_t)lt * P.max_list), (const uint32_t*)tl.nd, nw, lane);
-    copy_words((uint32_t*)(S.dfl + (size_t)lt * P.max_list), (const uint32_t*)tl.fl, fw, lane);
-  }
-}
-
-__device__ __forceinline__ void c_tile_step(const CP& P, const CS& S, int p, uint64_t barrier, uint32_t lt, const StepLds* sl)
-{
-  const uint64_t c0 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
-  const uint64_t r0 = S.prof ? __builtin_amdgcn_s_memrealtime() : 0;
-  Tile T(P, S, lt, 1 - p);
-  if (sl && sl->tree) { T.dq = &sl->tree->q; T.dnd = sl->tree->nd; T.dfl = sl->tree->fl; }
-  if (sl && sl->rq) T.rqp = sl->rq;
-  // 1. gather the inbox list
-  int32_t* head = headp(S, p);
-  const gg_cmsg* in = bufp(S, p);
-  uint32_t* idx = S.scratch + (size_t)lt * P.IC;
-  uint32_t n = 0;
-  for (int32_t i = head[lt]; i >= 0; i = (int32_t)in[i].link) {
-    if (n >= P.IC) { T.fail(GG_DERR_CAP); return; }
-    idx[n++] = (uint32_t)i;
-  }
-  head[lt] = -1;
-  // insertion sort by (sender, sequence)
-  for (uint32_t i = 1; i < n; ++i) {
-    const uint32_t v = idx[i];
-    const gg_cmsg& mv = in[v];
-    uint32_t j = i;
-    while (j > 0 && chan_lt(mv, in[idx[j - 1]])) { idx[j] = idx[j - 1]; --j; }
-    idx[j] = v;
-  }
-  const uint64_t c1 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
-  // merge the channels: repeatedly the channel head with the least (arrival, sender)
-  for (uint32_t k = 0; k < n; ++k) {
-    uint32_t best = ~0u, prev_src = ~0u;
-    for (uint32_t i = 0; i < n; ++i) {
-      if (idx[i] == ~0u) continue;
-      const gg_cmsg& m = in[idx[i]];
-      if (m.src == prev_src) continue;               // not the head of its channel
-      prev_src = m.src;
-      if (best == ~0u) { best = i; continue; }
-      const gg_cmsg& b = in[idx[best]];
-      if (m.arrival_ps < b.arrival_ps || (m.arrival_ps == b.arrival_ps && m.src < b.src)) best = i;
+  __device__ __forceinline__ void flush()
+  {
+    L1.flush(); L2.flush();
+    uint64_t* g = S.st + (size_t)lt * GG_NUM_TILE_STATS;
+    for (uint32_t k0 = 0; k0 < GG_NUM_TILE_STATS; k0 += 64) {
+      const uint32_t k = k0 + ln;
+      const uint64_t v = pick(st, k);
+      if (k == GG_CT_CLOCK_PS) g[k] = clk;
+      else if (k < GG_NUM_TILE_STATS && v) g[k] += v;
     }
-    const gg_cmsg m = in[idx[best]];
-    idx[best] = ~0u;
-    T.st[GG_CT_MSGS_RECEIVED]++;
-    const uint64_t h0 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
-    if (to_directory(m.type)) T.directory_msg(m); else T.l2_msg(m);
-    if (S.prof) atomicAdd(&S.prof[to_directory(m.type) ? 5 : 6], (unsigned long long)(__builtin_amdgcn_s_memtime() - h0));
+    S.rec[lt] = rec; S.clk[lt] = clk; S.pend_start[lt] = pend_start;
+    S.out_addr[lt] = out_addr; S.out_time[lt] = out_time;
+    S.blocked[lt] = blocked; S.seq[lt] = seq; S.nrep[lt] = nrep; S.nrq[lt] = nrq;
   }
-  const uint64_t c2 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
-  // 2. the trace
-  const uint64_t line_mask = ~((1ull << P.log_line) - 1);
-  while (!T.blocked) {
-    const uint64_t r = T.rec;
-    if (r >= T.rec_end) break;
-    const uint32_t meta = S.meta[r];
-    const uint64_t s = T.clk + (uint64_t)((meta & 0x7FFFFFFFu) >> 1) * P.gap_ps;
-    if (s >= barrier) break;
-    T.app_access(S.addr[r] & line_mask, (meta & GG_META_WRITE) != 0, s);
+};
+
+// ---------------------------------------------------------------------------
+// ordering helpers (lane-parallel, O(n^2 / 64) compares; arrays in LDS or in
+// the tile's global scratch, each phase closed by a workgroup barrier)
+// ---------------------------------------------------------------------------
+// The reference's per-channel FIFO merged by (arrival, sender): repeatedly the
+// channel head with the least (arrival, sender).  That order is the sort by
+// (P, sender, seq) with P = the largest arrival up to the message in its
+// channel (a head can only leave after its channel's earlier messages, and
+// every head waiting behind a larger arrival inherits it).  a = arrival,
+// k = sender << 32 | seq, idx = record; out = records in processing order.
+__device__ void order_inbox(uint32_t n, const uint64_t* a, const uint64_t* k, uint64_t* pm, const uint32_t* idx,
+                            uint32_t* out, uint32_t ln)
+{
+  for (uint32_t i = ln; i < n; i += 64) {
+    const uint64_t ki = k[i];
+    uint64_t m = 0;
+    for (uint32_t j = 0; j < n; ++j) {
+      const uint64_t kj = k[j];
+      if ((kj >> 32) == (ki >> 32) && kj <= ki) m = max(m, a[j]);
+    }
+    pm[i] = m;
   }
-  const uint64_t c3 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
+  __syncthreads();
+  for (uint32_t i = ln; i < n; i += 64) {
+    const uint64_t pi = pm[i], ki = k[i];
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < n; ++j) { const uint64_t pj = pm[j]; r += (pj < pi) || (pj == pi && k[j] < ki); }
+    out[r] = idx[i];
+  }
+  __syncthreads();
+}
+// (time, send time, sender << 32 | seq) order: a port's service order (the
+// canonical key of DESIGN.md §4)
+__device__ void order_port(uint32_t n, const uint64_t* t, const uint64_t* s, const uint64_t* k, const uint32_t* idx,
+                           uint32_t* out, uint32_t ln)
+{
+  for (uint32_t i = ln; i < n; i += 64) {
+    const uint64_t ti = t[i], si = s[i], ki = k[i];
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < n; ++j) {
+      const uint64_t tj = t[j], sj = s[j], kj = k[j];
+      r += (tj < ti) || (tj == ti && (sj < si || (sj == si && kj < ki)));
+    }
+    out[r] = idx[i];
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void copy_img(void* dst, const void* src, uint32_t bytes, uint32_t ln)
+{
+  uint4* d = (uint4*)dst; const uint4* s = (const uint4*)src;
+  for (uint32_t i = ln; i < bytes / 16; i += 64) d[i] = s[i];
+}
+// the LDS image of one queue (HQueue + max nodes) <-> its HBM storage
+__device__ __forceinline__ void img_in(uint8_t* img, const HQueue* q, const HNode* nd, uint32_t ms, uint32_t ln)
+{
+  copy_img(img, q, sizeof(HQueue), ln);
+  copy_img(img + sizeof(HQueue), nd, ms * sizeof(HNode), ln);
+}
+__device__ __forceinline__ void img_out(HQueue* q, HNode* nd, const uint8_t* img, uint32_t ms, uint32_t ln)
+{
+  copy_img(q, img, sizeof(HQueue), ln);
+  copy_img(nd, img + sizeof(HQueue), ms * sizeof(HNode), ln);
+}
+
+// one router output port + link (RouterModel::processPacket router_model.cc:71-108,
+// ElectricalLinkModel::processPacket electrical_link_model.cc:31-45) on a wave:
+// counters into c[kNetCtr] = {contention, router packets, buffer w+r (each), switch, crossbar, link}
+__device__ __forceinline__ void port_hop(const NocParams& np, HTree& tr, bool wave, uint32_t nf, uint64_t& t,
+                                         uint64_t& zl, uint64_t* c, uint32_t* err, uint32_t ln)
+{
+  uint64_t qd = 0;
+  if (np.qm) {
+    const uint64_t tc = time_to_cycles(t, np.f);
+    qd = wave ? tr.delay_wave(tc, nf, err, ln) : tr.delay(tc, nf, err);
+    c[0] += qd; c[1] += 1;
+  }
+  c[2] += nf; c[3] += 1; c[4] += nf; c[5] += nf;
+  const uint64_t zps = lat_to_ps((uint64_t)np.router_delay + np.link_delay, np.f), cps = lat_to_ps(qd, np.f);
+  t += zps + cps; zl += zps;
+}
+__device__ __forceinline__ void net_ctr_add(uint64_t* ctr, uint32_t tile, const uint64_t* c)
+{
+  cadd(ctr, tile, GG_NC_ROUTER_CONTENTION_CYCLES, c[0]); cadd(ctr, tile, GG_NC_ROUTER_PACKETS, c[1]);
+  cadd(ctr, tile, GG_NC_BUFFER_WRITES, c[2]); cadd(ctr, tile, GG_NC_BUFFER_READS, c[2]);
+  cadd(ctr, tile, GG_NC_SWITCH_ALLOC, c[3]); cadd(ctr, tile, GG_NC_CROSSBAR, c[4]);
+  cadd(ctr, tile, GG_NC_LINK_TRAVERSALS, c[5]);
+}
+
+// ---------------------------------------------------------------------------
+// the step
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t xy_stage_seg(const CP& P, const CS& S, uint32_t cur, uint32_t dst, bool& is_x)
+{
+  const uint32_t cx = cur % P.mw, cy = cur / P.mw, dx = dst % P.mw, dy = dst / P.mw;
+  if (cx != dx) { is_x = true; return S.tseg[(size_t)cur * 2] * 2 + (dx > cx ? 1u : 0u); }
+  is_x = false;
+  return S.tseg[(size_t)cur * 2 + 1] * 2 + (dy > cy ? 1u : 0u);
+}
+
+__global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t k, uint64_t barrier)
+{
+  const uint32_t ln = threadIdx.x, lt = blockIdx.x, p = k & 1u;
+  if (k > 0) {
+    if (*(volatile uint32_t*)S.quiet) return;
+    if (((volatile uint32_t*)S.ring)[(k - 1) & 3] == 0) {   // the previous step sent nothing: the quantum is done
+      if (lt == 0 && ln == 0) *S.quiet = 1;
+      return;
+    }
+  }
+  if (lt == 0 && ln == 0) { S.ri[GG_RI_STEPS]++; S.ring[(k + 2) & 3] = 0; S.npool[p ^ 1u] = 0; }
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  StepLds& sl = *reinterpret_cast<StepLds*>(smem);
+  Tile T(P, S, lt, p, sl);
+  const gg_cmsg* prev = pool(S, p ^ 1u);     // records delivered to this step
+  uint64_t* gscr = S.gscr + (size_t)lt * 5 * P.IC;
+  uint64_t nc_self[kNetCtr] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t rcv[5] = {0, 0, 0, 0, 0};          // packets, flits, bits received, latency, contention
+
+  // ---- 0. hop-by-hop: SELF output port + receive of last step's packets (routePacket
+  // at the receiver, hop_by_hop.cc:223-256; __processReceivedPacket, network_model.cc:118-150)
+  const uint32_t na = P.net == GG_NET_EMESH_HOP_BY_HOP ? narv(S, p)[lt] : 0u;
+  if (na) {
+    const uint32_t* al = arv(S, p) + (size_t)lt * P.IC;
+    const bool lds = na <= kInLds;
+    uint64_t* t_ = lds ? sl.x1 : gscr; uint64_t* s_ = lds ? sl.x2 : gscr + P.IC; uint64_t* k_ = lds ? sl.x3 : gscr + 2 * P.IC;
+    uint32_t* i_ = lds ? sl.i1 : (uint32_t*)(gscr + 3 * P.IC); uint32_t* o_ = lds ? sl.i2 : (uint32_t*)(gscr + 4 * P.IC);
+    for (uint32_t i = ln; i < na; i += 64) {
+      const uint32_t r = al[i];
+      const gg_cmsg& m = prev[r];
+      t_[i] = m.arrival_ps; s_[i] = m.send_ps; k_[i] = ((uint64_t)m.src << 32) | m.seq; i_[i] = r;
+    }
+    __syncthreads();
+    order_port(na, t_, s_, k_, i_, o_, ln);
+    const uint64_t qi = (uint64_t)T.tile * 6 + P_SELF;
+    HTree tr{S.nq + qi, S.nnd + qi * P.np.max_size, 1, P.np.analytical != 0};
+    const bool wave = P.np.qm && P.np.max_size <= kQMax;
+    if (wave) {
+      img_in(sl.pimg, S.nq + qi, S.nnd + qi * P.np.max_size, P.np.max_size, ln);
+      __syncthreads();
+      tr.q = reinterpret_cast<HQueue*>(sl.pimg); tr.nd = reinterpret_cast<HNode*>(sl.pimg + sizeof(HQueue));
+    }
+    for (uint32_t j = 0; j < na; ++j) {
+      const uint32_t r = o_[j];
+      gg_cmsg* m = const_cast<gg_cmsg*>(prev) + r;
+      const uint32_t bits = has_data(m->type) ? P.bits_data : P.bits_req;
+      const uint32_t nf = (uint32_t)nflits(P.np, bits);
+      uint64_t t = m->arrival_ps, zl = m->zero_load_ps;
+      port_hop(P.np, tr, wave, nf, t, zl, nc_self, S.err, ln);
+      const uint64_t ser = lat_to_ps(nf, P.np.f);
+      t += ser; zl += ser;
+      const uint64_t ct = t - m->send_ps - zl;
+      rcv[0] += 1; rcv[1] += nf; rcv[2] += bits; rcv[3] += zl + ct; rcv[4] += ct;
+      m->arrival_ps = t; m->zero_load_ps = zl;
+    }
+    if (wave) { __syncthreads(); img_out(S.nq + qi, S.nnd + qi * P.np.max_size, sl.pimg, P.np.max_size, ln); }
+    narv(S, p)[lt] = 0;
+    __syncthreads();
+  }
+
+  // ---- 1. the inbox, per-channel FIFO, channels merged by (arrival, sender)
+  const uint32_t ni = ninb(S, p)[lt];
+  const uint32_t n = ni + na;
+  // directory request FIFO in LDS when it cannot outgrow it this step
+  if (T.nrq + 2 * n + 2 <= kRqLds) {
+    const CReq* g = S.rq + (size_t)lt * P.QC;
+    for (uint32_t i = ln; i < T.nrq; i += 64) sl.rq[i] = g[i];
+    T.rqp = sl.rq; T.rq_lds = true;
+  }
+  if (P.dram_qm && P.max_list <= kQMax && n) {
+    img_in(sl.dimg, T.dq, T.dnd, P.max_list, ln);
+    T.dq = reinterpret_cast<HQueue*>(sl.dimg); T.dnd = reinterpret_cast<HNode*>(sl.dimg + sizeof(HQueue));
+    T.dq_lds = true;
+  }
+  __syncthreads();
+  if (n) {
+    const bool lds = n <= kInLds;
+    uint64_t* a_ = lds ? sl.x1 : gscr; uint64_t* k_ = lds ? sl.x2 : gscr + P.IC; uint64_t* m_ = lds ? sl.x3 : gscr + 2 * P.IC;
+    uint32_t* i_ = lds ? sl.i1 : (uint32_t*)(gscr + 3 * P.IC); uint32_t* o_ = lds ? sl.i2 : (uint32_t*)(gscr + 4 * P.IC);
+    const uint32_t* il = inb(S, p) + (size_t)lt * P.IC;
+    const uint32_t* al = arv(S, p) + (size_t)lt * P.IC;
+    for (uint32_t i = ln; i < n; i += 64) {
+      const uint32_t r = i < ni ? il[i] : al[i - ni];
+      const gg_cmsg& m = prev[r];
+      a_[i] = m.arrival_ps; k_[i] = ((uint64_t)m.src << 32) | m.seq; i_[i] = r;
+    }
+    __syncthreads();
+    ninb(S, p)[lt] = 0;
+    order_inbox(n, a_, k_, m_, i_, o_, ln);
+    for (uint32_t j = 0; j < n && !T.failed; ++j) {
+      const gg_cmsg m = prev[o_[j]];
+      T.st[GG_CT_MSGS_RECEIVED]++;
+      if (to_directory(m.type)) T.directory_msg(m); else T.l2_msg(m);
+    }
+  }
+
+  // ---- 2. the trace (records fetched 64 at a time, one per lane)
+  {
+    const uint64_t line_mask = ~((1ull << P.log_line) - 1);
+    uint64_t wbase = ~0ull, wa = 0;
+    uint32_t wm = 0;
+    while (!T.blocked && !T.failed) {
+      const uint64_t r = T.rec;
+      if (r >= T.rec_end) break;
+      if (wbase == ~0ull || r >= wbase + 64) {
+        wbase = r;
+        wa = 0; wm = 0;
+        if (r + ln < T.rec_end) { wa = S.addr[r + ln]; wm = S.meta[r + ln]; }
+      }
+      const int o = (int)(r - wbase);
+      const uint32_t meta = (uint32_t)__shfl((int)wm, o);
+      const uint64_t s = T.clk + (uint64_t)((meta & 0x7FFFFFFFu) >> 1) * P.gap_ps;
+      if (s >= barrier) break;
+      T.app_access(shfl64(wa, o) & line_mask, (meta & GG_META_WRITE) != 0, s);
+    }
+  }
+
+  // ---- 3. publish this step's records
+  if (T.nch) sl.ch[2 * (T.nch - 1) + 1] = T.cused;
+  __syncthreads();
+  gg_cmsg* cur = pool(S, p);
+  const uint32_t np_ = T.nsent;
+  uint64_t ri_net = 0, ri_self = 0, ri_bnd = 0;
+  if (np_) {
+    const bool lds = np_ <= kInLds;
+    uint64_t* t_ = lds ? sl.x1 : gscr; uint64_t* s_ = lds ? sl.x2 : gscr + P.IC; uint64_t* k_ = lds ? sl.x3 : gscr + 2 * P.IC;
+    uint32_t* i_ = lds ? sl.i1 : (uint32_t*)(gscr + 3 * P.IC); uint32_t* o_ = lds ? sl.i2 : (uint32_t*)(gscr + 4 * P.IC);
+    if (!lds && np_ > P.IC) T.fail(GG_DERR_CAP);
+    // the records of the chunks, in allocation order
+    uint32_t off = 0;
+    for (uint32_t c = 0; c < T.nch && !T.failed; ++c) {
+      const uint32_t b = sl.ch[2 * c], u = sl.ch[2 * c + 1];
+      for (uint32_t r = ln; r < u; r += 64) i_[off + r] = b + r;
+      off += u;
+    }
+    __syncthreads();
+    const uint32_t nloc = T.failed ? 0u : off;
+    if (P.net != GG_NET_EMESH_HOP_BY_HOP) {
+      // NetworkModel::routePacket closed form (hop counter / magic) + delivery
+      for (uint32_t i = ln; i < nloc; i += 64) {
+        const uint32_t r = i_[i];
+        gg_cmsg m = cur[r];
+        uint64_t zl;
+        m.arrival_ps = route_closed_form(P.np, m.src, m.dst, has_data(m.type) ? P.bits_data : P.bits_req, m.send_ps,
+                                         zl, S.ctr);
+        m.zero_load_ps = zl;
+        if (m.src == m.dst) ri_self++; else ri_net++;
+        if (S.shard[m.src] == S.shard[m.dst]) {
+          const int32_t ld = S.ltile[m.dst];
+          const uint32_t j = atomicAdd(&ninb(S, p ^ 1u)[ld], 1u);
+          if (j >= P.IC) { atomicOr(S.err, GG_DERR_CAP); continue; }
+          cur[r].arrival_ps = m.arrival_ps; cur[r].zero_load_ps = zl;
+          inb(S, p ^ 1u)[(size_t)ld * P.IC + j] = r;
+        } else {
+          const uint32_t j = atomicAdd(S.bnd_cnt, 1u);
+          if (j >= P.msg_cap) { atomicOr(S.err, GG_DERR_CAP); continue; }
+          S.bnd[j] = m;
+          ri_bnd++;
+        }
+      }
+    } else {
+      // self-sends: straight to the next inbox (processCornerCases, network_model.cc:413-424)
+      uint32_t nn = 0;
+      for (uint32_t i0 = 0; i0 < nloc; i0 += 64) {
+        const uint32_t i = i0 + ln;
+        bool self = false, net = false;
+        uint32_t r = 0;
+        if (i < nloc) { r = i_[i]; self = cur[r].dst == T.tile; net = !self; }
+        if (self) {
+          const uint32_t j = atomicAdd(&ninb(S, p ^ 1u)[lt], 1u);
+          if (j >= P.IC) atomicOr(S.err, GG_DERR_CAP);
+          else inb(S, p ^ 1u)[(size_t)lt * P.IC + j] = r;
+          ri_self++;
+        }
+        const uint64_t m = __ballot(net);
+        const uint32_t pos = nn + (uint32_t)__builtin_popcountll(m & ((1ull << ln) - 1));
+        if (net) {
+          const gg_cmsg& g = cur[r];
+          t_[pos] = g.send_ps; s_[pos] = g.send_ps; k_[pos] = ((uint64_t)g.src << 32) | g.seq; o_[pos] = r;
+          ri_net++;
+        }
+        nn += (uint32_t)__builtin_popcountll(m);
+      }
+      __syncthreads();
+      if (nn) {
+        // the injection port (routePacket SEND_TILE, hop_by_hop.cc:151-159) in (time, key) order
+        for (uint32_t i = ln; i < nn; i += 64) i_[i] = o_[i];
+        __syncthreads();
+        order_port(nn, t_, s_, k_, i_, o_, ln);
+        const uint64_t qi = (uint64_t)T.tile * 6 + P_INJ;
+        HTree tr{S.nq + qi, S.nnd + qi * P.np.max_size, 1, P.np.analytical != 0};
+        const bool wave = P.np.qm && P.np.max_size <= kQMax;
+        if (wave) {
+          img_in(sl.pimg, S.nq + qi, S.nnd + qi * P.np.max_size, P.np.max_size, ln);
+          __syncthreads();
+          tr.q = reinterpret_cast<HQueue*>(sl.pimg); tr.nd = reinterpret_cast<HNode*>(sl.pimg + sizeof(HQueue));
+        }
+        uint64_t ps = 0, fs = 0, bs = 0;
+        for (uint32_t j = 0; j < nn; ++j) {
+          const uint32_t r = o_[j];
+          gg_cmsg* g = cur + r;
+          const uint32_t bits = has_data(g->type) ? P.bits_data : P.bits_req;
+          const uint64_t nf = nflits(P.np, bits);
+          ps += 1; fs += nf; bs += bits;                               // updateSendCounters (network_model.cc:228-251)
+          uint64_t qd = 0;
+          if (P.np.qm) {
+            const uint64_t tc = time_to_cycles(g->send_ps, P.np.f);
+            qd = wave ? tr.delay_wave(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err);
+          }
+          g->arrival_ps = g->send_ps + lat_to_ps(0, P.np.f) + lat_to_ps(qd, P.np.f);
+          g->zero_load_ps = 0;
+          g->hop = T.tile;
+        }
+        if (wave) { __syncthreads(); img_out(S.nq + qi, S.nnd + qi * P.np.max_size, sl.pimg, P.np.max_size, ln); }
+        if (ln == 0) {
+          cadd(S.ctr, T.tile, GG_NC_PACKETS_SENT, ps); cadd(S.ctr, T.tile, GG_NC_FLITS_SENT, fs);
+          cadd(S.ctr, T.tile, GG_NC_BITS_SENT, bs);
+        }
+        __syncthreads();
+        // onto the X (or Y) segment the packet enters
+        for (uint32_t i = ln; i < nn; i += 64) {
+          const uint32_t r = o_[i];
+          bool is_x;
+          const uint32_t sg = xy_stage_seg(P, S, T.tile, cur[r].dst, is_x);
+          uint32_t* cnt = is_x ? S.nxl : S.nyl;
+          const uint32_t j = atomicAdd(&cnt[sg], 1u);
+          if (j >= P.seg_cap) { atomicOr(S.err, GG_DERR_CAP); continue; }
+          (is_x ? S.xl : S.yl)[(size_t)sg * P.seg_cap + j] = r;
+        }
+      }
+    }
+  }
+
+  // ---- 4. write back
+  if (T.rq_lds) {
+    CReq* g = S.rq + (size_t)lt * P.QC;
+    for (uint32_t i = ln; i < T.nrq; i += 64) g[i] = sl.rq[i];
+  }
+  if (T.dq_lds) img_out(S.dq + lt, S.dnd + (size_t)lt * P.max_list, sl.dimg, P.max_list, ln);
   T.flush();
-  if (sl && sl->nrq_out) *sl->nrq_out = T.nrq;
-  if (S.prof) {
-    const uint64_t c4 = __builtin_amdgcn_s_memtime();
-    atomicAdd(&S.prof[0], (unsigned long long)(c1 - c0));     // tile load + inbox gather + sort
-    atomicAdd(&S.prof[1], (unsigned long long)(c2 - c1));     // message handlers
-    atomicAdd(&S.prof[2], (unsigned long long)(c3 - c2));     // trace
-    atomicAdd(&S.prof[3], (unsigned long long)(c4 - c3));     // flush
-    atomicAdd(&S.prof[4], (unsigned long long)n);
-    atomicAdd(&S.prof[7], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - r0));   // 100 MHz ticks
-    const uint32_t st = (uint32_t)S.ri[GG_RI_STEPS];
-    if (st < S.prof_steps) atomicMax(&S.prof[16 + st], (unsigned long long)(c4 - c0));
+  // NoC counters of the tile's own SELF port and receiver
+  {
+    if (ln == 0 && na) {
+      net_ctr_add(S.ctr, T.tile, nc_self);
+      cadd(S.ctr, T.tile, GG_NC_PACKETS_RECEIVED, rcv[0]); cadd(S.ctr, T.tile, GG_NC_FLITS_RECEIVED, rcv[1]);
+      cadd(S.ctr, T.tile, GG_NC_BITS_RECEIVED, rcv[2]); cadd(S.ctr, T.tile, GG_NC_TOTAL_LATENCY_PS, rcv[3]);
+      cadd(S.ctr, T.tile, GG_NC_TOTAL_CONTENTION_PS, rcv[4]);
+    }
+  }
+  {
+    const uint32_t a = wave_sum((uint32_t)ri_net), b = wave_sum((uint32_t)ri_self), c = wave_sum((uint32_t)ri_bnd);
+    if (ln == 0) {
+      if (a) atomicAdd((unsigned long long*)&S.ri[GG_RI_NET_MSGS], (unsigned long long)a);
+      if (b) atomicAdd((unsigned long long*)&S.ri[GG_RI_SELF_MSGS], (unsigned long long)b);
+      if (c) atomicAdd((unsigned long long*)&S.ri[GG_RI_BOUNDARY_MSGS], (unsigned long long)c);
+      if (np_) atomicAdd(&S.ring[k & 3], np_);
+    }
   }
 }
 
-// A step's messages: network latency (closed form, or the arrival the
-// hop-by-hop pipeline computed), then delivery (same shard: the next step's
-// inbox list; otherwise the quantum-boundary buffer).
-__global__ void k_c_route(CP P, CS S, int p, const uint64_t* hbh_arrival)
+// ---------------------------------------------------------------------------
+// hop-by-hop: one wave per X (stage 0) or Y (stage 1) segment
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_c_walk(CP P, CS S, uint32_t k, int stage)
 {
   if (*(volatile uint32_t*)S.quiet) return;
-  const int po = 1 - p;
-  const uint32_t n = min(S.cnt[po], (uint32_t)P.msg_cap);
-  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid == 0) {
-    if (n == 0) *S.quiet = 1;
-    S.cnt[p] = 0;                                  // the outbox of the next step
+  const uint32_t ln = threadIdx.x, sg = blockIdx.x, p = k & 1u;
+  uint32_t* cntp = (stage == 0 ? S.nxl : S.nyl) + sg;
+  const uint32_t n0 = *cntp;
+  if (n0 == 0) return;
+  const uint32_t n = min(n0, P.seg_cap);
+  const uint32_t* list = (stage == 0 ? S.xl : S.yl) + (size_t)sg * P.seg_cap;
+  const Seg sd = (stage == 0 ? S.segx : S.segy)[sg >> 1];
+  const uint32_t dir = sg & 1u;
+  const int port = stage == 0 ? (dir ? P_RIGHT : P_LEFT) : (dir ? P_UP : P_DOWN);
+  auto tile_at = [&](uint32_t pos) -> uint32_t { return stage == 0 ? sd.line * P.mw + pos : pos * P.mw + sd.line; };
+  auto pos_of = [&](uint32_t tile) -> uint32_t { return stage == 0 ? tile % P.mw : tile / P.mw; };
+  gg_cmsg* cur = pool(S, p);
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t npos = sd.hi - sd.lo + 1;
+  uint8_t* qimg = smem;
+  uint64_t* lc = reinterpret_cast<uint64_t*>(smem + (size_t)npos * P.qimg);     // [npos][kNetCtr]
+  uint8_t* pk = reinterpret_cast<uint8_t*>(lc + (size_t)npos * kNetCtr);
+  if (n > P.walk_pk) { if (ln == 0) atomicOr(S.err, GG_DERR_CAP); if (ln == 0) *cntp = 0; return; }
+  uint64_t* Pt = reinterpret_cast<uint64_t*>(pk);
+  uint64_t* Ph = Pt + P.walk_pk; uint64_t* Pk = Ph + P.walk_pk; uint64_t* Pz = Pk + P.walk_pk;
+  uint32_t* Pi = reinterpret_cast<uint32_t*>(Pz + P.walk_pk);
+  uint32_t* Pp = Pi + P.walk_pk; uint32_t* Pd = Pp + P.walk_pk; uint32_t* Pf = Pd + P.walk_pk;   // pos, exit pos, flits | status << 24
+  for (uint32_t i = ln; i < n; i += 64) {
+    const uint32_t r = list[i];
+    const gg_cmsg& m = cur[r];
+    Pt[i] = m.arrival_ps; Ph[i] = m.send_ps; Pk[i] = ((uint64_t)m.src << 32) | m.seq; Pz[i] = m.zero_load_ps;
+    Pi[i] = r; Pp[i] = pos_of(m.hop); Pd[i] = pos_of(m.dst);
+    Pf[i] = (uint32_t)nflits(P.np, has_data(m.type) ? P.bits_data : P.bits_req);
   }
-  gg_cmsg* B = bufp(S, po);
-  int32_t* head = headp(S, po);
-  for (uint32_t i = gid; i < n; i += gridDim.x * blockDim.x) {
-    gg_cmsg m = B[i];
-    if (hbh_arrival) {
-      m.arrival_ps = hbh_arrival[i];
-    } else {
-      uint64_t zl;
-      m.arrival_ps = route_closed_form(P.np, m.src, m.dst, has_data(m.type) ? P.bits_data : P.bits_req,
-                                       m.send_ps, zl, S.ctr);
+  for (uint32_t i = ln; i < npos * kNetCtr; i += 64) lc[i] = 0;
+  __syncthreads();
+  // the queues of the positions the packets can visit
+  uint32_t lo = ~0u, hi = 0;
+  for (uint32_t i = ln; i < n; i += 64) {
+    const uint32_t a = Pp[i], z = Pd[i];
+    const uint32_t zz = dir ? min(z - 1, sd.hi) : max(z + 1, sd.lo);
+    lo = min(lo, min(a, zz)); hi = max(hi, max(a, zz));
+  }
+  lo = wave_min(lo);
+  hi = (uint32_t)(~wave_min(~hi));
+  const bool qm = P.np.qm != 0;
+  if (qm)
+    for (uint32_t q = lo; q <= hi; ++q) {
+      const uint64_t qi = (uint64_t)tile_at(q) * 6 + port;
+      img_in(qimg + (size_t)(q - sd.lo) * P.qimg, S.nq + qi, S.nnd + qi * P.np.max_size, P.np.max_size, ln);
     }
-    atomicAdd((unsigned long long*)&S.ri[m.src == m.dst ? GG_RI_SELF_MSGS : GG_RI_NET_MSGS], 1ull);
-    const uint32_t ss = (uint32_t)(((uint64_t)m.src * P.K) / P.T), ds = (uint32_t)(((uint64_t)m.dst * P.K) / P.T);
-    if (ss == ds) {
-      m.link = (uint32_t)atomicExch(&head[m.dst - P.tb], (int32_t)i);
-      B[i] = m;
-    } else {
+  __syncthreads();
+  // events in (time, send time, sender << 32 | seq) order
+  for (;;) {
+    uint64_t bt = ~0ull, bh = ~0ull, bk = ~0ull;
+    uint32_t bi = ~0u;
+    for (uint32_t i = ln; i < n; i += 64) {
+      if (Pf[i] >> 24) continue;
+      const uint64_t t = Pt[i], h = Ph[i], kk = Pk[i];
+      if (t < bt || (t == bt && (h < bh || (h == bh && kk < bk)))) { bt = t; bh = h; bk = kk; bi = i; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint64_t t = shfl64(bt, ln ^ o), h = shfl64(bh, ln ^ o), kk = shfl64(bk, ln ^ o);
+      const uint32_t i = (uint32_t)__shfl((int)bi, ln ^ o);
+      if (t < bt || (t == bt && (h < bh || (h == bh && kk < bk)))) { bt = t; bh = h; bk = kk; bi = i; }
+    }
+    if (bi == ~0u) break;
+    const uint32_t i = bi;
+    const uint32_t c = Pp[i], d = Pd[i], nf = Pf[i] & 0xFFFFFFu;
+    uint64_t t = Pt[i], zl = Pz[i];
+    HTree tr{reinterpret_cast<HQueue*>(qimg + (size_t)(c - sd.lo) * P.qimg),
+             reinterpret_cast<HNode*>(qimg + (size_t)(c - sd.lo) * P.qimg + sizeof(HQueue)), 1, P.np.analytical != 0};
+    uint64_t cc[kNetCtr] = {0, 0, 0, 0, 0, 0, 0};
+    port_hop(P.np, tr, P.np.max_size <= kQMax, nf, t, zl, cc, S.err, ln);
+    const uint32_t nx = dir ? c + 1 : c - 1;
+    uint32_t status = 0;
+    if (nx < sd.lo || nx > sd.hi) status = 2;                  // next router in another shard: held
+    else if (nx == d) status = 1;                              // leaves the chain: next stage
+    wave_sync();
+    if (ln == 0) {
+      Pt[i] = t; Pz[i] = zl; Pp[i] = nx; Pf[i] = nf | (status << 24);
+      uint64_t* l = lc + (size_t)(c - sd.lo) * kNetCtr;
+#pragma unroll
+      for (int q = 0; q < (int)kNetCtr; ++q) l[q] += cc[q];
+    }
+    wave_sync();
+  }
+  __syncthreads();
+  // hand-off
+  uint32_t nb = 0;
+  for (uint32_t i = ln; i < n; i += 64) {
+    const uint32_t r = Pi[i], stt = Pf[i] >> 24;
+    const uint32_t h = tile_at(Pp[i]);
+    gg_cmsg* m = cur + r;
+    m->arrival_ps = Pt[i]; m->zero_load_ps = Pz[i]; m->hop = h;
+    if (stt == 2) {                                            // held for the quantum boundary
       const uint32_t j = atomicAdd(S.bnd_cnt, 1u);
       if (j >= P.msg_cap) { atomicOr(S.err, GG_DERR_CAP); continue; }
-      S.bnd[j] = m;
-      atomicAdd((unsigned long long*)&S.ri[GG_RI_BOUNDARY_MSGS], 1ull);
+      gg_cmsg g = *m;
+      g.arrival_ps = Pt[i]; g.zero_load_ps = Pz[i]; g.hop = h;
+      S.bnd[j] = g;
+      ++nb;
+      continue;
+    }
+    const uint32_t dst = m->dst;
+    if (h == dst) {                                            // the SELF port of the destination, next step
+      const int32_t ld = S.ltile[dst];
+      const uint32_t j = atomicAdd(&narv(S, p ^ 1u)[ld], 1u);
+      if (j >= P.IC) { atomicOr(S.err, GG_DERR_CAP); continue; }
+      arv(S, p ^ 1u)[(size_t)ld * P.IC + j] = r;
+    } else {                                                   // X done: the Y segment of the destination column
+      bool is_x;
+      const uint32_t s2 = xy_stage_seg(P, S, h, dst, is_x);
+      const uint32_t j = atomicAdd(&S.nyl[s2], 1u);
+      if (j >= P.seg_cap) { atomicOr(S.err, GG_DERR_CAP); continue; }
+      S.yl[(size_t)s2 * P.seg_cap + j] = r;
     }
   }
-}
-
-// hop-by-hop: the step's messages as packets, keyed (send time, sender, sequence)
-// — the order the oracle routes a step's batch in (oracle/gg_coherent.inc c_route_step)
-__global__ void k_c_packets(CP P, CS S, int p)
-{
-  if (*(volatile uint32_t*)S.quiet) return;
-  const int po = 1 - p;
-  const uint32_t n = min(S.cnt[po], (uint32_t)P.msg_cap);
-  const gg_cmsg* B = bufp(S, po);
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const gg_cmsg m = B[i];
-    S.pk_src[i] = m.src; S.pk_dst[i] = m.dst;
-    S.pk_len[i] = has_data(m.type) ? P.bits_data : P.bits_req;
-    S.pk_t0[i] = m.send_ps; S.pk_khi[i] = m.send_ps; S.pk_klo[i] = ((uint64_t)m.src << 32) | m.seq;
+  nb = wave_sum(nb);
+  if (ln == 0 && nb) atomicAdd((unsigned long long*)&S.ri[GG_RI_BOUNDARY_MSGS], (unsigned long long)nb);
+  if (qm)
+    for (uint32_t q = lo; q <= hi; ++q) {
+      const uint64_t qi = (uint64_t)tile_at(q) * 6 + port;
+      img_out(S.nq + qi, S.nnd + qi * P.np.max_size, qimg + (size_t)(q - sd.lo) * P.qimg, P.np.max_size, ln);
+    }
+  for (uint32_t i = ln; i < npos * 6u; i += 64) {
+    const uint32_t q = i / 6, f = i % 6;
+    const uint64_t* l = lc + (size_t)q * kNetCtr;
+    const uint32_t tl = tile_at(sd.lo + q);
+    switch (f) {
+    case 0: cadd(S.ctr, tl, GG_NC_ROUTER_CONTENTION_CYCLES, l[0]); break;
+    case 1: cadd(S.ctr, tl, GG_NC_ROUTER_PACKETS, l[1]); break;
+    case 2: cadd(S.ctr, tl, GG_NC_BUFFER_WRITES, l[2]); cadd(S.ctr, tl, GG_NC_BUFFER_READS, l[2]); break;
+    case 3: cadd(S.ctr, tl, GG_NC_SWITCH_ALLOC, l[3]); break;
+    case 4: cadd(S.ctr, tl, GG_NC_CROSSBAR, l[4]); break;
+    default: cadd(S.ctr, tl, GG_NC_LINK_TRAVERSALS, l[5]); break;
+    }
   }
+  if (ln == 0) *cntp = 0;
 }
 
-// Deliver imported (boundary) messages into the inbox of the quantum's first step.
+// Deliver the records of the quantum boundary: messages into the inbox of the
+// quantum's first step (records in pool 1), held packets back into the walk
+// of that step (records in pool 0): the X / Y segment at their router, or
+// the destination's SELF list of step 1.
 __global__ void k_c_import(CP P, CS S, const gg_cmsg* in, uint32_t n)
 {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  gg_cmsg m = in[i];
-  if (m.dst < P.tb || m.dst >= P.tb + P.lt) { atomicOr(S.err, GG_DERR_STATE); return; }
-  m.link = (uint32_t)atomicExch(&S.head0[m.dst - P.tb], (int32_t)i);
-  S.buf0[i] = m;
+  const gg_cmsg m = in[i];
+  const uint32_t at = m.hop == GG_HOP_NONE ? m.dst : m.hop;
+  if (at >= P.T || m.dst >= P.T || S.ltile[at] < 0) { atomicOr(S.err, GG_DERR_STATE); return; }
+  if (m.hop == GG_HOP_NONE) {
+    const uint32_t r = atomicAdd(&S.npool[1], 1u);
+    if (r >= P.msg_cap) { atomicOr(S.err, GG_DERR_CAP); return; }
+    S.pool1[r] = m;
+    const int32_t ld = S.ltile[m.dst];
+    const uint32_t j = atomicAdd(&S.ninb0[ld], 1u);
+    if (j >= P.IC) { atomicOr(S.err, GG_DERR_CAP); return; }
+    S.inb0[(size_t)ld * P.IC + j] = r;
+    return;
+  }
+  const uint32_t r = atomicAdd(&S.npool[0], 1u);
+  if (r >= P.msg_cap) { atomicOr(S.err, GG_DERR_CAP); return; }
+  S.pool0[r] = m;
+  atomicAdd(&S.ring[0], 1u);
+  if (m.hop == m.dst) {
+    const int32_t ld = S.ltile[m.dst];
+    const uint32_t j = atomicAdd(&S.narv1[ld], 1u);
+    if (j >= P.IC) { atomicOr(S.err, GG_DERR_CAP); return; }
+    S.arv1[(size_t)ld * P.IC + j] = r;
+    return;
+  }
+  bool is_x;
+  const uint32_t sg = xy_stage_seg(P, S, m.hop, m.dst, is_x);
+  uint32_t* cnt = is_x ? S.nxl : S.nyl;
+  const uint32_t j = atomicAdd(&cnt[sg], 1u);
+  if (j >= P.seg_cap) { atomicOr(S.err, GG_DERR_CAP); return; }
+  (is_x ? S.xl : S.yl)[(size_t)sg * P.seg_cap + j] = r;
 }
 
 // Status after a quantum: active / blocked tiles, least next-access start.
 __global__ void k_c_status(CP P, CS S, uint64_t* out /* [active, blocked, min_next] */)
 {
   const uint32_t lt = blockIdx.x * blockDim.x + threadIdx.x;
-  if (lt >= P.lt) return;
+  if (lt >= P.L) return;
   const uint64_t r = S.rec[lt];
   if (r >= S.rec_end[lt]) return;
   atomicAdd((unsigned long long*)&out[0], 1ull);
@@ -1052,7 +1462,7 @@ __global__ void k_c_status(CP P, CS S, uint64_t* out /* [active, blocked, min_ne
 __global__ void k_c_reset(CP P, CS S, const uint64_t* offs)
 {
   const uint32_t lt = blockIdx.x * blockDim.x + threadIdx.x;
-  if (lt >= P.lt) return;
+  if (lt >= P.L) return;
   for (uint32_t i = 0; i < P.s1 * P.a1; ++i) { S.l1_tag[(size_t)lt * P.s1 * P.a1 + i] = INV_ADDR;
                                                S.l1_meta[(size_t)lt * P.s1 * P.a1 + i] = (uint8_t)((i % P.a1) << 3); }
   for (uint32_t i = 0; i < P.s1; ++i) S.l1_rr[(size_t)lt * P.s1 + i] = (uint8_t)(P.a1 - 1);
@@ -1064,38 +1474,41 @@ __global__ void k_c_reset(CP P, CS S, const uint64_t* offs)
   for (uint32_t i = 0; i < P.E; ++i) S.dir[(size_t)lt * P.E + i] = DEnt{INV_ADDR, -1, DS_UNCACHED, 0};
   for (uint64_t i = 0; i < (uint64_t)P.E * P.W; ++i) S.dsh[(size_t)lt * P.E * P.W + i] = 0;
   S.nrep[lt] = 0; S.nrq[lt] = 0;
-  const uint32_t tile = P.tb + lt;
+  const uint32_t tile = S.gtile[lt];
   S.rec[lt] = offs[tile]; S.rec_end[lt] = offs[tile + 1];
   S.clk[lt] = 0; S.pend_start[lt] = 0; S.out_addr[lt] = INV_ADDR; S.out_time[lt] = 0;
   S.blocked[lt] = 0; S.seq[lt] = 0;
-  S.head0[lt] = -1; S.head1[lt] = -1;
+  S.ninb0[lt] = 0; S.ninb1[lt] = 0; S.narv0[lt] = 0; S.narv1[lt] = 0;
   if (P.dram_qm)                                     // QueueModel::create(dram/queue_model/type, min_processing_time)
-    hq_init(S.dq + lt, S.dnd + (size_t)lt * P.max_list, S.dfl + (size_t)lt * P.max_list, P.max_list, P.dram_qtype,
-            P.dram_qaux);
+    hq_init(S.dq + lt, S.dnd + (size_t)lt * P.max_list, P.max_list, P.dram_qtype, P.dram_qaux);
 }
 
 __global__ void k_c_final_stats(CP P, CS S)
 {
   const uint32_t lt = blockIdx.x * blockDim.x + threadIdx.x;
-  if (lt >= P.lt || !P.dram_qm) return;
+  if (lt >= P.L || !P.dram_qm) return;
   S.st[(size_t)lt * GG_NUM_TILE_STATS + GG_CT_DRAM_QUEUE_ANALYTICAL] = S.dq[lt].analytical;
   S.st[(size_t)lt * GG_NUM_TILE_STATS + GG_CT_DRAM_QUEUE_UTILIZED_NS] = S.dq[lt].util;
   S.st[(size_t)lt * GG_NUM_TILE_STATS + GG_CT_DRAM_QUEUE_LAST_NS] = S.dq[lt].last_req;
 }
 
-// export: group the boundary messages by destination shard
-__global__ void k_c_export_count(CP P, const gg_cmsg* b, uint32_t n, uint32_t* counts)
+// export: group the boundary records by the shard they continue in
+__device__ __forceinline__ uint32_t rec_shard(const CS& S, const gg_cmsg& m)
+{
+  return S.shard[m.hop == GG_HOP_NONE ? m.dst : m.hop];
+}
+__global__ void k_c_export_count(CS S, const gg_cmsg* b, uint32_t n, uint32_t* counts)
 {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  atomicAdd(&counts[((uint64_t)b[i].dst * P.K) / P.T], 1u);
+  atomicAdd(&counts[rec_shard(S, b[i])], 1u);
 }
-__global__ void k_c_export_scatter(CP P, const gg_cmsg* b, uint32_t n, const uint32_t* base, uint32_t* cursor,
+__global__ void k_c_export_scatter(CS S, const gg_cmsg* b, uint32_t n, const uint32_t* base, uint32_t* cursor,
                                    gg_cmsg* out)
 {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint32_t k = (uint32_t)(((uint64_t)b[i].dst * P.K) / P.T);
+  const uint32_t k = rec_shard(S, b[i]);
   out[base[k] + atomicAdd(&cursor[k], 1u)] = b[i];
 }
 
@@ -1112,6 +1525,7 @@ struct gg_coh_state {
   uint32_t* ecount_dev = nullptr;    // export counts + cursors
   uint64_t* offs_dev = nullptr;
   uint64_t n_records = 0;
+  size_t step_lds = 0, walk_lds = 0;
   bool begun = false;
 };
 
@@ -1124,6 +1538,14 @@ template <class T> static gg_status dalloc(gg_coh_state* C, T** p, uint64_t n)
   hipError_t e = hipMalloc((void**)p, sizeof(T) * (n ? n : 1));
   if (e != hipSuccess) return gg_hip_check(e, "hipMalloc(coherent state)");
   C->allocs.push_back((void*)*p);
+  return GG_OK;
+}
+template <class T> static gg_status dupload(gg_coh_state* C, const T** p, const std::vector<T>& v)
+{
+  T* d = nullptr;
+  if (gg_status st = dalloc(C, &d, v.size())) return st;
+  if (!v.empty()) GG_HIP(hipMemcpy(d, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice));
+  *p = d;
   return GG_OK;
 }
 
@@ -1143,18 +1565,38 @@ static gg_status coh_alloc(gg_ctx* ctx)
   gg_coh_state* C = new gg_coh_state();
   ctx->coh = C;
   CP& P = C->P;
+  CS& S = C->S;
   P.T = c.num_tiles;
   P.K = c.num_shards ? c.num_shards : 1;
   const uint32_t k0 = c.shard_begin, k1 = c.shard_end ? c.shard_end : P.K;
   if (k0 >= k1 || k1 > P.K || P.K > P.T) return gg_fail(GG_ERR_INVALID, "bad shard range [%u, %u) of %u", k0, k1, P.K);
-  // tiles of shard k: { t : t*K/T == k } = [ceil(k*T/K), ceil((k+1)*T/K))
-  P.tb = (uint32_t)(((uint64_t)k0 * P.T + P.K - 1) / P.K);
-  const uint32_t te = (uint32_t)(((uint64_t)k1 * P.T + P.K - 1) / P.K);
-  P.lt = te - P.tb;
-  if (c.net_model == GG_NET_EMESH_HOP_BY_HOP && P.K > 1)
-    return gg_fail(GG_ERR_UNSUPPORTED, "coherent mode: emesh_hop_by_hop with more than one logical shard "
-                   "(router queues split by shard) is not built yet");
+  if (P.T > 4096) return gg_fail(GG_ERR_UNSUPPORTED, "coherent mode: more than 4096 tiles (sharer words per lane)");
   if (c.l1d_assoc > 31 || c.l2_assoc > 31) return gg_fail(GG_ERR_UNSUPPORTED, "coherent mode: associativity above 31");
+  if (c.dir_assoc > 64) return gg_fail(GG_ERR_UNSUPPORTED, "coherent mode: directory associativity above 64");
+  if (c.line_size != 64)       // AddressHomeLookup and the directory auto sizing use 64-byte lines here and in the oracle
+    return gg_fail(GG_ERR_UNSUPPORTED, "coherent mode: line size %u (64 only)", c.line_size);
+  // logical shards (the reference's hop-by-hop process blocks) and the owned tiles
+  std::vector<uint32_t> shard(P.T);
+  if (gg_status st = gg_shard_map(P.T, P.K, shard.data())) return st;
+  std::vector<std::vector<uint32_t>> by(P.K);
+  for (uint32_t t = 0; t < P.T; ++t) by[shard[t]].push_back(t);
+  std::vector<uint32_t> gtile;
+  {
+    // equal owned shards are interleaved, so blocks b, b + ns, ... of one shard
+    // share an XCD under round-robin placement (speed only)
+    const uint32_t ns = k1 - k0;
+    bool eq = true;
+    for (uint32_t s = k0; s < k1; ++s) eq = eq && by[s].size() == by[k0].size();
+    if (eq) {
+      for (size_t j = 0; j < by[k0].size(); ++j)
+        for (uint32_t s = 0; s < ns; ++s) gtile.push_back(by[k0 + s][j]);
+    } else {
+      for (uint32_t s = k0; s < k1; ++s) gtile.insert(gtile.end(), by[s].begin(), by[s].end());
+    }
+  }
+  P.L = (uint32_t)gtile.size();
+  std::vector<int32_t> ltile(P.T, -1);
+  for (uint32_t l = 0; l < P.L; ++l) ltile[gtile[l]] = (int32_t)l;
   P.log_line = (uint32_t)ilog2(c.line_size);
   P.s1 = c.l1d_size_kb * 1024u / (c.l1d_assoc * c.line_size); P.a1 = c.l1d_assoc; P.pol1 = c.l1d_policy;
   P.s2 = c.l2_size_kb * 1024u / (c.l2_assoc * c.line_size); P.a2 = c.l2_assoc; P.pol2 = c.l2_policy;
@@ -1194,28 +1636,58 @@ static gg_status coh_alloc(gg_ctx* ctx)
   P.dram_qm = c.dram_queue_model_enabled;
   P.dram_qtype = c.dram_queue_model_type;
   P.dram_qaux = hq_aux(c.dram_queue_model_type, c.basic_moving_avg, c.history_list_no_interleaving);
-  if (P.dram_qm)
-    if (gg_status e = gg_check_queue_model(P.dram_qtype, P.dram_qaux, c.max_list_size ? c.max_list_size : 100)) return e;
   P.max_list = c.max_list_size ? c.max_list_size : 100;
+  if (P.dram_qm)
+    if (gg_status e = gg_check_queue_model(P.dram_qtype, P.dram_qaux, P.max_list)) return e;
   P.analytical = c.analytical_enabled;
   P.dram_proc = (uint64_t)((float)c.line_size / c.dram_bandwidth) + 1;
   P.dram_cost = (uint64_t)(float)c.dram_latency_ns;
-  P.msg_cap = (uint64_t)64 * P.T + 65536;
-  // a wave per tile (default; GG_COH_TILES_PER_BLOCK=64 packs a lane per tile, for A/B runs)
-  { const char* e = getenv("GG_COH_TILES_PER_BLOCK"); P.tiles_per_block = (e && atoi(e) == 64) ? 64 : 1; }
-  {
-    const uint64_t rq = (uint64_t)P.QC * sizeof(CReq);
-    const char* r = getenv("GG_COH_STAGE_RQ");
-    P.stage_rq = (P.tiles_per_block == 1 && rq <= 48 * 1024 && !(r && atoi(r) == 0)) ? 1 : 0;
-  }
-  if (getenv("GG_COH_PROFILE") && atoi(getenv("GG_COH_PROFILE"))) {
-    C->S.prof_steps = 1u << 16;
-    if (gg_status st = dalloc(C, &C->S.prof, 16 + C->S.prof_steps)) return st;
-    GG_HIP(hipMemset(C->S.prof, 0, sizeof(unsigned long long) * (16 + C->S.prof_steps)));
-  }
+  P.msg_cap = (uint32_t)std::min<uint64_t>((uint64_t)64 * P.T + (uint64_t)kChunk * 2 * P.T + 65536, 0x7FFFFFFFull);
   P.np = gg_noc_params(ctx);
-  const uint64_t L = P.lt;
-  CS& S = C->S;
+  P.net = c.net_model;
+  P.mw = P.np.w; P.mh = P.np.h;
+  P.qimg = (uint32_t)((sizeof(HQueue) + (size_t)P.np.max_size * sizeof(HNode) + 15) & ~(size_t)15);
+  // hop-by-hop chain segments: the runs of each row / column inside one owned shard
+  std::vector<Seg> segx, segy;
+  std::vector<uint32_t> tseg((size_t)P.T * 2, ~0u);
+  if (P.net == GG_NET_EMESH_HOP_BY_HOP) {
+    if (P.mw * P.mh != P.T) return gg_fail(GG_ERR_UNSUPPORTED, "emesh_hop_by_hop needs a full W x H mesh (hop_by_hop.cc:55-59)");
+    auto owned = [&](uint32_t t) { return ltile[t] >= 0; };
+    for (int pass = 0; pass < 2; ++pass) {
+      const uint32_t lines = pass == 0 ? P.mh : P.mw, len = pass == 0 ? P.mw : P.mh;
+      std::vector<Seg>& out = pass == 0 ? segx : segy;
+      for (uint32_t ln = 0; ln < lines; ++ln) {
+        auto at = [&](uint32_t pos) { return pass == 0 ? ln * P.mw + pos : pos * P.mw + ln; };
+        uint32_t a = 0;
+        while (a < len) {
+          uint32_t b = a;
+          while (b + 1 < len && shard[at(b + 1)] == shard[at(a)]) ++b;
+          if (owned(at(a))) {
+            for (uint32_t q = a; q <= b; ++q) tseg[(size_t)at(q) * 2 + pass] = (uint32_t)out.size();
+            out.push_back(Seg{ln, a, b, 0});
+          }
+          a = b + 1;
+        }
+      }
+    }
+  }
+  P.nsx = (uint32_t)segx.size() * 2; P.nsy = (uint32_t)segy.size() * 2;
+  uint32_t maxrun = 1;
+  for (const Seg& s : segx) maxrun = std::max(maxrun, s.hi - s.lo + 1);
+  for (const Seg& s : segy) maxrun = std::max(maxrun, s.hi - s.lo + 1);
+  {
+    const size_t fixed = (size_t)maxrun * (P.qimg + kNetCtr * 8);
+    if (P.net == GG_NET_EMESH_HOP_BY_HOP && fixed + 64 * kWalkPkBytes > kWalkLdsMax)
+      return gg_fail(GG_ERR_UNSUPPORTED, "emesh_hop_by_hop: a shard's %u-router run does not fit the LDS of one walker", maxrun);
+    P.walk_pk = (uint32_t)std::min<size_t>(4096, (kWalkLdsMax - fixed) / kWalkPkBytes);
+    C->walk_lds = fixed + (size_t)P.walk_pk * kWalkPkBytes;
+  }
+  P.seg_cap = P.msg_cap;
+  C->step_lds = sizeof(StepLds);
+  GG_HIP(hipFuncSetAttribute((const void*)k_c_step, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C->step_lds));
+  if (P.net == GG_NET_EMESH_HOP_BY_HOP)
+    GG_HIP(hipFuncSetAttribute((const void*)k_c_walk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C->walk_lds));
+  const uint64_t L = P.L;
   gg_status st = GG_OK;
 #define A(ptr, n) if (st == GG_OK) st = dalloc(C, &S.ptr, (n))
   A(l1_tag, L * P.s1 * P.a1); A(l1_meta, L * P.s1 * P.a1); A(l1_rr, L * P.s1);
@@ -1226,29 +1698,40 @@ static gg_status coh_alloc(gg_ctx* ctx)
   A(dir, L * P.E); A(dsh, L * P.E * P.W);
   A(rep, L * P.R); A(rsh, L * P.R * P.W); A(nrep, L);
   A(rq, L * P.QC); A(nrq, L);
-  A(dq, L); A(dnd, L * P.max_list); A(dfl, L * P.max_list);
-  A(buf0, P.msg_cap); A(buf1, P.msg_cap); A(cnt, 2);
-  A(head0, L); A(head1, L);
+  A(dq, L); A(dnd, L * P.max_list);
+  A(pool0, P.msg_cap); A(pool1, P.msg_cap); A(npool, 2);
+  A(inb0, L * P.IC); A(inb1, L * P.IC); A(ninb0, L); A(ninb1, L);
+  const uint64_t al = P.net == GG_NET_EMESH_HOP_BY_HOP ? L * P.IC : 1;
+  A(arv0, al); A(arv1, al); A(narv0, L); A(narv1, L);
+  A(xl, (uint64_t)std::max(P.nsx, 1u) * P.seg_cap); A(nxl, std::max(P.nsx, 1u));
+  A(yl, (uint64_t)std::max(P.nsy, 1u) * P.seg_cap); A(nyl, std::max(P.nsy, 1u));
   A(bnd, P.msg_cap); A(bnd_cnt, 1);
-  A(scratch, L * P.IC);
-  A(quiet, 1); A(ri, GG_NUM_RUN_INFO);
-  const uint64_t pk = (c.net_model == GG_NET_EMESH_HOP_BY_HOP) ? P.msg_cap : 1;
-  A(pk_src, pk); A(pk_dst, pk); A(pk_len, pk); A(pk_t0, pk); A(pk_khi, pk); A(pk_klo, pk);
+  A(ring, 5); A(ri, GG_NUM_RUN_INFO);
+  A(gscr, L * 5 * P.IC);
 #undef A
-  if (st == GG_OK) st = dalloc(C, &C->status_dev, 4);
-  if (st == GG_OK) st = dalloc(C, &C->ecount_dev, 2 * (uint64_t)P.K + 2);
-  if (st == GG_OK) st = dalloc(C, &C->offs_dev, (uint64_t)P.T + 1);
+  if (st) return st;
+  S.quiet = S.ring + 4;
+  if ((st = dupload(C, &S.gtile, gtile))) return st;
+  if ((st = dupload(C, &S.ltile, ltile))) return st;
+  if ((st = dupload(C, &S.shard, shard))) return st;
+  if ((st = dupload(C, &S.segx, segx))) return st;
+  if ((st = dupload(C, &S.segy, segy))) return st;
+  if ((st = dupload(C, &S.tseg, tseg))) return st;
+  if ((st = dalloc(C, &C->status_dev, 4))) return st;
+  if ((st = dalloc(C, &C->ecount_dev, 2 * (uint64_t)P.K + 2))) return st;
+  if ((st = dalloc(C, &C->offs_dev, (uint64_t)P.T + 1))) return st;
   S.ctr = gg_noc_ctr(ctx);
+  gg_noc_queues(ctx, &S.nq, &S.nnd);
   S.err = ctx->err_dev;
-  return st;
+  return GG_OK;
 }
 
 static gg_status coh_check(gg_ctx* ctx)
 {
   uint32_t e = 0;
   GG_HIP(hipMemcpy(&e, ctx->err_dev, sizeof(e), hipMemcpyDeviceToHost));
-  if (e & GG_DERR_CAP) return gg_fail(GG_ERR_UNSUPPORTED, "coherent mode: a device capacity (messages / inbox / "
-                                      "request queue / replaced entries / call chain) was exceeded");
+  if (e & GG_DERR_CAP) return gg_fail(GG_ERR_UNSUPPORTED, "coherent mode: a device capacity (records / inbox / "
+                                      "request queue / replaced entries / call chain / segment) was exceeded");
   if (e & GG_DERR_STATE) return gg_fail(GG_ERR_STATE, "coherent mode: a state the reference would reject "
                                         "(LOG_ASSERT_ERROR / assert)");
   return GG_OK;
@@ -1273,9 +1756,12 @@ gg_status gg_coherent_begin(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_ou
   if (gg_status st = gg_noc_reset(ctx, s)) return st;
   GG_HIP(hipMemsetAsync(ctx->err_dev, 0, sizeof(uint32_t), s));
   GG_HIP(hipMemsetAsync(C->S.ri, 0, sizeof(uint64_t) * GG_NUM_RUN_INFO, s));
-  GG_HIP(hipMemsetAsync(C->S.cnt, 0, sizeof(uint32_t) * 2, s));
+  GG_HIP(hipMemsetAsync(C->S.npool, 0, sizeof(uint32_t) * 2, s));
+  GG_HIP(hipMemsetAsync(C->S.ring, 0, sizeof(uint32_t) * 5, s));
   GG_HIP(hipMemsetAsync(C->S.bnd_cnt, 0, sizeof(uint32_t), s));
-  hipLaunchKernelGGL(k_c_reset, dim3((P.lt + 63) / 64), dim3(64), 0, s, P, C->S, (const uint64_t*)C->offs_dev);
+  GG_HIP(hipMemsetAsync(C->S.nxl, 0, sizeof(uint32_t) * std::max(P.nsx, 1u), s));
+  GG_HIP(hipMemsetAsync(C->S.nyl, 0, sizeof(uint32_t) * std::max(P.nsy, 1u), s));
+  hipLaunchKernelGGL(k_c_reset, dim3((P.L + 63) / 64), dim3(64), 0, s, P, C->S, (const uint64_t*)C->offs_dev);
   GG_HIP(hipGetLastError());
   GG_HIP(hipStreamSynchronize(s));
   C->begun = true;
@@ -1292,34 +1778,17 @@ gg_status gg_coherent_quantum(gg_ctx* ctx, uint64_t q, gg_coherent_status* out)
   const CP& P = C->P;
   const uint64_t quantum_ps = (uint64_t)ctx->cfg.quantum_ns * 1000ull;
   const uint64_t barrier = (q + 1) * quantum_ps;
-  GG_HIP(hipMemsetAsync(C->S.quiet, 0, sizeof(uint32_t), s));
-  const uint32_t tb = (P.lt + 63) / 64;
-  const uint32_t rb = (uint32_t)std::min<uint64_t>((P.msg_cap + 255) / 256, 1024);
-  const uint32_t dyn_lds = P.stage_rq ? P.QC * (uint32_t)sizeof(CReq) : 0u;
-  if (dyn_lds)
-    GG_HIP(hipFuncSetAttribute((const void*)k_c_tiles, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)(dyn_lds + sizeof(TreeLds) + 16)));
-  uint64_t steps = 0;
-  uint32_t batch = 8;
+  const bool hbh = P.net == GG_NET_EMESH_HOP_BY_HOP;
+  uint32_t k = 0, batch = 8;
   for (;;) {
-    for (uint32_t k = 0; k < batch; ++k) {
-      const int p = (int)((steps + k) & 1);
-      if (P.tiles_per_block == 1)
-        hipLaunchKernelGGL(k_c_tiles, dim3(P.lt), dim3(64), dyn_lds, s, P, C->S, p, barrier);
-      else
-        hipLaunchKernelGGL(k_c_tiles, dim3(tb), dim3(64), 0, s, P, C->S, p, barrier);
-      if (ctx->cfg.net_model == GG_NET_EMESH_HOP_BY_HOP) {
-        hipLaunchKernelGGL(k_c_packets, dim3(rb), dim3(256), 0, s, P, C->S, p);
-        if (gg_status e = gg_noc_hbh(ctx, C->S.pk_src, C->S.pk_dst, C->S.pk_len, C->S.pk_t0, C->S.pk_khi,
-                                     C->S.pk_klo, P.msg_cap, C->S.cnt + (1 - p), s))
-          return e;
-        hipLaunchKernelGGL(k_c_route, dim3(rb), dim3(256), 0, s, P, C->S, p, gg_noc_packet_times(ctx));
-      } else {
-        hipLaunchKernelGGL(k_c_route, dim3(rb), dim3(256), 0, s, P, C->S, p, (const uint64_t*)nullptr);
+    for (uint32_t b = 0; b < batch; ++b, ++k) {
+      hipLaunchKernelGGL(k_c_step, dim3(P.L), dim3(64), C->step_lds, s, P, C->S, k, barrier);
+      if (hbh) {
+        if (P.nsx) hipLaunchKernelGGL(k_c_walk, dim3(P.nsx), dim3(64), C->walk_lds, s, P, C->S, k, 0);
+        if (P.nsy) hipLaunchKernelGGL(k_c_walk, dim3(P.nsy), dim3(64), C->walk_lds, s, P, C->S, k, 1);
       }
     }
     GG_HIP(hipGetLastError());
-    steps += batch;
     uint32_t quiet = 0, err = 0;
     GG_HIP(hipMemcpyAsync(&quiet, C->S.quiet, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     GG_HIP(hipMemcpyAsync(&err, ctx->err_dev, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -1328,9 +1797,11 @@ gg_status gg_coherent_quantum(gg_ctx* ctx, uint64_t q, gg_coherent_status* out)
     if (quiet) break;
     if (batch < 64) batch *= 2;
   }
+  // the next quantum starts from empty step counters
+  GG_HIP(hipMemsetAsync(C->S.ring, 0, sizeof(uint32_t) * 5, s));
   uint64_t init[4] = {0, 0, ~0ull, 0};
   GG_HIP(hipMemcpyAsync(C->status_dev, init, sizeof(init), hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(k_c_status, dim3(tb), dim3(64), 0, s, P, C->S, C->status_dev);
+  hipLaunchKernelGGL(k_c_status, dim3((P.L + 63) / 64), dim3(64), 0, s, P, C->S, C->status_dev);
   GG_HIP(hipGetLastError());
   uint64_t res[4];
   uint32_t nb = 0;
@@ -1360,20 +1831,20 @@ gg_status gg_coherent_export(gg_ctx* ctx, gg_cmsg* out_dev, uint64_t cap, uint64
   const CP& P = C->P;
   uint32_t nb = 0;
   GG_HIP(hipMemcpy(&nb, C->S.bnd_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost));
-  if (nb > cap) return gg_fail(GG_ERR_RANGE, "export buffer holds %llu messages, %u waiting",
+  if (nb > cap) return gg_fail(GG_ERR_RANGE, "export buffer holds %llu records, %u waiting",
                                (unsigned long long)cap, nb);
   if (nb && !out_dev) return gg_fail(GG_ERR_INVALID, "NULL export buffer");
   std::vector<uint32_t> counts(P.K, 0), base(P.K, 0);
   if (nb) {
     GG_HIP(hipMemsetAsync(C->ecount_dev, 0, sizeof(uint32_t) * 2 * P.K, s));
-    hipLaunchKernelGGL(k_c_export_count, dim3((nb + 255) / 256), dim3(256), 0, s, P, C->S.bnd, nb, C->ecount_dev);
+    hipLaunchKernelGGL(k_c_export_count, dim3((nb + 255) / 256), dim3(256), 0, s, C->S, C->S.bnd, nb, C->ecount_dev);
     GG_HIP(hipMemcpyAsync(counts.data(), C->ecount_dev, sizeof(uint32_t) * P.K, hipMemcpyDeviceToHost, s));
     GG_HIP(hipStreamSynchronize(s));
     uint32_t a = 0;
     for (uint32_t k = 0; k < P.K; ++k) { base[k] = a; a += counts[k]; }
     GG_HIP(hipMemcpyAsync(C->ecount_dev, base.data(), sizeof(uint32_t) * P.K, hipMemcpyHostToDevice, s));
     GG_HIP(hipMemsetAsync(C->ecount_dev + P.K, 0, sizeof(uint32_t) * P.K, s));
-    hipLaunchKernelGGL(k_c_export_scatter, dim3((nb + 255) / 256), dim3(256), 0, s, P, C->S.bnd, nb,
+    hipLaunchKernelGGL(k_c_export_scatter, dim3((nb + 255) / 256), dim3(256), 0, s, C->S, C->S.bnd, nb,
                        C->ecount_dev, C->ecount_dev + P.K, out_dev);
     GG_HIP(hipGetLastError());
   }
@@ -1390,12 +1861,12 @@ gg_status gg_coherent_import(gg_ctx* ctx, const gg_cmsg* in_dev, uint64_t n)
   if (!C || !C->begun) return gg_fail(GG_ERR_INVALID, "gg_coherent_begin first");
   if (n == 0) return GG_OK;
   if (!in_dev) return gg_fail(GG_ERR_INVALID, "NULL import buffer");
-  if (n > C->P.msg_cap) return gg_fail(GG_ERR_UNSUPPORTED, "import of %llu messages beyond the step buffer",
+  if (n > C->P.msg_cap) return gg_fail(GG_ERR_UNSUPPORTED, "import of %llu records beyond the step pool",
                                        (unsigned long long)n);
   hipSetDevice(ctx->device);
   hipStream_t s = ctx->last_stream;
-  // the quantum's first step reads buffer 0; its outbox (buffer 1) starts empty
-  GG_HIP(hipMemsetAsync(C->S.cnt + 1, 0, sizeof(uint32_t), s));
+  // the quantum's first step reads pool 1 (messages) and walks pool 0 (held packets)
+  GG_HIP(hipMemsetAsync(C->S.npool, 0, sizeof(uint32_t) * 2, s));
   hipLaunchKernelGGL(k_c_import, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, C->P, C->S, in_dev, (uint32_t)n);
   GG_HIP(hipGetLastError());
   GG_HIP(hipStreamSynchronize(s));
@@ -1415,38 +1886,36 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
   const uint64_t quantum_ps = (uint64_t)c.quantum_ns * 1000ull;
   gg_timer_begin(ctx, "coherent_run", s);
   uint64_t q = 0;
+  gg_cmsg* xfer = nullptr;
+  GG_HIP(hipMalloc((void**)&xfer, sizeof(gg_cmsg) * C->P.msg_cap));
+  gg_status rc = GG_OK;
   for (;;) {
     gg_coherent_status st;
-    if (gg_status e = gg_coherent_quantum(ctx, q, &st)) return e;
+    if ((rc = gg_coherent_quantum(ctx, q, &st))) break;
     const uint64_t nb = st.boundary_msgs;
-    if (nb) {                                          // the boundary: held messages -> next inboxes
-      GG_HIP(hipMemcpyAsync(C->S.buf1, C->S.bnd, sizeof(gg_cmsg) * nb, hipMemcpyDeviceToDevice, s));
-      GG_HIP(hipMemsetAsync(C->S.bnd_cnt, 0, sizeof(uint32_t), s));
-      if (gg_status e = gg_coherent_import(ctx, C->S.buf1, nb)) return e;
+    if (nb) {                                          // the boundary: held records -> the next quantum
+      if (hipMemcpyAsync(xfer, C->S.bnd, sizeof(gg_cmsg) * nb, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+          hipMemsetAsync(C->S.bnd_cnt, 0, sizeof(uint32_t), s) != hipSuccess) {
+        rc = gg_fail(GG_ERR_HIP, "boundary copy");
+        break;
+      }
+      if ((rc = gg_coherent_import(ctx, xfer, nb))) break;
     }
     if (st.active_tiles == 0 && nb == 0) break;
     if (nb == 0 && st.blocked_tiles == 0) {
       const uint64_t nq = st.min_next_ps / quantum_ps;
       q = nq > q + 1 ? nq : q + 1;
     } else if (nb == 0) {
-      return gg_fail(GG_ERR_STATE, "coherent run deadlocked: tiles blocked with no message in flight");
+      rc = gg_fail(GG_ERR_STATE, "coherent run deadlocked: tiles blocked with no message in flight");
+      break;
     } else {
       q = q + 1;
     }
   }
+  hipFree(xfer);
+  if (rc) return rc;
   gg_timer_end(ctx, "coherent_run", s);
   GG_HIP(hipStreamSynchronize(s));
-  if (C->S.prof) {
-    std::vector<unsigned long long> h(16 + C->S.prof_steps);
-    GG_HIP(hipMemcpy(h.data(), C->S.prof, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
-    unsigned long long crit = 0, nst = 0;
-    for (uint32_t i = 0; i < C->S.prof_steps; ++i) { crit += h[16 + i]; nst += h[16 + i] ? 1 : 0; }
-    fprintf(stderr, "[gg_coh] tile-step cycles summed over tiles: gather+sort %llu handlers %llu (directory %llu, L2 %llu)"
-            " trace %llu flush %llu | msgs %llu | critical path (max tile per step, %llu steps) %llu cycles"
-            " | memtime/memrealtime %.1f MHz | dget %llu dram %llu send %llu\n",
-            h[0], h[1], h[5], h[6], h[2], h[3], h[4], nst, crit,
-            h[7] ? 100.0 * (double)(h[0] + h[1] + h[2] + h[3]) / (double)h[7] : 0.0, h[9], h[10], h[11]);
-  }
   return coh_check(ctx);
 }
 
@@ -1458,18 +1927,26 @@ gg_status gg_coherent_get_stats(gg_ctx* ctx, uint64_t* tile_stats, uint64_t* cac
   hipSetDevice(ctx->device);
   hipStream_t s = ctx->last_stream;
   const CP& P = C->P;
-  hipLaunchKernelGGL(k_c_final_stats, dim3((P.lt + 63) / 64), dim3(64), 0, s, P, C->S);
+  hipLaunchKernelGGL(k_c_final_stats, dim3((P.L + 63) / 64), dim3(64), 0, s, P, C->S);
   GG_HIP(hipGetLastError());
   GG_HIP(hipStreamSynchronize(s));
+  std::vector<uint32_t> gtile(P.L);
+  GG_HIP(hipMemcpy(gtile.data(), C->S.gtile, sizeof(uint32_t) * P.L, hipMemcpyDeviceToHost));
   if (tile_stats) {
+    std::vector<uint64_t> v((size_t)P.L * GG_NUM_TILE_STATS);
+    GG_HIP(hipMemcpy(v.data(), C->S.st, sizeof(uint64_t) * v.size(), hipMemcpyDeviceToHost));
     std::memset(tile_stats, 0, sizeof(uint64_t) * P.T * GG_NUM_TILE_STATS);
-    GG_HIP(hipMemcpy(tile_stats + (size_t)P.tb * GG_NUM_TILE_STATS, C->S.st,
-                     sizeof(uint64_t) * P.lt * GG_NUM_TILE_STATS, hipMemcpyDeviceToHost));
+    for (uint32_t l = 0; l < P.L; ++l)
+      std::memcpy(tile_stats + (size_t)gtile[l] * GG_NUM_TILE_STATS, v.data() + (size_t)l * GG_NUM_TILE_STATS,
+                  sizeof(uint64_t) * GG_NUM_TILE_STATS);
   }
   if (cache) {
-    std::memset(cache, 0, sizeof(uint64_t) * P.T * 2 * GG_NUM_CACHE_COUNTERS);
-    GG_HIP(hipMemcpy(cache + (size_t)P.tb * 2 * GG_NUM_CACHE_COUNTERS, C->S.cc,
-                     sizeof(uint64_t) * P.lt * 2 * GG_NUM_CACHE_COUNTERS, hipMemcpyDeviceToHost));
+    const size_t per = 2 * GG_NUM_CACHE_COUNTERS;
+    std::vector<uint64_t> v((size_t)P.L * per);
+    GG_HIP(hipMemcpy(v.data(), C->S.cc, sizeof(uint64_t) * v.size(), hipMemcpyDeviceToHost));
+    std::memset(cache, 0, sizeof(uint64_t) * P.T * per);
+    for (uint32_t l = 0; l < P.L; ++l)
+      std::memcpy(cache + (size_t)gtile[l] * per, v.data() + (size_t)l * per, sizeof(uint64_t) * per);
   }
   if (run_info) GG_HIP(hipMemcpy(run_info, C->S.ri, sizeof(uint64_t) * GG_NUM_RUN_INFO, hipMemcpyDeviceToHost));
   return coh_check(ctx);

@@ -8,25 +8,39 @@ namespace gg {
 
 // ---------------------------------------------------------------------------
 // Queue models (QueueModel::create, queue_model.cc:19-39).  One storage
-// layout for all three: HQueue + max_size HNode + max_size int16 free list.
-//   history_tree (interval_tree.cc:40-394 + queue_model_history_tree.cc:44-167):
-//     AVL nodes + free list;
-//   history_list (queue_model_history_list.cc:40-134): the free-interval
-//     list as nd[0..size) in list order (first/second);
+// layout for all three: HQueue + max_size 16-byte HNode slots.
+//   history_tree (queue_model_history_tree.cc:44-167 over interval_tree.cc):
+//     the free intervals as nd[0..size), sorted by start.  The reference keeps
+//     them in an AVL tree and finds the interval with searchTree
+//     (interval_tree.cc:366-394); the free intervals are disjoint and, since
+//     every processing time and min_processing_time is >= 1 (router queues 1,
+//     router_model.cc:23-27; DRAM 13, dram_perf_model.cc:48,92), separated by
+//     at least one busy cycle and at least min_processing_time long.  For such
+//     a set searchTree returns the FIRST interval (lowest start) that either
+//     contains [t, t+p] or starts after t with length >= p, whatever the tree
+//     shape: a left subtree it skips (t + p >= node start) holds only
+//     intervals that end at or before the node's start, so none contains
+//     [t, t+p] and none starting after t is long enough.  search(0, 1) is
+//     then nd[0] (the min-key node the pruning removes, :52-56).  The
+//     outputs (delays, analytical count, utilization) are those of the AVL
+//     (tests/test_queue_flat.py checks 600k random requests against the
+//     oracle's AVL restatement; the reference fixtures run on the GPU).
+//   history_list (queue_model_history_list.cc:40-134): nd[0..size) in list order;
 //   basic (queue_model_basic.cc:34-61): the MovingAverage window
 //     (moving_average.h, window + 1 slots) as raw u64 words over nd[].
 // ---------------------------------------------------------------------------
-struct HNode { uint64_t first, second; int16_t parent, left, right, height; };
+struct HNode { uint64_t first, second; };
 struct HQueue {
-  int32_t root; uint32_t size; int32_t free_tail; uint32_t max_size;
+  uint32_t size; uint32_t max_size; uint32_t type, aux;   // GG_QM_*; list: no-interleaving flag; basic: basic_moving_avg
   double sig_sq, sig; uint64_t n, newest;          // QueueModelMG1
   uint64_t analytical;                              // _total_requests_using_analytical_model
   uint64_t util, last_req, total_req;               // QueueModel utilization counters
-  uint32_t type, aux;                               // GG_QM_*; list: no-interleaving flag; basic: basic_moving_avg
   uint32_t front, back;                             // basic: ModuloNum window ends (modulo window + 1)
   double mean;                                      // basic: MovingArithmeticMean::_arithmetic_mean
   uint64_t qtime;                                   // basic: QueueModelBasic::_queue_time
+  uint64_t pad;
 };
+static_assert(sizeof(HQueue) % 16 == 0 && sizeof(HNode) == 16, "16-byte queue images");
 
 // the model-specific parameter of a queue of type `type` (gg_config fields)
 __host__ __device__ inline uint32_t hq_aux(uint32_t type, uint32_t basic_moving_avg, uint32_t list_no_interleaving)
@@ -39,185 +53,46 @@ __host__ __device__ inline uint32_t hq_window(uint32_t aux) { return (aux & 0xFF
 inline gg_status gg_check_queue_model(uint32_t type, uint32_t aux, uint32_t max_size)
 {
   if (type > GG_QM_BASIC) return gg_fail(GG_ERR_INVALID, "unknown queue model type");
+  if (max_size < 2) return gg_fail(GG_ERR_UNSUPPORTED, "max_list_size below 2");
   if (type == GG_QM_BASIC) {
     if ((aux >> 16) == GG_MAVG_GEOMETRIC_MEAN) return gg_fail(GG_ERR_UNSUPPORTED, "geometric_mean moving average");
     if ((aux >> 16) > GG_MAVG_GEOMETRIC_MEAN) return gg_fail(GG_ERR_INVALID, "unknown moving average type");
-    if (hq_window(aux) + 1 > 3 * max_size)
-      return gg_fail(GG_ERR_UNSUPPORTED, "moving_avg_window_size + 1 exceeds 3 * max_list_size queue words");
+    if (hq_window(aux) + 1 > 2 * max_size)
+      return gg_fail(GG_ERR_UNSUPPORTED, "moving_avg_window_size + 1 exceeds 2 * max_list_size queue words");
   }
   return GG_OK;
 }
 
 // QueueModel{HistoryTree,HistoryList,Basic} constructors on one queue's storage
-__device__ inline void hq_init(HQueue* q, HNode* N, int16_t* f, uint32_t max_size, uint32_t type, uint32_t aux)
+__device__ inline void hq_init(HQueue* q, HNode* N, uint32_t max_size, uint32_t type, uint32_t aux)
 {
   HQueue Q{};
   Q.max_size = max_size;
   Q.type = type;
   Q.aux = aux;
-  if (type == GG_QM_HISTORY_LIST) {
-    N[0].first = 0; N[0].second = ~0ull;            // push_back(make_pair(0, UINT64_MAX))
-    Q.size = 1;
-  } else if (type == GG_QM_BASIC) {
+  if (type == GG_QM_BASIC) {
     uint64_t* w = reinterpret_cast<uint64_t*>(N);
     for (uint32_t j = 0; j <= hq_window(aux); ++j) w[j] = 0;   // _num_list.resize(window + 1)
   } else {
-    for (uint32_t j = 0; j < max_size; ++j) f[j] = (int16_t)j;  // allocateMemory
-    Q.free_tail = (int32_t)max_size - 1;
-    const int r = f[Q.free_tail--];                             // allocateNode(PAIR(0, UINT64_MAX))
-    N[r].first = 0; N[r].second = ~0ull; N[r].parent = N[r].left = N[r].right = -1; N[r].height = 1;
-    Q.root = r; Q.size = 1;
+    N[0].first = 0; N[0].second = ~0ull;            // history_tree: allocateNode(PAIR(0, UINT64_MAX));
+    Q.size = 1;                                     // history_list: push_back(make_pair(0, UINT64_MAX))
   }
   *q = Q;
 }
 
-struct HTree {
-  HQueue* q; HNode* nd; int16_t* fl; uint64_t min_proc; bool analytical;
+// One wave's lane id and wave-level ordering of LDS accesses between lanes.
+__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+__device__ __forceinline__ void wave_sync()
+{
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ uint64_t ballot64(bool b) { return __ballot(b); }
 
-  __device__ __forceinline__ int32_t h(int x) const { return x < 0 ? 0 : nd[x].height; }
-  __device__ __forceinline__ void upd_child(int node, int child, int dir)      // updateChildPointer
-  {
-    if (node < 0) return;
-    if (dir == 0) { if (nd[node].first < nd[child].first) nd[node].right = child; else nd[node].left = child; }
-    else if (dir == 1) nd[node].left = child;
-    else nd[node].right = child;
-  }
-  __device__ __forceinline__ void upd_parent(int node, int parent)             // updateParentPointer
-  {
-    if (node >= 0) nd[node].parent = parent;
-    if (parent < 0) q->root = node;
-  }
-  __device__ __forceinline__ bool balanced(int x) const { int d = h(nd[x].left) - h(nd[x].right); return d >= -1 && d <= 1; }
-  __device__ __forceinline__ void upd_height(int x) { int a = h(nd[x].left), b = h(nd[x].right); nd[x].height = (int16_t)((a > b ? a : b) + 1); }
-  __device__ __forceinline__ void rotate(int y, bool cw)                       // performRotation
-  {
-    int x;
-    if (cw) {
-      x = nd[y].left;
-      upd_parent(x, nd[y].parent); upd_child(nd[x].parent, x, 0);
-      nd[y].left = nd[x].right; upd_parent(nd[y].left, y);
-      nd[x].right = (int16_t)y; upd_parent(y, x);
-    } else {
-      x = nd[y].right;
-      upd_parent(x, nd[y].parent); upd_child(nd[x].parent, x, 0);
-      nd[y].right = nd[x].left; upd_parent(nd[y].right, y);
-      nd[x].left = (int16_t)y; upd_parent(y, x);
-    }
-    upd_height(y); upd_height(x);
-  }
-  __device__ __forceinline__ int balance(int z)                                // balanceHeight
-  {
-    int zl = nd[z].left, zr = nd[z].right;
-    bool y_left = h(zl) > h(zr);
-    int y = y_left ? zl : zr;
-    int yl = nd[y].left, yr = nd[y].right;
-    int x; bool x_left;
-    if (h(yl) != h(yr)) { x_left = h(yl) > h(yr); x = x_left ? yl : yr; }
-    else if (y_left) { x = yl; x_left = true; }
-    else { x = yr; x_left = false; }
-    if (y_left) {
-      if (!x_left) { rotate(y, false); rotate(z, true); return x; }
-      rotate(z, true); return y;
-    } else {
-      if (x_left) { rotate(y, true); rotate(z, false); return x; }
-      rotate(z, false); return y;
-    }
-  }
-  __device__ __forceinline__ void rebalance(int r)                             // rebalanceAVLTree
-  {
-    while (r >= 0) {
-      int old = nd[r].height, nr = r;
-      if (!balanced(r)) nr = balance(r); else upd_height(r);
-      if (nd[nr].height == old) return;
-      r = nd[nr].parent;
-    }
-  }
-  __device__ __forceinline__ void insert(int node)                             // insert / insertInTree
-  {
-    q->size++;
-    int r = q->root;
-    for (;;) {
-      if (nd[node].first < nd[r].first) {
-        if (nd[r].left >= 0) r = nd[r].left;
-        else { nd[r].left = (int16_t)node; nd[node].parent = (int16_t)r; rebalance(r); return; }
-      } else if (nd[node].first > nd[r].first) {
-        if (nd[r].right >= 0) r = nd[r].right;
-        else { nd[r].right = (int16_t)node; nd[node].parent = (int16_t)r; rebalance(r); return; }
-      } else return;   // duplicate key: the reference aborts (LOG_PRINT_ERROR)
-    }
-  }
-  // removeFromTree (interval_tree.cc:322-356) without recursion: the successor
-  // of a two-child node has no left child, so its removal is the one-child case
-  __device__ __forceinline__ void remove_leafish(int node)
-  {
-    if (nd[node].left < 0) {
-      int p = nd[node].parent;
-      if (p >= 0) upd_child(p, nd[node].right, (nd[p].first < nd[node].first) ? 2 : 1);
-      upd_parent(nd[node].right, p);
-      rebalance(p);
-    } else {
-      int p = nd[node].parent;
-      upd_child(p, nd[node].left, 0);
-      upd_parent(nd[node].left, p);
-      rebalance(p);
-    }
-  }
-  __device__ __forceinline__ int remove_rec(int node)
-  {
-    if (nd[node].left < 0 || nd[node].right < 0) { remove_leafish(node); return node; }
-    int succ = nd[node].right;
-    while (nd[succ].left >= 0) succ = nd[succ].left;           // findMinKeyNode
-    remove_leafish(succ);                                      // successor has no left child
-    uint64_t f = nd[node].first, s = nd[node].second;          // swap key/interval
-    nd[node].first = nd[succ].first; nd[node].second = nd[succ].second;
-    nd[succ].first = f; nd[succ].second = s;
-    return succ;
-  }
-  __device__ __forceinline__ int remove(int node) { q->size--; return remove_rec(node); }
-  // searchTree (interval_tree.cc:366-394).  The recursion comes back to a
-  // node only after searching its LEFT subtree (it descends left only when
-  // b < first), so the pending nodes are exactly the ancestors entered through
-  // their left child: falling off the tree right after a left descent resumes
-  // that node; otherwise the walk climbs parent pointers to the nearest
-  // ancestor whose left subtree it is leaving.  No explicit stack (a
-  // dynamically indexed array would live in scratch memory).
-  __device__ __forceinline__ int search(uint64_t a, uint64_t b) const
-  {
-    int n = q->root, last = -1;
-    bool went_left = false;
-    for (;;) {
-      if (n < 0) {
-        int p;
-        if (went_left) {
-          p = last;
-        } else {
-          int c = last;
-          for (;;) {
-            if (c < 0) return -1;
-            p = nd[c].parent;
-            if (p < 0) return -1;
-            if (nd[p].left == c) break;
-            c = p;
-          }
-        }
-        if (a < nd[p].first && (nd[p].second - nd[p].first) >= (b - a)) return p;
-        last = p; went_left = false; n = nd[p].right;
-        continue;
-      }
-      if (a >= nd[n].first && b <= nd[n].second) return n;
-      if (b < nd[n].first) { last = n; went_left = true; n = nd[n].left; continue; }
-      if (a < nd[n].first && (nd[n].second - nd[n].first) >= (b - a)) return n;
-      last = n; went_left = false; n = nd[n].right;
-    }
-  }
-  __device__ __forceinline__ int alloc(uint64_t a, uint64_t b)                 // allocateNode
-  {
-    if (q->free_tail < 0) return -1;
-    int i = fl[q->free_tail--];
-    nd[i].first = a; nd[i].second = b; nd[i].parent = nd[i].left = nd[i].right = -1; nd[i].height = 1;
-    return i;
-  }
-  __device__ __forceinline__ void release(int i) { fl[++q->free_tail] = (int16_t)i; }
+struct HTree {
+  HQueue* q; HNode* nd; uint64_t min_proc; bool analytical;
+
   __device__ __forceinline__ uint64_t mg1_delay() const                         // QueueModelMG1::computeQueueDelay
   {
     if (q->n == 0) return 0;
@@ -228,11 +103,52 @@ struct HTree {
     return (uint64_t)ceil(0.5 * service_rate * arrival_rate * ((1 / (service_rate * service_rate)) + variance) /
                           (service_rate - arrival_rate));
   }
-  // ---- history_list: nd[0..size) in list order ----
+  // ---- sorted interval array nd[0..size) (history_tree and history_list) ----
   __device__ __forceinline__ void l_erase(uint32_t i)
   {
-    for (uint32_t j = i + 1; j < q->size; ++j) { nd[j - 1].first = nd[j].first; nd[j - 1].second = nd[j].second; }
+    for (uint32_t j = i + 1; j < q->size; ++j) nd[j - 1] = nd[j];
     q->size--;
+  }
+  __device__ __forceinline__ void l_insert(uint32_t i, uint64_t a, uint64_t b)   // before position i
+  {
+    for (uint32_t j = q->size; j > i; --j) nd[j] = nd[j - 1];
+    nd[i].first = a; nd[i].second = b;
+    q->size++;
+  }
+  // ---- history_tree ----
+  // first fit (searchTree, see above): the last interval starting at or before
+  // t if it holds [t, t+p], else the first later one of length >= p
+  __device__ __forceinline__ int first_fit(uint64_t t, uint64_t p) const
+  {
+    const int n = (int)q->size;
+    int lo = 0, hi = n;
+    if (n && nd[n - 1].first <= t) lo = n;
+    while (lo < hi) { const int mid = (lo + hi) >> 1; if (nd[mid].first <= t) lo = mid + 1; else hi = mid; }
+    const int j = lo - 1;
+    if (j >= 0 && t + p <= nd[j].second) return j;
+    for (int i = j + 1; i < n; ++i) if (nd[i].second - nd[i].first >= p) return i;
+    return -1;
+  }
+  __device__ __forceinline__ uint64_t tree_delay(uint64_t t, uint64_t p, uint32_t* err)   // computeQueueDelay (:44-126)
+  {
+    if (q->size >= q->max_size) l_erase(0);                    // prune the min node (:52-56)
+    if (analytical && nd[0].first > (t + p)) { q->analytical++; return mg1_delay(); }
+    const int i = first_fit(t, p);
+    if (i < 0) { atomicOr(err, GG_DERR_STATE); return 0; }
+    const uint64_t a = nd[i].first, b = nd[i].second;
+    if (t >= a) {
+      if ((t - a) >= min_proc) {
+        if ((b - (t + p)) >= min_proc) l_insert((uint32_t)i + 1, t + p, b);
+        nd[i].second = t;
+      } else {
+        if ((b - (t + p)) >= min_proc) nd[i].first = t + p;
+        else l_erase((uint32_t)i);
+      }
+      return 0;
+    }
+    if ((b - (a + p)) >= min_proc) nd[i].first = a + p;
+    else l_erase((uint32_t)i);
+    return a - t;
   }
   // replace interval i by up to two intervals (in list order).  The list may
   // overgrow by one only here, and then loses its front (the size check after
@@ -243,13 +159,13 @@ struct HTree {
     if (!k1 && k2) { nd[i].first = a2; nd[i].second = b2; return; }
     if (!k1) { l_erase(i); return; }
     if (q->size < q->max_size) {
-      for (uint32_t j = q->size; j > i + 1; --j) { nd[j].first = nd[j - 1].first; nd[j].second = nd[j - 1].second; }
+      for (uint32_t j = q->size; j > i + 1; --j) nd[j] = nd[j - 1];
       nd[i].first = a1; nd[i].second = b1; nd[i + 1].first = a2; nd[i + 1].second = b2;
       q->size++;
     } else if (i == 0) {                        // the first new interval is the front that goes
       nd[0].first = a2; nd[0].second = b2;
     } else {                                    // drop the front: [1, i) moves down by one
-      for (uint32_t j = 1; j < i; ++j) { nd[j - 1].first = nd[j].first; nd[j - 1].second = nd[j].second; }
+      for (uint32_t j = 1; j < i; ++j) nd[j - 1] = nd[j];
       nd[i - 1].first = a1; nd[i - 1].second = b1; nd[i].first = a2; nd[i].second = b2;
     }
   }
@@ -316,40 +232,12 @@ struct HTree {
   __device__ __forceinline__ uint64_t delay(uint64_t t, uint64_t p, uint32_t* err)   // computeQueueDelay
   {
     if (q->type == GG_QM_BASIC) return basic_delay(t, p);
-    uint64_t qd = ~0ull;
+    uint64_t qd;
     if (q->type == GG_QM_HISTORY_LIST) {
       if (analytical && (t + p) < nd[0].first) { q->analytical++; qd = mg1_delay(); }
       else qd = list_scan(t, p);
-      mg1_update(t, p, qd);
-      return qd;
-    }
-    int mn = search(0, 1);
-    if (q->size >= q->max_size) release(remove(mn));
-    mn = search(0, 1);
-    if (analytical && nd[mn].first > (t + p)) {
-      q->analytical++;
-      qd = mg1_delay();
     } else {
-      int node = search(t, t + p);
-      if (node < 0) { atomicOr(err, GG_DERR_STATE); return 0; }
-      if (t >= nd[node].first) {
-        qd = 0;
-        if ((t - nd[node].first) >= min_proc) {
-          if ((nd[node].second - (t + p)) >= min_proc) {
-            int nx = alloc(t + p, nd[node].second);
-            if (nx < 0) { atomicOr(err, GG_DERR_STATE); return 0; }
-            insert(nx);
-          }
-          nd[node].second = t;
-        } else {
-          if ((nd[node].second - (t + p)) >= min_proc) nd[node].first = t + p;
-          else release(remove(node));
-        }
-      } else {
-        qd = nd[node].first - t;
-        if ((nd[node].second - (nd[node].first + p)) >= min_proc) nd[node].first = nd[node].first + p;
-        else release(remove(node));
-      }
+      qd = tree_delay(t, p, err);
     }
     mg1_update(t, p, qd);
     return qd;
@@ -363,6 +251,87 @@ struct HTree {
     q->util += p;                                                // updateQueueUtilizationCounters
     { uint64_t x = t + qd + p; if (x > q->last_req) q->last_req = x; }
     q->total_req++;
+  }
+
+  // ---- the same request by a whole wave on a queue in LDS (all 64 lanes, uniform
+  // t / p; the history tree's search and shifts lane-parallel, the other models
+  // run redundantly on every lane).  Returns the delay on every lane. ----
+  __device__ __forceinline__ void w_erase(uint32_t i, uint32_t n, uint32_t lane)
+  {
+    HNode v[2]; bool m[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) { const uint32_t j = lane + 64u * h; m[h] = j > i && j < n; if (m[h]) v[h] = nd[j]; }
+    wave_sync();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) if (m[h]) nd[lane + 64u * h - 1] = v[h];
+    wave_sync();
+  }
+  __device__ __forceinline__ void w_insert(uint32_t i, uint32_t n, uint64_t a, uint64_t b, uint32_t lane)   // before i
+  {
+    HNode v[2]; bool m[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) { const uint32_t j = lane + 64u * h; m[h] = j >= i && j < n; if (m[h]) v[h] = nd[j]; }
+    wave_sync();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) if (m[h]) nd[lane + 64u * h + 1] = v[h];
+    if (lane == 0) { nd[i].first = a; nd[i].second = b; }
+    wave_sync();
+  }
+  __device__ __forceinline__ uint64_t delay_wave(uint64_t t, uint64_t p, uint32_t* err, uint32_t lane)
+  {
+    if (q->type != GG_QM_HISTORY_TREE || q->max_size > 128) {
+      uint64_t r = 0;
+      // the scalar model on lane 0 only (its writes are not idempotent across lanes)
+      if (lane == 0) r = delay(t, p, err);
+      wave_sync();
+      return __shfl(r, 0);
+    }
+    uint32_t n = q->size;
+    if (n >= q->max_size) {                                      // prune the min node (:52-56)
+      w_erase(0, n, lane); --n;
+      if (lane == 0) q->size = n;
+      wave_sync();
+    }
+    uint64_t qd = 0;
+    bool upd = true;
+    if (analytical && nd[0].first > (t + p)) {
+      qd = mg1_delay();
+      if (lane == 0) q->analytical++;
+    } else {
+      bool c[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t j = lane + 64u * h;
+        c[h] = false;
+        if (j < n) {
+          const uint64_t a = nd[j].first, b = nd[j].second;
+          c[h] = (a <= t && t + p <= b) || (a > t && b - a >= p);
+        }
+      }
+      const uint64_t m0 = ballot64(c[0]), m1 = ballot64(c[1]);
+      if (!m0 && !m1) { if (lane == 0) atomicOr(err, GG_DERR_STATE); upd = false; }
+      else {
+        const uint32_t i = m0 ? (uint32_t)__builtin_ctzll(m0) : 64u + (uint32_t)__builtin_ctzll(m1);
+        const uint64_t a = nd[i].first, b = nd[i].second;
+        wave_sync();
+        if (t >= a) {
+          if ((t - a) >= min_proc) {
+            if ((b - (t + p)) >= min_proc) { w_insert(i + 1, n, t + p, b, lane); ++n; }
+            if (lane == 0) nd[i].second = t;
+          } else if ((b - (t + p)) >= min_proc) {
+            if (lane == 0) nd[i].first = t + p;
+          } else { w_erase(i, n, lane); --n; }
+        } else {
+          qd = a - t;
+          if ((b - (a + p)) >= min_proc) { if (lane == 0) nd[i].first = a + p; }
+          else { w_erase(i, n, lane); --n; }
+        }
+        if (lane == 0) q->size = n;
+      }
+    }
+    if (upd && lane == 0) mg1_update(t, p, qd);
+    wave_sync();
+    return qd;
   }
 };
 
@@ -429,3 +398,5 @@ uint64_t* gg_noc_ctr(gg_ctx* ctx);
 gg_status gg_noc_hbh(gg_ctx* ctx, const uint32_t* src, const uint32_t* dst, const uint32_t* len, const uint64_t* t0,
                      const uint64_t* khi, const uint64_t* klo, uint64_t cap, const uint32_t* n_dev, hipStream_t s);
 const uint64_t* gg_noc_packet_times(gg_ctx* ctx);   // arrival times of the last pipeline run
+// the router queues [tile * 6 + port] (ports 0..4 mesh SELF LEFT RIGHT DOWN UP, 5 injection)
+void gg_noc_queues(gg_ctx* ctx, gg::HQueue** q, gg::HNode** nd);

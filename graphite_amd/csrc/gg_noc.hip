@@ -71,13 +71,13 @@ __device__ __forceinline__ Ev heap_pop(Ev* h, uint32_t& n)
 
 struct NocDev {
   NocParams P;
-  HQueue* q; HNode* nd; int16_t* fl;   // queue (tile*6 + port): ports 0..4 mesh, 5 injection
+  HQueue* q; HNode* nd;                // queue (tile*6 + port): ports 0..4 mesh, 5 injection
   uint64_t* ctr;
   uint32_t* err;
   __device__ HTree tree(uint32_t tile, int port) const
   {
     const uint64_t qi = (uint64_t)tile * 6 + port;
-    HTree t{q + qi, nd + qi * P.max_size, fl + qi * P.max_size, 1, P.analytical != 0};
+    HTree t{q + qi, nd + qi * P.max_size, 1, P.analytical != 0};
     return t;
   }
 };
@@ -139,17 +139,15 @@ __device__ void mesh_hop(const NocDev& D, uint32_t tile, int port, uint32_t bits
 // rebalance); from HBM/L2 each costs a memory round trip.  The staged
 // kernels copy the queues a workgroup owns (a chain's w or h ports, or 16
 // tiles' injection / SELF ports) into LDS once per launch, run the same code
-// on the LDS image and write it back.  Image = HQueue | max_size HNode |
-// max_size int16 free list.
+// on the LDS image and write it back.  Image = HQueue | max_size HNode.
 // ---------------------------------------------------------------------------
 __host__ __device__ inline uint32_t qimg_bytes(uint32_t ms)
 {
-  return (uint32_t)((sizeof(HQueue) + ms * sizeof(HNode) + ms * sizeof(int16_t) + 15) & ~15u);
+  return (uint32_t)((sizeof(HQueue) + ms * sizeof(HNode) + 15) & ~15u);
 }
 __device__ inline HTree qimg_tree(uint8_t* img, uint32_t ms, bool analytical)
 {
-  HTree t{reinterpret_cast<HQueue*>(img), reinterpret_cast<HNode*>(img + sizeof(HQueue)),
-          reinterpret_cast<int16_t*>(img + sizeof(HQueue) + ms * sizeof(HNode)), 1, analytical};
+  HTree t{reinterpret_cast<HQueue*>(img), reinterpret_cast<HNode*>(img + sizeof(HQueue)), 1, analytical};
   return t;
 }
 static_assert(sizeof(HQueue) % 8 == 0 && sizeof(HNode) % 8 == 0, "8-byte images");
@@ -165,7 +163,7 @@ __device__ void qimg_copy_set(const NocDev& D, uint32_t n, Qid qid, Skip skip, u
   const uint32_t ms = D.P.max_size, tid = threadIdx.x, nt = blockDim.x;
   constexpr uint32_t QW = sizeof(HQueue) / 8;
   const uint32_t NW = ms * (uint32_t)(sizeof(HNode) / 8);
-  const uint32_t per = QW + NW + ms;               // 8-byte words of queue + nodes, int16 free-list entries
+  const uint32_t per = QW + NW;                    // 8-byte words of queue + nodes
   const uint32_t total = n * per;
   constexpr uint32_t U = 8;
   for (uint32_t i0 = tid; i0 < total; i0 += U * nt) {
@@ -179,13 +177,10 @@ __device__ void qimg_copy_set(const NocDev& D, uint32_t n, Qid qid, Skip skip, u
       const uint64_t qi = qid(s);
       uint8_t* img = base + (size_t)s * qb;
       if (w < QW) v[u] = TO_LDS ? reinterpret_cast<const uint64_t*>(D.q + qi)[w] : reinterpret_cast<uint64_t*>(img)[w];
-      else if (w < QW + NW) {
+      else {
         const uint32_t j = w - QW;
         v[u] = TO_LDS ? reinterpret_cast<const uint64_t*>(D.nd + qi * ms)[j]
                       : reinterpret_cast<uint64_t*>(img + sizeof(HQueue))[j];
-      } else {
-        const uint32_t j = w - QW - NW;
-        v[u] = (uint16_t)(TO_LDS ? D.fl[qi * ms + j] : reinterpret_cast<int16_t*>(img + sizeof(HQueue) + ms * sizeof(HNode))[j]);
       }
     }
     #pragma unroll
@@ -198,14 +193,10 @@ __device__ void qimg_copy_set(const NocDev& D, uint32_t n, Qid qid, Skip skip, u
       uint8_t* img = base + (size_t)s * qb;
       if (w < QW) {
         if (TO_LDS) reinterpret_cast<uint64_t*>(img)[w] = v[u]; else reinterpret_cast<uint64_t*>(D.q + qi)[w] = v[u];
-      } else if (w < QW + NW) {
+      } else {
         const uint32_t j = w - QW;
         if (TO_LDS) reinterpret_cast<uint64_t*>(img + sizeof(HQueue))[j] = v[u];
         else reinterpret_cast<uint64_t*>(D.nd + qi * ms)[j] = v[u];
-      } else {
-        const uint32_t j = w - QW - NW;
-        if (TO_LDS) reinterpret_cast<int16_t*>(img + sizeof(HQueue) + ms * sizeof(HNode))[j] = (int16_t)(uint16_t)v[u];
-        else D.fl[qi * ms + j] = (int16_t)(uint16_t)v[u];
       }
     }
   }
@@ -579,19 +570,23 @@ __global__ void k_init_pkts(const uint32_t* __restrict__ src, const uint64_t* __
   S.t[k] = t0[k]; S.zl[k] = 0; S.ct[k] = 0; S.cur[k] = src[k];
 }
 
-__global__ void k_htree_reset(HQueue* q, HNode* nd, int16_t* fl, uint64_t nq, uint32_t max_size, uint32_t type,
-                              uint32_t aux)
+__global__ void k_htree_reset(HQueue* q, HNode* nd, uint64_t nq, uint32_t max_size, uint32_t type, uint32_t aux)
 {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nq) return;
-  hq_init(q + i, nd + i * max_size, fl + i * max_size, max_size, type, aux);
+  hq_init(q + i, nd + i * max_size, max_size, type, aux);
 }
 
-__global__ void k_htree_seq(HQueue* q, HNode* nd, int16_t* fl, uint64_t min_proc, uint32_t analytical,
+// processing times of 0 are outside the reference's call sites (flits >= 1,
+// DRAM 13) and outside the interval argument of gg_dev.h: rejected
+__global__ void k_htree_seq(HQueue* q, HNode* nd, uint64_t min_proc, uint32_t analytical,
                             const uint64_t* t, const uint64_t* p, uint64_t n, uint64_t* d, uint32_t* err)
 {
-  HTree tr{q, nd, fl, min_proc, analytical != 0};
-  for (uint64_t i = 0; i < n; ++i) d[i] = tr.delay(t[i], p[i], err);
+  HTree tr{q, nd, min_proc, analytical != 0};
+  for (uint64_t i = 0; i < n; ++i) {
+    if (p[i] == 0) { atomicOr(err, GG_DERR_RANGE); d[i] = 0; continue; }
+    d[i] = tr.delay(t[i], p[i], err);
+  }
 }
 
 __global__ void k_analytical(const HQueue* q, uint32_t tiles, uint64_t* ctr)
@@ -611,7 +606,7 @@ __global__ void k_analytical(const HQueue* q, uint32_t tiles, uint64_t* ctr)
 
 struct gg_noc_state {
   NocParams P;
-  HQueue* q = nullptr; HNode* nd = nullptr; int16_t* fl = nullptr; uint64_t nq = 0;
+  HQueue* q = nullptr; HNode* nd = nullptr; uint64_t nq = 0;
   uint64_t* ctr = nullptr;
   // batch scratch
   uint64_t cap = 0;
@@ -653,7 +648,6 @@ gg_status gg_noc_alloc(gg_ctx* ctx)
   S->nq = (uint64_t)c.num_tiles * 6 + 1;
   GG_HIP(hipMalloc((void**)&S->q, sizeof(HQueue) * S->nq));
   GG_HIP(hipMalloc((void**)&S->nd, sizeof(HNode) * S->nq * P.max_size));
-  GG_HIP(hipMalloc((void**)&S->fl, sizeof(int16_t) * S->nq * P.max_size));
   return GG_OK;
 }
 
@@ -661,7 +655,7 @@ void gg_noc_free(gg_ctx* ctx)
 {
   gg_noc_state* S = ctx->noc;
   if (!S) return;
-  void* ps[] = {S->q, S->nd, S->fl, S->ctr, S->t, S->zl, S->ct, S->cur, S->keys, S->ids, S->heap,
+  void* ps[] = {S->q, S->nd, S->ctr, S->t, S->zl, S->ct, S->cur, S->keys, S->ids, S->heap,
                 S->counts, S->cursor, S->off};
   for (void* p : ps) if (p) hipFree(p);
   delete S;
@@ -672,7 +666,7 @@ gg_status gg_noc_reset(gg_ctx* ctx, hipStream_t s)
 {
   gg_noc_state* S = ctx->noc;
   GG_HIP(hipMemsetAsync(S->ctr, 0, sizeof(uint64_t) * S->P.tiles * GG_NUM_NET_COUNTERS, s));
-  hipLaunchKernelGGL(k_htree_reset, dim3((uint32_t)((S->nq + 255) / 256)), dim3(256), 0, s, S->q, S->nd, S->fl,
+  hipLaunchKernelGGL(k_htree_reset, dim3((uint32_t)((S->nq + 255) / 256)), dim3(256), 0, s, S->q, S->nd,
                      S->nq, S->P.max_size, S->P.qtype, S->P.qaux);
   GG_HIP(hipGetLastError());
   return GG_OK;
@@ -745,7 +739,7 @@ gg_status gg_noc_hbh(gg_ctx* ctx, const uint32_t* src, const uint32_t* dst, cons
   if (cap >= (1ull << 32)) return gg_fail(GG_ERR_RANGE, "batch larger than 2^32 packets");
   const uint32_t nb_max = std::max(P.tiles, 2 * std::max(P.w, P.h));
   if (gg_status st = noc_grow(S, cap, nb_max)) return st;
-  NocDev D{P, S->q, S->nd, S->fl, S->ctr, ctx->err_dev};
+  NocDev D{P, S->q, S->nd, S->ctr, ctx->err_dev};
   PktState PS{S->t, S->zl, S->ct, S->cur, khi, klo};
   const uint32_t blocks = (uint32_t)((cap + 255) / 256);
   gg_timer_begin(ctx, "noc_hop_by_hop", s);
@@ -804,13 +798,13 @@ gg_status gg_htree_run(gg_ctx* ctx, uint64_t min_proc, const uint64_t* t, const 
   hipStream_t s = ctx->last_stream;
   const uint64_t qi = (uint64_t)S->P.tiles * 6;   // the stand-alone queue
   hipLaunchKernelGGL(k_htree_reset, dim3(1), dim3(1), 0, s, S->q + qi, S->nd + qi * S->P.max_size,
-                     S->fl + qi * S->P.max_size, 1ull, S->P.max_size, S->P.qtype, S->P.qaux);
+                     1ull, S->P.max_size, S->P.qtype, S->P.qaux);
   uint64_t* buf = nullptr;
   GG_HIP(hipMalloc((void**)&buf, 24 * (n ? n : 1)));
   GG_HIP(hipMemcpyAsync(buf, t, 8 * n, hipMemcpyHostToDevice, s));
   GG_HIP(hipMemcpyAsync(buf + n, p, 8 * n, hipMemcpyHostToDevice, s));
   hipLaunchKernelGGL(k_htree_seq, dim3(1), dim3(1), 0, s, S->q + qi, S->nd + qi * S->P.max_size,
-                     S->fl + qi * S->P.max_size, min_proc, S->P.analytical, buf, buf + n, n, buf + 2 * n, ctx->err_dev);
+                     min_proc, S->P.analytical, buf, buf + n, n, buf + 2 * n, ctx->err_dev);
   GG_HIP(hipGetLastError());
   GG_HIP(hipMemcpyAsync(d, buf + 2 * n, 8 * n, hipMemcpyDeviceToHost, s));
   GG_HIP(hipStreamSynchronize(s));
@@ -819,4 +813,5 @@ gg_status gg_htree_run(gg_ctx* ctx, uint64_t min_proc, const uint64_t* t, const 
 }
 
 gg::NocParams gg_noc_params(gg_ctx* ctx) { return ctx->noc->P; }
+void gg_noc_queues(gg_ctx* ctx, gg::HQueue** q, gg::HNode** nd) { *q = ctx->noc->q; *nd = ctx->noc->nd; }
 uint64_t* gg_noc_ctr(gg_ctx* ctx) { return ctx->noc->ctr; }

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define GG_ABI_VERSION 2
+#define GG_ABI_VERSION 3
 
 typedef int gg_status;
 enum {
@@ -238,19 +238,36 @@ enum {
   GG_MSG_WB_REP, GG_MSG_NULLIFY_REQ
 };
 
-/* One ShmemMsg in flight (48 bytes).  The per-sender sequence number keeps
+/* One ShmemMsg in flight (64 bytes).  The per-sender sequence number keeps
  * the per-channel FIFO order of the reference transports
- * (socktransport.cc:225,366).                                                */
+ * (socktransport.cc:225,366).  A record is either a message for dst's inbox
+ * (hop == GG_HOP_NONE) or, under emesh_hop_by_hop with several logical
+ * shards, a packet still in the mesh, held at a shard edge: it has left the
+ * output port of a router in one shard and continues at router `hop` of
+ * another shard after the quantum boundary (arrival_ps = its time at `hop`,
+ * contention so far = arrival_ps - send_ps - zero_load_ps).                 */
+#define GG_HOP_NONE 0xFFFFFFFFu
 typedef struct gg_cmsg {
   uint64_t addr;         /* line byte address                                   */
   uint64_t send_ps;      /* NetPacket::time when sent (MemoryManager::sendMsg)  */
   uint64_t arrival_ps;   /* time handed to the receiver, after the network      */
+  uint64_t zero_load_ps; /* zero-load part of the network time so far           */
   uint32_t src, dst;     /* sender / receiver tile                              */
   uint32_t requester;    /* ShmemMsg::_requester                                */
   uint32_t seq;          /* per-sender sequence number                          */
   uint32_t type;         /* GG_MSG_*                                            */
   uint32_t link;         /* backend-private (ignored on import)                 */
+  uint32_t hop;          /* GG_HOP_NONE, or the router tile of a held packet    */
+  uint32_t pad;
 } gg_cmsg;
+
+/* Logical shards: on a full W x H mesh (W = floor(sqrt
+ * num_tiles)) the tiles of shard k are the 2-D block the reference gives
+ * process k of num_shards under emesh_hop_by_hop
+ * (NetworkModelEMeshHopByHop::computeProcessToTileMapping,
+ * network_model_emesh_hop_by_hop.cc:367-433); otherwise contiguous tile
+ * ranges.  Writes tile_shard[num_tiles]; GG_ERR_INVALID if a shard is empty. */
+gg_status gg_shard_map(uint32_t num_tiles, uint32_t num_shards, uint32_t* tile_shard);
 
 /* Per-access output word of the coherent mode: (latency_ps << 2) | level,
  * latency = Core::initiateMemoryAccess final - initial time (core.cc:245-251). */
@@ -285,7 +302,8 @@ enum { GG_RI_QUANTA = 0, GG_RI_STEPS, GG_RI_NET_MSGS, GG_RI_SELF_MSGS, GG_RI_BOU
 /* Result of one quantum on the shards a context owns. */
 typedef struct gg_coherent_status {
   uint64_t steps;           /* steps run                                                */
-  uint64_t boundary_msgs;   /* cross-shard messages waiting for the quantum boundary     */
+  uint64_t boundary_msgs;   /* cross-shard records waiting for the quantum boundary      */
+                            /* (messages + held hop-by-hop packets)                      */
   uint64_t min_next_ps;     /* earliest next-access start of a gated owned tile, ~0 if none */
   uint32_t active_tiles;    /* owned tiles whose trace is not finished                  */
   uint32_t blocked_tiles;   /* owned tiles waiting for EX_REP / SH_REP                  */

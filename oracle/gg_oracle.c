@@ -1001,6 +1001,10 @@ static int cmp_inj(const void* x, const void* y)
   return ev_lt(*a, *b) ? -1 : (ev_lt(*b, *a) ? 1 : 0);
 }
 
+static void noc_hbh_walk(oracle_noc* on, uint64_t n, const uint32_t* src, const uint32_t* dst, const uint32_t* len,
+                         uint32_t* cur, uint64_t* t, uint64_t* zl, uint64_t* ct, const uint8_t* inj,
+                         const uint32_t* shard, uint8_t* held);
+
 /*
  * Route a batch.  emesh_hop_counter: one closed-form hop per packet
  * (network_model_emesh_hop_counter.cc:143-157).  emesh_hop_by_hop: the
@@ -1060,27 +1064,50 @@ int oracle_noc_route(oracle_noc* on, uint64_t n, const uint32_t* src, const uint
 
   if (on->cfg.net_model != GG_NET_EMESH_HOP_BY_HOP) return GG_ERR_UNSUPPORTED;
   if (on->n != on->w * on->h) return GG_ERR_UNSUPPORTED;     /* hop_by_hop.cc:55-59 */
-  const int qm = on->cfg.queue_model_enabled != 0;
-
-  uint64_t* cur = (uint64_t*)malloc(sizeof(uint64_t) * (n ? n : 1));   /* current tile */
-  /* 1. injection ports (routePacket SEND_TILE, hop_by_hop.cc:151-159) */
-  n_ev* inj = (n_ev*)malloc(sizeof(n_ev) * (n ? n : 1));
-  uint64_t ninj = 0;
+  uint32_t* cur = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+  uint8_t* inj = (uint8_t*)malloc(n ? n : 1);
   for (uint64_t k = 0; k < n; ++k) {
-    arrival[k] = time_ps[k]; zero_load[k] = 0; contention[k] = 0; cur[k] = src[k];
-    if (src[k] == dst[k]) continue;                  /* self: zero time, no counters */
-    inj[ninj].t = time_ps[k]; inj[ninj].id = k; ++ninj;
+    arrival[k] = time_ps[k]; zero_load[k] = 0; contention[k] = 0; cur[k] = src[k]; inj[k] = 1;
   }
+  noc_hbh_walk(on, n, src, dst, len, cur, arrival, zero_load, contention, inj, NULL, NULL);
+  free(cur); free(inj);
+  return 0;
+}
+
+/*
+ * emesh_hop_by_hop walk of a batch (hop_by_hop.cc:146-264) in the canonical
+ * discrete-event order: the injection port of every tile serves its NEW
+ * packets (inj[k] != 0) in (time, packet index) order (routePacket SEND_TILE,
+ * :151-159), then every mesh router output port serves the packets that reach
+ * it in (arrival time, packet index) order — what one global event queue keyed
+ * (time_ps, packet index) produces.  Packet state in/out: cur (router tile),
+ * t (time), zl, ct.  With a tile -> logical shard table `shard`, a packet whose
+ * next router lies in another shard stops after the output port + link of its
+ * current router (held[k] = 1, cur[k] = that next router): it continues there
+ * after the quantum boundary.  Self packets (src == dst)
+ * are left untouched (processCornerCases, network_model.cc:413-424).
+ */
+static void noc_hbh_walk(oracle_noc* on, uint64_t n, const uint32_t* src, const uint32_t* dst, const uint32_t* len,
+                         uint32_t* cur, uint64_t* t, uint64_t* zl, uint64_t* ct, const uint8_t* inj,
+                         const uint32_t* shard, uint8_t* held)
+{
+  const double f = on->cfg.frequency_ghz;
+  const int qm = on->cfg.queue_model_enabled != 0;
+  n_heap heap = { 0, 0, 0 };
+  /* 1. injection ports of the new packets: stable grouping by source, (time, index) order */
   {
-    /* stable grouping by source: sort by (src, time, id) */
     uint64_t* cnt = (uint64_t*)calloc(on->n + 1, sizeof(uint64_t));
-    for (uint64_t i = 0; i < ninj; ++i) cnt[src[inj[i].id] + 1]++;
+    uint64_t ninj = 0;
+    for (uint64_t k = 0; k < n; ++k) if (inj[k] && src[k] != dst[k]) { cnt[src[k] + 1]++; ninj++; }
     for (uint32_t s = 0; s < on->n; ++s) cnt[s + 1] += cnt[s];
     n_ev* by = (n_ev*)malloc(sizeof(n_ev) * (ninj ? ninj : 1));
     uint64_t* pos = (uint64_t*)malloc(sizeof(uint64_t) * (on->n + 1));
     memcpy(pos, cnt, sizeof(uint64_t) * (on->n + 1));
-    for (uint64_t i = 0; i < ninj; ++i) by[pos[src[inj[i].id]]++] = inj[i];
-    n_heap heap = { 0, 0, 0 };
+    for (uint64_t k = 0; k < n; ++k) {
+      if (src[k] == dst[k]) continue;                            /* self: zero time, no counters */
+      if (inj[k]) { n_ev e = { t[k], k }; by[pos[src[k]]++] = e; }
+      else { n_ev e = { t[k], k }; heap_push(&heap, e); }          /* held packet resuming at cur[k] */
+    }
     for (uint32_t s = 0; s < on->n; ++s) {
       uint64_t b = cnt[s], e = cnt[s + 1];
       qsort(by + b, e - b, sizeof(n_ev), cmp_inj);
@@ -1088,50 +1115,49 @@ int oracle_noc_route(oracle_noc* on, uint64_t n, const uint32_t* src, const uint
         uint64_t k = by[i].id;
         n_send_counters(on, src[k], len[k]);
         uint64_t qd = 0;
-        if (qm) qd = oracle_htree_delay(on->inj[s], time_to_cycles(arrival[k], f), n_flits(on, len[k]));
+        if (qm) qd = oracle_htree_delay(on->inj[s], time_to_cycles(t[k], f), n_flits(on, len[k]));
         uint64_t cps = lat_to_ps(qd, f);
-        arrival[k] += lat_to_ps(0, f) + cps; contention[k] += cps;
-        n_ev ev = { arrival[k], k };
+        t[k] += lat_to_ps(0, f) + cps; ct[k] += cps;
+        n_ev ev = { t[k], k };
         heap_push(&heap, ev);
       }
     }
     free(cnt); free(by); free(pos);
-    /* 2. mesh hops in global (time, index) order (hop_by_hop.cc:223-256) */
-    while (heap.n) {
-      n_ev ev = heap_pop(&heap);
-      uint64_t k = ev.id;
-      uint32_t c = (uint32_t)cur[k];
-      int cx = (int)(c % on->w), cy = (int)(c / on->w);
-      int dx = (int)(dst[k] % on->w), dy = (int)(dst[k] / on->w);
-      int port; uint32_t next;
-      if (cx > dx)      { port = P_LEFT;  next = c - 1; }
-      else if (cx < dx) { port = P_RIGHT; next = c + 1; }
-      else if (cy > dy) { port = P_DOWN;  next = c - on->w; }
-      else if (cy < dy) { port = P_UP;    next = c + on->w; }
-      else              { port = P_SELF;  next = c; }
-      uint64_t nf = n_flits(on, len[k]);
-      uint64_t zlc = on->cfg.router_delay, qd = 0;   /* RouterModel::processPacket (router_model.cc:71-108) */
-      uint64_t* cc = ncnt(on, c);
-      if (qm) {
-        qd = oracle_htree_delay(on->q[(size_t)c * NPORTS + port], time_to_cycles(arrival[k], f), nf);
-        cc[GG_NC_ROUTER_CONTENTION_CYCLES] += qd; cc[GG_NC_ROUTER_PACKETS]++;
-      }
-      cc[GG_NC_BUFFER_WRITES] += nf; cc[GG_NC_BUFFER_READS] += nf; cc[GG_NC_SWITCH_ALLOC] += 1; cc[GG_NC_CROSSBAR] += nf;
-      zlc += on->cfg.link_delay;                      /* ElectricalLinkModel::processPacket (electrical_link_model.cc:31-45) */
-      cc[GG_NC_LINK_TRAVERSALS] += nf;
-      uint64_t zps = lat_to_ps(zlc, f), cps = lat_to_ps(qd, f);
-      arrival[k] += zps + cps; zero_load[k] += zps; contention[k] += cps;
-      if (port == P_SELF) {
-        n_receive(on, dst[k], len[k], &arrival[k], &zero_load[k], contention[k]);
-      } else {
-        cur[k] = next;
-        n_ev ne = { arrival[k], k };
-        heap_push(&heap, ne);
-      }
-    }
-    free(heap.a);
   }
-  free(inj); free(cur);
-  return 0;
+  /* 2. mesh hops in global (time, index) order (hop_by_hop.cc:223-256) */
+  while (heap.n) {
+    n_ev ev = heap_pop(&heap);
+    uint64_t k = ev.id;
+    uint32_t c = cur[k];
+    int cx = (int)(c % on->w), cy = (int)(c / on->w);
+    int dx = (int)(dst[k] % on->w), dy = (int)(dst[k] / on->w);
+    int port; uint32_t next;
+    if (cx > dx)      { port = P_LEFT;  next = c - 1; }
+    else if (cx < dx) { port = P_RIGHT; next = c + 1; }
+    else if (cy > dy) { port = P_DOWN;  next = c - on->w; }
+    else if (cy < dy) { port = P_UP;    next = c + on->w; }
+    else              { port = P_SELF;  next = c; }
+    uint64_t nf = n_flits(on, len[k]);
+    uint64_t zlc = on->cfg.router_delay, qd = 0;   /* RouterModel::processPacket (router_model.cc:71-108) */
+    uint64_t* cc = ncnt(on, c);
+    if (qm) {
+      qd = oracle_htree_delay(on->q[(size_t)c * NPORTS + port], time_to_cycles(t[k], f), nf);
+      cc[GG_NC_ROUTER_CONTENTION_CYCLES] += qd; cc[GG_NC_ROUTER_PACKETS]++;
+    }
+    cc[GG_NC_BUFFER_WRITES] += nf; cc[GG_NC_BUFFER_READS] += nf; cc[GG_NC_SWITCH_ALLOC] += 1; cc[GG_NC_CROSSBAR] += nf;
+    zlc += on->cfg.link_delay;                      /* ElectricalLinkModel::processPacket (electrical_link_model.cc:31-45) */
+    cc[GG_NC_LINK_TRAVERSALS] += nf;
+    uint64_t zps = lat_to_ps(zlc, f), cps = lat_to_ps(qd, f);
+    t[k] += zps + cps; zl[k] += zps; ct[k] += cps;
+    if (port == P_SELF) {
+      n_receive(on, dst[k], len[k], &t[k], &zl[k], ct[k]);
+    } else {
+      cur[k] = next;
+      if (shard && shard[next] != shard[c]) { held[k] = 1; continue; }   /* leaves the shard: held */
+      n_ev ne = { t[k], k };
+      heap_push(&heap, ne);
+    }
+  }
+  free(heap.a);
 }
 #include "gg_coherent.inc"

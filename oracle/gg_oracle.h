@@ -82,6 +82,8 @@ void oracle_noc_counters(const oracle_noc* on, uint64_t* out); /* [tile][GG_NUM_
  * quanta in the canonical schedule (oracle/gg_coherent.inc).  The context
  * owns shards [cfg.shard_begin, cfg.shard_end) of cfg.num_shards.          */
 typedef struct oracle_coh oracle_coh;
+/* tile -> logical shard (emesh_hop_by_hop process mapping, hop_by_hop.cc:367-433) */
+int  oracle_shard_map(uint32_t num_tiles, uint32_t num_shards, uint32_t* tile_shard);
 oracle_coh* oracle_coh_create(const gg_config* cfg);
 void        oracle_coh_destroy(oracle_coh* C);
 int  oracle_coh_begin(oracle_coh* C, const uint64_t* addr, const uint32_t* meta,

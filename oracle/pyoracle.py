@@ -71,6 +71,8 @@ def lib():
         L.oracle_split_lines.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _u64p, ctypes.c_uint32]
         L.oracle_gen_hotspot.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u64p, _u32p]
+        L.oracle_shard_map.restype = ctypes.c_int
+        L.oracle_shard_map.argtypes = [ctypes.c_uint32, ctypes.c_uint32, _u32p]
         L.oracle_coh_create.restype = vp
         L.oracle_coh_create.argtypes = [ctypes.POINTER(GGConfig)]
         L.oracle_coh_destroy.argtypes = [vp]
@@ -116,6 +118,14 @@ def gen_trace(tiles, per_tile, **kw):
     meta = np.concatenate([p[1] for p in parts]) if parts else np.zeros(0, np.uint32)
     offs = np.arange(tiles + 1, dtype=np.uint64) * np.uint64(per_tile)
     return addr, meta, offs
+
+
+def shard_map(num_tiles, num_shards):
+    """tile -> logical shard of the oracle (hop_by_hop.cc:367-433 restated)."""
+    out = np.zeros(num_tiles, np.uint32)
+    if lib().oracle_shard_map(num_tiles, num_shards, out) != 0:
+        raise ValueError("no shard map for %d tiles in %d shards" % (num_tiles, num_shards))
+    return out
 
 
 class OracleCoherent:

@@ -98,7 +98,39 @@ static const UInt64* g_addr; static const UInt32* g_meta; static UInt64* g_out;
 static UInt64 g_barrier;
 static UInt32 g_cur;          // tile whose code is running
 
-static UInt32 shard_of(UInt32 t) { return (UInt32)(((UInt64)t * H.K) / H.T); }
+// Logical shards = the process -> tile mapping NetworkModelEMeshHopByHop::
+// computeProcessToTileMapping gives K processes (network_model_emesh_hop_by_hop.cc:
+// 367-433; its translation unit pulls DSENT / Berkeley-DB headers through
+// router_model.h, so it is restated here): 2-D blocks of the W x H mesh, or
+// contiguous tile ranges when the tile count is not a full mesh.
+static vector<UInt32> g_shard;
+static void build_shard_map()
+{
+  const SInt32 T = (SInt32)H.T, K = (SInt32)H.K;
+  g_shard.assign(T, 0);
+  const SInt32 W = (SInt32)floor(sqrt(T)), Hh = (SInt32)ceil(1.0 * T / W);
+  if (W * Hh != T) { for (SInt32 t = 0; t < T; ++t) g_shard[t] = (UInt32)(((UInt64)t * K) / T); return; }
+  const SInt32 pw = (SInt32)floor(sqrt(K)), ph = (SInt32)floor(1.0 * K / pw);
+  const SInt32 hl = (SInt32)((1.0 * Hh * pw * ph) / K);
+  for (SInt32 i = 0; i < pw; i++)
+    for (SInt32 j = 0; j < ph; j++) {
+      SInt32 sx = W / pw, sy = hl / ph;
+      const SInt32 bx = i * sx, by = j * sy;
+      if (i == pw - 1) sx = W - (pw - 1) * sx;
+      if (j == ph - 1) sy = hl - (ph - 1) * sy;
+      for (SInt32 ii = 0; ii < sx; ii++)
+        for (SInt32 jj = 0; jj < sy; jj++) g_shard[(bx + ii) + (by + jj) * W] = (UInt32)(i + j * pw);
+    }
+  const SInt32 left = K - pw * ph;
+  for (SInt32 i = pw * ph; i < K; i++) {
+    SInt32 sx = W / left;
+    const SInt32 sy = Hh - hl, bx = (i - pw * ph) * sx, by = hl;
+    if (i == K - 1) sx = W - (left - 1) * sx;
+    for (SInt32 ii = 0; ii < sx; ii++)
+      for (SInt32 jj = 0; jj < sy; jj++) g_shard[(bx + ii) + (by + jj) * W] = (UInt32)i;
+  }
+}
+static UInt32 shard_of(UInt32 t) { return g_shard[t]; }
 static int tile_of(MemoryManager* mm) { return mm->getTile()->getId(); }
 
 // ===========================================================================
@@ -759,6 +791,7 @@ static void run_case(FILE* man, bool first, const char* name, UInt32 T, UInt32 N
                      UInt32 dir_entries, UInt32 dir_assoc)
 {
   H.T = T; H.K = K; H.net = net; H.dir_entries = dir_entries; H.dir_assoc = dir_assoc; H.quantum_ps = 1000000;
+  build_shard_map();
   g_t.clear(); g_t.resize(T); g_step.clear(); g_bnd.clear(); g_cc.clear(); g_dc.clear(); g_dram.clear();
   vector<UInt64> addr((size_t)T * N); vector<UInt32> meta((size_t)T * N); vector<UInt64> out((size_t)T * N, 0);
   for (UInt32 t = 0; t < T; ++t) gen_hotspot(t, N, hot, &addr[(size_t)t * N], &meta[(size_t)t * N]);
@@ -822,6 +855,8 @@ int main(int argc, char** argv)
   run_case(man, false, "hot16magic", 16, 1000, 8, 1, 0, 0, 16);
   run_case(man, false, "dir16", 16, 1000, 32, 1, 1, 64, 4);
   run_case(man, false, "shard64", 64, 400, 32, 8, 1, 0, 16);
+  run_case(man, false, "hot256", 256, 120, 64, 1, 1, 0, 16);
+  run_case(man, false, "shard256", 256, 150, 64, 8, 1, 0, 16);
   fprintf(man, "\n}\n");
   fclose(man);
   return 0;

@@ -257,14 +257,15 @@ static const UInt64 kKat[10][3] = {
   {10, 10, 0}, {21, 10, 0}, {32, 10, 0}, {43, 10, 0}, {0, 1, 0},
   {0, 10, 53}, {45, 10, 18}, {60, 4, 13}, {70, 8, 7}, {75, 10, 10}};
 
-static void gen_htree(const char* name, uint64_t seed, int n, UInt64 span, UInt64 maxp, int max_size, bool an) {
+static void gen_htree(const char* name, uint64_t seed, int n, UInt64 span, UInt64 maxp, int max_size, bool an,
+                      UInt64 gap = 0) {
   RefHistoryTree h(1, max_size, an);
   vector<UInt64> rows;
   UInt64 base = 0;
   for (int i = 0; i < n; ++i) {
     uint64_t z = sm_at(seed, (uint64_t)i);
     // mostly increasing arrival times with out-of-order stragglers
-    base += (z & 7);
+    base += gap + (z & 7);
     UInt64 t = ((z >> 8) % 4 == 0 && base > span) ? base - ((z >> 16) % span) : base;
     UInt64 p = 1 + ((z >> 32) % maxp);
     UInt64 d = h.delay(t, p);
@@ -449,6 +450,11 @@ int main(int argc, char** argv) {
   gen_htree("htree_rand_b", 2, 4000, 300, 3, 100, true);
   gen_htree("htree_rand_c", 3, 3000, 40, 12, 16, true);
   gen_htree("htree_rand_noan", 4, 3000, 64, 9, 100, false);
+  // sparse arrivals grow the history to max_list_size, so the oldest free
+  // intervals are pruned and stragglers behind them take the M/G/1 branch
+  // (queue_model_history_tree.cc:52-64)
+  gen_htree("htree_analytical", 13, 4000, 4000, 9, 16, true, 12);
+  gen_htree("htree_analytical8", 14, 4000, 2000, 9, 8, true, 12);
   // 2b. history_list and basic queue models on the same arrival process
   gen_qlist("qlist_rand_a", 1, 4000, 64, 9, 100, true, true);
   gen_qlist("qlist_rand_b", 2, 4000, 300, 3, 100, true, true);

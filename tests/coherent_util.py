@@ -22,7 +22,8 @@ class OracleEngine:
         import torch
         msgs = self.o.export(1 << 20)
         K = self.cfg.num_shards
-        shard = (msgs["dst"].astype(np.int64) * K) // self.cfg.num_tiles
+        at = np.where(msgs["hop"] == C.HOP_NONE, msgs["dst"], msgs["hop"])
+        shard = C.shard_map(self.cfg.num_tiles, K)[at]
         counts = np.bincount(shard, minlength=K)
         return torch.from_numpy(msgs.view(np.uint8).copy()), counts
 

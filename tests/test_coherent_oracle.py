@@ -76,3 +76,43 @@ def test_directory_replacement_nullify():
     check_invariants(st, oc.cache_counters(), out, o, per_tile_expected=N)
     assert st[:, C.TILE_STATS.index("dir_evictions")].sum() > 0
     assert st[:, C.TILE_STATS.index("dir_back_invalidations")].sum() > 0
+
+
+@pytest.mark.parametrize("T,K", [(16, 2), (64, 8), (256, 8)])
+def test_hop_by_hop_shards_invariants_and_determinism(T, K):
+    """emesh_hop_by_hop across logical shards (packets held at the shard edge
+    and resumed after the quantum boundary): invariants, determinism, and the
+    same network totals as a run with one shard wherever they must agree."""
+    N = 300
+    a, m, o = po.gen_trace(T, N, hot_lines=32)
+    cfg = C.default_config(T, num_shards=K, net_model=C.NET_EMESH_HOP_BY_HOP)
+    runs = []
+    for _ in range(2):
+        oc = po.OracleCoherent(cfg)
+        out = oc.run(a, m, o)
+        runs.append((out, oc.tile_stats(), oc.cache_counters(), oc.net_counters(), oc.run_info()))
+        check_invariants(runs[-1][1], runs[-1][2], out, o, per_tile_expected=N)
+    for x, y in zip(*runs):
+        np.testing.assert_array_equal(x, y)
+    nc = runs[0][3]
+    names = C.NET_COUNTERS
+    assert nc[:, names.index("packets_sent")].sum() == nc[:, names.index("packets_received")].sum()
+    assert runs[0][4][C.RUN_INFO.index("boundary_msgs")] > 0
+
+
+def test_shard_blocks_keep_routes_inside():
+    """Every XY route between two tiles of one 2-D block shard stays in it."""
+    for T, K in [(64, 8), (256, 4), (1024, 8), (256, 5)]:
+        sm = C.shard_map(T, K)
+        w = int(np.sqrt(T))
+        for s in range(0, T, 7):
+            for d in range(0, T, 5):
+                if sm[s] != sm[d]:
+                    continue
+                x, y = s % w, s // w
+                while x != d % w:
+                    x += 1 if d % w > x else -1
+                    assert sm[y * w + x] == sm[s]
+                while y != d // w:
+                    y += 1 if d // w > y else -1
+                    assert sm[y * w + x] == sm[s]

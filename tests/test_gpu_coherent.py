@@ -56,6 +56,14 @@ def _compare(cfg, a, m, o):
     (16, 1500, 8, 1, C.NET_EMESH_HOP_BY_HOP),      # configs[2]: router / link contention
     (64, 700, 64, 1, C.NET_EMESH_HOP_BY_HOP),
     (256, 200, 64, 1, C.NET_EMESH_HOP_BY_HOP),
+    # hop-by-hop across logical shards: packets held at a shard's edge router
+    # continue in the next quantum (2-D block shards, hop_by_hop.cc:367-433)
+    (16, 1200, 8, 2, C.NET_EMESH_HOP_BY_HOP),
+    (64, 600, 32, 8, C.NET_EMESH_HOP_BY_HOP),
+    (256, 150, 64, 4, C.NET_EMESH_HOP_BY_HOP),
+    (256, 150, 64, 8, C.NET_EMESH_HOP_BY_HOP),
+    (1024, 48, 256, 8, C.NET_EMESH_HOP_BY_HOP),     # configs[3]: 1024 tiles x 8 shards (reduced per-tile length)
+    (1024, 64, 256, 8, C.NET_EMESH_HOP_COUNTER),
 ])
 def test_coherent_matches_oracle(T, N, hot, K, net):
     from oracle import pyoracle as po
@@ -128,15 +136,52 @@ def test_gpu_hotspot_generator_matches_oracle():
     np.testing.assert_array_equal(to_np(meta, np.uint32), m)
 
 
-def test_coherent_rejects_unbuilt_config():
+@pytest.mark.parametrize("net", [C.NET_EMESH_HOP_BY_HOP, C.NET_EMESH_HOP_COUNTER])
+def test_coherent_contexts_split_equals_one_context(net):
+    """1 context x 8 logical shards == 2 contexts x 4 shards each (exchanging
+    messages and held hop-by-hop packets at every quantum boundary) == 4
+    contexts x 2, bit for bit: the schedule depends on the shard count only."""
     torch = torch_dev()
     from graphite_amd import backend as B
+    from graphite_amd import coherent as CO
     from oracle import pyoracle as po
-    cfg = C.default_config(16, net_model=C.NET_EMESH_HOP_BY_HOP, num_shards=2)   # router queues split by shard: not built
-    a, m, o = po.gen_trace(16, 10)
-    be = B.Backend(cfg)
-    with pytest.raises(B.GGError):
-        be.coherent_run(to_dev(torch, a, torch.int64), to_dev(torch, m, torch.int32), o)
+    T, N, K = 64, 500, 8
+    a, m, o = po.gen_trace(T, N, hot_lines=32)
+    addr, meta = to_dev(torch, a, torch.int64), to_dev(torch, m, torch.int32)
+    results = []
+    for R in (1, 2, 4):
+        outs, engines, bes = [], [], []
+        for r in range(R):
+            k0, k1 = CO.shard_range(r, R, K)
+            be = B.Backend(C.default_config(T, num_shards=K, shard_begin=k0, shard_end=k1, net_model=net))
+            out = torch.zeros(len(a), dtype=torch.int64, device="cuda")
+            engines.append(B.CoherentEngine(be, addr, meta, o, out))
+            outs.append(out); bes.append(be)
+        CO.run_local(engines, 1000 * 1000, K)
+        torch.cuda.synchronize()
+        got = sum(to_np(x, np.uint64) for x in outs)
+        st = sum(be.coherent_stats()[0] for be in bes)
+        nc = sum(be.noc_counters() for be in bes)
+        results.append((got, st, nc))
+    for g in results[1:]:
+        for x, y in zip(results[0], g):
+            np.testing.assert_array_equal(x, y)
+    ref = _oracle_run(C.default_config(T, num_shards=K, net_model=net), a, m, o)
+    np.testing.assert_array_equal(results[0][0], ref[0])
+    np.testing.assert_array_equal(results[0][1], ref[1])
+    np.testing.assert_array_equal(results[0][2], ref[3])
+
+
+def test_coherent_hop_by_hop_holds_packets_at_shard_edges():
+    """With 8 shards some packets stop at a shard's edge router and resume in
+    the next quantum; every message still arrives (sent == received)."""
+    from oracle import pyoracle as po
+    T, N, K = 256, 100, 8
+    cfg = C.default_config(T, num_shards=K, net_model=C.NET_EMESH_HOP_BY_HOP)
+    a, m, o = po.gen_trace(T, N, hot_lines=64)
+    g = _compare(cfg, a, m, o)
+    ri = g[4]
+    assert ri[C.RUN_INFO.index("boundary_msgs")] > 0
 
 
 @pytest.mark.parametrize("name", sorted(__import__("golden_util").coh_manifest()))
