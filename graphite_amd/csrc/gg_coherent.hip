@@ -80,6 +80,10 @@ __device__ __forceinline__ bool has_data(uint32_t t)
 struct DEnt { uint64_t addr; int32_t owner; uint16_t dstate; uint16_t nsh; };   // 16 B
 struct CReq { uint64_t addr, time; uint32_t type, requester; };                 // 24 B
 struct Seg { uint32_t line, lo, hi, pad; };       // a run of row (X) / column (Y) `line`: positions [lo, hi]
+// device-driven quantum loop (gg_coherent_run): current quantum, launch index
+// of its step 0, run over, quantum-end arrivals, active / blocked tiles, least
+// next start, quanta completed, quantum length
+enum { QS_Q = 0, QS_START, QS_DONE, QS_ARRIVED, QS_ACTIVE, QS_BLOCKED, QS_MIN_NEXT, QS_COUNT, QS_QPS, QS_N };
 
 constexpr uint32_t kInLds = 512;       // inbox / port batch entries ordered in LDS (more: global scratch)
 constexpr uint32_t kRqLds = 512;       // directory request FIFO entries staged in LDS
@@ -88,7 +92,7 @@ constexpr uint32_t kChunk = 16;        // records per chunk
 constexpr uint32_t kQMax = 128;        // largest max_list_size of a queue staged in LDS (wave ops: 2 per lane)
 constexpr uint32_t kNetCtr = 7;        // router / link counters a walker accumulates per position
 constexpr size_t kWalkLdsMax = 160 * 1024;
-constexpr uint32_t kWalkPkBytes = 5 * 8 + 4 * 4;   // t, khi, klo, zl, (pad) | idx, pos, dpos, nf/status
+constexpr uint32_t kWalkPkBytes = 5 * 8 + 7 * 4;   // t, send, key, zl, queue t | idx, pos, dpos, nf/status, rank, queue rank, queue slot
 
 struct CP {
   uint32_t T, K, L;                      // tiles, logical shards, owned tiles
@@ -122,11 +126,20 @@ struct CS {
   const uint32_t* tseg;                  // [T][2]: X run, Y run of a tile (~0 if not owned)
   gg_cmsg* bnd; uint32_t* bnd_cnt;       // held for the quantum boundary
   uint32_t* ring; uint32_t* quiet;       // records sent per step (mod 4); quiet flag of the quantum
+  uint32_t* imp;                         // [2] held packets imported for the quantum of parity Q & 1
+  uint32_t* live;                        // [4] launch L & 3: step index + 1 of a step launch, 0 otherwise
+  uint64_t* qs;                          // device-driven run: QS_* below
   uint64_t* ri; uint32_t* err;
   HQueue* nq; HNode* nnd;                // router queues [tile * 6 + port]
   uint64_t* ctr;                         // NoC counters [T][GG_NUM_NET_COUNTERS]
   uint64_t* gscr;                        // [L][5 * IC] ordering scratch beyond kInLds
+  unsigned long long* prof;              // GG_COH_PROFILE=1: shader-clock cycles per phase (diagnostics)
 };
+// profile slots: step phases 0..5 summed over tiles, 8 = sum over steps of the slowest tile;
+// walker: 16 staging+load, 17 event loop, 18 hand-off+write back, 19 events, 20 sum of slowest walker per launch (X),
+// 21 (Y), 22 launches
+#define PROF_T0() const uint64_t _p0 = S.prof ? __builtin_amdgcn_s_memtime() : 0
+#define PROF_AT(var) const uint64_t var = S.prof ? __builtin_amdgcn_s_memtime() : 0
 
 __device__ __forceinline__ gg_cmsg* pool(const CS& S, uint32_t p) { return p ? S.pool1 : S.pool0; }
 __device__ __forceinline__ uint32_t* inb(const CS& S, uint32_t p) { return p ? S.inb1 : S.inb0; }
@@ -178,13 +191,30 @@ struct Cache {
   uint64_t* tag; uint8_t* meta; uint8_t* rr; uint64_t* cg;
   uint32_t sets, ways, log_line, pol, wb, ln;
   uint32_t c[GG_NUM_CACHE_COUNTERS];   // this step's counter increments, flushed to cg
+  // the last set this lane loaded (its way), kept in step with every store, so
+  // consecutive operations on one set load it once
+  uint32_t cset; uint64_t ctv; uint32_t cmv;
 
   __device__ __forceinline__ uint32_t set_of(uint64_t a) const { return (uint32_t)((a >> log_line) & (sets - 1)); }   // cache_hash_fn.h:17
   __device__ __forceinline__ uint64_t tag_of(uint64_t a) const { return a >> log_line; }                             // cache.cc:495
-  __device__ __forceinline__ void ld(uint32_t s, uint64_t& tv, uint32_t& mv) const
+  __device__ __forceinline__ void ld(uint32_t s, uint64_t& tv, uint32_t& mv)
   {
-    tv = INV_ADDR; mv = 0;
-    if (ln < ways) { tv = tag[(size_t)s * ways + ln]; mv = meta[(size_t)s * ways + ln]; }
+    if (s != cset) {
+      ctv = INV_ADDR; cmv = 0;
+      if (ln < ways) { ctv = tag[(size_t)s * ways + ln]; cmv = meta[(size_t)s * ways + ln]; }
+      cset = s;
+    }
+    tv = ctv; mv = cmv;
+  }
+  __device__ __forceinline__ void st_meta(uint32_t s, uint32_t v)      // this lane's way
+  {
+    meta[(size_t)s * ways + ln] = (uint8_t)v;
+    if (s == cset) cmv = v;
+  }
+  __device__ __forceinline__ void st_tag(uint32_t s, uint64_t v)
+  {
+    tag[(size_t)s * ways + ln] = v;
+    if (s == cset) ctv = v;
   }
   // CacheSet::find (cache_set.cc:57-70): tags are unique, so any matching lane is the way
   __device__ __forceinline__ int way_of(uint64_t tv, uint64_t t) const
@@ -201,7 +231,7 @@ struct Cache {
       uint32_t nv = mv;
       if ((int)ln == w) nv = mv & 7u;
       else if (a < acc) nv = (mv & 7u) | ((a + 1) << 3);
-      if (nv != mv) meta[(size_t)s * ways + ln] = (uint8_t)nv;
+      if (nv != mv) st_meta(s, nv);
     }
   }
   __device__ __forceinline__ void miss_counters(bool wr, bool miss)                                               // cache.cc:321-360
@@ -229,8 +259,8 @@ struct Cache {
     const int w = way_of(tv, tag_of(a));
     if (w < 0) return false;
     if ((int)ln == w) {
-      meta[(size_t)s * ways + ln] = (uint8_t)((mv & 0xF8u) | st | (loc << 2));
-      if (st == ST_I) tag[(size_t)s * ways + ln] = INV_ADDR;
+      st_meta(s, (mv & 0xF8u) | st | (loc << 2));
+      if (st == ST_I) st_tag(s, INV_ADDR);
     }
     c[GG_CC_TAG_WRITES]++;
     return true;
@@ -272,8 +302,8 @@ struct Cache {
     if (ev) { ev_addr = vt << log_line; ev_st = vm & 3u; ev_loc = (vm >> 2) & 1u; }
     if ((int)ln == w) {
       const uint32_t nm = (vm & 0xF8u) | st | (loc << 2);
-      tag[(size_t)s * ways + ln] = tag_of(a);
-      meta[(size_t)s * ways + ln] = (uint8_t)nm;
+      st_tag(s, tag_of(a));
+      st_meta(s, nm);
       mv = nm;
     }
     touch(s, w, mv);
@@ -285,11 +315,6 @@ struct Cache {
     }
     c[GG_CC_TAG_WRITES]++; c[GG_CC_DATA_WRITES]++;
     return true;
-  }
-  __device__ __forceinline__ void flush()
-  {
-    const uint32_t v = pick(c, ln);
-    if (ln < GG_NUM_CACHE_COUNTERS && v) cg[ln] += v;
   }
 };
 
@@ -324,14 +349,15 @@ struct Tile {
   CReq* rqp; bool rq_lds;
   uint32_t nch, cbase, cused, ccap, nsent;
   bool failed;
+  uint64_t ccv, stv;                    // lane k's cache counter k (of 2 x 12) and statistic k, loaded at step start
 
   __device__ __forceinline__ Tile(const CP& P_, const CS& S_, uint32_t l, uint32_t par, StepLds& s_)
       : P(P_), S(S_), lt(l), tile(S_.gtile[l]), ln(lane_id()), p(par), sl(s_)
   {
     L1 = Cache{S.l1_tag + (size_t)lt * P.s1 * P.a1, S.l1_meta + (size_t)lt * P.s1 * P.a1, S.l1_rr + (size_t)lt * P.s1,
-               S.cc + (size_t)lt * 2 * GG_NUM_CACHE_COUNTERS, P.s1, P.a1, P.log_line, P.pol1, 0, ln, {}};
+               S.cc + (size_t)lt * 2 * GG_NUM_CACHE_COUNTERS, P.s1, P.a1, P.log_line, P.pol1, 0, ln, {}, ~0u, 0, 0};
     L2 = Cache{S.l2_tag + (size_t)lt * P.s2 * P.a2, S.l2_meta + (size_t)lt * P.s2 * P.a2, S.l2_rr + (size_t)lt * P.s2,
-               S.cc + ((size_t)lt * 2 + 1) * GG_NUM_CACHE_COUNTERS, P.s2, P.a2, P.log_line, P.pol2, 1, ln, {}};
+               S.cc + ((size_t)lt * 2 + 1) * GG_NUM_CACHE_COUNTERS, P.s2, P.a2, P.log_line, P.pol2, 1, ln, {}, ~0u, 0, 0};
 #pragma unroll
     for (int k = 0; k < GG_NUM_TILE_STATS; ++k) st[k] = 0;
     rec = S.rec[lt]; rec_end = S.rec_end[lt]; clk = S.clk[lt]; pend_start = S.pend_start[lt];
@@ -340,6 +366,8 @@ struct Tile {
     dq = S.dq + lt; dnd = S.dnd + (size_t)lt * P.max_list; dq_lds = false;
     rqp = S.rq + (size_t)lt * P.QC; rq_lds = false;
     nch = 0; cbase = 0; cused = 0; ccap = 0; nsent = 0; failed = false;
+    ccv = ln < 2 * GG_NUM_CACHE_COUNTERS ? S.cc[(size_t)lt * 2 * GG_NUM_CACHE_COUNTERS + ln] : 0;
+    stv = ln < GG_NUM_TILE_STATS ? S.st[(size_t)lt * GG_NUM_TILE_STATS + ln] : 0;
   }
   __device__ __forceinline__ void fail(uint32_t e = GG_DERR_STATE)
   {
@@ -562,11 +590,11 @@ struct Tile {
   // ---- DramCntlr / DramPerfModel --------------------------------------------
   __device__ __forceinline__ uint64_t dram_ps(uint64_t t)
   {
-    const uint64_t pkt_ns = (uint64_t)ceil(t / 1000.0);
+    const uint64_t pkt_ns = time_to_cycles(t, 1.0);                  // ceil(t / 1000.0)
     uint64_t qd = 0;
     if (P.dram_qm) {
       HTree tr{dq, dnd, P.dram_proc, P.analytical != 0};
-      qd = dq_lds ? tr.delay_wave(pkt_ns, P.dram_proc, S.err, ln) : tr.delay(pkt_ns, P.dram_proc, S.err);
+      qd = tr.delay(pkt_ns, P.dram_proc, S.err);      // every lane, identical (LDS image or HBM)
       st[GG_CT_DRAM_QUEUE_REQUESTS]++;
     }
     const uint64_t lat = qd + P.dram_proc + P.dram_cost;
@@ -887,15 +915,18 @@ struct Tile {
     }
   }
 
+  // store-only write back: the counters were loaded with the tile
   __device__ __forceinline__ void flush()
   {
-    L1.flush(); L2.flush();
-    uint64_t* g = S.st + (size_t)lt * GG_NUM_TILE_STATS;
-    for (uint32_t k0 = 0; k0 < GG_NUM_TILE_STATS; k0 += 64) {
-      const uint32_t k = k0 + ln;
-      const uint64_t v = pick(st, k);
-      if (k == GG_CT_CLOCK_PS) g[k] = clk;
-      else if (k < GG_NUM_TILE_STATS && v) g[k] += v;
+    {
+      const uint32_t d = ln < GG_NUM_CACHE_COUNTERS ? pick(L1.c, ln) : pick(L2.c, ln - GG_NUM_CACHE_COUNTERS);
+      if (ln < 2 * GG_NUM_CACHE_COUNTERS && d) S.cc[(size_t)lt * 2 * GG_NUM_CACHE_COUNTERS + ln] = ccv + d;
+    }
+    {
+      const uint64_t d = pick(st, ln);
+      uint64_t* g = S.st + (size_t)lt * GG_NUM_TILE_STATS;
+      if (ln == GG_CT_CLOCK_PS) g[ln] = clk;
+      else if (ln < GG_NUM_TILE_STATS && d) g[ln] = stv + d;
     }
     S.rec[lt] = rec; S.clk[lt] = clk; S.pend_start[lt] = pend_start;
     S.out_addr[lt] = out_addr; S.out_time[lt] = out_time;
@@ -951,21 +982,49 @@ __device__ void order_port(uint32_t n, const uint64_t* t, const uint64_t* s, con
   __syncthreads();
 }
 
-__device__ __forceinline__ void copy_img(void* dst, const void* src, uint32_t bytes, uint32_t ln)
+// Queue images (HQueue + max_size nodes, all 16-byte words) between HBM and
+// LDS: image slot i of `img` (stride qimg bytes) <-> queue qi_of(i).  One
+// flat index over every word of every image, 16 loads in flight per lane
+// before their stores (a per-image copy waits one round trip per image).
+template <bool IN, class QiOf>
+__device__ __forceinline__ void imgs_copy(uint8_t* img, uint32_t qimg, uint32_t nimg, QiOf qi_of, HQueue* q, HNode* nd,
+                                          uint32_t ms, uint32_t ln)
 {
-  uint4* d = (uint4*)dst; const uint4* s = (const uint4*)src;
-  for (uint32_t i = ln; i < bytes / 16; i += 64) d[i] = s[i];
+  constexpr uint32_t HW = sizeof(HQueue) / 16, U = 16;
+  const uint32_t per = HW + ms, total = nimg * per;
+  for (uint32_t j0 = 0; j0 < total; j0 += U * 64) {
+    uint4 v[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t j = j0 + u * 64 + ln;
+      v[u] = make_uint4(0, 0, 0, 0);
+      if (j < total) {
+        const uint32_t i = j / per, w = j % per;
+        const uint64_t qi = qi_of(i);
+        uint4* g = w < HW ? reinterpret_cast<uint4*>(q + qi) + w : reinterpret_cast<uint4*>(nd + qi * ms) + (w - HW);
+        uint4* l = reinterpret_cast<uint4*>(img + (size_t)i * qimg) + w;
+        v[u] = IN ? *g : *l;
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t j = j0 + u * 64 + ln;
+      if (j >= total) continue;
+      const uint32_t i = j / per, w = j % per;
+      const uint64_t qi = qi_of(i);
+      uint4* g = w < HW ? reinterpret_cast<uint4*>(q + qi) + w : reinterpret_cast<uint4*>(nd + qi * ms) + (w - HW);
+      uint4* l = reinterpret_cast<uint4*>(img + (size_t)i * qimg) + w;
+      if (IN) *l = v[u]; else *g = v[u];
+    }
+  }
 }
-// the LDS image of one queue (HQueue + max nodes) <-> its HBM storage
-__device__ __forceinline__ void img_in(uint8_t* img, const HQueue* q, const HNode* nd, uint32_t ms, uint32_t ln)
+__device__ __forceinline__ void img_in(uint8_t* img, HQueue* q, HNode* nd, uint32_t ms, uint32_t ln)
 {
-  copy_img(img, q, sizeof(HQueue), ln);
-  copy_img(img + sizeof(HQueue), nd, ms * sizeof(HNode), ln);
+  imgs_copy<true>(img, 0, 1, [](uint32_t) { return (uint64_t)0; }, q, nd, ms, ln);
 }
-__device__ __forceinline__ void img_out(HQueue* q, HNode* nd, const uint8_t* img, uint32_t ms, uint32_t ln)
+__device__ __forceinline__ void img_out(HQueue* q, HNode* nd, uint8_t* img, uint32_t ms, uint32_t ln)
 {
-  copy_img(q, img, sizeof(HQueue), ln);
-  copy_img(nd, img + sizeof(HQueue), ms * sizeof(HNode), ln);
+  imgs_copy<false>(img, 0, 1, [](uint32_t) { return (uint64_t)0; }, q, nd, ms, ln);
 }
 
 // one router output port + link (RouterModel::processPacket router_model.cc:71-108,
@@ -977,7 +1036,7 @@ __device__ __forceinline__ void port_hop(const NocParams& np, HTree& tr, bool wa
   uint64_t qd = 0;
   if (np.qm) {
     const uint64_t tc = time_to_cycles(t, np.f);
-    qd = wave ? tr.delay_wave(tc, nf, err, ln) : tr.delay(tc, nf, err);
+    qd = tr.delay(tc, nf, err);
     c[0] += qd; c[1] += 1;
   }
   c[2] += nf; c[3] += 1; c[4] += nf; c[5] += nf;
@@ -1003,17 +1062,85 @@ __device__ __forceinline__ uint32_t xy_stage_seg(const CP& P, const CS& S, uint3
   return S.tseg[(size_t)cur * 2 + 1] * 2 + (dy > cy ? 1u : 0u);
 }
 
-__global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t k, uint64_t barrier)
+__device__ __forceinline__ void import_one(const CP& P, const CS& S, const gg_cmsg& m, uint32_t* resumed);
+
+// The end of a quantum in the device-driven loop (the launch after the step
+// that sent nothing): every tile adds its status, the blocks deliver the held
+// boundary records into the next quantum, and the last block to arrive picks
+// the next quantum as gg_coherent_run / oracle_coh_run do (empty quanta
+// skipped; blocked tiles with nothing in flight = deadlock).
+__device__ void quantum_end(const CP& P, const CS& S, uint32_t L, uint64_t q, uint64_t Q)
 {
-  const uint32_t ln = threadIdx.x, lt = blockIdx.x, p = k & 1u;
+  const uint32_t ln = threadIdx.x, lt = blockIdx.x;
+  volatile uint64_t* qs = S.qs;
+  if (ln == 0) {
+    const uint64_t r = S.rec[lt];
+    if (r < S.rec_end[lt]) {
+      atomicAdd((unsigned long long*)&S.qs[QS_ACTIVE], 1ull);
+      if (S.blocked[lt]) atomicAdd((unsigned long long*)&S.qs[QS_BLOCKED], 1ull);
+      else atomicMin((unsigned long long*)&S.qs[QS_MIN_NEXT],
+                     (unsigned long long)(S.clk[lt] + (uint64_t)((S.meta[r] & 0x7FFFFFFFu) >> 1) * P.gap_ps));
+    }
+  }
+  const uint32_t nb = *(volatile uint32_t*)S.bnd_cnt;
+  for (uint32_t i = lt * 64 + ln; i < nb; i += gridDim.x * 64) import_one(P, S, S.bnd[i], &S.imp[(Q + 1) & 1]);
+  __syncthreads();
+  if (ln != 0) return;
+  __threadfence();
+  if (atomicAdd((unsigned long long*)&S.qs[QS_ARRIVED], 1ull) != gridDim.x - 1) return;
+  __threadfence();
+  const uint64_t active = qs[QS_ACTIVE], blocked = qs[QS_BLOCKED], mn = qs[QS_MIN_NEXT], qps = qs[QS_QPS];
+  S.ri[GG_RI_QUANTA]++;
+  S.ri[GG_RI_FINAL_QUANTUM] = q;
+  uint64_t nq = q + 1, done = 0;
+  if (active == 0 && nb == 0) done = 1;
+  else if (nb == 0 && blocked == 0) nq = max(q + 1, mn / qps);
+  else if (nb == 0) done = 2;                                          // blocked, nothing in flight: deadlock
+  for (int i = 0; i < 4; ++i) S.ring[i] = 0;
+  S.imp[Q & 1] = 0;
+  *S.bnd_cnt = 0;
+  qs[QS_ARRIVED] = 0; qs[QS_ACTIVE] = 0; qs[QS_BLOCKED] = 0; qs[QS_MIN_NEXT] = ~0ull;
+  qs[QS_Q] = nq; qs[QS_START] = L + 1; qs[QS_COUNT] = Q + 1;
+  qs[QS_DONE] = done;
+  __threadfence();
+}
+
+// devloop: the quantum, its barrier and the step index come from S.qs (the
+// quantum loop runs on the device, gg_coherent_run); otherwise the host
+// drives one quantum (gg_coherent_quantum) and L is the step index.
+__global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t L, uint32_t devloop, uint64_t barrier_arg)
+{
+  const uint32_t ln = threadIdx.x, lt = blockIdx.x;
+  PROF_T0();
+  uint32_t k = L;
+  uint64_t barrier = barrier_arg, q = 0, Q = 0;
+  // one round trip: the launch state (written by earlier launches)
+  uint64_t qsv[QS_N];
+  uint32_t rv[11];
+#pragma unroll
+  for (int i = 0; i < QS_N; ++i) qsv[i] = devloop ? S.qs[i] : 0;
+#pragma unroll
+  for (int i = 0; i < 11; ++i) rv[i] = S.ring[i];           // ring[4], quiet, imp[2], live[4]
+  if (devloop) {
+    if (qsv[QS_DONE]) { if (lt == 0 && ln == 0) S.live[L & 3] = 0; return; }
+    q = qsv[QS_Q]; Q = qsv[QS_COUNT];
+    k = L - (uint32_t)qsv[QS_START];
+    barrier = (q + 1) * qsv[QS_QPS];
+  }
+  const uint32_t p = k & 1u;
   if (k > 0) {
-    if (*(volatile uint32_t*)S.quiet) return;
-    if (((volatile uint32_t*)S.ring)[(k - 1) & 3] == 0) {   // the previous step sent nothing: the quantum is done
-      if (lt == 0 && ln == 0) *S.quiet = 1;
+    if (!devloop && rv[4]) { if (lt == 0 && ln == 0) S.live[L & 3] = 0; return; }
+    const uint32_t sent = rv[(k - 1) & 3] + (k == 1 ? rv[5 + (Q & 1)] : 0u);
+    if (sent == 0) {                                 // the previous step sent nothing: the quantum is done
+      if (lt == 0 && ln == 0) { S.live[L & 3] = 0; if (!devloop) *S.quiet = 1; }
+      if (devloop) quantum_end(P, S, L, q, Q);
       return;
     }
   }
-  if (lt == 0 && ln == 0) { S.ri[GG_RI_STEPS]++; S.ring[(k + 2) & 3] = 0; S.npool[p ^ 1u] = 0; }
+  if (lt == 0 && ln == 0) {
+    S.ri[GG_RI_STEPS]++; S.ring[(k + 2) & 3] = 0; S.npool[p ^ 1u] = 0;
+    S.live[L & 3] = k + 1;
+  }
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   StepLds& sl = *reinterpret_cast<StepLds*>(smem);
   Tile T(P, S, lt, p, sl);
@@ -1063,6 +1190,7 @@ __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t k, uint64_t 
     __syncthreads();
   }
 
+  PROF_AT(_p1);
   // ---- 1. the inbox, per-channel FIFO, channels merged by (arrival, sender)
   const uint32_t ni = ninb(S, p)[lt];
   const uint32_t n = ni + na;
@@ -1073,7 +1201,7 @@ __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t k, uint64_t 
     T.rqp = sl.rq; T.rq_lds = true;
   }
   if (P.dram_qm && P.max_list <= kQMax && n) {
-    img_in(sl.dimg, T.dq, T.dnd, P.max_list, ln);
+    img_in(sl.dimg, S.dq + lt, S.dnd + (size_t)lt * P.max_list, P.max_list, ln);
     T.dq = reinterpret_cast<HQueue*>(sl.dimg); T.dnd = reinterpret_cast<HNode*>(sl.dimg + sizeof(HQueue));
     T.dq_lds = true;
   }
@@ -1092,6 +1220,8 @@ __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t k, uint64_t 
     __syncthreads();
     ninb(S, p)[lt] = 0;
     order_inbox(n, a_, k_, m_, i_, o_, ln);
+    PROF_AT(_p1b);
+    if (S.prof && ln == 0) atomicAdd(&S.prof[9], (unsigned long long)(_p1b - _p1));
     for (uint32_t j = 0; j < n && !T.failed; ++j) {
       const gg_cmsg m = prev[o_[j]];
       T.st[GG_CT_MSGS_RECEIVED]++;
@@ -1099,6 +1229,7 @@ __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t k, uint64_t 
     }
   }
 
+  PROF_AT(_p2);
   // ---- 2. the trace (records fetched 64 at a time, one per lane)
   {
     const uint64_t line_mask = ~((1ull << P.log_line) - 1);
@@ -1120,6 +1251,7 @@ __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t k, uint64_t 
     }
   }
 
+  PROF_AT(_p3);
   // ---- 3. publish this step's records
   if (T.nch) sl.ch[2 * (T.nch - 1) + 1] = T.cused;
   __syncthreads();
@@ -1210,7 +1342,7 @@ __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t k, uint64_t 
           uint64_t qd = 0;
           if (P.np.qm) {
             const uint64_t tc = time_to_cycles(g->send_ps, P.np.f);
-            qd = wave ? tr.delay_wave(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err);
+            qd = tr.delay(tc, nf, S.err);
           }
           g->arrival_ps = g->send_ps + lat_to_ps(0, P.np.f) + lat_to_ps(qd, P.np.f);
           g->zero_load_ps = 0;
@@ -1236,6 +1368,7 @@ __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t k, uint64_t 
     }
   }
 
+  PROF_AT(_p4);
   // ---- 4. write back
   if (T.rq_lds) {
     CReq* g = S.rq + (size_t)lt * P.QC;
@@ -1261,15 +1394,24 @@ __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t k, uint64_t 
       if (np_) atomicAdd(&S.ring[k & 3], np_);
     }
   }
+  if (S.prof && ln == 0) {
+    const uint64_t e = __builtin_amdgcn_s_memtime();
+    atomicAdd(&S.prof[0], (unsigned long long)(_p1 - _p0)); atomicAdd(&S.prof[1], (unsigned long long)(_p2 - _p1));
+    atomicAdd(&S.prof[2], (unsigned long long)(_p3 - _p2)); atomicAdd(&S.prof[3], (unsigned long long)(_p4 - _p3));
+    atomicAdd(&S.prof[4], (unsigned long long)(e - _p4));
+    atomicMax(&S.prof[1024 + (L & 65535)], (unsigned long long)(e - _p0));
+  }
 }
 
 // ---------------------------------------------------------------------------
 // hop-by-hop: one wave per X (stage 0) or Y (stage 1) segment
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_c_walk(CP P, CS S, uint32_t k, int stage)
+__global__ void __launch_bounds__(64) k_c_walk(CP P, CS S, uint32_t L, int stage)
 {
-  if (*(volatile uint32_t*)S.quiet) return;
-  const uint32_t ln = threadIdx.x, sg = blockIdx.x, p = k & 1u;
+  const uint32_t live = ((volatile uint32_t*)S.live)[L & 3];
+  if (!live) return;                                 // launch L was no step
+  const uint32_t ln = threadIdx.x, sg = blockIdx.x, p = (live - 1) & 1u;
+  PROF_T0();
   uint32_t* cntp = (stage == 0 ? S.nxl : S.nyl) + sg;
   const uint32_t n0 = *cntp;
   if (n0 == 0) return;
@@ -1291,6 +1433,9 @@ __global__ void __launch_bounds__(64) k_c_walk(CP P, CS S, uint32_t k, int stage
   uint64_t* Ph = Pt + P.walk_pk; uint64_t* Pk = Ph + P.walk_pk; uint64_t* Pz = Pk + P.walk_pk;
   uint32_t* Pi = reinterpret_cast<uint32_t*>(Pz + P.walk_pk);
   uint32_t* Pp = Pi + P.walk_pk; uint32_t* Pd = Pp + P.walk_pk; uint32_t* Pf = Pd + P.walk_pk;   // pos, exit pos, flits | status << 24
+  uint32_t* Pr = Pf + P.walk_pk;                                   // rank in (send time, sender, seq) order
+  uint64_t* Qt = reinterpret_cast<uint64_t*>(Pr + P.walk_pk);      // event queue, sorted by (time, rank)
+  uint32_t* Qr = reinterpret_cast<uint32_t*>(Qt + P.walk_pk); uint32_t* Qs = Qr + P.walk_pk;
   for (uint32_t i = ln; i < n; i += 64) {
     const uint32_t r = list[i];
     const gg_cmsg& m = cur[r];
@@ -1300,6 +1445,21 @@ __global__ void __launch_bounds__(64) k_c_walk(CP P, CS S, uint32_t k, int stage
   }
   for (uint32_t i = ln; i < npos * kNetCtr; i += 64) lc[i] = 0;
   __syncthreads();
+  // canonical ranks, then the initial event queue in (time, rank) order
+  for (uint32_t i = ln; i < n; i += 64) {
+    const uint64_t hi_ = Ph[i], ki = Pk[i];
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < n; ++j) { const uint64_t hj = Ph[j]; r += hj < hi_ || (hj == hi_ && Pk[j] < ki); }
+    Pr[i] = r;
+  }
+  __syncthreads();
+  for (uint32_t i = ln; i < n; i += 64) {
+    const uint64_t ti = Pt[i];
+    const uint32_t ri = Pr[i];
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < n; ++j) { const uint64_t tj = Pt[j]; r += tj < ti || (tj == ti && Pr[j] < ri); }
+    Qt[r] = ti; Qr[r] = ri; Qs[r] = i;
+  }
   // the queues of the positions the packets can visit
   uint32_t lo = ~0u, hi = 0;
   for (uint32_t i = ln; i < n; i += 64) {
@@ -1310,49 +1470,60 @@ __global__ void __launch_bounds__(64) k_c_walk(CP P, CS S, uint32_t k, int stage
   lo = wave_min(lo);
   hi = (uint32_t)(~wave_min(~hi));
   const bool qm = P.np.qm != 0;
-  if (qm)
-    for (uint32_t q = lo; q <= hi; ++q) {
-      const uint64_t qi = (uint64_t)tile_at(q) * 6 + port;
-      img_in(qimg + (size_t)(q - sd.lo) * P.qimg, S.nq + qi, S.nnd + qi * P.np.max_size, P.np.max_size, ln);
-    }
+  auto qi_of = [&](uint32_t i) { return (uint64_t)tile_at(lo + i) * 6 + port; };
+  if (qm && lo <= hi)
+    imgs_copy<true>(qimg + (size_t)(lo - sd.lo) * P.qimg, P.qimg, hi - lo + 1, qi_of, S.nq, S.nnd, P.np.max_size, ln);
   __syncthreads();
-  // events in (time, send time, sender << 32 | seq) order
-  for (;;) {
-    uint64_t bt = ~0ull, bh = ~0ull, bk = ~0ull;
-    uint32_t bi = ~0u;
-    for (uint32_t i = ln; i < n; i += 64) {
-      if (Pf[i] >> 24) continue;
-      const uint64_t t = Pt[i], h = Ph[i], kk = Pk[i];
-      if (t < bt || (t == bt && (h < bh || (h == bh && kk < bk)))) { bt = t; bh = h; bk = kk; bi = i; }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const uint64_t t = shfl64(bt, ln ^ o), h = shfl64(bh, ln ^ o), kk = shfl64(bk, ln ^ o);
-      const uint32_t i = (uint32_t)__shfl((int)bi, ln ^ o);
-      if (t < bt || (t == bt && (h < bh || (h == bh && kk < bk)))) { bt = t; bh = h; bk = kk; bi = i; }
-    }
-    if (bi == ~0u) break;
-    const uint32_t i = bi;
+  PROF_AT(_w1);
+  uint32_t nev = 0;
+  // events in (time, send time, sender << 32 | seq) order: the head of the
+  // sorted queue [qh, n); a packet that stays in the segment goes back in at
+  // its new time (lanes count the smaller keys by ballot and shift them down)
+  const bool wave_q = P.np.max_size <= kQMax;
+  for (uint32_t qh = 0; qh < n;) {
+    const uint32_t i = Qs[qh], ri = Qr[qh];
+    ++nev;
     const uint32_t c = Pp[i], d = Pd[i], nf = Pf[i] & 0xFFFFFFu;
     uint64_t t = Pt[i], zl = Pz[i];
     HTree tr{reinterpret_cast<HQueue*>(qimg + (size_t)(c - sd.lo) * P.qimg),
              reinterpret_cast<HNode*>(qimg + (size_t)(c - sd.lo) * P.qimg + sizeof(HQueue)), 1, P.np.analytical != 0};
     uint64_t cc[kNetCtr] = {0, 0, 0, 0, 0, 0, 0};
-    port_hop(P.np, tr, P.np.max_size <= kQMax, nf, t, zl, cc, S.err, ln);
+    port_hop(P.np, tr, wave_q, nf, t, zl, cc, S.err, ln);
     const uint32_t nx = dir ? c + 1 : c - 1;
     uint32_t status = 0;
     if (nx < sd.lo || nx > sd.hi) status = 2;                  // next router in another shard: held
     else if (nx == d) status = 1;                              // leaves the chain: next stage
-    wave_sync();
     if (ln == 0) {
       Pt[i] = t; Pz[i] = zl; Pp[i] = nx; Pf[i] = nf | (status << 24);
       uint64_t* l = lc + (size_t)(c - sd.lo) * kNetCtr;
 #pragma unroll
       for (int q = 0; q < (int)kNetCtr; ++q) l[q] += cc[q];
     }
+    if (status) { ++qh; wave_sync(); continue; }
+    // re-insert (t, ri): the keys below it in (qh, n) are a prefix of the queue
+    uint32_t below = 0;
+    for (uint32_t b = qh + 1; b < n; b += 64) {
+      const uint32_t j = b + ln;
+      bool lt_ = false;
+      if (j < n) { const uint64_t tj = Qt[j]; lt_ = tj < t || (tj == t && Qr[j] < ri); }
+      const uint32_t c2 = (uint32_t)__builtin_popcountll(__ballot(lt_));
+      below += c2;
+      if (c2 < 64) break;
+    }
+    for (uint32_t b = qh + 1; b <= qh + below; b += 64) {          // (qh, qh + below] moves down by one
+      const uint32_t j = b + ln;
+      const bool mv = j <= qh + below;
+      uint64_t vt = 0; uint32_t vr = 0, vs = 0;
+      if (mv) { vt = Qt[j]; vr = Qr[j]; vs = Qs[j]; }
+      wave_sync();
+      if (mv) { Qt[j - 1] = vt; Qr[j - 1] = vr; Qs[j - 1] = vs; }
+      wave_sync();
+    }
+    if (ln == 0) { Qt[qh + below] = t; Qr[qh + below] = ri; Qs[qh + below] = i; }
     wave_sync();
   }
   __syncthreads();
+  PROF_AT(_w2);
   // hand-off
   uint32_t nb = 0;
   for (uint32_t i = ln; i < n; i += 64) {
@@ -1385,11 +1556,8 @@ __global__ void __launch_bounds__(64) k_c_walk(CP P, CS S, uint32_t k, int stage
   }
   nb = wave_sum(nb);
   if (ln == 0 && nb) atomicAdd((unsigned long long*)&S.ri[GG_RI_BOUNDARY_MSGS], (unsigned long long)nb);
-  if (qm)
-    for (uint32_t q = lo; q <= hi; ++q) {
-      const uint64_t qi = (uint64_t)tile_at(q) * 6 + port;
-      img_out(S.nq + qi, S.nnd + qi * P.np.max_size, qimg + (size_t)(q - sd.lo) * P.qimg, P.np.max_size, ln);
-    }
+  if (qm && lo <= hi)
+    imgs_copy<false>(qimg + (size_t)(lo - sd.lo) * P.qimg, P.qimg, hi - lo + 1, qi_of, S.nq, S.nnd, P.np.max_size, ln);
   for (uint32_t i = ln; i < npos * 6u; i += 64) {
     const uint32_t q = i / 6, f = i % 6;
     const uint64_t* l = lc + (size_t)q * kNetCtr;
@@ -1404,17 +1572,22 @@ __global__ void __launch_bounds__(64) k_c_walk(CP P, CS S, uint32_t k, int stage
     }
   }
   if (ln == 0) *cntp = 0;
+  if (S.prof && ln == 0) {
+    const uint64_t e = __builtin_amdgcn_s_memtime();
+    atomicAdd(&S.prof[16], (unsigned long long)(_w1 - _p0)); atomicAdd(&S.prof[17], (unsigned long long)(_w2 - _w1));
+    atomicAdd(&S.prof[18], (unsigned long long)(e - _w2)); atomicAdd(&S.prof[19], (unsigned long long)nev);
+    atomicAdd(&S.prof[22], 1ull);
+    atomicMax(&S.prof[1024 + 65536 + 2 * (L & 65535) + stage], (unsigned long long)(e - _p0));
+    atomicMax(&S.prof[24 + stage], (unsigned long long)nev);
+  }
 }
 
-// Deliver the records of the quantum boundary: messages into the inbox of the
-// quantum's first step (records in pool 1), held packets back into the walk
-// of that step (records in pool 0): the X / Y segment at their router, or
-// the destination's SELF list of step 1.
-__global__ void k_c_import(CP P, CS S, const gg_cmsg* in, uint32_t n)
+// Deliver a record of the quantum boundary: a message into the inbox of the
+// quantum's first step (records in pool 1), a held packet back into the walk
+// of that step (records in pool 0): the X / Y segment at its router, or the
+// destination's SELF list of step 1.  `resumed` counts the held packets.
+__device__ __forceinline__ void import_one(const CP& P, const CS& S, const gg_cmsg& m, uint32_t* resumed)
 {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const gg_cmsg m = in[i];
   const uint32_t at = m.hop == GG_HOP_NONE ? m.dst : m.hop;
   if (at >= P.T || m.dst >= P.T || S.ltile[at] < 0) { atomicOr(S.err, GG_DERR_STATE); return; }
   if (m.hop == GG_HOP_NONE) {
@@ -1430,7 +1603,7 @@ __global__ void k_c_import(CP P, CS S, const gg_cmsg* in, uint32_t n)
   const uint32_t r = atomicAdd(&S.npool[0], 1u);
   if (r >= P.msg_cap) { atomicOr(S.err, GG_DERR_CAP); return; }
   S.pool0[r] = m;
-  atomicAdd(&S.ring[0], 1u);
+  atomicAdd(resumed, 1u);
   if (m.hop == m.dst) {
     const int32_t ld = S.ltile[m.dst];
     const uint32_t j = atomicAdd(&S.narv1[ld], 1u);
@@ -1444,6 +1617,13 @@ __global__ void k_c_import(CP P, CS S, const gg_cmsg* in, uint32_t n)
   const uint32_t j = atomicAdd(&cnt[sg], 1u);
   if (j >= P.seg_cap) { atomicOr(S.err, GG_DERR_CAP); return; }
   (is_x ? S.xl : S.yl)[(size_t)sg * P.seg_cap + j] = r;
+}
+
+__global__ void k_c_import(CP P, CS S, const gg_cmsg* in, uint32_t n)
+{
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  import_one(P, S, in[i], &S.imp[0]);
 }
 
 // Status after a quantum: active / blocked tiles, least next-access start.
@@ -1706,11 +1886,15 @@ static gg_status coh_alloc(gg_ctx* ctx)
   A(xl, (uint64_t)std::max(P.nsx, 1u) * P.seg_cap); A(nxl, std::max(P.nsx, 1u));
   A(yl, (uint64_t)std::max(P.nsy, 1u) * P.seg_cap); A(nyl, std::max(P.nsy, 1u));
   A(bnd, P.msg_cap); A(bnd_cnt, 1);
-  A(ring, 5); A(ri, GG_NUM_RUN_INFO);
+  A(ring, 11); A(ri, GG_NUM_RUN_INFO); A(qs, QS_N);
   A(gscr, L * 5 * P.IC);
 #undef A
+  if (getenv("GG_COH_PROFILE") && atoi(getenv("GG_COH_PROFILE"))) {
+    if ((st = dalloc(C, &S.prof, 1024 + 3 * 65536))) return st;
+    GG_HIP(hipMemset(S.prof, 0, sizeof(unsigned long long) * (1024 + 3 * 65536)));
+  }
   if (st) return st;
-  S.quiet = S.ring + 4;
+  S.quiet = S.ring + 4; S.imp = S.ring + 5; S.live = S.ring + 7;
   if ((st = dupload(C, &S.gtile, gtile))) return st;
   if ((st = dupload(C, &S.ltile, ltile))) return st;
   if ((st = dupload(C, &S.shard, shard))) return st;
@@ -1757,7 +1941,11 @@ gg_status gg_coherent_begin(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_ou
   GG_HIP(hipMemsetAsync(ctx->err_dev, 0, sizeof(uint32_t), s));
   GG_HIP(hipMemsetAsync(C->S.ri, 0, sizeof(uint64_t) * GG_NUM_RUN_INFO, s));
   GG_HIP(hipMemsetAsync(C->S.npool, 0, sizeof(uint32_t) * 2, s));
-  GG_HIP(hipMemsetAsync(C->S.ring, 0, sizeof(uint32_t) * 5, s));
+  GG_HIP(hipMemsetAsync(C->S.ring, 0, sizeof(uint32_t) * 11, s));
+  {
+    uint64_t q0[QS_N] = {0, 0, 0, 0, 0, 0, ~0ull, 0, (uint64_t)ctx->cfg.quantum_ns * 1000ull};
+    GG_HIP(hipMemcpyAsync(C->S.qs, q0, sizeof(q0), hipMemcpyHostToDevice, s));
+  }
   GG_HIP(hipMemsetAsync(C->S.bnd_cnt, 0, sizeof(uint32_t), s));
   GG_HIP(hipMemsetAsync(C->S.nxl, 0, sizeof(uint32_t) * std::max(P.nsx, 1u), s));
   GG_HIP(hipMemsetAsync(C->S.nyl, 0, sizeof(uint32_t) * std::max(P.nsy, 1u), s));
@@ -1782,7 +1970,7 @@ gg_status gg_coherent_quantum(gg_ctx* ctx, uint64_t q, gg_coherent_status* out)
   uint32_t k = 0, batch = 8;
   for (;;) {
     for (uint32_t b = 0; b < batch; ++b, ++k) {
-      hipLaunchKernelGGL(k_c_step, dim3(P.L), dim3(64), C->step_lds, s, P, C->S, k, barrier);
+      hipLaunchKernelGGL(k_c_step, dim3(P.L), dim3(64), C->step_lds, s, P, C->S, k, 0u, barrier);
       if (hbh) {
         if (P.nsx) hipLaunchKernelGGL(k_c_walk, dim3(P.nsx), dim3(64), C->walk_lds, s, P, C->S, k, 0);
         if (P.nsy) hipLaunchKernelGGL(k_c_walk, dim3(P.nsy), dim3(64), C->walk_lds, s, P, C->S, k, 1);
@@ -1797,8 +1985,8 @@ gg_status gg_coherent_quantum(gg_ctx* ctx, uint64_t q, gg_coherent_status* out)
     if (quiet) break;
     if (batch < 64) batch *= 2;
   }
-  // the next quantum starts from empty step counters
-  GG_HIP(hipMemsetAsync(C->S.ring, 0, sizeof(uint32_t) * 5, s));
+  // the next quantum starts from empty step counters (ring, quiet, imported packets)
+  GG_HIP(hipMemsetAsync(C->S.ring, 0, sizeof(uint32_t) * 7, s));
   uint64_t init[4] = {0, 0, ~0ull, 0};
   GG_HIP(hipMemcpyAsync(C->status_dev, init, sizeof(init), hipMemcpyHostToDevice, s));
   hipLaunchKernelGGL(k_c_status, dim3((P.L + 63) / 64), dim3(64), 0, s, P, C->S, C->status_dev);
@@ -1883,40 +2071,49 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
   if (gg_status st = gg_coherent_begin(ctx, tr, access_out_dev, stream)) return st;
   gg_coh_state* C = ctx->coh;
   hipStream_t s = ctx->last_stream;
-  const uint64_t quantum_ps = (uint64_t)c.quantum_ns * 1000ull;
   gg_timer_begin(ctx, "coherent_run", s);
-  uint64_t q = 0;
-  gg_cmsg* xfer = nullptr;
-  GG_HIP(hipMalloc((void**)&xfer, sizeof(gg_cmsg) * C->P.msg_cap));
-  gg_status rc = GG_OK;
+  // the quantum loop on the device (k_c_step's quantum_end): the host only
+  // streams launches and looks at the run-over flag once per batch
+  const CP& P = C->P;
+  const bool hbh = P.net == GG_NET_EMESH_HOP_BY_HOP;
+  uint32_t L = 0, batch = 16;
   for (;;) {
-    gg_coherent_status st;
-    if ((rc = gg_coherent_quantum(ctx, q, &st))) break;
-    const uint64_t nb = st.boundary_msgs;
-    if (nb) {                                          // the boundary: held records -> the next quantum
-      if (hipMemcpyAsync(xfer, C->S.bnd, sizeof(gg_cmsg) * nb, hipMemcpyDeviceToDevice, s) != hipSuccess ||
-          hipMemsetAsync(C->S.bnd_cnt, 0, sizeof(uint32_t), s) != hipSuccess) {
-        rc = gg_fail(GG_ERR_HIP, "boundary copy");
-        break;
+    for (uint32_t b = 0; b < batch; ++b, ++L) {
+      hipLaunchKernelGGL(k_c_step, dim3(P.L), dim3(64), C->step_lds, s, P, C->S, L, 1u, (uint64_t)0);
+      if (hbh) {
+        if (P.nsx) hipLaunchKernelGGL(k_c_walk, dim3(P.nsx), dim3(64), C->walk_lds, s, P, C->S, L, 0);
+        if (P.nsy) hipLaunchKernelGGL(k_c_walk, dim3(P.nsy), dim3(64), C->walk_lds, s, P, C->S, L, 1);
       }
-      if ((rc = gg_coherent_import(ctx, xfer, nb))) break;
     }
-    if (st.active_tiles == 0 && nb == 0) break;
-    if (nb == 0 && st.blocked_tiles == 0) {
-      const uint64_t nq = st.min_next_ps / quantum_ps;
-      q = nq > q + 1 ? nq : q + 1;
-    } else if (nb == 0) {
-      rc = gg_fail(GG_ERR_STATE, "coherent run deadlocked: tiles blocked with no message in flight");
-      break;
-    } else {
-      q = q + 1;
-    }
+    GG_HIP(hipGetLastError());
+    uint64_t done = 0;
+    uint32_t err = 0;
+    GG_HIP(hipMemcpyAsync(&done, C->S.qs + QS_DONE, sizeof(done), hipMemcpyDeviceToHost, s));
+    GG_HIP(hipMemcpyAsync(&err, ctx->err_dev, sizeof(err), hipMemcpyDeviceToHost, s));
+    GG_HIP(hipStreamSynchronize(s));
+    if (err) break;
+    if (done) break;
+    if (batch < 256) batch *= 2;
   }
-  hipFree(xfer);
-  if (rc) return rc;
   gg_timer_end(ctx, "coherent_run", s);
   GG_HIP(hipStreamSynchronize(s));
-  return coh_check(ctx);
+  if (C->S.prof) {
+    // per-launch maxima in slots L mod 65536
+    std::vector<unsigned long long> h(1024 + 3 * 65536);
+    GG_HIP(hipMemcpy(h.data(), C->S.prof, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
+    unsigned long long crit = 0, wx = 0, wy = 0;
+    for (int i = 0; i < 65536; ++i) { crit += h[1024 + i]; wx += h[1024 + 65536 + 2 * i]; wy += h[1024 + 65536 + 2 * i + 1]; }
+    fprintf(stderr, "[gg_coh] step cycles over tiles: self %llu inbox+handlers %llu (order %llu) trace %llu publish %llu "
+            "writeback %llu | slowest tile per launch %llu\n"
+            "[gg_coh] walkers: %llu launches, staging %llu events %llu loop %llu handoff %llu, max events X %llu Y %llu | "
+            "slowest walker per launch X %llu Y %llu (s_memtime cycles)\n",
+            h[0], h[1], h[9], h[2], h[3], h[4], crit, h[22], h[16], h[19], h[17], h[18], h[24], h[25], wx, wy);
+  }
+  if (gg_status e = coh_check(ctx)) return e;
+  uint64_t done = 0;
+  GG_HIP(hipMemcpy(&done, C->S.qs + QS_DONE, sizeof(done), hipMemcpyDeviceToHost));
+  if (done == 2) return gg_fail(GG_ERR_STATE, "coherent run deadlocked: tiles blocked with no message in flight");
+  return GG_OK;
 }
 
 gg_status gg_coherent_get_stats(gg_ctx* ctx, uint64_t* tile_stats, uint64_t* cache, uint64_t* run_info)

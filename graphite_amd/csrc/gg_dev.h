@@ -10,7 +10,11 @@ namespace gg {
 // Queue models (QueueModel::create, queue_model.cc:19-39).  One storage
 // layout for all three: HQueue + max_size 16-byte HNode slots.
 //   history_tree (queue_model_history_tree.cc:44-167 over interval_tree.cc):
-//     the free intervals as nd[0..size), sorted by start.  The reference keeps
+//     the free intervals sorted by start in a circular list of max_size
+//     slots (interval i at slot (head + i) mod max_size), so the pruning of
+//     the oldest interval is head + 1 and the usual update — at the newest
+//     interval, the packets of a port arriving in time order — touches one
+//     slot.  The reference keeps
 //     them in an AVL tree and finds the interval with searchTree
 //     (interval_tree.cc:366-394); the free intervals are disjoint and, since
 //     every processing time and min_processing_time is >= 1 (router queues 1,
@@ -38,7 +42,7 @@ struct HQueue {
   uint32_t front, back;                             // basic: ModuloNum window ends (modulo window + 1)
   double mean;                                      // basic: MovingArithmeticMean::_arithmetic_mean
   uint64_t qtime;                                   // basic: QueueModelBasic::_queue_time
-  uint64_t pad;
+  uint32_t head, pad;                               // history_tree: slot of interval 0 (circular list)
 };
 static_assert(sizeof(HQueue) % 16 == 0 && sizeof(HNode) == 16, "16-byte queue images");
 
@@ -95,10 +99,12 @@ struct HTree {
 
   __device__ __forceinline__ uint64_t mg1_delay() const                         // QueueModelMG1::computeQueueDelay
   {
-    if (q->n == 0) return 0;
-    double variance = (q->sig_sq / q->n) - ((q->sig / q->n) * (q->sig / q->n));
-    double service_rate = 1.0 / (q->sig / q->n);
-    double arrival_rate = ((double)q->n) / q->newest;
+    const uint64_t n = q->n, newest = q->newest;
+    const double sig_sq = q->sig_sq, sig = q->sig;
+    if (n == 0) return 0;
+    double variance = (sig_sq / n) - ((sig / n) * (sig / n));
+    double service_rate = 1.0 / (sig / n);
+    double arrival_rate = ((double)n) / newest;
     if (arrival_rate >= service_rate) arrival_rate = 0.999 * service_rate;
     return (uint64_t)ceil(0.5 * service_rate * arrival_rate * ((1 / (service_rate * service_rate)) + variance) /
                           (service_rate - arrival_rate));
@@ -115,40 +121,72 @@ struct HTree {
     nd[i].first = a; nd[i].second = b;
     q->size++;
   }
-  // ---- history_tree ----
-  // first fit (searchTree, see above): the last interval starting at or before
-  // t if it holds [t, t+p], else the first later one of length >= p
-  __device__ __forceinline__ int first_fit(uint64_t t, uint64_t p) const
-  {
-    const int n = (int)q->size;
-    int lo = 0, hi = n;
-    if (n && nd[n - 1].first <= t) lo = n;
-    while (lo < hi) { const int mid = (lo + hi) >> 1; if (nd[mid].first <= t) lo = mid + 1; else hi = mid; }
-    const int j = lo - 1;
-    if (j >= 0 && t + p <= nd[j].second) return j;
-    for (int i = j + 1; i < n; ++i) if (nd[i].second - nd[i].first >= p) return i;
-    return -1;
-  }
+  // ---- history_tree: circular sorted list.  The header words live in
+  // registers for the request (the queue may sit in LDS or HBM; stores to
+  // the interval slots would otherwise force them to be reloaded) ----
+  struct TL {
+    HNode* nd; uint32_t head, cap, n;
+    __device__ __forceinline__ uint32_t ph(uint32_t i) const { const uint32_t j = head + i; return j >= cap ? j - cap : j; }
+    __device__ __forceinline__ HNode& iv(uint32_t i) const { return nd[ph(i)]; }
+    __device__ __forceinline__ void erase(uint32_t i)
+    {
+      if (i == 0) { head = ph(1); --n; return; }
+      for (uint32_t j = i + 1; j < n; ++j) iv(j - 1) = iv(j);
+      --n;
+    }
+    __device__ __forceinline__ void insert(uint32_t i, uint64_t a, uint64_t b)     // before position i (n < cap)
+    {
+      for (uint32_t j = n; j > i; --j) iv(j) = iv(j - 1);
+      HNode& x = iv(i);
+      x.first = a; x.second = b;
+      ++n;
+    }
+    // first fit (searchTree, see above): the last interval starting at or
+    // before t if it holds [t, t+p], else the first later one of length >= p
+    __device__ __forceinline__ int first_fit(uint64_t t, uint64_t p) const
+    {
+      int lo = 0, hi = (int)n;
+      if (n) { const HNode& l = iv(n - 1); if (l.first <= t) { if (t + p <= l.second) return (int)n - 1; lo = (int)n; } }
+      while (lo < hi) { const int mid = (lo + hi) >> 1; if (iv(mid).first <= t) lo = mid + 1; else hi = mid; }
+      const int j = lo - 1;
+      if (j >= 0 && t + p <= iv(j).second) return j;
+      for (int i = j + 1; i < (int)n; ++i) { const HNode& x = iv(i); if (x.second - x.first >= p) return i; }
+      return -1;
+    }
+  };
   __device__ __forceinline__ uint64_t tree_delay(uint64_t t, uint64_t p, uint32_t* err)   // computeQueueDelay (:44-126)
   {
-    if (q->size >= q->max_size) l_erase(0);                    // prune the min node (:52-56)
-    if (analytical && nd[0].first > (t + p)) { q->analytical++; return mg1_delay(); }
-    const int i = first_fit(t, p);
-    if (i < 0) { atomicOr(err, GG_DERR_STATE); return 0; }
-    const uint64_t a = nd[i].first, b = nd[i].second;
-    if (t >= a) {
-      if ((t - a) >= min_proc) {
-        if ((b - (t + p)) >= min_proc) l_insert((uint32_t)i + 1, t + p, b);
-        nd[i].second = t;
-      } else {
-        if ((b - (t + p)) >= min_proc) nd[i].first = t + p;
-        else l_erase((uint32_t)i);
+    TL L{nd, q->head, q->max_size, q->size};
+    uint64_t qd = 0;
+    if (L.n >= L.cap) L.erase(0);                              // prune the min node (:52-56)
+    const HNode x0 = L.iv(0);
+    if (analytical && x0.first > (t + p)) {
+      q->analytical++;
+      qd = mg1_delay();
+    } else {
+      const int i = L.first_fit(t, p);
+      if (i < 0) { atomicOr(err, GG_DERR_STATE); }
+      else {
+        HNode& x = L.iv((uint32_t)i);
+        const uint64_t a = x.first, b = x.second;
+        if (t >= a) {
+          if ((t - a) >= min_proc) {
+            if ((b - (t + p)) >= min_proc) L.insert((uint32_t)i + 1, t + p, b);
+            L.iv((uint32_t)i).second = t;
+          } else if ((b - (t + p)) >= min_proc) {
+            x.first = t + p;
+          } else {
+            L.erase((uint32_t)i);
+          }
+        } else {
+          qd = a - t;
+          if ((b - (a + p)) >= min_proc) x.first = a + p;
+          else L.erase((uint32_t)i);
+        }
       }
-      return 0;
     }
-    if ((b - (a + p)) >= min_proc) nd[i].first = a + p;
-    else l_erase((uint32_t)i);
-    return a - t;
+    q->head = L.head; q->size = L.n;
+    return qd;
   }
   // replace interval i by up to two intervals (in list order).  The list may
   // overgrow by one only here, and then loses its front (the size check after
@@ -244,99 +282,36 @@ struct HTree {
   }
   __device__ __forceinline__ void mg1_update(uint64_t t, uint64_t p, uint64_t qd)
   {
-    q->sig_sq += (double)p * (double)p;                          // QueueModelMG1::updateQueue
-    q->sig += (double)p;
-    q->n++;
-    { uint64_t x = t + qd + p; if (x > q->newest) q->newest = x; }
-    q->util += p;                                                // updateQueueUtilizationCounters
-    { uint64_t x = t + qd + p; if (x > q->last_req) q->last_req = x; }
-    q->total_req++;
+    const double ss = q->sig_sq, sg = q->sig;
+    const uint64_t nn = q->n, nw = q->newest, ut = q->util, lr = q->last_req, tr = q->total_req;
+    const uint64_t x = t + qd + p;
+    q->sig_sq = ss + (double)p * (double)p;                      // QueueModelMG1::updateQueue
+    q->sig = sg + (double)p;
+    q->n = nn + 1;
+    q->newest = x > nw ? x : nw;
+    q->util = ut + p;                                            // updateQueueUtilizationCounters
+    q->last_req = x > lr ? x : lr;
+    q->total_req = tr + 1;
   }
 
-  // ---- the same request by a whole wave on a queue in LDS (all 64 lanes, uniform
-  // t / p; the history tree's search and shifts lane-parallel, the other models
-  // run redundantly on every lane).  Returns the delay on every lane. ----
-  __device__ __forceinline__ void w_erase(uint32_t i, uint32_t n, uint32_t lane)
-  {
-    HNode v[2]; bool m[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) { const uint32_t j = lane + 64u * h; m[h] = j > i && j < n; if (m[h]) v[h] = nd[j]; }
-    wave_sync();
-#pragma unroll
-    for (int h = 0; h < 2; ++h) if (m[h]) nd[lane + 64u * h - 1] = v[h];
-    wave_sync();
-  }
-  __device__ __forceinline__ void w_insert(uint32_t i, uint32_t n, uint64_t a, uint64_t b, uint32_t lane)   // before i
-  {
-    HNode v[2]; bool m[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) { const uint32_t j = lane + 64u * h; m[h] = j >= i && j < n; if (m[h]) v[h] = nd[j]; }
-    wave_sync();
-#pragma unroll
-    for (int h = 0; h < 2; ++h) if (m[h]) nd[lane + 64u * h + 1] = v[h];
-    if (lane == 0) { nd[i].first = a; nd[i].second = b; }
-    wave_sync();
-  }
-  __device__ __forceinline__ uint64_t delay_wave(uint64_t t, uint64_t p, uint32_t* err, uint32_t lane)
-  {
-    if (q->type != GG_QM_HISTORY_TREE || q->max_size > 128) {
-      uint64_t r = 0;
-      // the scalar model on lane 0 only (its writes are not idempotent across lanes)
-      if (lane == 0) r = delay(t, p, err);
-      wave_sync();
-      return __shfl(r, 0);
-    }
-    uint32_t n = q->size;
-    if (n >= q->max_size) {                                      // prune the min node (:52-56)
-      w_erase(0, n, lane); --n;
-      if (lane == 0) q->size = n;
-      wave_sync();
-    }
-    uint64_t qd = 0;
-    bool upd = true;
-    if (analytical && nd[0].first > (t + p)) {
-      qd = mg1_delay();
-      if (lane == 0) q->analytical++;
-    } else {
-      bool c[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const uint32_t j = lane + 64u * h;
-        c[h] = false;
-        if (j < n) {
-          const uint64_t a = nd[j].first, b = nd[j].second;
-          c[h] = (a <= t && t + p <= b) || (a > t && b - a >= p);
-        }
-      }
-      const uint64_t m0 = ballot64(c[0]), m1 = ballot64(c[1]);
-      if (!m0 && !m1) { if (lane == 0) atomicOr(err, GG_DERR_STATE); upd = false; }
-      else {
-        const uint32_t i = m0 ? (uint32_t)__builtin_ctzll(m0) : 64u + (uint32_t)__builtin_ctzll(m1);
-        const uint64_t a = nd[i].first, b = nd[i].second;
-        wave_sync();
-        if (t >= a) {
-          if ((t - a) >= min_proc) {
-            if ((b - (t + p)) >= min_proc) { w_insert(i + 1, n, t + p, b, lane); ++n; }
-            if (lane == 0) nd[i].second = t;
-          } else if ((b - (t + p)) >= min_proc) {
-            if (lane == 0) nd[i].first = t + p;
-          } else { w_erase(i, n, lane); --n; }
-        } else {
-          qd = a - t;
-          if ((b - (a + p)) >= min_proc) { if (lane == 0) nd[i].first = a + p; }
-          else { w_erase(i, n, lane); --n; }
-        }
-        if (lane == 0) q->size = n;
-      }
-    }
-    if (upd && lane == 0) mg1_update(t, p, qd);
-    wave_sync();
-    return qd;
-  }
 };
 
-__device__ __forceinline__ uint64_t lat_to_ps(uint64_t cycles, double f) { return (uint64_t)ceil(((double)1000 * cycles) / f); }
-__device__ __forceinline__ uint64_t time_to_cycles(uint64_t ps, double f) { return (uint64_t)ceil(((double)ps * f) / 1.0e3); }
+// Latency::toPicosec / Time::toCycles (time_types.h:81-109), double and ceil.
+// At 1 GHz (every clock domain of carbon_sim.cfg) both are exact integer
+// maps below 2^52 ps: 1000 * cycles / 1.0 is exact, and the correctly
+// rounded ps / 1000.0 of a non-multiple of 1000 stays more than 2^-11 away
+// from an integer, so its ceil is (ps + 999) / 1000.  Integer arithmetic
+// there, the double formula elsewhere.
+__device__ __forceinline__ uint64_t lat_to_ps(uint64_t cycles, double f)
+{
+  if (f == 1.0 && cycles < (1ull << 42)) return 1000 * cycles;
+  return (uint64_t)ceil(((double)1000 * cycles) / f);
+}
+__device__ __forceinline__ uint64_t time_to_cycles(uint64_t ps, double f)
+{
+  if (f == 1.0 && ps < (1ull << 52)) return (ps + 999) / 1000;
+  return (uint64_t)ceil(((double)ps * f) / 1.0e3);
+}
 
 struct NocParams {
   uint32_t tiles, w, h, flit_width, router_delay, link_delay, qm, analytical, max_size, net_model;

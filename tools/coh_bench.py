@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Coherent-mode (Mode C) timing experiment: GPU gg_coherent_run vs the C
-oracle on the same hotspot trace.  usage: coh_bench.py T N [K] [hot] [--no-oracle]"""
+oracle on the same hotspot trace.  usage: coh_bench.py T N [K] [hot] [--no-oracle] [--hbh]"""
 import os
 import sys
 import time
@@ -18,7 +18,8 @@ def main():
     T, N = int(args[0]), int(args[1])
     K = int(args[2]) if len(args) > 2 else 1
     hot = int(args[3]) if len(args) > 3 else 64
-    cfg = C.default_config(T, num_shards=K)
+    net = C.NET_EMESH_HOP_BY_HOP if "--hbh" in sys.argv else C.NET_EMESH_HOP_COUNTER
+    cfg = C.default_config(T, num_shards=K, net_model=net)
     be = B.Backend(cfg)
     be.set_timing(True)
     addr = torch.empty(T * N, dtype=torch.int64, device="cuda")
@@ -32,8 +33,8 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     st, cc, ri = be.coherent_stats()
-    print("gpu  T=%d N=%d K=%d: %.3f s  %.3g acc/s  quanta %d steps %d msgs %d  clk max %d ns" %
-          (T, N, K, dt, T * N / dt, ri[0], ri[1], ri[2] + ri[3], st[:, 0].max() // 1000), flush=True)
+    print("gpu  %s T=%d N=%d K=%d: %.3f s  %.3g acc/s  quanta %d steps %d msgs %d  clk max %d ns" %
+          ("hbh" if net == C.NET_EMESH_HOP_BY_HOP else "hc", T, N, K, dt, T * N / dt, ri[0], ri[1], ri[2] + ri[3], st[:, 0].max() // 1000), flush=True)
     if "--no-oracle" not in sys.argv:
         from oracle import pyoracle as po
         a, m, o = po.gen_trace(T, N, hot_lines=hot)
