@@ -1,31 +1,39 @@
 #!/usr/bin/env python3
 """bench.py — simulated memory accesses per second of the MI355X backend.
 
-Metric (BASELINE.json): "simulated mem accesses/sec (node) ... bit-exact stats".
-Workload (round 1): the metric's scale — 1024 tiles per GPU (BASELINE.json
-configs[3] tile count), 2^20 line accesses per tile (configs[3] length) — with
-the configs[1] uniform-random private generator, 32 KB/4-way L1-D + 512 KB/8-way
-L2 (carbon_sim.cfg defaults), private-cache (decoupled) mode.  The coherent
-MSI + hop-by-hop mode of configs[3] is not built yet.
-`--tiles 64 --per-tile 4194304` runs configs[1] exactly.  One step = one full
-replay of the batch from the constructor cache state: the single-pass
-streaming replay kernel k_cache_stream (graphite_amd/csrc/gg_cache.hip; one
-workgroup per tile), inputs resident in HBM.
+Metric (BASELINE.json): "simulated mem accesses/sec (node) at 1024 tiles,
+1/2/4/8 GPU; bit-exact stats".
 
-Multi-GPU: one process per GPU (torchrun); rank r simulates its own tiles
-(global tiles r*T .. r*T+T-1) — units are independent in private mode, so
-there is no collective on the data path ("weak" scaling); only the timing is
-max-reduced over ranks (graphite_amd/dist.py).
+Headline = the metric's configuration, BASELINE.json configs[3]: 1024 tiles
+(32 x 32 mesh), the hotspot trace (80 % private lines, 20 % to 256 lines
+shared by every tile, WRITE p = 1/3, ~2-cycle gaps), the full
+pr_l1_pr_l2_dram_directory_msi protocol (L1-D / L2, full-map DRAM directory,
+DRAM history-tree queue) on emesh_hop_by_hop with history-tree router
+contention, lax-barrier quantum 1000 ns, 8 logical shards = the reference's
+8-process 2-D blocks (network_model_emesh_hop_by_hop.cc:367-433).  The trace
+is shortened to --per-tile accesses per tile (named in config.workload): the
+configs[3] length (2^20) would take hours at this rate.  One step = one whole
+coherent run of the workload from the reset state (every tile's trace to its
+end), inputs resident in HBM.  With N GPUs each rank owns 8/N of the shards
+and the held cross-shard records are exchanged at every quantum boundary;
+the work is the same at every N ("strong" scaling) and the results are
+bit-identical.
 
-Also reported: the dominant kernel's roofline (algorithmic 16 B/access: 8 B
-address + 4 B metadata in, 4 B result out) from HIP
-events on its own stream, and the CPU baseline (the C oracle, a bounded sample,
-threads = cores used).  Bit-exactness is checked in the same run: one tile's
-counters and per-access results against the oracle.
+Reported with it: the kernels' device time from HIP events around every
+launch (gg_kernel_stats) and the step kernel's roofline at 20 algorithmic
+bytes per access (8 B address + 4 B meta in, 8 B access word out); the C
+oracle on the same workload as the CPU baseline, on 1 thread and on one
+OpenMP thread per logical shard (oracle_coh_run_parallel); and a bit-exact
+check of every output against the oracle in the same run.  Sections under
+their own keys: the same workload on emesh_hop_counter, configs[0] (captured
+FFT), the configs[1] private-cache replay (round 1's headline), NoC batches
+and the configs[4] stress geometry.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import threading
 import time
@@ -36,8 +44,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-ALGO_BYTES_PER_ACCESS = 16     # whole path: 8 B addr + 4 B meta in, 4 B result out
-# Algorithmic bytes per access of each kernel of the path
+ALGO_BYTES_PER_ACCESS = 16     # Mode P: 8 B addr + 4 B meta in, 4 B result out
+COH_BYTES_PER_ACCESS = 20      # Mode C: 8 B addr + 4 B meta in, 8 B access word out
+# Algorithmic bytes per access of each Mode P kernel
 KERNEL_BYTES = {
     "cache_stream": 16,    # single pass (default): read addr (8) + meta (4), write result (4); state < 1%
     "cache_hist": 8,       # read addr (+ per-chunk set counts, scans: < 1%)
@@ -46,124 +55,193 @@ KERNEL_BYTES = {
     "cache_unshard": 12,   # read slot (4) + result (4), write program-order result (4)
 }
 KERNEL_SYMBOL = {"cache_stream": "k_cache_stream", "cache_hist": "k_shard_hist", "cache_scatter": "k_shard_scatter",
-                 "cache_replay": "k_cache_replay_lean", "cache_unshard": "k_unshard"}
+                 "cache_replay": "k_cache_replay_lean", "cache_unshard": "k_unshard",
+                 "coherent_step": "k_c_step", "coherent_walk_x": "k_c_walk (X)", "coherent_walk_y": "k_c_walk (Y)"}
+NET = {"hop_counter": 1, "hop_by_hop": 2, "magic": 0}
 
 
-def pmc_traffic(kernel, tiles, per_tile):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    of this workload (profiles/<round>/summary.json: FETCH_SIZE x2 (16-B loads,
-    MI355X_MICROARCH.md) + WRITE_SIZE, separate passes; tools/gpu_pmc.sh)."""
+def pmc_traffic(kernel, key):
+    """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC summary
+    (profiles/<round>/summary*.json, FETCH_SIZE / WRITE_SIZE in separate
+    passes, calibrated per MI355X_MICROARCH.md; tools/pmc_summary.py) of the
+    workload `key`, or None."""
     import glob
     best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "summary.json"))):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "summary*.json"))):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if d.get("workload", {}).get("tiles") not in (None, tiles) or \
-           d.get("workload", {}).get("per_tile") not in (None, per_tile):
+        if d.get("workload_key") != key:
             continue
-        for k, v in d.get("kernels", {}).items():
-            if k.split("<")[0] == kernel and "hbm_bytes" in v:
-                best = {"bytes": v["hbm_bytes"], "source": os.path.relpath(f, ROOT)}
+        v = d.get("kernels", {}).get(kernel)
+        if v and "hbm_bytes" in v:
+            best = {"bytes": v["hbm_bytes"], "source": os.path.relpath(f, ROOT)}
     return best
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=5)
-    p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--tiles", type=int, default=1024, help="tiles per GPU")
-    p.add_argument("--per-tile", type=int, default=1 << 20, help="line accesses per tile")
-    p.add_argument("--cpu-sample-tiles", type=int, default=480, help="tile replays in the CPU baseline sample")
-    p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu count)")
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--tiles", type=int, default=1024, help="headline tiles (configs[3]: 1024)")
+    p.add_argument("--per-tile", type=int, default=256, help="headline accesses per tile")
+    p.add_argument("--hot-lines", type=int, default=256, help="shared hot lines (configs[3]: 256)")
+    p.add_argument("--shards", type=int, default=8, help="logical shards (the 8-process blocks)")
+    p.add_argument("--net", default="hop_by_hop", choices=sorted(NET), help="headline memory network model")
+    p.add_argument("--cpu-threads", type=int, default=0, help="all-core oracle threads (0 = one per shard, <= cores)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
-    p.add_argument("--replay-kernel", type=int, default=0,
-                   help="0 = single-pass streaming replay, 1 = sharded generic, 2 = sharded lean")
-    p.add_argument("--stress-tiles", type=int, default=4096,
-                   help="configs[4] private-part section: tiles (0 = skip)")
+    p.add_argument("--sections", default="hop_counter,fft,private,noc,stress",
+                   help="extra sections at N = 1 (comma list; '' = none)")
+    p.add_argument("--hc-per-tile", type=int, default=1024, help="hop_counter section: accesses per tile")
+    p.add_argument("--private-per-tile", type=int, default=1 << 20)
+    p.add_argument("--cpu-sample-tiles", type=int, default=480, help="private section: tile replays of its CPU sample")
+    p.add_argument("--replay-kernel", type=int, default=0)
+    p.add_argument("--stress-tiles", type=int, default=4096)
     p.add_argument("--stress-per-tile", type=int, default=1 << 18)
-    p.add_argument("--coherent-tiles", type=int, default=1024,
-                   help="coherent-mode (Mode C) section: total tiles (0 = skip); configs[2] = 256, configs[3] = 1024")
-    p.add_argument("--coherent-per-tile", type=int, default=2048, help="coherent-mode accesses per tile")
-    p.add_argument("--coherent-hot-lines", type=int, default=0,
-                   help="shared hot lines of the hotspot trace (0 = 64 up to 256 tiles (configs[2]), else 256 (configs[3]))")
-    p.add_argument("--coherent-shards", type=int, default=0, help="logical shards (0 = 1, or 8 with --gpus > 1)")
-    p.add_argument("--noc-packets", type=int, default=1 << 18, help="NoC section batch size (0 = skip)")
+    p.add_argument("--noc-packets", type=int, default=1 << 18)
     p.add_argument("--noc-tiles", type=int, default=1024)
-    p.add_argument("--coherent-net", default="hop_counter", choices=["hop_counter", "hop_by_hop", "magic"],
-                   help="memory-network model of the coherent section (hop_by_hop needs one logical shard)")
-    p.add_argument("--coherent", action="store_true",
-                   help="run the coherent section on N > 1 ranks too (RCCL all-to-all per quantum)")
     p.add_argument("--fft-m", type=int, default=14,
-                   help="configs[0] section: captured FFT of 2^m points on 16 tiles (0 = skip; configs[0] is m=20)")
+                   help="configs[0] section: captured FFT of 2^m points on 16 tiles (configs[0] is m=20)")
     return p.parse_args()
 
 
-def coherent_section(args, world, rank, dev, backend_name):
-    """Mode C: the full MSI protocol (directory, DRAM, NoC, lax-barrier quanta)
-    on the configs[2..4] hotspot trace, tiles sharded over the ranks by logical
-    shard, cross-shard messages exchanged once per quantum (RCCL all-to-all on
-    N > 1).  Timed once (the run is deterministic), checked bit-exact against
-    the C oracle on rank 0 at N = 1, whose run is also the CPU baseline."""
+def maybe_spawn(args):
+    """--gpus N without a torchrun environment: start N ranks (one process per
+    GPU) through torch.distributed.run before anything touches the GPU, and
+    exit with their status."""
+    if args.gpus <= 1 or "RANK" in os.environ:
+        return
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
+
+
+def coherent_workload(T, N, H, dev):
+    import torch
+    from graphite_amd import backend as B
+    addr = torch.empty(T * N, dtype=torch.int64, device=dev)
+    meta = torch.empty(T * N, dtype=torch.int32, device=dev)
+    B.gen_hotspot_trace(addr, meta, 0, T, N, hot_lines=H)
+    offs = np.arange(T + 1, dtype=np.uint64) * np.uint64(N)
+    return addr, meta, offs
+
+
+def coherent_run(args, T, N, H, K, net, world, rank, dev, steps, warmup, verify, cpu):
+    """One measurement of Mode C: `warmup` untimed + `steps` timed whole runs,
+    barrier + synchronize around the timed region, max over ranks."""
     import torch
     from graphite_amd import config as C
     from graphite_amd import backend as B
     from graphite_amd import coherent as CO
     from graphite_amd import dist as D
-    T, N = args.coherent_tiles, args.coherent_per_tile
-    H = args.coherent_hot_lines or (64 if T <= 256 else 256)
-    K = args.coherent_shards or (8 if world > 1 else 1)
     k0, k1 = CO.shard_range(rank, world, K)
-    net = {"hop_counter": C.NET_EMESH_HOP_COUNTER, "hop_by_hop": C.NET_EMESH_HOP_BY_HOP, "magic": C.NET_MAGIC}[args.coherent_net]
     cfg = C.default_config(T, num_shards=K, shard_begin=k0, shard_end=k1, net_model=net)
     be = B.Backend(cfg)
-    addr = torch.empty(T * N, dtype=torch.int64, device=dev)
-    meta = torch.empty(T * N, dtype=torch.int32, device=dev)
+    be.set_timing(True)
+    addr, meta, offs = coherent_workload(T, N, H, dev)
     out = torch.zeros(T * N, dtype=torch.int64, device=dev)
-    B.gen_hotspot_trace(addr, meta, 0, T, N, hot_lines=H)
-    offs = np.arange(T + 1, dtype=np.uint64) * np.uint64(N)
+
+    def step():
+        if world == 1:
+            be.coherent_run(addr, meta, offs, out)
+        else:
+            eng = B.CoherentEngine(be, addr, meta, offs, out)
+            CO.run(eng, cfg.quantum_ns * 1000, K, world, rank, "nccl", str(dev))
+
+    for _ in range(warmup):
+        step()
     torch.cuda.synchronize()
     D.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if world == 1 and K == 1:
-        be.coherent_run(addr, meta, offs, out)
-        quanta = None
-    else:
-        eng = B.CoherentEngine(be, addr, meta, offs, out)
-        quanta = CO.run(eng, cfg.quantum_ns * 1000, K, world, rank, backend_name,
-                        str(dev) if backend_name == "nccl" else "cpu")
+    for _ in range(steps):
+        step()
     torch.cuda.synchronize()
     D.barrier()
+    torch.cuda.synchronize()
     elapsed = D.max_over_ranks(time.perf_counter() - t0)
     st, cc, ri = be.coherent_stats()
-    res = {"workload": "configs[2..3]-style hotspot trace: %d tiles x %d accesses (20%% to %d shared lines, "
-                       "WRITE 1/3, gap ~2 cycles), MSI full-map directory + DRAM history tree + "
-                       "%s, quantum 1000 ns, %d logical shard(s)" % (T, N, H, "magic" if args.coherent_net == "magic" else "emesh_" + args.coherent_net, K),
-           "value": T * N / elapsed, "unit": "accesses/s", "seconds": elapsed,
-           "quanta": int(ri[C.RUN_INFO.index("quanta")]) if quanta is None else quanta,
-           "steps": int(ri[C.RUN_INFO.index("steps")]),
+    nc = be.noc_counters()
+    kern = {}
+    for name in ("coherent_step", "coherent_walk_x", "coherent_walk_y"):
+        try:
+            ms, n = be.kernel_stats(name)
+        except Exception:
+            continue
+        if n:
+            kern[name] = {"total_ms_last_run": ms, "launches": n, "avg_us": 1e3 * ms / n}
+    res = {"value": T * N * steps / elapsed, "seconds_per_run": elapsed / steps, "elapsed": elapsed,
+           "quanta": int(ri[C.RUN_INFO.index("quanta")]), "steps": int(ri[C.RUN_INFO.index("steps")]),
            "messages": int(ri[C.RUN_INFO.index("net_msgs")] + ri[C.RUN_INFO.index("self_msgs")]),
-           "simulated_ns": int(st[:, 0].max()) // 1000}
-    if rank == 0 and world == 1 and not args.no_verify:
+           "boundary_records": int(ri[C.RUN_INFO.index("boundary_msgs")]),
+           "simulated_ns": int(st[:, 0].max()) // 1000, "kernels": kern}
+    if world > 1:
+        # every rank holds its own tiles' outputs: the node's totals for the check
+        import torch.distributed as dist
+        tot = [torch.from_numpy(x.view(np.int64).copy()).to(dev) for x in (st, cc, nc)]
+        for x in tot + [out]:
+            dist.all_reduce(x)
+        st, cc, nc = [x.cpu().numpy().view(np.uint64).reshape(y.shape) for x, y in zip(tot, (st, cc, nc))]
+    if rank == 0 and verify:
         from oracle import pyoracle as po
-        a, m, o = po.gen_trace(T, N, hot_lines=H)
-        oc = po.OracleCoherent(C.default_config(T, num_shards=K, net_model=net))
+        a = addr.cpu().numpy().view(np.uint64)
+        m = meta.cpu().numpy().view(np.uint32)
+        ocfg = C.default_config(T, num_shards=K, net_model=net)
+        threads = args.cpu_threads or max(1, min(K, os.cpu_count() or 1))
         c0 = time.perf_counter()
-        ref = oc.run(a, m, o)
-        cdt = time.perf_counter() - c0
-        res["bit_exact_checked"] = bool(np.array_equal(out.cpu().numpy().view(np.uint64), ref) and
-                                        np.array_equal(st, oc.tile_stats()) and
-                                        np.array_equal(cc, oc.cache_counters()))
+        ref = po.coherent_run_parallel(ocfg, a, m, offs, threads)
+        pdt = time.perf_counter() - c0
+        got = out.cpu().numpy().view(np.uint64)
+        res["bit_exact_checked"] = bool(np.array_equal(got, ref[0]) and np.array_equal(st, ref[1]) and
+                                        np.array_equal(cc, ref[2]) and np.array_equal(nc, ref[3]))
         if not res["bit_exact_checked"]:
             print("bench.py: COHERENT BIT-EXACT CHECK FAILED", file=sys.stderr)
-        res["cpu_baseline"] = {"value": T * N / cdt, "unit": "accesses/s", "cores": 1, "kind": "port",
-                               "sample": "the whole coherent workload, oracle/gg_coherent.inc -O3, 1 thread, "
-                                         "%.2f s" % cdt}
+        if cpu:
+            oc = po.OracleCoherent(ocfg)
+            c0 = time.perf_counter()
+            ref1 = oc.run(a, m, offs)
+            sdt = time.perf_counter() - c0
+            res["bit_exact_checked"] = res["bit_exact_checked"] and bool(np.array_equal(ref1, ref[0]))
+            res["cpu_baseline"] = {
+                "value": T * N / pdt, "unit": "accesses/s", "cores": threads, "kind": "port",
+                "sample": "the whole workload once (%d tiles x %d accesses): oracle/gg_coherent.inc -O3, one context "
+                          "per logical shard on %d OpenMP threads, %.2f s" % (T, N, threads, pdt),
+                "one_thread": {"value": T * N / sdt, "cores": 1, "seconds": sdt},
+                "host": host_info()}
     be.close()
     return res
+
+
+def host_info():
+    info = {"nproc": os.cpu_count()}
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name"):
+                info["model"] = line.split(":", 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return info
+
+
+def hop_counter_section(args, dev):
+    """The headline workload at --hc-per-tile accesses per tile on
+    emesh_hop_counter (closed-form routes, no router contention)."""
+    from graphite_amd import config as C
+    T, N, H, K = args.tiles, args.hc_per_tile, args.hot_lines, args.shards
+    r = coherent_run(args, T, N, H, K, C.NET_EMESH_HOP_COUNTER, 1, 0, dev, 1, 0, not args.no_verify,
+                     not args.no_cpu_baseline)
+    r["workload"] = ("%d tiles x %d hotspot accesses (%d hot lines), MSI + DRAM + emesh_hop_counter, %d logical shards"
+                     % (T, N, H, K))
+    r["unit"] = "accesses/s"
+    return r
 
 
 def fft_section(args, dev):
@@ -361,129 +439,160 @@ def cpu_baseline(tiles, per_tile, threads):
     return tiles * per_tile / dt, dt
 
 
-def main():
-    args = parse()
+def private_section(args, dev):
+    """Mode P (round 1's headline): configs[1]'s uniform-random private trace at
+    configs[3] scale (1024 tiles x --private-per-tile), single-pass streaming
+    replay k_cache_stream; 3 timed replays; one tile bit-exact vs the oracle;
+    the oracle on --cpu-sample-tiles tile replays as its CPU baseline."""
     import torch
-    import torch.distributed as dist
     from graphite_amd import config as C
     from graphite_amd import backend as B
-
-    from graphite_amd import dist as D
-    world, rank, local = D.env()
-    torch.cuda.set_device(local)
-    D.init("nccl")
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-
-    T, N = args.tiles, args.per_tile
-    cfg = C.default_config(T, device=local, replay_kernel=args.replay_kernel)
+    T, N = args.tiles, args.private_per_tile
+    cfg = C.default_config(T, replay_kernel=args.replay_kernel)
     be = B.Backend(cfg)
     be.set_timing(True)
     stream = torch.cuda.current_stream(dev)
-
-    # synthetic configs[1] trace of this rank's tiles, resident in HBM
     n = T * N
     addr = torch.empty(n, dtype=torch.int64, device=dev)
     meta = torch.empty(n, dtype=torch.int32, device=dev)
     result = torch.empty(n, dtype=torch.int32, device=dev)
-    B.gen_uniform_trace(addr, meta, rank * T, T, N, stream=stream)
+    B.gen_uniform_trace(addr, meta, 0, T, N, stream=stream)
     offs = np.arange(T + 1, dtype=np.uint64) * np.uint64(N)
-
-    def step():
-        be.reset()
-        be.cache_access_batch(addr, meta, offs, result, None, stream)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    D.barrier()
-    torch.cuda.synchronize()
     kms = {k: [] for k in KERNEL_BYTES}
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        for k in KERNEL_BYTES:
-            kms[k].append(be.kernel_time_ms(k))
-    torch.cuda.synchronize()
-    D.barrier()
-    torch.cuda.synchronize()
-    elapsed = D.max_over_ranks(time.perf_counter() - t0)
-
-    # bit-exact check of this run (rank 0): one tile's results + counters vs the oracle
-    verified = None
-    if not args.no_verify and rank == 0:
+    times = []
+    for it in range(4):                               # the first replay warms up
+        be.reset()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        be.cache_access_batch(addr, meta, offs, result, None, stream)
+        torch.cuda.synchronize()
+        if it:
+            times.append(time.perf_counter() - t0)
+            for k in KERNEL_BYTES:
+                kms[k].append(be.kernel_time_ms(k))
+    kern = {}
+    for k, v in kms.items():
+        v = [x for x in v if x >= 0]
+        if v:
+            ms = float(np.mean(v))
+            kern[k] = {"ms": ms, "bytes_per_access": KERNEL_BYTES[k], "GB_s": n * KERNEL_BYTES[k] / (ms * 1e-3) / 1e9}
+    dom = max(kern, key=lambda k: kern[k]["ms"])
+    res = {"workload": "configs[1] uniform-random private generator at %d tiles x %d accesses, 32KB/4w L1-D + "
+                       "512KB/8w L2, private-cache mode" % (T, N),
+           "value": n / float(np.mean(times)), "unit": "accesses/s",
+           "roofline": {"bound": "hbm", "kernel": KERNEL_SYMBOL[dom], "achieved": kern[dom]["GB_s"],
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": kern[dom]["GB_s"] / HBM_PEAK_GBS,
+                        "kernel_ms": kern[dom]["ms"], "bytes_per_access": KERNEL_BYTES[dom], "kernels": kern}}
+    prof = pmc_traffic(KERNEL_SYMBOL[dom], "private_%dx%d" % (T, N))
+    res["roofline"]["traffic"] = prof["bytes"] if prof else None
+    if prof:
+        res["roofline"]["traffic_source"] = prof["source"]
+    if not args.no_verify:
         from oracle import pyoracle as po
         cnt = be.cache_counters()
-        t = T - 1                                   # last local tile = global tile rank*T + T-1
-        a, m = po.gen_uniform(rank * T + t, 0, N)
+        t = T - 1
+        a, m = po.gen_uniform(t, 0, N)
         oc = po.OracleCache(C.default_config(1))
-        ref = oc.run(a - np.uint64((rank * T + t) << 26), m, np.array([0, N], np.uint64))
+        ref = oc.run(a - np.uint64(t << 26), m, np.array([0, N], np.uint64))
         got = result[t * N:(t + 1) * N].cpu().numpy().view(np.uint32)
-        verified = bool(np.array_equal(got, ref) and np.array_equal(cnt[t], oc.counters()[0]))
-        if not verified:
-            print("bench.py: BIT-EXACT CHECK FAILED", file=sys.stderr)
+        res["bit_exact_checked"] = bool(np.array_equal(got, ref) and np.array_equal(cnt[t], oc.counters()[0]))
+        if not res["bit_exact_checked"]:
+            print("bench.py: PRIVATE BIT-EXACT CHECK FAILED", file=sys.stderr)
+    if not args.no_cpu_baseline:
+        threads = min(16, os.cpu_count() or 1)
+        cps, cdt = cpu_baseline(args.cpu_sample_tiles, N, threads)
+        res["cpu_baseline"] = {"value": cps, "unit": "accesses/s", "cores": threads, "kind": "port",
+                               "sample": "%d tiles x %d accesses, oracle/gg_oracle.c -O3, one tile per thread, %.1f s"
+                                         % (args.cpu_sample_tiles, N, cdt)}
+    be.close()
+    del addr, meta, result
+    torch.cuda.empty_cache()
+    return res
 
+
+def main():
+    args = parse()
+    maybe_spawn(args)
+    import torch
+    import torch.distributed as dist
+    from graphite_amd import config as C
+    from graphite_amd import dist as D
+    world, rank, local = D.env()
+    if world != args.gpus and "RANK" in os.environ:
+        args.gpus = world
+    torch.cuda.set_device(local)
+    D.init("nccl")
+    dev = torch.device("cuda", local)
+    net = NET[args.net]
+    T, N, H, K = args.tiles, args.per_tile, args.hot_lines, args.shards
+    if K % world:
+        raise SystemExit("bench.py: %d logical shards do not split over %d ranks" % (K, world))
+    head = coherent_run(args, T, N, H, K, net, world, rank, dev, args.steps, args.warmup,
+                        not args.no_verify, world == 1 and not args.no_cpu_baseline)
     if rank == 0:
-        total = world * n * args.steps
-        value = total / elapsed
-        kern = {}
-        for k, v in kms.items():
-            v = [x for x in v if x >= 0]          # kernels of this path only (negative = not launched)
-            if not v:
-                continue
-            ms = float(np.mean(v[1:] if len(v) > 1 else v))
-            kern[k] = {"ms": ms, "bytes_per_access": KERNEL_BYTES[k],
-                       "GB_s": n * KERNEL_BYTES[k] / (ms * 1e-3) / 1e9}
-        dom = max(kern, key=lambda k: kern[k]["ms"])
-        achieved = kern[dom]["GB_s"]
+        kern = head["kernels"]
+        dom = max(kern, key=lambda k: kern[k]["total_ms_last_run"]) if kern else None
+        step = kern.get("coherent_step")
+        achieved = COH_BYTES_PER_ACCESS * T * N / (step["total_ms_last_run"] * 1e-3) / 1e9 if step else None
+        wl = ("configs[3]: %d tiles (%dx%d mesh) x %d accesses per tile of the hotspot trace (20%% to %d lines "
+              "shared by all tiles, WRITE p=1/3, ~2-cycle gaps), pr_l1_pr_l2_dram_directory_msi + full-map directory "
+              "+ DRAM history-tree queue + %s (history-tree router contention), quantum 1000 ns, %d logical shards "
+              "(2-D blocks) over %d GPU(s)" % (T, int(T ** 0.5), int(T ** 0.5), N, H,
+                                              {1: "emesh_hop_counter", 2: "emesh_hop_by_hop", 0: "magic"}[net], K, world))
         out = {
-            "metric": "simulated mem accesses/sec (node); bit-exact stats",
-            "value": value,
+            "metric": "simulated mem accesses/sec (node) at 1024 tiles, 1/2/4/8 GPU; bit-exact stats",
+            "value": head["value"],
             "unit": "accesses/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
+            "ms_per_step": head["seconds_per_run"] * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "u64",
-            "data": "synthetic (configs[1] SplitMix64 uniform-random private trace, generated on device)",
-            "config": {"workload": ("configs[1] exactly (64 tiles x 2^22)" if (T, N) == (64, 1 << 22) else
-                                    "%d tiles/GPU x %d accesses/tile (configs[3] scale) with the configs[1] "
-                                    "uniform-random private generator" % (T, N)) +
-                                   "; 32KB/4w L1-D + 512KB/8w L2, private-cache mode",
-                       "tiles_per_gpu": T, "accesses_per_tile": N, "mode": "private",
-                       "parallelism": "tiles sharded over %d rank(s), no data-path collective" % world},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": KERNEL_SYMBOL[dom] if (dom != "cache_replay" or args.replay_kernel != 1)
-                         else "k_cache_replay", "kernel_ms": kern[dom]["ms"],
-                         "bytes_per_access": KERNEL_BYTES[dom], "launch_accesses": n,
-                         "kernels": kern,
-                         "path_GB_s": n * ALGO_BYTES_PER_ACCESS / (elapsed / args.steps) / 1e9},
-            "bit_exact_checked": verified,
+            "data": "synthetic (configs[2..4] SplitMix64 hotspot trace, generated on device)",
+            "config": {"workload": wl, "tiles": T, "accesses_per_tile": N, "hot_lines": H, "logical_shards": K,
+                       "mode": "coherent", "network": args.net,
+                       "parallelism": "%d logical shards over %d rank(s); held cross-shard records exchanged once "
+                                      "per quantum" % (K, world)},
+            "roofline": {"bound": "hbm", "kernel": "k_c_step", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                         "bytes_per_access": COH_BYTES_PER_ACCESS, "launch_accesses": T * N / step["launches"] if step else None,
+                         "kernel_avg_us": step["avg_us"] if step else None,
+                         "dominant_kernel_by_time": KERNEL_SYMBOL.get(dom, dom),
+                         "note": "Mode C is latency-bound: a step is a chain of dependent accesses per tile and the "
+                                 "hop-by-hop walks are serial per chain (DESIGN.md §4); the fraction measures how far "
+                                 "that is from the HBM bound, not an HBM bottleneck"},
+            "coherent": {k: head[k] for k in ("quanta", "steps", "messages", "boundary_records", "simulated_ns",
+                                              "kernels", "seconds_per_run")},
+            "bit_exact_checked": head.get("bit_exact_checked"),
         }
-        prof = pmc_traffic(out["roofline"]["kernel"], T, N)
+        prof = pmc_traffic("k_c_step", "coherent_%s_%dx%d_k%d" % (args.net, T, N, K))
         if prof:
             out["roofline"]["traffic"] = prof["bytes"]
             out["roofline"]["traffic_source"] = prof["source"]
-        if not args.no_cpu_baseline:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            cps, cdt = cpu_baseline(args.cpu_sample_tiles, N, threads)
-            out["cpu_baseline"] = {"value": cps, "unit": "accesses/s", "cores": threads, "kind": "port",
-                                   "sample": "%d tiles x %d accesses of the same workload, oracle/gg_oracle.c "
-                                             "-O3, one tile per thread, %.1f s" % (args.cpu_sample_tiles, N, cdt)}
-    if args.coherent_tiles and (world == 1 or args.coherent):
-        coh = coherent_section(args, world, rank, dev, "nccl")
-        if rank == 0:
-            out["coherent"] = coh
-    if args.fft_m and world == 1:
-        out["fft"] = fft_section(args, dev)
-    if args.noc_packets and world == 1:
-        out["noc"] = noc_section(args, dev)
-    if args.stress_tiles and world == 1:
-        out["stress"] = stress_section(args, dev)
+        if "cpu_baseline" in head:
+            out["cpu_baseline"] = head["cpu_baseline"]
+    secs = [x for x in args.sections.split(",") if x] if world == 1 else []
+    for name in secs:
+        try:
+            if name == "hop_counter":
+                r = hop_counter_section(args, dev)
+            elif name == "fft" and args.fft_m:
+                r = fft_section(args, dev)
+            elif name == "private":
+                r = private_section(args, dev)
+            elif name == "noc" and args.noc_packets:
+                r = noc_section(args, dev)
+            elif name == "stress" and args.stress_tiles:
+                r = stress_section(args, dev)
+            else:
+                continue
+        except Exception as e:            # a section failing must not hide the headline
+            r = {"error": repr(e)}
+            print("bench.py: section %s failed: %r" % (name, e), file=sys.stderr)
+        out[name] = r
     if rank == 0:
         print(json.dumps(out))
     if world > 1:

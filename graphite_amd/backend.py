@@ -56,7 +56,8 @@ EXPORTS = ["gg_abi_version", "gg_last_error", "gg_config_default", "gg_create", 
            "gg_noc_route_batch", "gg_noc_get_counters", "gg_queue_delay_batch",
            "gg_gen_uniform_trace", "gg_kernel_time_ms", "gg_set_timing",
            "gg_coherent_begin", "gg_coherent_quantum", "gg_coherent_export", "gg_coherent_import",
-           "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace", "gg_shard_map"]
+           "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace", "gg_shard_map",
+           "gg_kernel_stats"]
 
 
 class _CStatus(ctypes.Structure):
@@ -105,8 +106,10 @@ def load():
     L.gg_coherent_get_stats.argtypes = [vp, vp, vp, vp]
     L.gg_gen_hotspot_trace.argtypes = [vp, vp, u32, u32, u64, u64, u32, u32, u32, u32, vp]
     L.gg_shard_map.argtypes = [u32, u32, vp]
-    for name in ["gg_shard_map", "gg_coherent_begin", "gg_coherent_quantum", "gg_coherent_export", "gg_coherent_import",
-                 "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace", "gg_shard_map"]:
+    L.gg_kernel_stats.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64)]
+    for name in ["gg_kernel_stats", "gg_shard_map", "gg_coherent_begin", "gg_coherent_quantum", "gg_coherent_export", "gg_coherent_import",
+                 "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace", "gg_shard_map",
+           "gg_kernel_stats"]:
         getattr(L, name).restype = i32
     for name in ["gg_reset", "gg_cache_access_batch", "gg_cache_get_counters", "gg_cache_get_line_info",
                  "gg_cache_set_line_info", "gg_cache_access_line", "gg_cache_insert_line",
@@ -168,6 +171,13 @@ class Backend:
 
     def kernel_time_ms(self, name):
         return load().gg_kernel_time_ms(self.h, name.encode())
+
+    def kernel_stats(self, name):
+        """(total device ms, launches) of a coherent-mode kernel since the last
+        coherent begin (timing must be on): HIP events around every launch."""
+        ms, n = ctypes.c_double(0), ctypes.c_uint64(0)
+        _check(load().gg_kernel_stats(self.h, name.encode(), ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
 
     # ---- cache ----------------------------------------------------------
     def cache_access_batch(self, addr, meta, tile_offsets, result=None, evicted=None, stream=None):

@@ -359,6 +359,14 @@ float gg_kernel_time_ms(gg_ctx* ctx, const char* kernel)
 
 void gg_set_timing(gg_ctx* ctx, int enabled) { if (ctx) ctx->timing = enabled != 0; }
 
+gg_status gg_kernel_stats(gg_ctx* ctx, const char* kernel, double* total_ms, uint64_t* launches)
+{
+  if (!ctx || !kernel || !total_ms || !launches) return gg_fail(GG_ERR_INVALID, "NULL argument");
+  if (gg_coh_kernel_stats(ctx, kernel, total_ms, launches) != GG_OK)
+    return gg_fail(GG_ERR_INVALID, "no launch statistics for kernel '%s'", kernel);
+  return GG_OK;
+}
+
 gg_status gg_gen_uniform_trace(uint64_t* addr_dev, uint32_t* meta_dev, uint32_t tile_begin, uint32_t tiles,
                                uint64_t per_tile, uint64_t first, uint32_t lines_log2, uint32_t base_shift, void* stream)
 {

@@ -1707,7 +1707,50 @@ struct gg_coh_state {
   uint64_t n_records = 0;
   size_t step_lds = 0, walk_lds = 0;
   bool begun = false;
+  // live kernel timing (gg_set_timing): an event pair around every launch,
+  // harvested at the batch syncs; totals since gg_coherent_begin
+  std::vector<hipEvent_t> tev;
+  std::vector<int> tkind;
+  uint32_t tused = 0;
+  double ksum[3] = {0, 0, 0};
+  uint64_t kcnt[3] = {0, 0, 0};
 };
+static const char* kKernelNames[3] = {"coherent_step", "coherent_walk_x", "coherent_walk_y"};
+
+template <class F> static void timed_launch(gg_ctx* ctx, gg_coh_state* C, hipStream_t s, int kind, F&& fn)
+{
+  if (!ctx->timing) { fn(); return; }
+  if (C->tev.size() < 2 * (size_t)(C->tused + 1)) {
+    const size_t n0 = C->tev.size();
+    C->tev.resize(n0 + 512);
+    for (size_t i = n0; i < C->tev.size(); ++i) hipEventCreate(&C->tev[i]);
+    C->tkind.resize(C->tev.size() / 2);
+  }
+  hipEventRecord(C->tev[2 * C->tused], s);
+  fn();
+  hipEventRecord(C->tev[2 * C->tused + 1], s);
+  C->tkind[C->tused++] = kind;
+}
+static void timed_harvest(gg_coh_state* C)
+{
+  for (uint32_t i = 0; i < C->tused; ++i) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, C->tev[2 * i], C->tev[2 * i + 1]) == hipSuccess) {
+      C->ksum[C->tkind[i]] += ms;
+      C->kcnt[C->tkind[i]]++;
+    }
+  }
+  C->tused = 0;
+}
+
+gg_status gg_coh_kernel_stats(gg_ctx* ctx, const char* name, double* total_ms, uint64_t* launches)
+{
+  gg_coh_state* C = ctx->coh;
+  for (int k = 0; k < 3; ++k)
+    if (C && std::strcmp(name, kKernelNames[k]) == 0) { *total_ms = C->ksum[k]; *launches = C->kcnt[k]; return GG_OK; }
+  *total_ms = 0; *launches = 0;
+  return GG_ERR_INVALID;
+}
 
 static int ilog2(uint64_t v) { int p = -1; while (v) { v >>= 1; ++p; } return p; }
 static int clog2(uint64_t v) { int p = ilog2(v); return ((1ull << p) == v) ? p : p + 1; }
@@ -1733,6 +1776,7 @@ void gg_coh_free(gg_ctx* ctx)
 {
   gg_coh_state* C = ctx->coh;
   if (!C) return;
+  for (hipEvent_t e : C->tev) hipEventDestroy(e);
   for (void* p : C->allocs) hipFree(p);
   delete C;
   ctx->coh = nullptr;
@@ -1936,6 +1980,8 @@ gg_status gg_coherent_begin(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_ou
   if (tr->num_records && (!tr->addr_dev || !tr->meta_dev)) return gg_fail(GG_ERR_INVALID, "NULL trace pointers");
   C->S.addr = tr->addr_dev; C->S.meta = tr->meta_dev; C->S.out = access_out_dev;
   C->n_records = tr->num_records;
+  for (int k = 0; k < 3; ++k) { C->ksum[k] = 0; C->kcnt[k] = 0; }
+  C->tused = 0;
   GG_HIP(hipMemcpyAsync(C->offs_dev, tr->tile_offsets, sizeof(uint64_t) * (P.T + 1), hipMemcpyHostToDevice, s));
   if (gg_status st = gg_noc_reset(ctx, s)) return st;
   GG_HIP(hipMemsetAsync(ctx->err_dev, 0, sizeof(uint32_t), s));
@@ -1970,10 +2016,10 @@ gg_status gg_coherent_quantum(gg_ctx* ctx, uint64_t q, gg_coherent_status* out)
   uint32_t k = 0, batch = 8;
   for (;;) {
     for (uint32_t b = 0; b < batch; ++b, ++k) {
-      hipLaunchKernelGGL(k_c_step, dim3(P.L), dim3(64), C->step_lds, s, P, C->S, k, 0u, barrier);
+      timed_launch(ctx, C, s, 0, [&] { hipLaunchKernelGGL(k_c_step, dim3(P.L), dim3(64), C->step_lds, s, P, C->S, k, 0u, barrier); });
       if (hbh) {
-        if (P.nsx) hipLaunchKernelGGL(k_c_walk, dim3(P.nsx), dim3(64), C->walk_lds, s, P, C->S, k, 0);
-        if (P.nsy) hipLaunchKernelGGL(k_c_walk, dim3(P.nsy), dim3(64), C->walk_lds, s, P, C->S, k, 1);
+        if (P.nsx) timed_launch(ctx, C, s, 1, [&] { hipLaunchKernelGGL(k_c_walk, dim3(P.nsx), dim3(64), C->walk_lds, s, P, C->S, k, 0); });
+        if (P.nsy) timed_launch(ctx, C, s, 2, [&] { hipLaunchKernelGGL(k_c_walk, dim3(P.nsy), dim3(64), C->walk_lds, s, P, C->S, k, 1); });
       }
     }
     GG_HIP(hipGetLastError());
@@ -1981,6 +2027,7 @@ gg_status gg_coherent_quantum(gg_ctx* ctx, uint64_t q, gg_coherent_status* out)
     GG_HIP(hipMemcpyAsync(&quiet, C->S.quiet, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     GG_HIP(hipMemcpyAsync(&err, ctx->err_dev, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     GG_HIP(hipStreamSynchronize(s));
+    timed_harvest(C);
     if (err) return coh_check(ctx);
     if (quiet) break;
     if (batch < 64) batch *= 2;
@@ -2079,10 +2126,10 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
   uint32_t L = 0, batch = 16;
   for (;;) {
     for (uint32_t b = 0; b < batch; ++b, ++L) {
-      hipLaunchKernelGGL(k_c_step, dim3(P.L), dim3(64), C->step_lds, s, P, C->S, L, 1u, (uint64_t)0);
+      timed_launch(ctx, C, s, 0, [&] { hipLaunchKernelGGL(k_c_step, dim3(P.L), dim3(64), C->step_lds, s, P, C->S, L, 1u, (uint64_t)0); });
       if (hbh) {
-        if (P.nsx) hipLaunchKernelGGL(k_c_walk, dim3(P.nsx), dim3(64), C->walk_lds, s, P, C->S, L, 0);
-        if (P.nsy) hipLaunchKernelGGL(k_c_walk, dim3(P.nsy), dim3(64), C->walk_lds, s, P, C->S, L, 1);
+        if (P.nsx) timed_launch(ctx, C, s, 1, [&] { hipLaunchKernelGGL(k_c_walk, dim3(P.nsx), dim3(64), C->walk_lds, s, P, C->S, L, 0); });
+        if (P.nsy) timed_launch(ctx, C, s, 2, [&] { hipLaunchKernelGGL(k_c_walk, dim3(P.nsy), dim3(64), C->walk_lds, s, P, C->S, L, 1); });
       }
     }
     GG_HIP(hipGetLastError());
@@ -2091,6 +2138,7 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
     GG_HIP(hipMemcpyAsync(&done, C->S.qs + QS_DONE, sizeof(done), hipMemcpyDeviceToHost, s));
     GG_HIP(hipMemcpyAsync(&err, ctx->err_dev, sizeof(err), hipMemcpyDeviceToHost, s));
     GG_HIP(hipStreamSynchronize(s));
+    timed_harvest(C);
     if (err) break;
     if (done) break;
     if (batch < 256) batch *= 2;

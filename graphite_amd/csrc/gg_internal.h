@@ -130,3 +130,4 @@ gg_status gg_noc_counters(gg_ctx* ctx, uint64_t* out);
 // coherent path (gg_coherent.hip)
 void      gg_coh_free(gg_ctx* ctx);
 gg_status gg_htree_run(gg_ctx* ctx, uint64_t min_proc, const uint64_t* t, const uint64_t* p, uint64_t n, uint64_t* d);
+gg_status gg_coh_kernel_stats(gg_ctx* ctx, const char* name, double* total_ms, uint64_t* launches);

@@ -98,6 +98,10 @@ void oracle_coh_tile_stats(const oracle_coh* C, uint64_t* out);      /* [tile][G
 void oracle_coh_cache_counters(const oracle_coh* C, uint64_t* out);  /* [tile][2][12] */
 void oracle_coh_net_counters(const oracle_coh* C, uint64_t* out);    /* [tile][GG_NUM_NET_COUNTERS] */
 void oracle_coh_run_info(const oracle_coh* C, uint64_t* out);        /* [GG_NUM_RUN_INFO] */
+/* the whole run with one context per logical shard, `threads` OpenMP threads */
+int  oracle_coh_run_parallel(const gg_config* cfg, int threads, const uint64_t* addr, const uint32_t* meta,
+                             const uint64_t* tile_offsets, uint64_t* access_out, uint64_t* tile_stats,
+                             uint64_t* cache, uint64_t* net, uint64_t* run_info);
 
 /* Network::netSend line split of Core::initiateMemoryAccess (core.cc:167-201):
  * returns the number of line accesses [addr, addr+size) produces and writes

@@ -73,6 +73,9 @@ def lib():
                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u64p, _u32p]
         L.oracle_shard_map.restype = ctypes.c_int
         L.oracle_shard_map.argtypes = [ctypes.c_uint32, ctypes.c_uint32, _u32p]
+        L.oracle_coh_run_parallel.restype = ctypes.c_int
+        L.oracle_coh_run_parallel.argtypes = [ctypes.POINTER(GGConfig), ctypes.c_int, _u64p, _u32p, _u64p, vp, vp, vp,
+                                              vp, vp]
         L.oracle_coh_create.restype = vp
         L.oracle_coh_create.argtypes = [ctypes.POINTER(GGConfig)]
         L.oracle_coh_destroy.argtypes = [vp]
@@ -118,6 +121,25 @@ def gen_trace(tiles, per_tile, **kw):
     meta = np.concatenate([p[1] for p in parts]) if parts else np.zeros(0, np.uint32)
     offs = np.arange(tiles + 1, dtype=np.uint64) * np.uint64(per_tile)
     return addr, meta, offs
+
+
+def coherent_run_parallel(cfg, addr, meta, tile_offsets, threads):
+    """The coherent run as one oracle context per logical shard, the shards'
+    quanta on `threads` OpenMP threads (the all-core CPU baseline); returns
+    (access words, tile stats, cache counters, net counters, run info)."""
+    T = cfg.num_tiles
+    out = np.zeros(len(addr), np.uint64)
+    st = np.zeros((T, NUM_TILE_STATS), np.uint64)
+    cc = np.zeros((T, 2, NUM_CACHE_COUNTERS), np.uint64)
+    nc = np.zeros((T, NUM_NET_COUNTERS), np.uint64)
+    ri = np.zeros(NUM_RUN_INFO, np.uint64)
+    rc = lib().oracle_coh_run_parallel(ctypes.byref(cfg), threads, np.ascontiguousarray(addr, np.uint64),
+                                       np.ascontiguousarray(meta, np.uint32),
+                                       np.ascontiguousarray(tile_offsets, np.uint64), out.ctypes.data,
+                                       st.ctypes.data, cc.ctypes.data, nc.ctypes.data, ri.ctypes.data)
+    if rc != 0:
+        raise RuntimeError("coherent oracle (parallel) rc=%d" % rc)
+    return out, st, cc, nc, ri
 
 
 def shard_map(num_tiles, num_shards):

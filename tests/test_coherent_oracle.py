@@ -116,3 +116,23 @@ def test_shard_blocks_keep_routes_inside():
                 while y != d // w:
                     y += 1 if d // w > y else -1
                     assert sm[y * w + x] == sm[s]
+
+
+@pytest.mark.parametrize("T,K,net", [(64, 8, C.NET_EMESH_HOP_BY_HOP), (64, 4, C.NET_EMESH_HOP_COUNTER),
+                                     (256, 8, C.NET_EMESH_HOP_BY_HOP)])
+def test_parallel_oracle_equals_single_context(T, K, net):
+    """The all-core CPU baseline (one oracle context per shard, OpenMP) is the
+    same schedule as one context owning every shard: identical outputs."""
+    N = 200
+    a, m, o = po.gen_trace(T, N, hot_lines=32)
+    cfg = C.default_config(T, num_shards=K, net_model=net)
+    oc = po.OracleCoherent(cfg)
+    out = oc.run(a, m, o)
+    got = po.coherent_run_parallel(cfg, a, m, o, threads=4)
+    np.testing.assert_array_equal(got[0], out)
+    np.testing.assert_array_equal(got[1], oc.tile_stats())
+    np.testing.assert_array_equal(got[2], oc.cache_counters())
+    np.testing.assert_array_equal(got[3], oc.net_counters())
+    ri = oc.run_info()
+    for k in ("quanta", "steps", "net_msgs", "self_msgs", "boundary_msgs"):
+        assert got[4][C.RUN_INFO.index(k)] == ri[C.RUN_INFO.index(k)], k
