@@ -190,11 +190,12 @@ template <int N> __device__ __forceinline__ uint32_t pick(const uint32_t (&a)[N]
 struct Cache {
   uint64_t* tag; uint8_t* meta; uint8_t* rr; uint64_t* cg;
   uint32_t sets, ways, log_line, pol, wb, ln;
-  uint32_t c[GG_NUM_CACHE_COUNTERS];   // this step's counter increments, flushed to cg
+  uint32_t cd;                         // this step's counter increments: lane k holds counter k
   // the last set this lane loaded (its way), kept in step with every store, so
   // consecutive operations on one set load it once
   uint32_t cset; uint64_t ctv; uint32_t cmv;
 
+  __device__ __forceinline__ void cnt(uint32_t k) { if (ln == k) ++cd; }
   __device__ __forceinline__ uint32_t set_of(uint64_t a) const { return (uint32_t)((a >> log_line) & (sets - 1)); }   // cache_hash_fn.h:17
   __device__ __forceinline__ uint64_t tag_of(uint64_t a) const { return a >> log_line; }                             // cache.cc:495
   __device__ __forceinline__ void ld(uint32_t s, uint64_t& tv, uint32_t& mv)
@@ -236,9 +237,9 @@ struct Cache {
   }
   __device__ __forceinline__ void miss_counters(bool wr, bool miss)                                               // cache.cc:321-360
   {
-    c[GG_CC_ACCESSES]++;
-    if (wr) c[GG_CC_WRITE_ACCESSES]++; else c[GG_CC_READ_ACCESSES]++;
-    if (miss) { c[GG_CC_MISSES]++; if (wr) c[GG_CC_WRITE_MISSES]++; else c[GG_CC_READ_MISSES]++; }
+    cnt(GG_CC_ACCESSES);
+    if (wr) cnt(GG_CC_WRITE_ACCESSES); else cnt(GG_CC_READ_ACCESSES);
+    if (miss) { cnt(GG_CC_MISSES); if (wr) cnt(GG_CC_WRITE_MISSES); else cnt(GG_CC_READ_MISSES); }
   }
   // getCacheLineInfo (cache.cc:187-215): state / loc of the line, I / 0 when absent
   __device__ __forceinline__ void get(uint64_t a, uint32_t& st, uint32_t& loc)
@@ -246,7 +247,7 @@ struct Cache {
     uint64_t tv; uint32_t mv;
     ld(set_of(a), tv, mv);
     const int w = way_of(tv, tag_of(a));
-    c[GG_CC_TAG_READS]++;
+    cnt(GG_CC_TAG_READS);
     if (w >= 0) { const uint32_t m = (uint32_t)__shfl((int)mv, w); st = m & 3u; loc = (m >> 2) & 1u; }
     else { st = ST_I; loc = 0; }
   }
@@ -262,7 +263,7 @@ struct Cache {
       st_meta(s, (mv & 0xF8u) | st | (loc << 2));
       if (st == ST_I) st_tag(s, INV_ADDR);
     }
-    c[GG_CC_TAG_WRITES]++;
+    cnt(GG_CC_TAG_WRITES);
     return true;
   }
   // accessCacheLine (cache.cc:84-112)
@@ -274,7 +275,7 @@ struct Cache {
     const int w = way_of(tv, tag_of(a));
     if (w < 0) return false;
     touch(s, w, mv);
-    if (store) c[GG_CC_DATA_WRITES]++; else c[GG_CC_DATA_READS]++;
+    if (store) cnt(GG_CC_DATA_WRITES); else cnt(GG_CC_DATA_READS);
     return true;
   }
   // insertCacheLine (cache.cc:114-184) with getReplacementWay: LRU (lru:23-38) = first
@@ -307,13 +308,13 @@ struct Cache {
       mv = nm;
     }
     touch(s, w, mv);
-    c[GG_CC_TAG_READS]++;
+    cnt(GG_CC_TAG_READS);
     if (ev) {
-      c[GG_CC_DATA_READS]++;
-      c[GG_CC_EVICTIONS]++;
-      if (wb && ev_st == ST_M) c[GG_CC_DIRTY_EVICTIONS]++;
+      cnt(GG_CC_DATA_READS);
+      cnt(GG_CC_EVICTIONS);
+      if (wb && ev_st == ST_M) cnt(GG_CC_DIRTY_EVICTIONS);
     }
-    c[GG_CC_TAG_WRITES]++; c[GG_CC_DATA_WRITES]++;
+    cnt(GG_CC_TAG_WRITES); cnt(GG_CC_DATA_WRITES);
     return true;
   }
 };
@@ -332,6 +333,7 @@ struct StepLds {
   uint64_t x1[kInLds], x2[kInLds], x3[kInLds];
   uint32_t i1[kInLds], i2[kInLds];
   uint32_t ch[2 * kChunks];                               // record chunks: base, used
+  Work wstack[WSTACK];                                    // directory work loop continuations
 };
 
 // ---------------------------------------------------------------------------
@@ -342,7 +344,7 @@ struct Tile {
   uint32_t lt, tile, ln, p;             // local index, tile id, lane, step parity
   StepLds& sl;
   Cache L1, L2;
-  uint64_t st[GG_NUM_TILE_STATS];       // this step's statistics increments
+  uint64_t sd;                          // this step's statistics increments: lane k holds statistic k
   uint64_t rec, rec_end, clk, pend_start, out_addr, out_time;
   uint32_t blocked, seq, nrep, nrq;
   HQueue* dq; HNode* dnd; bool dq_lds;
@@ -355,11 +357,10 @@ struct Tile {
       : P(P_), S(S_), lt(l), tile(S_.gtile[l]), ln(lane_id()), p(par), sl(s_)
   {
     L1 = Cache{S.l1_tag + (size_t)lt * P.s1 * P.a1, S.l1_meta + (size_t)lt * P.s1 * P.a1, S.l1_rr + (size_t)lt * P.s1,
-               S.cc + (size_t)lt * 2 * GG_NUM_CACHE_COUNTERS, P.s1, P.a1, P.log_line, P.pol1, 0, ln, {}, ~0u, 0, 0};
+               S.cc + (size_t)lt * 2 * GG_NUM_CACHE_COUNTERS, P.s1, P.a1, P.log_line, P.pol1, 0, ln, 0, ~0u, 0, 0};
     L2 = Cache{S.l2_tag + (size_t)lt * P.s2 * P.a2, S.l2_meta + (size_t)lt * P.s2 * P.a2, S.l2_rr + (size_t)lt * P.s2,
-               S.cc + ((size_t)lt * 2 + 1) * GG_NUM_CACHE_COUNTERS, P.s2, P.a2, P.log_line, P.pol2, 1, ln, {}, ~0u, 0, 0};
-#pragma unroll
-    for (int k = 0; k < GG_NUM_TILE_STATS; ++k) st[k] = 0;
+               S.cc + ((size_t)lt * 2 + 1) * GG_NUM_CACHE_COUNTERS, P.s2, P.a2, P.log_line, P.pol2, 1, ln, 0, ~0u, 0, 0};
+    sd = 0;
     rec = S.rec[lt]; rec_end = S.rec_end[lt]; clk = S.clk[lt]; pend_start = S.pend_start[lt];
     out_addr = S.out_addr[lt]; out_time = S.out_time[lt];
     blocked = S.blocked[lt]; seq = S.seq[lt]; nrep = S.nrep[lt]; nrq = S.nrq[lt];
@@ -369,6 +370,7 @@ struct Tile {
     ccv = ln < 2 * GG_NUM_CACHE_COUNTERS ? S.cc[(size_t)lt * 2 * GG_NUM_CACHE_COUNTERS + ln] : 0;
     stv = ln < GG_NUM_TILE_STATS ? S.st[(size_t)lt * GG_NUM_TILE_STATS + ln] : 0;
   }
+  __device__ __forceinline__ void stat(uint32_t k, uint64_t v) { if (ln == k) sd += v; }
   __device__ __forceinline__ void fail(uint32_t e = GG_DERR_STATE)
   {
     failed = true;
@@ -405,9 +407,8 @@ struct Tile {
   }
   __device__ __forceinline__ void count_sent(uint32_t type, uint64_t n)
   {
-    st[GG_CT_MSGS_SENT] += n;
-#pragma unroll
-    for (int k = 0; k < 11; ++k) if (type == (uint32_t)k + 1) st[GG_CT_SENT_BY_TYPE + k] += n;
+    stat(GG_CT_MSGS_SENT, n);
+    if (type - 1u < 11u) stat(GG_CT_SENT_BY_TYPE + type - 1u, n);
   }
   __device__ __forceinline__ void send(uint32_t dst, uint32_t type, uint32_t requester, uint64_t addr, uint64_t t)
   {
@@ -460,7 +461,7 @@ struct Tile {
   __device__ __forceinline__ int32_t dget(uint64_t a, uint64_t& t)
   {
     t += P.lat_dir;
-    st[GG_CT_DIR_ACCESSES]++;
+    stat(GG_CT_DIR_ACCESSES, 1);
     const uint32_t base = dset(a) * P.dassoc;
     DEnt* d = S.dir + (size_t)lt * P.E;
     const uint64_t v = ln < P.dassoc ? d[base + ln].addr : 0;
@@ -491,9 +492,9 @@ struct Tile {
     for (uint32_t w = 0; w < P.W; ++w) { sr[w] = so[w]; so[w] = 0; }
     d[slot] = DEnt{a, -1, DS_UNCACHED, 0};
     t += P.lat_dir;
-    st[GG_CT_DIR_ACCESSES]++;
-    st[GG_CT_DIR_EVICTIONS]++;
-    if (ent(-(int32_t)r - 1)->dstate != DS_UNCACHED) st[GG_CT_DIR_BACK_INVALIDATIONS]++;
+    stat(GG_CT_DIR_ACCESSES, 1);
+    stat(GG_CT_DIR_EVICTIONS, 1);
+    if (ent(-(int32_t)r - 1)->dstate != DS_UNCACHED) stat(GG_CT_DIR_BACK_INVALIDATIONS, 1);
     return slot;
   }
   // invalidateDirectoryEntry (directory_cache.cc:215-231): erase from the replaced list
@@ -595,19 +596,19 @@ struct Tile {
     if (P.dram_qm) {
       HTree tr{dq, dnd, P.dram_proc, P.analytical != 0};
       qd = tr.delay(pkt_ns, P.dram_proc, S.err);      // every lane, identical (LDS image or HBM)
-      st[GG_CT_DRAM_QUEUE_REQUESTS]++;
+      stat(GG_CT_DRAM_QUEUE_REQUESTS, 1);
     }
     const uint64_t lat = qd + P.dram_proc + P.dram_cost;
-    st[GG_CT_DRAM_ACCESSES]++;
-    st[GG_CT_DRAM_LATENCY_NS] += lat;
-    st[GG_CT_DRAM_QUEUE_DELAY_NS] += qd;
+    stat(GG_CT_DRAM_ACCESSES, 1);
+    stat(GG_CT_DRAM_LATENCY_NS, lat);
+    stat(GG_CT_DRAM_QUEUE_DELAY_NS, qd);
     return lat_to_ps(lat, 1.0);
   }
 
   // ---- DramDirectoryCntlr: the call chains as a work loop -------------------
   __device__ __forceinline__ void directory_run(Work w, uint64_t& t)
   {
-    Work stack[WSTACK];
+    Work* stack = sl.wstack;                 // LDS: every lane writes / reads the same entry
     int sp = 0;
     for (;;) {
       if (failed) return;
@@ -811,9 +812,9 @@ struct Tile {
     const uint64_t r = rec;
     const uint64_t lat = end - start;
     if (S.out) S.out[r] = (lat << 2) | level;
-    st[GG_CT_ACCESSES]++;
-    st[GG_CT_LATENCY_PS] += lat;
-    if (level == GG_LVL_L1) st[GG_CT_L1_HITS]++; else if (level == GG_LVL_L2) st[GG_CT_L2_HITS]++; else st[GG_CT_L2_MISSES]++;
+    stat(GG_CT_ACCESSES, 1);
+    stat(GG_CT_LATENCY_PS, lat);
+    if (level == GG_LVL_L1) stat(GG_CT_L1_HITS, 1); else if (level == GG_LVL_L2) stat(GG_CT_L2_HITS, 1); else stat(GG_CT_L2_MISSES, 1);
     clk = end;
     rec = r + 1;
   }
@@ -919,11 +920,12 @@ struct Tile {
   __device__ __forceinline__ void flush()
   {
     {
-      const uint32_t d = ln < GG_NUM_CACHE_COUNTERS ? pick(L1.c, ln) : pick(L2.c, ln - GG_NUM_CACHE_COUNTERS);
+      const uint32_t d2 = (uint32_t)__shfl((int)L2.cd, (int)((ln - GG_NUM_CACHE_COUNTERS) & 63u));
+      const uint32_t d = ln < GG_NUM_CACHE_COUNTERS ? L1.cd : d2;
       if (ln < 2 * GG_NUM_CACHE_COUNTERS && d) S.cc[(size_t)lt * 2 * GG_NUM_CACHE_COUNTERS + ln] = ccv + d;
     }
     {
-      const uint64_t d = pick(st, ln);
+      const uint64_t d = sd;
       uint64_t* g = S.st + (size_t)lt * GG_NUM_TILE_STATS;
       if (ln == GG_CT_CLOCK_PS) g[ln] = clk;
       else if (ln < GG_NUM_TILE_STATS && d) g[ln] = stv + d;
@@ -1043,6 +1045,18 @@ __device__ __forceinline__ void port_hop(const NocParams& np, HTree& tr, bool wa
   const uint64_t zps = lat_to_ps((uint64_t)np.router_delay + np.link_delay, np.f), cps = lat_to_ps(qd, np.f);
   t += zps + cps; zl += zps;
 }
+// the same with the counters lane-distributed: lane k of c holds counter k
+// (0-5 as above, 6 = buffer reads)
+__device__ __forceinline__ void port_hop_lane(const NocParams& np, HTree& tr, uint32_t nf, uint64_t& t, uint64_t& zl,
+                                              uint64_t& c, uint32_t* err, uint32_t ln)
+{
+  uint64_t qd = 0;
+  if (np.qm) qd = tr.delay(time_to_cycles(t, np.f), nf, err);
+  c += ln == 0 ? qd : ln == 1 ? (uint64_t)(np.qm != 0) : ln == 3 ? 1ull
+       : (ln == 2 || ln == 4 || ln == 5 || ln == 6) ? (uint64_t)nf : 0ull;
+  const uint64_t zps = lat_to_ps((uint64_t)np.router_delay + np.link_delay, np.f), cps = lat_to_ps(qd, np.f);
+  t += zps + cps; zl += zps;
+}
 __device__ __forceinline__ void net_ctr_add(uint64_t* ctr, uint32_t tile, const uint64_t* c)
 {
   cadd(ctr, tile, GG_NC_ROUTER_CONTENTION_CYCLES, c[0]); cadd(ctr, tile, GG_NC_ROUTER_PACKETS, c[1]);
@@ -1069,7 +1083,7 @@ __device__ __forceinline__ void import_one(const CP& P, const CS& S, const gg_cm
 // boundary records into the next quantum, and the last block to arrive picks
 // the next quantum as gg_coherent_run / oracle_coh_run do (empty quanta
 // skipped; blocked tiles with nothing in flight = deadlock).
-__device__ void quantum_end(const CP& P, const CS& S, uint32_t L, uint64_t q, uint64_t Q)
+__device__ __forceinline__ void quantum_end(const CP& P, const CS& S, uint32_t L, uint64_t q, uint64_t Q)
 {
   const uint32_t ln = threadIdx.x, lt = blockIdx.x;
   volatile uint64_t* qs = S.qs;
@@ -1146,8 +1160,9 @@ __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t L, uint32_t 
   Tile T(P, S, lt, p, sl);
   const gg_cmsg* prev = pool(S, p ^ 1u);     // records delivered to this step
   uint64_t* gscr = S.gscr + (size_t)lt * 5 * P.IC;
-  uint64_t nc_self[kNetCtr] = {0, 0, 0, 0, 0, 0, 0};
-  uint64_t rcv[5] = {0, 0, 0, 0, 0};          // packets, flits, bits received, latency, contention
+  // NoC counters of the SELF port (lanes 0-6, port_hop_lane) and of the receiver
+  // (lanes 8-12: packets, flits, bits received, latency, contention)
+  uint64_t ncd = 0;
 
   // ---- 0. hop-by-hop: SELF output port + receive of last step's packets (routePacket
   // at the receiver, hop_by_hop.cc:223-256; __processReceivedPacket, network_model.cc:118-150)
@@ -1178,11 +1193,11 @@ __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t L, uint32_t 
       const uint32_t bits = has_data(m->type) ? P.bits_data : P.bits_req;
       const uint32_t nf = (uint32_t)nflits(P.np, bits);
       uint64_t t = m->arrival_ps, zl = m->zero_load_ps;
-      port_hop(P.np, tr, wave, nf, t, zl, nc_self, S.err, ln);
+      port_hop_lane(P.np, tr, nf, t, zl, ncd, S.err, ln);
       const uint64_t ser = lat_to_ps(nf, P.np.f);
       t += ser; zl += ser;
       const uint64_t ct = t - m->send_ps - zl;
-      rcv[0] += 1; rcv[1] += nf; rcv[2] += bits; rcv[3] += zl + ct; rcv[4] += ct;
+      ncd += ln == 8 ? 1ull : ln == 9 ? (uint64_t)nf : ln == 10 ? (uint64_t)bits : ln == 11 ? zl + ct : ln == 12 ? ct : 0ull;
       m->arrival_ps = t; m->zero_load_ps = zl;
     }
     if (wave) { __syncthreads(); img_out(S.nq + qi, S.nnd + qi * P.np.max_size, sl.pimg, P.np.max_size, ln); }
@@ -1224,7 +1239,7 @@ __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t L, uint32_t 
     if (S.prof && ln == 0) atomicAdd(&S.prof[9], (unsigned long long)(_p1b - _p1));
     for (uint32_t j = 0; j < n && !T.failed; ++j) {
       const gg_cmsg m = prev[o_[j]];
-      T.st[GG_CT_MSGS_RECEIVED]++;
+      T.stat(GG_CT_MSGS_RECEIVED, 1);
       if (to_directory(m.type)) T.directory_msg(m); else T.l2_msg(m);
     }
   }
@@ -1378,11 +1393,13 @@ __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t L, uint32_t 
   T.flush();
   // NoC counters of the tile's own SELF port and receiver
   {
-    if (ln == 0 && na) {
-      net_ctr_add(S.ctr, T.tile, nc_self);
-      cadd(S.ctr, T.tile, GG_NC_PACKETS_RECEIVED, rcv[0]); cadd(S.ctr, T.tile, GG_NC_FLITS_RECEIVED, rcv[1]);
-      cadd(S.ctr, T.tile, GG_NC_BITS_RECEIVED, rcv[2]); cadd(S.ctr, T.tile, GG_NC_TOTAL_LATENCY_PS, rcv[3]);
-      cadd(S.ctr, T.tile, GG_NC_TOTAL_CONTENTION_PS, rcv[4]);
+    if (na) {
+      const int ci = ln == 0 ? GG_NC_ROUTER_CONTENTION_CYCLES : ln == 1 ? GG_NC_ROUTER_PACKETS
+                   : ln == 2 ? GG_NC_BUFFER_WRITES : ln == 3 ? GG_NC_SWITCH_ALLOC : ln == 4 ? GG_NC_CROSSBAR
+                   : ln == 5 ? GG_NC_LINK_TRAVERSALS : ln == 6 ? GG_NC_BUFFER_READS : ln == 8 ? GG_NC_PACKETS_RECEIVED
+                   : ln == 9 ? GG_NC_FLITS_RECEIVED : ln == 10 ? GG_NC_BITS_RECEIVED : ln == 11 ? GG_NC_TOTAL_LATENCY_PS
+                   : ln == 12 ? GG_NC_TOTAL_CONTENTION_PS : -1;
+      if (ci >= 0 && ncd) cadd(S.ctr, T.tile, (uint32_t)ci, ncd);
     }
   }
   {

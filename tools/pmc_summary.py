@@ -68,7 +68,7 @@ def main():
         kern[short(r["Name"])] = {"launches": int(r["Calls"]), "mean_ms": float(r["AverageNs"]) / 1e6,
                                   "total_pct": float(r["Percentage"])}
     pmc = collections.defaultdict(lambda: collections.defaultdict(list))
-    for p in ("fetch", "write", "sq", "sq2"):
+    for p in ("fetch", "write", "l2", "sq", "sq2"):
         try:
             rows = list(csv.DictReader(open("%s/%s/run_counter_collection.csv" % (pmc_dir, p))))
         except OSError:
