@@ -174,7 +174,8 @@ class Backend:
 
     def kernel_stats(self, name):
         """(total device ms, launches) of a coherent-mode kernel since the last
-        coherent begin (timing must be on): HIP events around every launch."""
+        coherent begin (timing must be on): HIP events around every 16th launch,
+        total = their mean x launches."""
         ms, n = ctypes.c_double(0), ctypes.c_uint64(0)
         _check(load().gg_kernel_stats(self.h, name.encode(), ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value

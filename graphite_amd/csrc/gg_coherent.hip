@@ -595,7 +595,7 @@ struct Tile {
     uint64_t qd = 0;
     if (P.dram_qm) {
       HTree tr{dq, dnd, P.dram_proc, P.analytical != 0};
-      qd = tr.delay(pkt_ns, P.dram_proc, S.err);      // every lane, identical (LDS image or HBM)
+      qd = dq_lds ? tr.delay_w(pkt_ns, P.dram_proc, S.err, ln) : tr.delay(pkt_ns, P.dram_proc, S.err);
       stat(GG_CT_DRAM_QUEUE_REQUESTS, 1);
     }
     const uint64_t lat = qd + P.dram_proc + P.dram_cost;
@@ -1038,7 +1038,7 @@ __device__ __forceinline__ void port_hop(const NocParams& np, HTree& tr, bool wa
   uint64_t qd = 0;
   if (np.qm) {
     const uint64_t tc = time_to_cycles(t, np.f);
-    qd = tr.delay(tc, nf, err);
+    qd = wave ? tr.delay_w(tc, nf, err, ln) : tr.delay(tc, nf, err);
     c[0] += qd; c[1] += 1;
   }
   c[2] += nf; c[3] += 1; c[4] += nf; c[5] += nf;
@@ -1047,11 +1047,11 @@ __device__ __forceinline__ void port_hop(const NocParams& np, HTree& tr, bool wa
 }
 // the same with the counters lane-distributed: lane k of c holds counter k
 // (0-5 as above, 6 = buffer reads)
-__device__ __forceinline__ void port_hop_lane(const NocParams& np, HTree& tr, uint32_t nf, uint64_t& t, uint64_t& zl,
-                                              uint64_t& c, uint32_t* err, uint32_t ln)
+__device__ __forceinline__ void port_hop_lane(const NocParams& np, HTree& tr, bool wave, uint32_t nf, uint64_t& t,
+                                              uint64_t& zl, uint64_t& c, uint32_t* err, uint32_t ln)
 {
   uint64_t qd = 0;
-  if (np.qm) qd = tr.delay(time_to_cycles(t, np.f), nf, err);
+  if (np.qm) qd = wave ? tr.delay_w(time_to_cycles(t, np.f), nf, err, ln) : tr.delay(time_to_cycles(t, np.f), nf, err);
   c += ln == 0 ? qd : ln == 1 ? (uint64_t)(np.qm != 0) : ln == 3 ? 1ull
        : (ln == 2 || ln == 4 || ln == 5 || ln == 6) ? (uint64_t)nf : 0ull;
   const uint64_t zps = lat_to_ps((uint64_t)np.router_delay + np.link_delay, np.f), cps = lat_to_ps(qd, np.f);
@@ -1193,7 +1193,7 @@ __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t L, uint32_t 
       const uint32_t bits = has_data(m->type) ? P.bits_data : P.bits_req;
       const uint32_t nf = (uint32_t)nflits(P.np, bits);
       uint64_t t = m->arrival_ps, zl = m->zero_load_ps;
-      port_hop_lane(P.np, tr, nf, t, zl, ncd, S.err, ln);
+      port_hop_lane(P.np, tr, wave, nf, t, zl, ncd, S.err, ln);
       const uint64_t ser = lat_to_ps(nf, P.np.f);
       t += ser; zl += ser;
       const uint64_t ct = t - m->send_ps - zl;
@@ -1357,7 +1357,7 @@ __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t L, uint32_t 
           uint64_t qd = 0;
           if (P.np.qm) {
             const uint64_t tc = time_to_cycles(g->send_ps, P.np.f);
-            qd = tr.delay(tc, nf, S.err);
+            qd = wave ? tr.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err);
           }
           g->arrival_ps = g->send_ps + lat_to_ps(0, P.np.f) + lat_to_ps(qd, P.np.f);
           g->zero_load_ps = 0;
@@ -1724,19 +1724,23 @@ struct gg_coh_state {
   uint64_t n_records = 0;
   size_t step_lds = 0, walk_lds = 0;
   bool begun = false;
-  // live kernel timing (gg_set_timing): an event pair around every launch,
-  // harvested at the batch syncs; totals since gg_coherent_begin
+  // live kernel timing (gg_set_timing): an event pair around every
+  // kTimeSample-th launch of each kernel (a pair around every launch costs
+  // ~18 % of a hop-by-hop run), harvested at the batch syncs; since
+  // gg_coherent_begin
   std::vector<hipEvent_t> tev;
   std::vector<int> tkind;
   uint32_t tused = 0;
   double ksum[3] = {0, 0, 0};
-  uint64_t kcnt[3] = {0, 0, 0};
+  uint64_t kcnt[3] = {0, 0, 0};      // timed launches
+  uint64_t nlaunch[3] = {0, 0, 0};   // all launches
 };
+constexpr uint64_t kTimeSample = 16;
 static const char* kKernelNames[3] = {"coherent_step", "coherent_walk_x", "coherent_walk_y"};
 
 template <class F> static void timed_launch(gg_ctx* ctx, gg_coh_state* C, hipStream_t s, int kind, F&& fn)
 {
-  if (!ctx->timing) { fn(); return; }
+  if (!ctx->timing || C->nlaunch[kind]++ % kTimeSample) { fn(); return; }
   if (C->tev.size() < 2 * (size_t)(C->tused + 1)) {
     const size_t n0 = C->tev.size();
     C->tev.resize(n0 + 512);
@@ -1764,7 +1768,11 @@ gg_status gg_coh_kernel_stats(gg_ctx* ctx, const char* name, double* total_ms, u
 {
   gg_coh_state* C = ctx->coh;
   for (int k = 0; k < 3; ++k)
-    if (C && std::strcmp(name, kKernelNames[k]) == 0) { *total_ms = C->ksum[k]; *launches = C->kcnt[k]; return GG_OK; }
+    if (C && std::strcmp(name, kKernelNames[k]) == 0) {
+      *total_ms = C->kcnt[k] ? C->ksum[k] / (double)C->kcnt[k] * (double)C->nlaunch[k] : 0.0;
+      *launches = C->nlaunch[k];
+      return GG_OK;
+    }
   *total_ms = 0; *launches = 0;
   return GG_ERR_INVALID;
 }
@@ -1997,7 +2005,7 @@ gg_status gg_coherent_begin(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_ou
   if (tr->num_records && (!tr->addr_dev || !tr->meta_dev)) return gg_fail(GG_ERR_INVALID, "NULL trace pointers");
   C->S.addr = tr->addr_dev; C->S.meta = tr->meta_dev; C->S.out = access_out_dev;
   C->n_records = tr->num_records;
-  for (int k = 0; k < 3; ++k) { C->ksum[k] = 0; C->kcnt[k] = 0; }
+  for (int k = 0; k < 3; ++k) { C->ksum[k] = 0; C->kcnt[k] = 0; C->nlaunch[k] = 0; }
   C->tused = 0;
   GG_HIP(hipMemcpyAsync(C->offs_dev, tr->tile_offsets, sizeof(uint64_t) * (P.T + 1), hipMemcpyHostToDevice, s));
   if (gg_status st = gg_noc_reset(ctx, s)) return st;

@@ -188,6 +188,89 @@ struct HTree {
     q->head = L.head; q->size = L.n;
     return qd;
   }
+  // ---- history_tree on a whole wave (every lane, identical arguments; the
+  // image in LDS, max_size <= 128): logical interval i in lane i & 63, slot
+  // i >> 6.  The same request as tree_delay: the search is two ballots, an
+  // insert / erase a shift of the lanes' registers, the write back one
+  // store round of the slots that changed (same circular layout) ----
+  __device__ __forceinline__ static uint64_t sh64(uint64_t v, uint32_t src) { return (uint64_t)__shfl((long long)v, (int)src); }
+  __device__ __forceinline__ static uint64_t rl64(uint64_t v, uint32_t l)
+  {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), (int)l) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
+  }
+  __device__ __forceinline__ uint64_t tree_delay_wave(uint64_t t, uint64_t p, uint32_t* err, uint32_t ln)
+  {
+    const uint32_t cap = q->max_size;
+    uint32_t head = q->head, n = q->size;
+    if (n >= cap) { head = head + 1 == cap ? 0u : head + 1; --n; }    // prune the min node (:52-56)
+    const bool two = cap > 64;
+    auto phys = [&](uint32_t i) { uint32_t j = head + i; if (j >= cap) j -= cap; if (j >= cap) j -= cap; return j; };
+    uint64_t a0 = 0, b0 = 0, a1 = 0, b1 = 0;
+    if (ln < n) { const HNode x = nd[phys(ln)]; a0 = x.first; b0 = x.second; }
+    if (two && ln + 64 < n) { const HNode x = nd[phys(ln + 64)]; a1 = x.first; b1 = x.second; }
+    uint64_t qd = 0;
+    uint32_t ch = n, nn = n;                       // first logical slot that changed, new size
+    if (analytical && rl64(a0, 0) > t + p) {
+      q->analytical++;
+      qd = mg1_delay();
+    } else {
+      // first fit: j = the last interval starting at or before t
+      const bool v0 = ln < n, v1 = ln + 64 < n;
+      const uint32_t cnt = (uint32_t)__builtin_popcountll(__ballot(v0 && a0 <= t)) +
+                           (uint32_t)__builtin_popcountll(__ballot(v1 && a1 <= t));
+      int i = -1;
+      if (cnt > 0) {
+        const uint32_t j = cnt - 1;
+        const uint64_t bj = j < 64 ? rl64(b0, j) : rl64(b1, j - 64);
+        if (t + p <= bj) i = (int)j;
+      }
+      if (i < 0) {
+        const uint64_t m0 = __ballot(v0 && ln >= cnt && b0 - a0 >= p);
+        const uint64_t m1 = __ballot(v1 && ln + 64 >= cnt && b1 - a1 >= p);
+        i = m0 ? (int)__builtin_ctzll(m0) : (m1 ? 64 + (int)__builtin_ctzll(m1) : -1);
+      }
+      if (i < 0) {
+        if (ln == 0) atomicOr(err, GG_DERR_STATE);
+      } else {
+        const uint32_t ui = (uint32_t)i;
+        const uint64_t a = ui < 64 ? rl64(a0, ui) : rl64(a1, ui - 64);
+        const uint64_t b = ui < 64 ? rl64(b0, ui) : rl64(b1, ui - 64);
+        uint64_t na = a, nb = b;                    // new interval ui (if it stays)
+        int op = 0;                                 // 0 modify, 1 insert (t + p, b) after ui, 2 erase ui
+        if (t >= a) {
+          if ((t - a) >= min_proc) { nb = t; if ((b - (t + p)) >= min_proc) op = 1; }
+          else if ((b - (t + p)) >= min_proc) na = t + p;
+          else op = 2;
+        } else {
+          qd = a - t;
+          if ((b - (a + p)) >= min_proc) na = a + p; else op = 2;
+        }
+        ch = ui;
+        if (op == 1) {                              // new(k) = old(k - 1) for k > ui + 1
+          const uint32_t s = (ln + 63) & 63;
+          const uint64_t pa0 = sh64(a0, s), pb0 = sh64(b0, s), pa1 = sh64(a1, s), pb1 = sh64(b1, s);
+          if (ln > ui + 1) { a0 = pa0; b0 = pb0; }
+          if (ln + 64 > ui + 1) { a1 = ln == 0 ? pa0 : pa1; b1 = ln == 0 ? pb0 : pb1; }
+          const uint32_t k = ui + 1;
+          if ((k & 63) == ln) { if (k < 64) { a0 = t + p; b0 = b; } else { a1 = t + p; b1 = b; } }
+          nn = n + 1;
+        } else if (op == 2) {                       // new(k) = old(k + 1) for k >= ui
+          const uint32_t s = (ln + 1) & 63;
+          const uint64_t na0 = sh64(a0, s), nb0 = sh64(b0, s), na1 = sh64(a1, s), nb1 = sh64(b1, s);
+          if (ln >= ui) { a0 = ln == 63 ? na1 : na0; b0 = ln == 63 ? nb1 : nb0; }
+          if (ln + 64 >= ui) { a1 = na1; b1 = nb1; }
+          nn = n - 1;
+        }
+        if (op != 2 && (ui & 63) == ln) { if (ui < 64) { a0 = na; b0 = nb; } else { a1 = na; b1 = nb; } }
+      }
+    }
+    if (ln >= ch && ln < nn) nd[phys(ln)] = HNode{a0, b0};
+    if (two && ln + 64 >= ch && ln + 64 < nn) nd[phys(ln + 64)] = HNode{a1, b1};
+    q->head = head; q->size = nn;
+    wave_sync();
+    return qd;
+  }
   // replace interval i by up to two intervals (in list order).  The list may
   // overgrow by one only here, and then loses its front (the size check after
   // the scan, queue_model_history_list.cc:128-131): done in place.
@@ -277,6 +360,15 @@ struct HTree {
     } else {
       qd = tree_delay(t, p, err);
     }
+    mg1_update(t, p, qd);
+    return qd;
+  }
+  // computeQueueDelay on a whole wave (every lane, identical arguments, the
+  // queue image in LDS): history_tree lane-parallel, the others as delay()
+  __device__ __forceinline__ uint64_t delay_w(uint64_t t, uint64_t p, uint32_t* err, uint32_t ln)
+  {
+    if (q->type != GG_QM_HISTORY_TREE || q->max_size > 128) return delay(t, p, err);
+    const uint64_t qd = tree_delay_wave(t, p, err, ln);
     mg1_update(t, p, qd);
     return qd;
   }

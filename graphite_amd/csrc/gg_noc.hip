@@ -579,13 +579,51 @@ __global__ void k_htree_reset(HQueue* q, HNode* nd, uint64_t nq, uint32_t max_si
 
 // processing times of 0 are outside the reference's call sites (flits >= 1,
 // DRAM 13) and outside the interval argument of gg_dev.h: rejected
-__global__ void k_htree_seq(HQueue* q, HNode* nd, uint64_t min_proc, uint32_t analytical,
-                            const uint64_t* t, const uint64_t* p, uint64_t n, uint64_t* d, uint32_t* err)
+// One wave: the queue image in LDS and every request on the whole wave
+// (HTree::delay_w, the path of the coherent walkers); one lane on the HBM
+// image beyond 128 slots.
+__global__ void __launch_bounds__(64) k_htree_seq(HQueue* q, HNode* nd, uint64_t min_proc, uint32_t analytical,
+                                                  const uint64_t* t, const uint64_t* p, uint64_t n, uint64_t* d,
+                                                  uint32_t* err)
 {
-  HTree tr{q, nd, min_proc, analytical != 0};
-  for (uint64_t i = 0; i < n; ++i) {
-    if (p[i] == 0) { atomicOr(err, GG_DERR_RANGE); d[i] = 0; continue; }
-    d[i] = tr.delay(t[i], p[i], err);
+  __shared__ __attribute__((aligned(16))) uint8_t img[sizeof(HQueue) + 128 * sizeof(HNode)];
+  const uint32_t ln = threadIdx.x, ms = q->max_size;
+  if (ms > 128) {
+    if (ln != 0) return;
+    HTree tr{q, nd, min_proc, analytical != 0};
+    for (uint64_t i = 0; i < n; ++i) {
+      if (p[i] == 0) { atomicOr(err, GG_DERR_RANGE); d[i] = 0; continue; }
+      d[i] = tr.delay(t[i], p[i], err);
+    }
+    return;
+  }
+  HQueue* lq = reinterpret_cast<HQueue*>(img);
+  HNode* lnd = reinterpret_cast<HNode*>(img + sizeof(HQueue));
+  for (uint32_t w = ln; w < sizeof(HQueue) / 16 + ms; w += 64)
+    reinterpret_cast<uint4*>(img)[w] = w < sizeof(HQueue) / 16 ? reinterpret_cast<const uint4*>(q)[w]
+                                                              : reinterpret_cast<const uint4*>(nd)[w - sizeof(HQueue) / 16];
+  __syncthreads();
+  HTree tr{lq, lnd, min_proc, analytical != 0};
+  __shared__ uint64_t ct[512], cp[512], cd[512];          // requests staged 512 at a time
+  for (uint64_t b = 0; b < n; b += 512) {
+    const uint32_t m = (uint32_t)min<uint64_t>(512, n - b);
+    for (uint32_t k = ln; k < m; k += 64) { ct[k] = t[b + k]; cp[k] = p[b + k]; }
+    __syncthreads();
+    for (uint32_t k = 0; k < m; ++k) {
+      const uint64_t ti = ct[k], pi = cp[k];
+      uint64_t r = 0;
+      if (pi == 0) { if (ln == 0) atomicOr(err, GG_DERR_RANGE); }
+      else r = tr.delay_w(ti, pi, err, ln);
+      cd[k] = r;
+    }
+    __syncthreads();
+    for (uint32_t k = ln; k < m; k += 64) d[b + k] = cd[k];
+    __syncthreads();
+  }
+  for (uint32_t w = ln; w < sizeof(HQueue) / 16 + ms; w += 64) {
+    const uint4 v = reinterpret_cast<const uint4*>(img)[w];
+    if (w < sizeof(HQueue) / 16) reinterpret_cast<uint4*>(q)[w] = v;
+    else reinterpret_cast<uint4*>(nd)[w - sizeof(HQueue) / 16] = v;
   }
 }
 
@@ -803,7 +841,7 @@ gg_status gg_htree_run(gg_ctx* ctx, uint64_t min_proc, const uint64_t* t, const 
   GG_HIP(hipMalloc((void**)&buf, 24 * (n ? n : 1)));
   GG_HIP(hipMemcpyAsync(buf, t, 8 * n, hipMemcpyHostToDevice, s));
   GG_HIP(hipMemcpyAsync(buf + n, p, 8 * n, hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(k_htree_seq, dim3(1), dim3(1), 0, s, S->q + qi, S->nd + qi * S->P.max_size,
+  hipLaunchKernelGGL(k_htree_seq, dim3(1), dim3(64), 0, s, S->q + qi, S->nd + qi * S->P.max_size,
                      min_proc, S->P.analytical, buf, buf + n, n, buf + 2 * n, ctx->err_dev);
   GG_HIP(hipGetLastError());
   GG_HIP(hipMemcpyAsync(d, buf + 2 * n, 8 * n, hipMemcpyDeviceToHost, s));

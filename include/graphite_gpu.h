@@ -410,9 +410,10 @@ gg_status gg_gen_hotspot_trace(uint64_t* addr_dev, uint32_t* meta_dev, uint32_t 
  * events on the stream the kernel ran on; negative if not launched.           */
 float     gg_kernel_time_ms(gg_ctx* ctx, const char* kernel);
 void      gg_set_timing(gg_ctx* ctx, int enabled);
-/* With timing on, every launch of the coherent mode's kernels is bracketed by
- * HIP events on its stream: total device time and launch count since the last
- * gg_coherent_begin of "coherent_step", "coherent_walk_x", "coherent_walk_y". */
+/* With timing on, every 16th launch of each coherent-mode kernel is bracketed
+ * by HIP events on its stream: launches since the last gg_coherent_begin of
+ * "coherent_step", "coherent_walk_x", "coherent_walk_y", and their total
+ * device time estimated as (mean of the timed launches) x launches.        */
 gg_status gg_kernel_stats(gg_ctx* ctx, const char* kernel, double* total_ms, uint64_t* launches);
 
 #ifdef __cplusplus

@@ -30,6 +30,39 @@ def test_history_tree_fixtures_on_gpu(name):
     np.testing.assert_array_equal(be.queue_delay_batch(rows[:, 0], rows[:, 1]), rows[:, 2])
 
 
+@pytest.mark.parametrize("max_size", [2, 7, 64, 65, 100, 128, 129])
+@pytest.mark.parametrize("analytical", [0, 1])
+def test_history_tree_wave_op_matches_avl_on_random_streams(max_size, analytical):
+    """gg_queue_delay_batch runs every request on a whole wave over an LDS image
+    (HTree::delay_w, the coherent walkers' path; the one-lane HBM path beyond
+    128 slots): delays equal the oracle's AVL restatement on request streams
+    with backward jumps (mid-list inserts / erases, prunes, the M/G/1 branch)."""
+    import ctypes
+    torch_dev()
+    L = po.lib()
+    L.oracle_htree_create.restype = ctypes.c_void_p
+    L.oracle_htree_create.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
+    L.oracle_htree_delay.restype = ctypes.c_uint64
+    L.oracle_htree_delay.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64]
+    L.oracle_htree_destroy.argtypes = [ctypes.c_void_p]
+    rng = np.random.default_rng(max_size * 2 + analytical)
+    for min_proc in (1, 3, 13):
+        n = 3000
+        base, span, maxp, jump = 0, int(rng.integers(50, 4000)), int(rng.integers(min_proc, 40)), int(rng.integers(1, 30))
+        t = np.zeros(n, np.uint64)
+        p = rng.integers(1, maxp + 1, n).astype(np.uint64)
+        for i in range(n):
+            base += int(rng.integers(0, jump))
+            t[i] = base - int(rng.integers(0, span)) if (rng.random() < 0.3 and base > span) else base
+        be = B.Backend(C.default_config(4, max_list_size=max_size, analytical_enabled=analytical))
+        got = be.queue_delay_batch(t, p, min_processing_time=min_proc)
+        h = L.oracle_htree_create(min_proc, max_size, analytical)
+        ref = np.array([L.oracle_htree_delay(h, int(a), int(b)) for a, b in zip(t, p)], np.uint64)
+        L.oracle_htree_destroy(h)
+        np.testing.assert_array_equal(got, ref, err_msg="min_proc %d" % min_proc)
+        be.close()
+
+
 def packets(T, n, seed, span_ps, self_frac=0.05):
     rng = np.random.default_rng(seed)
     src = rng.integers(0, T, n).astype(np.uint32)

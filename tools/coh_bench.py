@@ -21,12 +21,14 @@ def main():
     net = C.NET_EMESH_HOP_BY_HOP if "--hbh" in sys.argv else C.NET_EMESH_HOP_COUNTER
     cfg = C.default_config(T, num_shards=K, net_model=net)
     be = B.Backend(cfg)
-    be.set_timing(True)
+    be.set_timing("--no-timing" not in sys.argv)
     addr = torch.empty(T * N, dtype=torch.int64, device="cuda")
     meta = torch.empty(T * N, dtype=torch.int32, device="cuda")
     out = torch.zeros(T * N, dtype=torch.int64, device="cuda")
     B.gen_hotspot_trace(addr, meta, 0, T, N, hot_lines=hot)
     offs = np.arange(T + 1, dtype=np.uint64) * np.uint64(N)
+    if "--warm" in sys.argv:
+        be.coherent_run(addr, meta, offs, out)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     be.coherent_run(addr, meta, offs, out)
