@@ -101,6 +101,7 @@ struct CP {
   uint32_t bits_req, bits_data, max_list, analytical, dram_qm, dram_qtype, dram_qaux;
   uint32_t net, nsx, nsy, mw, mh, qimg;  // network model; X / Y segments; mesh; bytes of a queue image
   uint32_t msg_cap, seg_cap, walk_pk;    // pool records per parity; entries per segment list; walker LDS packets
+  uint32_t seg_xcd;                      // > 0: runs interleaved by shard (seg_xcd shards), XCD-grouped walker blocks
   uint64_t lat_l1d, lat_l1t, lat_l2d, lat_l2t, lat_dir, gap_ps, dram_proc, dram_cost;
   NocParams np;
 };
@@ -152,6 +153,12 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v)
+{
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += (uint64_t)__shfl_xor((long long)v, o);
   return v;
 }
 __device__ __forceinline__ uint32_t wave_min(uint32_t v)
@@ -1029,34 +1036,11 @@ __device__ __forceinline__ void img_out(HQueue* q, HNode* nd, uint8_t* img, uint
   imgs_copy<false>(img, 0, 1, [](uint32_t) { return (uint64_t)0; }, q, nd, ms, ln);
 }
 
-// one router output port + link (RouterModel::processPacket router_model.cc:71-108,
-// ElectricalLinkModel::processPacket electrical_link_model.cc:31-45) on a wave:
-// counters into c[kNetCtr] = {contention, router packets, buffer w+r (each), switch, crossbar, link}
-__device__ __forceinline__ void port_hop(const NocParams& np, HTree& tr, bool wave, uint32_t nf, uint64_t& t,
-                                         uint64_t& zl, uint64_t* c, uint32_t* err, uint32_t ln)
-{
-  uint64_t qd = 0;
-  if (np.qm) {
-    const uint64_t tc = time_to_cycles(t, np.f);
-    qd = wave ? tr.delay_w(tc, nf, err, ln) : tr.delay(tc, nf, err);
-    c[0] += qd; c[1] += 1;
-  }
-  c[2] += nf; c[3] += 1; c[4] += nf; c[5] += nf;
-  const uint64_t zps = lat_to_ps((uint64_t)np.router_delay + np.link_delay, np.f), cps = lat_to_ps(qd, np.f);
-  t += zps + cps; zl += zps;
-}
-// the same with the counters lane-distributed: lane k of c holds counter k
-// (0-5 as above, 6 = buffer reads)
-__device__ __forceinline__ void port_hop_lane(const NocParams& np, HTree& tr, bool wave, uint32_t nf, uint64_t& t,
-                                              uint64_t& zl, uint64_t& c, uint32_t* err, uint32_t ln)
-{
-  uint64_t qd = 0;
-  if (np.qm) qd = wave ? tr.delay_w(time_to_cycles(t, np.f), nf, err, ln) : tr.delay(time_to_cycles(t, np.f), nf, err);
-  c += ln == 0 ? qd : ln == 1 ? (uint64_t)(np.qm != 0) : ln == 3 ? 1ull
-       : (ln == 2 || ln == 4 || ln == 5 || ln == 6) ? (uint64_t)nf : 0ull;
-  const uint64_t zps = lat_to_ps((uint64_t)np.router_delay + np.link_delay, np.f), cps = lat_to_ps(qd, np.f);
-  t += zps + cps; zl += zps;
-}
+// A router output port + link (RouterModel::processPacket router_model.cc:71-108,
+// ElectricalLinkModel::processPacket electrical_link_model.cc:31-45): the
+// port's queue delay, then router + link delay (zero-load part) and the
+// counters {contention, router packets, buffer w+r (each), switch, crossbar,
+// link}; done batch-wise by the walkers and k_c_step's SELF / injection ports.
 __device__ __forceinline__ void net_ctr_add(uint64_t* ctr, uint32_t tile, const uint64_t* c)
 {
   cadd(ctr, tile, GG_NC_ROUTER_CONTENTION_CYCLES, c[0]); cadd(ctr, tile, GG_NC_ROUTER_PACKETS, c[1]);
@@ -1160,7 +1144,7 @@ __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t L, uint32_t 
   Tile T(P, S, lt, p, sl);
   const gg_cmsg* prev = pool(S, p ^ 1u);     // records delivered to this step
   uint64_t* gscr = S.gscr + (size_t)lt * 5 * P.IC;
-  // NoC counters of the SELF port (lanes 0-6, port_hop_lane) and of the receiver
+  // NoC counters of the SELF port (lanes 0-6) and of the receiver
   // (lanes 8-12: packets, flits, bits received, latency, contention)
   uint64_t ncd = 0;
 
@@ -1180,27 +1164,61 @@ __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t L, uint32_t 
     __syncthreads();
     order_port(na, t_, s_, k_, i_, o_, ln);
     const uint64_t qi = (uint64_t)T.tile * 6 + P_SELF;
-    HTree tr{S.nq + qi, S.nnd + qi * P.np.max_size, 1, P.np.analytical != 0};
-    const bool wave = P.np.qm && P.np.max_size <= kQMax;
+    HQueue* gq = S.nq + qi;
+    HNode* gnd = S.nnd + qi * P.np.max_size;
+    // the port's queue in registers for the batch (RegQueue); other models on an LDS image
+    const bool regq = P.np.qm && P.np.qtype == GG_QM_HISTORY_TREE && P.np.max_size <= kQMax;
+    const bool wave = P.np.qm && P.np.max_size <= kQMax && !regq;
+    HTree tr{gq, gnd, 1, P.np.analytical != 0};
     if (wave) {
-      img_in(sl.pimg, S.nq + qi, S.nnd + qi * P.np.max_size, P.np.max_size, ln);
+      img_in(sl.pimg, gq, gnd, P.np.max_size, ln);
       __syncthreads();
       tr.q = reinterpret_cast<HQueue*>(sl.pimg); tr.nd = reinterpret_cast<HNode*>(sl.pimg + sizeof(HQueue));
     }
-    for (uint32_t j = 0; j < na; ++j) {
-      const uint32_t r = o_[j];
-      gg_cmsg* m = const_cast<gg_cmsg*>(prev) + r;
-      const uint32_t bits = has_data(m->type) ? P.bits_data : P.bits_req;
-      const uint32_t nf = (uint32_t)nflits(P.np, bits);
-      uint64_t t = m->arrival_ps, zl = m->zero_load_ps;
-      port_hop_lane(P.np, tr, wave, nf, t, zl, ncd, S.err, ln);
-      const uint64_t ser = lat_to_ps(nf, P.np.f);
-      t += ser; zl += ser;
-      const uint64_t ct = t - m->send_ps - zl;
-      ncd += ln == 8 ? 1ull : ln == 9 ? (uint64_t)nf : ln == 10 ? (uint64_t)bits : ln == 11 ? zl + ct : ln == 12 ? ct : 0ull;
-      m->arrival_ps = t; m->zero_load_ps = zl;
+    RegQueue rq;
+    if (regq) rq.load(gq, gnd, 1, P.np.analytical != 0, ln);
+    const uint64_t zps = lat_to_ps((uint64_t)P.np.router_delay + P.np.link_delay, P.np.f);
+    uint64_t cq = 0, cf = 0;                                   // uniform: contention cycles, flits
+    uint64_t rf = 0, rb = 0, rl = 0, rc = 0, rn = 0;           // this lane's packets: flits, bits, latency, contention
+    gg_cmsg* pv = const_cast<gg_cmsg*>(prev);
+    for (uint32_t c0 = 0; c0 < na; c0 += 64) {
+      const uint32_t cnt = min(64u, na - c0);
+      uint32_t r = 0, nf_ = 0, bits = 0;
+      uint64_t t_ = 0, z_ = 0, sp = 0;
+      if (ln < cnt) {
+        r = o_[c0 + ln];
+        const gg_cmsg& g = pv[r];
+        t_ = g.arrival_ps; z_ = g.zero_load_ps; sp = g.send_ps;
+        bits = has_data(g.type) ? P.bits_data : P.bits_req;
+        nf_ = (uint32_t)nflits(P.np, bits);
+      }
+      uint64_t ot = t_;
+      for (uint32_t k = 0; k < cnt; ++k) {
+        const uint64_t t = rl64(t_, k);
+        const uint32_t nf = (uint32_t)__builtin_amdgcn_readlane((int)nf_, (int)k);
+        uint64_t qd = 0;
+        if (P.np.qm) {
+          const uint64_t tc = time_to_cycles(t, P.np.f);
+          qd = regq ? rq.request(tc, nf, S.err) : (wave ? tr.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
+        }
+        cq += qd; cf += nf;
+        if (ln == k) ot = t + zps + lat_to_ps(qd, P.np.f);
+      }
+      if (ln < cnt) {                                           // serialization + receive (network_model.cc:118-150)
+        const uint64_t ser = lat_to_ps(nf_, P.np.f);
+        const uint64_t t2 = ot + ser, z2 = z_ + zps + ser;
+        const uint64_t ct = t2 - sp - z2;
+        pv[r].arrival_ps = t2; pv[r].zero_load_ps = z2;
+        rn += 1; rf += nf_; rb += bits; rl += z2 + ct; rc += ct;
+      }
     }
-    if (wave) { __syncthreads(); img_out(S.nq + qi, S.nnd + qi * P.np.max_size, sl.pimg, P.np.max_size, ln); }
+    if (regq) rq.store(gq, gnd);
+    if (wave) { __syncthreads(); img_out(gq, gnd, sl.pimg, P.np.max_size, ln); }
+    rn = wave_sum64(rn); rf = wave_sum64(rf); rb = wave_sum64(rb); rl = wave_sum64(rl); rc = wave_sum64(rc);
+    // lanes 0-6: the SELF port (contention, router packets, buffer writes, switch, crossbar, link, buffer reads), 8-12: the receiver
+    ncd = ln == 0 ? (P.np.qm ? cq : 0ull) : ln == 1 ? (P.np.qm ? (uint64_t)na : 0ull) : ln == 3 ? (uint64_t)na
+        : (ln == 2 || ln == 4 || ln == 5 || ln == 6) ? cf : ln == 8 ? rn : ln == 9 ? rf : ln == 10 ? rb
+        : ln == 11 ? rl : ln == 12 ? rc : 0ull;
     narv(S, p)[lt] = 0;
     __syncthreads();
   }
@@ -1340,30 +1358,51 @@ __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t L, uint32_t 
         __syncthreads();
         order_port(nn, t_, s_, k_, i_, o_, ln);
         const uint64_t qi = (uint64_t)T.tile * 6 + P_INJ;
-        HTree tr{S.nq + qi, S.nnd + qi * P.np.max_size, 1, P.np.analytical != 0};
-        const bool wave = P.np.qm && P.np.max_size <= kQMax;
+        HQueue* gq = S.nq + qi;
+        HNode* gnd = S.nnd + qi * P.np.max_size;
+        const bool regq = P.np.qm && P.np.qtype == GG_QM_HISTORY_TREE && P.np.max_size <= kQMax;
+        const bool wave = P.np.qm && P.np.max_size <= kQMax && !regq;
+        HTree tr{gq, gnd, 1, P.np.analytical != 0};
         if (wave) {
-          img_in(sl.pimg, S.nq + qi, S.nnd + qi * P.np.max_size, P.np.max_size, ln);
+          img_in(sl.pimg, gq, gnd, P.np.max_size, ln);
           __syncthreads();
           tr.q = reinterpret_cast<HQueue*>(sl.pimg); tr.nd = reinterpret_cast<HNode*>(sl.pimg + sizeof(HQueue));
         }
+        RegQueue rq;
+        if (regq) rq.load(gq, gnd, 1, P.np.analytical != 0, ln);
         uint64_t ps = 0, fs = 0, bs = 0;
-        for (uint32_t j = 0; j < nn; ++j) {
-          const uint32_t r = o_[j];
-          gg_cmsg* g = cur + r;
-          const uint32_t bits = has_data(g->type) ? P.bits_data : P.bits_req;
-          const uint64_t nf = nflits(P.np, bits);
-          ps += 1; fs += nf; bs += bits;                               // updateSendCounters (network_model.cc:228-251)
-          uint64_t qd = 0;
-          if (P.np.qm) {
-            const uint64_t tc = time_to_cycles(g->send_ps, P.np.f);
-            qd = wave ? tr.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err);
+        for (uint32_t c0 = 0; c0 < nn; c0 += 64) {
+          const uint32_t cnt = min(64u, nn - c0);
+          uint32_t r = 0, nf_ = 0, bits = 0;
+          uint64_t sp = 0;
+          if (ln < cnt) {
+            r = o_[c0 + ln];
+            const gg_cmsg& g = cur[r];
+            sp = g.send_ps;
+            bits = has_data(g.type) ? P.bits_data : P.bits_req;
+            nf_ = (uint32_t)nflits(P.np, bits);
           }
-          g->arrival_ps = g->send_ps + lat_to_ps(0, P.np.f) + lat_to_ps(qd, P.np.f);
-          g->zero_load_ps = 0;
-          g->hop = T.tile;
+          uint64_t oq = 0;
+          for (uint32_t k = 0; k < cnt; ++k) {
+            const uint32_t nf = (uint32_t)__builtin_amdgcn_readlane((int)nf_, (int)k);
+            uint64_t qd = 0;
+            if (P.np.qm) {
+              const uint64_t tc = time_to_cycles(rl64(sp, k), P.np.f);
+              qd = regq ? rq.request(tc, nf, S.err) : (wave ? tr.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
+            }
+            if (ln == k) oq = qd;
+          }
+          if (ln < cnt) {                                       // updateSendCounters (network_model.cc:228-251)
+            gg_cmsg* g = cur + r;
+            g->arrival_ps = sp + lat_to_ps(0, P.np.f) + lat_to_ps(oq, P.np.f);
+            g->zero_load_ps = 0;
+            g->hop = T.tile;
+            ps += 1; fs += nf_; bs += bits;
+          }
         }
-        if (wave) { __syncthreads(); img_out(S.nq + qi, S.nnd + qi * P.np.max_size, sl.pimg, P.np.max_size, ln); }
+        if (regq) rq.store(gq, gnd);
+        if (wave) { __syncthreads(); img_out(gq, gnd, sl.pimg, P.np.max_size, ln); }
+        ps = wave_sum64(ps); fs = wave_sum64(fs); bs = wave_sum64(bs);
         if (ln == 0) {
           cadd(S.ctr, T.tile, GG_NC_PACKETS_SENT, ps); cadd(S.ctr, T.tile, GG_NC_FLITS_SENT, fs);
           cadd(S.ctr, T.tile, GG_NC_BITS_SENT, bs);
@@ -1427,7 +1466,15 @@ __global__ void __launch_bounds__(64) k_c_walk(CP P, CS S, uint32_t L, int stage
 {
   const uint32_t live = ((volatile uint32_t*)S.live)[L & 3];
   if (!live) return;                                 // launch L was no step
-  const uint32_t ln = threadIdx.x, sg = blockIdx.x, p = (live - 1) & 1u;
+  // block -> (run slot, direction): with runs interleaved by shard, block b
+  // takes slot (b mod ns) + ns * (b div 2ns) in direction (b div ns) & 1, so
+  // every block of shard k is k mod ns (the XCD of its tiles' blocks)
+  uint32_t sg = blockIdx.x;
+  if (P.seg_xcd) {
+    const uint32_t ns = P.seg_xcd, b = blockIdx.x;
+    sg = 2 * ((b % ns) + ns * (b / (2 * ns))) + ((b / ns) & 1u);
+  }
+  const uint32_t ln = threadIdx.x, p = (live - 1) & 1u;
   PROF_T0();
   uint32_t* cntp = (stage == 0 ? S.nxl : S.nyl) + sg;
   const uint32_t n0 = *cntp;
@@ -1458,6 +1505,7 @@ __global__ void __launch_bounds__(64) k_c_walk(CP P, CS S, uint32_t L, int stage
     const gg_cmsg& m = cur[r];
     Pt[i] = m.arrival_ps; Ph[i] = m.send_ps; Pk[i] = ((uint64_t)m.src << 32) | m.seq; Pz[i] = m.zero_load_ps;
     Pi[i] = r; Pp[i] = pos_of(m.hop); Pd[i] = pos_of(m.dst);
+    if (m.arrival_ps >> 51) atomicOr(S.err, GG_DERR_CAP);        // batch keys are time << 12 | rank
     Pf[i] = (uint32_t)nflits(P.np, has_data(m.type) ? P.bits_data : P.bits_req);
   }
   for (uint32_t i = ln; i < npos * kNetCtr; i += 64) lc[i] = 0;
@@ -1470,13 +1518,6 @@ __global__ void __launch_bounds__(64) k_c_walk(CP P, CS S, uint32_t L, int stage
     Pr[i] = r;
   }
   __syncthreads();
-  for (uint32_t i = ln; i < n; i += 64) {
-    const uint64_t ti = Pt[i];
-    const uint32_t ri = Pr[i];
-    uint32_t r = 0;
-    for (uint32_t j = 0; j < n; ++j) { const uint64_t tj = Pt[j]; r += tj < ti || (tj == ti && Pr[j] < ri); }
-    Qt[r] = ti; Qr[r] = ri; Qs[r] = i;
-  }
   // the queues of the positions the packets can visit
   uint32_t lo = ~0u, hi = 0;
   for (uint32_t i = ln; i < n; i += 64) {
@@ -1493,51 +1534,92 @@ __global__ void __launch_bounds__(64) k_c_walk(CP P, CS S, uint32_t L, int stage
   __syncthreads();
   PROF_AT(_w1);
   uint32_t nev = 0;
-  // events in (time, send time, sender << 32 | seq) order: the head of the
-  // sorted queue [qh, n); a packet that stays in the segment goes back in at
-  // its new time (lanes count the smaller keys by ballot and shift them down)
+  // Position sweep.  In a run the packets move one way, so the requests a
+  // port sees depend only on the ports before it: serving the positions in
+  // the direction of travel, each port's batch in (time, rank) order, is the
+  // (time, rank) event order of the whole run at every port.  Each batch runs
+  // through the port's queue held in the wave's registers (RegQueue), the
+  // batch's fields in lanes (readlane per request).
+  const bool regq = qm && P.np.qtype == GG_QM_HISTORY_TREE && P.np.max_size <= kQMax;
   const bool wave_q = P.np.max_size <= kQMax;
-  for (uint32_t qh = 0; qh < n;) {
-    const uint32_t i = Qs[qh], ri = Qr[qh];
-    ++nev;
-    const uint32_t c = Pp[i], d = Pd[i], nf = Pf[i] & 0xFFFFFFu;
-    uint64_t t = Pt[i], zl = Pz[i];
-    HTree tr{reinterpret_cast<HQueue*>(qimg + (size_t)(c - sd.lo) * P.qimg),
-             reinterpret_cast<HNode*>(qimg + (size_t)(c - sd.lo) * P.qimg + sizeof(HQueue)), 1, P.np.analytical != 0};
-    uint64_t cc[kNetCtr] = {0, 0, 0, 0, 0, 0, 0};
-    port_hop(P.np, tr, wave_q, nf, t, zl, cc, S.err, ln);
-    const uint32_t nx = dir ? c + 1 : c - 1;
-    uint32_t status = 0;
-    if (nx < sd.lo || nx > sd.hi) status = 2;                  // next router in another shard: held
-    else if (nx == d) status = 1;                              // leaves the chain: next stage
-    if (ln == 0) {
-      Pt[i] = t; Pz[i] = zl; Pp[i] = nx; Pf[i] = nf | (status << 24);
-      uint64_t* l = lc + (size_t)(c - sd.lo) * kNetCtr;
-#pragma unroll
-      for (int q = 0; q < (int)kNetCtr; ++q) l[q] += cc[q];
+  const uint64_t zps = lat_to_ps((uint64_t)P.np.router_delay + P.np.link_delay, P.np.f);
+  uint64_t* K = Qt; uint32_t* B = Qr; uint32_t* O = Qs;           // batch keys, batch, batch in order
+  uint64_t pr_a = 0, pr_b = 0, pr_c = 0, pr_d = 0;                // GG_COH_PROFILE: batch, queue load, requests, write back
+  uint64_t pf_ = 0, pa_ = 0, pg_ = 0;                              // requests: last interval, M/G/1, search
+  for (uint32_t s_ = 0; lo <= hi && s_ <= hi - lo; ++s_) {
+    const uint64_t _s0 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
+    const uint32_t pos = dir ? lo + s_ : hi - s_;
+    uint32_t m = 0;
+    for (uint32_t b0 = 0; b0 < n; b0 += 64) {
+      const uint32_t i = b0 + ln;
+      const bool at = i < n && Pp[i] == pos && (Pf[i] >> 24) == 0;
+      const uint64_t bm = __ballot(at);
+      if (at) {
+        const uint32_t k = m + (uint32_t)__builtin_popcountll(bm & ((1ull << ln) - 1));
+        B[k] = i; K[k] = (Pt[i] << 12) | Pr[i];
+      }
+      m += (uint32_t)__builtin_popcountll(bm);
     }
-    if (status) { ++qh; wave_sync(); continue; }
-    // re-insert (t, ri): the keys below it in (qh, n) are a prefix of the queue
-    uint32_t below = 0;
-    for (uint32_t b = qh + 1; b < n; b += 64) {
-      const uint32_t j = b + ln;
-      bool lt_ = false;
-      if (j < n) { const uint64_t tj = Qt[j]; lt_ = tj < t || (tj == t && Qr[j] < ri); }
-      const uint32_t c2 = (uint32_t)__builtin_popcountll(__ballot(lt_));
-      below += c2;
-      if (c2 < 64) break;
-    }
-    for (uint32_t b = qh + 1; b <= qh + below; b += 64) {          // (qh, qh + below] moves down by one
-      const uint32_t j = b + ln;
-      const bool mv = j <= qh + below;
-      uint64_t vt = 0; uint32_t vr = 0, vs = 0;
-      if (mv) { vt = Qt[j]; vr = Qr[j]; vs = Qs[j]; }
-      wave_sync();
-      if (mv) { Qt[j - 1] = vt; Qr[j - 1] = vr; Qs[j - 1] = vs; }
-      wave_sync();
-    }
-    if (ln == 0) { Qt[qh + below] = t; Qr[qh + below] = ri; Qs[qh + below] = i; }
+    if (m == 0) continue;
     wave_sync();
+    for (uint32_t k = ln; k < m; k += 64) {
+      const uint64_t kk = K[k];
+      uint32_t r = 0;
+      for (uint32_t j = 0; j < m; ++j) r += K[j] < kk;
+      O[r] = B[k];
+    }
+    wave_sync();
+    uint8_t* im = qimg + (size_t)(pos - sd.lo) * P.qimg;
+    HQueue* qq = reinterpret_cast<HQueue*>(im);
+    HNode* qn = reinterpret_cast<HNode*>(im + sizeof(HQueue));
+    const uint64_t _s1 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
+    RegQueue rq;
+    if (regq) rq.load(qq, qn, 1, P.np.analytical != 0, ln);
+    HTree tr{qq, qn, 1, P.np.analytical != 0};
+    uint64_t cq = 0, cf = 0;
+    const uint32_t nx = dir ? pos + 1 : pos - 1;
+    if (S.prof) { const uint64_t _s2 = __builtin_amdgcn_s_memtime(); pr_a += _s1 - _s0; pr_b += _s2 - _s1; }
+    for (uint32_t c0 = 0; c0 < m; c0 += 64) {
+      const uint32_t cnt = min(64u, m - c0);
+      uint32_t i = 0, f_ = 0, d_ = 0;
+      uint64_t t_ = 0, z_ = 0;
+      if (ln < cnt) { i = O[c0 + ln]; t_ = Pt[i]; z_ = Pz[i]; f_ = Pf[i]; d_ = Pd[i]; }
+      uint64_t ot = t_;
+      const uint64_t _s3 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
+      for (uint32_t k = 0; k < cnt; ++k) {
+        const uint64_t t = rl64(t_, k);
+        const uint32_t nf = (uint32_t)__builtin_amdgcn_readlane((int)f_, (int)k) & 0xFFFFFFu;
+        uint64_t qd = 0;
+        if (qm) {
+          const uint64_t tc = time_to_cycles(t, P.np.f);
+          qd = regq ? rq.request(tc, nf, S.err) : (wave_q ? tr.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
+        }
+        cq += qd; cf += nf;
+        if (ln == k) ot = t + zps + lat_to_ps(qd, P.np.f);
+      }
+      nev += cnt;
+      if (S.prof) pr_c += __builtin_amdgcn_s_memtime() - _s3;
+      if (ln < cnt) {
+        uint32_t status = 0;
+        if (nx < sd.lo || nx > sd.hi) status = 2;            // next router in another shard: held
+        else if (nx == d_) status = 1;                       // leaves the chain: next stage
+        Pt[i] = ot; Pz[i] = z_ + zps; Pp[i] = nx; Pf[i] = (f_ & 0xFFFFFFu) | (status << 24);
+      }
+    }
+    const uint64_t _s4 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
+    if (regq) rq.store(qq, qn);
+    if (S.prof) { pr_d += __builtin_amdgcn_s_memtime() - _s4; pf_ += rq.n_fast; pa_ += rq.n_anl; pg_ += rq.n_gen; }
+    if (ln == 0) {          // port_hop's counters: contention, router packets, buffer w+r, switch, crossbar, link
+      uint64_t* l = lc + (size_t)(pos - sd.lo) * kNetCtr;
+      l[0] += qm ? cq : 0; l[1] += qm ? m : 0; l[2] += cf; l[3] += m; l[4] += cf; l[5] += cf;
+    }
+    wave_sync();
+  }
+  if (S.prof && ln == 0) {
+    atomicAdd(&S.prof[26], (unsigned long long)pr_a); atomicAdd(&S.prof[27], (unsigned long long)pr_b);
+    atomicAdd(&S.prof[28], (unsigned long long)pr_c); atomicAdd(&S.prof[29], (unsigned long long)pr_d);
+    atomicAdd(&S.prof[30], (unsigned long long)pf_); atomicAdd(&S.prof[31], (unsigned long long)pa_);
+    atomicAdd(&S.prof[32], (unsigned long long)pg_);
   }
   __syncthreads();
   PROF_AT(_w2);
@@ -1899,26 +1981,45 @@ static gg_status coh_alloc(gg_ctx* ctx)
   // hop-by-hop chain segments: the runs of each row / column inside one owned shard
   std::vector<Seg> segx, segy;
   std::vector<uint32_t> tseg((size_t)P.T * 2, ~0u);
+  P.seg_xcd = 0;
   if (P.net == GG_NET_EMESH_HOP_BY_HOP) {
     if (P.mw * P.mh != P.T) return gg_fail(GG_ERR_UNSUPPORTED, "emesh_hop_by_hop needs a full W x H mesh (hop_by_hop.cc:55-59)");
     auto owned = [&](uint32_t t) { return ltile[t] >= 0; };
+    const uint32_t ns = k1 - k0;
+    bool inter = true;                 // every owned shard has the same number of runs per pass
     for (int pass = 0; pass < 2; ++pass) {
       const uint32_t lines = pass == 0 ? P.mh : P.mw, len = pass == 0 ? P.mw : P.mh;
-      std::vector<Seg>& out = pass == 0 ? segx : segy;
+      std::vector<std::vector<Seg>> per(ns);
       for (uint32_t ln = 0; ln < lines; ++ln) {
         auto at = [&](uint32_t pos) { return pass == 0 ? ln * P.mw + pos : pos * P.mw + ln; };
         uint32_t a = 0;
         while (a < len) {
           uint32_t b = a;
           while (b + 1 < len && shard[at(b + 1)] == shard[at(a)]) ++b;
-          if (owned(at(a))) {
-            for (uint32_t q = a; q <= b; ++q) tseg[(size_t)at(q) * 2 + pass] = (uint32_t)out.size();
-            out.push_back(Seg{ln, a, b, 0});
-          }
+          if (owned(at(a))) per[shard[at(a)] - k0].push_back(Seg{ln, a, b, 0});
           a = b + 1;
         }
       }
+      for (uint32_t k = 1; k < ns; ++k) inter = inter && per[k].size() == per[0].size();
+      // runs of one shard interleaved (run j of shard k at slot j * ns + k), so
+      // with the walker block decode of k_c_walk a shard's walkers share the
+      // XCD of its tiles under round-robin placement (speed only)
+      std::vector<Seg>& out = pass == 0 ? segx : segy;
+      if (inter) {
+        for (size_t j = 0; j < per[0].size(); ++j)
+          for (uint32_t k = 0; k < ns; ++k) out.push_back(per[k][j]);
+      } else {
+        for (uint32_t k = 0; k < ns; ++k) out.insert(out.end(), per[k].begin(), per[k].end());
+      }
+      for (uint32_t i = 0; i < out.size(); ++i) {
+        const Seg& g = out[i];
+        for (uint32_t q = g.lo; q <= g.hi; ++q) {
+          const uint32_t t = pass == 0 ? g.line * P.mw + q : q * P.mw + g.line;
+          tseg[(size_t)t * 2 + pass] = i;
+        }
+      }
     }
+    P.seg_xcd = inter ? ns : 0;
   }
   P.nsx = (uint32_t)segx.size() * 2; P.nsy = (uint32_t)segy.size() * 2;
   uint32_t maxrun = 1;
@@ -2179,8 +2280,8 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
     fprintf(stderr, "[gg_coh] step cycles over tiles: self %llu inbox+handlers %llu (order %llu) trace %llu publish %llu "
             "writeback %llu | slowest tile per launch %llu\n"
             "[gg_coh] walkers: %llu launches, staging %llu events %llu loop %llu handoff %llu, max events X %llu Y %llu | "
-            "slowest walker per launch X %llu Y %llu (s_memtime cycles)\n",
-            h[0], h[1], h[9], h[2], h[3], h[4], crit, h[22], h[16], h[19], h[17], h[18], h[24], h[25], wx, wy);
+            "slowest walker per launch X %llu Y %llu | sweep: batch %llu queue load %llu requests %llu store %llu (s_memtime cycles); requests fast %llu M/G/1 %llu search %llu\n",
+            h[0], h[1], h[9], h[2], h[3], h[4], crit, h[22], h[16], h[19], h[17], h[18], h[24], h[25], wx, wy, h[26], h[27], h[28], h[29], h[30], h[31], h[32]);
   }
   if (gg_status e = coh_check(ctx)) return e;
   uint64_t done = 0;

@@ -36,7 +36,7 @@ namespace gg {
 struct HNode { uint64_t first, second; };
 struct HQueue {
   uint32_t size; uint32_t max_size; uint32_t type, aux;   // GG_QM_*; list: no-interleaving flag; basic: basic_moving_avg
-  double sig_sq, sig; uint64_t n, newest;          // QueueModelMG1
+  uint64_t sig_sq, sig, n, newest;                  // QueueModelMG1: sums of p^2 and p (integers, see mg1_queue_delay)
   uint64_t analytical;                              // _total_requests_using_analytical_model
   uint64_t util, last_req, total_req;               // QueueModel utilization counters
   uint32_t front, back;                             // basic: ModuloNum window ends (modulo window + 1)
@@ -94,21 +94,27 @@ __device__ __forceinline__ void wave_sync()
 }
 __device__ __forceinline__ uint64_t ballot64(bool b) { return __ballot(b); }
 
+// QueueModelMG1::computeQueueDelay (queue_model_m_g_1.cc).  The reference
+// accumulates _service_time_sum(2) in doubles; every term is an integer
+// processing time, so while the sums stay below 2^53 the double sums are the
+// exact integers kept here (mg1_update flags GG_DERR_RANGE beyond).
+__device__ __forceinline__ uint64_t mg1_queue_delay(uint64_t n, uint64_t newest, uint64_t ssq, uint64_t ss)
+{
+  if (n == 0) return 0;
+  const double sig_sq = (double)ssq, sig = (double)ss;
+  double variance = (sig_sq / n) - ((sig / n) * (sig / n));
+  double service_rate = 1.0 / (sig / n);
+  double arrival_rate = ((double)n) / newest;
+  if (arrival_rate >= service_rate) arrival_rate = 0.999 * service_rate;
+  return (uint64_t)ceil(0.5 * service_rate * arrival_rate * ((1 / (service_rate * service_rate)) + variance) /
+                        (service_rate - arrival_rate));
+}
+constexpr uint64_t kMg1Exact = 1ull << 53;
+
 struct HTree {
   HQueue* q; HNode* nd; uint64_t min_proc; bool analytical;
 
-  __device__ __forceinline__ uint64_t mg1_delay() const                         // QueueModelMG1::computeQueueDelay
-  {
-    const uint64_t n = q->n, newest = q->newest;
-    const double sig_sq = q->sig_sq, sig = q->sig;
-    if (n == 0) return 0;
-    double variance = (sig_sq / n) - ((sig / n) * (sig / n));
-    double service_rate = 1.0 / (sig / n);
-    double arrival_rate = ((double)n) / newest;
-    if (arrival_rate >= service_rate) arrival_rate = 0.999 * service_rate;
-    return (uint64_t)ceil(0.5 * service_rate * arrival_rate * ((1 / (service_rate * service_rate)) + variance) /
-                          (service_rate - arrival_rate));
-  }
+  __device__ __forceinline__ uint64_t mg1_delay() const { return mg1_queue_delay(q->n, q->newest, q->sig_sq, q->sig); }
   // ---- sorted interval array nd[0..size) (history_tree and history_list) ----
   __device__ __forceinline__ void l_erase(uint32_t i)
   {
@@ -204,8 +210,28 @@ struct HTree {
     const uint32_t cap = q->max_size;
     uint32_t head = q->head, n = q->size;
     if (n >= cap) { head = head + 1 == cap ? 0u : head + 1; --n; }    // prune the min node (:52-56)
-    const bool two = cap > 64;
     auto phys = [&](uint32_t i) { uint32_t j = head + i; if (j >= cap) j -= cap; if (j >= cap) j -= cap; return j; };
+    {
+      // the last interval is always [x, UINT64_MAX) (the initial node's end; a
+      // request only cuts finite pieces).  A request at t >= x is served there
+      // with no delay, and interval 0 starts at or before x, so the M/G/1
+      // branch cannot be taken: O(1) on uniform values
+      const uint32_t pl = phys(n - 1);
+      const HNode last = nd[pl];
+      if (last.first <= t) {
+        if (t - last.first >= min_proc) {
+          nd[pl].second = t;
+          nd[phys(n)] = HNode{t + p, last.second};
+          ++n;
+        } else {
+          nd[pl].first = t + p;
+        }
+        q->head = head; q->size = n;
+        wave_sync();
+        return 0;
+      }
+    }
+    const bool two = cap > 64;
     uint64_t a0 = 0, b0 = 0, a1 = 0, b1 = 0;
     if (ln < n) { const HNode x = nd[phys(ln)]; a0 = x.first; b0 = x.second; }
     if (two && ln + 64 < n) { const HNode x = nd[phys(ln + 64)]; a1 = x.first; b1 = x.second; }
@@ -360,7 +386,7 @@ struct HTree {
     } else {
       qd = tree_delay(t, p, err);
     }
-    mg1_update(t, p, qd);
+    mg1_update(t, p, qd, err);
     return qd;
   }
   // computeQueueDelay on a whole wave (every lane, identical arguments, the
@@ -369,16 +395,18 @@ struct HTree {
   {
     if (q->type != GG_QM_HISTORY_TREE || q->max_size > 128) return delay(t, p, err);
     const uint64_t qd = tree_delay_wave(t, p, err, ln);
-    mg1_update(t, p, qd);
+    mg1_update(t, p, qd, err);
     return qd;
   }
-  __device__ __forceinline__ void mg1_update(uint64_t t, uint64_t p, uint64_t qd)
+  __device__ __forceinline__ void mg1_update(uint64_t t, uint64_t p, uint64_t qd, uint32_t* err)
   {
-    const double ss = q->sig_sq, sg = q->sig;
+    const uint64_t ss = q->sig_sq, sg = q->sig;
     const uint64_t nn = q->n, nw = q->newest, ut = q->util, lr = q->last_req, tr = q->total_req;
     const uint64_t x = t + qd + p;
-    q->sig_sq = ss + (double)p * (double)p;                      // QueueModelMG1::updateQueue
-    q->sig = sg + (double)p;
+    const uint64_t ss2 = ss + p * p;
+    if (ss2 >= kMg1Exact || p >= (1ull << 26)) atomicOr(err, GG_DERR_RANGE);
+    q->sig_sq = ss2;                                             // QueueModelMG1::updateQueue
+    q->sig = sg + p;
     q->n = nn + 1;
     q->newest = x > nw ? x : nw;
     q->util = ut + p;                                            // updateQueueUtilizationCounters
@@ -386,6 +414,144 @@ struct HTree {
     q->total_req = tr + 1;
   }
 
+};
+
+// ---------------------------------------------------------------------------
+// One history-tree queue held in a wave's registers for a batch of requests
+// (every lane calls every method with identical arguments).  Logical interval
+// i (< 128 = max_size bound) sits in lane i & 63 of slot i >> 6, so the
+// queue's state costs no memory round trip per request: the search is two
+// ballots, an insert / erase a one-lane shift of the slots (DPP wave_shr /
+// wave_shl), the header and M/G/1 sums are uniform registers.  load / store
+// move the image (HQueue + circular node list, any head) in one round each;
+// store writes it back with head 0.  Same request as HTree::tree_delay +
+// mg1_update (the in-order request, t at or after the start of the last
+// interval [x, UINT64_MAX), is the O(1) first branch).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l)
+{
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), (int)l) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
+}
+template <int CTRL> __device__ __forceinline__ uint64_t dpp64(uint64_t v)
+{
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)v, (int)(uint32_t)v, CTRL, 0xf, 0xf, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(v >> 32), (int)(uint32_t)(v >> 32), CTRL, 0xf, 0xf, false);
+  return ((uint64_t)hi << 32) | lo;
+}
+constexpr int kDppWaveShl1 = 0x130;    // lane l <- lane l + 1
+constexpr int kDppWaveShr1 = 0x138;    // lane l <- lane l - 1
+
+struct RegQueue {
+  uint64_t a0, b0, a1, b1;             // this lane's intervals of slot 0 / slot 1
+  uint32_t sz, cap, ln;
+  uint64_t sig_sq, sig, nreq, newest, util, last_req, total_req, anl;
+  uint64_t min_proc;
+  bool analytical;
+  uint32_t n_fast = 0, n_anl = 0, n_gen = 0;   // requests by branch (diagnostics)
+
+  __device__ __forceinline__ void load(const HQueue* q, const HNode* nd, uint64_t mp, bool an, uint32_t lane)
+  {
+    ln = lane; min_proc = mp; analytical = an;
+    sz = q->size; cap = q->max_size;
+    const uint32_t head = q->head;
+    sig_sq = q->sig_sq; sig = q->sig; nreq = q->n; newest = q->newest;
+    util = q->util; last_req = q->last_req; total_req = q->total_req; anl = q->analytical;
+    a0 = b0 = a1 = b1 = 0;
+    uint32_t j = head + ln; if (j >= cap) j -= cap;
+    if (ln < sz) { const HNode x = nd[j]; a0 = x.first; b0 = x.second; }
+    j = head + ln + 64; if (j >= cap) j -= cap; if (j >= cap) j -= cap;
+    if (ln + 64 < sz) { const HNode x = nd[j]; a1 = x.first; b1 = x.second; }
+  }
+  __device__ __forceinline__ void store(HQueue* q, HNode* nd) const
+  {
+    if (ln < sz) nd[ln] = HNode{a0, b0};
+    if (ln + 64 < sz) nd[ln + 64] = HNode{a1, b1};
+    q->size = sz; q->head = 0;
+    q->sig_sq = sig_sq; q->sig = sig; q->n = nreq; q->newest = newest;
+    q->util = util; q->last_req = last_req; q->total_req = total_req; q->analytical = anl;
+  }
+  __device__ __forceinline__ uint64_t A(uint32_t i) const { return i < 64 ? rl64(a0, i) : rl64(a1, i - 64); }
+  __device__ __forceinline__ uint64_t B(uint32_t i) const { return i < 64 ? rl64(b0, i) : rl64(b1, i - 64); }
+  __device__ __forceinline__ void set(uint32_t i, uint64_t a, uint64_t b)
+  {
+    if ((i & 63) == ln) { if (i < 64) { a0 = a; b0 = b; } else { a1 = a; b1 = b; } }
+  }
+  // new[x] = old[x - 1] for x > k
+  __device__ __forceinline__ void shift_up(uint32_t k)
+  {
+    const uint64_t ca = rl64(a0, 63), cb = rl64(b0, 63);
+    const uint64_t pa0 = dpp64<kDppWaveShr1>(a0), pb0 = dpp64<kDppWaveShr1>(b0);
+    const uint64_t pa1 = dpp64<kDppWaveShr1>(a1), pb1 = dpp64<kDppWaveShr1>(b1);
+    if (ln > k) { a0 = pa0; b0 = pb0; }
+    if (ln + 64 > k) { a1 = ln == 0 ? ca : pa1; b1 = ln == 0 ? cb : pb1; }
+  }
+  // new[x] = old[x + 1] for x >= k
+  __device__ __forceinline__ void shift_down(uint32_t k)
+  {
+    const uint64_t ca = rl64(a1, 0), cb = rl64(b1, 0);
+    const uint64_t na0 = dpp64<kDppWaveShl1>(a0), nb0 = dpp64<kDppWaveShl1>(b0);
+    const uint64_t na1 = dpp64<kDppWaveShl1>(a1), nb1 = dpp64<kDppWaveShl1>(b1);
+    if (ln >= k) { a0 = ln == 63 ? ca : na0; b0 = ln == 63 ? cb : nb0; }
+    if (ln + 64 >= k) { a1 = na1; b1 = nb1; }
+  }
+  // computeQueueDelay (queue_model_history_tree.cc:44-126) + QueueModelMG1::updateQueue
+  __device__ __forceinline__ uint64_t request(uint64_t t, uint64_t p, uint32_t* err)
+  {
+    if (sz >= cap) { shift_down(0); --sz; }                          // prune the min node (:52-56)
+    uint64_t qd = 0;
+    const uint64_t la = A(sz - 1), lb = B(sz - 1);
+    if (la <= t && t + p <= lb && lb - (t + p) >= min_proc) {        // the last interval: no search, no delay
+      ++n_fast;
+      if (t - la >= min_proc) { set(sz - 1, la, t); set(sz, t + p, lb); ++sz; }
+      else set(sz - 1, t + p, lb);
+    } else if (analytical && A(0) > t + p) {
+      ++anl; ++n_anl;
+      qd = mg1_queue_delay(nreq, newest, sig_sq, sig);
+    } else {
+      ++n_gen;
+      const bool v0 = ln < sz, v1 = ln + 64 < sz;
+      const uint32_t cnt = (uint32_t)__builtin_popcountll(__ballot(v0 && a0 <= t)) +
+                           (uint32_t)__builtin_popcountll(__ballot(v1 && a1 <= t));
+      int i = -1;
+      if (cnt > 0 && t + p <= B(cnt - 1)) i = (int)cnt - 1;
+      if (i < 0) {
+        const uint64_t m0 = __ballot(v0 && ln >= cnt && b0 - a0 >= p);
+        const uint64_t m1 = __ballot(v1 && ln + 64 >= cnt && b1 - a1 >= p);
+        i = m0 ? (int)__builtin_ctzll(m0) : (m1 ? 64 + (int)__builtin_ctzll(m1) : -1);
+      }
+      if (i < 0) {
+        if (ln == 0) atomicOr(err, GG_DERR_STATE);
+      } else {
+        const uint32_t ui = (uint32_t)i;
+        const uint64_t a = A(ui), b = B(ui);
+        if (t >= a) {
+          if (t - a >= min_proc) {
+            if (b - (t + p) >= min_proc) { shift_up(ui + 1); set(ui + 1, t + p, b); ++sz; }
+            set(ui, a, t);
+          } else if (b - (t + p) >= min_proc) {
+            set(ui, t + p, b);
+          } else {
+            shift_down(ui); --sz;
+          }
+        } else {
+          qd = a - t;
+          if (b - (a + p) >= min_proc) set(ui, a + p, b);
+          else { shift_down(ui); --sz; }
+        }
+      }
+    }
+    sig_sq += p * p;                                                 // QueueModelMG1::updateQueue
+    sig += p;
+    if (sig_sq >= kMg1Exact || p >= (1ull << 26)) { if (ln == 0) atomicOr(err, GG_DERR_RANGE); }
+    ++nreq;
+    const uint64_t x = t + qd + p;
+    newest = x > newest ? x : newest;
+    util += p;                                                       // updateQueueUtilizationCounters
+    last_req = x > last_req ? x : last_req;
+    ++total_req;
+    return qd;
+  }
 };
 
 // Latency::toPicosec / Time::toCycles (time_types.h:81-109), double and ceil.

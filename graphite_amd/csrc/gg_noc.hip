@@ -604,6 +604,10 @@ __global__ void __launch_bounds__(64) k_htree_seq(HQueue* q, HNode* nd, uint64_t
                                                               : reinterpret_cast<const uint4*>(nd)[w - sizeof(HQueue) / 16];
   __syncthreads();
   HTree tr{lq, lnd, min_proc, analytical != 0};
+  // a history tree lives in the wave's registers for the whole stream (RegQueue)
+  const bool reg = lq->type == GG_QM_HISTORY_TREE;
+  RegQueue rq;
+  if (reg) rq.load(lq, lnd, min_proc, analytical != 0, ln);
   __shared__ uint64_t ct[512], cp[512], cd[512];          // requests staged 512 at a time
   for (uint64_t b = 0; b < n; b += 512) {
     const uint32_t m = (uint32_t)min<uint64_t>(512, n - b);
@@ -613,13 +617,14 @@ __global__ void __launch_bounds__(64) k_htree_seq(HQueue* q, HNode* nd, uint64_t
       const uint64_t ti = ct[k], pi = cp[k];
       uint64_t r = 0;
       if (pi == 0) { if (ln == 0) atomicOr(err, GG_DERR_RANGE); }
-      else r = tr.delay_w(ti, pi, err, ln);
+      else r = reg ? rq.request(ti, pi, err) : tr.delay_w(ti, pi, err, ln);
       cd[k] = r;
     }
     __syncthreads();
     for (uint32_t k = ln; k < m; k += 64) d[b + k] = cd[k];
     __syncthreads();
   }
+  if (reg) rq.store(lq, lnd);
   for (uint32_t w = ln; w < sizeof(HQueue) / 16 + ms; w += 64) {
     const uint4 v = reinterpret_cast<const uint4*>(img)[w];
     if (w < sizeof(HQueue) / 16) reinterpret_cast<uint4*>(q)[w] = v;
