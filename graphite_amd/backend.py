@@ -57,7 +57,7 @@ EXPORTS = ["gg_abi_version", "gg_last_error", "gg_config_default", "gg_create", 
            "gg_gen_uniform_trace", "gg_kernel_time_ms", "gg_set_timing",
            "gg_coherent_begin", "gg_coherent_quantum", "gg_coherent_export", "gg_coherent_import",
            "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace", "gg_shard_map",
-           "gg_kernel_stats"]
+           "gg_kernel_stats", "gg_round_exchange", "gg_coherent_run_ranks"]
 
 
 class _CStatus(ctypes.Structure):
@@ -107,9 +107,11 @@ def load():
     L.gg_gen_hotspot_trace.argtypes = [vp, vp, u32, u32, u64, u64, u32, u32, u32, u32, vp]
     L.gg_shard_map.argtypes = [u32, u32, vp]
     L.gg_kernel_stats.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64)]
-    for name in ["gg_kernel_stats", "gg_shard_map", "gg_coherent_begin", "gg_coherent_quantum", "gg_coherent_export", "gg_coherent_import",
-                 "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace", "gg_shard_map",
-           "gg_kernel_stats"]:
+    L.gg_round_exchange.argtypes = [vp, vp, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(i32)]
+    L.gg_coherent_run_ranks.argtypes = [vp, vp, ctypes.POINTER(_Trace), vp, vp]
+    for name in ["gg_kernel_stats", "gg_shard_map", "gg_coherent_begin", "gg_coherent_quantum", "gg_coherent_export",
+                 "gg_coherent_import", "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace",
+                 "gg_round_exchange", "gg_coherent_run_ranks"]:
         getattr(L, name).restype = i32
     for name in ["gg_reset", "gg_cache_access_batch", "gg_cache_get_counters", "gg_cache_get_line_info",
                  "gg_cache_set_line_info", "gg_cache_access_line", "gg_cache_insert_line",
@@ -259,6 +261,17 @@ class Backend:
             _need_dev(out, torch.int64, addr.numel())
         tr = self._trace(addr, meta, tile_offsets)
         _check(load().gg_coherent_run(self.h, ctypes.byref(tr), _ptr(out), _stream(stream)))
+
+    def coherent_run_ranks(self, comm_ptr, addr, meta, tile_offsets, out=None, stream=None):
+        """The whole coherent run over the ranks of an RCCL communicator
+        (gg_coherent_run_ranks; comm_ptr = ncclComm_t as an int, e.g.
+        ProcessGroupNCCL._comm_ptr()).  This context owns the rank's shards."""
+        import torch
+        if out is not None:
+            _need_dev(out, torch.int64, addr.numel())
+        tr = self._trace(addr, meta, tile_offsets)
+        _check(load().gg_coherent_run_ranks(self.h, ctypes.c_void_p(comm_ptr), ctypes.byref(tr), _ptr(out),
+                                            _stream(stream)))
 
     def coherent_begin(self, addr, meta, tile_offsets, out=None, stream=None):
         import torch

@@ -121,3 +121,23 @@ def run_local(engines, quantum_ps, num_shards):
         if nq is None:
             return quanta
         q = nq
+
+
+def rccl_comm_ptr(group=None):
+    """The ncclComm_t (RCCL) of a torch.distributed "nccl" process group, as an
+    int for the C ABI (created by a first collective if still lazy)."""
+    import torch
+    import torch.distributed as dist
+    pg = group or dist.distributed_c10d._get_default_group()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    t = torch.zeros(1, device=dev)
+    dist.all_reduce(t, group=pg)
+    return pg._get_backend(dev)._comm_ptr()
+
+
+def run_rccl(backend, addr, meta, tile_offsets, out=None, group=None, stream=None):
+    """The whole coherent run of this rank's shards with the exchange in the C
+    ABI (gg_coherent_run_ranks: gg_round_exchange over the group's RCCL
+    communicator at every quantum boundary) - the same rounds as `run`,
+    without a host round trip per collective."""
+    backend.coherent_run_ranks(rccl_comm_ptr(group), addr, meta, tile_offsets, out, stream)

@@ -1846,6 +1846,8 @@ static void timed_harvest(gg_coh_state* C)
   C->tused = 0;
 }
 
+uint64_t gg_coherent_msg_cap(gg_ctx* ctx) { return ctx->coh ? ctx->coh->P.msg_cap : 0; }
+
 gg_status gg_coh_kernel_stats(gg_ctx* ctx, const char* name, double* total_ms, uint64_t* launches)
 {
   gg_coh_state* C = ctx->coh;

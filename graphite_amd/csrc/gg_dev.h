@@ -505,6 +505,27 @@ struct RegQueue {
       ++n_fast;
       if (t - la >= min_proc) { set(sz - 1, la, t); set(sz, t + p, lb); ++sz; }
       else set(sz - 1, t + p, lb);
+    } else if (sz >= 2 && t < la && t >= A(sz - 2)) {
+      // the tail: interval sz-2 is the last one starting at or before t (and
+      // interval 0 starts before t: no M/G/1).  Either [t, t+p] fits in it, or
+      // the first later interval long enough is the last one (unbounded)
+      ++n_fast;
+      const uint32_t i2 = sz - 2, i1 = sz - 1;
+      const uint64_t a2 = A(i2), b2 = B(i2);
+      if (t + p <= b2) {
+        if (t - a2 >= min_proc) {
+          if (b2 - (t + p) >= min_proc) { set(i1 + 1, la, lb); set(i1, t + p, b2); ++sz; }
+          set(i2, a2, t);
+        } else if (b2 - (t + p) >= min_proc) {
+          set(i2, t + p, b2);
+        } else {
+          set(i2, la, lb); --sz;                                       // erase interval sz-2
+        }
+      } else {
+        qd = la - t;                                                   // queued behind the busy period
+        if (lb - (la + p) >= min_proc) set(i1, la + p, lb);
+        else --sz;                                                     // erase the last interval
+      }
     } else if (analytical && A(0) > t + p) {
       ++anl; ++n_anl;
       qd = mg1_queue_delay(nreq, newest, sig_sq, sig);

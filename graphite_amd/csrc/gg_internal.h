@@ -102,7 +102,12 @@ struct gg_ctx {
   // timing
   bool timing = false;
   std::vector<gg_timer> timers;
+  // multi-rank round buffers (gg_round.hip), freed by gg_destroy
+  void* round = nullptr;
+  void (*round_free)(void*) = nullptr;
 };
+inline void* gg_round_state(gg_ctx* ctx) { return ctx->round; }
+inline void gg_round_state_set(gg_ctx* ctx, void* p, void (*f)(void*)) { ctx->round = p; ctx->round_free = f; }
 
 // error reporting (gg_capi.hip)
 gg_status gg_fail(gg_status code, const char* fmt, ...);
@@ -131,3 +136,4 @@ gg_status gg_noc_counters(gg_ctx* ctx, uint64_t* out);
 void      gg_coh_free(gg_ctx* ctx);
 gg_status gg_htree_run(gg_ctx* ctx, uint64_t min_proc, const uint64_t* t, const uint64_t* p, uint64_t n, uint64_t* d);
 gg_status gg_coh_kernel_stats(gg_ctx* ctx, const char* name, double* total_ms, uint64_t* launches);
+uint64_t  gg_coherent_msg_cap(gg_ctx* ctx);     // records a quantum boundary can hold (after gg_coherent_begin)

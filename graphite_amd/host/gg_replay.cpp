@@ -11,14 +11,24 @@
 //       configs[2..4] hotspot trace generated on the device; prints every
 //       tile's memory block (MemoryManager::outputSummary) and memory-network
 //       block (Network::outputSummary, network.cc:79-89, the Memory network)
+//   gg_replay --coherent ... --shards K --ranks W --rank R --id-file FILE
+//       the same over W processes (one per GPU, device R mod #devices), rank R
+//       owning logical shards [R*K/W, (R+1)*K/W): RCCL communicator from the
+//       unique id rank 0 writes to FILE, the run by gg_coherent_run_ranks
+//       (gg_round_exchange at every quantum boundary), the statistics summed
+//       over ranks and printed by rank 0
 //   gg_replay --summary-selftest
 //       prints writeCacheSummary() for fixed counters (no GPU needed)
+#include <rccl/rccl.h>
+
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <iostream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "graphite_host.hpp"
@@ -38,7 +48,9 @@ int main(int argc, char** argv)
   uint32_t tiles = 4, lines_log2 = 15, batches = 1, l2_assoc = 8, hot_lines = 64, net = GG_NET_EMESH_HOP_COUNTER;
   bool coherent = false;
   uint64_t per_tile = 100000;
-  std::string trace;
+  std::string trace, id_file;
+  int ranks = 1, rank = 0;
+  uint32_t shards = 1;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&]() -> const char* { if (i + 1 >= argc) { std::fprintf(stderr, "missing value for %s\n", a.c_str()); std::exit(2); } return argv[++i]; };
@@ -49,6 +61,10 @@ int main(int argc, char** argv)
     else if (a == "--l2-assoc") l2_assoc = (uint32_t)std::strtoul(next(), nullptr, 0);
     else if (a == "--trace") trace = next();
     else if (a == "--coherent") coherent = true;
+    else if (a == "--shards") shards = (uint32_t)std::strtoul(next(), nullptr, 0);
+    else if (a == "--ranks") ranks = std::atoi(next());
+    else if (a == "--rank") rank = std::atoi(next());
+    else if (a == "--id-file") id_file = next();
     else if (a == "--hot-lines") hot_lines = (uint32_t)std::strtoul(next(), nullptr, 0);
     else if (a == "--net") {
       const std::string n = next();
@@ -105,11 +121,44 @@ int main(int argc, char** argv)
     } else { std::fprintf(stderr, "unknown option %s\n", a.c_str()); return 2; }
   }
   if (coherent) {
+    ncclComm_t comm = nullptr;
     try {
       gg_config cfg;
       gg_config_default(&cfg, tiles);
       cfg.l2_assoc = l2_assoc;
       cfg.net_model = net;
+      cfg.num_shards = shards;
+      if (!id_file.empty()) {
+        // one process per GPU: the RCCL communicator of `ranks` processes
+        if (rank < 0 || rank >= ranks || shards % (uint32_t)ranks) {
+          std::fprintf(stderr, "gg_replay: rank %d of %d, %u shards\n", rank, ranks, shards);
+          return 2;
+        }
+        int ndev = 1;
+        hip_check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
+        cfg.device = rank % ndev;
+        hip_check(hipSetDevice(cfg.device), "hipSetDevice");
+        ncclUniqueId id;
+        if (rank == 0) {
+          if (ncclGetUniqueId(&id) != ncclSuccess) { std::fprintf(stderr, "gg_replay: ncclGetUniqueId\n"); return 1; }
+          const std::string tmp = id_file + ".tmp";
+          std::ofstream(tmp, std::ios::binary).write(reinterpret_cast<const char*>(&id), sizeof(id));
+          std::rename(tmp.c_str(), id_file.c_str());
+        } else {
+          for (int w = 0;; ++w) {
+            std::ifstream f(id_file, std::ios::binary);
+            if (f && f.read(reinterpret_cast<char*>(&id), sizeof(id))) break;
+            if (w > 6000) { std::fprintf(stderr, "gg_replay: no RCCL id in %s\n", id_file.c_str()); return 1; }
+            std::this_thread::sleep_for(std::chrono::milliseconds(10));
+          }
+        }
+        if (ncclCommInitRank(&comm, ranks, id, rank) != ncclSuccess) {
+          std::fprintf(stderr, "gg_replay: ncclCommInitRank\n");
+          return 1;
+        }
+        cfg.shard_begin = (uint32_t)rank * (shards / ranks);
+        cfg.shard_end = ((uint32_t)rank + 1) * (shards / ranks);
+      }
       Backend be(cfg);
       const uint64_t n = (uint64_t)tiles * per_tile;
       DeviceBuffer<uint64_t> addr;
@@ -120,23 +169,42 @@ int main(int argc, char** argv)
       std::vector<uint64_t> offs(tiles + 1);
       for (uint32_t t = 0; t <= tiles; ++t) offs[t] = (uint64_t)t * per_tile;
       gg_trace tr{addr.p, meta.p, offs.data(), n};
-      check(gg_coherent_run(be.ctx(), &tr, nullptr, nullptr), "gg_coherent_run");
+      if (comm) check(gg_coherent_run_ranks(be.ctx(), comm, &tr, nullptr, nullptr), "gg_coherent_run_ranks");
+      else check(gg_coherent_run(be.ctx(), &tr, nullptr, nullptr), "gg_coherent_run");
       std::vector<uint64_t> st((size_t)tiles * GG_NUM_TILE_STATS), cc((size_t)tiles * 2 * GG_NUM_CACHE_COUNTERS),
           nc((size_t)tiles * GG_NUM_NET_COUNTERS);
       check(gg_coherent_get_stats(be.ctx(), st.data(), cc.data(), nullptr), "gg_coherent_get_stats");
       check(gg_noc_get_counters(be.ctx(), nc.data()), "gg_noc_get_counters");
-      for (uint32_t t = 0; t < tiles; ++t) {
+      if (comm) {
+        // every statistic is kept by the rank owning its tile: the node's totals are the sums
+        for (std::vector<uint64_t>* v : {&st, &cc, &nc}) {
+          DeviceBuffer<uint64_t> d;
+          d.resize(v->size());
+          hip_check(hipMemcpy(d.p, v->data(), sizeof(uint64_t) * v->size(), hipMemcpyHostToDevice), "hipMemcpy");
+          if (ncclAllReduce(d.p, d.p, v->size(), ncclUint64, ncclSum, comm, nullptr) != ncclSuccess)
+            throw Error(GG_ERR_STATE, "ncclAllReduce");
+          hip_check(hipMemcpy(v->data(), d.p, sizeof(uint64_t) * v->size(), hipMemcpyDeviceToHost), "hipMemcpy");
+        }
+      }
+      const uint64_t zero_net[GG_NUM_NET_COUNTERS] = {0};
+      for (uint32_t t = 0; rank == 0 && t < tiles; ++t) {
         std::cout << "Tile " << t << " Summary:" << std::endl;
         writeMemorySummary(std::cout, cfg, &st[(size_t)t * GG_NUM_TILE_STATS],
                            &cc[(size_t)t * 2 * GG_NUM_CACHE_COUNTERS]);
-        std::cout << "Network Summary: " << std::endl << "  Network (Memory): " << std::endl;
+        // Network::outputSummary (network.cc:79-89): the static networks below SYSTEM,
+        // User (no traffic in a trace-driven run; emesh_hop_counter, carbon_sim.cfg [network]) then Memory
+        std::cout << "Network Summary: " << std::endl << "  Network (User): " << std::endl;
+        writeNetworkSummary(std::cout, zero_net, cfg.frequency_ghz, GG_NET_EMESH_HOP_COUNTER);
+        std::cout << "  Network (Memory): " << std::endl;
         writeNetworkSummary(std::cout, &nc[(size_t)t * GG_NUM_NET_COUNTERS], cfg.frequency_ghz, cfg.net_model,
                             cfg.queue_model_enabled != 0);
       }
     } catch (const Error& e) {
       std::fprintf(stderr, "gg_replay: %s\n", e.what());
+      if (comm) ncclCommDestroy(comm);
       return 1;
     }
+    if (comm) ncclCommDestroy(comm);
     return 0;
   }
   try {

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define GG_ABI_VERSION 3
+#define GG_ABI_VERSION 4
 
 typedef int gg_status;
 enum {
@@ -379,6 +379,21 @@ gg_status gg_coherent_quantum(gg_ctx* ctx, uint64_t q, gg_coherent_status* st);
 gg_status gg_coherent_export(gg_ctx* ctx, gg_cmsg* out_dev, uint64_t cap, uint64_t* per_shard_counts);
 gg_status gg_coherent_import(gg_ctx* ctx, const gg_cmsg* in_dev, uint64_t n);
 gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* trace, uint64_t* access_out_dev, void* stream);
+/* The coherent mode over ranks (one process per GPU), RCCL over xGMI.
+ * nccl_comm is an ncclComm_t (RCCL) of W ranks; rank r's context must own
+ * logical shards [r*K/W, (r+1)*K/W) (cfg.shard_begin / shard_end, K =
+ * num_shards).  gg_round_exchange runs quantum q on the context
+ * (gg_coherent_quantum), sends the held cross-shard records to the ranks that
+ * own their shards and receives this rank's (grouped ncclSend / ncclRecv on
+ * stream), imports them, and all-reduces the status; *next_q is the quantum
+ * every rank runs next and *done 1 when the run is over (GG_ERR_STATE on a
+ * deadlock).  It replaces the reference's per-message transport
+ * (common/transport/socktransport.cc) plus its lax barrier round
+ * (lax_barrier_sync_client.cc:31-69, lax_barrier_sync_server.cc:57-160).
+ * gg_coherent_run_ranks = gg_coherent_begin + rounds from quantum 0 until done. */
+gg_status gg_round_exchange(gg_ctx* ctx, void* nccl_comm, void* stream, uint64_t q, uint64_t* next_q, int* done);
+gg_status gg_coherent_run_ranks(gg_ctx* ctx, void* nccl_comm, const gg_trace* trace, uint64_t* access_out_dev,
+                                void* stream);
 /* tile_stats: [tiles][GG_NUM_TILE_STATS]; cache: [tiles][2][GG_NUM_CACHE_COUNTERS]
  * (either may be NULL); run_info: [GG_NUM_RUN_INFO] (may be NULL).  Tiles a
  * context does not own read 0.  Network counters: gg_noc_get_counters.      */

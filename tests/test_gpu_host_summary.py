@@ -18,9 +18,9 @@ from tests.test_host_mirror import (REPLAY, reference_summary, reference_dram_su
 pytestmark = pytest.mark.gpu
 
 
-def _expected(T, N, net, hop_by_hop):
+def _expected(T, N, net, hop_by_hop, shards=1):
     from oracle import pyoracle as po
-    cfg = C.default_config(T, net_model=net)
+    cfg = C.default_config(T, net_model=net, num_shards=shards)
     a, m, o = po.gen_trace(T, N, hot_lines=64)
     oc = po.OracleCoherent(cfg)
     oc.run(a, m, o)
@@ -50,7 +50,12 @@ def _expected(T, N, net, hop_by_hop):
         L += reference_summary("L1-D", [int(x) for x in cc[t, 0]], False)
         L += reference_summary("L2", [int(x) for x in cc[t, 1]], True)
         L += reference_dram_summary(d, True) + reference_directory_summary(d, auto)
-        L += ["Network Summary: ", "  Network (Memory): "]
+        # Network::outputSummary prints the static networks below SYSTEM: User (no traffic), Memory
+        z = dict(ps=0, fs=0, bs=0, pr=0, fr=0, br=0, lat=0, con=0, bw=0, brd=0, sa=0, xb=0, lt=0, rcc=0, rpk=0, an=0,
+                 util=[0] * 5, last=[0] * 5)
+        L += ["Network Summary: ", "  Network (User): "]
+        L += reference_net_summary(z, cfg.frequency_ghz, True, hop_by_hop=False, contention=False)
+        L += ["  Network (Memory): "]
         L += reference_net_summary(nd, cfg.frequency_ghz, net == C.NET_EMESH_HOP_COUNTER,
                                    hop_by_hop=hop_by_hop, contention=hop_by_hop and bool(cfg.queue_model_enabled))
     return L
@@ -65,6 +70,26 @@ def test_coherent_sim_out_matches_oracle(T, N, net):
     netid = C.NET_EMESH_HOP_BY_HOP if net == "hop_by_hop" else C.NET_EMESH_HOP_COUNTER
     exp = _expected(T, N, netid, net == "hop_by_hop")
     got = out.splitlines()
+    assert len(got) == len(exp)
+    for i, (x, y) in enumerate(zip(got, exp)):
+        assert x == y, "line %d: %r != %r" % (i, x, y)
+
+
+def test_coherent_sim_out_over_rccl_ranks(tmp_path):
+    """gg_replay's rank mode: an RCCL communicator (here of one rank, the
+    only one a one-GPU box can form), the run by gg_coherent_run_ranks with
+    gg_round_exchange at every quantum boundary: the sim.out of the 4-shard
+    canonical schedule."""
+    if not os.path.exists(REPLAY):
+        pytest.skip("gg_replay not built")
+    T, N = 16, 300
+    out = subprocess.run([REPLAY, "--coherent", "--tiles", str(T), "--per-tile", str(N), "--hot-lines", "64",
+                          "--net", "hop_by_hop", "--shards", "4", "--ranks", "1", "--rank", "0",
+                          "--id-file", str(tmp_path / "rccl.id")],
+                         capture_output=True, text=True, check=True, timeout=120).stdout
+    exp = _expected(T, N, C.NET_EMESH_HOP_BY_HOP, True, shards=4)
+    got = out.splitlines()
+    got = got[got.index("Tile 0 Summary:"):]          # RCCL prints its version banner on stdout first
     assert len(got) == len(exp)
     for i, (x, y) in enumerate(zip(got, exp)):
         assert x == y, "line %d: %r != %r" % (i, x, y)
