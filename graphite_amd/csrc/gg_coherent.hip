@@ -475,7 +475,14 @@ struct Tile {
     const uint64_t hit = __ballot(ln < P.dassoc && v == a);
     if (hit) return (int32_t)(base + __builtin_ctzll(hit));
     const uint64_t fr = __ballot(ln < P.dassoc && v == INV_ADDR);
-    if (fr) { const uint32_t i = base + (uint32_t)__builtin_ctzll(fr); d[i].addr = a; return (int32_t)i; }
+    if (fr) {
+      // a never-used slot: its sharer words are zeroed here, not at reset
+      // (full-map vectors of every entry are 2 GB at 1024 tiles)
+      const uint32_t i = base + (uint32_t)__builtin_ctzll(fr);
+      d[i].addr = a;
+      if (ln < P.W) shw((int32_t)i)[ln] = 0;
+      return (int32_t)i;
+    }
     const uint64_t rv = ln < nrep ? ent(-(int32_t)ln - 1)->addr : 0;
     const uint64_t rh = __ballot(ln < nrep && rv == a);
     if (rh) return -(int32_t)__builtin_ctzll(rh) - 1;
@@ -1738,28 +1745,30 @@ __global__ void k_c_status(CP P, CS S, uint64_t* out /* [active, blocked, min_ne
   atomicMin((unsigned long long*)&out[2], (unsigned long long)s);
 }
 
-__global__ void k_c_reset(CP P, CS S, const uint64_t* offs)
+// constructor state of one owned tile per workgroup (its threads stride the
+// tile's arrays); directory sharer words are zeroed when a slot is first used
+__global__ void __launch_bounds__(256) k_c_reset(CP P, CS S, const uint64_t* offs)
 {
-  const uint32_t lt = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lt = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   if (lt >= P.L) return;
-  for (uint32_t i = 0; i < P.s1 * P.a1; ++i) { S.l1_tag[(size_t)lt * P.s1 * P.a1 + i] = INV_ADDR;
-                                               S.l1_meta[(size_t)lt * P.s1 * P.a1 + i] = (uint8_t)((i % P.a1) << 3); }
-  for (uint32_t i = 0; i < P.s1; ++i) S.l1_rr[(size_t)lt * P.s1 + i] = (uint8_t)(P.a1 - 1);
-  for (uint32_t i = 0; i < P.s2 * P.a2; ++i) { S.l2_tag[(size_t)lt * P.s2 * P.a2 + i] = INV_ADDR;
-                                               S.l2_meta[(size_t)lt * P.s2 * P.a2 + i] = (uint8_t)((i % P.a2) << 3); }
-  for (uint32_t i = 0; i < P.s2; ++i) S.l2_rr[(size_t)lt * P.s2 + i] = (uint8_t)(P.a2 - 1);
-  for (uint32_t i = 0; i < 2 * GG_NUM_CACHE_COUNTERS; ++i) S.cc[(size_t)lt * 2 * GG_NUM_CACHE_COUNTERS + i] = 0;
-  for (uint32_t i = 0; i < GG_NUM_TILE_STATS; ++i) S.st[(size_t)lt * GG_NUM_TILE_STATS + i] = 0;
-  for (uint32_t i = 0; i < P.E; ++i) S.dir[(size_t)lt * P.E + i] = DEnt{INV_ADDR, -1, DS_UNCACHED, 0};
-  for (uint64_t i = 0; i < (uint64_t)P.E * P.W; ++i) S.dsh[(size_t)lt * P.E * P.W + i] = 0;
-  S.nrep[lt] = 0; S.nrq[lt] = 0;
-  const uint32_t tile = S.gtile[lt];
-  S.rec[lt] = offs[tile]; S.rec_end[lt] = offs[tile + 1];
-  S.clk[lt] = 0; S.pend_start[lt] = 0; S.out_addr[lt] = INV_ADDR; S.out_time[lt] = 0;
-  S.blocked[lt] = 0; S.seq[lt] = 0;
-  S.ninb0[lt] = 0; S.ninb1[lt] = 0; S.narv0[lt] = 0; S.narv1[lt] = 0;
-  if (P.dram_qm)                                     // QueueModel::create(dram/queue_model/type, min_processing_time)
-    hq_init(S.dq + lt, S.dnd + (size_t)lt * P.max_list, P.max_list, P.dram_qtype, P.dram_qaux);
+  const size_t n1 = (size_t)P.s1 * P.a1, n2 = (size_t)P.s2 * P.a2;
+  for (size_t i = tid; i < n1; i += nt) { S.l1_tag[lt * n1 + i] = INV_ADDR; S.l1_meta[lt * n1 + i] = (uint8_t)((i % P.a1) << 3); }
+  for (size_t i = tid; i < P.s1; i += nt) S.l1_rr[(size_t)lt * P.s1 + i] = (uint8_t)(P.a1 - 1);
+  for (size_t i = tid; i < n2; i += nt) { S.l2_tag[lt * n2 + i] = INV_ADDR; S.l2_meta[lt * n2 + i] = (uint8_t)((i % P.a2) << 3); }
+  for (size_t i = tid; i < P.s2; i += nt) S.l2_rr[(size_t)lt * P.s2 + i] = (uint8_t)(P.a2 - 1);
+  for (size_t i = tid; i < P.E; i += nt) S.dir[(size_t)lt * P.E + i] = DEnt{INV_ADDR, -1, DS_UNCACHED, 0};
+  if (tid < 2 * GG_NUM_CACHE_COUNTERS) S.cc[(size_t)lt * 2 * GG_NUM_CACHE_COUNTERS + tid] = 0;
+  if (tid < GG_NUM_TILE_STATS) S.st[(size_t)lt * GG_NUM_TILE_STATS + tid] = 0;
+  if (tid == 0) {
+    S.nrep[lt] = 0; S.nrq[lt] = 0;
+    const uint32_t tile = S.gtile[lt];
+    S.rec[lt] = offs[tile]; S.rec_end[lt] = offs[tile + 1];
+    S.clk[lt] = 0; S.pend_start[lt] = 0; S.out_addr[lt] = INV_ADDR; S.out_time[lt] = 0;
+    S.blocked[lt] = 0; S.seq[lt] = 0;
+    S.ninb0[lt] = 0; S.ninb1[lt] = 0; S.narv0[lt] = 0; S.narv1[lt] = 0;
+    if (P.dram_qm)                                   // QueueModel::create(dram/queue_model/type, min_processing_time)
+      hq_init(S.dq + lt, S.dnd + (size_t)lt * P.max_list, P.max_list, P.dram_qtype, P.dram_qaux);
+  }
 }
 
 __global__ void k_c_final_stats(CP P, CS S)
@@ -2123,7 +2132,7 @@ gg_status gg_coherent_begin(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_ou
   GG_HIP(hipMemsetAsync(C->S.bnd_cnt, 0, sizeof(uint32_t), s));
   GG_HIP(hipMemsetAsync(C->S.nxl, 0, sizeof(uint32_t) * std::max(P.nsx, 1u), s));
   GG_HIP(hipMemsetAsync(C->S.nyl, 0, sizeof(uint32_t) * std::max(P.nsy, 1u), s));
-  hipLaunchKernelGGL(k_c_reset, dim3((P.L + 63) / 64), dim3(64), 0, s, P, C->S, (const uint64_t*)C->offs_dev);
+  hipLaunchKernelGGL(k_c_reset, dim3(P.L), dim3(256), 0, s, P, C->S, (const uint64_t*)C->offs_dev);
   GG_HIP(hipGetLastError());
   GG_HIP(hipStreamSynchronize(s));
   C->begun = true;

@@ -1,7 +1,12 @@
 #!/usr/bin/env python3
 """Aggregate rocprofv3 per-dispatch counter CSVs into per-kernel means (for
 runs with tens of thousands of dispatches, whose raw CSVs are too large to
-keep).  usage: pmc_agg.py OUT_DIR -> OUT_DIR/agg.json"""
+keep).  usage: pmc_agg.py OUT_DIR [WORKLOAD_KEY] -> OUT_DIR/agg.json
+
+HBM bytes per launch = 2 x FETCH_SIZE (gfx950 reports half the bytes of
+16-B-per-lane reads, MI355X_MICROARCH.md §HBM) + WRITE_SIZE, in KiB units;
+the coherent kernels mix 8-/16-B accesses, so the figure is an estimate of
+the order of magnitude (calibration: tools/calib)."""
 import collections
 import csv
 import glob
@@ -18,6 +23,8 @@ def short(name):
 def main():
     d = sys.argv[1]
     res = {"kernels": collections.defaultdict(dict)}
+    if len(sys.argv) > 2:
+        res["workload_key"] = sys.argv[2]
     for f in glob.glob(os.path.join(d, "trace", "**", "*kernel_stats.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             res["kernels"][short(r["Name"])].update(
@@ -42,6 +49,8 @@ def main():
             v["fetch_bytes_per_launch_x2"] = pm["FETCH_SIZE"] * 1024 * 2   # MI355X_MICROARCH.md §HBM (16-B loads)
         if "WRITE_SIZE" in pm:
             v["write_bytes_per_launch"] = pm["WRITE_SIZE"] * 1024
+        if "FETCH_SIZE" in pm and "WRITE_SIZE" in pm:
+            v["hbm_bytes"] = v["fetch_bytes_per_launch_x2"] + v["write_bytes_per_launch"]
     json.dump(res, open(os.path.join(d, "agg.json"), "w"), indent=1)
 
 

@@ -7,7 +7,7 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 OUT="$GRAFT_REPO_ROOT/gpurun_out/pmc/${PMC_NAME:-coh}"
 mkdir -p "$OUT"
-ARGS=${PMC_ARGS:-1024 256 8 256 --hbh --no-oracle}
+ARGS=${PMC_ARGS:-1024 256 8 256 --hbh --no-oracle --no-timing}
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
   python3 "$GRAFT_REPO_ROOT/tools/coh_bench.py" $ARGS > "$OUT/trace.log" 2>&1 || exit $?
@@ -25,7 +25,7 @@ pass write WRITE_SIZE &&
 pass l2 TCC_HIT_sum TCC_MISS_sum &&
 pass sq SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS
 rc=$?
-python3 "$GRAFT_REPO_ROOT/tools/pmc_agg.py" "$OUT" || exit 1
+python3 "$GRAFT_REPO_ROOT/tools/pmc_agg.py" "$OUT" ${PMC_KEY:-} || exit 1
 find "$OUT" -name "*counter_collection.csv" -delete
 find "$OUT" -name "*kernel_trace.csv" -delete
 exit $rc
