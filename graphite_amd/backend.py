@@ -57,7 +57,7 @@ EXPORTS = ["gg_abi_version", "gg_last_error", "gg_config_default", "gg_create", 
            "gg_gen_uniform_trace", "gg_kernel_time_ms", "gg_set_timing",
            "gg_coherent_begin", "gg_coherent_quantum", "gg_coherent_export", "gg_coherent_import",
            "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace", "gg_shard_map",
-           "gg_kernel_stats", "gg_round_exchange", "gg_coherent_run_ranks"]
+           "gg_kernel_stats", "gg_round_exchange", "gg_coherent_run_ranks", "gg_gen_stress_trace"]
 
 
 class _CStatus(ctypes.Structure):
@@ -108,10 +108,11 @@ def load():
     L.gg_shard_map.argtypes = [u32, u32, vp]
     L.gg_kernel_stats.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64)]
     L.gg_round_exchange.argtypes = [vp, vp, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(i32)]
+    L.gg_gen_stress_trace.argtypes = [vp, vp, u32, u32, u64, u64, u32, u32, u32, u32, u32, vp]
     L.gg_coherent_run_ranks.argtypes = [vp, vp, ctypes.POINTER(_Trace), vp, vp]
     for name in ["gg_kernel_stats", "gg_shard_map", "gg_coherent_begin", "gg_coherent_quantum", "gg_coherent_export",
                  "gg_coherent_import", "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace",
-                 "gg_round_exchange", "gg_coherent_run_ranks"]:
+                 "gg_round_exchange", "gg_coherent_run_ranks", "gg_gen_stress_trace"]:
         getattr(L, name).restype = i32
     for name in ["gg_reset", "gg_cache_access_batch", "gg_cache_get_counters", "gg_cache_get_line_info",
                  "gg_cache_set_line_info", "gg_cache_access_line", "gg_cache_insert_line",
@@ -334,6 +335,13 @@ def gen_hotspot_trace(addr, meta, tile_begin, tiles, per_tile, first=0, lines_lo
     """Fill device tensors with the configs[2..4] hotspot trace."""
     _check(load().gg_gen_hotspot_trace(_ptr(addr), _ptr(meta), tile_begin, tiles, per_tile, first, lines_log2,
                                        base_shift, hot_lines, hot_frac256, _stream(stream)))
+
+
+def gen_stress_trace(addr, meta, tile_begin, tiles, per_tile, num_tiles, first=0, lines_log2=15, base_shift=26,
+                     pool_lines=4096, pool_frac256=77, stream=None):
+    """Fill device tensors with the configs[4] coherent stress trace."""
+    _check(load().gg_gen_stress_trace(_ptr(addr), _ptr(meta), tile_begin, tiles, per_tile, first, lines_log2,
+                                      base_shift, num_tiles, pool_lines, pool_frac256, _stream(stream)))
 
 
 class CoherentEngine:

@@ -48,6 +48,41 @@ __global__ void k_gen_hotspot(uint64_t* addr, uint32_t* meta, uint32_t tile_begi
   meta[i] = ((((z >> 32) & 0xFF) % 3) == 0 ? GG_META_WRITE : 0u) | (gap << 1);
 }
 
+// configs[4] coherent stress generator (the same bit
+// recipe as oracle_gen_stress, the checker): WRITE p = 1/2; with p =
+// pool_frac256 / 256 a line of the shared pool [0, pool_lines) at byte 2^45,
+// else a private line.  Tiles fall into max(1, T/64) groups by a 32-bit hash
+// of the tile id; pool line L is shared by group L mod groups, and a tile's
+// pool accesses pick among its group's lines, so every pool line has ~64
+// sharers spread over the mesh.
+__host__ __device__ inline uint32_t stress_group(uint32_t t, uint32_t groups)
+{
+  uint32_t x = t + 0x9E3779B9u;                      // lowbias32
+  x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15; x *= 0x846CA68Bu; x ^= x >> 16;
+  return x % groups;
+}
+__global__ void k_gen_stress(uint64_t* addr, uint32_t* meta, uint32_t tile_begin, uint32_t tiles, uint64_t per_tile,
+                             uint64_t first, uint32_t lines_log2, uint32_t base_shift, uint32_t num_tiles,
+                             uint32_t pool_lines, uint32_t pool_frac256)
+{
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (uint64_t)tiles * per_tile) return;
+  const uint32_t t = tile_begin + (uint32_t)(i / per_tile);
+  const uint64_t k = first + i % per_tile;
+  uint64_t z = (0x9E3779B97F4A7C15ull ^ (uint64_t)t) + (k + 1) * 0x9E3779B97F4A7C15ull;   // SplitMix64
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  const uint32_t groups = num_tiles >= 128 ? num_tiles / 64 : 1;
+  const uint32_t per_group = pool_lines / groups ? pool_lines / groups : 1;
+  const bool pool = pool_lines && (((z >> 40) & 0xFF) < pool_frac256);
+  addr[i] = pool ? (1ull << 45) + (uint64_t)(stress_group(t, groups) + groups * ((uint32_t)(z & 0xFFFFFFFFull) % per_group)) * 64ull
+                 : ((uint64_t)t << base_shift) + ((z & ((1ull << lines_log2) - 1)) << 6);
+  const uint32_t gap = (uint32_t)__builtin_ctz((uint32_t)(((z >> 48) & 0xFF) | 0x100)) +
+                       (uint32_t)__builtin_ctz((uint32_t)(((z >> 56) & 0xFF) | 0x100));
+  meta[i] = (uint32_t)((z >> 32) & 1u) * GG_META_WRITE | (gap << 1);
+}
+
 int floor_log2(uint64_t n) { int p = -1; while (n) { n >>= 1; ++p; } return p; }
 bool is_pow2(uint64_t n) { return n && !(n & (n - 1)); }
 }  // namespace
@@ -376,6 +411,22 @@ gg_status gg_gen_uniform_trace(uint64_t* addr_dev, uint32_t* meta_dev, uint32_t 
   if (n == 0) return GG_OK;
   hipLaunchKernelGGL(k_gen_uniform, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      addr_dev, meta_dev, tile_begin, tiles, per_tile, first, lines_log2, base_shift);
+  GG_HIP(hipGetLastError());
+  return GG_OK;
+}
+
+gg_status gg_gen_stress_trace(uint64_t* addr_dev, uint32_t* meta_dev, uint32_t tile_begin, uint32_t tiles,
+                              uint64_t per_tile, uint64_t first, uint32_t lines_log2, uint32_t base_shift,
+                              uint32_t num_tiles, uint32_t pool_lines, uint32_t pool_frac256, void* stream)
+{
+  if (!addr_dev || !meta_dev || lines_log2 > 31 || pool_frac256 > 256 || (uint64_t)tile_begin + tiles > (1ull << 17) ||
+      pool_lines > (1u << 24))
+    return gg_fail(GG_ERR_INVALID, "gg_gen_stress_trace: bad arguments");
+  const uint64_t n = (uint64_t)tiles * per_tile;
+  if (!n) return GG_OK;
+  hipLaunchKernelGGL(k_gen_stress, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     addr_dev, meta_dev, tile_begin, tiles, per_tile, first, lines_log2, base_shift, num_tiles,
+                     pool_lines, pool_frac256);
   GG_HIP(hipGetLastError());
   return GG_OK;
 }

@@ -415,6 +415,17 @@ gg_status gg_gen_uniform_trace(uint64_t* addr_dev, uint32_t* meta_dev, uint32_t 
  * 1 << 44, else line z mod 2^lines_log2 at t << base_shift; WRITE iff
  * ((z >> 32) & 0xFF) % 3 == 0; gap = ctz(((z>>48)&0xFF)|0x100) +
  * ctz(((z>>56)&0xFF)|0x100) core cycles in meta bits 1..30.                 */
+/* configs[4] coherent stress trace: record i of tile t
+ * is z = SplitMix64(0x9E3779B97F4A7C15 ^ t) step first+i+1; WRITE iff bit 32 of
+ * z; with probability pool_frac256/256 (bits 40-47) line
+ * g(t) + G * ((z mod 2^32) mod (pool_lines / G)) of the shared pool at byte
+ * 2^45, where G = max(1, num_tiles / 64) groups and g(t) the tile's group
+ * (lowbias32 hash of t + 0x9E3779B9, mod G), so each pool line has ~64
+ * sharers; else line z mod 2^lines_log2 at byte t << base_shift; gap cycles as
+ * the hotspot trace.                                                         */
+gg_status gg_gen_stress_trace(uint64_t* addr_dev, uint32_t* meta_dev, uint32_t tile_begin, uint32_t tiles,
+                              uint64_t per_tile, uint64_t first, uint32_t lines_log2, uint32_t base_shift,
+                              uint32_t num_tiles, uint32_t pool_lines, uint32_t pool_frac256, void* stream);
 gg_status gg_gen_hotspot_trace(uint64_t* addr_dev, uint32_t* meta_dev, uint32_t tile_begin, uint32_t tiles,
                                uint64_t per_tile, uint64_t first, uint32_t lines_log2, uint32_t base_shift,
                                uint32_t hot_lines, uint32_t hot_frac256, void* stream);

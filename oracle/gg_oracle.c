@@ -77,6 +77,33 @@ void oracle_gen_hotspot(uint32_t tile, uint64_t first, uint64_t n, uint32_t line
   }
 }
 
+/* configs[4] coherent stress generator: the recipe of gg_gen_stress_trace
+ * (include/graphite_gpu.h).  Synthetic workload of the
+ * SURVEY.md §8d config 5 description, not a reference algorithm.           */
+static uint32_t stress_group(uint32_t t, uint32_t groups)
+{
+  uint32_t x = t + 0x9E3779B9u;
+  x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15; x *= 0x846CA68Bu; x ^= x >> 16;
+  return x % groups;
+}
+void oracle_gen_stress(uint32_t tile, uint64_t first, uint64_t n, uint32_t lines_log2, uint32_t base_shift,
+                       uint32_t num_tiles, uint32_t pool_lines, uint32_t pool_frac256, uint64_t* addr, uint32_t* meta)
+{
+  const uint64_t seed = 0x9E3779B97F4A7C15ull ^ (uint64_t)tile;
+  const uint64_t mask = (1ull << lines_log2) - 1;
+  const uint32_t groups = num_tiles >= 128 ? num_tiles / 64 : 1;
+  const uint32_t per_group = pool_lines / groups ? pool_lines / groups : 1;
+  for (uint64_t k = 0; k < n; ++k) {
+    uint64_t z = oracle_splitmix64_at(seed, first + k);
+    int pool = pool_lines && (((z >> 40) & 0xFF) < pool_frac256);
+    if (pool) addr[k] = (1ull << 45) + (uint64_t)(stress_group(tile, groups) + groups * ((uint32_t)(z & 0xFFFFFFFFull) % per_group)) * 64ull;
+    else addr[k] = ((uint64_t)tile << base_shift) + ((z & mask) << 6);
+    uint32_t gap = (uint32_t)__builtin_ctz((uint32_t)(((z >> 48) & 0xFF) | 0x100)) +
+                   (uint32_t)__builtin_ctz((uint32_t)(((z >> 56) & 0xFF) | 0x100));
+    meta[k] = (uint32_t)((z >> 32) & 1u) * GG_META_WRITE | (gap << 1);
+  }
+}
+
 /* Core::initiateMemoryAccess line split (common/tile/core/core.cc:167-201) */
 uint32_t oracle_split_lines(uint64_t addr, uint32_t size, uint32_t line, uint64_t* lines, uint32_t cap)
 {

@@ -38,6 +38,9 @@ void oracle_gen_hotspot(uint32_t tile, uint64_t first, uint64_t n, uint32_t line
                         uint32_t base_shift, uint32_t hot_lines, uint32_t hot_frac256,
                         uint64_t* addr, uint32_t* meta);
 
+void oracle_gen_stress(uint32_t tile, uint64_t first, uint64_t n, uint32_t lines_log2, uint32_t base_shift,
+                       uint32_t num_tiles, uint32_t pool_lines, uint32_t pool_frac256, uint64_t* addr, uint32_t* meta);
+
 /* ---------------- private cache replay (mode P) ---------------------------- */
 typedef struct oracle_cache oracle_cache;
 oracle_cache* oracle_cache_create(const gg_config* cfg);

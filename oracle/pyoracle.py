@@ -71,6 +71,8 @@ def lib():
         L.oracle_split_lines.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _u64p, ctypes.c_uint32]
         L.oracle_gen_hotspot.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u64p, _u32p]
+        L.oracle_gen_stress.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                        ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u64p, _u32p]
         L.oracle_shard_map.restype = ctypes.c_int
         L.oracle_shard_map.argtypes = [ctypes.c_uint32, ctypes.c_uint32, _u32p]
         L.oracle_coh_run_parallel.restype = ctypes.c_int
@@ -112,6 +114,23 @@ def gen_hotspot(tile, first, n, lines_log2=15, base_shift=26, hot_lines=64, hot_
     meta = np.empty(n, np.uint32)
     lib().oracle_gen_hotspot(tile, first, n, lines_log2, base_shift, hot_lines, hot_frac256, addr, meta)
     return addr, meta
+
+
+def gen_stress(tile, first, n, num_tiles, lines_log2=15, base_shift=26, pool_lines=4096, pool_frac256=77):
+    """configs[4] stress records of one tile (oracle_gen_stress)."""
+    addr = np.zeros(n, np.uint64)
+    meta = np.zeros(n, np.uint32)
+    lib().oracle_gen_stress(tile, first, n, lines_log2, base_shift, num_tiles, pool_lines, pool_frac256, addr, meta)
+    return addr, meta
+
+
+def gen_stress_trace(tiles, per_tile, **kw):
+    """Tile-major configs[4] stress trace of `tiles` tiles x `per_tile` records + offsets."""
+    parts = [gen_stress(t, 0, per_tile, tiles, **kw) for t in range(tiles)]
+    addr = np.concatenate([p[0] for p in parts]) if parts else np.zeros(0, np.uint64)
+    meta = np.concatenate([p[1] for p in parts]) if parts else np.zeros(0, np.uint32)
+    offs = np.arange(tiles + 1, dtype=np.uint64) * np.uint64(per_tile)
+    return addr, meta, offs
 
 
 def gen_trace(tiles, per_tile, **kw):

@@ -136,6 +136,35 @@ def test_gpu_hotspot_generator_matches_oracle():
     np.testing.assert_array_equal(to_np(meta, np.uint32), m)
 
 
+def test_gpu_stress_generator_matches_oracle():
+    """configs[4] stress generator: device (gg_gen_stress_trace) == oracle (oracle_gen_stress)."""
+    torch = torch_dev()
+    from graphite_amd import backend as B
+    from oracle import pyoracle as po
+    T0, T, N, TT = 1000, 24, 3000, 4096
+    addr = torch.empty(T * N, dtype=torch.int64, device="cuda")
+    meta = torch.empty(T * N, dtype=torch.int32, device="cuda")
+    B.gen_stress_trace(addr, meta, T0, T, N, TT, first=7)
+    parts = [po.gen_stress(t, 7, N, TT) for t in range(T0, T0 + T)]
+    np.testing.assert_array_equal(to_np(addr, np.uint64), np.concatenate([p[0] for p in parts]))
+    np.testing.assert_array_equal(to_np(meta, np.uint32), np.concatenate([p[1] for p in parts]))
+
+
+@pytest.mark.parametrize("T,N,K,net", [
+    (4096, 12, 1, C.NET_EMESH_HOP_COUNTER),     # configs[4]: 4096 tiles, 16-way L2 (reduced length)
+    (4096, 8, 8, C.NET_EMESH_HOP_COUNTER),
+    (1024, 24, 8, C.NET_EMESH_HOP_BY_HOP),      # the stress pool under router contention, 8 shards
+])
+def test_coherent_stress_matches_oracle(T, N, K, net):
+    """configs[4] coherent stress workload (50/50 R/W,
+    30 % of accesses to a 4096-line pool shared by ~64-tile groups), 16-way
+    L2: bit-exact against the oracle."""
+    from oracle import pyoracle as po
+    cfg = C.default_config(T, l2_assoc=16, num_shards=K, net_model=net)
+    a, m, o = po.gen_stress_trace(T, N)
+    _compare(cfg, a, m, o)
+
+
 @pytest.mark.parametrize("net", [C.NET_EMESH_HOP_BY_HOP, C.NET_EMESH_HOP_COUNTER])
 def test_coherent_contexts_split_equals_one_context(net):
     """1 context x 8 logical shards == 2 contexts x 4 shards each (exchanging
