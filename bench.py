@@ -93,14 +93,15 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0, help="all-core oracle threads (0 = one per shard, <= cores)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
-    p.add_argument("--sections", default="hop_counter,fft,private,noc,stress",
+    p.add_argument("--sections", default="hop_counter,stress,fft,private,private_16way,noc",
                    help="extra sections at N = 1 (comma list; '' = none)")
     p.add_argument("--hc-per-tile", type=int, default=1024, help="hop_counter section: accesses per tile")
     p.add_argument("--private-per-tile", type=int, default=1 << 20)
     p.add_argument("--cpu-sample-tiles", type=int, default=480, help="private section: tile replays of its CPU sample")
     p.add_argument("--replay-kernel", type=int, default=0)
     p.add_argument("--stress-tiles", type=int, default=4096)
-    p.add_argument("--stress-per-tile", type=int, default=1 << 18)
+    p.add_argument("--stress-per-tile", type=int, default=64, help="configs[4] coherent stress: records per tile")
+    p.add_argument("--private16-per-tile", type=int, default=1 << 18)
     p.add_argument("--noc-packets", type=int, default=1 << 18)
     p.add_argument("--noc-tiles", type=int, default=1024)
     p.add_argument("--fft-m", type=int, default=14,
@@ -123,17 +124,20 @@ def maybe_spawn(args):
     sys.exit(subprocess.call(cmd))
 
 
-def coherent_workload(T, N, H, dev):
+def coherent_workload(T, N, H, dev, workload="hotspot"):
     import torch
     from graphite_amd import backend as B
     addr = torch.empty(T * N, dtype=torch.int64, device=dev)
     meta = torch.empty(T * N, dtype=torch.int32, device=dev)
-    B.gen_hotspot_trace(addr, meta, 0, T, N, hot_lines=H)
+    if workload == "stress":
+        B.gen_stress_trace(addr, meta, 0, T, N, T)
+    else:
+        B.gen_hotspot_trace(addr, meta, 0, T, N, hot_lines=H)
     offs = np.arange(T + 1, dtype=np.uint64) * np.uint64(N)
     return addr, meta, offs
 
 
-def coherent_run(args, T, N, H, K, net, world, rank, dev, steps, warmup, verify, cpu):
+def coherent_run(args, T, N, H, K, net, world, rank, dev, steps, warmup, verify, cpu, workload="hotspot", l2_assoc=8):
     """One measurement of Mode C: `warmup` untimed + `steps` timed whole runs,
     barrier + synchronize around the timed region, max over ranks."""
     import torch
@@ -142,10 +146,10 @@ def coherent_run(args, T, N, H, K, net, world, rank, dev, steps, warmup, verify,
     from graphite_amd import coherent as CO
     from graphite_amd import dist as D
     k0, k1 = CO.shard_range(rank, world, K)
-    cfg = C.default_config(T, num_shards=K, shard_begin=k0, shard_end=k1, net_model=net)
+    cfg = C.default_config(T, num_shards=K, shard_begin=k0, shard_end=k1, net_model=net, l2_assoc=l2_assoc)
     be = B.Backend(cfg)
     be.set_timing(True)
-    addr, meta, offs = coherent_workload(T, N, H, dev)
+    addr, meta, offs = coherent_workload(T, N, H, dev, workload)
     out = torch.zeros(T * N, dtype=torch.int64, device=dev)
 
     def step():
@@ -193,7 +197,7 @@ def coherent_run(args, T, N, H, K, net, world, rank, dev, steps, warmup, verify,
         from oracle import pyoracle as po
         a = addr.cpu().numpy().view(np.uint64)
         m = meta.cpu().numpy().view(np.uint32)
-        ocfg = C.default_config(T, num_shards=K, net_model=net)
+        ocfg = C.default_config(T, num_shards=K, net_model=net, l2_assoc=l2_assoc)
         threads = args.cpu_threads or max(1, min(K, os.cpu_count() or 1))
         c0 = time.perf_counter()
         ref = po.coherent_run_parallel(ocfg, a, m, offs, threads)
@@ -342,7 +346,25 @@ def noc_section(args, dev):
 
 
 def stress_section(args, dev):
-    """configs[4] geometry in Mode P (its private part): 4096 tiles,
+    """configs[4] coherent stress workload: 4096 tiles
+    (64 x 64), 16-way L2 (512 sets), MSI + DRAM + emesh_hop_counter (the memory
+    network of carbon_sim.cfg), 8 logical shards; the stress trace (WRITE p =
+    1/2, 30 % of accesses to a 4096-line pool shared by ~64-tile groups) at
+    --stress-per-tile records per tile.  One warm-up run, one timed; bit-exact
+    against the all-core oracle, which is the CPU baseline with the 1-thread
+    oracle beside it."""
+    from graphite_amd import config as C
+    T, N, K = args.stress_tiles, args.stress_per_tile, 8
+    r = coherent_run(args, T, N, 0, K, C.NET_EMESH_HOP_COUNTER, 1, 0, dev, 1, 1, not args.no_verify,
+                     not args.no_cpu_baseline, workload="stress", l2_assoc=16)
+    r["workload"] = ("configs[4]: %d tiles x %d stress accesses (WRITE p=1/2, 30%% to a 4096-line pool, ~64 sharers "
+                     "per pool line), 16-way L2, MSI + DRAM + emesh_hop_counter, %d logical shards" % (T, N, K))
+    r["unit"] = "accesses/s"
+    return r
+
+
+def private16_section(args, dev):
+    """configs[4] cache geometry in Mode P (the private part): 4096 tiles,
     32KB/4w L1-D + 512KB/16w L2 (512 sets), 2^18 accesses per tile from the
     configs[1] uniform-random private generator (WRITE p = 1/3).  16-way L2
     sets do not fit the streaming kernel's LDS budget, so the batch runs the
@@ -353,7 +375,7 @@ def stress_section(args, dev):
     from graphite_amd import config as C
     from graphite_amd import backend as B
     from oracle import pyoracle as po
-    T, N = args.stress_tiles, args.stress_per_tile
+    T, N = args.stress_tiles, args.private16_per_tile
     cfg = C.default_config(T, l2_assoc=16)
     be = B.Backend(cfg)
     be.set_timing(True)
@@ -587,6 +609,8 @@ def main():
                 r = noc_section(args, dev)
             elif name == "stress" and args.stress_tiles:
                 r = stress_section(args, dev)
+            elif name == "private_16way" and args.stress_tiles:
+                r = private16_section(args, dev)
             else:
                 continue
         except Exception as e:            # a section failing must not hide the headline
