@@ -50,6 +50,7 @@
 #include "gg_dev.h"
 
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <cstring>
 #include <cstdlib>
@@ -102,6 +103,7 @@ struct CP {
   uint32_t net, nsx, nsy, mw, mh, qimg;  // network model; X / Y segments; mesh; bytes of a queue image
   uint32_t msg_cap, seg_cap, walk_pk;    // pool records per parity; entries per segment list; walker LDS packets
   uint32_t seg_xcd;                      // > 0: runs interleaved by shard (seg_xcd shards), XCD-grouped walker blocks
+  uint32_t cache_lds_off, cache_lds_bytes; // k_c_persist<true>: the tile's cache state in LDS after the step's
   uint64_t lat_l1d, lat_l1t, lat_l2d, lat_l2t, lat_dir, gap_ps, dram_proc, dram_cost;
   NocParams np;
 };
@@ -135,6 +137,7 @@ struct CS {
   uint64_t* ctr;                         // NoC counters [T][GG_NUM_NET_COUNTERS]
   uint64_t* gscr;                        // [L][5 * IC] ordering scratch beyond kInLds
   unsigned long long* prof;              // GG_COH_PROFILE=1: shader-clock cycles per phase (diagnostics)
+  uint32_t* gbar;                        // grid barrier counter of k_c_persist
 };
 // profile slots: step phases 0..5 summed over tiles, 8 = sum over steps of the slowest tile;
 // walker: 16 staging+load, 17 event loop, 18 hand-off+write back, 19 events, 20 sum of slowest walker per launch (X),
@@ -149,6 +152,8 @@ __device__ __forceinline__ uint32_t* arv(const CS& S, uint32_t p) { return p ? S
 __device__ __forceinline__ uint32_t* narv(const CS& S, uint32_t p) { return p ? S.narv1 : S.narv0; }
 
 __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) { return (uint64_t)__shfl((long long)v, src); }
+// lane l's value for a wave-uniform l (v_readlane, no LDS permute)
+__device__ __forceinline__ uint32_t rl32(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 {
 #pragma unroll
@@ -203,6 +208,7 @@ struct Cache {
   uint32_t cset; uint64_t ctv; uint32_t cmv;
 
   __device__ __forceinline__ void cnt(uint32_t k) { if (ln == k) ++cd; }
+  __device__ __forceinline__ void cnt_add(uint32_t k, uint32_t v) { if (ln == k) cd += v; }
   __device__ __forceinline__ uint32_t set_of(uint64_t a) const { return (uint32_t)((a >> log_line) & (sets - 1)); }   // cache_hash_fn.h:17
   __device__ __forceinline__ uint64_t tag_of(uint64_t a) const { return a >> log_line; }                             // cache.cc:495
   __device__ __forceinline__ void ld(uint32_t s, uint64_t& tv, uint32_t& mv)
@@ -233,7 +239,7 @@ struct Cache {
   __device__ __forceinline__ void touch(uint32_t s, int w, uint32_t mv)                                           // lru:40-50
   {
     if (pol != GG_POLICY_LRU) return;
-    const uint32_t acc = (uint32_t)__shfl((int)mv, w) >> 3;
+    const uint32_t acc = rl32(mv, (uint32_t)w) >> 3;
     if (ln < ways) {
       const uint32_t a = mv >> 3;
       uint32_t nv = mv;
@@ -255,7 +261,7 @@ struct Cache {
     ld(set_of(a), tv, mv);
     const int w = way_of(tv, tag_of(a));
     cnt(GG_CC_TAG_READS);
-    if (w >= 0) { const uint32_t m = (uint32_t)__shfl((int)mv, w); st = m & 3u; loc = (m >> 2) & 1u; }
+    if (w >= 0) { const uint32_t m = rl32(mv, (uint32_t)w); st = m & 3u; loc = (m >> 2) & 1u; }
     else { st = ST_I; loc = 0; }
   }
   // setCacheLineInfo (cache.cc:218-241): st == I writes the invalid tag (CacheLineInfo::invalidate)
@@ -304,8 +310,8 @@ struct Cache {
       w = (int)cur;
     }
     if (w < 0 || (uint32_t)w >= ways) return false;
-    const uint64_t vt = shfl64(tv, w);
-    const uint32_t vm = (uint32_t)__shfl((int)mv, w);
+    const uint64_t vt = rl64(tv, (uint32_t)w);
+    const uint32_t vm = rl32(mv, (uint32_t)w);
     ev = vt != INV_ADDR;
     if (ev) { ev_addr = vt << log_line; ev_st = vm & 3u; ev_loc = (vm >> 2) & 1u; }
     if ((int)ln == w) {
@@ -360,13 +366,30 @@ struct Tile {
   bool failed;
   uint64_t ccv, stv;                    // lane k's cache counter k (of 2 x 12) and statistic k, loaded at step start
 
-  __device__ __forceinline__ Tile(const CP& P_, const CS& S_, uint32_t l, uint32_t par, StepLds& s_)
+  // LC: the tile's L1-D / L2 tags, meta bytes and RR counters live in LDS at
+  // clds for the whole launch (k_c_persist; layout of cache_lds_bytes)
+  template <bool LC>
+  __device__ __forceinline__ Tile(const CP& P_, const CS& S_, uint32_t l, uint32_t par, StepLds& s_, uint8_t* clds,
+                                  std::integral_constant<bool, LC>)
       : P(P_), S(S_), lt(l), tile(S_.gtile[l]), ln(lane_id()), p(par), sl(s_)
   {
-    L1 = Cache{S.l1_tag + (size_t)lt * P.s1 * P.a1, S.l1_meta + (size_t)lt * P.s1 * P.a1, S.l1_rr + (size_t)lt * P.s1,
-               S.cc + (size_t)lt * 2 * GG_NUM_CACHE_COUNTERS, P.s1, P.a1, P.log_line, P.pol1, 0, ln, 0, ~0u, 0, 0};
-    L2 = Cache{S.l2_tag + (size_t)lt * P.s2 * P.a2, S.l2_meta + (size_t)lt * P.s2 * P.a2, S.l2_rr + (size_t)lt * P.s2,
-               S.cc + ((size_t)lt * 2 + 1) * GG_NUM_CACHE_COUNTERS, P.s2, P.a2, P.log_line, P.pol2, 1, ln, 0, ~0u, 0, 0};
+    const size_t n1 = (size_t)P.s1 * P.a1, n2 = (size_t)P.s2 * P.a2;
+    if constexpr (LC) {
+      uint64_t* t1 = reinterpret_cast<uint64_t*>(clds);
+      uint64_t* t2 = t1 + n1;
+      uint8_t* m1 = reinterpret_cast<uint8_t*>(t2 + n2);
+      uint8_t* m2 = m1 + n1;
+      uint8_t* r1 = m2 + n2;
+      uint8_t* r2 = r1 + P.s1;
+      L1 = Cache{t1, m1, r1, S.cc + (size_t)lt * 2 * GG_NUM_CACHE_COUNTERS, P.s1, P.a1, P.log_line, P.pol1, 0, ln, 0, ~0u, 0, 0};
+      L2 = Cache{t2, m2, r2, S.cc + ((size_t)lt * 2 + 1) * GG_NUM_CACHE_COUNTERS, P.s2, P.a2, P.log_line, P.pol2, 1, ln, 0,
+                 ~0u, 0, 0};
+    } else {
+      L1 = Cache{S.l1_tag + lt * n1, S.l1_meta + lt * n1, S.l1_rr + (size_t)lt * P.s1,
+                 S.cc + (size_t)lt * 2 * GG_NUM_CACHE_COUNTERS, P.s1, P.a1, P.log_line, P.pol1, 0, ln, 0, ~0u, 0, 0};
+      L2 = Cache{S.l2_tag + lt * n2, S.l2_meta + lt * n2, S.l2_rr + (size_t)lt * P.s2,
+                 S.cc + ((size_t)lt * 2 + 1) * GG_NUM_CACHE_COUNTERS, P.s2, P.a2, P.log_line, P.pol2, 1, ln, 0, ~0u, 0, 0};
+    }
     sd = 0;
     rec = S.rec[lt]; rec_end = S.rec_end[lt]; clk = S.clk[lt]; pend_start = S.pend_start[lt];
     out_addr = S.out_addr[lt]; out_time = S.out_time[lt];
@@ -832,6 +855,66 @@ struct Tile {
     clk = end;
     rec = r + 1;
   }
+  // A run of L1 hits, one record per lane (records wbase + lane, window from
+  // lane o).  Until the next miss nothing changes the L1 tags or states (a hit
+  // only ages the LRU bits), so every lane looks its record up at once; the
+  // issue times are a prefix sum (s = clk + gap, clk = s + lat_l1d on a hit);
+  // the leading run of hits before the lax barrier is then retired in order:
+  // the LRU touches (L1, and L2 for write-through stores) one by one, the
+  // counters, statistics and access words in bulk.  Exactly app_access's hit
+  // path applied record by record.  Returns the number of records retired.
+  __device__ __forceinline__ uint32_t l1_hit_run(uint64_t wbase, uint32_t o, uint64_t wa, uint32_t wm, uint64_t line_mask,
+                                                 uint64_t barrier)
+  {
+    const uint64_t a = wa & line_mask;
+    const bool wr = (wm & GG_META_WRITE) != 0;
+    const bool mine = ln >= o && wbase + ln < rec_end;
+    bool hit = false;
+    if (mine) {
+      const uint32_t st = L1.set_of(a);
+      const uint64_t tg = L1.tag_of(a);
+      const uint64_t* tr = L1.tag + (size_t)st * L1.ways;
+      int fw = -1;
+#pragma unroll 8
+      for (uint32_t w = 0; w < L1.ways; ++w) fw = tr[w] == tg ? (int)w : fw;   // independent loads, tags unique
+      if (fw >= 0) {
+        const uint32_t cs = L1.meta[(size_t)st * L1.ways + fw] & 3u;
+        hit = wr ? cs == ST_M : cs != ST_I;
+      }
+    }
+    // inclusive prefix sum of gap + lat_l1d over the window
+    uint64_t e = mine ? (uint64_t)((wm & 0x7FFFFFFFu) >> 1) * P.gap_ps + P.lat_l1d : 0;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t v = shfl64(e, (int)ln - d);
+      if ((int)ln >= d) e += v;
+    }
+    e += clk;                                                        // this record's end time if all before it hit
+    const bool ok = mine && hit && e - P.lat_l1d < barrier;
+    const uint64_t m = __ballot(ok) >> o;
+    const uint32_t n = ~m ? (uint32_t)__builtin_ctzll(~m) : 64u - o;
+    if (!n) return 0;
+    uint32_t nw = 0;
+    for (uint32_t k = 0; k < n && !failed; ++k) {
+      const uint32_t l = o + k;
+      const uint64_t ak = rl64(a, l);
+      const bool wk = (__builtin_amdgcn_readlane((int)wm, (int)l) & GG_META_WRITE) != 0;
+      nw += wk;
+      l1_access(ak, wk);
+    }
+    const uint32_t nr = n - nw;
+    L1.cnt_add(GG_CC_TAG_READS, n);
+    L1.cnt_add(GG_CC_ACCESSES, n);
+    L1.cnt_add(GG_CC_READ_ACCESSES, nr);
+    L1.cnt_add(GG_CC_WRITE_ACCESSES, nw);
+    if (S.out && ln >= o && ln < o + n) S.out[wbase + ln] = ((uint64_t)P.lat_l1d << 2) | GG_LVL_L1;
+    stat(GG_CT_ACCESSES, n);
+    stat(GG_CT_LATENCY_PS, (uint64_t)n * P.lat_l1d);
+    stat(GG_CT_L1_HITS, n);
+    clk = rl64(e, o + n - 1);
+    rec += n;
+    return n;
+  }
   // Core::initiateMemoryAccess -> L1CacheCntlr::processMemOpFromCore, first attempt (l1:89-180)
   __device__ __forceinline__ void app_access(uint64_t a, bool wr, uint64_t s)
   {
@@ -1113,7 +1196,13 @@ __device__ __forceinline__ void quantum_end(const CP& P, const CS& S, uint32_t L
 // devloop: the quantum, its barrier and the step index come from S.qs (the
 // quantum loop runs on the device, gg_coherent_run); otherwise the host
 // drives one quantum (gg_coherent_quantum) and L is the step index.
-__global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t L, uint32_t devloop, uint64_t barrier_arg)
+// the tile's trace window: records wbase + lane (kept across the steps of a
+// persistent launch; the records are read-only for the whole run)
+struct TraceWin { uint64_t wbase, wa; uint32_t wm; };
+
+template <bool LC>
+__device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, uint32_t devloop, uint64_t barrier_arg,
+                                          TraceWin& W)
 {
   const uint32_t ln = threadIdx.x, lt = blockIdx.x;
   PROF_T0();
@@ -1148,7 +1237,7 @@ __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t L, uint32_t 
   }
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   StepLds& sl = *reinterpret_cast<StepLds*>(smem);
-  Tile T(P, S, lt, p, sl);
+  Tile T(P, S, lt, p, sl, smem + P.cache_lds_off, std::integral_constant<bool, LC>());
   const gg_cmsg* prev = pool(S, p ^ 1u);     // records delivered to this step
   uint64_t* gscr = S.gscr + (size_t)lt * 5 * P.IC;
   // NoC counters of the SELF port (lanes 0-6) and of the receiver
@@ -1273,8 +1362,8 @@ __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t L, uint32_t 
   // ---- 2. the trace (records fetched 64 at a time, one per lane)
   {
     const uint64_t line_mask = ~((1ull << P.log_line) - 1);
-    uint64_t wbase = ~0ull, wa = 0;
-    uint32_t wm = 0;
+    uint64_t wbase = W.wbase, wa = W.wa;
+    uint32_t wm = W.wm;
     while (!T.blocked && !T.failed) {
       const uint64_t r = T.rec;
       if (r >= T.rec_end) break;
@@ -1284,11 +1373,19 @@ __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t L, uint32_t 
         if (r + ln < T.rec_end) { wa = S.addr[r + ln]; wm = S.meta[r + ln]; }
       }
       const int o = (int)(r - wbase);
-      const uint32_t meta = (uint32_t)__shfl((int)wm, o);
+      PROF_AT(_h0);
+      const uint32_t nh = T.l1_hit_run(wbase, (uint32_t)o, wa, wm, line_mask, barrier);
+      PROF_AT(_h1);
+      if (S.prof && ln == 0) { atomicAdd(&S.prof[33], (unsigned long long)(_h1 - _h0)); atomicAdd(&S.prof[34], (unsigned long long)nh); }
+      if (nh) continue;
+      const uint32_t meta = rl32(wm, (uint32_t)o);
       const uint64_t s = T.clk + (uint64_t)((meta & 0x7FFFFFFFu) >> 1) * P.gap_ps;
       if (s >= barrier) break;
-      T.app_access(shfl64(wa, o) & line_mask, (meta & GG_META_WRITE) != 0, s);
+      T.app_access(rl64(wa, (uint32_t)o) & line_mask, (meta & GG_META_WRITE) != 0, s);
+      PROF_AT(_h2);
+      if (S.prof && ln == 0) { atomicAdd(&S.prof[35], (unsigned long long)(_h2 - _h1)); atomicAdd(&S.prof[36], 1ull); }
     }
+    W.wbase = wbase; W.wa = wa; W.wm = wm;
   }
 
   PROF_AT(_p3);
@@ -1466,19 +1563,25 @@ __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t L, uint32_t 
   }
 }
 
+__global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t L, uint32_t devloop, uint64_t barrier_arg)
+{
+  TraceWin W{~0ull, 0, 0};
+  step_body<false>(P, S, L, devloop, barrier_arg, W);
+}
+
 // ---------------------------------------------------------------------------
 // hop-by-hop: one wave per X (stage 0) or Y (stage 1) segment
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_c_walk(CP P, CS S, uint32_t L, int stage)
+__device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, int stage, uint32_t blk)
 {
   const uint32_t live = ((volatile uint32_t*)S.live)[L & 3];
   if (!live) return;                                 // launch L was no step
   // block -> (run slot, direction): with runs interleaved by shard, block b
   // takes slot (b mod ns) + ns * (b div 2ns) in direction (b div ns) & 1, so
   // every block of shard k is k mod ns (the XCD of its tiles' blocks)
-  uint32_t sg = blockIdx.x;
+  uint32_t sg = blk;
   if (P.seg_xcd) {
-    const uint32_t ns = P.seg_xcd, b = blockIdx.x;
+    const uint32_t ns = P.seg_xcd, b = blk;
     sg = 2 * ((b % ns) + ns * (b / (2 * ns))) + ((b / ns) & 1u);
   }
   const uint32_t ln = threadIdx.x, p = (live - 1) & 1u;
@@ -1688,6 +1791,85 @@ __global__ void __launch_bounds__(64) k_c_walk(CP P, CS S, uint32_t L, int stage
   }
 }
 
+__global__ void __launch_bounds__(64) k_c_walk(CP P, CS S, uint32_t L, int stage)
+{
+  walk_body(P, S, L, stage, blockIdx.x);
+}
+
+// A barrier of every workgroup of the launch (one wave each): release of the
+// wave's stores, an arrival count, a relaxed poll, an acquire
+// (MI355X_MICROARCH.md, inter-workgroup visibility).  The poll is bounded: a
+// barrier that never completes flags GG_DERR_STATE instead of hanging.
+__device__ __forceinline__ void grid_sync(const CS& S, uint32_t& gen)
+{
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ++gen;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(S.gbar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t target = gen * gridDim.x;
+    for (uint32_t spin = 0; __hip_atomic_load(S.gbar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spin) {
+      if (spin > (1u << 24)) { atomicOr(S.err, GG_DERR_STATE); break; }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+// Small meshes (P.L <= kPersistTiles): the device-driven loop of
+// gg_coherent_run in ONE launch — launch indices [L0, L1) of step + X walk +
+// Y walk, separated by grid barriers instead of kernel boundaries.  Every
+// workgroup holds one owned tile (its step) and walks runs b, b + grid, ...
+// LC (closed-form networks): the workgroup's tile keeps its L1-D / L2 state in
+// LDS for the whole launch, loaded at the start, written back at the end.
+template <bool LC>
+__device__ __forceinline__ void cache_state_copy(const CP& P, const CS& S, uint32_t lt, uint8_t* clds, bool in)
+{
+  const size_t n1 = (size_t)P.s1 * P.a1, n2 = (size_t)P.s2 * P.a2;
+  uint64_t* t1 = reinterpret_cast<uint64_t*>(clds);
+  uint64_t* t2 = t1 + n1;
+  uint8_t* m1 = reinterpret_cast<uint8_t*>(t2 + n2);
+  uint8_t* m2 = m1 + n1;
+  uint8_t* r1 = m2 + n2;
+  uint8_t* r2 = r1 + P.s1;
+  uint64_t* g1 = S.l1_tag + lt * n1; uint64_t* g2 = S.l2_tag + lt * n2;
+  uint8_t* gm1 = S.l1_meta + lt * n1; uint8_t* gm2 = S.l2_meta + lt * n2;
+  uint8_t* gr1 = S.l1_rr + (size_t)lt * P.s1; uint8_t* gr2 = S.l2_rr + (size_t)lt * P.s2;
+  for (size_t i = threadIdx.x; i < n1; i += 64) { if (in) { t1[i] = g1[i]; m1[i] = gm1[i]; } else { g1[i] = t1[i]; gm1[i] = m1[i]; } }
+  for (size_t i = threadIdx.x; i < n2; i += 64) { if (in) { t2[i] = g2[i]; m2[i] = gm2[i]; } else { g2[i] = t2[i]; gm2[i] = m2[i]; } }
+  for (size_t i = threadIdx.x; i < P.s1; i += 64) { if (in) r1[i] = gr1[i]; else gr1[i] = r1[i]; }
+  for (size_t i = threadIdx.x; i < P.s2; i += 64) { if (in) r2[i] = gr2[i]; else gr2[i] = r2[i]; }
+  __syncthreads();
+}
+
+template <bool LC>
+__global__ void __launch_bounds__(64) k_c_persist(CP P, CS S, uint32_t L0, uint32_t L1)
+{
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const bool hbh = P.net == GG_NET_EMESH_HOP_BY_HOP;
+  uint32_t gen = 0;
+  TraceWin W{~0ull, 0, 0};
+  if (LC) cache_state_copy<LC>(P, S, blockIdx.x, smem + P.cache_lds_off, true);
+  for (uint32_t L = L0; L < L1; ++L) {
+    step_body<LC>(P, S, L, 1u, 0, W);
+    grid_sync(S, gen);
+    if (hbh) {
+      for (uint32_t b = blockIdx.x; b < P.nsx; b += gridDim.x) walk_body(P, S, L, 0, b);
+      grid_sync(S, gen);
+      for (uint32_t b = blockIdx.x; b < P.nsy; b += gridDim.x) walk_body(P, S, L, 1, b);
+      grid_sync(S, gen);
+    }
+    const uint64_t done = __hip_atomic_load(&S.qs[QS_DONE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t e = __hip_atomic_load(S.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (done || e) break;
+  }
+  if (LC) cache_state_copy<LC>(P, S, blockIdx.x, smem + P.cache_lds_off, false);
+}
+
 // Deliver a record of the quantum boundary: a message into the inbox of the
 // quantum's first step (records in pool 1), a held packet back into the walk
 // of that step (records in pool 0): the X / Y segment at its router, or the
@@ -1814,6 +1996,7 @@ struct gg_coh_state {
   uint64_t* offs_dev = nullptr;
   uint64_t n_records = 0;
   size_t step_lds = 0, walk_lds = 0;
+  bool persist_lc = false;
   bool begun = false;
   // live kernel timing (gg_set_timing): an event pair around every
   // kTimeSample-th launch of each kernel (a pair around every launch costs
@@ -1822,12 +2005,14 @@ struct gg_coh_state {
   std::vector<hipEvent_t> tev;
   std::vector<int> tkind;
   uint32_t tused = 0;
-  double ksum[3] = {0, 0, 0};
-  uint64_t kcnt[3] = {0, 0, 0};      // timed launches
-  uint64_t nlaunch[3] = {0, 0, 0};   // all launches
+  double ksum[4] = {0, 0, 0, 0};
+  uint64_t kcnt[4] = {0, 0, 0, 0};      // timed launches
+  uint64_t nlaunch[4] = {0, 0, 0, 0};   // all launches
 };
 constexpr uint64_t kTimeSample = 16;
-static const char* kKernelNames[3] = {"coherent_step", "coherent_walk_x", "coherent_walk_y"};
+constexpr uint32_t kPersistTiles = 64;        // owned tiles up to which gg_coherent_run uses k_c_persist
+constexpr uint32_t kPersistLaunches = 16384;  // launch indices per k_c_persist launch
+static const char* kKernelNames[4] = {"coherent_step", "coherent_walk_x", "coherent_walk_y", "coherent_persist"};
 
 template <class F> static void timed_launch(gg_ctx* ctx, gg_coh_state* C, hipStream_t s, int kind, F&& fn)
 {
@@ -1860,7 +2045,7 @@ uint64_t gg_coherent_msg_cap(gg_ctx* ctx) { return ctx->coh ? ctx->coh->P.msg_ca
 gg_status gg_coh_kernel_stats(gg_ctx* ctx, const char* name, double* total_ms, uint64_t* launches)
 {
   gg_coh_state* C = ctx->coh;
-  for (int k = 0; k < 3; ++k)
+  for (int k = 0; k < 4; ++k)
     if (C && std::strcmp(name, kKernelNames[k]) == 0) {
       *total_ms = C->kcnt[k] ? C->ksum[k] / (double)C->kcnt[k] * (double)C->nlaunch[k] : 0.0;
       *launches = C->nlaunch[k];
@@ -2045,9 +2230,21 @@ static gg_status coh_alloc(gg_ctx* ctx)
   }
   P.seg_cap = P.msg_cap;
   C->step_lds = sizeof(StepLds);
+  {
+    // cache state in LDS for persistent launches of closed-form networks (no walkers)
+    const size_t n1 = (size_t)P.s1 * P.a1, n2 = (size_t)P.s2 * P.a2;
+    P.cache_lds_off = (uint32_t)((C->step_lds + 15) & ~(size_t)15);
+    P.cache_lds_bytes = (uint32_t)(9 * (n1 + n2) + P.s1 + P.s2);
+    C->persist_lc = P.net != GG_NET_EMESH_HOP_BY_HOP && (size_t)P.cache_lds_off + P.cache_lds_bytes <= 160 * 1024;
+    if (C->persist_lc)
+      GG_HIP(hipFuncSetAttribute((const void*)k_c_persist<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)(P.cache_lds_off + P.cache_lds_bytes)));
+  }
   GG_HIP(hipFuncSetAttribute((const void*)k_c_step, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C->step_lds));
   if (P.net == GG_NET_EMESH_HOP_BY_HOP)
     GG_HIP(hipFuncSetAttribute((const void*)k_c_walk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C->walk_lds));
+    GG_HIP(hipFuncSetAttribute((const void*)k_c_persist<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)std::max(C->walk_lds, C->step_lds)));
   const uint64_t L = P.L;
   gg_status st = GG_OK;
 #define A(ptr, n) if (st == GG_OK) st = dalloc(C, &S.ptr, (n))
@@ -2067,7 +2264,7 @@ static gg_status coh_alloc(gg_ctx* ctx)
   A(xl, (uint64_t)std::max(P.nsx, 1u) * P.seg_cap); A(nxl, std::max(P.nsx, 1u));
   A(yl, (uint64_t)std::max(P.nsy, 1u) * P.seg_cap); A(nyl, std::max(P.nsy, 1u));
   A(bnd, P.msg_cap); A(bnd_cnt, 1);
-  A(ring, 11); A(ri, GG_NUM_RUN_INFO); A(qs, QS_N);
+  A(ring, 11); A(ri, GG_NUM_RUN_INFO); A(qs, QS_N); A(gbar, 1);
   A(gscr, L * 5 * P.IC);
 #undef A
   if (getenv("GG_COH_PROFILE") && atoi(getenv("GG_COH_PROFILE"))) {
@@ -2117,7 +2314,7 @@ gg_status gg_coherent_begin(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_ou
   if (tr->num_records && (!tr->addr_dev || !tr->meta_dev)) return gg_fail(GG_ERR_INVALID, "NULL trace pointers");
   C->S.addr = tr->addr_dev; C->S.meta = tr->meta_dev; C->S.out = access_out_dev;
   C->n_records = tr->num_records;
-  for (int k = 0; k < 3; ++k) { C->ksum[k] = 0; C->kcnt[k] = 0; C->nlaunch[k] = 0; }
+  for (int k = 0; k < 4; ++k) { C->ksum[k] = 0; C->kcnt[k] = 0; C->nlaunch[k] = 0; }
   C->tused = 0;
   GG_HIP(hipMemcpyAsync(C->offs_dev, tr->tile_offsets, sizeof(uint64_t) * (P.T + 1), hipMemcpyHostToDevice, s));
   if (gg_status st = gg_noc_reset(ctx, s)) return st;
@@ -2261,7 +2458,31 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
   const CP& P = C->P;
   const bool hbh = P.net == GG_NET_EMESH_HOP_BY_HOP;
   uint32_t L = 0, batch = 16;
-  for (;;) {
+  // small meshes: the whole loop in persistent launches (k_c_persist), one
+  // workgroup per owned tile, all resident (<= kPersistTiles << CUs)
+  const char* np_env = getenv("GG_COH_NO_PERSIST");
+  const bool persist = P.L <= kPersistTiles && !(np_env && atoi(np_env));
+  while (persist) {
+    GG_HIP(hipMemsetAsync(C->S.gbar, 0, sizeof(uint32_t), s));
+    const char* nl_env = getenv("GG_COH_NO_LDS_CACHE");
+    if (C->persist_lc && !(nl_env && atoi(nl_env))) {
+      const size_t lds = P.cache_lds_off + P.cache_lds_bytes;
+      timed_launch(ctx, C, s, 3, [&] { hipLaunchKernelGGL(k_c_persist<true>, dim3(P.L), dim3(64), lds, s, P, C->S, L, L + kPersistLaunches); });
+    } else {
+      const size_t lds = std::max(C->walk_lds, C->step_lds);
+      timed_launch(ctx, C, s, 3, [&] { hipLaunchKernelGGL(k_c_persist<false>, dim3(P.L), dim3(64), lds, s, P, C->S, L, L + kPersistLaunches); });
+    }
+    GG_HIP(hipGetLastError());
+    L += kPersistLaunches;
+    uint64_t done = 0;
+    uint32_t err = 0;
+    GG_HIP(hipMemcpyAsync(&done, C->S.qs + QS_DONE, sizeof(done), hipMemcpyDeviceToHost, s));
+    GG_HIP(hipMemcpyAsync(&err, ctx->err_dev, sizeof(err), hipMemcpyDeviceToHost, s));
+    GG_HIP(hipStreamSynchronize(s));
+    timed_harvest(C);
+    if (err || done) break;
+  }
+  for (; !persist;) {
     for (uint32_t b = 0; b < batch; ++b, ++L) {
       timed_launch(ctx, C, s, 0, [&] { hipLaunchKernelGGL(k_c_step, dim3(P.L), dim3(64), C->step_lds, s, P, C->S, L, 1u, (uint64_t)0); });
       if (hbh) {
@@ -2293,6 +2514,8 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
             "[gg_coh] walkers: %llu launches, staging %llu events %llu loop %llu handoff %llu, max events X %llu Y %llu | "
             "slowest walker per launch X %llu Y %llu | sweep: batch %llu queue load %llu requests %llu store %llu (s_memtime cycles); requests fast %llu M/G/1 %llu search %llu\n",
             h[0], h[1], h[9], h[2], h[3], h[4], crit, h[22], h[16], h[19], h[17], h[18], h[24], h[25], wx, wy, h[26], h[27], h[28], h[29], h[30], h[31], h[32]);
+    fprintf(stderr, "[gg_coh] trace: hit runs %llu cycles for %llu records; other accesses %llu cycles for %llu\n",
+            h[33], h[34], h[35], h[36]);
   }
   if (gg_status e = coh_check(ctx)) return e;
   uint64_t done = 0;

@@ -72,6 +72,22 @@ def test_coherent_matches_oracle(T, N, hot, K, net):
     _compare(cfg, a, m, o)
 
 
+@pytest.mark.parametrize("T,N,hot,K,net", [(16, 1500, 8, 1, C.NET_EMESH_HOP_BY_HOP),
+                                            (64, 600, 32, 8, C.NET_EMESH_HOP_BY_HOP),
+                                            (64, 1000, 32, 8, C.NET_EMESH_HOP_COUNTER)])
+@pytest.mark.parametrize("env", ["GG_COH_NO_PERSIST", "GG_COH_NO_LDS_CACHE"])
+def test_coherent_small_mesh_launch_path(T, N, hot, K, net, env, monkeypatch):
+    """Small meshes run the loop in persistent launches (k_c_persist, grid
+    barriers; closed-form networks keep the cache state in LDS);
+    GG_COH_NO_PERSIST=1 forces the per-step launches, GG_COH_NO_LDS_CACHE=1
+    the persistent kernel on the HBM cache arrays: all bit-exact."""
+    from oracle import pyoracle as po
+    monkeypatch.setenv(env, "1")
+    cfg = C.default_config(T, num_shards=K, net_model=net)
+    a, m, o = po.gen_trace(T, N, hot_lines=hot)
+    _compare(cfg, a, m, o)
+
+
 def test_coherent_directory_replacements():
     """A small directory: DirectoryCache replacement, NULLIFY, back-invalidations."""
     from oracle import pyoracle as po
