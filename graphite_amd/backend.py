@@ -57,7 +57,8 @@ EXPORTS = ["gg_abi_version", "gg_last_error", "gg_config_default", "gg_create", 
            "gg_gen_uniform_trace", "gg_kernel_time_ms", "gg_set_timing",
            "gg_coherent_begin", "gg_coherent_quantum", "gg_coherent_export", "gg_coherent_import",
            "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace", "gg_shard_map",
-           "gg_kernel_stats", "gg_round_exchange", "gg_coherent_run_ranks", "gg_gen_stress_trace"]
+           "gg_kernel_stats", "gg_round_exchange", "gg_coherent_run_ranks", "gg_gen_stress_trace",
+           "gg_split_accesses", "gg_combine_accesses"]
 
 
 class _CStatus(ctypes.Structure):
@@ -110,9 +111,12 @@ def load():
     L.gg_round_exchange.argtypes = [vp, vp, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(i32)]
     L.gg_gen_stress_trace.argtypes = [vp, vp, u32, u32, u64, u64, u32, u32, u32, u32, u32, vp]
     L.gg_coherent_run_ranks.argtypes = [vp, vp, ctypes.POINTER(_Trace), vp, vp]
+    L.gg_split_accesses.argtypes = [vp, vp, vp, vp, u32, u32, vp, vp, vp, u64, ctypes.POINTER(u64), vp, vp]
+    L.gg_combine_accesses.argtypes = [vp, vp, u64, vp, vp, vp]
     for name in ["gg_kernel_stats", "gg_shard_map", "gg_coherent_begin", "gg_coherent_quantum", "gg_coherent_export",
                  "gg_coherent_import", "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace",
-                 "gg_round_exchange", "gg_coherent_run_ranks", "gg_gen_stress_trace"]:
+                 "gg_round_exchange", "gg_coherent_run_ranks", "gg_gen_stress_trace", "gg_split_accesses",
+                 "gg_combine_accesses"]:
         getattr(L, name).restype = i32
     for name in ["gg_reset", "gg_cache_access_batch", "gg_cache_get_counters", "gg_cache_get_line_info",
                  "gg_cache_set_line_info", "gg_cache_access_line", "gg_cache_insert_line",
@@ -342,6 +346,42 @@ def gen_stress_trace(addr, meta, tile_begin, tiles, per_tile, num_tiles, first=0
     """Fill device tensors with the configs[4] coherent stress trace."""
     _check(load().gg_gen_stress_trace(_ptr(addr), _ptr(meta), tile_begin, tiles, per_tile, first, lines_log2,
                                       base_shift, num_tiles, pool_lines, pool_frac256, _stream(stream)))
+
+
+def split_accesses(addr, size, meta, tile_offsets, line_size=64, stream=None):
+    """Multi-line accesses -> line records (gg_split_accesses, core.cc:139-266).
+    addr (int64 byte addresses), size (int32 bytes), meta (int32) are device
+    tensors of a tile-major access trace with host tile_offsets [tiles + 1].
+    Returns (line_addr, line_meta, first, line_tile_offsets): device tensors
+    of the line trace (later lines GG_META_CONT), each access's first line
+    (n + 1 entries) and the line trace's host tile offsets."""
+    import torch
+    offs = np.ascontiguousarray(tile_offsets, dtype=np.uint64)
+    tiles = len(offs) - 1
+    n = int(offs[-1]) if tiles > 0 else 0
+    first = torch.empty(n + 1, dtype=torch.int64, device=addr.device)
+    nl = ctypes.c_uint64(0)
+    loffs = np.zeros(tiles + 1, np.uint64)
+    L = load()
+    _check(L.gg_split_accesses(_ptr(addr), _ptr(size), _ptr(meta), offs.ctypes.data_as(ctypes.c_void_p), tiles,
+                               line_size, _ptr(first), None, None, 0, ctypes.byref(nl), None, _stream(stream)))
+    la = torch.empty(max(nl.value, 1), dtype=torch.int64, device=addr.device)
+    lm = torch.empty(max(nl.value, 1), dtype=torch.int32, device=addr.device)
+    _check(L.gg_split_accesses(_ptr(addr), _ptr(size), _ptr(meta), offs.ctypes.data_as(ctypes.c_void_p), tiles,
+                               line_size, _ptr(first), _ptr(la), _ptr(lm), nl.value, ctypes.byref(nl),
+                               loffs.ctypes.data_as(ctypes.c_void_p), _stream(stream)))
+    return la[:nl.value], lm[:nl.value], first, loffs
+
+
+def combine_accesses(line_out, first, stream=None):
+    """Per-access (latency_ps, misses) of a coherent run over a split trace
+    (gg_combine_accesses, core.cc:239-266): device int64 / int32 tensors."""
+    import torch
+    n = first.numel() - 1
+    lat = torch.empty(max(n, 0), dtype=torch.int64, device=first.device)
+    miss = torch.empty(max(n, 0), dtype=torch.int32, device=first.device)
+    _check(load().gg_combine_accesses(_ptr(line_out), _ptr(first), max(n, 0), _ptr(lat), _ptr(miss), _stream(stream)))
+    return lat, miss
 
 
 class CoherentEngine:

@@ -104,6 +104,8 @@ struct CP {
   uint32_t msg_cap, seg_cap, walk_pk;    // pool records per parity; entries per segment list; walker LDS packets
   uint32_t seg_xcd;                      // > 0: runs interleaved by shard (seg_xcd shards), XCD-grouped walker blocks
   uint32_t cache_lds_off, cache_lds_bytes; // k_c_persist<true>: the tile's cache state in LDS after the step's
+  uint32_t touch_each;                     // hit runs touch LRU rows one record at a time (> 16 ways; GG_COH_TOUCH_EACH=1)
+  uint32_t no_hit_runs;                    // GG_COH_NO_HIT_RUNS=1: every record through app_access
   uint64_t lat_l1d, lat_l1t, lat_l2d, lat_l2t, lat_dir, gap_ps, dram_proc, dram_cost;
   NocParams np;
 };
@@ -199,6 +201,45 @@ template <int N> __device__ __forceinline__ uint32_t pick(const uint32_t (&a)[N]
 // one private cache (Cache + CacheSet + replacement policy, cache.cc / cache_set.cc):
 // lane w handles way w of the set an operation touches
 // ---------------------------------------------------------------------------
+// a set's row of meta bytes (way i in byte i % 8 of half i / 8), <= 16 ways
+__device__ __forceinline__ void load_row(const uint8_t* mr, uint32_t ways, uint64_t& ra, uint64_t& rb)
+{
+  if (ways == 4) { ra = *reinterpret_cast<const uint32_t*>(mr); rb = 0; }
+  else if (ways == 8) { ra = *reinterpret_cast<const uint64_t*>(mr); rb = 0; }
+  else if (ways == 16) { ra = reinterpret_cast<const uint64_t*>(mr)[0]; rb = reinterpret_cast<const uint64_t*>(mr)[1]; }
+  else {
+    ra = rb = 0;
+    for (uint32_t w = 0; w < ways; ++w) { const uint64_t v = (uint64_t)mr[w] << (8 * (w & 7)); if (w < 8) ra |= v; else rb |= v; }
+  }
+}
+__device__ __forceinline__ uint32_t row_byte(uint64_t ra, uint64_t rb, uint32_t w) { return (uint32_t)((w < 8 ? ra : rb) >> (8 * (w & 7))) & 0xFFu; }
+// one record lane's share of a run's LRU row update (see l1_hit_run): the last
+// touch of a way writes its age (distinct ways touched after it), the set's
+// last record writes the untouched ways (a_i + #{touched t: a_t > a_i})
+__device__ __forceinline__ void lru_run_store(uint8_t* mr, uint32_t ways, uint64_t ra, uint64_t rb, uint32_t w, uint32_t tm, uint32_t af)
+{
+  if (!((af >> w) & 1)) mr[w] = (uint8_t)((row_byte(ra, rb, w) & 7u) | ((uint32_t)__builtin_popcount(af) << 3));
+  if (af) return;
+  uint32_t am = 0;                                                   // ages of the touched ways
+  for (uint32_t i = 0; i < ways; ++i) if ((tm >> i) & 1) am |= 1u << (row_byte(ra, rb, i) >> 3);
+  for (uint32_t i = 0; i < ways; ++i) {
+    if ((tm >> i) & 1) continue;
+    const uint32_t b = row_byte(ra, rb, i), ai = b >> 3;
+    mr[i] = (uint8_t)((b & 7u) | ((ai + (uint32_t)__builtin_popcount(am >> (ai + 1))) << 3));
+  }
+}
+// inclusive prefix sum over the wave (DPP row shifts, then the row broadcasts)
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v)
+{
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);   // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);   // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);   // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);   // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);   // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);   // row_bcast:31
+  return v;
+}
+
 struct Cache {
   uint64_t* tag; uint8_t* meta; uint8_t* rr; uint64_t* cg;
   uint32_t sets, ways, log_line, pol, wb, ln;
@@ -263,6 +304,14 @@ struct Cache {
     cnt(GG_CC_TAG_READS);
     if (w >= 0) { const uint32_t m = rl32(mv, (uint32_t)w); st = m & 3u; loc = (m >> 2) & 1u; }
     else { st = ST_I; loc = 0; }
+  }
+  // the line's state without the TAG_READ count (hit-run predictor)
+  __device__ __forceinline__ uint32_t probe(uint64_t a)
+  {
+    uint64_t tv; uint32_t mv;
+    ld(set_of(a), tv, mv);
+    const int w = way_of(tv, tag_of(a));
+    return w >= 0 ? rl32(mv, (uint32_t)w) & 3u : (uint32_t)ST_I;
   }
   // setCacheLineInfo (cache.cc:218-241): st == I writes the invalid tag (CacheLineInfo::invalidate)
   __device__ __forceinline__ bool set(uint64_t a, uint32_t st, uint32_t loc)
@@ -869,44 +918,106 @@ struct Tile {
     const uint64_t a = wa & line_mask;
     const bool wr = (wm & GG_META_WRITE) != 0;
     const bool mine = ln >= o && wbase + ln < rec_end;
-    bool hit = false;
+    bool hit = false, l2ok = true;
+    uint32_t s1 = 0, w1 = 0, s2 = 0, w2 = 0;
+    const bool rows = L1.ways <= 16 && L2.ways <= 16 && !P.touch_each;
+    uint64_t r1a = 0, r1b = 0, r2a = 0, r2b = 0;                     // the record's set rows of meta bytes
     if (mine) {
-      const uint32_t st = L1.set_of(a);
+      s1 = L1.set_of(a);
       const uint64_t tg = L1.tag_of(a);
-      const uint64_t* tr = L1.tag + (size_t)st * L1.ways;
+      const uint64_t* tr = L1.tag + (size_t)s1 * L1.ways;
       int fw = -1;
 #pragma unroll 8
       for (uint32_t w = 0; w < L1.ways; ++w) fw = tr[w] == tg ? (int)w : fw;   // independent loads, tags unique
+      if (rows) load_row(L1.meta + (size_t)s1 * L1.ways, L1.ways, r1a, r1b);
       if (fw >= 0) {
-        const uint32_t cs = L1.meta[(size_t)st * L1.ways + fw] & 3u;
+        const uint32_t cs = (rows ? row_byte(r1a, r1b, (uint32_t)fw) : L1.meta[(size_t)s1 * L1.ways + fw]) & 3u;
         hit = wr ? cs == ST_M : cs != ST_I;
+        w1 = (uint32_t)fw;
+      }
+      if (hit && wr) {                                               // the write-through L2 line (l2:66-70)
+        s2 = L2.set_of(a);
+        const uint64_t* t2 = L2.tag + (size_t)s2 * L2.ways;
+        int f2 = -1;
+#pragma unroll 8
+        for (uint32_t w = 0; w < L2.ways; ++w) f2 = t2[w] == tg ? (int)w : f2;
+        l2ok = f2 >= 0;                                              // absent: the general path fails as the reference asserts
+        w2 = (uint32_t)f2;
+        if (rows) load_row(L2.meta + (size_t)s2 * L2.ways, L2.ways, r2a, r2b);
       }
     }
-    // inclusive prefix sum of gap + lat_l1d over the window
-    uint64_t e = mine ? (uint64_t)((wm & 0x7FFFFFFFu) >> 1) * P.gap_ps + P.lat_l1d : 0;
+    // end times: e = clk + gap_ps * (inclusive sum of gaps) + lat_l1d * (records so far)
+    const uint32_t g = mine ? (wm & 0x7FFFFFFFu) >> 1 : 0;
+    uint64_t e;
+    if (!__ballot(g >= (1u << 25))) {
+      e = (uint64_t)wave_incl_scan32(g) * P.gap_ps;
+    } else {
+      e = (uint64_t)g * P.gap_ps;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint64_t v = shfl64(e, (int)ln - d);
-      if ((int)ln >= d) e += v;
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t v = shfl64(e, (int)ln - d);
+        if ((int)ln >= d) e += v;
+      }
     }
-    e += clk;                                                        // this record's end time if all before it hit
-    const bool ok = mine && hit && e - P.lat_l1d < barrier;
+    e += clk + (uint64_t)(ln - o + 1) * P.lat_l1d;                   // this record's end time if all before it hit
+    const bool ok = mine && hit && l2ok && (e - P.lat_l1d < barrier || (wm & GG_META_CONT));
     const uint64_t m = __ballot(ok) >> o;
     const uint32_t n = ~m ? (uint32_t)__builtin_ctzll(~m) : 64u - o;
+    if (S.prof && ln == 0) { atomicAdd(&S.prof[37], (unsigned long long)__builtin_amdgcn_s_memtime()); atomicAdd(&S.prof[38], 1ull); }
     if (!n) return 0;
-    uint32_t nw = 0;
-    for (uint32_t k = 0; k < n && !failed; ++k) {
-      const uint32_t l = o + k;
-      const uint64_t ak = rl64(a, l);
-      const bool wk = (__builtin_amdgcn_readlane((int)wm, (int)l) & GG_META_WRITE) != 0;
-      nw += wk;
-      l1_access(ak, wk);
+    const uint64_t run = (n == 64 ? ~0ull : ((1ull << n) - 1)) << o;
+    const bool inrun = (run >> ln) & 1;
+    const uint64_t wmask = __ballot(wr) & run;
+    const uint32_t nw = (uint32_t)__builtin_popcountll(wmask);
+    const bool lru1 = L1.pol == GG_POLICY_LRU, lru2 = L2.pol == GG_POLICY_LRU && nw;
+    if ((lru1 || lru2) && rows) {
+      // the run's LRU touches (lru:40-50) in closed form: ages are a
+      // permutation of 0..ways-1 in every set (reset to the way index; touch
+      // and insert permute them), so after the run a touched way's age is the
+      // number of distinct ways of its set touched after its last touch, and an
+      // untouched way i gets a_i + #{touched t: a_t > a_i}.  Lane = record:
+      // tm = ways of my set touched in the run, af = those touched after me.
+      uint32_t tm1 = 0, af1 = 0, tm2 = 0, af2 = 0;
+      const bool w2l = inrun && wr;
+      for (uint32_t k = 0; k < n; ++k) {
+        const uint32_t l = o + k;
+        if (lru1) {
+          const uint32_t bit = 1u << rl32(w1, l);
+          const bool same = s1 == rl32(s1, l);
+          tm1 |= same ? bit : 0u;
+          af1 |= same && l > ln ? bit : 0u;
+        }
+        if (lru2 && ((wmask >> l) & 1)) {
+          const uint32_t bit = 1u << rl32(w2, l);
+          const bool same = s2 == rl32(s2, l);
+          tm2 |= same ? bit : 0u;
+          af2 |= same && l > ln ? bit : 0u;
+        }
+      }
+      PROF_AT(_q1);
+      if (S.prof && ln == 0) atomicAdd(&S.prof[40], (unsigned long long)_q1);
+      if (lru1 && inrun) lru_run_store(L1.meta + (size_t)s1 * L1.ways, L1.ways, r1a, r1b, w1, tm1, af1);
+      if (lru2 && w2l) lru_run_store(L2.meta + (size_t)s2 * L2.ways, L2.ways, r2a, r2b, w2, tm2, af2);
+      L1.cset = ~0u; L2.cset = ~0u;                                  // the one-row caches reload
+      PROF_AT(_q2);
+      if (S.prof && ln == 0) { atomicAdd(&S.prof[41], (unsigned long long)_q2); atomicAdd(&S.prof[42], 1ull); }
+    } else if (lru1 || lru2) {                                       // > 16 ways: one touch at a time
+      for (uint32_t k = 0; k < n; ++k) {
+        const uint32_t l = o + k;
+        uint64_t tv;
+        uint32_t mv;
+        if (lru1) { const uint32_t sk = rl32(s1, l); L1.ld(sk, tv, mv); L1.touch(sk, (int)rl32(w1, l), mv); }
+        if (lru2 && ((wmask >> l) & 1)) { const uint32_t sk = rl32(s2, l); L2.ld(sk, tv, mv); L2.touch(sk, (int)rl32(w2, l), mv); }
+      }
     }
     const uint32_t nr = n - nw;
     L1.cnt_add(GG_CC_TAG_READS, n);
     L1.cnt_add(GG_CC_ACCESSES, n);
     L1.cnt_add(GG_CC_READ_ACCESSES, nr);
     L1.cnt_add(GG_CC_WRITE_ACCESSES, nw);
+    L1.cnt_add(GG_CC_DATA_READS, nr);
+    L1.cnt_add(GG_CC_DATA_WRITES, nw);
+    L2.cnt_add(GG_CC_DATA_WRITES, nw);
     if (S.out && ln >= o && ln < o + n) S.out[wbase + ln] = ((uint64_t)P.lat_l1d << 2) | GG_LVL_L1;
     stat(GG_CT_ACCESSES, n);
     stat(GG_CT_LATENCY_PS, (uint64_t)n * P.lat_l1d);
@@ -1200,7 +1311,9 @@ __device__ __forceinline__ void quantum_end(const CP& P, const CS& S, uint32_t L
 // persistent launch; the records are read-only for the whole run)
 struct TraceWin { uint64_t wbase, wa; uint32_t wm; };
 
-template <bool LC>
+// LC: cache state in LDS; HR: L1 hit runs (persistent small meshes, where
+// long runs of hits between misses pay for the window look-up)
+template <bool LC, bool HR>
 __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, uint32_t devloop, uint64_t barrier_arg,
                                           TraceWin& W)
 {
@@ -1364,6 +1477,7 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
     const uint64_t line_mask = ~((1ull << P.log_line) - 1);
     uint64_t wbase = W.wbase, wa = W.wa;
     uint32_t wm = W.wm;
+    uint64_t stop = ~0ull;
     while (!T.blocked && !T.failed) {
       const uint64_t r = T.rec;
       if (r >= T.rec_end) break;
@@ -1373,17 +1487,30 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
         if (r + ln < T.rec_end) { wa = S.addr[r + ln]; wm = S.meta[r + ln]; }
       }
       const int o = (int)(r - wbase);
-      PROF_AT(_h0);
-      const uint32_t nh = T.l1_hit_run(wbase, (uint32_t)o, wa, wm, line_mask, barrier);
-      PROF_AT(_h1);
-      if (S.prof && ln == 0) { atomicAdd(&S.prof[33], (unsigned long long)(_h1 - _h0)); atomicAdd(&S.prof[34], (unsigned long long)nh); }
-      if (nh) continue;
+      // a run that ended inside the window ended on a record that is not a
+      // plain L1 hit before the barrier: that one goes straight to app_access
+      // hit runs pay a window look-up: start one only on a record that hits
+      bool try_run = HR && r != stop && !P.no_hit_runs;
+      if (try_run) {
+        const uint32_t m0 = rl32(wm, (uint32_t)o);
+        const uint32_t cs = T.L1.probe(rl64(wa, (uint32_t)o) & line_mask);
+        try_run = (m0 & GG_META_WRITE) ? cs == ST_M : cs != ST_I;
+      }
+      if (try_run) {
+        PROF_AT(_h0);
+        if (S.prof && ln == 0) atomicAdd(&S.prof[39], (unsigned long long)_h0);
+        const uint32_t nh = T.l1_hit_run(wbase, (uint32_t)o, wa, wm, line_mask, barrier);
+        PROF_AT(_h1);
+        if (S.prof && ln == 0) { atomicAdd(&S.prof[33], (unsigned long long)(_h1 - _h0)); atomicAdd(&S.prof[34], (unsigned long long)nh); }
+        if (nh) { if (o + nh < 64) stop = T.rec; continue; }
+      }
+      PROF_AT(_ha);
       const uint32_t meta = rl32(wm, (uint32_t)o);
       const uint64_t s = T.clk + (uint64_t)((meta & 0x7FFFFFFFu) >> 1) * P.gap_ps;
-      if (s >= barrier) break;
+      if (s >= barrier && !(meta & GG_META_CONT)) break;             // a multi-line access is one instruction
       T.app_access(rl64(wa, (uint32_t)o) & line_mask, (meta & GG_META_WRITE) != 0, s);
       PROF_AT(_h2);
-      if (S.prof && ln == 0) { atomicAdd(&S.prof[35], (unsigned long long)(_h2 - _h1)); atomicAdd(&S.prof[36], 1ull); }
+      if (S.prof && ln == 0) { atomicAdd(&S.prof[35], (unsigned long long)(_h2 - _ha)); atomicAdd(&S.prof[36], 1ull); }
     }
     W.wbase = wbase; W.wa = wa; W.wm = wm;
   }
@@ -1566,7 +1693,7 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
 __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t L, uint32_t devloop, uint64_t barrier_arg)
 {
   TraceWin W{~0ull, 0, 0};
-  step_body<false>(P, S, L, devloop, barrier_arg, W);
+  step_body<false, false>(P, S, L, devloop, barrier_arg, W);
 }
 
 // ---------------------------------------------------------------------------
@@ -1855,7 +1982,7 @@ __global__ void __launch_bounds__(64) k_c_persist(CP P, CS S, uint32_t L0, uint3
   TraceWin W{~0ull, 0, 0};
   if (LC) cache_state_copy<LC>(P, S, blockIdx.x, smem + P.cache_lds_off, true);
   for (uint32_t L = L0; L < L1; ++L) {
-    step_body<LC>(P, S, L, 1u, 0, W);
+    step_body<LC, true>(P, S, L, 1u, 0, W);
     grid_sync(S, gen);
     if (hbh) {
       for (uint32_t b = blockIdx.x; b < P.nsx; b += gridDim.x) walk_body(P, S, L, 0, b);
@@ -2229,6 +2356,12 @@ static gg_status coh_alloc(gg_ctx* ctx)
     C->walk_lds = fixed + (size_t)P.walk_pk * kWalkPkBytes;
   }
   P.seg_cap = P.msg_cap;
+  {
+    const char* te = getenv("GG_COH_TOUCH_EACH");
+    P.touch_each = te && atoi(te) ? 1u : 0u;
+    const char* nh = getenv("GG_COH_NO_HIT_RUNS");
+    P.no_hit_runs = nh && atoi(nh) ? 1u : 0u;
+  }
   C->step_lds = sizeof(StepLds);
   {
     // cache state in LDS for persistent launches of closed-form networks (no walkers)
@@ -2514,8 +2647,9 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
             "[gg_coh] walkers: %llu launches, staging %llu events %llu loop %llu handoff %llu, max events X %llu Y %llu | "
             "slowest walker per launch X %llu Y %llu | sweep: batch %llu queue load %llu requests %llu store %llu (s_memtime cycles); requests fast %llu M/G/1 %llu search %llu\n",
             h[0], h[1], h[9], h[2], h[3], h[4], crit, h[22], h[16], h[19], h[17], h[18], h[24], h[25], wx, wy, h[26], h[27], h[28], h[29], h[30], h[31], h[32]);
-    fprintf(stderr, "[gg_coh] trace: hit runs %llu cycles for %llu records; other accesses %llu cycles for %llu\n",
-            h[33], h[34], h[35], h[36]);
+    fprintf(stderr, "[gg_coh] trace: hit runs %llu cycles for %llu records (%llu calls, look-up part %llu; %llu row updates: "
+            "loop %llu stores %llu); other accesses %llu cycles for %llu\n",
+            h[33], h[34], h[38], h[37] - h[39], h[42], h[40] - h[37] + 0, h[41] - h[40], h[35], h[36]);
   }
   if (gg_status e = coh_check(ctx)) return e;
   uint64_t done = 0;

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define GG_ABI_VERSION 4
+#define GG_ABI_VERSION 5
 
 typedef int gg_status;
 enum {
@@ -84,8 +84,13 @@ enum { GG_LOC_INVALID = 0, GG_LOC_L1I = 2, GG_LOC_L1D = 3 };
  *   bit 0      : 1 = WRITE (Core::WRITE), 0 = READ (Core::READ)
  *   bits 1..30 : gap in core cycles before this access (coherent/timing modes;
  *                ignored by the private-cache mode)
- *   bit 31     : reserved, must be 0                                           */
+ *   bit 31     : GG_META_CONT — a later line of a multi-line access
+ *                (gg_split_accesses): coherent mode issues it at the previous
+ *                record's completion and never cuts it at the lax barrier (the
+ *                access is one instruction, core.cc:139-266); gap must be 0.
+ *                The private-cache mode ignores it.                          */
 #define GG_META_WRITE 1u
+#define GG_META_CONT 0x80000000u
 
 /* Per-access result word written by gg_cache_access_batch: one flag per 4-bit
  * field, so result words of up to 15 accesses can be summed field-wise (the
@@ -429,6 +434,32 @@ gg_status gg_gen_stress_trace(uint64_t* addr_dev, uint32_t* meta_dev, uint32_t t
 gg_status gg_gen_hotspot_trace(uint64_t* addr_dev, uint32_t* meta_dev, uint32_t tile_begin, uint32_t tiles,
                                uint64_t per_tile, uint64_t first, uint32_t lines_log2, uint32_t base_shift,
                                uint32_t hot_lines, uint32_t hot_frac256, void* stream);
+
+/* Multi-line accesses (replaces the line loop of Core::initiateMemoryAccess,
+ * common/tile/core/core.cc:139-266, for the coherent mode).  Input: a
+ * tile-major trace of accesses, device arrays addr_dev (byte address),
+ * size_dev (bytes), meta_dev (WRITE bit, gap cycles), host tile_offsets
+ * [tiles + 1].  Access i becomes the line records first_dev[i] ..
+ * first_dev[i+1]-1 (first_dev: device, n + 1 entries): lines begin_aligned ..
+ * end_aligned with the zero-size tail skipped (core.cc:167-197); the first
+ * keeps the access's WRITE bit and gap, the others are WRITE | GG_META_CONT.
+ * A zero-size access makes no line (core.cc:145-155); its gap cycles go to
+ * the tile's next access.  line_addr_dev / line_meta_dev (capacity cap) may
+ * both be NULL: then only *num_lines and first_dev are produced (size the
+ * buffers, call again).  line_tile_offsets (host, may be NULL) receives the
+ * line trace's tile offsets.  Synchronous on stream.  Errors: GG_ERR_INVALID
+ * (bad arguments, more lines than cap, a carried gap >= 2^30 cycles).       */
+gg_status gg_split_accesses(const uint64_t* addr_dev, const uint32_t* size_dev, const uint32_t* meta_dev,
+                            const uint64_t* tile_offsets, uint32_t tiles, uint32_t line_size, uint64_t* first_dev,
+                            uint64_t* line_addr_dev, uint32_t* line_meta_dev, uint64_t cap, uint64_t* num_lines,
+                            uint64_t* line_tile_offsets, void* stream);
+/* Per-access results of a coherent run of a split trace (core.cc:239-266):
+ * latency_ps_dev[i] = final - initial time = the sum of the access's line
+ * latencies (back to back); misses_dev[i] = its lines that did not hit the
+ * L1-D on the first attempt (MemoryManager::__coreInitiateMemoryAccess's
+ * return, l1_cache_cntlr.cc:100-179).  Either output may be NULL.           */
+gg_status gg_combine_accesses(const uint64_t* line_out_dev, const uint64_t* first_dev, uint64_t n,
+                              uint64_t* latency_ps_dev, uint32_t* misses_dev, void* stream);
 
 /* Device time (ms) of the most recent launch of a named kernel
  * ("cache_hist", "cache_scatter", "cache_replay", "cache_unshard",

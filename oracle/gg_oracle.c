@@ -123,6 +123,62 @@ uint32_t oracle_split_lines(uint64_t addr, uint32_t size, uint32_t line, uint64_
   return cnt;
 }
 
+/* Multi-line accesses (core.cc:139-266) as line records: access i (byte addr,
+ * size, meta) becomes lines first[i] .. first[i+1]-1; the first line keeps the
+ * access's WRITE bit and gap, the others are GG_META_CONT (issued at the
+ * previous line's completion, never cut at the lax barrier: one instruction).
+ * A zero-size access makes no line (core.cc:145-155); its gap cycles move to
+ * the tile's next access (the core clock keeps running).  Returns the number
+ * of lines, or ~0 when a carried gap exceeds 30 bits.  line_addr / line_meta
+ * may be NULL (count only).  tile_offsets: [tiles + 1] access offsets.      */
+uint64_t oracle_split_accesses(const uint64_t* addr, const uint32_t* size, const uint32_t* meta,
+                               const uint64_t* tile_offsets, uint32_t tiles, uint32_t line,
+                               uint64_t* first, uint64_t* line_addr, uint32_t* line_meta)
+{
+  uint64_t nl = 0;
+  uint64_t buf[64];
+  for (uint32_t t = 0; t < tiles; ++t) {
+    uint64_t carry = 0;
+    for (uint64_t i = tile_offsets[t]; i < tile_offsets[t + 1]; ++i) {
+      first[i] = nl;
+      const uint64_t gap = carry + ((meta[i] & 0x7FFFFFFFu) >> 1);
+      if (size[i] == 0) { carry = gap; continue; }
+      carry = 0;
+      if (gap >= (1ull << 30)) return ~0ull;
+      /* an access spans at most size / line + 2 lines: count first, then fill */
+      uint32_t k = oracle_split_lines(addr[i], size[i], line, buf, 64);
+      for (uint32_t j = 0; j < k; ++j) {
+        const uint64_t a = j < 64 ? buf[j] : (addr[i] - addr[i] % line) + (uint64_t)j * line;
+        if (line_addr) line_addr[nl] = a;
+        if (line_meta) line_meta[nl] = j == 0 ? (meta[i] & GG_META_WRITE) | ((uint32_t)gap << 1)
+                                              : (meta[i] & GG_META_WRITE) | GG_META_CONT;
+        ++nl;
+      }
+    }
+  }
+  if (tiles) first[tile_offsets[tiles]] = nl;
+  return nl;
+}
+
+/* Per-access results of a split trace (core.cc:239-251): latency = the
+ * access's final - initial time = the sum of its lines' latencies (each line
+ * starts at the previous one's completion); misses = lines that did not hit
+ * the L1-D on their first attempt (l1_cache_cntlr.cc:100-179).              */
+void oracle_combine_accesses(const uint64_t* line_out, const uint64_t* first, uint64_t n,
+                             uint64_t* latency_ps, uint32_t* misses)
+{
+  for (uint64_t i = 0; i < n; ++i) {
+    uint64_t lat = 0;
+    uint32_t m = 0;
+    for (uint64_t l = first[i]; l < first[i + 1]; ++l) {
+      lat += line_out[l] >> 2;
+      m += (line_out[l] & 3u) != GG_LVL_L1;
+    }
+    latency_ps[i] = lat;
+    misses[i] = m;
+  }
+}
+
 /* ======================================================================== */
 /* Cache (common/tile/memory_subsystem/cache/)                               */
 /* ======================================================================== */

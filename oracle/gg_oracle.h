@@ -111,6 +111,13 @@ int  oracle_coh_run_parallel(const gg_config* cfg, int threads, const uint64_t* 
  * their line-aligned addresses to lines (capacity cap).                    */
 uint32_t oracle_split_lines(uint64_t addr, uint32_t size, uint32_t line_size,
                             uint64_t* lines, uint32_t cap);
+/* Multi-line accesses as line records (GG_META_CONT) and their per-access
+ * latency / miss count (core.cc:139-266); see gg_oracle.c.                 */
+uint64_t oracle_split_accesses(const uint64_t* addr, const uint32_t* size, const uint32_t* meta,
+                               const uint64_t* tile_offsets, uint32_t tiles, uint32_t line,
+                               uint64_t* first, uint64_t* line_addr, uint32_t* line_meta);
+void oracle_combine_accesses(const uint64_t* line_out, const uint64_t* first, uint64_t n,
+                             uint64_t* latency_ps, uint32_t* misses);
 
 #ifdef __cplusplus
 }

@@ -69,6 +69,9 @@ def lib():
         L.oracle_noc_counters.argtypes = [vp, _u64p]
         L.oracle_split_lines.restype = ctypes.c_uint32
         L.oracle_split_lines.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _u64p, ctypes.c_uint32]
+        L.oracle_split_accesses.restype = ctypes.c_uint64
+        L.oracle_split_accesses.argtypes = [_u64p, _u32p, _u32p, _u64p, ctypes.c_uint32, ctypes.c_uint32, _u64p, vp, vp]
+        L.oracle_combine_accesses.argtypes = [_u64p, _u64p, ctypes.c_uint64, _u64p, _u32p]
         L.oracle_gen_hotspot.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u64p, _u32p]
         L.oracle_gen_stress.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
@@ -346,6 +349,34 @@ class OracleNoc:
         out = np.zeros(self.cfg.num_tiles * NUM_NET_COUNTERS, np.uint64)
         lib().oracle_noc_counters(self.h, out)
         return out.reshape(self.cfg.num_tiles, NUM_NET_COUNTERS)
+
+
+def split_accesses(addr, size, meta, tile_offsets, line=64):
+    """Multi-line accesses -> (line_addr, line_meta, first, line_tile_offsets) (oracle_split_accesses)."""
+    addr = np.ascontiguousarray(addr, np.uint64)
+    size = np.ascontiguousarray(size, np.uint32)
+    meta = np.ascontiguousarray(meta, np.uint32)
+    offs = np.ascontiguousarray(tile_offsets, np.uint64)
+    tiles = len(offs) - 1
+    first = np.zeros(len(addr) + 1, np.uint64)
+    n = lib().oracle_split_accesses(addr, size, meta, offs, tiles, line, first, None, None)
+    if n == (1 << 64) - 1:
+        raise ValueError("carried gap above 2^30 cycles")
+    la = np.zeros(max(n, 1), np.uint64)
+    lm = np.zeros(max(n, 1), np.uint32)
+    lib().oracle_split_accesses(addr, size, meta, offs, tiles, line, first,
+                                la.ctypes.data_as(ctypes.c_void_p), lm.ctypes.data_as(ctypes.c_void_p))
+    return la[:n], lm[:n], first, first[offs.astype(np.int64)]
+
+
+def combine_accesses(line_out, first):
+    """Per-access (latency_ps, misses) of a split trace's line results (oracle_combine_accesses)."""
+    n = len(first) - 1
+    lat = np.zeros(max(n, 1), np.uint64)
+    miss = np.zeros(max(n, 1), np.uint32)
+    lib().oracle_combine_accesses(np.ascontiguousarray(line_out, np.uint64), np.ascontiguousarray(first, np.uint64),
+                                  n, lat, miss)
+    return lat[:n], miss[:n]
 
 
 def split_lines(addr, size, line=64):

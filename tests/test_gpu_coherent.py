@@ -88,6 +88,26 @@ def test_coherent_small_mesh_launch_path(T, N, hot, K, net, env, monkeypatch):
     _compare(cfg, a, m, o)
 
 
+@pytest.mark.parametrize("a1,p1,a2,p2,hot,each", [
+    (4, C.POLICY_LRU, 8, C.POLICY_LRU, 16, 1),     # the touch-at-a-time path (> 16 ways)
+    (2, C.POLICY_LRU, 16, C.POLICY_LRU, 16, 0),    # 2-way L1: rows loaded byte by byte
+    (2, C.POLICY_LRU, 16, C.POLICY_LRU, 16, 1),
+    (4, C.POLICY_ROUND_ROBIN, 16, C.POLICY_LRU, 16, 0),
+    (4, C.POLICY_LRU, 8, C.POLICY_ROUND_ROBIN, 16, 0),
+    (8, C.POLICY_LRU, 16, C.POLICY_LRU, 0, 0),
+])
+def test_coherent_cache_geometries(a1, p1, a2, p2, hot, each, monkeypatch):
+    """L1-D / L2 associativity and policy variants through the L1 hit runs
+    (closed-form LRU rows up to 16 ways; GG_COH_TOUCH_EACH=1 forces the
+    one-touch-at-a-time path that > 16-way caches take)."""
+    from oracle import pyoracle as po
+    if each:
+        monkeypatch.setenv("GG_COH_TOUCH_EACH", "1")
+    cfg = C.default_config(16, l1d_assoc=a1, l1d_policy=p1, l2_assoc=a2, l2_policy=p2)
+    a, m, o = po.gen_trace(16, 2500, hot_lines=hot)
+    _compare(cfg, a, m, o)
+
+
 def test_coherent_directory_replacements():
     """A small directory: DirectoryCache replacement, NULLIFY, back-invalidations."""
     from oracle import pyoracle as po
@@ -318,3 +338,30 @@ def test_coherent_other_queue_models(qtype, aux, net):
                            basic_moving_avg=aux)
     a, m, o = po.gen_trace(16, 1500, hot_lines=16)
     _compare(cfg, a, m, o)
+
+
+@pytest.mark.parametrize("T,N,quantum,net", [(16, 600, 1000, C.NET_EMESH_HOP_COUNTER),
+                                             (16, 400, 20, C.NET_EMESH_HOP_COUNTER),   # accesses straddle barriers
+                                             (64, 200, 1000, C.NET_EMESH_HOP_BY_HOP)])
+def test_coherent_multiline_accesses(T, N, quantum, net):
+    """Multi-line accesses (core.cc:139-266): gg_split_accesses on the GPU
+    equals the oracle's split, the coherent run of the line trace is bit-exact,
+    and gg_combine_accesses gives the oracle's per-access latency / misses."""
+    from oracle import pyoracle as po
+    from graphite_amd import backend as B
+    from tests.access_util import gen_multiline
+    torch = torch_dev()
+    addr, size, meta, offs = gen_multiline(T, N)
+    la, lm, first, loffs = B.split_accesses(to_dev(torch, addr, torch.int64), to_dev(torch, size, torch.int32),
+                                            to_dev(torch, meta, torch.int32), offs)
+    ra, rm, rf, rlo = po.split_accesses(addr, size, meta, offs)
+    np.testing.assert_array_equal(to_np(la, np.uint64), ra)
+    np.testing.assert_array_equal(to_np(lm, np.uint32), rm)
+    np.testing.assert_array_equal(to_np(first, np.uint64), rf)
+    np.testing.assert_array_equal(loffs, rlo)
+    cfg = C.default_config(T, net_model=net, quantum_ns=quantum)
+    g = _compare(cfg, ra, rm, rlo)
+    lat, miss = B.combine_accesses(to_dev(torch, g[0], torch.int64), first)
+    rl, rmiss = po.combine_accesses(g[0], rf)
+    np.testing.assert_array_equal(to_np(lat, np.uint64), rl)
+    np.testing.assert_array_equal(to_np(miss, np.uint32), rmiss)
