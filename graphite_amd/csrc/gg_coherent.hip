@@ -146,6 +146,15 @@ struct CS {
 // 21 (Y), 22 launches
 #define PROF_T0() const uint64_t _p0 = S.prof ? __builtin_amdgcn_s_memtime() : 0
 #define PROF_AT(var) const uint64_t var = S.prof ? __builtin_amdgcn_s_memtime() : 0
+// GG_COH_PROFILE batch shapes: per port kind (0 SELF, 1 injection, 2 walker),
+// requests by batch size bucket (1, 2-3, 4-7, ..., 64+), requests at or after
+// the last interval's start at the batch's start (a tail run)
+__device__ __forceinline__ void prof_batch(const CS& S, int kind, uint32_t m, uint32_t tail)
+{
+  const int b = m <= 1 ? 0 : m <= 3 ? 1 : m <= 7 ? 2 : m <= 15 ? 3 : m <= 31 ? 4 : m <= 63 ? 5 : 6;
+  atomicAdd(&S.prof[50 + 8 * kind + b], (unsigned long long)m);
+  atomicAdd(&S.prof[80 + kind], (unsigned long long)tail);
+}
 
 __device__ __forceinline__ gg_cmsg* pool(const CS& S, uint32_t p) { return p ? S.pool1 : S.pool0; }
 __device__ __forceinline__ uint32_t* inb(const CS& S, uint32_t p) { return p ? S.inb1 : S.inb0; }
@@ -1359,8 +1368,11 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
 
   // ---- 0. hop-by-hop: SELF output port + receive of last step's packets (routePacket
   // at the receiver, hop_by_hop.cc:223-256; __processReceivedPacket, network_model.cc:118-150)
+  PROF_AT(_sa);
   const uint32_t na = P.net == GG_NET_EMESH_HOP_BY_HOP ? narv(S, p)[lt] : 0u;
+  uint64_t _sb = 0, _sc = 0, _sd = 0, _se = 0;
   if (na) {
+    if (S.prof) _sb = __builtin_amdgcn_s_memtime();
     const uint32_t* al = arv(S, p) + (size_t)lt * P.IC;
     const bool lds = na <= kInLds;
     uint64_t* t_ = lds ? sl.x1 : gscr; uint64_t* s_ = lds ? sl.x2 : gscr + P.IC; uint64_t* k_ = lds ? sl.x3 : gscr + 2 * P.IC;
@@ -1371,7 +1383,9 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
       t_[i] = m.arrival_ps; s_[i] = m.send_ps; k_[i] = ((uint64_t)m.src << 32) | m.seq; i_[i] = r;
     }
     __syncthreads();
+    if (S.prof) _sc = __builtin_amdgcn_s_memtime();
     order_port(na, t_, s_, k_, i_, o_, ln);
+    if (S.prof) _sd = __builtin_amdgcn_s_memtime();
     const uint64_t qi = (uint64_t)T.tile * 6 + P_SELF;
     HQueue* gq = S.nq + qi;
     HNode* gnd = S.nnd + qi * P.np.max_size;
@@ -1386,6 +1400,7 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
     }
     RegQueue rq;
     if (regq) rq.load(gq, gnd, 1, P.np.analytical != 0, ln);
+    if (S.prof) { (void)__builtin_amdgcn_readfirstlane((int)rq.a0); _se = __builtin_amdgcn_s_memtime(); }
     const uint64_t zps = lat_to_ps((uint64_t)P.np.router_delay + P.np.link_delay, P.np.f);
     uint64_t cq = 0, cf = 0;                                   // uniform: contention cycles, flits
     uint64_t rf = 0, rb = 0, rl = 0, rc = 0, rn = 0;           // this lane's packets: flits, bits, latency, contention
@@ -1402,17 +1417,21 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
         nf_ = (uint32_t)nflits(P.np, bits);
       }
       uint64_t ot = t_;
+      const uint64_t x0 = S.prof && regq ? rq.A(rq.sz - 1) : 0;
+      uint32_t ntail = 0;
       for (uint32_t k = 0; k < cnt; ++k) {
         const uint64_t t = rl64(t_, k);
         const uint32_t nf = (uint32_t)__builtin_amdgcn_readlane((int)nf_, (int)k);
         uint64_t qd = 0;
         if (P.np.qm) {
           const uint64_t tc = time_to_cycles(t, P.np.f);
+          ntail += tc >= x0;
           qd = regq ? rq.request(tc, nf, S.err) : (wave ? tr.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
         }
         cq += qd; cf += nf;
         if (ln == k) ot = t + zps + lat_to_ps(qd, P.np.f);
       }
+      if (S.prof && ln == 0) prof_batch(S, 0, cnt, ntail);
       if (ln < cnt) {                                           // serialization + receive (network_model.cc:118-150)
         const uint64_t ser = lat_to_ps(nf_, P.np.f);
         const uint64_t t2 = ot + ser, z2 = z_ + zps + ser;
@@ -1433,7 +1452,13 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
   }
 
   PROF_AT(_p1);
-  // ---- 1. the inbox, per-channel FIFO, channels merged by (arrival, sender)
+  if (S.prof && ln == 0 && na) {
+    atomicAdd(&S.prof[90], (unsigned long long)(_sa - _p0)); atomicAdd(&S.prof[91], (unsigned long long)(_sb - _sa));
+    atomicAdd(&S.prof[92], (unsigned long long)(_sc - _sb)); atomicAdd(&S.prof[93], (unsigned long long)(_sd - _sc));
+    atomicAdd(&S.prof[94], (unsigned long long)(_se - _sd)); atomicAdd(&S.prof[95], (unsigned long long)(_p1 - _se));
+    atomicAdd(&S.prof[96], 1ull);
+  }
+  if (S.prof && ln == 0 && !na) { atomicAdd(&S.prof[97], (unsigned long long)(_sa - _p0)); atomicAdd(&S.prof[98], 1ull); }
   const uint32_t ni = ninb(S, p)[lt];
   const uint32_t n = ni + na;
   // directory request FIFO in LDS when it cannot outgrow it this step
@@ -1614,15 +1639,19 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
             nf_ = (uint32_t)nflits(P.np, bits);
           }
           uint64_t oq = 0;
+          const uint64_t x0 = S.prof && regq ? rq.A(rq.sz - 1) : 0;
+          uint32_t ntail = 0;
           for (uint32_t k = 0; k < cnt; ++k) {
             const uint32_t nf = (uint32_t)__builtin_amdgcn_readlane((int)nf_, (int)k);
             uint64_t qd = 0;
             if (P.np.qm) {
               const uint64_t tc = time_to_cycles(rl64(sp, k), P.np.f);
+              ntail += tc >= x0;
               qd = regq ? rq.request(tc, nf, S.err) : (wave ? tr.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
             }
             if (ln == k) oq = qd;
           }
+          if (S.prof && ln == 0) prof_batch(S, 1, cnt, ntail);
           if (ln < cnt) {                                       // updateSendCounters (network_model.cc:228-251)
             gg_cmsg* g = cur + r;
             g->arrival_ps = sp + lat_to_ps(0, P.np.f) + lat_to_ps(oq, P.np.f);
@@ -1687,6 +1716,18 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
     atomicAdd(&S.prof[2], (unsigned long long)(_p3 - _p2)); atomicAdd(&S.prof[3], (unsigned long long)(_p4 - _p3));
     atomicAdd(&S.prof[4], (unsigned long long)(e - _p4));
     atomicMax(&S.prof[1024 + (L & 65535)], (unsigned long long)(e - _p0));
+    atomicMax(&S.prof[1024 + 3 * 65536 + (L & 65535)], (unsigned long long)(na + T.nsent));
+    {
+      // the slowest tile's shape: (total << 24) | payload, max per launch
+      const uint64_t tot = (e - _p0) << 24;
+      auto c8 = [](uint64_t v) { return v > 255 ? 255ull : v; };
+      auto c24 = [](uint64_t v) { v >>= 8; return v > 0xFFFFFF ? 0xFFFFFFull : v; };
+      const size_t b = 1024 + 6 * 65536 + 4 * (L & 16383);
+      atomicMax(&S.prof[b + 0], (unsigned long long)(tot | (c8(ni) << 16) | (c8(na) << 8) | c8(T.nsent)));
+      atomicMax(&S.prof[b + 1], (unsigned long long)(tot | c24(_p1 - _p0)));
+      atomicMax(&S.prof[b + 2], (unsigned long long)(tot | c24(_p2 - _p1)));
+      atomicMax(&S.prof[b + 3], (unsigned long long)(tot | c24(_p3 - _p2)));
+    }
   }
 }
 
@@ -1823,12 +1864,15 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
       if (ln < cnt) { i = O[c0 + ln]; t_ = Pt[i]; z_ = Pz[i]; f_ = Pf[i]; d_ = Pd[i]; }
       uint64_t ot = t_;
       const uint64_t _s3 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
+      const uint64_t x0 = S.prof && regq ? rq.A(rq.sz - 1) : 0;
+      uint32_t ntail = 0;
       for (uint32_t k = 0; k < cnt; ++k) {
         const uint64_t t = rl64(t_, k);
         const uint32_t nf = (uint32_t)__builtin_amdgcn_readlane((int)f_, (int)k) & 0xFFFFFFu;
         uint64_t qd = 0;
         if (qm) {
           const uint64_t tc = time_to_cycles(t, P.np.f);
+          ntail += tc >= x0;
           qd = regq ? rq.request(tc, nf, S.err) : (wave_q ? tr.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
         }
         cq += qd; cf += nf;
@@ -1836,6 +1880,7 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
       }
       nev += cnt;
       if (S.prof) pr_c += __builtin_amdgcn_s_memtime() - _s3;
+      if (S.prof && ln == 0) prof_batch(S, 2, cnt, ntail);
       if (ln < cnt) {
         uint32_t status = 0;
         if (nx < sd.lo || nx > sd.hi) status = 2;            // next router in another shard: held
@@ -1914,6 +1959,7 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
     atomicAdd(&S.prof[18], (unsigned long long)(e - _w2)); atomicAdd(&S.prof[19], (unsigned long long)nev);
     atomicAdd(&S.prof[22], 1ull);
     atomicMax(&S.prof[1024 + 65536 + 2 * (L & 65535) + stage], (unsigned long long)(e - _p0));
+    atomicMax(&S.prof[1024 + 4 * 65536 + 2 * (L & 65535) + stage], (unsigned long long)nev);
     atomicMax(&S.prof[24 + stage], (unsigned long long)nev);
   }
 }
@@ -2401,8 +2447,8 @@ static gg_status coh_alloc(gg_ctx* ctx)
   A(gscr, L * 5 * P.IC);
 #undef A
   if (getenv("GG_COH_PROFILE") && atoi(getenv("GG_COH_PROFILE"))) {
-    if ((st = dalloc(C, &S.prof, 1024 + 3 * 65536))) return st;
-    GG_HIP(hipMemset(S.prof, 0, sizeof(unsigned long long) * (1024 + 3 * 65536)));
+    if ((st = dalloc(C, &S.prof, 1024 + 8 * 65536))) return st;
+    GG_HIP(hipMemset(S.prof, 0, sizeof(unsigned long long) * (1024 + 8 * 65536)));
   }
   if (st) return st;
   S.quiet = S.ring + 4; S.imp = S.ring + 5; S.live = S.ring + 7;
@@ -2638,7 +2684,7 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
   GG_HIP(hipStreamSynchronize(s));
   if (C->S.prof) {
     // per-launch maxima in slots L mod 65536
-    std::vector<unsigned long long> h(1024 + 3 * 65536);
+    std::vector<unsigned long long> h(1024 + 8 * 65536);
     GG_HIP(hipMemcpy(h.data(), C->S.prof, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
     unsigned long long crit = 0, wx = 0, wy = 0;
     for (int i = 0; i < 65536; ++i) { crit += h[1024 + i]; wx += h[1024 + 65536 + 2 * i]; wy += h[1024 + 65536 + 2 * i + 1]; }
@@ -2647,6 +2693,27 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
             "[gg_coh] walkers: %llu launches, staging %llu events %llu loop %llu handoff %llu, max events X %llu Y %llu | "
             "slowest walker per launch X %llu Y %llu | sweep: batch %llu queue load %llu requests %llu store %llu (s_memtime cycles); requests fast %llu M/G/1 %llu search %llu\n",
             h[0], h[1], h[9], h[2], h[3], h[4], crit, h[22], h[16], h[19], h[17], h[18], h[24], h[25], wx, wy, h[26], h[27], h[28], h[29], h[30], h[31], h[32]);
+    {
+      unsigned long long mt = 0, mx = 0, my = 0;
+      for (int i = 0; i < 65536; ++i) { mt += h[1024 + 3 * 65536 + i]; mx += h[1024 + 4 * 65536 + 2 * i]; my += h[1024 + 4 * 65536 + 2 * i + 1]; }
+      fprintf(stderr, "[gg_coh] tiles with SELF arrivals: %llu; cycles prologue %llu, narv %llu, gather %llu, order %llu, queue load %llu, "
+              "requests + store %llu | tiles without: %llu, prologue %llu\n", h[96], h[90], h[91], h[92], h[93], h[94], h[95], h[98], h[97]);
+      fprintf(stderr, "[gg_coh] per-launch max requests summed: tile (self+sent) %llu walker X %llu Y %llu\n", mt, mx, my);
+      unsigned long long sn = 0, sa = 0, ss = 0, c1 = 0, c2 = 0, c3 = 0, ct = 0, nl = 0;
+      for (int i = 0; i < 16384; ++i) {
+        const unsigned long long* b = &h[1024 + 6 * 65536 + 4 * i];
+        if (!b[0]) continue;
+        ++nl; ct += b[0] >> 24;
+        sn += (b[0] >> 16) & 255; sa += (b[0] >> 8) & 255; ss += b[0] & 255;
+        c1 += (b[1] & 0xFFFFFF) << 8; c2 += (b[2] & 0xFFFFFF) << 8; c3 += (b[3] & 0xFFFFFF) << 8;
+      }
+      fprintf(stderr, "[gg_coh] slowest tile per launch (%llu launches, last 16384 indices): cycles %llu; inbox msgs %llu, SELF arrivals %llu, "
+              "sent %llu; cycles self-phase %llu inbox+handlers %llu trace %llu\n", nl, ct, sn, sa, ss, c1, c2, c3);
+      const char* kn[3] = {"SELF", "injection", "walker"};
+      for (int k = 0; k < 3; ++k)
+        fprintf(stderr, "[gg_coh] %s batches, requests by size 1|2-3|4-7|8-15|16-31|32-63|64+: %llu %llu %llu %llu %llu %llu %llu; tail requests %llu\n",
+                kn[k], h[50 + 8 * k], h[51 + 8 * k], h[52 + 8 * k], h[53 + 8 * k], h[54 + 8 * k], h[55 + 8 * k], h[56 + 8 * k], h[80 + k]);
+    }
     fprintf(stderr, "[gg_coh] trace: hit runs %llu cycles for %llu records (%llu calls, look-up part %llu; %llu row updates: "
             "loop %llu stores %llu); other accesses %llu cycles for %llu\n",
             h[33], h[34], h[38], h[37] - h[39], h[42], h[40] - h[37] + 0, h[41] - h[40], h[35], h[36]);
