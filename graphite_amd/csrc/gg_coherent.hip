@@ -1205,17 +1205,17 @@ __device__ void order_port(uint32_t n, const uint64_t* t, const uint64_t* s, con
 // LDS: image slot i of `img` (stride qimg bytes) <-> queue qi_of(i).  One
 // flat index over every word of every image, 16 loads in flight per lane
 // before their stores (a per-image copy waits one round trip per image).
-template <bool IN, class QiOf>
+template <bool IN, class QiOf, uint32_t U = 16>
 __device__ __forceinline__ void imgs_copy(uint8_t* img, uint32_t qimg, uint32_t nimg, QiOf qi_of, HQueue* q, HNode* nd,
-                                          uint32_t ms, uint32_t ln)
+                                          uint32_t ms, uint32_t ln, uint32_t nl = 64)
 {
-  constexpr uint32_t HW = sizeof(HQueue) / 16, U = 16;
+  constexpr uint32_t HW = sizeof(HQueue) / 16;
   const uint32_t per = HW + ms, total = nimg * per;
-  for (uint32_t j0 = 0; j0 < total; j0 += U * 64) {
+  for (uint32_t j0 = 0; j0 < total; j0 += U * nl) {
     uint4 v[U];
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u) {
-      const uint32_t j = j0 + u * 64 + ln;
+      const uint32_t j = j0 + u * nl + ln;
       v[u] = make_uint4(0, 0, 0, 0);
       if (j < total) {
         const uint32_t i = j / per, w = j % per;
@@ -1227,7 +1227,7 @@ __device__ __forceinline__ void imgs_copy(uint8_t* img, uint32_t qimg, uint32_t 
     }
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u) {
-      const uint32_t j = j0 + u * 64 + ln;
+      const uint32_t j = j0 + u * nl + ln;
       if (j >= total) continue;
       const uint32_t i = j / per, w = j % per;
       const uint64_t qi = qi_of(i);
@@ -1738,8 +1738,67 @@ __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t L, uint32_t 
 }
 
 // ---------------------------------------------------------------------------
-// hop-by-hop: one wave per X (stage 0) or Y (stage 1) segment
+// hop-by-hop: one workgroup per X (stage 0) or Y (stage 1) run of routers
+// (one direction).  In a run the packets move one way, so the requests a port
+// sees depend only on the ports before it; the canonical order at a port is
+// (arrival time, rank) over the step's packets.
+// * one wave (64 threads, the persistent small-mesh kernel): the positions
+//   are served in the direction of travel, each position's whole batch in
+//   (time, rank) order (sweep_positions);
+// * one wave per position (k_c_walk): the positions are served concurrently
+//   as a pipeline.  Wave w serves its port's pending packets in (time, rank)
+//   order; a packet is safe once its time is below the horizon of the wave
+//   before it: that wave's published lower bound on the time of any packet it
+//   will still serve, plus the router + link delay (a packet leaves a port no
+//   earlier than it arrived there, plus that delay).  Same requests, same
+//   order, at every port (pipeline_positions).
 // ---------------------------------------------------------------------------
+constexpr uint32_t kWalkSync = 512;                  // LDS: per-wave horizon / done words, run bounds
+constexpr uint32_t kMaxWalkWaves = 16;
+
+__device__ __forceinline__ uint64_t wave_min64(uint64_t v)
+{
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { const uint64_t u = (uint64_t)__shfl_xor((long long)v, o); v = u < v ? u : v; }
+  return v;
+}
+__device__ __forceinline__ uint64_t lds_load_acq(const uint64_t* p)
+{
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_store_rel(uint64_t* p, uint64_t v)
+{
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+struct WalkLds {
+  uint64_t *Pt, *Ph, *Pk, *Pz;
+  uint32_t *Pi, *Pp, *Pd, *Pf, *Pr;
+  uint64_t *Qt; uint32_t *Qr, *Qs;
+};
+
+// the port of position pos serves one packet i (RouterModel + link, the
+// canonical request): queue delay at the port, router + link delay; the
+// packet moves to the next position (status 2: held at the shard's edge, 1:
+// leaves the run, 0: continues)
+template <class Q>
+__device__ __forceinline__ uint64_t serve_packet(const CP& P, const CS& S, const WalkLds& W, Q&& request, uint32_t i,
+                                                 uint32_t nx, const Seg& sd, uint64_t zps, uint64_t& cf)
+{
+  const uint64_t t = W.Pt[i];
+  const uint32_t f = W.Pf[i], nf = f & 0xFFFFFFu, d = W.Pd[i];
+  const uint64_t qd = request(t, nf);
+  cf += nf;
+  uint32_t status = 0;
+  if (nx < sd.lo || nx > sd.hi) status = 2;            // next router in another shard: held
+  else if (nx == d) status = 1;                        // leaves the run: next stage
+  W.Pt[i] = t + zps + lat_to_ps(qd, P.np.f);
+  W.Pz[i] += zps;
+  W.Pf[i] = nf | (status << 24);
+  return qd;
+}
+
+template <bool PIPE>
 __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, int stage, uint32_t blk)
 {
   const uint32_t live = ((volatile uint32_t*)S.live)[L & 3];
@@ -1752,7 +1811,7 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
     const uint32_t ns = P.seg_xcd, b = blk;
     sg = 2 * ((b % ns) + ns * (b / (2 * ns))) + ((b / ns) & 1u);
   }
-  const uint32_t ln = threadIdx.x, p = (live - 1) & 1u;
+  const uint32_t tid = threadIdx.x, nthr = blockDim.x, ln = tid & 63, wv = tid >> 6, p = (live - 1) & 1u;
   PROF_T0();
   uint32_t* cntp = (stage == 0 ? S.nxl : S.nyl) + sg;
   const uint32_t n0 = *cntp;
@@ -1769,154 +1828,194 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
   const uint32_t npos = sd.hi - sd.lo + 1;
   uint8_t* qimg = smem;
   uint64_t* lc = reinterpret_cast<uint64_t*>(smem + (size_t)npos * P.qimg);     // [npos][kNetCtr]
-  uint8_t* pk = reinterpret_cast<uint8_t*>(lc + (size_t)npos * kNetCtr);
-  if (n > P.walk_pk) { if (ln == 0) atomicOr(S.err, GG_DERR_CAP); if (ln == 0) *cntp = 0; return; }
-  uint64_t* Pt = reinterpret_cast<uint64_t*>(pk);
-  uint64_t* Ph = Pt + P.walk_pk; uint64_t* Pk = Ph + P.walk_pk; uint64_t* Pz = Pk + P.walk_pk;
-  uint32_t* Pi = reinterpret_cast<uint32_t*>(Pz + P.walk_pk);
-  uint32_t* Pp = Pi + P.walk_pk; uint32_t* Pd = Pp + P.walk_pk; uint32_t* Pf = Pd + P.walk_pk;   // pos, exit pos, flits | status << 24
-  uint32_t* Pr = Pf + P.walk_pk;                                   // rank in (send time, sender, seq) order
-  uint64_t* Qt = reinterpret_cast<uint64_t*>(Pr + P.walk_pk);      // event queue, sorted by (time, rank)
-  uint32_t* Qr = reinterpret_cast<uint32_t*>(Qt + P.walk_pk); uint32_t* Qs = Qr + P.walk_pk;
-  for (uint32_t i = ln; i < n; i += 64) {
+  uint64_t* wlow = lc + (size_t)npos * kNetCtr;                                  // [kMaxWalkWaves] horizons
+  uint64_t* wfin = wlow + kMaxWalkWaves;                                         // [kMaxWalkWaves] done flags
+  uint32_t* rlohi = reinterpret_cast<uint32_t*>(wfin + kMaxWalkWaves);           // lo, ~hi of the visited positions
+  uint8_t* pk = reinterpret_cast<uint8_t*>(wlow) + kWalkSync;
+  if (n > P.walk_pk) { if (tid == 0) { atomicOr(S.err, GG_DERR_CAP); *cntp = 0; } return; }
+  WalkLds W;
+  W.Pt = reinterpret_cast<uint64_t*>(pk);
+  W.Ph = W.Pt + P.walk_pk; W.Pk = W.Ph + P.walk_pk; W.Pz = W.Pk + P.walk_pk;
+  W.Pi = reinterpret_cast<uint32_t*>(W.Pz + P.walk_pk);
+  W.Pp = W.Pi + P.walk_pk; W.Pd = W.Pp + P.walk_pk; W.Pf = W.Pd + P.walk_pk;   // pos, exit pos, flits | status << 24
+  W.Pr = W.Pf + P.walk_pk;                                       // rank in (send time, sender, seq) order
+  W.Qt = reinterpret_cast<uint64_t*>(W.Pr + P.walk_pk);          // batch scratch of the one-wave sweep
+  W.Qr = reinterpret_cast<uint32_t*>(W.Qt + P.walk_pk); W.Qs = W.Qr + P.walk_pk;
+  for (uint32_t i = tid; i < n; i += nthr) {
     const uint32_t r = list[i];
     const gg_cmsg& m = cur[r];
-    Pt[i] = m.arrival_ps; Ph[i] = m.send_ps; Pk[i] = ((uint64_t)m.src << 32) | m.seq; Pz[i] = m.zero_load_ps;
-    Pi[i] = r; Pp[i] = pos_of(m.hop); Pd[i] = pos_of(m.dst);
+    W.Pt[i] = m.arrival_ps; W.Ph[i] = m.send_ps; W.Pk[i] = ((uint64_t)m.src << 32) | m.seq; W.Pz[i] = m.zero_load_ps;
+    W.Pi[i] = r; W.Pp[i] = pos_of(m.hop); W.Pd[i] = pos_of(m.dst);
     if (m.arrival_ps >> 51) atomicOr(S.err, GG_DERR_CAP);        // batch keys are time << 12 | rank
-    Pf[i] = (uint32_t)nflits(P.np, has_data(m.type) ? P.bits_data : P.bits_req);
+    W.Pf[i] = (uint32_t)nflits(P.np, has_data(m.type) ? P.bits_data : P.bits_req);
   }
-  for (uint32_t i = ln; i < npos * kNetCtr; i += 64) lc[i] = 0;
+  for (uint32_t i = tid; i < npos * kNetCtr; i += nthr) lc[i] = 0;
+  for (uint32_t i = tid; i < kMaxWalkWaves; i += nthr) { wlow[i] = 0; wfin[i] = 0; }
+  if (tid == 0) { rlohi[0] = ~0u; rlohi[1] = ~0u; }
   __syncthreads();
-  // canonical ranks, then the initial event queue in (time, rank) order
-  for (uint32_t i = ln; i < n; i += 64) {
-    const uint64_t hi_ = Ph[i], ki = Pk[i];
-    uint32_t r = 0;
-    for (uint32_t j = 0; j < n; ++j) { const uint64_t hj = Ph[j]; r += hj < hi_ || (hj == hi_ && Pk[j] < ki); }
-    Pr[i] = r;
-  }
-  __syncthreads();
-  // the queues of the positions the packets can visit
+  // canonical ranks; the positions the packets can visit
   uint32_t lo = ~0u, hi = 0;
-  for (uint32_t i = ln; i < n; i += 64) {
-    const uint32_t a = Pp[i], z = Pd[i];
+  for (uint32_t i = tid; i < n; i += nthr) {
+    const uint64_t hi_ = W.Ph[i], ki = W.Pk[i];
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < n; ++j) { const uint64_t hj = W.Ph[j]; r += hj < hi_ || (hj == hi_ && W.Pk[j] < ki); }
+    W.Pr[i] = r;
+    const uint32_t a = W.Pp[i], z = W.Pd[i];
     const uint32_t zz = dir ? min(z - 1, sd.hi) : max(z + 1, sd.lo);
     lo = min(lo, min(a, zz)); hi = max(hi, max(a, zz));
   }
   lo = wave_min(lo);
   hi = (uint32_t)(~wave_min(~hi));
+  if (ln == 0 && lo != ~0u) { atomicMin(&rlohi[0], lo); atomicMin(&rlohi[1], ~hi); }
+  __syncthreads();
+  lo = rlohi[0]; hi = ~rlohi[1];
   const bool qm = P.np.qm != 0;
   auto qi_of = [&](uint32_t i) { return (uint64_t)tile_at(lo + i) * 6 + port; };
   if (qm && lo <= hi)
-    imgs_copy<true>(qimg + (size_t)(lo - sd.lo) * P.qimg, P.qimg, hi - lo + 1, qi_of, S.nq, S.nnd, P.np.max_size, ln);
+    imgs_copy<true, decltype(qi_of), 4>(qimg + (size_t)(lo - sd.lo) * P.qimg, P.qimg, hi - lo + 1, qi_of, S.nq, S.nnd,
+                                        P.np.max_size, tid, nthr);
   __syncthreads();
   PROF_AT(_w1);
-  uint32_t nev = 0;
-  // Position sweep.  In a run the packets move one way, so the requests a
-  // port sees depend only on the ports before it: serving the positions in
-  // the direction of travel, each port's batch in (time, rank) order, is the
-  // (time, rank) event order of the whole run at every port.  Each batch runs
-  // through the port's queue held in the wave's registers (RegQueue), the
-  // batch's fields in lanes (readlane per request).
   const bool regq = qm && P.np.qtype == GG_QM_HISTORY_TREE && P.np.max_size <= kQMax;
   const bool wave_q = P.np.max_size <= kQMax;
   const uint64_t zps = lat_to_ps((uint64_t)P.np.router_delay + P.np.link_delay, P.np.f);
-  uint64_t* K = Qt; uint32_t* B = Qr; uint32_t* O = Qs;           // batch keys, batch, batch in order
-  uint64_t pr_a = 0, pr_b = 0, pr_c = 0, pr_d = 0;                // GG_COH_PROFILE: batch, queue load, requests, write back
-  uint64_t pf_ = 0, pa_ = 0, pg_ = 0;                              // requests: last interval, M/G/1, search
-  for (uint32_t s_ = 0; lo <= hi && s_ <= hi - lo; ++s_) {
-    const uint64_t _s0 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
-    const uint32_t pos = dir ? lo + s_ : hi - s_;
-    uint32_t m = 0;
-    for (uint32_t b0 = 0; b0 < n; b0 += 64) {
-      const uint32_t i = b0 + ln;
-      const bool at = i < n && Pp[i] == pos && (Pf[i] >> 24) == 0;
-      const uint64_t bm = __ballot(at);
-      if (at) {
-        const uint32_t k = m + (uint32_t)__builtin_popcountll(bm & ((1ull << ln) - 1));
-        B[k] = i; K[k] = (Pt[i] << 12) | Pr[i];
-      }
-      m += (uint32_t)__builtin_popcountll(bm);
-    }
-    if (m == 0) continue;
-    wave_sync();
-    for (uint32_t k = ln; k < m; k += 64) {
-      const uint64_t kk = K[k];
-      uint32_t r = 0;
-      for (uint32_t j = 0; j < m; ++j) r += K[j] < kk;
-      O[r] = B[k];
-    }
-    wave_sync();
+  uint32_t nev = 0;
+  // the port of one position, its queue in registers (history tree) or the LDS image
+  auto port_queue = [&](uint32_t pos, RegQueue& rq, HTree& tr) {
     uint8_t* im = qimg + (size_t)(pos - sd.lo) * P.qimg;
-    HQueue* qq = reinterpret_cast<HQueue*>(im);
-    HNode* qn = reinterpret_cast<HNode*>(im + sizeof(HQueue));
-    const uint64_t _s1 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
-    RegQueue rq;
-    if (regq) rq.load(qq, qn, 1, P.np.analytical != 0, ln);
-    HTree tr{qq, qn, 1, P.np.analytical != 0};
-    uint64_t cq = 0, cf = 0;
-    const uint32_t nx = dir ? pos + 1 : pos - 1;
-    if (S.prof) { const uint64_t _s2 = __builtin_amdgcn_s_memtime(); pr_a += _s1 - _s0; pr_b += _s2 - _s1; }
-    for (uint32_t c0 = 0; c0 < m; c0 += 64) {
-      const uint32_t cnt = min(64u, m - c0);
-      uint32_t i = 0, f_ = 0, d_ = 0;
-      uint64_t t_ = 0, z_ = 0;
-      if (ln < cnt) { i = O[c0 + ln]; t_ = Pt[i]; z_ = Pz[i]; f_ = Pf[i]; d_ = Pd[i]; }
-      uint64_t ot = t_;
-      const uint64_t _s3 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
-      const uint64_t x0 = S.prof && regq ? rq.A(rq.sz - 1) : 0;
-      uint32_t ntail = 0;
-      for (uint32_t k = 0; k < cnt; ++k) {
-        const uint64_t t = rl64(t_, k);
-        const uint32_t nf = (uint32_t)__builtin_amdgcn_readlane((int)f_, (int)k) & 0xFFFFFFu;
-        uint64_t qd = 0;
-        if (qm) {
-          const uint64_t tc = time_to_cycles(t, P.np.f);
-          ntail += tc >= x0;
-          qd = regq ? rq.request(tc, nf, S.err) : (wave_q ? tr.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
+    tr = HTree{reinterpret_cast<HQueue*>(im), reinterpret_cast<HNode*>(im + sizeof(HQueue)), 1, P.np.analytical != 0};
+    if (regq) rq.load(tr.q, tr.nd, 1, P.np.analytical != 0, ln);
+  };
+  auto add_ctr = [&](uint32_t pos, uint64_t cq, uint64_t m, uint64_t cf) {
+    // port_hop's counters: contention, router packets, buffer w+r, switch, crossbar, link
+    uint64_t* l = lc + (size_t)(pos - sd.lo) * kNetCtr;
+    l[0] += qm ? cq : 0; l[1] += qm ? m : 0; l[2] += cf; l[3] += m; l[4] += cf; l[5] += cf;
+  };
+  if (!PIPE) {
+    // ---- one wave: position sweep, each position's batch in (time, rank) order
+    uint64_t* K = W.Qt; uint32_t* B = W.Qr; uint32_t* O = W.Qs;
+    for (uint32_t s_ = 0; lo <= hi && s_ <= hi - lo; ++s_) {
+      const uint32_t pos = dir ? lo + s_ : hi - s_;
+      uint32_t m = 0;
+      for (uint32_t b0 = 0; b0 < n; b0 += 64) {
+        const uint32_t i = b0 + ln;
+        const bool at = i < n && W.Pp[i] == pos && (W.Pf[i] >> 24) == 0;
+        const uint64_t bm = __ballot(at);
+        if (at) {
+          const uint32_t k = m + (uint32_t)__builtin_popcountll(bm & ((1ull << ln) - 1));
+          B[k] = i; K[k] = (W.Pt[i] << 12) | W.Pr[i];
         }
-        cq += qd; cf += nf;
-        if (ln == k) ot = t + zps + lat_to_ps(qd, P.np.f);
+        m += (uint32_t)__builtin_popcountll(bm);
       }
-      nev += cnt;
-      if (S.prof) pr_c += __builtin_amdgcn_s_memtime() - _s3;
-      if (S.prof && ln == 0) prof_batch(S, 2, cnt, ntail);
-      if (ln < cnt) {
-        uint32_t status = 0;
-        if (nx < sd.lo || nx > sd.hi) status = 2;            // next router in another shard: held
-        else if (nx == d_) status = 1;                       // leaves the chain: next stage
-        Pt[i] = ot; Pz[i] = z_ + zps; Pp[i] = nx; Pf[i] = (f_ & 0xFFFFFFu) | (status << 24);
+      if (m == 0) continue;
+      wave_sync();
+      for (uint32_t k = ln; k < m; k += 64) {
+        const uint64_t kk = K[k];
+        uint32_t r = 0;
+        for (uint32_t j = 0; j < m; ++j) r += K[j] < kk;
+        O[r] = B[k];
       }
+      wave_sync();
+      RegQueue rq; HTree tr;
+      port_queue(pos, rq, tr);
+      auto request = [&](uint64_t t, uint32_t nf) -> uint64_t {
+        if (!qm) return 0;
+        const uint64_t tc = time_to_cycles(t, P.np.f);
+        return regq ? rq.request(tc, nf, S.err) : (wave_q ? tr.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
+      };
+      const uint32_t nx = dir ? pos + 1 : pos - 1;
+      uint64_t cq = 0, cf = 0;
+      for (uint32_t k = 0; k < m; ++k) {
+        const uint32_t i = O[k];
+        cq += serve_packet(P, S, W, request, i, nx, sd, zps, cf);
+        if (ln == 0) W.Pp[i] = nx;
+        wave_sync();
+      }
+      nev += m;
+      if (regq) rq.store(tr.q, tr.nd);
+      if (ln == 0) add_ctr(pos, cq, m, cf);
+      wave_sync();
     }
-    const uint64_t _s4 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
-    if (regq) rq.store(qq, qn);
-    if (S.prof) { pr_d += __builtin_amdgcn_s_memtime() - _s4; pf_ += rq.n_fast; pa_ += rq.n_anl; pg_ += rq.n_gen; }
-    if (ln == 0) {          // port_hop's counters: contention, router packets, buffer w+r, switch, crossbar, link
-      uint64_t* l = lc + (size_t)(pos - sd.lo) * kNetCtr;
-      l[0] += qm ? cq : 0; l[1] += qm ? m : 0; l[2] += cf; l[3] += m; l[4] += cf; l[5] += cf;
+  } else if (wv < npos) {
+    // ---- one wave per position (blockDim.x = 64 x positions): the pipeline
+    const uint32_t pos = dir ? sd.lo + wv : sd.hi - wv;
+    const uint32_t nx = dir ? pos + 1 : pos - 1;
+    constexpr uint64_t kInf = ~0ull;
+    const bool visited = lo <= hi && pos >= lo && pos <= hi;
+    RegQueue rq; HTree tr;
+    if (visited) port_queue(pos, rq, tr);
+    auto request = [&](uint64_t t, uint32_t nf) -> uint64_t {
+      if (!qm) return 0;
+      const uint64_t tc = time_to_cycles(t, P.np.f);
+      return regq ? rq.request(tc, nf, S.err) : (wave_q ? tr.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
+    };
+    uint64_t cq = 0, cf = 0, m = 0;
+    uint32_t spin = 0;
+    while (visited) {
+      // the horizon: packets still to come from upstream arrive at or after bound
+      bool up_fin = true;
+      uint64_t bound = kInf;
+      if (wv > 0) {
+        up_fin = lds_load_acq(&wfin[wv - 1]) != 0;
+        if (!up_fin) {
+          const uint64_t ul = lds_load_acq(&wlow[wv - 1]);
+          bound = ul == kInf ? kInf : ul + zps;
+        }
+      }
+      // the least pending packet at this position, by (time, rank)
+      uint64_t mk = kInf;
+      uint32_t mi = 0;
+      for (uint32_t b0 = 0; b0 < n; b0 += 64) {
+        const uint32_t i = b0 + ln;
+        if (i < n && W.Pp[i] == pos && (W.Pf[i] >> 24) == 0) {
+          const uint64_t k = (W.Pt[i] << 12) | W.Pr[i];
+          if (k < mk) { mk = k; mi = i; }
+        }
+      }
+      const uint64_t wk = wave_min64(mk);
+      if (wk == kInf && up_fin) break;                                 // nothing pending, nothing to come
+      const uint64_t T = wk == kInf ? kInf : wk >> 12;
+      if (!up_fin && T >= bound) {
+        // wait for upstream progress; publish what this port can still serve
+        if (ln == 0) lds_store_rel(&wlow[wv], T < bound ? T : bound);
+        if (++spin > (1u << 20)) { if (ln == 0) atomicOr(S.err, GG_DERR_STATE); break; }
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      const uint32_t i = (uint32_t)__builtin_amdgcn_readfirstlane(
+          (int)__builtin_amdgcn_readlane((int)mi, (int)__builtin_ctzll(__ballot(mk == wk))));
+      cq += serve_packet(P, S, W, request, i, nx, sd, zps, cf);
+      ++m;
+      // Pt / Pz / Pf of the packet before it appears downstream (Pp), then the horizon
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (ln == 0) {
+        __hip_atomic_store(&W.Pp[i], nx, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        lds_store_rel(&wlow[wv], T);
+      }
+      wave_sync();
     }
-    wave_sync();
-  }
-  if (S.prof && ln == 0) {
-    atomicAdd(&S.prof[26], (unsigned long long)pr_a); atomicAdd(&S.prof[27], (unsigned long long)pr_b);
-    atomicAdd(&S.prof[28], (unsigned long long)pr_c); atomicAdd(&S.prof[29], (unsigned long long)pr_d);
-    atomicAdd(&S.prof[30], (unsigned long long)pf_); atomicAdd(&S.prof[31], (unsigned long long)pa_);
-    atomicAdd(&S.prof[32], (unsigned long long)pg_);
+    if (ln == 0) {
+      lds_store_rel(&wlow[wv], kInf);
+      lds_store_rel(&wfin[wv], 1ull);
+    }
+    if (regq && visited) rq.store(tr.q, tr.nd);
+    if (ln == 0 && visited) add_ctr(pos, cq, m, cf);
+    nev = (uint32_t)m;
   }
   __syncthreads();
   PROF_AT(_w2);
   // hand-off
   uint32_t nb = 0;
-  for (uint32_t i = ln; i < n; i += 64) {
-    const uint32_t r = Pi[i], stt = Pf[i] >> 24;
-    const uint32_t h = tile_at(Pp[i]);
+  for (uint32_t i = tid; i < n; i += nthr) {
+    const uint32_t r = W.Pi[i], stt = W.Pf[i] >> 24;
+    const uint32_t h = tile_at(W.Pp[i]);
     gg_cmsg* m = cur + r;
-    m->arrival_ps = Pt[i]; m->zero_load_ps = Pz[i]; m->hop = h;
+    m->arrival_ps = W.Pt[i]; m->zero_load_ps = W.Pz[i]; m->hop = h;
     if (stt == 2) {                                            // held for the quantum boundary
       const uint32_t j = atomicAdd(S.bnd_cnt, 1u);
       if (j >= P.msg_cap) { atomicOr(S.err, GG_DERR_CAP); continue; }
       gg_cmsg g = *m;
-      g.arrival_ps = Pt[i]; g.zero_load_ps = Pz[i]; g.hop = h;
+      g.arrival_ps = W.Pt[i]; g.zero_load_ps = W.Pz[i]; g.hop = h;
       S.bnd[j] = g;
       ++nb;
       continue;
@@ -1938,8 +2037,9 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
   nb = wave_sum(nb);
   if (ln == 0 && nb) atomicAdd((unsigned long long*)&S.ri[GG_RI_BOUNDARY_MSGS], (unsigned long long)nb);
   if (qm && lo <= hi)
-    imgs_copy<false>(qimg + (size_t)(lo - sd.lo) * P.qimg, P.qimg, hi - lo + 1, qi_of, S.nq, S.nnd, P.np.max_size, ln);
-  for (uint32_t i = ln; i < npos * 6u; i += 64) {
+    imgs_copy<false, decltype(qi_of), 4>(qimg + (size_t)(lo - sd.lo) * P.qimg, P.qimg, hi - lo + 1, qi_of, S.nq, S.nnd,
+                                         P.np.max_size, tid, nthr);
+  for (uint32_t i = tid; i < npos * 6u; i += nthr) {
     const uint32_t q = i / 6, f = i % 6;
     const uint64_t* l = lc + (size_t)q * kNetCtr;
     const uint32_t tl = tile_at(sd.lo + q);
@@ -1952,21 +2052,27 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
     default: cadd(S.ctr, tl, GG_NC_LINK_TRAVERSALS, l[5]); break;
     }
   }
-  if (ln == 0) *cntp = 0;
-  if (S.prof && ln == 0) {
-    const uint64_t e = __builtin_amdgcn_s_memtime();
-    atomicAdd(&S.prof[16], (unsigned long long)(_w1 - _p0)); atomicAdd(&S.prof[17], (unsigned long long)(_w2 - _w1));
-    atomicAdd(&S.prof[18], (unsigned long long)(e - _w2)); atomicAdd(&S.prof[19], (unsigned long long)nev);
-    atomicAdd(&S.prof[22], 1ull);
-    atomicMax(&S.prof[1024 + 65536 + 2 * (L & 65535) + stage], (unsigned long long)(e - _p0));
-    atomicMax(&S.prof[1024 + 4 * 65536 + 2 * (L & 65535) + stage], (unsigned long long)nev);
-    atomicMax(&S.prof[24 + stage], (unsigned long long)nev);
+  if (tid == 0) *cntp = 0;
+  if (S.prof) {
+    nev = wave_sum(ln == 0 ? nev : 0u);
+    if (ln == 0) {
+      const uint64_t e = __builtin_amdgcn_s_memtime();
+      atomicAdd(&S.prof[19], (unsigned long long)nev);
+      if (wv == 0) {
+        atomicAdd(&S.prof[16], (unsigned long long)(_w1 - _p0)); atomicAdd(&S.prof[17], (unsigned long long)(_w2 - _w1));
+        atomicAdd(&S.prof[18], (unsigned long long)(e - _w2));
+        atomicAdd(&S.prof[22], 1ull);
+        atomicMax(&S.prof[1024 + 65536 + 2 * (L & 65535) + stage], (unsigned long long)(e - _p0));
+      }
+      atomicMax(&S.prof[24 + stage], (unsigned long long)nev);
+    }
   }
 }
 
-__global__ void __launch_bounds__(64) k_c_walk(CP P, CS S, uint32_t L, int stage)
+template <bool PIPE>
+__global__ void __launch_bounds__(PIPE ? 64 * kMaxWalkWaves : 64) k_c_walk(CP P, CS S, uint32_t L, int stage)
 {
-  walk_body(P, S, L, stage, blockIdx.x);
+  walk_body<PIPE>(P, S, L, stage, blockIdx.x);
 }
 
 // A barrier of every workgroup of the launch (one wave each): release of the
@@ -2031,9 +2137,9 @@ __global__ void __launch_bounds__(64) k_c_persist(CP P, CS S, uint32_t L0, uint3
     step_body<LC, true>(P, S, L, 1u, 0, W);
     grid_sync(S, gen);
     if (hbh) {
-      for (uint32_t b = blockIdx.x; b < P.nsx; b += gridDim.x) walk_body(P, S, L, 0, b);
+      for (uint32_t b = blockIdx.x; b < P.nsx; b += gridDim.x) walk_body<false>(P, S, L, 0, b);
       grid_sync(S, gen);
-      for (uint32_t b = blockIdx.x; b < P.nsy; b += gridDim.x) walk_body(P, S, L, 1, b);
+      for (uint32_t b = blockIdx.x; b < P.nsy; b += gridDim.x) walk_body<false>(P, S, L, 1, b);
       grid_sync(S, gen);
     }
     const uint64_t done = __hip_atomic_load(&S.qs[QS_DONE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2169,6 +2275,7 @@ struct gg_coh_state {
   uint64_t* offs_dev = nullptr;
   uint64_t n_records = 0;
   size_t step_lds = 0, walk_lds = 0;
+  uint32_t wtx = 64, wty = 64;          // threads of an X / Y walker workgroup
   bool persist_lc = false;
   bool begun = false;
   // live kernel timing (gg_set_timing): an event pair around every
@@ -2183,6 +2290,13 @@ struct gg_coh_state {
   uint64_t nlaunch[4] = {0, 0, 0, 0};   // all launches
 };
 constexpr uint64_t kTimeSample = 16;
+static void launch_walk(gg_coh_state* C, hipStream_t s, uint32_t blocks, uint32_t threads, uint32_t L, int stage)
+{
+  if (threads > 64)
+    hipLaunchKernelGGL(k_c_walk<true>, dim3(blocks), dim3(threads), C->walk_lds, s, C->P, C->S, L, stage);
+  else
+    hipLaunchKernelGGL(k_c_walk<false>, dim3(blocks), dim3(64), C->walk_lds, s, C->P, C->S, L, stage);
+}
 constexpr uint32_t kPersistTiles = 64;        // owned tiles up to which gg_coherent_run uses k_c_persist
 constexpr uint32_t kPersistLaunches = 16384;  // launch indices per k_c_persist launch
 static const char* kKernelNames[4] = {"coherent_step", "coherent_walk_x", "coherent_walk_y", "coherent_persist"};
@@ -2391,11 +2505,20 @@ static gg_status coh_alloc(gg_ctx* ctx)
     P.seg_xcd = inter ? ns : 0;
   }
   P.nsx = (uint32_t)segx.size() * 2; P.nsy = (uint32_t)segy.size() * 2;
-  uint32_t maxrun = 1;
-  for (const Seg& s : segx) maxrun = std::max(maxrun, s.hi - s.lo + 1);
-  for (const Seg& s : segy) maxrun = std::max(maxrun, s.hi - s.lo + 1);
+  uint32_t maxrun = 1, mrx = 1, mry = 1;
+  for (const Seg& s : segx) mrx = std::max(mrx, s.hi - s.lo + 1);
+  for (const Seg& s : segy) mry = std::max(mry, s.hi - s.lo + 1);
+  maxrun = std::max(mrx, mry);
   {
-    const size_t fixed = (size_t)maxrun * (P.qimg + kNetCtr * 8);
+    // walkers: one wave per position (the pipeline) when a run has at most
+    // kMaxWalkWaves routers, else one wave sweeping the positions
+    const char* sw = getenv("GG_COH_WALK_SWEEP");
+    const bool sweep = sw && atoi(sw);
+    C->wtx = !sweep && mrx <= kMaxWalkWaves ? 64 * mrx : 64;
+    C->wty = !sweep && mry <= kMaxWalkWaves ? 64 * mry : 64;
+  }
+  {
+    const size_t fixed = (size_t)maxrun * (P.qimg + kNetCtr * 8) + kWalkSync;
     if (P.net == GG_NET_EMESH_HOP_BY_HOP && fixed + 64 * kWalkPkBytes > kWalkLdsMax)
       return gg_fail(GG_ERR_UNSUPPORTED, "emesh_hop_by_hop: a shard's %u-router run does not fit the LDS of one walker", maxrun);
     P.walk_pk = (uint32_t)std::min<size_t>(4096, (kWalkLdsMax - fixed) / kWalkPkBytes);
@@ -2421,7 +2544,8 @@ static gg_status coh_alloc(gg_ctx* ctx)
   }
   GG_HIP(hipFuncSetAttribute((const void*)k_c_step, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C->step_lds));
   if (P.net == GG_NET_EMESH_HOP_BY_HOP)
-    GG_HIP(hipFuncSetAttribute((const void*)k_c_walk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C->walk_lds));
+    for (const void* f : {(const void*)k_c_walk<true>, (const void*)k_c_walk<false>})
+      GG_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C->walk_lds));
     GG_HIP(hipFuncSetAttribute((const void*)k_c_persist<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)std::max(C->walk_lds, C->step_lds)));
   const uint64_t L = P.L;
@@ -2531,8 +2655,8 @@ gg_status gg_coherent_quantum(gg_ctx* ctx, uint64_t q, gg_coherent_status* out)
     for (uint32_t b = 0; b < batch; ++b, ++k) {
       timed_launch(ctx, C, s, 0, [&] { hipLaunchKernelGGL(k_c_step, dim3(P.L), dim3(64), C->step_lds, s, P, C->S, k, 0u, barrier); });
       if (hbh) {
-        if (P.nsx) timed_launch(ctx, C, s, 1, [&] { hipLaunchKernelGGL(k_c_walk, dim3(P.nsx), dim3(64), C->walk_lds, s, P, C->S, k, 0); });
-        if (P.nsy) timed_launch(ctx, C, s, 2, [&] { hipLaunchKernelGGL(k_c_walk, dim3(P.nsy), dim3(64), C->walk_lds, s, P, C->S, k, 1); });
+        if (P.nsx) timed_launch(ctx, C, s, 1, [&] { launch_walk(C, s, P.nsx, C->wtx, k, 0); });
+        if (P.nsy) timed_launch(ctx, C, s, 2, [&] { launch_walk(C, s, P.nsy, C->wty, k, 1); });
       }
     }
     GG_HIP(hipGetLastError());
@@ -2665,8 +2789,8 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
     for (uint32_t b = 0; b < batch; ++b, ++L) {
       timed_launch(ctx, C, s, 0, [&] { hipLaunchKernelGGL(k_c_step, dim3(P.L), dim3(64), C->step_lds, s, P, C->S, L, 1u, (uint64_t)0); });
       if (hbh) {
-        if (P.nsx) timed_launch(ctx, C, s, 1, [&] { hipLaunchKernelGGL(k_c_walk, dim3(P.nsx), dim3(64), C->walk_lds, s, P, C->S, L, 0); });
-        if (P.nsy) timed_launch(ctx, C, s, 2, [&] { hipLaunchKernelGGL(k_c_walk, dim3(P.nsy), dim3(64), C->walk_lds, s, P, C->S, L, 1); });
+        if (P.nsx) timed_launch(ctx, C, s, 1, [&] { launch_walk(C, s, P.nsx, C->wtx, L, 0); });
+        if (P.nsy) timed_launch(ctx, C, s, 2, [&] { launch_walk(C, s, P.nsy, C->wty, L, 1); });
       }
     }
     GG_HIP(hipGetLastError());
