@@ -1951,6 +1951,15 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
     };
     uint64_t cq = 0, cf = 0, m = 0;
     uint32_t spin = 0;
+    // up to 128 packets: lane l watches packets l and l + 64 if their route
+    // crosses this port (entered at or before it, leaving after it)
+    const bool small = n <= 128;
+    auto crosses = [&](uint32_t i) {
+      if (i >= n) return false;
+      const uint32_t a = W.Pp[i], z = W.Pd[i];
+      return dir ? (a <= pos && pos < z) : (a >= pos && pos > z);
+    };
+    const bool c0 = small && crosses(ln), c1 = small && crosses(ln + 64);
     while (visited) {
       // the horizon: packets still to come from upstream arrive at or after bound
       bool up_fin = true;
@@ -1962,17 +1971,32 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
           bound = ul == kInf ? kInf : ul + zps;
         }
       }
-      // the least pending packet at this position, by (time, rank)
+      // the least pending packet at this position, by (time, rank): each lane
+      // its least, then a scalar pass over the lanes holding one (usually few)
       uint64_t mk = kInf;
       uint32_t mi = 0;
-      for (uint32_t b0 = 0; b0 < n; b0 += 64) {
-        const uint32_t i = b0 + ln;
-        if (i < n && W.Pp[i] == pos && (W.Pf[i] >> 24) == 0) {
-          const uint64_t k = (W.Pt[i] << 12) | W.Pr[i];
-          if (k < mk) { mk = k; mi = i; }
+      if (small) {
+        if (c0 && W.Pp[ln] == pos && (W.Pf[ln] >> 24) == 0) { mk = (W.Pt[ln] << 12) | W.Pr[ln]; mi = ln; }
+        if (c1 && W.Pp[ln + 64] == pos && (W.Pf[ln + 64] >> 24) == 0) {
+          const uint64_t k = (W.Pt[ln + 64] << 12) | W.Pr[ln + 64];
+          if (k < mk) { mk = k; mi = ln + 64; }
+        }
+      } else {
+        for (uint32_t b0 = 0; b0 < n; b0 += 64) {
+          const uint32_t i = b0 + ln;
+          if (i < n && W.Pp[i] == pos && (W.Pf[i] >> 24) == 0) {
+            const uint64_t k = (W.Pt[i] << 12) | W.Pr[i];
+            if (k < mk) { mk = k; mi = i; }
+          }
         }
       }
-      const uint64_t wk = wave_min64(mk);
+      uint64_t wk = kInf;
+      uint32_t wl = 0;
+      for (uint64_t bm = __ballot(mk != kInf); bm; bm &= bm - 1) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(bm);
+        const uint64_t k = rl64(mk, l);
+        if (k < wk) { wk = k; wl = l; }
+      }
       if (wk == kInf && up_fin) break;                                 // nothing pending, nothing to come
       const uint64_t T = wk == kInf ? kInf : wk >> 12;
       if (!up_fin && T >= bound) {
@@ -1982,8 +2006,7 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
         __builtin_amdgcn_s_sleep(1);
         continue;
       }
-      const uint32_t i = (uint32_t)__builtin_amdgcn_readfirstlane(
-          (int)__builtin_amdgcn_readlane((int)mi, (int)__builtin_ctzll(__ballot(mk == wk))));
+      const uint32_t i = (uint32_t)__builtin_amdgcn_readlane((int)mi, (int)wl);
       cq += serve_packet(P, S, W, request, i, nx, sd, zps, cf);
       ++m;
       // Pt / Pz / Pf of the packet before it appears downstream (Pp), then the horizon
