@@ -407,6 +407,26 @@ struct StepLds {
   Work wstack[WSTACK];                                    // directory work loop continuations
 };
 
+// the tile's per-step state words, loaded at kernel entry together with the
+// launch state (one memory round trip instead of a chain behind it)
+struct TilePre {
+  uint32_t tile;
+  uint64_t rec, rec_end, clk, pend_start, out_addr, out_time;
+  uint32_t blocked, seq, nrep, nrq;
+  uint64_t ccv, stv;
+  uint32_t narv[2], ninb[2];
+  __device__ __forceinline__ void load(const CS& S, uint32_t lt, uint32_t ln)
+  {
+    tile = S.gtile[lt];
+    rec = S.rec[lt]; rec_end = S.rec_end[lt]; clk = S.clk[lt]; pend_start = S.pend_start[lt];
+    out_addr = S.out_addr[lt]; out_time = S.out_time[lt];
+    blocked = S.blocked[lt]; seq = S.seq[lt]; nrep = S.nrep[lt]; nrq = S.nrq[lt];
+    ccv = ln < 2 * GG_NUM_CACHE_COUNTERS ? S.cc[(size_t)lt * 2 * GG_NUM_CACHE_COUNTERS + ln] : 0;
+    stv = ln < GG_NUM_TILE_STATS ? S.st[(size_t)lt * GG_NUM_TILE_STATS + ln] : 0;
+    narv[0] = S.narv0[lt]; narv[1] = S.narv1[lt]; ninb[0] = S.ninb0[lt]; ninb[1] = S.ninb1[lt];
+  }
+};
+
 // ---------------------------------------------------------------------------
 // one tile's controllers (every lane, identical values)
 // ---------------------------------------------------------------------------
@@ -422,14 +442,15 @@ struct Tile {
   CReq* rqp; bool rq_lds;
   uint32_t nch, cbase, cused, ccap, nsent;
   bool failed;
+  uint32_t ferr;                         // GG_DERR_* gathered by fail()
   uint64_t ccv, stv;                    // lane k's cache counter k (of 2 x 12) and statistic k, loaded at step start
 
   // LC: the tile's L1-D / L2 tags, meta bytes and RR counters live in LDS at
   // clds for the whole launch (k_c_persist; layout of cache_lds_bytes)
   template <bool LC>
   __device__ __forceinline__ Tile(const CP& P_, const CS& S_, uint32_t l, uint32_t par, StepLds& s_, uint8_t* clds,
-                                  std::integral_constant<bool, LC>)
-      : P(P_), S(S_), lt(l), tile(S_.gtile[l]), ln(lane_id()), p(par), sl(s_)
+                                  std::integral_constant<bool, LC>, const TilePre& pre)
+      : P(P_), S(S_), lt(l), tile(pre.tile), ln(lane_id()), p(par), sl(s_)
   {
     const size_t n1 = (size_t)P.s1 * P.a1, n2 = (size_t)P.s2 * P.a2;
     if constexpr (LC) {
@@ -449,20 +470,25 @@ struct Tile {
                  S.cc + ((size_t)lt * 2 + 1) * GG_NUM_CACHE_COUNTERS, P.s2, P.a2, P.log_line, P.pol2, 1, ln, 0, ~0u, 0, 0};
     }
     sd = 0;
-    rec = S.rec[lt]; rec_end = S.rec_end[lt]; clk = S.clk[lt]; pend_start = S.pend_start[lt];
-    out_addr = S.out_addr[lt]; out_time = S.out_time[lt];
-    blocked = S.blocked[lt]; seq = S.seq[lt]; nrep = S.nrep[lt]; nrq = S.nrq[lt];
+    rec = pre.rec; rec_end = pre.rec_end; clk = pre.clk; pend_start = pre.pend_start;
+    out_addr = pre.out_addr; out_time = pre.out_time;
+    blocked = pre.blocked; seq = pre.seq; nrep = pre.nrep; nrq = pre.nrq;
     dq = S.dq + lt; dnd = S.dnd + (size_t)lt * P.max_list; dq_lds = false;
     rqp = S.rq + (size_t)lt * P.QC; rq_lds = false;
-    nch = 0; cbase = 0; cused = 0; ccap = 0; nsent = 0; failed = false;
-    ccv = ln < 2 * GG_NUM_CACHE_COUNTERS ? S.cc[(size_t)lt * 2 * GG_NUM_CACHE_COUNTERS + ln] : 0;
-    stv = ln < GG_NUM_TILE_STATS ? S.st[(size_t)lt * GG_NUM_TILE_STATS + ln] : 0;
+    nch = 0; cbase = 0; cused = 0; ccap = 0; nsent = 0; failed = false; ferr = 0;
+    ccv = pre.ccv; stv = pre.stv;
   }
   __device__ __forceinline__ void stat(uint32_t k, uint64_t v) { if (ln == k) sd += v; }
+  // error flags are gathered in a register and reported once per step
+  // (flush_err): one atomic site instead of one per inlined check
   __device__ __forceinline__ void fail(uint32_t e = GG_DERR_STATE)
   {
     failed = true;
-    if (ln == 0) atomicOr(S.err, e);
+    ferr |= e;
+  }
+  __device__ __forceinline__ void flush_err()
+  {
+    if (ferr && ln == 0) atomicOr(S.err, ferr);
   }
 
   // ---- records (MemoryManager::sendMsg, …msi/memory_manager.cc:306-332) ------
@@ -1337,6 +1363,8 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
   for (int i = 0; i < QS_N; ++i) qsv[i] = devloop ? S.qs[i] : 0;
 #pragma unroll
   for (int i = 0; i < 11; ++i) rv[i] = S.ring[i];           // ring[4], quiet, imp[2], live[4]
+  TilePre pre;
+  pre.load(S, lt, ln);
   if (devloop) {
     if (qsv[QS_DONE]) { if (lt == 0 && ln == 0) S.live[L & 3] = 0; return; }
     q = qsv[QS_Q]; Q = qsv[QS_COUNT];
@@ -1359,7 +1387,7 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
   }
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   StepLds& sl = *reinterpret_cast<StepLds*>(smem);
-  Tile T(P, S, lt, p, sl, smem + P.cache_lds_off, std::integral_constant<bool, LC>());
+  Tile T(P, S, lt, p, sl, smem + P.cache_lds_off, std::integral_constant<bool, LC>(), pre);
   const gg_cmsg* prev = pool(S, p ^ 1u);     // records delivered to this step
   uint64_t* gscr = S.gscr + (size_t)lt * 5 * P.IC;
   // NoC counters of the SELF port (lanes 0-6) and of the receiver
@@ -1369,7 +1397,7 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
   // ---- 0. hop-by-hop: SELF output port + receive of last step's packets (routePacket
   // at the receiver, hop_by_hop.cc:223-256; __processReceivedPacket, network_model.cc:118-150)
   PROF_AT(_sa);
-  const uint32_t na = P.net == GG_NET_EMESH_HOP_BY_HOP ? narv(S, p)[lt] : 0u;
+  const uint32_t na = P.net == GG_NET_EMESH_HOP_BY_HOP ? pre.narv[p] : 0u;
   uint64_t _sb = 0, _sc = 0, _sd = 0, _se = 0;
   if (na) {
     if (S.prof) _sb = __builtin_amdgcn_s_memtime();
@@ -1459,7 +1487,7 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
     atomicAdd(&S.prof[96], 1ull);
   }
   if (S.prof && ln == 0 && !na) { atomicAdd(&S.prof[97], (unsigned long long)(_sa - _p0)); atomicAdd(&S.prof[98], 1ull); }
-  const uint32_t ni = ninb(S, p)[lt];
+  const uint32_t ni = pre.ninb[p];
   const uint32_t n = ni + na;
   // directory request FIFO in LDS when it cannot outgrow it this step
   if (T.nrq + 2 * n + 2 <= kRqLds) {
@@ -1690,6 +1718,7 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
   }
   if (T.dq_lds) img_out(S.dq + lt, S.dnd + (size_t)lt * P.max_list, sl.dimg, P.max_list, ln);
   T.flush();
+  T.flush_err();
   // NoC counters of the tile's own SELF port and receiver
   {
     if (na) {
@@ -1853,13 +1882,31 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
   for (uint32_t i = tid; i < kMaxWalkWaves; i += nthr) { wlow[i] = 0; wfin[i] = 0; }
   if (tid == 0) { rlohi[0] = ~0u; rlohi[1] = ~0u; }
   __syncthreads();
-  // canonical ranks; the positions the packets can visit
+  // canonical ranks (by send time, sender, seq); the positions the packets can visit
+  if (!PIPE) {
+    for (uint32_t i = tid; i < n; i += nthr) {
+      const uint64_t hi_ = W.Ph[i], ki = W.Pk[i];
+      uint32_t r = 0;
+      for (uint32_t j = 0; j < n; ++j) { const uint64_t hj = W.Ph[j]; r += hj < hi_ || (hj == hi_ && W.Pk[j] < ki); }
+      W.Pr[i] = r;
+    }
+  } else {
+    // a wave per packet: its lanes compare against 64 packets at a time
+    const uint32_t nw = nthr >> 6;
+    for (uint32_t i = wv; i < n; i += nw) {
+      const uint64_t hi_ = W.Ph[i], ki = W.Pk[i];
+      uint32_t r = 0;
+      for (uint32_t b0 = 0; b0 < n; b0 += 64) {
+        const uint32_t j = b0 + ln;
+        bool lt = false;
+        if (j < n) { const uint64_t hj = W.Ph[j]; lt = hj < hi_ || (hj == hi_ && W.Pk[j] < ki); }
+        r += (uint32_t)__builtin_popcountll(__ballot(lt));
+      }
+      if (ln == 0) W.Pr[i] = r;
+    }
+  }
   uint32_t lo = ~0u, hi = 0;
   for (uint32_t i = tid; i < n; i += nthr) {
-    const uint64_t hi_ = W.Ph[i], ki = W.Pk[i];
-    uint32_t r = 0;
-    for (uint32_t j = 0; j < n; ++j) { const uint64_t hj = W.Ph[j]; r += hj < hi_ || (hj == hi_ && W.Pk[j] < ki); }
-    W.Pr[i] = r;
     const uint32_t a = W.Pp[i], z = W.Pd[i];
     const uint32_t zz = dir ? min(z - 1, sd.hi) : max(z + 1, sd.lo);
     lo = min(lo, min(a, zz)); hi = max(hi, max(a, zz));

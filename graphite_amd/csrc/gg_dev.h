@@ -449,10 +449,12 @@ struct RegQueue {
   uint64_t min_proc;
   bool analytical;
   uint32_t n_fast = 0, n_anl = 0, n_gen = 0;   // requests by branch (diagnostics)
+  uint32_t errs = 0;                   // GG_DERR_* of the batch, reported by store()
+  uint32_t* errp = nullptr;
 
   __device__ __forceinline__ void load(const HQueue* q, const HNode* nd, uint64_t mp, bool an, uint32_t lane)
   {
-    ln = lane; min_proc = mp; analytical = an;
+    ln = lane; min_proc = mp; analytical = an; errs = 0; errp = nullptr;
     sz = q->size; cap = q->max_size;
     const uint32_t head = q->head;
     sig_sq = q->sig_sq; sig = q->sig; nreq = q->n; newest = q->newest;
@@ -465,6 +467,7 @@ struct RegQueue {
   }
   __device__ __forceinline__ void store(HQueue* q, HNode* nd) const
   {
+    if (errs && errp && ln == 0) atomicOr(errp, errs);
     if (ln < sz) nd[ln] = HNode{a0, b0};
     if (ln + 64 < sz) nd[ln + 64] = HNode{a1, b1};
     q->size = sz; q->head = 0;
@@ -498,6 +501,7 @@ struct RegQueue {
   // computeQueueDelay (queue_model_history_tree.cc:44-126) + QueueModelMG1::updateQueue
   __device__ __forceinline__ uint64_t request(uint64_t t, uint64_t p, uint32_t* err)
   {
+    errp = err;
     if (sz >= cap) { shift_down(0); --sz; }                          // prune the min node (:52-56)
     uint64_t qd = 0;
     const uint64_t la = A(sz - 1), lb = B(sz - 1);
@@ -542,7 +546,7 @@ struct RegQueue {
         i = m0 ? (int)__builtin_ctzll(m0) : (m1 ? 64 + (int)__builtin_ctzll(m1) : -1);
       }
       if (i < 0) {
-        if (ln == 0) atomicOr(err, GG_DERR_STATE);
+        errs |= GG_DERR_STATE;
       } else {
         const uint32_t ui = (uint32_t)i;
         const uint64_t a = A(ui), b = B(ui);
@@ -564,7 +568,7 @@ struct RegQueue {
     }
     sig_sq += p * p;                                                 // QueueModelMG1::updateQueue
     sig += p;
-    if (sig_sq >= kMg1Exact || p >= (1ull << 26)) { if (ln == 0) atomicOr(err, GG_DERR_RANGE); }
+    if (sig_sq >= kMg1Exact || p >= (1ull << 26)) errs |= GG_DERR_RANGE;
     ++nreq;
     const uint64_t x = t + qd + p;
     newest = x > newest ? x : newest;
