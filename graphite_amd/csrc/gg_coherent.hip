@@ -414,7 +414,7 @@ struct TilePre {
   uint64_t rec, rec_end, clk, pend_start, out_addr, out_time;
   uint32_t blocked, seq, nrep, nrq;
   uint64_t ccv, stv;
-  uint32_t narv[2], ninb[2];
+  uint32_t narv0, narv1, ninb0, ninb1;   // both parities (scalars: no dynamically indexed private array)
   __device__ __forceinline__ void load(const CS& S, uint32_t lt, uint32_t ln)
   {
     tile = S.gtile[lt];
@@ -423,7 +423,7 @@ struct TilePre {
     blocked = S.blocked[lt]; seq = S.seq[lt]; nrep = S.nrep[lt]; nrq = S.nrq[lt];
     ccv = ln < 2 * GG_NUM_CACHE_COUNTERS ? S.cc[(size_t)lt * 2 * GG_NUM_CACHE_COUNTERS + ln] : 0;
     stv = ln < GG_NUM_TILE_STATS ? S.st[(size_t)lt * GG_NUM_TILE_STATS + ln] : 0;
-    narv[0] = S.narv0[lt]; narv[1] = S.narv1[lt]; ninb[0] = S.ninb0[lt]; ninb[1] = S.ninb1[lt];
+    narv0 = S.narv0[lt]; narv1 = S.narv1[lt]; ninb0 = S.ninb0[lt]; ninb1 = S.ninb1[lt];
   }
 };
 
@@ -1374,7 +1374,9 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
   const uint32_t p = k & 1u;
   if (k > 0) {
     if (!devloop && rv[4]) { if (lt == 0 && ln == 0) S.live[L & 3] = 0; return; }
-    const uint32_t sent = rv[(k - 1) & 3] + (k == 1 ? rv[5 + (Q & 1)] : 0u);
+    const uint32_t km = (k - 1) & 3;                  // selects, not a dynamically indexed (private) array
+    const uint32_t sent = (km == 0 ? rv[0] : km == 1 ? rv[1] : km == 2 ? rv[2] : rv[3]) +
+                          (k == 1 ? ((Q & 1) ? rv[6] : rv[5]) : 0u);
     if (sent == 0) {                                 // the previous step sent nothing: the quantum is done
       if (lt == 0 && ln == 0) { S.live[L & 3] = 0; if (!devloop) *S.quiet = 1; }
       if (devloop) quantum_end(P, S, L, q, Q);
@@ -1397,7 +1399,7 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
   // ---- 0. hop-by-hop: SELF output port + receive of last step's packets (routePacket
   // at the receiver, hop_by_hop.cc:223-256; __processReceivedPacket, network_model.cc:118-150)
   PROF_AT(_sa);
-  const uint32_t na = P.net == GG_NET_EMESH_HOP_BY_HOP ? pre.narv[p] : 0u;
+  const uint32_t na = P.net == GG_NET_EMESH_HOP_BY_HOP ? (p ? pre.narv1 : pre.narv0) : 0u;
   uint64_t _sb = 0, _sc = 0, _sd = 0, _se = 0;
   if (na) {
     if (S.prof) _sb = __builtin_amdgcn_s_memtime();
@@ -1487,7 +1489,7 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
     atomicAdd(&S.prof[96], 1ull);
   }
   if (S.prof && ln == 0 && !na) { atomicAdd(&S.prof[97], (unsigned long long)(_sa - _p0)); atomicAdd(&S.prof[98], 1ull); }
-  const uint32_t ni = pre.ninb[p];
+  const uint32_t ni = p ? pre.ninb1 : pre.ninb0;
   const uint32_t n = ni + na;
   // directory request FIFO in LDS when it cannot outgrow it this step
   if (T.nrq + 2 * n + 2 <= kRqLds) {
@@ -2006,7 +2008,10 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
       const uint32_t a = W.Pp[i], z = W.Pd[i];
       return dir ? (a <= pos && pos < z) : (a >= pos && pos > z);
     };
-    const bool c0 = small && crosses(ln), c1 = small && crosses(ln + 64);
+    bool c0 = small && crosses(ln), c1 = small && crosses(ln + 64);
+    // a candidate's rank is fixed, and it is pending here only with status 0:
+    // it reaches this port on a continuing hop (or starts here)
+    const uint32_t r0 = c0 ? W.Pr[ln] : 0u, r1 = c1 ? W.Pr[ln + 64] : 0u;
     while (visited) {
       // the horizon: packets still to come from upstream arrive at or after bound
       bool up_fin = true;
@@ -2023,15 +2028,20 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
       uint64_t mk = kInf;
       uint32_t mi = 0;
       if (small) {
-        if (c0 && W.Pp[ln] == pos && (W.Pf[ln] >> 24) == 0) { mk = (W.Pt[ln] << 12) | W.Pr[ln]; mi = ln; }
-        if (c1 && W.Pp[ln + 64] == pos && (W.Pf[ln + 64] >> 24) == 0) {
-          const uint64_t k = (W.Pt[ln + 64] << 12) | W.Pr[ln + 64];
+        // a candidate is pending once it sits at this port (status 0 there)
+        // acquire: the packet's time, written before its position, is then current
+        const uint32_t q0 = c0 ? __hip_atomic_load(&W.Pp[ln], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) : ~0u;
+        const uint32_t q1 = c1 ? __hip_atomic_load(&W.Pp[ln + 64], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) : ~0u;
+        if (q0 == pos) { mk = (W.Pt[ln] << 12) | r0; mi = ln; }
+        if (q1 == pos) {
+          const uint64_t k = (W.Pt[ln + 64] << 12) | r1;
           if (k < mk) { mk = k; mi = ln + 64; }
         }
       } else {
         for (uint32_t b0 = 0; b0 < n; b0 += 64) {
           const uint32_t i = b0 + ln;
-          if (i < n && W.Pp[i] == pos && (W.Pf[i] >> 24) == 0) {
+          if (i < n && __hip_atomic_load(&W.Pp[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == pos &&
+              (W.Pf[i] >> 24) == 0) {
             const uint64_t k = (W.Pt[i] << 12) | W.Pr[i];
             if (k < mk) { mk = k; mi = i; }
           }
@@ -2056,6 +2066,7 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
       const uint32_t i = (uint32_t)__builtin_amdgcn_readlane((int)mi, (int)wl);
       cq += serve_packet(P, S, W, request, i, nx, sd, zps, cf);
       ++m;
+      if (small && ln == (i & 63)) { if (i < 64) c0 = false; else c1 = false; }   // served here: no longer a candidate
       // Pt / Pz / Pf of the packet before it appears downstream (Pp), then the horizon
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (ln == 0) {
