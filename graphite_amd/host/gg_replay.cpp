@@ -17,6 +17,11 @@
 //       unique id rank 0 writes to FILE, the run by gg_coherent_run_ranks
 //       (gg_round_exchange at every quantum boundary), the statistics summed
 //       over ranks and printed by rank 0
+//   gg_replay --coherent ... --table
+//       the tiles' summaries as TileManager::outputSummary's table
+//       (tile_manager_summary.cc:135-244) instead of one block per tile
+//   gg_replay --format-table FILE...
+//       that table for per-tile summary texts read from the files
 //   gg_replay --summary-selftest
 //       prints writeCacheSummary() for fixed counters (no GPU needed)
 #include <rccl/rccl.h>
@@ -27,6 +32,8 @@
 #include <cstring>
 #include <fstream>
 #include <iostream>
+#include <iterator>
+#include <sstream>
 #include <string>
 #include <thread>
 #include <vector>
@@ -46,7 +53,7 @@ static uint64_t splitmix_at(uint64_t seed, uint64_t i)
 int main(int argc, char** argv)
 {
   uint32_t tiles = 4, lines_log2 = 15, batches = 1, l2_assoc = 8, hot_lines = 64, net = GG_NET_EMESH_HOP_COUNTER;
-  bool coherent = false;
+  bool coherent = false, table = false;
   uint64_t per_tile = 100000;
   std::string trace, id_file;
   int ranks = 1, rank = 0;
@@ -61,6 +68,18 @@ int main(int argc, char** argv)
     else if (a == "--l2-assoc") l2_assoc = (uint32_t)std::strtoul(next(), nullptr, 0);
     else if (a == "--trace") trace = next();
     else if (a == "--coherent") coherent = true;
+    else if (a == "--table") table = true;
+    else if (a == "--format-table") {
+      // TileManager::outputSummary's table of the per-tile summary texts in the files that follow
+      std::vector<std::string> per_tile;
+      for (++i; i < argc; ++i) {
+        std::ifstream f(argv[i], std::ios::binary);
+        if (!f) { std::fprintf(stderr, "cannot open %s\n", argv[i]); return 2; }
+        per_tile.push_back(std::string(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>()));
+      }
+      std::cout << formatTileSummaries(per_tile);
+      return 0;
+    }
     else if (a == "--shards") shards = (uint32_t)std::strtoul(next(), nullptr, 0);
     else if (a == "--ranks") ranks = std::atoi(next());
     else if (a == "--rank") rank = std::atoi(next());
@@ -187,18 +206,21 @@ int main(int argc, char** argv)
         }
       }
       const uint64_t zero_net[GG_NUM_NET_COUNTERS] = {0};
+      std::vector<std::string> per_tile;
       for (uint32_t t = 0; rank == 0 && t < tiles; ++t) {
-        std::cout << "Tile " << t << " Summary:" << std::endl;
-        writeMemorySummary(std::cout, cfg, &st[(size_t)t * GG_NUM_TILE_STATS],
-                           &cc[(size_t)t * 2 * GG_NUM_CACHE_COUNTERS]);
+        std::ostringstream os;
+        writeMemorySummary(os, cfg, &st[(size_t)t * GG_NUM_TILE_STATS], &cc[(size_t)t * 2 * GG_NUM_CACHE_COUNTERS]);
         // Network::outputSummary (network.cc:79-89): the static networks below SYSTEM,
         // User (no traffic in a trace-driven run; emesh_hop_counter, carbon_sim.cfg [network]) then Memory
-        std::cout << "Network Summary: " << std::endl << "  Network (User): " << std::endl;
-        writeNetworkSummary(std::cout, zero_net, cfg.frequency_ghz, GG_NET_EMESH_HOP_COUNTER);
-        std::cout << "  Network (Memory): " << std::endl;
-        writeNetworkSummary(std::cout, &nc[(size_t)t * GG_NUM_NET_COUNTERS], cfg.frequency_ghz, cfg.net_model,
+        os << "Network Summary: " << std::endl << "  Network (User): " << std::endl;
+        writeNetworkSummary(os, zero_net, cfg.frequency_ghz, GG_NET_EMESH_HOP_COUNTER);
+        os << "  Network (Memory): " << std::endl;
+        writeNetworkSummary(os, &nc[(size_t)t * GG_NUM_NET_COUNTERS], cfg.frequency_ghz, cfg.net_model,
                             cfg.queue_model_enabled != 0);
+        if (table) per_tile.push_back(os.str());
+        else std::cout << "Tile " << t << " Summary:" << std::endl << os.str();
       }
+      if (table && rank == 0) std::cout << formatTileSummaries(per_tile);
     } catch (const Error& e) {
       std::fprintf(stderr, "gg_replay: %s\n", e.what());
       if (comm) ncclCommDestroy(comm);

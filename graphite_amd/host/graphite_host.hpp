@@ -27,6 +27,8 @@
 #include <ostream>
 #include <queue>
 #include <stdexcept>
+#include <algorithm>
+#include <sstream>
 #include <string>
 #include <vector>
 
@@ -290,6 +292,50 @@ inline void writeMemorySummary(std::ostream& out, const gg_config& c, const uint
   writeCacheSummary(out, "L2", cache_counters + GG_NUM_CACHE_COUNTERS, true);
   writeDramSummary(out, tile_stats, c.dram_queue_model_enabled != 0, c.dram_queue_model_type);
   writeDirectorySummary(out, tile_stats, directorySizing(c));
+}
+
+// TileManager::outputSummary's table (tile_manager_summary.cc:60-198): every
+// tile's summary text ("label: value" lines) becomes one column, the row
+// headings are the labels of tile 0's lines, the columns are padded to their
+// widest cell and closed by " | ".  Restated with the reference's own string
+// scanning (std::string::find, npos wrapping included), so summaries that do
+// not follow the "label: value" form come out exactly as the reference lays
+// them out.
+inline std::string formatTileSummaries(const std::vector<std::string>& summaries)
+{
+  if (summaries.empty()) return std::string();
+  const size_t cols = summaries.size() + 1;
+  const size_t rows = (size_t)std::count(summaries[0].begin(), summaries[0].end(), '\n') + 1;   // formatSummaries (:184-187)
+  std::vector<std::string> cell(rows * cols);
+  auto at = [&](size_t r, size_t c) -> std::string& { return cell[r * cols + c]; };
+  {                                                                 // addRowHeadings (:135-151)
+    const std::string& sum = summaries[0];
+    std::string::size_type pos = 0;
+    for (size_t i = 1; i < rows; ++i) {
+      const std::string::size_type end = sum.find(':', pos);
+      at(i, 0) = sum.substr(pos, end - pos);
+      pos = sum.find('\n', pos) + 1;
+    }
+  }
+  for (size_t i = 0; i + 1 < cols; ++i) at(0, i + 1) = "Tile " + std::to_string(i);   // addColHeadings (:153-161)
+  for (size_t t = 0; t < summaries.size(); ++t) {                   // addTileSummary (:163-176)
+    const std::string& summary = summaries[t];
+    std::string::size_type pos = summary.find(':') + 1;
+    for (size_t i = 1; i < rows; ++i) {
+      const std::string::size_type end = summary.find('\n', pos);
+      at(i, t + 1) = summary.substr(pos, end - pos);
+      pos = summary.find(':', pos) + 1;
+    }
+  }
+  std::vector<size_t> w(cols, 0);                                   // Table::flatten (:87-115)
+  for (size_t r = 0; r < rows; ++r)
+    for (size_t c = 0; c < cols; ++c) w[c] = std::max(w[c], at(r, c).length());
+  std::ostringstream out;
+  for (size_t r = 0; r < rows; ++r) {
+    for (size_t c = 0; c < cols; ++c) out << at(r, c) << std::string(w[c] - at(r, c).length(), ' ') << " | ";
+    out << '\n';
+  }
+  return out.str();
 }
 
 // One cache (tile, level) of a Backend with the reference Cache API.

@@ -93,3 +93,25 @@ def test_coherent_sim_out_over_rccl_ranks(tmp_path):
     assert len(got) == len(exp)
     for i, (x, y) in enumerate(zip(got, exp)):
         assert x == y, "line %d: %r != %r" % (i, x, y)
+
+
+@pytest.mark.gpu
+def test_coherent_summary_table_matches_reference_layout():
+    """gg_replay --table on a real coherent run: TileManager::outputSummary's
+    table (tile_manager_summary.cc:135-244) of exactly the per-tile blocks the
+    same run prints one by one."""
+    if not os.path.exists(REPLAY):
+        pytest.skip("gg_replay not built")
+    from tests.test_host_mirror import reference_table
+    args = [REPLAY, "--coherent", "--tiles", "16", "--per-tile", "200", "--hot-lines", "64", "--net", "hop_by_hop"]
+    blocks_txt = subprocess.run(args, capture_output=True, text=True, check=True, timeout=120).stdout
+    table = subprocess.run(args + ["--table"], capture_output=True, text=True, check=True, timeout=120).stdout
+    blocks, cur = [], None
+    for line in blocks_txt.splitlines(keepends=True):
+        if line.startswith("Tile ") and line.rstrip().endswith(" Summary:"):
+            cur = []
+            blocks.append(cur)
+        else:
+            cur.append(line)
+    assert len(blocks) == 16
+    assert table == reference_table(["".join(b) for b in blocks])

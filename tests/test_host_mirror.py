@@ -195,3 +195,55 @@ def test_memory_summary_format_matches_reference():
         reference_dram_summary(z, False) + reference_directory_summary(st, None) + \
         reference_dram_summary(st, False)
     assert out.splitlines() == exp
+
+
+def reference_table(summaries):
+    """TileManager::outputSummary's table (tile_manager_summary.cc:60-198),
+    restated with std::string::find semantics (npos + 1 wraps to 0)."""
+    def find(s, ch, pos):
+        i = s.find(ch, pos) if pos <= len(s) else -1
+        return i if i >= 0 else 2 ** 64 - 1
+
+    def substr(s, pos, n):
+        return s[pos:pos + n] if pos <= len(s) else None
+
+    npos1 = lambda v: (v + 1) % 2 ** 64
+    rows = summaries[0].count("\n") + 1
+    cols = len(summaries) + 1
+    cell = [[""] * cols for _ in range(rows)]
+    s0, pos = summaries[0], 0
+    for i in range(1, rows):                                  # addRowHeadings (:135-151)
+        end = find(s0, ":", pos)
+        cell[i][0] = substr(s0, pos, end - pos)
+        pos = npos1(find(s0, "\n", pos))
+    for i in range(cols - 1):                                 # addColHeadings (:153-161)
+        cell[0][i + 1] = "Tile %d" % i
+    for t, s in enumerate(summaries):                         # addTileSummary (:163-176)
+        pos = npos1(find(s, ":", 0))
+        for i in range(1, rows):
+            end = find(s, "\n", pos)
+            cell[i][t + 1] = substr(s, pos, end - pos)
+            pos = npos1(find(s, ":", pos))
+    w = [max(len(cell[r][c]) for r in range(rows)) for c in range(cols)]
+    return "".join("".join(cell[r][c] + " " * (w[c] - len(cell[r][c])) + " | " for c in range(cols)) + "\n"
+                   for r in range(rows))
+
+
+def test_tile_summary_table_matches_reference(tmp_path):
+    if not os.path.exists(REPLAY):
+        pytest.skip("gg_replay not built")
+    tiles = [
+        "Cache Summary:\n  Cache L1-D: \n    Cache Accesses: 1000\n    Miss Rate (%): 25\nNetwork Summary: \n",
+        "Cache Summary:\n  Cache L1-D: \n    Cache Accesses: 7\n    Miss Rate (%): 14.2857\nNetwork Summary: \n",
+        "Cache Summary:\n  Cache L1-D: \n    Cache Accesses: 123456789\n    Miss Rate (%): \nNetwork Summary: \n",
+        # not in "label: value" form: the reference's scanning drifts, and so must ours
+        "no colon here\n  a: b: c\ntail: 1\n\nx: y\n",
+    ]
+    files = []
+    for i, t in enumerate(tiles):
+        f = tmp_path / ("t%d.txt" % i)
+        f.write_text(t)
+        files.append(str(f))
+    for sel in (files[:3], files):
+        out = subprocess.run([REPLAY, "--format-table"] + sel, capture_output=True, text=True, check=True).stdout
+        assert out == reference_table([open(f).read() for f in sel])
