@@ -80,6 +80,30 @@ def pmc_traffic(kernel, key):
     return best
 
 
+# LDS peak: 256 B/clk/CU for the 16-B-per-lane ds_read_b128 the kernel issues
+# (MI355X_MICROARCH.md memory hierarchy: 64-256 B/clk by instruction) x 256 CUs
+# x 2.4 GHz
+LDS_PEAK_GBS = 256 * 256 * 2.4
+
+
+def pmc_lds(kernel, key):
+    """LDS bytes per launch of `kernel` (SQ_INSTS_LDS_{LOAD,STORE,ATOMIC}_BANDWIDTH,
+    64-B units, one PMC pass) from a committed summary of workload `key`."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "summary*.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("workload_key") != key:
+            continue
+        v = d.get("kernels", {}).get(kernel)
+        if v and "lds_bytes" in v:
+            best = {"bytes": v["lds_bytes"], "source": os.path.relpath(f, ROOT)}
+    return best
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -509,6 +533,12 @@ def private_section(args, dev):
     res["roofline"]["traffic"] = prof["bytes"] if prof else None
     if prof:
         res["roofline"]["traffic_source"] = prof["source"]
+    lds = pmc_lds(KERNEL_SYMBOL[dom], "private_%dx%d" % (T, N))
+    if lds:
+        # the kernel's LDS bytes per launch (PMC) over its live launch time
+        gbs = lds["bytes"] / (kern[dom]["ms"] * 1e-3) / 1e9
+        res["roofline"]["lds"] = {"achieved": gbs, "peak": LDS_PEAK_GBS, "unit": "GB/s", "frac": gbs / LDS_PEAK_GBS,
+                                  "bytes_per_launch": lds["bytes"], "source": lds["source"]}
     if not args.no_verify:
         from oracle import pyoracle as po
         cnt = be.cache_counters()
