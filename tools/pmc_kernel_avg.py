@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Per-kernel average of every PMC counter in a rocprofv3 counter_collection
-CSV (streams the file; prints one JSON line per kernel with >= 10 launches)."""
+CSV (streams the file; prints one JSON line per kernel with at least
+MIN_LAUNCHES launches, default 10).  usage: pmc_kernel_avg.py CSV [MIN_LAUNCHES]"""
 import collections
 import csv
 import json
@@ -15,9 +16,10 @@ def main():
             k = r["Kernel_Name"][:60]
             agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
             disp[k].add(r["Dispatch_Id"])
+    lim = int(sys.argv[2]) if len(sys.argv) > 2 else 10
     for k, v in agg.items():
         n = len(disp[k])
-        if n >= 10:
+        if n >= lim:
             print(json.dumps({"kernel": k, "launches": n, "per_launch": {c: round(x / n, 1) for c, x in sorted(v.items())}}))
 
 
