@@ -1970,7 +1970,7 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
       auto request = [&](uint64_t t, uint32_t nf) -> uint64_t {
         if (!qm) return 0;
         const uint64_t tc = time_to_cycles(t, P.np.f);
-        return regq ? rq.request(tc, nf, S.err) : (wave_q ? tr.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
+        return regq ? rq.request<false>(tc, nf, S.err) : (wave_q ? tr.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
       };
       const uint32_t nx = dir ? pos + 1 : pos - 1;
       uint64_t cq = 0, cf = 0;
@@ -1996,7 +1996,7 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
     auto request = [&](uint64_t t, uint32_t nf) -> uint64_t {
       if (!qm) return 0;
       const uint64_t tc = time_to_cycles(t, P.np.f);
-      return regq ? rq.request(tc, nf, S.err) : (wave_q ? tr.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
+      return regq ? rq.request<false>(tc, nf, S.err) : (wave_q ? tr.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
     };
     uint64_t cq = 0, cf = 0, m = 0;
     uint32_t spin = 0;

@@ -442,6 +442,15 @@ template <int CTRL> __device__ __forceinline__ uint64_t dpp64(uint64_t v)
 constexpr int kDppWaveShl1 = 0x130;    // lane l <- lane l + 1
 constexpr int kDppWaveShr1 = 0x138;    // lane l <- lane l - 1
 
+// lane mask of a 64-bit comparison (one v_cmp into an SGPR pair, no bool
+// materialization between compare and ballot)
+template <int PRED> __device__ __forceinline__ uint64_t cmp64(uint64_t a, uint64_t b)
+{
+  return __builtin_amdgcn_uicmpl(a, b, PRED);
+}
+constexpr int kCmpULE = 37, kCmpUGE = 35;     // ICmpInst predicates
+__device__ __forceinline__ uint64_t low_lanes(uint32_t n) { return n >= 64 ? ~0ull : ((1ull << n) - 1); }
+
 struct RegQueue {
   uint64_t a0, b0, a1, b1;             // this lane's intervals of slot 0 / slot 1
   uint32_t sz, cap, ln;
@@ -474,8 +483,15 @@ struct RegQueue {
     q->sig_sq = sig_sq; q->sig = sig; q->n = nreq; q->newest = newest;
     q->util = util; q->last_req = last_req; q->total_req = total_req; q->analytical = anl;
   }
-  __device__ __forceinline__ uint64_t A(uint32_t i) const { return i < 64 ? rl64(a0, i) : rl64(a1, i - 64); }
-  __device__ __forceinline__ uint64_t B(uint32_t i) const { return i < 64 ? rl64(b0, i) : rl64(b1, i - 64); }
+  // interval i's bounds: both slots read, then a scalar select (no branch)
+  __device__ __forceinline__ uint64_t A(uint32_t i) const
+  {
+    const uint32_t l = i & 63; const uint64_t u = rl64(a0, l), v = rl64(a1, l); return i < 64 ? u : v;
+  }
+  __device__ __forceinline__ uint64_t B(uint32_t i) const
+  {
+    const uint32_t l = i & 63; const uint64_t u = rl64(b0, l), v = rl64(b1, l); return i < 64 ? u : v;
+  }
   __device__ __forceinline__ void set(uint32_t i, uint64_t a, uint64_t b)
   {
     if ((i & 63) == ln) { if (i < 64) { a0 = a; b0 = b; } else { a1 = a; b1 = b; } }
@@ -498,7 +514,12 @@ struct RegQueue {
     if (ln >= k) { a0 = ln == 63 ? ca : na0; b0 = ln == 63 ? cb : nb0; }
     if (ln + 64 >= k) { a1 = na1; b1 = nb1; }
   }
-  // computeQueueDelay (queue_model_history_tree.cc:44-126) + QueueModelMG1::updateQueue
+  // computeQueueDelay (queue_model_history_tree.cc:44-126) + QueueModelMG1::updateQueue.
+  // TAIL: also the O(1) branch for requests served by the last two intervals
+  // (in-order streams: SELF / injection ports); the walkers' requests land
+  // mid-list 84 % of the time and skip that check (TAIL = false: the general
+  // search serves those requests too, with the same result).
+  template <bool TAIL = true>
   __device__ __forceinline__ uint64_t request(uint64_t t, uint64_t p, uint32_t* err)
   {
     errp = err;
@@ -509,7 +530,7 @@ struct RegQueue {
       ++n_fast;
       if (t - la >= min_proc) { set(sz - 1, la, t); set(sz, t + p, lb); ++sz; }
       else set(sz - 1, t + p, lb);
-    } else if (sz >= 2 && t < la && t >= A(sz - 2)) {
+    } else if (TAIL && sz >= 2 && t < la && t >= A(sz - 2)) {
       // the tail: interval sz-2 is the last one starting at or before t (and
       // interval 0 starts before t: no M/G/1).  Either [t, t+p] fits in it, or
       // the first later interval long enough is the last one (unbounded)
@@ -535,16 +556,18 @@ struct RegQueue {
       qd = mg1_queue_delay(nreq, newest, sig_sq, sig);
     } else {
       ++n_gen;
-      const bool v0 = ln < sz, v1 = ln + 64 < sz;
-      const uint32_t cnt = (uint32_t)__builtin_popcountll(__ballot(v0 && a0 <= t)) +
-                           (uint32_t)__builtin_popcountll(__ballot(v1 && a1 <= t));
-      int i = -1;
-      if (cnt > 0 && t + p <= B(cnt - 1)) i = (int)cnt - 1;
-      if (i < 0) {
-        const uint64_t m0 = __ballot(v0 && ln >= cnt && b0 - a0 >= p);
-        const uint64_t m1 = __ballot(v1 && ln + 64 >= cnt && b1 - a1 >= p);
-        i = m0 ? (int)__builtin_ctzll(m0) : (m1 ? 64 + (int)__builtin_ctzll(m1) : -1);
-      }
+      // fit: a <= t && t + p <= b — at most one interval (the intervals are
+      // disjoint and sorted: any earlier one ends before the last start <= t),
+      // the last one starting at or before t; else the first later one
+      // (a > t) with b - a >= p.  Lane masks straight from the compares.
+      const uint64_t tp = t + p;
+      const uint64_t v0 = low_lanes(sz), v1 = sz > 64 ? low_lanes(sz - 64) : 0ull;
+      const uint64_t le0 = cmp64<kCmpULE>(a0, t) & v0, le1 = cmp64<kCmpULE>(a1, t) & v1;
+      const uint64_t f0 = le0 & cmp64<kCmpUGE>(b0, tp), f1 = le1 & cmp64<kCmpUGE>(b1, tp);
+      const uint64_t l0 = ~le0 & v0 & cmp64<kCmpUGE>(b0 - a0, p), l1 = ~le1 & v1 & cmp64<kCmpUGE>(b1 - a1, p);
+      const bool fit = (f0 | f1) != 0;
+      const uint64_t m0 = fit ? f0 : l0, m1 = fit ? f1 : l1;
+      const int i = m0 ? (int)__builtin_ctzll(m0) : (m1 ? 64 + (int)__builtin_ctzll(m1) : -1);
       if (i < 0) {
         errs |= GG_DERR_STATE;
       } else {
