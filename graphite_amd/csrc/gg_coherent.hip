@@ -1859,9 +1859,8 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
   const uint32_t npos = sd.hi - sd.lo + 1;
   uint8_t* qimg = smem;
   uint64_t* lc = reinterpret_cast<uint64_t*>(smem + (size_t)npos * P.qimg);     // [npos][kNetCtr]
-  uint64_t* wlow = lc + (size_t)npos * kNetCtr;                                  // [kMaxWalkWaves] horizons
-  uint64_t* wfin = wlow + kMaxWalkWaves;                                         // [kMaxWalkWaves] done flags
-  uint32_t* rlohi = reinterpret_cast<uint32_t*>(wfin + kMaxWalkWaves);           // lo, ~hi of the visited positions
+  uint64_t* wlow = lc + (size_t)npos * kNetCtr;                                  // [kMaxWalkWaves] horizons (kInf: done)
+  uint32_t* rlohi = reinterpret_cast<uint32_t*>(wlow + kMaxWalkWaves);           // lo, ~hi of the visited positions
   uint8_t* pk = reinterpret_cast<uint8_t*>(wlow) + kWalkSync;
   if (n > P.walk_pk) { if (tid == 0) { atomicOr(S.err, GG_DERR_CAP); *cntp = 0; } return; }
   WalkLds W;
@@ -1881,7 +1880,7 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
     W.Pf[i] = (uint32_t)nflits(P.np, has_data(m.type) ? P.bits_data : P.bits_req);
   }
   for (uint32_t i = tid; i < npos * kNetCtr; i += nthr) lc[i] = 0;
-  for (uint32_t i = tid; i < kMaxWalkWaves; i += nthr) { wlow[i] = 0; wfin[i] = 0; }
+  for (uint32_t i = tid; i < kMaxWalkWaves; i += nthr) wlow[i] = 0;
   if (tid == 0) { rlohi[0] = ~0u; rlohi[1] = ~0u; }
   __syncthreads();
   // canonical ranks (by send time, sender, seq); the positions the packets can visit
@@ -2001,7 +2000,8 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
     uint64_t cq = 0, cf = 0, m = 0;
     uint32_t spin = 0;
     // up to 128 packets: lane l watches packets l and l + 64 if their route
-    // crosses this port (entered at or before it, leaving after it)
+    // crosses this port (entered at or before it, leaving after it); their
+    // rank, flits and exit position are fixed, so they stay in registers
     const bool small = n <= 128;
     auto crosses = [&](uint32_t i) {
       if (i >= n) return false;
@@ -2009,33 +2009,32 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
       return dir ? (a <= pos && pos < z) : (a >= pos && pos > z);
     };
     bool c0 = small && crosses(ln), c1 = small && crosses(ln + 64);
-    // a candidate's rank is fixed, and it is pending here only with status 0:
-    // it reaches this port on a continuing hop (or starts here)
     const uint32_t r0 = c0 ? W.Pr[ln] : 0u, r1 = c1 ? W.Pr[ln + 64] : 0u;
+    const uint32_t f0 = c0 ? W.Pf[ln] & 0xFFFFFFu : 0u, f1 = c1 ? W.Pf[ln + 64] & 0xFFFFFFu : 0u;
+    const uint32_t d0 = c0 ? W.Pd[ln] : 0u, d1 = c1 ? W.Pd[ln + 64] : 0u;
     while (visited) {
-      // the horizon: packets still to come from upstream arrive at or after bound
+      // the horizon: packets still to come from upstream arrive at or after
+      // bound; the wave before publishes kInf once it has served its last one
       bool up_fin = true;
       uint64_t bound = kInf;
       if (wv > 0) {
-        up_fin = lds_load_acq(&wfin[wv - 1]) != 0;
-        if (!up_fin) {
-          const uint64_t ul = lds_load_acq(&wlow[wv - 1]);
-          bound = ul == kInf ? kInf : ul + zps;
-        }
+        const uint64_t ul = lds_load_acq(&wlow[wv - 1]);
+        up_fin = ul == kInf;
+        bound = up_fin ? kInf : ul + zps;
       }
       // the least pending packet at this position, by (time, rank): each lane
       // its least, then a scalar pass over the lanes holding one (usually few)
       uint64_t mk = kInf;
-      uint32_t mi = 0;
+      uint32_t mi = 0, mf = 0, md = 0;
       if (small) {
         // a candidate is pending once it sits at this port (status 0 there)
         // acquire: the packet's time, written before its position, is then current
         const uint32_t q0 = c0 ? __hip_atomic_load(&W.Pp[ln], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) : ~0u;
         const uint32_t q1 = c1 ? __hip_atomic_load(&W.Pp[ln + 64], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) : ~0u;
-        if (q0 == pos) { mk = (W.Pt[ln] << 12) | r0; mi = ln; }
+        if (q0 == pos) { mk = (W.Pt[ln] << 12) | r0; mi = ln; mf = f0; md = d0; }
         if (q1 == pos) {
           const uint64_t k = (W.Pt[ln + 64] << 12) | r1;
-          if (k < mk) { mk = k; mi = ln + 64; }
+          if (k < mk) { mk = k; mi = ln + 64; mf = f1; md = d1; }
         }
       } else {
         for (uint32_t b0 = 0; b0 < n; b0 += 64) {
@@ -2043,7 +2042,7 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
           if (i < n && __hip_atomic_load(&W.Pp[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == pos &&
               (W.Pf[i] >> 24) == 0) {
             const uint64_t k = (W.Pt[i] << 12) | W.Pr[i];
-            if (k < mk) { mk = k; mi = i; }
+            if (k < mk) { mk = k; mi = i; mf = W.Pf[i] & 0xFFFFFFu; md = W.Pd[i]; }
           }
         }
       }
@@ -2063,22 +2062,27 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
         __builtin_amdgcn_s_sleep(1);
         continue;
       }
+      // serve it (the router + link of serve_packet, its fields from the lanes)
       const uint32_t i = (uint32_t)__builtin_amdgcn_readlane((int)mi, (int)wl);
-      cq += serve_packet(P, S, W, request, i, nx, sd, zps, cf);
-      ++m;
+      const uint32_t nf = (uint32_t)__builtin_amdgcn_readlane((int)mf, (int)wl);
+      const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)md, (int)wl);
+      const uint64_t qd = request(T, nf);
+      cq += qd; cf += nf; ++m;
+      uint32_t status = 0;
+      if (nx < sd.lo || nx > sd.hi) status = 2;            // next router in another shard: held
+      else if (nx == d) status = 1;                        // leaves the run: next stage
       if (small && ln == (i & 63)) { if (i < 64) c0 = false; else c1 = false; }   // served here: no longer a candidate
-      // Pt / Pz / Pf of the packet before it appears downstream (Pp), then the horizon
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (ln == 0) {
+        // time and status (the zero-load part: + zps per port, added at the
+        // hand-off) before the packet appears downstream (Pp), then the horizon
+        W.Pt[i] = T + zps + lat_to_ps(qd, P.np.f);
+        W.Pf[i] = nf | (status << 24);
         __hip_atomic_store(&W.Pp[i], nx, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         lds_store_rel(&wlow[wv], T);
       }
       wave_sync();
     }
-    if (ln == 0) {
-      lds_store_rel(&wlow[wv], kInf);
-      lds_store_rel(&wfin[wv], 1ull);
-    }
+    if (ln == 0) lds_store_rel(&wlow[wv], kInf);
     if (regq && visited) rq.store(tr.q, tr.nd);
     if (ln == 0 && visited) add_ctr(pos, cq, m, cf);
     nev = (uint32_t)m;
@@ -2091,12 +2095,17 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
     const uint32_t r = W.Pi[i], stt = W.Pf[i] >> 24;
     const uint32_t h = tile_at(W.Pp[i]);
     gg_cmsg* m = cur + r;
-    m->arrival_ps = W.Pt[i]; m->zero_load_ps = W.Pz[i]; m->hop = h;
+    uint64_t z = W.Pz[i];
+    if (PIPE) {                                                // the pipeline adds zps per port here
+      const uint32_t p0 = pos_of(m->hop), p1 = W.Pp[i];
+      z += (uint64_t)(dir ? p1 - p0 : p0 - p1) * zps;
+    }
+    m->arrival_ps = W.Pt[i]; m->zero_load_ps = z; m->hop = h;
     if (stt == 2) {                                            // held for the quantum boundary
       const uint32_t j = atomicAdd(S.bnd_cnt, 1u);
       if (j >= P.msg_cap) { atomicOr(S.err, GG_DERR_CAP); continue; }
       gg_cmsg g = *m;
-      g.arrival_ps = W.Pt[i]; g.zero_load_ps = W.Pz[i]; g.hop = h;
+      g.arrival_ps = W.Pt[i]; g.zero_load_ps = z; g.hop = h;
       S.bnd[j] = g;
       ++nb;
       continue;
