@@ -1786,6 +1786,9 @@ __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t L, uint32_t 
 // ---------------------------------------------------------------------------
 constexpr uint32_t kWalkSync = 512;                  // LDS: per-wave horizon / done words, run bounds
 constexpr uint32_t kMaxWalkWaves = 16;
+#ifndef GG_WALK_SLEEP
+#define GG_WALK_SLEEP 1                              // s_sleep units (64 cycles) between horizon polls
+#endif
 
 __device__ __forceinline__ uint64_t wave_min64(uint64_t v)
 {
@@ -2059,7 +2062,7 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
         // wait for upstream progress; publish what this port can still serve
         if (ln == 0) lds_store_rel(&wlow[wv], T < bound ? T : bound);
         if (++spin > (1u << 20)) { if (ln == 0) atomicOr(S.err, GG_DERR_STATE); break; }
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(GG_WALK_SLEEP);
         continue;
       }
       // serve it (the router + link of serve_packet, its fields from the lanes)
