@@ -332,7 +332,9 @@ def noc_section(args, dev):
     d = lambda x: torch.from_numpy(x.view(np.int64 if x.dtype == np.uint64 else np.int32)).to(dev)
     res = {"workload": "uniform-random packets of %d bits on the %d-tile mesh (configs[3]), one batch per model, "
                        "injection times ~50 ps apart" % (C.shmem_modeled_bits(T, True), T),
-           "bytes_per_packet": 44}
+           "bytes_per_packet": 44,
+           "bytes_per_packet_note": "44 B = this ABI's I/O (src, dst, bits u32; time u64 in; arrival, zero-load, "
+                                    "contention u64 out); SURVEY.md section 8d's packed format is 24 B (GB_s_24)"}
     # the closed-form model is one thread per packet: a large batch; the hop-by-hop walk is serial per chain
     for name, model, n in (("hop_counter", C.NET_EMESH_HOP_COUNTER, 64 * args.noc_packets),
                            ("hop_by_hop", C.NET_EMESH_HOP_BY_HOP, args.noc_packets)):
@@ -351,7 +353,8 @@ def noc_section(args, dev):
         e1.record()
         torch.cuda.synchronize()
         dt = e0.elapsed_time(e1) / 1e3
-        r = {"packets": n, "value": n / dt, "unit": "packets/s", "seconds": dt, "GB_s": 44 * n / dt / 1e9}
+        r = {"packets": n, "value": n / dt, "unit": "packets/s", "seconds": dt, "GB_s": 44 * n / dt / 1e9,
+             "GB_s_24": 24 * n / dt / 1e9}
         if not args.no_verify:
             on = po.OracleNoc(C.default_config(T, net_model=model))
             c0 = time.perf_counter()

@@ -21,5 +21,5 @@ mkdir -p $OUT/lds
     python3 "$GRAFT_REPO_ROOT/bench.py" --sections private --no-cpu-baseline --no-verify --steps 1 --warmup 0 \
     > "$GRAFT_REPO_ROOT/$OUT/lds/bench.json" 2> "$GRAFT_REPO_ROOT/$OUT/lds/bench.err" )
 rc=$?; echo "lds pmc rc=$rc"; [ $rc -eq 0 ] || exit $rc
-python3 tools/pmc_kernel_avg.py /tmp/ldspmc/p_counter_collection.csv > $OUT/lds/avg.jsonl
+python3 tools/pmc_kernel_avg.py /tmp/ldspmc/p_counter_collection.csv 1 > $OUT/lds/avg.jsonl
 exit $?
