@@ -105,6 +105,7 @@ struct CP {
   uint32_t seg_xcd;                      // > 0: runs interleaved by shard (seg_xcd shards), XCD-grouped walker blocks
   uint32_t cache_lds_off, cache_lds_bytes; // k_c_persist<true>: the tile's cache state in LDS after the step's
   uint32_t touch_each;                     // hit runs touch LRU rows one record at a time (> 16 ways; GG_COH_TOUCH_EACH=1)
+  uint32_t walk_wide;                      // pipelined walkers scan every packet (the > 128-packet path; GG_COH_WALK_WIDE=1)
   uint32_t no_hit_runs;                    // GG_COH_NO_HIT_RUNS=1: every record through app_access
   uint64_t lat_l1d, lat_l1t, lat_l2d, lat_l2t, lat_dir, gap_ps, dram_proc, dram_cost;
   NocParams np;
@@ -2005,7 +2006,7 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
     // up to 128 packets: lane l watches packets l and l + 64 if their route
     // crosses this port (entered at or before it, leaving after it); their
     // rank, flits and exit position are fixed, so they stay in registers
-    const bool small = n <= 128;
+    const bool small = n <= 128 && !P.walk_wide;
     auto crosses = [&](uint32_t i) {
       if (i >= n) return false;
       const uint32_t a = W.Pp[i], z = W.Pd[i];
@@ -2621,6 +2622,8 @@ static gg_status coh_alloc(gg_ctx* ctx)
   {
     const char* te = getenv("GG_COH_TOUCH_EACH");
     P.touch_each = te && atoi(te) ? 1u : 0u;
+    const char* ww = getenv("GG_COH_WALK_WIDE");
+    P.walk_wide = ww && atoi(ww) ? 1u : 0u;
     const char* nh = getenv("GG_COH_NO_HIT_RUNS");
     P.no_hit_runs = nh && atoi(nh) ? 1u : 0u;
   }

@@ -88,6 +88,21 @@ def test_coherent_small_mesh_launch_path(T, N, hot, K, net, env, monkeypatch):
     _compare(cfg, a, m, o)
 
 
+@pytest.mark.parametrize("T,N,hot,K", [(256, 300, 64, 8), (256, 300, 64, 1)])
+@pytest.mark.parametrize("env", ["GG_COH_WALK_SWEEP", "GG_COH_WALK_WIDE"])
+def test_coherent_walker_variants(T, N, hot, K, env, monkeypatch):
+    """The hop-by-hop walkers' three forms give the same run: the pipeline
+    (one wave per router position) with its per-lane candidate packets (the
+    default), the pipeline scanning every packet (GG_COH_WALK_WIDE=1, the
+    path of runs with more than 128 packets in a step) and the one-wave
+    position sweep (GG_COH_WALK_SWEEP=1, runs longer than 16 routers)."""
+    from oracle import pyoracle as po
+    monkeypatch.setenv(env, "1")
+    cfg = C.default_config(T, num_shards=K, net_model=C.NET_EMESH_HOP_BY_HOP)
+    a, m, o = po.gen_trace(T, N, hot_lines=hot)
+    _compare(cfg, a, m, o)
+
+
 @pytest.mark.parametrize("a1,p1,a2,p2,hot,each", [
     (4, C.POLICY_LRU, 8, C.POLICY_LRU, 16, 1),     # the touch-at-a-time path (> 16 ways)
     (2, C.POLICY_LRU, 16, C.POLICY_LRU, 16, 0),    # 2-way L1: rows loaded byte by byte
