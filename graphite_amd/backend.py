@@ -53,7 +53,7 @@ class _PacketOut(ctypes.Structure):
 EXPORTS = ["gg_abi_version", "gg_last_error", "gg_config_default", "gg_create", "gg_destroy", "gg_reset",
            "gg_cache_access_batch", "gg_cache_get_counters", "gg_cache_get_line_info",
            "gg_cache_set_line_info", "gg_cache_access_line", "gg_cache_insert_line",
-           "gg_noc_route_batch", "gg_noc_get_counters", "gg_queue_delay_batch",
+           "gg_noc_route_batch", "gg_noc_route_tree", "gg_noc_get_counters", "gg_queue_delay_batch",
            "gg_gen_uniform_trace", "gg_kernel_time_ms", "gg_set_timing",
            "gg_coherent_begin", "gg_coherent_quantum", "gg_coherent_export", "gg_coherent_import",
            "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace", "gg_shard_map",
@@ -93,6 +93,8 @@ def load():
     L.gg_cache_insert_line.argtypes = [vp, u32, i32, u64, ctypes.POINTER(LineInfo), ctypes.POINTER(i32),
                                        ctypes.POINTER(u64), ctypes.POINTER(LineInfo)]
     L.gg_noc_route_batch.argtypes = [vp, ctypes.POINTER(_Packets), ctypes.POINTER(_PacketOut), vp]
+    L.gg_noc_route_tree.argtypes = [vp, ctypes.POINTER(_Packets), ctypes.POINTER(_PacketOut),
+                                    ctypes.POINTER(_PacketOut), u64, vp]
     L.gg_noc_get_counters.argtypes = [vp, vp]
     L.gg_queue_delay_batch.argtypes = [vp, u64, vp, vp, u64, vp]
     L.gg_gen_uniform_trace.argtypes = [vp, vp, u32, u32, u64, u64, u32, u32, vp]
@@ -120,7 +122,8 @@ def load():
         getattr(L, name).restype = i32
     for name in ["gg_reset", "gg_cache_access_batch", "gg_cache_get_counters", "gg_cache_get_line_info",
                  "gg_cache_set_line_info", "gg_cache_access_line", "gg_cache_insert_line",
-                 "gg_noc_route_batch", "gg_noc_get_counters", "gg_queue_delay_batch", "gg_gen_uniform_trace"]:
+                 "gg_noc_route_batch", "gg_noc_route_tree", "gg_noc_get_counters", "gg_queue_delay_batch",
+                 "gg_gen_uniform_trace"]:
         getattr(L, name).restype = i32
     _lib = L
     return L
@@ -240,6 +243,24 @@ class Backend:
         pk = _Packets(src.data_ptr(), dst.data_ptr(), length_bits.data_ptr(), time_ps.data_ptr(), n)
         out = _PacketOut(arrival.data_ptr(), zero_load.data_ptr(), contention.data_ptr())
         _check(load().gg_noc_route_batch(self.h, ctypes.byref(pk), ctypes.byref(out), _stream(stream)))
+
+    def noc_route_tree(self, src, dst, length_bits, time_ps, arrival, zero_load, contention,
+                       b_arrival, b_zero_load, b_contention, num_broadcasts, stream=None):
+        """gg_noc_route_tree: dst == config.BROADCAST takes the hop-by-hop broadcast
+        tree; b_* hold num_broadcasts x num_tiles deliveries (batch order)."""
+        import torch
+        n = src.numel()
+        for t, dt in ((src, torch.int32), (dst, torch.int32), (length_bits, torch.int32), (time_ps, torch.int64),
+                      (arrival, torch.int64), (zero_load, torch.int64), (contention, torch.int64)):
+            _need_dev(t, dt, n)
+        nbt = num_broadcasts * self.cfg.num_tiles
+        for t in (b_arrival, b_zero_load, b_contention):
+            _need_dev(t, torch.int64, nbt)
+        pk = _Packets(src.data_ptr(), dst.data_ptr(), length_bits.data_ptr(), time_ps.data_ptr(), n)
+        out = _PacketOut(arrival.data_ptr(), zero_load.data_ptr(), contention.data_ptr())
+        bout = _PacketOut(b_arrival.data_ptr(), b_zero_load.data_ptr(), b_contention.data_ptr())
+        _check(load().gg_noc_route_tree(self.h, ctypes.byref(pk), ctypes.byref(out), ctypes.byref(bout),
+                                        num_broadcasts, _stream(stream)))
 
     def noc_counters(self):
         out = np.zeros(self.cfg.num_tiles * NUM_NET_COUNTERS, np.uint64)

@@ -50,7 +50,10 @@ NET_COUNTERS = ["packets_sent", "flits_sent", "bits_sent", "packets_received",
                 "total_contention_ps", "buffer_writes", "buffer_reads",
                 "switch_alloc", "crossbar", "link_traversals",
                 "router_contention_cycles", "router_packets", "analytical_requests"] + \
-               ["port%d_utilized_cycles" % p for p in range(5)] + ["port%d_last_cycles" % p for p in range(5)]
+               ["port%d_utilized_cycles" % p for p in range(5)] + ["port%d_last_cycles" % p for p in range(5)] + \
+               ["packets_broadcasted", "flits_broadcasted", "bits_broadcasted"] + \
+               ["crossbar%d" % m for m in range(2, 6)]
+BROADCAST = 0xDEADBABE   # NetPacket::BROADCAST (network.h:54), GG_BROADCAST
 NUM_CACHE_COUNTERS = len(CACHE_COUNTERS)
 
 # coherent mode (include/graphite_gpu.h)

@@ -311,6 +311,16 @@ gg_status gg_noc_route_batch(gg_ctx* ctx, const gg_packets* pk, const gg_packet_
   return gg_noc_run(ctx, pk, out, s);
 }
 
+gg_status gg_noc_route_tree(gg_ctx* ctx, const gg_packets* pk, const gg_packet_out* out,
+                            const gg_packet_out* bcast_out, uint64_t num_broadcasts, void* stream)
+{
+  if (!ctx || !pk || !out) return gg_fail(GG_ERR_INVALID, "NULL argument");
+  hipSetDevice(ctx->device);
+  hipStream_t s = (hipStream_t)stream;
+  ctx->last_stream = s;
+  return gg_noc_tree(ctx, pk, out, bcast_out, num_broadcasts, s);
+}
+
 gg_status gg_noc_get_counters(gg_ctx* ctx, uint64_t* out)
 {
   if (!ctx || !out) return gg_fail(GG_ERR_INVALID, "NULL argument");

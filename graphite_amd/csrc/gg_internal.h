@@ -131,6 +131,8 @@ gg_status gg_noc_alloc(gg_ctx* ctx);
 void      gg_noc_free(gg_ctx* ctx);
 gg_status gg_noc_reset(gg_ctx* ctx, hipStream_t s);
 gg_status gg_noc_run(gg_ctx* ctx, const gg_packets* pk, const gg_packet_out* out, hipStream_t s);
+gg_status gg_noc_tree(gg_ctx* ctx, const gg_packets* pk, const gg_packet_out* out, const gg_packet_out* bout,
+                      uint64_t nb, hipStream_t s);
 gg_status gg_noc_counters(gg_ctx* ctx, uint64_t* out);
 // coherent path (gg_coherent.hip)
 void      gg_coh_free(gg_ctx* ctx);

@@ -647,6 +647,130 @@ __global__ void k_analytical(const HQueue* q, uint32_t tiles, uint64_t* ctr)
 
 }  // namespace
 
+// ---------------------------------------------------------------------------
+// Broadcast tree (gg_noc_route_tree): NetworkModelEMeshHopByHop::routePacket's
+// broadcast branch (network_model_emesh_hop_by_hop.cc:163-221).  A broadcast
+// event at router c asks all its listed output-port queues at one time and
+// forwards every copy with the max delay (RouterModel::processPacket over a
+// port list, router_model.cc:71-108), so the row (X) and column (Y) port
+// chains are no longer independent stages: the walk is one global
+// (time, packet index) event order — injection events (SEND_TILE, :151-159)
+// and router events in one heap, every event carrying its copy's time,
+// zero-load and contention sums.  One lane walks; the heap lives in HBM.
+// ---------------------------------------------------------------------------
+struct TEv { uint64_t t, zl, ct; uint32_t id, at; };   // at: router tile, | kInjBit = injection port of src
+constexpr uint32_t kInjBit = 0x80000000u;
+__device__ __forceinline__ bool tev_lt(const TEv& a, const TEv& b) { return a.t < b.t || (a.t == b.t && a.id < b.id); }
+__device__ __forceinline__ void theap_push(TEv* h, uint64_t& n, const TEv& e)
+{
+  uint64_t i = n++;
+  while (i > 0) { uint64_t p = (i - 1) / 2; if (!tev_lt(e, h[p])) break; h[i] = h[p]; i = p; }
+  h[i] = e;
+}
+__device__ __forceinline__ TEv theap_pop(TEv* h, uint64_t& n)
+{
+  TEv top = h[0], last = h[--n];
+  uint64_t i = 0;
+  for (;;) {
+    uint64_t l = 2 * i + 1, r = l + 1, m = i;
+    TEv cand = last;
+    if (l < n && tev_lt(h[l], cand)) { m = l; cand = h[l]; }
+    if (r < n && tev_lt(h[r], cand)) m = r;
+    if (m == i) break;
+    h[i] = h[m]; i = m;
+  }
+  if (n) h[i] = last;
+  return top;
+}
+
+__global__ __launch_bounds__(64) void k_tree_walk(NocDev D, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                                                  const uint32_t* __restrict__ len, const uint64_t* __restrict__ t0,
+                                                  uint64_t n, uint64_t nb, TEv* heap, uint64_t hcap, uint32_t* bidx,
+                                                  gg_packet_out out, gg_packet_out bout)
+{
+  if (threadIdx.x != 0) return;
+  const NocParams& P = D.P;
+  // validate, number the broadcasts in batch order, seed the injection events
+  uint64_t m = 0, hn = 0;
+  for (uint64_t k = 0; k < n; ++k) {
+    const uint32_t s = src[k], d = dst[k];
+    if (s >= P.tiles || (d >= P.tiles && d != GG_BROADCAST)) { atomicOr(D.err, GG_DERR_RANGE); return; }
+    bidx[k] = d == GG_BROADCAST ? (uint32_t)m++ : ~0u;
+  }
+  if (m != nb || n + nb * P.tiles > hcap) { atomicOr(D.err, GG_DERR_CAP); return; }
+  for (uint64_t k = 0; k < n; ++k) {
+    const uint32_t s = src[k], d = dst[k];
+    if (s == d) { out.arrival_ps_dev[k] = t0[k]; out.zero_load_ps_dev[k] = 0; out.contention_ps_dev[k] = 0; continue; }
+    theap_push(heap, hn, TEv{t0[k], 0, 0, (uint32_t)k, s | kInjBit});
+  }
+  const uint32_t W = P.w, H = P.h;
+  while (hn) {
+    const TEv e = theap_pop(heap, hn);
+    const uint32_t k = e.id, s = src[k], d = dst[k], bits = len[k];
+    const uint64_t nf = nflits(P, bits);
+    if (e.at & kInjBit) {                          // injection router: delay 0, port 0
+      cadd(D.ctr, s, GG_NC_PACKETS_SENT, 1); cadd(D.ctr, s, GG_NC_FLITS_SENT, nf); cadd(D.ctr, s, GG_NC_BITS_SENT, bits);
+      if (d == GG_BROADCAST) {                     // updateSendCounters (network_model.cc:244-250)
+        cadd(D.ctr, s, GG_NC_PACKETS_BROADCASTED, 1); cadd(D.ctr, s, GG_NC_FLITS_BROADCASTED, nf);
+        cadd(D.ctr, s, GG_NC_BITS_BROADCASTED, bits);
+      }
+      uint64_t qd = 0;
+      if (P.qm) { HTree tr = D.tree(s, 5); qd = tr.delay(time_to_cycles(e.t, P.f), nf, D.err); }
+      const uint64_t cps = lat_to_ps(qd, P.f);
+      theap_push(heap, hn, TEv{e.t + lat_to_ps(0, P.f) + cps, 0, cps, k, s});
+      continue;
+    }
+    const uint32_t c = e.at, cx = c % W, cy = c / W;
+    int ports[5]; uint32_t nxt[5]; int np = 0;
+    if (d != GG_BROADCAST) {                       // XY (:223-256)
+      const uint32_t dx = d % W, dy = d / W;
+      if (cx > dx)      { ports[0] = P_LEFT;  nxt[0] = c - 1; }
+      else if (cx < dx) { ports[0] = P_RIGHT; nxt[0] = c + 1; }
+      else if (cy > dy) { ports[0] = P_DOWN;  nxt[0] = c - W; }
+      else if (cy < dy) { ports[0] = P_UP;    nxt[0] = c + W; }
+      else              { ports[0] = P_SELF;  nxt[0] = c; }
+      np = 1;
+    } else {                                       // broadcast tree (:163-221), next_dest_list order
+      const uint32_t sx = s % W, sy = s / W;
+      if (cy >= sy && cy + 1 < H) { ports[np] = P_UP;   nxt[np++] = c + W; }
+      if (cy <= sy && cy >= 1)    { ports[np] = P_DOWN; nxt[np++] = c - W; }
+      if (cy == sy) {
+        if (cx >= sx && cx + 1 < W) { ports[np] = P_RIGHT; nxt[np++] = c + 1; }
+        if (cx <= sx && cx >= 1)    { ports[np] = P_LEFT;  nxt[np++] = c - 1; }
+      }
+      ports[np] = P_SELF; nxt[np++] = c;
+    }
+    uint64_t qd = 0;
+    if (P.qm) {
+      for (int i = 0; i < np; ++i) {
+        HTree tr = D.tree(c, ports[i]);
+        qd = max(qd, tr.delay(time_to_cycles(e.t, P.f), nf, D.err));
+      }
+      cadd(D.ctr, c, GG_NC_ROUTER_CONTENTION_CYCLES, qd * (uint64_t)np);   // updateContentionCounters, per listed port
+      cadd(D.ctr, c, GG_NC_ROUTER_PACKETS, (uint64_t)np);
+    }
+    cadd(D.ctr, c, GG_NC_BUFFER_WRITES, nf); cadd(D.ctr, c, GG_NC_BUFFER_READS, nf);
+    cadd(D.ctr, c, GG_NC_SWITCH_ALLOC, 1);
+    cadd(D.ctr, c, np == 1 ? (int)GG_NC_CROSSBAR : (int)GG_NC_CROSSBAR_MULTI + np - 2, nf);
+    cadd(D.ctr, c, GG_NC_LINK_TRAVERSALS, nf * (uint64_t)np);
+    const uint64_t zps = lat_to_ps((uint64_t)P.router_delay + P.link_delay, P.f), cps = lat_to_ps(qd, P.f);
+    const uint64_t t = e.t + zps + cps, zl = e.zl + zps, ct = e.ct + cps;
+    for (int i = 0; i < np; ++i) {
+      if (ports[i] != P_SELF) { theap_push(heap, hn, TEv{t, zl, ct, k, nxt[i]}); continue; }
+      const uint64_t ser = lat_to_ps(nf, P.f);     // receive at c (network_model.cc:118-150,253-272)
+      cadd(D.ctr, c, GG_NC_PACKETS_RECEIVED, 1); cadd(D.ctr, c, GG_NC_FLITS_RECEIVED, nf);
+      cadd(D.ctr, c, GG_NC_BITS_RECEIVED, bits);
+      cadd(D.ctr, c, GG_NC_TOTAL_LATENCY_PS, zl + ser + ct); cadd(D.ctr, c, GG_NC_TOTAL_CONTENTION_PS, ct);
+      if (d == GG_BROADCAST) {
+        const uint64_t o = (uint64_t)bidx[k] * P.tiles + c;
+        bout.arrival_ps_dev[o] = t + ser; bout.zero_load_ps_dev[o] = zl + ser; bout.contention_ps_dev[o] = ct;
+      } else {
+        out.arrival_ps_dev[k] = t + ser; out.zero_load_ps_dev[k] = zl + ser; out.contention_ps_dev[k] = ct;
+      }
+    }
+  }
+}
+
 struct gg_noc_state {
   NocParams P;
   HQueue* q = nullptr; HNode* nd = nullptr; uint64_t nq = 0;
@@ -658,6 +782,7 @@ struct gg_noc_state {
   Ev* heap = nullptr;
   uint32_t* counts = nullptr; uint32_t* cursor = nullptr; uint64_t* off = nullptr; uint32_t nb_cap = 0;
   bool staged = true;   // LDS-staged stage kernels where the queues fit (GG_NOC_STAGED=0: HBM-resident, A/B)
+  TEv* theap = nullptr; uint32_t* bidx = nullptr; uint64_t tcap = 0, bcap = 0;   // broadcast-tree walk scratch
 };
 
 gg_status gg_noc_alloc(gg_ctx* ctx)
@@ -699,7 +824,7 @@ void gg_noc_free(gg_ctx* ctx)
   gg_noc_state* S = ctx->noc;
   if (!S) return;
   void* ps[] = {S->q, S->nd, S->ctr, S->t, S->zl, S->ct, S->cur, S->keys, S->ids, S->heap,
-                S->counts, S->cursor, S->off};
+                S->counts, S->cursor, S->off, S->theap, S->bidx};
   for (void* p : ps) if (p) hipFree(p);
   delete S;
   ctx->noc = nullptr;
@@ -765,6 +890,42 @@ gg_status gg_noc_run(gg_ctx* ctx, const gg_packets* pk, const gg_packet_out* out
   GG_HIP(hipMemcpyAsync(out->arrival_ps_dev, S->t, 8 * n, hipMemcpyDeviceToDevice, s));
   GG_HIP(hipMemcpyAsync(out->zero_load_ps_dev, S->zl, 8 * n, hipMemcpyDeviceToDevice, s));
   GG_HIP(hipMemcpyAsync(out->contention_ps_dev, S->ct, 8 * n, hipMemcpyDeviceToDevice, s));
+  return GG_OK;
+}
+
+gg_status gg_noc_tree(gg_ctx* ctx, const gg_packets* pk, const gg_packet_out* out, const gg_packet_out* bout,
+                      uint64_t nb, hipStream_t s)
+{
+  gg_noc_state* S = ctx->noc;
+  const NocParams& P = S->P;
+  const uint64_t n = pk->num_packets;
+  if (P.net_model != GG_NET_EMESH_HOP_BY_HOP)
+    return gg_fail(GG_ERR_UNSUPPORTED, "broadcast tree: emesh_hop_by_hop only (network.cc:187-195 unrolls the others)");
+  if (P.w * P.h != P.tiles) return gg_fail(GG_ERR_UNSUPPORTED, "emesh_hop_by_hop needs a full W x H mesh (hop_by_hop.cc:55-59)");
+  if (n == 0) return GG_OK;
+  if (!pk->src_dev || !pk->dst_dev || !pk->length_bits_dev || !pk->time_ps_dev ||
+      !out->arrival_ps_dev || !out->zero_load_ps_dev || !out->contention_ps_dev ||
+      (nb && (!bout || !bout->arrival_ps_dev || !bout->zero_load_ps_dev || !bout->contention_ps_dev)))
+    return gg_fail(GG_ERR_INVALID, "NULL packet or output pointer");
+  if (n >= (1ull << 32) || nb > n) return gg_fail(GG_ERR_RANGE, "batch larger than 2^32 packets or num_broadcasts > packets");
+  const uint64_t hcap = n + nb * P.tiles;          // live copies of a broadcast <= tiles
+  if (hcap > S->tcap) {
+    if (S->theap) hipFree(S->theap);
+    GG_HIP(hipMalloc((void**)&S->theap, sizeof(TEv) * hcap));
+    S->tcap = hcap;
+  }
+  if (n > S->bcap) {
+    if (S->bidx) hipFree(S->bidx);
+    GG_HIP(hipMalloc((void**)&S->bidx, 4 * n));
+    S->bcap = n;
+  }
+  NocDev D{P, S->q, S->nd, S->ctr, ctx->err_dev};
+  const gg_packet_out none{nullptr, nullptr, nullptr};
+  gg_timer_begin(ctx, "noc_tree", s);
+  hipLaunchKernelGGL(k_tree_walk, dim3(1), dim3(64), 0, s, D, pk->src_dev, pk->dst_dev, pk->length_bits_dev,
+                     pk->time_ps_dev, n, nb, S->theap, S->tcap, S->bidx, *out, nb ? *bout : none);
+  GG_HIP(hipGetLastError());
+  gg_timer_end(ctx, "noc_tree", s);
   return GG_OK;
 }
 

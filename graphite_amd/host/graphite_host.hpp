@@ -143,8 +143,8 @@ inline void writeCacheSummary(std::ostream& out, const std::string& name, const 
 // GG_NC_* counters, followed for emesh_hop_counter by its event counters
 // (network_model_emesh_hop_counter.cc:160-165,226-236).  Time::toCycles /
 // toNanosec (misc/time_types.h:104-114) on the picosecond sums; averages are
-// float, printed with the default ostream format.  No broadcasts are modeled
-// (full_map never broadcasts), so the broadcast lines read 0.  The
+// float, printed with the default ostream format.  The broadcast lines count
+// gg_noc_route_tree's broadcasts (full_map itself never broadcasts).  The
 // asynchronous-communication block is empty in a single DVFS domain.
 inline void writeNetworkSummary(std::ostream& out, const uint64_t* nc, double frequency_ghz, uint32_t net_model,
                                 bool contention_model_enabled = false)
@@ -154,9 +154,9 @@ inline void writeNetworkSummary(std::ostream& out, const uint64_t* nc, double fr
   out << "    Total Packets Sent: " << nc[GG_NC_PACKETS_SENT] << std::endl;
   out << "    Total Flits Sent: " << nc[GG_NC_FLITS_SENT] << std::endl;
   out << "    Total Bits Sent: " << nc[GG_NC_BITS_SENT] << std::endl;
-  out << "    Total Packets Broadcasted: " << 0 << std::endl;
-  out << "    Total Flits Broadcasted: " << 0 << std::endl;
-  out << "    Total Bits Broadcasted: " << 0 << std::endl;
+  out << "    Total Packets Broadcasted: " << nc[GG_NC_PACKETS_BROADCASTED] << std::endl;
+  out << "    Total Flits Broadcasted: " << nc[GG_NC_FLITS_BROADCASTED] << std::endl;
+  out << "    Total Bits Broadcasted: " << nc[GG_NC_BITS_BROADCASTED] << std::endl;
   out << "    Total Packets Received: " << nc[GG_NC_PACKETS_RECEIVED] << std::endl;
   out << "    Total Flits Received: " << nc[GG_NC_FLITS_RECEIVED] << std::endl;
   out << "    Total Bits Received: " << nc[GG_NC_BITS_RECEIVED] << std::endl;
@@ -182,14 +182,15 @@ inline void writeNetworkSummary(std::ostream& out, const uint64_t* nc, double fr
     out << "      Link Traversals: " << nc[GG_NC_LINK_TRAVERSALS] << std::endl;
   }
   if (net_model == GG_NET_EMESH_HOP_BY_HOP) {
-    // outputEventCountSummary (network_model_emesh_hop_by_hop.cc:436-462): unicast
-    // only (full_map never broadcasts), so every crossbar traversal is Crossbar[1]
+    // outputEventCountSummary (network_model_emesh_hop_by_hop.cc:436-462):
+    // Crossbar[m] = traversals of routings to m output ports (m > 1: broadcast tree)
     out << "    Event Counters:" << std::endl;
     out << "      Buffer Writes: " << nc[GG_NC_BUFFER_WRITES] << std::endl;
     out << "      Buffer Reads: " << nc[GG_NC_BUFFER_READS] << std::endl;
     out << "      Switch Allocator Requests: " << nc[GG_NC_SWITCH_ALLOC] << std::endl;
     for (int i = 1; i <= 5; ++i)
-      out << "      Crossbar[" << i << "] Traversals: " << (i == 1 ? nc[GG_NC_CROSSBAR] : 0) << std::endl;
+      out << "      Crossbar[" << i << "] Traversals: " << (i == 1 ? nc[GG_NC_CROSSBAR] : nc[GG_NC_CROSSBAR_MULTI + i - 2])
+          << std::endl;
     out << "      Link Traversals: " << nc[GG_NC_LINK_TRAVERSALS] << std::endl;
     if (contention_model_enabled) {
       // outputContentionModelsSummary (:464-486) over mesh ports 0..4 with

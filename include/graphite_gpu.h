@@ -30,6 +30,10 @@
  *                              (network_model.cc:118-150) at the receiver:
  *                              emesh_hop_counter (models/network_model_emesh_hop_counter.cc:143-157)
  *                              and emesh_hop_by_hop (models/network_model_emesh_hop_by_hop.cc:146-264)
+ *   gg_noc_route_tree          the same with broadcast packets (receiver GG_BROADCAST):
+ *                              the emesh_hop_by_hop broadcast tree
+ *                              (network_model_emesh_hop_by_hop.cc:163-221,
+ *                              network/emesh_hop_by_hop/broadcast_tree_enabled)
  *   gg_noc_get_counters        NetworkModel / RouterModel counters
  *                              (network_model.cc:228-316, router_model.cc:120-145)
  *   gg_queue_delay_batch       QueueModelHistoryTree::computeQueueDelay
@@ -52,7 +56,7 @@
 extern "C" {
 #endif
 
-#define GG_ABI_VERSION 5
+#define GG_ABI_VERSION 6
 
 typedef int gg_status;
 enum {
@@ -128,7 +132,13 @@ enum {
    * DOWN, UP), for RouterModel::getAverageLinkUtilization (router_model.cc:168-182) */
   GG_NC_PORT_UTILIZED_CYCLES,
   GG_NC_PORT_LAST_CYCLES = GG_NC_PORT_UTILIZED_CYCLES + 5,
-  GG_NUM_NET_COUNTERS = GG_NC_PORT_LAST_CYCLES + 5
+  /* broadcasts (gg_noc_route_tree): updateSendCounters' broadcast totals
+   * (network_model.cc:244-250) and RouterModel::updateEventCounters'
+   * Crossbar[2..5] traversals (router_model.cc:126; GG_NC_CROSSBAR = Crossbar[1]) */
+  GG_NC_PACKETS_BROADCASTED = GG_NC_PORT_LAST_CYCLES + 5,
+  GG_NC_FLITS_BROADCASTED, GG_NC_BITS_BROADCASTED,
+  GG_NC_CROSSBAR_MULTI,                 /* + (ports - 2), ports = 2..5 */
+  GG_NUM_NET_COUNTERS = GG_NC_CROSSBAR_MULTI + 4
 };
 
 /* Queue model types (the type strings of QueueModel::create) and the
@@ -357,6 +367,25 @@ gg_status gg_cache_insert_line(gg_ctx* ctx, uint32_t tile, int level,
  * context's router queue state.  Asynchronous on stream.                      */
 gg_status gg_noc_route_batch(gg_ctx* ctx, const gg_packets* pk,
                              const gg_packet_out* out, void* stream);
+/* NetPacket::BROADCAST (common/network/network.h:54) as a receiver id.     */
+#define GG_BROADCAST 0xDEADBABEu
+/* NoC with broadcasts: as gg_noc_route_batch, and packets whose dst is
+ * GG_BROADCAST take the emesh_hop_by_hop broadcast tree
+ * (network_model_emesh_hop_by_hop.cc:163-221: UP / DOWN by the router's row
+ * against the sender's, LEFT / RIGHT in the sender's row, SELF at every
+ * router; one RouterModel::processPacket per router over the port list,
+ * router_model.cc:71-108, contention = the max over its ports) and are
+ * received by every tile, the sender included.  emesh_hop_by_hop only (the
+ * other models have no broadcast capability: network.cc:187-195 unrolls such
+ * a packet into one unicast per tile, which the caller does with
+ * gg_noc_route_batch).  out[k] is written for unicast packets; the deliveries
+ * of the b-th broadcast packet of the batch (batch order) land in
+ * bcast_out[b * num_tiles + tile], num_broadcasts = their count.  One device
+ * walk in global (time, packet index) order: the router ports a broadcast
+ * serves together couple the X and Y chains that gg_noc_route_batch runs
+ * independently.  Asynchronous on stream.                                   */
+gg_status gg_noc_route_tree(gg_ctx* ctx, const gg_packets* pk, const gg_packet_out* out,
+                            const gg_packet_out* bcast_out, uint64_t num_broadcasts, void* stream);
 /* out: num_tiles * GG_NUM_NET_COUNTERS, [tile][counter].                      */
 gg_status gg_noc_get_counters(gg_ctx* ctx, uint64_t* out);
 

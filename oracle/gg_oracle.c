@@ -1158,6 +1158,157 @@ int oracle_noc_route(oracle_noc* on, uint64_t n, const uint32_t* src, const uint
 }
 
 /*
+ * emesh_hop_by_hop with broadcast packets (dst == GG_BROADCAST): the broadcast
+ * tree of NetworkModelEMeshHopByHop::routePacket (hop_by_hop.cc:163-221).  A
+ * broadcast event at router c = (cx, cy) of a packet sent by s = (sx, sy)
+ * forks to UP if cy >= sy, DOWN if cy <= sy, and in the sender's row RIGHT if
+ * cx >= sx, LEFT if cx <= sx — each only when that neighbour exists
+ * (computeTileID, :274-280) — plus SELF (RECEIVE_TILE at c).  Every listed
+ * link adds its delay (the max over equal link delays is link_delay, :185-205)
+ * and RouterModel::processPacket(pkt, list) (router_model.cc:71-108) asks
+ * every listed output-port queue and keeps the largest delay; its contention
+ * counters add that max to each listed port (:135-143), the event counters
+ * add one crossbar traversal of list size (:120-127).  Order: injection ports
+ * first as in oracle_noc_route, then one global heap of (time, packet index)
+ * events, each carrying its copy's zero-load / contention sums.  Unicast
+ * packets take the XY hops of noc_hbh_walk.  Deliveries of the b-th broadcast
+ * of the batch go to b_*[b * tiles + tile].
+ */
+typedef struct { uint64_t t, zl, ct, id; uint32_t at; } n_tev;
+typedef struct { n_tev* a; uint64_t n, cap; } n_theap;
+static int tev_lt(const n_tev* x, const n_tev* y) { return x->t < y->t || (x->t == y->t && x->id < y->id); }
+static void theap_push(n_theap* h, n_tev e)
+{
+  if (h->n == h->cap) { h->cap = h->cap ? h->cap * 2 : 1024; h->a = (n_tev*)realloc(h->a, sizeof(n_tev) * h->cap); }
+  uint64_t i = h->n++;
+  while (i > 0) { uint64_t p = (i - 1) / 2; if (!tev_lt(&e, &h->a[p])) break; h->a[i] = h->a[p]; i = p; }
+  h->a[i] = e;
+}
+static n_tev theap_pop(n_theap* h)
+{
+  n_tev top = h->a[0], last = h->a[--h->n];
+  uint64_t i = 0;
+  for (;;) {
+    uint64_t l = 2 * i + 1, r = l + 1, m = i;
+    const n_tev* cand = &last;
+    if (l < h->n && tev_lt(&h->a[l], cand)) { m = l; cand = &h->a[l]; }
+    if (r < h->n && tev_lt(&h->a[r], cand)) { m = r; }
+    if (m == i) break;
+    h->a[i] = h->a[m]; i = m;
+  }
+  if (h->n) h->a[i] = last;
+  return top;
+}
+
+int oracle_noc_route_tree(oracle_noc* on, uint64_t n, const uint32_t* src, const uint32_t* dst,
+                          const uint32_t* len, const uint64_t* time_ps,
+                          uint64_t* arrival, uint64_t* zero_load, uint64_t* contention,
+                          uint64_t* b_arrival, uint64_t* b_zero_load, uint64_t* b_contention)
+{
+  if (on->cfg.net_model != GG_NET_EMESH_HOP_BY_HOP) return GG_ERR_UNSUPPORTED;
+  if (on->n != on->w * on->h) return GG_ERR_UNSUPPORTED;
+  for (uint64_t k = 0; k < n; ++k)
+    if (src[k] >= on->n || (dst[k] >= on->n && dst[k] != GG_BROADCAST)) return GG_ERR_INVALID;
+  const double f = on->cfg.frequency_ghz;
+  const int qm = on->cfg.queue_model_enabled != 0;
+  const int W = (int)on->w, H = (int)on->h;
+  uint64_t* bidx = (uint64_t*)malloc(sizeof(uint64_t) * (n ? n : 1));
+  uint64_t nb = 0;
+  for (uint64_t k = 0; k < n; ++k) bidx[k] = dst[k] == GG_BROADCAST ? nb++ : ~0ull;
+  n_theap heap = { 0, 0, 0 };
+  /* 1. injection ports (SEND_TILE, :151-159) in (time, index) order per source */
+  {
+    uint64_t* cnt = (uint64_t*)calloc(on->n + 1, sizeof(uint64_t));
+    for (uint64_t k = 0; k < n; ++k) {
+      if (src[k] == dst[k]) { arrival[k] = time_ps[k]; zero_load[k] = 0; contention[k] = 0; continue; }
+      cnt[src[k] + 1]++;
+    }
+    for (uint32_t s = 0; s < on->n; ++s) cnt[s + 1] += cnt[s];
+    n_ev* by = (n_ev*)malloc(sizeof(n_ev) * (cnt[on->n] ? cnt[on->n] : 1));
+    uint64_t* pos = (uint64_t*)malloc(sizeof(uint64_t) * (on->n + 1));
+    memcpy(pos, cnt, sizeof(uint64_t) * (on->n + 1));
+    for (uint64_t k = 0; k < n; ++k)
+      if (src[k] != dst[k]) { n_ev e = { time_ps[k], k }; by[pos[src[k]]++] = e; }
+    for (uint32_t s = 0; s < on->n; ++s) {
+      qsort(by + cnt[s], cnt[s + 1] - cnt[s], sizeof(n_ev), cmp_inj);
+      for (uint64_t i = cnt[s]; i < cnt[s + 1]; ++i) {
+        uint64_t k = by[i].id;
+        uint64_t nf = n_flits(on, len[k]);
+        n_send_counters(on, s, len[k]);
+        if (dst[k] == GG_BROADCAST) {                      /* updateSendCounters (network_model.cc:244-250) */
+          uint64_t* cs = ncnt(on, s);
+          cs[GG_NC_PACKETS_BROADCASTED]++; cs[GG_NC_FLITS_BROADCASTED] += nf; cs[GG_NC_BITS_BROADCASTED] += len[k];
+        }
+        uint64_t qd = qm ? oracle_htree_delay(on->inj[s], time_to_cycles(time_ps[k], f), nf) : 0;
+        uint64_t cps = lat_to_ps(qd, f);
+        n_tev e = { time_ps[k] + lat_to_ps(0, f) + cps, 0, cps, k, s };
+        theap_push(&heap, e);
+      }
+    }
+    free(cnt); free(by); free(pos);
+  }
+  /* 2. mesh routers in global (time, index) order */
+  while (heap.n) {
+    n_tev e = theap_pop(&heap);
+    uint64_t k = e.id;
+    uint32_t c = e.at;
+    int cx = (int)(c % on->w), cy = (int)(c / on->w);
+    int ports[5], np = 0;
+    uint32_t nxt[5];
+    if (dst[k] != GG_BROADCAST) {
+      int dx = (int)(dst[k] % on->w), dy = (int)(dst[k] / on->w);
+      if (cx > dx)      { ports[0] = P_LEFT;  nxt[0] = c - 1; }
+      else if (cx < dx) { ports[0] = P_RIGHT; nxt[0] = c + 1; }
+      else if (cy > dy) { ports[0] = P_DOWN;  nxt[0] = c - on->w; }
+      else if (cy < dy) { ports[0] = P_UP;    nxt[0] = c + on->w; }
+      else              { ports[0] = P_SELF;  nxt[0] = c; }
+      np = 1;
+    } else {
+      int sx = (int)(src[k] % on->w), sy = (int)(src[k] / on->w);
+      if (cy >= sy && cy + 1 < H) { ports[np] = P_UP;    nxt[np++] = c + on->w; }
+      if (cy <= sy && cy - 1 >= 0) { ports[np] = P_DOWN;  nxt[np++] = c - on->w; }
+      if (cy == sy) {
+        if (cx >= sx && cx + 1 < W) { ports[np] = P_RIGHT; nxt[np++] = c + 1; }
+        if (cx <= sx && cx - 1 >= 0) { ports[np] = P_LEFT;  nxt[np++] = c - 1; }
+      }
+      ports[np] = P_SELF; nxt[np++] = c;
+    }
+    uint64_t nf = n_flits(on, len[k]);
+    uint64_t zlc = (uint64_t)on->cfg.router_delay + on->cfg.link_delay, qd = 0;
+    uint64_t* cc = ncnt(on, c);
+    if (qm) {
+      for (int i = 0; i < np; ++i) {
+        uint64_t d = oracle_htree_delay(on->q[(size_t)c * NPORTS + ports[i]], time_to_cycles(e.t, f), nf);
+        if (d > qd) qd = d;
+      }
+      cc[GG_NC_ROUTER_CONTENTION_CYCLES] += qd * (uint64_t)np; cc[GG_NC_ROUTER_PACKETS] += (uint64_t)np;
+    }
+    cc[GG_NC_BUFFER_WRITES] += nf; cc[GG_NC_BUFFER_READS] += nf; cc[GG_NC_SWITCH_ALLOC] += 1;
+    if (np == 1) cc[GG_NC_CROSSBAR] += nf; else cc[GG_NC_CROSSBAR_MULTI + np - 2] += nf;
+    cc[GG_NC_LINK_TRAVERSALS] += nf * (uint64_t)np;
+    uint64_t zps = lat_to_ps(zlc, f), cps = lat_to_ps(qd, f);
+    uint64_t t = e.t + zps + cps, zl = e.zl + zps, ct = e.ct + cps;
+    for (int i = 0; i < np; ++i) {
+      if (ports[i] == P_SELF) {
+        uint64_t tt = t, zz = zl;
+        n_receive(on, c, len[k], &tt, &zz, ct);
+        if (dst[k] == GG_BROADCAST) {
+          size_t o = (size_t)bidx[k] * on->n + c;
+          b_arrival[o] = tt; b_zero_load[o] = zz; b_contention[o] = ct;
+        } else {
+          arrival[k] = tt; zero_load[k] = zz; contention[k] = ct;
+        }
+      } else {
+        n_tev ne = { t, zl, ct, k, nxt[i] };
+        theap_push(&heap, ne);
+      }
+    }
+  }
+  free(heap.a); free(bidx);
+  return 0;
+}
+
+/*
  * emesh_hop_by_hop walk of a batch (hop_by_hop.cc:146-264) in the canonical
  * discrete-event order: the injection port of every tile serves its NEW
  * packets (inj[k] != 0) in (time, packet index) order (routePacket SEND_TILE,

@@ -78,6 +78,11 @@ void        oracle_noc_destroy(oracle_noc* on);
 int  oracle_noc_route(oracle_noc* on, uint64_t n, const uint32_t* src, const uint32_t* dst,
                       const uint32_t* length_bits, const uint64_t* time_ps,
                       uint64_t* arrival_ps, uint64_t* zero_load_ps, uint64_t* contention_ps);
+/* broadcast tree (dst == GG_BROADCAST): b_* = [broadcast ordinal][tile] */
+int  oracle_noc_route_tree(oracle_noc* on, uint64_t n, const uint32_t* src, const uint32_t* dst,
+                           const uint32_t* len, const uint64_t* time_ps,
+                           uint64_t* arrival, uint64_t* zero_load, uint64_t* contention,
+                           uint64_t* b_arrival, uint64_t* b_zero_load, uint64_t* b_contention);
 void oracle_noc_counters(const oracle_noc* on, uint64_t* out); /* [tile][GG_NUM_NET_COUNTERS] */
 
 /* ---------------- coherent mode (Mode C) ----------------

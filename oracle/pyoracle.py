@@ -11,7 +11,7 @@ import subprocess
 import numpy as np
 
 from graphite_amd.config import (GGConfig, NUM_CACHE_COUNTERS, NUM_NET_COUNTERS, NUM_TILE_STATS,
-                                 NUM_RUN_INFO, CMSG_DTYPE)
+                                 NUM_RUN_INFO, CMSG_DTYPE, BROADCAST)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "liboracle.so")
@@ -66,6 +66,8 @@ def lib():
         L.oracle_noc_destroy.argtypes = [vp]
         L.oracle_noc_route.restype = ctypes.c_int
         L.oracle_noc_route.argtypes = [vp, ctypes.c_uint64, _u32p, _u32p, _u32p, _u64p, _u64p, _u64p, _u64p]
+        L.oracle_noc_route_tree.restype = ctypes.c_int
+        L.oracle_noc_route_tree.argtypes = [vp, ctypes.c_uint64, _u32p, _u32p, _u32p, _u64p] + [_u64p] * 6
         L.oracle_noc_counters.argtypes = [vp, _u64p]
         L.oracle_split_lines.restype = ctypes.c_uint32
         L.oracle_split_lines.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _u64p, ctypes.c_uint32]
@@ -344,6 +346,21 @@ class OracleNoc:
         if rc != 0:
             raise RuntimeError("oracle noc rc=%d" % rc)
         return arr, zl, ct
+
+    def route_tree(self, src, dst, length_bits, time_ps):
+        """Broadcast-tree batch (oracle_noc_route_tree): (arrival, zl, ct) per packet
+        and (arrival, zl, ct)[broadcast ordinal, tile] of the broadcast deliveries."""
+        n, T = len(src), self.cfg.num_tiles
+        dst = np.ascontiguousarray(dst, np.uint32)
+        nb = int((dst == BROADCAST).sum())
+        o = [np.zeros(n, np.uint64) for _ in range(3)]
+        b = [np.zeros(max(nb, 1) * T, np.uint64) for _ in range(3)]
+        rc = lib().oracle_noc_route_tree(self.h, n, np.ascontiguousarray(src, np.uint32), dst,
+                                         np.ascontiguousarray(length_bits, np.uint32),
+                                         np.ascontiguousarray(time_ps, np.uint64), *o, *b)
+        if rc != 0:
+            raise RuntimeError("oracle noc rc=%d" % rc)
+        return o, [x[:nb * T].reshape(nb, T) for x in b]
 
     def counters(self):
         out = np.zeros(self.cfg.num_tiles * NUM_NET_COUNTERS, np.uint64)

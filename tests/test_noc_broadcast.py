@@ -1,0 +1,158 @@
+"""emesh_hop_by_hop broadcast tree (network_model_emesh_hop_by_hop.cc:163-221):
+the oracle restatement's properties on CPU, and gg_noc_route_tree (the HIP
+global-order walk) bit-exact against it on the GPU.  The NoC oracle is
+parity-unpinned (the router model cannot be compiled here); the
+CPU tests pin the tree's zero-load shape from the reference's routing rules."""
+import numpy as np
+import pytest
+
+from graphite_amd import config as C
+from oracle import pyoracle as po
+
+K = {n: i for i, n in enumerate(C.NET_COUNTERS)}
+
+
+def _cfg(T, **kw):
+    return C.default_config(T, net_model=C.NET_EMESH_HOP_BY_HOP, **kw)
+
+
+def mixed_packets(T, n, seed, span_ps, bcast_frac=0.1):
+    rng = np.random.default_rng(seed)
+    src = rng.integers(0, T, n).astype(np.uint32)
+    dst = rng.integers(0, T, n).astype(np.uint32)
+    self_m = rng.random(n) < 0.03
+    dst[self_m] = src[self_m]
+    dst[rng.random(n) < bcast_frac] = C.BROADCAST
+    bits = np.where(rng.random(n) < 0.5, C.shmem_modeled_bits(T, False),
+                    C.shmem_modeled_bits(T, True)).astype(np.uint32)
+    t = np.sort(rng.integers(0, span_ps, n)).astype(np.uint64)
+    t[rng.random(n) < 0.1] += np.uint64(7)
+    return src, dst, bits, t
+
+
+@pytest.mark.parametrize("T", [16, 64])
+def test_lone_broadcast_zero_load_tree(T):
+    """One broadcast on an idle mesh: every tile (the sender included) receives
+    it after (XY distance + 1) router+link hops plus serialization; the
+    router at c routes to 1 + its listed ports; counters add up."""
+    cfg = _cfg(T)
+    on = po.OracleNoc(cfg)
+    w = int(np.floor(np.sqrt(T)))
+    s = 2 * w + 1
+    bits = 600
+    (arr, zl, ct), (ba, bz, bc) = on.route_tree(np.array([s], np.uint32), np.array([C.BROADCAST], np.uint32),
+                                                np.array([bits], np.uint32), np.array([1000], np.uint64))
+    nf = -(-bits // cfg.flit_width)
+    hop = (cfg.router_delay + cfg.link_delay) * 1000       # 1 GHz
+    for c in range(T):
+        d = abs(c % w - s % w) + abs(c // w - s // w)
+        assert int(bz[0, c]) == (d + 1) * hop + nf * 1000
+        assert int(bc[0, c]) == 0
+        assert int(ba[0, c]) == 1000 + int(bz[0, c])
+    nc = on.counters()
+    assert nc[:, K["packets_received"]].tolist() == [1] * T
+    assert int(nc[s, K["packets_broadcasted"]]) == 1 and int(nc[s, K["bits_broadcasted"]]) == bits
+    assert int(nc[:, K["switch_alloc"]].sum()) == T                 # one router event per tile
+    # tree edges + one SELF per tile: T - 1 links between routers + T ejections
+    assert int(nc[:, K["link_traversals"]].sum()) == nf * (2 * T - 1)
+    xb = [int(nc[:, K["crossbar"]].sum())] + [int(nc[:, K["crossbar%d" % m]].sum()) for m in range(2, 6)]
+    assert sum(xb) == nf * T
+
+
+def test_tree_walk_equals_unicast_walk_without_broadcasts():
+    T = 64
+    cfg = _cfg(T)
+    src, dst, bits, t = mixed_packets(T, 6000, 5, 300000, bcast_frac=0.0)
+    a = po.OracleNoc(cfg)
+    ref = a.route(src, dst, bits, t)
+    b = po.OracleNoc(cfg)
+    got, _ = b.route_tree(src, dst, bits, t)
+    for g, r in zip(got, ref):
+        np.testing.assert_array_equal(g, r)
+    np.testing.assert_array_equal(a.counters(), b.counters())
+    assert int(ref[2].sum()) > 0
+
+
+def test_broadcast_rejected_outside_hop_by_hop():
+    on = po.OracleNoc(C.default_config(16, net_model=C.NET_EMESH_HOP_COUNTER))
+    with pytest.raises(RuntimeError):
+        on.route_tree(np.array([0], np.uint32), np.array([C.BROADCAST], np.uint32),
+                      np.array([88], np.uint32), np.array([0], np.uint64))
+
+
+# ---- GPU: gg_noc_route_tree vs the oracle ------------------------------------
+def run_tree(torch, cfg, src, dst, bits, t, batches=1):
+    from graphite_amd import backend as B
+    from gpu_util import to_dev, to_np
+    be = B.Backend(cfg)
+    n, T = len(src), cfg.num_tiles
+    outs = [np.zeros(n, np.uint64) for _ in range(3)]
+    bouts = [[] for _ in range(3)]
+    cuts = [n * k // batches for k in range(batches + 1)]
+    for k in range(batches):
+        sl = slice(cuts[k], cuts[k + 1])
+        m = cuts[k + 1] - cuts[k]
+        nb = int((dst[sl] == C.BROADCAST).sum())
+        dev = [to_dev(torch, src[sl], torch.int32), to_dev(torch, dst[sl].view(np.int32), torch.int32),
+               to_dev(torch, bits[sl], torch.int32), to_dev(torch, t[sl], torch.int64)]
+        o = [torch.zeros(m, dtype=torch.int64, device="cuda") for _ in range(3)]
+        bo = [torch.zeros(nb * T, dtype=torch.int64, device="cuda") for _ in range(3)]
+        be.noc_route_tree(*dev, *o, *bo, nb)
+        torch.cuda.synchronize()
+        for i in range(3):
+            outs[i][sl] = to_np(o[i], np.uint64)
+            bouts[i].append(to_np(bo[i], np.uint64).reshape(nb, T))
+    return be, outs, [np.concatenate(b) for b in bouts]
+
+
+def oracle_tree(cfg, src, dst, bits, t, batches=1):
+    on = po.OracleNoc(cfg)
+    n = len(src)
+    outs = [np.zeros(n, np.uint64) for _ in range(3)]
+    bouts = [[] for _ in range(3)]
+    cuts = [n * k // batches for k in range(batches + 1)]
+    for k in range(batches):
+        sl = slice(cuts[k], cuts[k + 1])
+        o, b = on.route_tree(src[sl], dst[sl], bits[sl], t[sl])
+        for i in range(3):
+            outs[i][sl] = o[i]
+            bouts[i].append(b[i])
+    return on, outs, [np.concatenate(b) for b in bouts]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,n,span,batches,frac,qm", [(16, 3000, 200000, 1, 0.1, 1), (64, 4000, 400000, 2, 0.05, 1),
+                                                      (64, 3000, 100000, 1, 0.02, 1), (16, 2000, 100000, 1, 0.2, 0),
+                                                      (256, 2000, 400000, 1, 0.01, 1)])
+def test_broadcast_tree_matches_oracle_on_gpu(T, n, span, batches, frac, qm):
+    from gpu_util import torch_dev
+    torch = torch_dev()
+    cfg = _cfg(T, queue_model_enabled=qm)
+    src, dst, bits, t = mixed_packets(T, n, T + n + batches, span, bcast_frac=frac)
+    be, got, bgot = run_tree(torch, cfg, src, dst, bits, t, batches)
+    on, ref, bref = oracle_tree(cfg, src, dst, bits, t, batches)
+    uni = dst != C.BROADCAST
+    for g, r in zip(got, ref):
+        np.testing.assert_array_equal(g[uni], r[uni])
+    for g, r in zip(bgot, bref):
+        np.testing.assert_array_equal(g, r)
+    np.testing.assert_array_equal(be.noc_counters(), on.counters())
+    assert bref[0].shape[0] > 0
+    if qm:
+        assert int(bref[2].sum()) > 0                              # broadcast copies were contended
+
+
+@pytest.mark.gpu
+def test_tree_walk_equals_stage_pipeline_without_broadcasts():
+    """A unicast-only batch through gg_noc_route_tree (global-order walk) equals
+    gg_noc_route_batch (independent X / Y chain stages) bit for bit."""
+    from gpu_util import torch_dev
+    from test_gpu_noc import run_noc
+    torch = torch_dev()
+    cfg = _cfg(64)
+    src, dst, bits, t = mixed_packets(64, 5000, 11, 300000, bcast_frac=0.0)
+    be1, got1, _ = run_tree(torch, cfg, src, dst, bits, t)
+    be2, got2 = run_noc(torch, cfg, src, dst, bits, t)
+    for a, b in zip(got1, got2):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(be1.noc_counters(), be2.noc_counters())
