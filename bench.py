@@ -369,7 +369,59 @@ def noc_section(args, dev):
                                  "sample": "the whole batch, oracle/gg_oracle.c -O3, 1 thread, %.2f s" % cdt}
         res[name] = r
         be.close()
+    res["broadcast_tree"] = noc_tree_bench(args, dev, T)
     return res
+
+
+def noc_tree_bench(args, dev, T):
+    """gg_noc_route_tree: the hop-by-hop broadcast tree (hop_by_hop.cc:163-221) on
+    the same mesh, 2 % of the packets broadcast (each reaches all T tiles), one
+    global-order device walk; deliveries counted per (packet, receiving tile)."""
+    import torch
+    from graphite_amd import config as C
+    from graphite_amd import backend as B
+    from oracle import pyoracle as po
+    n = max(64, args.noc_packets // 16)
+    rng = np.random.default_rng(9)
+    src = rng.integers(0, T, n).astype(np.uint32)
+    dst = rng.integers(0, T, n).astype(np.uint32)
+    dst[rng.random(n) < 0.02] = C.BROADCAST
+    nb = int((dst == C.BROADCAST).sum())
+    bits = np.full(n, C.shmem_modeled_bits(T, True), np.uint32)
+    t = np.sort(rng.integers(0, 50 * n, n)).astype(np.uint64)
+    cfg = C.default_config(T, net_model=C.NET_EMESH_HOP_BY_HOP)
+    be = B.Backend(cfg)
+    d = lambda x: torch.from_numpy(x.view(np.int64 if x.dtype == np.uint64 else np.int32)).to(dev)
+    ins = [d(src), d(dst), d(bits), d(t)]
+    outs = [torch.zeros(n, dtype=torch.int64, device=dev) for _ in range(3)]
+    bouts = [torch.zeros(nb * T, dtype=torch.int64, device=dev) for _ in range(3)]
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    be.noc_route_tree(*ins, *outs, *bouts, nb)
+    e1.record()
+    torch.cuda.synchronize()
+    dt = e0.elapsed_time(e1) / 1e3
+    deliveries = (n - nb) + nb * T
+    r = {"packets": n, "broadcasts": nb, "deliveries": deliveries, "value": deliveries / dt,
+         "unit": "deliveries/s", "seconds": dt,
+         "note": "one lane walks the global (time, index) event order (the broadcast's shared port delay "
+                 "couples the X and Y chains); heap in HBM at this size"}
+    if not args.no_verify:
+        on = po.OracleNoc(cfg)
+        c0 = time.perf_counter()
+        (ra, rz, rc), (ba, bz, bc) = on.route_tree(src, dst, bits, t)
+        cdt = time.perf_counter() - c0
+        uni = dst != C.BROADCAST
+        ok = all(np.array_equal(o.cpu().numpy().view(np.uint64)[uni], x[uni]) for o, x in zip(outs, (ra, rz, rc)))
+        ok = ok and all(np.array_equal(o.cpu().numpy().view(np.uint64), x.reshape(-1)) for o, x in zip(bouts, (ba, bz, bc)))
+        r["bit_exact_checked"] = bool(ok and np.array_equal(be.noc_counters(), on.counters()))
+        if not r["bit_exact_checked"]:
+            print("bench.py: NOC broadcast_tree BIT-EXACT CHECK FAILED", file=sys.stderr)
+        r["cpu_baseline"] = {"value": deliveries / cdt, "unit": "deliveries/s", "cores": 1, "kind": "port",
+                             "sample": "the whole batch, oracle/gg_oracle.c -O3, 1 thread, %.2f s" % cdt}
+    be.close()
+    return r
 
 
 def stress_section(args, dev):

@@ -655,10 +655,14 @@ __global__ void k_analytical(const HQueue* q, uint32_t tiles, uint64_t* ctr)
 // port list, router_model.cc:71-108), so the row (X) and column (Y) port
 // chains are no longer independent stages: the walk is one global
 // (time, packet index) event order — injection events (SEND_TILE, :151-159)
-// and router events in one heap, every event carrying its copy's time,
-// zero-load and contention sums.  One lane walks; the heap lives in HBM.
+// and router events in one heap, an event being the packet, its router and
+// its time (zero-load = XY distance from the sender + 1 hops x router+link
+// delay, every tree path being a shortest path; contention = the rest).  One
+// lane walks; the heap lives in LDS when its bound (packets + broadcasts x
+// tiles) fits, else in HBM.
 // ---------------------------------------------------------------------------
-struct TEv { uint64_t t, zl, ct; uint32_t id, at; };   // at: router tile, | kInjBit = injection port of src
+struct TEv { uint64_t t; uint32_t id, at; };   // at: router tile, | kInjBit = injection port of src
+constexpr uint32_t kTreeLdsEv = 160 * 1024 / sizeof(TEv);
 constexpr uint32_t kInjBit = 0x80000000u;
 __device__ __forceinline__ bool tev_lt(const TEv& a, const TEv& b) { return a.t < b.t || (a.t == b.t && a.id < b.id); }
 __device__ __forceinline__ void theap_push(TEv* h, uint64_t& n, const TEv& e)
@@ -683,91 +687,238 @@ __device__ __forceinline__ TEv theap_pop(TEv* h, uint64_t& n)
   return top;
 }
 
-__global__ __launch_bounds__(64) void k_tree_walk(NocDev D, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
-                                                  const uint32_t* __restrict__ len, const uint64_t* __restrict__ t0,
-                                                  uint64_t n, uint64_t nb, TEv* heap, uint64_t hcap, uint32_t* bidx,
-                                                  gg_packet_out out, gg_packet_out bout)
+struct TreeIO {
+  const uint32_t* src; const uint32_t* dst; const uint32_t* len; const uint64_t* t0;
+  uint32_t* bidx; gg_packet_out out, bout;
+};
+
+// SEND_TILE: the injection router (delay 0, port 0) -> the router event at the source
+__device__ __forceinline__ TEv tree_inject(const NocDev& D, const TreeIO& IO, const TEv& e)
 {
+  const NocParams& P = D.P;
+  const uint32_t k = e.id, s = IO.src[k], bits = IO.len[k];
+  const uint64_t nf = nflits(P, bits);
+  cadd(D.ctr, s, GG_NC_PACKETS_SENT, 1); cadd(D.ctr, s, GG_NC_FLITS_SENT, nf); cadd(D.ctr, s, GG_NC_BITS_SENT, bits);
+  if (IO.dst[k] == GG_BROADCAST) {                 // updateSendCounters (network_model.cc:244-250)
+    cadd(D.ctr, s, GG_NC_PACKETS_BROADCASTED, 1); cadd(D.ctr, s, GG_NC_FLITS_BROADCASTED, nf);
+    cadd(D.ctr, s, GG_NC_BITS_BROADCASTED, bits);
+  }
+  uint64_t qd = 0;
+  if (P.qm) { HTree tr = D.tree(s, 5); qd = tr.delay(time_to_cycles(e.t, P.f), nf, D.err); }
+  return TEv{e.t + lat_to_ps(0, P.f) + lat_to_ps(qd, P.f), k, s};
+}
+
+// EMESH: one router event (unicast XY or broadcast fork); forwarded copies go to push(TEv)
+template <class Push>
+__device__ __forceinline__ void tree_router(const NocDev& D, const TreeIO& IO, const TEv& e, Push push)
+{
+  const NocParams& P = D.P;
+  const uint32_t W = P.w, H = P.h;
+  const uint32_t k = e.id, s = IO.src[k], d = IO.dst[k], bits = IO.len[k];
+  const uint64_t nf = nflits(P, bits);
+  const uint32_t c = e.at, cx = c % W, cy = c / W, sx = s % W, sy = s / W;
+  int ports[5]; uint32_t nxt[5]; int np = 0;
+  if (d != GG_BROADCAST) {                         // XY (:223-256)
+    const uint32_t dx = d % W, dy = d / W;
+    if (cx > dx)      { ports[0] = P_LEFT;  nxt[0] = c - 1; }
+    else if (cx < dx) { ports[0] = P_RIGHT; nxt[0] = c + 1; }
+    else if (cy > dy) { ports[0] = P_DOWN;  nxt[0] = c - W; }
+    else if (cy < dy) { ports[0] = P_UP;    nxt[0] = c + W; }
+    else              { ports[0] = P_SELF;  nxt[0] = c; }
+    np = 1;
+  } else {                                         // broadcast tree (:163-221), next_dest_list order
+    if (cy >= sy && cy + 1 < H) { ports[np] = P_UP;   nxt[np++] = c + W; }
+    if (cy <= sy && cy >= 1)    { ports[np] = P_DOWN; nxt[np++] = c - W; }
+    if (cy == sy) {
+      if (cx >= sx && cx + 1 < W) { ports[np] = P_RIGHT; nxt[np++] = c + 1; }
+      if (cx <= sx && cx >= 1)    { ports[np] = P_LEFT;  nxt[np++] = c - 1; }
+    }
+    ports[np] = P_SELF; nxt[np++] = c;
+  }
+  uint64_t qd = 0;
+  if (P.qm) {
+    for (int i = 0; i < np; ++i) {
+      HTree tr = D.tree(c, ports[i]);
+      qd = max(qd, tr.delay(time_to_cycles(e.t, P.f), nf, D.err));
+    }
+    cadd(D.ctr, c, GG_NC_ROUTER_CONTENTION_CYCLES, qd * (uint64_t)np);   // updateContentionCounters, per listed port
+    cadd(D.ctr, c, GG_NC_ROUTER_PACKETS, (uint64_t)np);
+  }
+  cadd(D.ctr, c, GG_NC_BUFFER_WRITES, nf); cadd(D.ctr, c, GG_NC_BUFFER_READS, nf);
+  cadd(D.ctr, c, GG_NC_SWITCH_ALLOC, 1);
+  cadd(D.ctr, c, np == 1 ? (int)GG_NC_CROSSBAR : (int)GG_NC_CROSSBAR_MULTI + np - 2, nf);
+  cadd(D.ctr, c, GG_NC_LINK_TRAVERSALS, nf * (uint64_t)np);
+  const uint64_t zps = lat_to_ps((uint64_t)P.router_delay + P.link_delay, P.f), cps = lat_to_ps(qd, P.f);
+  const uint64_t hops = (uint64_t)((cx > sx ? cx - sx : sx - cx) + (cy > sy ? cy - sy : sy - cy)) + 1;
+  const uint64_t t = e.t + zps + cps, zl = hops * zps, ct = t - IO.t0[k] - zl;
+  for (int i = 0; i < np; ++i) {
+    if (ports[i] != P_SELF) { push(TEv{t, k, nxt[i]}); continue; }
+    const uint64_t ser = lat_to_ps(nf, P.f);       // receive at c (network_model.cc:118-150,253-272)
+    cadd(D.ctr, c, GG_NC_PACKETS_RECEIVED, 1); cadd(D.ctr, c, GG_NC_FLITS_RECEIVED, nf);
+    cadd(D.ctr, c, GG_NC_BITS_RECEIVED, bits);
+    cadd(D.ctr, c, GG_NC_TOTAL_LATENCY_PS, zl + ser + ct); cadd(D.ctr, c, GG_NC_TOTAL_CONTENTION_PS, ct);
+    if (d == GG_BROADCAST) {
+      const uint64_t o = (uint64_t)IO.bidx[k] * P.tiles + c;
+      IO.bout.arrival_ps_dev[o] = t + ser; IO.bout.zero_load_ps_dev[o] = zl + ser; IO.bout.contention_ps_dev[o] = ct;
+    } else {
+      IO.out.arrival_ps_dev[k] = t + ser; IO.out.zero_load_ps_dev[k] = zl + ser; IO.out.contention_ps_dev[k] = ct;
+    }
+  }
+}
+
+// The serial form: one lane, one heap (zero router + link delay, where the
+// windowed form below has no lookahead, or meshes beyond kTreeMaxT).
+template <bool LDS>
+__global__ __launch_bounds__(64) void k_tree_walk(NocDev D, TreeIO IO, uint64_t n, uint64_t nb, TEv* gheap, uint64_t hcap)
+{
+  extern __shared__ __align__(16) uint8_t tree_lds[];
+  TEv* heap = LDS ? reinterpret_cast<TEv*>(tree_lds) : gheap;
   if (threadIdx.x != 0) return;
   const NocParams& P = D.P;
   // validate, number the broadcasts in batch order, seed the injection events
   uint64_t m = 0, hn = 0;
   for (uint64_t k = 0; k < n; ++k) {
-    const uint32_t s = src[k], d = dst[k];
+    const uint32_t s = IO.src[k], d = IO.dst[k];
     if (s >= P.tiles || (d >= P.tiles && d != GG_BROADCAST)) { atomicOr(D.err, GG_DERR_RANGE); return; }
-    bidx[k] = d == GG_BROADCAST ? (uint32_t)m++ : ~0u;
+    IO.bidx[k] = d == GG_BROADCAST ? (uint32_t)m++ : ~0u;
   }
   if (m != nb || n + nb * P.tiles > hcap) { atomicOr(D.err, GG_DERR_CAP); return; }
   for (uint64_t k = 0; k < n; ++k) {
-    const uint32_t s = src[k], d = dst[k];
-    if (s == d) { out.arrival_ps_dev[k] = t0[k]; out.zero_load_ps_dev[k] = 0; out.contention_ps_dev[k] = 0; continue; }
-    theap_push(heap, hn, TEv{t0[k], 0, 0, (uint32_t)k, s | kInjBit});
+    const uint32_t s = IO.src[k], d = IO.dst[k];
+    if (s == d) { IO.out.arrival_ps_dev[k] = IO.t0[k]; IO.out.zero_load_ps_dev[k] = 0; IO.out.contention_ps_dev[k] = 0; continue; }
+    theap_push(heap, hn, TEv{IO.t0[k], (uint32_t)k, s | kInjBit});
   }
-  const uint32_t W = P.w, H = P.h;
   while (hn) {
     const TEv e = theap_pop(heap, hn);
-    const uint32_t k = e.id, s = src[k], d = dst[k], bits = len[k];
-    const uint64_t nf = nflits(P, bits);
-    if (e.at & kInjBit) {                          // injection router: delay 0, port 0
-      cadd(D.ctr, s, GG_NC_PACKETS_SENT, 1); cadd(D.ctr, s, GG_NC_FLITS_SENT, nf); cadd(D.ctr, s, GG_NC_BITS_SENT, bits);
-      if (d == GG_BROADCAST) {                     // updateSendCounters (network_model.cc:244-250)
-        cadd(D.ctr, s, GG_NC_PACKETS_BROADCASTED, 1); cadd(D.ctr, s, GG_NC_FLITS_BROADCASTED, nf);
-        cadd(D.ctr, s, GG_NC_BITS_BROADCASTED, bits);
-      }
-      uint64_t qd = 0;
-      if (P.qm) { HTree tr = D.tree(s, 5); qd = tr.delay(time_to_cycles(e.t, P.f), nf, D.err); }
-      const uint64_t cps = lat_to_ps(qd, P.f);
-      theap_push(heap, hn, TEv{e.t + lat_to_ps(0, P.f) + cps, 0, cps, k, s});
-      continue;
+    if (e.at & kInjBit) { theap_push(heap, hn, tree_inject(D, IO, e)); continue; }
+    tree_router(D, IO, e, [&](const TEv& x) { theap_push(heap, hn, x); });
+  }
+}
+
+// The windowed form (conservative time windows, one workgroup): a router
+// event at time t forwards its copies at t + router + link delay or later
+// (zps > 0), so in a window [t_min, t_min + zps) every router's events depend
+// only on that router's own queues: each router (one thread) serves its
+// window events in (time, index) order and the routers run in parallel.
+// Window loop: min over the pending events -> group the window's events by
+// router (counting sort in LDS) and carry the rest over -> serve, forwarding
+// copies to the next pending list.  Injection ports first: each tile serves
+// its packets in (time, index) order (the injection port is its own queue).
+constexpr uint32_t kTreeMaxT = 4096;
+constexpr uint32_t kTreeThreads = 1024;
+// exclusive block-wide scan of one value per thread (DPP-free shuffles within
+// the wave, the wave totals through LDS); *total = the block sum
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t* total)
+{
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  uint32_t x = v;
+  #pragma unroll
+  for (int o = 1; o < 64; o <<= 1) { const uint32_t y = __shfl_up(x, o, 64); if (lane >= (uint32_t)o) x += y; }
+  if (lane == 63) wsum[wid] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) { uint32_t a = 0; for (uint32_t i = 0; i < nw; ++i) { const uint32_t t = wsum[i]; wsum[i] = a; a += t; } wsum[nw] = a; }
+  __syncthreads();
+  const uint32_t r = wsum[wid] + x - v;
+  *total = wsum[nw];
+  __syncthreads();
+  return r;
+}
+__global__ __launch_bounds__(kTreeThreads) void k_tree_win(NocDev D, TreeIO IO, uint64_t n, uint64_t nb,
+                                                           TEv* E0, TEv* E1, TEv* G, uint64_t hcap)
+{
+  __shared__ uint32_t cnt[kTreeMaxT];
+  __shared__ uint32_t off[kTreeMaxT + 1];
+  __shared__ uint32_t wsum[kTreeThreads / 64 + 1];
+  __shared__ unsigned long long s_min;
+  __shared__ uint32_t s_n0, s_n1, s_err;
+  const NocParams& P = D.P;
+  const uint32_t T = P.tiles, tid = threadIdx.x, nt = blockDim.x;
+  const uint64_t zps = lat_to_ps((uint64_t)P.router_delay + P.link_delay, P.f);
+  // block-wide exclusive scan of cnt[0..T) into off (T <= 4 * nt)
+  auto scan_counts = [&]() {
+    const uint32_t per = (T + nt - 1) / nt;
+    uint32_t a = 0, tot;
+    for (uint32_t i = tid * per; i < min(T, (tid + 1) * per); ++i) a += cnt[i];
+    a = block_excl_scan(a, wsum, &tot);
+    for (uint32_t i = tid * per; i < min(T, (tid + 1) * per); ++i) { off[i] = a; a += cnt[i]; cnt[i] = 0; }
+    if (tid == 0) off[T] = tot;
+    __syncthreads();
+  };
+  if (tid == 0) { s_err = 0; s_n0 = 0; s_n1 = 0; }
+  for (uint32_t i = tid; i < T; i += nt) cnt[i] = 0;
+  __syncthreads();
+  // 1. validate; broadcast ordinals (per-thread chunk counts, scanned); bucket the packets by source
+  const uint64_t per = (n + nt - 1) / nt, k0 = min(n, tid * per), k1 = min(n, k0 + per);
+  uint32_t mine = 0;
+  for (uint64_t k = k0; k < k1; ++k) {
+    const uint32_t s = IO.src[k], d = IO.dst[k];
+    if (s >= T || (d >= T && d != GG_BROADCAST)) atomicOr(&s_err, GG_DERR_RANGE);
+    mine += d == GG_BROADCAST;
+    if (s < T && s != d) atomicAdd(&cnt[s], 1u);
+  }
+  uint32_t nbc;
+  mine = block_excl_scan(mine, wsum, &nbc);
+  if (tid == 0 && (nbc != nb || n + nb * T > hcap)) s_err |= GG_DERR_CAP;
+  __syncthreads();
+  if (s_err) { if (tid == 0) atomicOr(D.err, s_err); return; }
+  for (uint64_t k = k0; k < k1; ++k) IO.bidx[k] = IO.dst[k] == GG_BROADCAST ? mine++ : ~0u;
+  __syncthreads();
+  scan_counts();
+  for (uint64_t k = k0; k < k1; ++k) {
+    const uint32_t s = IO.src[k], d = IO.dst[k];
+    if (s == d) { IO.out.arrival_ps_dev[k] = IO.t0[k]; IO.out.zero_load_ps_dev[k] = 0; IO.out.contention_ps_dev[k] = 0; continue; }
+    G[off[s] + atomicAdd(&cnt[s], 1u)] = TEv{IO.t0[k], (uint32_t)k, s | kInjBit};
+  }
+  __syncthreads();
+  // injection ports: each tile's packets heap-ordered in place, served in (time, index) order
+  for (uint32_t r = tid; r < T; r += nt) {
+    TEv* h = G + off[r];
+    uint64_t m = off[r + 1] - off[r], hn = 0;
+    for (uint64_t i = 0; i < m; ++i) { const TEv e = h[i]; theap_push(h, hn, e); }
+    while (hn) {
+      const TEv e = theap_pop(h, hn);
+      E0[atomicAdd(&s_n0, 1u)] = tree_inject(D, IO, e);
     }
-    const uint32_t c = e.at, cx = c % W, cy = c / W;
-    int ports[5]; uint32_t nxt[5]; int np = 0;
-    if (d != GG_BROADCAST) {                       // XY (:223-256)
-      const uint32_t dx = d % W, dy = d / W;
-      if (cx > dx)      { ports[0] = P_LEFT;  nxt[0] = c - 1; }
-      else if (cx < dx) { ports[0] = P_RIGHT; nxt[0] = c + 1; }
-      else if (cy > dy) { ports[0] = P_DOWN;  nxt[0] = c - W; }
-      else if (cy < dy) { ports[0] = P_UP;    nxt[0] = c + W; }
-      else              { ports[0] = P_SELF;  nxt[0] = c; }
-      np = 1;
-    } else {                                       // broadcast tree (:163-221), next_dest_list order
-      const uint32_t sx = s % W, sy = s / W;
-      if (cy >= sy && cy + 1 < H) { ports[np] = P_UP;   nxt[np++] = c + W; }
-      if (cy <= sy && cy >= 1)    { ports[np] = P_DOWN; nxt[np++] = c - W; }
-      if (cy == sy) {
-        if (cx >= sx && cx + 1 < W) { ports[np] = P_RIGHT; nxt[np++] = c + 1; }
-        if (cx <= sx && cx >= 1)    { ports[np] = P_LEFT;  nxt[np++] = c - 1; }
-      }
-      ports[np] = P_SELF; nxt[np++] = c;
+  }
+  for (uint32_t i = tid; i < T; i += nt) cnt[i] = 0;
+  __syncthreads();
+  // 2. windows
+  for (;;) {
+    const uint32_t n0 = s_n0;
+    if (n0 == 0) break;
+    if (tid == 0) s_min = ~0ull;
+    __syncthreads();
+    unsigned long long lm = ~0ull;
+    for (uint32_t i = tid; i < n0; i += nt) lm = min(lm, (unsigned long long)E0[i].t);
+    atomicMin(&s_min, lm);
+    __syncthreads();
+    const uint64_t wend = s_min + zps;
+    for (uint32_t i = tid; i < n0; i += nt) {
+      const TEv e = E0[i];
+      if (e.t < wend) atomicAdd(&cnt[e.at], 1u);
+      else E1[atomicAdd(&s_n1, 1u)] = e;
     }
-    uint64_t qd = 0;
-    if (P.qm) {
-      for (int i = 0; i < np; ++i) {
-        HTree tr = D.tree(c, ports[i]);
-        qd = max(qd, tr.delay(time_to_cycles(e.t, P.f), nf, D.err));
-      }
-      cadd(D.ctr, c, GG_NC_ROUTER_CONTENTION_CYCLES, qd * (uint64_t)np);   // updateContentionCounters, per listed port
-      cadd(D.ctr, c, GG_NC_ROUTER_PACKETS, (uint64_t)np);
+    __syncthreads();
+    scan_counts();
+    for (uint32_t i = tid; i < n0; i += nt) {
+      const TEv e = E0[i];
+      if (e.t < wend) G[off[e.at] + atomicAdd(&cnt[e.at], 1u)] = e;
     }
-    cadd(D.ctr, c, GG_NC_BUFFER_WRITES, nf); cadd(D.ctr, c, GG_NC_BUFFER_READS, nf);
-    cadd(D.ctr, c, GG_NC_SWITCH_ALLOC, 1);
-    cadd(D.ctr, c, np == 1 ? (int)GG_NC_CROSSBAR : (int)GG_NC_CROSSBAR_MULTI + np - 2, nf);
-    cadd(D.ctr, c, GG_NC_LINK_TRAVERSALS, nf * (uint64_t)np);
-    const uint64_t zps = lat_to_ps((uint64_t)P.router_delay + P.link_delay, P.f), cps = lat_to_ps(qd, P.f);
-    const uint64_t t = e.t + zps + cps, zl = e.zl + zps, ct = e.ct + cps;
-    for (int i = 0; i < np; ++i) {
-      if (ports[i] != P_SELF) { theap_push(heap, hn, TEv{t, zl, ct, k, nxt[i]}); continue; }
-      const uint64_t ser = lat_to_ps(nf, P.f);     // receive at c (network_model.cc:118-150,253-272)
-      cadd(D.ctr, c, GG_NC_PACKETS_RECEIVED, 1); cadd(D.ctr, c, GG_NC_FLITS_RECEIVED, nf);
-      cadd(D.ctr, c, GG_NC_BITS_RECEIVED, bits);
-      cadd(D.ctr, c, GG_NC_TOTAL_LATENCY_PS, zl + ser + ct); cadd(D.ctr, c, GG_NC_TOTAL_CONTENTION_PS, ct);
-      if (d == GG_BROADCAST) {
-        const uint64_t o = (uint64_t)bidx[k] * P.tiles + c;
-        bout.arrival_ps_dev[o] = t + ser; bout.zero_load_ps_dev[o] = zl + ser; bout.contention_ps_dev[o] = ct;
-      } else {
-        out.arrival_ps_dev[k] = t + ser; out.zero_load_ps_dev[k] = zl + ser; out.contention_ps_dev[k] = ct;
+    __syncthreads();
+    for (uint32_t r = tid; r < T; r += nt) {
+      TEv* h = G + off[r];
+      uint64_t m = off[r + 1] - off[r], hn = 0;
+      for (uint64_t i = 0; i < m; ++i) { const TEv e = h[i]; theap_push(h, hn, e); }
+      while (hn) {
+        const TEv e = theap_pop(h, hn);
+        tree_router(D, IO, e, [&](const TEv& x) { E1[atomicAdd(&s_n1, 1u)] = x; });
       }
     }
+    for (uint32_t i = tid; i < T; i += nt) cnt[i] = 0;
+    __syncthreads();
+    if (tid == 0) { s_n0 = s_n1; s_n1 = 0; }
+    TEv* x = E0; E0 = E1; E1 = x;
+    __syncthreads();
   }
 }
 
@@ -810,6 +961,8 @@ gg_status gg_noc_alloc(gg_ctx* ctx)
   GG_HIP(hipFuncSetAttribute((const void*)k_port_staged<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
   GG_HIP(hipFuncSetAttribute((const void*)k_port_staged<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
   GG_HIP(hipFuncSetAttribute((const void*)k_chain_staged, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
+  GG_HIP(hipFuncSetAttribute((const void*)k_tree_walk<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)(kTreeLdsEv * sizeof(TEv))));
   GG_HIP(hipMalloc((void**)&S->ctr, sizeof(uint64_t) * c.num_tiles * GG_NUM_NET_COUNTERS));
   // one history tree per mesh output port (5) + the injection port, per tile; the
   // stand-alone gg_queue_delay_batch queue lives at index tiles*6
@@ -909,10 +1062,14 @@ gg_status gg_noc_tree(gg_ctx* ctx, const gg_packets* pk, const gg_packet_out* ou
     return gg_fail(GG_ERR_INVALID, "NULL packet or output pointer");
   if (n >= (1ull << 32) || nb > n) return gg_fail(GG_ERR_RANGE, "batch larger than 2^32 packets or num_broadcasts > packets");
   const uint64_t hcap = n + nb * P.tiles;          // live copies of a broadcast <= tiles
-  if (hcap > S->tcap) {
+  const bool win = (uint64_t)P.router_delay + P.link_delay > 0 &&   // lookahead: a hop takes >= 1 cycle P.tiles <= kTreeMaxT && hcap < (1ull << 32) &&
+                   !(getenv("GG_NOC_TREE_SERIAL") && atoi(getenv("GG_NOC_TREE_SERIAL")));
+  const bool lds = !win && hcap <= kTreeLdsEv;
+  const uint64_t need = win ? 3 * hcap : lds ? 0 : hcap;
+  if (need > S->tcap) {
     if (S->theap) hipFree(S->theap);
-    GG_HIP(hipMalloc((void**)&S->theap, sizeof(TEv) * hcap));
-    S->tcap = hcap;
+    GG_HIP(hipMalloc((void**)&S->theap, sizeof(TEv) * need));
+    S->tcap = need;
   }
   if (n > S->bcap) {
     if (S->bidx) hipFree(S->bidx);
@@ -921,9 +1078,15 @@ gg_status gg_noc_tree(gg_ctx* ctx, const gg_packets* pk, const gg_packet_out* ou
   }
   NocDev D{P, S->q, S->nd, S->ctr, ctx->err_dev};
   const gg_packet_out none{nullptr, nullptr, nullptr};
+  TreeIO IO{pk->src_dev, pk->dst_dev, pk->length_bits_dev, pk->time_ps_dev, S->bidx, *out, nb ? *bout : none};
   gg_timer_begin(ctx, "noc_tree", s);
-  hipLaunchKernelGGL(k_tree_walk, dim3(1), dim3(64), 0, s, D, pk->src_dev, pk->dst_dev, pk->length_bits_dev,
-                     pk->time_ps_dev, n, nb, S->theap, S->tcap, S->bidx, *out, nb ? *bout : none);
+  if (win)
+    hipLaunchKernelGGL(k_tree_win, dim3(1), dim3(kTreeThreads), 0, s, D, IO, n, nb, S->theap, S->theap + hcap,
+                       S->theap + 2 * hcap, hcap);
+  else if (lds)
+    hipLaunchKernelGGL(k_tree_walk<true>, dim3(1), dim3(64), hcap * sizeof(TEv), s, D, IO, n, nb, nullptr, hcap);
+  else
+    hipLaunchKernelGGL(k_tree_walk<false>, dim3(1), dim3(64), 0, s, D, IO, n, nb, S->theap, hcap);
   GG_HIP(hipGetLastError());
   gg_timer_end(ctx, "noc_tree", s);
   return GG_OK;

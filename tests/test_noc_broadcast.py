@@ -123,7 +123,7 @@ def oracle_tree(cfg, src, dst, bits, t, batches=1):
 @pytest.mark.gpu
 @pytest.mark.parametrize("T,n,span,batches,frac,qm", [(16, 3000, 200000, 1, 0.1, 1), (64, 4000, 400000, 2, 0.05, 1),
                                                       (64, 3000, 100000, 1, 0.02, 1), (16, 2000, 100000, 1, 0.2, 0),
-                                                      (256, 2000, 400000, 1, 0.01, 1)])
+                                                      (256, 2000, 400000, 1, 0.01, 1), (256, 3000, 600000, 1, 0.03, 1)])
 def test_broadcast_tree_matches_oracle_on_gpu(T, n, span, batches, frac, qm):
     from gpu_util import torch_dev
     torch = torch_dev()
@@ -156,3 +156,36 @@ def test_tree_walk_equals_stage_pipeline_without_broadcasts():
     for a, b in zip(got1, got2):
         np.testing.assert_array_equal(a, b)
     np.testing.assert_array_equal(be1.noc_counters(), be2.noc_counters())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,n,frac", [(16, 2000, 0.1), (256, 3000, 0.03)])
+def test_serial_tree_walk_matches_oracle_on_gpu(T, n, frac, monkeypatch):
+    """The one-lane form (heap in LDS at 16 tiles, in HBM at 256), used where
+    the windowed form has no lookahead (router + link delay 0)."""
+    from gpu_util import torch_dev
+    torch = torch_dev()
+    monkeypatch.setenv("GG_NOC_TREE_SERIAL", "1")
+    cfg = _cfg(T)
+    src, dst, bits, t = mixed_packets(T, n, 3 * T + n, 300000, bcast_frac=frac)
+    be, got, bgot = run_tree(torch, cfg, src, dst, bits, t)
+    on, ref, bref = oracle_tree(cfg, src, dst, bits, t)
+    uni = dst != C.BROADCAST
+    for g, r in zip(got, ref):
+        np.testing.assert_array_equal(g[uni], r[uni])
+    for g, r in zip(bgot, bref):
+        np.testing.assert_array_equal(g, r)
+    np.testing.assert_array_equal(be.noc_counters(), on.counters())
+
+
+@pytest.mark.gpu
+def test_zero_delay_mesh_takes_serial_walk():
+    from gpu_util import torch_dev
+    torch = torch_dev()
+    cfg = _cfg(16, router_delay=0, link_delay=0)
+    src, dst, bits, t = mixed_packets(16, 1500, 77, 100000, bcast_frac=0.1)
+    be, got, bgot = run_tree(torch, cfg, src, dst, bits, t)
+    on, ref, bref = oracle_tree(cfg, src, dst, bits, t)
+    for g, r in zip(bgot, bref):
+        np.testing.assert_array_equal(g, r)
+    np.testing.assert_array_equal(be.noc_counters(), on.counters())
