@@ -22,6 +22,9 @@
 //       (tile_manager_summary.cc:135-244) instead of one block per tile
 //   gg_replay --format-table FILE...
 //       that table for per-tile summary texts read from the files
+//   gg_replay --tiles T --route FILE
+//       NetworkModel::routePacket (the host mirror, broadcasts through the
+//       hop-by-hop broadcast tree) on a packet file; hops + network summaries
 //   gg_replay --summary-selftest
 //       prints writeCacheSummary() for fixed counters (no GPU needed)
 #include <rccl/rccl.h>
@@ -78,6 +81,35 @@ int main(int argc, char** argv)
         per_tile.push_back(std::string(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>()));
       }
       std::cout << formatTileSummaries(per_tile);
+      return 0;
+    }
+    else if (a == "--route") {
+      // NetworkModel::routePacket on a packet file {u32 src, u32 dst (0xDEADBABE = broadcast),
+      // u32 bits, u32 0, u64 time_ps} under emesh_hop_by_hop: one line per hop
+      // "tile time zero_load contention", then each tile's Network::outputSummary
+      std::ifstream f(next(), std::ios::binary);
+      if (!f) { std::fprintf(stderr, "cannot open packet file\n"); return 2; }
+      std::vector<char> raw((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+      std::vector<NetPacket> pk(raw.size() / 24);
+      for (size_t k = 0; k < pk.size(); ++k) {
+        uint32_t w[4]; uint64_t t;
+        std::memcpy(w, &raw[24 * k], 16); std::memcpy(&t, &raw[24 * k + 16], 8);
+        pk[k].sender = w[0]; pk[k].receiver = w[1]; pk[k].modeled_length_bits = w[2]; pk[k].time_ps = t;
+      }
+      gg_config cfg;
+      gg_config_default(&cfg, tiles);
+      cfg.net_model = GG_NET_EMESH_HOP_BY_HOP;
+      Backend be(cfg);
+      graphite_amd::NetworkModel nm(be);
+      std::vector<Hop> hops;
+      nm.routePackets(pk, hops);
+      for (const Hop& h : hops)
+        std::printf("%u %llu %llu %llu\n", h.next_tile_id, (unsigned long long)h.time_ps,
+                    (unsigned long long)h.zero_load_delay_ps, (unsigned long long)h.contention_delay_ps);
+      std::vector<uint64_t> nc((size_t)tiles * GG_NUM_NET_COUNTERS);
+      check(gg_noc_get_counters(be.ctx(), nc.data()), "gg_noc_get_counters");
+      for (uint32_t t = 0; t < tiles; ++t)
+        writeNetworkSummary(std::cout, &nc[(size_t)t * GG_NUM_NET_COUNTERS], cfg.frequency_ghz, cfg.net_model, true);
       return 0;
     }
     else if (a == "--shards") shards = (uint32_t)std::strtoul(next(), nullptr, 0);

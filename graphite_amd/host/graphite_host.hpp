@@ -539,7 +539,7 @@ class NetworkModel {
   explicit NetworkModel(Backend& be) : _be(be) {}
   // Routes every packet of the batch to its receiver (all hops, in the
   // canonical order of DESIGN.md §NoC) and returns one RECEIVE_TILE hop per
-  // packet, after the receiver's serialization delay.
+  // packet (per tile for a broadcast), after the receiver's serialization delay.
   void routePackets(const std::vector<NetPacket>& pkts, std::vector<Hop>& hops, hipStream_t stream = nullptr)
   {
     const size_t n = pkts.size();
@@ -558,28 +558,51 @@ class NetworkModel {
     }
     gg_packets pk{_s.p, _d.p, _l.p, _t.p, n};
     gg_packet_out out{_a.p, _z.p, _c.p};
-    check(gg_noc_route_batch(_be.ctx(), &pk, &out, stream), "gg_noc_route_batch");
+    // broadcasts (receiver NetPacket::BROADCAST): the hop-by-hop broadcast tree,
+    // one RECEIVE_TILE hop per tile (network_model_emesh_hop_by_hop.cc:163-221)
+    const size_t nb = (size_t)std::count(dst.begin(), dst.end(), GG_BROADCAST);
+    const size_t T = _be.config().num_tiles;
+    std::vector<uint64_t> barr(nb * T), bzl(nb * T), bct(nb * T);
+    if (nb) {
+      _ba.resize(nb * T); _bz.resize(nb * T); _bc.resize(nb * T);
+      gg_packet_out bout{_ba.p, _bz.p, _bc.p};
+      check(gg_noc_route_tree(_be.ctx(), &pk, &out, &bout, nb, stream), "gg_noc_route_tree");
+      hip_check(hipMemcpyAsync(barr.data(), _ba.p, 8 * nb * T, hipMemcpyDeviceToHost, stream), "copy");
+      hip_check(hipMemcpyAsync(bzl.data(), _bz.p, 8 * nb * T, hipMemcpyDeviceToHost, stream), "copy");
+      hip_check(hipMemcpyAsync(bct.data(), _bc.p, 8 * nb * T, hipMemcpyDeviceToHost, stream), "copy");
+    } else {
+      check(gg_noc_route_batch(_be.ctx(), &pk, &out, stream), "gg_noc_route_batch");
+    }
     if (n) {
       hip_check(hipMemcpyAsync(arr.data(), _a.p, 8 * n, hipMemcpyDeviceToHost, stream), "copy");
       hip_check(hipMemcpyAsync(zl.data(), _z.p, 8 * n, hipMemcpyDeviceToHost, stream), "copy");
       hip_check(hipMemcpyAsync(ct.data(), _c.p, 8 * n, hipMemcpyDeviceToHost, stream), "copy");
     }
     hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
-    hops.resize(n);
-    for (size_t k = 0; k < n; ++k)
-      hops[k] = Hop{dst[k], RECEIVE_TILE, arr[k], zl[k], ct[k]};
+    hops.clear();
+    hops.reserve(n + nb * (T ? T - 1 : 0));
+    size_t b = 0;
+    for (size_t k = 0; k < n; ++k) {
+      if (dst[k] != GG_BROADCAST) { hops.push_back(Hop{dst[k], RECEIVE_TILE, arr[k], zl[k], ct[k]}); continue; }
+      for (size_t c = 0; c < T; ++c) {
+        const size_t o = b * T + c;
+        hops.push_back(Hop{(uint32_t)c, RECEIVE_TILE, barr[o], bzl[o], bct[o]});
+      }
+      ++b;
+    }
   }
-  // The single-packet form of the reference: pushes the packet's delivery hop.
+  // The single-packet form of the reference: pushes the packet's delivery hop
+  // (a broadcast: one per tile, in tile order).
   void routePacket(const NetPacket& pkt, std::queue<Hop>& next_hops)
   {
     std::vector<Hop> h;
     routePackets(std::vector<NetPacket>(1, pkt), h);
-    next_hops.push(h[0]);
+    for (const Hop& x : h) next_hops.push(x);
   }
  private:
   Backend& _be;
   DeviceBuffer<uint32_t> _s, _d, _l;
-  DeviceBuffer<uint64_t> _t, _a, _z, _c;
+  DeviceBuffer<uint64_t> _t, _a, _z, _c, _ba, _bz, _bc;
 };
 
 }  // namespace graphite_amd

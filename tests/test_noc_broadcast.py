@@ -189,3 +189,40 @@ def test_zero_delay_mesh_takes_serial_walk():
     for g, r in zip(bgot, bref):
         np.testing.assert_array_equal(g, r)
     np.testing.assert_array_equal(be.noc_counters(), on.counters())
+
+
+@pytest.mark.gpu
+def test_host_mirror_route_packet_broadcast(tmp_path):
+    """graphite_amd::NetworkModel::routePackets (the C++ mirror, via gg_replay
+    --route): one RECEIVE_TILE hop per unicast packet and one per tile of a
+    broadcast, equal to the oracle; the summaries' broadcast lines count them."""
+    import os
+    import subprocess
+    replay = os.path.join(os.path.dirname(__file__), "..", "graphite_amd", "host", "gg_replay")
+    if not os.path.exists(replay):
+        pytest.skip("gg_replay not built")
+    T = 16
+    cfg = _cfg(T)
+    src, dst, bits, t = mixed_packets(T, 600, 123, 60000, bcast_frac=0.05)
+    rec = np.zeros((len(src), 6), np.uint32)
+    rec[:, 0], rec[:, 1], rec[:, 2] = src, dst, bits
+    rec[:, 4:6] = t.view(np.uint32).reshape(-1, 2)
+    f = tmp_path / "pk.bin"
+    rec.tofile(str(f))
+    out = subprocess.run([replay, "--tiles", str(T), "--route", str(f)], capture_output=True, text=True,
+                         check=True, timeout=120).stdout.splitlines()
+    on = po.OracleNoc(cfg)
+    (ra, rz, rc), (ba, bz, bc) = on.route_tree(src, dst, bits, t)
+    exp, b = [], 0
+    for k in range(len(src)):
+        if dst[k] != C.BROADCAST:
+            exp.append("%d %d %d %d" % (dst[k], ra[k], rz[k], rc[k]))
+        else:
+            exp += ["%d %d %d %d" % (c, ba[b, c], bz[b, c], bc[b, c]) for c in range(T)]
+            b += 1
+    assert out[:len(exp)] == exp
+    nc = on.counters()
+    got_b = [int(x.split(":")[1]) for x in out[len(exp):] if x.startswith("    Total Packets Broadcasted:")]
+    assert got_b == nc[:, K["packets_broadcasted"]].tolist() and sum(got_b) == b
+    x2 = [int(x.split(":")[1]) for x in out[len(exp):] if x.startswith("      Crossbar[2] Traversals:")]
+    assert x2 == nc[:, K["crossbar2"]].tolist()
