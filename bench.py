@@ -405,8 +405,9 @@ def noc_tree_bench(args, dev, T):
     deliveries = (n - nb) + nb * T
     r = {"packets": n, "broadcasts": nb, "deliveries": deliveries, "value": deliveries / dt,
          "unit": "deliveries/s", "seconds": dt,
-         "note": "one lane walks the global (time, index) event order (the broadcast's shared port delay "
-                 "couples the X and Y chains); heap in HBM at this size"}
+         "note": "k_tree_win: conservative time windows of one router + link delay (a broadcast's shared port "
+                 "delay couples the X and Y chains, so the unicast stage pipeline does not apply), one workgroup, "
+                 "one thread per router inside a window"}
     if not args.no_verify:
         on = po.OracleNoc(cfg)
         c0 = time.perf_counter()
