@@ -22,7 +22,7 @@
 //       (tile_manager_summary.cc:135-244) instead of one block per tile
 //   gg_replay --format-table FILE...
 //       that table for per-tile summary texts read from the files
-//   gg_replay --tiles T --route FILE
+//   gg_replay --tiles T --net M --route FILE
 //       NetworkModel::routePacket (the host mirror, broadcasts through the
 //       hop-by-hop broadcast tree) on a packet file; hops + network summaries
 //   gg_replay --summary-selftest
@@ -85,7 +85,7 @@ int main(int argc, char** argv)
     }
     else if (a == "--route") {
       // NetworkModel::routePacket on a packet file {u32 src, u32 dst (0xDEADBABE = broadcast),
-      // u32 bits, u32 0, u64 time_ps} under emesh_hop_by_hop: one line per hop
+      // u32 bits, u32 0, u64 time_ps} under --net (given before --route): one line per hop
       // "tile time zero_load contention", then each tile's Network::outputSummary
       std::ifstream f(next(), std::ios::binary);
       if (!f) { std::fprintf(stderr, "cannot open packet file\n"); return 2; }
@@ -98,7 +98,7 @@ int main(int argc, char** argv)
       }
       gg_config cfg;
       gg_config_default(&cfg, tiles);
-      cfg.net_model = GG_NET_EMESH_HOP_BY_HOP;
+      cfg.net_model = net;
       Backend be(cfg);
       graphite_amd::NetworkModel nm(be);
       std::vector<Hop> hops;
@@ -109,7 +109,8 @@ int main(int argc, char** argv)
       std::vector<uint64_t> nc((size_t)tiles * GG_NUM_NET_COUNTERS);
       check(gg_noc_get_counters(be.ctx(), nc.data()), "gg_noc_get_counters");
       for (uint32_t t = 0; t < tiles; ++t)
-        writeNetworkSummary(std::cout, &nc[(size_t)t * GG_NUM_NET_COUNTERS], cfg.frequency_ghz, cfg.net_model, true);
+        writeNetworkSummary(std::cout, &nc[(size_t)t * GG_NUM_NET_COUNTERS], cfg.frequency_ghz, cfg.net_model,
+                            cfg.net_model == GG_NET_EMESH_HOP_BY_HOP);
       return 0;
     }
     else if (a == "--shards") shards = (uint32_t)std::strtoul(next(), nullptr, 0);

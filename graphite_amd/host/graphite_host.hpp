@@ -539,9 +539,33 @@ class NetworkModel {
   explicit NetworkModel(Backend& be) : _be(be) {}
   // Routes every packet of the batch to its receiver (all hops, in the
   // canonical order of DESIGN.md §NoC) and returns one RECEIVE_TILE hop per
-  // packet (per tile for a broadcast), after the receiver's serialization delay.
+  // packet (per tile for a broadcast: the application tiles, then the system
+  // tiles), after the receiver's serialization delay.
   void routePackets(const std::vector<NetPacket>& pkts, std::vector<Hop>& hops, hipStream_t stream = nullptr)
   {
+    const gg_config& cfg = _be.config();
+    const size_t T = cfg.num_tiles, TT = cfg.total_tiles ? cfg.total_tiles : cfg.num_tiles + 2;
+    const bool any_bcast = std::any_of(pkts.begin(), pkts.end(), [](const NetPacket& p) { return p.receiver == GG_BROADCAST; });
+    if (any_bcast && cfg.net_model != GG_NET_EMESH_HOP_BY_HOP) {
+      // no broadcast capability: Network::netSend sends one packet per tile
+      // (network.cc:187-195); a receiver that is a system tile (MCP, thread
+      // spawners) gets a zero-latency hop (processCornerCases, network_model.cc:440-443)
+      std::vector<NetPacket> ex;
+      for (const NetPacket& p : pkts) {
+        if (p.receiver != GG_BROADCAST) { ex.push_back(p); continue; }
+        for (size_t c = 0; c < T; ++c) { NetPacket q = p; q.receiver = (uint32_t)c; ex.push_back(q); }
+      }
+      std::vector<Hop> h;
+      routePackets(ex, h, stream);
+      hops.clear();
+      size_t i = 0;
+      for (const NetPacket& p : pkts) {
+        if (p.receiver != GG_BROADCAST) { hops.push_back(h[i++]); continue; }
+        for (size_t c = 0; c < T; ++c) hops.push_back(h[i++]);
+        for (size_t c = T; c < TT; ++c) hops.push_back(Hop{(uint32_t)c, RECEIVE_TILE, p.time_ps, 0, 0});
+      }
+      return;
+    }
     const size_t n = pkts.size();
     std::vector<uint32_t> src(n), dst(n), len(n);
     std::vector<uint64_t> t(n), arr(n), zl(n), ct(n);
@@ -561,7 +585,6 @@ class NetworkModel {
     // broadcasts (receiver NetPacket::BROADCAST): the hop-by-hop broadcast tree,
     // one RECEIVE_TILE hop per tile (network_model_emesh_hop_by_hop.cc:163-221)
     const size_t nb = (size_t)std::count(dst.begin(), dst.end(), GG_BROADCAST);
-    const size_t T = _be.config().num_tiles;
     std::vector<uint64_t> barr(nb * T), bzl(nb * T), bct(nb * T);
     if (nb) {
       _ba.resize(nb * T); _bz.resize(nb * T); _bc.resize(nb * T);
@@ -588,6 +611,8 @@ class NetworkModel {
         const size_t o = b * T + c;
         hops.push_back(Hop{(uint32_t)c, RECEIVE_TILE, barr[o], bzl[o], bct[o]});
       }
+      // the system tiles: zero-latency hops pushed by processCornerCases (network_model.cc:451-458)
+      for (size_t c = T; c < TT; ++c) hops.push_back(Hop{(uint32_t)c, RECEIVE_TILE, t[k], 0, 0});
       ++b;
     }
   }

@@ -191,26 +191,33 @@ def test_zero_delay_mesh_takes_serial_walk():
     np.testing.assert_array_equal(be.noc_counters(), on.counters())
 
 
-@pytest.mark.gpu
-def test_host_mirror_route_packet_broadcast(tmp_path):
-    """graphite_amd::NetworkModel::routePackets (the C++ mirror, via gg_replay
-    --route): one RECEIVE_TILE hop per unicast packet and one per tile of a
-    broadcast, equal to the oracle; the summaries' broadcast lines count them."""
+def _replay_route(tmp_path, T, net, src, dst, bits, t):
     import os
     import subprocess
     replay = os.path.join(os.path.dirname(__file__), "..", "graphite_amd", "host", "gg_replay")
     if not os.path.exists(replay):
         pytest.skip("gg_replay not built")
-    T = 16
-    cfg = _cfg(T)
-    src, dst, bits, t = mixed_packets(T, 600, 123, 60000, bcast_frac=0.05)
     rec = np.zeros((len(src), 6), np.uint32)
     rec[:, 0], rec[:, 1], rec[:, 2] = src, dst, bits
     rec[:, 4:6] = t.view(np.uint32).reshape(-1, 2)
     f = tmp_path / "pk.bin"
     rec.tofile(str(f))
-    out = subprocess.run([replay, "--tiles", str(T), "--route", str(f)], capture_output=True, text=True,
-                         check=True, timeout=120).stdout.splitlines()
+    return subprocess.run([replay, "--tiles", str(T), "--net", net, "--route", str(f)], capture_output=True,
+                          text=True, check=True, timeout=120).stdout.splitlines()
+
+
+@pytest.mark.gpu
+def test_host_mirror_route_packet_broadcast(tmp_path):
+    """graphite_amd::NetworkModel::routePackets (the C++ mirror, via gg_replay
+    --route) under emesh_hop_by_hop: one RECEIVE_TILE hop per unicast packet;
+    a broadcast takes the tree, one hop per application tile, then a
+    zero-latency hop per system tile (processCornerCases,
+    network_model.cc:451-458); equal to the oracle, and the summaries'
+    broadcast lines count them."""
+    T = 16
+    cfg = _cfg(T)
+    src, dst, bits, t = mixed_packets(T, 600, 123, 60000, bcast_frac=0.05)
+    out = _replay_route(tmp_path, T, "hop_by_hop", src, dst, bits, t)
     on = po.OracleNoc(cfg)
     (ra, rz, rc), (ba, bz, bc) = on.route_tree(src, dst, bits, t)
     exp, b = [], 0
@@ -219,6 +226,7 @@ def test_host_mirror_route_packet_broadcast(tmp_path):
             exp.append("%d %d %d %d" % (dst[k], ra[k], rz[k], rc[k]))
         else:
             exp += ["%d %d %d %d" % (c, ba[b, c], bz[b, c], bc[b, c]) for c in range(T)]
+            exp += ["%d %d 0 0" % (c, t[k]) for c in (T, T + 1)]
             b += 1
     assert out[:len(exp)] == exp
     nc = on.counters()
@@ -226,3 +234,31 @@ def test_host_mirror_route_packet_broadcast(tmp_path):
     assert got_b == nc[:, K["packets_broadcasted"]].tolist() and sum(got_b) == b
     x2 = [int(x.split(":")[1]) for x in out[len(exp):] if x.startswith("      Crossbar[2] Traversals:")]
     assert x2 == nc[:, K["crossbar2"]].tolist()
+
+
+@pytest.mark.gpu
+def test_host_mirror_unrolls_broadcast_without_tree(tmp_path):
+    """emesh_hop_counter has no broadcast capability: Network::netSend sends one
+    unicast per tile (network.cc:187-195, the sender's own copy a zero-latency
+    self packet), the system tiles zero-latency hops."""
+    T = 16
+    cfg = C.default_config(T, net_model=C.NET_EMESH_HOP_COUNTER)
+    src, dst, bits, t = mixed_packets(T, 300, 321, 60000, bcast_frac=0.1)
+    out = _replay_route(tmp_path, T, "hop_counter", src, dst, bits, t)
+    es, ed, eb, et, sys_after = [], [], [], [], []
+    for k in range(len(src)):
+        rcv = range(T) if dst[k] == C.BROADCAST else [dst[k]]
+        for c in rcv:
+            es.append(src[k]); ed.append(c); eb.append(bits[k]); et.append(t[k])
+        sys_after.append(dst[k] == C.BROADCAST)
+    on = po.OracleNoc(cfg)
+    ra, rz, rc = on.route(np.array(es, np.uint32), np.array(ed, np.uint32), np.array(eb, np.uint32),
+                          np.array(et, np.uint64))
+    exp, i = [], 0
+    for k in range(len(src)):
+        n = T if sys_after[k] else 1
+        exp += ["%d %d %d %d" % (ed[i + j], ra[i + j], rz[i + j], rc[i + j]) for j in range(n)]
+        i += n
+        if sys_after[k]:
+            exp += ["%d %d 0 0" % (c, t[k]) for c in (T, T + 1)]
+    assert out[:len(exp)] == exp
