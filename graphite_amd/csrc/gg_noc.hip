@@ -687,6 +687,38 @@ __device__ __forceinline__ TEv theap_pop(TEv* h, uint64_t& n)
   return top;
 }
 
+// GG_TREE_DBG (diagnostic builds only, results not valid): 1 = no counter
+// atomics, 2 = no queue requests in the tree walk
+#ifndef GG_TREE_DBG
+#define GG_TREE_DBG 0
+#endif
+__device__ __forceinline__ void tcadd(uint64_t* c, uint32_t tile, int k, uint64_t v)
+{
+  if (!(GG_TREE_DBG & 1)) cadd(c, tile, k, v);
+}
+// a router's event counters, summed in registers over its events and added
+// to HBM once (the windowed walk: one thread owns a router)
+struct TreeAcc {
+  uint64_t rcc = 0, rpk = 0, buf = 0, sw = 0, xb[5] = {0, 0, 0, 0, 0}, link = 0, prcv = 0, frcv = 0, brcv = 0, lat = 0, con = 0;
+  __device__ __forceinline__ void crossbar(int np, uint64_t nf)
+  {
+    // constant indices only (a dynamically indexed private array would go to scratch)
+    if (np == 1) xb[0] += nf; else if (np == 2) xb[1] += nf; else if (np == 3) xb[2] += nf;
+    else if (np == 4) xb[3] += nf; else xb[4] += nf;
+  }
+  __device__ __forceinline__ void flush(uint64_t* c, uint32_t tile)
+  {
+    tcadd(c, tile, GG_NC_ROUTER_CONTENTION_CYCLES, rcc); tcadd(c, tile, GG_NC_ROUTER_PACKETS, rpk);
+    tcadd(c, tile, GG_NC_BUFFER_WRITES, buf); tcadd(c, tile, GG_NC_BUFFER_READS, buf);
+    tcadd(c, tile, GG_NC_SWITCH_ALLOC, sw); tcadd(c, tile, GG_NC_CROSSBAR, xb[0]);
+    tcadd(c, tile, GG_NC_CROSSBAR_MULTI + 0, xb[1]); tcadd(c, tile, GG_NC_CROSSBAR_MULTI + 1, xb[2]);
+    tcadd(c, tile, GG_NC_CROSSBAR_MULTI + 2, xb[3]); tcadd(c, tile, GG_NC_CROSSBAR_MULTI + 3, xb[4]);
+    tcadd(c, tile, GG_NC_LINK_TRAVERSALS, link); tcadd(c, tile, GG_NC_PACKETS_RECEIVED, prcv);
+    tcadd(c, tile, GG_NC_FLITS_RECEIVED, frcv); tcadd(c, tile, GG_NC_BITS_RECEIVED, brcv);
+    tcadd(c, tile, GG_NC_TOTAL_LATENCY_PS, lat); tcadd(c, tile, GG_NC_TOTAL_CONTENTION_PS, con);
+    *this = TreeAcc();
+  }
+};
 struct TreeIO {
   const uint32_t* src; const uint32_t* dst; const uint32_t* len; const uint64_t* t0;
   uint32_t* bidx; gg_packet_out out, bout;
@@ -698,19 +730,19 @@ __device__ __forceinline__ TEv tree_inject(const NocDev& D, const TreeIO& IO, co
   const NocParams& P = D.P;
   const uint32_t k = e.id, s = IO.src[k], bits = IO.len[k];
   const uint64_t nf = nflits(P, bits);
-  cadd(D.ctr, s, GG_NC_PACKETS_SENT, 1); cadd(D.ctr, s, GG_NC_FLITS_SENT, nf); cadd(D.ctr, s, GG_NC_BITS_SENT, bits);
+  tcadd(D.ctr, s, GG_NC_PACKETS_SENT, 1); tcadd(D.ctr, s, GG_NC_FLITS_SENT, nf); tcadd(D.ctr, s, GG_NC_BITS_SENT, bits);
   if (IO.dst[k] == GG_BROADCAST) {                 // updateSendCounters (network_model.cc:244-250)
-    cadd(D.ctr, s, GG_NC_PACKETS_BROADCASTED, 1); cadd(D.ctr, s, GG_NC_FLITS_BROADCASTED, nf);
-    cadd(D.ctr, s, GG_NC_BITS_BROADCASTED, bits);
+    tcadd(D.ctr, s, GG_NC_PACKETS_BROADCASTED, 1); tcadd(D.ctr, s, GG_NC_FLITS_BROADCASTED, nf);
+    tcadd(D.ctr, s, GG_NC_BITS_BROADCASTED, bits);
   }
   uint64_t qd = 0;
-  if (P.qm) { HTree tr = D.tree(s, 5); qd = tr.delay(time_to_cycles(e.t, P.f), nf, D.err); }
+  if (P.qm && !(GG_TREE_DBG & 2)) { HTree tr = D.tree(s, 5); qd = tr.delay(time_to_cycles(e.t, P.f), nf, D.err); }
   return TEv{e.t + lat_to_ps(0, P.f) + lat_to_ps(qd, P.f), k, s};
 }
 
 // EMESH: one router event (unicast XY or broadcast fork); forwarded copies go to push(TEv)
 template <class Push>
-__device__ __forceinline__ void tree_router(const NocDev& D, const TreeIO& IO, const TEv& e, Push push)
+__device__ __forceinline__ void tree_router(const NocDev& D, const TreeIO& IO, const TEv& e, Push push, TreeAcc& A)
 {
   const NocParams& P = D.P;
   const uint32_t W = P.w, H = P.h;
@@ -736,27 +768,24 @@ __device__ __forceinline__ void tree_router(const NocDev& D, const TreeIO& IO, c
     ports[np] = P_SELF; nxt[np++] = c;
   }
   uint64_t qd = 0;
-  if (P.qm) {
+  if (P.qm && !(GG_TREE_DBG & 2)) {
     for (int i = 0; i < np; ++i) {
       HTree tr = D.tree(c, ports[i]);
       qd = max(qd, tr.delay(time_to_cycles(e.t, P.f), nf, D.err));
     }
-    cadd(D.ctr, c, GG_NC_ROUTER_CONTENTION_CYCLES, qd * (uint64_t)np);   // updateContentionCounters, per listed port
-    cadd(D.ctr, c, GG_NC_ROUTER_PACKETS, (uint64_t)np);
+    A.rcc += qd * (uint64_t)np;                    // updateContentionCounters, per listed port
+    A.rpk += (uint64_t)np;
   }
-  cadd(D.ctr, c, GG_NC_BUFFER_WRITES, nf); cadd(D.ctr, c, GG_NC_BUFFER_READS, nf);
-  cadd(D.ctr, c, GG_NC_SWITCH_ALLOC, 1);
-  cadd(D.ctr, c, np == 1 ? (int)GG_NC_CROSSBAR : (int)GG_NC_CROSSBAR_MULTI + np - 2, nf);
-  cadd(D.ctr, c, GG_NC_LINK_TRAVERSALS, nf * (uint64_t)np);
+  A.buf += nf; A.sw += 1; A.crossbar(np, nf);
+  A.link += nf * (uint64_t)np;
   const uint64_t zps = lat_to_ps((uint64_t)P.router_delay + P.link_delay, P.f), cps = lat_to_ps(qd, P.f);
   const uint64_t hops = (uint64_t)((cx > sx ? cx - sx : sx - cx) + (cy > sy ? cy - sy : sy - cy)) + 1;
   const uint64_t t = e.t + zps + cps, zl = hops * zps, ct = t - IO.t0[k] - zl;
   for (int i = 0; i < np; ++i) {
     if (ports[i] != P_SELF) { push(TEv{t, k, nxt[i]}); continue; }
     const uint64_t ser = lat_to_ps(nf, P.f);       // receive at c (network_model.cc:118-150,253-272)
-    cadd(D.ctr, c, GG_NC_PACKETS_RECEIVED, 1); cadd(D.ctr, c, GG_NC_FLITS_RECEIVED, nf);
-    cadd(D.ctr, c, GG_NC_BITS_RECEIVED, bits);
-    cadd(D.ctr, c, GG_NC_TOTAL_LATENCY_PS, zl + ser + ct); cadd(D.ctr, c, GG_NC_TOTAL_CONTENTION_PS, ct);
+    A.prcv += 1; A.frcv += nf; A.brcv += bits;
+    A.lat += zl + ser + ct; A.con += ct;
     if (d == GG_BROADCAST) {
       const uint64_t o = (uint64_t)IO.bidx[k] * P.tiles + c;
       IO.bout.arrival_ps_dev[o] = t + ser; IO.bout.zero_load_ps_dev[o] = zl + ser; IO.bout.contention_ps_dev[o] = ct;
@@ -791,7 +820,9 @@ __global__ __launch_bounds__(64) void k_tree_walk(NocDev D, TreeIO IO, uint64_t 
   while (hn) {
     const TEv e = theap_pop(heap, hn);
     if (e.at & kInjBit) { theap_push(heap, hn, tree_inject(D, IO, e)); continue; }
-    tree_router(D, IO, e, [&](const TEv& x) { theap_push(heap, hn, x); });
+    TreeAcc A;
+    tree_router(D, IO, e, [&](const TEv& x) { theap_push(heap, hn, x); }, A);
+    A.flush(D.ctr, e.at);
   }
 }
 
@@ -882,7 +913,8 @@ __global__ __launch_bounds__(kTreeThreads) void k_tree_win(NocDev D, TreeIO IO, 
   }
   for (uint32_t i = tid; i < T; i += nt) cnt[i] = 0;
   __syncthreads();
-  // 2. windows
+  // 2. windows (router tid's counters in registers when every thread owns one router)
+  TreeAcc acc;
   for (;;) {
     const uint32_t n0 = s_n0;
     if (n0 == 0) break;
@@ -911,8 +943,9 @@ __global__ __launch_bounds__(kTreeThreads) void k_tree_win(NocDev D, TreeIO IO, 
       for (uint64_t i = 0; i < m; ++i) { const TEv e = h[i]; theap_push(h, hn, e); }
       while (hn) {
         const TEv e = theap_pop(h, hn);
-        tree_router(D, IO, e, [&](const TEv& x) { E1[atomicAdd(&s_n1, 1u)] = x; });
+        tree_router(D, IO, e, [&](const TEv& x) { E1[atomicAdd(&s_n1, 1u)] = x; }, acc);
       }
+      if (T > nt) acc.flush(D.ctr, r);             // a thread owns several routers: flush per batch
     }
     for (uint32_t i = tid; i < T; i += nt) cnt[i] = 0;
     __syncthreads();
@@ -920,6 +953,7 @@ __global__ __launch_bounds__(kTreeThreads) void k_tree_win(NocDev D, TreeIO IO, 
     TEv* x = E0; E0 = E1; E1 = x;
     __syncthreads();
   }
+  if (T <= nt && tid < T) acc.flush(D.ctr, tid);
 }
 
 struct gg_noc_state {
