@@ -15,6 +15,8 @@
 // one global event queue exactly.
 #include "gg_dev.h"
 
+#include <hip/hip_cooperative_groups.h>
+
 #include <algorithm>
 
 namespace {
@@ -854,8 +856,13 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
   __syncthreads();
   return r;
 }
+// Control words of the grid form: [0] pending count, [1] next pending count,
+// [2..3] the window minimum (u64)
+struct TreeCtl { uint32_t n0, n1; unsigned long long tmin; };
+
+template <bool GRID>
 __global__ __launch_bounds__(kTreeThreads) void k_tree_win(NocDev D, TreeIO IO, uint64_t n, uint64_t nb,
-                                                           TEv* E0, TEv* E1, TEv* G, uint64_t hcap)
+                                                           TEv* E0, TEv* E1, TEv* G, uint64_t hcap, TreeCtl* ctl)
 {
   __shared__ uint32_t cnt[kTreeMaxT];
   __shared__ uint32_t off[kTreeMaxT + 1];
@@ -913,6 +920,10 @@ __global__ __launch_bounds__(kTreeThreads) void k_tree_win(NocDev D, TreeIO IO, 
   }
   for (uint32_t i = tid; i < T; i += nt) cnt[i] = 0;
   __syncthreads();
+  if (GRID) {                                      // the windows run in k_tree_grid
+    if (tid == 0) { ctl->n0 = s_n0; ctl->n1 = 0; ctl->tmin = ~0ull; }
+    return;
+  }
   // 2. windows (router tid's counters in registers when every thread owns one router)
   TreeAcc acc;
   for (;;) {
@@ -956,6 +967,69 @@ __global__ __launch_bounds__(kTreeThreads) void k_tree_win(NocDev D, TreeIO IO, 
   if (T <= nt && tid < T) acc.flush(D.ctr, tid);
 }
 
+// The window loop over a cooperative grid (k_tree_win<true> did the
+// injection ports): the same phases as k_tree_win with the grouping arrays in
+// HBM and grid barriers between phases, so the routers' queue requests use
+// the memory pipelines of kTreeGridBlocks CUs instead of one.  Measured: 92 ms
+// against 80 ms for one workgroup on the bench batch (six grid barriers per
+// window outweigh the spread), so it is the A/B form (GG_NOC_TREE_GRID=1).  Global thread
+// g owns router g (T <= kTreeGridBlocks * kTreeGridThreads).
+constexpr uint32_t kTreeGridBlocks = 16, kTreeGridThreads = 256;
+__global__ __launch_bounds__(kTreeGridThreads) void k_tree_grid(NocDev D, TreeIO IO, TEv* E0, TEv* E1, TEv* G,
+                                                                 uint32_t* cnt, uint32_t* off, TreeCtl* ctl)
+{
+  __shared__ uint32_t wsum[kTreeGridThreads / 64 + 1];
+  cooperative_groups::grid_group grid = cooperative_groups::this_grid();
+  const NocParams& P = D.P;
+  const uint32_t T = P.tiles, g = blockIdx.x * blockDim.x + threadIdx.x, ng = gridDim.x * blockDim.x;
+  const uint64_t zps = lat_to_ps((uint64_t)P.router_delay + P.link_delay, P.f);
+  TreeAcc acc;
+  for (;;) {
+    grid.sync();
+    const uint32_t n0 = __hip_atomic_load(&ctl->n0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (n0 == 0) break;
+    unsigned long long lm = ~0ull;
+    for (uint32_t i = g; i < n0; i += ng) lm = min(lm, (unsigned long long)E0[i].t);
+    if (lm != ~0ull) atomicMin(&ctl->tmin, lm);
+    grid.sync();
+    const uint64_t wend = __hip_atomic_load(&ctl->tmin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + zps;
+    for (uint32_t i = g; i < n0; i += ng) {
+      const TEv e = E0[i];
+      if (e.t < wend) atomicAdd(&cnt[e.at], 1u);
+      else E1[atomicAdd(&ctl->n1, 1u)] = e;
+    }
+    grid.sync();
+    if (blockIdx.x == 0) {                         // exclusive scan of cnt -> off, cnt reset (cursor)
+      const uint32_t per = (T + blockDim.x - 1) / blockDim.x, t0 = threadIdx.x * per;
+      uint32_t a = 0, tot;
+      for (uint32_t i = t0; i < min(T, t0 + per); ++i) a += cnt[i];
+      a = block_excl_scan(a, wsum, &tot);
+      for (uint32_t i = t0; i < min(T, t0 + per); ++i) { off[i] = a; a += cnt[i]; cnt[i] = 0; }
+      if (threadIdx.x == 0) { off[T] = tot; ctl->tmin = ~0ull; }
+    }
+    grid.sync();
+    for (uint32_t i = g; i < n0; i += ng) {
+      const TEv e = E0[i];
+      if (e.t < wend) G[off[e.at] + atomicAdd(&cnt[e.at], 1u)] = e;
+    }
+    grid.sync();
+    if (g < T) {
+      TEv* h = G + off[g];
+      uint64_t m = off[g + 1] - off[g], hn = 0;
+      for (uint64_t i = 0; i < m; ++i) { const TEv e = h[i]; theap_push(h, hn, e); }
+      while (hn) {
+        const TEv e = theap_pop(h, hn);
+        tree_router(D, IO, e, [&](const TEv& x) { E1[atomicAdd(&ctl->n1, 1u)] = x; }, acc);
+      }
+      cnt[g] = 0;
+    }
+    grid.sync();
+    if (g == 0) { ctl->n0 = ctl->n1; ctl->n1 = 0; }
+    TEv* x = E0; E0 = E1; E1 = x;
+  }
+  if (g < T) acc.flush(D.ctr, g);
+}
+
 struct gg_noc_state {
   NocParams P;
   HQueue* q = nullptr; HNode* nd = nullptr; uint64_t nq = 0;
@@ -968,6 +1042,7 @@ struct gg_noc_state {
   uint32_t* counts = nullptr; uint32_t* cursor = nullptr; uint64_t* off = nullptr; uint32_t nb_cap = 0;
   bool staged = true;   // LDS-staged stage kernels where the queues fit (GG_NOC_STAGED=0: HBM-resident, A/B)
   TEv* theap = nullptr; uint32_t* bidx = nullptr; uint64_t tcap = 0, bcap = 0;   // broadcast-tree walk scratch
+  uint32_t* tctl = nullptr;                       // grid form: TreeCtl | cnt[kTreeMaxT] | off[kTreeMaxT + 1]
 };
 
 gg_status gg_noc_alloc(gg_ctx* ctx)
@@ -1011,7 +1086,7 @@ void gg_noc_free(gg_ctx* ctx)
   gg_noc_state* S = ctx->noc;
   if (!S) return;
   void* ps[] = {S->q, S->nd, S->ctr, S->t, S->zl, S->ct, S->cur, S->keys, S->ids, S->heap,
-                S->counts, S->cursor, S->off, S->theap, S->bidx};
+                S->counts, S->cursor, S->off, S->theap, S->bidx, S->tctl};
   for (void* p : ps) if (p) hipFree(p);
   delete S;
   ctx->noc = nullptr;
@@ -1099,6 +1174,14 @@ gg_status gg_noc_tree(gg_ctx* ctx, const gg_packets* pk, const gg_packet_out* ou
   const bool win = (uint64_t)P.router_delay + P.link_delay > 0 &&   // lookahead: a hop takes >= 1 cycle P.tiles <= kTreeMaxT && hcap < (1ull << 32) &&
                    !(getenv("GG_NOC_TREE_SERIAL") && atoi(getenv("GG_NOC_TREE_SERIAL")));
   const bool lds = !win && hcap <= kTreeLdsEv;
+  // the window loop over a cooperative grid of CUs: A/B form (GG_NOC_TREE_GRID=1),
+  // measured slower than one workgroup
+  const bool grid = win && P.tiles <= kTreeGridBlocks * kTreeGridThreads &&
+                    getenv("GG_NOC_TREE_GRID") && atoi(getenv("GG_NOC_TREE_GRID")) == 1;
+  if (grid && !S->tctl) {
+    GG_HIP(hipMalloc((void**)&S->tctl, 4 * (4 + 2 * kTreeMaxT + 1)));
+    GG_HIP(hipMemsetAsync(S->tctl, 0, 4 * (4 + 2 * kTreeMaxT + 1), s));
+  }
   const uint64_t need = win ? 3 * hcap : lds ? 0 : hcap;
   if (need > S->tcap) {
     if (S->theap) hipFree(S->theap);
@@ -1114,9 +1197,17 @@ gg_status gg_noc_tree(gg_ctx* ctx, const gg_packets* pk, const gg_packet_out* ou
   const gg_packet_out none{nullptr, nullptr, nullptr};
   TreeIO IO{pk->src_dev, pk->dst_dev, pk->length_bits_dev, pk->time_ps_dev, S->bidx, *out, nb ? *bout : none};
   gg_timer_begin(ctx, "noc_tree", s);
-  if (win)
-    hipLaunchKernelGGL(k_tree_win, dim3(1), dim3(kTreeThreads), 0, s, D, IO, n, nb, S->theap, S->theap + hcap,
-                       S->theap + 2 * hcap, hcap);
+  if (win && grid) {
+    TEv *E0 = S->theap, *E1 = S->theap + hcap, *G = S->theap + 2 * hcap;
+    TreeCtl* ctl = reinterpret_cast<TreeCtl*>(S->tctl);
+    uint32_t *cnt = S->tctl + 4, *off = S->tctl + 4 + kTreeMaxT;
+    hipLaunchKernelGGL(k_tree_win<true>, dim3(1), dim3(kTreeThreads), 0, s, D, IO, n, nb, E0, E1, G, hcap, ctl);
+    GG_HIP(hipGetLastError());
+    void* args[] = {(void*)&D, (void*)&IO, (void*)&E0, (void*)&E1, (void*)&G, (void*)&cnt, (void*)&off, (void*)&ctl};
+    GG_HIP(hipLaunchCooperativeKernel((const void*)k_tree_grid, dim3(kTreeGridBlocks), dim3(kTreeGridThreads), args, 0, s));
+  } else if (win)
+    hipLaunchKernelGGL(k_tree_win<false>, dim3(1), dim3(kTreeThreads), 0, s, D, IO, n, nb, S->theap, S->theap + hcap,
+                       S->theap + 2 * hcap, hcap, nullptr);
   else if (lds)
     hipLaunchKernelGGL(k_tree_walk<true>, dim3(1), dim3(64), hcap * sizeof(TEv), s, D, IO, n, nb, nullptr, hcap);
   else
