@@ -1171,8 +1171,10 @@ gg_status gg_noc_tree(gg_ctx* ctx, const gg_packets* pk, const gg_packet_out* ou
     return gg_fail(GG_ERR_INVALID, "NULL packet or output pointer");
   if (n >= (1ull << 32) || nb > n) return gg_fail(GG_ERR_RANGE, "batch larger than 2^32 packets or num_broadcasts > packets");
   const uint64_t hcap = n + nb * P.tiles;          // live copies of a broadcast <= tiles
-  const bool win = (uint64_t)P.router_delay + P.link_delay > 0 &&   // lookahead: a hop takes >= 1 cycle P.tiles <= kTreeMaxT && hcap < (1ull << 32) &&
-                   !(getenv("GG_NOC_TREE_SERIAL") && atoi(getenv("GG_NOC_TREE_SERIAL")));
+  // the windowed walk needs lookahead (a hop takes >= 1 cycle), its LDS per-router
+  // arrays (kTreeMaxT) and 32-bit event indices; everything else takes the serial walk
+  const bool win = (uint64_t)P.router_delay + P.link_delay > 0 && P.tiles <= kTreeMaxT &&
+                   hcap < (1ull << 32) && !(getenv("GG_NOC_TREE_SERIAL") && atoi(getenv("GG_NOC_TREE_SERIAL")));
   const bool lds = !win && hcap <= kTreeLdsEv;
   // the window loop over a cooperative grid of CUs: A/B form (GG_NOC_TREE_GRID=1),
   // measured slower than one workgroup
