@@ -107,6 +107,10 @@ struct CP {
   uint32_t touch_each;                     // hit runs touch LRU rows one record at a time (> 16 ways; GG_COH_TOUCH_EACH=1)
   uint32_t walk_wide;                      // pipelined walkers scan every packet (the > 128-packet path; GG_COH_WALK_WIDE=1)
   uint32_t no_hit_runs;                    // GG_COH_NO_HIT_RUNS=1: every record through app_access
+  // k_c_shard (one workgroup per logical shard): most tiles / X / Y segments of a
+  // shard, bytes of a wave's LDS area, LDS offsets of the shard arrays, record
+  // pool and boundary region per shard, walker packets a wave's global scratch holds
+  uint32_t sh_nt, sh_nxs, sh_nys, sh_wave, sh_arr, sh_pcap, sh_bcap, sh_gpk, sh_gbytes, sh_segw, sh_segmax, sh_k0;
   uint64_t lat_l1d, lat_l1t, lat_l2d, lat_l2t, lat_dir, gap_ps, dram_proc, dram_cost;
   NocParams np;
 };
@@ -140,7 +144,13 @@ struct CS {
   uint64_t* ctr;                         // NoC counters [T][GG_NUM_NET_COUNTERS]
   uint64_t* gscr;                        // [L][5 * IC] ordering scratch beyond kInLds
   unsigned long long* prof;              // GG_COH_PROFILE=1: shader-clock cycles per phase (diagnostics)
-  uint32_t* gbar;                        // grid barrier counter of k_c_persist
+  uint32_t* gbar;                        // grid barrier counter of k_c_persist / k_c_shard
+  // k_c_shard: local tile -> index within its shard; per owned shard its tiles
+  // (offsets [ns + 1]), X / Y segments (offsets), segment -> index within its
+  // shard ([2][max(nsx, nsy)]); quantum-end slots [2][ns][8]; boundary regions
+  // [2][ns][sh_bcap]; walker scratch [ns][waves][sh_gbytes]
+  const uint32_t *tsi, *sh_toff, *sh_tiles, *sh_xoff, *sh_xsegs, *sh_yoff, *sh_ysegs, *seg_loc;
+  uint64_t* sh_slot; gg_cmsg* sbnd; uint8_t* wscr;
 };
 // profile slots: step phases 0..5 summed over tiles, 8 = sum over steps of the slowest tile;
 // walker: 16 staging+load, 17 event loop, 18 hand-off+write back, 19 events, 20 sum of slowest walker per launch (X),
@@ -397,15 +407,82 @@ enum { W_NONE = 0, W_PROC, W_CONT, W_NEXT, W_NULLIFY };
 struct Work { uint64_t addr; uint32_t kind, type, requester, cached; int32_t h; };
 #define WSTACK 32
 
-// LDS of one tile step
-struct StepLds {
-  CReq rq[kRqLds];
+// LDS of one tile step (IN: inbox / port batch entries ordered in LDS, RQ:
+// directory request FIFO entries staged in LDS; beyond them global scratch)
+template <uint32_t IN, uint32_t RQ>
+struct StepLdsT {
+  static constexpr uint32_t kIn = IN, kRq = RQ;
+  CReq rq[RQ];
   uint8_t dimg[sizeof(HQueue) + kQMax * sizeof(HNode)];   // DRAM queue image
   uint8_t pimg[sizeof(HQueue) + kQMax * sizeof(HNode)];   // SELF / injection port image
-  uint64_t x1[kInLds], x2[kInLds], x3[kInLds];
-  uint32_t i1[kInLds], i2[kInLds];
+  uint64_t x1[IN], x2[IN], x3[IN];
+  uint32_t i1[IN], i2[IN];
   uint32_t ch[2 * kChunks];                               // record chunks: base, used
   Work wstack[WSTACK];                                    // directory work loop continuations
+};
+using StepLds = StepLdsT<kInLds, kRqLds>;                 // one tile per workgroup (k_c_step, k_c_persist)
+using StepLdsS = StepLdsT<128, 64>;                       // one tile per wave of a shard workgroup (k_c_shard)
+
+// The lanes of ONE wave exchange data through LDS / global memory between the
+// phases of a tile step; in a multi-wave workgroup the other waves run other
+// tiles, so this is a wave barrier with workgroup-scope fences (every wait a
+// __syncthreads would imply, no s_barrier).
+__device__ __forceinline__ void tsync()
+{
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// Where a tile step's deliveries go.  GHooks: the per-step launches
+// (k_c_step / k_c_persist) keep the inbox / arrival / segment counters and the
+// record pools in HBM, shared by every block of the launch.  ShardHooks
+// (k_c_shard, below): one workgroup owns a logical shard for the whole run and
+// keeps them in its LDS.  Slot functions return the list position or ~0u
+// (capacity exceeded, reported through S.err).
+struct GHooks {
+  const CP& P; const CS& S;
+  // n contiguous records of the parity-p pool (wave-uniform)
+  __device__ __forceinline__ uint32_t pool_alloc(uint32_t p, uint32_t want) const
+  {
+    uint32_t b = 0;
+    if (lane_id() == 0) b = atomicAdd(&(p ? S.npool[1] : S.npool[0]), want);
+    b = (uint32_t)__shfl((int)b, 0);
+    return (uint64_t)b + want > P.msg_cap ? ~0u : b;
+  }
+  __device__ __forceinline__ uint32_t inbox_slot(uint32_t pn, uint32_t ld) const
+  {
+    const uint32_t j = atomicAdd(&(pn ? S.ninb1 : S.ninb0)[ld], 1u);
+    return j < P.IC ? j : ~0u;
+  }
+  __device__ __forceinline__ uint32_t arv_slot(uint32_t pn, uint32_t ld) const
+  {
+    const uint32_t j = atomicAdd(&(pn ? S.narv1 : S.narv0)[ld], 1u);
+    return j < P.IC ? j : ~0u;
+  }
+  __device__ __forceinline__ uint32_t seg_slot(bool is_x, uint32_t sg) const
+  {
+    const uint32_t j = atomicAdd(&(is_x ? S.nxl : S.nyl)[sg], 1u);
+    return j < P.seg_cap ? j : ~0u;
+  }
+  __device__ __forceinline__ bool bnd_put(const gg_cmsg& m) const
+  {
+    const uint32_t j = atomicAdd(S.bnd_cnt, 1u);
+    if (j >= P.msg_cap) return false;
+    S.bnd[j] = m;
+    return true;
+  }
+  // the tile's delivery counts of parity p were consumed
+  __device__ __forceinline__ void clear_arv(uint32_t p, uint32_t lt) const { (p ? S.narv1 : S.narv0)[lt] = 0; }
+  __device__ __forceinline__ void clear_inb(uint32_t p, uint32_t lt) const { (p ? S.ninb1 : S.ninb0)[lt] = 0; }
+  // lane 0: the step's run-info counts
+  __device__ __forceinline__ void step_counts(uint32_t k, uint32_t net, uint32_t self, uint32_t bnd, uint32_t sent) const
+  {
+    if (net) atomicAdd((unsigned long long*)&S.ri[GG_RI_NET_MSGS], (unsigned long long)net);
+    if (self) atomicAdd((unsigned long long*)&S.ri[GG_RI_SELF_MSGS], (unsigned long long)self);
+    if (bnd) atomicAdd((unsigned long long*)&S.ri[GG_RI_BOUNDARY_MSGS], (unsigned long long)bnd);
+    if (sent) atomicAdd(&S.ring[k & 3], sent);
+  }
 };
 
 // the tile's per-step state words, loaded at kernel entry together with the
@@ -431,10 +508,12 @@ struct TilePre {
 // ---------------------------------------------------------------------------
 // one tile's controllers (every lane, identical values)
 // ---------------------------------------------------------------------------
+template <class SL, class H>
 struct Tile {
   const CP& P; const CS& S;
   uint32_t lt, tile, ln, p;             // local index, tile id, lane, step parity
-  StepLds& sl;
+  SL& sl;
+  const H& hk;
   Cache L1, L2;
   uint64_t sd;                          // this step's statistics increments: lane k holds statistic k
   uint64_t rec, rec_end, clk, pend_start, out_addr, out_time;
@@ -449,9 +528,9 @@ struct Tile {
   // LC: the tile's L1-D / L2 tags, meta bytes and RR counters live in LDS at
   // clds for the whole launch (k_c_persist; layout of cache_lds_bytes)
   template <bool LC>
-  __device__ __forceinline__ Tile(const CP& P_, const CS& S_, uint32_t l, uint32_t par, StepLds& s_, uint8_t* clds,
+  __device__ __forceinline__ Tile(const CP& P_, const CS& S_, uint32_t l, uint32_t par, SL& s_, const H& h_, uint8_t* clds,
                                   std::integral_constant<bool, LC>, const TilePre& pre)
-      : P(P_), S(S_), lt(l), tile(pre.tile), ln(lane_id()), p(par), sl(s_)
+      : P(P_), S(S_), lt(l), tile(pre.tile), ln(lane_id()), p(par), sl(s_), hk(h_)
   {
     const size_t n1 = (size_t)P.s1 * P.a1, n2 = (size_t)P.s2 * P.a2;
     if constexpr (LC) {
@@ -500,10 +579,8 @@ struct Tile {
     if (cused + n > ccap) {
       if (nch) sl.ch[2 * (nch - 1) + 1] = cused;
       const uint32_t want = n > kChunk ? n : kChunk;
-      uint32_t b = 0;
-      if (ln == 0) b = atomicAdd(&S.npool[p], want);
-      b = (uint32_t)__shfl((int)b, 0);
-      if ((uint64_t)b + want > P.msg_cap || nch >= kChunks) { fail(GG_DERR_CAP); return ~0u; }
+      const uint32_t b = hk.pool_alloc(p, want);
+      if (b == ~0u || nch >= kChunks) { fail(GG_DERR_CAP); return ~0u; }
       sl.ch[2 * nch] = b; sl.ch[2 * nch + 1] = 0;
       ++nch; cbase = b; ccap = want; cused = 0;
     }
@@ -672,7 +749,7 @@ struct Tile {
   }
   __device__ __forceinline__ void qpush(uint64_t a, uint64_t t, uint32_t type, uint32_t req)
   {
-    if (nrq >= (rq_lds ? kRqLds : P.QC)) { fail(GG_DERR_CAP); return; }
+    if (nrq >= (rq_lds ? SL::kRq : P.QC)) { fail(GG_DERR_CAP); return; }
     rqp[nrq] = CReq{a, t, type, req};
     if (rq_lds) wave_sync();
     ++nrq;
@@ -1202,14 +1279,14 @@ __device__ void order_inbox(uint32_t n, const uint64_t* a, const uint64_t* k, ui
     }
     pm[i] = m;
   }
-  __syncthreads();
+  tsync();
   for (uint32_t i = ln; i < n; i += 64) {
     const uint64_t pi = pm[i], ki = k[i];
     uint32_t r = 0;
     for (uint32_t j = 0; j < n; ++j) { const uint64_t pj = pm[j]; r += (pj < pi) || (pj == pi && k[j] < ki); }
     out[r] = idx[i];
   }
-  __syncthreads();
+  tsync();
 }
 // (time, send time, sender << 32 | seq) order: a port's service order (the
 // canonical key of DESIGN.md §4)
@@ -1225,7 +1302,7 @@ __device__ void order_port(uint32_t n, const uint64_t* t, const uint64_t* s, con
     }
     out[r] = idx[i];
   }
-  __syncthreads();
+  tsync();
 }
 
 // Queue images (HQueue + max_size nodes, all 16-byte words) between HBM and
@@ -1346,6 +1423,12 @@ __device__ __forceinline__ void quantum_end(const CP& P, const CS& S, uint32_t L
 // the tile's trace window: records wbase + lane (kept across the steps of a
 // persistent launch; the records are read-only for the whole run)
 struct TraceWin { uint64_t wbase, wa; uint32_t wm; };
+constexpr uint64_t kNsFin = ~0ull, kNsBlk = ~0ull - 1;   // next start of a finished / blocked tile
+
+template <bool LC, bool HR, class SL, class H>
+__device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t lt, uint32_t k, uint32_t L, uint64_t barrier,
+                                          TraceWin& W, SL& sl, uint8_t* clds, const TilePre& pre, const H& hk,
+                                          uint32_t na, uint32_t ni);
 
 // LC: cache state in LDS; HR: L1 hit runs (persistent small meshes, where
 // long runs of hits between misses pay for the window look-up)
@@ -1354,7 +1437,6 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
                                           TraceWin& W)
 {
   const uint32_t ln = threadIdx.x, lt = blockIdx.x;
-  PROF_T0();
   uint32_t k = L;
   uint64_t barrier = barrier_arg, q = 0, Q = 0;
   // one round trip: the launch state (written by earlier launches)
@@ -1390,7 +1472,24 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
   }
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   StepLds& sl = *reinterpret_cast<StepLds*>(smem);
-  Tile T(P, S, lt, p, sl, smem + P.cache_lds_off, std::integral_constant<bool, LC>(), pre);
+  const GHooks hk{P, S};
+  const uint32_t na = P.net == GG_NET_EMESH_HOP_BY_HOP ? (p ? pre.narv1 : pre.narv0) : 0u;
+  const uint32_t ni = p ? pre.ninb1 : pre.ninb0;
+  tile_step<LC, HR>(P, S, lt, k, L, barrier, W, sl, smem + P.cache_lds_off, pre, hk, na, ni);
+}
+
+// One tile's step k (parity k & 1) of the quantum that ends at `barrier`, on
+// the calling wave: the SELF port + receive of the packets that
+// reached the tile (na), the inbox (ni records), the trace, publish, write
+// back.  Deliveries go through the hooks.
+template <bool LC, bool HR, class SL, class H>
+__device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t lt, uint32_t k, uint32_t L, uint64_t barrier,
+                                          TraceWin& W, SL& sl, uint8_t* clds, const TilePre& pre, const H& hk,
+                                          uint32_t na, uint32_t ni)
+{
+  const uint32_t ln = lane_id(), p = k & 1u;
+  PROF_T0();
+  Tile<SL, H> T(P, S, lt, p, sl, hk, clds, std::integral_constant<bool, LC>(), pre);
   const gg_cmsg* prev = pool(S, p ^ 1u);     // records delivered to this step
   uint64_t* gscr = S.gscr + (size_t)lt * 5 * P.IC;
   // NoC counters of the SELF port (lanes 0-6) and of the receiver
@@ -1400,12 +1499,11 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
   // ---- 0. hop-by-hop: SELF output port + receive of last step's packets (routePacket
   // at the receiver, hop_by_hop.cc:223-256; __processReceivedPacket, network_model.cc:118-150)
   PROF_AT(_sa);
-  const uint32_t na = P.net == GG_NET_EMESH_HOP_BY_HOP ? (p ? pre.narv1 : pre.narv0) : 0u;
   uint64_t _sb = 0, _sc = 0, _sd = 0, _se = 0;
   if (na) {
     if (S.prof) _sb = __builtin_amdgcn_s_memtime();
     const uint32_t* al = arv(S, p) + (size_t)lt * P.IC;
-    const bool lds = na <= kInLds;
+    const bool lds = na <= SL::kIn;
     uint64_t* t_ = lds ? sl.x1 : gscr; uint64_t* s_ = lds ? sl.x2 : gscr + P.IC; uint64_t* k_ = lds ? sl.x3 : gscr + 2 * P.IC;
     uint32_t* i_ = lds ? sl.i1 : (uint32_t*)(gscr + 3 * P.IC); uint32_t* o_ = lds ? sl.i2 : (uint32_t*)(gscr + 4 * P.IC);
     for (uint32_t i = ln; i < na; i += 64) {
@@ -1413,7 +1511,7 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
       const gg_cmsg& m = prev[r];
       t_[i] = m.arrival_ps; s_[i] = m.send_ps; k_[i] = ((uint64_t)m.src << 32) | m.seq; i_[i] = r;
     }
-    __syncthreads();
+    tsync();
     if (S.prof) _sc = __builtin_amdgcn_s_memtime();
     order_port(na, t_, s_, k_, i_, o_, ln);
     if (S.prof) _sd = __builtin_amdgcn_s_memtime();
@@ -1426,7 +1524,7 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
     HTree tr{gq, gnd, 1, P.np.analytical != 0};
     if (wave) {
       img_in(sl.pimg, gq, gnd, P.np.max_size, ln);
-      __syncthreads();
+      tsync();
       tr.q = reinterpret_cast<HQueue*>(sl.pimg); tr.nd = reinterpret_cast<HNode*>(sl.pimg + sizeof(HQueue));
     }
     RegQueue rq;
@@ -1472,14 +1570,14 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
       }
     }
     if (regq) rq.store(gq, gnd);
-    if (wave) { __syncthreads(); img_out(gq, gnd, sl.pimg, P.np.max_size, ln); }
+    if (wave) { tsync(); img_out(gq, gnd, sl.pimg, P.np.max_size, ln); }
     rn = wave_sum64(rn); rf = wave_sum64(rf); rb = wave_sum64(rb); rl = wave_sum64(rl); rc = wave_sum64(rc);
     // lanes 0-6: the SELF port (contention, router packets, buffer writes, switch, crossbar, link, buffer reads), 8-12: the receiver
     ncd = ln == 0 ? (P.np.qm ? cq : 0ull) : ln == 1 ? (P.np.qm ? (uint64_t)na : 0ull) : ln == 3 ? (uint64_t)na
         : (ln == 2 || ln == 4 || ln == 5 || ln == 6) ? cf : ln == 8 ? rn : ln == 9 ? rf : ln == 10 ? rb
         : ln == 11 ? rl : ln == 12 ? rc : 0ull;
-    narv(S, p)[lt] = 0;
-    __syncthreads();
+    hk.clear_arv(p, lt);
+    tsync();
   }
 
   PROF_AT(_p1);
@@ -1490,10 +1588,9 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
     atomicAdd(&S.prof[96], 1ull);
   }
   if (S.prof && ln == 0 && !na) { atomicAdd(&S.prof[97], (unsigned long long)(_sa - _p0)); atomicAdd(&S.prof[98], 1ull); }
-  const uint32_t ni = p ? pre.ninb1 : pre.ninb0;
   const uint32_t n = ni + na;
   // directory request FIFO in LDS when it cannot outgrow it this step
-  if (T.nrq + 2 * n + 2 <= kRqLds) {
+  if (T.nrq + 2 * n + 2 <= SL::kRq) {
     const CReq* g = S.rq + (size_t)lt * P.QC;
     for (uint32_t i = ln; i < T.nrq; i += 64) sl.rq[i] = g[i];
     T.rqp = sl.rq; T.rq_lds = true;
@@ -1503,9 +1600,9 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
     T.dq = reinterpret_cast<HQueue*>(sl.dimg); T.dnd = reinterpret_cast<HNode*>(sl.dimg + sizeof(HQueue));
     T.dq_lds = true;
   }
-  __syncthreads();
+  tsync();
   if (n) {
-    const bool lds = n <= kInLds;
+    const bool lds = n <= SL::kIn;
     uint64_t* a_ = lds ? sl.x1 : gscr; uint64_t* k_ = lds ? sl.x2 : gscr + P.IC; uint64_t* m_ = lds ? sl.x3 : gscr + 2 * P.IC;
     uint32_t* i_ = lds ? sl.i1 : (uint32_t*)(gscr + 3 * P.IC); uint32_t* o_ = lds ? sl.i2 : (uint32_t*)(gscr + 4 * P.IC);
     const uint32_t* il = inb(S, p) + (size_t)lt * P.IC;
@@ -1515,8 +1612,8 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
       const gg_cmsg& m = prev[r];
       a_[i] = m.arrival_ps; k_[i] = ((uint64_t)m.src << 32) | m.seq; i_[i] = r;
     }
-    __syncthreads();
-    ninb(S, p)[lt] = 0;
+    tsync();
+    hk.clear_inb(p, lt);
     order_inbox(n, a_, k_, m_, i_, o_, ln);
     PROF_AT(_p1b);
     if (S.prof && ln == 0) atomicAdd(&S.prof[9], (unsigned long long)(_p1b - _p1));
@@ -1574,12 +1671,12 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
   PROF_AT(_p3);
   // ---- 3. publish this step's records
   if (T.nch) sl.ch[2 * (T.nch - 1) + 1] = T.cused;
-  __syncthreads();
+  tsync();
   gg_cmsg* cur = pool(S, p);
   const uint32_t np_ = T.nsent;
   uint64_t ri_net = 0, ri_self = 0, ri_bnd = 0;
   if (np_) {
-    const bool lds = np_ <= kInLds;
+    const bool lds = np_ <= SL::kIn;
     uint64_t* t_ = lds ? sl.x1 : gscr; uint64_t* s_ = lds ? sl.x2 : gscr + P.IC; uint64_t* k_ = lds ? sl.x3 : gscr + 2 * P.IC;
     uint32_t* i_ = lds ? sl.i1 : (uint32_t*)(gscr + 3 * P.IC); uint32_t* o_ = lds ? sl.i2 : (uint32_t*)(gscr + 4 * P.IC);
     if (!lds && np_ > P.IC) T.fail(GG_DERR_CAP);
@@ -1590,7 +1687,7 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
       for (uint32_t r = ln; r < u; r += 64) i_[off + r] = b + r;
       off += u;
     }
-    __syncthreads();
+    tsync();
     const uint32_t nloc = T.failed ? 0u : off;
     if (P.net != GG_NET_EMESH_HOP_BY_HOP) {
       // NetworkModel::routePacket closed form (hop counter / magic) + delivery
@@ -1604,14 +1701,12 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
         if (m.src == m.dst) ri_self++; else ri_net++;
         if (S.shard[m.src] == S.shard[m.dst]) {
           const int32_t ld = S.ltile[m.dst];
-          const uint32_t j = atomicAdd(&ninb(S, p ^ 1u)[ld], 1u);
-          if (j >= P.IC) { atomicOr(S.err, GG_DERR_CAP); continue; }
+          const uint32_t j = hk.inbox_slot(p ^ 1u, (uint32_t)ld);
+          if (j == ~0u) { atomicOr(S.err, GG_DERR_CAP); continue; }
           cur[r].arrival_ps = m.arrival_ps; cur[r].zero_load_ps = zl;
           inb(S, p ^ 1u)[(size_t)ld * P.IC + j] = r;
         } else {
-          const uint32_t j = atomicAdd(S.bnd_cnt, 1u);
-          if (j >= P.msg_cap) { atomicOr(S.err, GG_DERR_CAP); continue; }
-          S.bnd[j] = m;
+          if (!hk.bnd_put(m)) { atomicOr(S.err, GG_DERR_CAP); continue; }
           ri_bnd++;
         }
       }
@@ -1624,8 +1719,8 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
         uint32_t r = 0;
         if (i < nloc) { r = i_[i]; self = cur[r].dst == T.tile; net = !self; }
         if (self) {
-          const uint32_t j = atomicAdd(&ninb(S, p ^ 1u)[lt], 1u);
-          if (j >= P.IC) atomicOr(S.err, GG_DERR_CAP);
+          const uint32_t j = hk.inbox_slot(p ^ 1u, lt);
+          if (j == ~0u) atomicOr(S.err, GG_DERR_CAP);
           else inb(S, p ^ 1u)[(size_t)lt * P.IC + j] = r;
           ri_self++;
         }
@@ -1638,11 +1733,11 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
         }
         nn += (uint32_t)__builtin_popcountll(m);
       }
-      __syncthreads();
+      tsync();
       if (nn) {
         // the injection port (routePacket SEND_TILE, hop_by_hop.cc:151-159) in (time, key) order
         for (uint32_t i = ln; i < nn; i += 64) i_[i] = o_[i];
-        __syncthreads();
+        tsync();
         order_port(nn, t_, s_, k_, i_, o_, ln);
         const uint64_t qi = (uint64_t)T.tile * 6 + P_INJ;
         HQueue* gq = S.nq + qi;
@@ -1652,7 +1747,7 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
         HTree tr{gq, gnd, 1, P.np.analytical != 0};
         if (wave) {
           img_in(sl.pimg, gq, gnd, P.np.max_size, ln);
-          __syncthreads();
+          tsync();
           tr.q = reinterpret_cast<HQueue*>(sl.pimg); tr.nd = reinterpret_cast<HNode*>(sl.pimg + sizeof(HQueue));
         }
         RegQueue rq;
@@ -1692,21 +1787,20 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
           }
         }
         if (regq) rq.store(gq, gnd);
-        if (wave) { __syncthreads(); img_out(gq, gnd, sl.pimg, P.np.max_size, ln); }
+        if (wave) { tsync(); img_out(gq, gnd, sl.pimg, P.np.max_size, ln); }
         ps = wave_sum64(ps); fs = wave_sum64(fs); bs = wave_sum64(bs);
         if (ln == 0) {
           cadd(S.ctr, T.tile, GG_NC_PACKETS_SENT, ps); cadd(S.ctr, T.tile, GG_NC_FLITS_SENT, fs);
           cadd(S.ctr, T.tile, GG_NC_BITS_SENT, bs);
         }
-        __syncthreads();
+        tsync();
         // onto the X (or Y) segment the packet enters
         for (uint32_t i = ln; i < nn; i += 64) {
           const uint32_t r = o_[i];
           bool is_x;
           const uint32_t sg = xy_stage_seg(P, S, T.tile, cur[r].dst, is_x);
-          uint32_t* cnt = is_x ? S.nxl : S.nyl;
-          const uint32_t j = atomicAdd(&cnt[sg], 1u);
-          if (j >= P.seg_cap) { atomicOr(S.err, GG_DERR_CAP); continue; }
+          const uint32_t j = hk.seg_slot(is_x, sg);
+          if (j == ~0u) { atomicOr(S.err, GG_DERR_CAP); continue; }
           (is_x ? S.xl : S.yl)[(size_t)sg * P.seg_cap + j] = r;
         }
       }
@@ -1735,12 +1829,7 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
   }
   {
     const uint32_t a = wave_sum((uint32_t)ri_net), b = wave_sum((uint32_t)ri_self), c = wave_sum((uint32_t)ri_bnd);
-    if (ln == 0) {
-      if (a) atomicAdd((unsigned long long*)&S.ri[GG_RI_NET_MSGS], (unsigned long long)a);
-      if (b) atomicAdd((unsigned long long*)&S.ri[GG_RI_SELF_MSGS], (unsigned long long)b);
-      if (c) atomicAdd((unsigned long long*)&S.ri[GG_RI_BOUNDARY_MSGS], (unsigned long long)c);
-      if (np_) atomicAdd(&S.ring[k & 3], np_);
-    }
+    if (ln == 0) hk.step_counts(k, a, b, c, np_);
   }
   if (S.prof && ln == 0) {
     const uint64_t e = __builtin_amdgcn_s_memtime();
@@ -1761,6 +1850,10 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
       atomicMax(&S.prof[b + 3], (unsigned long long)(tot | c24(_p3 - _p2)));
     }
   }
+  // the tile's next start for the shard scheduler: finished, blocked, or clock + gap
+  if (T.rec >= T.rec_end) return kNsFin;
+  if (T.blocked) return kNsBlk;
+  return T.clk + (uint64_t)((S.meta[T.rec] & 0x7FFFFFFFu) >> 1) * P.gap_ps;
 }
 
 __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t L, uint32_t devloop, uint64_t barrier_arg)
@@ -2355,6 +2448,487 @@ __global__ void k_c_export_scatter(CS S, const gg_cmsg* b, uint32_t n, const uin
   out[base[k] + atomicAdd(&cursor[k], 1u)] = b[i];
 }
 
+// ---------------------------------------------------------------------------
+// k_c_shard: the device-driven run with ONE WORKGROUP PER LOGICAL SHARD.
+// Within a quantum a logical shard evolves on its own: every message or packet
+// that leaves it is held to the quantum boundary.  So each
+// shard runs its own step loop — the tiles with work (an LDS worklist: the
+// tiles that got deliveries, and at step 0 every tile with a record before
+// the barrier), one tile per wave; then its X and Y segments, one segment per
+// wave; workgroup barriers between the phases — and its quantum ends after
+// its first step that sends nothing (a shard that sent nothing stays idle to
+// the end of the quantum, so the quantum's global step count is its busiest
+// shard's).  The counters the per-step launches keep in HBM (inbox / arrival /
+// segment counts, record pools, boundary records) live in the workgroup's
+// LDS; tile, directory and queue state stays in HBM, read back by the CU that
+// wrote it (its L1 and XCD L2, no kernel-boundary write-back / invalidate).
+// At the quantum boundary the shards meet in a grid barrier (agent-scope
+// release / acquire, grid_sync), import the records held for them and pick
+// the next quantum by quantum_end's rule.  Every queue, directory and cache
+// sees the same requests in the same order as under the per-step launches:
+// bit-identical results.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kShardWaves = 4, kShardThreads = 64 * kShardWaves;   // 1 wave per SIMD: the tile step needs ~500 registers
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+constexpr uint32_t kShardMaxSteps = 1u << 20;        // longer quanta are reported (GG_DERR_STATE)
+constexpr uint32_t kShardSlot = 8;                   // u64 words of a shard's quantum-end slot
+
+struct ShardHdr {
+  uint32_t npool[2];                 // records allocated in this shard's region of pool 0 / 1
+  uint32_t nbnd;                     // records held in this shard's boundary region this quantum
+  uint32_t sent[2];                  // records sent in the step of parity 0 / 1
+  uint32_t nwl[2];                   // tiles listed for the step of parity 0 / 1
+  uint32_t ht, hx, hy;               // work cursors of the tile / X / Y phase
+  uint32_t nxw, nyw;                 // X / Y segments with packets this step
+  uint32_t imp_held;                 // held packets imported for step 0
+  uint32_t pad;
+  unsigned long long ri_net, ri_self, ri_bnd;
+  unsigned long long act, blk, mn;   // quantum-end statistics of the shard
+};
+
+struct ShardArr {                    // the shard's LDS arrays (sizes from CP)
+  ShardHdr* h;
+  uint64_t* nst;                         // [nt] next start (kNsFin / kNsBlk)
+  uint32_t *ninb, *narv, *listed, *wl;   // [2][nt]
+  uint32_t *nsx, *xwl, *nsy, *ywl;       // [nxs], [nxs], [nys], [nys]
+};
+
+__device__ __forceinline__ ShardArr shard_arr(const CP& P, uint8_t* smem)
+{
+  ShardArr A;
+  uint8_t* b = smem + P.sh_arr;
+  A.h = reinterpret_cast<ShardHdr*>(b); b += (sizeof(ShardHdr) + 15) & ~(size_t)15;
+  A.nst = reinterpret_cast<uint64_t*>(b); b += 8 * (size_t)P.sh_nt;
+  A.ninb = reinterpret_cast<uint32_t*>(b); b += 8 * (size_t)P.sh_nt;
+  A.narv = reinterpret_cast<uint32_t*>(b); b += 8 * (size_t)P.sh_nt;
+  A.listed = reinterpret_cast<uint32_t*>(b); b += 8 * (size_t)P.sh_nt;
+  A.wl = reinterpret_cast<uint32_t*>(b); b += 8 * (size_t)P.sh_nt;
+  A.nsx = reinterpret_cast<uint32_t*>(b); b += 4 * (size_t)P.sh_nxs;
+  A.xwl = reinterpret_cast<uint32_t*>(b); b += 4 * (size_t)P.sh_nxs;
+  A.nsy = reinterpret_cast<uint32_t*>(b); b += 4 * (size_t)P.sh_nys;
+  A.ywl = reinterpret_cast<uint32_t*>(b);
+  return A;
+}
+// bytes of the shard arrays after P.sh_arr (host and device)
+__host__ __device__ inline size_t shard_arr_bytes(uint32_t nt, uint32_t nxs, uint32_t nys)
+{
+  return ((sizeof(ShardHdr) + 15) & ~(size_t)15) + 40 * (size_t)nt + 8 * (size_t)nxs + 8 * (size_t)nys;
+}
+
+// the deliveries of a shard workgroup: LDS counters, a tile is listed for the
+// step that reads its first delivery, a segment for the walk its first packet enters
+struct ShardHooks {
+  const CP& P; const CS& S; const ShardArr& A;
+  uint32_t pbase;                    // this shard's first record in pool 0 / 1
+  gg_cmsg* bnd;                      // this shard's boundary region of the quantum
+  __device__ __forceinline__ uint32_t pool_alloc(uint32_t p, uint32_t want) const
+  {
+    uint32_t b = 0;
+    if (lane_id() == 0) b = atomicAdd(&A.h->npool[p], want);
+    b = (uint32_t)__shfl((int)b, 0);
+    return (uint64_t)b + want > P.sh_pcap ? ~0u : pbase + b;
+  }
+  __device__ __forceinline__ void list_tile(uint32_t pn, uint32_t si, uint32_t ld) const
+  {
+    if (atomicOr(&A.listed[pn * P.sh_nt + si], 1u) == 0) A.wl[pn * P.sh_nt + atomicAdd(&A.h->nwl[pn], 1u)] = ld;
+  }
+  __device__ __forceinline__ uint32_t inbox_slot(uint32_t pn, uint32_t ld) const
+  {
+    const uint32_t si = S.tsi[ld];
+    const uint32_t j = atomicAdd(&A.ninb[pn * P.sh_nt + si], 1u);
+    if (j == 0) list_tile(pn, si, ld);
+    return j < P.IC ? j : ~0u;
+  }
+  __device__ __forceinline__ uint32_t arv_slot(uint32_t pn, uint32_t ld) const
+  {
+    const uint32_t si = S.tsi[ld];
+    const uint32_t j = atomicAdd(&A.narv[pn * P.sh_nt + si], 1u);
+    if (j == 0) list_tile(pn, si, ld);
+    return j < P.IC ? j : ~0u;
+  }
+  __device__ __forceinline__ uint32_t seg_slot(bool is_x, uint32_t sg) const
+  {
+    const uint32_t loc = S.seg_loc[(is_x ? 0u : 1u) * P.sh_segw + sg];
+    const uint32_t j = atomicAdd(&(is_x ? A.nsx : A.nsy)[loc], 1u);
+    if (j == 0) {
+      if (is_x) A.xwl[atomicAdd(&A.h->nxw, 1u)] = sg;
+      else A.ywl[atomicAdd(&A.h->nyw, 1u)] = sg;
+    }
+    return j < P.seg_cap ? j : ~0u;
+  }
+  __device__ __forceinline__ bool bnd_put(const gg_cmsg& m) const
+  {
+    const uint32_t j = atomicAdd(&A.h->nbnd, 1u);
+    if (j >= P.sh_bcap) return false;
+    bnd[j] = m;
+    return true;
+  }
+  __device__ __forceinline__ void clear_arv(uint32_t p, uint32_t lt) const { A.narv[p * P.sh_nt + S.tsi[lt]] = 0; }
+  __device__ __forceinline__ void clear_inb(uint32_t p, uint32_t lt) const { A.ninb[p * P.sh_nt + S.tsi[lt]] = 0; }
+  __device__ __forceinline__ void step_counts(uint32_t k, uint32_t net, uint32_t self, uint32_t nb, uint32_t sent) const
+  {
+    if (net) atomicAdd(&A.h->ri_net, (unsigned long long)net);
+    if (self) atomicAdd(&A.h->ri_self, (unsigned long long)self);
+    if (nb) atomicAdd(&A.h->ri_bnd, (unsigned long long)nb);
+    if (sent) atomicAdd(&A.h->sent[k & 1u], sent);
+  }
+};
+
+// One segment (stage 0: X, 1: Y) walked by the calling wave: the positions
+// swept in the direction of travel, each position's batch in (time, rank)
+// order through the port's queue (RegQueue loaded from HBM for the history
+// tree, HTree on HBM for the other models) — walk_body<false>'s sweep.  pk:
+// the packet arrays (cap packets; LDS, or the wave's HBM scratch for long
+// lists), lc: [npos][kNetCtr] router / link counters.
+template <class H>
+__device__ __forceinline__ void walk_sweep_wave(const CP& P, const CS& S, const H& hk, uint32_t p, int stage,
+                                                uint32_t sg, uint32_t n, uint8_t* pk, uint32_t cap, uint64_t* lc)
+{
+  const uint32_t ln = lane_id();
+  const uint32_t* list = (stage == 0 ? S.xl : S.yl) + (size_t)sg * P.seg_cap;
+  const Seg sd = (stage == 0 ? S.segx : S.segy)[sg >> 1];
+  const uint32_t dir = sg & 1u;
+  const int port = stage == 0 ? (dir ? P_RIGHT : P_LEFT) : (dir ? P_UP : P_DOWN);
+  auto tile_at = [&](uint32_t pos) -> uint32_t { return stage == 0 ? sd.line * P.mw + pos : pos * P.mw + sd.line; };
+  auto pos_of = [&](uint32_t tile) -> uint32_t { return stage == 0 ? tile % P.mw : tile / P.mw; };
+  gg_cmsg* cur = pool(S, p);
+  const uint32_t npos = sd.hi - sd.lo + 1;
+  WalkLds W;
+  W.Pt = reinterpret_cast<uint64_t*>(pk);
+  W.Ph = W.Pt + cap; W.Pk = W.Ph + cap; W.Pz = W.Pk + cap;
+  W.Pi = reinterpret_cast<uint32_t*>(W.Pz + cap);
+  W.Pp = W.Pi + cap; W.Pd = W.Pp + cap; W.Pf = W.Pd + cap; W.Pr = W.Pf + cap;
+  W.Qt = reinterpret_cast<uint64_t*>(W.Pr + cap);                  // cap is even: 8-byte aligned
+  W.Qr = reinterpret_cast<uint32_t*>(W.Qt + cap); W.Qs = W.Qr + cap;
+  uint32_t lo = ~0u, hi = 0;
+  for (uint32_t i = ln; i < n; i += 64) {
+    const uint32_t r = list[i];
+    const gg_cmsg& m = cur[r];
+    const uint32_t a = pos_of(m.hop), z = pos_of(m.dst);
+    W.Pt[i] = m.arrival_ps; W.Ph[i] = m.send_ps; W.Pk[i] = ((uint64_t)m.src << 32) | m.seq; W.Pz[i] = m.zero_load_ps;
+    W.Pi[i] = r; W.Pp[i] = a; W.Pd[i] = z;
+    if (m.arrival_ps >> 51) atomicOr(S.err, GG_DERR_CAP);        // batch keys are time << 12 | rank
+    W.Pf[i] = (uint32_t)nflits(P.np, has_data(m.type) ? P.bits_data : P.bits_req);
+    const uint32_t zz = dir ? min(z - 1, sd.hi) : max(z + 1, sd.lo);
+    lo = min(lo, min(a, zz)); hi = max(hi, max(a, zz));
+  }
+  for (uint32_t i = ln; i < npos * kNetCtr; i += 64) lc[i] = 0;
+  lo = wave_min(lo);
+  hi = (uint32_t)(~wave_min(~hi));
+  tsync();
+  // canonical ranks (by send time, sender, seq)
+  for (uint32_t i = ln; i < n; i += 64) {
+    const uint64_t hi_ = W.Ph[i], ki = W.Pk[i];
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < n; ++j) { const uint64_t hj = W.Ph[j]; r += hj < hi_ || (hj == hi_ && W.Pk[j] < ki); }
+    W.Pr[i] = r;
+  }
+  tsync();
+  const bool qm = P.np.qm != 0;
+  const bool regq = qm && P.np.qtype == GG_QM_HISTORY_TREE && P.np.max_size <= kQMax;
+  const uint64_t zps = lat_to_ps((uint64_t)P.np.router_delay + P.np.link_delay, P.np.f);
+  uint64_t* K = W.Qt; uint32_t* B = W.Qr; uint32_t* O = W.Qs;
+  for (uint32_t s_ = 0; lo <= hi && s_ <= hi - lo; ++s_) {
+    const uint32_t pos = dir ? lo + s_ : hi - s_;
+    uint32_t m = 0;
+    for (uint32_t b0 = 0; b0 < n; b0 += 64) {
+      const uint32_t i = b0 + ln;
+      const bool at = i < n && W.Pp[i] == pos && (W.Pf[i] >> 24) == 0;
+      const uint64_t bm = __ballot(at);
+      if (at) {
+        const uint32_t k = m + (uint32_t)__builtin_popcountll(bm & ((1ull << ln) - 1));
+        B[k] = i; K[k] = (W.Pt[i] << 12) | W.Pr[i];
+      }
+      m += (uint32_t)__builtin_popcountll(bm);
+    }
+    if (m == 0) continue;
+    tsync();
+    for (uint32_t k = ln; k < m; k += 64) {
+      const uint64_t kk = K[k];
+      uint32_t r = 0;
+      for (uint32_t j = 0; j < m; ++j) r += K[j] < kk;
+      O[r] = B[k];
+    }
+    tsync();
+    const uint64_t qi = (uint64_t)tile_at(pos) * 6 + port;
+    HTree tr{S.nq + qi, S.nnd + qi * P.np.max_size, 1, P.np.analytical != 0};
+    RegQueue rq;
+    if (regq) rq.load(tr.q, tr.nd, 1, P.np.analytical != 0, ln);
+    auto request = [&](uint64_t t, uint32_t nf) -> uint64_t {
+      if (!qm) return 0;
+      const uint64_t tc = time_to_cycles(t, P.np.f);
+      return regq ? rq.request<false>(tc, nf, S.err) : tr.delay(tc, nf, S.err);
+    };
+    const uint32_t nx = dir ? pos + 1 : pos - 1;
+    uint64_t cq = 0, cf = 0;
+    for (uint32_t k = 0; k < m; ++k) {
+      const uint32_t i = O[k];
+      cq += serve_packet(P, S, W, request, i, nx, sd, zps, cf);
+      if (ln == 0) W.Pp[i] = nx;
+      tsync();
+    }
+    if (regq) rq.store(tr.q, tr.nd);
+    if (ln == 0) {
+      uint64_t* l = lc + (size_t)(pos - sd.lo) * kNetCtr;
+      l[0] += qm ? cq : 0; l[1] += qm ? m : 0; l[2] += cf; l[3] += m; l[4] += cf; l[5] += cf;
+    }
+    tsync();
+  }
+  // hand-off
+  uint32_t nb = 0;
+  for (uint32_t i = ln; i < n; i += 64) {
+    const uint32_t r = W.Pi[i], stt = W.Pf[i] >> 24;
+    const uint32_t h = tile_at(W.Pp[i]);
+    gg_cmsg* m = cur + r;
+    const uint64_t z = W.Pz[i];
+    m->arrival_ps = W.Pt[i]; m->zero_load_ps = z; m->hop = h;
+    if (stt == 2) {                                            // held for the quantum boundary
+      gg_cmsg g = *m;
+      g.arrival_ps = W.Pt[i]; g.zero_load_ps = z; g.hop = h;
+      if (!hk.bnd_put(g)) { atomicOr(S.err, GG_DERR_CAP); continue; }
+      ++nb;
+      continue;
+    }
+    const uint32_t dst = m->dst;
+    if (h == dst) {                                            // the SELF port of the destination, next step
+      const int32_t ld = S.ltile[dst];
+      const uint32_t j = hk.arv_slot(p ^ 1u, (uint32_t)ld);
+      if (j == ~0u) { atomicOr(S.err, GG_DERR_CAP); continue; }
+      arv(S, p ^ 1u)[(size_t)ld * P.IC + j] = r;
+    } else {                                                   // X done: the Y segment of the destination column
+      bool is_x;
+      const uint32_t s2 = xy_stage_seg(P, S, h, dst, is_x);
+      const uint32_t j = hk.seg_slot(false, s2);
+      if (j == ~0u) { atomicOr(S.err, GG_DERR_CAP); continue; }
+      S.yl[(size_t)s2 * P.seg_cap + j] = r;
+    }
+  }
+  nb = wave_sum(nb);
+  if (ln == 0 && nb) hk.step_counts(0, 0, 0, nb, 0);
+  for (uint32_t i = ln; i < npos * 6u; i += 64) {
+    const uint32_t q = i / 6, f = i % 6;
+    const uint64_t* l = lc + (size_t)q * kNetCtr;
+    const uint32_t tl = tile_at(sd.lo + q);
+    switch (f) {
+    case 0: cadd(S.ctr, tl, GG_NC_ROUTER_CONTENTION_CYCLES, l[0]); break;
+    case 1: cadd(S.ctr, tl, GG_NC_ROUTER_PACKETS, l[1]); break;
+    case 2: cadd(S.ctr, tl, GG_NC_BUFFER_WRITES, l[2]); cadd(S.ctr, tl, GG_NC_BUFFER_READS, l[2]); break;
+    case 3: cadd(S.ctr, tl, GG_NC_SWITCH_ALLOC, l[3]); break;
+    case 4: cadd(S.ctr, tl, GG_NC_CROSSBAR, l[4]); break;
+    default: cadd(S.ctr, tl, GG_NC_LINK_TRAVERSALS, l[5]); break;
+    }
+  }
+  tsync();
+}
+
+// a record of the quantum boundary held for this shard (import_one with the
+// shard's LDS counters): a message into the inbox of step 0 (pool 1), a held
+// packet into step 0's walk (pool 0) or the destination's SELF list of step 1
+__device__ __forceinline__ void shard_import(const CP& P, const CS& S, const ShardHooks& hk, const gg_cmsg& m)
+{
+  const uint32_t at = m.hop == GG_HOP_NONE ? m.dst : m.hop;
+  if (at >= P.T || m.dst >= P.T || S.ltile[at] < 0) { atomicOr(S.err, GG_DERR_STATE); return; }
+  if (m.hop == GG_HOP_NONE) {
+    const uint32_t r = atomicAdd(&hk.A.h->npool[1], 1u);
+    if (r >= P.sh_pcap) { atomicOr(S.err, GG_DERR_CAP); return; }
+    S.pool1[hk.pbase + r] = m;
+    const int32_t ld = S.ltile[m.dst];
+    const uint32_t j = hk.inbox_slot(0, (uint32_t)ld);
+    if (j == ~0u) { atomicOr(S.err, GG_DERR_CAP); return; }
+    S.inb0[(size_t)ld * P.IC + j] = hk.pbase + r;
+    return;
+  }
+  const uint32_t r = atomicAdd(&hk.A.h->npool[0], 1u);
+  if (r >= P.sh_pcap) { atomicOr(S.err, GG_DERR_CAP); return; }
+  S.pool0[hk.pbase + r] = m;
+  atomicAdd(&hk.A.h->imp_held, 1u);
+  if (m.hop == m.dst) {
+    const int32_t ld = S.ltile[m.dst];
+    const uint32_t j = hk.arv_slot(1, (uint32_t)ld);
+    if (j == ~0u) { atomicOr(S.err, GG_DERR_CAP); return; }
+    S.arv1[(size_t)ld * P.IC + j] = hk.pbase + r;
+    return;
+  }
+  bool is_x;
+  const uint32_t sg = xy_stage_seg(P, S, m.hop, m.dst, is_x);
+  const uint32_t j = hk.seg_slot(is_x, sg);
+  if (j == ~0u) { atomicOr(S.err, GG_DERR_CAP); return; }
+  (is_x ? S.xl : S.yl)[(size_t)sg * P.seg_cap + j] = hk.pbase + r;
+}
+
+template <bool HR>
+__global__ void __launch_bounds__(kShardThreads) k_c_shard(CP P, CS S, uint64_t tlimit)
+{
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t s = blockIdx.x, ns = gridDim.x, tid = threadIdx.x, ln = tid & 63, wv = tid >> 6;
+  const ShardArr A = shard_arr(P, smem);
+  ShardHdr* h = A.h;
+  const uint32_t t0 = S.sh_toff[s], nt = S.sh_toff[s + 1] - t0;
+  const bool hbh = P.net == GG_NET_EMESH_HOP_BY_HOP;
+  uint8_t* area = smem + (size_t)wv * P.sh_wave;
+  StepLdsS& sl = *reinterpret_cast<StepLdsS*>(area);
+  uint8_t* garea = S.wscr + ((size_t)s * kShardWaves + wv) * P.sh_gbytes;
+  const uint64_t qps = S.qs[QS_QPS];
+  const uint64_t t_begin = __builtin_amdgcn_s_memrealtime();
+  if (tid < sizeof(ShardHdr) / 4) reinterpret_cast<uint32_t*>(h)[tid] = 0;
+  for (uint32_t i = tid; i < 2 * P.sh_nt; i += kShardThreads) { A.ninb[i] = 0; A.narv[i] = 0; A.listed[i] = 0; }
+  for (uint32_t i = tid; i < P.sh_nxs; i += kShardThreads) A.nsx[i] = 0;
+  for (uint32_t i = tid; i < P.sh_nys; i += kShardThreads) A.nsy[i] = 0;
+  for (uint32_t i = tid; i < nt; i += kShardThreads) {
+    const uint32_t lt = S.sh_tiles[t0 + i];
+    const uint64_t r = S.rec[lt];
+    A.nst[i] = r >= S.rec_end[lt] ? kNsFin : S.blocked[lt] ? kNsBlk
+             : S.clk[lt] + (uint64_t)((S.meta[r] & 0x7FFFFFFFu) >> 1) * P.gap_ps;
+  }
+  __syncthreads();
+  uint64_t q = 0, Q = 0, done = 0;
+  uint32_t gen = 0;
+  const uint32_t wcap = (P.sh_wave - kNetCtr * 8 * P.sh_segmax) / kWalkPkBytes & ~1u;   // packets in a wave's LDS area
+  for (;;) {
+    const uint64_t barrier = (q + 1) * qps;
+    const ShardHooks hk{P, S, A, s * P.sh_pcap, S.sbnd + ((size_t)(Q & 1) * ns + s) * P.sh_bcap};
+    uint32_t k = 0;
+    for (;; ++k) {
+      const uint32_t p = k & 1u;
+      if (k == 0)      // step 0: every tile with a record before the barrier (imports listed theirs)
+        for (uint32_t i = tid; i < nt; i += kShardThreads)
+          if (A.nst[i] < barrier) hk.list_tile(0, i, S.sh_tiles[t0 + i]);
+      if (tid == 0) {
+        h->npool[p ^ 1u] = 0; h->sent[p] = 0; h->ht = 0;
+        if (k > 0) h->nwl[p ^ 1u] = 0;                       // the previous step's list, consumed
+      }
+      __syncthreads();
+      const uint64_t c0 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
+      // ---- tiles: one per wave
+      const uint32_t nw = rfl(h->nwl[p]);
+      for (;;) {
+        uint32_t i = 0;
+        if (ln == 0) i = atomicAdd(&h->ht, 1u);
+        i = rfl((uint32_t)__shfl((int)i, 0));
+        if (i >= nw) break;
+        // wave-uniform values in scalar registers: every address of the tile step derives from them
+        const uint32_t lt = rfl(A.wl[p * P.sh_nt + i]);
+        const uint32_t si = rfl(S.tsi[lt]);
+        const uint32_t na = hbh ? rfl(A.narv[p * P.sh_nt + si]) : 0u, ni = rfl(A.ninb[p * P.sh_nt + si]);
+        if (ln == 0) A.listed[p * P.sh_nt + si] = 0;
+        TilePre pre;
+        pre.load(S, lt, ln);
+        TraceWin W{~0ull, 0, 0};
+        const uint64_t nx = tile_step<false, HR>(P, S, lt, k, k, barrier, W, sl, nullptr, pre, hk, na, ni);
+        if (ln == 0) A.nst[si] = nx;
+        tsync();
+      }
+      __syncthreads();
+      const uint64_t c1 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
+      if (S.prof && tid == 0) {
+        unsigned long long* pr = S.prof + 200 + 16 * s;
+        pr[0] += c1 - c0; pr[1] += nw; pr[2] += 1;
+      }
+      // ---- walks: one segment per wave, X then Y
+      if (hbh) {
+        for (int stage = 0; stage < 2; ++stage) {
+          const uint32_t nsg = rfl(stage == 0 ? h->nxw : h->nyw);
+          uint32_t* cursor = stage == 0 ? &h->hx : &h->hy;
+          for (;;) {
+            uint32_t i = 0;
+            if (ln == 0) i = atomicAdd(cursor, 1u);
+            i = rfl((uint32_t)__shfl((int)i, 0));
+            if (i >= nsg) break;
+            const uint32_t sg = rfl((stage == 0 ? A.xwl : A.ywl)[i]);
+            uint32_t* cnt = (stage == 0 ? A.nsx : A.nsy) + rfl(S.seg_loc[(uint32_t)stage * P.sh_segw + sg]);
+            const uint32_t n = min(rfl(*cnt), P.seg_cap);
+            uint64_t* lc = reinterpret_cast<uint64_t*>(area);
+            if (n <= wcap) {
+              walk_sweep_wave(P, S, hk, p, stage, sg, n, area + (size_t)kNetCtr * 8 * P.sh_segmax, wcap, lc);
+            } else if (n <= P.sh_gpk) {
+              walk_sweep_wave(P, S, hk, p, stage, sg, n, garea, P.sh_gpk, lc);
+            } else if (ln == 0) {
+              atomicOr(S.err, GG_DERR_CAP);
+            }
+            if (ln == 0) *cnt = 0;
+            tsync();
+          }
+          __syncthreads();
+        }
+        // the walk lists are empty again (imports at the quantum boundary fill step 0's)
+        if (tid == 0) { h->hx = 0; h->hy = 0; h->nxw = 0; h->nyw = 0; }
+      }
+      if (S.prof && tid == 0) {
+        unsigned long long* pr = S.prof + 200 + 16 * s;
+        pr[3] += __builtin_amdgcn_s_memtime() - c1;
+      }
+      const uint32_t sent = h->sent[p] + (k == 0 ? h->imp_held : 0u);
+      if (sent == 0) break;
+      if (k + 1 >= kShardMaxSteps) { if (tid == 0) atomicOr(S.err, GG_DERR_STATE); break; }
+    }
+    // ---- quantum end: this shard's statistics into its slot, then the grid barrier
+    const uint64_t c2 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
+    {
+      unsigned long long act = 0, blk = 0, mn = ~0ull;
+      for (uint32_t i = tid; i < nt; i += kShardThreads) {
+        const uint64_t v = A.nst[i];
+        if (v != kNsFin) { ++act; if (v == kNsBlk) ++blk; else mn = v < mn ? v : mn; }
+      }
+      act = wave_sum64(act); blk = wave_sum64(blk); mn = wave_min64(mn);
+      if (tid == 0) { h->act = 0; h->blk = 0; h->mn = ~0ull; }
+      __syncthreads();
+      if (ln == 0) { atomicAdd(&h->act, act); atomicAdd(&h->blk, blk); atomicMin(&h->mn, mn); }
+      __syncthreads();
+      if (tid == 0) {
+        uint64_t* sl_ = S.sh_slot + ((size_t)(Q & 1) * ns + s) * kShardSlot;
+        sl_[0] = h->act; sl_[1] = h->blk; sl_[2] = h->mn; sl_[3] = h->nbnd; sl_[4] = k + 1;
+      }
+    }
+    grid_sync(S, gen);
+    const uint64_t c3 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
+    const uint32_t err = __hip_atomic_load(S.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t active = 0, blocked = 0, mn = ~0ull, nb = 0, steps = 0;
+    for (uint32_t j = 0; j < ns; ++j) {
+      const uint64_t* sl_ = S.sh_slot + ((size_t)(Q & 1) * ns + j) * kShardSlot;
+      active += sl_[0]; blocked += sl_[1]; mn = sl_[2] < mn ? sl_[2] : mn;
+      nb += min(sl_[3], (uint64_t)P.sh_bcap); steps = sl_[4] > steps ? sl_[4] : steps;
+    }
+    uint64_t nq = q + 1;
+    if (active == 0 && nb == 0) done = 1;
+    else if (nb == 0 && blocked == 0) nq = max(q + 1, mn / qps);
+    else if (nb == 0) done = 2;                                       // blocked, nothing in flight: deadlock
+    if (s == 0 && tid == 0) { S.ri[GG_RI_QUANTA]++; S.ri[GG_RI_FINAL_QUANTUM] = q; S.ri[GG_RI_STEPS] += steps; }
+    if (!done && (err || __builtin_amdgcn_s_memrealtime() - t_begin > tlimit)) {
+      if (s == 0 && tid == 0) atomicOr(S.err, err ? 0u : GG_DERR_STATE);
+      done = 3;
+    }
+    if (done) break;
+    // ---- import the records held for this shard into the next quantum
+    if (tid == 0) {
+      h->npool[0] = 0; h->npool[1] = 0; h->nwl[0] = 0; h->nwl[1] = 0; h->imp_held = 0; h->nbnd = 0;
+    }
+    __syncthreads();
+    for (uint32_t j = 0; j < ns; ++j) {
+      const uint64_t* sl_ = S.sh_slot + ((size_t)(Q & 1) * ns + j) * kShardSlot;
+      const uint32_t c = (uint32_t)min(sl_[3], (uint64_t)P.sh_bcap);
+      const gg_cmsg* reg = S.sbnd + ((size_t)(Q & 1) * ns + j) * P.sh_bcap;
+      for (uint32_t i = tid; i < c; i += kShardThreads) {
+        const gg_cmsg m = reg[i];
+        const uint32_t at = m.hop == GG_HOP_NONE ? m.dst : m.hop;
+        if (at < P.T && S.shard[at] - P.sh_k0 == s) shard_import(P, S, hk, m);
+      }
+    }
+    __syncthreads();
+    if (S.prof && tid == 0) {
+      unsigned long long* pr = S.prof + 200 + 16 * s;
+      pr[4] += c3 - c2; pr[5] += __builtin_amdgcn_s_memtime() - c3; pr[6] += 1;
+    }
+    ++Q;
+    q = nq;
+  }
+  if (tid == 0) {
+    if (h->ri_net) atomicAdd((unsigned long long*)&S.ri[GG_RI_NET_MSGS], h->ri_net);
+    if (h->ri_self) atomicAdd((unsigned long long*)&S.ri[GG_RI_SELF_MSGS], h->ri_self);
+    if (h->ri_bnd) atomicAdd((unsigned long long*)&S.ri[GG_RI_BOUNDARY_MSGS], h->ri_bnd);
+    if (s == 0) { S.qs[QS_DONE] = done; S.qs[QS_Q] = q; S.qs[QS_COUNT] = Q; }
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -2372,6 +2946,10 @@ struct gg_coh_state {
   uint32_t wtx = 64, wty = 64;          // threads of an X / Y walker workgroup
   bool persist_lc = false;
   bool begun = false;
+  // k_c_shard (one workgroup per owned logical shard): usable, dynamic LDS bytes
+  bool shard_ok = false;
+  size_t shard_lds = 0;
+  uint32_t shard_n = 0;
   // live kernel timing (gg_set_timing): an event pair around every
   // kTimeSample-th launch of each kernel (a pair around every launch costs
   // ~18 % of a hop-by-hop run), harvested at the batch syncs; since
@@ -2379,9 +2957,9 @@ struct gg_coh_state {
   std::vector<hipEvent_t> tev;
   std::vector<int> tkind;
   uint32_t tused = 0;
-  double ksum[4] = {0, 0, 0, 0};
-  uint64_t kcnt[4] = {0, 0, 0, 0};      // timed launches
-  uint64_t nlaunch[4] = {0, 0, 0, 0};   // all launches
+  double ksum[5] = {0, 0, 0, 0, 0};
+  uint64_t kcnt[5] = {0, 0, 0, 0, 0};      // timed launches
+  uint64_t nlaunch[5] = {0, 0, 0, 0, 0};   // all launches
 };
 constexpr uint64_t kTimeSample = 16;
 static void launch_walk(gg_coh_state* C, hipStream_t s, uint32_t blocks, uint32_t threads, uint32_t L, int stage)
@@ -2393,7 +2971,8 @@ static void launch_walk(gg_coh_state* C, hipStream_t s, uint32_t blocks, uint32_
 }
 constexpr uint32_t kPersistTiles = 64;        // owned tiles up to which gg_coherent_run uses k_c_persist
 constexpr uint32_t kPersistLaunches = 16384;  // launch indices per k_c_persist launch
-static const char* kKernelNames[4] = {"coherent_step", "coherent_walk_x", "coherent_walk_y", "coherent_persist"};
+static const char* kKernelNames[5] = {"coherent_step", "coherent_walk_x", "coherent_walk_y", "coherent_persist",
+                                     "coherent_shard"};
 
 template <class F> static void timed_launch(gg_ctx* ctx, gg_coh_state* C, hipStream_t s, int kind, F&& fn)
 {
@@ -2426,7 +3005,7 @@ uint64_t gg_coherent_msg_cap(gg_ctx* ctx) { return ctx->coh ? ctx->coh->P.msg_ca
 gg_status gg_coh_kernel_stats(gg_ctx* ctx, const char* name, double* total_ms, uint64_t* launches)
 {
   gg_coh_state* C = ctx->coh;
-  for (int k = 0; k < 4; ++k)
+  for (int k = 0; k < 5; ++k)
     if (C && std::strcmp(name, kKernelNames[k]) == 0) {
       *total_ms = C->kcnt[k] ? C->ksum[k] / (double)C->kcnt[k] * (double)C->nlaunch[k] : 0.0;
       *launches = C->nlaunch[k];
@@ -2684,6 +3263,66 @@ static gg_status coh_alloc(gg_ctx* ctx)
   S.ctr = gg_noc_ctr(ctx);
   gg_noc_queues(ctx, &S.nq, &S.nnd);
   S.err = ctx->err_dev;
+  // k_c_shard: one workgroup per owned logical shard (gg_coherent_run)
+  {
+    const uint32_t ns = k1 - k0;
+    std::vector<uint32_t> toff(ns + 1, 0), tl, tsi(P.L, 0);
+    for (uint32_t sh = 0; sh < ns; ++sh) {
+      toff[sh] = (uint32_t)tl.size();
+      for (uint32_t l = 0; l < P.L; ++l)
+        if (shard[gtile[l]] == k0 + sh) { tsi[l] = (uint32_t)tl.size() - toff[sh]; tl.push_back(l); }
+    }
+    toff[ns] = (uint32_t)tl.size();
+    uint32_t nt = 1;
+    for (uint32_t sh = 0; sh < ns; ++sh) nt = std::max(nt, toff[sh + 1] - toff[sh]);
+    const uint32_t segw = std::max(std::max(P.nsx, P.nsy), 1u);
+    std::vector<uint32_t> segloc(2 * (size_t)segw, 0), nx(ns, 0), ny(ns, 0);
+    for (uint32_t sg = 0; sg < P.nsx; ++sg) {
+      const Seg& g = segx[sg >> 1];
+      const uint32_t sh = shard[g.line * P.mw + g.lo] - k0;
+      segloc[sg] = nx[sh]++;
+    }
+    for (uint32_t sg = 0; sg < P.nsy; ++sg) {
+      const Seg& g = segy[sg >> 1];
+      const uint32_t sh = shard[g.lo * P.mw + g.line] - k0;
+      segloc[segw + sg] = ny[sh]++;
+    }
+    uint32_t nxs = 1, nys = 1;
+    for (uint32_t sh = 0; sh < ns; ++sh) { nxs = std::max(nxs, nx[sh]); nys = std::max(nys, ny[sh]); }
+    P.sh_nt = nt; P.sh_nxs = nxs; P.sh_nys = nys; P.sh_segw = segw; P.sh_segmax = maxrun; P.sh_k0 = k0;
+    const size_t walk_need = (size_t)kNetCtr * 8 * maxrun + 192 * (size_t)kWalkPkBytes;
+    P.sh_wave = (uint32_t)((std::max(sizeof(StepLdsS), walk_need) + 15) & ~(size_t)15);
+    P.sh_arr = kShardWaves * P.sh_wave;
+    C->shard_lds = P.sh_arr + shard_arr_bytes(nt, nxs, nys);
+    P.sh_pcap = P.msg_cap / ns;
+    P.sh_bcap = P.msg_cap / ns;
+    P.sh_gpk = (uint32_t)std::min<uint64_t>(P.seg_cap, 16384) & ~1u;
+    P.sh_gbytes = (uint32_t)(((size_t)P.sh_gpk * kWalkPkBytes + 15) & ~(size_t)15);
+    C->shard_n = ns;
+    const char* se = getenv("GG_COH_SHARD");
+    const bool want = se && atoi(se) != 0;                 // A/B form until it beats the per-step launches
+    bool ok = want && C->shard_lds <= 160 * 1024 && ns <= (uint32_t)ctx->num_cus;
+    if (ok) {
+      for (const void* fn : {(const void*)k_c_shard<true>, (const void*)k_c_shard<false>}) {
+        GG_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C->shard_lds));
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kShardThreads, C->shard_lds) != hipSuccess ||
+            per_cu < 1)
+          ok = false;
+      }
+    }
+    if (ok) {
+      const bool hbh = P.net == GG_NET_EMESH_HOP_BY_HOP;
+      if ((st = dupload(C, &S.tsi, tsi))) return st;
+      if ((st = dupload(C, &S.sh_toff, toff))) return st;
+      if ((st = dupload(C, &S.sh_tiles, tl))) return st;
+      if ((st = dupload(C, &S.seg_loc, segloc))) return st;
+      if ((st = dalloc(C, &S.sh_slot, 2 * (uint64_t)ns * kShardSlot))) return st;
+      if ((st = dalloc(C, &S.sbnd, 2 * (uint64_t)ns * P.sh_bcap))) return st;
+      if ((st = dalloc(C, &S.wscr, hbh ? (uint64_t)ns * kShardWaves * P.sh_gbytes : 1))) return st;
+    }
+    C->shard_ok = ok;
+  }
   return GG_OK;
 }
 
@@ -2713,7 +3352,7 @@ gg_status gg_coherent_begin(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_ou
   if (tr->num_records && (!tr->addr_dev || !tr->meta_dev)) return gg_fail(GG_ERR_INVALID, "NULL trace pointers");
   C->S.addr = tr->addr_dev; C->S.meta = tr->meta_dev; C->S.out = access_out_dev;
   C->n_records = tr->num_records;
-  for (int k = 0; k < 4; ++k) { C->ksum[k] = 0; C->kcnt[k] = 0; C->nlaunch[k] = 0; }
+  for (int k = 0; k < 5; ++k) { C->ksum[k] = 0; C->kcnt[k] = 0; C->nlaunch[k] = 0; }
   C->tused = 0;
   GG_HIP(hipMemcpyAsync(C->offs_dev, tr->tile_offsets, sizeof(uint64_t) * (P.T + 1), hipMemcpyHostToDevice, s));
   if (gg_status st = gg_noc_reset(ctx, s)) return st;
@@ -2857,10 +3496,26 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
   const CP& P = C->P;
   const bool hbh = P.net == GG_NET_EMESH_HOP_BY_HOP;
   uint32_t L = 0, batch = 16;
+  // one workgroup per logical shard for the whole run (k_c_shard)
+  if (C->shard_ok) {
+    GG_HIP(hipMemsetAsync(C->S.gbar, 0, sizeof(uint32_t), s));
+    const char* hr_env = getenv("GG_COH_SHARD_HR");
+    const bool hr = hr_env ? atoi(hr_env) != 0 : !hbh;      // L1 hit runs: the closed-form networks (long hit runs)
+    const uint64_t tlimit = 100000000ull * 600;               // s_memrealtime ticks (100 MHz): 10 minutes
+    timed_launch(ctx, C, s, 4, [&] {
+      if (hr)
+        hipLaunchKernelGGL(k_c_shard<true>, dim3(C->shard_n), dim3(kShardThreads), C->shard_lds, s, P, C->S, tlimit);
+      else
+        hipLaunchKernelGGL(k_c_shard<false>, dim3(C->shard_n), dim3(kShardThreads), C->shard_lds, s, P, C->S, tlimit);
+    });
+    GG_HIP(hipGetLastError());
+    GG_HIP(hipStreamSynchronize(s));
+    timed_harvest(C);
+  }
   // small meshes: the whole loop in persistent launches (k_c_persist), one
   // workgroup per owned tile, all resident (<= kPersistTiles << CUs)
   const char* np_env = getenv("GG_COH_NO_PERSIST");
-  const bool persist = P.L <= kPersistTiles && !(np_env && atoi(np_env));
+  const bool persist = !C->shard_ok && P.L <= kPersistTiles && !(np_env && atoi(np_env));
   while (persist) {
     GG_HIP(hipMemsetAsync(C->S.gbar, 0, sizeof(uint32_t), s));
     const char* nl_env = getenv("GG_COH_NO_LDS_CACHE");
@@ -2881,7 +3536,7 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
     timed_harvest(C);
     if (err || done) break;
   }
-  for (; !persist;) {
+  for (; !persist && !C->shard_ok;) {
     for (uint32_t b = 0; b < batch; ++b, ++L) {
       timed_launch(ctx, C, s, 0, [&] { hipLaunchKernelGGL(k_c_step, dim3(P.L), dim3(64), C->step_lds, s, P, C->S, L, 1u, (uint64_t)0); });
       if (hbh) {
@@ -2902,7 +3557,16 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
   }
   gg_timer_end(ctx, "coherent_run", s);
   GG_HIP(hipStreamSynchronize(s));
-  if (C->S.prof) {
+  if (C->S.prof && C->shard_ok) {
+    std::vector<unsigned long long> h(1024);
+    GG_HIP(hipMemcpy(h.data(), C->S.prof, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
+    for (uint32_t k = 0; k < C->shard_n && k < 48; ++k) {
+      const unsigned long long* pr = &h[200 + 16 * k];
+      fprintf(stderr, "[gg_shard %u] steps %llu tiles %llu | cycles: tiles %llu walks %llu quantum-end+barrier %llu import %llu (quanta %llu)\n",
+              k, pr[2], pr[1], pr[0], pr[3], pr[4], pr[5], pr[6]);
+    }
+  }
+  if (C->S.prof && !C->shard_ok) {
     // per-launch maxima in slots L mod 65536
     std::vector<unsigned long long> h(1024 + 8 * 65536);
     GG_HIP(hipMemcpy(h.data(), C->S.prof, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));

@@ -65,6 +65,8 @@ struct HCfg {
   UInt32 dir_entries;         // 0 = auto
   UInt32 dir_assoc;
   UInt64 quantum_ps;
+  UInt32 l2_assoc;            // l2_cache/T1/associativity (carbon_sim.cfg:233: 8; configs[4]: 16)
+  UInt32 workload;            // 0 hotspot (configs[2..3]), 1 stress (configs[4])
 };
 static HCfg H;
 
@@ -517,8 +519,8 @@ MSI::MemoryManager::MemoryManager(Tile* tile) : ::MemoryManager(tile), _dram_dir
   _dram_directory_home_lookup = new AddressHomeLookup(ceilLog2(64), ctrl, 64);
   _L1_cache_cntlr = new L1CacheCntlr(this, 64, 16, 4, 1, "lru", 1, 1, "parallel", false,
                                      32, 4, 1, "lru", 1, 1, "parallel", false);
-  _L2_cache_cntlr = new L2CacheCntlr(this, _L1_cache_cntlr, _dram_directory_home_lookup, 64, 512, 8, 1, "lru", 8, 3,
-                                     "parallel", false);
+  _L2_cache_cntlr = new L2CacheCntlr(this, _L1_cache_cntlr, _dram_directory_home_lookup, 64, 512, H.l2_assoc, 1, "lru",
+                                     8, 3, "parallel", false);
   _L1_cache_cntlr->setL2CacheCntlr(_L2_cache_cntlr);
 }
 MSI::MemoryManager::~MemoryManager() {}
@@ -774,6 +776,32 @@ static void gen_hotspot(UInt32 tile, UInt64 n, UInt32 hot_lines, UInt64* addr, U
   }
 }
 
+// the configs[4] stress generator (oracle_gen_stress):
+// WRITE p = 1/2; 77/256 of the records to a 4096-line pool at byte 2^45, pool
+// line L shared by the tiles of group L mod groups (T/64 groups by a 32-bit
+// hash of the tile), the rest private as the hotspot generator
+static UInt32 stress_group(UInt32 t, UInt32 groups)
+{
+  UInt32 x = t + 0x9E3779B9u;
+  x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15; x *= 0x846CA68Bu; x ^= x >> 16;
+  return x % groups;
+}
+static void gen_stress(UInt32 tile, UInt64 n, UInt32 num_tiles, UInt64* addr, UInt32* meta)
+{
+  const UInt64 seed = 0x9E3779B97F4A7C15ull ^ (UInt64)tile;
+  const UInt32 pool_lines = 4096, groups = num_tiles >= 128 ? num_tiles / 64 : 1;
+  const UInt32 per_group = pool_lines / groups ? pool_lines / groups : 1;
+  for (UInt64 k = 0; k < n; ++k) {
+    UInt64 z = splitmix_at(seed, k);
+    bool pool = ((z >> 40) & 0xFF) < 77;
+    addr[k] = pool ? (1ull << 45) + (UInt64)(stress_group(tile, groups) + groups * ((UInt32)(z & 0xFFFFFFFFull) % per_group)) * 64ull
+                   : ((UInt64)tile << 26) + ((z & 0x7FFF) << 6);
+    UInt32 gap = (UInt32)__builtin_ctz((UInt32)(((z >> 48) & 0xFF) | 0x100)) +
+                 (UInt32)__builtin_ctz((UInt32)(((z >> 56) & 0xFF) | 0x100));
+    meta[k] = (UInt32)((z >> 32) & 1u) | (gap << 1);
+  }
+}
+
 // ===========================================================================
 // fixtures
 // ===========================================================================
@@ -788,13 +816,17 @@ static void write_bin(const string& name, const void* p, size_t bytes)
 }
 
 static void run_case(FILE* man, bool first, const char* name, UInt32 T, UInt32 N, UInt32 hot, UInt32 K, UInt32 net,
-                     UInt32 dir_entries, UInt32 dir_assoc)
+                     UInt32 dir_entries, UInt32 dir_assoc, UInt32 l2_assoc = 8, UInt32 workload = 0)
 {
   H.T = T; H.K = K; H.net = net; H.dir_entries = dir_entries; H.dir_assoc = dir_assoc; H.quantum_ps = 1000000;
+  H.l2_assoc = l2_assoc; H.workload = workload;
   build_shard_map();
   g_t.clear(); g_t.resize(T); g_step.clear(); g_bnd.clear(); g_cc.clear(); g_dc.clear(); g_dram.clear();
   vector<UInt64> addr((size_t)T * N); vector<UInt32> meta((size_t)T * N); vector<UInt64> out((size_t)T * N, 0);
-  for (UInt32 t = 0; t < T; ++t) gen_hotspot(t, N, hot, &addr[(size_t)t * N], &meta[(size_t)t * N]);
+  for (UInt32 t = 0; t < T; ++t) {
+    if (workload == 1) gen_stress(t, N, T, &addr[(size_t)t * N], &meta[(size_t)t * N]);
+    else gen_hotspot(t, N, hot, &addr[(size_t)t * N], &meta[(size_t)t * N]);
+  }
   g_addr = &addr[0]; g_meta = &meta[0]; g_out = &out[0];
   for (UInt32 t = 0; t < T; ++t) {
     HTile& X = g_t[t];
@@ -804,7 +836,7 @@ static void run_case(FILE* man, bool first, const char* name, UInt32 T, UInt32 N
     X.rec = (UInt64)t * N; X.rec_end = X.rec + N; X.clk = 0; X.blocked = false; X.resumed_by_handler = false;
     X.pend_start = 0; X.seq = 0;
     memset(X.st, 0, sizeof(X.st)); memset(X.net, 0, sizeof(X.net));
-    X.stack.resize(1 << 20);
+    X.stack.resize(T > 256 ? 1 << 18 : 1 << 20);
     getcontext(&X.app_ctx);
     X.app_ctx.uc_stack.ss_sp = &X.stack[0];
     X.app_ctx.uc_stack.ss_size = X.stack.size();
@@ -835,9 +867,10 @@ static void run_case(FILE* man, bool first, const char* name, UInt32 T, UInt32 N
   write_bin("coh_" + n + "_cache.u64", &cc[0], cc.size() * 8);
   write_bin("coh_" + n + "_net.u64", &nc[0], nc.size() * 8);
   fprintf(man, "%s  \"%s\": {\"tiles\": %u, \"per_tile\": %u, \"hot_lines\": %u, \"num_shards\": %u, \"net\": %u, "
-          "\"dir_entries\": %u, \"dir_assoc\": %u, \"quanta\": %llu, \"steps\": %llu}",
-          first ? "" : ",\n", name, T, N, hot, K, net, dir_entries, dir_assoc, (unsigned long long)quanta,
-          (unsigned long long)steps);
+          "\"dir_entries\": %u, \"dir_assoc\": %u, \"l2_assoc\": %u, \"workload\": \"%s\", \"quanta\": %llu, "
+          "\"steps\": %llu}",
+          first ? "" : ",\n", name, T, N, hot, K, net, dir_entries, dir_assoc, l2_assoc, workload ? "stress" : "hotspot",
+          (unsigned long long)quanta, (unsigned long long)steps);
   printf("  coh %-10s tiles %u x %u: %llu quanta, %llu steps\n", name, T, N, (unsigned long long)quanta,
          (unsigned long long)steps);
   for (UInt32 t = 0; t < T; ++t) delete g_t[t].tile;
@@ -857,6 +890,11 @@ int main(int argc, char** argv)
   run_case(man, false, "shard64", 64, 400, 32, 8, 1, 0, 16);
   run_case(man, false, "hot256", 256, 120, 64, 1, 1, 0, 16);
   run_case(man, false, "shard256", 256, 150, 64, 8, 1, 0, 16);
+  // configs[4] shape: 16-way L2 (512 sets), the stress generator (50/50 R/W,
+  // 4096-line pool, ~64 sharers per pool line), 8 logical shards
+  run_case(man, false, "stress256w16", 256, 96, 0, 8, 1, 0, 16, 16, 1);
+  // configs[3] scale: 1024 tiles x 8 logical shards, 256 hot lines, reduced length
+  run_case(man, false, "shard1024", 1024, 24, 256, 8, 1, 0, 16);
   fprintf(man, "\n}\n");
   fclose(man);
   return 0;

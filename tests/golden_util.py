@@ -52,8 +52,12 @@ def coh_case(name, m):
     kw = dict(num_shards=m["num_shards"], net_model=C.NET_EMESH_HOP_COUNTER if m["net"] == 1 else C.NET_MAGIC)
     if m["dir_entries"]:
         kw.update(dir_total_entries=m["dir_entries"], dir_assoc=m["dir_assoc"])
+    kw.update(l2_assoc=m.get("l2_assoc", 8))
     cfg = C.default_config(T, **kw)
-    a, meta, o = po.gen_trace(T, N, hot_lines=m["hot_lines"])
+    if m.get("workload", "hotspot") == "stress":
+        a, meta, o = po.gen_stress_trace(T, N)
+    else:
+        a, meta, o = po.gen_trace(T, N, hot_lines=m["hot_lines"])
     exp = {"out": load("coh_%s_out.u64" % name, np.uint64),
            "stats": load("coh_%s_stats.u64" % name, np.uint64).reshape(T, 32),
            "cache": load("coh_%s_cache.u64" % name, np.uint64).reshape(T, 2, 12),
