@@ -19,15 +19,19 @@ and the held cross-shard records are exchanged at every quantum boundary;
 the work is the same at every N ("strong" scaling) and the results are
 bit-identical.
 
-Reported with it: the kernels' device time from HIP events around every
-launch (gg_kernel_stats) and the step kernel's roofline at 20 algorithmic
-bytes per access (8 B address + 4 B meta in, 8 B access word out); the C
-oracle on the same workload as the CPU baseline, on 1 thread and on one
-OpenMP thread per logical shard (oracle_coh_run_parallel); and a bit-exact
-check of every output against the oracle in the same run.  Sections under
-their own keys: the same workload on emesh_hop_counter, configs[0] (captured
-FFT), the configs[1] private-cache replay (round 1's headline), NoC batches
-and the configs[4] stress geometry.
+Reported with it: the roofline of the dominant kernel by device time
+(k_c_walk: the X and Y walks are one kernel symbol) at SURVEY.md §8d's 16
+algorithmic bytes per access (8 B address + 4 B meta in, 4 B result out),
+accesses per launch from the run, the average launch duration from HIP events
+around EVERY launch in one extra untimed run (events around every launch add
+gaps between launches, so the timed runs carry none); the C oracle on the
+same workload as the CPU baseline, tile-parallel on the host's CPU share
+(oracle_coh_set_threads) and on one thread; and a bit-exact check of every
+output against the oracle in the same run.  Sections under their own keys:
+the headline workload at 8x the trace length (coherent_long), the same
+workload on emesh_hop_counter, configs[0] (captured FFT), the configs[1]
+private-cache replay (round 1's headline), NoC batches and the configs[4]
+stress geometry.
 """
 import argparse
 import json
@@ -45,7 +49,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 ALGO_BYTES_PER_ACCESS = 16     # Mode P: 8 B addr + 4 B meta in, 4 B result out
-COH_BYTES_PER_ACCESS = 20      # Mode C: 8 B addr + 4 B meta in, 8 B access word out
+COH_BYTES_PER_ACCESS = 16      # Mode C: 8 B addr + 4 B meta in, 4 B result out
 # Algorithmic bytes per access of each Mode P kernel
 KERNEL_BYTES = {
     "cache_stream": 16,    # single pass (default): read addr (8) + meta (4), write result (4); state < 1%
@@ -56,7 +60,7 @@ KERNEL_BYTES = {
 }
 KERNEL_SYMBOL = {"cache_stream": "k_cache_stream", "cache_hist": "k_shard_hist", "cache_scatter": "k_shard_scatter",
                  "cache_replay": "k_cache_replay_lean", "cache_unshard": "k_unshard",
-                 "coherent_step": "k_c_step", "coherent_walk_x": "k_c_walk (X)", "coherent_walk_y": "k_c_walk (Y)"}
+                 "coherent_step": "k_c_step", "coherent_walk": "k_c_walk", "coherent_persist": "k_c_persist"}
 NET = {"hop_counter": 1, "hop_by_hop": 2, "magic": 0}
 
 
@@ -114,10 +118,12 @@ def parse():
     p.add_argument("--hot-lines", type=int, default=256, help="shared hot lines (configs[3]: 256)")
     p.add_argument("--shards", type=int, default=8, help="logical shards (the 8-process blocks)")
     p.add_argument("--net", default="hop_by_hop", choices=sorted(NET), help="headline memory network model")
-    p.add_argument("--cpu-threads", type=int, default=0, help="all-core oracle threads (0 = one per shard, <= cores)")
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="CPU-baseline oracle threads (0 = the host CPU share: OMP_NUM_THREADS, else the affinity set)")
+    p.add_argument("--long-per-tile", type=int, default=2048, help="coherent_long section: accesses per tile")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
-    p.add_argument("--sections", default="hop_counter,stress,fft,private,private_16way,noc",
+    p.add_argument("--sections", default="coherent_long,hop_counter,stress,fft,private,private_16way,noc",
                    help="extra sections at N = 1 (comma list; '' = none)")
     p.add_argument("--hc-per-tile", type=int, default=1024, help="hop_counter section: accesses per tile")
     p.add_argument("--private-per-tile", type=int, default=1 << 20)
@@ -161,9 +167,23 @@ def coherent_workload(T, N, H, dev, workload="hotspot"):
     return addr, meta, offs
 
 
-def coherent_run(args, T, N, H, K, net, world, rank, dev, steps, warmup, verify, cpu, workload="hotspot", l2_assoc=8):
+def cpu_share():
+    """Threads of the host's CPU share: OMP_NUM_THREADS when set (the GPU box
+    sets it to the CPUs it allots one GPU), else the process affinity set."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(int(env), aff) if env and env.isdigit() else aff)
+
+
+def coherent_run(args, T, N, H, K, net, world, rank, dev, steps, warmup, verify, cpu, workload="hotspot", l2_assoc=8,
+                 kernel_profile=True):
     """One measurement of Mode C: `warmup` untimed + `steps` timed whole runs,
-    barrier + synchronize around the timed region, max over ranks."""
+    barrier + synchronize around the timed region, max over ranks; then (if
+    kernel_profile) one untimed run with HIP events around every launch for
+    the per-kernel averages."""
     import torch
     from graphite_amd import config as C
     from graphite_amd import backend as B
@@ -172,7 +192,6 @@ def coherent_run(args, T, N, H, K, net, world, rank, dev, steps, warmup, verify,
     k0, k1 = CO.shard_range(rank, world, K)
     cfg = C.default_config(T, num_shards=K, shard_begin=k0, shard_end=k1, net_model=net, l2_assoc=l2_assoc)
     be = B.Backend(cfg)
-    be.set_timing(True)
     addr, meta, offs = coherent_workload(T, N, H, dev, workload)
     out = torch.zeros(T * N, dtype=torch.int64, device=dev)
 
@@ -180,8 +199,7 @@ def coherent_run(args, T, N, H, K, net, world, rank, dev, steps, warmup, verify,
         if world == 1:
             be.coherent_run(addr, meta, offs, out)
         else:
-            eng = B.CoherentEngine(be, addr, meta, offs, out)
-            CO.run(eng, cfg.quantum_ns * 1000, K, world, rank, "nccl", str(dev))
+            CO.run_rccl(be, addr, meta, offs, out)     # gg_coherent_run_ranks: the exchange in the C ABI (RCCL)
 
     for _ in range(warmup):
         step()
@@ -198,13 +216,28 @@ def coherent_run(args, T, N, H, K, net, world, rank, dev, steps, warmup, verify,
     st, cc, ri = be.coherent_stats()
     nc = be.noc_counters()
     kern = {}
-    for name in ("coherent_step", "coherent_walk_x", "coherent_walk_y"):
-        try:
-            ms, n = be.kernel_stats(name)
-        except Exception:
-            continue
-        if n:
-            kern[name] = {"total_ms_last_run": ms, "launches": n, "avg_us": 1e3 * ms / n}
+    if kernel_profile:
+        be.set_timing(True, every_launch=True)
+        c0 = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        prof_s = time.perf_counter() - c0
+        be.set_timing(False)
+        for name in ("coherent_step", "coherent_walk_x", "coherent_walk_y", "coherent_persist"):
+            try:
+                ms, n = be.kernel_stats(name)
+            except Exception:
+                continue
+            if n:
+                kern[name] = {"total_ms": ms, "launches": n, "avg_us": 1e3 * ms / n}
+        # the X and Y walks are one kernel symbol (k_c_walk<true>) in rocprof
+        wx, wy = kern.pop("coherent_walk_x", None), kern.pop("coherent_walk_y", None)
+        if wx or wy:
+            ms = sum(w["total_ms"] for w in (wx, wy) if w)
+            n = sum(w["launches"] for w in (wx, wy) if w)
+            kern["coherent_walk"] = {"total_ms": ms, "launches": n, "avg_us": 1e3 * ms / n,
+                                     "x": wx, "y": wy}
+        kern["_profile_run_seconds"] = prof_s
     res = {"value": T * N * steps / elapsed, "seconds_per_run": elapsed / steps, "elapsed": elapsed,
            "quanta": int(ri[C.RUN_INFO.index("quanta")]), "steps": int(ri[C.RUN_INFO.index("steps")]),
            "messages": int(ri[C.RUN_INFO.index("net_msgs")] + ri[C.RUN_INFO.index("self_msgs")]),
@@ -222,25 +255,29 @@ def coherent_run(args, T, N, H, K, net, world, rank, dev, steps, warmup, verify,
         a = addr.cpu().numpy().view(np.uint64)
         m = meta.cpu().numpy().view(np.uint32)
         ocfg = C.default_config(T, num_shards=K, net_model=net, l2_assoc=l2_assoc)
-        threads = args.cpu_threads or max(1, min(K, os.cpu_count() or 1))
+        threads = args.cpu_threads or cpu_share()
+        oc = po.OracleCoherent(ocfg, threads=threads)
         c0 = time.perf_counter()
-        ref = po.coherent_run_parallel(ocfg, a, m, offs, threads)
+        ref = oc.run(a, m, offs)
         pdt = time.perf_counter() - c0
         got = out.cpu().numpy().view(np.uint64)
-        res["bit_exact_checked"] = bool(np.array_equal(got, ref[0]) and np.array_equal(st, ref[1]) and
-                                        np.array_equal(cc, ref[2]) and np.array_equal(nc, ref[3]))
+        res["bit_exact_checked"] = bool(np.array_equal(got, ref) and np.array_equal(st, oc.tile_stats()) and
+                                        np.array_equal(cc, oc.cache_counters()) and
+                                        np.array_equal(nc, oc.net_counters()))
         if not res["bit_exact_checked"]:
             print("bench.py: COHERENT BIT-EXACT CHECK FAILED", file=sys.stderr)
         if cpu:
-            oc = po.OracleCoherent(ocfg)
+            o1 = po.OracleCoherent(ocfg)
             c0 = time.perf_counter()
-            ref1 = oc.run(a, m, offs)
+            ref1 = o1.run(a, m, offs)
             sdt = time.perf_counter() - c0
-            res["bit_exact_checked"] = res["bit_exact_checked"] and bool(np.array_equal(ref1, ref[0]))
+            res["bit_exact_checked"] = res["bit_exact_checked"] and bool(np.array_equal(ref1, ref))
             res["cpu_baseline"] = {
                 "value": T * N / pdt, "unit": "accesses/s", "cores": threads, "kind": "port",
-                "sample": "the whole workload once (%d tiles x %d accesses): oracle/gg_coherent.inc -O3, one context "
-                          "per logical shard on %d OpenMP threads, %.2f s" % (T, N, threads, pdt),
+                "sample": "the whole workload once (%d tiles x %d accesses): oracle/gg_coherent.inc -O3, tile-parallel "
+                          "steps (each step's tiles, then the hop-by-hop routing stage by stage: injection per source, "
+                          "X per row, Y per column, SELF per destination) on %d OpenMP threads = the host CPU share, "
+                          "%.2f s" % (T, N, threads, pdt),
                 "one_thread": {"value": T * N / sdt, "cores": 1, "seconds": sdt},
                 "host": host_info()}
     be.close()
@@ -248,7 +285,11 @@ def coherent_run(args, T, N, H, K, net, world, rank, dev, steps, warmup, verify,
 
 
 def host_info():
-    info = {"nproc": os.cpu_count()}
+    info = {"nproc": os.cpu_count(), "cpu_share": cpu_share(), "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        pass
     try:
         out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
         for line in out.splitlines():
@@ -259,13 +300,27 @@ def host_info():
     return info
 
 
+def coherent_long_section(args, dev):
+    """The headline workload at --long-per-tile accesses per tile (8x the
+    headline's trace): one warm-up-free timed run, bit-exact against the
+    tile-parallel oracle — the rate past the cold-start phase."""
+    from graphite_amd import config as C
+    T, N, H, K = args.tiles, args.long_per_tile, args.hot_lines, args.shards
+    r = coherent_run(args, T, N, H, K, NET[args.net], 1, 0, dev, 1, 0, not args.no_verify, False,
+                     kernel_profile=False)
+    r["workload"] = ("%d tiles x %d hotspot accesses (%d hot lines), MSI + DRAM + %s, %d logical shards: the headline "
+                     "at %dx its trace length" % (T, N, H, args.net, K, N // max(1, args.per_tile)))
+    r["unit"] = "accesses/s"
+    return r
+
+
 def hop_counter_section(args, dev):
     """The headline workload at --hc-per-tile accesses per tile on
     emesh_hop_counter (closed-form routes, no router contention)."""
     from graphite_amd import config as C
     T, N, H, K = args.tiles, args.hc_per_tile, args.hot_lines, args.shards
     r = coherent_run(args, T, N, H, K, C.NET_EMESH_HOP_COUNTER, 1, 0, dev, 1, 0, not args.no_verify,
-                     not args.no_cpu_baseline)
+                     not args.no_cpu_baseline, kernel_profile=False)
     r["workload"] = ("%d tiles x %d hotspot accesses (%d hot lines), MSI + DRAM + emesh_hop_counter, %d logical shards"
                      % (T, N, H, K))
     r["unit"] = "accesses/s"
@@ -436,7 +491,7 @@ def stress_section(args, dev):
     from graphite_amd import config as C
     T, N, K = args.stress_tiles, args.stress_per_tile, 8
     r = coherent_run(args, T, N, 0, K, C.NET_EMESH_HOP_COUNTER, 1, 0, dev, 1, 1, not args.no_verify,
-                     not args.no_cpu_baseline, workload="stress", l2_assoc=16)
+                     not args.no_cpu_baseline, workload="stress", l2_assoc=16, kernel_profile=False)
     r["workload"] = ("configs[4]: %d tiles x %d stress accesses (WRITE p=1/2, 30%% to a 4096-line pool, ~64 sharers "
                      "per pool line), 16-way L2, MSI + DRAM + emesh_hop_counter, %d logical shards" % (T, N, K))
     r["unit"] = "accesses/s"
@@ -607,7 +662,7 @@ def private_section(args, dev):
         if not res["bit_exact_checked"]:
             print("bench.py: PRIVATE BIT-EXACT CHECK FAILED", file=sys.stderr)
     if not args.no_cpu_baseline:
-        threads = min(16, os.cpu_count() or 1)
+        threads = args.cpu_threads or cpu_share()
         cps, cdt = cpu_baseline(args.cpu_sample_tiles, N, threads)
         res["cpu_baseline"] = {"value": cps, "unit": "accesses/s", "cores": threads, "kind": "port",
                                "sample": "%d tiles x %d accesses, oracle/gg_oracle.c -O3, one tile per thread, %.1f s"
@@ -638,10 +693,12 @@ def main():
     head = coherent_run(args, T, N, H, K, net, world, rank, dev, args.steps, args.warmup,
                         not args.no_verify, world == 1 and not args.no_cpu_baseline)
     if rank == 0:
-        kern = head["kernels"]
-        dom = max(kern, key=lambda k: kern[k]["total_ms_last_run"]) if kern else None
-        step = kern.get("coherent_step")
-        achieved = COH_BYTES_PER_ACCESS * T * N / (step["total_ms_last_run"] * 1e-3) / 1e9 if step else None
+        kern = {k: v for k, v in head["kernels"].items() if not k.startswith("_")}
+        dom = max(kern, key=lambda k: kern[k]["total_ms"]) if kern else None
+        dk = kern.get(dom) if dom else None
+        # accesses per launch of the dominant kernel x 16 B / its average launch time
+        lacc = T * N / dk["launches"] if dk else None
+        achieved = COH_BYTES_PER_ACCESS * lacc / (dk["avg_us"] * 1e-6) / 1e9 if dk else None
         wl = ("configs[3]: %d tiles (%dx%d mesh) x %d accesses per tile of the hotspot trace (20%% to %d lines "
               "shared by all tiles, WRITE p=1/3, ~2-cycle gaps), pr_l1_pr_l2_dram_directory_msi + full-map directory "
               "+ DRAM history-tree queue + %s (history-tree router contention), quantum 1000 ns, %d logical shards "
@@ -663,20 +720,22 @@ def main():
             "config": {"workload": wl, "tiles": T, "accesses_per_tile": N, "hot_lines": H, "logical_shards": K,
                        "mode": "coherent", "network": args.net,
                        "parallelism": "%d logical shards over %d rank(s); held cross-shard records exchanged once "
-                                      "per quantum" % (K, world)},
-            "roofline": {"bound": "hbm", "kernel": "k_c_step", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
-                         "bytes_per_access": COH_BYTES_PER_ACCESS, "launch_accesses": T * N / step["launches"] if step else None,
-                         "kernel_avg_us": step["avg_us"] if step else None,
-                         "dominant_kernel_by_time": KERNEL_SYMBOL.get(dom, dom),
-                         "note": "Mode C is latency-bound: a step is a chain of dependent accesses per tile and the "
-                                 "hop-by-hop walks are serial per chain (DESIGN.md §4); the fraction measures how far "
-                                 "that is from the HBM bound, not an HBM bottleneck"},
+                                      "per quantum%s" % (K, world, " (gg_coherent_run_ranks, RCCL)" if world > 1 else "")},
+            "roofline": {"bound": "hbm", "kernel": KERNEL_SYMBOL.get(dom, dom), "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                         "traffic": None, "bytes_per_access": COH_BYTES_PER_ACCESS, "launch_accesses": lacc,
+                         "kernel_avg_us": dk["avg_us"] if dk else None, "kernel_launches": dk["launches"] if dk else None,
+                         "kernels": kern,
+                         "timing": "HIP events around every launch, one extra untimed run on the launch stream "
+                                   "(the timed runs carry no events)",
+                         "note": "Mode C is latency-bound: a step is a chain of dependent accesses per tile and each "
+                                 "router port serves its packets one by one in the canonical order (DESIGN.md §4); "
+                                 "the fraction measures how far that is from the HBM bound, not an HBM bottleneck"},
             "coherent": {k: head[k] for k in ("quanta", "steps", "messages", "boundary_records", "simulated_ns",
-                                              "kernels", "seconds_per_run")},
+                                              "seconds_per_run")},
             "bit_exact_checked": head.get("bit_exact_checked"),
         }
-        prof = pmc_traffic("k_c_step", "coherent_%s_%dx%d_k%d" % (args.net, T, N, K))
+        prof = pmc_traffic(KERNEL_SYMBOL.get(dom, dom), "coherent_%s_%dx%d_k%d" % (args.net, T, N, K))
         if prof:
             out["roofline"]["traffic"] = prof["bytes"]
             out["roofline"]["traffic_source"] = prof["source"]
@@ -685,7 +744,9 @@ def main():
     secs = [x for x in args.sections.split(",") if x] if world == 1 else []
     for name in secs:
         try:
-            if name == "hop_counter":
+            if name == "coherent_long" and args.long_per_tile:
+                r = coherent_long_section(args, dev)
+            elif name == "hop_counter":
                 r = hop_counter_section(args, dev)
             elif name == "fft" and args.fft_m:
                 r = fft_section(args, dev)

@@ -176,16 +176,18 @@ class Backend:
     def reset(self):
         _check(load().gg_reset(self.h))
 
-    def set_timing(self, on=True):
-        load().gg_set_timing(self.h, int(on))
+    def set_timing(self, on=True, every_launch=False):
+        """HIP-event kernel timing: off, sampled (coherent launches: 1 in 16)
+        or around every launch (every_launch=True; adds launch gaps)."""
+        load().gg_set_timing(self.h, (2 if every_launch else 1) if on else 0)
 
     def kernel_time_ms(self, name):
         return load().gg_kernel_time_ms(self.h, name.encode())
 
     def kernel_stats(self, name):
         """(total device ms, launches) of a coherent-mode kernel since the last
-        coherent begin (timing must be on): HIP events around every 16th launch,
-        total = their mean x launches."""
+        coherent begin (timing must be on): mean over the timed launches (every
+        16th, or every one) x launches."""
         ms, n = ctypes.c_double(0), ctypes.c_uint64(0)
         _check(load().gg_kernel_stats(self.h, name.encode(), ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value

@@ -403,7 +403,7 @@ float gg_kernel_time_ms(gg_ctx* ctx, const char* kernel)
   return -1.0f;
 }
 
-void gg_set_timing(gg_ctx* ctx, int enabled) { if (ctx) ctx->timing = enabled != 0; }
+void gg_set_timing(gg_ctx* ctx, int enabled) { if (ctx) ctx->timing = enabled < 0 ? 0 : enabled; }
 
 gg_status gg_kernel_stats(gg_ctx* ctx, const char* kernel, double* total_ms, uint64_t* launches)
 {

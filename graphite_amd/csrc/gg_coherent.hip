@@ -107,10 +107,6 @@ struct CP {
   uint32_t touch_each;                     // hit runs touch LRU rows one record at a time (> 16 ways; GG_COH_TOUCH_EACH=1)
   uint32_t walk_wide;                      // pipelined walkers scan every packet (the > 128-packet path; GG_COH_WALK_WIDE=1)
   uint32_t no_hit_runs;                    // GG_COH_NO_HIT_RUNS=1: every record through app_access
-  // k_c_shard (one workgroup per logical shard): most tiles / X / Y segments of a
-  // shard, bytes of a wave's LDS area, LDS offsets of the shard arrays, record
-  // pool and boundary region per shard, walker packets a wave's global scratch holds
-  uint32_t sh_nt, sh_nxs, sh_nys, sh_wave, sh_arr, sh_pcap, sh_bcap, sh_gpk, sh_gbytes, sh_segw, sh_segmax, sh_k0;
   uint64_t lat_l1d, lat_l1t, lat_l2d, lat_l2t, lat_dir, gap_ps, dram_proc, dram_cost;
   NocParams np;
 };
@@ -144,13 +140,7 @@ struct CS {
   uint64_t* ctr;                         // NoC counters [T][GG_NUM_NET_COUNTERS]
   uint64_t* gscr;                        // [L][5 * IC] ordering scratch beyond kInLds
   unsigned long long* prof;              // GG_COH_PROFILE=1: shader-clock cycles per phase (diagnostics)
-  uint32_t* gbar;                        // grid barrier counter of k_c_persist / k_c_shard
-  // k_c_shard: local tile -> index within its shard; per owned shard its tiles
-  // (offsets [ns + 1]), X / Y segments (offsets), segment -> index within its
-  // shard ([2][max(nsx, nsy)]); quantum-end slots [2][ns][8]; boundary regions
-  // [2][ns][sh_bcap]; walker scratch [ns][waves][sh_gbytes]
-  const uint32_t *tsi, *sh_toff, *sh_tiles, *sh_xoff, *sh_xsegs, *sh_yoff, *sh_ysegs, *seg_loc;
-  uint64_t* sh_slot; gg_cmsg* sbnd; uint8_t* wscr;
+  uint32_t* gbar;                        // grid barrier counter of k_c_persist
 };
 // profile slots: step phases 0..5 summed over tiles, 8 = sum over steps of the slowest tile;
 // walker: 16 staging+load, 17 event loop, 18 hand-off+write back, 19 events, 20 sum of slowest walker per launch (X),
@@ -421,7 +411,6 @@ struct StepLdsT {
   Work wstack[WSTACK];                                    // directory work loop continuations
 };
 using StepLds = StepLdsT<kInLds, kRqLds>;                 // one tile per workgroup (k_c_step, k_c_persist)
-using StepLdsS = StepLdsT<128, 64>;                       // one tile per wave of a shard workgroup (k_c_shard)
 
 // The lanes of ONE wave exchange data through LDS / global memory between the
 // phases of a tile step; in a multi-wave workgroup the other waves run other
@@ -436,10 +425,8 @@ __device__ __forceinline__ void tsync()
 
 // Where a tile step's deliveries go.  GHooks: the per-step launches
 // (k_c_step / k_c_persist) keep the inbox / arrival / segment counters and the
-// record pools in HBM, shared by every block of the launch.  ShardHooks
-// (k_c_shard, below): one workgroup owns a logical shard for the whole run and
-// keeps them in its LDS.  Slot functions return the list position or ~0u
-// (capacity exceeded, reported through S.err).
+// record pools in HBM, shared by every block of the launch.  Slot functions
+// return the list position or ~0u (capacity exceeded, reported through S.err).
 struct GHooks {
   const CP& P; const CS& S;
   // n contiguous records of the parity-p pool (wave-uniform)
@@ -2448,485 +2435,50 @@ __global__ void k_c_export_scatter(CS S, const gg_cmsg* b, uint32_t n, const uin
   out[base[k] + atomicAdd(&cursor[k], 1u)] = b[i];
 }
 
-// ---------------------------------------------------------------------------
-// k_c_shard: the device-driven run with ONE WORKGROUP PER LOGICAL SHARD.
-// Within a quantum a logical shard evolves on its own: every message or packet
-// that leaves it is held to the quantum boundary.  So each
-// shard runs its own step loop — the tiles with work (an LDS worklist: the
-// tiles that got deliveries, and at step 0 every tile with a record before
-// the barrier), one tile per wave; then its X and Y segments, one segment per
-// wave; workgroup barriers between the phases — and its quantum ends after
-// its first step that sends nothing (a shard that sent nothing stays idle to
-// the end of the quantum, so the quantum's global step count is its busiest
-// shard's).  The counters the per-step launches keep in HBM (inbox / arrival /
-// segment counts, record pools, boundary records) live in the workgroup's
-// LDS; tile, directory and queue state stays in HBM, read back by the CU that
-// wrote it (its L1 and XCD L2, no kernel-boundary write-back / invalidate).
-// At the quantum boundary the shards meet in a grid barrier (agent-scope
-// release / acquire, grid_sync), import the records held for them and pick
-// the next quantum by quantum_end's rule.  Every queue, directory and cache
-// sees the same requests in the same order as under the per-step launches:
-// bit-identical results.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kShardWaves = 4, kShardThreads = 64 * kShardWaves;   // 1 wave per SIMD: the tile step needs ~500 registers
-__device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
-constexpr uint32_t kShardMaxSteps = 1u << 20;        // longer quanta are reported (GG_DERR_STATE)
-constexpr uint32_t kShardSlot = 8;                   // u64 words of a shard's quantum-end slot
-
-struct ShardHdr {
-  uint32_t npool[2];                 // records allocated in this shard's region of pool 0 / 1
-  uint32_t nbnd;                     // records held in this shard's boundary region this quantum
-  uint32_t sent[2];                  // records sent in the step of parity 0 / 1
-  uint32_t nwl[2];                   // tiles listed for the step of parity 0 / 1
-  uint32_t ht, hx, hy;               // work cursors of the tile / X / Y phase
-  uint32_t nxw, nyw;                 // X / Y segments with packets this step
-  uint32_t imp_held;                 // held packets imported for step 0
-  uint32_t pad;
-  unsigned long long ri_net, ri_self, ri_bnd;
-  unsigned long long act, blk, mn;   // quantum-end statistics of the shard
-};
-
-struct ShardArr {                    // the shard's LDS arrays (sizes from CP)
-  ShardHdr* h;
-  uint64_t* nst;                         // [nt] next start (kNsFin / kNsBlk)
-  uint32_t *ninb, *narv, *listed, *wl;   // [2][nt]
-  uint32_t *nsx, *xwl, *nsy, *ywl;       // [nxs], [nxs], [nys], [nys]
-};
-
-__device__ __forceinline__ ShardArr shard_arr(const CP& P, uint8_t* smem)
+// gg_round_exchange's device side (gg_coh_export_slots / _round_status / _import_slots)
+__global__ void k_c_ri_quantum(CS S, uint64_t q)
 {
-  ShardArr A;
-  uint8_t* b = smem + P.sh_arr;
-  A.h = reinterpret_cast<ShardHdr*>(b); b += (sizeof(ShardHdr) + 15) & ~(size_t)15;
-  A.nst = reinterpret_cast<uint64_t*>(b); b += 8 * (size_t)P.sh_nt;
-  A.ninb = reinterpret_cast<uint32_t*>(b); b += 8 * (size_t)P.sh_nt;
-  A.narv = reinterpret_cast<uint32_t*>(b); b += 8 * (size_t)P.sh_nt;
-  A.listed = reinterpret_cast<uint32_t*>(b); b += 8 * (size_t)P.sh_nt;
-  A.wl = reinterpret_cast<uint32_t*>(b); b += 8 * (size_t)P.sh_nt;
-  A.nsx = reinterpret_cast<uint32_t*>(b); b += 4 * (size_t)P.sh_nxs;
-  A.xwl = reinterpret_cast<uint32_t*>(b); b += 4 * (size_t)P.sh_nxs;
-  A.nsy = reinterpret_cast<uint32_t*>(b); b += 4 * (size_t)P.sh_nys;
-  A.ywl = reinterpret_cast<uint32_t*>(b);
-  return A;
+  S.ri[GG_RI_QUANTA]++;
+  S.ri[GG_RI_FINAL_QUANTUM] = q;
 }
-// bytes of the shard arrays after P.sh_arr (host and device)
-__host__ __device__ inline size_t shard_arr_bytes(uint32_t nt, uint32_t nxs, uint32_t nys)
+__global__ void k_slot_clear(gg_cmsg* slots, uint32_t world, uint64_t region)
 {
-  return ((sizeof(ShardHdr) + 15) & ~(size_t)15) + 40 * (size_t)nt + 8 * (size_t)nxs + 8 * (size_t)nys;
+  for (uint32_t r = threadIdx.x; r < world; r += blockDim.x) slots[(size_t)r * (region + 1)].addr = 0;
 }
-
-// the deliveries of a shard workgroup: LDS counters, a tile is listed for the
-// step that reads its first delivery, a segment for the walk its first packet enters
-struct ShardHooks {
-  const CP& P; const CS& S; const ShardArr& A;
-  uint32_t pbase;                    // this shard's first record in pool 0 / 1
-  gg_cmsg* bnd;                      // this shard's boundary region of the quantum
-  __device__ __forceinline__ uint32_t pool_alloc(uint32_t p, uint32_t want) const
-  {
-    uint32_t b = 0;
-    if (lane_id() == 0) b = atomicAdd(&A.h->npool[p], want);
-    b = (uint32_t)__shfl((int)b, 0);
-    return (uint64_t)b + want > P.sh_pcap ? ~0u : pbase + b;
-  }
-  __device__ __forceinline__ void list_tile(uint32_t pn, uint32_t si, uint32_t ld) const
-  {
-    if (atomicOr(&A.listed[pn * P.sh_nt + si], 1u) == 0) A.wl[pn * P.sh_nt + atomicAdd(&A.h->nwl[pn], 1u)] = ld;
-  }
-  __device__ __forceinline__ uint32_t inbox_slot(uint32_t pn, uint32_t ld) const
-  {
-    const uint32_t si = S.tsi[ld];
-    const uint32_t j = atomicAdd(&A.ninb[pn * P.sh_nt + si], 1u);
-    if (j == 0) list_tile(pn, si, ld);
-    return j < P.IC ? j : ~0u;
-  }
-  __device__ __forceinline__ uint32_t arv_slot(uint32_t pn, uint32_t ld) const
-  {
-    const uint32_t si = S.tsi[ld];
-    const uint32_t j = atomicAdd(&A.narv[pn * P.sh_nt + si], 1u);
-    if (j == 0) list_tile(pn, si, ld);
-    return j < P.IC ? j : ~0u;
-  }
-  __device__ __forceinline__ uint32_t seg_slot(bool is_x, uint32_t sg) const
-  {
-    const uint32_t loc = S.seg_loc[(is_x ? 0u : 1u) * P.sh_segw + sg];
-    const uint32_t j = atomicAdd(&(is_x ? A.nsx : A.nsy)[loc], 1u);
-    if (j == 0) {
-      if (is_x) A.xwl[atomicAdd(&A.h->nxw, 1u)] = sg;
-      else A.ywl[atomicAdd(&A.h->nyw, 1u)] = sg;
-    }
-    return j < P.seg_cap ? j : ~0u;
-  }
-  __device__ __forceinline__ bool bnd_put(const gg_cmsg& m) const
-  {
-    const uint32_t j = atomicAdd(&A.h->nbnd, 1u);
-    if (j >= P.sh_bcap) return false;
-    bnd[j] = m;
-    return true;
-  }
-  __device__ __forceinline__ void clear_arv(uint32_t p, uint32_t lt) const { A.narv[p * P.sh_nt + S.tsi[lt]] = 0; }
-  __device__ __forceinline__ void clear_inb(uint32_t p, uint32_t lt) const { A.ninb[p * P.sh_nt + S.tsi[lt]] = 0; }
-  __device__ __forceinline__ void step_counts(uint32_t k, uint32_t net, uint32_t self, uint32_t nb, uint32_t sent) const
-  {
-    if (net) atomicAdd(&A.h->ri_net, (unsigned long long)net);
-    if (self) atomicAdd(&A.h->ri_self, (unsigned long long)self);
-    if (nb) atomicAdd(&A.h->ri_bnd, (unsigned long long)nb);
-    if (sent) atomicAdd(&A.h->sent[k & 1u], sent);
-  }
-};
-
-// One segment (stage 0: X, 1: Y) walked by the calling wave: the positions
-// swept in the direction of travel, each position's batch in (time, rank)
-// order through the port's queue (RegQueue loaded from HBM for the history
-// tree, HTree on HBM for the other models) — walk_body<false>'s sweep.  pk:
-// the packet arrays (cap packets; LDS, or the wave's HBM scratch for long
-// lists), lc: [npos][kNetCtr] router / link counters.
-template <class H>
-__device__ __forceinline__ void walk_sweep_wave(const CP& P, const CS& S, const H& hk, uint32_t p, int stage,
-                                                uint32_t sg, uint32_t n, uint8_t* pk, uint32_t cap, uint64_t* lc)
+__global__ void k_c_export_slots(CS S, const gg_cmsg* b, const uint32_t* n_dev, uint32_t per_rank, uint64_t region,
+                                 gg_cmsg* slots)
 {
-  const uint32_t ln = lane_id();
-  const uint32_t* list = (stage == 0 ? S.xl : S.yl) + (size_t)sg * P.seg_cap;
-  const Seg sd = (stage == 0 ? S.segx : S.segy)[sg >> 1];
-  const uint32_t dir = sg & 1u;
-  const int port = stage == 0 ? (dir ? P_RIGHT : P_LEFT) : (dir ? P_UP : P_DOWN);
-  auto tile_at = [&](uint32_t pos) -> uint32_t { return stage == 0 ? sd.line * P.mw + pos : pos * P.mw + sd.line; };
-  auto pos_of = [&](uint32_t tile) -> uint32_t { return stage == 0 ? tile % P.mw : tile / P.mw; };
-  gg_cmsg* cur = pool(S, p);
-  const uint32_t npos = sd.hi - sd.lo + 1;
-  WalkLds W;
-  W.Pt = reinterpret_cast<uint64_t*>(pk);
-  W.Ph = W.Pt + cap; W.Pk = W.Ph + cap; W.Pz = W.Pk + cap;
-  W.Pi = reinterpret_cast<uint32_t*>(W.Pz + cap);
-  W.Pp = W.Pi + cap; W.Pd = W.Pp + cap; W.Pf = W.Pd + cap; W.Pr = W.Pf + cap;
-  W.Qt = reinterpret_cast<uint64_t*>(W.Pr + cap);                  // cap is even: 8-byte aligned
-  W.Qr = reinterpret_cast<uint32_t*>(W.Qt + cap); W.Qs = W.Qr + cap;
-  uint32_t lo = ~0u, hi = 0;
-  for (uint32_t i = ln; i < n; i += 64) {
-    const uint32_t r = list[i];
-    const gg_cmsg& m = cur[r];
-    const uint32_t a = pos_of(m.hop), z = pos_of(m.dst);
-    W.Pt[i] = m.arrival_ps; W.Ph[i] = m.send_ps; W.Pk[i] = ((uint64_t)m.src << 32) | m.seq; W.Pz[i] = m.zero_load_ps;
-    W.Pi[i] = r; W.Pp[i] = a; W.Pd[i] = z;
-    if (m.arrival_ps >> 51) atomicOr(S.err, GG_DERR_CAP);        // batch keys are time << 12 | rank
-    W.Pf[i] = (uint32_t)nflits(P.np, has_data(m.type) ? P.bits_data : P.bits_req);
-    const uint32_t zz = dir ? min(z - 1, sd.hi) : max(z + 1, sd.lo);
-    lo = min(lo, min(a, zz)); hi = max(hi, max(a, zz));
+  const uint32_t n = *n_dev;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t r = rec_shard(S, b[i]) / per_rank;
+    gg_cmsg* sl = slots + (size_t)r * (region + 1);
+    const uint64_t j = atomicAdd((unsigned long long*)&sl[0].addr, 1ull);
+    if (j < region) sl[1 + j] = b[i];
+    else atomicOr(S.err, GG_DERR_CAP);
   }
-  for (uint32_t i = ln; i < npos * kNetCtr; i += 64) lc[i] = 0;
-  lo = wave_min(lo);
-  hi = (uint32_t)(~wave_min(~hi));
-  tsync();
-  // canonical ranks (by send time, sender, seq)
-  for (uint32_t i = ln; i < n; i += 64) {
-    const uint64_t hi_ = W.Ph[i], ki = W.Pk[i];
-    uint32_t r = 0;
-    for (uint32_t j = 0; j < n; ++j) { const uint64_t hj = W.Ph[j]; r += hj < hi_ || (hj == hi_ && W.Pk[j] < ki); }
-    W.Pr[i] = r;
-  }
-  tsync();
-  const bool qm = P.np.qm != 0;
-  const bool regq = qm && P.np.qtype == GG_QM_HISTORY_TREE && P.np.max_size <= kQMax;
-  const uint64_t zps = lat_to_ps((uint64_t)P.np.router_delay + P.np.link_delay, P.np.f);
-  uint64_t* K = W.Qt; uint32_t* B = W.Qr; uint32_t* O = W.Qs;
-  for (uint32_t s_ = 0; lo <= hi && s_ <= hi - lo; ++s_) {
-    const uint32_t pos = dir ? lo + s_ : hi - s_;
-    uint32_t m = 0;
-    for (uint32_t b0 = 0; b0 < n; b0 += 64) {
-      const uint32_t i = b0 + ln;
-      const bool at = i < n && W.Pp[i] == pos && (W.Pf[i] >> 24) == 0;
-      const uint64_t bm = __ballot(at);
-      if (at) {
-        const uint32_t k = m + (uint32_t)__builtin_popcountll(bm & ((1ull << ln) - 1));
-        B[k] = i; K[k] = (W.Pt[i] << 12) | W.Pr[i];
-      }
-      m += (uint32_t)__builtin_popcountll(bm);
-    }
-    if (m == 0) continue;
-    tsync();
-    for (uint32_t k = ln; k < m; k += 64) {
-      const uint64_t kk = K[k];
-      uint32_t r = 0;
-      for (uint32_t j = 0; j < m; ++j) r += K[j] < kk;
-      O[r] = B[k];
-    }
-    tsync();
-    const uint64_t qi = (uint64_t)tile_at(pos) * 6 + port;
-    HTree tr{S.nq + qi, S.nnd + qi * P.np.max_size, 1, P.np.analytical != 0};
-    RegQueue rq;
-    if (regq) rq.load(tr.q, tr.nd, 1, P.np.analytical != 0, ln);
-    auto request = [&](uint64_t t, uint32_t nf) -> uint64_t {
-      if (!qm) return 0;
-      const uint64_t tc = time_to_cycles(t, P.np.f);
-      return regq ? rq.request<false>(tc, nf, S.err) : tr.delay(tc, nf, S.err);
-    };
-    const uint32_t nx = dir ? pos + 1 : pos - 1;
-    uint64_t cq = 0, cf = 0;
-    for (uint32_t k = 0; k < m; ++k) {
-      const uint32_t i = O[k];
-      cq += serve_packet(P, S, W, request, i, nx, sd, zps, cf);
-      if (ln == 0) W.Pp[i] = nx;
-      tsync();
-    }
-    if (regq) rq.store(tr.q, tr.nd);
-    if (ln == 0) {
-      uint64_t* l = lc + (size_t)(pos - sd.lo) * kNetCtr;
-      l[0] += qm ? cq : 0; l[1] += qm ? m : 0; l[2] += cf; l[3] += m; l[4] += cf; l[5] += cf;
-    }
-    tsync();
-  }
-  // hand-off
-  uint32_t nb = 0;
-  for (uint32_t i = ln; i < n; i += 64) {
-    const uint32_t r = W.Pi[i], stt = W.Pf[i] >> 24;
-    const uint32_t h = tile_at(W.Pp[i]);
-    gg_cmsg* m = cur + r;
-    const uint64_t z = W.Pz[i];
-    m->arrival_ps = W.Pt[i]; m->zero_load_ps = z; m->hop = h;
-    if (stt == 2) {                                            // held for the quantum boundary
-      gg_cmsg g = *m;
-      g.arrival_ps = W.Pt[i]; g.zero_load_ps = z; g.hop = h;
-      if (!hk.bnd_put(g)) { atomicOr(S.err, GG_DERR_CAP); continue; }
-      ++nb;
-      continue;
-    }
-    const uint32_t dst = m->dst;
-    if (h == dst) {                                            // the SELF port of the destination, next step
-      const int32_t ld = S.ltile[dst];
-      const uint32_t j = hk.arv_slot(p ^ 1u, (uint32_t)ld);
-      if (j == ~0u) { atomicOr(S.err, GG_DERR_CAP); continue; }
-      arv(S, p ^ 1u)[(size_t)ld * P.IC + j] = r;
-    } else {                                                   // X done: the Y segment of the destination column
-      bool is_x;
-      const uint32_t s2 = xy_stage_seg(P, S, h, dst, is_x);
-      const uint32_t j = hk.seg_slot(false, s2);
-      if (j == ~0u) { atomicOr(S.err, GG_DERR_CAP); continue; }
-      S.yl[(size_t)s2 * P.seg_cap + j] = r;
-    }
-  }
-  nb = wave_sum(nb);
-  if (ln == 0 && nb) hk.step_counts(0, 0, 0, nb, 0);
-  for (uint32_t i = ln; i < npos * 6u; i += 64) {
-    const uint32_t q = i / 6, f = i % 6;
-    const uint64_t* l = lc + (size_t)q * kNetCtr;
-    const uint32_t tl = tile_at(sd.lo + q);
-    switch (f) {
-    case 0: cadd(S.ctr, tl, GG_NC_ROUTER_CONTENTION_CYCLES, l[0]); break;
-    case 1: cadd(S.ctr, tl, GG_NC_ROUTER_PACKETS, l[1]); break;
-    case 2: cadd(S.ctr, tl, GG_NC_BUFFER_WRITES, l[2]); cadd(S.ctr, tl, GG_NC_BUFFER_READS, l[2]); break;
-    case 3: cadd(S.ctr, tl, GG_NC_SWITCH_ALLOC, l[3]); break;
-    case 4: cadd(S.ctr, tl, GG_NC_CROSSBAR, l[4]); break;
-    default: cadd(S.ctr, tl, GG_NC_LINK_TRAVERSALS, l[5]); break;
-    }
-  }
-  tsync();
 }
-
-// a record of the quantum boundary held for this shard (import_one with the
-// shard's LDS counters): a message into the inbox of step 0 (pool 1), a held
-// packet into step 0's walk (pool 0) or the destination's SELF list of step 1
-__device__ __forceinline__ void shard_import(const CP& P, const CS& S, const ShardHooks& hk, const gg_cmsg& m)
+__global__ void k_round_status(const uint64_t* st, const gg_cmsg* slots, uint32_t world, uint64_t region,
+                               const uint32_t* err, uint32_t host_err, uint64_t* dv)
 {
-  const uint32_t at = m.hop == GG_HOP_NONE ? m.dst : m.hop;
-  if (at >= P.T || m.dst >= P.T || S.ltile[at] < 0) { atomicOr(S.err, GG_DERR_STATE); return; }
-  if (m.hop == GG_HOP_NONE) {
-    const uint32_t r = atomicAdd(&hk.A.h->npool[1], 1u);
-    if (r >= P.sh_pcap) { atomicOr(S.err, GG_DERR_CAP); return; }
-    S.pool1[hk.pbase + r] = m;
-    const int32_t ld = S.ltile[m.dst];
-    const uint32_t j = hk.inbox_slot(0, (uint32_t)ld);
-    if (j == ~0u) { atomicOr(S.err, GG_DERR_CAP); return; }
-    S.inb0[(size_t)ld * P.IC + j] = hk.pbase + r;
-    return;
+  if (threadIdx.x != 0) return;
+  uint64_t sent = 0, mx = 0;
+  for (uint32_t r = 0; r < world; ++r) {
+    const uint64_t c = slots[(size_t)r * (region + 1)].addr;
+    sent += c; mx = c > mx ? c : mx;
   }
-  const uint32_t r = atomicAdd(&hk.A.h->npool[0], 1u);
-  if (r >= P.sh_pcap) { atomicOr(S.err, GG_DERR_CAP); return; }
-  S.pool0[hk.pbase + r] = m;
-  atomicAdd(&hk.A.h->imp_held, 1u);
-  if (m.hop == m.dst) {
-    const int32_t ld = S.ltile[m.dst];
-    const uint32_t j = hk.arv_slot(1, (uint32_t)ld);
-    if (j == ~0u) { atomicOr(S.err, GG_DERR_CAP); return; }
-    S.arv1[(size_t)ld * P.IC + j] = hk.pbase + r;
-    return;
-  }
-  bool is_x;
-  const uint32_t sg = xy_stage_seg(P, S, m.hop, m.dst, is_x);
-  const uint32_t j = hk.seg_slot(is_x, sg);
-  if (j == ~0u) { atomicOr(S.err, GG_DERR_CAP); return; }
-  (is_x ? S.xl : S.yl)[(size_t)sg * P.seg_cap + j] = hk.pbase + r;
+  dv[0] = sent; dv[1] = st[0]; dv[2] = st[1];
+  dv[3] = (uint64_t)(*err | host_err); dv[4] = mx;
+  dv[5] = st[2];
 }
-
-template <bool HR>
-__global__ void __launch_bounds__(kShardThreads) k_c_shard(CP P, CS S, uint64_t tlimit)
+__global__ void k_c_import_slots(CP P, CS S, const gg_cmsg* slots, uint64_t region, uint64_t lo, uint64_t hi,
+                                 const uint64_t* skip)
 {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const uint32_t s = blockIdx.x, ns = gridDim.x, tid = threadIdx.x, ln = tid & 63, wv = tid >> 6;
-  const ShardArr A = shard_arr(P, smem);
-  ShardHdr* h = A.h;
-  const uint32_t t0 = S.sh_toff[s], nt = S.sh_toff[s + 1] - t0;
-  const bool hbh = P.net == GG_NET_EMESH_HOP_BY_HOP;
-  uint8_t* area = smem + (size_t)wv * P.sh_wave;
-  StepLdsS& sl = *reinterpret_cast<StepLdsS*>(area);
-  uint8_t* garea = S.wscr + ((size_t)s * kShardWaves + wv) * P.sh_gbytes;
-  const uint64_t qps = S.qs[QS_QPS];
-  const uint64_t t_begin = __builtin_amdgcn_s_memrealtime();
-  if (tid < sizeof(ShardHdr) / 4) reinterpret_cast<uint32_t*>(h)[tid] = 0;
-  for (uint32_t i = tid; i < 2 * P.sh_nt; i += kShardThreads) { A.ninb[i] = 0; A.narv[i] = 0; A.listed[i] = 0; }
-  for (uint32_t i = tid; i < P.sh_nxs; i += kShardThreads) A.nsx[i] = 0;
-  for (uint32_t i = tid; i < P.sh_nys; i += kShardThreads) A.nsy[i] = 0;
-  for (uint32_t i = tid; i < nt; i += kShardThreads) {
-    const uint32_t lt = S.sh_tiles[t0 + i];
-    const uint64_t r = S.rec[lt];
-    A.nst[i] = r >= S.rec_end[lt] ? kNsFin : S.blocked[lt] ? kNsBlk
-             : S.clk[lt] + (uint64_t)((S.meta[r] & 0x7FFFFFFFu) >> 1) * P.gap_ps;
-  }
-  __syncthreads();
-  uint64_t q = 0, Q = 0, done = 0;
-  uint32_t gen = 0;
-  const uint32_t wcap = (P.sh_wave - kNetCtr * 8 * P.sh_segmax) / kWalkPkBytes & ~1u;   // packets in a wave's LDS area
-  for (;;) {
-    const uint64_t barrier = (q + 1) * qps;
-    const ShardHooks hk{P, S, A, s * P.sh_pcap, S.sbnd + ((size_t)(Q & 1) * ns + s) * P.sh_bcap};
-    uint32_t k = 0;
-    for (;; ++k) {
-      const uint32_t p = k & 1u;
-      if (k == 0)      // step 0: every tile with a record before the barrier (imports listed theirs)
-        for (uint32_t i = tid; i < nt; i += kShardThreads)
-          if (A.nst[i] < barrier) hk.list_tile(0, i, S.sh_tiles[t0 + i]);
-      if (tid == 0) {
-        h->npool[p ^ 1u] = 0; h->sent[p] = 0; h->ht = 0;
-        if (k > 0) h->nwl[p ^ 1u] = 0;                       // the previous step's list, consumed
-      }
-      __syncthreads();
-      const uint64_t c0 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
-      // ---- tiles: one per wave
-      const uint32_t nw = rfl(h->nwl[p]);
-      for (;;) {
-        uint32_t i = 0;
-        if (ln == 0) i = atomicAdd(&h->ht, 1u);
-        i = rfl((uint32_t)__shfl((int)i, 0));
-        if (i >= nw) break;
-        // wave-uniform values in scalar registers: every address of the tile step derives from them
-        const uint32_t lt = rfl(A.wl[p * P.sh_nt + i]);
-        const uint32_t si = rfl(S.tsi[lt]);
-        const uint32_t na = hbh ? rfl(A.narv[p * P.sh_nt + si]) : 0u, ni = rfl(A.ninb[p * P.sh_nt + si]);
-        if (ln == 0) A.listed[p * P.sh_nt + si] = 0;
-        TilePre pre;
-        pre.load(S, lt, ln);
-        TraceWin W{~0ull, 0, 0};
-        const uint64_t nx = tile_step<false, HR>(P, S, lt, k, k, barrier, W, sl, nullptr, pre, hk, na, ni);
-        if (ln == 0) A.nst[si] = nx;
-        tsync();
-      }
-      __syncthreads();
-      const uint64_t c1 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
-      if (S.prof && tid == 0) {
-        unsigned long long* pr = S.prof + 200 + 16 * s;
-        pr[0] += c1 - c0; pr[1] += nw; pr[2] += 1;
-      }
-      // ---- walks: one segment per wave, X then Y
-      if (hbh) {
-        for (int stage = 0; stage < 2; ++stage) {
-          const uint32_t nsg = rfl(stage == 0 ? h->nxw : h->nyw);
-          uint32_t* cursor = stage == 0 ? &h->hx : &h->hy;
-          for (;;) {
-            uint32_t i = 0;
-            if (ln == 0) i = atomicAdd(cursor, 1u);
-            i = rfl((uint32_t)__shfl((int)i, 0));
-            if (i >= nsg) break;
-            const uint32_t sg = rfl((stage == 0 ? A.xwl : A.ywl)[i]);
-            uint32_t* cnt = (stage == 0 ? A.nsx : A.nsy) + rfl(S.seg_loc[(uint32_t)stage * P.sh_segw + sg]);
-            const uint32_t n = min(rfl(*cnt), P.seg_cap);
-            uint64_t* lc = reinterpret_cast<uint64_t*>(area);
-            if (n <= wcap) {
-              walk_sweep_wave(P, S, hk, p, stage, sg, n, area + (size_t)kNetCtr * 8 * P.sh_segmax, wcap, lc);
-            } else if (n <= P.sh_gpk) {
-              walk_sweep_wave(P, S, hk, p, stage, sg, n, garea, P.sh_gpk, lc);
-            } else if (ln == 0) {
-              atomicOr(S.err, GG_DERR_CAP);
-            }
-            if (ln == 0) *cnt = 0;
-            tsync();
-          }
-          __syncthreads();
-        }
-        // the walk lists are empty again (imports at the quantum boundary fill step 0's)
-        if (tid == 0) { h->hx = 0; h->hy = 0; h->nxw = 0; h->nyw = 0; }
-      }
-      if (S.prof && tid == 0) {
-        unsigned long long* pr = S.prof + 200 + 16 * s;
-        pr[3] += __builtin_amdgcn_s_memtime() - c1;
-      }
-      const uint32_t sent = h->sent[p] + (k == 0 ? h->imp_held : 0u);
-      if (sent == 0) break;
-      if (k + 1 >= kShardMaxSteps) { if (tid == 0) atomicOr(S.err, GG_DERR_STATE); break; }
-    }
-    // ---- quantum end: this shard's statistics into its slot, then the grid barrier
-    const uint64_t c2 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
-    {
-      unsigned long long act = 0, blk = 0, mn = ~0ull;
-      for (uint32_t i = tid; i < nt; i += kShardThreads) {
-        const uint64_t v = A.nst[i];
-        if (v != kNsFin) { ++act; if (v == kNsBlk) ++blk; else mn = v < mn ? v : mn; }
-      }
-      act = wave_sum64(act); blk = wave_sum64(blk); mn = wave_min64(mn);
-      if (tid == 0) { h->act = 0; h->blk = 0; h->mn = ~0ull; }
-      __syncthreads();
-      if (ln == 0) { atomicAdd(&h->act, act); atomicAdd(&h->blk, blk); atomicMin(&h->mn, mn); }
-      __syncthreads();
-      if (tid == 0) {
-        uint64_t* sl_ = S.sh_slot + ((size_t)(Q & 1) * ns + s) * kShardSlot;
-        sl_[0] = h->act; sl_[1] = h->blk; sl_[2] = h->mn; sl_[3] = h->nbnd; sl_[4] = k + 1;
-      }
-    }
-    grid_sync(S, gen);
-    const uint64_t c3 = S.prof ? __builtin_amdgcn_s_memtime() : 0;
-    const uint32_t err = __hip_atomic_load(S.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint64_t active = 0, blocked = 0, mn = ~0ull, nb = 0, steps = 0;
-    for (uint32_t j = 0; j < ns; ++j) {
-      const uint64_t* sl_ = S.sh_slot + ((size_t)(Q & 1) * ns + j) * kShardSlot;
-      active += sl_[0]; blocked += sl_[1]; mn = sl_[2] < mn ? sl_[2] : mn;
-      nb += min(sl_[3], (uint64_t)P.sh_bcap); steps = sl_[4] > steps ? sl_[4] : steps;
-    }
-    uint64_t nq = q + 1;
-    if (active == 0 && nb == 0) done = 1;
-    else if (nb == 0 && blocked == 0) nq = max(q + 1, mn / qps);
-    else if (nb == 0) done = 2;                                       // blocked, nothing in flight: deadlock
-    if (s == 0 && tid == 0) { S.ri[GG_RI_QUANTA]++; S.ri[GG_RI_FINAL_QUANTUM] = q; S.ri[GG_RI_STEPS] += steps; }
-    if (!done && (err || __builtin_amdgcn_s_memrealtime() - t_begin > tlimit)) {
-      if (s == 0 && tid == 0) atomicOr(S.err, err ? 0u : GG_DERR_STATE);
-      done = 3;
-    }
-    if (done) break;
-    // ---- import the records held for this shard into the next quantum
-    if (tid == 0) {
-      h->npool[0] = 0; h->npool[1] = 0; h->nwl[0] = 0; h->nwl[1] = 0; h->imp_held = 0; h->nbnd = 0;
-    }
-    __syncthreads();
-    for (uint32_t j = 0; j < ns; ++j) {
-      const uint64_t* sl_ = S.sh_slot + ((size_t)(Q & 1) * ns + j) * kShardSlot;
-      const uint32_t c = (uint32_t)min(sl_[3], (uint64_t)P.sh_bcap);
-      const gg_cmsg* reg = S.sbnd + ((size_t)(Q & 1) * ns + j) * P.sh_bcap;
-      for (uint32_t i = tid; i < c; i += kShardThreads) {
-        const gg_cmsg m = reg[i];
-        const uint32_t at = m.hop == GG_HOP_NONE ? m.dst : m.hop;
-        if (at < P.T && S.shard[at] - P.sh_k0 == s) shard_import(P, S, hk, m);
-      }
-    }
-    __syncthreads();
-    if (S.prof && tid == 0) {
-      unsigned long long* pr = S.prof + 200 + 16 * s;
-      pr[4] += c3 - c2; pr[5] += __builtin_amdgcn_s_memtime() - c3; pr[6] += 1;
-    }
-    ++Q;
-    q = nq;
-  }
-  if (tid == 0) {
-    if (h->ri_net) atomicAdd((unsigned long long*)&S.ri[GG_RI_NET_MSGS], h->ri_net);
-    if (h->ri_self) atomicAdd((unsigned long long*)&S.ri[GG_RI_SELF_MSGS], h->ri_self);
-    if (h->ri_bnd) atomicAdd((unsigned long long*)&S.ri[GG_RI_BOUNDARY_MSGS], h->ri_bnd);
-    if (s == 0) { S.qs[QS_DONE] = done; S.qs[QS_Q] = q; S.qs[QS_COUNT] = Q; }
-  }
+  if (skip && *skip) return;
+  const gg_cmsg* sl = slots + (size_t)blockIdx.y * (region + 1);
+  const uint64_t c = sl[0].addr;
+  const uint64_t e = c < hi ? c : hi;
+  for (uint64_t i = lo + blockIdx.x * blockDim.x + threadIdx.x; i < e; i += (uint64_t)gridDim.x * blockDim.x)
+    import_one(P, S, sl[1 + i], &S.imp[0]);
 }
 
 }  // namespace
@@ -2946,14 +2498,10 @@ struct gg_coh_state {
   uint32_t wtx = 64, wty = 64;          // threads of an X / Y walker workgroup
   bool persist_lc = false;
   bool begun = false;
-  // k_c_shard (one workgroup per owned logical shard): usable, dynamic LDS bytes
-  bool shard_ok = false;
-  size_t shard_lds = 0;
-  uint32_t shard_n = 0;
   // live kernel timing (gg_set_timing): an event pair around every
-  // kTimeSample-th launch of each kernel (a pair around every launch costs
-  // ~18 % of a hop-by-hop run), harvested at the batch syncs; since
-  // gg_coherent_begin
+  // kTimeSample-th launch of each kernel (mode 1; a pair around every launch,
+  // mode 2, costs ~18 % of a hop-by-hop run), harvested at the batch syncs;
+  // since gg_coherent_begin
   std::vector<hipEvent_t> tev;
   std::vector<int> tkind;
   uint32_t tused = 0;
@@ -2972,11 +2520,11 @@ static void launch_walk(gg_coh_state* C, hipStream_t s, uint32_t blocks, uint32_
 constexpr uint32_t kPersistTiles = 64;        // owned tiles up to which gg_coherent_run uses k_c_persist
 constexpr uint32_t kPersistLaunches = 16384;  // launch indices per k_c_persist launch
 static const char* kKernelNames[5] = {"coherent_step", "coherent_walk_x", "coherent_walk_y", "coherent_persist",
-                                     "coherent_shard"};
+                                     "coherent_unused"};
 
 template <class F> static void timed_launch(gg_ctx* ctx, gg_coh_state* C, hipStream_t s, int kind, F&& fn)
 {
-  if (!ctx->timing || C->nlaunch[kind]++ % kTimeSample) { fn(); return; }
+  if (!ctx->timing || C->nlaunch[kind]++ % (ctx->timing >= 2 ? 1 : kTimeSample)) { fn(); return; }
   if (C->tev.size() < 2 * (size_t)(C->tused + 1)) {
     const size_t n0 = C->tev.size();
     C->tev.resize(n0 + 512);
@@ -3263,66 +2811,6 @@ static gg_status coh_alloc(gg_ctx* ctx)
   S.ctr = gg_noc_ctr(ctx);
   gg_noc_queues(ctx, &S.nq, &S.nnd);
   S.err = ctx->err_dev;
-  // k_c_shard: one workgroup per owned logical shard (gg_coherent_run)
-  {
-    const uint32_t ns = k1 - k0;
-    std::vector<uint32_t> toff(ns + 1, 0), tl, tsi(P.L, 0);
-    for (uint32_t sh = 0; sh < ns; ++sh) {
-      toff[sh] = (uint32_t)tl.size();
-      for (uint32_t l = 0; l < P.L; ++l)
-        if (shard[gtile[l]] == k0 + sh) { tsi[l] = (uint32_t)tl.size() - toff[sh]; tl.push_back(l); }
-    }
-    toff[ns] = (uint32_t)tl.size();
-    uint32_t nt = 1;
-    for (uint32_t sh = 0; sh < ns; ++sh) nt = std::max(nt, toff[sh + 1] - toff[sh]);
-    const uint32_t segw = std::max(std::max(P.nsx, P.nsy), 1u);
-    std::vector<uint32_t> segloc(2 * (size_t)segw, 0), nx(ns, 0), ny(ns, 0);
-    for (uint32_t sg = 0; sg < P.nsx; ++sg) {
-      const Seg& g = segx[sg >> 1];
-      const uint32_t sh = shard[g.line * P.mw + g.lo] - k0;
-      segloc[sg] = nx[sh]++;
-    }
-    for (uint32_t sg = 0; sg < P.nsy; ++sg) {
-      const Seg& g = segy[sg >> 1];
-      const uint32_t sh = shard[g.lo * P.mw + g.line] - k0;
-      segloc[segw + sg] = ny[sh]++;
-    }
-    uint32_t nxs = 1, nys = 1;
-    for (uint32_t sh = 0; sh < ns; ++sh) { nxs = std::max(nxs, nx[sh]); nys = std::max(nys, ny[sh]); }
-    P.sh_nt = nt; P.sh_nxs = nxs; P.sh_nys = nys; P.sh_segw = segw; P.sh_segmax = maxrun; P.sh_k0 = k0;
-    const size_t walk_need = (size_t)kNetCtr * 8 * maxrun + 192 * (size_t)kWalkPkBytes;
-    P.sh_wave = (uint32_t)((std::max(sizeof(StepLdsS), walk_need) + 15) & ~(size_t)15);
-    P.sh_arr = kShardWaves * P.sh_wave;
-    C->shard_lds = P.sh_arr + shard_arr_bytes(nt, nxs, nys);
-    P.sh_pcap = P.msg_cap / ns;
-    P.sh_bcap = P.msg_cap / ns;
-    P.sh_gpk = (uint32_t)std::min<uint64_t>(P.seg_cap, 16384) & ~1u;
-    P.sh_gbytes = (uint32_t)(((size_t)P.sh_gpk * kWalkPkBytes + 15) & ~(size_t)15);
-    C->shard_n = ns;
-    const char* se = getenv("GG_COH_SHARD");
-    const bool want = se && atoi(se) != 0;                 // A/B form until it beats the per-step launches
-    bool ok = want && C->shard_lds <= 160 * 1024 && ns <= (uint32_t)ctx->num_cus;
-    if (ok) {
-      for (const void* fn : {(const void*)k_c_shard<true>, (const void*)k_c_shard<false>}) {
-        GG_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C->shard_lds));
-        int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kShardThreads, C->shard_lds) != hipSuccess ||
-            per_cu < 1)
-          ok = false;
-      }
-    }
-    if (ok) {
-      const bool hbh = P.net == GG_NET_EMESH_HOP_BY_HOP;
-      if ((st = dupload(C, &S.tsi, tsi))) return st;
-      if ((st = dupload(C, &S.sh_toff, toff))) return st;
-      if ((st = dupload(C, &S.sh_tiles, tl))) return st;
-      if ((st = dupload(C, &S.seg_loc, segloc))) return st;
-      if ((st = dalloc(C, &S.sh_slot, 2 * (uint64_t)ns * kShardSlot))) return st;
-      if ((st = dalloc(C, &S.sbnd, 2 * (uint64_t)ns * P.sh_bcap))) return st;
-      if ((st = dalloc(C, &S.wscr, hbh ? (uint64_t)ns * kShardWaves * P.sh_gbytes : 1))) return st;
-    }
-    C->shard_ok = ok;
-  }
   return GG_OK;
 }
 
@@ -3374,12 +2862,14 @@ gg_status gg_coherent_begin(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_ou
   return coh_check(ctx);
 }
 
-gg_status gg_coherent_quantum(gg_ctx* ctx, uint64_t q, gg_coherent_status* out)
+// the steps of quantum q on the owned shards (host-driven batches, one sync
+// per batch to look at the quiet flag), then, enqueued without a sync: the
+// step counters reset for the next quantum, the status kernel into
+// C->status_dev = {active, blocked, min next start, -} and the run-info
+// quantum count
+static gg_status coh_quantum_steps(gg_ctx* ctx, uint64_t q)
 {
-  if (!ctx || !out) return gg_fail(GG_ERR_INVALID, "NULL argument");
   gg_coh_state* C = ctx->coh;
-  if (!C || !C->begun) return gg_fail(GG_ERR_INVALID, "gg_coherent_begin first");
-  hipSetDevice(ctx->device);
   hipStream_t s = ctx->last_stream;
   const CP& P = C->P;
   const uint64_t quantum_ps = (uint64_t)ctx->cfg.quantum_ns * 1000ull;
@@ -3406,26 +2896,90 @@ gg_status gg_coherent_quantum(gg_ctx* ctx, uint64_t q, gg_coherent_status* out)
   }
   // the next quantum starts from empty step counters (ring, quiet, imported packets)
   GG_HIP(hipMemsetAsync(C->S.ring, 0, sizeof(uint32_t) * 7, s));
-  uint64_t init[4] = {0, 0, ~0ull, 0};
+  const uint64_t init[4] = {0, 0, ~0ull, 0};
   GG_HIP(hipMemcpyAsync(C->status_dev, init, sizeof(init), hipMemcpyHostToDevice, s));
   hipLaunchKernelGGL(k_c_status, dim3((P.L + 63) / 64), dim3(64), 0, s, P, C->S, C->status_dev);
+  hipLaunchKernelGGL(k_c_ri_quantum, dim3(1), dim3(1), 0, s, C->S, q);
   GG_HIP(hipGetLastError());
+  return GG_OK;
+}
+
+gg_status gg_coherent_quantum(gg_ctx* ctx, uint64_t q, gg_coherent_status* out)
+{
+  if (!ctx || !out) return gg_fail(GG_ERR_INVALID, "NULL argument");
+  gg_coh_state* C = ctx->coh;
+  if (!C || !C->begun) return gg_fail(GG_ERR_INVALID, "gg_coherent_begin first");
+  hipSetDevice(ctx->device);
+  hipStream_t s = ctx->last_stream;
+  if (gg_status st = coh_quantum_steps(ctx, q)) return st;
   uint64_t res[4];
   uint32_t nb = 0;
-  uint64_t ri[GG_NUM_RUN_INFO];
   GG_HIP(hipMemcpyAsync(res, C->status_dev, sizeof(res), hipMemcpyDeviceToHost, s));
   GG_HIP(hipMemcpyAsync(&nb, C->S.bnd_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-  GG_HIP(hipMemcpyAsync(ri, C->S.ri, sizeof(ri), hipMemcpyDeviceToHost, s));
   GG_HIP(hipStreamSynchronize(s));
-  ri[GG_RI_QUANTA]++;
-  ri[GG_RI_FINAL_QUANTUM] = q;
-  GG_HIP(hipMemcpyAsync(C->S.ri, ri, sizeof(ri), hipMemcpyHostToDevice, s));
   out->steps = 0;
   out->boundary_msgs = nb;
   out->min_next_ps = res[2];
   out->active_tiles = (uint32_t)res[0];
   out->blocked_tiles = (uint32_t)res[1];
   return coh_check(ctx);
+}
+
+// ---- the exchange of gg_round_exchange (gg_round.hip), enqueued on the
+// context's stream without a host sync.  Send slots: per destination rank r
+// a header record (word 0 = count) and `region` records; the records held at
+// the quantum boundary are scattered to the rank that owns their shard (export
+// order inside a slot does not matter: import lists them by atomics and every
+// consumer orders by the canonical keys).
+gg_status gg_coh_export_slots(gg_ctx* ctx, gg_cmsg* slots, uint32_t world, uint32_t per_rank, uint64_t region)
+{
+  gg_coh_state* C = ctx->coh;
+  if (!C || !C->begun) return gg_fail(GG_ERR_INVALID, "gg_coherent_begin first");
+  hipStream_t s = ctx->last_stream;
+  hipLaunchKernelGGL(k_slot_clear, dim3(1), dim3(64), 0, s, slots, world, region);
+  hipLaunchKernelGGL(k_c_export_slots, dim3(256), dim3(256), 0, s, C->S, (const gg_cmsg*)C->S.bnd,
+                     (const uint32_t*)C->S.bnd_cnt, per_rank, region, slots);
+  GG_HIP(hipMemsetAsync(C->S.bnd_cnt, 0, sizeof(uint32_t), s));
+  GG_HIP(hipGetLastError());
+  return GG_OK;
+}
+
+// the rank's status words for the all-reduces: dv = {records sent, active,
+// blocked | error flags, largest send-slot count | min next start}
+gg_status gg_coh_round_status(gg_ctx* ctx, const gg_cmsg* slots, uint32_t world, uint64_t region, uint32_t host_err,
+                              uint64_t* dv)
+{
+  gg_coh_state* C = ctx->coh;
+  if (!C || !C->begun) return gg_fail(GG_ERR_INVALID, "gg_coherent_begin first");
+  hipStream_t s = ctx->last_stream;
+  hipLaunchKernelGGL(k_round_status, dim3(1), dim3(64), 0, s, (const uint64_t*)C->status_dev, slots, world, region,
+                     (const uint32_t*)ctx->err_dev, host_err, dv);
+  GG_HIP(hipGetLastError());
+  return GG_OK;
+}
+
+// import records [lo, min(count, hi)) of every received slot; `first`: the
+// quantum's first import (the record pools of its first step start empty);
+// nothing when *skip_if_dev != 0 (the round's reduced error flag)
+gg_status gg_coh_import_slots(gg_ctx* ctx, const gg_cmsg* slots, uint32_t world, uint64_t region, uint64_t lo,
+                              uint64_t hi, bool first, const uint64_t* skip_if_dev)
+{
+  gg_coh_state* C = ctx->coh;
+  if (!C || !C->begun) return gg_fail(GG_ERR_INVALID, "gg_coherent_begin first");
+  hipStream_t s = ctx->last_stream;
+  if (first) GG_HIP(hipMemsetAsync(C->S.npool, 0, sizeof(uint32_t) * 2, s));
+  hipLaunchKernelGGL(k_c_import_slots, dim3(64, world), dim3(256), 0, s, C->P, C->S, slots, region, lo, hi, skip_if_dev);
+  GG_HIP(hipGetLastError());
+  return GG_OK;
+}
+
+gg_status gg_coh_check(gg_ctx* ctx) { return coh_check(ctx); }
+gg_status gg_coh_quantum_async(gg_ctx* ctx, uint64_t q)
+{
+  gg_coh_state* C = ctx->coh;
+  if (!C || !C->begun) return gg_fail(GG_ERR_INVALID, "gg_coherent_begin first");
+  hipSetDevice(ctx->device);
+  return coh_quantum_steps(ctx, q);
 }
 
 gg_status gg_coherent_export(gg_ctx* ctx, gg_cmsg* out_dev, uint64_t cap, uint64_t* per_shard_counts)
@@ -3496,26 +3050,10 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
   const CP& P = C->P;
   const bool hbh = P.net == GG_NET_EMESH_HOP_BY_HOP;
   uint32_t L = 0, batch = 16;
-  // one workgroup per logical shard for the whole run (k_c_shard)
-  if (C->shard_ok) {
-    GG_HIP(hipMemsetAsync(C->S.gbar, 0, sizeof(uint32_t), s));
-    const char* hr_env = getenv("GG_COH_SHARD_HR");
-    const bool hr = hr_env ? atoi(hr_env) != 0 : !hbh;      // L1 hit runs: the closed-form networks (long hit runs)
-    const uint64_t tlimit = 100000000ull * 600;               // s_memrealtime ticks (100 MHz): 10 minutes
-    timed_launch(ctx, C, s, 4, [&] {
-      if (hr)
-        hipLaunchKernelGGL(k_c_shard<true>, dim3(C->shard_n), dim3(kShardThreads), C->shard_lds, s, P, C->S, tlimit);
-      else
-        hipLaunchKernelGGL(k_c_shard<false>, dim3(C->shard_n), dim3(kShardThreads), C->shard_lds, s, P, C->S, tlimit);
-    });
-    GG_HIP(hipGetLastError());
-    GG_HIP(hipStreamSynchronize(s));
-    timed_harvest(C);
-  }
   // small meshes: the whole loop in persistent launches (k_c_persist), one
   // workgroup per owned tile, all resident (<= kPersistTiles << CUs)
   const char* np_env = getenv("GG_COH_NO_PERSIST");
-  const bool persist = !C->shard_ok && P.L <= kPersistTiles && !(np_env && atoi(np_env));
+  const bool persist = P.L <= kPersistTiles && !(np_env && atoi(np_env));
   while (persist) {
     GG_HIP(hipMemsetAsync(C->S.gbar, 0, sizeof(uint32_t), s));
     const char* nl_env = getenv("GG_COH_NO_LDS_CACHE");
@@ -3536,7 +3074,7 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
     timed_harvest(C);
     if (err || done) break;
   }
-  for (; !persist && !C->shard_ok;) {
+  for (; !persist;) {
     for (uint32_t b = 0; b < batch; ++b, ++L) {
       timed_launch(ctx, C, s, 0, [&] { hipLaunchKernelGGL(k_c_step, dim3(P.L), dim3(64), C->step_lds, s, P, C->S, L, 1u, (uint64_t)0); });
       if (hbh) {
@@ -3557,16 +3095,7 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
   }
   gg_timer_end(ctx, "coherent_run", s);
   GG_HIP(hipStreamSynchronize(s));
-  if (C->S.prof && C->shard_ok) {
-    std::vector<unsigned long long> h(1024);
-    GG_HIP(hipMemcpy(h.data(), C->S.prof, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
-    for (uint32_t k = 0; k < C->shard_n && k < 48; ++k) {
-      const unsigned long long* pr = &h[200 + 16 * k];
-      fprintf(stderr, "[gg_shard %u] steps %llu tiles %llu | cycles: tiles %llu walks %llu quantum-end+barrier %llu import %llu (quanta %llu)\n",
-              k, pr[2], pr[1], pr[0], pr[3], pr[4], pr[5], pr[6]);
-    }
-  }
-  if (C->S.prof && !C->shard_ok) {
+  if (C->S.prof) {
     // per-launch maxima in slots L mod 65536
     std::vector<unsigned long long> h(1024 + 8 * 65536);
     GG_HIP(hipMemcpy(h.data(), C->S.prof, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));

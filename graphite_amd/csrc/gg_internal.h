@@ -100,7 +100,7 @@ struct gg_ctx {
   // replay kernel choice: 0 = lean when instantiated (default), 1 = generic
   int replay_variant = 0;
   // timing
-  bool timing = false;
+  int timing = 0;                // gg_set_timing: 0 off, 1 sampled coherent launches, 2 every launch
   std::vector<gg_timer> timers;
   // multi-rank round buffers (gg_round.hip), freed by gg_destroy
   void* round = nullptr;
@@ -139,3 +139,11 @@ void      gg_coh_free(gg_ctx* ctx);
 gg_status gg_htree_run(gg_ctx* ctx, uint64_t min_proc, const uint64_t* t, const uint64_t* p, uint64_t n, uint64_t* d);
 gg_status gg_coh_kernel_stats(gg_ctx* ctx, const char* name, double* total_ms, uint64_t* launches);
 uint64_t  gg_coherent_msg_cap(gg_ctx* ctx);     // records a quantum boundary can hold (after gg_coherent_begin)
+// the quantum steps and the per-rank slot exchange of gg_round_exchange (gg_coherent.hip)
+gg_status gg_coh_quantum_async(gg_ctx* ctx, uint64_t q);
+gg_status gg_coh_export_slots(gg_ctx* ctx, gg_cmsg* slots, uint32_t world, uint32_t per_rank, uint64_t region);
+gg_status gg_coh_round_status(gg_ctx* ctx, const gg_cmsg* slots, uint32_t world, uint64_t region, uint32_t host_err,
+                              uint64_t* dv);
+gg_status gg_coh_import_slots(gg_ctx* ctx, const gg_cmsg* slots, uint32_t world, uint64_t region, uint64_t lo,
+                              uint64_t hi, bool first, const uint64_t* skip_if_dev);
+gg_status gg_coh_check(gg_ctx* ctx);

@@ -2,26 +2,40 @@
 // RCCL over xGMI: one process per GPU, each owning a block of logical shards.
 //
 // Reference: every process exchanges ShmemMsgs over its transport in real
-// time (common/transport/socktransport.cc) and the clocks meet at the lax
-// barrier once per quantum (clock_skew_management_schemes/
+// time (common/transport/socktransport.cc:401-448) and the clocks meet at the
+// lax barrier once per quantum (clock_skew_management_schemes/
 // lax_barrier_sync_client.cc:31-69, lax_barrier_sync_server.cc:57-160).
 // Here the records that cross a rank's shards are held to the quantum
-// boundary and exchanged there in one grouped send / receive
-// per peer; the status (records in flight, active / blocked tiles, earliest
-// next start) is all-reduced, and every rank derives the same next quantum
-// (the rule of oracle_coh_run and graphite_amd.coherent.next_quantum).
+// boundary and exchanged there in ONE grouped send / receive of
+// fixed-capacity per-peer slots (a header record carries the count, so no
+// count exchange precedes the data), followed by the status all-reduces and
+// the import — all enqueued on the context's stream, then one host sync.
+// Only a quantum whose records overflow a slot takes a second, sized round.
+//
+// Failure is decided collectively: a rank whose quantum or export failed still
+// posts every send / receive and all-reduce (with its error flag in the
+// max-reduced status word), the imports are skipped on the device when the
+// reduced flag is set, and every rank returns the error together — no peer is
+// left blocked inside RCCL.
 #include "gg_internal.h"
 
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <string>
 #include <vector>
 
 namespace {
 
+constexpr uint64_t kSlotDefault = 1024;   // records per peer and quantum sent in the fixed round (64 KB)
+constexpr int kDv = 8;                    // status words: sent, active, blocked | err, max slot count | min next
+
 struct RoundBufs {
-  gg_cmsg* send = nullptr; gg_cmsg* recv = nullptr; uint64_t* cnt = nullptr;   // cnt: [W] send, [W] recv, [4] status
-  uint64_t cap = 0; int world = 0;
+  gg_cmsg* send = nullptr; gg_cmsg* recv = nullptr;   // [world][1 + region] each
+  uint64_t* dv = nullptr;                             // [kDv + 2 * world]: status, send counts, recv counts
+  uint64_t* host = nullptr;                           // pinned copy of dv
+  uint64_t region = 0; int world = 0;
 };
 
 #define GG_NCCL(x)                                                                                         \
@@ -30,22 +44,44 @@ struct RoundBufs {
     if (r_ != ncclSuccess) return gg_fail(GG_ERR_STATE, "%s: %s", #x, ncclGetErrorString(r_));              \
   } while (0)
 
-gg_status bufs_for(gg_ctx* ctx, RoundBufs*& B, int world, uint64_t cap)
+void bufs_free(void* p)
+{
+  RoundBufs* b = static_cast<RoundBufs*>(p);
+  hipFree(b->send); hipFree(b->recv); hipFree(b->dv); hipHostFree(b->host);
+  delete b;
+}
+
+gg_status bufs_for(gg_ctx* ctx, RoundBufs*& B, int world, uint64_t region)
 {
   B = static_cast<RoundBufs*>(gg_round_state(ctx));
-  if (B && B->world == world && B->cap >= cap) return GG_OK;
-  if (B) { hipFree(B->send); hipFree(B->recv); hipFree(B->cnt); delete B; }
+  if (B && B->world == world && B->region >= region) return GG_OK;
+  if (B) bufs_free(B);
+  gg_round_state_set(ctx, nullptr, nullptr);
   B = new RoundBufs();
-  B->cap = cap; B->world = world;
-  GG_HIP(hipMalloc((void**)&B->send, sizeof(gg_cmsg) * cap));
-  GG_HIP(hipMalloc((void**)&B->recv, sizeof(gg_cmsg) * cap));
-  GG_HIP(hipMalloc((void**)&B->cnt, sizeof(uint64_t) * (2 * (size_t)world + 4)));
-  gg_round_state_set(ctx, B, [](void* p) {
-    RoundBufs* b = static_cast<RoundBufs*>(p);
-    hipFree(b->send); hipFree(b->recv); hipFree(b->cnt);
-    delete b;
-  });
+  B->region = region; B->world = world;
+  gg_round_state_set(ctx, B, bufs_free);
+  const size_t slots = (size_t)world * (region + 1);
+  GG_HIP(hipMalloc((void**)&B->send, sizeof(gg_cmsg) * slots));
+  GG_HIP(hipMalloc((void**)&B->recv, sizeof(gg_cmsg) * slots));
+  GG_HIP(hipMalloc((void**)&B->dv, sizeof(uint64_t) * (kDv + 2 * (size_t)world)));
+  GG_HIP(hipHostMalloc((void**)&B->host, sizeof(uint64_t) * (kDv + 2 * (size_t)world)));
   return GG_OK;
+}
+
+// the slot counts (header word 0) of the send and the received slots
+__global__ void k_slot_counts(const gg_cmsg* send, const gg_cmsg* recv, uint32_t world, uint64_t region, uint64_t* out)
+{
+  for (uint32_t r = threadIdx.x; r < world; r += blockDim.x) {
+    out[r] = send[(size_t)r * (region + 1)].addr;
+    out[world + r] = recv[(size_t)r * (region + 1)].addr;
+  }
+}
+
+uint64_t slot_records(uint64_t region)
+{
+  const char* e = getenv("GG_ROUND_SLOT");          // test knob: a small slot forces the overflow round
+  uint64_t v = e ? strtoull(e, nullptr, 10) : kSlotDefault;
+  return std::max<uint64_t>(1, std::min(v, region));
 }
 
 }  // namespace
@@ -67,59 +103,65 @@ gg_status gg_round_exchange(gg_ctx* ctx, void* nccl_comm, void* stream, uint64_t
                    (R + 1) * per, c.shard_begin, k1);
   hipSetDevice(ctx->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const uint64_t cap = gg_coherent_msg_cap(ctx);
-  if (!cap) return gg_fail(GG_ERR_INVALID, "gg_coherent_begin first");
+  if (s != ctx->last_stream) return gg_fail(GG_ERR_INVALID, "gg_round_exchange needs the stream of gg_coherent_begin");
+  const uint64_t region = gg_coherent_msg_cap(ctx);
+  if (!region) return gg_fail(GG_ERR_INVALID, "gg_coherent_begin first");
   RoundBufs* B = nullptr;
-  if (gg_status st = bufs_for(ctx, B, W, cap)) return st;
+  if (gg_status st = bufs_for(ctx, B, W, region)) return st;
+  const uint64_t slot = slot_records(region);
+  const size_t sbytes = sizeof(gg_cmsg) * (slot + 1);
 
-  gg_coherent_status st;
-  if (gg_status e = gg_coherent_quantum(ctx, q, &st)) return e;
-  std::vector<uint64_t> per_shard(K, 0);
-  if (gg_status e = gg_coherent_export(ctx, B->send, B->cap, per_shard.data())) return e;
-  std::vector<uint64_t> h(2 * (size_t)W + 4, 0);
-  uint64_t sent = 0;
-  for (int r = 0; r < W; ++r)
-    for (uint32_t k = r * per; k < (r + 1) * per; ++k) { h[r] += per_shard[k]; sent += per_shard[k]; }
-  // counts, then the records (grouped by destination rank: export orders them by shard)
-  GG_HIP(hipMemcpyAsync(B->cnt, h.data(), sizeof(uint64_t) * W, hipMemcpyHostToDevice, s));
+  // the quantum and the export; a failure turns into the error flag of the round
+  uint32_t herr = 0;
+  std::string emsg;
+  gg_status est = GG_OK;
+  if ((est = gg_coh_quantum_async(ctx, q)) || (est = gg_coh_export_slots(ctx, B->send, (uint32_t)W, per, region))) {
+    herr = GG_DERR_STATE;
+    emsg = gg_last_error();
+    (void)hipMemsetAsync(B->send, 0, sizeof(gg_cmsg) * (size_t)W * (region + 1), s);   // nothing to send
+  }
+  if (gg_status st = gg_coh_round_status(ctx, B->send, (uint32_t)W, region, herr, B->dv)) return st;
+  // ONE group: every peer's fixed slot; then the status all-reduces
   GG_NCCL(ncclGroupStart());
   for (int r = 0; r < W; ++r) {
-    GG_NCCL(ncclSend(B->cnt + r, 1, ncclUint64, r, comm, s));
-    GG_NCCL(ncclRecv(B->cnt + W + r, 1, ncclUint64, r, comm, s));
+    GG_NCCL(ncclSend(B->send + (size_t)r * (region + 1), sbytes, ncclUint8, r, comm, s));
+    GG_NCCL(ncclRecv(B->recv + (size_t)r * (region + 1), sbytes, ncclUint8, r, comm, s));
   }
   GG_NCCL(ncclGroupEnd());
-  GG_HIP(hipMemcpyAsync(h.data() + W, B->cnt + W, sizeof(uint64_t) * W, hipMemcpyDeviceToHost, s));
-  GG_HIP(hipStreamSynchronize(s));
-  uint64_t total = 0;
-  for (int r = 0; r < W; ++r) total += h[W + r];
-  if (total > B->cap) return gg_fail(GG_ERR_UNSUPPORTED, "%llu records arrive, the round buffer holds %llu",
-                                     (unsigned long long)total, (unsigned long long)B->cap);
-  uint64_t so = 0, ro = 0;
   GG_NCCL(ncclGroupStart());
-  for (int r = 0; r < W; ++r) {
-    if (h[r]) GG_NCCL(ncclSend(B->send + so, h[r] * sizeof(gg_cmsg), ncclUint8, r, comm, s));
-    if (h[W + r]) GG_NCCL(ncclRecv(B->recv + ro, h[W + r] * sizeof(gg_cmsg), ncclUint8, r, comm, s));
-    so += h[r]; ro += h[W + r];
+  GG_NCCL(ncclAllReduce(B->dv, B->dv, 3, ncclUint64, ncclSum, comm, s));
+  GG_NCCL(ncclAllReduce(B->dv + 3, B->dv + 3, 2, ncclUint64, ncclMax, comm, s));
+  GG_NCCL(ncclAllReduce(B->dv + 5, B->dv + 5, 1, ncclUint64, ncclMin, comm, s));
+  GG_NCCL(ncclGroupEnd());
+  // the received records (skipped on the device when any rank failed), the counts, one sync
+  if (gg_status st = gg_coh_import_slots(ctx, B->recv, (uint32_t)W, region, 0, slot, true, B->dv + 3)) return st;
+  hipLaunchKernelGGL(k_slot_counts, dim3(1), dim3(64), 0, s, B->send, B->recv, (uint32_t)W, region, B->dv + kDv);
+  GG_HIP(hipMemcpyAsync(B->host, B->dv, sizeof(uint64_t) * (kDv + 2 * (size_t)W), hipMemcpyDeviceToHost, s));
+  GG_HIP(hipStreamSynchronize(s));
+  const uint64_t* h = B->host;
+  if (h[3]) {
+    if (herr) return gg_fail(est ? est : GG_ERR_STATE, "%s", emsg.c_str());
+    if (gg_status st = gg_coh_check(ctx)) return st;
+    return gg_fail(GG_ERR_STATE, "quantum %llu failed on another rank", (unsigned long long)q);
   }
-  GG_NCCL(ncclGroupEnd());
-  GG_HIP(hipStreamSynchronize(s));
-  if (total) if (gg_status e = gg_coherent_import(ctx, B->recv, total)) return e;
-  // status over ranks: sums of (records in flight, active, blocked), min of the next start
-  uint64_t sum[3] = {sent, st.active_tiles, st.blocked_tiles}, mn = st.min_next_ps;
-  uint64_t* dv = B->cnt + 2 * W;
-  GG_HIP(hipMemcpyAsync(dv, sum, sizeof(sum), hipMemcpyHostToDevice, s));
-  GG_HIP(hipMemcpyAsync(dv + 3, &mn, sizeof(mn), hipMemcpyHostToDevice, s));
-  GG_NCCL(ncclGroupStart());
-  GG_NCCL(ncclAllReduce(dv, dv, 3, ncclUint64, ncclSum, comm, s));
-  GG_NCCL(ncclAllReduce(dv + 3, dv + 3, 1, ncclUint64, ncclMin, comm, s));
-  GG_NCCL(ncclGroupEnd());
-  GG_HIP(hipMemcpyAsync(sum, dv, sizeof(sum), hipMemcpyDeviceToHost, s));
-  GG_HIP(hipMemcpyAsync(&mn, dv + 3, sizeof(mn), hipMemcpyDeviceToHost, s));
-  GG_HIP(hipStreamSynchronize(s));
-  const uint64_t msgs = sum[0], active = sum[1], blocked = sum[2];
+  // a slot overflowed somewhere: every rank takes the sized round (the counts are known on both sides now)
+  if (h[4] > slot) {
+    const uint64_t* sc = h + kDv;
+    const uint64_t* rc = h + kDv + W;
+    GG_NCCL(ncclGroupStart());
+    for (int r = 0; r < W; ++r) {
+      const size_t o = (size_t)r * (region + 1) + 1 + slot;
+      if (sc[r] > slot) GG_NCCL(ncclSend(B->send + o, sizeof(gg_cmsg) * (sc[r] - slot), ncclUint8, r, comm, s));
+      if (rc[r] > slot) GG_NCCL(ncclRecv(B->recv + o, sizeof(gg_cmsg) * (rc[r] - slot), ncclUint8, r, comm, s));
+    }
+    GG_NCCL(ncclGroupEnd());
+    if (gg_status st = gg_coh_import_slots(ctx, B->recv, (uint32_t)W, region, slot, region, false, nullptr)) return st;
+    GG_HIP(hipStreamSynchronize(s));
+  }
+  const uint64_t msgs = h[0], active = h[1], blocked = h[2], mn = h[5];
   const uint64_t qps = (uint64_t)c.quantum_ns * 1000ull;
   *done = 0;
-  if (active == 0 && msgs == 0) { *done = 1; *next_q = q; return GG_OK; }
+  if (active == 0 && msgs == 0) { *done = 1; *next_q = q; return gg_coh_check(ctx); }
   if (msgs == 0 && blocked != 0) return gg_fail(GG_ERR_STATE, "coherent run deadlocked: tiles blocked with no message in flight");
   *next_q = (msgs == 0) ? std::max<uint64_t>(q + 1, mn / qps) : q + 1;
   return GG_OK;

@@ -13,6 +13,7 @@
 #include "gg_oracle.h"
 
 #include <math.h>
+#include <omp.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -1321,6 +1322,42 @@ int oracle_noc_route_tree(oracle_noc* on, uint64_t n, const uint32_t* src, const
  * after the quantum boundary.  Self packets (src == dst)
  * are left untouched (processCornerCases, network_model.cc:413-424).
  */
+/* One hop of packet k at router cur[k] (hop_by_hop.cc:223-256): XY port
+ * choice, RouterModel::processPacket (router_model.cc:71-108) through the
+ * port's queue, ElectricalLinkModel (electrical_link_model.cc:31-45); at the
+ * destination's SELF port the packet is received (network_model.cc:142-150). */
+enum { HOP_MOVED = 0, HOP_DELIVERED, HOP_HELD };
+static int hbh_hop(oracle_noc* on, uint64_t k, const uint32_t* dst, const uint32_t* len, uint32_t* cur,
+                   uint64_t* t, uint64_t* zl, uint64_t* ct, const uint32_t* shard, uint8_t* held)
+{
+  const double f = on->cfg.frequency_ghz;
+  const uint32_t c = cur[k];
+  const int cx = (int)(c % on->w), cy = (int)(c / on->w);
+  const int dx = (int)(dst[k] % on->w), dy = (int)(dst[k] / on->w);
+  int port; uint32_t next;
+  if (cx > dx)      { port = P_LEFT;  next = c - 1; }
+  else if (cx < dx) { port = P_RIGHT; next = c + 1; }
+  else if (cy > dy) { port = P_DOWN;  next = c - on->w; }
+  else if (cy < dy) { port = P_UP;    next = c + on->w; }
+  else              { port = P_SELF;  next = c; }
+  const uint64_t nf = n_flits(on, len[k]);
+  uint64_t zlc = on->cfg.router_delay, qd = 0;
+  uint64_t* cc = ncnt(on, c);
+  if (on->cfg.queue_model_enabled) {
+    qd = oracle_htree_delay(on->q[(size_t)c * NPORTS + port], time_to_cycles(t[k], f), nf);
+    cc[GG_NC_ROUTER_CONTENTION_CYCLES] += qd; cc[GG_NC_ROUTER_PACKETS]++;
+  }
+  cc[GG_NC_BUFFER_WRITES] += nf; cc[GG_NC_BUFFER_READS] += nf; cc[GG_NC_SWITCH_ALLOC] += 1; cc[GG_NC_CROSSBAR] += nf;
+  zlc += on->cfg.link_delay;
+  cc[GG_NC_LINK_TRAVERSALS] += nf;
+  const uint64_t zps = lat_to_ps(zlc, f), cps = lat_to_ps(qd, f);
+  t[k] += zps + cps; zl[k] += zps; ct[k] += cps;
+  if (port == P_SELF) { n_receive(on, dst[k], len[k], &t[k], &zl[k], ct[k]); return HOP_DELIVERED; }
+  cur[k] = next;
+  if (shard && shard[next] != shard[c]) { held[k] = 1; return HOP_HELD; }   /* leaves the shard: held */
+  return HOP_MOVED;
+}
+
 static void noc_hbh_walk(oracle_noc* on, uint64_t n, const uint32_t* src, const uint32_t* dst, const uint32_t* len,
                          uint32_t* cur, uint64_t* t, uint64_t* zl, uint64_t* ct, const uint8_t* inj,
                          const uint32_t* shard, uint8_t* held)
@@ -1361,37 +1398,148 @@ static void noc_hbh_walk(oracle_noc* on, uint64_t n, const uint32_t* src, const 
   /* 2. mesh hops in global (time, index) order (hop_by_hop.cc:223-256) */
   while (heap.n) {
     n_ev ev = heap_pop(&heap);
-    uint64_t k = ev.id;
-    uint32_t c = cur[k];
-    int cx = (int)(c % on->w), cy = (int)(c / on->w);
-    int dx = (int)(dst[k] % on->w), dy = (int)(dst[k] / on->w);
-    int port; uint32_t next;
-    if (cx > dx)      { port = P_LEFT;  next = c - 1; }
-    else if (cx < dx) { port = P_RIGHT; next = c + 1; }
-    else if (cy > dy) { port = P_DOWN;  next = c - on->w; }
-    else if (cy < dy) { port = P_UP;    next = c + on->w; }
-    else              { port = P_SELF;  next = c; }
-    uint64_t nf = n_flits(on, len[k]);
-    uint64_t zlc = on->cfg.router_delay, qd = 0;   /* RouterModel::processPacket (router_model.cc:71-108) */
-    uint64_t* cc = ncnt(on, c);
-    if (qm) {
-      qd = oracle_htree_delay(on->q[(size_t)c * NPORTS + port], time_to_cycles(t[k], f), nf);
-      cc[GG_NC_ROUTER_CONTENTION_CYCLES] += qd; cc[GG_NC_ROUTER_PACKETS]++;
-    }
-    cc[GG_NC_BUFFER_WRITES] += nf; cc[GG_NC_BUFFER_READS] += nf; cc[GG_NC_SWITCH_ALLOC] += 1; cc[GG_NC_CROSSBAR] += nf;
-    zlc += on->cfg.link_delay;                      /* ElectricalLinkModel::processPacket (electrical_link_model.cc:31-45) */
-    cc[GG_NC_LINK_TRAVERSALS] += nf;
-    uint64_t zps = lat_to_ps(zlc, f), cps = lat_to_ps(qd, f);
-    t[k] += zps + cps; zl[k] += zps; ct[k] += cps;
-    if (port == P_SELF) {
-      n_receive(on, dst[k], len[k], &t[k], &zl[k], ct[k]);
-    } else {
-      cur[k] = next;
-      if (shard && shard[next] != shard[c]) { held[k] = 1; continue; }   /* leaves the shard: held */
+    const uint64_t k = ev.id;
+    if (hbh_hop(on, k, dst, len, cur, t, zl, ct, shard, held) == HOP_MOVED) {
       n_ev ne = { t[k], k };
       heap_push(&heap, ne);
     }
   }
   free(heap.a);
+}
+
+/* The same walk, stage by stage on `threads` OpenMP threads (the tile-parallel
+ * CPU baseline, oracle_coh_set_threads).  A port's requests depend only on the
+ * ports before it on the packets' XY routes, and its order is (arrival time,
+ * packet index) whatever else runs: so the injection ports (per source), then
+ * the X hops row by row (each direction swept in its direction of travel,
+ * each position's batch in (time, index) order), then the Y hops column by
+ * column, then the SELF ports (per destination) see exactly the requests, in
+ * exactly the order, of the global event queue above — the GPU's stage
+ * decomposition.  Rows / columns / tiles run in parallel: each
+ * touches only its own routers' queues and counters. */
+static void hbh_sweep(oracle_noc* on, uint64_t m, uint64_t* ids, uint32_t npos, int stage, int dir,
+                      const uint32_t* dst, const uint32_t* len, uint32_t* cur, uint64_t* t, uint64_t* zl,
+                      uint64_t* ct, const uint32_t* shard, uint8_t* held, n_ev* tmp, uint64_t* nxt, uint64_t* head)
+{
+  /* per position a list of the packets there (row / column-local indices into ids) */
+  for (uint32_t p = 0; p < npos; ++p) head[p] = ~0ull;
+  const uint32_t W = on->w;
+  for (uint64_t i = 0; i < m; ++i) {
+    const uint32_t c = cur[ids[i]], p = stage == 0 ? c % W : c / W;
+    nxt[i] = head[p]; head[p] = i;
+  }
+  for (uint32_t s = 0; s < npos; ++s) {
+    const uint32_t p = dir > 0 ? s : npos - 1 - s;
+    uint64_t nb = 0;
+    for (uint64_t i = head[p]; i != ~0ull; i = nxt[i]) { n_ev e = { t[ids[i]], i }; tmp[nb++] = e; }
+    if (!nb) continue;
+    for (uint64_t j = 0; j < nb; ++j) tmp[j].id = ids[tmp[j].id] << 20 | tmp[j].id;   /* order by packet index */
+    qsort(tmp, nb, sizeof(n_ev), cmp_inj);
+    for (uint64_t j = 0; j < nb; ++j) {
+      const uint64_t i = tmp[j].id & ((1u << 20) - 1), k = tmp[j].id >> 20;
+      if (hbh_hop(on, k, dst, len, cur, t, zl, ct, shard, held) != HOP_MOVED) continue;
+      const uint32_t c = cur[k], dx = dst[k] % W, dy = dst[k] / W;
+      if (stage == 0 ? c % W == dx : c / W == dy) continue;          /* this stage is over for k */
+      const uint32_t q = stage == 0 ? c % W : c / W;                 /* the next position, later in the sweep */
+      nxt[i] = head[q]; head[q] = i;
+    }
+  }
+}
+
+static void noc_hbh_walk_par(oracle_noc* on, uint64_t n, const uint32_t* src, const uint32_t* dst, const uint32_t* len,
+                             uint32_t* cur, uint64_t* t, uint64_t* zl, uint64_t* ct, const uint8_t* inj,
+                             const uint32_t* shard, uint8_t* held, int threads)
+{
+  const double f = on->cfg.frequency_ghz;
+  const int qm = on->cfg.queue_model_enabled != 0;
+  const uint32_t W = on->w, H = on->h, T = on->n;
+  if (n >= (1ull << 20)) { noc_hbh_walk(on, n, src, dst, len, cur, t, zl, ct, inj, shard, held); return; }
+  uint32_t* key = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+  uint64_t* cnt = (uint64_t*)malloc(sizeof(uint64_t) * ((size_t)T + 1));
+  uint64_t* ids = (uint64_t*)malloc(sizeof(uint64_t) * (n ? n : 1));
+  /* group the packets k with key[k] < nk by key (stable): ids[cnt[g] .. cnt[g+1]) */
+#define GROUP(nk)                                                                  \
+  do {                                                                             \
+    memset(cnt, 0, sizeof(uint64_t) * ((size_t)(nk) + 1));                         \
+    for (uint64_t k = 0; k < n; ++k) if (key[k] < (nk)) cnt[key[k] + 1]++;         \
+    for (uint32_t g = 0; g < (nk); ++g) cnt[g + 1] += cnt[g];                      \
+    uint64_t* pos_ = (uint64_t*)malloc(sizeof(uint64_t) * ((size_t)(nk) + 1));     \
+    memcpy(pos_, cnt, sizeof(uint64_t) * ((size_t)(nk) + 1));                      \
+    for (uint64_t k = 0; k < n; ++k) if (key[k] < (nk)) ids[pos_[key[k]]++] = k;   \
+    free(pos_);                                                                    \
+  } while (0)
+  /* 1. injection ports, per source */
+  for (uint64_t k = 0; k < n; ++k) key[k] = (inj[k] && src[k] != dst[k]) ? src[k] : ~0u;
+  GROUP(T);
+#pragma omp parallel num_threads(threads)
+  {
+    n_ev* by = (n_ev*)malloc(sizeof(n_ev) * (n ? n : 1));
+#pragma omp for schedule(dynamic, 16)
+    for (uint32_t s = 0; s < T; ++s) {
+      const uint64_t b = cnt[s], e = cnt[s + 1];
+      for (uint64_t i = b; i < e; ++i) { n_ev x = { t[ids[i]], ids[i] }; by[i - b] = x; }
+      qsort(by, e - b, sizeof(n_ev), cmp_inj);
+      for (uint64_t i = 0; i < e - b; ++i) {
+        const uint64_t k = by[i].id;
+        n_send_counters(on, src[k], len[k]);
+        uint64_t qd = 0;
+        if (qm) qd = oracle_htree_delay(on->inj[s], time_to_cycles(t[k], f), n_flits(on, len[k]));
+        const uint64_t cps = lat_to_ps(qd, f);
+        t[k] += lat_to_ps(0, f) + cps; ct[k] += cps;
+      }
+    }
+    free(by);
+  }
+  /* 2-3. X hops per row, Y hops per column */
+  for (int stage = 0; stage < 2; ++stage) {
+    const uint32_t nlines = stage == 0 ? H : W, npos = stage == 0 ? W : H;
+    for (uint64_t k = 0; k < n; ++k) {
+      key[k] = ~0u;
+      if (src[k] == dst[k] || held[k]) continue;
+      const uint32_t c = cur[k];
+      if (stage == 0 && c % W != dst[k] % W) key[k] = c / W;
+      if (stage == 1 && c % W == dst[k] % W && c / W != dst[k] / W) key[k] = c % W;
+    }
+    GROUP(nlines);
+#pragma omp parallel num_threads(threads)
+    {
+      n_ev* tmp = (n_ev*)malloc(sizeof(n_ev) * (n ? n : 1));
+      uint64_t* nxt = (uint64_t*)malloc(sizeof(uint64_t) * (n ? n : 1));
+      uint64_t* head = (uint64_t*)malloc(sizeof(uint64_t) * npos);
+      uint64_t* sub = (uint64_t*)malloc(sizeof(uint64_t) * (n ? n : 1));
+#pragma omp for schedule(dynamic, 1)
+      for (uint32_t ln = 0; ln < nlines; ++ln) {
+        /* the line's packets by direction (before either sweep moves them): RIGHT / UP, then LEFT / DOWN */
+        const uint64_t b = cnt[ln], e = cnt[ln + 1];
+        uint64_t m = 0, r = e - b;
+        for (uint64_t i = b; i < e; ++i) {
+          const uint64_t k = ids[i];
+          const uint32_t c = cur[k];
+          if (stage == 0 ? dst[k] % W > c % W : dst[k] / W > c / W) sub[m++] = k;
+          else sub[--r] = k;
+        }
+        if (m) hbh_sweep(on, m, sub, npos, stage, 1, dst, len, cur, t, zl, ct, shard, held, tmp, nxt, head);
+        if (e - b > m) hbh_sweep(on, e - b - m, sub + m, npos, stage, -1, dst, len, cur, t, zl, ct, shard, held, tmp, nxt, head);
+      }
+      free(tmp); free(nxt); free(head); free(sub);
+    }
+  }
+  /* 4. SELF ports, per destination */
+  for (uint64_t k = 0; k < n; ++k) key[k] = (src[k] != dst[k] && !held[k] && cur[k] == dst[k]) ? dst[k] : ~0u;
+  GROUP(T);
+#pragma omp parallel num_threads(threads)
+  {
+    n_ev* by = (n_ev*)malloc(sizeof(n_ev) * (n ? n : 1));
+#pragma omp for schedule(dynamic, 16)
+    for (uint32_t d = 0; d < T; ++d) {
+      const uint64_t b = cnt[d], e = cnt[d + 1];
+      for (uint64_t i = b; i < e; ++i) { n_ev x = { t[ids[i]], ids[i] }; by[i - b] = x; }
+      qsort(by, e - b, sizeof(n_ev), cmp_inj);
+      for (uint64_t i = 0; i < e - b; ++i) hbh_hop(on, by[i].id, dst, len, cur, t, zl, ct, shard, held);
+    }
+    free(by);
+  }
+#undef GROUP
+  free(key); free(cnt); free(ids);
 }
 #include "gg_coherent.inc"

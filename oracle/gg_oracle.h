@@ -107,6 +107,8 @@ void oracle_coh_cache_counters(const oracle_coh* C, uint64_t* out);  /* [tile][2
 void oracle_coh_net_counters(const oracle_coh* C, uint64_t* out);    /* [tile][GG_NUM_NET_COUNTERS] */
 void oracle_coh_run_info(const oracle_coh* C, uint64_t* out);        /* [GG_NUM_RUN_INFO] */
 /* the whole run with one context per logical shard, `threads` OpenMP threads */
+/* tile-parallel steps on `threads` OpenMP threads (bit-identical results) */
+int  oracle_coh_set_threads(oracle_coh* C, int threads);
 int  oracle_coh_run_parallel(const gg_config* cfg, int threads, const uint64_t* addr, const uint32_t* meta,
                              const uint64_t* tile_offsets, uint64_t* access_out, uint64_t* tile_stats,
                              uint64_t* cache, uint64_t* net, uint64_t* run_info);

@@ -85,6 +85,8 @@ def lib():
                                               vp, vp]
         L.oracle_coh_create.restype = vp
         L.oracle_coh_create.argtypes = [ctypes.POINTER(GGConfig)]
+        L.oracle_coh_set_threads.restype = ctypes.c_int
+        L.oracle_coh_set_threads.argtypes = [vp, ctypes.c_int]
         L.oracle_coh_destroy.argtypes = [vp]
         L.oracle_coh_begin.restype = ctypes.c_int
         L.oracle_coh_begin.argtypes = [vp, _u64p, _u32p, _u64p, vp]
@@ -178,9 +180,14 @@ class OracleCoherent:
     """Coherent (Mode C) run: MSI directory + DRAM + NoC + lax-barrier quanta,
     canonical schedule (oracle/gg_coherent.inc)."""
 
-    def __init__(self, cfg):
+    def __init__(self, cfg, threads=1):
+        """threads > 1: tile-parallel steps (each step's tiles, then the
+        hop-by-hop routing stage by stage, on OpenMP threads): the all-core CPU
+        baseline, bit-identical to one thread."""
         self.cfg = cfg
         self.h = lib().oracle_coh_create(ctypes.byref(cfg))
+        if threads > 1:
+            lib().oracle_coh_set_threads(self.h, int(threads))
 
     def __del__(self):
         if getattr(self, "h", None):

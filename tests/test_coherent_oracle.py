@@ -136,3 +136,24 @@ def test_parallel_oracle_equals_single_context(T, K, net):
     ri = oc.run_info()
     for k in ("quanta", "steps", "net_msgs", "self_msgs", "boundary_msgs"):
         assert got[4][C.RUN_INFO.index(k)] == ri[C.RUN_INFO.index(k)], k
+
+
+@pytest.mark.parametrize("T,K,net,hot", [(64, 8, C.NET_EMESH_HOP_BY_HOP, 32), (64, 1, C.NET_EMESH_HOP_BY_HOP, 32),
+                                         (64, 4, C.NET_EMESH_HOP_COUNTER, 32), (256, 8, C.NET_EMESH_HOP_BY_HOP, 64)])
+def test_tile_parallel_oracle_equals_serial(T, K, net, hot):
+    """The tile-parallel CPU baseline (oracle_coh_set_threads: each step's tiles,
+    then the hop-by-hop routing stage by stage - injection per source, X per
+    row, Y per column, SELF per destination - on OpenMP threads) produces the
+    serial global-event-queue run's outputs bit for bit."""
+    N = 200
+    a, m, o = po.gen_trace(T, N, hot_lines=hot)
+    cfg = C.default_config(T, num_shards=K, net_model=net)
+    ref = po.OracleCoherent(cfg)
+    out = ref.run(a, m, o)
+    par = po.OracleCoherent(cfg, threads=4)
+    got = par.run(a, m, o)
+    np.testing.assert_array_equal(got, out)
+    np.testing.assert_array_equal(par.tile_stats(), ref.tile_stats())
+    np.testing.assert_array_equal(par.cache_counters(), ref.cache_counters())
+    np.testing.assert_array_equal(par.net_counters(), ref.net_counters())
+    np.testing.assert_array_equal(par.run_info(), ref.run_info())

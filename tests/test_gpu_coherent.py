@@ -220,7 +220,8 @@ def test_coherent_stress_matches_oracle(T, N, K, net):
 def test_coherent_contexts_split_equals_one_context(net):
     """1 context x 8 logical shards == 2 contexts x 4 shards each (exchanging
     messages and held hop-by-hop packets at every quantum boundary) == 4
-    contexts x 2, bit for bit: the schedule depends on the shard count only."""
+    contexts x 2 == 8 contexts x 1, bit for bit: the schedule depends on the
+    shard count only."""
     torch = torch_dev()
     from graphite_amd import backend as B
     from graphite_amd import coherent as CO
@@ -229,7 +230,7 @@ def test_coherent_contexts_split_equals_one_context(net):
     a, m, o = po.gen_trace(T, N, hot_lines=32)
     addr, meta = to_dev(torch, a, torch.int64), to_dev(torch, m, torch.int32)
     results = []
-    for R in (1, 2, 4):
+    for R in (1, 2, 4, 8):
         outs, engines, bes = [], [], []
         for r in range(R):
             k0, k1 = CO.shard_range(r, R, K)

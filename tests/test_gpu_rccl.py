@@ -3,7 +3,9 @@
 torch.distributed "nccl" (= RCCL) process group (ProcessGroupNCCL._comm_ptr).
 A one-GPU box forms a one-rank communicator only (RCCL refuses two ranks on
 one device); the exchange logic over several ranks is the same as
-graphite_amd.coherent.run, covered by the gloo tests (tests/test_coherent_dist.py)."""
+graphite_amd.coherent.run, covered by the gloo tests (tests/test_coherent_dist.py).
+The run is repeated with one-record peer slots (GG_ROUND_SLOT=1) so that the
+sized overflow round of gg_round_exchange runs too."""
 import os
 import socket
 import subprocess
@@ -15,7 +17,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 SCRIPT = r"""
-import sys, numpy as np, torch, torch.distributed as dist
+import os, sys, numpy as np, torch, torch.distributed as dist
 sys.path.insert(0, %r)
 from graphite_amd import config as C, backend as B, coherent as CO
 from oracle import pyoracle as po
@@ -25,11 +27,13 @@ T, N, K = 64, 200, 8
 a, m, o = po.gen_trace(T, N, hot_lines=32)
 addr = torch.from_numpy(a.view(np.int64)).cuda(); meta = torch.from_numpy(m.view(np.int32)).cuda()
 res = []
-for mode in ("rccl", "single"):
+for mode in ("rccl", "rccl_slot1", "single"):
+    # rccl_slot1: one record per peer slot, so nearly every quantum takes the sized overflow round
+    os.environ["GG_ROUND_SLOT"] = "1" if mode == "rccl_slot1" else "1024"
     cfg = C.default_config(T, num_shards=K, net_model=C.NET_EMESH_HOP_BY_HOP)
     be = B.Backend(cfg)
     out = torch.zeros(T * N, dtype=torch.int64, device="cuda")
-    if mode == "rccl":
+    if mode.startswith("rccl"):
         CO.run_rccl(be, addr, meta, o, out)
     else:
         be.coherent_run(addr, meta, o, out)
@@ -37,7 +41,7 @@ for mode in ("rccl", "single"):
     st, cc, ri = be.coherent_stats()
     res.append((out.cpu().numpy(), st, cc, be.noc_counters(), ri[:2]))
     be.close()
-ok = all(np.array_equal(x, y) for x, y in zip(res[0], res[1]))
+ok = all(np.array_equal(x, y) for r in res[1:] for x, y in zip(res[0], r))
 oc = po.OracleCoherent(C.default_config(T, num_shards=K, net_model=C.NET_EMESH_HOP_BY_HOP))
 ref = oc.run(a, m, o)
 ok = ok and np.array_equal(res[0][0].view(np.uint64), ref) and np.array_equal(res[0][1], oc.tile_stats())
