@@ -22,9 +22,11 @@ bit-identical.
 Reported with it: the roofline of the dominant kernel by device time
 (k_c_walk: the X and Y walks are one kernel symbol) at SURVEY.md §8d's 16
 algorithmic bytes per access (8 B address + 4 B meta in, 4 B result out),
-accesses per launch from the run, the average launch duration from HIP events
-around EVERY launch in one extra untimed run (events around every launch add
-gaps between launches, so the timed runs carry none); the C oracle on the
+accesses per launch from the run, the average launch duration measured live
+in one extra untimed run: every launch stamps its first workgroup's start and
+its last workgroup's end on the GPU's 100 MHz s_memrealtime clock (the span
+rocprofv3's kernel trace reports; an event pair around a launch adds its
+dispatch gap, ~7 %); the timed runs carry no instrumentation.  The C oracle on the
 same workload as the CPU baseline, tile-parallel on the host's CPU share
 (oracle_coh_set_threads) and on one thread; and a bit-exact check of every
 output against the oracle in the same run.  Sections under their own keys:
@@ -726,8 +728,9 @@ def main():
                          "traffic": None, "bytes_per_access": COH_BYTES_PER_ACCESS, "launch_accesses": lacc,
                          "kernel_avg_us": dk["avg_us"] if dk else None, "kernel_launches": dk["launches"] if dk else None,
                          "kernels": kern,
-                         "timing": "HIP events around every launch, one extra untimed run on the launch stream "
-                                   "(the timed runs carry no events)",
+                         "timing": "in-kernel launch spans (first workgroup start to last workgroup end, "
+                                   "s_memrealtime 100 MHz) of every launch, one extra untimed run; the timed runs "
+                                   "carry no instrumentation",
                          "note": "Mode C is latency-bound: a step is a chain of dependent accesses per tile and each "
                                  "router port serves its packets one by one in the canonical order (DESIGN.md §4); "
                                  "the fraction measures how far that is from the HBM bound, not an HBM bottleneck"},

@@ -177,8 +177,9 @@ class Backend:
         _check(load().gg_reset(self.h))
 
     def set_timing(self, on=True, every_launch=False):
-        """HIP-event kernel timing: off, sampled (coherent launches: 1 in 16)
-        or around every launch (every_launch=True; adds launch gaps)."""
+        """Kernel timing: off, sampled HIP events (coherent launches: 1 in 16),
+        or every_launch=True: every coherent step / walk launch stamps its
+        span (first workgroup start, last workgroup end) in-kernel."""
         load().gg_set_timing(self.h, (2 if every_launch else 1) if on else 0)
 
     def kernel_time_ms(self, name):

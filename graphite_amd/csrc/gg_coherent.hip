@@ -141,6 +141,9 @@ struct CS {
   uint64_t* gscr;                        // [L][5 * IC] ordering scratch beyond kInLds
   unsigned long long* prof;              // GG_COH_PROFILE=1: shader-clock cycles per phase (diagnostics)
   uint32_t* gbar;                        // grid barrier counter of k_c_persist
+  // in-kernel launch timing (gg_set_timing mode 2): per timed launch slot
+  // {first workgroup start, last workgroup end} on the s_memrealtime clock
+  unsigned long long* kt; uint32_t kt_slot;
 };
 // profile slots: step phases 0..5 summed over tiles, 8 = sum over steps of the slowest tile;
 // walker: 16 staging+load, 17 event loop, 18 hand-off+write back, 19 events, 20 sum of slowest walker per launch (X),
@@ -1843,10 +1846,27 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
   return T.clk + (uint64_t)((S.meta[T.rec] & 0x7FFFFFFFu) >> 1) * P.gap_ps;
 }
 
+// in-kernel launch timing (timing mode 2): the first workgroup start and the
+// last workgroup end of the launch on the 100 MHz s_memrealtime clock — the
+// kernel's execution span as rocprofv3's kernel trace sees it, without the
+// dispatch gap an event pair around the launch adds
+__device__ __forceinline__ void kt_begin(const CS& S)
+{
+  if (S.kt && threadIdx.x == 0) atomicMin(&S.kt[2 * S.kt_slot], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+__device__ __forceinline__ void kt_end(const CS& S)
+{
+  if (!S.kt) return;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(&S.kt[2 * S.kt_slot + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+
 __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t L, uint32_t devloop, uint64_t barrier_arg)
 {
+  kt_begin(S);
   TraceWin W{~0ull, 0, 0};
   step_body<false, false>(P, S, L, devloop, barrier_arg, W);
+  kt_end(S);
 }
 
 // ---------------------------------------------------------------------------
@@ -2246,7 +2266,9 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
 template <bool PIPE>
 __global__ void __launch_bounds__(PIPE ? 64 * kMaxWalkWaves : 64) k_c_walk(CP P, CS S, uint32_t L, int stage)
 {
+  kt_begin(S);
   walk_body<PIPE>(P, S, L, stage, blockIdx.x);
+  kt_end(S);
 }
 
 // A barrier of every workgroup of the launch (one wave each): release of the
@@ -2318,6 +2340,9 @@ __global__ void __launch_bounds__(64) k_c_persist(CP P, CS S, uint32_t L0, uint3
     }
     const uint64_t done = __hip_atomic_load(&S.qs[QS_DONE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t e = __hip_atomic_load(S.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // every block has read this step's flags before any block starts the next
+    // step (which may set them): all blocks leave the loop at the same step
+    grid_sync(S, gen);
     if (done || e) break;
   }
   if (LC) cache_state_copy<LC>(P, S, blockIdx.x, smem + P.cache_lds_off, false);
@@ -2505,11 +2530,17 @@ struct gg_coh_state {
   std::vector<hipEvent_t> tev;
   std::vector<int> tkind;
   uint32_t tused = 0;
+  // mode 2: in-kernel spans, slot s of kind k at kt[2 * (k * kKtRing + s)]
+  unsigned long long* kt_dev = nullptr;
+  std::vector<unsigned long long> kt_host;
+  std::vector<int> kt_kind;             // kind of each slot used since the last harvest
+  double kt_tick_ns = 10.0;             // s_memrealtime period
   double ksum[5] = {0, 0, 0, 0, 0};
   uint64_t kcnt[5] = {0, 0, 0, 0, 0};      // timed launches
   uint64_t nlaunch[5] = {0, 0, 0, 0, 0};   // all launches
 };
 constexpr uint64_t kTimeSample = 16;
+constexpr uint32_t kKtRing = 4096;      // in-kernel timing slots between two harvests (a batch is <= 256 steps)
 static void launch_walk(gg_coh_state* C, hipStream_t s, uint32_t blocks, uint32_t threads, uint32_t L, int stage)
 {
   if (threads > 64)
@@ -2524,6 +2555,15 @@ static const char* kKernelNames[5] = {"coherent_step", "coherent_walk_x", "coher
 
 template <class F> static void timed_launch(gg_ctx* ctx, gg_coh_state* C, hipStream_t s, int kind, F&& fn)
 {
+  if (ctx->timing >= 2 && C->kt_dev && kind < 3 && C->kt_kind.size() < kKtRing) {
+    C->nlaunch[kind]++;
+    C->S.kt = C->kt_dev;
+    C->S.kt_slot = (uint32_t)C->kt_kind.size();
+    C->kt_kind.push_back(kind);
+    fn();
+    C->S.kt = nullptr;
+    return;
+  }
   if (!ctx->timing || C->nlaunch[kind]++ % (ctx->timing >= 2 ? 1 : kTimeSample)) { fn(); return; }
   if (C->tev.size() < 2 * (size_t)(C->tused + 1)) {
     const size_t n0 = C->tev.size();
@@ -2538,6 +2578,19 @@ template <class F> static void timed_launch(gg_ctx* ctx, gg_coh_state* C, hipStr
 }
 static void timed_harvest(gg_coh_state* C)
 {
+  if (!C->kt_kind.empty()) {
+    const size_t n = C->kt_kind.size();
+    C->kt_host.resize(2 * n);
+    if (hipMemcpy(C->kt_host.data(), C->kt_dev, 16 * n, hipMemcpyDeviceToHost) == hipSuccess) {
+      for (size_t i = 0; i < n; ++i) {
+        const unsigned long long a = C->kt_host[2 * i], b = C->kt_host[2 * i + 1];
+        if (b >= a && a != ~0ull) { C->ksum[C->kt_kind[i]] += (double)(b - a) * C->kt_tick_ns * 1e-6; C->kcnt[C->kt_kind[i]]++; }
+      }
+    }
+    for (size_t i = 0; i < n; ++i) { C->kt_host[2 * i] = ~0ull; C->kt_host[2 * i + 1] = 0; }
+    (void)hipMemcpy(C->kt_dev, C->kt_host.data(), 16 * n, hipMemcpyHostToDevice);
+    C->kt_kind.clear();
+  }
   for (uint32_t i = 0; i < C->tused; ++i) {
     float ms = 0;
     if (hipEventElapsedTime(&ms, C->tev[2 * i], C->tev[2 * i + 1]) == hipSuccess) {
@@ -2793,6 +2846,14 @@ static gg_status coh_alloc(gg_ctx* ctx)
   A(ring, 11); A(ri, GG_NUM_RUN_INFO); A(qs, QS_N); A(gbar, 1);
   A(gscr, L * 5 * P.IC);
 #undef A
+  {
+    // in-kernel launch timing slots, reset to {~0, 0}
+    if ((st = dalloc(C, &C->kt_dev, 2ull * kKtRing))) return st;
+    std::vector<unsigned long long> init(2 * kKtRing);
+    for (uint32_t i = 0; i < kKtRing; ++i) { init[2 * i] = ~0ull; init[2 * i + 1] = 0; }
+    GG_HIP(hipMemcpy(C->kt_dev, init.data(), 16ull * kKtRing, hipMemcpyHostToDevice));
+    S.kt = nullptr; S.kt_slot = 0;
+  }
   if (getenv("GG_COH_PROFILE") && atoi(getenv("GG_COH_PROFILE"))) {
     if ((st = dalloc(C, &S.prof, 1024 + 8 * 65536))) return st;
     GG_HIP(hipMemset(S.prof, 0, sizeof(unsigned long long) * (1024 + 8 * 65536)));
@@ -3053,11 +3114,22 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
   // small meshes: the whole loop in persistent launches (k_c_persist), one
   // workgroup per owned tile, all resident (<= kPersistTiles << CUs)
   const char* np_env = getenv("GG_COH_NO_PERSIST");
-  const bool persist = P.L <= kPersistTiles && !(np_env && atoi(np_env));
+  const char* nl_env = getenv("GG_COH_NO_LDS_CACHE");
+  const bool plc = C->persist_lc && !(nl_env && atoi(nl_env));
+  bool persist = P.L <= kPersistTiles && !(np_env && atoi(np_env));
+  if (persist) {
+    // the grid barrier needs every workgroup resident at once (a partitioned
+    // device has fewer CUs): else the per-step launches
+    const void* fn = plc ? (const void*)k_c_persist<true> : (const void*)k_c_persist<false>;
+    const size_t lds = plc ? (size_t)P.cache_lds_off + P.cache_lds_bytes : std::max(C->walk_lds, C->step_lds);
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, lds) != hipSuccess ||
+        (uint64_t)per_cu * (uint64_t)ctx->num_cus < P.L)
+      persist = false;
+  }
   while (persist) {
     GG_HIP(hipMemsetAsync(C->S.gbar, 0, sizeof(uint32_t), s));
-    const char* nl_env = getenv("GG_COH_NO_LDS_CACHE");
-    if (C->persist_lc && !(nl_env && atoi(nl_env))) {
+    if (plc) {
       const size_t lds = P.cache_lds_off + P.cache_lds_bytes;
       timed_launch(ctx, C, s, 3, [&] { hipLaunchKernelGGL(k_c_persist<true>, dim3(P.L), dim3(64), lds, s, P, C->S, L, L + kPersistLaunches); });
     } else {

@@ -429,15 +429,17 @@ __global__ __launch_bounds__(64) void k_port_staged(NocDev D, const uint32_t* __
   qimg_copy_set<false>(D, nt, pq, pskip, qlds, qb);
 }
 
-// Staged stages X / Y: one workgroup per chain (row or column, direction),
-// the chain's w (or h) output-port queues in LDS; thread 0 walks the events.
-__global__ __launch_bounds__(64) void k_chain_staged(NocDev D, int stage, const uint32_t* __restrict__ dst,
+// Staged stages X / Y, the general form: one workgroup per chain (row or
+// column, direction), the chain's w (or h) output-port queues in LDS; thread
+// 0 walks the events.  k_chain_sweep falls back to it for chains outside its
+// limits (any queue model, any batch size or time range).
+__device__ void chain_staged(NocDev D, int stage, const uint32_t* __restrict__ dst,
     const uint32_t* __restrict__ len, const uint64_t* __restrict__ bucket_off,
-    const uint32_t* __restrict__ bucket_ids, Ev* heap, PktState S)
+    const uint32_t* __restrict__ bucket_ids, Ev* heap, PktState S, uint32_t c)
 {
   extern __shared__ __attribute__((aligned(16))) uint8_t qlds[];
   const NocParams& P = D.P;
-  const uint32_t c = blockIdx.x, line = c / 2, dir = c % 2;
+  const uint32_t line = c / 2, dir = c % 2;
   const uint64_t b = bucket_off[c], e = bucket_off[c + 1];
   if (b == e) return;
   const uint32_t ms = P.max_size, qb = qimg_bytes(ms);
@@ -513,6 +515,166 @@ __global__ __launch_bounds__(64) void k_chain_staged(NocDev D, int stage, const 
   if (lp) lpk_store(L, np, S);
   if (lp) lctr_flush(D, lcb, Lq, tile_at);
   qimg_copy_set<false>(D, Lq, cq, cskip, qlds, qb);
+}
+
+// ---------------------------------------------------------------------------
+// Stages X / Y as a position sweep (the default): one workgroup per chain.
+// In a chain the packets move one way, so the requests a port sees depend
+// only on the ports before it: the sweep visits the positions in the
+// direction of travel; the batch of a position = the packets that left the
+// position before it + those whose route starts there, sorted by (arrival
+// time, packet index) — the order of the global event queue at that port —
+// by the workgroup's threads (bitonic, LDS); one wave serves the batch
+// through the port's history tree held in its registers (RegQueue); the
+// lanes then split the batch into packets leaving the chain (time, zero-load
+// / contention parts and position written back) and the next position's
+// arrivals.  A batch entry is (time, i), i the packet's rank by index among
+// the chain's packets (their ids sorted first).  Limits (else chain_staged):
+// <= kSweepPk packets, <= kSweepPos positions, history_tree queues of <=
+// kQMaxNoc intervals (or no queue model), flits < 2^16.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kSweepPk = 6144, kSweepSort = 8192, kSweepPos = 256, kSweepThreads = 256, kQMaxNoc = 128;
+struct SK { uint64_t t; uint32_t i, pad; };
+static_assert(sizeof(SK) == 16 && sizeof(Ev) >= 2 * sizeof(SK), "start runs + arrivals fit a bucket's Ev scratch");
+constexpr size_t kSweepLds = (size_t)kSweepSort * sizeof(SK) + (size_t)kSweepPk * 4 + kSweepPos * 8 + 64;
+__device__ __forceinline__ bool sk_lt(const SK& a, const SK& b) { return a.t < b.t || (a.t == b.t && a.i < b.i); }
+
+// ascending bitonic sort of a[0, M), M a power of two, all threads of the block
+template <class T, class Lt>
+__device__ void block_bitonic(T* a, uint32_t M, Lt lt)
+{
+  for (uint32_t k = 2; k <= M; k <<= 1)
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = threadIdx.x; i < M; i += blockDim.x) {
+        const uint32_t l = i ^ j;
+        if (l > i) {
+          const T x = a[i], y = a[l];
+          if (((i & k) == 0) == lt(y, x)) { a[i] = y; a[l] = x; }
+        }
+      }
+      __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kSweepThreads) void k_chain_sweep(NocDev D, int stage, const uint32_t* __restrict__ dst,
+    const uint32_t* __restrict__ len, const uint64_t* __restrict__ bucket_off, uint32_t* __restrict__ bucket_ids,
+    Ev* heap, PktState S)
+{
+  extern __shared__ __attribute__((aligned(16))) uint8_t qlds[];
+  const NocParams& P = D.P;
+  const uint32_t c = blockIdx.x, line = c / 2, dir = c % 2, tid = threadIdx.x, ln = tid & 63;
+  const uint64_t b = bucket_off[c], e = bucket_off[c + 1];
+  if (b == e) return;
+  const uint32_t n = (uint32_t)min<uint64_t>(e - b, 0xFFFFFFFFull);
+  const uint32_t npos = stage == 0 ? P.w : P.h;
+  const bool regq = P.qtype == GG_QM_HISTORY_TREE && P.max_size <= kQMaxNoc;
+  __shared__ uint32_t s_bad, s_na;
+  if (tid == 0) s_bad = 0;
+  __syncthreads();
+  if (n > kSweepPk || npos > kSweepPos || (P.qm && !regq)) { chain_staged(D, stage, dst, len, bucket_off, bucket_ids, heap, S, c); return; }
+  SK* A = reinterpret_cast<SK*>(qlds);                                   // [kSweepSort] the batch being sorted / served
+  uint32_t* info = reinterpret_cast<uint32_t*>(A + kSweepSort);          // [kSweepPk] flits | exit position << 16
+  uint64_t* pc = reinterpret_cast<uint64_t*>(info + kSweepPk);           // [kSweepPos + 1] start-run offsets
+  uint32_t* ids = bucket_ids + b;
+  SK* G = reinterpret_cast<SK*>(heap + b);                               // [n] start runs (HBM: the bucket's Ev scratch)
+  SK* Bq = G + n;                                                        // [n] arrivals for the next position
+  // 1. the chain's packet ids in index order (i = rank by index), then their info
+  uint32_t M = 1;
+  while (M < n) M <<= 1;
+  uint32_t* ia = reinterpret_cast<uint32_t*>(A);
+  for (uint32_t i = tid; i < M; i += blockDim.x) ia[i] = i < n ? ids[i] : 0xFFFFFFFFu;
+  __syncthreads();
+  block_bitonic(ia, M, [](uint32_t x, uint32_t y) { return x < y; });
+  auto pos_of = [&](uint32_t tile) { return stage == 0 ? tile % P.w : tile / P.w; };
+  auto tile_at = [&](uint32_t pos) -> uint32_t { return stage == 0 ? line * P.w + pos : pos * P.w + line; };
+  for (uint32_t i = tid; i < n; i += blockDim.x) {
+    const uint32_t k = ia[i];
+    ids[i] = k;
+    const uint64_t nf = nflits(P, len[k]);
+    if (nf >= (1u << 16)) atomicOr(&s_bad, 1u);
+    info[i] = (uint32_t)nf | (pos_of(dst[k]) << 16);
+  }
+  for (uint32_t p = tid; p <= npos; p += blockDim.x) pc[p] = 0;
+  __syncthreads();
+  if (s_bad) { chain_staged(D, stage, dst, len, bucket_off, bucket_ids, heap, S, c); return; }
+  // 2. start runs: the packets bucketed by start position (counting sort into G)
+  for (uint32_t i = tid; i < n; i += blockDim.x) atomicAdd((unsigned long long*)&pc[pos_of(S.cur[ids[i]]) + 1], 1ull);
+  __syncthreads();
+  if (tid == 0) for (uint32_t p = 0; p < npos; ++p) pc[p + 1] += pc[p];
+  __syncthreads();
+  for (uint32_t i = tid; i < n; i += blockDim.x) {
+    const uint32_t k = ids[i];
+    const uint64_t j = atomicAdd((unsigned long long*)&pc[pos_of(S.cur[k])], 1ull);   // pc[p] ends at run p's end
+    G[j] = SK{S.t[k], i, 0};
+  }
+  __syncthreads();
+  // run p = [p ? pc[p - 1] : 0, pc[p])
+  const uint64_t zps = lat_to_ps((uint64_t)P.router_delay + P.link_delay, P.f);
+  const int port = stage == 0 ? (dir ? P_RIGHT : P_LEFT) : (dir ? P_UP : P_DOWN);
+  uint32_t nb = 0;                                                       // arrivals waiting in Bq
+  for (uint32_t s_ = 0; s_ < npos; ++s_) {
+    const uint32_t pos = dir ? s_ : npos - 1 - s_;
+    const uint64_t r0 = pos ? pc[pos - 1] : 0, r1 = pc[pos];
+    const uint32_t m = nb + (uint32_t)(r1 - r0);
+    if (m == 0) continue;
+    M = 1;
+    while (M < m) M <<= 1;
+    for (uint32_t i = tid; i < M; i += blockDim.x)
+      A[i] = i < nb ? Bq[i] : i < m ? G[r0 + (i - nb)] : SK{~0ull, ~0u, 0};
+    __syncthreads();
+    block_bitonic(A, M, sk_lt);
+    const uint32_t tile = tile_at(pos);
+    if (tid < 64) {
+      // one wave serves the batch in order through the port's queue (registers)
+      RegQueue rq;
+      HQueue* q = D.q + (uint64_t)tile * 6 + port;
+      HNode* nd = D.nd + ((uint64_t)tile * 6 + port) * P.max_size;
+      if (P.qm) rq.load(q, nd, 1, P.analytical != 0, ln);
+      uint64_t cq = 0, cf = 0;
+      for (uint32_t j0 = 0; j0 < m; j0 += 64) {
+        const uint32_t cnt = min(64u, m - j0);
+        const uint64_t myt = ln < cnt ? A[j0 + ln].t : 0;
+        const uint32_t myinfo = ln < cnt ? info[A[j0 + ln].i] : 0;
+        uint64_t out = 0;
+        for (uint32_t j = 0; j < cnt; ++j) {
+          const uint64_t t = rl64(myt, j);
+          const uint32_t nf = (uint32_t)__builtin_amdgcn_readlane((int)myinfo, (int)j) & 0xFFFFu;
+          const uint64_t qd = P.qm ? rq.request<true>(time_to_cycles(t, P.f), nf, D.err) : 0;
+          cq += qd; cf += nf;
+          if (ln == j) out = t + zps + lat_to_ps(qd, P.f);
+        }
+        if (ln < cnt) A[j0 + ln].t = out;
+      }
+      if (P.qm) rq.store(q, nd);
+      if (ln == 0) {
+        if (P.qm) { cadd(D.ctr, tile, GG_NC_ROUTER_CONTENTION_CYCLES, cq); cadd(D.ctr, tile, GG_NC_ROUTER_PACKETS, m); }
+        cadd(D.ctr, tile, GG_NC_BUFFER_WRITES, cf); cadd(D.ctr, tile, GG_NC_BUFFER_READS, cf);
+        cadd(D.ctr, tile, GG_NC_SWITCH_ALLOC, m); cadd(D.ctr, tile, GG_NC_CROSSBAR, cf);
+        cadd(D.ctr, tile, GG_NC_LINK_TRAVERSALS, cf);
+        s_na = 0;
+      }
+    }
+    __syncthreads();
+    // the served batch: packets leaving the chain are written back, the rest arrive at the next position
+    const uint32_t nx = dir ? pos + 1 : pos - 1;
+    for (uint32_t j = tid; j < m; j += blockDim.x) {
+      const SK x = A[j];
+      if ((info[x.i] >> 16) == nx) {
+        const uint32_t k = ids[x.i];
+        const uint64_t t0 = S.t[k];
+        const uint32_t a = pos_of(S.cur[k]);
+        const uint64_t hz = (uint64_t)(dir ? nx - a : a - nx) * zps;   // zero-load part: router + link per hop
+        S.zl[k] += hz;
+        S.ct[k] += x.t - t0 - hz;
+        S.t[k] = x.t;
+        S.cur[k] = tile_at(nx);
+      } else {
+        Bq[atomicAdd(&s_na, 1u)] = x;
+      }
+    }
+    __syncthreads();
+    nb = s_na;
+  }
 }
 
 // bucket keys: 0 = injection (src tile), 1 = X chain, 2 = Y chain, 3 = SELF (dst tile); ~0 = not in stage
@@ -1069,7 +1231,8 @@ gg_status gg_noc_alloc(gg_ctx* ctx)
   S->staged = !(getenv("GG_NOC_STAGED") && atoi(getenv("GG_NOC_STAGED")) == 0);
   GG_HIP(hipFuncSetAttribute((const void*)k_port_staged<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
   GG_HIP(hipFuncSetAttribute((const void*)k_port_staged<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
-  GG_HIP(hipFuncSetAttribute((const void*)k_chain_staged, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
+  GG_HIP(hipFuncSetAttribute((const void*)k_chain_sweep, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
+  static_assert(kSweepLds <= kStageLdsMax, "the sweep's LDS arrays fit the stage budget");
   GG_HIP(hipFuncSetAttribute((const void*)k_tree_walk<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)(kTreeLdsEv * sizeof(TEv))));
   GG_HIP(hipMalloc((void**)&S->ctr, sizeof(uint64_t) * c.num_tiles * GG_NUM_NET_COUNTERS));
@@ -1257,8 +1420,8 @@ gg_status gg_noc_hbh(gg_ctx* ctx, const uint32_t* src, const uint32_t* dst, cons
       else
         hipLaunchKernelGGL(k_port_staged<true>, dim3(pb), dim3(64), kStageLdsMax, s, D, dst, len, S->off, S->ids, S->heap, PS);
     } else if (staged) {
-      hipLaunchKernelGGL(k_chain_staged, dim3(nb), dim3(64), kStageLdsMax, s, D, stage - 1, dst, len, S->off, S->ids,
-                         S->heap, PS);
+      hipLaunchKernelGGL(k_chain_sweep, dim3(nb), dim3(kSweepThreads), kStageLdsMax, s, D, stage - 1, dst, len, S->off,
+                         S->ids, S->heap, PS);
     } else if (stage == 0)
       hipLaunchKernelGGL(k_inject, dim3(tb), dim3(64), 0, s, D, src, dst, len, S->off, S->ids, S->heap, PS);
     else if (stage == 3)

@@ -496,7 +496,8 @@ gg_status gg_combine_accesses(const uint64_t* line_out_dev, const uint64_t* firs
  * events on the stream the kernel ran on; negative if not launched.           */
 float     gg_kernel_time_ms(gg_ctx* ctx, const char* kernel);
 /* enabled: 0 off; 1 on, coherent-mode launches sampled (an event pair around
- * every 16th launch of each kernel); 2 on, an event pair around every launch. */
+ * every 16th launch of each kernel); 2 on, every coherent step / walk launch
+ * timed in-kernel (first workgroup start to last workgroup end). */
 void      gg_set_timing(gg_ctx* ctx, int enabled);
 /* With timing on, every 16th launch of each coherent-mode kernel is bracketed
  * by HIP events on its stream: launches since the last gg_coherent_begin of

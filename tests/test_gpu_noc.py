@@ -120,8 +120,13 @@ def test_hop_counter_matches_oracle(T):
 
 
 @pytest.mark.parametrize("T,n,span,batches", [(16, 4000, 200000, 1), (64, 20000, 2000000, 2),
-                                              (256, 30000, 1000000, 1), (64, 30000, 100000, 3)])
+                                              (256, 30000, 1000000, 1), (64, 30000, 100000, 3),
+                                              (16, 80000, 4000000, 1),      # chains beyond the sweep's LDS: general walk
+                                              (1024, 131072, 50 * 131072, 1)])   # the bench batch's shape
 def test_hop_by_hop_matches_oracle(T, n, span, batches):
+    """gg_noc_route_batch under emesh_hop_by_hop: X / Y chains as position
+    sweeps (k_chain_sweep), or the general serial walk for chains beyond its
+    limits, bit-exact vs the oracle's global event queue."""
     torch = torch_dev()
     cfg = C.default_config(T, net_model=C.NET_EMESH_HOP_BY_HOP)
     src, dst, bits, t = packets(T, n, T + n, span)
@@ -131,6 +136,20 @@ def test_hop_by_hop_matches_oracle(T, n, span, batches):
         np.testing.assert_array_equal(g, r)
     np.testing.assert_array_equal(be.noc_counters(), on.counters())
     assert int(ref[2].sum()) > 0                                   # contention was exercised
+
+
+@pytest.mark.parametrize("max_size", [2, 129])
+def test_hop_by_hop_list_sizes_match_oracle(max_size):
+    """max_list_size 2 (the prune on almost every request) and 129 (beyond the
+    register queue: the general walk)."""
+    torch = torch_dev()
+    cfg = C.default_config(64, net_model=C.NET_EMESH_HOP_BY_HOP, max_list_size=max_size)
+    src, dst, bits, t = packets(64, 20000, 5 + max_size, 500000)
+    be, got = run_noc(torch, cfg, src, dst, bits, t)
+    on, ref = oracle_noc(cfg, src, dst, bits, t)
+    for g, r in zip(got, ref):
+        np.testing.assert_array_equal(g, r)
+    np.testing.assert_array_equal(be.noc_counters(), on.counters())
 
 
 def test_hop_by_hop_without_queue_model():

@@ -123,7 +123,12 @@ def oracle_tree(cfg, src, dst, bits, t, batches=1):
 @pytest.mark.gpu
 @pytest.mark.parametrize("T,n,span,batches,frac,qm", [(16, 3000, 200000, 1, 0.1, 1), (64, 4000, 400000, 2, 0.05, 1),
                                                       (64, 3000, 100000, 1, 0.02, 1), (16, 2000, 100000, 1, 0.2, 0),
-                                                      (256, 2000, 400000, 1, 0.01, 1), (256, 3000, 600000, 1, 0.03, 1)])
+                                                      (256, 2000, 400000, 1, 0.01, 1), (256, 3000, 600000, 1, 0.03, 1),
+                                                      # one thread owns several routers (T > the workgroup's threads)
+                                                      (2048, 1500, 400000, 1, 0.004, 1),
+                                                      (4096, 1500, 400000, 1, 0.004, 1),
+                                                      # beyond the windowed walk's LDS arrays: the serial walk
+                                                      (4225, 600, 200000, 1, 0.01, 1)])
 def test_broadcast_tree_matches_oracle_on_gpu(T, n, span, batches, frac, qm):
     from gpu_util import torch_dev
     torch = torch_dev()
