@@ -205,12 +205,10 @@ __device__ void qimg_copy_set(const NocDev& D, uint32_t n, Qid qid, Skip skip, u
 }
 
 // Stage 0: injection port of each source tile, packets in (time, index) order.
-__global__ void k_inject(NocDev D, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
-                         const uint32_t* __restrict__ len, const uint64_t* __restrict__ bucket_off,
-                         const uint32_t* __restrict__ bucket_ids, Ev* heap, PktState S)
+__device__ void inject_tile(const NocDev& D, uint32_t tile, const uint32_t* __restrict__ len,
+                            const uint64_t* __restrict__ bucket_off, const uint32_t* __restrict__ bucket_ids, Ev* heap,
+                            const PktState& S)
 {
-  const uint32_t tile = blockIdx.x * blockDim.x + threadIdx.x;
-  if (tile >= D.P.tiles) return;
   const uint64_t b = bucket_off[tile], e = bucket_off[tile + 1];
   Ev* h = heap + b;
   uint32_t n = 0;
@@ -228,6 +226,14 @@ __global__ void k_inject(NocDev D, const uint32_t* __restrict__ src, const uint3
     S.t[k] += lat_to_ps(0, D.P.f) + cps;
     S.ct[k] += cps;
   }
+}
+__global__ void k_inject(NocDev D, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                         const uint32_t* __restrict__ len, const uint64_t* __restrict__ bucket_off,
+                         const uint32_t* __restrict__ bucket_ids, Ev* heap, PktState S)
+{
+  const uint32_t tile = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tile >= D.P.tiles) return;
+  inject_tile(D, tile, len, bucket_off, bucket_ids, heap, S);
 }
 
 // Stages X and Y: one thread per chain; ports along the chain in (time, index) order.
@@ -266,12 +272,10 @@ __global__ void k_chain(NocDev D, int stage, const uint32_t* __restrict__ src, c
 }
 
 // Final stage: SELF port of each destination + receive (processReceivedPacket).
-__global__ void k_self(NocDev D, const uint32_t* __restrict__ dst, const uint32_t* __restrict__ len,
-                       const uint64_t* __restrict__ bucket_off, const uint32_t* __restrict__ bucket_ids,
-                       Ev* heap, PktState S)
+__device__ void self_tile(const NocDev& D, uint32_t tile, const uint32_t* __restrict__ len,
+                          const uint64_t* __restrict__ bucket_off, const uint32_t* __restrict__ bucket_ids, Ev* heap,
+                          const PktState& S)
 {
-  const uint32_t tile = blockIdx.x * blockDim.x + threadIdx.x;
-  if (tile >= D.P.tiles) return;
   const uint64_t b = bucket_off[tile], e = bucket_off[tile + 1];
   Ev* h = heap + b;
   uint32_t n = 0;
@@ -289,6 +293,14 @@ __global__ void k_self(NocDev D, const uint32_t* __restrict__ dst, const uint32_
     cadd(D.ctr, tile, GG_NC_TOTAL_LATENCY_PS, zl + ct); cadd(D.ctr, tile, GG_NC_TOTAL_CONTENTION_PS, ct);
     S.t[k] = t; S.zl[k] = zl; S.ct[k] = ct;
   }
+}
+__global__ void k_self(NocDev D, const uint32_t* __restrict__ dst, const uint32_t* __restrict__ len,
+                       const uint64_t* __restrict__ bucket_off, const uint32_t* __restrict__ bucket_ids,
+                       Ev* heap, PktState S)
+{
+  const uint32_t tile = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tile >= D.P.tiles) return;
+  self_tile(D, tile, len, bucket_off, bucket_ids, heap, S);
 }
 
 // Staged packets: a workgroup's packets (a contiguous bucket range [B, E))
@@ -538,6 +550,12 @@ struct SK { uint64_t t; uint32_t i, pad; };
 static_assert(sizeof(SK) == 16 && sizeof(Ev) >= 2 * sizeof(SK), "start runs + arrivals fit a bucket's Ev scratch");
 constexpr size_t kSweepLds = (size_t)kSweepSort * sizeof(SK) + (size_t)kSweepPk * 4 + kSweepPos * 8 + 64;
 __device__ __forceinline__ bool sk_lt(const SK& a, const SK& b) { return a.t < b.t || (a.t == b.t && a.i < b.i); }
+__device__ __forceinline__ uint64_t wave_sum64n(uint64_t v)
+{
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += (uint64_t)__shfl_xor((long long)v, o);
+  return v;
+}
 
 // ascending bitonic sort of a[0, M), M a power of two, all threads of the block
 template <class T, class Lt>
@@ -558,8 +576,12 @@ __device__ void block_bitonic(T* a, uint32_t M, Lt lt)
 
 __global__ __launch_bounds__(kSweepThreads) void k_chain_sweep(NocDev D, int stage, const uint32_t* __restrict__ dst,
     const uint32_t* __restrict__ len, const uint64_t* __restrict__ bucket_off, uint32_t* __restrict__ bucket_ids,
-    Ev* heap, PktState S)
+    Ev* heap, PktState S, unsigned long long* prof)
 {
+  // prof (GG_NOC_PROFILE=1, diagnostics): shader-clock cycles of the setup, the
+  // per-position sorts, serves and hand-offs, requests served, over the chains
+  const uint64_t c_0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+  uint64_t c_sort = 0, c_serve = 0, c_part = 0, c_set = 0, nreq = 0;
   extern __shared__ __attribute__((aligned(16))) uint8_t qlds[];
   const NocParams& P = D.P;
   const uint32_t c = blockIdx.x, line = c / 2, dir = c % 2, tid = threadIdx.x, ln = tid & 63;
@@ -612,7 +634,9 @@ __global__ __launch_bounds__(kSweepThreads) void k_chain_sweep(NocDev D, int sta
   const uint64_t zps = lat_to_ps((uint64_t)P.router_delay + P.link_delay, P.f);
   const int port = stage == 0 ? (dir ? P_RIGHT : P_LEFT) : (dir ? P_UP : P_DOWN);
   uint32_t nb = 0;                                                       // arrivals waiting in Bq
+  if (prof) c_set = __builtin_amdgcn_s_memtime() - c_0;
   for (uint32_t s_ = 0; s_ < npos; ++s_) {
+    const uint64_t c_a = prof ? __builtin_amdgcn_s_memtime() : 0;
     const uint32_t pos = dir ? s_ : npos - 1 - s_;
     const uint64_t r0 = pos ? pc[pos - 1] : 0, r1 = pc[pos];
     const uint32_t m = nb + (uint32_t)(r1 - r0);
@@ -623,6 +647,7 @@ __global__ __launch_bounds__(kSweepThreads) void k_chain_sweep(NocDev D, int sta
       A[i] = i < nb ? Bq[i] : i < m ? G[r0 + (i - nb)] : SK{~0ull, ~0u, 0};
     __syncthreads();
     block_bitonic(A, M, sk_lt);
+    const uint64_t c_b = prof ? __builtin_amdgcn_s_memtime() : 0;
     const uint32_t tile = tile_at(pos);
     if (tid < 64) {
       // one wave serves the batch in order through the port's queue (registers)
@@ -655,6 +680,7 @@ __global__ __launch_bounds__(kSweepThreads) void k_chain_sweep(NocDev D, int sta
       }
     }
     __syncthreads();
+    const uint64_t c_c = prof ? __builtin_amdgcn_s_memtime() : 0;
     // the served batch: packets leaving the chain are written back, the rest arrive at the next position
     const uint32_t nx = dir ? pos + 1 : pos - 1;
     for (uint32_t j = tid; j < m; j += blockDim.x) {
@@ -674,6 +700,126 @@ __global__ __launch_bounds__(kSweepThreads) void k_chain_sweep(NocDev D, int sta
     }
     __syncthreads();
     nb = s_na;
+    if (prof) { c_sort += c_b - c_a; c_serve += c_c - c_b; c_part += __builtin_amdgcn_s_memtime() - c_c; nreq += m; }
+  }
+  if (prof && tid == 0) {
+    atomicAdd(&prof[8 * stage + 0], (unsigned long long)c_set); atomicAdd(&prof[8 * stage + 1], (unsigned long long)c_sort);
+    atomicAdd(&prof[8 * stage + 2], (unsigned long long)c_serve); atomicAdd(&prof[8 * stage + 3], (unsigned long long)c_part);
+    atomicAdd(&prof[8 * stage + 4], (unsigned long long)nreq); atomicAdd(&prof[8 * stage + 5], 1ull);
+    atomicMax(&prof[8 * stage + 6], (unsigned long long)(__builtin_amdgcn_s_memtime() - c_0));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Stages 0 / 3 (injection ports / SELF ports + receive), the default: one
+// wave per tile (kPortWaves tiles per workgroup).  The tile's packets sorted
+// by (time, packet index) in the wave's LDS (bitonic), served in order by the
+// wave through the port's history tree held in its registers (RegQueue), the
+// per-packet results and the tile's counters written by the lanes.  Tiles
+// beyond kPortPk packets or with another queue model: the lane-serial walk
+// (inject_tile / self_tile).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kPortWaves = 4, kPortPk = 2048;
+constexpr size_t kPortLds = (size_t)kPortWaves * kPortPk * sizeof(SK);
+
+__device__ __forceinline__ void nsync()   // LDS ordering between the lanes of one wave of a multi-wave workgroup
+{
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+template <bool SELF>
+__global__ __launch_bounds__(64 * kPortWaves) void k_port_sweep(NocDev D, const uint32_t* __restrict__ len,
+    const uint64_t* __restrict__ bucket_off, const uint32_t* __restrict__ bucket_ids, Ev* heap, PktState S)
+{
+  extern __shared__ __attribute__((aligned(16))) uint8_t qlds[];
+  const NocParams& P = D.P;
+  const uint32_t ln = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t tile = blockIdx.x * kPortWaves + wv;
+  if (tile >= P.tiles) return;
+  const uint64_t b = bucket_off[tile], e = bucket_off[tile + 1];
+  if (b == e) return;
+  const uint32_t n = (uint32_t)min<uint64_t>(e - b, 0xFFFFFFFFull);
+  const bool regq = P.qtype == GG_QM_HISTORY_TREE && P.max_size <= kQMaxNoc;
+  if (n > kPortPk || (P.qm && !regq)) {
+    if (ln == 0) {
+      if (SELF) self_tile(D, tile, len, bucket_off, bucket_ids, heap, S);
+      else inject_tile(D, tile, len, bucket_off, bucket_ids, heap, S);
+    }
+    return;
+  }
+  SK* A = reinterpret_cast<SK*>(qlds) + (size_t)wv * kPortPk;
+  uint32_t M = 1;
+  while (M < n) M <<= 1;
+  // (time, packet index) keys; i = the packet id itself (unique)
+  for (uint32_t i = ln; i < M; i += 64) {
+    if (i < n) { const uint32_t k = bucket_ids[b + i]; A[i] = SK{S.t[k], k, 0}; }
+    else A[i] = SK{~0ull, ~0u, 0};
+  }
+  nsync();
+  for (uint32_t kk = 2; kk <= M; kk <<= 1)
+    for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = ln; i < M; i += 64) {
+        const uint32_t l = i ^ j;
+        if (l > i) {
+          const SK x = A[i], y = A[l];
+          if (((i & kk) == 0) == sk_lt(y, x)) { A[i] = y; A[l] = x; }
+        }
+      }
+      nsync();
+    }
+  const int port = SELF ? P_SELF : 5;
+  HQueue* q = D.q + (uint64_t)tile * 6 + port;
+  HNode* nd = D.nd + ((uint64_t)tile * 6 + port) * P.max_size;
+  RegQueue rq;
+  if (P.qm) rq.load(q, nd, 1, P.analytical != 0, ln);
+  const uint64_t zps = lat_to_ps((uint64_t)P.router_delay + P.link_delay, P.f);
+  uint64_t cq = 0;                                         // uniform: contention cycles of the port
+  uint64_t sf = 0, sb = 0, sl = 0, sc = 0;                  // this lane's packets: flits, bits, latency, contention
+  for (uint32_t j0 = 0; j0 < n; j0 += 64) {
+    const uint32_t cnt = min(64u, n - j0);
+    const bool mine = ln < cnt;
+    const uint32_t k = mine ? A[j0 + ln].i : 0u;
+    const uint32_t bits = mine ? len[k] : 0u;
+    const uint64_t myt = mine ? A[j0 + ln].t : 0;
+    const uint32_t mynf = mine ? (uint32_t)nflits(P, bits) : 0u;
+    uint64_t qmine = 0;
+    for (uint32_t j = 0; j < cnt; ++j) {
+      const uint64_t t = rl64(myt, j);
+      const uint32_t nf = (uint32_t)__builtin_amdgcn_readlane((int)mynf, (int)j);
+      const uint64_t qd = P.qm ? rq.request<true>(time_to_cycles(t, P.f), nf, D.err) : 0;
+      cq += qd;
+      if (ln == j) qmine = qd;
+    }
+    if (mine) {
+      const uint64_t cps = lat_to_ps(qmine, P.f);
+      if (!SELF) {                                          // injection router: delay 0 + queue delay
+        S.t[k] = myt + lat_to_ps(0, P.f) + cps;
+        S.ct[k] += cps;
+        sf += mynf; sb += bits;
+      } else {                                              // SELF hop + serialization + receive
+        const uint64_t ser = lat_to_ps(mynf, P.f);
+        const uint64_t t2 = myt + zps + cps + ser, z2 = S.zl[k] + zps + ser, c2 = S.ct[k] + cps;
+        S.t[k] = t2; S.zl[k] = z2; S.ct[k] = c2;
+        sf += mynf; sb += bits; sl += z2 + c2; sc += c2;
+      }
+    }
+  }
+  if (P.qm) rq.store(q, nd);
+  sf = wave_sum64n(sf); sb = wave_sum64n(sb); sl = wave_sum64n(sl); sc = wave_sum64n(sc);
+  if (ln == 0) {
+    if (!SELF) {
+      cadd(D.ctr, tile, GG_NC_PACKETS_SENT, n); cadd(D.ctr, tile, GG_NC_FLITS_SENT, sf); cadd(D.ctr, tile, GG_NC_BITS_SENT, sb);
+    } else {
+      if (P.qm) { cadd(D.ctr, tile, GG_NC_ROUTER_CONTENTION_CYCLES, cq); cadd(D.ctr, tile, GG_NC_ROUTER_PACKETS, n); }
+      cadd(D.ctr, tile, GG_NC_BUFFER_WRITES, sf); cadd(D.ctr, tile, GG_NC_BUFFER_READS, sf);
+      cadd(D.ctr, tile, GG_NC_SWITCH_ALLOC, n); cadd(D.ctr, tile, GG_NC_CROSSBAR, sf);
+      cadd(D.ctr, tile, GG_NC_LINK_TRAVERSALS, sf);
+      cadd(D.ctr, tile, GG_NC_PACKETS_RECEIVED, n); cadd(D.ctr, tile, GG_NC_FLITS_RECEIVED, sf);
+      cadd(D.ctr, tile, GG_NC_BITS_RECEIVED, sb);
+      cadd(D.ctr, tile, GG_NC_TOTAL_LATENCY_PS, sl); cadd(D.ctr, tile, GG_NC_TOTAL_CONTENTION_PS, sc);
+    }
   }
 }
 
@@ -1205,6 +1351,7 @@ struct gg_noc_state {
   bool staged = true;   // LDS-staged stage kernels where the queues fit (GG_NOC_STAGED=0: HBM-resident, A/B)
   TEv* theap = nullptr; uint32_t* bidx = nullptr; uint64_t tcap = 0, bcap = 0;   // broadcast-tree walk scratch
   uint32_t* tctl = nullptr;                       // grid form: TreeCtl | cnt[kTreeMaxT] | off[kTreeMaxT + 1]
+  unsigned long long* prof = nullptr;             // GG_NOC_PROFILE=1: k_chain_sweep phase cycles (diagnostics)
 };
 
 gg_status gg_noc_alloc(gg_ctx* ctx)
@@ -1229,9 +1376,15 @@ gg_status gg_noc_alloc(gg_ctx* ctx)
   P.qaux = hq_aux(c.queue_model_type, c.basic_moving_avg, c.history_list_no_interleaving);
   if (gg_status e = gg_check_queue_model(c.queue_model_type, P.qaux, P.max_size)) return e;
   S->staged = !(getenv("GG_NOC_STAGED") && atoi(getenv("GG_NOC_STAGED")) == 0);
+  if (getenv("GG_NOC_PROFILE") && atoi(getenv("GG_NOC_PROFILE"))) {
+    GG_HIP(hipMalloc((void**)&S->prof, 16 * sizeof(unsigned long long)));
+    GG_HIP(hipMemset(S->prof, 0, 16 * sizeof(unsigned long long)));
+  }
   GG_HIP(hipFuncSetAttribute((const void*)k_port_staged<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
   GG_HIP(hipFuncSetAttribute((const void*)k_port_staged<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
   GG_HIP(hipFuncSetAttribute((const void*)k_chain_sweep, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
+  GG_HIP(hipFuncSetAttribute((const void*)k_port_sweep<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPortLds));
+  GG_HIP(hipFuncSetAttribute((const void*)k_port_sweep<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPortLds));
   static_assert(kSweepLds <= kStageLdsMax, "the sweep's LDS arrays fit the stage budget");
   GG_HIP(hipFuncSetAttribute((const void*)k_tree_walk<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)(kTreeLdsEv * sizeof(TEv))));
@@ -1249,7 +1402,7 @@ void gg_noc_free(gg_ctx* ctx)
   gg_noc_state* S = ctx->noc;
   if (!S) return;
   void* ps[] = {S->q, S->nd, S->ctr, S->t, S->zl, S->ct, S->cur, S->keys, S->ids, S->heap,
-                S->counts, S->cursor, S->off, S->theap, S->bidx, S->tctl};
+                S->counts, S->cursor, S->off, S->theap, S->bidx, S->tctl, S->prof};
   for (void* p : ps) if (p) hipFree(p);
   delete S;
   ctx->noc = nullptr;
@@ -1412,7 +1565,15 @@ gg_status gg_noc_hbh(gg_ctx* ctx, const uint32_t* src, const uint32_t* dst, cons
     const size_t qb = qimg_bytes(P.max_size);
     const size_t port_lds = kPortTiles * qb, chain_lds = (stage == 1 ? P.w : P.h) * qb;
     const bool staged = S->staged && ((stage == 0 || stage == 3) ? port_lds : chain_lds) <= kStageLdsMax;
-    if (staged && (stage == 0 || stage == 3)) {
+    if (S->staged && (stage == 0 || stage == 3)) {
+      const uint32_t pb = (P.tiles + kPortWaves - 1) / kPortWaves;
+      if (stage == 0)
+        hipLaunchKernelGGL(k_port_sweep<false>, dim3(pb), dim3(64 * kPortWaves), kPortLds, s, D, len, S->off, S->ids,
+                           S->heap, PS);
+      else
+        hipLaunchKernelGGL(k_port_sweep<true>, dim3(pb), dim3(64 * kPortWaves), kPortLds, s, D, len, S->off, S->ids,
+                           S->heap, PS);
+    } else if (staged && (stage == 0 || stage == 3)) {
       const uint32_t pb = (P.tiles + kPortTiles - 1) / kPortTiles;
       // the whole LDS budget: the packet count of a workgroup is known on the device only
       if (stage == 0)
@@ -1421,7 +1582,7 @@ gg_status gg_noc_hbh(gg_ctx* ctx, const uint32_t* src, const uint32_t* dst, cons
         hipLaunchKernelGGL(k_port_staged<true>, dim3(pb), dim3(64), kStageLdsMax, s, D, dst, len, S->off, S->ids, S->heap, PS);
     } else if (staged) {
       hipLaunchKernelGGL(k_chain_sweep, dim3(nb), dim3(kSweepThreads), kStageLdsMax, s, D, stage - 1, dst, len, S->off,
-                         S->ids, S->heap, PS);
+                         S->ids, S->heap, PS, S->prof);
     } else if (stage == 0)
       hipLaunchKernelGGL(k_inject, dim3(tb), dim3(64), 0, s, D, src, dst, len, S->off, S->ids, S->heap, PS);
     else if (stage == 3)
@@ -1432,6 +1593,16 @@ gg_status gg_noc_hbh(gg_ctx* ctx, const uint32_t* src, const uint32_t* dst, cons
     GG_HIP(hipGetLastError());
   }
   gg_timer_end(ctx, "noc_hop_by_hop", s);
+  if (S->prof) {
+    unsigned long long h[16];
+    GG_HIP(hipMemcpyAsync(h, S->prof, sizeof(h), hipMemcpyDeviceToHost, s));
+    GG_HIP(hipStreamSynchronize(s));
+    for (int st = 0; st < 2; ++st)
+      fprintf(stderr, "[gg_noc sweep %c] chains %llu requests %llu | cycles summed over chains: setup %llu sort %llu "
+              "serve %llu hand-off %llu | slowest chain %llu\n", st ? 'Y' : 'X', h[8 * st + 5], h[8 * st + 4],
+              h[8 * st + 0], h[8 * st + 1], h[8 * st + 2], h[8 * st + 3], h[8 * st + 6]);
+    GG_HIP(hipMemsetAsync(S->prof, 0, sizeof(h), s));
+  }
   return GG_OK;
 }
 

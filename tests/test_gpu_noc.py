@@ -138,10 +138,13 @@ def test_hop_by_hop_matches_oracle(T, n, span, batches):
     assert int(ref[2].sum()) > 0                                   # contention was exercised
 
 
-@pytest.mark.parametrize("max_size", [2, 129])
+@pytest.mark.parametrize("max_size", [3, 129])
 def test_hop_by_hop_list_sizes_match_oracle(max_size):
-    """max_list_size 2 (the prune on almost every request) and 129 (beyond the
-    register queue: the general walk)."""
+    """max_list_size 3 (the prune on almost every request, the M/G/1 branch
+    often) and 129 (beyond the register queue: the general walk).  At 2 the
+    M/G/1 branch reaches delays of ~1e16 cycles whose picosecond value
+    overflows UInt64 (Latency::toPicosec's double -> UInt64 cast,
+    time_types.h:81-90, is undefined there): outside the domain."""
     torch = torch_dev()
     cfg = C.default_config(64, net_model=C.NET_EMESH_HOP_BY_HOP, max_list_size=max_size)
     src, dst, bits, t = packets(64, 20000, 5 + max_size, 500000)

@@ -125,7 +125,7 @@ def oracle_tree(cfg, src, dst, bits, t, batches=1):
                                                       (64, 3000, 100000, 1, 0.02, 1), (16, 2000, 100000, 1, 0.2, 0),
                                                       (256, 2000, 400000, 1, 0.01, 1), (256, 3000, 600000, 1, 0.03, 1),
                                                       # one thread owns several routers (T > the workgroup's threads)
-                                                      (2048, 1500, 400000, 1, 0.004, 1),
+                                                      (2116, 1500, 400000, 1, 0.004, 1),
                                                       (4096, 1500, 400000, 1, 0.004, 1),
                                                       # beyond the windowed walk's LDS arrays: the serial walk
                                                       (4225, 600, 200000, 1, 0.01, 1)])
