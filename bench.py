@@ -125,7 +125,7 @@ def parse():
     p.add_argument("--long-per-tile", type=int, default=2048, help="coherent_long section: accesses per tile")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
-    p.add_argument("--sections", default="coherent_long,hop_counter,stress,fft,private,private_16way,noc",
+    p.add_argument("--sections", default="coherent_long,exchange,hop_counter,stress,fft,private,private_16way,noc",
                    help="extra sections at N = 1 (comma list; '' = none)")
     p.add_argument("--hc-per-tile", type=int, default=1024, help="hop_counter section: accesses per tile")
     p.add_argument("--private-per-tile", type=int, default=1 << 20)
@@ -314,6 +314,58 @@ def coherent_long_section(args, dev):
                      "at %dx its trace length" % (T, N, H, args.net, K, N // max(1, args.per_tile)))
     r["unit"] = "accesses/s"
     return r
+
+
+def exchange_section(args, dev):
+    """The per-quantum cost of the multi-rank exchange (gg_round_exchange:
+    grouped per-peer slot send / receive + status all-reduces over RCCL, one
+    host sync) measured on one GPU: the headline workload through
+    gg_coherent_run_ranks over a one-rank RCCL communicator against the
+    device-driven single-context loop (gg_coherent_run); same results bit for
+    bit (checked)."""
+    import socket
+    import torch
+    import torch.distributed as dist
+    from graphite_amd import config as C
+    from graphite_amd import backend as B
+    from graphite_amd import coherent as CO
+    if dist.is_initialized():
+        return {"skipped": "a process group already exists"}
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, world_size=1, rank=0)
+    try:
+        T, N, H, K = args.tiles, args.per_tile, args.hot_lines, args.shards
+        cfg = C.default_config(T, num_shards=K, net_model=NET[args.net])
+        addr, meta, offs = coherent_workload(T, N, H, dev)
+        res, outs = {}, {}
+        for mode in ("single", "rccl", "single", "rccl"):        # the second of each is timed
+            be = B.Backend(cfg)
+            out = torch.zeros(T * N, dtype=torch.int64, device=dev)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            if mode == "rccl":
+                CO.run_rccl(be, addr, meta, offs, out)
+            else:
+                be.coherent_run(addr, meta, offs, out)
+            torch.cuda.synchronize()
+            res[mode] = time.perf_counter() - t0
+            ri = be.coherent_stats()[2]
+            outs[mode] = out.cpu().numpy()
+            quanta = int(ri[C.RUN_INFO.index("quanta")])
+            be.close()
+        same = bool(np.array_equal(outs["single"], outs["rccl"]))
+        return {"workload": "the headline workload (%d tiles x %d accesses, %s, %d shards) on one GPU" % (T, N, args.net, K),
+                "quanta": quanta, "single_context_seconds": res["single"], "rccl_one_rank_seconds": res["rccl"],
+                "exchange_us_per_quantum": 1e6 * (res["rccl"] - res["single"]) / max(1, quanta),
+                "bit_identical": same,
+                "note": "the one-rank round still runs every quantum's steps from the host (two syncs per quantum: "
+                        "the step batches' quiet flag and the exchange) where the single context runs the quantum "
+                        "loop on the device; the difference per quantum bounds the exchange's fixed cost"}
+    finally:
+        dist.destroy_process_group()
 
 
 def hop_counter_section(args, dev):
@@ -749,6 +801,8 @@ def main():
         try:
             if name == "coherent_long" and args.long_per_tile:
                 r = coherent_long_section(args, dev)
+            elif name == "exchange":
+                r = exchange_section(args, dev)
             elif name == "hop_counter":
                 r = hop_counter_section(args, dev)
             elif name == "fft" and args.fft_m:

@@ -58,7 +58,7 @@ EXPORTS = ["gg_abi_version", "gg_last_error", "gg_config_default", "gg_create", 
            "gg_coherent_begin", "gg_coherent_quantum", "gg_coherent_export", "gg_coherent_import",
            "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace", "gg_shard_map",
            "gg_kernel_stats", "gg_round_exchange", "gg_coherent_run_ranks", "gg_gen_stress_trace",
-           "gg_split_accesses", "gg_combine_accesses"]
+           "gg_split_accesses", "gg_combine_accesses", "gg_dump_summary"]
 
 
 class _CStatus(ctypes.Structure):
@@ -115,10 +115,11 @@ def load():
     L.gg_coherent_run_ranks.argtypes = [vp, vp, ctypes.POINTER(_Trace), vp, vp]
     L.gg_split_accesses.argtypes = [vp, vp, vp, vp, u32, u32, vp, vp, vp, u64, ctypes.POINTER(u64), vp, vp]
     L.gg_combine_accesses.argtypes = [vp, vp, u64, vp, vp, vp]
+    L.gg_dump_summary.argtypes = [vp, i32, ctypes.c_char_p, u64, ctypes.POINTER(u64)]
     for name in ["gg_kernel_stats", "gg_shard_map", "gg_coherent_begin", "gg_coherent_quantum", "gg_coherent_export",
                  "gg_coherent_import", "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace",
                  "gg_round_exchange", "gg_coherent_run_ranks", "gg_gen_stress_trace", "gg_split_accesses",
-                 "gg_combine_accesses"]:
+                 "gg_combine_accesses", "gg_dump_summary"]:
         getattr(L, name).restype = i32
     for name in ["gg_reset", "gg_cache_access_batch", "gg_cache_get_counters", "gg_cache_get_line_info",
                  "gg_cache_set_line_info", "gg_cache_access_line", "gg_cache_insert_line",
@@ -334,6 +335,17 @@ class Backend:
         _check(load().gg_coherent_get_stats(self.h, st.ctypes.data_as(ctypes.c_void_p),
                                             cc.ctypes.data_as(ctypes.c_void_p), ri.ctypes.data_as(ctypes.c_void_p)))
         return st.reshape(T, NUM_TILE_STATS), cc.reshape(T, 2, NUM_CACHE_COUNTERS), ri
+
+    def dump_summary(self, table=False):
+        """The sim.out text of the context's statistics (gg_dump_summary): one
+        "Tile t Summary:" block per tile, or TileManager's table."""
+        L = load()
+        need = ctypes.c_uint64(0)
+        fmt = 1 if table else 0
+        _check(L.gg_dump_summary(self.h, fmt, None, 0, ctypes.byref(need)))
+        buf = ctypes.create_string_buffer(need.value)
+        _check(L.gg_dump_summary(self.h, fmt, buf, need.value, ctypes.byref(need)))
+        return buf.value.decode()
 
     def queue_delay_batch(self, pkt_time, proc_time, min_processing_time=1):
         t = np.ascontiguousarray(pkt_time, np.uint64)

@@ -238,18 +238,11 @@ int main(int argc, char** argv)
           hip_check(hipMemcpy(v->data(), d.p, sizeof(uint64_t) * v->size(), hipMemcpyDeviceToHost), "hipMemcpy");
         }
       }
-      const uint64_t zero_net[GG_NUM_NET_COUNTERS] = {0};
       std::vector<std::string> per_tile;
       for (uint32_t t = 0; rank == 0 && t < tiles; ++t) {
         std::ostringstream os;
-        writeMemorySummary(os, cfg, &st[(size_t)t * GG_NUM_TILE_STATS], &cc[(size_t)t * 2 * GG_NUM_CACHE_COUNTERS]);
-        // Network::outputSummary (network.cc:79-89): the static networks below SYSTEM,
-        // User (no traffic in a trace-driven run; emesh_hop_counter, carbon_sim.cfg [network]) then Memory
-        os << "Network Summary: " << std::endl << "  Network (User): " << std::endl;
-        writeNetworkSummary(os, zero_net, cfg.frequency_ghz, GG_NET_EMESH_HOP_COUNTER);
-        os << "  Network (Memory): " << std::endl;
-        writeNetworkSummary(os, &nc[(size_t)t * GG_NUM_NET_COUNTERS], cfg.frequency_ghz, cfg.net_model,
-                            cfg.queue_model_enabled != 0);
+        writeTileSummary(os, cfg, &st[(size_t)t * GG_NUM_TILE_STATS], &cc[(size_t)t * 2 * GG_NUM_CACHE_COUNTERS],
+                         &nc[(size_t)t * GG_NUM_NET_COUNTERS]);
         if (table) per_tile.push_back(os.str());
         else std::cout << "Tile " << t << " Summary:" << std::endl << os.str();
       }

@@ -295,6 +295,27 @@ inline void writeMemorySummary(std::ostream& out, const gg_config& c, const uint
   writeDirectorySummary(out, tile_stats, directorySizing(c));
 }
 
+// One tile's summary text in the coherent mode: the memory part, then
+// Network::outputSummary (network.cc:79-89): the static networks below SYSTEM,
+// User (no traffic in a trace-driven run; emesh_hop_counter, carbon_sim.cfg
+// [network]) then Memory.  Mode P (no tile statistics): the cache summary only,
+// then the networks.
+inline void writeTileSummary(std::ostream& os, const gg_config& cfg, const uint64_t* tile_stats,
+                             const uint64_t* cache_counters, const uint64_t* net_counters)
+{
+  static const uint64_t zero_net[GG_NUM_NET_COUNTERS] = {0};
+  if (tile_stats) writeMemorySummary(os, cfg, tile_stats, cache_counters);
+  else {
+    os << "Cache Summary:\n";
+    writeCacheSummary(os, "L1-D", cache_counters, false);
+    writeCacheSummary(os, "L2", cache_counters + GG_NUM_CACHE_COUNTERS, true);
+  }
+  os << "Network Summary: " << std::endl << "  Network (User): " << std::endl;
+  writeNetworkSummary(os, zero_net, cfg.frequency_ghz, GG_NET_EMESH_HOP_COUNTER);
+  os << "  Network (Memory): " << std::endl;
+  writeNetworkSummary(os, net_counters, cfg.frequency_ghz, cfg.net_model, cfg.queue_model_enabled != 0);
+}
+
 // TileManager::outputSummary's table (tile_manager_summary.cc:60-198): every
 // tile's summary text ("label: value" lines) becomes one column, the row
 // headings are the labels of tile 0's lines, the columns are padded to their

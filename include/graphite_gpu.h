@@ -433,6 +433,18 @@ gg_status gg_coherent_run_ranks(gg_ctx* ctx, void* nccl_comm, const gg_trace* tr
  * context does not own read 0.  Network counters: gg_noc_get_counters.      */
 gg_status gg_coherent_get_stats(gg_ctx* ctx, uint64_t* tile_stats, uint64_t* cache, uint64_t* run_info);
 
+/* The sim.out text of the context's statistics (replaces the per-tile
+ * outputSummary chain: TileManager::outputSummary, tile_manager_summary.cc:
+ * 60-244 -> Tile / MemoryManager / Cache / DramPerfModel / DirectoryCache /
+ * Network summaries).  GG_SUMMARY_BLOCKS: one "Tile t Summary:" block per
+ * tile; GG_SUMMARY_TABLE: TileManager's table (one column per tile).  Coherent
+ * mode after gg_coherent_run: memory (L1-D, L2, DRAM, directory) and network
+ * blocks; private-cache mode: the cache summaries and the network blocks.
+ * *needed = the text's bytes + 1; buf (host, cap bytes) receives the
+ * NUL-terminated text when it fits, else GG_ERR_RANGE (buf NULL: size query). */
+enum { GG_SUMMARY_BLOCKS = 0, GG_SUMMARY_TABLE = 1 };
+gg_status gg_dump_summary(gg_ctx* ctx, int format, char* buf, uint64_t cap, uint64_t* needed);
+
 /* Synthetic workload generator (not part of the reference boundary; the
  * reference has no trace capture): fills a tile-major trace of
  * `per_tile` records for tiles [tile_begin, tile_begin + tiles) with the

@@ -115,3 +115,34 @@ def test_coherent_summary_table_matches_reference_layout():
             cur.append(line)
     assert len(blocks) == 16
     assert table == reference_table(["".join(b) for b in blocks])
+
+
+@pytest.mark.parametrize("table", [False, True])
+def test_dump_summary_through_the_abi(table):
+    """gg_dump_summary (the sim.out text through the C ABI, for callers that
+    are not C++): the same blocks / table as the host mirror prints, against
+    the reference format filled with the oracle's statistics."""
+    import torch
+    from graphite_amd import backend as B
+    from oracle import pyoracle as po
+    T, N = 16, 400
+    cfg = C.default_config(T, net_model=C.NET_EMESH_HOP_BY_HOP)
+    a, m, o = po.gen_trace(T, N, hot_lines=64)
+    be = B.Backend(cfg)
+    be.coherent_run(torch.from_numpy(a.view(np.int64)).cuda(), torch.from_numpy(m.view(np.int32)).cuda(), o)
+    torch.cuda.synchronize()
+    txt = be.dump_summary(table=table)
+    exp = _expected(T, N, C.NET_EMESH_HOP_BY_HOP, True)
+    if not table:
+        assert txt.splitlines() == exp
+    else:
+        from tests.test_host_mirror import reference_table
+        blocks, cur = [], None
+        for line in exp:
+            if line.startswith("Tile ") and line.endswith(" Summary:"):
+                cur = []
+                blocks.append(cur)
+            else:
+                cur.append(line + "\n")
+        assert txt == reference_table(["".join(b) for b in blocks])
+    be.close()
