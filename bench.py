@@ -80,9 +80,13 @@ def pmc_traffic(kernel, key):
             continue
         if d.get("workload_key") != key:
             continue
-        v = d.get("kernels", {}).get(kernel)
+        ks = d.get("kernels", {})
+        # the summary keys are rocprof's names (template arguments included)
+        v = ks.get(kernel) or next((ks[k] for k in ks if k.split("<")[0] == kernel), None)
         if v and "hbm_bytes" in v:
             best = {"bytes": v["hbm_bytes"], "source": os.path.relpath(f, ROOT)}
+            if "traffic_factors" in v:
+                best["factors"] = v["traffic_factors"]
     return best
 
 
@@ -125,6 +129,8 @@ def parse():
     p.add_argument("--long-per-tile", type=int, default=2048, help="coherent_long section: accesses per tile")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--no-kernel-profile", action="store_true",
+                   help="skip the extra instrumented run (for an external rocprofv3 trace of the timed runs alone)")
     p.add_argument("--sections", default="coherent_long,exchange,hop_counter,stress,fft,private,private_16way,noc",
                    help="extra sections at N = 1 (comma list; '' = none)")
     p.add_argument("--hc-per-tile", type=int, default=1024, help="hop_counter section: accesses per tile")
@@ -730,6 +736,11 @@ def private_section(args, dev):
 def main():
     args = parse()
     maybe_spawn(args)
+    # stdout carries the one JSON line only: libraries that print on stdout
+    # (RCCL's version banner at communicator creation) go to stderr
+    json_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
     from graphite_amd import config as C
@@ -745,7 +756,8 @@ def main():
     if K % world:
         raise SystemExit("bench.py: %d logical shards do not split over %d ranks" % (K, world))
     head = coherent_run(args, T, N, H, K, net, world, rank, dev, args.steps, args.warmup,
-                        not args.no_verify, world == 1 and not args.no_cpu_baseline)
+                        not args.no_verify, world == 1 and not args.no_cpu_baseline,
+                        kernel_profile=not args.no_kernel_profile)
     if rank == 0:
         kern = {k: v for k, v in head["kernels"].items() if not k.startswith("_")}
         dom = max(kern, key=lambda k: kern[k]["total_ms"]) if kern else None
@@ -794,6 +806,12 @@ def main():
         if prof:
             out["roofline"]["traffic"] = prof["bytes"]
             out["roofline"]["traffic_source"] = prof["source"]
+            if "factors" in prof:
+                out["roofline"]["traffic_factors"] = prof["factors"]
+            out["roofline"]["traffic_note"] = ("HBM bytes per launch (FETCH_SIZE / WRITE_SIZE, calibrated at 8-B loads / "
+                                               "scattered 4-B stores): router queue images and packet records read and "
+                                               "written back per launch, the state SURVEY.md §8d excludes from the "
+                                               "algorithmic bytes")
         if "cpu_baseline" in head:
             out["cpu_baseline"] = head["cpu_baseline"]
     secs = [x for x in args.sections.split(",") if x] if world == 1 else []
@@ -822,7 +840,7 @@ def main():
             print("bench.py: section %s failed: %r" % (name, e), file=sys.stderr)
         out[name] = r
     if rank == 0:
-        print(json.dumps(out))
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     if world > 1:
         D.barrier()
         dist.destroy_process_group()

@@ -31,7 +31,7 @@ fi
 if [ -n "$PROF" ]; then
   cd /tmp
   timeout -k 10 ${PROF_LIMIT:-300} rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run -- \
-    python3 "$GRAFT_REPO_ROOT/bench.py" --sections "" --no-cpu-baseline --no-verify --steps 3 --warmup 1 $PROF_ARGS \
+    python3 "$GRAFT_REPO_ROOT/bench.py" --sections "" --no-cpu-baseline --no-verify --no-kernel-profile --steps 3 --warmup 1 $PROF_ARGS \
     > "$GRAFT_REPO_ROOT/$OUT/prof.json" 2> "$GRAFT_REPO_ROOT/$OUT/prof.err" || { tail -20 "$GRAFT_REPO_ROOT/$OUT/prof.err"; exit 1; }
   cd "$GRAFT_REPO_ROOT"
   f=$(find $OUT/prof -name "*kernel_stats.csv" | head -1)
