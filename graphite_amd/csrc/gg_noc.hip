@@ -550,6 +550,12 @@ struct SK { uint64_t t; uint32_t i, pad; };
 static_assert(sizeof(SK) == 16 && sizeof(Ev) >= 2 * sizeof(SK), "start runs + arrivals fit a bucket's Ev scratch");
 constexpr size_t kSweepLds = (size_t)kSweepSort * sizeof(SK) + (size_t)kSweepPk * 4 + kSweepPos * 8 + 64;
 __device__ __forceinline__ bool sk_lt(const SK& a, const SK& b) { return a.t < b.t || (a.t == b.t && a.i < b.i); }
+__device__ __forceinline__ void nsync()   // LDS ordering between the lanes of one wave of a multi-wave workgroup
+{
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
 __device__ __forceinline__ uint64_t wave_sum64n(uint64_t v)
 {
 #pragma unroll
@@ -574,9 +580,9 @@ __device__ void block_bitonic(T* a, uint32_t M, Lt lt)
     }
 }
 
-__global__ __launch_bounds__(kSweepThreads) void k_chain_sweep(NocDev D, int stage, const uint32_t* __restrict__ dst,
+__device__ void chain_sweep(NocDev D, int stage, const uint32_t* __restrict__ dst,
     const uint32_t* __restrict__ len, const uint64_t* __restrict__ bucket_off, uint32_t* __restrict__ bucket_ids,
-    Ev* heap, PktState S, unsigned long long* prof)
+    Ev* heap, PktState S, unsigned long long* prof, uint32_t c)
 {
   // prof (GG_NOC_PROFILE=1, diagnostics): shader-clock cycles of the setup, the
   // per-position sorts, serves and hand-offs, requests served, over the chains
@@ -584,7 +590,7 @@ __global__ __launch_bounds__(kSweepThreads) void k_chain_sweep(NocDev D, int sta
   uint64_t c_sort = 0, c_serve = 0, c_part = 0, c_set = 0, nreq = 0;
   extern __shared__ __attribute__((aligned(16))) uint8_t qlds[];
   const NocParams& P = D.P;
-  const uint32_t c = blockIdx.x, line = c / 2, dir = c % 2, tid = threadIdx.x, ln = tid & 63;
+  const uint32_t line = c / 2, dir = c % 2, tid = threadIdx.x, ln = tid & 63;
   const uint64_t b = bucket_off[c], e = bucket_off[c + 1];
   if (b == e) return;
   const uint32_t n = (uint32_t)min<uint64_t>(e - b, 0xFFFFFFFFull);
@@ -709,6 +715,267 @@ __global__ __launch_bounds__(kSweepThreads) void k_chain_sweep(NocDev D, int sta
     atomicMax(&prof[8 * stage + 6], (unsigned long long)(__builtin_amdgcn_s_memtime() - c_0));
   }
 }
+__global__ __launch_bounds__(kSweepThreads) void k_chain_sweep(NocDev D, int stage, const uint32_t* __restrict__ dst,
+    const uint32_t* __restrict__ len, const uint64_t* __restrict__ bucket_off, uint32_t* __restrict__ bucket_ids,
+    Ev* heap, PktState S, unsigned long long* prof)
+{
+  chain_sweep(D, stage, dst, len, bucket_off, bucket_ids, heap, S, prof, blockIdx.x);
+}
+
+// ---------------------------------------------------------------------------
+// Stages X / Y as a pipeline of time slabs (the default for chains of <=
+// kPipePos positions): the positions of a chain serve concurrently, one wave
+// per kPipeK positions.  Time is cut into slabs [T_{r-1}, T_r); at diagonal
+// step d the position of travel index s serves its pending packets of slab
+// r = d - s in (time, index) order.  That is the global event order at the
+// port: a packet reaching position s before T_r left position s - 1 before
+// T_r (a hop takes >= router + link delay >= 0), so position s - 1 served it
+// in a slab <= r, at a step <= d - 1; and every packet still to come to s
+// arrives at T_r or later.  Each position keeps its pending packets in an HBM
+// pool (only its wave touches it) and receives the packets of the position
+// before it through a two-parity incoming list (written at step d, taken at
+// step d + 1); the slab's packets are sorted in the wave's LDS (bitonic) and
+// served through the port's history tree held in the wave's registers
+// (RegQueue) for the whole chain.  A slab part too large for the LDS batch
+// is cut at a lower time bound (bisection) and served in parts: the order is
+// unchanged.  Chains beyond the limits take the position sweep.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kPipePos = 32, kPipeK = 2, kPipeWaves = kPipePos / kPipeK, kPipeBatch = 256, kPipePk = 6144;
+constexpr size_t kPipeLds = (size_t)kPipeWaves * kPipeBatch * sizeof(SK) + (size_t)kPipePk * 4 + 3 * kPipePos * 4 + 64;
+static_assert(kPipeLds <= kStageLdsMax, "pipeline LDS");
+
+// one position of a pipelined chain, held by a wave across the slabs
+struct PipePos {
+  RegQueue rq;
+  uint64_t cq, cf, m;       // contention cycles, flits, requests (wave-uniform)
+};
+
+__device__ __forceinline__ bool sk_below(const SK& x, uint64_t bt, uint32_t bi) { return x.t < bt || (x.t == bt && x.i < bi); }
+
+__global__ __launch_bounds__(64 * kPipeWaves) void k_chain_pipe(NocDev D, int stage, const uint32_t* __restrict__ dst,
+    const uint32_t* __restrict__ len, const uint64_t* __restrict__ bucket_off, uint32_t* __restrict__ bucket_ids,
+    Ev* heap, PktState S, SK* pscr, uint64_t pstride, unsigned long long* prof)
+{
+  extern __shared__ __attribute__((aligned(16))) uint8_t qlds[];
+  const NocParams& P = D.P;
+  const uint32_t c = blockIdx.x, line = c / 2, dir = c % 2, tid = threadIdx.x, ln = tid & 63, wv = tid >> 6;
+  const uint64_t b = bucket_off[c], e = bucket_off[c + 1];
+  if (b == e) return;
+  const uint32_t npos = stage == 0 ? P.w : P.h;
+  const bool regq = P.qtype == GG_QM_HISTORY_TREE && P.max_size <= kQMaxNoc;
+  if (e - b > kPipePk || npos > kPipePos || (P.qm && !regq)) {
+    chain_sweep(D, stage, dst, len, bucket_off, bucket_ids, heap, S, prof, c);
+    return;
+  }
+  const uint32_t n = (uint32_t)(e - b);
+  SK* A = reinterpret_cast<SK*>(qlds);                                         // [waves][kPipeBatch] slab batches
+  uint32_t* info = reinterpret_cast<uint32_t*>(A + (size_t)kPipeWaves * kPipeBatch);   // [n] flits | exit position << 16
+  uint32_t* npool = info + kPipePk;                                            // [npos] pool counts
+  uint32_t* ninc = npool + kPipePos;                                           // [2][npos] incoming counts
+  __shared__ uint32_t s_bad, s_left;
+  __shared__ uint64_t s_tmin, s_tmax;
+  uint32_t* ids = bucket_ids + b;
+  // per position (travel index s) in HBM: pool [n], incoming [2][n]
+  SK* base = pscr + (size_t)b * pstride;
+  auto pool = [&](uint32_t s) { return base + (size_t)s * 3 * n; };
+  auto inc = [&](uint32_t s, uint32_t par) { return base + (size_t)s * 3 * n + (size_t)(1 + par) * n; };
+  auto pos_of = [&](uint32_t tile) { return stage == 0 ? tile % P.w : tile / P.w; };
+  auto tile_at = [&](uint32_t pos) -> uint32_t { return stage == 0 ? line * P.w + pos : pos * P.w + line; };
+  auto sidx = [&](uint32_t pos) { return dir ? pos : npos - 1 - pos; };        // travel index of a position
+  auto pos_at = [&](uint32_t s) { return dir ? s : npos - 1 - s; };
+  if (tid == 0) { s_bad = 0; s_left = n; s_tmin = ~0ull; s_tmax = 0; }
+  for (uint32_t i = tid; i < kPipePos; i += blockDim.x) { npool[i] = 0; ninc[i] = 0; ninc[kPipePos + i] = 0; }
+  __syncthreads();
+  // 1. the chain's ids in index order (i = rank by index), info, start pools
+  uint32_t M = 1;
+  while (M < n) M <<= 1;
+  uint32_t* ia = reinterpret_cast<uint32_t*>(A);                               // n <= kPipePk <= waves * batch * 4
+  for (uint32_t i = tid; i < M; i += blockDim.x) ia[i] = i < n ? ids[i] : 0xFFFFFFFFu;
+  __syncthreads();
+  block_bitonic(ia, M, [](uint32_t x, uint32_t y) { return x < y; });
+  for (uint32_t i = tid; i < n; i += blockDim.x) {
+    const uint32_t k = ia[i];
+    ids[i] = k;
+    const uint64_t nf = nflits(P, len[k]);
+    if (nf >= (1u << 16)) atomicOr(&s_bad, 1u);
+    info[i] = (uint32_t)nf | (pos_of(dst[k]) << 16);
+  }
+  __syncthreads();
+  if (s_bad) { chain_sweep(D, stage, dst, len, bucket_off, bucket_ids, heap, S, prof, c); return; }
+  uint64_t tmn = ~0ull, tmx = 0;
+  for (uint32_t i = tid; i < n; i += blockDim.x) {
+    const uint32_t k = ids[i];
+    const uint64_t t = S.t[k];
+    const uint32_t s = sidx(pos_of(S.cur[k]));
+    pool(s)[atomicAdd(&npool[s], 1u)] = SK{t, i, 0};
+    tmn = t < tmn ? t : tmn; tmx = t > tmx ? t : tmx;
+  }
+  atomicMin((unsigned long long*)&s_tmin, (unsigned long long)tmn);
+  atomicMax((unsigned long long*)&s_tmax, (unsigned long long)tmx);
+  __syncthreads();
+  // slab width: about 64 packets of the chain's start times per slab
+  const uint64_t t0 = s_tmin;
+  const uint64_t delta = max<uint64_t>(1, (s_tmax - s_tmin) / max<uint32_t>(1, n / 64) + 1);
+  const uint64_t zps = lat_to_ps((uint64_t)P.router_delay + P.link_delay, P.f);
+  const int port = stage == 0 ? (dir ? P_RIGHT : P_LEFT) : (dir ? P_UP : P_DOWN);
+  // this wave's positions: travel indices wv + j * waves
+  PipePos pp[kPipeK];
+#pragma unroll
+  for (uint32_t j = 0; j < kPipeK; ++j) {
+    const uint32_t s = wv + j * kPipeWaves;
+    pp[j].cq = 0; pp[j].cf = 0; pp[j].m = 0;
+    if (s < npos && P.qm) {
+      const uint32_t tile = tile_at(pos_at(s));
+      pp[j].rq.load(D.q + (uint64_t)tile * 6 + port, D.nd + ((uint64_t)tile * 6 + port) * P.max_size, 1,
+                    P.analytical != 0, ln);
+    }
+  }
+  SK* mine = A + (size_t)wv * kPipeBatch;
+  constexpr uint64_t kMaxSteps = 1ull << 24;
+  for (uint64_t d = 0;; ++d) {
+    const uint32_t par = (uint32_t)(d & 1);
+#pragma unroll
+    for (uint32_t j = 0; j < kPipeK; ++j) {
+      const uint32_t s = wv + j * kPipeWaves;
+      if (s >= npos || d < s) continue;
+      const uint64_t r = d - s;
+      const uint64_t Tr = (r + 1 >= (~0ull - t0) / delta) ? ~0ull : t0 + (r + 1) * delta;   // slab r = [.., Tr)
+      // take the incoming packets of the last step into the pool
+      SK* pl = pool(s);
+      uint32_t np = npool[s];
+      {
+        const uint32_t q = par ^ 1u;                                           // the parity written at step d - 1
+        uint32_t* cnt = &ninc[q * kPipePos + s];
+        const uint32_t k_in = *cnt;
+        const SK* src = inc(s, q);
+        for (uint32_t i = ln; i < k_in; i += 64) pl[np + i] = src[i];
+        np += k_in;
+        nsync();
+        if (ln == 0) *cnt = 0;
+      }
+      // serve every pending packet below (Tr, 0), in parts of <= kPipeBatch: a part ends at a
+      // lower bound (time, index) found by bisection (on the time, then on the index)
+      const uint32_t pos = pos_at(s), nx = dir ? pos + 1 : pos - 1;
+      const uint32_t tile = tile_at(pos);
+      (void)tile;
+      for (;;) {
+        auto count_below = [&](uint64_t bt, uint32_t bi) {
+          uint32_t cm = 0;
+          for (uint32_t i = ln; i < np; i += 64) cm += sk_below(pl[i], bt, bi);
+          return (uint32_t)wave_sum64n(cm);
+        };
+        const uint32_t cntb = count_below(Tr, 0);
+        if (cntb == 0) break;
+        uint64_t bt = Tr;
+        uint32_t bi = 0;
+        if (cntb > kPipeBatch) {
+          uint64_t lo = 0, hi = Tr;                                           // count(< lo) <= batch < count(< hi)
+          while (hi - lo > 1) {
+            const uint64_t mid = lo + (hi - lo) / 2;
+            if (count_below(mid, 0) <= kPipeBatch) lo = mid; else hi = mid;
+          }
+          bt = lo;
+          if (count_below(lo, 0) == 0) {                                      // > batch packets at time lo: by index
+            uint32_t ilo = 0, ihi = n;                                        // count(< (lo, ilo)) <= batch < count(< (lo, ihi))
+            while (ihi - ilo > 1) {
+              const uint32_t mid = ilo + (ihi - ilo) / 2;
+              if (count_below(lo, mid) <= kPipeBatch) ilo = mid; else ihi = mid;
+            }
+            bi = ilo;
+          }
+        }
+        // split the pool: the part below bound to LDS, the rest compacted in place
+        uint32_t m = 0, keep = 0;
+        for (uint32_t i0 = 0; i0 < np; i0 += 64) {
+          const uint32_t i = i0 + ln;
+          SK x{~0ull, ~0u, 0};
+          if (i < np) x = pl[i];
+          const bool take = i < np && sk_below(x, bt, bi);
+          const bool kp = i < np && !take;
+          const uint64_t bt = __ballot(take), bk = __ballot(kp);
+          const uint64_t below = (1ull << ln) - 1;
+          if (take) mine[m + __builtin_popcountll(bt & below)] = x;
+          nsync();
+          if (kp) pl[keep + __builtin_popcountll(bk & below)] = x;
+          m += (uint32_t)__builtin_popcountll(bt);
+          keep += (uint32_t)__builtin_popcountll(bk);
+        }
+        np = keep;
+        uint32_t Mb = 1;
+        while (Mb < m) Mb <<= 1;
+        for (uint32_t i = m + ln; i < Mb; i += 64) mine[i] = SK{~0ull, ~0u, 0};
+        nsync();
+        for (uint32_t kk = 2; kk <= Mb; kk <<= 1)
+          for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
+            for (uint32_t i = ln; i < Mb; i += 64) {
+              const uint32_t l = i ^ jj;
+              if (l > i) {
+                const SK x = mine[i], y = mine[l];
+                if (((i & kk) == 0) == sk_lt(y, x)) { mine[i] = y; mine[l] = x; }
+              }
+            }
+            nsync();
+          }
+        // serve in order
+        for (uint32_t j0 = 0; j0 < m; j0 += 64) {
+          const uint32_t cnt = min(64u, m - j0);
+          const bool ok = ln < cnt;
+          const SK x = ok ? mine[j0 + ln] : SK{0, 0, 0};
+          const uint32_t inf = ok ? info[x.i] : 0u;
+          uint64_t out = 0;
+          for (uint32_t jj = 0; jj < cnt; ++jj) {
+            const uint64_t t = rl64(x.t, jj);
+            const uint32_t nf = (uint32_t)__builtin_amdgcn_readlane((int)inf, (int)jj) & 0xFFFFu;
+            uint64_t qd = 0;
+            if (P.qm) qd = j == 0 ? pp[0].rq.request<true>(time_to_cycles(t, P.f), nf, D.err)
+                                  : pp[kPipeK - 1].rq.request<true>(time_to_cycles(t, P.f), nf, D.err);
+            if (j == 0) { pp[0].cq += qd; pp[0].cf += nf; } else { pp[kPipeK - 1].cq += qd; pp[kPipeK - 1].cf += nf; }
+            if (ln == jj) out = t + zps + lat_to_ps(qd, P.f);
+          }
+          // hand the served packets on: leave the chain, or arrive at the next position
+          if (ok) {
+            if ((inf >> 16) == nx) {
+              const uint32_t k = ids[x.i];
+              const uint64_t ts = S.t[k];
+              const uint32_t a = pos_of(S.cur[k]);
+              const uint64_t hz = (uint64_t)(dir ? nx - a : a - nx) * zps;
+              S.zl[k] += hz;
+              S.ct[k] += out - ts - hz;
+              S.t[k] = out;
+              S.cur[k] = tile_at(nx);
+              atomicSub(&s_left, 1u);
+            } else {
+              const uint32_t s2 = s + 1;
+              inc(s2, par)[atomicAdd(&ninc[par * kPipePos + s2], 1u)] = SK{out, x.i, 0};
+            }
+          }
+          nsync();
+        }
+        if (j == 0) pp[0].m += m; else pp[kPipeK - 1].m += m;
+        if (bt == Tr && bi == 0) break;
+      }
+      if (ln == 0) npool[s] = np;
+    }
+    __syncthreads();
+    if (s_left == 0) break;
+    if (d + 1 >= kMaxSteps) { if (tid == 0) atomicOr(D.err, GG_DERR_STATE); break; }
+  }
+  // write the queues back, the counters once per position
+#pragma unroll
+  for (uint32_t j = 0; j < kPipeK; ++j) {
+    const uint32_t s = wv + j * kPipeWaves;
+    if (s >= npos) continue;
+    const uint32_t tile = tile_at(pos_at(s));
+    if (P.qm) pp[j].rq.store(D.q + (uint64_t)tile * 6 + port, D.nd + ((uint64_t)tile * 6 + port) * P.max_size);
+    if (ln == 0 && pp[j].m) {
+      const uint64_t m = pp[j].m, cf = pp[j].cf;
+      if (P.qm) { cadd(D.ctr, tile, GG_NC_ROUTER_CONTENTION_CYCLES, pp[j].cq); cadd(D.ctr, tile, GG_NC_ROUTER_PACKETS, m); }
+      cadd(D.ctr, tile, GG_NC_BUFFER_WRITES, cf); cadd(D.ctr, tile, GG_NC_BUFFER_READS, cf);
+      cadd(D.ctr, tile, GG_NC_SWITCH_ALLOC, m); cadd(D.ctr, tile, GG_NC_CROSSBAR, cf);
+      cadd(D.ctr, tile, GG_NC_LINK_TRAVERSALS, cf);
+    }
+  }
+}
 
 // ---------------------------------------------------------------------------
 // Stages 0 / 3 (injection ports / SELF ports + receive), the default: one
@@ -721,13 +988,6 @@ __global__ __launch_bounds__(kSweepThreads) void k_chain_sweep(NocDev D, int sta
 // ---------------------------------------------------------------------------
 constexpr uint32_t kPortWaves = 4, kPortPk = 2048;
 constexpr size_t kPortLds = (size_t)kPortWaves * kPortPk * sizeof(SK);
-
-__device__ __forceinline__ void nsync()   // LDS ordering between the lanes of one wave of a multi-wave workgroup
-{
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
 
 template <bool SELF>
 __global__ __launch_bounds__(64 * kPortWaves) void k_port_sweep(NocDev D, const uint32_t* __restrict__ len,
@@ -1352,6 +1612,8 @@ struct gg_noc_state {
   TEv* theap = nullptr; uint32_t* bidx = nullptr; uint64_t tcap = 0, bcap = 0;   // broadcast-tree walk scratch
   uint32_t* tctl = nullptr;                       // grid form: TreeCtl | cnt[kTreeMaxT] | off[kTreeMaxT + 1]
   unsigned long long* prof = nullptr;             // GG_NOC_PROFILE=1: k_chain_sweep phase cycles (diagnostics)
+  SK* pscr = nullptr; uint64_t pscr_cap = 0;       // k_chain_pipe: per packet 3 x positions pool / incoming slots
+  bool pipe = true;                               // GG_NOC_PIPE=0: the position sweep for every chain (A/B)
 };
 
 gg_status gg_noc_alloc(gg_ctx* ctx)
@@ -1376,6 +1638,7 @@ gg_status gg_noc_alloc(gg_ctx* ctx)
   P.qaux = hq_aux(c.queue_model_type, c.basic_moving_avg, c.history_list_no_interleaving);
   if (gg_status e = gg_check_queue_model(c.queue_model_type, P.qaux, P.max_size)) return e;
   S->staged = !(getenv("GG_NOC_STAGED") && atoi(getenv("GG_NOC_STAGED")) == 0);
+  S->pipe = !(getenv("GG_NOC_PIPE") && atoi(getenv("GG_NOC_PIPE")) == 0);
   if (getenv("GG_NOC_PROFILE") && atoi(getenv("GG_NOC_PROFILE"))) {
     GG_HIP(hipMalloc((void**)&S->prof, 16 * sizeof(unsigned long long)));
     GG_HIP(hipMemset(S->prof, 0, 16 * sizeof(unsigned long long)));
@@ -1383,6 +1646,7 @@ gg_status gg_noc_alloc(gg_ctx* ctx)
   GG_HIP(hipFuncSetAttribute((const void*)k_port_staged<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
   GG_HIP(hipFuncSetAttribute((const void*)k_port_staged<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
   GG_HIP(hipFuncSetAttribute((const void*)k_chain_sweep, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
+  GG_HIP(hipFuncSetAttribute((const void*)k_chain_pipe, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
   GG_HIP(hipFuncSetAttribute((const void*)k_port_sweep<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPortLds));
   GG_HIP(hipFuncSetAttribute((const void*)k_port_sweep<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPortLds));
   static_assert(kSweepLds <= kStageLdsMax, "the sweep's LDS arrays fit the stage budget");
@@ -1402,7 +1666,7 @@ void gg_noc_free(gg_ctx* ctx)
   gg_noc_state* S = ctx->noc;
   if (!S) return;
   void* ps[] = {S->q, S->nd, S->ctr, S->t, S->zl, S->ct, S->cur, S->keys, S->ids, S->heap,
-                S->counts, S->cursor, S->off, S->theap, S->bidx, S->tctl, S->prof};
+                S->counts, S->cursor, S->off, S->theap, S->bidx, S->tctl, S->prof, S->pscr};
   for (void* p : ps) if (p) hipFree(p);
   delete S;
   ctx->noc = nullptr;
@@ -1580,6 +1844,16 @@ gg_status gg_noc_hbh(gg_ctx* ctx, const uint32_t* src, const uint32_t* dst, cons
         hipLaunchKernelGGL(k_port_staged<false>, dim3(pb), dim3(64), kStageLdsMax, s, D, dst, len, S->off, S->ids, S->heap, PS);
       else
         hipLaunchKernelGGL(k_port_staged<true>, dim3(pb), dim3(64), kStageLdsMax, s, D, dst, len, S->off, S->ids, S->heap, PS);
+    } else if (staged && S->pipe && std::max(P.w, P.h) <= kPipePos) {
+      const uint64_t stride = 3ull * std::max(P.w, P.h);
+      if (S->pscr_cap < cap * stride) {
+        if (S->pscr) hipFree(S->pscr);
+        S->pscr = nullptr; S->pscr_cap = 0;
+        GG_HIP(hipMalloc((void**)&S->pscr, sizeof(SK) * cap * stride));
+        S->pscr_cap = cap * stride;
+      }
+      hipLaunchKernelGGL(k_chain_pipe, dim3(nb), dim3(64 * kPipeWaves), kStageLdsMax, s, D, stage - 1, dst, len, S->off,
+                         S->ids, S->heap, PS, S->pscr, stride, S->prof);
     } else if (staged) {
       hipLaunchKernelGGL(k_chain_sweep, dim3(nb), dim3(kSweepThreads), kStageLdsMax, s, D, stage - 1, dst, len, S->off,
                          S->ids, S->heap, PS, S->prof);
