@@ -1496,10 +1496,23 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
     const bool lds = na <= SL::kIn;
     uint64_t* t_ = lds ? sl.x1 : gscr; uint64_t* s_ = lds ? sl.x2 : gscr + P.IC; uint64_t* k_ = lds ? sl.x3 : gscr + 2 * P.IC;
     uint32_t* i_ = lds ? sl.i1 : (uint32_t*)(gscr + 3 * P.IC); uint32_t* o_ = lds ? sl.i2 : (uint32_t*)(gscr + 4 * P.IC);
-    for (uint32_t i = ln; i < na; i += 64) {
-      const uint32_t r = al[i];
-      const gg_cmsg& m = prev[r];
-      t_[i] = m.arrival_ps; s_[i] = m.send_ps; k_[i] = ((uint64_t)m.src << 32) | m.seq; i_[i] = r;
+    // 4 records per lane in flight: the list words, then the records (a
+    // fan-in of hundreds of acknowledgements at a hot line's home otherwise
+    // waits two dependent memory round trips per 64 records)
+    for (uint32_t i0 = ln; i0 < na; i0 += 256) {
+      uint32_t rr[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) rr[u] = i0 + 64 * u < na ? al[i0 + 64 * u] : 0u;
+      uint64_t ta[4], sa[4];
+      uint32_t sr[4], sq[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u)
+        if (i0 + 64 * u < na) { const gg_cmsg& m = prev[rr[u]]; ta[u] = m.arrival_ps; sa[u] = m.send_ps; sr[u] = m.src; sq[u] = m.seq; }
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) {
+        const uint32_t i = i0 + 64 * u;
+        if (i < na) { t_[i] = ta[u]; s_[i] = sa[u]; k_[i] = ((uint64_t)sr[u] << 32) | sq[u]; i_[i] = rr[u]; }
+      }
     }
     tsync();
     if (S.prof) _sc = __builtin_amdgcn_s_memtime();
@@ -1597,10 +1610,23 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
     uint32_t* i_ = lds ? sl.i1 : (uint32_t*)(gscr + 3 * P.IC); uint32_t* o_ = lds ? sl.i2 : (uint32_t*)(gscr + 4 * P.IC);
     const uint32_t* il = inb(S, p) + (size_t)lt * P.IC;
     const uint32_t* al = arv(S, p) + (size_t)lt * P.IC;
-    for (uint32_t i = ln; i < n; i += 64) {
-      const uint32_t r = i < ni ? il[i] : al[i - ni];
-      const gg_cmsg& m = prev[r];
-      a_[i] = m.arrival_ps; k_[i] = ((uint64_t)m.src << 32) | m.seq; i_[i] = r;
+    for (uint32_t i0 = ln; i0 < n; i0 += 256) {                   // 4 records per lane in flight
+      uint32_t rr[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) {
+        const uint32_t i = i0 + 64 * u;
+        rr[u] = i < n ? (i < ni ? il[i] : al[i - ni]) : 0u;
+      }
+      uint64_t ta[4];
+      uint32_t sr[4], sq[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u)
+        if (i0 + 64 * u < n) { const gg_cmsg& m = prev[rr[u]]; ta[u] = m.arrival_ps; sr[u] = m.src; sq[u] = m.seq; }
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) {
+        const uint32_t i = i0 + 64 * u;
+        if (i < n) { a_[i] = ta[u]; k_[i] = ((uint64_t)sr[u] << 32) | sq[u]; i_[i] = rr[u]; }
+      }
     }
     tsync();
     hk.clear_inb(p, lt);
