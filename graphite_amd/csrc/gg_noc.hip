@@ -308,7 +308,6 @@ __global__ void k_self(NocDev D, const uint32_t* __restrict__ dst, const uint32_
 // and the canonical keys — so the serial event walk touches no HBM; written
 // back at the end.  Used when they fit (kPktLdsBytes per packet), else the
 // walk keeps its heap and packet state in HBM.
-constexpr uint32_t kPortTiles = 16;
 constexpr size_t kStageLdsMax = 160 * 1024 - 64;   // leaves room for k_chain_staged's static position range
 constexpr uint32_t kPktLdsBytes = sizeof(Ev) + 5 * 8 + 4 * 4;
 constexpr uint32_t kCtrBytes = GG_NUM_NET_COUNTERS * 8;   // a tile's counter block in LDS
@@ -348,97 +347,6 @@ __device__ void lpk_store(const LPk& L, uint32_t np, const PktState& S)
     const uint32_t k = L.gid[i];
     S.t[k] = L.t[i]; S.zl[k] = L.zl[i]; S.ct[k] = L.ct[i]; S.cur[k] = L.cur[i];
   }
-}
-
-// Staged stage 0 / 3: kPortTiles tiles per workgroup, one thread per tile,
-// their injection (port 5) or SELF (port 0) queues in LDS.
-template <bool SELF>
-__global__ __launch_bounds__(64) void k_port_staged(NocDev D, const uint32_t* __restrict__ dst,
-    const uint32_t* __restrict__ len, const uint64_t* __restrict__ bucket_off,
-    const uint32_t* __restrict__ bucket_ids, Ev* heap, PktState S)
-{
-  extern __shared__ __attribute__((aligned(16))) uint8_t qlds[];
-  const uint32_t ms = D.P.max_size, qb = qimg_bytes(ms);
-  const uint32_t t0 = blockIdx.x * kPortTiles;
-  const uint32_t nt = min(kPortTiles, D.P.tiles - t0);
-  const uint64_t B = bucket_off[t0], E = bucket_off[t0 + nt];
-  if (B == E) return;                                                // no packet in these tiles
-  const uint32_t np = (uint32_t)(E - B);
-  const bool lp = (size_t)nt * (qb + kCtrBytes) + (size_t)np * kPktLdsBytes <= kStageLdsMax;
-  uint64_t* lcb = reinterpret_cast<uint64_t*>(qlds + nt * qb);
-  LPk L(qlds + nt * (qb + kCtrBytes), lp ? np : 0u);
-  const int port = SELF ? P_SELF : 5;
-  uint32_t empty = 0;                                 // tiles of this workgroup without packets: queues untouched
-  for (uint32_t i = 0; i < nt; ++i) empty |= (bucket_off[t0 + i] == bucket_off[t0 + i + 1]) ? (1u << i) : 0u;
-  auto pq = [&](uint32_t i) { return (uint64_t)(t0 + i) * 6 + port; };
-  auto pskip = [&](uint32_t i) { return ((empty >> i) & 1u) != 0; };
-  qimg_copy_set<true>(D, nt, pq, pskip, qlds, qb);
-  if (lp) lpk_load(L, B, np, bucket_ids, S, dst, len);
-  if (lp) lctr_zero(lcb, nt);
-  __syncthreads();
-  if (threadIdx.x < nt) {
-    const uint32_t tile = t0 + threadIdx.x;
-    uint64_t* lc = lcb + threadIdx.x * GG_NUM_NET_COUNTERS;
-    const uint64_t b = bucket_off[tile], e = bucket_off[tile + 1];
-    HTree tr = qimg_tree(qlds + threadIdx.x * qb, ms, D.P.analytical != 0);
-    if (lp) {
-      Ev* h = L.heap + (b - B);
-      uint32_t n = 0;
-      for (uint32_t i = (uint32_t)(b - B); i < (uint32_t)(e - B); ++i) heap_push(h, n, L.ev(i));
-      while (n) {
-        const uint32_t i = heap_pop(h, n).id;
-        const uint64_t nf = nflits(D.P, L.len[i]);
-        if (!SELF) {                                  // k_inject
-          lc[GG_NC_PACKETS_SENT] += 1; lc[GG_NC_FLITS_SENT] += nf;
-          lc[GG_NC_BITS_SENT] += L.len[i];
-          uint64_t qd = 0;
-          if (D.P.qm) qd = tr.delay(time_to_cycles(L.t[i], D.P.f), nf, D.err);
-          const uint64_t cps = lat_to_ps(qd, D.P.f);
-          L.t[i] += lat_to_ps(0, D.P.f) + cps;
-          L.ct[i] += cps;
-        } else {                                      // k_self
-          uint64_t t = L.t[i], zl = L.zl[i], ct = L.ct[i];
-          mesh_hop_q(D, tile, tr, L.len[i], t, zl, ct, lc);
-          const uint64_t ser = lat_to_ps(nf, D.P.f);
-          t += ser; zl += ser;
-          lc[GG_NC_PACKETS_RECEIVED] += 1; lc[GG_NC_FLITS_RECEIVED] += nf;
-          lc[GG_NC_BITS_RECEIVED] += L.len[i];
-          lc[GG_NC_TOTAL_LATENCY_PS] += zl + ct; lc[GG_NC_TOTAL_CONTENTION_PS] += ct;
-          L.t[i] = t; L.zl[i] = zl; L.ct[i] = ct;
-        }
-      }
-    } else {
-      Ev* h = heap + b;
-      uint32_t n = 0;
-      for (uint64_t i = b; i < e; ++i) { uint32_t k = bucket_ids[i]; heap_push(h, n, mkev(S, S.t[k], k)); }
-      while (n) {
-        const uint32_t k = heap_pop(h, n).id;
-        const uint64_t nf = nflits(D.P, len[k]);
-        if (!SELF) {
-          cadd(D.ctr, tile, GG_NC_PACKETS_SENT, 1); cadd(D.ctr, tile, GG_NC_FLITS_SENT, nf);
-          cadd(D.ctr, tile, GG_NC_BITS_SENT, len[k]);
-          uint64_t qd = 0;
-          if (D.P.qm) qd = tr.delay(time_to_cycles(S.t[k], D.P.f), nf, D.err);
-          const uint64_t cps = lat_to_ps(qd, D.P.f);
-          S.t[k] += lat_to_ps(0, D.P.f) + cps;
-          S.ct[k] += cps;
-        } else {
-          uint64_t t = S.t[k], zl = S.zl[k], ct = S.ct[k];
-          mesh_hop_q(D, tile, tr, len[k], t, zl, ct);
-          const uint64_t ser = lat_to_ps(nf, D.P.f);
-          t += ser; zl += ser;
-          cadd(D.ctr, tile, GG_NC_PACKETS_RECEIVED, 1); cadd(D.ctr, tile, GG_NC_FLITS_RECEIVED, nf);
-          cadd(D.ctr, tile, GG_NC_BITS_RECEIVED, len[k]);
-          cadd(D.ctr, tile, GG_NC_TOTAL_LATENCY_PS, zl + ct); cadd(D.ctr, tile, GG_NC_TOTAL_CONTENTION_PS, ct);
-          S.t[k] = t; S.zl[k] = zl; S.ct[k] = ct;
-        }
-      }
-    }
-  }
-  __syncthreads();
-  if (lp) lpk_store(L, np, S);
-  if (lp) lctr_flush(D, lcb, nt, [&](uint32_t i) { return t0 + i; });
-  qimg_copy_set<false>(D, nt, pq, pskip, qlds, qb);
 }
 
 // Staged stages X / Y, the general form: one workgroup per chain (row or
@@ -1643,8 +1551,6 @@ gg_status gg_noc_alloc(gg_ctx* ctx)
     GG_HIP(hipMalloc((void**)&S->prof, 16 * sizeof(unsigned long long)));
     GG_HIP(hipMemset(S->prof, 0, 16 * sizeof(unsigned long long)));
   }
-  GG_HIP(hipFuncSetAttribute((const void*)k_port_staged<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
-  GG_HIP(hipFuncSetAttribute((const void*)k_port_staged<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
   GG_HIP(hipFuncSetAttribute((const void*)k_chain_sweep, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
   GG_HIP(hipFuncSetAttribute((const void*)k_chain_pipe, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
   GG_HIP(hipFuncSetAttribute((const void*)k_port_sweep<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPortLds));
@@ -1827,8 +1733,10 @@ gg_status gg_noc_hbh(gg_ctx* ctx, const uint32_t* src, const uint32_t* dst, cons
     hipLaunchKernelGGL(k_bucket, dim3(blocks), dim3(256), 0, s, S->keys, cap, n_dev, S->off, S->cursor, S->ids);
     const uint32_t tb = (nb + 63) / 64;
     const size_t qb = qimg_bytes(P.max_size);
-    const size_t port_lds = kPortTiles * qb, chain_lds = (stage == 1 ? P.w : P.h) * qb;
-    const bool staged = S->staged && ((stage == 0 || stage == 3) ? port_lds : chain_lds) <= kStageLdsMax;
+    // chains: the general walk (chain_staged, the fallback of the pipeline and the sweep) stages the
+    // chain's queue images in LDS
+    const size_t chain_lds = (stage == 1 ? P.w : P.h) * qb;
+    const bool staged = S->staged && chain_lds <= kStageLdsMax;
     if (S->staged && (stage == 0 || stage == 3)) {
       const uint32_t pb = (P.tiles + kPortWaves - 1) / kPortWaves;
       if (stage == 0)
@@ -1837,13 +1745,6 @@ gg_status gg_noc_hbh(gg_ctx* ctx, const uint32_t* src, const uint32_t* dst, cons
       else
         hipLaunchKernelGGL(k_port_sweep<true>, dim3(pb), dim3(64 * kPortWaves), kPortLds, s, D, len, S->off, S->ids,
                            S->heap, PS);
-    } else if (staged && (stage == 0 || stage == 3)) {
-      const uint32_t pb = (P.tiles + kPortTiles - 1) / kPortTiles;
-      // the whole LDS budget: the packet count of a workgroup is known on the device only
-      if (stage == 0)
-        hipLaunchKernelGGL(k_port_staged<false>, dim3(pb), dim3(64), kStageLdsMax, s, D, dst, len, S->off, S->ids, S->heap, PS);
-      else
-        hipLaunchKernelGGL(k_port_staged<true>, dim3(pb), dim3(64), kStageLdsMax, s, D, dst, len, S->off, S->ids, S->heap, PS);
     } else if (staged && S->pipe && std::max(P.w, P.h) <= kPipePos) {
       const uint64_t stride = 3ull * std::max(P.w, P.h);
       if (S->pscr_cap < cap * stride) {
