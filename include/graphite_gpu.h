@@ -511,10 +511,10 @@ float     gg_kernel_time_ms(gg_ctx* ctx, const char* kernel);
  * every 16th launch of each kernel); 2 on, every coherent step / walk launch
  * timed in-kernel (first workgroup start to last workgroup end). */
 void      gg_set_timing(gg_ctx* ctx, int enabled);
-/* With timing on, every 16th launch of each coherent-mode kernel is bracketed
- * by HIP events on its stream: launches since the last gg_coherent_begin of
- * "coherent_step", "coherent_walk_x", "coherent_walk_y", and their total
- * device time estimated as (mean of the timed launches) x launches.        */
+/* Launches since the last gg_coherent_begin of "coherent_step",
+ * "coherent_walk_x", "coherent_walk_y" and their total device time: with
+ * timing 1, (mean of the event-timed launches) x launches; with timing 2, the
+ * sum of every launch's in-kernel span (s_memrealtime, 100 MHz).           */
 gg_status gg_kernel_stats(gg_ctx* ctx, const char* kernel, double* total_ms, uint64_t* launches);
 
 #ifdef __cplusplus
