@@ -15,8 +15,6 @@
 // one global event queue exactly.
 #include "gg_dev.h"
 
-#include <hip/hip_cooperative_groups.h>
-
 #include <algorithm>
 
 namespace {
@@ -1304,17 +1302,7 @@ __global__ __launch_bounds__(64) void k_tree_walk(NocDev D, TreeIO IO, uint64_t 
   }
 }
 
-// The windowed form (conservative time windows, one workgroup): a router
-// event at time t forwards its copies at t + router + link delay or later
-// (zps > 0), so in a window [t_min, t_min + zps) every router's events depend
-// only on that router's own queues: each router (one thread) serves its
-// window events in (time, index) order and the routers run in parallel.
-// Window loop: min over the pending events -> group the window's events by
-// router (counting sort in LDS) and carry the rest over -> serve, forwarding
-// copies to the next pending list.  Injection ports first: each tile serves
-// its packets in (time, index) order (the injection port is its own queue).
-constexpr uint32_t kTreeMaxT = 4096;
-constexpr uint32_t kTreeThreads = 1024;
+constexpr uint32_t kTreeMaxT = 4096;                  // the windowed walk's per-router LDS arrays
 // exclusive block-wide scan of one value per thread (DPP-free shuffles within
 // the wave, the wave totals through LDS); *total = the block sum
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t* total)
@@ -1332,43 +1320,107 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
   __syncthreads();
   return r;
 }
-// Control words of the grid form: [0] pending count, [1] next pending count,
-// [2..3] the window minimum (u64)
-struct TreeCtl { uint32_t n0, n1; unsigned long long tmin; };
-
-template <bool GRID>
-__global__ __launch_bounds__(kTreeThreads) void k_tree_win(NocDev D, TreeIO IO, uint64_t n, uint64_t nb,
-                                                           TEv* E0, TEv* E1, TEv* G, uint64_t hcap, TreeCtl* ctl)
+// ---------------------------------------------------------------------------
+// The windowed walk (k_tree_pool, one workgroup): a router event at time t
+// forwards its copies at t + router + link delay (zps > 0) or later, so in a
+// window [t_min, t_min + zps) every router's events depend only on that
+// router's own queues: the routers serve their window events in (time, index)
+// order in parallel.  The per-window work is kept off HBM:
+// * injection ports are served once at the start; each tile's router events
+//   are a (time, index)-sorted run in HBM whose head time sits in LDS, so a
+//   window takes the due heads instead of rescanning every pending injection;
+// * the pending forwarded copies live in an LDS pool (two buffers, one per
+//   window parity), continued in HBM beyond its capacity;
+// * the window's due events are LDS records holding their packet's fields,
+//   linked per router and sorted there by (time, index);
+// * a router's listed output ports are separate queues whose requests come in
+//   the router's event order, so every (router, port) with requests is a task
+//   of its own and an event's delay is the max over its ports (an LDS atomic
+//   max): the memory round trips of one event's ports overlap.
+// Beyond the LDS capacities the due records and the pool continue in HBM, so
+// results never depend on them (only the speed).
+constexpr uint32_t kTpThreads = 1024;
+constexpr uint32_t kTpNil = 0xFFFFFFFFu;
+constexpr size_t kTpLds = 160 * 1024 - 256;
+struct TGe {                                     // a due router event of the window
+  uint64_t t, t0, q;                             // time at the router, injection time, max port delay (cycles)
+  uint32_t k, at, src, dst, len, bidx, next, mask;   // next: the router's list; mask: listed ports (1 << P_*)
+};
+__device__ __forceinline__ uint64_t tp_wave_min64(uint64_t v)
 {
-  __shared__ uint32_t cnt[kTreeMaxT];
-  __shared__ uint32_t off[kTreeMaxT + 1];
-  __shared__ uint32_t wsum[kTreeThreads / 64 + 1];
-  __shared__ unsigned long long s_min;
-  __shared__ uint32_t s_n0, s_n1, s_err;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { const uint64_t u = (uint64_t)__shfl_xor((long long)v, o); v = u < v ? u : v; }
+  return v;
+}
+// listed output ports of packet (s, d) at router c (hop_by_hop.cc:163-256)
+__device__ __forceinline__ uint32_t tree_ports(const NocParams& P, uint32_t c, uint32_t s, uint32_t d)
+{
+  const uint32_t W = P.w, H = P.h, cx = c % W, cy = c / W, sx = s % W, sy = s / W;
+  if (d != GG_BROADCAST) {
+    const uint32_t dx = d % W, dy = d / W;
+    return 1u << (cx > dx ? P_LEFT : cx < dx ? P_RIGHT : cy > dy ? P_DOWN : cy < dy ? P_UP : P_SELF);
+  }
+  uint32_t m = 1u << P_SELF;
+  if (cy >= sy && cy + 1 < H) m |= 1u << P_UP;
+  if (cy <= sy && cy >= 1) m |= 1u << P_DOWN;
+  if (cy == sy) {
+    if (cx >= sx && cx + 1 < W) m |= 1u << P_RIGHT;
+    if (cx <= sx && cx >= 1) m |= 1u << P_LEFT;
+  }
+  return m;
+}
+__device__ __forceinline__ uint32_t tree_next(const NocParams& P, uint32_t c, int port)
+{
+  return port == P_LEFT ? c - 1 : port == P_RIGHT ? c + 1 : port == P_DOWN ? c - P.w : port == P_UP ? c + P.w : c;
+}
+struct TpBufs {
+  TEv* run;        // [n] the tiles' injection router events, (time, index)-sorted per tile
+  TEv* heap;       // [n] setup scratch
+  TEv* hp[2];      // [hcap] the pool buffers beyond their LDS part
+  TGe* gh;         // [hcap] due records beyond their LDS part
+};
+// LDS bytes of k_tree_pool for T tiles, gcap due records and ecap pool events per buffer
+__host__ __device__ inline size_t tp_lds_bytes(uint32_t T, uint32_t gcap, uint32_t ecap)
+{
+  return 8ull * T + 2ull * ecap * sizeof(TEv) + (size_t)gcap * sizeof(TGe) + 4ull * (T + 1) + 12ull * T + T;
+}
+
+__global__ __launch_bounds__(kTpThreads) void k_tree_pool(NocDev D, TreeIO IO, uint64_t n, uint64_t nb, TpBufs B,
+                                                         uint64_t hcap, uint32_t gcap, uint32_t ecap,
+                                                         unsigned long long* prof)
+{
+  extern __shared__ __align__(16) uint8_t tp_lds[];
+  __shared__ uint32_t wsum[kTpThreads / 64 + 1];
+  __shared__ unsigned long long s_tmin, s_pmin, s_pmin1;
+  __shared__ uint32_t s_n0, s_n1, s_nd, s_na, s_err;
   const NocParams& P = D.P;
-  const uint32_t T = P.tiles, tid = threadIdx.x, nt = blockDim.x;
+  const uint32_t T = P.tiles, tid = threadIdx.x, nt = blockDim.x, ln = tid & 63;
   const uint64_t zps = lat_to_ps((uint64_t)P.router_delay + P.link_delay, P.f);
-  // block-wide exclusive scan of cnt[0..T) into off (T <= 4 * nt)
-  auto scan_counts = [&]() {
-    const uint32_t per = (T + nt - 1) / nt;
-    uint32_t a = 0, tot;
-    for (uint32_t i = tid * per; i < min(T, (tid + 1) * per); ++i) a += cnt[i];
-    a = block_excl_scan(a, wsum, &tot);
-    for (uint32_t i = tid * per; i < min(T, (tid + 1) * per); ++i) { off[i] = a; a += cnt[i]; cnt[i] = 0; }
-    if (tid == 0) off[T] = tot;
-    __syncthreads();
-  };
-  if (tid == 0) { s_err = 0; s_n0 = 0; s_n1 = 0; }
-  for (uint32_t i = tid; i < T; i += nt) cnt[i] = 0;
+  uint64_t* hd = reinterpret_cast<uint64_t*>(tp_lds);                   // [T] head time of each tile's injection run
+  TEv* El[2] = {reinterpret_cast<TEv*>(hd + T), reinterpret_cast<TEv*>(hd + T) + ecap};
+  TGe* Gl = reinterpret_cast<TGe*>(El[1] + ecap);                       // [gcap]
+  uint32_t* off = reinterpret_cast<uint32_t*>(Gl + gcap);               // [T + 1] run offsets
+  uint32_t* cur = off + T + 1;                                          // [T] run cursors
+  uint32_t* head = cur + T;                                             // [T] the router's due list
+  uint32_t* act = head + T;                                             // [na] routers with due events
+  uint8_t* um = reinterpret_cast<uint8_t*>(act + T);                    // [na] union of their events' ports
+  // the due records and the pool buffers: LDS part, then HBM
+  auto with_g = [&](uint32_t i, auto f) { if (i < gcap) f(Gl[i]); else f(B.gh[i - gcap]); };
+  auto with_e = [&](uint32_t b, uint32_t i, auto f) { if (i < ecap) f(El[b][i]); else f(B.hp[b][i - ecap]); };
+  unsigned long long pc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pw = 0, pn = 0, pt = __builtin_amdgcn_s_memtime();
+  auto lap = [&](int i) { if (prof) { const unsigned long long x = __builtin_amdgcn_s_memtime(); pc[i] += x - pt; pt = x; } };
+
+  // 1. validate; broadcast ordinals; the packets bucketed by source
+  if (tid == 0) { s_err = 0; s_n0 = 0; s_pmin = ~0ull; }
+  for (uint32_t i = tid; i < T; i += nt) { cur[i] = 0; head[i] = kTpNil; }
   __syncthreads();
-  // 1. validate; broadcast ordinals (per-thread chunk counts, scanned); bucket the packets by source
   const uint64_t per = (n + nt - 1) / nt, k0 = min(n, tid * per), k1 = min(n, k0 + per);
   uint32_t mine = 0;
   for (uint64_t k = k0; k < k1; ++k) {
     const uint32_t s = IO.src[k], d = IO.dst[k];
     if (s >= T || (d >= T && d != GG_BROADCAST)) atomicOr(&s_err, GG_DERR_RANGE);
     mine += d == GG_BROADCAST;
-    if (s < T && s != d) atomicAdd(&cnt[s], 1u);
+    if (s < T && s != d) atomicAdd(&cur[s], 1u);
   }
   uint32_t nbc;
   mine = block_excl_scan(mine, wsum, &nbc);
@@ -1376,134 +1428,192 @@ __global__ __launch_bounds__(kTreeThreads) void k_tree_win(NocDev D, TreeIO IO, 
   __syncthreads();
   if (s_err) { if (tid == 0) atomicOr(D.err, s_err); return; }
   for (uint64_t k = k0; k < k1; ++k) IO.bidx[k] = IO.dst[k] == GG_BROADCAST ? mine++ : ~0u;
-  __syncthreads();
-  scan_counts();
+  {
+    const uint32_t pt_ = (T + nt - 1) / nt;
+    uint32_t a = 0, tot;
+    for (uint32_t i = tid * pt_; i < min(T, (tid + 1) * pt_); ++i) a += cur[i];
+    a = block_excl_scan(a, wsum, &tot);
+    for (uint32_t i = tid * pt_; i < min(T, (tid + 1) * pt_); ++i) { off[i] = a; a += cur[i]; cur[i] = 0; }
+    if (tid == 0) off[T] = tot;
+    __syncthreads();
+  }
   for (uint64_t k = k0; k < k1; ++k) {
     const uint32_t s = IO.src[k], d = IO.dst[k];
     if (s == d) { IO.out.arrival_ps_dev[k] = IO.t0[k]; IO.out.zero_load_ps_dev[k] = 0; IO.out.contention_ps_dev[k] = 0; continue; }
-    G[off[s] + atomicAdd(&cnt[s], 1u)] = TEv{IO.t0[k], (uint32_t)k, s | kInjBit};
+    B.heap[off[s] + atomicAdd(&cur[s], 1u)] = TEv{IO.t0[k], (uint32_t)k, s | kInjBit};
   }
   __syncthreads();
-  // injection ports: each tile's packets heap-ordered in place, served in (time, index) order
+  // 2. injection ports: each tile's packets in (time, index) order; the router
+  //    events they produce re-sorted into the tile's run
   for (uint32_t r = tid; r < T; r += nt) {
-    TEv* h = G + off[r];
-    uint64_t m = off[r + 1] - off[r], hn = 0;
+    TEv* h = B.heap + off[r];
+    TEv* h2 = B.run + off[r];
+    const uint64_t m = off[r + 1] - off[r];
+    uint64_t hn = 0, hn2 = 0;
     for (uint64_t i = 0; i < m; ++i) { const TEv e = h[i]; theap_push(h, hn, e); }
-    while (hn) {
-      const TEv e = theap_pop(h, hn);
-      E0[atomicAdd(&s_n0, 1u)] = tree_inject(D, IO, e);
-    }
+    while (hn) { const TEv e = theap_pop(h, hn); theap_push(h2, hn2, tree_inject(D, IO, e)); }
+    for (uint64_t i = 0; i < m; ++i) h[i] = theap_pop(h2, hn2);     // sorted run into the scratch half ...
+    for (uint64_t i = 0; i < m; ++i) h2[i] = h[i];                  // ... and back
+    cur[r] = off[r];
+    hd[r] = m ? h2[0].t : ~0ull;
   }
-  for (uint32_t i = tid; i < T; i += nt) cnt[i] = 0;
   __syncthreads();
-  if (GRID) {                                      // the windows run in k_tree_grid
-    if (tid == 0) { ctl->n0 = s_n0; ctl->n1 = 0; ctl->tmin = ~0ull; }
-    return;
-  }
-  // 2. windows (router tid's counters in registers when every thread owns one router)
-  TreeAcc acc;
+  lap(0);
+  // 3. windows
+  uint32_t pb = 0;                                   // pool buffer holding the pending events
   for (;;) {
+    if (tid == 0) s_tmin = s_pmin;
+    __syncthreads();
+    {
+      unsigned long long lm = ~0ull;
+      for (uint32_t r = tid; r < T; r += nt) lm = min(lm, (unsigned long long)hd[r]);
+      lm = tp_wave_min64(lm);
+      if (ln == 0 && lm != ~0ull) atomicMin(&s_tmin, lm);
+    }
+    __syncthreads();
+    const uint64_t tmin = s_tmin;
+    if (tmin == ~0ull) break;
+    const uint64_t wend = tmin + zps;
     const uint32_t n0 = s_n0;
-    if (n0 == 0) break;
-    if (tid == 0) s_min = ~0ull;
+    pw++; pn += n0;
     __syncthreads();
-    unsigned long long lm = ~0ull;
-    for (uint32_t i = tid; i < n0; i += nt) lm = min(lm, (unsigned long long)E0[i].t);
-    atomicMin(&s_min, lm);
+    if (tid == 0) { s_n1 = 0; s_nd = 0; s_na = 0; s_pmin1 = ~0ull; }
     __syncthreads();
-    const uint64_t wend = s_min + zps;
+    lap(1);
+    // due events -> records linked per router; the rest carried to the other pool buffer
+    auto add_due = [&](const TEv& e) {
+      const uint32_t slot = atomicAdd(&s_nd, 1u), k = e.id, c = e.at;
+      const uint32_t s = IO.src[k], d = IO.dst[k];
+      const TGe g{e.t, IO.t0[k], 0, k, c, s, d, IO.len[k], d == GG_BROADCAST ? IO.bidx[k] : 0u, 0u,
+                  tree_ports(P, c, s, d)};
+      const uint32_t nx = atomicExch(&head[c], slot);
+      if (nx == kTpNil) act[atomicAdd(&s_na, 1u)] = c;
+      with_g(slot, [&](TGe& x) { x = g; x.next = nx; });
+    };
+    unsigned long long cm = ~0ull;
     for (uint32_t i = tid; i < n0; i += nt) {
-      const TEv e = E0[i];
-      if (e.t < wend) atomicAdd(&cnt[e.at], 1u);
-      else E1[atomicAdd(&s_n1, 1u)] = e;
+      TEv e;
+      with_e(pb, i, [&](TEv& x) { e = x; });
+      if (e.t < wend) add_due(e);
+      else { with_e(pb ^ 1u, atomicAdd(&s_n1, 1u), [&](TEv& x) { x = e; }); cm = min(cm, (unsigned long long)e.t); }
     }
-    __syncthreads();
-    scan_counts();
-    for (uint32_t i = tid; i < n0; i += nt) {
-      const TEv e = E0[i];
-      if (e.t < wend) G[off[e.at] + atomicAdd(&cnt[e.at], 1u)] = e;
-    }
-    __syncthreads();
     for (uint32_t r = tid; r < T; r += nt) {
-      TEv* h = G + off[r];
-      uint64_t m = off[r + 1] - off[r], hn = 0;
-      for (uint64_t i = 0; i < m; ++i) { const TEv e = h[i]; theap_push(h, hn, e); }
-      while (hn) {
-        const TEv e = theap_pop(h, hn);
-        tree_router(D, IO, e, [&](const TEv& x) { E1[atomicAdd(&s_n1, 1u)] = x; }, acc);
+      while (hd[r] < wend) {
+        const uint32_t c = cur[r], e1 = off[r + 1];
+        const TEv e = B.run[c];
+        hd[r] = c + 1 < e1 ? B.run[c + 1].t : ~0ull;
+        cur[r] = c + 1;
+        add_due(e);
       }
-      if (T > nt) acc.flush(D.ctr, r);             // a thread owns several routers: flush per batch
     }
-    for (uint32_t i = tid; i < T; i += nt) cnt[i] = 0;
+    cm = tp_wave_min64(cm);
+    if (ln == 0 && cm != ~0ull) atomicMin(&s_pmin1, cm);
     __syncthreads();
-    if (tid == 0) { s_n0 = s_n1; s_n1 = 0; }
-    TEv* x = E0; E0 = E1; E1 = x;
+    lap(2);
+    const uint32_t na = s_na;
+    // each router's due list sorted by (time, index); the union of its ports
+    for (uint32_t i = tid; i < na; i += nt) {
+      const uint32_t c = act[i];
+      uint32_t sorted = kTpNil, x = head[c], u = 0;
+      while (x != kTpNil) {
+        TGe gx;
+        with_g(x, [&](TGe& g) { gx = g; });
+        const uint32_t nx = gx.next;
+        u |= gx.mask;
+        auto lt = [&](uint32_t y) { uint64_t ty; uint32_t ky; with_g(y, [&](TGe& g) { ty = g.t; ky = g.k; });
+                                    return gx.t < ty || (gx.t == ty && gx.k < ky); };
+        if (sorted == kTpNil || lt(sorted)) { with_g(x, [&](TGe& g) { g.next = sorted; }); sorted = x; }
+        else {
+          uint32_t y = sorted;
+          for (;;) {
+            uint32_t yn;
+            with_g(y, [&](TGe& g) { yn = g.next; });
+            if (yn == kTpNil || lt(yn)) { with_g(x, [&](TGe& g) { g.next = yn; }); with_g(y, [&](TGe& g) { g.next = x; }); break; }
+            y = yn;
+          }
+        }
+        x = nx;
+      }
+      head[c] = sorted;
+      um[i] = (uint8_t)u;
+    }
+    __syncthreads();
+    lap(3);
+    // (router, port) tasks: the port's requests in the router's event order
+    if (P.qm) {
+      for (uint32_t j = tid; j < NPORTS * na; j += nt) {
+        const uint32_t i = j % na, port = j / na;
+        if (!((um[i] >> port) & 1u)) continue;
+        const uint32_t c = act[i];
+        HTree tr = D.tree(c, (int)port);
+        uint32_t x = head[c];
+        while (x != kTpNil) {
+          with_g(x, [&](TGe& g) {
+            if ((g.mask >> port) & 1u) {
+              const uint64_t qd = tr.delay(time_to_cycles(g.t, P.f), nflits(P, g.len), D.err);
+              if (qd) atomicMax((unsigned long long*)&g.q, (unsigned long long)qd);
+            }
+            x = g.next;
+          });
+        }
+      }
+      __syncthreads();
+    }
+    lap(4);
+    // each router's events in order: counters, forwarded copies, deliveries
+    {
+      unsigned long long fm = ~0ull;
+      for (uint32_t i = tid; i < na; i += nt) {
+        const uint32_t c = act[i], cx = c % P.w, cy = c / P.w;
+        TreeAcc A;
+        uint32_t x = head[c];
+        while (x != kTpNil) {
+          TGe g;
+          with_g(x, [&](TGe& y) { g = y; });
+          x = g.next;
+          const uint64_t nf = nflits(P, g.len), qd = g.q;
+          const int np = __builtin_popcount(g.mask);
+          if (P.qm) { A.rcc += qd * (uint64_t)np; A.rpk += (uint64_t)np; }
+          A.buf += nf; A.sw += 1; A.crossbar(np, nf);
+          A.link += nf * (uint64_t)np;
+          const uint32_t sx = g.src % P.w, sy = g.src / P.w;
+          const uint64_t cps = lat_to_ps(qd, P.f);
+          const uint64_t hops = (uint64_t)((cx > sx ? cx - sx : sx - cx) + (cy > sy ? cy - sy : sy - cy)) + 1;
+          const uint64_t t = g.t + zps + cps, zl = hops * zps, ct = t - g.t0 - zl;
+          for (int port = P_LEFT; port < NPORTS; ++port) {
+            if (!((g.mask >> port) & 1u)) continue;
+            const TEv f{t, g.k, tree_next(P, c, port)};
+            with_e(pb ^ 1u, atomicAdd(&s_n1, 1u), [&](TEv& y) { y = f; });
+            fm = min(fm, (unsigned long long)t);
+          }
+          if (g.mask & (1u << P_SELF)) {
+            const uint64_t ser = lat_to_ps(nf, P.f);   // receive at c (network_model.cc:118-150,253-272)
+            A.prcv += 1; A.frcv += nf; A.brcv += g.len;
+            A.lat += zl + ser + ct; A.con += ct;
+            if (g.dst == GG_BROADCAST) {
+              const uint64_t o = (uint64_t)g.bidx * P.tiles + c;
+              IO.bout.arrival_ps_dev[o] = t + ser; IO.bout.zero_load_ps_dev[o] = zl + ser; IO.bout.contention_ps_dev[o] = ct;
+            } else {
+              IO.out.arrival_ps_dev[g.k] = t + ser; IO.out.zero_load_ps_dev[g.k] = zl + ser; IO.out.contention_ps_dev[g.k] = ct;
+            }
+          }
+        }
+        A.flush(D.ctr, c);
+        head[c] = kTpNil;
+      }
+      fm = tp_wave_min64(fm);
+      if (ln == 0 && fm != ~0ull) atomicMin(&s_pmin1, fm);
+    }
+    __syncthreads();
+    lap(5);
+    if (tid == 0) { s_n0 = s_n1; s_pmin = s_pmin1; }
+    pb ^= 1u;
     __syncthreads();
   }
-  if (T <= nt && tid < T) acc.flush(D.ctr, tid);
-}
-
-// The window loop over a cooperative grid (k_tree_win<true> did the
-// injection ports): the same phases as k_tree_win with the grouping arrays in
-// HBM and grid barriers between phases, so the routers' queue requests use
-// the memory pipelines of kTreeGridBlocks CUs instead of one.  Measured: 92 ms
-// against 80 ms for one workgroup on the bench batch (six grid barriers per
-// window outweigh the spread), so it is the A/B form (GG_NOC_TREE_GRID=1).  Global thread
-// g owns router g (T <= kTreeGridBlocks * kTreeGridThreads).
-constexpr uint32_t kTreeGridBlocks = 16, kTreeGridThreads = 256;
-__global__ __launch_bounds__(kTreeGridThreads) void k_tree_grid(NocDev D, TreeIO IO, TEv* E0, TEv* E1, TEv* G,
-                                                                 uint32_t* cnt, uint32_t* off, TreeCtl* ctl)
-{
-  __shared__ uint32_t wsum[kTreeGridThreads / 64 + 1];
-  cooperative_groups::grid_group grid = cooperative_groups::this_grid();
-  const NocParams& P = D.P;
-  const uint32_t T = P.tiles, g = blockIdx.x * blockDim.x + threadIdx.x, ng = gridDim.x * blockDim.x;
-  const uint64_t zps = lat_to_ps((uint64_t)P.router_delay + P.link_delay, P.f);
-  TreeAcc acc;
-  for (;;) {
-    grid.sync();
-    const uint32_t n0 = __hip_atomic_load(&ctl->n0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (n0 == 0) break;
-    unsigned long long lm = ~0ull;
-    for (uint32_t i = g; i < n0; i += ng) lm = min(lm, (unsigned long long)E0[i].t);
-    if (lm != ~0ull) atomicMin(&ctl->tmin, lm);
-    grid.sync();
-    const uint64_t wend = __hip_atomic_load(&ctl->tmin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + zps;
-    for (uint32_t i = g; i < n0; i += ng) {
-      const TEv e = E0[i];
-      if (e.t < wend) atomicAdd(&cnt[e.at], 1u);
-      else E1[atomicAdd(&ctl->n1, 1u)] = e;
-    }
-    grid.sync();
-    if (blockIdx.x == 0) {                         // exclusive scan of cnt -> off, cnt reset (cursor)
-      const uint32_t per = (T + blockDim.x - 1) / blockDim.x, t0 = threadIdx.x * per;
-      uint32_t a = 0, tot;
-      for (uint32_t i = t0; i < min(T, t0 + per); ++i) a += cnt[i];
-      a = block_excl_scan(a, wsum, &tot);
-      for (uint32_t i = t0; i < min(T, t0 + per); ++i) { off[i] = a; a += cnt[i]; cnt[i] = 0; }
-      if (threadIdx.x == 0) { off[T] = tot; ctl->tmin = ~0ull; }
-    }
-    grid.sync();
-    for (uint32_t i = g; i < n0; i += ng) {
-      const TEv e = E0[i];
-      if (e.t < wend) G[off[e.at] + atomicAdd(&cnt[e.at], 1u)] = e;
-    }
-    grid.sync();
-    if (g < T) {
-      TEv* h = G + off[g];
-      uint64_t m = off[g + 1] - off[g], hn = 0;
-      for (uint64_t i = 0; i < m; ++i) { const TEv e = h[i]; theap_push(h, hn, e); }
-      while (hn) {
-        const TEv e = theap_pop(h, hn);
-        tree_router(D, IO, e, [&](const TEv& x) { E1[atomicAdd(&ctl->n1, 1u)] = x; }, acc);
-      }
-      cnt[g] = 0;
-    }
-    grid.sync();
-    if (g == 0) { ctl->n0 = ctl->n1; ctl->n1 = 0; }
-    TEv* x = E0; E0 = E1; E1 = x;
+  if (prof && tid == 0) {
+    for (int i = 0; i < 6; ++i) prof[i] += pc[i];
+    prof[6] += pw; prof[7] += pn;
   }
-  if (g < T) acc.flush(D.ctr, g);
 }
 
 struct gg_noc_state {
@@ -1518,9 +1628,9 @@ struct gg_noc_state {
   uint32_t* counts = nullptr; uint32_t* cursor = nullptr; uint64_t* off = nullptr; uint32_t nb_cap = 0;
   bool staged = true;   // LDS-staged stage kernels where the queues fit (GG_NOC_STAGED=0: HBM-resident, A/B)
   TEv* theap = nullptr; uint32_t* bidx = nullptr; uint64_t tcap = 0, bcap = 0;   // broadcast-tree walk scratch
-  uint32_t* tctl = nullptr;                       // grid form: TreeCtl | cnt[kTreeMaxT] | off[kTreeMaxT + 1]
   unsigned long long* prof = nullptr;             // GG_NOC_PROFILE=1: k_chain_sweep phase cycles (diagnostics)
   SK* pscr = nullptr; uint64_t pscr_cap = 0;       // k_chain_pipe: per packet 3 x positions pool / incoming slots
+  uint8_t* tp = nullptr; uint64_t tp_bytes = 0;     // k_tree_pool: TpBufs
   bool pipe = true;                               // GG_NOC_PIPE=0: the position sweep for every chain (A/B)
 };
 
@@ -1556,6 +1666,7 @@ gg_status gg_noc_alloc(gg_ctx* ctx)
   GG_HIP(hipFuncSetAttribute((const void*)k_port_sweep<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPortLds));
   GG_HIP(hipFuncSetAttribute((const void*)k_port_sweep<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPortLds));
   static_assert(kSweepLds <= kStageLdsMax, "the sweep's LDS arrays fit the stage budget");
+  GG_HIP(hipFuncSetAttribute((const void*)k_tree_pool, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTpLds));
   GG_HIP(hipFuncSetAttribute((const void*)k_tree_walk<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)(kTreeLdsEv * sizeof(TEv))));
   GG_HIP(hipMalloc((void**)&S->ctr, sizeof(uint64_t) * c.num_tiles * GG_NUM_NET_COUNTERS));
@@ -1572,7 +1683,7 @@ void gg_noc_free(gg_ctx* ctx)
   gg_noc_state* S = ctx->noc;
   if (!S) return;
   void* ps[] = {S->q, S->nd, S->ctr, S->t, S->zl, S->ct, S->cur, S->keys, S->ids, S->heap,
-                S->counts, S->cursor, S->off, S->theap, S->bidx, S->tctl, S->prof, S->pscr};
+                S->counts, S->cursor, S->off, S->theap, S->bidx, S->prof, S->pscr, S->tp};
   for (void* p : ps) if (p) hipFree(p);
   delete S;
   ctx->noc = nullptr;
@@ -1661,16 +1772,12 @@ gg_status gg_noc_tree(gg_ctx* ctx, const gg_packets* pk, const gg_packet_out* ou
   // arrays (kTreeMaxT) and 32-bit event indices; everything else takes the serial walk
   const bool win = (uint64_t)P.router_delay + P.link_delay > 0 && P.tiles <= kTreeMaxT &&
                    hcap < (1ull << 32) && !(getenv("GG_NOC_TREE_SERIAL") && atoi(getenv("GG_NOC_TREE_SERIAL")));
-  const bool lds = !win && hcap <= kTreeLdsEv;
-  // the window loop over a cooperative grid of CUs: A/B form (GG_NOC_TREE_GRID=1),
-  // measured slower than one workgroup
-  const bool grid = win && P.tiles <= kTreeGridBlocks * kTreeGridThreads &&
-                    getenv("GG_NOC_TREE_GRID") && atoi(getenv("GG_NOC_TREE_GRID")) == 1;
-  if (grid && !S->tctl) {
-    GG_HIP(hipMalloc((void**)&S->tctl, 4 * (4 + 2 * kTreeMaxT + 1)));
-    GG_HIP(hipMemsetAsync(S->tctl, 0, 4 * (4 + 2 * kTreeMaxT + 1), s));
-  }
-  const uint64_t need = win ? 3 * hcap : lds ? 0 : hcap;
+  const uint32_t tp_gcap = P.tiles <= 2048 ? 1024u : 512u;
+  const size_t tp_base = tp_lds_bytes(P.tiles, tp_gcap, 0);
+  const uint32_t tp_ecap = tp_base < kTpLds ? (uint32_t)((kTpLds - tp_base) / (2 * sizeof(TEv))) : 0u;
+  const bool pool = win && tp_ecap >= 64;
+  const bool lds = !pool && hcap <= kTreeLdsEv;
+  const uint64_t need = pool || lds ? 0 : hcap;
   if (need > S->tcap) {
     if (S->theap) hipFree(S->theap);
     GG_HIP(hipMalloc((void**)&S->theap, sizeof(TEv) * need));
@@ -1681,27 +1788,40 @@ gg_status gg_noc_tree(gg_ctx* ctx, const gg_packets* pk, const gg_packet_out* ou
     GG_HIP(hipMalloc((void**)&S->bidx, 4 * n));
     S->bcap = n;
   }
+  TpBufs TB{};
+  if (pool) {
+    const uint64_t need_b = 2 * n * sizeof(TEv) + 2 * hcap * sizeof(TEv) + hcap * sizeof(TGe);
+    if (need_b > S->tp_bytes) {
+      if (S->tp) hipFree(S->tp);
+      GG_HIP(hipMalloc((void**)&S->tp, need_b));
+      S->tp_bytes = need_b;
+    }
+    TEv* e = reinterpret_cast<TEv*>(S->tp);
+    TB.run = e; TB.heap = e + n; TB.hp[0] = e + 2 * n; TB.hp[1] = e + 2 * n + hcap;
+    TB.gh = reinterpret_cast<TGe*>(e + 2 * n + 2 * hcap);
+  }
   NocDev D{P, S->q, S->nd, S->ctr, ctx->err_dev};
   const gg_packet_out none{nullptr, nullptr, nullptr};
   TreeIO IO{pk->src_dev, pk->dst_dev, pk->length_bits_dev, pk->time_ps_dev, S->bidx, *out, nb ? *bout : none};
   gg_timer_begin(ctx, "noc_tree", s);
-  if (win && grid) {
-    TEv *E0 = S->theap, *E1 = S->theap + hcap, *G = S->theap + 2 * hcap;
-    TreeCtl* ctl = reinterpret_cast<TreeCtl*>(S->tctl);
-    uint32_t *cnt = S->tctl + 4, *off = S->tctl + 4 + kTreeMaxT;
-    hipLaunchKernelGGL(k_tree_win<true>, dim3(1), dim3(kTreeThreads), 0, s, D, IO, n, nb, E0, E1, G, hcap, ctl);
-    GG_HIP(hipGetLastError());
-    void* args[] = {(void*)&D, (void*)&IO, (void*)&E0, (void*)&E1, (void*)&G, (void*)&cnt, (void*)&off, (void*)&ctl};
-    GG_HIP(hipLaunchCooperativeKernel((const void*)k_tree_grid, dim3(kTreeGridBlocks), dim3(kTreeGridThreads), args, 0, s));
-  } else if (win)
-    hipLaunchKernelGGL(k_tree_win<false>, dim3(1), dim3(kTreeThreads), 0, s, D, IO, n, nb, S->theap, S->theap + hcap,
-                       S->theap + 2 * hcap, hcap, nullptr);
+  if (pool)
+    hipLaunchKernelGGL(k_tree_pool, dim3(1), dim3(kTpThreads), tp_lds_bytes(P.tiles, tp_gcap, tp_ecap), s, D, IO, n, nb,
+                       TB, hcap, tp_gcap, tp_ecap, S->prof);
   else if (lds)
     hipLaunchKernelGGL(k_tree_walk<true>, dim3(1), dim3(64), hcap * sizeof(TEv), s, D, IO, n, nb, nullptr, hcap);
   else
     hipLaunchKernelGGL(k_tree_walk<false>, dim3(1), dim3(64), 0, s, D, IO, n, nb, S->theap, hcap);
   GG_HIP(hipGetLastError());
   gg_timer_end(ctx, "noc_tree", s);
+  if (S->prof && pool) {
+    unsigned long long h[16];
+    GG_HIP(hipMemcpyAsync(h, S->prof, sizeof(h), hipMemcpyDeviceToHost, s));
+    GG_HIP(hipStreamSynchronize(s));
+    fprintf(stderr, "[gg_noc tree] k_tree_pool gcap %u ecap %u: windows %llu pending %llu | cycles: setup+injection %llu "
+            "min %llu due %llu router sort %llu port tasks %llu forward %llu\n", tp_gcap, tp_ecap, h[6], h[7], h[0],
+            h[1], h[2], h[3], h[4], h[5]);
+    GG_HIP(hipMemsetAsync(S->prof, 0, sizeof(h), s));
+  }
   return GG_OK;
 }
 

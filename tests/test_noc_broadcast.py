@@ -124,7 +124,7 @@ def oracle_tree(cfg, src, dst, bits, t, batches=1):
 @pytest.mark.parametrize("T,n,span,batches,frac,qm", [(16, 3000, 200000, 1, 0.1, 1), (64, 4000, 400000, 2, 0.05, 1),
                                                       (64, 3000, 100000, 1, 0.02, 1), (16, 2000, 100000, 1, 0.2, 0),
                                                       (256, 2000, 400000, 1, 0.01, 1), (256, 3000, 600000, 1, 0.03, 1),
-                                                      # one thread owns several routers (T > the workgroup's threads)
+                                                      # more routers than the workgroup's threads
                                                       (2116, 1500, 400000, 1, 0.004, 1),
                                                       (4096, 1500, 400000, 1, 0.004, 1),
                                                       # beyond the windowed walk's LDS arrays: the serial walk
@@ -145,6 +145,32 @@ def test_broadcast_tree_matches_oracle_on_gpu(T, n, span, batches, frac, qm):
     assert bref[0].shape[0] > 0
     if qm:
         assert int(bref[2].sum()) > 0                              # broadcast copies were contended
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,n,qtype,max_list,analytical", [
+    (64, 3000, C.QM_HISTORY_TREE, 3, 1),      # pruned every request, M/G/1 branch taken
+    (64, 3000, C.QM_HISTORY_TREE, 8, 0),
+    (256, 3000, C.QM_HISTORY_TREE, 100, 0),
+    (64, 3000, C.QM_HISTORY_LIST, 16, 1),
+    (64, 3000, C.QM_BASIC, 100, 1)])
+def test_broadcast_tree_queue_models_on_gpu(T, n, qtype, max_list, analytical):
+    """The windowed walk's port tasks (a history tree's in-order requests from
+    registers, every other request on memory) under each queue model, short
+    lists (every request prunes; out-of-order requests) and the M/G/1 branch."""
+    from gpu_util import torch_dev
+    torch = torch_dev()
+    cfg = _cfg(T, queue_model_type=qtype, max_list_size=max_list, analytical_enabled=analytical)
+    src, dst, bits, t = mixed_packets(T, n, 7 * T + max_list, 150000, bcast_frac=0.05)
+    be, got, bgot = run_tree(torch, cfg, src, dst, bits, t)
+    on, ref, bref = oracle_tree(cfg, src, dst, bits, t)
+    uni = dst != C.BROADCAST
+    for g, r in zip(got, ref):
+        np.testing.assert_array_equal(g[uni], r[uni])
+    for g, r in zip(bgot, bref):
+        np.testing.assert_array_equal(g, r)
+    np.testing.assert_array_equal(be.noc_counters(), on.counters())
+    assert int(bref[2].sum()) > 0
 
 
 @pytest.mark.gpu
@@ -267,23 +293,3 @@ def test_host_mirror_unrolls_broadcast_without_tree(tmp_path):
         if sys_after[k]:
             exp += ["%d %d 0 0" % (c, t[k]) for c in (T, T + 1)]
     assert out[:len(exp)] == exp
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("T,n,frac", [(64, 3000, 0.05), (256, 3000, 0.03)])
-def test_grid_window_loop_matches_oracle_on_gpu(T, n, frac, monkeypatch):
-    """The window loop over a cooperative grid of CUs (GG_NOC_TREE_GRID=1, the
-    A/B form) instead of one workgroup: the same deliveries and counters."""
-    from gpu_util import torch_dev
-    torch = torch_dev()
-    monkeypatch.setenv("GG_NOC_TREE_GRID", "1")
-    cfg = _cfg(T)
-    src, dst, bits, t = mixed_packets(T, n, 5 * T + n, 300000, bcast_frac=frac)
-    be, got, bgot = run_tree(torch, cfg, src, dst, bits, t)
-    on, ref, bref = oracle_tree(cfg, src, dst, bits, t)
-    uni = dst != C.BROADCAST
-    for g, r in zip(got, ref):
-        np.testing.assert_array_equal(g[uni], r[uni])
-    for g, r in zip(bgot, bref):
-        np.testing.assert_array_equal(g, r)
-    np.testing.assert_array_equal(be.noc_counters(), on.counters())
