@@ -598,6 +598,11 @@ def private16_section(args, dev):
                        "configs[1] uniform-random private generator (WRITE p=1/3), Mode P" % (T, N),
            "value": n / dt, "unit": "accesses/s", "seconds": dt, "kernels_ms": kern,
            "path_GB_s": n * ALGO_BYTES_PER_ACCESS / dt / 1e9}
+    if "cache_stream" in kern:                # the single-pass streaming replay (16-way form)
+        gbs = n * ALGO_BYTES_PER_ACCESS / (kern["cache_stream"] / 1e3) / 1e9
+        res["roofline"] = {"bound": "hbm", "kernel": "k_cache_stream", "achieved": gbs, "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "bytes_per_access": ALGO_BYTES_PER_ACCESS,
+                           "kernel_ms": kern["cache_stream"]}
     if not args.no_verify:
         t = T - 1
         a, m = po.gen_uniform(t, 0, N)

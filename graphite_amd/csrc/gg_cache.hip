@@ -22,6 +22,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <cstdio>
+#include <type_traits>
 
 namespace {
 
@@ -802,6 +803,27 @@ __device__ __forceinline__ int victim_nib(uint32_t states, uint32_t ages)
   return ip ? fi : lw;
 }
 
+// 16 nibble ages (16-way L2, ages 0..15 leave no spare bit per nibble): the
+// same update with the even and the odd nibbles compared as bytes
+__device__ __forceinline__ uint64_t lru_nib64(uint64_t ages, uint32_t way)
+{
+  constexpr uint64_t L = 0x0F0F0F0F0F0F0F0Full, G = 0x8080808080808080ull;
+  const uint32_t sh = 4 * way;
+  const uint64_t accb = ((ages >> sh) & 0xFull) * 0x0101010101010101ull;
+  uint64_t e = ages & L, o = (ages >> 4) & L;
+  e += (~((e | G) - accb) & G) >> 7;                 // +1 where age < the accessed way's age
+  o += (~((o | G) - accb) & G) >> 7;
+  return (e | (o << 4)) & ~(0xFull << sh);
+}
+__device__ __forceinline__ int victim_nib64(uint32_t states, uint64_t ages)
+{
+  const uint32_t ip = ~(states | (states >> 1)) & 0x55555555u;
+  const int fi = (int)(__builtin_ctz(ip | 0x80000000u) >> 1);
+  const uint64_t zn = (uint64_t)zero_nibbles(~(uint32_t)ages) | ((uint64_t)zero_nibbles(~(uint32_t)(ages >> 32)) << 32);
+  const int lw = zn ? (int)((63 - __builtin_clzll(zn)) >> 2) : -1;
+  return ip ? fi : lw;
+}
+
 template <int A1, int A2, bool LRU1, bool LRU2>
 __global__ __launch_bounds__(64) void k_cache_replay_lean(gg_cache_state cs, gg_geom g,
     const uint64_t* __restrict__ sh_key, const uint32_t* __restrict__ unit_len,
@@ -1150,7 +1172,7 @@ constexpr uint16_t kLgkm0 = 0xC07F;         // s_waitcnt lgkmcnt(0) (vmcnt/expcn
 size_t stream_lds_bytes(uint32_t u1, uint32_t s2, uint32_t a2)
 {
   const size_t tq = (a2 + 3) / 4;
-  return (size_t)s2 * u1 * (tq * 16 + 8) + (size_t)kRing * u1 * 8 + (size_t)u1 * 12 + 16 + (size_t)u1 * 8 + (size_t)u1 * 4;
+  return (size_t)s2 * u1 * (tq * 16 + (a2 > 8 ? 16 : 8)) + (size_t)kRing * u1 * 8 + (size_t)u1 * 12 + 16 + (size_t)u1 * 8 + (size_t)u1 * 4;
 }
 
 template <int A1, int A2, bool LRU1, bool LRU2, int NCW, bool EV>
@@ -1158,14 +1180,29 @@ __global__ __launch_bounds__((NCW + 1) * GG_WAVE) void k_cache_stream(gg_cache_s
     const uint64_t* __restrict__ addr, const uint32_t* __restrict__ meta, const uint64_t* __restrict__ tile_off,
     uint32_t* __restrict__ result, uint64_t* __restrict__ evicted, uint32_t* err, unsigned long long* dbg)
 {
-  static_assert(A1 <= 4 && A2 <= 8, "streaming replay covers L1-D assoc <= 4, L2 assoc <= 8");
+  static_assert(A1 <= 4 && (A2 <= 8 || A2 == 16), "streaming replay covers L1-D assoc <= 4, L2 assoc <= 8 or 16");
   constexpr uint32_t U1 = NCW * GG_WAVE;   // == g.u1 (host-checked)
   constexpr int TQ = (A2 + 3) / 4;
+  constexpr int MW = (A2 + 7) / 8;         // HBM meta words per L2 set
+  // per (L2 set, unit): LRU ages (nibble per way), 2-bit states, round-robin
+  // way; 16 ways take 64-bit ages in a 16-B record
+  constexpr bool W16 = A2 > 8;
+  using AgT = typename std::conditional<W16, uint64_t, uint32_t>::type;
+  using MtT = typename std::conditional<W16, uint4, uint2>::type;
+  auto mt_pack = [](AgT ages, uint32_t st, uint32_t rr) -> MtT {
+    if constexpr (W16) return make_uint4((uint32_t)ages, (uint32_t)((uint64_t)ages >> 32), st, rr);
+    else return make_uint2((uint32_t)ages, st | (rr << 16));
+  };
+  auto mt_ages = [](const MtT& m) -> AgT {
+    if constexpr (W16) return ((uint64_t)m.y << 32) | m.x; else return m.x;
+  };
+  auto mt_st = [](const MtT& m) -> uint32_t { if constexpr (W16) return m.z; else return m.y & 0xFFFFu; };
+  auto mt_rr = [](const MtT& m) -> uint32_t { if constexpr (W16) return m.w & 0xFFu; else return (m.y >> 16) & 0xFFu; };
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t S2 = g.s2;
   uint4* T = reinterpret_cast<uint4*>(smem);                                            // [s][q][u]
-  uint2* Mt = reinterpret_cast<uint2*>(smem + (size_t)S2 * U1 * TQ * 16);                // [s][u]
-  uint64_t* ring = reinterpret_cast<uint64_t*>(smem + (size_t)S2 * U1 * (TQ * 16 + 8));  // [kRing][u]
+  MtT* Mt = reinterpret_cast<MtT*>(smem + (size_t)S2 * U1 * TQ * 16);                    // [s][u]
+  uint64_t* ring = reinterpret_cast<uint64_t*>(smem + (size_t)S2 * U1 * (TQ * 16 + sizeof(MtT)));  // [kRing][u]
   uint32_t* tailp = reinterpret_cast<uint32_t*>(ring + kRing * U1);                      // [u]
   uint32_t* headp = tailp + U1;                                                          // [u]
   uint32_t* resv = headp + U1;                                                           // [u] producer-private
@@ -1215,15 +1252,18 @@ __global__ __launch_bounds__((NCW + 1) * GG_WAVE) void k_cache_stream(gg_cache_s
 #pragma unroll
       for (int w = 0; w < 4 * TQ; ++w)
         tg[w] = (w < A2) ? cs.l2_tag[(uint64_t)(s * A2 + w) * g.units + gu] : GG_L2_INV_TAG;
-      const uint64_t mw = cs.l2_meta[(uint64_t)s * g.units + gu];
-      uint32_t ages = 0xFFFFFFFFu, st = 0;
+      uint64_t mwv[MW];
+#pragma unroll
+      for (int k = 0; k < MW; ++k) mwv[k] = cs.l2_meta[(uint64_t)(s * MW + k) * g.units + gu];
+      AgT ages = ~(AgT)0;
+      uint32_t st = 0;
 #pragma unroll
       for (int w = 0; w < A2; ++w) {
-        const uint32_t b = (uint32_t)(mw >> (8 * w)) & 0xFFu;
+        const uint32_t b = (uint32_t)(mwv[w / 8] >> (8 * (w % 8))) & 0xFFu;
         const bool valid = tg[w] != GG_L2_INV_TAG;
         errv |= (valid != (GG_M_STATE(b) != GG_MS_I)) ? GG_DERR_STATE : 0u;
         st |= (valid ? GG_M_STATE(b) : 0u) << (2 * w);
-        ages = (ages & ~(0xFu << (4 * w))) | ((GG_M_AGE(b) & 0xFu) << (4 * w));
+        ages = (ages & ~((AgT)0xF << (4 * w))) | ((AgT)(GG_M_AGE(b) & 0xFu) << (4 * w));
         const uint64_t ln = ((uint64_t)tg[w] << g.log_l2) | ((uint64_t)s << g.log_u1) | l1set;
         int hw = -1;
 #pragma unroll
@@ -1236,7 +1276,7 @@ __global__ __launch_bounds__((NCW + 1) * GG_WAVE) void k_cache_stream(gg_cache_s
       for (int q = 0; q < TQ; ++q)
         T[((size_t)s * TQ + q) * U1 + u] = make_uint4(tg[4 * q], tg[4 * q + 1], tg[4 * q + 2], tg[4 * q + 3]);
       const uint32_t rr = LRU2 ? 0u : cs.l2_rr[(uint64_t)s * g.units + gu];
-      Mt[s * U1 + u] = make_uint2(ages, st | (rr << 16));
+      Mt[s * U1 + u] = mt_pack(ages, st, rr);
     }
     uint32_t nvalid = 0;
 #pragma unroll
@@ -1437,8 +1477,9 @@ __global__ __launch_bounds__((NCW + 1) * GG_WAVE) void k_cache_stream(gg_cache_s
       const uint4 v = *reinterpret_cast<const uint4*>(tag0 + tq0 + q * 4 * U1);
       tg[4 * q] = v.x; tg[4 * q + 1] = v.y; tg[4 * q + 2] = v.z; tg[4 * q + 3] = v.w;
     }
-    const uint2 mt = Mt[s * U1 + u];
-    uint32_t ages2 = mt.x, st2 = mt.y & 0xFFFFu, rr2 = mt.y >> 16;
+    const MtT mt = Mt[s * U1 + u];
+    AgT ages2 = mt_ages(mt);
+    uint32_t st2 = mt_st(mt), rr2 = mt_rr(mt);
     // L2 lookup (valid tags are unique in a set; invalid ways hold the invalid tag)
     bool eq[A2];
 #pragma unroll
@@ -1447,7 +1488,8 @@ __global__ __launch_bounds__((NCW + 1) * GG_WAVE) void k_cache_stream(gg_cache_s
 #pragma unroll
     for (int w = A2 - 1; w >= 0; --w) w2 = eq[w] ? (uint32_t)w : w2;
     const uint32_t has2m = w2 < A2 ? 0xFFFFFFFFu : 0u;
-    const uint32_t s2 = __builtin_amdgcn_ubfe(st2, 2 * w2, 2);            // 0 when absent
+    // 0 when absent (8 ways and fewer: the bits above the states are 0)
+    const uint32_t s2 = W16 ? (__builtin_amdgcn_ubfe(st2, 2 * (w2 & 15u), 2) & has2m) : __builtin_amdgcn_ubfe(st2, 2 * w2, 2);
     // L1-D lookup: the way naming the line's L2 slot; hit = readable (READ) or MODIFIED (WRITE)
     const uint32_t slot = s * A2 + w2;
     const uint32_t zb1 = zero_bytes32(pos1 ^ __builtin_amdgcn_perm(0u, slot, 0u)) & has2m;
@@ -1469,7 +1511,9 @@ __global__ __launch_bounds__((NCW + 1) * GG_WAVE) void k_cache_stream(gg_cache_s
     st2 = upg ? (st2 & ~(3u << (2 * w2))) : st2;
     *(upg ? tag0 + tq0 + (w2 / 4) * 4 * U1 + (w2 % 4) : my_dummy) = GG_L2_INV_TAG;
     // L2 victim (l2_cache_cntlr.cc:74-116)
-    int v2 = LRU2 ? victim_nib<A2>(st2, ages2) : (int)rr2;
+    int v2;
+    if constexpr (W16) v2 = LRU2 ? victim_nib64(st2, ages2) : (int)rr2;
+    else v2 = LRU2 ? victim_nib<A2>(st2, ages2) : (int)rr2;
     errv |= (miss2 && v2 < 0) ? GG_DERR_STATE : 0u;
     const uint32_t vw = (uint32_t)v2 & (A2 - 1);
     const uint32_t sv = __builtin_amdgcn_ubfe(st2, 2 * vw, 2);
@@ -1493,10 +1537,12 @@ __global__ __launch_bounds__((NCW + 1) * GG_WAVE) void k_cache_stream(gg_cache_s
     *(miss2 ? tag0 + tq0 + (vw / 4) * 4 * U1 + (vw % 4) : my_dummy) = tag2;
     if (!LRU2) rr2 = miss2 ? (rr2 ? rr2 - 1 : (A2 - 1)) : rr2;
     if (LRU2) {
-      const uint32_t nb = lru_nib(ages2, miss2 ? vw : (w2 & (A2 - 1)));
+      AgT nb;
+      if constexpr (W16) nb = lru_nib64(ages2, miss2 ? vw : (w2 & (A2 - 1)));
+      else nb = lru_nib(ages2, miss2 ? vw : (w2 & (A2 - 1)));
       ages2 = (!hit1 || wr) ? nb : ages2;
     }
-    Mt[s * U1 + u] = make_uint2(ages2, st2 | (rr2 << 16));
+    Mt[s * U1 + u] = mt_pack(ages2, st2, rr2);
     // L1-D insert (insertCacheLineInL1, l2_cache_cntlr.cc:133-165) after both invalidations
     uint32_t v1;
     bool l1ev;
@@ -1613,21 +1659,26 @@ __global__ __launch_bounds__((NCW + 1) * GG_WAVE) void k_cache_stream(gg_cache_s
     cs.l1_meta[gu] = m1;
     cs.l1_rr[gu] = (uint8_t)rr1;
     for (uint32_t s = 0; s < S2; ++s) {
-      const uint2 mt = Mt[s * U1 + u];
-      uint64_t mw = 0;
+      const MtT mt = Mt[s * U1 + u];
+      const AgT ages = mt_ages(mt);
+      const uint32_t sts = mt_st(mt);
+      uint64_t mwv[MW];
 #pragma unroll
-      for (int w = 0; w < 8; ++w) {
+      for (int k = 0; k < MW; ++k) mwv[k] = 0;
+#pragma unroll
+      for (int w = 0; w < 8 * MW; ++w) {
         if (w < A2) {
-          const uint32_t st = (mt.y >> (2 * w)) & 3u;
+          const uint32_t st = (sts >> (2 * w)) & 3u;
           const uint32_t zb = zero_bytes32(pos1 ^ ((s * A2 + w) * 0x01010101u));
-          mw |= (uint64_t)GG_M_MAKE(st, (zb != 0) ? 1u : 0u, (mt.x >> (4 * w)) & 0xFu) << (8 * w);
+          mwv[w / 8] |= (uint64_t)GG_M_MAKE(st, (zb != 0) ? 1u : 0u, (uint32_t)(ages >> (4 * w)) & 0xFu) << (8 * (w % 8));
           cs.l2_tag[(uint64_t)(s * A2 + w) * g.units + gu] = tag_at(s, w);
         } else {
-          mw |= 0xF8ull << (8 * w);
+          mwv[w / 8] |= 0xF8ull << (8 * (w % 8));
         }
       }
-      cs.l2_meta[(uint64_t)s * g.units + gu] = mw;
-      if (!LRU2) cs.l2_rr[(uint64_t)s * g.units + gu] = (uint8_t)((mt.y >> 16) & 0xFFu);
+#pragma unroll
+      for (int k = 0; k < MW; ++k) cs.l2_meta[(uint64_t)(s * MW + k) * g.units + gu] = mwv[k];
+      if (!LRU2) cs.l2_rr[(uint64_t)s * g.units + gu] = (uint8_t)mt_rr(mt);
     }
   }
   if (errv) atomicOr(err, errv);
@@ -1831,6 +1882,7 @@ const StreamKern kStream[] = {
   GG_STREAM(4, 8, 1, 1, 2), GG_STREAM(4, 8, 0, 0, 2), GG_STREAM(4, 8, 1, 0, 2), GG_STREAM(4, 8, 0, 1, 2),
   GG_STREAM(4, 4, 1, 1, 2), GG_STREAM(2, 4, 1, 1, 2), GG_STREAM(2, 8, 1, 1, 2), GG_STREAM(4, 2, 1, 1, 2),
   GG_STREAM(4, 8, 1, 1, 1), GG_STREAM(4, 8, 1, 1, 4),
+  GG_STREAM(4, 16, 1, 1, 2), GG_STREAM(4, 16, 0, 0, 2),      // configs[4]: 16-way L2
 };
 
 const StreamKern* find_stream(const gg_geom& g)

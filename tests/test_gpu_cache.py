@@ -76,6 +76,7 @@ def ragged_trace(T, seed, lines_log2, max_len):
 @pytest.mark.parametrize("geom", [
     dict(),                                                      # reference defaults
     dict(l2_assoc=16),                                           # configs[4]: 16-way L2
+    dict(l2_assoc=16, l1d_policy=C.POLICY_ROUND_ROBIN, l2_policy=C.POLICY_ROUND_ROBIN),
     dict(l1d_size_kb=4, l1d_assoc=2, l2_size_kb=16, l2_assoc=4),
     dict(l1d_policy=C.POLICY_ROUND_ROBIN, l2_policy=C.POLICY_ROUND_ROBIN),
     dict(l1d_size_kb=16, l1d_assoc=8, l2_size_kb=256, l2_assoc=8),
