@@ -15,6 +15,8 @@
 // one global event queue exactly.
 #include "gg_dev.h"
 
+#include <hip/hip_cooperative_groups.h>
+
 #include <algorithm>
 
 namespace {
@@ -1174,6 +1176,7 @@ __device__ __forceinline__ void tcadd(uint64_t* c, uint32_t tile, int k, uint64_
 }
 // a router's event counters, summed in registers over its events and added
 // to HBM once (the windowed walk: one thread owns a router)
+constexpr uint32_t kNetCtrTree = 15;   // TreeAcc's fields: rcc rpk buf sw xb[5] link prcv frcv brcv lat con
 struct TreeAcc {
   uint64_t rcc = 0, rpk = 0, buf = 0, sw = 0, xb[5] = {0, 0, 0, 0, 0}, link = 0, prcv = 0, frcv = 0, brcv = 0, lat = 0, con = 0;
   __device__ __forceinline__ void crossbar(int np, uint64_t nf)
@@ -1616,6 +1619,414 @@ __global__ __launch_bounds__(kTpThreads) void k_tree_pool(NocDev D, TreeIO IO, u
   }
 }
 
+// ---------------------------------------------------------------------------
+// The windowed walk over the whole chip (k_tree_grid, the default where its
+// LDS fits): the same windows as k_tree_pool, with the routers spread over
+// G workgroups (one per CU), each owning a block of R consecutive routers
+// and their six output-port queues as LDS images for the whole batch, so a
+// queue request costs LDS latency instead of HBM round trips.  Per window:
+//   grid barrier -> the window start (min over every pending event, kept in
+//   three rotating words) -> the copies other blocks pushed during the last
+//   window drained from the block's inbox into its pool -> the due events
+//   (pool and the tiles' injection runs) linked per router, sorted by
+//   (time, index) -> one task per (router, output port) -> per router:
+//   counters, deliveries, forwarded copies (to the own pool, or appended to
+//   the owner block's inbox for the next window) -> the next window's start
+//   contributed by atomic min.
+// One grid barrier per window (cooperative launch: every workgroup
+// resident).  k_tree_setup (one workgroup) validates and buckets the packets
+// by source first.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kTgThreads = 256;
+constexpr uint32_t kTgBarShards = 32;                // grid barrier counter shards
+constexpr uint32_t kTgBarFlags = 8;                  // grid barrier release flag replicas
+struct TgBufs {
+  uint32_t* off;             // [T + 1] packets per source (k_tree_setup)
+  TEv* pk;                   // [n] the packets bucketed by source; heap scratch
+  TEv* run;                  // [n] each tile's injection router events, (time, index)-sorted
+  TEv* spill;                // [2][G][bwg] the pool buffers beyond LDS
+  TEv* inbox;                // [2][G][bwg] copies pushed by other blocks, per window parity
+  TGe* gh;                   // [G][bwg] due records beyond LDS
+  uint32_t* icnt;            // [2][G] inbox counts
+  unsigned long long* gmin;  // [3] window starts (rotating)
+  uint32_t* flag;            // [1] nonzero: setup rejected the batch
+  uint32_t* bar;             // [kTgBarShards + kTgBarFlags][32] barrier arrival shards, release flags (128-B lines)
+};
+
+__global__ __launch_bounds__(1024) void k_tree_setup(NocDev D, TreeIO IO, uint64_t n, uint64_t nb, TgBufs B, uint64_t hcap)
+{
+  __shared__ uint32_t wsum[1024 / 64 + 1];
+  __shared__ uint32_t s_err;
+  extern __shared__ __align__(16) uint8_t ts_lds[];
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(ts_lds);          // [T]
+  const NocParams& P = D.P;
+  const uint32_t T = P.tiles, tid = threadIdx.x, nt = blockDim.x;
+  if (tid == 0) s_err = 0;
+  for (uint32_t i = tid; i < T; i += nt) cnt[i] = 0;
+  __syncthreads();
+  const uint64_t per = (n + nt - 1) / nt, k0 = min(n, tid * per), k1 = min(n, k0 + per);
+  uint32_t mine = 0;
+  for (uint64_t k = k0; k < k1; ++k) {
+    const uint32_t s = IO.src[k], d = IO.dst[k];
+    if (s >= T || (d >= T && d != GG_BROADCAST)) atomicOr(&s_err, GG_DERR_RANGE);
+    mine += d == GG_BROADCAST;
+    if (s < T && s != d) atomicAdd(&cnt[s], 1u);
+  }
+  uint32_t nbc;
+  mine = block_excl_scan(mine, wsum, &nbc);
+  if (tid == 0 && (nbc != nb || n + nb * T > hcap)) s_err |= GG_DERR_CAP;
+  __syncthreads();
+  if (s_err) { if (tid == 0) { atomicOr(D.err, s_err); *B.flag = 1; } return; }
+  if (tid == 0) *B.flag = 0;
+  for (uint64_t k = k0; k < k1; ++k) IO.bidx[k] = IO.dst[k] == GG_BROADCAST ? mine++ : ~0u;
+  {
+    const uint32_t pt = (T + nt - 1) / nt;
+    uint32_t a = 0, tot;
+    for (uint32_t i = tid * pt; i < min(T, (tid + 1) * pt); ++i) a += cnt[i];
+    a = block_excl_scan(a, wsum, &tot);
+    for (uint32_t i = tid * pt; i < min(T, (tid + 1) * pt); ++i) { B.off[i] = a; a += cnt[i]; cnt[i] = 0; }
+    if (tid == 0) B.off[T] = tot;
+    __syncthreads();
+  }
+  for (uint64_t k = k0; k < k1; ++k) {
+    const uint32_t s = IO.src[k], d = IO.dst[k];
+    if (s == d) { IO.out.arrival_ps_dev[k] = IO.t0[k]; IO.out.zero_load_ps_dev[k] = 0; IO.out.contention_ps_dev[k] = 0; continue; }
+    B.pk[B.off[s] + atomicAdd(&cnt[s], 1u)] = TEv{IO.t0[k], (uint32_t)k, s | kInjBit};
+  }
+}
+
+// LDS bytes of k_tree_grid: R routers' six queue images, run heads, two pool
+// buffers of ecap events, gcap due records, per-router lists and counters
+__host__ __device__ inline size_t tg_lds_bytes(uint32_t R, uint32_t qb, uint32_t ecap, uint32_t gcap)
+{
+  return (size_t)R * 6 * qb + 8ull * R + 8ull * R * kNetCtrTree + 2ull * ecap * sizeof(TEv) + (size_t)gcap * sizeof(TGe) +
+         20ull * R;
+}
+
+__global__ __launch_bounds__(kTgThreads) void k_tree_grid(NocDev D, TreeIO IO, TgBufs B, uint32_t R, uint32_t qb,
+                                                         uint64_t bwg, uint32_t ecap, uint32_t gcap,
+                                                         unsigned long long* prof)
+{
+  // prof (GG_NOC_PROFILE=1, diagnostics): block 0's shader clocks per phase
+  unsigned long long pc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pw = 0, pt = __builtin_amdgcn_s_memtime();
+  auto lap = [&](int i) { if (prof) { const unsigned long long x = __builtin_amdgcn_s_memtime(); pc[i] += x - pt; pt = x; } };
+  if (*B.flag) return;                                   // rejected in setup: every block leaves before a barrier
+  extern __shared__ __align__(16) uint8_t tg_lds[];
+  __shared__ unsigned long long s_pmin;
+  __shared__ uint32_t s_n0, s_n1, s_nd, s_na;
+  const NocParams& P = D.P;
+  const uint32_t T = P.tiles, g = blockIdx.x, G = gridDim.x, tid = threadIdx.x, nt = blockDim.x, ln = tid & 63;
+  const uint32_t r0 = g * R, nr = r0 < T ? min(R, T - r0) : 0u;
+  const uint64_t zps = lat_to_ps((uint64_t)P.router_delay + P.link_delay, P.f);
+  uint8_t* img = tg_lds;                                                        // [R][6] queue images
+  uint64_t* hd = reinterpret_cast<uint64_t*>(img + (size_t)R * 6 * qb);          // [R] run head times
+  uint64_t* lctr = hd + R;                                                      // [R][kNetCtrTree] router counters
+  TEv* El[2] = {reinterpret_cast<TEv*>(lctr + (size_t)R * kNetCtrTree), reinterpret_cast<TEv*>(lctr + (size_t)R * kNetCtrTree) + ecap};
+  TGe* Gl = reinterpret_cast<TGe*>(El[1] + ecap);                               // [gcap]
+  uint32_t* cur = reinterpret_cast<uint32_t*>(Gl + gcap);                       // [R] run cursors
+  uint32_t* end = cur + R;                                                      // [R]
+  uint32_t* head = end + R;                                                     // [R] due list per local router
+  uint32_t* act = head + R;                                                     // [R] local routers with due events
+  uint32_t* um = act + R;                                                       // [R] their ports
+  TEv* const sp[2] = {B.spill + (size_t)g * bwg, B.spill + ((size_t)G + g) * bwg};
+  TGe* const gh = B.gh + (size_t)g * bwg;
+  auto with_g = [&](uint32_t i, auto f) { if (i < gcap) f(Gl[i]); else f(gh[i - gcap]); };
+  auto with_e = [&](uint32_t b, uint32_t i, auto f) { if (i < ecap) f(El[b][i]); else f(sp[b][i - ecap]); };
+  // Cross-block data (inbox records and counts, window starts) moves with
+  // agent-scope (sc1) stores / loads and atomics only, so the grid barrier
+  // needs no L2 write-back or invalidate: every wave waits for its stores,
+  // the workgroup meets, one lane adds to the arrival counter and polls it
+  // with sc1 loads (MI355X_MICROARCH.md, inter-workgroup hand-offs, row 1).
+  // Arrivals: each block adds 1 to its shard of a sharded counter
+  // (kTgBarShards words, one 128-B line each, so the adds do not serialize on
+  // one address); block 0 polls every shard and then publishes the
+  // generation in kTgBarFlags replicated flags; every other block polls its
+  // replica (one line read by G / kTgBarFlags blocks, not by all G).
+  unsigned long long pbw = 0, pbp = 0, pbn = 0;
+  uint32_t* const flags = B.bar + kTgBarShards * 32;
+  auto gbar = [&](uint32_t gen) {
+    const unsigned long long b0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const unsigned long long b1 = prof ? __builtin_amdgcn_s_memtime() : 0;
+    if (tid < 64) {
+      if (tid == 0) atomicAdd(&B.bar[(g % kTgBarShards) * 32], 1u);
+      uint32_t spin = 0;
+      if (g == 0) {
+        const uint32_t target = gen * G;
+        for (;; ++spin) {
+          const uint32_t v = tid < kTgBarShards ? __hip_atomic_load(&B.bar[tid * 32], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+          uint32_t sum = v;
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) sum += (uint32_t)__shfl_xor((int)sum, o);
+          if (sum >= target) break;
+          if (spin > (1u << 26)) { if (tid == 0) atomicOr(D.err, GG_DERR_STATE); break; }
+          __builtin_amdgcn_s_sleep(1);
+          ++pbn;
+        }
+        if (tid < kTgBarFlags) __hip_atomic_store(&flags[tid * 32], gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else if (tid == 0) {
+        uint32_t* f = &flags[(g % kTgBarFlags) * 32];
+        for (; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gen; ++spin) {
+          if (spin > (1u << 26)) { atomicOr(D.err, GG_DERR_STATE); break; }
+          __builtin_amdgcn_s_sleep(1);
+          ++pbn;
+        }
+      }
+    }
+    __syncthreads();
+    if (prof) { const unsigned long long b2 = __builtin_amdgcn_s_memtime(); pbw += b1 - b0; pbp += b2 - b1; }
+  };
+  auto ld_ev = [](const TEv* p) {
+    const uint64_t a = __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t b = __hip_atomic_load(reinterpret_cast<const uint64_t*>(p) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return TEv{a, (uint32_t)b, (uint32_t)(b >> 32)};
+  };
+  auto st_ev = [](TEv* p, const TEv& e) {
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(p), e.t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(p) + 1, (uint64_t)e.id | ((uint64_t)e.at << 32), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  };
+  auto qtree = [&](uint32_t lr, int port) {
+    uint8_t* q = img + ((size_t)lr * 6 + port) * qb;
+    return HTree{reinterpret_cast<HQueue*>(q), reinterpret_cast<HNode*>(q + sizeof(HQueue)), 1, P.analytical != 0};
+  };
+  // the block's queue images into LDS; counters zero
+  {
+    const uint32_t words = qb / 16, per_q = words;
+    for (uint32_t i = tid; i < nr * 6 * per_q; i += nt) {
+      const uint32_t qi = i / per_q, wd = i % per_q, lr = qi / 6, port = qi % 6;
+      const uint64_t gq = (uint64_t)(r0 + lr) * 6 + port;
+      uint4 v;
+      if (wd * 16 < sizeof(HQueue)) v = reinterpret_cast<const uint4*>(D.q + gq)[wd];
+      else v = reinterpret_cast<const uint4*>(D.nd + gq * P.max_size)[wd - sizeof(HQueue) / 16];
+      reinterpret_cast<uint4*>(img + (size_t)qi * qb)[wd] = v;
+    }
+    for (uint32_t i = tid; i < nr * kNetCtrTree; i += nt) lctr[i] = 0;
+    for (uint32_t i = tid; i < nr; i += nt) head[i] = kTpNil;
+    if (tid == 0) { s_n0 = 0; s_pmin = ~0ull; }
+  }
+  __syncthreads();
+  // injection ports of the block's tiles: each tile's packets in (time, index)
+  // order through its injection queue; the router events re-sorted into its run
+  for (uint32_t lr = tid; lr < nr; lr += nt) {
+    const uint32_t r = r0 + lr, o = B.off[r], m = B.off[r + 1] - o;
+    TEv* h = B.pk + o;
+    TEv* h2 = B.run + o;
+    uint64_t hn = 0, hn2 = 0;
+    for (uint32_t i = 0; i < m; ++i) { const TEv e = h[i]; theap_push(h, hn, e); }
+    HTree tq = qtree(lr, 5);
+    while (hn) {
+      const TEv e = theap_pop(h, hn);
+      const uint32_t k = e.id, bits = IO.len[k];
+      const uint64_t nf = nflits(P, bits);
+      tcadd(D.ctr, r, GG_NC_PACKETS_SENT, 1); tcadd(D.ctr, r, GG_NC_FLITS_SENT, nf); tcadd(D.ctr, r, GG_NC_BITS_SENT, bits);
+      if (IO.dst[k] == GG_BROADCAST) {                 // updateSendCounters (network_model.cc:244-250)
+        tcadd(D.ctr, r, GG_NC_PACKETS_BROADCASTED, 1); tcadd(D.ctr, r, GG_NC_FLITS_BROADCASTED, nf);
+        tcadd(D.ctr, r, GG_NC_BITS_BROADCASTED, bits);
+      }
+      const uint64_t qd = P.qm ? tq.delay(time_to_cycles(e.t, P.f), nf, D.err) : 0;
+      theap_push(h2, hn2, TEv{e.t + lat_to_ps(0, P.f) + lat_to_ps(qd, P.f), k, r});
+    }
+    for (uint32_t i = 0; i < m; ++i) h[i] = theap_pop(h2, hn2);
+    for (uint32_t i = 0; i < m; ++i) h2[i] = h[i];
+    cur[lr] = o; end[lr] = o + m;
+    hd[lr] = m ? h2[0].t : ~0ull;
+    if (m) atomicMin(&B.gmin[0], (unsigned long long)h2[0].t);
+  }
+  // 3. windows
+  lap(0);
+  for (uint32_t w = 0;; ++w) {
+    gbar(w + 1);
+    lap(1);
+    const uint64_t tmin = __hip_atomic_load(&B.gmin[w % 3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tmin == ~0ull) break;
+    ++pw;
+    if (g == 0 && tid == 0) __hip_atomic_store(&B.gmin[(w + 2) % 3], ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t wend = tmin + zps;
+    const uint32_t pin = w & 1u, pout = pin ^ 1u, pb = w & 1u;      // pool buffer pb holds the pending events
+    // the copies other blocks pushed in the last window join the pool
+    const uint32_t nin = __hip_atomic_load(&B.icnt[pin * G + g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const TEv* inb = B.inbox + ((size_t)pin * G + g) * bwg;
+    const uint32_t n0 = s_n0;
+    for (uint32_t i = tid; i < nin; i += nt) { const TEv e = ld_ev(inb + i); with_e(pb, n0 + i, [&](TEv& x) { x = e; }); }
+    __syncthreads();
+    if (tid == 0) {
+      __hip_atomic_store(&B.icnt[pin * G + g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_n0 = n0 + nin; s_n1 = 0; s_nd = 0; s_na = 0; s_pmin = ~0ull;
+    }
+    __syncthreads();
+    const uint32_t np0 = s_n0;
+    auto add_due = [&](const TEv& e) {
+      const uint32_t slot = atomicAdd(&s_nd, 1u), k = e.id, c = e.at, lr = c - r0;
+      const uint32_t s = IO.src[k], d = IO.dst[k];
+      const TGe gr{e.t, IO.t0[k], 0, k, c, s, d, IO.len[k], d == GG_BROADCAST ? IO.bidx[k] : 0u, 0u,
+                   tree_ports(P, c, s, d)};
+      const uint32_t nx = atomicExch(&head[lr], slot);
+      if (nx == kTpNil) act[atomicAdd(&s_na, 1u)] = lr;
+      with_g(slot, [&](TGe& x) { x = gr; x.next = nx; });
+    };
+    unsigned long long cm = ~0ull;
+    for (uint32_t i = tid; i < np0; i += nt) {
+      TEv e;
+      with_e(pb, i, [&](TEv& x) { e = x; });
+      if (e.t < wend) add_due(e);
+      else { with_e(pb ^ 1u, atomicAdd(&s_n1, 1u), [&](TEv& x) { x = e; }); cm = min(cm, (unsigned long long)e.t); }
+    }
+    for (uint32_t lr = tid; lr < nr; lr += nt) {
+      while (hd[lr] < wend) {
+        const uint32_t c = cur[lr];
+        const TEv e = B.run[c];
+        hd[lr] = c + 1 < end[lr] ? B.run[c + 1].t : ~0ull;
+        cur[lr] = c + 1;
+        add_due(e);
+      }
+      cm = min(cm, (unsigned long long)hd[lr]);
+    }
+    cm = tp_wave_min64(cm);
+    if (ln == 0 && cm != ~0ull) atomicMin(&s_pmin, cm);
+    __syncthreads();
+    lap(2);
+    const uint32_t na = s_na;
+    // each router's due list sorted by (time, index); the union of its ports
+    for (uint32_t i = tid; i < na; i += nt) {
+      const uint32_t lr = act[i];
+      uint32_t sorted = kTpNil, x = head[lr], u = 0;
+      while (x != kTpNil) {
+        TGe gx;
+        with_g(x, [&](TGe& y) { gx = y; });
+        const uint32_t nx = gx.next;
+        u |= gx.mask;
+        auto lt = [&](uint32_t y) { uint64_t ty; uint32_t ky; with_g(y, [&](TGe& z) { ty = z.t; ky = z.k; });
+                                    return gx.t < ty || (gx.t == ty && gx.k < ky); };
+        if (sorted == kTpNil || lt(sorted)) { with_g(x, [&](TGe& y) { y.next = sorted; }); sorted = x; }
+        else {
+          uint32_t y = sorted;
+          for (;;) {
+            uint32_t yn;
+            with_g(y, [&](TGe& z) { yn = z.next; });
+            if (yn == kTpNil || lt(yn)) { with_g(x, [&](TGe& z) { z.next = yn; }); with_g(y, [&](TGe& z) { z.next = x; }); break; }
+            y = yn;
+          }
+        }
+        x = nx;
+      }
+      head[lr] = sorted;
+      um[i] = u;
+    }
+    __syncthreads();
+    lap(3);
+    // (router, port) tasks on the LDS queue images
+    if (P.qm) {
+      for (uint32_t j = tid; j < NPORTS * na; j += nt) {
+        const uint32_t i = j % na, port = j / na;
+        if (!((um[i] >> port) & 1u)) continue;
+        const uint32_t lr = act[i];
+        HTree tr = qtree(lr, (int)port);
+        uint32_t x = head[lr];
+        while (x != kTpNil) {
+          with_g(x, [&](TGe& gx) {
+            if ((gx.mask >> port) & 1u) {
+              const uint64_t qd = tr.delay(time_to_cycles(gx.t, P.f), nflits(P, gx.len), D.err);
+              if (qd) atomicMax((unsigned long long*)&gx.q, (unsigned long long)qd);
+            }
+            x = gx.next;
+          });
+        }
+      }
+      __syncthreads();
+    }
+    lap(4);
+    // per router, in order: counters, deliveries, forwarded copies
+    {
+      unsigned long long fm = ~0ull, rm = ~0ull;
+      for (uint32_t i = tid; i < na; i += nt) {
+        const uint32_t lr = act[i], c = r0 + lr, cx = c % P.w, cy = c / P.w;
+        uint64_t* L = lctr + (size_t)lr * kNetCtrTree;
+        uint32_t x = head[lr];
+        while (x != kTpNil) {
+          TGe gx;
+          with_g(x, [&](TGe& y) { gx = y; });
+          x = gx.next;
+          const uint64_t nf = nflits(P, gx.len), qd = gx.q;
+          const int np = __builtin_popcount(gx.mask);
+          if (P.qm) { L[0] += qd * (uint64_t)np; L[1] += (uint64_t)np; }
+          L[2] += nf; L[3] += 1; L[4 + min(np, 5) - 1] += nf; L[9] += nf * (uint64_t)np;
+          const uint32_t sx = gx.src % P.w, sy = gx.src / P.w;
+          const uint64_t cps = lat_to_ps(qd, P.f);
+          const uint64_t hops = (uint64_t)((cx > sx ? cx - sx : sx - cx) + (cy > sy ? cy - sy : sy - cy)) + 1;
+          const uint64_t t = gx.t + zps + cps, zl = hops * zps, ct = t - gx.t0 - zl;
+          for (int port = P_LEFT; port < NPORTS; ++port) {
+            if (!((gx.mask >> port) & 1u)) continue;
+            const uint32_t nc = tree_next(P, c, port), og = nc / R;
+            const TEv f{t, gx.k, nc};
+            if (og == g) { with_e(pb ^ 1u, atomicAdd(&s_n1, 1u), [&](TEv& y) { y = f; }); fm = min(fm, (unsigned long long)t); }
+            else {
+              const uint32_t slot = atomicAdd(&B.icnt[pout * G + og], 1u);
+              if (slot >= bwg) { atomicOr(D.err, GG_DERR_CAP); continue; }
+              st_ev(B.inbox + ((size_t)pout * G + og) * bwg + slot, f);
+              rm = min(rm, (unsigned long long)t);
+            }
+          }
+          if (gx.mask & (1u << P_SELF)) {
+            const uint64_t ser = lat_to_ps(nf, P.f);   // receive at c (network_model.cc:118-150,253-272)
+            L[10] += 1; L[11] += nf; L[12] += gx.len; L[13] += zl + ser + ct; L[14] += ct;
+            if (gx.dst == GG_BROADCAST) {
+              const uint64_t o = (uint64_t)gx.bidx * P.tiles + c;
+              IO.bout.arrival_ps_dev[o] = t + ser; IO.bout.zero_load_ps_dev[o] = zl + ser; IO.bout.contention_ps_dev[o] = ct;
+            } else {
+              IO.out.arrival_ps_dev[gx.k] = t + ser; IO.out.zero_load_ps_dev[gx.k] = zl + ser; IO.out.contention_ps_dev[gx.k] = ct;
+            }
+          }
+        }
+        head[lr] = kTpNil;
+      }
+      fm = tp_wave_min64(fm);
+      if (ln == 0 && fm != ~0ull) atomicMin(&s_pmin, fm);
+      rm = tp_wave_min64(rm);
+      if (ln == 0 && rm != ~0ull) atomicMin(&B.gmin[(w + 1) % 3], rm);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      if (s_pmin != ~0ull) atomicMin(&B.gmin[(w + 1) % 3], s_pmin);
+      s_n0 = s_n1;
+    }
+    lap(5);
+  }
+  if (prof && g == 0 && tid == 0) {
+    for (int i = 0; i < 6; ++i) prof[i] += pc[i];
+    prof[6] += pw;
+  }
+  if (prof && tid == 0) {                        // the busiest block: most work, least barrier wait
+    atomicMax(&prof[8], pc[2] + pc[3] + pc[4] + pc[5]);
+    atomicMin(&prof[9], pc[1]);
+    if (g == 0) { prof[10] += pbw; prof[11] += pbp; prof[12] += pbn; }
+  }
+  // the queue images and the counters back to HBM
+  {
+    const uint32_t per_q = qb / 16;
+    for (uint32_t i = tid; i < nr * 6 * per_q; i += nt) {
+      const uint32_t qi = i / per_q, wd = i % per_q, lr = qi / 6, port = qi % 6;
+      const uint64_t gq = (uint64_t)(r0 + lr) * 6 + port;
+      const uint4 v = reinterpret_cast<const uint4*>(img + (size_t)qi * qb)[wd];
+      if (wd * 16 < sizeof(HQueue)) reinterpret_cast<uint4*>(D.q + gq)[wd] = v;
+      else reinterpret_cast<uint4*>(D.nd + gq * P.max_size)[wd - sizeof(HQueue) / 16] = v;
+    }
+    for (uint32_t lr = tid; lr < nr; lr += nt) {
+      const uint64_t* L = lctr + (size_t)lr * kNetCtrTree;
+      const uint32_t c = r0 + lr;
+      tcadd(D.ctr, c, GG_NC_ROUTER_CONTENTION_CYCLES, L[0]); tcadd(D.ctr, c, GG_NC_ROUTER_PACKETS, L[1]);
+      tcadd(D.ctr, c, GG_NC_BUFFER_WRITES, L[2]); tcadd(D.ctr, c, GG_NC_BUFFER_READS, L[2]);
+      tcadd(D.ctr, c, GG_NC_SWITCH_ALLOC, L[3]); tcadd(D.ctr, c, GG_NC_CROSSBAR, L[4]);
+      tcadd(D.ctr, c, GG_NC_CROSSBAR_MULTI + 0, L[5]); tcadd(D.ctr, c, GG_NC_CROSSBAR_MULTI + 1, L[6]);
+      tcadd(D.ctr, c, GG_NC_CROSSBAR_MULTI + 2, L[7]); tcadd(D.ctr, c, GG_NC_CROSSBAR_MULTI + 3, L[8]);
+      tcadd(D.ctr, c, GG_NC_LINK_TRAVERSALS, L[9]); tcadd(D.ctr, c, GG_NC_PACKETS_RECEIVED, L[10]);
+      tcadd(D.ctr, c, GG_NC_FLITS_RECEIVED, L[11]); tcadd(D.ctr, c, GG_NC_BITS_RECEIVED, L[12]);
+      tcadd(D.ctr, c, GG_NC_TOTAL_LATENCY_PS, L[13]); tcadd(D.ctr, c, GG_NC_TOTAL_CONTENTION_PS, L[14]);
+    }
+  }
+}
+
 struct gg_noc_state {
   NocParams P;
   HQueue* q = nullptr; HNode* nd = nullptr; uint64_t nq = 0;
@@ -1631,6 +2042,7 @@ struct gg_noc_state {
   unsigned long long* prof = nullptr;             // GG_NOC_PROFILE=1: k_chain_sweep phase cycles (diagnostics)
   SK* pscr = nullptr; uint64_t pscr_cap = 0;       // k_chain_pipe: per packet 3 x positions pool / incoming slots
   uint8_t* tp = nullptr; uint64_t tp_bytes = 0;     // k_tree_pool: TpBufs
+  uint8_t* tg = nullptr; uint64_t tg_bytes = 0;     // k_tree_setup / k_tree_grid: TgBufs
   bool pipe = true;                               // GG_NOC_PIPE=0: the position sweep for every chain (A/B)
 };
 
@@ -1660,6 +2072,7 @@ gg_status gg_noc_alloc(gg_ctx* ctx)
   if (getenv("GG_NOC_PROFILE") && atoi(getenv("GG_NOC_PROFILE"))) {
     GG_HIP(hipMalloc((void**)&S->prof, 16 * sizeof(unsigned long long)));
     GG_HIP(hipMemset(S->prof, 0, 16 * sizeof(unsigned long long)));
+    GG_HIP(hipMemset(S->prof + 9, 0xFF, sizeof(unsigned long long)));
   }
   GG_HIP(hipFuncSetAttribute((const void*)k_chain_sweep, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
   GG_HIP(hipFuncSetAttribute((const void*)k_chain_pipe, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
@@ -1667,6 +2080,7 @@ gg_status gg_noc_alloc(gg_ctx* ctx)
   GG_HIP(hipFuncSetAttribute((const void*)k_port_sweep<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPortLds));
   static_assert(kSweepLds <= kStageLdsMax, "the sweep's LDS arrays fit the stage budget");
   GG_HIP(hipFuncSetAttribute((const void*)k_tree_pool, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTpLds));
+  GG_HIP(hipFuncSetAttribute((const void*)k_tree_grid, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTpLds));
   GG_HIP(hipFuncSetAttribute((const void*)k_tree_walk<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)(kTreeLdsEv * sizeof(TEv))));
   GG_HIP(hipMalloc((void**)&S->ctr, sizeof(uint64_t) * c.num_tiles * GG_NUM_NET_COUNTERS));
@@ -1683,7 +2097,7 @@ void gg_noc_free(gg_ctx* ctx)
   gg_noc_state* S = ctx->noc;
   if (!S) return;
   void* ps[] = {S->q, S->nd, S->ctr, S->t, S->zl, S->ct, S->cur, S->keys, S->ids, S->heap,
-                S->counts, S->cursor, S->off, S->theap, S->bidx, S->prof, S->pscr, S->tp};
+                S->counts, S->cursor, S->off, S->theap, S->bidx, S->prof, S->pscr, S->tp, S->tg};
   for (void* p : ps) if (p) hipFree(p);
   delete S;
   ctx->noc = nullptr;
@@ -1775,9 +2189,29 @@ gg_status gg_noc_tree(gg_ctx* ctx, const gg_packets* pk, const gg_packet_out* ou
   const uint32_t tp_gcap = P.tiles <= 2048 ? 1024u : 512u;
   const size_t tp_base = tp_lds_bytes(P.tiles, tp_gcap, 0);
   const uint32_t tp_ecap = tp_base < kTpLds ? (uint32_t)((kTpLds - tp_base) / (2 * sizeof(TEv))) : 0u;
-  const bool pool = win && tp_ecap >= 64;
-  const bool lds = !pool && hcap <= kTreeLdsEv;
-  const uint64_t need = pool || lds ? 0 : hcap;
+  // the grid form where its LDS, its scratch and a co-resident grid fit
+  // (GG_NOC_TREE_POOL=1: the one-workgroup form, A/B)
+  const uint32_t tg_qb = (uint32_t)(sizeof(HQueue) + (size_t)P.max_size * sizeof(HNode));
+  const uint32_t tg_G0 = std::min<uint32_t>((uint32_t)ctx->num_cus, P.tiles);
+  const uint32_t tg_R = (P.tiles + tg_G0 - 1) / tg_G0, tg_G = (P.tiles + tg_R - 1) / tg_R;
+  const uint32_t tg_gcap = 256;
+  const size_t tg_base = tg_lds_bytes(tg_R, tg_qb, 0, tg_gcap);
+  const uint32_t tg_ecap = tg_base < kTpLds ? (uint32_t)std::min<size_t>(2048, (kTpLds - tg_base) / (2 * sizeof(TEv))) : 0u;
+  const uint64_t tg_bwg = (n - nb) + nb * tg_R + 64;
+  const uint64_t tg_need = 4 * n * sizeof(TEv) + 4ull * (P.tiles + 1) + (uint64_t)tg_G * tg_bwg * (4 * sizeof(TEv) + sizeof(TGe)) +
+                           8 * (uint64_t)tg_G + 128ull * (kTgBarShards + kTgBarFlags) + 256;
+  bool gridf = win && tg_ecap >= 64 && tg_need <= (2ull << 30) &&
+               !(getenv("GG_NOC_TREE_POOL") && atoi(getenv("GG_NOC_TREE_POOL")));
+  const size_t tg_lds = tg_lds_bytes(tg_R, tg_qb, tg_ecap, tg_gcap);
+  if (gridf) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_tree_grid, kTgThreads, tg_lds) != hipSuccess ||
+        (uint64_t)per_cu * (uint64_t)ctx->num_cus < tg_G)
+      gridf = false;
+  }
+  const bool pool = win && !gridf && tp_ecap >= 64;
+  const bool lds = !gridf && !pool && hcap <= kTreeLdsEv;
+  const uint64_t need = gridf || pool || lds ? 0 : hcap;
   if (need > S->tcap) {
     if (S->theap) hipFree(S->theap);
     GG_HIP(hipMalloc((void**)&S->theap, sizeof(TEv) * need));
@@ -1787,6 +2221,29 @@ gg_status gg_noc_tree(gg_ctx* ctx, const gg_packets* pk, const gg_packet_out* ou
     if (S->bidx) hipFree(S->bidx);
     GG_HIP(hipMalloc((void**)&S->bidx, 4 * n));
     S->bcap = n;
+  }
+  TgBufs GB{};
+  if (gridf) {
+    if (tg_need > S->tg_bytes) {
+      if (S->tg) hipFree(S->tg);
+      GG_HIP(hipMalloc((void**)&S->tg, tg_need));
+      S->tg_bytes = tg_need;
+    }
+    uint8_t* b = S->tg;
+    auto take = [&](uint64_t bytes) { uint8_t* r = b; b += (bytes + 15) & ~15ull; return r; };
+    GB.pk = reinterpret_cast<TEv*>(take(n * sizeof(TEv)));
+    GB.run = reinterpret_cast<TEv*>(take(n * sizeof(TEv)));
+    GB.spill = reinterpret_cast<TEv*>(take(2ull * tg_G * tg_bwg * sizeof(TEv)));
+    GB.inbox = reinterpret_cast<TEv*>(take(2ull * tg_G * tg_bwg * sizeof(TEv)));
+    GB.gh = reinterpret_cast<TGe*>(take((uint64_t)tg_G * tg_bwg * sizeof(TGe)));
+    GB.off = reinterpret_cast<uint32_t*>(take(4ull * (P.tiles + 1)));
+    GB.icnt = reinterpret_cast<uint32_t*>(take(8ull * tg_G));
+    GB.gmin = reinterpret_cast<unsigned long long*>(take(3 * 8));
+    GB.flag = reinterpret_cast<uint32_t*>(take(4));
+    GB.bar = reinterpret_cast<uint32_t*>(take(128ull * (kTgBarShards + kTgBarFlags)));
+    GG_HIP(hipMemsetAsync(GB.icnt, 0, 8ull * tg_G, s));
+    GG_HIP(hipMemsetAsync(GB.bar, 0, 128ull * (kTgBarShards + kTgBarFlags), s));
+    GG_HIP(hipMemsetAsync(GB.gmin, 0xFF, 3 * 8, s));
   }
   TpBufs TB{};
   if (pool) {
@@ -1804,7 +2261,15 @@ gg_status gg_noc_tree(gg_ctx* ctx, const gg_packets* pk, const gg_packet_out* ou
   const gg_packet_out none{nullptr, nullptr, nullptr};
   TreeIO IO{pk->src_dev, pk->dst_dev, pk->length_bits_dev, pk->time_ps_dev, S->bidx, *out, nb ? *bout : none};
   gg_timer_begin(ctx, "noc_tree", s);
-  if (pool)
+  if (gridf) {
+    hipLaunchKernelGGL(k_tree_setup, dim3(1), dim3(1024), 4 * P.tiles, s, D, IO, n, nb, GB, hcap);
+    GG_HIP(hipGetLastError());
+    uint32_t R = tg_R, qb = tg_qb, ec = tg_ecap, gc = tg_gcap;
+    uint64_t bwg = tg_bwg;
+    unsigned long long* pr = S->prof;
+    void* args[] = {(void*)&D, (void*)&IO, (void*)&GB, (void*)&R, (void*)&qb, (void*)&bwg, (void*)&ec, (void*)&gc, (void*)&pr};
+    GG_HIP(hipLaunchCooperativeKernel((const void*)k_tree_grid, dim3(tg_G), dim3(kTgThreads), args, (unsigned)tg_lds, s));
+  } else if (pool)
     hipLaunchKernelGGL(k_tree_pool, dim3(1), dim3(kTpThreads), tp_lds_bytes(P.tiles, tp_gcap, tp_ecap), s, D, IO, n, nb,
                        TB, hcap, tp_gcap, tp_ecap, S->prof);
   else if (lds)
@@ -1813,6 +2278,17 @@ gg_status gg_noc_tree(gg_ctx* ctx, const gg_packets* pk, const gg_packet_out* ou
     hipLaunchKernelGGL(k_tree_walk<false>, dim3(1), dim3(64), 0, s, D, IO, n, nb, S->theap, hcap);
   GG_HIP(hipGetLastError());
   gg_timer_end(ctx, "noc_tree", s);
+  if (S->prof && gridf) {
+    unsigned long long h[16];
+    GG_HIP(hipMemcpyAsync(h, S->prof, sizeof(h), hipMemcpyDeviceToHost, s));
+    GG_HIP(hipStreamSynchronize(s));
+    fprintf(stderr, "[gg_noc tree] k_tree_grid %u blocks x %u routers, ecap %u: windows %llu | block 0 cycles: setup+injection "
+            "%llu barrier %llu inbox+due %llu router sort %llu port tasks %llu forward %llu | busiest block: work %llu, "
+            "least barrier wait %llu | block 0 barrier: store wait %llu poll %llu (%llu polls)\n", tg_G, tg_R, tg_ecap, h[6], h[0],
+            h[1], h[2], h[3], h[4], h[5], h[8], h[9], h[10], h[11], h[12]);
+    GG_HIP(hipMemsetAsync(S->prof, 0, sizeof(h), s));
+    GG_HIP(hipMemsetAsync(S->prof + 9, 0xFF, 8, s));
+  }
   if (S->prof && pool) {
     unsigned long long h[16];
     GG_HIP(hipMemcpyAsync(h, S->prof, sizeof(h), hipMemcpyDeviceToHost, s));

@@ -293,3 +293,24 @@ def test_host_mirror_unrolls_broadcast_without_tree(tmp_path):
         if sys_after[k]:
             exp += ["%d %d 0 0" % (c, t[k]) for c in (T, T + 1)]
     assert out[:len(exp)] == exp
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,n,frac", [(64, 3000, 0.05), (256, 3000, 0.03), (1024, 4000, 0.01)])
+def test_one_workgroup_window_loop_matches_oracle_on_gpu(T, n, frac, monkeypatch):
+    """The one-workgroup windowed form (GG_NOC_TREE_POOL=1, k_tree_pool; the
+    default where the grid form's LDS does not fit, e.g. 4096 tiles) against
+    the oracle: the same deliveries and counters as the grid form."""
+    from gpu_util import torch_dev
+    torch = torch_dev()
+    monkeypatch.setenv("GG_NOC_TREE_POOL", "1")
+    cfg = _cfg(T)
+    src, dst, bits, t = mixed_packets(T, n, 5 * T + n, 300000, bcast_frac=frac)
+    be, got, bgot = run_tree(torch, cfg, src, dst, bits, t)
+    on, ref, bref = oracle_tree(cfg, src, dst, bits, t)
+    uni = dst != C.BROADCAST
+    for g, r in zip(got, ref):
+        np.testing.assert_array_equal(g[uni], r[uni])
+    for g, r in zip(bgot, bref):
+        np.testing.assert_array_equal(g, r)
+    np.testing.assert_array_equal(be.noc_counters(), on.counters())
