@@ -520,9 +520,9 @@ def noc_tree_bench(args, dev, T):
     deliveries = (n - nb) + nb * T
     r = {"packets": n, "broadcasts": nb, "deliveries": deliveries, "value": deliveries / dt,
          "unit": "deliveries/s", "seconds": dt,
-         "note": "k_tree_pool: conservative time windows of one router + link delay (a broadcast's shared port "
-                 "delay couples the X and Y chains, so the unicast stage pipeline does not apply), one workgroup; "
-                 "per window the due events in LDS, one task per (router, output port) (DESIGN.md section 4b)"}
+         "note": "k_tree_grid: conservative time windows of one router + link delay (a broadcast's shared port "
+                 "delay couples the X and Y chains, so the unicast stage pipeline does not apply), one block per CU "
+                 "owning its routers' queues in LDS, one grid barrier per window (DESIGN.md section 4b)"}
     if not args.no_verify:
         on = po.OracleNoc(cfg)
         c0 = time.perf_counter()

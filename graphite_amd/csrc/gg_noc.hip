@@ -1697,10 +1697,15 @@ __global__ __launch_bounds__(1024) void k_tree_setup(NocDev D, TreeIO IO, uint64
 
 // LDS bytes of k_tree_grid: R routers' six queue images, run heads, two pool
 // buffers of ecap events, gcap due records, per-router lists and counters
+constexpr uint32_t kTgStage = 512;                   // staged copies for other blocks per window
+__host__ __device__ inline size_t tg_stage_off(uint32_t R, uint32_t qb, uint32_t ecap, uint32_t gcap)
+{
+  return ((size_t)R * 6 * qb + 8ull * R + 8ull * R * kNetCtrTree + 2ull * ecap * sizeof(TEv) + (size_t)gcap * sizeof(TGe) +
+          20ull * R + 15) & ~(size_t)15;
+}
 __host__ __device__ inline size_t tg_lds_bytes(uint32_t R, uint32_t qb, uint32_t ecap, uint32_t gcap)
 {
-  return (size_t)R * 6 * qb + 8ull * R + 8ull * R * kNetCtrTree + 2ull * ecap * sizeof(TEv) + (size_t)gcap * sizeof(TGe) +
-         20ull * R;
+  return tg_stage_off(R, qb, ecap, gcap) + (size_t)kTgStage * (sizeof(TEv) + 8);
 }
 
 __global__ __launch_bounds__(kTgThreads) void k_tree_grid(NocDev D, TreeIO IO, TgBufs B, uint32_t R, uint32_t qb,
@@ -1713,7 +1718,7 @@ __global__ __launch_bounds__(kTgThreads) void k_tree_grid(NocDev D, TreeIO IO, T
   if (*B.flag) return;                                   // rejected in setup: every block leaves before a barrier
   extern __shared__ __align__(16) uint8_t tg_lds[];
   __shared__ unsigned long long s_pmin;
-  __shared__ uint32_t s_n0, s_n1, s_nd, s_na;
+  __shared__ uint32_t s_n0, s_n1, s_nd, s_na, s_ns;
   const NocParams& P = D.P;
   const uint32_t T = P.tiles, g = blockIdx.x, G = gridDim.x, tid = threadIdx.x, nt = blockDim.x, ln = tid & 63;
   const uint32_t r0 = g * R, nr = r0 < T ? min(R, T - r0) : 0u;
@@ -1728,6 +1733,9 @@ __global__ __launch_bounds__(kTgThreads) void k_tree_grid(NocDev D, TreeIO IO, T
   uint32_t* head = end + R;                                                     // [R] due list per local router
   uint32_t* act = head + R;                                                     // [R] local routers with due events
   uint32_t* um = act + R;                                                       // [R] their ports
+  TEv* stg = reinterpret_cast<TEv*>(tg_lds + tg_stage_off(R, qb, ecap, gcap));     // [kTgStage] copies for other blocks
+  uint32_t* stg_og = reinterpret_cast<uint32_t*>(stg + kTgStage);               // [kTgStage] their block
+  uint32_t* stg_base = stg_og + kTgStage;                                       // [kTgStage] slot of a block's first copy
   TEv* const sp[2] = {B.spill + (size_t)g * bwg, B.spill + ((size_t)G + g) * bwg};
   TGe* const gh = B.gh + (size_t)g * bwg;
   auto with_g = [&](uint32_t i, auto f) { if (i < gcap) f(Gl[i]); else f(gh[i - gcap]); };
@@ -1853,7 +1861,7 @@ __global__ __launch_bounds__(kTgThreads) void k_tree_grid(NocDev D, TreeIO IO, T
     __syncthreads();
     if (tid == 0) {
       __hip_atomic_store(&B.icnt[pin * G + g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_n0 = n0 + nin; s_n1 = 0; s_nd = 0; s_na = 0; s_pmin = ~0ull;
+      s_n0 = n0 + nin; s_n1 = 0; s_nd = 0; s_na = 0; s_ns = 0; s_pmin = ~0ull;
     }
     __syncthreads();
     const uint32_t np0 = s_n0;
@@ -1962,10 +1970,12 @@ __global__ __launch_bounds__(kTgThreads) void k_tree_grid(NocDev D, TreeIO IO, T
             const TEv f{t, gx.k, nc};
             if (og == g) { with_e(pb ^ 1u, atomicAdd(&s_n1, 1u), [&](TEv& y) { y = f; }); fm = min(fm, (unsigned long long)t); }
             else {
-              const uint32_t slot = atomicAdd(&B.icnt[pout * G + og], 1u);
+              rm = min(rm, (unsigned long long)t);
+              const uint32_t j = atomicAdd(&s_ns, 1u);
+              if (j < kTgStage) { stg[j] = f; stg_og[j] = og; continue; }
+              const uint32_t slot = atomicAdd(&B.icnt[pout * G + og], 1u);   // staging full: one by one
               if (slot >= bwg) { atomicOr(D.err, GG_DERR_CAP); continue; }
               st_ev(B.inbox + ((size_t)pout * G + og) * bwg + slot, f);
-              rm = min(rm, (unsigned long long)t);
             }
           }
           if (gx.mask & (1u << P_SELF)) {
@@ -1985,6 +1995,28 @@ __global__ __launch_bounds__(kTgThreads) void k_tree_grid(NocDev D, TreeIO IO, T
       if (ln == 0 && fm != ~0ull) atomicMin(&s_pmin, fm);
       rm = tp_wave_min64(rm);
       if (ln == 0 && rm != ~0ull) atomicMin(&B.gmin[(w + 1) % 3], rm);
+    }
+    __syncthreads();
+    // the staged copies: one slot reservation per destination block (its
+    // first copy's thread adds the block's count), then every copy stored
+    {
+      const uint32_t ns = min(s_ns, kTgStage);
+      for (uint32_t j = tid; j < ns; j += nt) {
+        const uint32_t og = stg_og[j];
+        bool first = true;
+        uint32_t tot = 0;
+        for (uint32_t k = 0; k < ns; ++k) { const bool same = stg_og[k] == og; tot += same; first = first && !(same && k < j); }
+        if (first) stg_base[j] = atomicAdd(&B.icnt[pout * G + og], tot);
+      }
+      __syncthreads();
+      for (uint32_t j = tid; j < ns; j += nt) {
+        const uint32_t og = stg_og[j];
+        uint32_t lead = j, rank = 0;
+        for (uint32_t k = 0; k < j; ++k) if (stg_og[k] == og) { ++rank; lead = min(lead, k); }
+        const uint32_t slot = stg_base[lead] + rank;
+        if (slot >= bwg) { atomicOr(D.err, GG_DERR_CAP); continue; }
+        st_ev(B.inbox + ((size_t)pout * G + og) * bwg + slot, stg[j]);
+      }
     }
     __syncthreads();
     if (tid == 0) {
