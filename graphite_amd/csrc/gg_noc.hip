@@ -2025,14 +2025,14 @@ __global__ __launch_bounds__(kTgThreads) void k_tree_grid(NocDev D, TreeIO IO, T
     }
     lap(5);
   }
-  if (prof && g == 0 && tid == 0) {
-    for (int i = 0; i < 6; ++i) prof[i] += pc[i];
-    prof[6] += pw;
+  if (prof && g == 0 && tid == 0) {               // slots 16..: the chain sweep uses 0..15
+    for (int i = 0; i < 6; ++i) prof[16 + i] += pc[i];
+    prof[22] += pw;
   }
   if (prof && tid == 0) {                        // the busiest block: most work, least barrier wait
-    atomicMax(&prof[8], pc[2] + pc[3] + pc[4] + pc[5]);
-    atomicMin(&prof[9], pc[1]);
-    if (g == 0) { prof[10] += pbw; prof[11] += pbp; prof[12] += pbn; }
+    atomicMax(&prof[24], pc[2] + pc[3] + pc[4] + pc[5]);
+    atomicMin(&prof[25], pc[1]);
+    if (g == 0) { prof[26] += pbw; prof[27] += pbp; prof[28] += pbn; }
   }
   // the queue images and the counters back to HBM
   {
@@ -2102,9 +2102,9 @@ gg_status gg_noc_alloc(gg_ctx* ctx)
   S->staged = !(getenv("GG_NOC_STAGED") && atoi(getenv("GG_NOC_STAGED")) == 0);
   S->pipe = !(getenv("GG_NOC_PIPE") && atoi(getenv("GG_NOC_PIPE")) == 0);
   if (getenv("GG_NOC_PROFILE") && atoi(getenv("GG_NOC_PROFILE"))) {
-    GG_HIP(hipMalloc((void**)&S->prof, 16 * sizeof(unsigned long long)));
-    GG_HIP(hipMemset(S->prof, 0, 16 * sizeof(unsigned long long)));
-    GG_HIP(hipMemset(S->prof + 9, 0xFF, sizeof(unsigned long long)));
+    GG_HIP(hipMalloc((void**)&S->prof, 32 * sizeof(unsigned long long)));
+    GG_HIP(hipMemset(S->prof, 0, 32 * sizeof(unsigned long long)));
+    GG_HIP(hipMemset(S->prof + 25, 0xFF, sizeof(unsigned long long)));
   }
   GG_HIP(hipFuncSetAttribute((const void*)k_chain_sweep, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
   GG_HIP(hipFuncSetAttribute((const void*)k_chain_pipe, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLdsMax));
@@ -2312,14 +2312,14 @@ gg_status gg_noc_tree(gg_ctx* ctx, const gg_packets* pk, const gg_packet_out* ou
   gg_timer_end(ctx, "noc_tree", s);
   if (S->prof && gridf) {
     unsigned long long h[16];
-    GG_HIP(hipMemcpyAsync(h, S->prof, sizeof(h), hipMemcpyDeviceToHost, s));
+    GG_HIP(hipMemcpyAsync(h, S->prof + 16, sizeof(h), hipMemcpyDeviceToHost, s));
     GG_HIP(hipStreamSynchronize(s));
     fprintf(stderr, "[gg_noc tree] k_tree_grid %u blocks x %u routers, ecap %u: windows %llu | block 0 cycles: setup+injection "
             "%llu barrier %llu inbox+due %llu router sort %llu port tasks %llu forward %llu | busiest block: work %llu, "
             "least barrier wait %llu | block 0 barrier: store wait %llu poll %llu (%llu polls)\n", tg_G, tg_R, tg_ecap, h[6], h[0],
             h[1], h[2], h[3], h[4], h[5], h[8], h[9], h[10], h[11], h[12]);
-    GG_HIP(hipMemsetAsync(S->prof, 0, sizeof(h), s));
-    GG_HIP(hipMemsetAsync(S->prof + 9, 0xFF, 8, s));
+    GG_HIP(hipMemsetAsync(S->prof + 16, 0, sizeof(h), s));
+    GG_HIP(hipMemsetAsync(S->prof + 25, 0xFF, 8, s));
   }
   if (S->prof && pool) {
     unsigned long long h[16];
