@@ -52,6 +52,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 ALGO_BYTES_PER_ACCESS = 16     # Mode P: 8 B addr + 4 B meta in, 4 B result out
 COH_BYTES_PER_ACCESS = 16      # Mode C: 8 B addr + 4 B meta in, 4 B result out
+CORE_BYTES_PER_RECORD = 12     # core model: 4 B meta + 8 B access word in (per-tile sums out)
 # Algorithmic bytes per access of each Mode P kernel
 KERNEL_BYTES = {
     "cache_stream": 16,    # single pass (default): read addr (8) + meta (4), write result (4); state < 1%
@@ -131,7 +132,8 @@ def parse():
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--no-kernel-profile", action="store_true",
                    help="skip the extra instrumented run (for an external rocprofv3 trace of the timed runs alone)")
-    p.add_argument("--sections", default="coherent_long,exchange,hop_counter,stress,fft,private,private_16way,noc",
+    p.add_argument("--sections",
+                   default="coherent_long,exchange,hop_counter,stress,fft,private,private_16way,noc,core_model",
                    help="extra sections at N = 1 (comma list; '' = none)")
     p.add_argument("--hc-per-tile", type=int, default=1024, help="hop_counter section: accesses per tile")
     p.add_argument("--private-per-tile", type=int, default=1 << 20)
@@ -142,6 +144,8 @@ def parse():
     p.add_argument("--private16-per-tile", type=int, default=1 << 18)
     p.add_argument("--noc-packets", type=int, default=1 << 18)
     p.add_argument("--noc-tiles", type=int, default=1024)
+    p.add_argument("--core-tiles", type=int, default=1024, help="core_model section: tiles of the synthetic trace")
+    p.add_argument("--core-per-tile", type=int, default=1 << 18, help="core_model section: records per tile")
     p.add_argument("--fft-m", type=int, default=14,
                    help="configs[0] section: captured FFT of 2^m points on 16 tiles (configs[0] is m=20)")
     return p.parse_args()
@@ -629,6 +633,82 @@ def private16_section(args, dev):
     return res
 
 
+def core_model_section(args, dev):
+    """§8f-4 core timing: gg_core_model_run (the simple core model over a
+    coherent run's access words, a segmented reduction streamed from HBM at
+    12 B per record: 4-B meta + 8-B access word).  (1) parity: a 64-tile
+    hotspot coherent run, its core statistics bit-exact against the oracle and
+    its completion times equal to the engine's clocks; (2) throughput: a
+    synthetic trace of args.core_tiles x args.core_per_tile records (CONT runs
+    included), HIP-event timed launch, 8 tiles checked against the oracle,
+    which is the 1-thread CPU baseline on the same 8 tiles."""
+    import torch
+    from graphite_amd import config as C
+    from graphite_amd import backend as B
+    from oracle import pyoracle as po
+    res = {}
+    cfg = C.default_config(64, num_shards=8, net_model=C.NET_EMESH_HOP_BY_HOP)
+    a, m, o = po.gen_trace(64, 200, hot_lines=32)
+    be = B.Backend(cfg)
+    am = torch.from_numpy(m.view(np.int32)).to(dev)
+    out = torch.zeros(len(a), dtype=torch.int64, device=dev)
+    be.coherent_run(torch.from_numpy(a.view(np.int64)).to(dev), am, o, out)
+    be.core_model_run(am, o, out)
+    core = be.core_stats()
+    clk = be.coherent_stats()[0][:, C.TILE_STATS.index("clock_ps")]
+    parity = bool(np.array_equal(core, po.core_model(m, out.cpu().numpy().view(np.uint64), o, cfg.frequency_ghz)) and
+                  np.array_equal(core[:, C.CORE_STATS.index("time_ps")], clk))
+    be.close()
+    T, N = args.core_tiles, args.core_per_tile
+    n = T * N
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    gap = torch.randint(0, 64, (n,), device=dev, dtype=torch.int32, generator=g)
+    wr = torch.randint(0, 2, (n,), device=dev, dtype=torch.int32, generator=g)
+    cont = torch.rand(n, device=dev, generator=g) < 0.25
+    cont.view(T, N)[:, 0] = False
+    meta = torch.where(cont, torch.full_like(gap, -0x7FFFFFFF), (gap << 1) | wr)   # CONT | WRITE = 0x80000001
+    acc = torch.randint(0, 1 << 40, (n,), device=dev, dtype=torch.int64, generator=g)
+    del gap, wr, cont
+    offs = np.arange(T + 1, dtype=np.uint64) * np.uint64(N)
+    be = B.Backend(C.default_config(T))
+    be.set_timing(True)
+    stream = torch.cuda.current_stream(dev)
+    times = []
+    for it in range(3):
+        torch.cuda.synchronize()
+        be.core_model_run(meta, offs, acc, stream)
+        torch.cuda.synchronize()
+        times.append(be.kernel_time_ms("core_model"))
+    kms = min(times[1:])
+    gbs = n * CORE_BYTES_PER_RECORD / (kms / 1e3) / 1e9
+    core = be.core_stats()
+    sample = list(range(0, T, max(1, T // 8)))[:8]
+    ok, cdt = True, 0.0
+    for t in sample:
+        mm = meta[t * N:(t + 1) * N].cpu().numpy().view(np.uint32)
+        aa = acc[t * N:(t + 1) * N].cpu().numpy().view(np.uint64)
+        c0 = time.perf_counter()
+        ref = po.core_model(mm, aa, np.array([0, N], np.uint64))
+        cdt += time.perf_counter() - c0
+        ok = ok and bool(np.array_equal(core[t], ref[0]))
+    res = {"workload": "gg_core_model_run: synthetic %d tiles x %d records (25%% CONT line records), plus the "
+                       "parity run (64-tile hotspot coherent run, hop-by-hop, 8 shards)" % (T, N),
+           "value": n / (kms / 1e3), "unit": "records/s", "kernel_ms": kms,
+           "roofline": {"bound": "hbm", "kernel": "k_core_model", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": gbs / HBM_PEAK_GBS, "bytes_per_record": CORE_BYTES_PER_RECORD},
+           "bit_exact_checked": bool(ok and parity), "parity_run_exact": parity,
+           "cpu_baseline": {"value": len(sample) * N / cdt, "unit": "records/s", "cores": 1, "kind": "port",
+                            "sample": "%d tiles x %d records, oracle_core_model -O3, 1 thread, %.2f s"
+                                      % (len(sample), N, cdt)}}
+    if not res["bit_exact_checked"]:
+        print("bench.py: CORE MODEL BIT-EXACT CHECK FAILED", file=sys.stderr)
+    be.close()
+    del meta, acc
+    torch.cuda.empty_cache()
+    return res
+
+
 def cpu_baseline(tiles, per_tile, threads):
     """Oracle (oracle/gg_oracle.c, -O3) on a bounded sample: `tiles` tile
     replays (fresh cache state each) cycling over 16 pre-generated tiles of
@@ -838,6 +918,8 @@ def main():
                 r = stress_section(args, dev)
             elif name == "private_16way" and args.stress_tiles:
                 r = private16_section(args, dev)
+            elif name == "core_model" and args.core_per_tile:
+                r = core_model_section(args, dev)
             else:
                 continue
         except Exception as e:            # a section failing must not hide the headline

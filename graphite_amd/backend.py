@@ -10,7 +10,7 @@ import os
 
 import numpy as np
 
-from .config import (GGConfig, NUM_CACHE_COUNTERS, NUM_NET_COUNTERS, NUM_TILE_STATS, NUM_RUN_INFO,
+from .config import (GGConfig, NUM_CACHE_COUNTERS, NUM_NET_COUNTERS, NUM_TILE_STATS, NUM_RUN_INFO, NUM_CORE_STATS,
                      CMSG_DTYPE)
 
 CMSG_BYTES = CMSG_DTYPE.itemsize
@@ -58,7 +58,7 @@ EXPORTS = ["gg_abi_version", "gg_last_error", "gg_config_default", "gg_create", 
            "gg_coherent_begin", "gg_coherent_quantum", "gg_coherent_export", "gg_coherent_import",
            "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace", "gg_shard_map",
            "gg_kernel_stats", "gg_round_exchange", "gg_coherent_run_ranks", "gg_gen_stress_trace",
-           "gg_split_accesses", "gg_combine_accesses", "gg_dump_summary"]
+           "gg_split_accesses", "gg_combine_accesses", "gg_dump_summary", "gg_core_model_run", "gg_core_get_stats"]
 
 
 class _CStatus(ctypes.Structure):
@@ -116,10 +116,12 @@ def load():
     L.gg_split_accesses.argtypes = [vp, vp, vp, vp, u32, u32, vp, vp, vp, u64, ctypes.POINTER(u64), vp, vp]
     L.gg_combine_accesses.argtypes = [vp, vp, u64, vp, vp, vp]
     L.gg_dump_summary.argtypes = [vp, i32, ctypes.c_char_p, u64, ctypes.POINTER(u64)]
+    L.gg_core_model_run.argtypes = [vp, ctypes.POINTER(_Trace), vp, vp]
+    L.gg_core_get_stats.argtypes = [vp, vp]
     for name in ["gg_kernel_stats", "gg_shard_map", "gg_coherent_begin", "gg_coherent_quantum", "gg_coherent_export",
                  "gg_coherent_import", "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace",
                  "gg_round_exchange", "gg_coherent_run_ranks", "gg_gen_stress_trace", "gg_split_accesses",
-                 "gg_combine_accesses", "gg_dump_summary"]:
+                 "gg_combine_accesses", "gg_dump_summary", "gg_core_model_run", "gg_core_get_stats"]:
         getattr(L, name).restype = i32
     for name in ["gg_reset", "gg_cache_access_batch", "gg_cache_get_counters", "gg_cache_get_line_info",
                  "gg_cache_set_line_info", "gg_cache_access_line", "gg_cache_insert_line",
@@ -335,6 +337,26 @@ class Backend:
         _check(load().gg_coherent_get_stats(self.h, st.ctypes.data_as(ctypes.c_void_p),
                                             cc.ctypes.data_as(ctypes.c_void_p), ri.ctypes.data_as(ctypes.c_void_p)))
         return st.reshape(T, NUM_TILE_STATS), cc.reshape(T, 2, NUM_CACHE_COUNTERS), ri
+
+    def core_model_run(self, meta, tile_offsets, access_out, stream=None):
+        """The simple core model over a coherent run's access words
+        (gg_core_model_run): meta (int32/uint32 device tensor of the trace's
+        meta words), host tile offsets, access_out (int64 device tensor)."""
+        import torch
+        self._offs = np.ascontiguousarray(tile_offsets, np.uint64)
+        if self._offs.size != self.cfg.num_tiles + 1:
+            raise ValueError("tile_offsets needs num_tiles + 1 entries")
+        n = int(self._offs[-1])
+        _need_dev(meta, torch.int32, n)
+        _need_dev(access_out, torch.int64, n)
+        tr = _Trace(None, meta.data_ptr(), self._offs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), n)
+        _check(load().gg_core_model_run(self.h, ctypes.byref(tr), access_out.data_ptr(), _stream(stream)))
+
+    def core_stats(self):
+        T = self.cfg.num_tiles
+        out = np.zeros(T * NUM_CORE_STATS, np.uint64)
+        _check(load().gg_core_get_stats(self.h, out.ctypes.data_as(ctypes.c_void_p)))
+        return out.reshape(T, NUM_CORE_STATS)
 
     def dump_summary(self, table=False):
         """The sim.out text of the context's statistics (gg_dump_summary): one

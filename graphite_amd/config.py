@@ -69,6 +69,10 @@ TILE_STATS = ["clock_ps", "accesses", "l1_hits", "l2_hits", "l2_misses", "latenc
 NUM_TILE_STATS = 32
 RUN_INFO = ["quanta", "steps", "net_msgs", "self_msgs", "boundary_msgs", "final_quantum"]
 NUM_RUN_INFO = 8
+# gg_core_model_run statistics (include/graphite_gpu.h GG_CORE_*)
+CORE_STATS = ["instructions", "time_ps", "memory_stall_ps", "execution_stall_ps", "l1d_read_stall_ps",
+              "l1d_write_stall_ps"]
+NUM_CORE_STATS = 8
 CMSG_DTYPE = None  # filled below (numpy view of gg_cmsg)
 NUM_NET_COUNTERS = len(NET_COUNTERS)
 

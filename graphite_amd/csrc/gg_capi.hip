@@ -224,6 +224,7 @@ void gg_destroy(gg_ctx* ctx)
   gg_cache_state_free(ctx);
   gg_noc_free(ctx);
   gg_coh_free(ctx);
+  gg_core_free(ctx);
   if (ctx->round && ctx->round_free) ctx->round_free(ctx->round);
   if (ctx->err_dev) hipFree(ctx->err_dev);
   for (gg_timer& t : ctx->timers) { hipEventDestroy(t.start); hipEventDestroy(t.stop); }

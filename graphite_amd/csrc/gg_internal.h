@@ -102,6 +102,11 @@ struct gg_ctx {
   // timing
   int timing = 0;                // gg_set_timing: 0 off, 1 sampled coherent launches, 2 every launch
   std::vector<gg_timer> timers;
+  // core timing (gg_core.hip): [tiles][GG_NUM_CORE_STATS] and its task list
+  uint64_t* core_dev = nullptr;
+  void* core_tasks = nullptr;
+  uint64_t core_task_cap = 0;
+  bool core_valid = false;
   // multi-rank round buffers (gg_round.hip), freed by gg_destroy
   void* round = nullptr;
   void (*round_free)(void*) = nullptr;
@@ -134,6 +139,8 @@ gg_status gg_noc_run(gg_ctx* ctx, const gg_packets* pk, const gg_packet_out* out
 gg_status gg_noc_tree(gg_ctx* ctx, const gg_packets* pk, const gg_packet_out* out, const gg_packet_out* bout,
                       uint64_t nb, hipStream_t s);
 gg_status gg_noc_counters(gg_ctx* ctx, uint64_t* out);
+// core timing (gg_core.hip)
+void      gg_core_free(gg_ctx* ctx);
 // coherent path (gg_coherent.hip)
 void      gg_coh_free(gg_ctx* ctx);
 gg_status gg_htree_run(gg_ctx* ctx, uint64_t min_proc, const uint64_t* t, const uint64_t* p, uint64_t n, uint64_t* d);

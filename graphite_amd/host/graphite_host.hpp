@@ -139,6 +139,56 @@ inline void writeCacheSummary(std::ostream& out, const std::string& name, const 
   out << "      Data Array Writes: " << c[GG_CC_DATA_WRITES] << std::endl;
 }
 
+// Time::toNanosec / toCycles (misc/time_types.h:104-114)
+inline uint64_t psToNanosec(uint64_t ps) { return (uint64_t)ceil(((double)ps) / double(1.0e3)); }
+inline uint64_t psToCycles(uint64_t ps, double f) { return (uint64_t)ceil(((double)ps * f) / double(1.0e3)); }
+
+// The core part of a tile's sim.out block for the simple core model over a
+// trace (GG_CORE_* statistics of gg_core_model_run): CoreModel::outputSummary
+// (core_model.cc:90-115) with the average frequency of the thread-exit
+// recomputeAverageFrequency (:183-190), the default one_bit branch predictor's
+// block (branch_predictor.cc:66-71: a memory trace has no branches), then
+// SimpleCoreModel's breakdown (simple_core_model.cc:29-36) and
+// Core::outputSummary's shared-memory block (core.cc:283-310; no L1-I).
+// McPATCoreInterface's parameter and micro-op tables (mcpat_core_interface.cc:
+// 780-1020) are not written: McPAT is not part of this path.
+inline void writeCoreSummary(std::ostream& os, const uint64_t* core, double frequency_ghz)
+{
+  const uint64_t n = core[GG_CORE_INSTRUCTIONS], t = core[GG_CORE_TIME_PS];
+  const uint64_t zero = 0;
+  const double avg_f = ((double)psToCycles(t, frequency_ghz)) / ((double)psToNanosec(t));
+  os << "Core Summary:" << std::endl;
+  os << "    Total Instructions: " << n << std::endl;
+  os << "    Completion Time (in nanoseconds): " << psToNanosec(t) << std::endl;
+  os << "    Average Frequency (in GHz): " << avg_f << std::endl;
+  os << "    Synchronization Stalls: " << zero << std::endl;
+  os << "    Network Recv Stalls: " << zero << std::endl;
+  os << "    Stall Time Breakdown (in nanoseconds): " << std::endl;
+  os << "      Memory: " << psToNanosec(core[GG_CORE_MEMORY_STALL_PS]) << std::endl;
+  os << "      Execution Unit: " << psToNanosec(core[GG_CORE_EXECUTION_STALL_PS]) << std::endl;
+  os << "      Synchronization: " << psToNanosec(0) << std::endl;
+  os << "      Network Recv: " << psToNanosec(0) << std::endl;
+  os << "    Branch Predictor Statistics:" << std::endl
+     << "      Num Correct: " << zero << std::endl
+     << "      Num Incorrect: " << zero << std::endl;
+  os << "    Fence Instructions: " << std::endl;
+  os << "      Explicit LFENCE, SFENCE, MFENCE: " << zero << std::endl;
+  os << "      Implicit MFENCE: " << zero << std::endl;
+  os << "    Detailed Stall Time Breakdown (in nanoseconds): " << std::endl;
+  os << "      L1-I Cache: " << psToNanosec(0) << std::endl;
+  os << "      L1-D Cache: "
+     << psToNanosec(core[GG_CORE_L1D_READ_STALL_PS]) + psToNanosec(core[GG_CORE_L1D_WRITE_STALL_PS]) << std::endl;
+  const uint64_t ni = 0, data_ns = psToNanosec(core[GG_CORE_MEMORY_STALL_PS]), instr_ns = psToNanosec(0);
+  os << "Shared Memory Model Summary: " << std::endl;
+  os << "    Total Memory Accesses: " << ni + n << std::endl;
+  os << "    Average Memory Access Latency (in nanoseconds): " << (1.0 * (instr_ns + data_ns) / (ni + n)) << std::endl;
+  os << "    Total Instruction Memory Accesses: " << ni << std::endl;
+  os << "    Instruction Buffer Hits: " << zero << std::endl;
+  os << "    Average Instruction Memory Access Latency (in nanoseconds): " << 1.0 * instr_ns / ni << std::endl;
+  os << "    Total Data Memory Accesses: " << n << std::endl;
+  os << "    Average Data Memory Access Latency (in nanoseconds): " << 1.0 * data_ns / n << std::endl;
+}
+
 // NetworkModel::outputSummary (network/network_model.cc:274-316) for one tile's
 // GG_NC_* counters, followed for emesh_hop_counter by its event counters
 // (network_model_emesh_hop_counter.cc:160-165,226-236).  Time::toCycles /
@@ -295,15 +345,18 @@ inline void writeMemorySummary(std::ostream& out, const gg_config& c, const uint
   writeDirectorySummary(out, tile_stats, directorySizing(c));
 }
 
-// One tile's summary text in the coherent mode: the memory part, then
+// One tile's summary text in the coherent mode: the core part when the core
+// model has run (gg_core_model_run), the memory part, then
 // Network::outputSummary (network.cc:79-89): the static networks below SYSTEM,
 // User (no traffic in a trace-driven run; emesh_hop_counter, carbon_sim.cfg
 // [network]) then Memory.  Mode P (no tile statistics): the cache summary only,
 // then the networks.
 inline void writeTileSummary(std::ostream& os, const gg_config& cfg, const uint64_t* tile_stats,
-                             const uint64_t* cache_counters, const uint64_t* net_counters)
+                             const uint64_t* cache_counters, const uint64_t* net_counters,
+                             const uint64_t* core_stats = nullptr)
 {
   static const uint64_t zero_net[GG_NUM_NET_COUNTERS] = {0};
+  if (core_stats) writeCoreSummary(os, core_stats, cfg.frequency_ghz);   // Tile::outputSummary (tile.cc:52-69)
   if (tile_stats) writeMemorySummary(os, cfg, tile_stats, cache_counters);
   else {
     os << "Cache Summary:\n";

@@ -502,6 +502,38 @@ gg_status gg_split_accesses(const uint64_t* addr_dev, const uint32_t* size_dev, 
 gg_status gg_combine_accesses(const uint64_t* line_out_dev, const uint64_t* first_dev, uint64_t n,
                               uint64_t* latency_ps_dev, uint32_t* misses_dev, void* stream);
 
+/* Core timing of a trace-driven tile: the simple core model
+ * (SimpleCoreModel::handleInstruction, common/tile/core/models/
+ * simple_core_model.cc:43-96) over a coherent run's per-access results.  Each
+ * access (a record without GG_META_CONT plus the CONT records that follow it)
+ * is one instruction: static cost = its gap cycles (execution-unit stall),
+ * one memory operand, read or write by the access's WRITE bit, whose latency
+ * is the sum of its line latencies (Core::initiateMemoryAccess's final -
+ * initial time, core.cc:239-256).  curr_time advances by cost + latency, which
+ * is the coherent engine's clock rule, so GG_CORE_TIME_PS equals the run's
+ * GG_CT_CLOCK_PS.  No L1-I is modeled (its stall is 0).  The iocoom model is
+ * not offered: it needs register operands a memory trace does not carry and
+ * would move the issue times the engine replays.
+ * Per-tile statistics, [tile][GG_NUM_CORE_STATS]:                            */
+enum {
+  GG_CORE_INSTRUCTIONS = 0,   /* CoreModel::_instruction_count = data memory accesses  */
+  GG_CORE_TIME_PS,            /* _curr_time                                             */
+  GG_CORE_MEMORY_STALL_PS,    /* _total_memory_stall_time = total data access latency  */
+  GG_CORE_EXECUTION_STALL_PS, /* _total_execution_unit_stall_time                      */
+  GG_CORE_L1D_READ_STALL_PS,  /* SimpleCoreModel::_total_l1dcache_read_stall_time      */
+  GG_CORE_L1D_WRITE_STALL_PS, /* _total_l1dcache_write_stall_time                      */
+  GG_NUM_CORE_STATS = 8
+};
+/* Runs the model over the tile-major trace (meta words and tile offsets of
+ * `trace`; addresses are not read) and the per-record access words of the
+ * coherent run (access_out_dev, (latency_ps << 2) | level), from the model's
+ * constructor state; the statistics stay in the context (gg_core_get_stats,
+ * gg_dump_summary's "Core Summary" block).  Asynchronous on stream.         */
+gg_status gg_core_model_run(gg_ctx* ctx, const gg_trace* trace, const uint64_t* access_out_dev, void* stream);
+/* out: num_tiles * GG_NUM_CORE_STATS (host).  Synchronizes.  GG_ERR_STATE if
+ * gg_core_model_run has not run on the context.                              */
+gg_status gg_core_get_stats(gg_ctx* ctx, uint64_t* out);
+
 /* Device time (ms) of the most recent launch of a named kernel
  * ("cache_hist", "cache_scatter", "cache_replay", "cache_unshard",
  * "noc_hop_counter", ...), measured with HIP

@@ -181,6 +181,77 @@ void oracle_combine_accesses(const uint64_t* line_out, const uint64_t* first, ui
 }
 
 /* ======================================================================== */
+/* Core timing: SimpleCoreModel (common/tile/core/models/simple_core_model.cc) */
+/* ======================================================================== */
+typedef struct {
+  uint64_t instruction_count, curr_time;                     /* CoreModel (core_model.cc:31-45) */
+  uint64_t total_memory_stall_time, total_execution_unit_stall_time;
+  uint64_t total_l1icache_stall_time, total_l1dcache_read_stall_time, total_l1dcache_write_stall_time;
+} o_core;
+
+/* DynamicMemoryInfo {read, latency} of one access (core.cc:258-263) */
+typedef struct { int read; uint64_t latency; } o_meminfo;
+
+/* SimpleCoreModel::handleInstruction (simple_core_model.cc:43-96) for an
+ * instruction of static cost `cost` with the memory operands `info` (one per
+ * access in a trace).  No L1-I is modeled: modelICache contributes 0.       */
+static void o_core_handle(o_core* c, uint64_t cost, const o_meminfo* info, int n)
+{
+  c->instruction_count++;                                            /* :50 */
+  uint64_t memory_stall_time = 0, execution_unit_stall_time = 0;
+  const uint64_t icache = 0;                                         /* :62-64 */
+  memory_stall_time += icache;
+  c->total_l1icache_stall_time += icache;
+  for (int i = 0; i < n; ++i) {
+    if (info[i].read) {                                              /* :69-78 */
+      memory_stall_time += info[i].latency;
+      c->total_l1dcache_read_stall_time += info[i].latency;
+    } else {                                                         /* :79-88 */
+      memory_stall_time += info[i].latency;
+      c->total_l1dcache_write_stall_time += info[i].latency;
+    }
+  }
+  execution_unit_stall_time += cost;                                 /* :90 */
+  c->curr_time += memory_stall_time + execution_unit_stall_time;     /* :92 */
+  c->total_memory_stall_time += memory_stall_time;                   /* core_model.cc:260-264 */
+  c->total_execution_unit_stall_time += execution_unit_stall_time;
+}
+
+/* A tile's trace is its instruction stream: each access (a record without
+ * GG_META_CONT and the CONT line records after it) is one instruction with
+ * static cost = gap cycles (Latency(1, f) per cycle, the engine's gap rule)
+ * and one memory operand, read unless the head record is a WRITE, whose
+ * latency is Core::initiateMemoryAccess's final - initial time = the sum of
+ * its line latencies (core.cc:239-256).                                    */
+void oracle_core_model(const uint32_t* meta, const uint64_t* access_out, const uint64_t* tile_offsets,
+                       uint32_t tiles, double frequency_ghz, uint64_t* stats)
+{
+  const uint64_t cyc = lat_to_ps(1, frequency_ghz);
+  for (uint32_t t = 0; t < tiles; ++t) {
+    o_core c;
+    memset(&c, 0, sizeof c);
+    uint64_t r = tile_offsets[t];
+    const uint64_t e = tile_offsets[t + 1];
+    while (r < e) {
+      o_meminfo info;
+      info.read = !(meta[r] & GG_META_WRITE);
+      info.latency = access_out[r] >> 2;
+      const uint64_t cost = (uint64_t)((meta[r] & 0x7FFFFFFFu) >> 1) * cyc;
+      for (++r; r < e && (meta[r] & GG_META_CONT); ++r) info.latency += access_out[r] >> 2;
+      o_core_handle(&c, cost, &info, 1);
+    }
+    uint64_t* o = stats + (size_t)t * GG_NUM_CORE_STATS;
+    memset(o, 0, sizeof(uint64_t) * GG_NUM_CORE_STATS);
+    o[GG_CORE_INSTRUCTIONS] = c.instruction_count;
+    o[GG_CORE_TIME_PS] = c.curr_time;
+    o[GG_CORE_MEMORY_STALL_PS] = c.total_memory_stall_time;
+    o[GG_CORE_EXECUTION_STALL_PS] = c.total_execution_unit_stall_time;
+    o[GG_CORE_L1D_READ_STALL_PS] = c.total_l1dcache_read_stall_time;
+    o[GG_CORE_L1D_WRITE_STALL_PS] = c.total_l1dcache_write_stall_time;
+  }
+}
+
+/* ======================================================================== */
 /* Cache (common/tile/memory_subsystem/cache/)                               */
 /* ======================================================================== */
 #define O_INVALID_TAG (~0ull)                        /* cache_line_info.h:21-22 */

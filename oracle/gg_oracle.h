@@ -125,6 +125,11 @@ uint64_t oracle_split_accesses(const uint64_t* addr, const uint32_t* size, const
                                uint64_t* first, uint64_t* line_addr, uint32_t* line_meta);
 void oracle_combine_accesses(const uint64_t* line_out, const uint64_t* first, uint64_t n,
                              uint64_t* latency_ps, uint32_t* misses);
+/* The simple core model over a coherent run's per-record access words
+ * (SimpleCoreModel::handleInstruction, simple_core_model.cc:43-96); see
+ * gg_oracle.c.  stats: [tiles][GG_NUM_CORE_STATS].                          */
+void oracle_core_model(const uint32_t* meta, const uint64_t* access_out, const uint64_t* tile_offsets,
+                       uint32_t tiles, double frequency_ghz, uint64_t* stats);
 
 #ifdef __cplusplus
 }

@@ -74,6 +74,8 @@ def lib():
         L.oracle_split_accesses.restype = ctypes.c_uint64
         L.oracle_split_accesses.argtypes = [_u64p, _u32p, _u32p, _u64p, ctypes.c_uint32, ctypes.c_uint32, _u64p, vp, vp]
         L.oracle_combine_accesses.argtypes = [_u64p, _u64p, ctypes.c_uint64, _u64p, _u32p]
+        L.oracle_core_model.argtypes = [_u32p, _u64p, _u64p, ctypes.c_uint32, ctypes.c_double, _u64p]
+        L.oracle_core_model.restype = None
         L.oracle_gen_hotspot.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u64p, _u32p]
         L.oracle_gen_stress.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
@@ -401,6 +403,16 @@ def combine_accesses(line_out, first):
     lib().oracle_combine_accesses(np.ascontiguousarray(line_out, np.uint64), np.ascontiguousarray(first, np.uint64),
                                   n, lat, miss)
     return lat[:n], miss[:n]
+
+
+def core_model(meta, access_out, tile_offsets, frequency_ghz=1.0):
+    """[tiles][GG_NUM_CORE_STATS] of the simple core model (oracle_core_model)."""
+    offs = np.ascontiguousarray(tile_offsets, np.uint64)
+    T = len(offs) - 1
+    out = np.zeros(max(T, 1) * 8, np.uint64)
+    lib().oracle_core_model(np.ascontiguousarray(meta, np.uint32), np.ascontiguousarray(access_out, np.uint64), offs,
+                            T, float(frequency_ghz), out)
+    return out[:T * 8].reshape(T, 8)
 
 
 def split_lines(addr, size, line=64):
