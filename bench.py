@@ -146,8 +146,9 @@ def parse():
     p.add_argument("--noc-tiles", type=int, default=1024)
     p.add_argument("--core-tiles", type=int, default=1024, help="core_model section: tiles of the synthetic trace")
     p.add_argument("--core-per-tile", type=int, default=1 << 18, help="core_model section: records per tile")
-    p.add_argument("--fft-m", type=int, default=14,
-                   help="configs[0] section: captured FFT of 2^m points on 16 tiles (configs[0] is m=20)")
+    p.add_argument("--fft-m", type=int, default=20,
+                   help="configs[0] section: the reference's FFT -p16 -m<m> (configs[0]: m=20; the trace build() "
+                        "captures; m=14 is committed)")
     return p.parse_args()
 
 
@@ -392,17 +393,30 @@ def hop_counter_section(args, dev):
 
 
 def fft_section(args, dev):
-    """configs[0]: the SPLASH-2-style FFT (-p16) captured by the source-level
-    front end (graphite_amd.capture), simulated in Mode C (MSI directory +
-    emesh_hop_counter, 16 tiles) on the GPU; bit-exact against the C oracle,
-    whose run is the CPU baseline."""
+    """configs[0]: SPLASH-2 FFT on 16 tiles, simulated in Mode C (MSI directory
+    + emesh_hop_counter) on the GPU; bit-exact against the C oracle, whose run
+    is the CPU baseline.  The trace is the reference's own fft.C (-p16
+    -m<fft_m>) captured by tools/fft_trace when that capture exists
+    (graphite_amd.capture.REAL_FFT_TRACES: -m20 written by build(), -m14
+    committed), else the source-level six-step lookalike (capture_fft)."""
     import torch
     from graphite_amd import config as C
     from graphite_amd import backend as B
     from graphite_amd import capture as cp
     m, p = args.fft_m, 16
-    a, meta, offs, X = cp.capture_fft(m, p)
-    fft_ok = bool(np.abs(X - np.fft.fft(cp.fft_input(m))).max() <= 1e-9 * np.abs(X).max())
+    path = cp.REAL_FFT_TRACES.get(m)
+    if not (path and os.path.exists(path)) and os.path.exists(cp.REAL_FFT_TRACES[14]):
+        m, path = 14, cp.REAL_FFT_TRACES[14]          # the -m20 capture is written by build() only
+    if path and os.path.exists(path):
+        a, meta, offs, bars = cp.load_fft_trace(path)
+        fft_ok, src = None, ("the reference's tests/benchmarks/fft/fft.C -p%d -m%d captured by tools/fft_trace "
+                             "(heap accesses, 1 cycle per access, %d BARRIER calls per thread not modelled)"
+                             % (p, m, len(bars[0])))
+    else:
+        m = min(m, 14)
+        a, meta, offs, X = cp.capture_fft(m, p)
+        fft_ok = bool(np.abs(X - np.fft.fft(cp.fft_input(m))).max() <= 1e-9 * np.abs(X).max())
+        src = "captured six-step FFT lookalike of 2^%d points (graphite_amd/capture)" % m
     cfg = C.default_config(p, net_model=C.NET_EMESH_HOP_COUNTER)
     be = B.Backend(cfg)
     addr = torch.from_numpy(a.view(np.int64)).to(dev)
@@ -414,8 +428,8 @@ def fft_section(args, dev):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     st, cc, ri = be.coherent_stats()
-    res = {"workload": "configs[0]: captured six-step FFT of 2^%d points, %d threads = %d tiles, %d accesses, "
-                       "pr_l1_pr_l2_dram_directory_msi + emesh_hop_counter" % (m, p, p, len(a)),
+    res = {"workload": "configs[0]: %s, %d threads = %d tiles, %d accesses, pr_l1_pr_l2_dram_directory_msi + "
+                       "emesh_hop_counter" % (src, p, p, len(a)),
            "value": len(a) / dt, "unit": "accesses/s", "seconds": dt, "fft_correct": fft_ok,
            "steps": int(ri[C.RUN_INFO.index("steps")]), "simulated_ns": int(st[:, 0].max()) // 1000}
     if not args.no_verify:

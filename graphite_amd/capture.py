@@ -1,5 +1,7 @@
 """Trace capture front end (BASELINE configs[0]): ctypes binding of
-libgg_capture.so (include/graphite_capture.h).
+libgg_capture.so (include/graphite_capture.h), and the loader of the traces
+of the reference's own FFT program captured by tools/fft_trace
+(load_fft_trace, REAL_FFT_TRACES).
 
 capture_fft(m, p) runs the source-instrumented six-step FFT of 2^m points on p
 threads and returns its per-thread traces in the gg_trace layout (addr u64,
@@ -61,6 +63,27 @@ def capture_fft(m, p):
         lib.gg_fft_capture_destroy(h)
     offs = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
     return addr, meta, offs, out[0::2] + 1j * out[1::2]
+
+
+ROOT = os.path.dirname(HERE)
+# the reference's own FFT (tests/benchmarks/fft/fft.C) captured by tools/fft_trace:
+# small committed fixtures, and the configs[0]-size -m20 trace build() writes
+REAL_FFT_TRACES = {10: os.path.join(ROOT, "tests", "golden", "fft_real_p16_m10.npz"),
+                   14: os.path.join(ROOT, "tests", "golden", "fft_real_p16_m14.npz"),
+                   20: os.path.join(ROOT, "tools", "fft_trace", "out", "fft_p16_m20.npz")}
+
+
+def load_fft_trace(path):
+    """A captured SPLASH-2 FFT trace (tools/fft_trace/make_traces.py) ->
+    (addr u64[n], meta u32[n], tile_offsets u64[p+1], barriers: list of u64
+    arrays, the trace positions of each tile's BARRIER calls)."""
+    z = np.load(path, allow_pickle=False)
+    addr = np.cumsum(z["addr_delta"]).astype(np.uint64)
+    meta = np.ascontiguousarray(z["meta"], np.uint32)
+    offs = np.ascontiguousarray(z["tile_offsets"], np.uint64)
+    b, bo = z["barriers"], z["barrier_offsets"]
+    bars = [np.asarray(b[int(bo[t]):int(bo[t + 1])], np.uint64) for t in range(len(bo) - 1)]
+    return addr, meta, offs, bars
 
 
 def fft_input(m):
