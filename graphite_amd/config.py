@@ -71,7 +71,9 @@ RUN_INFO = ["quanta", "steps", "net_msgs", "self_msgs", "boundary_msgs", "final_
 NUM_RUN_INFO = 8
 # gg_core_model_run statistics (include/graphite_gpu.h GG_CORE_*)
 CORE_STATS = ["instructions", "time_ps", "memory_stall_ps", "execution_stall_ps", "l1d_read_stall_ps",
-              "l1d_write_stall_ps"]
+              "l1d_write_stall_ps", "sync_instructions", "sync_stall_ps"]
+META_BARRIER = 0xFFFFFFFF     # GG_META_BARRIER: a BARRIER record of the trace
+LVL_SYNC = 3                  # GG_LVL_SYNC: its access word (stall << 2) | 3
 NUM_CORE_STATS = 8
 CMSG_DTYPE = None  # filled below (numpy view of gg_cmsg)
 NUM_NET_COUNTERS = len(NET_COUNTERS)

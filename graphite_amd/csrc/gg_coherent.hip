@@ -84,7 +84,14 @@ struct Seg { uint32_t line, lo, hi, pad; };       // a run of row (X) / column (
 // device-driven quantum loop (gg_coherent_run): current quantum, launch index
 // of its step 0, run over, quantum-end arrivals, active / blocked tiles, least
 // next start, quanta completed, quantum length
-enum { QS_Q = 0, QS_START, QS_DONE, QS_ARRIVED, QS_ACTIVE, QS_BLOCKED, QS_MIN_NEXT, QS_COUNT, QS_QPS, QS_N };
+enum { QS_Q = 0, QS_START, QS_DONE, QS_ARRIVED, QS_ACTIVE, QS_BLOCKED, QS_MIN_NEXT, QS_COUNT, QS_QPS,
+       QS_BWAIT, QS_BMAX, QS_REL, QS_N };   // barrier waits, their latest arrival, release (max + 1, or 0)
+constexpr uint32_t kBarWait = 2;          // Tile::blocked of a tile waiting at a BARRIER record
+// gap cycles before a record (a BARRIER record is taken at the tile's clock)
+__device__ __forceinline__ uint64_t rec_gap(uint32_t meta)
+{
+  return meta == GG_META_BARRIER ? 0ull : (uint64_t)((meta & 0x7FFFFFFFu) >> 1);
+}
 
 constexpr uint32_t kInLds = 512;       // inbox / port batch entries ordered in LDS (more: global scratch)
 constexpr uint32_t kRqLds = 512;       // directory request FIFO entries staged in LDS
@@ -1020,7 +1027,7 @@ struct Tile {
   {
     const uint64_t a = wa & line_mask;
     const bool wr = (wm & GG_META_WRITE) != 0;
-    const bool mine = ln >= o && wbase + ln < rec_end;
+    const bool mine = ln >= o && wbase + ln < rec_end && wm != GG_META_BARRIER;
     bool hit = false, l2ok = true;
     uint32_t s1 = 0, w1 = 0, s2 = 0, w2 = 0;
     const bool rows = L1.ways <= 16 && L2.ways <= 16 && !P.touch_each;
@@ -1379,9 +1386,13 @@ __device__ __forceinline__ void quantum_end(const CP& P, const CS& S, uint32_t L
     const uint64_t r = S.rec[lt];
     if (r < S.rec_end[lt]) {
       atomicAdd((unsigned long long*)&S.qs[QS_ACTIVE], 1ull);
-      if (S.blocked[lt]) atomicAdd((unsigned long long*)&S.qs[QS_BLOCKED], 1ull);
+      const uint32_t b = S.blocked[lt];
+      if (b == kBarWait) {
+        atomicAdd((unsigned long long*)&S.qs[QS_BWAIT], 1ull);
+        atomicMax((unsigned long long*)&S.qs[QS_BMAX], (unsigned long long)S.clk[lt]);
+      } else if (b) atomicAdd((unsigned long long*)&S.qs[QS_BLOCKED], 1ull);
       else atomicMin((unsigned long long*)&S.qs[QS_MIN_NEXT],
-                     (unsigned long long)(S.clk[lt] + (uint64_t)((S.meta[r] & 0x7FFFFFFFu) >> 1) * P.gap_ps));
+                     (unsigned long long)(S.clk[lt] + rec_gap(S.meta[r]) * P.gap_ps));
     }
   }
   const uint32_t nb = *(volatile uint32_t*)S.bnd_cnt;
@@ -1392,16 +1403,22 @@ __device__ __forceinline__ void quantum_end(const CP& P, const CS& S, uint32_t L
   if (atomicAdd((unsigned long long*)&S.qs[QS_ARRIVED], 1ull) != gridDim.x - 1) return;
   __threadfence();
   const uint64_t active = qs[QS_ACTIVE], blocked = qs[QS_BLOCKED], mn = qs[QS_MIN_NEXT], qps = qs[QS_QPS];
+  const uint64_t bw = qs[QS_BWAIT], bmax = qs[QS_BMAX];
   S.ri[GG_RI_QUANTA]++;
   S.ri[GG_RI_FINAL_QUANTUM] = q;
-  uint64_t nq = q + 1, done = 0;
+  uint64_t nq = q + 1, done = 0, rel = 0;
   if (active == 0 && nb == 0) done = 1;
+  else if (nb == 0 && blocked == 0 && bw == active) {   // every unfinished tile waits at a barrier: release
+    rel = bmax + 1;                                     // at the latest arrival, in the next quantum's step 0
+    nq = max(q + 1, bmax / qps);
+  }
   else if (nb == 0 && blocked == 0) nq = max(q + 1, mn / qps);
   else if (nb == 0) done = 2;                                          // blocked, nothing in flight: deadlock
   for (int i = 0; i < 4; ++i) S.ring[i] = 0;
   S.imp[Q & 1] = 0;
   *S.bnd_cnt = 0;
   qs[QS_ARRIVED] = 0; qs[QS_ACTIVE] = 0; qs[QS_BLOCKED] = 0; qs[QS_MIN_NEXT] = ~0ull;
+  qs[QS_BWAIT] = 0; qs[QS_BMAX] = 0; qs[QS_REL] = rel;
   qs[QS_Q] = nq; qs[QS_START] = L + 1; qs[QS_COUNT] = Q + 1;
   qs[QS_DONE] = done;
   __threadfence();
@@ -1418,7 +1435,7 @@ constexpr uint64_t kNsFin = ~0ull, kNsBlk = ~0ull - 1;   // next start of a fini
 template <bool LC, bool HR, class SL, class H>
 __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t lt, uint32_t k, uint32_t L, uint64_t barrier,
                                           TraceWin& W, SL& sl, uint8_t* clds, const TilePre& pre, const H& hk,
-                                          uint32_t na, uint32_t ni);
+                                          uint32_t na, uint32_t ni, uint64_t rel);
 
 // LC: cache state in LDS; HR: L1 hit runs (persistent small meshes, where
 // long runs of hits between misses pay for the window look-up)
@@ -1465,7 +1482,8 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
   const GHooks hk{P, S};
   const uint32_t na = P.net == GG_NET_EMESH_HOP_BY_HOP ? (p ? pre.narv1 : pre.narv0) : 0u;
   const uint32_t ni = p ? pre.ninb1 : pre.ninb0;
-  tile_step<LC, HR>(P, S, lt, k, L, barrier, W, sl, smem + P.cache_lds_off, pre, hk, na, ni);
+  tile_step<LC, HR>(P, S, lt, k, L, barrier, W, sl, smem + P.cache_lds_off, pre, hk, na, ni,
+                    devloop && k == 0 ? qsv[QS_REL] : 0ull);
 }
 
 // One tile's step k (parity k & 1) of the quantum that ends at `barrier`, on
@@ -1475,7 +1493,7 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
 template <bool LC, bool HR, class SL, class H>
 __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t lt, uint32_t k, uint32_t L, uint64_t barrier,
                                           TraceWin& W, SL& sl, uint8_t* clds, const TilePre& pre, const H& hk,
-                                          uint32_t na, uint32_t ni)
+                                          uint32_t na, uint32_t ni, uint64_t rel)
 {
   const uint32_t ln = lane_id(), p = k & 1u;
   PROF_T0();
@@ -1641,6 +1659,13 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
   }
 
   PROF_AT(_p2);
+  // a barrier released at the quantum boundary: continue at the latest
+  // arrival (the SyncInstruction of sync_client.cc:308-314 is the stall)
+  if (rel && T.blocked == kBarWait) {
+    const uint64_t t = rel - 1;
+    if (S.out && ln == 0) S.out[T.rec] = ((t - T.clk) << 2) | GG_LVL_SYNC;
+    T.clk = t; ++T.rec; T.blocked = 0;
+  }
   // ---- 2. the trace (records fetched 64 at a time, one per lane)
   {
     const uint64_t line_mask = ~((1ull << P.log_line) - 1);
@@ -1675,6 +1700,10 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
       }
       PROF_AT(_ha);
       const uint32_t meta = rl32(wm, (uint32_t)o);
+      if (meta == GG_META_BARRIER) {                                 // CarbonBarrierWait at the tile's clock
+        if (T.clk < barrier) T.blocked = kBarWait;
+        break;
+      }
       const uint64_t s = T.clk + (uint64_t)((meta & 0x7FFFFFFFu) >> 1) * P.gap_ps;
       if (s >= barrier && !(meta & GG_META_CONT)) break;             // a multi-line access is one instruction
       T.app_access(rl64(wa, (uint32_t)o) & line_mask, (meta & GG_META_WRITE) != 0, s);
@@ -1869,7 +1898,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
   // the tile's next start for the shard scheduler: finished, blocked, or clock + gap
   if (T.rec >= T.rec_end) return kNsFin;
   if (T.blocked) return kNsBlk;
-  return T.clk + (uint64_t)((S.meta[T.rec] & 0x7FFFFFFFu) >> 1) * P.gap_ps;
+  return T.clk + rec_gap(S.meta[T.rec]) * P.gap_ps;
 }
 
 // in-kernel launch timing (timing mode 2): the first workgroup start and the
@@ -2418,6 +2447,13 @@ __global__ void k_c_import(CP P, CS S, const gg_cmsg* in, uint32_t n)
   import_one(P, S, in[i], &S.imp[0]);
 }
 
+// any BARRIER record in the trace (only gg_coherent_run releases barriers)
+__global__ void k_has_barrier(const uint32_t* meta, uint64_t n, uint32_t* flag)
+{
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    if (meta[i] == GG_META_BARRIER) { *flag = 1; return; }
+}
+
 // Status after a quantum: active / blocked tiles, least next-access start.
 __global__ void k_c_status(CP P, CS S, uint64_t* out /* [active, blocked, min_next] */)
 {
@@ -2427,7 +2463,7 @@ __global__ void k_c_status(CP P, CS S, uint64_t* out /* [active, blocked, min_ne
   if (r >= S.rec_end[lt]) return;
   atomicAdd((unsigned long long*)&out[0], 1ull);
   if (S.blocked[lt]) { atomicAdd((unsigned long long*)&out[1], 1ull); return; }
-  const uint64_t s = S.clk[lt] + (uint64_t)((S.meta[r] & 0x7FFFFFFFu) >> 1) * P.gap_ps;
+  const uint64_t s = S.clk[lt] + rec_gap(S.meta[r]) * P.gap_ps;
   atomicMin((unsigned long long*)&out[2], (unsigned long long)s);
 }
 
@@ -2549,6 +2585,8 @@ struct gg_coh_state {
   uint32_t wtx = 64, wty = 64;          // threads of an X / Y walker workgroup
   bool persist_lc = false;
   bool begun = false;
+  bool has_barrier = false;             // the bound trace holds BARRIER records (gg_coherent_run only)
+  uint32_t* bar_flag = nullptr;
   // live kernel timing (gg_set_timing): an event pair around every
   // kTimeSample-th launch of each kernel (mode 1; a pair around every launch,
   // mode 2, costs ~18 % of a hop-by-hop run), harvested at the batch syncs;
@@ -2936,7 +2974,7 @@ gg_status gg_coherent_begin(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_ou
   GG_HIP(hipMemsetAsync(C->S.npool, 0, sizeof(uint32_t) * 2, s));
   GG_HIP(hipMemsetAsync(C->S.ring, 0, sizeof(uint32_t) * 11, s));
   {
-    uint64_t q0[QS_N] = {0, 0, 0, 0, 0, 0, ~0ull, 0, (uint64_t)ctx->cfg.quantum_ns * 1000ull};
+    uint64_t q0[QS_N] = {0, 0, 0, 0, 0, 0, ~0ull, 0, (uint64_t)ctx->cfg.quantum_ns * 1000ull, 0, 0, 0};
     GG_HIP(hipMemcpyAsync(C->S.qs, q0, sizeof(q0), hipMemcpyHostToDevice, s));
   }
   GG_HIP(hipMemsetAsync(C->S.bnd_cnt, 0, sizeof(uint32_t), s));
@@ -2944,7 +2982,20 @@ gg_status gg_coherent_begin(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_ou
   GG_HIP(hipMemsetAsync(C->S.nyl, 0, sizeof(uint32_t) * std::max(P.nsy, 1u), s));
   hipLaunchKernelGGL(k_c_reset, dim3(P.L), dim3(256), 0, s, P, C->S, (const uint64_t*)C->offs_dev);
   GG_HIP(hipGetLastError());
+  uint32_t hb = 0;
+  if (tr->num_records) {
+    if (!C->bar_flag) {
+      GG_HIP(hipMalloc((void**)&C->bar_flag, sizeof(uint32_t)));
+      C->allocs.push_back(C->bar_flag);
+    }
+    GG_HIP(hipMemsetAsync(C->bar_flag, 0, sizeof(uint32_t), s));
+    const uint64_t nb = std::min<uint64_t>(4096, (tr->num_records + 255) / 256);
+    hipLaunchKernelGGL(k_has_barrier, dim3((uint32_t)nb), dim3(256), 0, s, tr->meta_dev, tr->num_records, C->bar_flag);
+    GG_HIP(hipGetLastError());
+    GG_HIP(hipMemcpyAsync(&hb, C->bar_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  }
   GG_HIP(hipStreamSynchronize(s));
+  C->has_barrier = hb != 0;
   C->begun = true;
   return coh_check(ctx);
 }
@@ -2957,6 +3008,8 @@ gg_status gg_coherent_begin(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_ou
 static gg_status coh_quantum_steps(gg_ctx* ctx, uint64_t q)
 {
   gg_coh_state* C = ctx->coh;
+  if (C->has_barrier)
+    return gg_fail(GG_ERR_UNSUPPORTED, "BARRIER records are released by gg_coherent_run only (one context)");
   hipStream_t s = ctx->last_stream;
   const CP& P = C->P;
   const uint64_t quantum_ps = (uint64_t)ctx->cfg.quantum_ns * 1000ull;

@@ -16,7 +16,10 @@
 // kTaskRecords records of one tile, one wave each, 4 x 64 records in flight
 // per iteration; a CONT record takes the WRITE bit of the access it belongs
 // to from the last head before it (ballot over the wave, carried across
-// iterations, looked up behind the task's first record).
+// iterations, looked up behind the task's first record).  A BARRIER record
+// with a stall is the SyncInstruction of sync_client.cc:306-314 (dynamic:
+// curr_time += stall, CoreModel::updateDynamicInstructionCounters,
+// core_model.cc:237-250).
 #include "gg_internal.h"
 
 namespace {
@@ -39,9 +42,9 @@ __global__ void __launch_bounds__(64 * kCoreWaves) k_core_model(const uint32_t* 
   // the access the task's first record belongs to: its head is the last
   // non-CONT record at or before it (CONT records follow their head)
   uint64_t j = tk.begin;
-  while (j > tk.tile_begin && (meta[j] & GG_META_CONT)) --j;
+  while (j > tk.tile_begin && (meta[j] & GG_META_CONT) && meta[j] != GG_META_BARRIER) --j;
   uint32_t carry = rec_write(meta[j]);
-  uint64_t n_ins = 0, ex = 0, rd = 0, wr = 0;
+  uint64_t n_ins = 0, ex = 0, rd = 0, wr = 0, ns = 0, sy = 0;
   const uint64_t below = ln == 63 ? ~0ull : ((2ull << ln) - 1);   // lanes <= ln
   for (uint64_t b = tk.begin; b < tk.end; b += 256) {
     uint32_t m[4];
@@ -54,6 +57,7 @@ __global__ void __launch_bounds__(64 * kCoreWaves) k_core_model(const uint32_t* 
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
+      const bool bar = m[u] == GG_META_BARRIER;            // a released barrier: the SyncInstruction
       const bool head = !(m[u] & GG_META_CONT);
       const uint64_t heads = __ballot(head);
       const uint64_t mine = heads & below;
@@ -63,6 +67,7 @@ __global__ void __launch_bounds__(64 * kCoreWaves) k_core_model(const uint32_t* 
       const uint32_t op = mine ? from : carry;
       if (heads) carry = __shfl(own, 63 - __builtin_clzll(heads));
       const uint64_t lat = a[u] >> 2;
+      if (bar) { if (lat) { ++n_ins; ++ns; sy += lat; } continue; }
       if (head) { ++n_ins; ex += (uint64_t)((m[u] & 0x7FFFFFFFu) >> 1) * gap_ps; }
       if (op) wr += lat; else rd += lat;
     }
@@ -71,11 +76,14 @@ __global__ void __launch_bounds__(64 * kCoreWaves) k_core_model(const uint32_t* 
   for (int o = 32; o > 0; o >>= 1) {
     n_ins += __shfl_xor(n_ins, o); ex += __shfl_xor(ex, o);
     rd += __shfl_xor(rd, o); wr += __shfl_xor(wr, o);
+    ns += __shfl_xor(ns, o); sy += __shfl_xor(sy, o);
   }
   if (ln == 0) {
     unsigned long long* s = (unsigned long long*)(stats + (size_t)tk.tile * GG_NUM_CORE_STATS);
     atomicAdd(s + GG_CORE_INSTRUCTIONS, (unsigned long long)n_ins);
-    atomicAdd(s + GG_CORE_TIME_PS, (unsigned long long)(ex + rd + wr));
+    atomicAdd(s + GG_CORE_TIME_PS, (unsigned long long)(ex + rd + wr + sy));
+    atomicAdd(s + GG_CORE_SYNC_INSTRUCTIONS, (unsigned long long)ns);
+    atomicAdd(s + GG_CORE_SYNC_STALL_PS, (unsigned long long)sy);
     atomicAdd(s + GG_CORE_MEMORY_STALL_PS, (unsigned long long)(rd + wr));
     atomicAdd(s + GG_CORE_EXECUTION_STALL_PS, (unsigned long long)ex);
     atomicAdd(s + GG_CORE_L1D_READ_STALL_PS, (unsigned long long)rd);

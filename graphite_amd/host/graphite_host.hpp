@@ -161,12 +161,12 @@ inline void writeCoreSummary(std::ostream& os, const uint64_t* core, double freq
   os << "    Total Instructions: " << n << std::endl;
   os << "    Completion Time (in nanoseconds): " << psToNanosec(t) << std::endl;
   os << "    Average Frequency (in GHz): " << avg_f << std::endl;
-  os << "    Synchronization Stalls: " << zero << std::endl;
+  os << "    Synchronization Stalls: " << core[GG_CORE_SYNC_INSTRUCTIONS] << std::endl;
   os << "    Network Recv Stalls: " << zero << std::endl;
   os << "    Stall Time Breakdown (in nanoseconds): " << std::endl;
   os << "      Memory: " << psToNanosec(core[GG_CORE_MEMORY_STALL_PS]) << std::endl;
   os << "      Execution Unit: " << psToNanosec(core[GG_CORE_EXECUTION_STALL_PS]) << std::endl;
-  os << "      Synchronization: " << psToNanosec(0) << std::endl;
+  os << "      Synchronization: " << psToNanosec(core[GG_CORE_SYNC_STALL_PS]) << std::endl;
   os << "      Network Recv: " << psToNanosec(0) << std::endl;
   os << "    Branch Predictor Statistics:" << std::endl
      << "      Num Correct: " << zero << std::endl
@@ -179,14 +179,15 @@ inline void writeCoreSummary(std::ostream& os, const uint64_t* core, double freq
   os << "      L1-D Cache: "
      << psToNanosec(core[GG_CORE_L1D_READ_STALL_PS]) + psToNanosec(core[GG_CORE_L1D_WRITE_STALL_PS]) << std::endl;
   const uint64_t ni = 0, data_ns = psToNanosec(core[GG_CORE_MEMORY_STALL_PS]), instr_ns = psToNanosec(0);
+  const uint64_t nd = n - core[GG_CORE_SYNC_INSTRUCTIONS];          // data accesses (Core::_num_data_memory_accesses)
   os << "Shared Memory Model Summary: " << std::endl;
-  os << "    Total Memory Accesses: " << ni + n << std::endl;
-  os << "    Average Memory Access Latency (in nanoseconds): " << (1.0 * (instr_ns + data_ns) / (ni + n)) << std::endl;
+  os << "    Total Memory Accesses: " << ni + nd << std::endl;
+  os << "    Average Memory Access Latency (in nanoseconds): " << (1.0 * (instr_ns + data_ns) / (ni + nd)) << std::endl;
   os << "    Total Instruction Memory Accesses: " << ni << std::endl;
   os << "    Instruction Buffer Hits: " << zero << std::endl;
   os << "    Average Instruction Memory Access Latency (in nanoseconds): " << 1.0 * instr_ns / ni << std::endl;
-  os << "    Total Data Memory Accesses: " << n << std::endl;
-  os << "    Average Data Memory Access Latency (in nanoseconds): " << 1.0 * data_ns / n << std::endl;
+  os << "    Total Data Memory Accesses: " << nd << std::endl;
+  os << "    Average Data Memory Access Latency (in nanoseconds): " << 1.0 * data_ns / nd << std::endl;
 }
 
 // NetworkModel::outputSummary (network/network_model.cc:274-316) for one tile's

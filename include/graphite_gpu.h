@@ -95,6 +95,18 @@ enum { GG_LOC_INVALID = 0, GG_LOC_L1I = 2, GG_LOC_L1D = 3 };
  *                The private-cache mode ignores it.                          */
 #define GG_META_WRITE 1u
 #define GG_META_CONT 0x80000000u
+/* A BARRIER record (CarbonBarrierWait / SPLASH BARRIER, sync_client.cc:265-316;
+ * a CONT code with a nonzero gap, which no access carries; addr ignored):
+ * the tile waits until every tile with an unfinished trace waits at a
+ * barrier (SimBarrier::wait, sync_server.cc:133-170 with the count = those
+ * tiles), then all continue at the latest arrival time (SyncServer::
+ * barrierWait replies max_time, :357-383; the MCP is a system tile, so the
+ * messages cost no network time).  gg_coherent_run applies the release at the
+ * quantum boundary after the last arrival and writes the record's access
+ * word as (stall_ps << 2) | GG_LVL_SYNC.  Only gg_coherent_run takes traces
+ * with barriers (the per-quantum and multi-rank entry points return
+ * GG_ERR_UNSUPPORTED).                                                      */
+#define GG_META_BARRIER 0xFFFFFFFFu
 
 /* Per-access result word written by gg_cache_access_batch: one flag per 4-bit
  * field, so result words of up to 15 accesses can be summed field-wise (the
@@ -286,11 +298,11 @@ gg_status gg_shard_map(uint32_t num_tiles, uint32_t num_shards, uint32_t* tile_s
 
 /* Per-access output word of the coherent mode: (latency_ps << 2) | level,
  * latency = Core::initiateMemoryAccess final - initial time (core.cc:245-251). */
-enum { GG_LVL_L1 = 0, GG_LVL_L2 = 1, GG_LVL_DIR = 2 };
+enum { GG_LVL_L1 = 0, GG_LVL_L2 = 1, GG_LVL_DIR = 2, GG_LVL_SYNC = 3 /* a BARRIER record: latency = sync stall */ };
 
 /* Per-tile statistics of the coherent mode, [tile][GG_NUM_TILE_STATS]. */
 enum {
-  GG_CT_CLOCK_PS = 0,        /* core clock after the tile's last access              */
+  GG_CT_CLOCK_PS = 0,        /* core clock after the tile's last access / barrier release */
   GG_CT_ACCESSES, GG_CT_L1_HITS, GG_CT_L2_HITS, GG_CT_L2_MISSES, GG_CT_LATENCY_PS,
   GG_CT_DIR_ACCESSES,        /* DirectoryCache::_total_directory_accesses (directory_cache.cc:97-100) */
   GG_CT_DIR_EVICTIONS,       /* _total_evictions                                      */
@@ -511,7 +523,10 @@ gg_status gg_combine_accesses(const uint64_t* line_out_dev, const uint64_t* firs
  * is the sum of its line latencies (Core::initiateMemoryAccess's final -
  * initial time, core.cc:239-256).  curr_time advances by cost + latency, which
  * is the coherent engine's clock rule, so GG_CORE_TIME_PS equals the run's
- * GG_CT_CLOCK_PS.  No L1-I is modeled (its stall is 0).  The iocoom model is
+ * GG_CT_CLOCK_PS.  A BARRIER record whose access word holds a stall > 0 is
+ * the SyncInstruction of sync_client.cc:306-314 (a dynamic instruction:
+ * curr_time += stall, core_model.cc:237-240 counters).  No L1-I is modeled
+ * (its stall is 0).  The iocoom model is
  * not offered: it needs register operands a memory trace does not carry and
  * would move the issue times the engine replays.
  * Per-tile statistics, [tile][GG_NUM_CORE_STATS]:                            */
@@ -522,6 +537,8 @@ enum {
   GG_CORE_EXECUTION_STALL_PS, /* _total_execution_unit_stall_time                      */
   GG_CORE_L1D_READ_STALL_PS,  /* SimpleCoreModel::_total_l1dcache_read_stall_time      */
   GG_CORE_L1D_WRITE_STALL_PS, /* _total_l1dcache_write_stall_time                      */
+  GG_CORE_SYNC_INSTRUCTIONS,  /* _total_sync_instructions: released BARRIER records with a stall */
+  GG_CORE_SYNC_STALL_PS,      /* _total_sync_instruction_stall_time                    */
   GG_NUM_CORE_STATS = 8
 };
 /* Runs the model over the tile-major trace (meta words and tile offsets of

@@ -185,6 +185,7 @@ void oracle_combine_accesses(const uint64_t* line_out, const uint64_t* first, ui
 /* ======================================================================== */
 typedef struct {
   uint64_t instruction_count, curr_time;                     /* CoreModel (core_model.cc:31-45) */
+  uint64_t total_sync_instructions, total_sync_instruction_stall_time;
   uint64_t total_memory_stall_time, total_execution_unit_stall_time;
   uint64_t total_l1icache_stall_time, total_l1dcache_read_stall_time, total_l1dcache_write_stall_time;
 } o_core;
@@ -233,11 +234,22 @@ void oracle_core_model(const uint32_t* meta, const uint64_t* access_out, const u
     uint64_t r = tile_offsets[t];
     const uint64_t e = tile_offsets[t + 1];
     while (r < e) {
+      if (meta[r] == GG_META_BARRIER) {            /* SyncClient::barrierWait (sync_client.cc:306-314) */
+        const uint64_t stall = access_out[r] >> 2;
+        if (stall) {                               /* CoreModel::handleInstruction of a SyncInstruction */
+          c.instruction_count++;                   /* (dynamic: core_model.cc:237-250) */
+          c.curr_time += stall;
+          c.total_sync_instructions++;
+          c.total_sync_instruction_stall_time += stall;
+        }
+        ++r;
+        continue;
+      }
       o_meminfo info;
       info.read = !(meta[r] & GG_META_WRITE);
       info.latency = access_out[r] >> 2;
       const uint64_t cost = (uint64_t)((meta[r] & 0x7FFFFFFFu) >> 1) * cyc;
-      for (++r; r < e && (meta[r] & GG_META_CONT); ++r) info.latency += access_out[r] >> 2;
+      for (++r; r < e && (meta[r] & GG_META_CONT) && meta[r] != GG_META_BARRIER; ++r) info.latency += access_out[r] >> 2;
       o_core_handle(&c, cost, &info, 1);
     }
     uint64_t* o = stats + (size_t)t * GG_NUM_CORE_STATS;
@@ -248,6 +260,8 @@ void oracle_core_model(const uint32_t* meta, const uint64_t* access_out, const u
     o[GG_CORE_EXECUTION_STALL_PS] = c.total_execution_unit_stall_time;
     o[GG_CORE_L1D_READ_STALL_PS] = c.total_l1dcache_read_stall_time;
     o[GG_CORE_L1D_WRITE_STALL_PS] = c.total_l1dcache_write_stall_time;
+    o[GG_CORE_SYNC_INSTRUCTIONS] = c.total_sync_instructions;
+    o[GG_CORE_SYNC_STALL_PS] = c.total_sync_instruction_stall_time;
   }
 }
 

@@ -15,7 +15,7 @@ import pytest
 
 from graphite_amd import config as C
 
-CONT, WRITE = 0x80000000, 1
+CONT, WRITE, BARRIER = 0x80000000, 1, 0xFFFFFFFF
 
 
 def py_core_model(meta, acc, offs, f=1.0):
@@ -27,12 +27,19 @@ def py_core_model(meta, acc, offs, f=1.0):
     for t in range(T):
         n = tm = mem = ex = rd = wr = 0
         r, e = int(offs[t]), int(offs[t + 1])
+        ns = sy = 0
         while r < e:
+            if int(meta[r]) == BARRIER:          # sync_client.cc:306-314: a SyncInstruction if it stalled
+                lat = int(acc[r]) >> 2
+                if lat:
+                    n += 1; ns += 1; sy += lat; tm += lat
+                r += 1
+                continue
             read = not (int(meta[r]) & WRITE)
             lat = int(acc[r]) >> 2
             cost = ((int(meta[r]) & 0x7FFFFFFF) >> 1) * cyc
             r += 1
-            while r < e and (int(meta[r]) & CONT):
+            while r < e and (int(meta[r]) & CONT) and int(meta[r]) != BARRIER:
                 lat += int(acc[r]) >> 2
                 r += 1
             n += 1
@@ -43,7 +50,7 @@ def py_core_model(meta, acc, offs, f=1.0):
             mem += lat
             ex += cost
             tm += lat + cost
-        out[t, :6] = (n, tm, mem, ex, rd, wr)
+        out[t, :8] = (n, tm, mem, ex, rd, wr, ns, sy)
     return out
 
 
@@ -58,8 +65,14 @@ def synthetic(T, per_tile, seed, cont_frac=0.3, max_gap=40):
     cont[::per_tile] = False
     head_meta = (rng.integers(0, max_gap, n).astype(np.uint32) << 1) | rng.integers(0, 2, n).astype(np.uint32)
     meta[:] = np.where(cont, np.uint32(CONT | WRITE), head_meta)
+    bar = rng.random(n) < 0.02                     # BARRIER records (a stall or none), before a head
+    nxt = np.concatenate([~cont[1:], [True]])
+    bar &= nxt
+    bar[::per_tile] = False
+    meta[bar] = np.uint32(BARRIER)
     lat = rng.integers(1000, 400000, n).astype(np.uint64)
     acc = (lat << np.uint64(2)) | rng.integers(0, 3, n).astype(np.uint64)
+    acc[bar & (rng.random(n) < 0.3)] = np.uint64(3)  # released without a stall
     offs = np.arange(T + 1, dtype=np.uint64) * np.uint64(per_tile)
     return meta, acc, offs
 

@@ -6,7 +6,9 @@ tests/golden/fft_real_p16_m{10,14}.npz were written by
 tools/fft_trace/make_traces.py; when the reference is mounted (this container)
 the m10 capture is redone and must equal the fixture.  The GPU replays the
 traces in Mode C bit-exact against the oracle.  The traces' BARRIER positions
-are kept but not modelled by the replayer."""
+become GG_META_BARRIER records (load_fft_trace): the tiles wait for each
+other and continue at the latest arrival (SimBarrier, sync_server.cc:133-170),
+on the GPU and in the oracle alike."""
 import os
 
 import numpy as np
@@ -21,7 +23,7 @@ REF = os.environ.get("GRAPHITE_REFERENCE", "/root/reference")
 
 @pytest.mark.parametrize("m", [10, 14])
 def test_fixture_structure(m):
-    a, meta, offs, bars = cp.load_fft_trace(cp.REAL_FFT_TRACES[m])
+    a, meta, offs, bars = cp.load_fft_trace(cp.REAL_FFT_TRACES[m], barriers=False)
     assert len(offs) == 17 and offs[0] == 0 and offs[-1] == len(a) == len(meta)
     n = np.diff(offs.astype(np.int64))
     assert n.min() > 0 and n.max() - n.min() < 0.01 * n.max()     # equal shares of the transform
@@ -44,31 +46,75 @@ def test_capture_reproduces_fixture(tmp_path):
     out = str(tmp_path / "m10.npz")
     subprocess.check_call([sys.executable, os.path.join(root, "tools", "fft_trace", "make_traces.py"), out, "10"],
                           stdout=subprocess.DEVNULL)
-    got, ref = cp.load_fft_trace(out), cp.load_fft_trace(cp.REAL_FFT_TRACES[10])
+    got, ref = cp.load_fft_trace(out, False), cp.load_fft_trace(cp.REAL_FFT_TRACES[10], False)
     for x, y in zip(got[:3], ref[:3]):
         np.testing.assert_array_equal(x, y)
     for x, y in zip(got[3], ref[3]):
         np.testing.assert_array_equal(x, y)
 
 
+def barrier_times(meta, out, offs, gap_ps=1000):
+    """Per tile, the clock right after each released barrier, from the access
+    words alone: the sum of gaps and latencies up to the barrier plus its stall."""
+    res = []
+    for t in range(len(offs) - 1):
+        s, e = int(offs[t]), int(offs[t + 1])
+        m, w = meta[s:e], out[s:e]
+        bar = m == C.META_BARRIER
+        step = np.where(bar, 0, (m & 0x7FFFFFFF) >> 1).astype(np.uint64) * np.uint64(gap_ps) + (w >> np.uint64(2))
+        res.append(np.cumsum(step)[bar])
+    return np.array(res)
+
+
 def test_oracle_simulates_real_fft():
     from oracle import pyoracle as po
-    a, meta, offs, _ = cp.load_fft_trace(cp.REAL_FFT_TRACES[10])
     cfg = C.default_config(16, net_model=C.NET_EMESH_HOP_COUNTER)
+    a, meta, offs, _ = cp.load_fft_trace(cp.REAL_FFT_TRACES[10], barriers=False)
     oc = po.OracleCoherent(cfg)
     out = oc.run(a, meta, offs)
     check_invariants(oc.tile_stats(), oc.cache_counters(), out, offs)
     assert oc.tile_stats()[:, C.TILE_STATS.index("l2_misses")].sum() > 0
 
 
+def test_oracle_barriers_release_at_latest_arrival():
+    """Every tile leaves barrier i at the same time = the latest arrival, the
+    barrier records' words carry GG_LVL_SYNC, and the core model's completion
+    time (with the sync stalls) is the engine's clock."""
+    from oracle import pyoracle as po
+    cfg = C.default_config(16, net_model=C.NET_EMESH_HOP_COUNTER)
+    a, meta, offs, bars = cp.load_fft_trace(cp.REAL_FFT_TRACES[10])
+    oc = po.OracleCoherent(cfg)
+    out = oc.run(a, meta, offs)
+    st = oc.tile_stats()
+    bar = meta == C.META_BARRIER
+    assert int(bar.sum()) == 16 * 7 and np.all((out[bar] & 3) == C.LVL_SYNC)
+    bt = barrier_times(meta, out, offs)
+    assert bt.shape == (16, 7) and np.all(bt == bt[0])
+    assert np.all(np.diff(bt[0].astype(np.int64)) >= 0)
+    assert np.all((out[bar] >> 2).reshape(16, 7).min(axis=0) == 0)      # the last arrival waits for nobody
+    core = po.core_model(meta, out, offs, cfg.frequency_ghz)
+    np.testing.assert_array_equal(core[:, C.CORE_STATS.index("time_ps")], st[:, C.TILE_STATS.index("clock_ps")])
+    assert np.all(core[:, C.CORE_STATS.index("sync_instructions")] <= 7)
+    # accesses only: the same program without its barriers runs differently
+    a2, m2, o2, _ = cp.load_fft_trace(cp.REAL_FFT_TRACES[10], barriers=False)
+    oc2 = po.OracleCoherent(cfg)
+    oc2.run(a2, m2, o2)
+    assert not np.array_equal(oc2.tile_stats()[:, 0], st[:, 0])
+    # barrier traces are released by the whole run only, not quantum by quantum
+    oc3 = po.OracleCoherent(cfg)
+    oc3.begin(a, meta, offs)
+    with pytest.raises(Exception):
+        oc3.quantum(0)
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("m", [10, 14])
-def test_gpu_replays_real_fft(m):
+@pytest.mark.parametrize("m,barriers", [(10, True), (10, False), (14, True)])
+def test_gpu_replays_real_fft(m, barriers):
     from graphite_amd import backend as B
     from oracle import pyoracle as po
     from tests.gpu_util import torch_dev, to_dev, to_np
     torch = torch_dev()
-    a, meta, offs, _ = cp.load_fft_trace(cp.REAL_FFT_TRACES[m])
+    a, meta, offs, _ = cp.load_fft_trace(cp.REAL_FFT_TRACES[m], barriers=barriers)
     cfg = C.default_config(16, net_model=C.NET_EMESH_HOP_COUNTER)
     be = B.Backend(cfg)
     out = torch.zeros(len(a), dtype=torch.int64, device="cuda")
@@ -80,3 +126,22 @@ def test_gpu_replays_real_fft(m):
     np.testing.assert_array_equal(st, oc.tile_stats())
     np.testing.assert_array_equal(cc, oc.cache_counters())
     np.testing.assert_array_equal(be.noc_counters(), oc.net_counters())
+
+    if barriers:
+        be.core_model_run(to_dev(torch, meta, torch.int32), offs, out)
+        np.testing.assert_array_equal(be.core_stats(), po.core_model(meta, ref, offs, cfg.frequency_ghz))
+
+
+@pytest.mark.gpu
+def test_gpu_barrier_trace_needs_whole_run():
+    """gg_coherent_quantum (per-quantum / multi-rank driving) rejects a trace
+    with BARRIER records: the release is gg_coherent_run's quantum-end rule."""
+    from graphite_amd import backend as B
+    from tests.gpu_util import torch_dev, to_dev
+    torch = torch_dev()
+    a, meta, offs, _ = cp.load_fft_trace(cp.REAL_FFT_TRACES[10])
+    be = B.Backend(C.default_config(16, net_model=C.NET_EMESH_HOP_COUNTER))
+    out = torch.zeros(len(a), dtype=torch.int64, device="cuda")
+    be.coherent_begin(to_dev(torch, a, torch.int64), to_dev(torch, meta, torch.int32), offs, out)
+    with pytest.raises(B.GGError):
+        be.coherent_quantum(0)
