@@ -410,7 +410,7 @@ def fft_section(args, dev):
     if path and os.path.exists(path):
         a, meta, offs, bars = cp.load_fft_trace(path)
         fft_ok, src = None, ("the reference's tests/benchmarks/fft/fft.C -p%d -m%d captured by tools/fft_trace "
-                             "(heap accesses, 1 cycle per access, %d BARRIER calls per thread not modelled)"
+                             "(heap accesses, 1 cycle per access, %d BARRIER calls per thread as barrier records)"
                              % (p, m, len(bars[0])))
     else:
         m = min(m, 14)

@@ -521,13 +521,14 @@ struct Tile {
   bool failed;
   uint32_t ferr;                         // GG_DERR_* gathered by fail()
   uint64_t ccv, stv;                    // lane k's cache counter k (of 2 x 12) and statistic k, loaded at step start
+  const TilePre& p0;                    // the state loaded at step start (flush stores only what changed)
 
   // LC: the tile's L1-D / L2 tags, meta bytes and RR counters live in LDS at
   // clds for the whole launch (k_c_persist; layout of cache_lds_bytes)
   template <bool LC>
   __device__ __forceinline__ Tile(const CP& P_, const CS& S_, uint32_t l, uint32_t par, SL& s_, const H& h_, uint8_t* clds,
                                   std::integral_constant<bool, LC>, const TilePre& pre)
-      : P(P_), S(S_), lt(l), tile(pre.tile), ln(lane_id()), p(par), sl(s_), hk(h_)
+      : P(P_), S(S_), lt(l), tile(pre.tile), ln(lane_id()), p(par), sl(s_), hk(h_), p0(pre)
   {
     const size_t n1 = (size_t)P.s1 * P.a1, n2 = (size_t)P.s2 * P.a2;
     if constexpr (LC) {
@@ -1234,7 +1235,10 @@ struct Tile {
     }
   }
 
-  // store-only write back: the counters were loaded with the tile
+  // store-only write back of what the step changed: the counters were
+  // loaded with the tile, and an idle tile (most of them in a step) leaves
+  // its lines clean, so the launch's end writes back only the active tiles'
+  // state (the agent-scope release costs by the dirty bytes)
   __device__ __forceinline__ void flush()
   {
     {
@@ -1245,12 +1249,20 @@ struct Tile {
     {
       const uint64_t d = sd;
       uint64_t* g = S.st + (size_t)lt * GG_NUM_TILE_STATS;
-      if (ln == GG_CT_CLOCK_PS) g[ln] = clk;
+      if (ln == GG_CT_CLOCK_PS) { if (clk != p0.clk) g[ln] = clk; }
       else if (ln < GG_NUM_TILE_STATS && d) g[ln] = stv + d;
     }
-    S.rec[lt] = rec; S.clk[lt] = clk; S.pend_start[lt] = pend_start;
-    S.out_addr[lt] = out_addr; S.out_time[lt] = out_time;
-    S.blocked[lt] = blocked; S.seq[lt] = seq; S.nrep[lt] = nrep; S.nrq[lt] = nrq;
+    if (ln == 0) {
+      if (rec != p0.rec) S.rec[lt] = rec;
+      if (clk != p0.clk) S.clk[lt] = clk;
+      if (pend_start != p0.pend_start) S.pend_start[lt] = pend_start;
+      if (out_addr != p0.out_addr) S.out_addr[lt] = out_addr;
+      if (out_time != p0.out_time) S.out_time[lt] = out_time;
+      if (blocked != p0.blocked) S.blocked[lt] = blocked;
+      if (seq != p0.seq) S.seq[lt] = seq;
+      if (nrep != p0.nrep) S.nrep[lt] = nrep;
+      if (nrq != p0.nrq) S.nrq[lt] = nrq;
+    }
   }
 };
 
