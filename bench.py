@@ -914,7 +914,9 @@ def main():
         if "cpu_baseline" in head:
             out["cpu_baseline"] = head["cpu_baseline"]
     secs = [x for x in args.sections.split(",") if x] if world == 1 else []
+    t_sec = time.perf_counter()
     for name in secs:
+        print("bench.py: section %s (%.0f s)" % (name, time.perf_counter() - t_sec), file=sys.stderr, flush=True)
         try:
             if name == "coherent_long" and args.long_per_tile:
                 r = coherent_long_section(args, dev)
