@@ -145,3 +145,53 @@ def test_gpu_barrier_trace_needs_whole_run():
     be.coherent_begin(to_dev(torch, a, torch.int64), to_dev(torch, meta, torch.int32), offs, out)
     with pytest.raises(B.GGError):
         be.coherent_quantum(0)
+
+
+def with_barriers(a, m, offs, every):
+    """The hotspot trace with a BARRIER record after every `every` accesses of each tile."""
+    A, M = [], []
+    for t in range(len(offs) - 1):
+        s, e = int(offs[t]), int(offs[t + 1])
+        pos = np.arange(every, e - s, every)
+        A.append(np.insert(a[s:e], pos, np.uint64(0)))
+        M.append(np.insert(m[s:e], pos, np.uint32(C.META_BARRIER)))
+    o = np.concatenate([[0], np.cumsum([len(x) for x in A])]).astype(np.uint64)
+    return np.concatenate(A), np.concatenate(M), o
+
+
+@pytest.mark.parametrize("T,N,net,K", [(16, 300, C.NET_EMESH_HOP_COUNTER, 1), (64, 200, C.NET_EMESH_HOP_BY_HOP, 8)])
+def test_oracle_barriers_on_hotspot(T, N, net, K):
+    from oracle import pyoracle as po
+    a, m, o = po.gen_trace(T, N, hot_lines=16)
+    a, m, o = with_barriers(a, m, o, N // 4)
+    cfg = C.default_config(T, num_shards=K, net_model=net)
+    oc = po.OracleCoherent(cfg)
+    out = oc.run(a, m, o)
+    bt = barrier_times(m, out, o)
+    assert bt.shape == (T, 3) and np.all(bt == bt[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,N,net,K", [(16, 300, C.NET_EMESH_HOP_COUNTER, 1), (64, 200, C.NET_EMESH_HOP_BY_HOP, 8),
+                                       (256, 120, C.NET_EMESH_HOP_COUNTER, 8), (256, 100, C.NET_EMESH_HOP_BY_HOP, 8)])
+def test_gpu_barriers_on_hotspot(T, N, net, K):
+    """BARRIER records through the persistent small-mesh kernel (<= 64 tiles)
+    and the per-step launches (256 tiles), closed-form and hop-by-hop networks:
+    bit-exact against the oracle."""
+    from graphite_amd import backend as B
+    from oracle import pyoracle as po
+    from tests.gpu_util import torch_dev, to_dev, to_np
+    torch = torch_dev()
+    a, m, o = po.gen_trace(T, N, hot_lines=16)
+    a, m, o = with_barriers(a, m, o, N // 4)
+    cfg = C.default_config(T, num_shards=K, net_model=net)
+    be = B.Backend(cfg)
+    out = torch.zeros(len(a), dtype=torch.int64, device="cuda")
+    be.coherent_run(to_dev(torch, a, torch.int64), to_dev(torch, m, torch.int32), o, out)
+    st, cc, _ = be.coherent_stats()
+    oc = po.OracleCoherent(cfg)
+    ref = oc.run(a, m, o)
+    np.testing.assert_array_equal(to_np(out, np.uint64), ref)
+    np.testing.assert_array_equal(st, oc.tile_stats())
+    np.testing.assert_array_equal(cc, oc.cache_counters())
+    np.testing.assert_array_equal(be.noc_counters(), oc.net_counters())
