@@ -133,9 +133,11 @@ def parse():
     p.add_argument("--no-kernel-profile", action="store_true",
                    help="skip the extra instrumented run (for an external rocprofv3 trace of the timed runs alone)")
     p.add_argument("--sections",
-                   default="coherent_long,exchange,hop_counter,stress,fft,private,private_16way,noc,core_model",
+                   default="coherent_long,exchange,hop_counter,hotspot256,stress,fft,private,private_16way,noc,"
+                           "core_model",
                    help="extra sections at N = 1 (comma list; '' = none)")
     p.add_argument("--hc-per-tile", type=int, default=1024, help="hop_counter section: accesses per tile")
+    p.add_argument("--h256-per-tile", type=int, default=1024, help="hotspot256 section (configs[2]): accesses per tile")
     p.add_argument("--private-per-tile", type=int, default=1 << 20)
     p.add_argument("--cpu-sample-tiles", type=int, default=480, help="private section: tile replays of its CPU sample")
     p.add_argument("--replay-kernel", type=int, default=0)
@@ -388,6 +390,21 @@ def hop_counter_section(args, dev):
                      not args.no_cpu_baseline, kernel_profile=False)
     r["workload"] = ("%d tiles x %d hotspot accesses (%d hot lines), MSI + DRAM + emesh_hop_counter, %d logical shards"
                      % (T, N, H, K))
+    r["unit"] = "accesses/s"
+    return r
+
+
+def hotspot256_section(args, dev):
+    """configs[2]: 256 tiles (16x16), the hotspot trace with 64 hot lines,
+    MSI + full-map directory + DRAM + emesh_hop_by_hop, one process (one
+    logical shard), --h256-per-tile accesses per tile; bit-exact against the
+    tile-parallel oracle, which is its CPU baseline."""
+    from graphite_amd import config as C
+    T, N = 256, args.h256_per_tile
+    r = coherent_run(args, T, N, 64, 1, C.NET_EMESH_HOP_BY_HOP, 1, 0, dev, 1, 0, not args.no_verify,
+                     not args.no_cpu_baseline, kernel_profile=False)
+    r["workload"] = ("configs[2]: %d tiles (16x16) x %d hotspot accesses (64 hot lines), MSI + DRAM + "
+                     "emesh_hop_by_hop, one process" % (T, N))
     r["unit"] = "accesses/s"
     return r
 
@@ -924,6 +941,8 @@ def main():
                 r = exchange_section(args, dev)
             elif name == "hop_counter":
                 r = hop_counter_section(args, dev)
+            elif name == "hotspot256" and args.h256_per_tile:
+                r = hotspot256_section(args, dev)
             elif name == "fft" and args.fft_m:
                 r = fft_section(args, dev)
             elif name == "private":
