@@ -58,7 +58,7 @@ EXPORTS = ["gg_abi_version", "gg_last_error", "gg_config_default", "gg_create", 
            "gg_coherent_begin", "gg_coherent_quantum", "gg_coherent_export", "gg_coherent_import",
            "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace", "gg_shard_map",
            "gg_kernel_stats", "gg_round_exchange", "gg_coherent_run_ranks", "gg_gen_stress_trace",
-           "gg_split_accesses", "gg_combine_accesses", "gg_dump_summary", "gg_core_model_run", "gg_core_get_stats"]
+           "gg_split_accesses", "gg_combine_accesses", "gg_dump_summary", "gg_core_model_run", "gg_core_get_stats", "gg_coherent_get_miss_types"]
 
 
 class _CStatus(ctypes.Structure):
@@ -118,10 +118,12 @@ def load():
     L.gg_dump_summary.argtypes = [vp, i32, ctypes.c_char_p, u64, ctypes.POINTER(u64)]
     L.gg_core_model_run.argtypes = [vp, ctypes.POINTER(_Trace), vp, vp]
     L.gg_core_get_stats.argtypes = [vp, vp]
+    L.gg_coherent_get_miss_types.argtypes = [vp, vp]
     for name in ["gg_kernel_stats", "gg_shard_map", "gg_coherent_begin", "gg_coherent_quantum", "gg_coherent_export",
                  "gg_coherent_import", "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace",
                  "gg_round_exchange", "gg_coherent_run_ranks", "gg_gen_stress_trace", "gg_split_accesses",
-                 "gg_combine_accesses", "gg_dump_summary", "gg_core_model_run", "gg_core_get_stats"]:
+                 "gg_combine_accesses", "gg_dump_summary", "gg_core_model_run", "gg_core_get_stats",
+                 "gg_coherent_get_miss_types"]:
         getattr(L, name).restype = i32
     for name in ["gg_reset", "gg_cache_access_batch", "gg_cache_get_counters", "gg_cache_get_line_info",
                  "gg_cache_set_line_info", "gg_cache_access_line", "gg_cache_insert_line",
@@ -351,6 +353,14 @@ class Backend:
         _need_dev(access_out, torch.int64, n)
         tr = _Trace(None, meta.data_ptr(), self._offs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), n)
         _check(load().gg_core_model_run(self.h, ctypes.byref(tr), access_out.data_ptr(), _stream(stream)))
+
+    def miss_types(self):
+        """[tiles][2][3] cold / capacity / sharing misses of the L1-D and L2
+        (gg_coherent_get_miss_types; zeros for an untracked cache)."""
+        T = self.cfg.num_tiles
+        out = np.zeros(T * 2 * 3, np.uint64)
+        _check(load().gg_coherent_get_miss_types(self.h, out.ctypes.data_as(ctypes.c_void_p)))
+        return out.reshape(T, 2, 3)
 
     def core_stats(self):
         T = self.cfg.num_tiles

@@ -72,6 +72,7 @@ NUM_RUN_INFO = 8
 # gg_core_model_run statistics (include/graphite_gpu.h GG_CORE_*)
 CORE_STATS = ["instructions", "time_ps", "memory_stall_ps", "execution_stall_ps", "l1d_read_stall_ps",
               "l1d_write_stall_ps", "sync_instructions", "sync_stall_ps"]
+MISS_TYPES = ["cold", "capacity", "sharing"]   # GG_MT_* (Cache::MissType)
 META_BARRIER = 0xFFFFFFFF     # GG_META_BARRIER: a BARRIER record of the trace
 LVL_SYNC = 3                  # GG_LVL_SYNC: its access word (stall << 2) | 3
 NUM_CORE_STATS = 8
@@ -118,6 +119,9 @@ class GGConfig(ctypes.Structure):
         ("dram_queue_model_type", ctypes.c_uint32),
         ("basic_moving_avg", ctypes.c_uint32),
         ("history_list_no_interleaving", ctypes.c_uint32),
+        ("l1i_track_miss_types", ctypes.c_uint32),
+        ("l2_track_miss_types", ctypes.c_uint32),
+        ("miss_track_lines", ctypes.c_uint32),
     ]
 
 

@@ -258,6 +258,8 @@ gg_status gg_cache_access_batch(gg_ctx* ctx, const gg_trace* trace, uint32_t* re
                                 uint64_t* evicted_dev, void* stream)
 {
   if (!ctx) return gg_fail(GG_ERR_INVALID, "ctx NULL");
+  if (ctx->cfg.l1i_track_miss_types || ctx->cfg.l2_track_miss_types)
+    return gg_fail(GG_ERR_UNSUPPORTED, "miss-type tracking is built for the coherent mode only");
   hipSetDevice(ctx->device);
   hipStream_t s = (hipStream_t)stream;
   ctx->last_stream = s;

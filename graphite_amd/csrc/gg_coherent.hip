@@ -114,6 +114,7 @@ struct CP {
   uint32_t touch_each;                     // hit runs touch LRU rows one record at a time (> 16 ways; GG_COH_TOUCH_EACH=1)
   uint32_t walk_wide;                      // pipelined walkers scan every packet (the > 128-packet path; GG_COH_WALK_WIDE=1)
   uint32_t no_hit_runs;                    // GG_COH_NO_HIT_RUNS=1: every record through app_access
+  uint32_t mt1, mt2, mt_log;               // miss-type tracking of the L1-D / L2 (cfg flags), log2 set capacity
   uint64_t lat_l1d, lat_l1t, lat_l2d, lat_l2t, lat_dir, gap_ps, dram_proc, dram_cost;
   NocParams np;
 };
@@ -122,6 +123,8 @@ struct CS {
   uint64_t* l1_tag; uint8_t* l1_meta; uint8_t* l1_rr;
   uint64_t* l2_tag; uint8_t* l2_meta; uint8_t* l2_rr;
   uint64_t* cc;                          // [L][2][12]
+  uint64_t* mtab;                        // [L][2][2^mt_log] address sets (line | E 1 I 2 F 4), ~0 empty; when tracking
+  unsigned long long* mtc;               // [L][2][GG_NUM_MISS_TYPES] when tracking
   uint64_t* st;                          // [L][GG_NUM_TILE_STATS]
   uint64_t *rec, *rec_end, *clk, *pend_start, *out_addr, *out_time;
   uint32_t *blocked, *seq;
@@ -267,6 +270,65 @@ struct Cache {
   // the last set this lane loaded (its way), kept in step with every store, so
   // consecutive operations on one set load it once
   uint32_t cset; uint64_t ctv; uint32_t cmv;
+  // miss-type tracking (track_miss_types, cache.cc:321-405): the evicted /
+  // invalidated / fetched address sets as one open-addressing table owned by
+  // the tile (line address | bits), probed 64 slots per wave load
+  uint64_t* mtab = nullptr; unsigned long long* mtc = nullptr; uint32_t mt_log = 0;
+  static constexpr uint64_t kMtEmpty = ~0ull;
+  static constexpr uint32_t kMtE = 1, kMtI = 2, kMtF = 4;
+  __device__ __forceinline__ uint64_t mt_slot(uint64_t a, uint32_t& bits, uint32_t& err)
+  {
+    const uint64_t cap = 1ull << mt_log;
+    uint64_t h = (a >> log_line) * 0x9E3779B97F4A7C15ull;
+    h ^= h >> 29;
+    for (uint64_t base = h & (cap - 1), n = 0; n < cap; base = (base + 64) & (cap - 1), n += 64) {
+      const uint64_t i = (base + ln) & (cap - 1);
+      const uint64_t k = mtab[i];
+      const uint64_t hit = __ballot(k != kMtEmpty && (k & ~7ull) == a), emp = __ballot(k == kMtEmpty);
+      const uint64_t any = hit | emp;                                  // probe order = lane order
+      if (any) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(any);
+        bits = (hit >> l) & 1 ? (uint32_t)(rl64(k, l) & 7u) : 0u;
+        return (base + l) & (cap - 1);
+      }
+    }
+    err |= GG_DERR_CAP;                                                // the table is full
+    bits = 0;
+    return 0;
+  }
+  __device__ __forceinline__ void mt_put(uint64_t i, uint64_t a, uint32_t bits)
+  {
+    if (ln == 0) mtab[i] = a | bits;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __device__ __forceinline__ void mt_or(uint64_t a, uint32_t b, uint32_t& err)
+  {
+    uint32_t bits;
+    const uint64_t i = mt_slot(a, bits, err);
+    mt_put(i, a, bits | b);
+  }
+  // insertCacheLine (cache.cc:131-148): the victim into the evicted set; the
+  // inserted line out of the first set that holds it (clearMissTypeTrackingSets,
+  // :398-404), then into the fetched set
+  __device__ __forceinline__ void mt_insert(uint64_t a, bool ev, uint64_t ev_addr, uint32_t& err)
+  {
+    if (ev) mt_or(ev_addr, kMtE, err);
+    uint32_t bits;
+    const uint64_t i = mt_slot(a, bits, err);
+    if (bits & kMtE) bits &= ~kMtE;
+    else if (bits & kMtI) bits &= ~kMtI;
+    else if (bits & kMtF) bits &= ~kMtF;
+    mt_put(i, a, bits | kMtF);
+  }
+  // getMissType + updateMissTypeCounters (cache.cc:363-396)
+  __device__ __forceinline__ void mt_classify(uint64_t a, uint32_t& err)
+  {
+    uint32_t bits;
+    (void)mt_slot(a, bits, err);
+    const uint32_t t = (bits & kMtE) ? GG_MT_CAPACITY : (bits & (kMtI | kMtF)) ? GG_MT_SHARING : GG_MT_COLD;
+    if (ln == 0) atomicAdd(&mtc[t], 1ull);
+  }
+  uint32_t mt_err = 0;
 
   __device__ __forceinline__ void cnt(uint32_t k) { if (ln == k) ++cd; }
   __device__ __forceinline__ void cnt_add(uint32_t k, uint32_t v) { if (ln == k) cd += v; }
@@ -309,11 +371,14 @@ struct Cache {
       if (nv != mv) st_meta(s, nv);
     }
   }
-  __device__ __forceinline__ void miss_counters(bool wr, bool miss)                                               // cache.cc:321-360
+  __device__ __forceinline__ void miss_counters(uint64_t a, bool wr, bool miss)                                   // cache.cc:321-360
   {
     cnt(GG_CC_ACCESSES);
     if (wr) cnt(GG_CC_WRITE_ACCESSES); else cnt(GG_CC_READ_ACCESSES);
-    if (miss) { cnt(GG_CC_MISSES); if (wr) cnt(GG_CC_WRITE_MISSES); else cnt(GG_CC_READ_MISSES); }
+    if (miss) {
+      cnt(GG_CC_MISSES); if (wr) cnt(GG_CC_WRITE_MISSES); else cnt(GG_CC_READ_MISSES);
+      if (mtab) mt_classify(a, mt_err);
+    }
   }
   // getCacheLineInfo (cache.cc:187-215): state / loc of the line, I / 0 when absent
   __device__ __forceinline__ void get(uint64_t a, uint32_t& st, uint32_t& loc)
@@ -341,6 +406,7 @@ struct Cache {
     ld(s, tv, mv);
     const int w = way_of(tv, tag_of(a));
     if (w < 0) return false;
+    if (mtab && st == ST_I) mt_or(a, kMtI, mt_err);                  // cache.cc:228-230
     if ((int)ln == w) {
       st_meta(s, (mv & 0xF8u) | st | (loc << 2));
       if (st == ST_I) st_tag(s, INV_ADDR);
@@ -383,6 +449,7 @@ struct Cache {
     const uint32_t vm = rl32(mv, (uint32_t)w);
     ev = vt != INV_ADDR;
     if (ev) { ev_addr = vt << log_line; ev_st = vm & 3u; ev_loc = (vm >> 2) & 1u; }
+    if (mtab) mt_insert(a, ev, vt << log_line, mt_err);
     if ((int)ln == w) {
       const uint32_t nm = (vm & 0xF8u) | st | (loc << 2);
       st_tag(s, tag_of(a));
@@ -547,6 +614,14 @@ struct Tile {
       L2 = Cache{S.l2_tag + lt * n2, S.l2_meta + lt * n2, S.l2_rr + (size_t)lt * P.s2,
                  S.cc + ((size_t)lt * 2 + 1) * GG_NUM_CACHE_COUNTERS, P.s2, P.a2, P.log_line, P.pol2, 1, ln, 0, ~0u, 0, 0};
     }
+    if (P.mt1) {
+      L1.mtab = S.mtab + ((size_t)lt * 2 << P.mt_log); L1.mtc = S.mtc + (size_t)lt * 2 * GG_NUM_MISS_TYPES;
+      L1.mt_log = P.mt_log;
+    }
+    if (P.mt2) {
+      L2.mtab = S.mtab + (((size_t)lt * 2 + 1) << P.mt_log); L2.mtc = S.mtc + ((size_t)lt * 2 + 1) * GG_NUM_MISS_TYPES;
+      L2.mt_log = P.mt_log;
+    }
     sd = 0;
     rec = pre.rec; rec_end = pre.rec_end; clk = pre.clk; pend_start = pre.pend_start;
     out_addr = pre.out_addr; out_time = pre.out_time;
@@ -566,6 +641,7 @@ struct Tile {
   }
   __device__ __forceinline__ void flush_err()
   {
+    ferr |= L1.mt_err | L2.mt_err;
     if (ferr && ln == 0) atomicOr(S.err, ferr);
   }
 
@@ -1144,14 +1220,14 @@ struct Tile {
     uint32_t cs, loc;
     L1.get(a, cs, loc);
     const bool hit = wr ? cs == ST_M : cs != ST_I;
-    L1.miss_counters(wr, !hit);
+    L1.miss_counters(a, wr, !hit);
     if (hit) { t += P.lat_l1d; l1_access(a, wr); finish(s, t, GG_LVL_L1); return; }
     t += P.lat_l1t;
     l1_invalidate(a);
     uint32_t c2, l2;                                                 // processShmemRequestFromL1Cache (l2:180-224)
     L2.get(a, c2, l2);
     const bool hit2 = wr ? c2 == ST_M : c2 != ST_I;
-    L2.miss_counters(wr, !hit2);
+    L2.miss_counters(a, wr, !hit2);
     if (hit2) {
       if (!L2.access(a, false)) fail();
       insert_in_l1(a, c2);
@@ -2906,6 +2982,15 @@ static gg_status coh_alloc(gg_ctx* ctx)
   A(l1_tag, L * P.s1 * P.a1); A(l1_meta, L * P.s1 * P.a1); A(l1_rr, L * P.s1);
   A(l2_tag, L * P.s2 * P.a2); A(l2_meta, L * P.s2 * P.a2); A(l2_rr, L * P.s2);
   A(cc, L * 2 * GG_NUM_CACHE_COUNTERS); A(st, L * GG_NUM_TILE_STATS);
+  // miss-type tracking (default off): one address table per (tile, cache)
+  P.mt1 = ctx->cfg.l1i_track_miss_types ? 1u : 0u;
+  P.mt2 = ctx->cfg.l2_track_miss_types ? 1u : 0u;
+  if (P.mt1 || P.mt2) {
+    const uint32_t lines = ctx->cfg.miss_track_lines ? ctx->cfg.miss_track_lines : 65536u;
+    if (lines & (lines - 1) || lines < 64) return gg_fail(GG_ERR_INVALID, "miss_track_lines must be a power of two >= 64");
+    P.mt_log = (uint32_t)__builtin_ctz(lines);
+    A(mtab, (size_t)L * 2 << P.mt_log); A(mtc, L * 2 * GG_NUM_MISS_TYPES);
+  }
   A(rec, L); A(rec_end, L); A(clk, L); A(pend_start, L); A(out_addr, L); A(out_time, L);
   A(blocked, L); A(seq, L);
   A(dir, L * P.E); A(dsh, L * P.E * P.W);
@@ -2990,6 +3075,10 @@ gg_status gg_coherent_begin(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_ou
     GG_HIP(hipMemcpyAsync(C->S.qs, q0, sizeof(q0), hipMemcpyHostToDevice, s));
   }
   GG_HIP(hipMemsetAsync(C->S.bnd_cnt, 0, sizeof(uint32_t), s));
+  if (C->S.mtab) {                                   // the miss-type address sets start empty
+    GG_HIP(hipMemsetAsync(C->S.mtab, 0xFF, sizeof(uint64_t) * ((size_t)P.L * 2 << P.mt_log), s));
+    GG_HIP(hipMemsetAsync(C->S.mtc, 0, sizeof(uint64_t) * P.L * 2 * GG_NUM_MISS_TYPES, s));
+  }
   GG_HIP(hipMemsetAsync(C->S.nxl, 0, sizeof(uint32_t) * std::max(P.nsx, 1u), s));
   GG_HIP(hipMemsetAsync(C->S.nyl, 0, sizeof(uint32_t) * std::max(P.nsy, 1u), s));
   hipLaunchKernelGGL(k_c_reset, dim3(P.L), dim3(256), 0, s, P, C->S, (const uint64_t*)C->offs_dev);
@@ -3299,6 +3388,26 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
   GG_HIP(hipMemcpy(&done, C->S.qs + QS_DONE, sizeof(done), hipMemcpyDeviceToHost));
   if (done == 2) return gg_fail(GG_ERR_STATE, "coherent run deadlocked: tiles blocked with no message in flight");
   return GG_OK;
+}
+
+gg_status gg_coherent_get_miss_types(gg_ctx* ctx, uint64_t* out)
+{
+  if (!ctx || !out) return gg_fail(GG_ERR_INVALID, "NULL argument");
+  gg_coh_state* C = ctx->coh;
+  if (!C) return gg_fail(GG_ERR_INVALID, "no coherent run on this context");
+  hipSetDevice(ctx->device);
+  const CP& P = C->P;
+  const size_t per = 2 * GG_NUM_MISS_TYPES;
+  std::memset(out, 0, sizeof(uint64_t) * P.T * per);
+  if (!C->S.mtc) return GG_OK;
+  GG_HIP(hipStreamSynchronize(ctx->last_stream));
+  std::vector<uint64_t> v((size_t)P.L * per);
+  std::vector<uint32_t> gtile(P.L);
+  GG_HIP(hipMemcpy(v.data(), C->S.mtc, sizeof(uint64_t) * v.size(), hipMemcpyDeviceToHost));
+  GG_HIP(hipMemcpy(gtile.data(), C->S.gtile, sizeof(uint32_t) * P.L, hipMemcpyDeviceToHost));
+  for (uint32_t l = 0; l < P.L; ++l)
+    std::memcpy(out + (size_t)gtile[l] * per, v.data() + (size_t)l * per, sizeof(uint64_t) * per);
+  return coh_check(ctx);
 }
 
 gg_status gg_coherent_get_stats(gg_ctx* ctx, uint64_t* tile_stats, uint64_t* cache, uint64_t* run_info)

@@ -27,6 +27,11 @@ gg_status gg_dump_summary(gg_ctx* ctx, int format, char* buf, uint64_t cap, uint
     if (gg_status e = gg_coherent_get_stats(ctx, st.data(), cc.data(), nullptr)) return e;
   } else if (gg_status e = gg_cache_get_counters(ctx, cc.data())) return e;
   if (gg_status e = gg_noc_get_counters(ctx, nc.data())) return e;
+  std::vector<uint64_t> mt;
+  if (coherent && (cfg.l1i_track_miss_types || cfg.l2_track_miss_types)) {
+    mt.resize((size_t)T * 2 * GG_NUM_MISS_TYPES);
+    if (gg_status e = gg_coherent_get_miss_types(ctx, mt.data())) return e;
+  }
   std::vector<uint64_t> core;
   if (ctx->core_valid) {                       // gg_core_model_run's statistics: the "Core Summary" blocks
     core.resize((size_t)T * GG_NUM_CORE_STATS);
@@ -40,7 +45,8 @@ gg_status gg_dump_summary(gg_ctx* ctx, int format, char* buf, uint64_t cap, uint
       std::ostringstream os;
       graphite_amd::writeTileSummary(os, cfg, coherent ? &st[(size_t)t * GG_NUM_TILE_STATS] : nullptr,
                                      &cc[(size_t)t * 2 * GG_NUM_CACHE_COUNTERS], &nc[(size_t)t * GG_NUM_NET_COUNTERS],
-                                     core.empty() ? nullptr : &core[(size_t)t * GG_NUM_CORE_STATS]);
+                                     core.empty() ? nullptr : &core[(size_t)t * GG_NUM_CORE_STATS],
+                                     mt.empty() ? nullptr : &mt[(size_t)t * 2 * GG_NUM_MISS_TYPES]);
       if (format == GG_SUMMARY_TABLE) per_tile.push_back(os.str());
       else all << "Tile " << t << " Summary:" << std::endl << os.str();
     }

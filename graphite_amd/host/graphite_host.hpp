@@ -107,7 +107,7 @@ class Backend {
 // write-miss-rate line keeps the reference's 4-space indent (cache.cc:445); the
 // asynchronous-communication block is empty in a single DVFS domain.
 inline void writeCacheSummary(std::ostream& out, const std::string& name, const uint64_t* c,
-                              bool write_back, bool instruction_cache = false)
+                              bool write_back, bool instruction_cache = false, const uint64_t* miss_types = nullptr)
 {
   out << "  Cache " << name << ": " << std::endl;
   out << "    Cache Accesses: " << c[GG_CC_ACCESSES] << std::endl;
@@ -132,6 +132,12 @@ inline void writeCacheSummary(std::ostream& out, const std::string& name, const 
   }
   out << "    Evictions: " << c[GG_CC_EVICTIONS] << std::endl;
   if (write_back) out << "    Dirty Evictions: " << c[GG_CC_DIRTY_EVICTIONS] << std::endl;
+  if (miss_types) {                                   // track_miss_types (cache.cc:459-466)
+    out << "    Miss Types:" << std::endl;
+    out << "      Cold Misses: " << miss_types[GG_MT_COLD] << std::endl;
+    out << "      Capacity Misses: " << miss_types[GG_MT_CAPACITY] << std::endl;
+    out << "      Sharing Misses: " << miss_types[GG_MT_SHARING] << std::endl;
+  }
   out << "    Event Counters:" << std::endl;
   out << "      Tag Array Reads: " << c[GG_CC_TAG_READS] << std::endl;
   out << "      Tag Array Writes: " << c[GG_CC_TAG_WRITES] << std::endl;
@@ -337,11 +343,13 @@ inline void writeDirectorySummary(std::ostream& out, const uint64_t* st, const D
 // (msi/memory_manager.cc:415-430): Cache Summary (L1-D, L2; no L1-I is
 // modeled), then the DRAM and directory summaries.
 inline void writeMemorySummary(std::ostream& out, const gg_config& c, const uint64_t* tile_stats,
-                               const uint64_t* cache_counters)
+                               const uint64_t* cache_counters, const uint64_t* miss_types = nullptr)
 {
   out << "Cache Summary:\n";
-  writeCacheSummary(out, "L1-D", cache_counters, false);
-  writeCacheSummary(out, "L2", cache_counters + GG_NUM_CACHE_COUNTERS, true);
+  writeCacheSummary(out, "L1-D", cache_counters, false, false,
+                    miss_types && c.l1i_track_miss_types ? miss_types : nullptr);
+  writeCacheSummary(out, "L2", cache_counters + GG_NUM_CACHE_COUNTERS, true, false,
+                    miss_types && c.l2_track_miss_types ? miss_types + GG_NUM_MISS_TYPES : nullptr);
   writeDramSummary(out, tile_stats, c.dram_queue_model_enabled != 0, c.dram_queue_model_type);
   writeDirectorySummary(out, tile_stats, directorySizing(c));
 }
@@ -354,11 +362,11 @@ inline void writeMemorySummary(std::ostream& out, const gg_config& c, const uint
 // then the networks.
 inline void writeTileSummary(std::ostream& os, const gg_config& cfg, const uint64_t* tile_stats,
                              const uint64_t* cache_counters, const uint64_t* net_counters,
-                             const uint64_t* core_stats = nullptr)
+                             const uint64_t* core_stats = nullptr, const uint64_t* miss_types = nullptr)
 {
   static const uint64_t zero_net[GG_NUM_NET_COUNTERS] = {0};
   if (core_stats) writeCoreSummary(os, core_stats, cfg.frequency_ghz);   // Tile::outputSummary (tile.cc:52-69)
-  if (tile_stats) writeMemorySummary(os, cfg, tile_stats, cache_counters);
+  if (tile_stats) writeMemorySummary(os, cfg, tile_stats, cache_counters, miss_types);
   else {
     os << "Cache Summary:\n";
     writeCacheSummary(os, "L1-D", cache_counters, false);

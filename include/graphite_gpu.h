@@ -56,7 +56,7 @@
 extern "C" {
 #endif
 
-#define GG_ABI_VERSION 6
+#define GG_ABI_VERSION 7
 
 typedef int gg_status;
 enum {
@@ -203,7 +203,16 @@ typedef struct gg_config {
   uint32_t basic_moving_avg;   /* queue_model/basic: moving_avg_window_size in bits 0..15
                                   (0 = 64) | GG_MAVG_* << 16 (0 = arithmetic_mean)  */
   uint32_t history_list_no_interleaving; /* queue_model/history_list/interleaving_enabled = false */
+  /* ---- miss-type classification (Cache track_miss_types, cache.cc:321-405) ---- */
+  uint32_t l1i_track_miss_types; /* l1_icache/T1/track_miss_types (false): the L1-D takes THIS flag
+                                    (L1CacheCntlr passes the L1-I one to both, l1_cache_cntlr.cc:69) */
+  uint32_t l2_track_miss_types;  /* l2_cache/T1/track_miss_types (false)               */
+  uint32_t miss_track_lines;     /* coherent mode, when tracking: address-set capacity per
+                                    (tile, cache) in lines, a power of two; 0 = 65536   */
 } gg_config;
+
+/* Miss types (Cache::MissType, cache.h:45-52), counted per (tile, cache). */
+enum { GG_MT_COLD = 0, GG_MT_CAPACITY, GG_MT_SHARING, GG_NUM_MISS_TYPES = 3 };
 
 /* Fill cfg with the reference defaults of carbon_sim.cfg for num_tiles tiles. */
 void gg_config_default(gg_config* cfg, uint32_t num_tiles);
@@ -444,6 +453,14 @@ gg_status gg_coherent_run_ranks(gg_ctx* ctx, void* nccl_comm, const gg_trace* tr
  * (either may be NULL); run_info: [GG_NUM_RUN_INFO] (may be NULL).  Tiles a
  * context does not own read 0.  Network counters: gg_noc_get_counters.      */
 gg_status gg_coherent_get_stats(gg_ctx* ctx, uint64_t* tile_stats, uint64_t* cache, uint64_t* run_info);
+/* The miss types of a coherent run with l1i_track_miss_types / l2_track_miss_types
+ * set: out [tiles][2][GG_NUM_MISS_TYPES] (L1-D, L2), zeros for an untracked
+ * cache.  Cache::getMissType (cache.cc:363-375) over the evicted /
+ * invalidated / fetched address sets that insertCacheLine and
+ * setCacheLineInfo keep (cache.cc:131-148, 228-230, 398-404).  The private
+ * (Mode P) replay does not track them: gg_cache_access_batch returns
+ * GG_ERR_UNSUPPORTED when either flag is set.                                */
+gg_status gg_coherent_get_miss_types(gg_ctx* ctx, uint64_t* out);
 
 /* The sim.out text of the context's statistics (replaces the per-tile
  * outputSummary chain: TileManager::outputSummary, tile_manager_summary.cc:

@@ -279,7 +279,65 @@ typedef struct {
   uint8_t*  lru;       /* [sets][ways]   LRUReplacementPolicy::_lru_bits_vec  */
   uint32_t* rr;        /* [sets]         RoundRobin::_replacement_index_vec   */
   uint64_t  c[GG_NUM_CACHE_COUNTERS];
+  /* miss-type tracking (track_miss_types, cache.cc:28-40,321-405): the
+   * evicted / invalidated / fetched address sets as one map address -> 3 bits */
+  int       track;
+  uint64_t* mt_key;    /* open addressing, ~0 = empty                            */
+  uint8_t*  mt_bits;   /* O_MT_EVICTED | O_MT_INVALIDATED | O_MT_FETCHED         */
+  uint64_t  mt_cap, mt_n;
+  uint64_t  mt[GG_NUM_MISS_TYPES];   /* _total_cold / capacity / sharing_misses */
 } o_cache;
+enum { O_MT_EVICTED = 1, O_MT_INVALIDATED = 2, O_MT_FETCHED = 4 };
+
+static uint64_t o_mt_slot(const o_cache* c, uint64_t addr)
+{
+  uint64_t h = (addr >> 6) * 0x9E3779B97F4A7C15ull;
+  h ^= h >> 29;
+  for (uint64_t i = h & (c->mt_cap - 1);; i = (i + 1) & (c->mt_cap - 1))
+    if (c->mt_key[i] == addr || c->mt_key[i] == ~0ull) return i;
+}
+static uint8_t o_mt_get(const o_cache* c, uint64_t addr)
+{
+  if (!c->mt_cap) return 0;
+  const uint64_t i = o_mt_slot(c, addr);
+  return c->mt_key[i] == addr ? c->mt_bits[i] : 0;
+}
+static void o_mt_put(o_cache* c, uint64_t addr, uint8_t bits)
+{
+  if (2 * (c->mt_n + 1) > c->mt_cap) {               /* grow at half load */
+    const uint64_t oc = c->mt_cap;
+    uint64_t* ok = c->mt_key; uint8_t* ob = c->mt_bits;
+    c->mt_cap = oc ? 2 * oc : 1024;
+    c->mt_key = (uint64_t*)malloc(sizeof(uint64_t) * c->mt_cap);
+    c->mt_bits = (uint8_t*)calloc(c->mt_cap, 1);
+    for (uint64_t i = 0; i < c->mt_cap; ++i) c->mt_key[i] = ~0ull;
+    for (uint64_t i = 0; i < oc; ++i)
+      if (ok[i] != ~0ull) { const uint64_t j = o_mt_slot(c, ok[i]); c->mt_key[j] = ok[i]; c->mt_bits[j] = ob[i]; }
+    free(ok); free(ob);
+  }
+  const uint64_t i = o_mt_slot(c, addr);
+  if (c->mt_key[i] != addr) { c->mt_key[i] = addr; c->mt_n++; }
+  c->mt_bits[i] = bits;
+}
+/* Cache::clearMissTypeTrackingSets (cache.cc:398-404): out of the first set
+ * that holds the address, in the order evicted, invalidated, fetched */
+static void o_mt_clear(o_cache* c, uint64_t addr)
+{
+  uint8_t b = o_mt_get(c, addr);
+  if (b & O_MT_EVICTED) b &= (uint8_t)~O_MT_EVICTED;
+  else if (b & O_MT_INVALIDATED) b &= (uint8_t)~O_MT_INVALIDATED;
+  else if (b & O_MT_FETCHED) b &= (uint8_t)~O_MT_FETCHED;
+  else return;
+  o_mt_put(c, addr, b);
+}
+/* Cache::getMissType + updateMissTypeCounters (cache.cc:363-396) */
+static void o_mt_classify(o_cache* c, uint64_t addr)
+{
+  const uint8_t b = o_mt_get(c, addr);
+  if (b & O_MT_EVICTED) c->mt[GG_MT_CAPACITY]++;
+  else if (b & (O_MT_INVALIDATED | O_MT_FETCHED)) c->mt[GG_MT_SHARING]++;
+  else c->mt[GG_MT_COLD]++;
+}
 
 static void o_cache_init(o_cache* c, uint32_t size_kb, uint32_t assoc, uint32_t line,
                          uint32_t policy, uint32_t write_back)
@@ -303,7 +361,7 @@ static void o_cache_init(o_cache* c, uint32_t size_kb, uint32_t assoc, uint32_t 
   }
 }
 
-static void o_cache_free(o_cache* c) { free(c->lines); free(c->lru); free(c->rr); }
+static void o_cache_free(o_cache* c) { free(c->lines); free(c->lru); free(c->rr); free(c->mt_key); free(c->mt_bits); }
 
 /* cache_hash_fn.h:17-18 and Cache::getTag (cache.cc:495-498) */
 static uint32_t o_set(const o_cache* c, uint64_t addr) { return (uint32_t)((addr >> c->log_line) & (c->sets - 1)); }
@@ -344,14 +402,15 @@ static int o_victim(o_cache* c, uint32_t set)
   return (int)cur;
 }
 
-/* Cache::updateMissCounters (cache.cc:321-360); track_miss_types=false (carbon_sim.cfg:228,239) */
-static void o_update_miss_counters(o_cache* c, int is_write, int miss)
+/* Cache::updateMissCounters (cache.cc:321-360), with the miss type when tracked */
+static void o_update_miss_counters(o_cache* c, uint64_t addr, int is_write, int miss)
 {
   c->c[GG_CC_ACCESSES]++;
   if (!is_write) c->c[GG_CC_READ_ACCESSES]++; else c->c[GG_CC_WRITE_ACCESSES]++;
   if (miss) {
     c->c[GG_CC_MISSES]++;
     if (!is_write) c->c[GG_CC_READ_MISSES]++; else c->c[GG_CC_WRITE_MISSES]++;
+    if (c->track) o_mt_classify(c, addr);
   }
 }
 
@@ -379,6 +438,11 @@ static int o_insert_line(o_cache* c, uint64_t addr, const o_line* in, int* evict
   *l = *in;
   o_policy_update(c, s, (uint32_t)w);
   *evicted_addr = evicted->tag << c->log_line;       /* getAddressFromTag (cache.cc:514-518) */
+  if (c->track) {                                    /* cache.cc:131-148 */
+    if (*eviction) o_mt_put(c, *evicted_addr, (uint8_t)(o_mt_get(c, *evicted_addr) | O_MT_EVICTED));
+    o_mt_clear(c, addr);
+    o_mt_put(c, addr, (uint8_t)(o_mt_get(c, addr) | O_MT_FETCHED));
+  }
   if (*eviction) {
     c->c[GG_CC_TAG_READS]++; c->c[GG_CC_DATA_READS]++;
     c->c[GG_CC_EVICTIONS]++;
@@ -406,6 +470,8 @@ static int o_set_line_info(o_cache* c, uint64_t addr, const o_line* in)
   uint32_t s = o_set(c, addr);
   int w = o_find(c, s, o_tag(c, addr));
   if (w < 0) return GG_ERR_STATE;
+  if (c->track && in->cstate == CS_I)                /* cache.cc:228-230 */
+    o_mt_put(c, addr, (uint8_t)(o_mt_get(c, addr) | O_MT_INVALIDATED));
   c->lines[(size_t)s * c->ways + w] = *in;
   c->c[GG_CC_TAG_WRITES]++;
   return 0;
@@ -432,6 +498,8 @@ oracle_cache* oracle_cache_create(const gg_config* cfg)
     /* L1-D is WRITE_THROUGH (l1_cache_cntlr.cc:55-71), L2 WRITE_BACK (l2_cache_cntlr.cc:31-46) */
     o_cache_init(&oc->t[i].l1, cfg->l1d_size_kb, cfg->l1d_assoc, cfg->line_size, cfg->l1d_policy, 0);
     o_cache_init(&oc->t[i].l2, cfg->l2_size_kb, cfg->l2_assoc, cfg->line_size, cfg->l2_policy, 1);
+    oc->t[i].l1.track = cfg->l1i_track_miss_types != 0;   /* the L1-D takes the L1-I flag (l1_cache_cntlr.cc:69) */
+    oc->t[i].l2.track = cfg->l2_track_miss_types != 0;
   }
   return oc;
 }
@@ -512,7 +580,7 @@ static uint32_t modep_access(o_tile* T, uint64_t addr, int is_write, uint64_t* e
     o_line info = o_default_line();
     o_get_line_info(&T->l1, addr, &info);
     int hit = is_write ? cs_writable(info.cstate) : cs_readable(info.cstate);
-    if (access_num == 1) o_update_miss_counters(&T->l1, is_write, !hit);
+    if (access_num == 1) o_update_miss_counters(&T->l1, addr, is_write, !hit);
     if (hit) { l1_access_cache(T, addr, is_write, err); return res; }
     if (access_num == 2) { *err = 1; return res; }   /* LOG_ASSERT_ERROR(access_num == 1 || 2) */
     res |= GG_RES_L1_MISS;
@@ -524,7 +592,7 @@ static uint32_t modep_access(o_tile* T, uint64_t addr, int is_write, uint64_t* e
     o_get_line_info(&T->l2, addr, &l2i);
     uint32_t cstate = l2i.cstate;
     int l2hit = is_write ? cs_writable(cstate) : cs_readable(cstate);  /* l2:504-527 */
-    o_update_miss_counters(&T->l2, is_write, !l2hit);
+    o_update_miss_counters(&T->l2, addr, is_write, !l2hit);
     if (l2hit) {
       if (o_access_line(&T->l2, addr, 0)) *err = 1;   /* readCacheLine */
       l2_insert_in_l1(T, addr, cstate, &res, err);
@@ -579,6 +647,14 @@ void oracle_cache_counters(const oracle_cache* oc, uint64_t* out)
   for (uint32_t t = 0; t < oc->ntiles; ++t) {
     memcpy(out + ((size_t)t * 2 + 0) * GG_NUM_CACHE_COUNTERS, oc->t[t].l1.c, sizeof(uint64_t) * GG_NUM_CACHE_COUNTERS);
     memcpy(out + ((size_t)t * 2 + 1) * GG_NUM_CACHE_COUNTERS, oc->t[t].l2.c, sizeof(uint64_t) * GG_NUM_CACHE_COUNTERS);
+  }
+}
+
+void oracle_cache_miss_types(const oracle_cache* oc, uint64_t* out)
+{
+  for (uint32_t t = 0; t < oc->ntiles; ++t) {
+    memcpy(out + ((size_t)t * 2 + 0) * GG_NUM_MISS_TYPES, oc->t[t].l1.mt, sizeof(uint64_t) * GG_NUM_MISS_TYPES);
+    memcpy(out + ((size_t)t * 2 + 1) * GG_NUM_MISS_TYPES, oc->t[t].l2.mt, sizeof(uint64_t) * GG_NUM_MISS_TYPES);
   }
 }
 

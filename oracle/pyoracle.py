@@ -101,8 +101,9 @@ def lib():
         L.oracle_coh_run.restype = ctypes.c_int
         L.oracle_coh_run.argtypes = [vp, _u64p, _u32p, _u64p, vp]
         for n in ("oracle_coh_tile_stats", "oracle_coh_cache_counters", "oracle_coh_net_counters",
-                  "oracle_coh_run_info"):
+                  "oracle_coh_run_info", "oracle_coh_miss_types", "oracle_cache_miss_types"):
             getattr(L, n).argtypes = [vp, _u64p]
+            getattr(L, n).restype = None
         _lib = L
     return _lib
 
@@ -255,6 +256,9 @@ class OracleCoherent:
     def run_info(self):
         return self._get("oracle_coh_run_info", (NUM_RUN_INFO,))
 
+    def miss_types(self):
+        return self._get("oracle_coh_miss_types", (self.cfg.num_tiles, 2, 3))
+
 
 class OracleCache:
     """Private-mode (decoupled) replay of L1-D/L2 per tile."""
@@ -286,6 +290,11 @@ class OracleCache:
         out = np.zeros(self.cfg.num_tiles * 2 * NUM_CACHE_COUNTERS, np.uint64)
         lib().oracle_cache_counters(self.h, out)
         return out.reshape(self.cfg.num_tiles, 2, NUM_CACHE_COUNTERS)
+
+    def miss_types(self):
+        out = np.zeros(self.cfg.num_tiles * 2 * 3, np.uint64)
+        lib().oracle_cache_miss_types(self.h, out)
+        return out.reshape(self.cfg.num_tiles, 2, 3)
 
     def get_line_info(self, tile, level, addr, default=None):
         li = default or LineInfo(0xFFFFFFFFFFFFFFFF, 0, 0)
