@@ -2004,10 +2004,8 @@ gg_status gg_cache_run_batch(gg_ctx* ctx, const gg_trace* tr, uint32_t* result, 
         GG_HIP(hipMemsetAsync(dbg, 0, 8 * sizeof(unsigned long long), s));
         if (dbg_on == 2) GG_HIP(hipMemsetAsync(dbg + 7, 1, 1, s));   // GG_STREAM_DEBUG=2: skip the cache step (builds with -DGG_STREAM_NOSTEP)
       }
-      // GG_STREAM_NORES=1 (diagnostics only): drop the result stores
-      static const bool nores = getenv("GG_STREAM_NORES") && atoi(getenv("GG_STREAM_NORES"));
       hipLaunchKernelGGL(fn, dim3(g.tiles), dim3((sk->ncw + 1) * GG_WAVE), lds, s, ctx->cs, g, tr->addr_dev,
-                         tr->meta_dev, (const uint64_t*)ctx->tile_off_dev, nores ? nullptr : result, evicted,
+                         tr->meta_dev, (const uint64_t*)ctx->tile_off_dev, result, evicted,
                          ctx->err_dev, dbg);
       GG_HIP(hipGetLastError());
       gg_timer_end(ctx, "cache_stream", s);
@@ -2081,10 +2079,9 @@ gg_status gg_cache_run_batch(gg_ctx* ctx, const gg_trace* tr, uint32_t* result, 
   if (evicted) { if (gg_status st = grow(&ctx->sh_ev, &ctx->sh_ev_cap, total)) return st; }
   if (nchunks) {
     gg_timer_begin(ctx, "cache_scatter", s);
-    // persistent (default): 8 one-wave workgroups per CU, a multiple of 8;
-    // GG_SCATTER_MODE=1 (A/B knob): one chunk per workgroup
-    static const int mode = getenv("GG_SCATTER_MODE") ? atoi(getenv("GG_SCATTER_MODE")) : 0;
-    const bool persist = mode != 1;
+    // persistent: 8 one-wave workgroups per CU, a multiple of 8 (measured
+    // ahead of one chunk per workgroup, which the template still builds)
+    const bool persist = true;
     const uint32_t grid = persist ? (uint32_t)std::min<uint64_t>((nchunks + 7) & ~7ull, (uint64_t)ctx->num_cus * 8)
                                   : (uint32_t)nchunks;
     const uint32_t per = std::max<uint32_t>(1, g.u1 / GG_WAVE);

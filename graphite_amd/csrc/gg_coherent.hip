@@ -113,7 +113,7 @@ struct CP {
   uint32_t cache_lds_off, cache_lds_bytes; // k_c_persist<true>: the tile's cache state in LDS after the step's
   uint32_t touch_each;                     // hit runs touch LRU rows one record at a time (> 16 ways; GG_COH_TOUCH_EACH=1)
   uint32_t walk_wide;                      // pipelined walkers scan every packet (the > 128-packet path; GG_COH_WALK_WIDE=1)
-  uint32_t no_hit_runs;                    // GG_COH_NO_HIT_RUNS=1: every record through app_access
+  uint32_t no_hit_runs;                    // 1: every record through app_access (hit runs off; 0 in the build)
   uint32_t mt1, mt2, mt_log;               // miss-type tracking of the L1-D / L2 (cfg flags), log2 set capacity
   uint64_t lat_l1d, lat_l1t, lat_l2d, lat_l2t, lat_dir, gap_ps, dram_proc, dram_cost;
   NocParams np;
@@ -2956,8 +2956,7 @@ static gg_status coh_alloc(gg_ctx* ctx)
     P.touch_each = te && atoi(te) ? 1u : 0u;
     const char* ww = getenv("GG_COH_WALK_WIDE");
     P.walk_wide = ww && atoi(ww) ? 1u : 0u;
-    const char* nh = getenv("GG_COH_NO_HIT_RUNS");
-    P.no_hit_runs = nh && atoi(nh) ? 1u : 0u;
+    P.no_hit_runs = 0u;
   }
   C->step_lds = sizeof(StepLds);
   {

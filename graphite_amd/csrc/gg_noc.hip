@@ -2069,13 +2069,13 @@ struct gg_noc_state {
   uint32_t *cur = nullptr, *keys = nullptr, *ids = nullptr;
   Ev* heap = nullptr;
   uint32_t* counts = nullptr; uint32_t* cursor = nullptr; uint64_t* off = nullptr; uint32_t nb_cap = 0;
-  bool staged = true;   // LDS-staged stage kernels where the queues fit (GG_NOC_STAGED=0: HBM-resident, A/B)
+  bool staged = true;   // LDS-staged stage kernels where the queues fit (else HBM-resident)
   TEv* theap = nullptr; uint32_t* bidx = nullptr; uint64_t tcap = 0, bcap = 0;   // broadcast-tree walk scratch
   unsigned long long* prof = nullptr;             // GG_NOC_PROFILE=1: k_chain_sweep phase cycles (diagnostics)
   SK* pscr = nullptr; uint64_t pscr_cap = 0;       // k_chain_pipe: per packet 3 x positions pool / incoming slots
   uint8_t* tp = nullptr; uint64_t tp_bytes = 0;     // k_tree_pool: TpBufs
   uint8_t* tg = nullptr; uint64_t tg_bytes = 0;     // k_tree_setup / k_tree_grid: TgBufs
-  bool pipe = true;                               // GG_NOC_PIPE=0: the position sweep for every chain (A/B)
+  bool pipe = true;                               // pipelined chains where they fit (else the position sweep)
 };
 
 gg_status gg_noc_alloc(gg_ctx* ctx)
@@ -2099,8 +2099,6 @@ gg_status gg_noc_alloc(gg_ctx* ctx)
   P.qtype = c.queue_model_type;
   P.qaux = hq_aux(c.queue_model_type, c.basic_moving_avg, c.history_list_no_interleaving);
   if (gg_status e = gg_check_queue_model(c.queue_model_type, P.qaux, P.max_size)) return e;
-  S->staged = !(getenv("GG_NOC_STAGED") && atoi(getenv("GG_NOC_STAGED")) == 0);
-  S->pipe = !(getenv("GG_NOC_PIPE") && atoi(getenv("GG_NOC_PIPE")) == 0);
   if (getenv("GG_NOC_PROFILE") && atoi(getenv("GG_NOC_PROFILE"))) {
     GG_HIP(hipMalloc((void**)&S->prof, 32 * sizeof(unsigned long long)));
     GG_HIP(hipMemset(S->prof, 0, 32 * sizeof(unsigned long long)));
