@@ -414,26 +414,19 @@ def fft_section(args, dev):
     + emesh_hop_counter) on the GPU; bit-exact against the C oracle, whose run
     is the CPU baseline.  The trace is the reference's own fft.C (-p16
     -m<fft_m>) captured by tools/fft_trace when that capture exists
-    (graphite_amd.capture.REAL_FFT_TRACES: -m20 written by build(), -m14
-    committed), else the source-level six-step lookalike (capture_fft)."""
+    (graphite_amd.capture.REAL_FFT_TRACES: -m20 written by build(), else the
+    committed -m14)."""
     import torch
     from graphite_amd import config as C
     from graphite_amd import backend as B
     from graphite_amd import capture as cp
     m, p = args.fft_m, 16
     path = cp.REAL_FFT_TRACES.get(m)
-    if not (path and os.path.exists(path)) and os.path.exists(cp.REAL_FFT_TRACES[14]):
+    if not (path and os.path.exists(path)):
         m, path = 14, cp.REAL_FFT_TRACES[14]          # the -m20 capture is written by build() only
-    if path and os.path.exists(path):
-        a, meta, offs, bars = cp.load_fft_trace(path)
-        fft_ok, src = None, ("the reference's tests/benchmarks/fft/fft.C -p%d -m%d captured by tools/fft_trace "
-                             "(heap accesses, 1 cycle per access, %d BARRIER calls per thread as barrier records)"
-                             % (p, m, len(bars[0])))
-    else:
-        m = min(m, 14)
-        a, meta, offs, X = cp.capture_fft(m, p)
-        fft_ok = bool(np.abs(X - np.fft.fft(cp.fft_input(m))).max() <= 1e-9 * np.abs(X).max())
-        src = "captured six-step FFT lookalike of 2^%d points (graphite_amd/capture)" % m
+    a, meta, offs, bars = cp.load_fft_trace(path)
+    src = ("the reference's tests/benchmarks/fft/fft.C -p%d -m%d captured by tools/fft_trace "
+           "(heap accesses, 1 cycle per access, %d BARRIER calls per thread as barrier records)" % (p, m, len(bars[0])))
     cfg = C.default_config(p, net_model=C.NET_EMESH_HOP_COUNTER)
     be = B.Backend(cfg)
     addr = torch.from_numpy(a.view(np.int64)).to(dev)
@@ -447,7 +440,7 @@ def fft_section(args, dev):
     st, cc, ri = be.coherent_stats()
     res = {"workload": "configs[0]: %s, %d threads = %d tiles, %d accesses, pr_l1_pr_l2_dram_directory_msi + "
                        "emesh_hop_counter" % (src, p, p, len(a)),
-           "value": len(a) / dt, "unit": "accesses/s", "seconds": dt, "fft_correct": fft_ok,
+           "value": len(a) / dt, "unit": "accesses/s", "seconds": dt,
            "steps": int(ri[C.RUN_INFO.index("steps")]), "simulated_ns": int(st[:, 0].max()) // 1000}
     if not args.no_verify:
         from oracle import pyoracle as po

@@ -108,6 +108,7 @@ __global__ void __launch_bounds__(kScanBlock) k_split_write(const uint64_t* addr
   for (uint32_t k = 0; k < w; ++k) before += wsum[k];
   const uint64_t f = before + v - x;
   if (i >= n) return;
+  if (meta[i] == GG_META_BARRIER) { atomicOr(err, GG_DERR_BARRIER); return; }   // not an access: insert after the split
   first[i] = f;
   if (i == n - 1) first[n] = f + x;
   if (!laddr || x == 0) return;
@@ -115,7 +116,7 @@ __global__ void __launch_bounds__(kScanBlock) k_split_write(const uint64_t* addr
   uint64_t gap = (meta[i] & 0x7FFFFFFFu) >> 1;
   const uint64_t t0 = tile_start(toff, tiles, i);
   for (uint64_t j = i; j > t0 && size[j - 1] == 0; --j) gap += (meta[j - 1] & 0x7FFFFFFFu) >> 1;
-  if (gap >= (1ull << 30)) { atomicOr(err, GG_DERR_RANGE); return; }
+  if (gap >= (1ull << 30)) { atomicOr(err, GG_DERR_RANGE); return; }   // (a BARRIER before it is flagged by its own thread)
   const uint64_t ba = addr[i] - addr[i] % line;
   const uint32_t wr = meta[i] & GG_META_WRITE;
   for (uint64_t k = 0; k < x && f + k < cap; ++k) {
@@ -189,6 +190,9 @@ gg_status gg_split_accesses(const uint64_t* addr_dev, const uint32_t* size_dev, 
       for (uint32_t t = 0; t <= tiles; ++t)
         GG_HIP(hipMemcpyAsync(&line_tile_offsets[t], first_dev + tile_offsets[t], sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     GG_HIP(hipStreamSynchronize(s));
+    if (e & GG_DERR_BARRIER)
+      return gg_fail(GG_ERR_UNSUPPORTED, "gg_split_accesses: a BARRIER record in the access trace (insert barriers "
+                     "into the line records after the split)");
     if (e) return gg_fail(GG_ERR_INVALID, "gg_split_accesses: carried gap above 2^30 cycles");
     if (line_addr_dev && *num_lines > cap)
       return gg_fail(GG_ERR_INVALID, "gg_split_accesses: %llu lines, capacity %llu", (unsigned long long)*num_lines,

@@ -150,7 +150,7 @@ __global__ void k_state_reset(gg_cache_state cs, gg_geom g)
 
 // Pass 1 of the stable (tile, L1-D set) partition: per-chunk set histogram.
 __global__ __launch_bounds__(256) void k_shard_hist(const uint64_t* __restrict__ addr,
-    const uint32_t* __restrict__ chunk_tile, const uint64_t* __restrict__ chunk_start,
+    const uint32_t* __restrict__ meta, const uint32_t* __restrict__ chunk_tile, const uint64_t* __restrict__ chunk_start,
     const uint32_t* __restrict__ chunk_len, uint32_t* __restrict__ cnt, gg_geom g, uint32_t* err)
 {
   __shared__ uint32_t h[1024];
@@ -163,9 +163,11 @@ __global__ __launch_bounds__(256) void k_shard_hist(const uint64_t* __restrict__
   for (uint32_t i = threadIdx.x; i < len; i += blockDim.x) {
     const uint64_t a = addr[start + i];
     bad |= (a >= g.addr_limit) ? 1u : 0u;
+    bad |= meta[start + i] == GG_META_BARRIER ? 2u : 0u;              // coherent-mode records only
     atomicAdd(&h[(a >> g.log_line) & (g.u1 - 1)], 1u);
   }
-  if (bad) atomicOr(err, GG_DERR_RANGE);
+  if (bad & 1u) atomicOr(err, GG_DERR_RANGE);
+  if (bad & 2u) atomicOr(err, GG_DERR_BARRIER);
   __syncthreads();
   for (uint32_t s = threadIdx.x; s < g.u1; s += blockDim.x) cnt[(uint64_t)c * g.u1 + s] = h[s];
 }
@@ -1330,6 +1332,7 @@ __global__ __launch_bounds__((NCW + 1) * GG_WAVE) void k_cache_stream(gg_cache_s
         const uint32_t j = c + k * GG_WAVE + lane;
         const bool valid = j < n;
         bad |= (valid && pa[k] >= g.addr_limit) ? 1u : 0u;
+        bad |= (valid && pm[k] == GG_META_BARRIER) ? 2u : 0u;      // coherent-mode records only
         const uint64_t line = pa[k] >> g.log_line;
         set[k] = valid ? (uint32_t)line & (U1 - 1) : U1;             // U1 = no record
         key[k] = ((uint64_t)(uint32_t)(line >> g.log_l2) << 32) | (j << (1 + log_s2)) |
@@ -1416,7 +1419,8 @@ __global__ __launch_bounds__((NCW + 1) * GG_WAVE) void k_cache_stream(gg_cache_s
     }
     __builtin_amdgcn_s_waitcnt(kLgkm0);
     if (lane == 0) st32(donep, 1u);
-    if (__ballot(bad) && lane == 0) atomicOr(err, GG_DERR_RANGE);
+    if (__ballot(bad & 1u) && lane == 0) atomicOr(err, GG_DERR_RANGE);
+    if (__ballot(bad & 2u) && lane == 0) atomicOr(err, GG_DERR_BARRIER);
     if (hung && lane == 0) atomicOr(err, GG_DERR_CAP);
     if (dbg && lane == 0) {
       atomicAdd(&dbg[0], (unsigned long long)d_batch);
@@ -2056,7 +2060,7 @@ gg_status gg_cache_run_batch(gg_ctx* ctx, const gg_trace* tr, uint32_t* result, 
 
   if (nchunks) {
     gg_timer_begin(ctx, "cache_hist", s);
-    hipLaunchKernelGGL(k_shard_hist, dim3((uint32_t)nchunks), dim3(256), 0, s, tr->addr_dev, ctx->chunk_tile,
+    hipLaunchKernelGGL(k_shard_hist, dim3((uint32_t)nchunks), dim3(256), 0, s, tr->addr_dev, tr->meta_dev, ctx->chunk_tile,
                        ctx->chunk_start, ctx->chunk_len, ctx->chunk_cnt, g, ctx->err_dev);
     GG_HIP(hipGetLastError());
   }

@@ -247,6 +247,9 @@ static gg_status check_device_errors(gg_ctx* ctx)
 {
   uint32_t e = 0;
   GG_HIP(hipMemcpy(&e, ctx->err_dev, sizeof(e), hipMemcpyDeviceToHost));
+  if (e & GG_DERR_BARRIER)
+    return gg_fail(GG_ERR_UNSUPPORTED, "a BARRIER record (GG_META_BARRIER) in a private-cache trace: barriers are "
+                   "released by gg_coherent_run only; the batch's results and counters are not valid");
   if (e & GG_DERR_RANGE) return gg_fail(GG_ERR_RANGE, "a trace address is beyond the compressed-tag range (%#llx)",
                                         (unsigned long long)ctx->g.addr_limit);
   if (e & GG_DERR_STATE) return gg_fail(GG_ERR_STATE, "cache state the reference would reject (LOG_ASSERT_ERROR)");

@@ -292,12 +292,13 @@ struct Cache {
         return (base + l) & (cap - 1);
       }
     }
-    err |= GG_DERR_CAP;                                                // the table is full
+    err |= GG_DERR_CAP;                                                // the table is full (miss_track_lines)
     bits = 0;
-    return 0;
+    return ~0ull;
   }
   __device__ __forceinline__ void mt_put(uint64_t i, uint64_t a, uint32_t bits)
   {
+    if (i == ~0ull) return;                                            // full: the run is flagged, no slot is overwritten
     if (ln == 0) mtab[i] = a | bits;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -3040,7 +3041,8 @@ static gg_status coh_check(gg_ctx* ctx)
   uint32_t e = 0;
   GG_HIP(hipMemcpy(&e, ctx->err_dev, sizeof(e), hipMemcpyDeviceToHost));
   if (e & GG_DERR_CAP) return gg_fail(GG_ERR_UNSUPPORTED, "coherent mode: a device capacity (records / inbox / "
-                                      "request queue / replaced entries / call chain / segment) was exceeded");
+                                      "request queue / replaced entries / call chain / segment, or with miss-type "
+                                      "tracking the miss_track_lines address table of a tile) was exceeded");
   if (e & GG_DERR_STATE) return gg_fail(GG_ERR_STATE, "coherent mode: a state the reference would reject "
                                         "(LOG_ASSERT_ERROR / assert)");
   return GG_OK;

@@ -16,7 +16,8 @@
 // kTaskRecords records of one tile, one wave each, 4 x 64 records in flight
 // per iteration; a CONT record takes the WRITE bit of the access it belongs
 // to from the last head before it (ballot over the wave, carried across
-// iterations, looked up behind the task's first record).  A BARRIER record
+// iterations, looked up behind the task's first record; a CONT record at the
+// tile's start or right after a BARRIER is a head, as in the oracle).  A BARRIER record
 // with a stall is the SyncInstruction of sync_client.cc:306-314 (dynamic:
 // curr_time += stall, CoreModel::updateDynamicInstructionCounters,
 // core_model.cc:237-250).
@@ -41,9 +42,12 @@ __global__ void __launch_bounds__(64 * kCoreWaves) k_core_model(const uint32_t* 
   const CoreTask tk = tasks[w];
   // the access the task's first record belongs to: its head is the last
   // non-CONT record at or before it (CONT records follow their head)
+  // (a CONT record right after a BARRIER or at the tile's start has no head
+  // before it: it is a head itself, as in the oracle's scan)
   uint64_t j = tk.begin;
-  while (j > tk.tile_begin && (meta[j] & GG_META_CONT) && meta[j] != GG_META_BARRIER) --j;
+  while (j > tk.tile_begin && (meta[j] & GG_META_CONT) && meta[j] != GG_META_BARRIER && meta[j - 1] != GG_META_BARRIER) --j;
   uint32_t carry = rec_write(meta[j]);
+  uint32_t prevm = tk.begin > tk.tile_begin ? meta[tk.begin - 1] : GG_META_BARRIER;   // the record before lane 0's
   uint64_t n_ins = 0, ex = 0, rd = 0, wr = 0, ns = 0, sy = 0;
   const uint64_t below = ln == 63 ? ~0ull : ((2ull << ln) - 1);   // lanes <= ln
   for (uint64_t b = tk.begin; b < tk.end; b += 256) {
@@ -58,7 +62,10 @@ __global__ void __launch_bounds__(64 * kCoreWaves) k_core_model(const uint32_t* 
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const bool bar = m[u] == GG_META_BARRIER;            // a released barrier: the SyncInstruction
-      const bool head = !(m[u] & GG_META_CONT);
+      const uint32_t up = (uint32_t)__shfl((int)m[u], (int)((ln + 63) & 63));
+      const uint32_t pm = ln == 0 ? prevm : up;            // the previous record's meta
+      prevm = (uint32_t)__shfl((int)m[u], 63);
+      const bool head = !(m[u] & GG_META_CONT) || pm == GG_META_BARRIER;
       const uint64_t heads = __ballot(head);
       const uint64_t mine = heads & below;
       const uint32_t own = rec_write(m[u]);

@@ -28,6 +28,7 @@
 #define GG_DERR_RANGE 1u   // address beyond the compressed-tag range
 #define GG_DERR_STATE 2u   // the reference would LOG_ASSERT_ERROR on this state
 #define GG_DERR_CAP 4u     // a device-side capacity (messages, queues, inbox) was exceeded
+#define GG_DERR_BARRIER 8u // a BARRIER record (GG_META_BARRIER) reached a path that has no barriers (Mode P)
 
 // Geometry derived from gg_config (cache.cc:44, cache_hash_fn.h:11).
 struct gg_geom {

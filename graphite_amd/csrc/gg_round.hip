@@ -103,7 +103,11 @@ gg_status gg_round_exchange(gg_ctx* ctx, void* nccl_comm, void* stream, uint64_t
                    (R + 1) * per, c.shard_begin, k1);
   hipSetDevice(ctx->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (s != ctx->last_stream) return gg_fail(GG_ERR_INVALID, "gg_round_exchange needs the stream of gg_coherent_begin");
+  // The checks above and these two return before any RCCL call: they depend
+  // only on arguments and on gg_coherent_begin having run, which every rank of
+  // one program gets identically, so they fail on every rank at once (the
+  // send-buffer allocation of the first round is the one rank-local failure
+  // that cannot be turned into the round's error flag: there is no buffer).
   const uint64_t region = gg_coherent_msg_cap(ctx);
   if (!region) return gg_fail(GG_ERR_INVALID, "gg_coherent_begin first");
   RoundBufs* B = nullptr;
@@ -111,16 +115,20 @@ gg_status gg_round_exchange(gg_ctx* ctx, void* nccl_comm, void* stream, uint64_t
   const uint64_t slot = slot_records(region);
   const size_t sbytes = sizeof(gg_cmsg) * (slot + 1);
 
-  // the quantum and the export; a failure turns into the error flag of the round
+  // the quantum and the export; a failure (a wrong stream included) turns into
+  // the error flag of the round, which every rank still takes part in
   uint32_t herr = 0;
   std::string emsg;
   gg_status est = GG_OK;
-  if ((est = gg_coh_quantum_async(ctx, q)) || (est = gg_coh_export_slots(ctx, B->send, (uint32_t)W, per, region))) {
+  const bool wrong_stream = s != ctx->last_stream;        // the context's kernels run on last_stream
+  if (wrong_stream) est = gg_fail(GG_ERR_INVALID, "gg_round_exchange needs the stream of gg_coherent_begin");
+  if (est || (est = gg_coh_quantum_async(ctx, q)) || (est = gg_coh_export_slots(ctx, B->send, (uint32_t)W, per, region))) {
     herr = GG_DERR_STATE;
     emsg = gg_last_error();
     (void)hipMemsetAsync(B->send, 0, sizeof(gg_cmsg) * (size_t)W * (region + 1), s);   // nothing to send
   }
   if (gg_status st = gg_coh_round_status(ctx, B->send, (uint32_t)W, region, herr, B->dv)) return st;
+  if (wrong_stream) GG_HIP(hipStreamSynchronize(ctx->last_stream));   // the status words before RCCL reads them on s
   // ONE group: every peer's fixed slot; then the status all-reduces
   GG_NCCL(ncclGroupStart());
   for (int r = 0; r < W; ++r) {
@@ -133,6 +141,10 @@ gg_status gg_round_exchange(gg_ctx* ctx, void* nccl_comm, void* stream, uint64_t
   GG_NCCL(ncclAllReduce(B->dv + 3, B->dv + 3, 2, ncclUint64, ncclMax, comm, s));
   GG_NCCL(ncclAllReduce(B->dv + 5, B->dv + 5, 1, ncclUint64, ncclMin, comm, s));
   GG_NCCL(ncclGroupEnd());
+  if (wrong_stream) {                                      // this rank failed: nothing to import
+    GG_HIP(hipStreamSynchronize(s));
+    return gg_fail(est, "%s", emsg.c_str());
+  }
   // the received records (skipped on the device when any rank failed), the counts, one sync
   if (gg_status st = gg_coh_import_slots(ctx, B->recv, (uint32_t)W, region, 0, slot, true, B->dv + 3)) return st;
   hipLaunchKernelGGL(k_slot_counts, dim3(1), dim3(64), 0, s, B->send, B->recv, (uint32_t)W, region, B->dv + kDv);

@@ -105,7 +105,12 @@ enum { GG_LOC_INVALID = 0, GG_LOC_L1I = 2, GG_LOC_L1D = 3 };
  * quantum boundary after the last arrival and writes the record's access
  * word as (stall_ps << 2) | GG_LVL_SYNC.  Only gg_coherent_run takes traces
  * with barriers (the per-quantum and multi-rank entry points return
- * GG_ERR_UNSUPPORTED).                                                      */
+ * GG_ERR_UNSUPPORTED; the private-cache batch flags one in the device error
+ * word, so the next gg_cache_get_counters returns GG_ERR_UNSUPPORTED;
+ * gg_split_accesses rejects one in its access trace: insert barriers into
+ * the line records it writes).  Barriers carry no id or count: one global
+ * barrier whose count is "every tile with an unfinished trace", released at
+ * the quantum boundary after its last arrival.                 */
 #define GG_META_BARRIER 0xFFFFFFFFu
 
 /* Per-access result word written by gg_cache_access_batch: one flag per 4-bit
@@ -208,7 +213,13 @@ typedef struct gg_config {
                                     (L1CacheCntlr passes the L1-I one to both, l1_cache_cntlr.cc:69) */
   uint32_t l2_track_miss_types;  /* l2_cache/T1/track_miss_types (false)               */
   uint32_t miss_track_lines;     /* coherent mode, when tracking: address-set capacity per
-                                    (tile, cache) in lines, a power of two; 0 = 65536   */
+                                    (tile, cache) in lines, a power of two; 0 = 65536.
+                                    The sets keep every line ever fetched, evicted or
+                                    invalidated, so size it from the trace's per-tile
+                                    footprint; allocated when tracking is on:
+                                    tiles x 2 x lines x 8 B (65536: 1 GiB at 1024 tiles,
+                                    4 GiB at 4096).  A full table stops the run with
+                                    GG_ERR_UNSUPPORTED (no set entry is overwritten). */
 } gg_config;
 
 /* Miss types (Cache::MissType, cache.h:45-52), counted per (tile, cache). */

@@ -185,3 +185,41 @@ def test_gpu_core_model_errors():
     acc = torch.zeros(8, dtype=torch.int64, device="cuda")
     with pytest.raises(B.GGError):
         be.core_model_run(meta, np.array([0, 4, 2, 6, 8], np.uint64), acc)   # offsets decrease
+
+
+def orphan_cont(T, per_tile, seed):
+    """synthetic() with CONT records that have no head before them: at a
+    tile's start, at a task edge, and right after a BARRIER record."""
+    meta, acc, offs = synthetic(T, per_tile, seed, cont_frac=0.5)
+    rng = np.random.default_rng(seed + 1)
+    for t in range(T):
+        b = int(offs[t])
+        meta[b] = np.uint32(CONT | (t & 1))                       # the tile starts with a CONT record
+        for k in rng.integers(1, per_tile - 1, 6):
+            meta[b + k] = np.uint32(BARRIER)
+            meta[b + k + 1] = np.uint32(CONT | ((t + int(k)) & 1))  # a CONT record right after a BARRIER
+    if per_tile > 16384:
+        meta[16383] = np.uint32(BARRIER)                          # ... on the last record of a device task
+        meta[16384] = np.uint32(CONT)
+    return meta, acc, offs
+
+
+def test_oracle_core_model_orphan_cont():
+    from oracle import pyoracle as po
+    meta, acc, offs = orphan_cont(4, 900, 5)
+    np.testing.assert_array_equal(po.core_model(meta, acc, offs, 1.0), py_core_model(meta, acc, offs, 1.0))
+
+
+@pytest.mark.gpu
+def test_gpu_core_model_orphan_cont():
+    """A CONT record with no head before it (the tile's first record, or the
+    one after a BARRIER) is an instruction of its own, as in the oracle."""
+    from graphite_amd import backend as B
+    from oracle import pyoracle as po
+    from tests.gpu_util import torch_dev, to_dev
+    torch = torch_dev()
+    for T, per_tile in ((5, 900), (2, 16384 * 2 + 5)):
+        meta, acc, offs = orphan_cont(T, per_tile, 7 + T)
+        be = B.Backend(C.default_config(T))
+        be.core_model_run(to_dev(torch, meta, torch.int32), offs, to_dev(torch, acc, torch.int64))
+        np.testing.assert_array_equal(be.core_stats(), po.core_model(meta, acc, offs, 1.0))

@@ -195,3 +195,32 @@ def test_gpu_barriers_on_hotspot(T, N, net, K):
     np.testing.assert_array_equal(st, oc.tile_stats())
     np.testing.assert_array_equal(cc, oc.cache_counters())
     np.testing.assert_array_equal(be.noc_counters(), oc.net_counters())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kern", [0, 1, 2])       # streaming, sharded generic, sharded lean
+def test_gpu_private_mode_rejects_barriers(kern):
+    """The private-cache batch has no barriers: a BARRIER record (the FFT
+    trace loaded with barriers=True) is reported as GG_ERR_UNSUPPORTED by the
+    next counter read instead of being replayed as a WRITE to address 0; the
+    same trace without them replays normally.  gg_split_accesses rejects
+    BARRIER records in its access trace too."""
+    from graphite_amd import backend as B
+    from tests.gpu_util import torch_dev, to_dev
+    torch = torch_dev()
+    for barriers in (True, False):
+        a, meta, offs, _ = cp.load_fft_trace(cp.REAL_FFT_TRACES[10], barriers=barriers)
+        cfg = C.default_config(16)
+        cfg.replay_kernel = kern
+        be = B.Backend(cfg)
+        r = torch.zeros(len(a), dtype=torch.int32, device="cuda")
+        be.cache_access_batch(to_dev(torch, a, torch.int64), to_dev(torch, meta, torch.int32), offs, r)
+        if barriers:
+            with pytest.raises(B.GGError, match="BARRIER"):
+                be.cache_counters()
+        else:
+            assert int(be.cache_counters()[:, 0, C.CACHE_COUNTERS.index("accesses")].sum()) == len(a)
+    a, meta, offs, _ = cp.load_fft_trace(cp.REAL_FFT_TRACES[10], barriers=True)
+    size = torch.full((len(a),), 8, dtype=torch.int32, device="cuda")
+    with pytest.raises(B.GGError, match="BARRIER"):
+        B.split_accesses(to_dev(torch, a, torch.int64), size, to_dev(torch, meta, torch.int32), offs)

@@ -331,17 +331,6 @@ def test_coherent_two_ranks_one_gpu(tmp_path):
     np.testing.assert_array_equal(np.load(tmp_path / "stats.npy"), ref[1])
 
 
-@pytest.mark.parametrize("m,p,net", [(10, 16, C.NET_EMESH_HOP_COUNTER), (8, 16, C.NET_EMESH_HOP_BY_HOP)])
-def test_coherent_fft_capture_matches_oracle(m, p, net):
-    """configs[0]: the captured SPLASH-2-style FFT trace (graphite_amd.capture)
-    on 16 tiles, MSI directory + EMesh, GPU vs oracle bit-exact."""
-    from graphite_amd import capture as cp
-    a, meta, offs, _ = cp.capture_fft(m, p)
-    cfg = C.default_config(p, net_model=net)
-    g = _compare(cfg, a, meta, offs)
-    assert g[1][:, C.TILE_STATS.index("l2_misses")].sum() > 0
-
-
 @pytest.mark.parametrize("qtype,aux,net", [
     (C.QM_HISTORY_LIST, 0, C.NET_EMESH_HOP_COUNTER),
     (C.QM_BASIC, 0, C.NET_EMESH_HOP_COUNTER),

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""configs[0] FFT capture through gg_coherent_run once (GG_COH_PROFILE=1 prints the phase profile)."""
+"""configs[0]: the reference FFT (tools/fft_trace capture, m in 10 / 14 / 20) through gg_coherent_run once (GG_COH_PROFILE=1 prints the phase profile)."""
 import os
 import sys
 import time
@@ -16,7 +16,7 @@ def main():
     from graphite_amd import capture as cp
     m = int(sys.argv[1]) if len(sys.argv) > 1 else 14
     runs = int(sys.argv[2]) if len(sys.argv) > 2 else 2
-    a, meta, offs, X = cp.capture_fft(m, 16)
+    a, meta, offs, _ = cp.load_fft_trace(cp.REAL_FFT_TRACES[m])
     cfg = C.default_config(16, net_model=C.NET_EMESH_HOP_COUNTER)
     be = B.Backend(cfg)
     addr = torch.from_numpy(a.view(np.int64)).cuda()
