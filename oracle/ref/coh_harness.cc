@@ -815,25 +815,48 @@ static void write_bin(const string& name, const void* p, size_t bytes)
   fclose(f);
 }
 
+// a captured trace (workload 2): tile-major records and tile offsets, raw
+// little-endian files <prefix>.addr (u64), .meta (u32), .offs (u64, T + 1)
+struct RawTrace { vector<UInt64> addr, offs; vector<UInt32> meta; };
+template <class V> static void read_raw(const string& path, V& v)
+{
+  FILE* f = fopen(path.c_str(), "rb");
+  CHECK(f);
+  fseek(f, 0, SEEK_END);
+  const long bytes = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  v.resize((size_t)bytes / sizeof(v[0]));
+  CHECK(fread(&v[0], sizeof(v[0]), v.size(), f) == v.size());
+  fclose(f);
+}
+
 static void run_case(FILE* man, bool first, const char* name, UInt32 T, UInt32 N, UInt32 hot, UInt32 K, UInt32 net,
-                     UInt32 dir_entries, UInt32 dir_assoc, UInt32 l2_assoc = 8, UInt32 workload = 0)
+                     UInt32 dir_entries, UInt32 dir_assoc, UInt32 l2_assoc = 8, UInt32 workload = 0,
+                     const RawTrace* raw = NULL)
 {
   H.T = T; H.K = K; H.net = net; H.dir_entries = dir_entries; H.dir_assoc = dir_assoc; H.quantum_ps = 1000000;
   H.l2_assoc = l2_assoc; H.workload = workload;
   build_shard_map();
   g_t.clear(); g_t.resize(T); g_step.clear(); g_bnd.clear(); g_cc.clear(); g_dc.clear(); g_dram.clear();
-  vector<UInt64> addr((size_t)T * N); vector<UInt32> meta((size_t)T * N); vector<UInt64> out((size_t)T * N, 0);
-  for (UInt32 t = 0; t < T; ++t) {
+  vector<UInt64> offs(T + 1);
+  for (UInt32 t = 0; t <= T; ++t) offs[t] = raw ? raw->offs[t] : (UInt64)t * N;
+  const size_t nrec = (size_t)offs[T];
+  vector<UInt64> addr(nrec); vector<UInt32> meta(nrec); vector<UInt64> out(nrec, 0);
+  if (raw) {
+    CHECK(raw->offs.size() == T + 1 && raw->addr.size() == nrec && raw->meta.size() == nrec);
+    addr = raw->addr; meta = raw->meta;
+  }
+  for (UInt32 t = 0; t < T && !raw; ++t) {
     if (workload == 1) gen_stress(t, N, T, &addr[(size_t)t * N], &meta[(size_t)t * N]);
     else gen_hotspot(t, N, hot, &addr[(size_t)t * N], &meta[(size_t)t * N]);
   }
-  g_addr = &addr[0]; g_meta = &meta[0]; g_out = &out[0];
+  g_addr = nrec ? &addr[0] : NULL; g_meta = nrec ? &meta[0] : NULL; g_out = nrec ? &out[0] : NULL;
   for (UInt32 t = 0; t < T; ++t) {
     HTile& X = g_t[t];
     X.tile = new Tile(t);
     X.mm = (MSI::MemoryManager*)X.tile->getMemoryManager();
     X.mm->enableModels();                                  // synthetic_memory.cc:96
-    X.rec = (UInt64)t * N; X.rec_end = X.rec + N; X.clk = 0; X.blocked = false; X.resumed_by_handler = false;
+    X.rec = offs[t]; X.rec_end = offs[t + 1]; X.clk = 0; X.blocked = false; X.resumed_by_handler = false;
     X.pend_start = 0; X.seq = 0;
     memset(X.st, 0, sizeof(X.st)); memset(X.net, 0, sizeof(X.net));
     X.stack.resize(T > 256 ? 1 << 18 : 1 << 20);
@@ -867,9 +890,10 @@ static void run_case(FILE* man, bool first, const char* name, UInt32 T, UInt32 N
   write_bin("coh_" + n + "_cache.u64", &cc[0], cc.size() * 8);
   write_bin("coh_" + n + "_net.u64", &nc[0], nc.size() * 8);
   fprintf(man, "%s  \"%s\": {\"tiles\": %u, \"per_tile\": %u, \"hot_lines\": %u, \"num_shards\": %u, \"net\": %u, "
-          "\"dir_entries\": %u, \"dir_assoc\": %u, \"l2_assoc\": %u, \"workload\": \"%s\", \"quanta\": %llu, "
-          "\"steps\": %llu}",
-          first ? "" : ",\n", name, T, N, hot, K, net, dir_entries, dir_assoc, l2_assoc, workload ? "stress" : "hotspot",
+          "\"dir_entries\": %u, \"dir_assoc\": %u, \"l2_assoc\": %u, \"workload\": \"%s\", \"records\": %llu, "
+          "\"quanta\": %llu, \"steps\": %llu}",
+          first ? "" : ",\n", name, T, N, hot, K, net, dir_entries, dir_assoc, l2_assoc,
+          workload == 2 ? "fft_real_p16_m10" : workload ? "stress" : "hotspot", (unsigned long long)nrec,
           (unsigned long long)quanta, (unsigned long long)steps);
   printf("  coh %-10s tiles %u x %u: %llu quanta, %llu steps\n", name, T, N, (unsigned long long)quanta,
          (unsigned long long)steps);
@@ -895,6 +919,17 @@ int main(int argc, char** argv)
   run_case(man, false, "stress256w16", 256, 96, 0, 8, 1, 0, 16, 16, 1);
   // configs[3] scale: 1024 tiles x 8 logical shards, 256 hot lines, reduced length
   run_case(man, false, "shard1024", 1024, 24, 256, 8, 1, 0, 16);
+  // configs[0]: the reference's own fft.C (-p16 -m10) as captured by
+  // tools/fft_trace (tests/golden/fft_real_p16_m10.npz, accesses only: the
+  // BARRIER release is restated, not the reference's SyncServer), 16 tiles,
+  // emesh_hop_counter; exported to raw files by make_golden.sh
+  if (argc > 2) {
+    RawTrace fft;
+    read_raw(string(argv[2]) + ".addr", fft.addr);
+    read_raw(string(argv[2]) + ".meta", fft.meta);
+    read_raw(string(argv[2]) + ".offs", fft.offs);
+    run_case(man, false, "fft10", 16, 0, 0, 1, 1, 0, 16, 8, 2, &fft);
+  }
   fprintf(man, "\n}\n");
   fclose(man);
   return 0;

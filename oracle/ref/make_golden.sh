@@ -4,8 +4,11 @@
 set -e
 HERE=$(cd "$(dirname "$0")" && pwd)
 REF=${REF:-/root/reference}
+GOLD="$HERE/../../tests/golden"
 make -s -C "$HERE" REF="$REF"
-mkdir -p "$HERE/../../tests/golden"
-"$HERE/../_ref/ref_harness" "$HERE/../../tests/golden"
-# coherent mode: the reference's MSI controllers in the canonical schedule (coh_harness.cc)
-"$HERE/../_ref/coh_harness" "$HERE/../../tests/golden"
+mkdir -p "$GOLD"
+"$HERE/../_ref/ref_harness" "$GOLD"
+# coherent mode: the reference's MSI controllers in the canonical schedule
+# (coh_harness.cc), plus configs[0]'s captured FFT trace (-m10 fixture)
+python3 "$HERE/export_trace.py" "$GOLD/fft_real_p16_m10.npz" "$HERE/../_ref/fft10"
+"$HERE/../_ref/coh_harness" "$GOLD" "$HERE/../_ref/fft10"

@@ -54,8 +54,12 @@ def coh_case(name, m):
         kw.update(dir_total_entries=m["dir_entries"], dir_assoc=m["dir_assoc"])
     kw.update(l2_assoc=m.get("l2_assoc", 8))
     cfg = C.default_config(T, **kw)
-    if m.get("workload", "hotspot") == "stress":
+    wl = m.get("workload", "hotspot")
+    if wl == "stress":
         a, meta, o = po.gen_stress_trace(T, N)
+    elif wl.startswith("fft_real_"):                 # configs[0]: the captured reference FFT, accesses only
+        from graphite_amd import capture as cp
+        a, meta, o, _ = cp.load_fft_trace(os.path.join(GOLDEN, wl + ".npz"), barriers=False)
     else:
         a, meta, o = po.gen_trace(T, N, hot_lines=m["hot_lines"])
     exp = {"out": load("coh_%s_out.u64" % name, np.uint64),
