@@ -112,7 +112,7 @@ struct CP {
   uint32_t seg_xcd;                      // > 0: runs interleaved by shard (seg_xcd shards), XCD-grouped walker blocks
   uint32_t cache_lds_off, cache_lds_bytes; // k_c_persist<true>: the tile's cache state in LDS after the step's
   uint32_t touch_each;                     // hit runs touch LRU rows one record at a time (> 16 ways; GG_COH_TOUCH_EACH=1)
-  uint32_t walk_wide;                      // pipelined walkers scan every packet (the > 128-packet path; GG_COH_WALK_WIDE=1)
+  uint32_t walk_wide;                      // pipelined walkers take the one-wave sweep (the > 128-packet path; GG_COH_WALK_WIDE=1)
   uint32_t no_hit_runs;                    // 1: every record through app_access (hit runs off; 0 in the build)
   uint32_t mt1, mt2, mt_log;               // miss-type tracking of the L1-D / L2 (cfg flags), log2 set capacity
   uint64_t lat_l1d, lat_l1t, lat_l2d, lat_l2t, lat_dir, gap_ps, dram_proc, dram_cost;
@@ -150,6 +150,14 @@ struct CS {
   uint64_t* ctr;                         // NoC counters [T][GG_NUM_NET_COUNTERS]
   uint64_t* gscr;                        // [L][5 * IC] ordering scratch beyond kInLds
   unsigned long long* prof;              // GG_COH_PROFILE=1: shader-clock cycles per phase (diagnostics)
+  // GG_COH_TRACE=n: per launch L < n, plain stores of every tile's / walker
+  // block's phase clocks (trs [L][owned tile][16], trw [L][stage][block][8]);
+  // no atomics, so the run's timing is barely disturbed (diagnostics)
+  unsigned long long* trs; unsigned long long* trw; uint32_t tr_n, tr_wb;
+  // GG_COH_TRACE_EV=n: walker events of launches [kTrEv0, kTrEv0 + n): per block
+  // 128 x {memtime at the serve decision, after the request, after the
+  // publish, packet | position << 16 | wave << 24 | poll count << 32} and a count
+  unsigned long long* tre; uint32_t tre_n;
   uint32_t* gbar;                        // grid barrier counter of k_c_persist
   // in-kernel launch timing (gg_set_timing mode 2): per timed launch slot
   // {first workgroup start, last workgroup end} on the s_memrealtime clock
@@ -158,8 +166,10 @@ struct CS {
 // profile slots: step phases 0..5 summed over tiles, 8 = sum over steps of the slowest tile;
 // walker: 16 staging+load, 17 event loop, 18 hand-off+write back, 19 events, 20 sum of slowest walker per launch (X),
 // 21 (Y), 22 launches
-#define PROF_T0() const uint64_t _p0 = S.prof ? __builtin_amdgcn_s_memtime() : 0
-#define PROF_AT(var) const uint64_t var = S.prof ? __builtin_amdgcn_s_memtime() : 0
+constexpr uint32_t kTrStep = 24;       // GG_COH_TRACE words per (launch, tile)
+constexpr uint32_t kTrEv0 = 200, kTrEvMax = 128;
+#define PROF_T0() const uint64_t _p0 = (S.prof || S.trs) ? __builtin_amdgcn_s_memtime() : 0
+#define PROF_AT(var) const uint64_t var = (S.prof || S.trs) ? __builtin_amdgcn_s_memtime() : 0
 // GG_COH_PROFILE batch shapes: per port kind (0 SELF, 1 injection, 2 walker),
 // requests by batch size bucket (1, 2-3, 4-7, ..., 64+), requests at or after
 // the last interval's start at the batch's start (a tail run)
@@ -1596,9 +1606,9 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
   // ---- 0. hop-by-hop: SELF output port + receive of last step's packets (routePacket
   // at the receiver, hop_by_hop.cc:223-256; __processReceivedPacket, network_model.cc:118-150)
   PROF_AT(_sa);
-  uint64_t _sb = 0, _sc = 0, _sd = 0, _se = 0;
+  uint64_t _sb = 0, _sc = 0, _sd = 0, _se = 0, _sf = 0, _q1 = 0, _q2 = 0, _q3 = 0, _q4 = 0, _q1b = 0;
   if (na) {
-    if (S.prof) _sb = __builtin_amdgcn_s_memtime();
+    if (S.prof || S.trs) _sb = __builtin_amdgcn_s_memtime();
     const uint32_t* al = arv(S, p) + (size_t)lt * P.IC;
     const bool lds = na <= SL::kIn;
     uint64_t* t_ = lds ? sl.x1 : gscr; uint64_t* s_ = lds ? sl.x2 : gscr + P.IC; uint64_t* k_ = lds ? sl.x3 : gscr + 2 * P.IC;
@@ -1622,9 +1632,9 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
       }
     }
     tsync();
-    if (S.prof) _sc = __builtin_amdgcn_s_memtime();
+    if (S.prof || S.trs) _sc = __builtin_amdgcn_s_memtime();
     order_port(na, t_, s_, k_, i_, o_, ln);
-    if (S.prof) _sd = __builtin_amdgcn_s_memtime();
+    if (S.prof || S.trs) _sd = __builtin_amdgcn_s_memtime();
     const uint64_t qi = (uint64_t)T.tile * 6 + P_SELF;
     HQueue* gq = S.nq + qi;
     HNode* gnd = S.nnd + qi * P.np.max_size;
@@ -1639,7 +1649,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
     }
     RegQueue rq;
     if (regq) rq.load(gq, gnd, 1, P.np.analytical != 0, ln);
-    if (S.prof) { (void)__builtin_amdgcn_readfirstlane((int)rq.a0); _se = __builtin_amdgcn_s_memtime(); }
+    if (S.prof || S.trs) { (void)__builtin_amdgcn_readfirstlane((int)rq.a0); _se = __builtin_amdgcn_s_memtime(); }
     const uint64_t zps = lat_to_ps((uint64_t)P.np.router_delay + P.np.link_delay, P.np.f);
     uint64_t cq = 0, cf = 0;                                   // uniform: contention cycles, flits
     uint64_t rf = 0, rb = 0, rl = 0, rc = 0, rn = 0;           // this lane's packets: flits, bits, latency, contention
@@ -1671,6 +1681,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
         if (ln == k) ot = t + zps + lat_to_ps(qd, P.np.f);
       }
       if (S.prof && ln == 0) prof_batch(S, 0, cnt, ntail);
+      if (S.trs) _sf = __builtin_amdgcn_s_memtime();
       if (ln < cnt) {                                           // serialization + receive (network_model.cc:118-150)
         const uint64_t ser = lat_to_ps(nf_, P.np.f);
         const uint64_t t2 = ot + ser, z2 = z_ + zps + ser;
@@ -1739,6 +1750,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
     hk.clear_inb(p, lt);
     order_inbox(n, a_, k_, m_, i_, o_, ln);
     PROF_AT(_p1b);
+    _q1b = _p1b;
     if (S.prof && ln == 0) atomicAdd(&S.prof[9], (unsigned long long)(_p1b - _p1));
     for (uint32_t j = 0; j < n && !T.failed; ++j) {
       const gg_cmsg m = prev[o_[j]];
@@ -1872,7 +1884,9 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
         // the injection port (routePacket SEND_TILE, hop_by_hop.cc:151-159) in (time, key) order
         for (uint32_t i = ln; i < nn; i += 64) i_[i] = o_[i];
         tsync();
+        if (S.trs) _q1 = __builtin_amdgcn_s_memtime();
         order_port(nn, t_, s_, k_, i_, o_, ln);
+        if (S.trs) _q2 = __builtin_amdgcn_s_memtime();
         const uint64_t qi = (uint64_t)T.tile * 6 + P_INJ;
         HQueue* gq = S.nq + qi;
         HNode* gnd = S.nnd + qi * P.np.max_size;
@@ -1886,6 +1900,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
         }
         RegQueue rq;
         if (regq) rq.load(gq, gnd, 1, P.np.analytical != 0, ln);
+        if (S.trs) { (void)__builtin_amdgcn_readfirstlane((int)rq.a0); _q3 = __builtin_amdgcn_s_memtime(); }
         uint64_t ps = 0, fs = 0, bs = 0;
         for (uint32_t c0 = 0; c0 < nn; c0 += 64) {
           const uint32_t cnt = min(64u, nn - c0);
@@ -1920,6 +1935,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
             ps += 1; fs += nf_; bs += bits;
           }
         }
+        if (S.trs) _q4 = __builtin_amdgcn_s_memtime();
         if (regq) rq.store(gq, gnd);
         if (wave) { tsync(); img_out(gq, gnd, sl.pimg, P.np.max_size, ln); }
         ps = wave_sum64(ps); fs = wave_sum64(fs); bs = wave_sum64(bs);
@@ -1984,6 +2000,13 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
       atomicMax(&S.prof[b + 3], (unsigned long long)(tot | c24(_p3 - _p2)));
     }
   }
+  if (S.trs && L < S.tr_n && ln == 0) {
+    unsigned long long* r = S.trs + ((size_t)L * P.L + lt) * kTrStep;
+    r[2] = _p0; r[3] = _sa; r[4] = _p1; r[5] = _p2; r[6] = _p3; r[7] = _p4; r[8] = __builtin_amdgcn_s_memtime();
+    r[9] = (unsigned long long)na | ((unsigned long long)ni << 16) | ((unsigned long long)T.nsent << 32);
+    r[10] = _sb; r[11] = _sc; r[12] = _sd; r[13] = _se; r[14] = _q1b; r[15] = _sf;
+    r[16] = _q1; r[17] = _q2; r[18] = _q3; r[19] = _q4;
+  }
   // the tile's next start for the shard scheduler: finished, blocked, or clock + gap
   if (T.rec >= T.rec_end) return kNsFin;
   if (T.blocked) return kNsBlk;
@@ -2008,8 +2031,13 @@ __device__ __forceinline__ void kt_end(const CS& S)
 __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t L, uint32_t devloop, uint64_t barrier_arg)
 {
   kt_begin(S);
+  const uint64_t r0 = S.trs ? __builtin_amdgcn_s_memrealtime() : 0;
   TraceWin W{~0ull, 0, 0};
   step_body<false, false>(P, S, L, devloop, barrier_arg, W);
+  if (S.trs && L < S.tr_n && threadIdx.x == 0) {
+    unsigned long long* r = S.trs + ((size_t)L * P.L + blockIdx.x) * kTrStep;
+    r[0] = r0; r[1] = __builtin_amdgcn_s_memrealtime();
+  }
   kt_end(S);
 }
 
@@ -2090,7 +2118,8 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
     const uint32_t ns = P.seg_xcd, b = blk;
     sg = 2 * ((b % ns) + ns * (b / (2 * ns))) + ((b / ns) & 1u);
   }
-  const uint32_t tid = threadIdx.x, nthr = blockDim.x, ln = tid & 63, wv = tid >> 6, p = (live - 1) & 1u;
+  const uint32_t tid = threadIdx.x, nthr = blockDim.x, ln = tid & 63, p = (live - 1) & 1u;
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));   // wave-uniform: SGPR control flow
   PROF_T0();
   uint32_t* cntp = (stage == 0 ? S.nxl : S.nyl) + sg;
   const uint32_t n0 = *cntp;
@@ -2129,7 +2158,7 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
   }
   for (uint32_t i = tid; i < npos * kNetCtr; i += nthr) lc[i] = 0;
   for (uint32_t i = tid; i < kMaxWalkWaves; i += nthr) wlow[i] = 0;
-  if (tid == 0) { rlohi[0] = ~0u; rlohi[1] = ~0u; }
+  if (tid == 0) { rlohi[0] = ~0u; rlohi[1] = ~0u; rlohi[2] = 0; }
   __syncthreads();
   // canonical ranks (by send time, sender, seq); the positions the packets can visit
   if (!PIPE) {
@@ -2187,7 +2216,8 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
     uint64_t* l = lc + (size_t)(pos - sd.lo) * kNetCtr;
     l[0] += qm ? cq : 0; l[1] += qm ? m : 0; l[2] += cf; l[3] += m; l[4] += cf; l[5] += cf;
   };
-  if (!PIPE) {
+  const bool sweep = !PIPE || n > 128 || P.walk_wide;     // more than 128 packets (or the A/B knob): wave 0 sweeps
+  if (sweep && wv == 0) {
     // ---- one wave: position sweep, each position's batch in (time, rank) order
     uint64_t* K = W.Qt; uint32_t* B = W.Qr; uint32_t* O = W.Qs;
     for (uint32_t s_ = 0; lo <= hi && s_ <= hi - lo; ++s_) {
@@ -2232,67 +2262,73 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
       if (ln == 0) add_ctr(pos, cq, m, cf);
       wave_sync();
     }
-  } else if (wv < npos) {
+  } else if (!sweep && wv < npos) {
     // ---- one wave per position (blockDim.x = 64 x positions): the pipeline
+    // (n <= 128: lane l watches packets l and l + 64 if their route crosses
+    // this port; the wide case took the sweep above)
     const uint32_t pos = dir ? sd.lo + wv : sd.hi - wv;
     const uint32_t nx = dir ? pos + 1 : pos - 1;
     constexpr uint64_t kInf = ~0ull;
     const bool visited = lo <= hi && pos >= lo && pos <= hi;
     RegQueue rq; HTree tr;
     if (visited) port_queue(pos, rq, tr);
-    auto request = [&](uint64_t t, uint32_t nf) -> uint64_t {
-      if (!qm) return 0;
-      const uint64_t tc = time_to_cycles(t, P.np.f);
-      return regq ? rq.request<false>(tc, nf, S.err) : (wave_q ? tr.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
-    };
+    const uint32_t status_nx = (nx < sd.lo || nx > sd.hi) ? 2u : 0u;   // next router in another shard: held
     uint64_t cq = 0, cf = 0, m = 0;
-    uint32_t spin = 0;
-    // up to 128 packets: lane l watches packets l and l + 64 if their route
-    // crosses this port (entered at or before it, leaving after it); their
-    // rank, flits and exit position are fixed, so they stay in registers
-    const bool small = n <= 128 && !P.walk_wide;
+    uint32_t spin = 0, polls = 0;
+    const bool tev = S.tre && L >= kTrEv0 && L < kTrEv0 + S.tre_n;
+    unsigned long long* tre = tev ? S.tre + (((size_t)(L - kTrEv0) * 2 + stage) * S.tr_wb + blk) * (kTrEvMax * 4 + 4) : nullptr;
     auto crosses = [&](uint32_t i) {
       if (i >= n) return false;
       const uint32_t a = W.Pp[i], z = W.Pd[i];
       return dir ? (a <= pos && pos < z) : (a >= pos && pos > z);
     };
-    bool c0 = small && crosses(ln), c1 = small && crosses(ln + 64);
+    // per lane: its packets' rank, flits and exit position (fixed) in registers
+    bool c0 = visited && crosses(ln), c1 = visited && crosses(ln + 64);
     const uint32_t r0 = c0 ? W.Pr[ln] : 0u, r1 = c1 ? W.Pr[ln + 64] : 0u;
-    const uint32_t f0 = c0 ? W.Pf[ln] & 0xFFFFFFu : 0u, f1 = c1 ? W.Pf[ln + 64] & 0xFFFFFFu : 0u;
-    const uint32_t d0 = c0 ? W.Pd[ln] : 0u, d1 = c1 ? W.Pd[ln + 64] : 0u;
-    while (visited) {
-      // the horizon: packets still to come from upstream arrive at or after
-      // bound; the wave before publishes kInf once it has served its last one
-      bool up_fin = true;
+    const uint32_t fd0 = c0 ? (W.Pf[ln] & 0xFFFFFFu) | (W.Pd[ln] << 24) : 0u;   // flits (< 2^24) | exit pos << 24
+    const uint32_t fd1 = c1 ? (W.Pf[ln + 64] & 0xFFFFFFu) | (W.Pd[ln + 64] << 24) : 0u;
+    uint64_t* wup = wv > 0 ? &wlow[wv - 1] : nullptr;
+    // one loop exit, a readfirstlane'd flag: the loop is wave-uniform, so its
+    // carried values stay scalar (no exec-masked loop, no VGPR phis)
+    uint32_t go = visited ? 1u : 0u;
+    uint64_t last_ul = 0;
+    bool waiting = false;
+    while (__builtin_amdgcn_readfirstlane((int)go)) {
+      // the horizon, in canonical keys (time << 12 | rank): the wave before
+      // publishes a lower bound on the key of every packet it will still
+      // serve (kInf once it has served its last one); such a packet reaches
+      // this port with a key at least that bound + zps << 12, so every
+      // pending packet with a key <= bound here is safe (keys are unique).
+      // A packet forwarded upstream with no queue delay is therefore safe at
+      // once, without waiting for the upstream port to move on.
       uint64_t bound = kInf;
-      if (wv > 0) {
-        const uint64_t ul = lds_load_acq(&wlow[wv - 1]);
-        up_fin = ul == kInf;
-        bound = up_fin ? kInf : ul + zps;
+      if (wup) {
+        const uint64_t ul = rq.rd64(lds_load_acq(wup));          // uniform (an atomic load is taken as divergent)
+        // a waiting wave re-evaluates only when the upstream word moved: every
+        // packet the wave before forwards comes with a new (larger) word, so
+        // an unchanged word means nothing new (the cheap poll keeps the
+        // waiting waves off the serving waves' issue slots)
+        if (waiting && ul == last_ul) {
+          if (++spin > (1u << 22)) { if (ln == 0) atomicOr(S.err, GG_DERR_STATE); go = 0; continue; }
+          __builtin_amdgcn_s_sleep(GG_WALK_SLEEP);
+          continue;
+        }
+        last_ul = ul;
+        bound = ul == kInf ? kInf : ul + (zps << 12);
       }
+      waiting = false;
+      const bool up_fin = bound == kInf;
       // the least pending packet at this position, by (time, rank): each lane
-      // its least, then a scalar pass over the lanes holding one (usually few)
+      // its least (acquire on the position: the packet's time, written before
+      // it, is then current), then a scalar pass over the lanes holding one
+      const uint32_t q0 = c0 ? __hip_atomic_load(&W.Pp[ln], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) : ~0u;
+      const uint32_t q1 = c1 ? __hip_atomic_load(&W.Pp[ln + 64], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) : ~0u;
       uint64_t mk = kInf;
-      uint32_t mi = 0, mf = 0, md = 0;
-      if (small) {
-        // a candidate is pending once it sits at this port (status 0 there)
-        // acquire: the packet's time, written before its position, is then current
-        const uint32_t q0 = c0 ? __hip_atomic_load(&W.Pp[ln], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) : ~0u;
-        const uint32_t q1 = c1 ? __hip_atomic_load(&W.Pp[ln + 64], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) : ~0u;
-        if (q0 == pos) { mk = (W.Pt[ln] << 12) | r0; mi = ln; mf = f0; md = d0; }
-        if (q1 == pos) {
-          const uint64_t k = (W.Pt[ln + 64] << 12) | r1;
-          if (k < mk) { mk = k; mi = ln + 64; mf = f1; md = d1; }
-        }
-      } else {
-        for (uint32_t b0 = 0; b0 < n; b0 += 64) {
-          const uint32_t i = b0 + ln;
-          if (i < n && __hip_atomic_load(&W.Pp[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == pos &&
-              (W.Pf[i] >> 24) == 0) {
-            const uint64_t k = (W.Pt[i] << 12) | W.Pr[i];
-            if (k < mk) { mk = k; mi = i; mf = W.Pf[i] & 0xFFFFFFu; md = W.Pd[i]; }
-          }
-        }
+      uint32_t mi = 0, mfd = 0;
+      if (q0 == pos) { mk = (W.Pt[ln] << 12) | r0; mi = ln; mfd = fd0; }
+      if (q1 == pos) {
+        const uint64_t k = (W.Pt[ln + 64] << 12) | r1;
+        if (k < mk) { mk = k; mi = ln + 64; mfd = fd1; }
       }
       uint64_t wk = kInf;
       uint32_t wl = 0;
@@ -2301,37 +2337,60 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
         const uint64_t k = rl64(mk, l);
         if (k < wk) { wk = k; wl = l; }
       }
-      if (wk == kInf && up_fin) break;                                 // nothing pending, nothing to come
-      const uint64_t T = wk == kInf ? kInf : wk >> 12;
-      if (!up_fin && T >= bound) {
-        // wait for upstream progress; publish what this port can still serve
-        if (ln == 0) lds_store_rel(&wlow[wv], T < bound ? T : bound);
-        if (++spin > (1u << 20)) { if (ln == 0) atomicOr(S.err, GG_DERR_STATE); break; }
+      if (wk == kInf && up_fin) { go = 0; continue; }                   // nothing pending, nothing to come
+      if (wk > bound) {
+        // wait for upstream progress; publish the least key this port can still serve
+        if (ln == 0) lds_store_rel(&wlow[wv], wk < bound ? wk : bound);
+        if (++spin > (1u << 22)) { if (ln == 0) atomicOr(S.err, GG_DERR_STATE); go = 0; continue; }
+        ++polls;
+        waiting = true;
         __builtin_amdgcn_s_sleep(GG_WALK_SLEEP);
         continue;
       }
-      // serve it (the router + link of serve_packet, its fields from the lanes)
+      const uint64_t T = wk >> 12;
+      const uint64_t ev0 = tev ? __builtin_amdgcn_s_memtime() : 0;
+      // serve it: the router + link (serve_packet's arithmetic); the packet
+      // moves downstream as soon as its queue delay is known, the port's
+      // queue is updated after that (request_pub)
       const uint32_t i = (uint32_t)__builtin_amdgcn_readlane((int)mi, (int)wl);
-      const uint32_t nf = (uint32_t)__builtin_amdgcn_readlane((int)mf, (int)wl);
-      const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)md, (int)wl);
-      const uint64_t qd = request(T, nf);
+      const uint32_t fd = (uint32_t)__builtin_amdgcn_readlane((int)mfd, (int)wl);
+      const uint32_t nf = fd & 0xFFFFFFu;
+      const uint32_t status = status_nx ? status_nx : (nx == (fd >> 24) ? 1u : 0u);   // 1: leaves the run
+      uint64_t evp = 0;
+      auto pub = [&](uint64_t qd) {
+        if (tev) evp = __builtin_amdgcn_s_memtime();
+        if (ln == 0) {
+          // time and status (the zero-load part: + zps per port, added at the
+          // hand-off) before the packet appears downstream (Pp), then the horizon
+          W.Pt[i] = T + zps + lat_to_ps(qd, P.np.f);
+          W.Pf[i] = nf | (status << 24);
+          __hip_atomic_store(&W.Pp[i], nx, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          lds_store_rel(&wlow[wv], wk + 1);                   // every later key served here is > wk
+        }
+      };
+      uint64_t qd = 0;
+      if (!qm) pub(0ull);
+      else {
+        const uint64_t tc = time_to_cycles(T, P.np.f);
+        if (regq) qd = rq.request_pub(tc, nf, pub);
+        else { qd = wave_q ? tr.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err); pub(qd); }
+      }
+      const uint64_t ev1 = tev ? __builtin_amdgcn_s_memtime() : 0;
       cq += qd; cf += nf; ++m;
-      uint32_t status = 0;
-      if (nx < sd.lo || nx > sd.hi) status = 2;            // next router in another shard: held
-      else if (nx == d) status = 1;                        // leaves the run: next stage
-      if (small && ln == (i & 63)) { if (i < 64) c0 = false; else c1 = false; }   // served here: no longer a candidate
-      if (ln == 0) {
-        // time and status (the zero-load part: + zps per port, added at the
-        // hand-off) before the packet appears downstream (Pp), then the horizon
-        W.Pt[i] = T + zps + lat_to_ps(qd, P.np.f);
-        W.Pf[i] = nf | (status << 24);
-        __hip_atomic_store(&W.Pp[i], nx, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        lds_store_rel(&wlow[wv], T);
+      if (ln == (i & 63)) { if (i < 64) c0 = false; else c1 = false; }   // served here: no longer a candidate
+      if (tev && ln == 0) {
+        const uint32_t k = atomicAdd(reinterpret_cast<unsigned int*>(&rlohi[2]), 1u);
+        if (k < kTrEvMax) {
+          unsigned long long* e = tre + 4 + 4 * k;
+          e[0] = ev0; e[1] = evp; e[2] = ev1;
+          e[3] = (unsigned long long)i | ((unsigned long long)pos << 16) | ((unsigned long long)wv << 24) |
+                 ((unsigned long long)polls << 32);
+        }
       }
       wave_sync();
     }
     if (ln == 0) lds_store_rel(&wlow[wv], kInf);
-    if (regq && visited) rq.store(tr.q, tr.nd);
+    if (regq && visited) { rq.errp = S.err; rq.store(tr.q, tr.nd); }
     if (ln == 0 && visited) add_ctr(pos, cq, m, cf);
     nev = (uint32_t)m;
   }
@@ -2344,7 +2403,7 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
     const uint32_t h = tile_at(W.Pp[i]);
     gg_cmsg* m = cur + r;
     uint64_t z = W.Pz[i];
-    if (PIPE) {                                                // the pipeline adds zps per port here
+    if (!sweep) {                                              // the pipeline adds zps per port here
       const uint32_t p0 = pos_of(m->hop), p1 = W.Pp[i];
       z += (uint64_t)(dir ? p1 - p0 : p0 - p1) * zps;
     }
@@ -2391,6 +2450,24 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
     }
   }
   if (tid == 0) *cntp = 0;
+  if (S.tre && L >= kTrEv0 && L < kTrEv0 + S.tre_n && tid == 0) {
+    unsigned long long* e = S.tre + (((size_t)(L - kTrEv0) * 2 + stage) * S.tr_wb + blk) * (kTrEvMax * 4 + 4);
+    e[0] = rlohi[2]; e[1] = _w1; e[2] = _w2; e[3] = n | ((unsigned long long)npos << 32);
+  }
+  if (S.trs && L < S.tr_n) {
+    nev = wave_sum(ln == 0 ? nev : 0u);
+    __shared__ uint32_t tr_ev;
+    if (tid == 0) tr_ev = 0;
+    __syncthreads();
+    if (ln == 0) atomicAdd(&tr_ev, nev);
+    __syncthreads();
+    if (tid == 0) {
+      unsigned long long* r = S.trw + (((size_t)L * 2 + stage) * S.tr_wb + blk) * 8;
+      r[1] = __builtin_amdgcn_s_memrealtime();
+      r[2] = _p0; r[3] = _w1; r[4] = _w2; r[5] = __builtin_amdgcn_s_memtime();
+      r[6] = (unsigned long long)n | ((unsigned long long)npos << 32); r[7] = tr_ev;
+    }
+  }
   if (S.prof) {
     nev = wave_sum(ln == 0 ? nev : 0u);
     if (ln == 0) {
@@ -2411,6 +2488,8 @@ template <bool PIPE>
 __global__ void __launch_bounds__(PIPE ? 64 * kMaxWalkWaves : 64) k_c_walk(CP P, CS S, uint32_t L, int stage)
 {
   kt_begin(S);
+  if (S.trs && L < S.tr_n && threadIdx.x == 0)
+    S.trw[(((size_t)L * 2 + stage) * S.tr_wb + blockIdx.x) * 8] = __builtin_amdgcn_s_memrealtime();
   walk_body<PIPE>(P, S, L, stage, blockIdx.x);
   kt_end(S);
 }
@@ -3015,6 +3094,17 @@ static gg_status coh_alloc(gg_ctx* ctx)
     GG_HIP(hipMemcpy(C->kt_dev, init.data(), 16ull * kKtRing, hipMemcpyHostToDevice));
     S.kt = nullptr; S.kt_slot = 0;
   }
+  S.trs = nullptr; S.trw = nullptr; S.tr_n = 0; S.tr_wb = std::max(std::max(P.nsx, P.nsy), 1u);
+  if (getenv("GG_COH_TRACE") && atoi(getenv("GG_COH_TRACE")) > 0) {
+    S.tr_n = (uint32_t)atoi(getenv("GG_COH_TRACE"));
+    if ((st = dalloc(C, &S.trs, (size_t)S.tr_n * P.L * kTrStep))) return st;
+    if ((st = dalloc(C, &S.trw, (size_t)S.tr_n * 2 * S.tr_wb * 8))) return st;
+  }
+  S.tre = nullptr; S.tre_n = 0;
+  if (getenv("GG_COH_TRACE_EV") && atoi(getenv("GG_COH_TRACE_EV")) > 0) {
+    S.tre_n = (uint32_t)atoi(getenv("GG_COH_TRACE_EV"));
+    if ((st = dalloc(C, &S.tre, (size_t)S.tre_n * 2 * S.tr_wb * (kTrEvMax * 4 + 4)))) return st;
+  }
   if (getenv("GG_COH_PROFILE") && atoi(getenv("GG_COH_PROFILE"))) {
     if ((st = dalloc(C, &S.prof, 1024 + 8 * 65536))) return st;
     GG_HIP(hipMemset(S.prof, 0, sizeof(unsigned long long) * (1024 + 8 * 65536)));
@@ -3076,6 +3166,12 @@ gg_status gg_coherent_begin(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_ou
     GG_HIP(hipMemcpyAsync(C->S.qs, q0, sizeof(q0), hipMemcpyHostToDevice, s));
   }
   GG_HIP(hipMemsetAsync(C->S.bnd_cnt, 0, sizeof(uint32_t), s));
+  if (C->S.tre)
+    GG_HIP(hipMemsetAsync(C->S.tre, 0, sizeof(unsigned long long) * C->S.tre_n * 2 * C->S.tr_wb * (kTrEvMax * 4 + 4), s));
+  if (C->S.trs) {
+    GG_HIP(hipMemsetAsync(C->S.trs, 0, sizeof(unsigned long long) * C->S.tr_n * P.L * kTrStep, s));
+    GG_HIP(hipMemsetAsync(C->S.trw, 0, sizeof(unsigned long long) * C->S.tr_n * 2 * C->S.tr_wb * 8, s));
+  }
   if (C->S.mtab) {                                   // the miss-type address sets start empty
     GG_HIP(hipMemsetAsync(C->S.mtab, 0xFF, sizeof(uint64_t) * ((size_t)P.L * 2 << P.mt_log), s));
     GG_HIP(hipMemsetAsync(C->S.mtc, 0, sizeof(uint64_t) * P.L * 2 * GG_NUM_MISS_TYPES, s));
@@ -3348,6 +3444,29 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
   }
   gg_timer_end(ctx, "coherent_run", s);
   GG_HIP(hipStreamSynchronize(s));
+  if (C->S.trs && getenv("GG_COH_TRACE_OUT")) {
+    // raw dumps for tools/coh_trace.py: steps [n][L][16], walkers [n][2][wb][8] (u64)
+    const std::string pre = getenv("GG_COH_TRACE_OUT");
+    const size_t ns = (size_t)C->S.tr_n * P.L * kTrStep, nw = (size_t)C->S.tr_n * 2 * C->S.tr_wb * 8;
+    std::vector<unsigned long long> h(std::max(ns, nw));
+    for (int k = 0; k < 2; ++k) {
+      const size_t cnt = k ? nw : ns;
+      GG_HIP(hipMemcpy(h.data(), k ? C->S.trw : C->S.trs, 8 * cnt, hipMemcpyDeviceToHost));
+      if (FILE* f = fopen((pre + (k ? ".walk" : ".step")).c_str(), "wb")) { fwrite(h.data(), 8, cnt, f); fclose(f); }
+    }
+    if (C->S.tre) {
+      const size_t ne = (size_t)C->S.tre_n * 2 * C->S.tr_wb * (kTrEvMax * 4 + 4);
+      std::vector<unsigned long long> he(ne);
+      GG_HIP(hipMemcpy(he.data(), C->S.tre, 8 * ne, hipMemcpyDeviceToHost));
+      if (FILE* f = fopen((pre + ".ev").c_str(), "wb")) { fwrite(he.data(), 8, ne, f); fclose(f); }
+    }
+    if (FILE* f = fopen((pre + ".meta").c_str(), "w")) {
+      fprintf(f, "{\"launches\": %u, \"tiles\": %u, \"walk_blocks\": %u, \"nsx\": %u, \"nsy\": %u, \"wtx\": %u, \"wty\": %u, "
+              "\"ev_first\": %u, \"ev_launches\": %u, \"ev_max\": %u}\n",
+              C->S.tr_n, P.L, C->S.tr_wb, P.nsx, P.nsy, C->wtx, C->wty, kTrEv0, C->S.tre_n, kTrEvMax);
+      fclose(f);
+    }
+  }
   if (C->S.prof) {
     // per-launch maxima in slots L mod 65536
     std::vector<unsigned long long> h(1024 + 8 * 65536);

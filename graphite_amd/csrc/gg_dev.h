@@ -600,6 +600,84 @@ struct RegQueue {
     ++total_req;
     return qd;
   }
+  // The same request (request<false>) with the delay handed to pub(qd) as
+  // soon as it is known, before the interval list and the M/G/1 sums are
+  // updated: a pipeline stage forwards its packet first and does the
+  // bookkeeping while the next stage runs (this queue's next request comes
+  // from the same wave, after it).  Uniform values are kept scalar
+  // (readfirstlane) so a loop around it carries them in SGPRs.
+  __device__ __forceinline__ uint64_t rd64(uint64_t v) const
+  {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  }
+  __device__ __forceinline__ uint64_t A1(uint32_t i) const { return i < 64 ? rl64(a0, i) : rl64(a1, i - 64); }
+  __device__ __forceinline__ uint64_t B1(uint32_t i) const { return i < 64 ? rl64(b0, i) : rl64(b1, i - 64); }
+  template <class Pub>
+  __device__ __forceinline__ uint64_t request_pub(uint64_t t, uint64_t p, Pub&& pub)
+  {
+    if (sz >= cap) { shift_down(0); --sz; }                          // prune the min node (:52-56)
+    uint64_t qd = 0;
+    const uint64_t tp = t + p;
+    const uint32_t il = sz - 1;
+    const uint64_t la = A1(il), lb = B1(il);
+    if (la <= t && tp <= lb && lb - tp >= min_proc) {                // the last interval: no search, no delay
+      pub(0ull);
+      ++n_fast;
+      if (t - la >= min_proc) { set(il, la, t); set(sz, tp, lb); ++sz; }
+      else set(il, tp, lb);
+    } else if (analytical && A1(0) > tp) {
+      qd = mg1_queue_delay(nreq, newest, sig_sq, sig);
+      pub(qd);
+      ++anl; ++n_anl;
+    } else {
+      ++n_gen;
+      const uint64_t v0 = low_lanes(sz), v1 = sz > 64 ? low_lanes(sz - 64) : 0ull;
+      const uint64_t le0 = cmp64<kCmpULE>(a0, t) & v0, le1 = cmp64<kCmpULE>(a1, t) & v1;
+      const uint64_t f0 = le0 & cmp64<kCmpUGE>(b0, tp), f1 = le1 & cmp64<kCmpUGE>(b1, tp);
+      const bool fit = (f0 | f1) != 0;
+      uint64_t m0 = f0, m1 = f1;
+      if (!fit) {
+        m0 = ~le0 & v0 & cmp64<kCmpUGE>(b0 - a0, p);
+        m1 = ~le1 & v1 & cmp64<kCmpUGE>(b1 - a1, p);
+      }
+      if ((m0 | m1) == 0) {
+        pub(0ull);
+        errs |= GG_DERR_STATE;
+      } else {
+        const uint32_t ui = m0 ? (uint32_t)__builtin_ctzll(m0) : 64u + (uint32_t)__builtin_ctzll(m1);
+        const uint64_t a = A1(ui), b = B1(ui);
+        if (fit) {                                                   // t >= a
+          pub(0ull);
+          if (t - a >= min_proc) {
+            if (b - tp >= min_proc) { shift_up(ui + 1); set(ui + 1, tp, b); ++sz; }
+            set(ui, a, t);
+          } else if (b - tp >= min_proc) {
+            set(ui, tp, b);
+          } else {
+            shift_down(ui); --sz;
+          }
+        } else {                                                     // the first later interval long enough
+          qd = a - t;
+          pub(qd);
+          if (b - (a + p) >= min_proc) set(ui, a + p, b);
+          else { shift_down(ui); --sz; }
+        }
+      }
+    }
+    sig_sq = rd64(sig_sq + p * p);                                   // QueueModelMG1::updateQueue
+    sig = rd64(sig + p);
+    if (sig_sq >= kMg1Exact || p >= (1ull << 26)) errs |= GG_DERR_RANGE;
+    nreq = rd64(nreq + 1);
+    const uint64_t x = t + qd + p;
+    newest = rd64(x > newest ? x : newest);
+    util = rd64(util + p);                                           // updateQueueUtilizationCounters
+    last_req = rd64(x > last_req ? x : last_req);
+    total_req = rd64(total_req + 1);
+    anl = rd64(anl);
+    sz = (uint32_t)__builtin_amdgcn_readfirstlane((int)sz);
+    return qd;
+  }
 };
 
 // Latency::toPicosec / Time::toCycles (time_types.h:81-109), double and ceil.
