@@ -765,15 +765,22 @@ def cpu_baseline(tiles, per_tile, threads):
     return tiles * per_tile / dt, dt
 
 
-def private_section(args, dev):
+def private_section(args, dev, world=1, rank=0):
     """Mode P (round 1's headline): configs[1]'s uniform-random private trace at
     configs[3] scale (1024 tiles x --private-per-tile), single-pass streaming
     replay k_cache_stream; 3 timed replays; one tile bit-exact vs the oracle;
-    the oracle on --cpu-sample-tiles tile replays as its CPU baseline."""
+    the oracle on --cpu-sample-tiles tile replays as its CPU baseline.
+    With N ranks (the path that shards with no data-path
+    collective) rank r simulates global tiles [r*T, (r+1)*T) of the same
+    generator (weak scaling, T = --tiles per GPU): each replay is bracketed by
+    a barrier + synchronize, its time is the max over ranks, the per-tile
+    counters are gathered and one tile of every rank is checked bit-exact."""
     import torch
     from graphite_amd import config as C
     from graphite_amd import backend as B
+    from graphite_amd import dist as D
     T, N = args.tiles, args.private_per_tile
+    t0g = rank * T                                    # this rank's first global tile
     cfg = C.default_config(T, replay_kernel=args.replay_kernel)
     be = B.Backend(cfg)
     be.set_timing(True)
@@ -782,18 +789,20 @@ def private_section(args, dev):
     addr = torch.empty(n, dtype=torch.int64, device=dev)
     meta = torch.empty(n, dtype=torch.int32, device=dev)
     result = torch.empty(n, dtype=torch.int32, device=dev)
-    B.gen_uniform_trace(addr, meta, 0, T, N, stream=stream)
+    B.gen_uniform_trace(addr, meta, t0g, T, N, stream=stream)
     offs = np.arange(T + 1, dtype=np.uint64) * np.uint64(N)
     kms = {k: [] for k in KERNEL_BYTES}
     times = []
     for it in range(4):                               # the first replay warms up
         be.reset()
         torch.cuda.synchronize()
+        D.barrier()
         t0 = time.perf_counter()
         be.cache_access_batch(addr, meta, offs, result, None, stream)
         torch.cuda.synchronize()
+        dt = D.max_over_ranks(time.perf_counter() - t0)
         if it:
-            times.append(time.perf_counter() - t0)
+            times.append(dt)
             for k in KERNEL_BYTES:
                 kms[k].append(be.kernel_time_ms(k))
     kern = {}
@@ -803,9 +812,11 @@ def private_section(args, dev):
             ms = float(np.mean(v))
             kern[k] = {"ms": ms, "bytes_per_access": KERNEL_BYTES[k], "GB_s": n * KERNEL_BYTES[k] / (ms * 1e-3) / 1e9}
     dom = max(kern, key=lambda k: kern[k]["ms"])
-    res = {"workload": "configs[1] uniform-random private generator at %d tiles x %d accesses, 32KB/4w L1-D + "
-                       "512KB/8w L2, private-cache mode" % (T, N),
-           "value": n / float(np.mean(times)), "unit": "accesses/s",
+    res = {"workload": "configs[1] uniform-random private generator at %d tiles x %d accesses%s, 32KB/4w L1-D + "
+                       "512KB/8w L2, private-cache mode" % (T, N, " per GPU (global tiles [r*%d, (r+1)*%d) on rank r, "
+                                                           "no data-path collective)" % (T, T) if world > 1 else ""),
+           "value": world * n / float(np.mean(times)), "unit": "accesses/s", "n_gpus": world,
+           "scaling": "weak", "seconds": float(np.mean(times)),
            "roofline": {"bound": "hbm", "kernel": KERNEL_SYMBOL[dom], "achieved": kern[dom]["GB_s"],
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": kern[dom]["GB_s"] / HBM_PEAK_GBS,
                         "kernel_ms": kern[dom]["ms"], "bytes_per_access": KERNEL_BYTES[dom], "kernels": kern}}
@@ -822,15 +833,21 @@ def private_section(args, dev):
     if not args.no_verify:
         from oracle import pyoracle as po
         cnt = be.cache_counters()
-        t = T - 1
-        a, m = po.gen_uniform(t, 0, N)
+        t = T - 1                                     # the rank's last tile, global id t0g + t
+        a, m = po.gen_uniform(t0g + t, 0, N)
         oc = po.OracleCache(C.default_config(1))
-        ref = oc.run(a - np.uint64(t << 26), m, np.array([0, N], np.uint64))
+        ref = oc.run(a - np.uint64((t0g + t) << 26), m, np.array([0, N], np.uint64))
         got = result[t * N:(t + 1) * N].cpu().numpy().view(np.uint32)
-        res["bit_exact_checked"] = bool(np.array_equal(got, ref) and np.array_equal(cnt[t], oc.counters()[0]))
+        ok = bool(np.array_equal(got, ref) and np.array_equal(cnt[t], oc.counters()[0]))
+        full = D.gather_tile_counters(cnt, rank, world)           # [world * T, 2, 12], global tile order
+        acc = full[:, 0, C.CACHE_COUNTERS.index("accesses")]
+        ok = ok and bool(np.all(acc == np.uint64(N)))
+        res["bit_exact_checked"] = D.max_over_ranks(0.0 if ok else 1.0) == 0.0
+        res["counters_gathered"] = {"tiles": int(full.shape[0]), "l1d_accesses": int(acc.sum()),
+                                    "l1d_misses": int(full[:, 0, C.CACHE_COUNTERS.index("misses")].sum())}
         if not res["bit_exact_checked"]:
             print("bench.py: PRIVATE BIT-EXACT CHECK FAILED", file=sys.stderr)
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and world == 1:
         threads = args.cpu_threads or cpu_share()
         cps, cdt = cpu_baseline(args.cpu_sample_tiles, N, threads)
         res["cpu_baseline"] = {"value": cps, "unit": "accesses/s", "cores": threads, "kind": "port",
@@ -923,7 +940,9 @@ def main():
                                                "algorithmic bytes")
         if "cpu_baseline" in head:
             out["cpu_baseline"] = head["cpu_baseline"]
-    secs = [x for x in args.sections.split(",") if x] if world == 1 else []
+    # N > 1: the naturally sharding Mode P leg (private_section, weak scaling,
+    # no data-path collective) beside the coherent headline
+    secs = [x for x in args.sections.split(",") if x] if world == 1 else ["private"]
     t_sec = time.perf_counter()
     for name in secs:
         print("bench.py: section %s (%.0f s)" % (name, time.perf_counter() - t_sec), file=sys.stderr, flush=True)
@@ -939,7 +958,7 @@ def main():
             elif name == "fft" and args.fft_m:
                 r = fft_section(args, dev)
             elif name == "private":
-                r = private_section(args, dev)
+                r = private_section(args, dev, world, rank)
             elif name == "noc" and args.noc_packets:
                 r = noc_section(args, dev)
             elif name == "stress" and args.stress_tiles:

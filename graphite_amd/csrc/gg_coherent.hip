@@ -148,7 +148,7 @@ struct CS {
   uint64_t* ri; uint32_t* err;
   HQueue* nq; HNode* nnd;                // router queues [tile * 6 + port]
   uint64_t* ctr;                         // NoC counters [T][GG_NUM_NET_COUNTERS]
-  uint64_t* gscr;                        // [L][5 * IC] ordering scratch beyond kInLds
+  uint64_t* gscr;                        // [L][6 * IC] ordering scratch beyond kInLds
   unsigned long long* prof;              // GG_COH_PROFILE=1: shader-clock cycles per phase (diagnostics)
   // GG_COH_TRACE=n: per launch L < n, plain stores of every tile's / walker
   // block's phase clocks (trs [L][owned tile][16], trw [L][stage][block][8]);
@@ -493,7 +493,7 @@ struct StepLdsT {
   CReq rq[RQ];
   uint8_t dimg[sizeof(HQueue) + kQMax * sizeof(HNode)];   // DRAM queue image
   uint8_t pimg[sizeof(HQueue) + kQMax * sizeof(HNode)];   // SELF / injection port image
-  uint64_t x1[IN], x2[IN], x3[IN];
+  uint64_t x1[IN], x2[IN], x3[IN], x4[IN];
   uint32_t i1[IN], i2[IN];
   uint32_t ch[2 * kChunks];                               // record chunks: base, used
   Work wstack[WSTACK];                                    // directory work loop continuations
@@ -568,9 +568,11 @@ struct TilePre {
   uint32_t blocked, seq, nrep, nrq;
   uint64_t ccv, stv;
   uint32_t narv0, narv1, ninb0, ninb1;   // both parities (scalars: no dynamically indexed private array)
+  uint32_t segx, segy;                   // the tile's X / Y run (hop-by-hop), ~0 otherwise
   __device__ __forceinline__ void load(const CS& S, uint32_t lt, uint32_t ln)
   {
     tile = S.gtile[lt];
+    segx = S.tseg[(size_t)tile * 2]; segy = S.tseg[(size_t)tile * 2 + 1];
     rec = S.rec[lt]; rec_end = S.rec_end[lt]; clk = S.clk[lt]; pend_start = S.pend_start[lt];
     out_addr = S.out_addr[lt]; out_time = S.out_time[lt];
     blocked = S.blocked[lt]; seq = S.seq[lt]; nrep = S.nrep[lt]; nrq = S.nrq[lt];
@@ -664,7 +666,10 @@ struct Tile {
     if (cused + n > ccap) {
       if (nch) sl.ch[2 * (nch - 1) + 1] = cused;
       const uint32_t want = n > kChunk ? n : kChunk;
-      const uint32_t b = hk.pool_alloc(p, want);
+      // the tile's first chunk of a step is its own slice of the pool (no
+      // atomic on the critical path); later ones come from the shared part
+      // above the P.L slices (the pool counters start there)
+      const uint32_t b = nch == 0 && want == kChunk ? lt * kChunk : hk.pool_alloc(p, want);
       if (b == ~0u || nch >= kChunks) { fail(GG_DERR_CAP); return ~0u; }
       sl.ch[2 * nch] = b; sl.ch[2 * nch + 1] = 0;
       ++nch; cbase = b; ccap = want; cused = 0;
@@ -681,6 +686,14 @@ struct Tile {
     m.src = tile; m.dst = dst; m.requester = requester; m.seq = sq; m.type = type; m.link = 0;
     m.hop = GG_HOP_NONE; m.pad = 0;
     pool(S, p)[i] = m;
+    // the step's sent list in LDS (slot = send order = sq - the step's first
+    // seq): publish reads its records' fields from here, not back from HBM
+    // (x3 / x4 are free once the inbox is ordered; sends come after that)
+    const uint32_t slot = sq - p0.seq;
+    if (slot < SL::kIn) {
+      sl.x3[slot] = (uint64_t)i | ((uint64_t)dst << 32) | (has_data(type) ? (1ull << 63) : 0ull);
+      sl.x4[slot] = t;
+    }
   }
   __device__ __forceinline__ void count_sent(uint32_t type, uint64_t n)
   {
@@ -1401,6 +1414,23 @@ __device__ void order_port(uint32_t n, const uint64_t* t, const uint64_t* s, con
   tsync();
 }
 
+// the same order, out[rank] = the entry's local index (its fields stay in
+// the gathered arrays, no reload of the record)
+__device__ void order_port_local(uint32_t n, const uint64_t* t, const uint64_t* s, const uint64_t* k, uint32_t* out,
+                                 uint32_t ln)
+{
+  for (uint32_t i = ln; i < n; i += 64) {
+    const uint64_t ti = t[i], si = s[i], ki = k[i];
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < n; ++j) {
+      const uint64_t tj = t[j], sj = s[j], kj = k[j];
+      r += (tj < ti) || (tj == ti && (sj < si || (sj == si && kj < ki)));
+    }
+    out[r] = i;
+  }
+  tsync();
+}
+
 // Queue images (HQueue + max_size nodes, all 16-byte words) between HBM and
 // LDS: image slot i of `img` (stride qimg bytes) <-> queue qi_of(i).  One
 // flat index over every word of every image, 16 loads in flight per lane
@@ -1573,7 +1603,7 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
     }
   }
   if (lt == 0 && ln == 0) {
-    S.ri[GG_RI_STEPS]++; S.ring[(k + 2) & 3] = 0; S.npool[p ^ 1u] = 0;
+    S.ri[GG_RI_STEPS]++; S.ring[(k + 2) & 3] = 0; S.npool[p ^ 1u] = P.L * kChunk;   // above the tiles' slices
     S.live[L & 3] = k + 1;
   }
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1583,6 +1613,120 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
   const uint32_t ni = p ? pre.ninb1 : pre.ninb0;
   tile_step<LC, HR>(P, S, lt, k, L, barrier, W, sl, smem + P.cache_lds_off, pre, hk, na, ni,
                     devloop && k == 0 ? qsv[QS_REL] : 0ull);
+}
+
+// Publish of a hop-by-hop step whose sent records all fit the LDS sent list
+// (Tile::put): self-sends to the next inbox (processCornerCases,
+// network_model.cc:413-424); the rest through the tile's injection port
+// (routePacket SEND_TILE, hop_by_hop.cc:151-159) in (send time, seq) order,
+// then onto the X (or Y) run each enters.  Every field comes from LDS (the
+// sent list, the tile's own run ids), and the port's queue is loaded while
+// the list is sorted, so no record is read back from HBM.
+template <class TT, class H>
+__device__ __forceinline__ void publish_hbh_lds(TT& T, gg_cmsg* cur, uint32_t nloc, uint64_t& ri_net, uint64_t& ri_self,
+                                                const H& hk, uint64_t& q1, uint64_t& q2, uint64_t& q3, uint64_t& q4)
+{
+  const CP& P = T.P; const CS& S = T.S;
+  auto& sl = T.sl;
+  const uint32_t ln = T.ln, lt = T.lt, tile = T.tile, p = T.p, seq0 = T.p0.seq;
+  const uint32_t cx = tile % P.mw, cy = tile / P.mw;
+  const uint64_t qi = (uint64_t)tile * 6 + P_INJ;
+  HQueue* gq = S.nq + qi;
+  HNode* gnd = S.nnd + qi * P.np.max_size;
+  const bool regq = P.np.qm && P.np.qtype == GG_QM_HISTORY_TREE && P.np.max_size <= kQMax;
+  const bool wave = P.np.qm && P.np.max_size <= kQMax && !regq;
+  RegQueue rq;
+  uint32_t nn = 0;
+  bool rq_loaded = false;
+  for (uint32_t i0 = 0; i0 < nloc; i0 += 64) {
+    const uint32_t i = i0 + ln;
+    uint64_t e = 0, ts = 0;
+    bool self = false, net = false;
+    if (i < nloc) { e = sl.x3[i]; ts = sl.x4[i]; self = (uint32_t)((e >> 32) & 0x7FFFFFFFu) == tile; net = !self; }
+    const uint32_t r = (uint32_t)e;
+    if (self) {
+      const uint32_t j = hk.inbox_slot(p ^ 1u, lt);
+      if (j == ~0u) atomicOr(S.err, GG_DERR_CAP);
+      else inb(S, p ^ 1u)[(size_t)lt * P.IC + j] = r;
+      ri_self++;
+    }
+    const uint64_t m = __ballot(net);
+    if (m && regq && !rq_loaded) { rq.load(gq, gnd, 1, P.np.analytical != 0, ln); rq_loaded = true; }
+    const uint32_t pos = nn + (uint32_t)__builtin_popcountll(m & ((1ull << ln) - 1));
+    if (net) {
+      const uint32_t d = (uint32_t)((e >> 32) & 0x7FFFFFFFu), dx = d % P.mw, dy = d / P.mw;
+      const uint32_t seg = cx != dx ? ((T.p0.segx * 2 + (dx > cx ? 1u : 0u)) | 0x80000000u)
+                                    : (T.p0.segy * 2 + (dy > cy ? 1u : 0u));
+      const uint64_t hd = e >> 63;
+      sl.x1[pos] = ts;
+      sl.x2[pos] = ((uint64_t)(seq0 + i) << 1) | hd;      // the sender is this tile: its seq orders equal times
+      sl.i1[pos] = r;
+      sl.x4[pos] = seg | (hd << 32);                      // (read above for slot i >= pos, in program order)
+      ri_net++;
+    }
+    nn += (uint32_t)__builtin_popcountll(m);
+  }
+  tsync();
+  if (!nn) return;
+  if (S.trs) q1 = __builtin_amdgcn_s_memtime();
+  order_port_local(nn, sl.x1, sl.x1, sl.x2, sl.i2, ln);
+  if (S.trs) q2 = __builtin_amdgcn_s_memtime();
+  HTree tr{gq, gnd, 1, P.np.analytical != 0};
+  if (wave) {
+    img_in(sl.pimg, gq, gnd, P.np.max_size, ln);
+    tsync();
+    tr.q = reinterpret_cast<HQueue*>(sl.pimg); tr.nd = reinterpret_cast<HNode*>(sl.pimg + sizeof(HQueue));
+  }
+  if (S.trs) { (void)__builtin_amdgcn_readfirstlane((int)rq.a0); q3 = __builtin_amdgcn_s_memtime(); }
+  uint64_t ps = 0, fs = 0, bs = 0;
+  for (uint32_t c0 = 0; c0 < nn; c0 += 64) {
+    const uint32_t cnt = min(64u, nn - c0);
+    uint32_t r = 0, nf_ = 0, bits = 0;
+    uint64_t sp = 0;
+    if (ln < cnt) {
+      const uint32_t e = sl.i2[c0 + ln];
+      r = sl.i1[e];
+      sp = sl.x1[e];
+      bits = (sl.x4[e] >> 32) ? P.bits_data : P.bits_req;
+      nf_ = (uint32_t)nflits(P.np, bits);
+    }
+    uint64_t oq = 0;
+    for (uint32_t k = 0; k < cnt; ++k) {
+      const uint32_t nf = (uint32_t)__builtin_amdgcn_readlane((int)nf_, (int)k);
+      uint64_t qd = 0;
+      if (P.np.qm) {
+        const uint64_t tc = time_to_cycles(rl64(sp, k), P.np.f);
+        qd = regq ? rq.request(tc, nf, S.err) : (wave ? tr.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
+      }
+      if (ln == k) oq = qd;
+      fs += nf; bs += (uint32_t)__builtin_amdgcn_readlane((int)bits, (int)k);   // updateSendCounters (network_model.cc:228-251)
+    }
+    ps += cnt;
+    if (ln < cnt) {
+      gg_cmsg* g = cur + r;
+      g->arrival_ps = sp + lat_to_ps(0, P.np.f) + lat_to_ps(oq, P.np.f);
+      g->zero_load_ps = 0;
+      g->hop = tile;
+    }
+  }
+  if (S.trs) q4 = __builtin_amdgcn_s_memtime();
+  if (regq) rq.store(gq, gnd);
+  if (wave) { tsync(); img_out(gq, gnd, sl.pimg, P.np.max_size, ln); }
+  if (ln == 0) {
+    cadd(S.ctr, tile, GG_NC_PACKETS_SENT, ps); cadd(S.ctr, tile, GG_NC_FLITS_SENT, fs);
+    cadd(S.ctr, tile, GG_NC_BITS_SENT, bs);
+  }
+  // onto the X (or Y) run the packet enters
+  for (uint32_t i = ln; i < nn; i += 64) {
+    const uint32_t e = sl.i2[i];
+    const uint32_t r = sl.i1[e], seg = (uint32_t)sl.x4[e];
+    const bool is_x = seg >> 31;
+    const uint32_t sg = seg & 0x7FFFFFFFu;
+    const uint32_t j = hk.seg_slot(is_x, sg);
+    if (j == ~0u) { atomicOr(S.err, GG_DERR_CAP); continue; }
+    (is_x ? S.xl : S.yl)[(size_t)sg * P.seg_cap + j] = r;
+  }
+  tsync();
 }
 
 // One tile's step k (parity k & 1) of the quantum that ends at `barrier`, on
@@ -1598,7 +1742,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
   PROF_T0();
   Tile<SL, H> T(P, S, lt, p, sl, hk, clds, std::integral_constant<bool, LC>(), pre);
   const gg_cmsg* prev = pool(S, p ^ 1u);     // records delivered to this step
-  uint64_t* gscr = S.gscr + (size_t)lt * 5 * P.IC;
+  uint64_t* gscr = S.gscr + (size_t)lt * 6 * P.IC;
   // NoC counters of the SELF port (lanes 0-6) and of the receiver
   // (lanes 8-12: packets, flits, bits received, latency, contention)
   uint64_t ncd = 0;
@@ -1612,64 +1756,74 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
     const uint32_t* al = arv(S, p) + (size_t)lt * P.IC;
     const bool lds = na <= SL::kIn;
     uint64_t* t_ = lds ? sl.x1 : gscr; uint64_t* s_ = lds ? sl.x2 : gscr + P.IC; uint64_t* k_ = lds ? sl.x3 : gscr + 2 * P.IC;
+    uint64_t* z_a = lds ? sl.x4 : gscr + 5 * P.IC;
     uint32_t* i_ = lds ? sl.i1 : (uint32_t*)(gscr + 3 * P.IC); uint32_t* o_ = lds ? sl.i2 : (uint32_t*)(gscr + 4 * P.IC);
+    // the port's queue in registers for the batch (RegQueue, its loads in
+    // flight beside the records'); other models on an LDS image
+    const uint64_t qi = (uint64_t)T.tile * 6 + P_SELF;
+    HQueue* gq = S.nq + qi;
+    HNode* gnd = S.nnd + qi * P.np.max_size;
+    const bool regq = P.np.qm && P.np.qtype == GG_QM_HISTORY_TREE && P.np.max_size <= kQMax;
+    const bool wave = P.np.qm && P.np.max_size <= kQMax && !regq;
+    RegQueue rq;
+    if (regq) rq.load(gq, gnd, 1, P.np.analytical != 0, ln);
     // 4 records per lane in flight: the list words, then the records (a
     // fan-in of hundreds of acknowledgements at a hot line's home otherwise
-    // waits two dependent memory round trips per 64 records)
+    // waits two dependent memory round trips per 64 records); every field
+    // the port and the receiver need goes to LDS (key bit 0: has data)
     for (uint32_t i0 = ln; i0 < na; i0 += 256) {
       uint32_t rr[4];
 #pragma unroll
       for (uint32_t u = 0; u < 4; ++u) rr[u] = i0 + 64 * u < na ? al[i0 + 64 * u] : 0u;
-      uint64_t ta[4], sa[4];
-      uint32_t sr[4], sq[4];
+      uint64_t ta[4], sa[4], za[4];
+      uint32_t sr[4], sq[4], ty[4];
 #pragma unroll
       for (uint32_t u = 0; u < 4; ++u)
-        if (i0 + 64 * u < na) { const gg_cmsg& m = prev[rr[u]]; ta[u] = m.arrival_ps; sa[u] = m.send_ps; sr[u] = m.src; sq[u] = m.seq; }
+        if (i0 + 64 * u < na) {
+          const gg_cmsg& m = prev[rr[u]];
+          ta[u] = m.arrival_ps; sa[u] = m.send_ps; za[u] = m.zero_load_ps; sr[u] = m.src; sq[u] = m.seq; ty[u] = m.type;
+        }
 #pragma unroll
       for (uint32_t u = 0; u < 4; ++u) {
         const uint32_t i = i0 + 64 * u;
-        if (i < na) { t_[i] = ta[u]; s_[i] = sa[u]; k_[i] = ((uint64_t)sr[u] << 32) | sq[u]; i_[i] = rr[u]; }
+        if (i < na) {
+          t_[i] = ta[u]; s_[i] = sa[u]; z_a[i] = za[u]; i_[i] = rr[u];
+          k_[i] = ((uint64_t)sr[u] << 33) | ((uint64_t)sq[u] << 1) | (has_data(ty[u]) ? 1u : 0u);
+        }
       }
     }
     tsync();
     if (S.prof || S.trs) _sc = __builtin_amdgcn_s_memtime();
-    order_port(na, t_, s_, k_, i_, o_, ln);
+    order_port_local(na, t_, s_, k_, o_, ln);
     if (S.prof || S.trs) _sd = __builtin_amdgcn_s_memtime();
-    const uint64_t qi = (uint64_t)T.tile * 6 + P_SELF;
-    HQueue* gq = S.nq + qi;
-    HNode* gnd = S.nnd + qi * P.np.max_size;
-    // the port's queue in registers for the batch (RegQueue); other models on an LDS image
-    const bool regq = P.np.qm && P.np.qtype == GG_QM_HISTORY_TREE && P.np.max_size <= kQMax;
-    const bool wave = P.np.qm && P.np.max_size <= kQMax && !regq;
     HTree tr{gq, gnd, 1, P.np.analytical != 0};
     if (wave) {
       img_in(sl.pimg, gq, gnd, P.np.max_size, ln);
       tsync();
       tr.q = reinterpret_cast<HQueue*>(sl.pimg); tr.nd = reinterpret_cast<HNode*>(sl.pimg + sizeof(HQueue));
     }
-    RegQueue rq;
-    if (regq) rq.load(gq, gnd, 1, P.np.analytical != 0, ln);
     if (S.prof || S.trs) { (void)__builtin_amdgcn_readfirstlane((int)rq.a0); _se = __builtin_amdgcn_s_memtime(); }
     const uint64_t zps = lat_to_ps((uint64_t)P.np.router_delay + P.np.link_delay, P.np.f);
     uint64_t cq = 0, cf = 0;                                   // uniform: contention cycles, flits
-    uint64_t rf = 0, rb = 0, rl = 0, rc = 0, rn = 0;           // this lane's packets: flits, bits, latency, contention
+    uint64_t rf = 0, rb = 0, rl = 0, rc = 0;                   // uniform: received flits, bits, latency, contention
+    const uint64_t rn = na;
     gg_cmsg* pv = const_cast<gg_cmsg*>(prev);
     for (uint32_t c0 = 0; c0 < na; c0 += 64) {
       const uint32_t cnt = min(64u, na - c0);
       uint32_t r = 0, nf_ = 0, bits = 0;
-      uint64_t t_ = 0, z_ = 0, sp = 0;
+      uint64_t tv = 0, z_ = 0, sp = 0;
       if (ln < cnt) {
-        r = o_[c0 + ln];
-        const gg_cmsg& g = pv[r];
-        t_ = g.arrival_ps; z_ = g.zero_load_ps; sp = g.send_ps;
-        bits = has_data(g.type) ? P.bits_data : P.bits_req;
+        const uint32_t e = o_[c0 + ln];                          // local index of the packet of rank c0 + ln
+        r = i_[e];
+        tv = t_[e]; z_ = z_a[e]; sp = s_[e];
+        bits = (k_[e] & 1u) ? P.bits_data : P.bits_req;
         nf_ = (uint32_t)nflits(P.np, bits);
       }
-      uint64_t ot = t_;
+      uint64_t ot = tv, oz = z_;
       const uint64_t x0 = S.prof && regq ? rq.A(rq.sz - 1) : 0;
       uint32_t ntail = 0;
       for (uint32_t k = 0; k < cnt; ++k) {
-        const uint64_t t = rl64(t_, k);
+        const uint64_t t = rl64(tv, k);
         const uint32_t nf = (uint32_t)__builtin_amdgcn_readlane((int)nf_, (int)k);
         uint64_t qd = 0;
         if (P.np.qm) {
@@ -1678,21 +1832,20 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
           qd = regq ? rq.request(tc, nf, S.err) : (wave ? tr.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
         }
         cq += qd; cf += nf;
-        if (ln == k) ot = t + zps + lat_to_ps(qd, P.np.f);
+        // serialization + receive (network_model.cc:118-150), uniform: the
+        // lane of packet k keeps its new arrival / zero-load for the store
+        const uint64_t ser = lat_to_ps(nf, P.np.f);
+        const uint64_t t2 = t + zps + lat_to_ps(qd, P.np.f) + ser, z2 = rl64(z_, k) + zps + ser;
+        const uint64_t ct = t2 - rl64(sp, k) - z2;
+        rf += nf; rb += (uint32_t)__builtin_amdgcn_readlane((int)bits, (int)k); rl += z2 + ct; rc += ct;
+        if (ln == k) { ot = t2; oz = z2; }
       }
       if (S.prof && ln == 0) prof_batch(S, 0, cnt, ntail);
       if (S.trs) _sf = __builtin_amdgcn_s_memtime();
-      if (ln < cnt) {                                           // serialization + receive (network_model.cc:118-150)
-        const uint64_t ser = lat_to_ps(nf_, P.np.f);
-        const uint64_t t2 = ot + ser, z2 = z_ + zps + ser;
-        const uint64_t ct = t2 - sp - z2;
-        pv[r].arrival_ps = t2; pv[r].zero_load_ps = z2;
-        rn += 1; rf += nf_; rb += bits; rl += z2 + ct; rc += ct;
-      }
+      if (ln < cnt) { pv[r].arrival_ps = ot; pv[r].zero_load_ps = oz; }
     }
     if (regq) rq.store(gq, gnd);
     if (wave) { tsync(); img_out(gq, gnd, sl.pimg, P.np.max_size, ln); }
-    rn = wave_sum64(rn); rf = wave_sum64(rf); rb = wave_sum64(rb); rl = wave_sum64(rl); rc = wave_sum64(rc);
     // lanes 0-6: the SELF port (contention, router packets, buffer writes, switch, crossbar, link, buffer reads), 8-12: the receiver
     ncd = ln == 0 ? (P.np.qm ? cq : 0ull) : ln == 1 ? (P.np.qm ? (uint64_t)na : 0ull) : ln == 3 ? (uint64_t)na
         : (ln == 2 || ln == 4 || ln == 5 || ln == 6) ? cf : ln == 8 ? rn : ln == 9 ? rf : ln == 10 ? rb
@@ -1856,6 +2009,8 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
           ri_bnd++;
         }
       }
+    } else if (lds && np_ == nloc) {
+      publish_hbh_lds(T, cur, nloc, ri_net, ri_self, hk, _q1, _q2, _q3, _q4);
     } else {
       // self-sends: straight to the next inbox (processCornerCases, network_model.cc:413-424)
       uint32_t nn = 0;
@@ -1925,20 +2080,20 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
               qd = regq ? rq.request(tc, nf, S.err) : (wave ? tr.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
             }
             if (ln == k) oq = qd;
+            fs += nf; bs += (uint32_t)__builtin_amdgcn_readlane((int)bits, (int)k);   // updateSendCounters, uniform
           }
+          ps += cnt;
           if (S.prof && ln == 0) prof_batch(S, 1, cnt, ntail);
-          if (ln < cnt) {                                       // updateSendCounters (network_model.cc:228-251)
+          if (ln < cnt) {                                       // (network_model.cc:228-251)
             gg_cmsg* g = cur + r;
             g->arrival_ps = sp + lat_to_ps(0, P.np.f) + lat_to_ps(oq, P.np.f);
             g->zero_load_ps = 0;
             g->hop = T.tile;
-            ps += 1; fs += nf_; bs += bits;
           }
         }
         if (S.trs) _q4 = __builtin_amdgcn_s_memtime();
         if (regq) rq.store(gq, gnd);
         if (wave) { tsync(); img_out(gq, gnd, sl.pimg, P.np.max_size, ln); }
-        ps = wave_sum64(ps); fs = wave_sum64(fs); bs = wave_sum64(bs);
         if (ln == 0) {
           cadd(S.ctr, T.tile, GG_NC_PACKETS_SENT, ps); cadd(S.ctr, T.tile, GG_NC_FLITS_SENT, fs);
           cadd(S.ctr, T.tile, GG_NC_BITS_SENT, bs);
@@ -2134,6 +2289,18 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
   gg_cmsg* cur = pool(S, p);
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t npos = sd.hi - sd.lo + 1;
+  const bool qm = P.np.qm != 0;
+  const bool regq = qm && P.np.qtype == GG_QM_HISTORY_TREE && P.np.max_size <= kQMax;
+  const bool sweep = !PIPE || n > 128 || P.walk_wide;     // more than 128 packets (or the A/B knob): wave 0 sweeps
+  // the pipeline with register queues: each wave loads its port's history
+  // tree straight from HBM into registers now, beside the packet staging
+  // (no LDS image copy in or out; written back only if the port served)
+  const bool direct = PIPE && regq && !sweep;
+  RegQueue rq;
+  if (direct && wv < npos) {
+    const uint64_t qi = (uint64_t)tile_at(dir ? sd.lo + wv : sd.hi - wv) * 6 + port;
+    rq.load(S.nq + qi, S.nnd + qi * P.np.max_size, 1, P.np.analytical != 0, ln);
+  }
   uint8_t* qimg = smem;
   uint64_t* lc = reinterpret_cast<uint64_t*>(smem + (size_t)npos * P.qimg);     // [npos][kNetCtr]
   uint64_t* wlow = lc + (size_t)npos * kNetCtr;                                  // [kMaxWalkWaves] horizons (kInf: done)
@@ -2194,14 +2361,12 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
   if (ln == 0 && lo != ~0u) { atomicMin(&rlohi[0], lo); atomicMin(&rlohi[1], ~hi); }
   __syncthreads();
   lo = rlohi[0]; hi = ~rlohi[1];
-  const bool qm = P.np.qm != 0;
   auto qi_of = [&](uint32_t i) { return (uint64_t)tile_at(lo + i) * 6 + port; };
-  if (qm && lo <= hi)
+  if (qm && lo <= hi && !direct)
     imgs_copy<true, decltype(qi_of), 4>(qimg + (size_t)(lo - sd.lo) * P.qimg, P.qimg, hi - lo + 1, qi_of, S.nq, S.nnd,
                                         P.np.max_size, tid, nthr);
   __syncthreads();
   PROF_AT(_w1);
-  const bool regq = qm && P.np.qtype == GG_QM_HISTORY_TREE && P.np.max_size <= kQMax;
   const bool wave_q = P.np.max_size <= kQMax;
   const uint64_t zps = lat_to_ps((uint64_t)P.np.router_delay + P.np.link_delay, P.np.f);
   uint32_t nev = 0;
@@ -2216,7 +2381,6 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
     uint64_t* l = lc + (size_t)(pos - sd.lo) * kNetCtr;
     l[0] += qm ? cq : 0; l[1] += qm ? m : 0; l[2] += cf; l[3] += m; l[4] += cf; l[5] += cf;
   };
-  const bool sweep = !PIPE || n > 128 || P.walk_wide;     // more than 128 packets (or the A/B knob): wave 0 sweeps
   if (sweep && wv == 0) {
     // ---- one wave: position sweep, each position's batch in (time, rank) order
     uint64_t* K = W.Qt; uint32_t* B = W.Qr; uint32_t* O = W.Qs;
@@ -2270,8 +2434,8 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
     const uint32_t nx = dir ? pos + 1 : pos - 1;
     constexpr uint64_t kInf = ~0ull;
     const bool visited = lo <= hi && pos >= lo && pos <= hi;
-    RegQueue rq; HTree tr;
-    if (visited) port_queue(pos, rq, tr);
+    HTree tr;
+    if (visited && !direct) port_queue(pos, rq, tr);
     const uint32_t status_nx = (nx < sd.lo || nx > sd.hi) ? 2u : 0u;   // next router in another shard: held
     uint64_t cq = 0, cf = 0, m = 0;
     uint32_t spin = 0, polls = 0;
@@ -2390,7 +2554,12 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
       wave_sync();
     }
     if (ln == 0) lds_store_rel(&wlow[wv], kInf);
-    if (regq && visited) { rq.errp = S.err; rq.store(tr.q, tr.nd); }
+    if (regq && visited && direct && m) {
+      const uint64_t qi = (uint64_t)tile_at(pos) * 6 + port;
+      rq.errp = S.err; rq.store(S.nq + qi, S.nnd + qi * P.np.max_size);
+    } else if (regq && visited && !direct) {
+      rq.errp = S.err; rq.store(tr.q, tr.nd);
+    }
     if (ln == 0 && visited) add_ctr(pos, cq, m, cf);
     nev = (uint32_t)m;
   }
@@ -2433,7 +2602,7 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
   }
   nb = wave_sum(nb);
   if (ln == 0 && nb) atomicAdd((unsigned long long*)&S.ri[GG_RI_BOUNDARY_MSGS], (unsigned long long)nb);
-  if (qm && lo <= hi)
+  if (qm && lo <= hi && !direct)
     imgs_copy<false, decltype(qi_of), 4>(qimg + (size_t)(lo - sd.lo) * P.qimg, P.qimg, hi - lo + 1, qi_of, S.nq, S.nnd,
                                          P.np.max_size, tid, nthr);
   for (uint32_t i = tid; i < npos * 6u; i += nthr) {
@@ -2849,6 +3018,14 @@ gg_status gg_coh_kernel_stats(gg_ctx* ctx, const char* name, double* total_ms, u
 }
 
 static int ilog2(uint64_t v) { int p = -1; while (v) { v >>= 1; ++p; } return p; }
+// both record pools empty: their shared parts start above the owned tiles'
+// first-chunk slices (Tile::alloc)
+__global__ void k_pool_reset(uint32_t* npool, uint32_t base) { if (threadIdx.x < 2) npool[threadIdx.x] = base; }
+static hipError_t coh_pool_reset(gg_coh_state* C, hipStream_t s)
+{
+  hipLaunchKernelGGL(k_pool_reset, dim3(1), dim3(64), 0, s, C->S.npool, C->P.L * kChunk);
+  return hipGetLastError();
+}
 static int clog2(uint64_t v) { int p = ilog2(v); return ((1ull << p) == v) ? p : p + 1; }
 static uint64_t lat_ps_host(uint64_t cycles, double f) { return (uint64_t)ceil(((double)1000 * cycles) / f); }
 
@@ -3084,7 +3261,7 @@ static gg_status coh_alloc(gg_ctx* ctx)
   A(yl, (uint64_t)std::max(P.nsy, 1u) * P.seg_cap); A(nyl, std::max(P.nsy, 1u));
   A(bnd, P.msg_cap); A(bnd_cnt, 1);
   A(ring, 11); A(ri, GG_NUM_RUN_INFO); A(qs, QS_N); A(gbar, 1);
-  A(gscr, L * 5 * P.IC);
+  A(gscr, L * 6 * P.IC);
 #undef A
   {
     // in-kernel launch timing slots, reset to {~0, 0}
@@ -3159,7 +3336,7 @@ gg_status gg_coherent_begin(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_ou
   if (gg_status st = gg_noc_reset(ctx, s)) return st;
   GG_HIP(hipMemsetAsync(ctx->err_dev, 0, sizeof(uint32_t), s));
   GG_HIP(hipMemsetAsync(C->S.ri, 0, sizeof(uint64_t) * GG_NUM_RUN_INFO, s));
-  GG_HIP(hipMemsetAsync(C->S.npool, 0, sizeof(uint32_t) * 2, s));
+  GG_HIP(coh_pool_reset(C, s));
   GG_HIP(hipMemsetAsync(C->S.ring, 0, sizeof(uint32_t) * 11, s));
   {
     uint64_t q0[QS_N] = {0, 0, 0, 0, 0, 0, ~0ull, 0, (uint64_t)ctx->cfg.quantum_ns * 1000ull, 0, 0, 0};
@@ -3305,7 +3482,7 @@ gg_status gg_coh_import_slots(gg_ctx* ctx, const gg_cmsg* slots, uint32_t world,
   gg_coh_state* C = ctx->coh;
   if (!C || !C->begun) return gg_fail(GG_ERR_INVALID, "gg_coherent_begin first");
   hipStream_t s = ctx->last_stream;
-  if (first) GG_HIP(hipMemsetAsync(C->S.npool, 0, sizeof(uint32_t) * 2, s));
+  if (first) GG_HIP(coh_pool_reset(C, s));
   hipLaunchKernelGGL(k_c_import_slots, dim3(64, world), dim3(256), 0, s, C->P, C->S, slots, region, lo, hi, skip_if_dev);
   GG_HIP(hipGetLastError());
   return GG_OK;
@@ -3365,7 +3542,7 @@ gg_status gg_coherent_import(gg_ctx* ctx, const gg_cmsg* in_dev, uint64_t n)
   hipSetDevice(ctx->device);
   hipStream_t s = ctx->last_stream;
   // the quantum's first step reads pool 1 (messages) and walks pool 0 (held packets)
-  GG_HIP(hipMemsetAsync(C->S.npool, 0, sizeof(uint32_t) * 2, s));
+  GG_HIP(coh_pool_reset(C, s));
   hipLaunchKernelGGL(k_c_import, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, C->P, C->S, in_dev, (uint32_t)n);
   GG_HIP(hipGetLastError());
   GG_HIP(hipStreamSynchronize(s));

@@ -53,11 +53,13 @@ __global__ void __launch_bounds__(64 * kCoreWaves) k_core_model(const uint32_t* 
   for (uint64_t b = tk.begin; b < tk.end; b += 256) {
     uint32_t m[4];
     uint64_t a[4];
+    bool vl[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const uint64_t r = b + 64 * u + ln;
-      m[u] = r < tk.end ? meta[r] : GG_META_CONT;
-      a[u] = r < tk.end ? acc[r] : 0;
+      vl[u] = r < tk.end;
+      m[u] = vl[u] ? meta[r] : GG_META_CONT;
+      a[u] = vl[u] ? acc[r] : 0;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -65,7 +67,7 @@ __global__ void __launch_bounds__(64 * kCoreWaves) k_core_model(const uint32_t* 
       const uint32_t up = (uint32_t)__shfl((int)m[u], (int)((ln + 63) & 63));
       const uint32_t pm = ln == 0 ? prevm : up;            // the previous record's meta
       prevm = (uint32_t)__shfl((int)m[u], 63);
-      const bool head = !(m[u] & GG_META_CONT) || pm == GG_META_BARRIER;
+      const bool head = vl[u] && (!(m[u] & GG_META_CONT) || pm == GG_META_BARRIER);   // (no padding lane)
       const uint64_t heads = __ballot(head);
       const uint64_t mine = heads & below;
       const uint32_t own = rec_write(m[u]);

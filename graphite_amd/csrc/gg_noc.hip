@@ -227,16 +227,9 @@ __device__ void inject_tile(const NocDev& D, uint32_t tile, const uint32_t* __re
     S.ct[k] += cps;
   }
 }
-__global__ void k_inject(NocDev D, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
-                         const uint32_t* __restrict__ len, const uint64_t* __restrict__ bucket_off,
-                         const uint32_t* __restrict__ bucket_ids, Ev* heap, PktState S)
-{
-  const uint32_t tile = blockIdx.x * blockDim.x + threadIdx.x;
-  if (tile >= D.P.tiles) return;
-  inject_tile(D, tile, len, bucket_off, bucket_ids, heap, S);
-}
-
-// Stages X and Y: one thread per chain; ports along the chain in (time, index) order.
+// Stages X and Y, chains whose queue images do not fit LDS (large
+// max_list_size): one thread per chain, ports along the chain in (time,
+// index) order, queues in HBM.
 __global__ void k_chain(NocDev D, int stage, const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
                         const uint32_t* __restrict__ len, const uint64_t* __restrict__ bucket_off,
                         const uint32_t* __restrict__ bucket_ids, Ev* heap, PktState S, uint32_t nchains)
@@ -294,15 +287,6 @@ __device__ void self_tile(const NocDev& D, uint32_t tile, const uint32_t* __rest
     S.t[k] = t; S.zl[k] = zl; S.ct[k] = ct;
   }
 }
-__global__ void k_self(NocDev D, const uint32_t* __restrict__ dst, const uint32_t* __restrict__ len,
-                       const uint64_t* __restrict__ bucket_off, const uint32_t* __restrict__ bucket_ids,
-                       Ev* heap, PktState S)
-{
-  const uint32_t tile = blockIdx.x * blockDim.x + threadIdx.x;
-  if (tile >= D.P.tiles) return;
-  self_tile(D, tile, len, bucket_off, bucket_ids, heap, S);
-}
-
 // Staged packets: a workgroup's packets (a contiguous bucket range [B, E))
 // gathered into LDS next to its queues — the event heap, the working times
 // and the canonical keys — so the serial event walk touches no HBM; written
@@ -2069,13 +2053,11 @@ struct gg_noc_state {
   uint32_t *cur = nullptr, *keys = nullptr, *ids = nullptr;
   Ev* heap = nullptr;
   uint32_t* counts = nullptr; uint32_t* cursor = nullptr; uint64_t* off = nullptr; uint32_t nb_cap = 0;
-  bool staged = true;   // LDS-staged stage kernels where the queues fit (else HBM-resident)
   TEv* theap = nullptr; uint32_t* bidx = nullptr; uint64_t tcap = 0, bcap = 0;   // broadcast-tree walk scratch
   unsigned long long* prof = nullptr;             // GG_NOC_PROFILE=1: k_chain_sweep phase cycles (diagnostics)
   SK* pscr = nullptr; uint64_t pscr_cap = 0;       // k_chain_pipe: per packet 3 x positions pool / incoming slots
   uint8_t* tp = nullptr; uint64_t tp_bytes = 0;     // k_tree_pool: TpBufs
   uint8_t* tg = nullptr; uint64_t tg_bytes = 0;     // k_tree_setup / k_tree_grid: TgBufs
-  bool pipe = true;                               // pipelined chains where they fit (else the position sweep)
 };
 
 gg_status gg_noc_alloc(gg_ctx* ctx)
@@ -2362,8 +2344,8 @@ gg_status gg_noc_hbh(gg_ctx* ctx, const uint32_t* src, const uint32_t* dst, cons
     // chains: the general walk (chain_staged, the fallback of the pipeline and the sweep) stages the
     // chain's queue images in LDS
     const size_t chain_lds = (stage == 1 ? P.w : P.h) * qb;
-    const bool staged = S->staged && chain_lds <= kStageLdsMax;
-    if (S->staged && (stage == 0 || stage == 3)) {
+    const bool staged = chain_lds <= kStageLdsMax;
+    if (stage == 0 || stage == 3) {
       const uint32_t pb = (P.tiles + kPortWaves - 1) / kPortWaves;
       if (stage == 0)
         hipLaunchKernelGGL(k_port_sweep<false>, dim3(pb), dim3(64 * kPortWaves), kPortLds, s, D, len, S->off, S->ids,
@@ -2371,7 +2353,7 @@ gg_status gg_noc_hbh(gg_ctx* ctx, const uint32_t* src, const uint32_t* dst, cons
       else
         hipLaunchKernelGGL(k_port_sweep<true>, dim3(pb), dim3(64 * kPortWaves), kPortLds, s, D, len, S->off, S->ids,
                            S->heap, PS);
-    } else if (staged && S->pipe && std::max(P.w, P.h) <= kPipePos) {
+    } else if (staged && std::max(P.w, P.h) <= kPipePos) {
       const uint64_t stride = 3ull * std::max(P.w, P.h);
       if (S->pscr_cap < cap * stride) {
         if (S->pscr) hipFree(S->pscr);
@@ -2384,13 +2366,10 @@ gg_status gg_noc_hbh(gg_ctx* ctx, const uint32_t* src, const uint32_t* dst, cons
     } else if (staged) {
       hipLaunchKernelGGL(k_chain_sweep, dim3(nb), dim3(kSweepThreads), kStageLdsMax, s, D, stage - 1, dst, len, S->off,
                          S->ids, S->heap, PS, S->prof);
-    } else if (stage == 0)
-      hipLaunchKernelGGL(k_inject, dim3(tb), dim3(64), 0, s, D, src, dst, len, S->off, S->ids, S->heap, PS);
-    else if (stage == 3)
-      hipLaunchKernelGGL(k_self, dim3(tb), dim3(64), 0, s, D, dst, len, S->off, S->ids, S->heap, PS);
-    else
+    } else {
       hipLaunchKernelGGL(k_chain, dim3(tb), dim3(64), 0, s, D, stage - 1, src, dst, len, S->off, S->ids, S->heap,
                          PS, nb);
+    }
     GG_HIP(hipGetLastError());
   }
   gg_timer_end(ctx, "noc_hop_by_hop", s);
