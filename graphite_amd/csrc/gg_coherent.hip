@@ -2233,6 +2233,14 @@ __device__ __forceinline__ void lds_store_rel(uint64_t* p, uint64_t v)
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// the pipeline's packet word: time << 12 | position << 2 | status (times
+// < 2^51 are checked at staging; positions < 1024)
+__device__ __forceinline__ uint64_t pipe_word(uint64_t t, uint32_t pos, uint32_t status)
+{
+  return (t << 12) | ((uint64_t)pos << 2) | status;
+}
+__device__ __forceinline__ uint32_t pipe_pos(uint64_t w) { return (uint32_t)(w >> 2) & 0x3FFu; }
+
 struct WalkLds {
   uint64_t *Pt, *Ph, *Pk, *Pz;
   uint32_t *Pi, *Pp, *Pd, *Pf, *Pr;
@@ -2260,7 +2268,15 @@ __device__ __forceinline__ uint64_t serve_packet(const CP& P, const CS& S, const
   return qd;
 }
 
-template <bool PIPE>
+// RQ: the ports' queues are history trees held in registers (RegQueue;
+// walk_regq) — a separate instance, so the pipeline loop carries only that
+// request path (no LDS-image / list / M/G/1-only code, no spills)
+__host__ __device__ inline bool walk_regq(const CP& P)
+{
+  return P.np.qm && P.np.qtype == GG_QM_HISTORY_TREE && P.np.max_size <= kQMax;
+}
+
+template <bool PIPE, bool RQ>
 __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, int stage, uint32_t blk)
 {
   const uint32_t live = ((volatile uint32_t*)S.live)[L & 3];
@@ -2289,8 +2305,8 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
   gg_cmsg* cur = pool(S, p);
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t npos = sd.hi - sd.lo + 1;
-  const bool qm = P.np.qm != 0;
-  const bool regq = qm && P.np.qtype == GG_QM_HISTORY_TREE && P.np.max_size <= kQMax;
+  const bool qm = RQ || P.np.qm != 0;
+  constexpr bool regq = RQ;
   const bool sweep = !PIPE || n > 128 || P.walk_wide;     // more than 128 packets (or the A/B knob): wave 0 sweeps
   // the pipeline with register queues: each wave loads its port's history
   // tree straight from HBM into registers now, beside the packet staging
@@ -2323,6 +2339,8 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
     if (m.arrival_ps >> 51) atomicOr(S.err, GG_DERR_CAP);        // batch keys are time << 12 | rank
     W.Pf[i] = (uint32_t)nflits(P.np, has_data(m.type) ? P.bits_data : P.bits_req);
   }
+  if (!sweep)                     // the pipeline's moving state: one word per packet (W.Qt, unused by it)
+    for (uint32_t i = tid; i < n; i += nthr) W.Qt[i] = pipe_word(W.Pt[i], W.Pp[i], 0u);
   for (uint32_t i = tid; i < npos * kNetCtr; i += nthr) lc[i] = 0;
   for (uint32_t i = tid; i < kMaxWalkWaves; i += nthr) wlow[i] = 0;
   if (tid == 0) { rlohi[0] = ~0u; rlohi[1] = ~0u; rlohi[2] = 0; }
@@ -2368,7 +2386,7 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
   __syncthreads();
   PROF_AT(_w1);
   const bool wave_q = P.np.max_size <= kQMax;
-  const uint64_t zps = lat_to_ps((uint64_t)P.np.router_delay + P.np.link_delay, P.np.f);
+  const uint64_t zps = rfl64(lat_to_ps((uint64_t)P.np.router_delay + P.np.link_delay, P.np.f));   // scalar
   uint32_t nev = 0;
   // the port of one position, its queue in registers (history tree) or the LDS image
   auto port_queue = [&](uint32_t pos, RegQueue& rq, HTree& tr) {
@@ -2483,15 +2501,16 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
       waiting = false;
       const bool up_fin = bound == kInf;
       // the least pending packet at this position, by (time, rank): each lane
-      // its least (acquire on the position: the packet's time, written before
-      // it, is then current), then a scalar pass over the lanes holding one
-      const uint32_t q0 = c0 ? __hip_atomic_load(&W.Pp[ln], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) : ~0u;
-      const uint32_t q1 = c1 ? __hip_atomic_load(&W.Pp[ln + 64], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) : ~0u;
+      // its least (the packet words, read after the acquire of the horizon
+      // word: every packet forwarded before that word was written is seen),
+      // then a scalar pass over the lanes holding one
+      const uint64_t w0 = c0 ? W.Qt[ln] : ~0ull;
+      const uint64_t w1 = c1 ? W.Qt[ln + 64] : ~0ull;
       uint64_t mk = kInf;
       uint32_t mi = 0, mfd = 0;
-      if (q0 == pos) { mk = (W.Pt[ln] << 12) | r0; mi = ln; mfd = fd0; }
-      if (q1 == pos) {
-        const uint64_t k = (W.Pt[ln + 64] << 12) | r1;
+      if (pipe_pos(w0) == pos) { mk = (w0 & ~0xFFFull) | r0; mi = ln; mfd = fd0; }
+      if (pipe_pos(w1) == pos) {
+        const uint64_t k = (w1 & ~0xFFFull) | r1;
         if (k < mk) { mk = k; mi = ln + 64; mfd = fd1; }
       }
       uint64_t wk = kInf;
@@ -2524,18 +2543,17 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
       auto pub = [&](uint64_t qd) {
         if (tev) evp = __builtin_amdgcn_s_memtime();
         if (ln == 0) {
-          // time and status (the zero-load part: + zps per port, added at the
-          // hand-off) before the packet appears downstream (Pp), then the horizon
-          W.Pt[i] = T + zps + lat_to_ps(qd, P.np.f);
-          W.Pf[i] = nf | (status << 24);
-          __hip_atomic_store(&W.Pp[i], nx, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          // the packet word (time, next position, status; the zero-load part,
+          // + zps per port, is added at the hand-off), then the horizon
+          // (release: the word is visible first)
+          W.Qt[i] = pipe_word(T + zps + lat_to_ps(qd, P.np.f), nx, status);
           lds_store_rel(&wlow[wv], wk + 1);                   // every later key served here is > wk
         }
       };
       uint64_t qd = 0;
       if (!qm) pub(0ull);
       else {
-        const uint64_t tc = time_to_cycles(T, P.np.f);
+        const uint64_t tc = rfl64(time_to_cycles(T, P.np.f));
         if (regq) qd = rq.request_pub(tc, nf, pub);
         else { qd = wave_q ? tr.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err); pub(qd); }
       }
@@ -2568,20 +2586,23 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
   // hand-off
   uint32_t nb = 0;
   for (uint32_t i = tid; i < n; i += nthr) {
-    const uint32_t r = W.Pi[i], stt = W.Pf[i] >> 24;
-    const uint32_t h = tile_at(W.Pp[i]);
+    const uint32_t r = W.Pi[i];
+    uint32_t stt = W.Pf[i] >> 24, p1 = W.Pp[i];
+    uint64_t ta = W.Pt[i], z = W.Pz[i];
     gg_cmsg* m = cur + r;
-    uint64_t z = W.Pz[i];
-    if (!sweep) {                                              // the pipeline adds zps per port here
-      const uint32_t p0 = pos_of(m->hop), p1 = W.Pp[i];
+    if (!sweep) {                                              // the pipeline's word; it adds zps per port here
+      const uint64_t w = W.Qt[i];
+      const uint32_t p0 = p1;
+      ta = w >> 12; p1 = pipe_pos(w); stt = (uint32_t)w & 3u;
       z += (uint64_t)(dir ? p1 - p0 : p0 - p1) * zps;
     }
-    m->arrival_ps = W.Pt[i]; m->zero_load_ps = z; m->hop = h;
+    const uint32_t h = tile_at(p1);
+    m->arrival_ps = ta; m->zero_load_ps = z; m->hop = h;
     if (stt == 2) {                                            // held for the quantum boundary
       const uint32_t j = atomicAdd(S.bnd_cnt, 1u);
       if (j >= P.msg_cap) { atomicOr(S.err, GG_DERR_CAP); continue; }
       gg_cmsg g = *m;
-      g.arrival_ps = W.Pt[i]; g.zero_load_ps = z; g.hop = h;
+      g.arrival_ps = ta; g.zero_load_ps = z; g.hop = h;
       S.bnd[j] = g;
       ++nb;
       continue;
@@ -2653,13 +2674,13 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
   }
 }
 
-template <bool PIPE>
+template <bool PIPE, bool RQ>
 __global__ void __launch_bounds__(PIPE ? 64 * kMaxWalkWaves : 64) k_c_walk(CP P, CS S, uint32_t L, int stage)
 {
   kt_begin(S);
   if (S.trs && L < S.tr_n && threadIdx.x == 0)
     S.trw[(((size_t)L * 2 + stage) * S.tr_wb + blockIdx.x) * 8] = __builtin_amdgcn_s_memrealtime();
-  walk_body<PIPE>(P, S, L, stage, blockIdx.x);
+  walk_body<PIPE, RQ>(P, S, L, stage, blockIdx.x);
   kt_end(S);
 }
 
@@ -2725,9 +2746,11 @@ __global__ void __launch_bounds__(64) k_c_persist(CP P, CS S, uint32_t L0, uint3
     step_body<LC, true>(P, S, L, 1u, 0, W);
     grid_sync(S, gen);
     if (hbh) {
-      for (uint32_t b = blockIdx.x; b < P.nsx; b += gridDim.x) walk_body<false>(P, S, L, 0, b);
+      for (uint32_t b = blockIdx.x; b < P.nsx; b += gridDim.x)
+        if (walk_regq(P)) walk_body<false, true>(P, S, L, 0, b); else walk_body<false, false>(P, S, L, 0, b);
       grid_sync(S, gen);
-      for (uint32_t b = blockIdx.x; b < P.nsy; b += gridDim.x) walk_body<false>(P, S, L, 1, b);
+      for (uint32_t b = blockIdx.x; b < P.nsy; b += gridDim.x)
+        if (walk_regq(P)) walk_body<false, true>(P, S, L, 1, b); else walk_body<false, false>(P, S, L, 1, b);
       grid_sync(S, gen);
     }
     const uint64_t done = __hip_atomic_load(&S.qs[QS_DONE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2944,10 +2967,15 @@ constexpr uint64_t kTimeSample = 16;
 constexpr uint32_t kKtRing = 4096;      // in-kernel timing slots between two harvests (a batch is <= 256 steps)
 static void launch_walk(gg_coh_state* C, hipStream_t s, uint32_t blocks, uint32_t threads, uint32_t L, int stage)
 {
-  if (threads > 64)
-    hipLaunchKernelGGL(k_c_walk<true>, dim3(blocks), dim3(threads), C->walk_lds, s, C->P, C->S, L, stage);
+  const bool rq = walk_regq(C->P);
+  if (threads > 64 && rq)
+    hipLaunchKernelGGL((k_c_walk<true, true>), dim3(blocks), dim3(threads), C->walk_lds, s, C->P, C->S, L, stage);
+  else if (threads > 64)
+    hipLaunchKernelGGL((k_c_walk<true, false>), dim3(blocks), dim3(threads), C->walk_lds, s, C->P, C->S, L, stage);
+  else if (rq)
+    hipLaunchKernelGGL((k_c_walk<false, true>), dim3(blocks), dim3(64), C->walk_lds, s, C->P, C->S, L, stage);
   else
-    hipLaunchKernelGGL(k_c_walk<false>, dim3(blocks), dim3(64), C->walk_lds, s, C->P, C->S, L, stage);
+    hipLaunchKernelGGL((k_c_walk<false, false>), dim3(blocks), dim3(64), C->walk_lds, s, C->P, C->S, L, stage);
 }
 constexpr uint32_t kPersistTiles = 64;        // owned tiles up to which gg_coherent_run uses k_c_persist
 constexpr uint32_t kPersistLaunches = 16384;  // launch indices per k_c_persist launch
@@ -3228,7 +3256,8 @@ static gg_status coh_alloc(gg_ctx* ctx)
   }
   GG_HIP(hipFuncSetAttribute((const void*)k_c_step, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C->step_lds));
   if (P.net == GG_NET_EMESH_HOP_BY_HOP)
-    for (const void* f : {(const void*)k_c_walk<true>, (const void*)k_c_walk<false>})
+    for (const void* f : {(const void*)k_c_walk<true, true>, (const void*)k_c_walk<true, false>,
+                          (const void*)k_c_walk<false, true>, (const void*)k_c_walk<false, false>})
       GG_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C->walk_lds));
     GG_HIP(hipFuncSetAttribute((const void*)k_c_persist<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)std::max(C->walk_lds, C->step_lds)));

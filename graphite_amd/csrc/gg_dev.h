@@ -433,6 +433,13 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l)
   return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), (int)l) << 32) |
          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
 }
+// a wave-uniform 64-bit value into SGPRs (values computed on the vector ALU,
+// e.g. FP64, or loaded by an atomic, are otherwise kept in VGPRs)
+__device__ __forceinline__ uint64_t rfl64(uint64_t v)
+{
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+}
 template <int CTRL> __device__ __forceinline__ uint64_t dpp64(uint64_t v)
 {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)v, (int)(uint32_t)v, CTRL, 0xf, 0xf, false);
@@ -448,7 +455,7 @@ template <int PRED> __device__ __forceinline__ uint64_t cmp64(uint64_t a, uint64
 {
   return __builtin_amdgcn_uicmpl(a, b, PRED);
 }
-constexpr int kCmpULE = 37, kCmpUGE = 35;     // ICmpInst predicates
+constexpr int kCmpULE = 37, kCmpUGE = 35, kCmpUGT = 34;     // ICmpInst predicates
 __device__ __forceinline__ uint64_t low_lanes(uint32_t n) { return n >= 64 ? ~0ull : ((1ull << n) - 1); }
 
 struct RegQueue {
@@ -463,11 +470,15 @@ struct RegQueue {
 
   __device__ __forceinline__ void load(const HQueue* q, const HNode* nd, uint64_t mp, bool an, uint32_t lane)
   {
+    // the header is wave-uniform: into SGPRs (a load from memory the kernel
+    // also writes lands in VGPRs, and the size would then steer every request
+    // through exec-masked branches)
     ln = lane; min_proc = mp; analytical = an; errs = 0; errp = nullptr;
-    sz = q->size; cap = q->max_size;
-    const uint32_t head = q->head;
-    sig_sq = q->sig_sq; sig = q->sig; nreq = q->n; newest = q->newest;
-    util = q->util; last_req = q->last_req; total_req = q->total_req; anl = q->analytical;
+    sz = (uint32_t)__builtin_amdgcn_readfirstlane((int)q->size);
+    cap = (uint32_t)__builtin_amdgcn_readfirstlane((int)q->max_size);
+    const uint32_t head = (uint32_t)__builtin_amdgcn_readfirstlane((int)q->head);
+    sig_sq = rfl64(q->sig_sq); sig = rfl64(q->sig); nreq = rfl64(q->n); newest = rfl64(q->newest);
+    util = rfl64(q->util); last_req = rfl64(q->last_req); total_req = rfl64(q->total_req); anl = rfl64(q->analytical);
     a0 = b0 = a1 = b1 = 0;
     uint32_t j = head + ln; if (j >= cap) j -= cap;
     if (ln < sz) { const HNode x = nd[j]; a0 = x.first; b0 = x.second; }
@@ -600,17 +611,19 @@ struct RegQueue {
     ++total_req;
     return qd;
   }
-  // The same request (request<false>) with the delay handed to pub(qd) as
-  // soon as it is known, before the interval list and the M/G/1 sums are
-  // updated: a pipeline stage forwards its packet first and does the
-  // bookkeeping while the next stage runs (this queue's next request comes
-  // from the same wave, after it).  Uniform values are kept scalar
-  // (readfirstlane) so a loop around it carries them in SGPRs.
-  __device__ __forceinline__ uint64_t rd64(uint64_t v) const
-  {
-    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
-           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
-  }
+  // The same request with the delay handed to pub(qd) as soon as it is
+  // known, before the interval list and the M/G/1 sums are updated: a
+  // pipeline stage forwards its packet first and does the bookkeeping while
+  // the next stage runs (this queue's next request comes from the same wave,
+  // after it).  One vector search serves every case (no last-interval
+  // pre-check: the walkers' requests land mid-list, and the last interval
+  // [x, inf) is found by the same compares): the interval holding t fits
+  // [t, t+p] -> no delay, published after two compares; otherwise either the
+  // analytical branch (interval 0 starts after t + p; never with a fit, whose
+  // interval starts at or before t) or the first later interval long enough.
+  // Uniform values are kept scalar (readfirstlane) so a loop around it
+  // carries them in SGPRs.
+  __device__ __forceinline__ uint64_t rd64(uint64_t v) const { return rfl64(v); }
   __device__ __forceinline__ uint64_t A1(uint32_t i) const { return i < 64 ? rl64(a0, i) : rl64(a1, i - 64); }
   __device__ __forceinline__ uint64_t B1(uint32_t i) const { return i < 64 ? rl64(b0, i) : rl64(b1, i - 64); }
   template <class Pub>
@@ -619,50 +632,41 @@ struct RegQueue {
     if (sz >= cap) { shift_down(0); --sz; }                          // prune the min node (:52-56)
     uint64_t qd = 0;
     const uint64_t tp = t + p;
-    const uint32_t il = sz - 1;
-    const uint64_t la = A1(il), lb = B1(il);
-    if (la <= t && tp <= lb && lb - tp >= min_proc) {                // the last interval: no search, no delay
+    const uint64_t v0 = low_lanes(sz), v1 = sz > 64 ? low_lanes(sz - 64) : 0ull;
+    const uint64_t le0 = cmp64<kCmpULE>(a0, t) & v0, le1 = cmp64<kCmpULE>(a1, t) & v1;
+    const uint64_t f0 = le0 & cmp64<kCmpUGE>(b0, tp), f1 = le1 & cmp64<kCmpUGE>(b1, tp);
+    if (f0 | f1) {                                                   // a <= t, t + p <= b: no delay
       pub(0ull);
-      ++n_fast;
-      if (t - la >= min_proc) { set(il, la, t); set(sz, tp, lb); ++sz; }
-      else set(il, tp, lb);
-    } else if (analytical && A1(0) > tp) {
+      ++n_gen;
+      const uint32_t ui = f0 ? (uint32_t)__builtin_ctzll(f0) : 64u + (uint32_t)__builtin_ctzll(f1);
+      const uint64_t a = A1(ui), b = B1(ui);
+      if (t - a >= min_proc) {
+        if (b - tp >= min_proc) { shift_up(ui + 1); set(ui + 1, tp, b); ++sz; }
+        set(ui, a, t);
+      } else if (b - tp >= min_proc) {
+        set(ui, tp, b);
+      } else {
+        shift_down(ui); --sz;
+      }
+    } else if (analytical && (cmp64<kCmpUGT>(a0, tp) & 1ull)) {     // interval 0 starts after t + p
       qd = mg1_queue_delay(nreq, newest, sig_sq, sig);
       pub(qd);
       ++anl; ++n_anl;
-    } else {
+    } else {                                                         // the first later interval long enough
       ++n_gen;
-      const uint64_t v0 = low_lanes(sz), v1 = sz > 64 ? low_lanes(sz - 64) : 0ull;
-      const uint64_t le0 = cmp64<kCmpULE>(a0, t) & v0, le1 = cmp64<kCmpULE>(a1, t) & v1;
-      const uint64_t f0 = le0 & cmp64<kCmpUGE>(b0, tp), f1 = le1 & cmp64<kCmpUGE>(b1, tp);
-      const bool fit = (f0 | f1) != 0;
-      uint64_t m0 = f0, m1 = f1;
-      if (!fit) {
-        m0 = ~le0 & v0 & cmp64<kCmpUGE>(b0 - a0, p);
-        m1 = ~le1 & v1 & cmp64<kCmpUGE>(b1 - a1, p);
-      }
+      const uint64_t m0 = ~le0 & v0 & cmp64<kCmpUGE>(b0 - a0, p);
+      const uint64_t m1 = ~le1 & v1 & cmp64<kCmpUGE>(b1 - a1, p);
       if ((m0 | m1) == 0) {
         pub(0ull);
         errs |= GG_DERR_STATE;
       } else {
         const uint32_t ui = m0 ? (uint32_t)__builtin_ctzll(m0) : 64u + (uint32_t)__builtin_ctzll(m1);
-        const uint64_t a = A1(ui), b = B1(ui);
-        if (fit) {                                                   // t >= a
-          pub(0ull);
-          if (t - a >= min_proc) {
-            if (b - tp >= min_proc) { shift_up(ui + 1); set(ui + 1, tp, b); ++sz; }
-            set(ui, a, t);
-          } else if (b - tp >= min_proc) {
-            set(ui, tp, b);
-          } else {
-            shift_down(ui); --sz;
-          }
-        } else {                                                     // the first later interval long enough
-          qd = a - t;
-          pub(qd);
-          if (b - (a + p) >= min_proc) set(ui, a + p, b);
-          else { shift_down(ui); --sz; }
-        }
+        const uint64_t a = A1(ui);
+        qd = a - t;
+        pub(qd);
+        const uint64_t b = B1(ui);
+        if (b - (a + p) >= min_proc) set(ui, a + p, b);
+        else { shift_down(ui); --sz; }
       }
     }
     sig_sq = rd64(sig_sq + p * p);                                   // QueueModelMG1::updateQueue
