@@ -80,6 +80,10 @@ __device__ __forceinline__ bool has_data(uint32_t t)
 
 struct DEnt { uint64_t addr; int32_t owner; uint16_t dstate; uint16_t nsh; };   // 16 B
 struct CReq { uint64_t addr, time; uint32_t type, requester; };                 // 24 B
+// address-space-typed pointers (a generic pointer whose origin the compiler
+// cannot see compiles to flat accesses)
+#define GG_LDS __attribute__((address_space(3)))
+#define GG_GLB __attribute__((address_space(1)))
 struct Seg { uint32_t line, lo, hi, pad; };       // a run of row (X) / column (Y) `line`: positions [lo, hi]
 // device-driven quantum loop (gg_coherent_run): current quantum, launch index
 // of its step 0, run over, quantum-end arrivals, active / blocked tiles, least
@@ -595,8 +599,8 @@ struct Tile {
   uint64_t sd;                          // this step's statistics increments: lane k holds statistic k
   uint64_t rec, rec_end, clk, pend_start, out_addr, out_time;
   uint32_t blocked, seq, nrep, nrq;
-  HQueue* dq; HNode* dnd; bool dq_lds;
-  CReq* rqp; bool rq_lds;
+  bool dq_lds;                          // the DRAM queue image in LDS (sl.dimg), else in HBM
+  GG_GLB CReq* rqg; bool rq_lds;         // the request FIFO in HBM, or in LDS (sl.rq) when it fits
   uint32_t nch, cbase, cused, ccap, nsent;
   bool failed;
   uint32_t ferr;                         // GG_DERR_* gathered by fail()
@@ -639,8 +643,8 @@ struct Tile {
     rec = pre.rec; rec_end = pre.rec_end; clk = pre.clk; pend_start = pre.pend_start;
     out_addr = pre.out_addr; out_time = pre.out_time;
     blocked = pre.blocked; seq = pre.seq; nrep = pre.nrep; nrq = pre.nrq;
-    dq = S.dq + lt; dnd = S.dnd + (size_t)lt * P.max_list; dq_lds = false;
-    rqp = S.rq + (size_t)lt * P.QC; rq_lds = false;
+    dq_lds = false;
+    rqg = (GG_GLB CReq*)(S.rq + (size_t)lt * P.QC); rq_lds = false;
     nch = 0; cbase = 0; cused = 0; ccap = 0; nsent = 0; failed = false; ferr = 0;
     ccv = pre.ccv; stv = pre.stv;
   }
@@ -710,14 +714,21 @@ struct Tile {
   __device__ __forceinline__ uint32_t home(uint64_t a) const { return (uint32_t)((a >> 6) % P.T); }   // address_home_lookup.cc:19-26
 
   // ---- directory (DirectoryCache + DirectoryEntryFullMap) ------------------
+  // (h is wave-uniform: readfirstlane keeps the entry / sharer-word pointers
+  // scalar — a per-lane select between the two arrays would hold both bases
+  // in VGPRs for the whole step; rep_ent serves the per-lane scans of the
+  // replaced list)
   __device__ __forceinline__ DEnt* ent(int32_t h) const
   {
+    h = __builtin_amdgcn_readfirstlane(h);
     return h >= 0 ? S.dir + (size_t)lt * P.E + h : S.rep + (size_t)lt * P.R + (-h - 1);
   }
   __device__ __forceinline__ uint64_t* shw(int32_t h) const
   {
+    h = __builtin_amdgcn_readfirstlane(h);
     return h >= 0 ? S.dsh + ((size_t)lt * P.E + h) * P.W : S.rsh + ((size_t)lt * P.R + (-h - 1)) * P.W;
   }
+  __device__ __forceinline__ const DEnt* rep_ent(uint32_t i) const { return S.rep + (size_t)lt * P.R + i; }
   __device__ __forceinline__ bool has(int32_t h, uint32_t s) const { return (shw(h)[s >> 6] >> (s & 63)) & 1ull; }
   __device__ __forceinline__ void add_sharer(int32_t h, uint32_t s)                 // addSharer (full_map.cc:27-33)
   {
@@ -766,7 +777,7 @@ struct Tile {
       if (ln < P.W) shw((int32_t)i)[ln] = 0;
       return (int32_t)i;
     }
-    const uint64_t rv = ln < nrep ? ent(-(int32_t)ln - 1)->addr : 0;
+    const uint64_t rv = ln < nrep ? rep_ent(ln)->addr : 0;
     const uint64_t rh = __ballot(ln < nrep && rv == a);
     if (rh) return -(int32_t)__builtin_ctzll(rh) - 1;
     return NO_ENT;
@@ -798,7 +809,7 @@ struct Tile {
   __device__ __forceinline__ void dinvalidate(uint64_t a)
   {
     const uint32_t nr = nrep;
-    const uint64_t rv = ln < nr ? ent(-(int32_t)ln - 1)->addr : 0;
+    const uint64_t rv = ln < nr ? rep_ent(ln)->addr : 0;
     const uint64_t rh = __ballot(ln < nr && rv == a);
     if (!rh) { fail(); return; }
     for (uint32_t k = (uint32_t)__builtin_ctzll(rh); k + 1 < nr; ++k) {
@@ -830,17 +841,33 @@ struct Tile {
   }
 
   // ---- per-address request FIFO (HashMapList<IntPtr, ShmemReq*>) -----------
+  // Every access branches on rq_lds with each side's pointer typed by its
+  // address space: a pointer merged from the two would compile to flat
+  // accesses, and a flat access waits for every store the step has in flight
+  __device__ __forceinline__ GG_LDS CReq* lrq() const { return (GG_LDS CReq*)sl.rq; }
+  __device__ __forceinline__ uint64_t rq_addr(uint32_t i) const { return rq_lds ? lrq()[i].addr : rqg[i].addr; }
+  __device__ __forceinline__ CReq rq_get(uint32_t i) const
+  {
+    if (rq_lds) { const GG_LDS CReq* x = lrq() + i; return CReq{x->addr, x->time, x->type, x->requester}; }
+    const GG_GLB CReq* x = rqg + i;
+    return CReq{x->addr, x->time, x->type, x->requester};
+  }
+  __device__ __forceinline__ void rq_put(uint32_t i, const CReq& v)
+  {
+    if (rq_lds) { GG_LDS CReq* x = lrq() + i; x->addr = v.addr; x->time = v.time; x->type = v.type; x->requester = v.requester; }
+    else { GG_GLB CReq* x = rqg + i; x->addr = v.addr; x->time = v.time; x->type = v.type; x->requester = v.requester; }
+  }
   __device__ __forceinline__ uint32_t qcount(uint64_t a) const
   {
     uint32_t c = 0;
-    for (uint32_t i = ln; i < nrq; i += 64) c += (rqp[i].addr == a);
+    for (uint32_t i = ln; i < nrq; i += 64) c += (rq_addr(i) == a);
     return wave_sum(c);
   }
   __device__ __forceinline__ int32_t qfront(uint64_t a) const
   {
     for (uint32_t b = 0; b < nrq; b += 64) {
       const uint32_t i = b + ln;
-      const uint64_t m = __ballot(i < nrq && rqp[i].addr == a);
+      const uint64_t m = __ballot(i < nrq && rq_addr(i) == a);
       if (m) return (int32_t)(b + __builtin_ctzll(m));
     }
     return -1;
@@ -848,7 +875,7 @@ struct Tile {
   __device__ __forceinline__ void qpush(uint64_t a, uint64_t t, uint32_t type, uint32_t req)
   {
     if (nrq >= (rq_lds ? SL::kRq : P.QC)) { fail(GG_DERR_CAP); return; }
-    rqp[nrq] = CReq{a, t, type, req};
+    rq_put(nrq, CReq{a, t, type, req});
     if (rq_lds) wave_sync();
     ++nrq;
   }
@@ -860,13 +887,13 @@ struct Tile {
       for (uint32_t b = (uint32_t)f + 1; b < nrq; b += 64) {
         const uint32_t i = b + ln;
         CReq v{};
-        if (i < nrq) v = rqp[i];
+        if (i < nrq) v = rq_get(i);
         wave_sync();
-        if (i < nrq) rqp[i - 1] = v;
+        if (i < nrq) rq_put(i - 1, v);
         wave_sync();
       }
     } else {
-      for (uint32_t k = (uint32_t)f; k + 1 < nrq; ++k) rqp[k] = rqp[k + 1];
+      for (uint32_t k = (uint32_t)f; k + 1 < nrq; ++k) rq_put(k, rq_get(k + 1));
     }
     --nrq;
   }
@@ -877,10 +904,10 @@ struct Tile {
   }
   __device__ __forceinline__ void front_update(int32_t f, uint64_t& t, uint32_t& type, uint32_t& requester)
   {
-    CReq r = rqp[f];
+    CReq r = rq_get(f);
     front_time(r, t);
     if (rq_lds) wave_sync();
-    rqp[f].time = r.time;
+    if (rq_lds) lrq()[f].time = r.time; else rqg[f].time = r.time;
     if (rq_lds) wave_sync();
     type = r.type; requester = r.requester;
   }
@@ -891,8 +918,16 @@ struct Tile {
     const uint64_t pkt_ns = time_to_cycles(t, 1.0);                  // ceil(t / 1000.0)
     uint64_t qd = 0;
     if (P.dram_qm) {
-      HTree tr{dq, dnd, P.dram_proc, P.analytical != 0};
-      qd = dq_lds ? tr.delay_w(pkt_ns, P.dram_proc, S.err, ln) : tr.delay(pkt_ns, P.dram_proc, S.err);
+      // each side's queue pointers derived where they are used (LDS / HBM):
+      // a pointer merged from the two would make every queue access flat
+      if (dq_lds) {
+        HTree tr{reinterpret_cast<HQueue*>(sl.dimg), reinterpret_cast<HNode*>(sl.dimg + sizeof(HQueue)), P.dram_proc,
+                 P.analytical != 0};
+        qd = tr.delay_w(pkt_ns, P.dram_proc, S.err, ln);
+      } else {
+        HTree tr{S.dq + lt, S.dnd + (size_t)lt * P.max_list, P.dram_proc, P.analytical != 0};
+        qd = tr.delay(pkt_ns, P.dram_proc, S.err);
+      }
       stat(GG_CT_DRAM_QUEUE_REQUESTS, 1);
     }
     const uint64_t lat = qd + P.dram_proc + P.dram_cost;
@@ -922,7 +957,7 @@ struct Tile {
           if (ln < P.dassoc) {
             const DEnt e = d[base + ln];
             uint32_t qc = 0;
-            for (uint32_t i = 0; i < nrq; ++i) qc += (rqp[i].addr == e.addr);
+            for (uint32_t i = 0; i < nrq; ++i) qc += (rq_addr(i) == e.addr);
             if (qc == 0) key = ((uint32_t)e.nsh << 8) | ln;
           }
           key = wave_min(key);
@@ -1671,11 +1706,14 @@ __device__ __forceinline__ void publish_hbh_lds(TT& T, gg_cmsg* cur, uint32_t nl
   if (S.trs) q1 = __builtin_amdgcn_s_memtime();
   order_port_local(nn, sl.x1, sl.x1, sl.x2, sl.i2, ln);
   if (S.trs) q2 = __builtin_amdgcn_s_memtime();
+  // the port's queue: tr in HBM, trl the LDS image (one address space each:
+  // a pointer merged from the two would make every queue access flat)
   HTree tr{gq, gnd, 1, P.np.analytical != 0};
+  HTree trl{reinterpret_cast<HQueue*>(sl.pimg), reinterpret_cast<HNode*>(sl.pimg + sizeof(HQueue)), 1,
+            P.np.analytical != 0};
   if (wave) {
     img_in(sl.pimg, gq, gnd, P.np.max_size, ln);
     tsync();
-    tr.q = reinterpret_cast<HQueue*>(sl.pimg); tr.nd = reinterpret_cast<HNode*>(sl.pimg + sizeof(HQueue));
   }
   if (S.trs) { (void)__builtin_amdgcn_readfirstlane((int)rq.a0); q3 = __builtin_amdgcn_s_memtime(); }
   uint64_t ps = 0, fs = 0, bs = 0;
@@ -1696,7 +1734,7 @@ __device__ __forceinline__ void publish_hbh_lds(TT& T, gg_cmsg* cur, uint32_t nl
       uint64_t qd = 0;
       if (P.np.qm) {
         const uint64_t tc = time_to_cycles(rl64(sp, k), P.np.f);
-        qd = regq ? rq.request(tc, nf, S.err) : (wave ? tr.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
+        qd = regq ? rq.request(tc, nf, S.err) : (wave ? trl.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
       }
       if (ln == k) oq = qd;
       fs += nf; bs += (uint32_t)__builtin_amdgcn_readlane((int)bits, (int)k);   // updateSendCounters (network_model.cc:228-251)
@@ -1754,10 +1792,6 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
   if (na) {
     if (S.prof || S.trs) _sb = __builtin_amdgcn_s_memtime();
     const uint32_t* al = arv(S, p) + (size_t)lt * P.IC;
-    const bool lds = na <= SL::kIn;
-    uint64_t* t_ = lds ? sl.x1 : gscr; uint64_t* s_ = lds ? sl.x2 : gscr + P.IC; uint64_t* k_ = lds ? sl.x3 : gscr + 2 * P.IC;
-    uint64_t* z_a = lds ? sl.x4 : gscr + 5 * P.IC;
-    uint32_t* i_ = lds ? sl.i1 : (uint32_t*)(gscr + 3 * P.IC); uint32_t* o_ = lds ? sl.i2 : (uint32_t*)(gscr + 4 * P.IC);
     // the port's queue in registers for the batch (RegQueue, its loads in
     // flight beside the records'); other models on an LDS image
     const uint64_t qi = (uint64_t)T.tile * 6 + P_SELF;
@@ -1767,6 +1801,18 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
     const bool wave = P.np.qm && P.np.max_size <= kQMax && !regq;
     RegQueue rq;
     if (regq) rq.load(gq, gnd, 1, P.np.analytical != 0, ln);
+    const uint64_t zps = lat_to_ps((uint64_t)P.np.router_delay + P.np.link_delay, P.np.f);
+    uint64_t cq = 0, cf = 0;                                   // uniform: contention cycles, flits
+    uint64_t rf = 0, rb = 0, rl = 0, rc = 0;                   // uniform: received flits, bits, latency, contention
+    const uint64_t rn = na;
+    gg_cmsg* pv = const_cast<gg_cmsg*>(prev);
+    // the batch in LDS (or, past kIn entries, in HBM scratch): one instance
+    // per place, so every access has one address space (no flat accesses)
+    auto self_batch = [&](auto in_lds) __attribute__((always_inline)) {
+    constexpr bool LD = decltype(in_lds)::value;
+    uint64_t* t_ = LD ? sl.x1 : gscr; uint64_t* s_ = LD ? sl.x2 : gscr + P.IC; uint64_t* k_ = LD ? sl.x3 : gscr + 2 * P.IC;
+    uint64_t* z_a = LD ? sl.x4 : gscr + 5 * P.IC;
+    uint32_t* i_ = LD ? sl.i1 : (uint32_t*)(gscr + 3 * P.IC); uint32_t* o_ = LD ? sl.i2 : (uint32_t*)(gscr + 4 * P.IC);
     // 4 records per lane in flight: the list words, then the records (a
     // fan-in of hundreds of acknowledgements at a hot line's home otherwise
     // waits two dependent memory round trips per 64 records); every field
@@ -1796,18 +1842,16 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
     if (S.prof || S.trs) _sc = __builtin_amdgcn_s_memtime();
     order_port_local(na, t_, s_, k_, o_, ln);
     if (S.prof || S.trs) _sd = __builtin_amdgcn_s_memtime();
+    // the port's queue: tr in HBM, trl the LDS image (one address space each:
+    // a pointer merged from the two would make every queue access flat)
     HTree tr{gq, gnd, 1, P.np.analytical != 0};
+    HTree trl{reinterpret_cast<HQueue*>(sl.pimg), reinterpret_cast<HNode*>(sl.pimg + sizeof(HQueue)), 1,
+              P.np.analytical != 0};
     if (wave) {
       img_in(sl.pimg, gq, gnd, P.np.max_size, ln);
       tsync();
-      tr.q = reinterpret_cast<HQueue*>(sl.pimg); tr.nd = reinterpret_cast<HNode*>(sl.pimg + sizeof(HQueue));
     }
     if (S.prof || S.trs) { (void)__builtin_amdgcn_readfirstlane((int)rq.a0); _se = __builtin_amdgcn_s_memtime(); }
-    const uint64_t zps = lat_to_ps((uint64_t)P.np.router_delay + P.np.link_delay, P.np.f);
-    uint64_t cq = 0, cf = 0;                                   // uniform: contention cycles, flits
-    uint64_t rf = 0, rb = 0, rl = 0, rc = 0;                   // uniform: received flits, bits, latency, contention
-    const uint64_t rn = na;
-    gg_cmsg* pv = const_cast<gg_cmsg*>(prev);
     for (uint32_t c0 = 0; c0 < na; c0 += 64) {
       const uint32_t cnt = min(64u, na - c0);
       uint32_t r = 0, nf_ = 0, bits = 0;
@@ -1829,7 +1873,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
         if (P.np.qm) {
           const uint64_t tc = time_to_cycles(t, P.np.f);
           ntail += tc >= x0;
-          qd = regq ? rq.request(tc, nf, S.err) : (wave ? tr.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
+          qd = regq ? rq.request(tc, nf, S.err) : (wave ? trl.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
         }
         cq += qd; cf += nf;
         // serialization + receive (network_model.cc:118-150), uniform: the
@@ -1844,6 +1888,8 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
       if (S.trs) _sf = __builtin_amdgcn_s_memtime();
       if (ln < cnt) { pv[r].arrival_ps = ot; pv[r].zero_load_ps = oz; }
     }
+    };
+    if (na <= SL::kIn) self_batch(std::true_type{}); else self_batch(std::false_type{});
     if (regq) rq.store(gq, gnd);
     if (wave) { tsync(); img_out(gq, gnd, sl.pimg, P.np.max_size, ln); }
     // lanes 0-6: the SELF port (contention, router packets, buffer writes, switch, crossbar, link, buffer reads), 8-12: the receiver
@@ -1867,20 +1913,22 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
   if (T.nrq + 2 * n + 2 <= SL::kRq) {
     const CReq* g = S.rq + (size_t)lt * P.QC;
     for (uint32_t i = ln; i < T.nrq; i += 64) sl.rq[i] = g[i];
-    T.rqp = sl.rq; T.rq_lds = true;
+    T.rq_lds = true;
   }
   if (P.dram_qm && P.max_list <= kQMax && n) {
     img_in(sl.dimg, S.dq + lt, S.dnd + (size_t)lt * P.max_list, P.max_list, ln);
-    T.dq = reinterpret_cast<HQueue*>(sl.dimg); T.dnd = reinterpret_cast<HNode*>(sl.dimg + sizeof(HQueue));
     T.dq_lds = true;
   }
   tsync();
   if (n) {
     const bool lds = n <= SL::kIn;
-    uint64_t* a_ = lds ? sl.x1 : gscr; uint64_t* k_ = lds ? sl.x2 : gscr + P.IC; uint64_t* m_ = lds ? sl.x3 : gscr + 2 * P.IC;
-    uint32_t* i_ = lds ? sl.i1 : (uint32_t*)(gscr + 3 * P.IC); uint32_t* o_ = lds ? sl.i2 : (uint32_t*)(gscr + 4 * P.IC);
     const uint32_t* il = inb(S, p) + (size_t)lt * P.IC;
     const uint32_t* al = arv(S, p) + (size_t)lt * P.IC;
+    // gather + order: one instance per place of the batch (as self_batch)
+    auto inbox_batch = [&](auto in_lds) __attribute__((always_inline)) {
+    constexpr bool LD = decltype(in_lds)::value;
+    uint64_t* a_ = LD ? sl.x1 : gscr; uint64_t* k_ = LD ? sl.x2 : gscr + P.IC; uint64_t* m_ = LD ? sl.x3 : gscr + 2 * P.IC;
+    uint32_t* i_ = LD ? sl.i1 : (uint32_t*)(gscr + 3 * P.IC); uint32_t* o_ = LD ? sl.i2 : (uint32_t*)(gscr + 4 * P.IC);
     for (uint32_t i0 = ln; i0 < n; i0 += 256) {                   // 4 records per lane in flight
       uint32_t rr[4];
 #pragma unroll
@@ -1902,11 +1950,14 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
     tsync();
     hk.clear_inb(p, lt);
     order_inbox(n, a_, k_, m_, i_, o_, ln);
+    };
+    if (lds) inbox_batch(std::true_type{}); else inbox_batch(std::false_type{});
+    const uint32_t* go_ = (const uint32_t*)(gscr + 4 * P.IC);
     PROF_AT(_p1b);
     _q1b = _p1b;
     if (S.prof && ln == 0) atomicAdd(&S.prof[9], (unsigned long long)(_p1b - _p1));
     for (uint32_t j = 0; j < n && !T.failed; ++j) {
-      const gg_cmsg m = prev[o_[j]];
+      const gg_cmsg m = prev[lds ? sl.i2[j] : go_[j]];
       T.stat(GG_CT_MSGS_RECEIVED, 1);
       if (to_directory(m.type)) T.directory_msg(m); else T.l2_msg(m);
     }
@@ -1975,10 +2026,12 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
   const uint32_t np_ = T.nsent;
   uint64_t ri_net = 0, ri_self = 0, ri_bnd = 0;
   if (np_) {
-    const bool lds = np_ <= SL::kIn;
-    uint64_t* t_ = lds ? sl.x1 : gscr; uint64_t* s_ = lds ? sl.x2 : gscr + P.IC; uint64_t* k_ = lds ? sl.x3 : gscr + 2 * P.IC;
-    uint32_t* i_ = lds ? sl.i1 : (uint32_t*)(gscr + 3 * P.IC); uint32_t* o_ = lds ? sl.i2 : (uint32_t*)(gscr + 4 * P.IC);
-    if (!lds && np_ > P.IC) T.fail(GG_DERR_CAP);
+    // one instance per place of the batch (as self_batch)
+    auto pub_batch = [&](auto in_lds) __attribute__((always_inline)) {
+    constexpr bool LD = decltype(in_lds)::value;
+    uint64_t* t_ = LD ? sl.x1 : gscr; uint64_t* s_ = LD ? sl.x2 : gscr + P.IC; uint64_t* k_ = LD ? sl.x3 : gscr + 2 * P.IC;
+    uint32_t* i_ = LD ? sl.i1 : (uint32_t*)(gscr + 3 * P.IC); uint32_t* o_ = LD ? sl.i2 : (uint32_t*)(gscr + 4 * P.IC);
+    if (!LD && np_ > P.IC) T.fail(GG_DERR_CAP);
     // the records of the chunks, in allocation order
     uint32_t off = 0;
     for (uint32_t c = 0; c < T.nch && !T.failed; ++c) {
@@ -2009,7 +2062,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
           ri_bnd++;
         }
       }
-    } else if (lds && np_ == nloc) {
+    } else if (LD && np_ == nloc) {
       publish_hbh_lds(T, cur, nloc, ri_net, ri_self, hk, _q1, _q2, _q3, _q4);
     } else {
       // self-sends: straight to the next inbox (processCornerCases, network_model.cc:413-424)
@@ -2047,12 +2100,15 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
         HNode* gnd = S.nnd + qi * P.np.max_size;
         const bool regq = P.np.qm && P.np.qtype == GG_QM_HISTORY_TREE && P.np.max_size <= kQMax;
         const bool wave = P.np.qm && P.np.max_size <= kQMax && !regq;
+        // the port's queue: tr in HBM, trl the LDS image (one address space each:
+        // a pointer merged from the two would make every queue access flat)
         HTree tr{gq, gnd, 1, P.np.analytical != 0};
+        HTree trl{reinterpret_cast<HQueue*>(sl.pimg), reinterpret_cast<HNode*>(sl.pimg + sizeof(HQueue)), 1,
+                  P.np.analytical != 0};
         if (wave) {
           img_in(sl.pimg, gq, gnd, P.np.max_size, ln);
           tsync();
-          tr.q = reinterpret_cast<HQueue*>(sl.pimg); tr.nd = reinterpret_cast<HNode*>(sl.pimg + sizeof(HQueue));
-        }
+            }
         RegQueue rq;
         if (regq) rq.load(gq, gnd, 1, P.np.analytical != 0, ln);
         if (S.trs) { (void)__builtin_amdgcn_readfirstlane((int)rq.a0); _q3 = __builtin_amdgcn_s_memtime(); }
@@ -2077,7 +2133,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
             if (P.np.qm) {
               const uint64_t tc = time_to_cycles(rl64(sp, k), P.np.f);
               ntail += tc >= x0;
-              qd = regq ? rq.request(tc, nf, S.err) : (wave ? tr.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
+              qd = regq ? rq.request(tc, nf, S.err) : (wave ? trl.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
             }
             if (ln == k) oq = qd;
             fs += nf; bs += (uint32_t)__builtin_amdgcn_readlane((int)bits, (int)k);   // updateSendCounters, uniform
@@ -2110,6 +2166,8 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
         }
       }
     }
+    };
+    if (np_ <= SL::kIn) pub_batch(std::true_type{}); else pub_batch(std::false_type{});
   }
 
   PROF_AT(_p4);
