@@ -170,7 +170,7 @@ struct CS {
 // profile slots: step phases 0..5 summed over tiles, 8 = sum over steps of the slowest tile;
 // walker: 16 staging+load, 17 event loop, 18 hand-off+write back, 19 events, 20 sum of slowest walker per launch (X),
 // 21 (Y), 22 launches
-constexpr uint32_t kTrStep = 24;       // GG_COH_TRACE words per (launch, tile)
+constexpr uint32_t kTrStep = 32;       // GG_COH_TRACE words per (launch, tile)
 constexpr uint32_t kTrEv0 = 200, kTrEvMax = 128;
 #define PROF_T0() const uint64_t _p0 = (S.prof || S.trs) ? __builtin_amdgcn_s_memtime() : 0
 #define PROF_AT(var) const uint64_t var = (S.prof || S.trs) ? __builtin_amdgcn_s_memtime() : 0
@@ -606,6 +606,8 @@ struct Tile {
   uint32_t ferr;                         // GG_DERR_* gathered by fail()
   uint64_t ccv, stv;                    // lane k's cache counter k (of 2 x 12) and statistic k, loaded at step start
   const TilePre& p0;                    // the state loaded at step start (flush stores only what changed)
+  bool tr_on = false;                   // GG_COH_TRACE: cycles by handler part (dget, sharers, DRAM, send, FIFO, sharer words)
+  uint64_t tra[6] = {0, 0, 0, 0, 0, 0};
 
   // LC: the tile's L1-D / L2 tags, meta bytes and RR counters live in LDS at
   // clds for the whole launch (k_c_persist; layout of cache_lds_bytes)
@@ -705,6 +707,8 @@ struct Tile {
     if (type - 1u < 11u) stat(GG_CT_SENT_BY_TYPE + type - 1u, n);
   }
   __device__ __forceinline__ void send(uint32_t dst, uint32_t type, uint32_t requester, uint64_t addr, uint64_t t)
+  { const uint64_t c0 = tr_on ? __builtin_amdgcn_s_memtime() : 0; send_(dst, type, requester, addr, t); if (tr_on) tra[3] += __builtin_amdgcn_s_memtime() - c0; }
+  __device__ __forceinline__ void send_(uint32_t dst, uint32_t type, uint32_t requester, uint64_t addr, uint64_t t)
   {
     const uint32_t i = alloc(1);
     if (i == ~0u) return;
@@ -730,7 +734,9 @@ struct Tile {
   }
   __device__ __forceinline__ const DEnt* rep_ent(uint32_t i) const { return S.rep + (size_t)lt * P.R + i; }
   __device__ __forceinline__ bool has(int32_t h, uint32_t s) const { return (shw(h)[s >> 6] >> (s & 63)) & 1ull; }
-  __device__ __forceinline__ void add_sharer(int32_t h, uint32_t s)                 // addSharer (full_map.cc:27-33)
+  __device__ __forceinline__ void add_sharer(int32_t h, uint32_t s)
+  { const uint64_t c0 = tr_on ? __builtin_amdgcn_s_memtime() : 0; add_sharer_(h, s); if (tr_on) tra[5] += __builtin_amdgcn_s_memtime() - c0; }
+  __device__ __forceinline__ void add_sharer_(int32_t h, uint32_t s)                 // addSharer (full_map.cc:27-33)
   {
     uint64_t* w = shw(h) + (s >> 6);
     const uint64_t v = *w;
@@ -738,7 +744,9 @@ struct Tile {
     *w = v | (1ull << (s & 63));
     ent(h)->nsh++;
   }
-  __device__ __forceinline__ void remove_sharer(int32_t h, uint32_t s)              // removeSharer (:35-41)
+  __device__ __forceinline__ void remove_sharer(int32_t h, uint32_t s)
+  { const uint64_t c0 = tr_on ? __builtin_amdgcn_s_memtime() : 0; remove_sharer_(h, s); if (tr_on) tra[5] += __builtin_amdgcn_s_memtime() - c0; }
+  __device__ __forceinline__ void remove_sharer_(int32_t h, uint32_t s)              // removeSharer (:35-41)
   {
     uint64_t* w = shw(h) + (s >> 6);
     const uint64_t v = *w;
@@ -760,6 +768,8 @@ struct Tile {
   }
   // getDirectoryEntry (directory_cache.cc:102-145): lane i checks way i, then replaced entry i
   __device__ __forceinline__ int32_t dget(uint64_t a, uint64_t& t)
+  { const uint64_t c0 = tr_on ? __builtin_amdgcn_s_memtime() : 0; const int32_t r_ = dget_(a, t); if (tr_on) tra[0] += __builtin_amdgcn_s_memtime() - c0; return r_; }
+  __device__ __forceinline__ int32_t dget_(uint64_t a, uint64_t& t)
   {
     t += P.lat_dir;
     stat(GG_CT_DIR_ACCESSES, 1);
@@ -822,6 +832,8 @@ struct Tile {
   // getSharersList (ascending, full_map.cc:48-66): one message per sharer,
   // lane k writes the messages of sharer word k
   __device__ __forceinline__ void send_sharers(int32_t h, uint32_t type, uint32_t requester, uint64_t a, uint64_t t)
+  { const uint64_t c0 = tr_on ? __builtin_amdgcn_s_memtime() : 0; send_sharers_(h, type, requester, a, t); if (tr_on) tra[1] += __builtin_amdgcn_s_memtime() - c0; }
+  __device__ __forceinline__ void send_sharers_(int32_t h, uint32_t type, uint32_t requester, uint64_t a, uint64_t t)
   {
     uint64_t bits = ln < P.W ? shw(h)[ln] : 0;
     const uint32_t c = (uint32_t)__builtin_popcountll(bits);
@@ -873,6 +885,8 @@ struct Tile {
     return -1;
   }
   __device__ __forceinline__ void qpush(uint64_t a, uint64_t t, uint32_t type, uint32_t req)
+  { const uint64_t c0 = tr_on ? __builtin_amdgcn_s_memtime() : 0; qpush_(a, t, type, req); if (tr_on) tra[4] += __builtin_amdgcn_s_memtime() - c0; }
+  __device__ __forceinline__ void qpush_(uint64_t a, uint64_t t, uint32_t type, uint32_t req)
   {
     if (nrq >= (rq_lds ? SL::kRq : P.QC)) { fail(GG_DERR_CAP); return; }
     rq_put(nrq, CReq{a, t, type, req});
@@ -880,6 +894,8 @@ struct Tile {
     ++nrq;
   }
   __device__ __forceinline__ void qpop(uint64_t a)
+  { const uint64_t c0 = tr_on ? __builtin_amdgcn_s_memtime() : 0; qpop_(a); if (tr_on) tra[4] += __builtin_amdgcn_s_memtime() - c0; }
+  __device__ __forceinline__ void qpop_(uint64_t a)
   {
     const int32_t f = qfront(a);
     if (f < 0) return;
@@ -914,13 +930,26 @@ struct Tile {
 
   // ---- DramCntlr / DramPerfModel --------------------------------------------
   __device__ __forceinline__ uint64_t dram_ps(uint64_t t)
+  { const uint64_t c0 = tr_on ? __builtin_amdgcn_s_memtime() : 0; const uint64_t r_ = dram_ps_(t); if (tr_on) tra[2] += __builtin_amdgcn_s_memtime() - c0; return r_; }
+  __device__ __forceinline__ uint64_t dram_ps_(uint64_t t)
   {
     const uint64_t pkt_ns = time_to_cycles(t, 1.0);                  // ceil(t / 1000.0)
     uint64_t qd = 0;
     if (P.dram_qm) {
       // each side's queue pointers derived where they are used (LDS / HBM):
       // a pointer merged from the two would make every queue access flat
-      if (dq_lds) {
+      if (dq_lds && P.dram_qtype == GG_QM_HISTORY_TREE) {
+        // a history tree: the image into registers (RegQueue), one request,
+        // back to the image — ~3x fewer cycles than the lane-parallel LDS form
+        HQueue* lq = reinterpret_cast<HQueue*>(sl.dimg);
+        HNode* lnd = reinterpret_cast<HNode*>(sl.dimg + sizeof(HQueue));
+        RegQueue rq;
+        rq.load(lq, lnd, P.dram_proc, P.analytical != 0, ln);
+        qd = rq.request(pkt_ns, P.dram_proc, S.err);
+        wave_sync();
+        rq.store(lq, lnd);
+        wave_sync();
+      } else if (dq_lds) {
         HTree tr{reinterpret_cast<HQueue*>(sl.dimg), reinterpret_cast<HNode*>(sl.dimg + sizeof(HQueue)), P.dram_proc,
                  P.analytical != 0};
         qd = tr.delay_w(pkt_ns, P.dram_proc, S.err, ln);
@@ -1411,7 +1440,7 @@ struct Tile {
 // channel (a head can only leave after its channel's earlier messages, and
 // every head waiting behind a larger arrival inherits it).  a = arrival,
 // k = sender << 32 | seq, idx = record; out = records in processing order.
-__device__ void order_inbox(uint32_t n, const uint64_t* a, const uint64_t* k, uint64_t* pm, const uint32_t* idx,
+__device__ __forceinline__ void order_inbox(uint32_t n, const uint64_t* a, const uint64_t* k, uint64_t* pm, const uint32_t* idx,
                             uint32_t* out, uint32_t ln)
 {
   for (uint32_t i = ln; i < n; i += 64) {
@@ -1434,7 +1463,7 @@ __device__ void order_inbox(uint32_t n, const uint64_t* a, const uint64_t* k, ui
 }
 // (time, send time, sender << 32 | seq) order: a port's service order (the
 // canonical key of DESIGN.md §4)
-__device__ void order_port(uint32_t n, const uint64_t* t, const uint64_t* s, const uint64_t* k, const uint32_t* idx,
+__device__ __forceinline__ void order_port(uint32_t n, const uint64_t* t, const uint64_t* s, const uint64_t* k, const uint32_t* idx,
                            uint32_t* out, uint32_t ln)
 {
   for (uint32_t i = ln; i < n; i += 64) {
@@ -1451,7 +1480,7 @@ __device__ void order_port(uint32_t n, const uint64_t* t, const uint64_t* s, con
 
 // the same order, out[rank] = the entry's local index (its fields stay in
 // the gathered arrays, no reload of the record)
-__device__ void order_port_local(uint32_t n, const uint64_t* t, const uint64_t* s, const uint64_t* k, uint32_t* out,
+__device__ __forceinline__ void order_port_local(uint32_t n, const uint64_t* t, const uint64_t* s, const uint64_t* k, uint32_t* out,
                                  uint32_t ln)
 {
   for (uint32_t i = ln; i < n; i += 64) {
@@ -1779,6 +1808,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
   const uint32_t ln = lane_id(), p = k & 1u;
   PROF_T0();
   Tile<SL, H> T(P, S, lt, p, sl, hk, clds, std::integral_constant<bool, LC>(), pre);
+  T.tr_on = S.trs != nullptr && L < S.tr_n;
   const gg_cmsg* prev = pool(S, p ^ 1u);     // records delivered to this step
   uint64_t* gscr = S.gscr + (size_t)lt * 6 * P.IC;
   // NoC counters of the SELF port (lanes 0-6) and of the receiver
@@ -1789,6 +1819,36 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
   // at the receiver, hop_by_hop.cc:223-256; __processReceivedPacket, network_model.cc:118-150)
   PROF_AT(_sa);
   uint64_t _sb = 0, _sc = 0, _sd = 0, _se = 0, _sf = 0, _q1 = 0, _q2 = 0, _q3 = 0, _q4 = 0, _q1b = 0;
+  uint64_t _hd = 0, _hl = 0, _hn = 0;                          // trace: handler cycles (directory / L2), counts
+  // The directory request FIFO (<= 64 entries) and the DRAM queue image are
+  // loaded now, in the same round as the SELF batch's loads, held in
+  // registers across the SELF phase and written to LDS after it (loaded
+  // after the SELF phase they would cost the inbox a round trip of their own)
+  const uint32_t n = ni + na;
+  const bool rq_fit = T.nrq + 2 * n + 2 <= SL::kRq, pre_rq = rq_fit && T.nrq <= 64;
+  const bool dq_fit = P.dram_qm && P.max_list <= kQMax && n;
+  constexpr uint32_t kHW = sizeof(HQueue) / 16;
+  static_assert(kHW + kQMax <= 3 * 64, "the DRAM image prefetch holds 3 words per lane");
+  uint64_t fq[3];
+  uint4 dv[3];
+  if (pre_rq) {
+    const uint64_t* g = reinterpret_cast<const uint64_t*>(S.rq + (size_t)lt * P.QC);   // 3 words per entry
+#pragma unroll
+    for (uint32_t u = 0; u < 3; ++u) { const uint32_t j = ln + 64 * u; fq[u] = j < 3 * T.nrq ? g[j] : 0ull; }
+  }
+  if (dq_fit) {
+    const uint4* gq_ = reinterpret_cast<const uint4*>(S.dq + lt);
+    const uint4* gn_ = reinterpret_cast<const uint4*>(S.dnd + (size_t)lt * P.max_list);
+#pragma unroll
+    for (uint32_t u = 0; u < 3; ++u) {
+      const uint32_t j = ln + 64 * u;
+      dv[u] = j < kHW ? gq_[j] : j < kHW + P.max_list ? gn_[j - kHW] : make_uint4(0, 0, 0, 0);
+    }
+  }
+  // SELF arrivals with no other inbox records: the SELF batch leaves the
+  // inbox keys (new arrival, sender << 32 | seq, record) in LDS, so the inbox
+  // is ordered without gathering its records again
+  const bool self_keys = ni == 0 && na && na <= SL::kIn;
   if (na) {
     if (S.prof || S.trs) _sb = __builtin_amdgcn_s_memtime();
     const uint32_t* al = arv(S, p) + (size_t)lt * P.IC;
@@ -1854,10 +1914,10 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
     if (S.prof || S.trs) { (void)__builtin_amdgcn_readfirstlane((int)rq.a0); _se = __builtin_amdgcn_s_memtime(); }
     for (uint32_t c0 = 0; c0 < na; c0 += 64) {
       const uint32_t cnt = min(64u, na - c0);
-      uint32_t r = 0, nf_ = 0, bits = 0;
+      uint32_t r = 0, nf_ = 0, bits = 0, e = 0;
       uint64_t tv = 0, z_ = 0, sp = 0;
       if (ln < cnt) {
-        const uint32_t e = o_[c0 + ln];                          // local index of the packet of rank c0 + ln
+        e = o_[c0 + ln];                                         // local index of the packet of rank c0 + ln
         r = i_[e];
         tv = t_[e]; z_ = z_a[e]; sp = s_[e];
         bits = (k_[e] & 1u) ? P.bits_data : P.bits_req;
@@ -1886,7 +1946,10 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
       }
       if (S.prof && ln == 0) prof_batch(S, 0, cnt, ntail);
       if (S.trs) _sf = __builtin_amdgcn_s_memtime();
-      if (ln < cnt) { pv[r].arrival_ps = ot; pv[r].zero_load_ps = oz; }
+      if (ln < cnt) {
+        pv[r].arrival_ps = ot; pv[r].zero_load_ps = oz;
+        if (LD && self_keys) { const uint64_t kk = k_[e]; t_[e] = ot; s_[e] = ((kk >> 33) << 32) | ((kk >> 1) & 0xFFFFFFFFull); }
+      }
     }
     };
     if (na <= SL::kIn) self_batch(std::true_type{}); else self_batch(std::false_type{});
@@ -1908,15 +1971,22 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
     atomicAdd(&S.prof[96], 1ull);
   }
   if (S.prof && ln == 0 && !na) { atomicAdd(&S.prof[97], (unsigned long long)(_sa - _p0)); atomicAdd(&S.prof[98], 1ull); }
-  const uint32_t n = ni + na;
   // directory request FIFO in LDS when it cannot outgrow it this step
-  if (T.nrq + 2 * n + 2 <= SL::kRq) {
-    const CReq* g = S.rq + (size_t)lt * P.QC;
-    for (uint32_t i = ln; i < T.nrq; i += 64) sl.rq[i] = g[i];
+  if (rq_fit) {
+    if (pre_rq) {
+      GG_LDS uint64_t* l = reinterpret_cast<GG_LDS uint64_t*>(T.lrq());
+#pragma unroll
+      for (uint32_t u = 0; u < 3; ++u) { const uint32_t j = ln + 64 * u; if (j < 3 * T.nrq) l[j] = fq[u]; }
+    } else {
+      const CReq* g = S.rq + (size_t)lt * P.QC;
+      for (uint32_t i = ln; i < T.nrq; i += 64) sl.rq[i] = g[i];
+    }
     T.rq_lds = true;
   }
-  if (P.dram_qm && P.max_list <= kQMax && n) {
-    img_in(sl.dimg, S.dq + lt, S.dnd + (size_t)lt * P.max_list, P.max_list, ln);
+  if (dq_fit) {
+    uint4* l = reinterpret_cast<uint4*>(sl.dimg);
+#pragma unroll
+    for (uint32_t u = 0; u < 3; ++u) { const uint32_t j = ln + 64 * u; if (j < kHW + P.max_list) l[j] = dv[u]; }
     T.dq_lds = true;
   }
   tsync();
@@ -1929,7 +1999,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
     constexpr bool LD = decltype(in_lds)::value;
     uint64_t* a_ = LD ? sl.x1 : gscr; uint64_t* k_ = LD ? sl.x2 : gscr + P.IC; uint64_t* m_ = LD ? sl.x3 : gscr + 2 * P.IC;
     uint32_t* i_ = LD ? sl.i1 : (uint32_t*)(gscr + 3 * P.IC); uint32_t* o_ = LD ? sl.i2 : (uint32_t*)(gscr + 4 * P.IC);
-    for (uint32_t i0 = ln; i0 < n; i0 += 256) {                   // 4 records per lane in flight
+    for (uint32_t i0 = ln; i0 < n && !(LD && self_keys); i0 += 256) {   // 4 records per lane in flight
       uint32_t rr[4];
 #pragma unroll
       for (uint32_t u = 0; u < 4; ++u) {
@@ -1959,7 +2029,13 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
     for (uint32_t j = 0; j < n && !T.failed; ++j) {
       const gg_cmsg m = prev[lds ? sl.i2[j] : go_[j]];
       T.stat(GG_CT_MSGS_RECEIVED, 1);
-      if (to_directory(m.type)) T.directory_msg(m); else T.l2_msg(m);
+      const uint64_t h0 = S.trs ? __builtin_amdgcn_s_memtime() : 0;
+      const bool dm = to_directory(m.type);
+      if (dm) T.directory_msg(m); else T.l2_msg(m);
+      if (S.trs) {
+        const uint64_t h1 = __builtin_amdgcn_s_memtime();
+        if (dm) { _hd += h1 - h0; _hn += 1; } else { _hl += h1 - h0; _hn += 1ull << 32; }
+      }
     }
   }
 
@@ -2219,6 +2295,8 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
     r[9] = (unsigned long long)na | ((unsigned long long)ni << 16) | ((unsigned long long)T.nsent << 32);
     r[10] = _sb; r[11] = _sc; r[12] = _sd; r[13] = _se; r[14] = _q1b; r[15] = _sf;
     r[16] = _q1; r[17] = _q2; r[18] = _q3; r[19] = _q4;
+    r[20] = _hd; r[21] = _hl; r[22] = _hn;
+    for (int i = 0; i < 6; ++i) r[23 + i] = T.tra[i];
   }
   // the tile's next start for the shard scheduler: finished, blocked, or clock + gap
   if (T.rec >= T.rec_end) return kNsFin;
@@ -2337,8 +2415,6 @@ __host__ __device__ inline bool walk_regq(const CP& P)
 template <bool PIPE, bool RQ>
 __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, int stage, uint32_t blk)
 {
-  const uint32_t live = ((volatile uint32_t*)S.live)[L & 3];
-  if (!live) return;                                 // launch L was no step
   // block -> (run slot, direction): with runs interleaved by shard, block b
   // takes slot (b mod ns) + ns * (b div 2ns) in direction (b div ns) & 1, so
   // every block of shard k is k mod ns (the XCD of its tiles' blocks)
@@ -2347,15 +2423,21 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
     const uint32_t ns = P.seg_xcd, b = blk;
     sg = 2 * ((b % ns) + ns * (b / (2 * ns))) + ((b / ns) & 1u);
   }
-  const uint32_t tid = threadIdx.x, nthr = blockDim.x, ln = tid & 63, p = (live - 1) & 1u;
+  const uint32_t tid = threadIdx.x, nthr = blockDim.x, ln = tid & 63;
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));   // wave-uniform: SGPR control flow
-  PROF_T0();
+  // one round of loads: the launch's live word, the run's count and bounds,
+  // and (speculatively: in bounds whatever the count) its first list words
   uint32_t* cntp = (stage == 0 ? S.nxl : S.nyl) + sg;
+  const uint32_t* list = (stage == 0 ? S.xl : S.yl) + (size_t)sg * P.seg_cap;
+  const uint32_t live = S.live[L & 3];
   const uint32_t n0 = *cntp;
+  const Seg sd = (stage == 0 ? S.segx : S.segy)[sg >> 1];
+  const uint32_t lw = tid < P.seg_cap ? list[tid] : 0u;
+  if (!live) return;                                 // launch L was no step
+  const uint32_t p = (live - 1) & 1u;
+  PROF_T0();
   if (n0 == 0) return;
   const uint32_t n = min(n0, P.seg_cap);
-  const uint32_t* list = (stage == 0 ? S.xl : S.yl) + (size_t)sg * P.seg_cap;
-  const Seg sd = (stage == 0 ? S.segx : S.segy)[sg >> 1];
   const uint32_t dir = sg & 1u;
   const int port = stage == 0 ? (dir ? P_RIGHT : P_LEFT) : (dir ? P_UP : P_DOWN);
   auto tile_at = [&](uint32_t pos) -> uint32_t { return stage == 0 ? sd.line * P.mw + pos : pos * P.mw + sd.line; };
@@ -2389,9 +2471,18 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
   W.Pr = W.Pf + P.walk_pk;                                       // rank in (send time, sender, seq) order
   W.Qt = reinterpret_cast<uint64_t*>(W.Pr + P.walk_pk);          // batch scratch of the one-wave sweep
   W.Qr = reinterpret_cast<uint32_t*>(W.Qt + P.walk_pk); W.Qs = W.Qr + P.walk_pk;
+  // the hand-off's lookups, issued now and consumed after the walk (lane i ==
+  // tid, the common case): the destination, and the receiver's local slot
+  // (the run ends at the destination) or the Y run the packet turns into
+  uint32_t pdst = 0, pf = 0;
   for (uint32_t i = tid; i < n; i += nthr) {
-    const uint32_t r = list[i];
+    const uint32_t r = i == tid ? lw : list[i];
     const gg_cmsg& m = cur[r];
+    if (i == tid) {
+      pdst = m.dst;
+      const uint32_t hx = tile_at(pos_of(m.dst));
+      pf = hx == m.dst ? (uint32_t)S.ltile[m.dst] : S.tseg[(size_t)hx * 2 + 1];
+    }
     W.Pt[i] = m.arrival_ps; W.Ph[i] = m.send_ps; W.Pk[i] = ((uint64_t)m.src << 32) | m.seq; W.Pz[i] = m.zero_load_ps;
     W.Pi[i] = r; W.Pp[i] = pos_of(m.hop); W.Pd[i] = pos_of(m.dst);
     if (m.arrival_ps >> 51) atomicOr(S.err, GG_DERR_CAP);        // batch keys are time << 12 | rank
@@ -2665,15 +2756,15 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
       ++nb;
       continue;
     }
-    const uint32_t dst = m->dst;
+    const uint32_t dst = i == tid ? pdst : m->dst;
     if (h == dst) {                                            // the SELF port of the destination, next step
-      const int32_t ld = S.ltile[dst];
+      const int32_t ld = i == tid ? (int32_t)pf : S.ltile[dst];
       const uint32_t j = atomicAdd(&narv(S, p ^ 1u)[ld], 1u);
       if (j >= P.IC) { atomicOr(S.err, GG_DERR_CAP); continue; }
       arv(S, p ^ 1u)[(size_t)ld * P.IC + j] = r;
     } else {                                                   // X done: the Y segment of the destination column
       bool is_x;
-      const uint32_t s2 = xy_stage_seg(P, S, h, dst, is_x);
+      const uint32_t s2 = i == tid ? pf * 2 + (dst / P.mw > h / P.mw ? 1u : 0u) : xy_stage_seg(P, S, h, dst, is_x);
       const uint32_t j = atomicAdd(&S.nyl[s2], 1u);
       if (j >= P.seg_cap) { atomicOr(S.err, GG_DERR_CAP); continue; }
       S.yl[(size_t)s2 * P.seg_cap + j] = r;

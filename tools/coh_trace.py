@@ -10,7 +10,7 @@ import sys
 
 import numpy as np
 
-W = 24          # kTrStep
+W = 32          # kTrStep
 
 
 def main():
@@ -29,7 +29,9 @@ def main():
            "publish": ["pub_build", "pub_order", "pub_qload", "pub_requests", "pub_seglists"]}
     keys = ["entry", "exit"] + phases + sum(sub.values(), []) + \
         ["span_step", "span_x", "span_y", "gap_sx", "gap_xy", "gap_ys", "crit_na", "crit_ni", "crit_sent",
-         "tiles_working", "qend", "crit_has_self", "crit_has_inbox", "crit_has_pub"]
+         "dir_msg_ns", "l2_msg_ns", "crit_dir_msgs", "crit_l2_msgs",
+         "h_dget", "h_sharers", "h_dram", "h_send", "h_fifo", "h_shwords",
+         "tiles_working", "clock_ghz", "qend", "crit_has_self", "crit_has_inbox", "crit_has_pub"]
     acc = {k: [] for k in keys}
     wacc = {s: {k: [] for k in ("entry", "staging", "loop", "handoff", "exit", "events", "n", "npos", "blocks")}
             for s in (0, 1)}
@@ -51,6 +53,7 @@ def main():
             span = (r[1] - r[0]) * tick
             cyc = r[8] - r[2]
             f = span / cyc if cyc > 0 else 0.0                     # ns per memtime cycle for this tile
+            if f > 0: acc["clock_ghz"].append(1.0 / f)
             acc["entry"].append((r[0] - k0) * tick)
             mt = [r[2], r[3], r[4], r[5], r[6], r[7], r[8]]
             for k, a, b in zip(phases, mt[:-1], mt[1:]):
@@ -66,6 +69,12 @@ def main():
                     acc[k].append((b - a) * f)
             if r[14] > 0:
                 acc["in_gather_order"].append((r[14] - r[4]) * f); acc["in_handlers"].append((r[5] - r[14]) * f)
+                hn = int(r[22]); nd, nl = hn & 0xFFFFFFFF, hn >> 32
+                acc["crit_dir_msgs"].append(nd); acc["crit_l2_msgs"].append(nl)
+                if nd: acc["dir_msg_ns"].append(r[20] * f / nd)
+                for i, k in enumerate(("h_dget", "h_sharers", "h_dram", "h_send", "h_fifo", "h_shwords")):
+                    acc[k].append(r[23 + i] * f)
+                if nl: acc["l2_msg_ns"].append(r[21] * f / nl)
             if r[16] > 0:
                 sp = [r[6], r[16], r[17], r[18], r[19], r[7]]
                 for k, a, b in zip(sub["publish"], sp[:-1], sp[1:]):
