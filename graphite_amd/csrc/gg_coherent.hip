@@ -606,6 +606,8 @@ struct Tile {
   uint32_t ferr;                         // GG_DERR_* gathered by fail()
   uint64_t ccv, stv;                    // lane k's cache counter k (of 2 x 12) and statistic k, loaded at step start
   const TilePre& p0;                    // the state loaded at step start (flush stores only what changed)
+  int32_t oh = NO_ENT; bool od = false;  // the open directory entry (eopen) and whether it changed
+  uint64_t oaddr = 0, osh = 0; int32_t oown = -1; uint32_t ost = 0, onsh = 0;
   bool tr_on = false;                   // GG_COH_TRACE: cycles by handler part (dget, sharers, DRAM, send, FIFO, sharer words)
   uint64_t tra[6] = {0, 0, 0, 0, 0, 0};
 
@@ -733,31 +735,63 @@ struct Tile {
     return h >= 0 ? S.dsh + ((size_t)lt * P.E + h) * P.W : S.rsh + ((size_t)lt * P.R + (-h - 1)) * P.W;
   }
   __device__ __forceinline__ const DEnt* rep_ent(uint32_t i) const { return S.rep + (size_t)lt * P.R + i; }
-  __device__ __forceinline__ bool has(int32_t h, uint32_t s) const { return (shw(h)[s >> 6] >> (s & 63)) & 1ull; }
+  // The open entry: the directory entry the current message works on, its
+  // fields in scalars and its sharer words in lanes 0..W-1 (W <= 64), so a
+  // handler's read-modify-writes of the entry are register operations (in
+  // HBM each load behind a store waits for that store: ~1 µs apiece).
+  // Written back when another entry opens, before the directory moves
+  // entries (dreplace / dinvalidate / the replacement scan) and at step end.
+  __device__ __forceinline__ void eopen(int32_t h)
+  {
+    h = __builtin_amdgcn_readfirstlane(h);
+    if (h == oh) return;
+    eclose();
+    const DEnt* e = ent(h);
+    oaddr = e->addr; oown = e->owner; ost = e->dstate; onsh = e->nsh;
+    osh = ln < P.W ? shw(h)[ln] : 0ull;
+    oh = h; od = false;
+  }
+  __device__ __forceinline__ void eflush()
+  {
+    if (oh == NO_ENT || !od) return;
+    DEnt* e = ent(oh);
+    e->owner = oown; e->dstate = (uint16_t)ost; e->nsh = (uint16_t)onsh;
+    if (ln < P.W) shw(oh)[ln] = osh;
+    od = false;
+  }
+  __device__ __forceinline__ void eclose() { eflush(); oh = NO_ENT; }
+  __device__ __forceinline__ uint32_t e_state(int32_t h) { eopen(h); return ost; }
+  __device__ __forceinline__ int32_t e_owner(int32_t h) { eopen(h); return oown; }
+  __device__ __forceinline__ uint32_t e_nsh(int32_t h) { eopen(h); return onsh; }
+  __device__ __forceinline__ void set_state(int32_t h, uint32_t st) { eopen(h); ost = st; od = true; }
+  __device__ __forceinline__ uint64_t e_word(int32_t h, uint32_t w)
+  {
+    eopen(h);
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(osh >> 32), (int)w) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)osh, (int)w);
+  }
+  __device__ __forceinline__ bool has(int32_t h, uint32_t s) { return (e_word(h, s >> 6) >> (s & 63)) & 1ull; }
   __device__ __forceinline__ void add_sharer(int32_t h, uint32_t s)
   { const uint64_t c0 = tr_on ? __builtin_amdgcn_s_memtime() : 0; add_sharer_(h, s); if (tr_on) tra[5] += __builtin_amdgcn_s_memtime() - c0; }
   __device__ __forceinline__ void add_sharer_(int32_t h, uint32_t s)                 // addSharer (full_map.cc:27-33)
   {
-    uint64_t* w = shw(h) + (s >> 6);
-    const uint64_t v = *w;
-    if ((v >> (s & 63)) & 1ull) fail();
-    *w = v | (1ull << (s & 63));
-    ent(h)->nsh++;
+    if (has(h, s)) fail();
+    if (ln == (s >> 6)) osh |= 1ull << (s & 63);
+    ++onsh; od = true;
   }
   __device__ __forceinline__ void remove_sharer(int32_t h, uint32_t s)
   { const uint64_t c0 = tr_on ? __builtin_amdgcn_s_memtime() : 0; remove_sharer_(h, s); if (tr_on) tra[5] += __builtin_amdgcn_s_memtime() - c0; }
   __device__ __forceinline__ void remove_sharer_(int32_t h, uint32_t s)              // removeSharer (:35-41)
   {
-    uint64_t* w = shw(h) + (s >> 6);
-    const uint64_t v = *w;
-    if (!((v >> (s & 63)) & 1ull)) { fail(); return; }
-    *w = v & ~(1ull << (s & 63));
-    ent(h)->nsh--;
+    if (!has(h, s)) { fail(); return; }
+    if (ln == (s >> 6)) osh &= ~(1ull << (s & 63));
+    --onsh; od = true;
   }
   __device__ __forceinline__ void set_owner(int32_t h, int32_t o)                   // DirectoryEntry::setOwner
   {
     if (o >= 0 && !has(h, (uint32_t)o)) fail();
-    ent(h)->owner = o;
+    eopen(h);
+    oown = o; od = true;
   }
   __device__ __forceinline__ uint32_t dset(uint64_t a) const                        // computeSetIndex (directory_cache.cc:332-348)
   {
@@ -783,6 +817,7 @@ struct Tile {
       // a never-used slot: its sharer words are zeroed here, not at reset
       // (full-map vectors of every entry are 2 GB at 1024 tiles)
       const uint32_t i = base + (uint32_t)__builtin_ctzll(fr);
+      if (oh == (int32_t)i) eclose();
       d[i].addr = a;
       if (ln < P.W) shw((int32_t)i)[ln] = 0;
       return (int32_t)i;
@@ -796,6 +831,7 @@ struct Tile {
   // entry, the old one moves to the replaced list
   __device__ __forceinline__ int32_t dreplace(uint64_t replaced, uint64_t a, uint64_t& t)
   {
+    eclose();                                     // the moves below work on HBM
     const uint32_t base = dset(replaced) * P.dassoc;
     DEnt* d = S.dir + (size_t)lt * P.E;
     const uint64_t v = ln < P.dassoc ? d[base + ln].addr : 0;
@@ -818,6 +854,7 @@ struct Tile {
   // invalidateDirectoryEntry (directory_cache.cc:215-231): erase from the replaced list
   __device__ __forceinline__ void dinvalidate(uint64_t a)
   {
+    eclose();                                     // the moves below work on HBM
     const uint32_t nr = nrep;
     const uint64_t rv = ln < nr ? rep_ent(ln)->addr : 0;
     const uint64_t rh = __ballot(ln < nr && rv == a);
@@ -835,7 +872,8 @@ struct Tile {
   { const uint64_t c0 = tr_on ? __builtin_amdgcn_s_memtime() : 0; send_sharers_(h, type, requester, a, t); if (tr_on) tra[1] += __builtin_amdgcn_s_memtime() - c0; }
   __device__ __forceinline__ void send_sharers_(int32_t h, uint32_t type, uint32_t requester, uint64_t a, uint64_t t)
   {
-    uint64_t bits = ln < P.W ? shw(h)[ln] : 0;
+    eopen(h);
+    uint64_t bits = ln < P.W ? osh : 0;
     const uint32_t c = (uint32_t)__builtin_popcountll(bits);
     const uint32_t pre = wave_excl_scan(c, ln);
     const uint32_t tot = wave_sum(c);
@@ -981,6 +1019,7 @@ struct Tile {
           if (dget(w.addr, t) != NO_ENT) fail();   // the assert in getReplacementCandidates (directory_cache.cc:161)
           const uint32_t base = dset(w.addr) * P.dassoc;
           const DEnt* d = S.dir + (size_t)lt * P.E;
+          eflush();                                 // the scan reads the ways' sharer counts from HBM
           // candidate (:138-149): fewest sharers among ways with no queued request, first wins
           uint32_t key = ~0u;
           if (ln < P.dassoc) {
@@ -1006,12 +1045,11 @@ struct Tile {
         continue;
       }
       case W_CONT: {                     // the directory-state switch
-        DEnt* e = ent(w.h);
-        const uint32_t ds = e->dstate;
+        const uint32_t ds = e_state(w.h);
         if (w.type == M_EX_REQ) {
           if (ds == DS_MODIFIED) {
             if (w.cached) fail();
-            send((uint32_t)e->owner, M_FLUSH_REQ, w.requester, w.addr, t);
+            send((uint32_t)e_owner(w.h), M_FLUSH_REQ, w.requester, w.addr, t);
             w.kind = W_NONE;
           } else if (ds == DS_SHARED) {
             if (w.cached) fail();
@@ -1020,7 +1058,7 @@ struct Tile {
           } else {
             add_sharer(w.h, w.requester);
             set_owner(w.h, (int32_t)w.requester);
-            ent(w.h)->dstate = DS_MODIFIED;
+            set_state(w.h, DS_MODIFIED);
             if (!w.cached) t += dram_ps(t);                         // retrieveDataAndSendToL2Cache (:382-408)
             send(w.requester, M_EX_REP, w.requester, w.addr, t);
             w.kind = W_NEXT;
@@ -1028,11 +1066,11 @@ struct Tile {
         } else {
           if (ds == DS_MODIFIED) {
             if (w.cached) fail();
-            send((uint32_t)e->owner, M_WB_REQ, w.requester, w.addr, t);
+            send((uint32_t)e_owner(w.h), M_WB_REQ, w.requester, w.addr, t);
             w.kind = W_NONE;
           } else {
             add_sharer(w.h, w.requester);
-            ent(w.h)->dstate = DS_SHARED;
+            set_state(w.h, DS_SHARED);
             if (!w.cached) t += dram_ps(t);
             send(w.requester, M_SH_REP, w.requester, w.addr, t);
             w.kind = W_NEXT;
@@ -1054,10 +1092,9 @@ struct Tile {
       case W_NULLIFY: {                  // processNullifyReq (:172-236)
         const int32_t h = dget(w.addr, t);
         if (h == NO_ENT) { fail(); return; }
-        DEnt* e = ent(h);
-        const uint32_t ds = e->dstate;
+        const uint32_t ds = e_state(h);
         if (ds == DS_MODIFIED) {
-          send((uint32_t)e->owner, M_FLUSH_REQ, w.requester, w.addr, t);
+          send((uint32_t)e_owner(h), M_FLUSH_REQ, w.requester, w.addr, t);
           w.kind = W_NONE;
         } else if (ds == DS_SHARED) {
           send_sharers(h, M_INV_REQ, w.requester, w.addr, t);
@@ -1088,13 +1125,12 @@ struct Tile {
     } else {
       const int32_t h = dget(a, t);
       if (h == NO_ENT) { fail(); return; }
-      DEnt* e = ent(h);
-      const uint32_t ds = e->dstate;
+      const uint32_t ds = e_state(h);
       if (m.type == M_INV_REP) {
         if (ds != DS_SHARED) { fail(); return; }
         remove_sharer(h, m.src);
-        const bool unc = e->nsh == 0;
-        if (unc) e->dstate = DS_UNCACHED;
+        const bool unc = e_nsh(h) == 0;
+        if (unc) set_state(h, DS_UNCACHED);
         const int32_t f = qfront(a);
         if (f >= 0) {
           uint32_t type, req;
@@ -1107,7 +1143,7 @@ struct Tile {
         if (ds != DS_MODIFIED) { fail(); return; }
         remove_sharer(h, m.src);
         set_owner(h, -1);
-        e->dstate = DS_UNCACHED;
+        set_state(h, DS_UNCACHED);
         const int32_t f = qfront(a);
         if (f < 0) { (void)dram_ps(t); return; }                    // putDataToDram: queue model, no latency
         uint32_t type, req;
@@ -1118,7 +1154,7 @@ struct Tile {
       } else if (m.type == M_WB_REP) {
         if (ds != DS_MODIFIED || !has(h, m.src)) { fail(); return; }
         set_owner(h, -1);
-        e->dstate = DS_SHARED;
+        set_state(h, DS_SHARED);
         const int32_t f = qfront(a);
         if (f < 0) { fail(); return; }
         uint32_t type, req;
@@ -2253,6 +2289,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
     for (uint32_t i = ln; i < T.nrq; i += 64) g[i] = sl.rq[i];
   }
   if (T.dq_lds) img_out(S.dq + lt, S.dnd + (size_t)lt * P.max_list, sl.dimg, P.max_list, ln);
+  T.eclose();
   T.flush();
   T.flush_err();
   // NoC counters of the tile's own SELF port and receiver
