@@ -331,7 +331,7 @@ def coherent_long_section(args, dev):
 
 def exchange_section(args, dev):
     """The per-quantum cost of the multi-rank exchange (gg_round_exchange:
-    grouped per-peer slot send / receive + status all-reduces over RCCL, one
+    grouped per-peer slot send / receive + one status all-gather over RCCL, one
     host sync) measured on one GPU: the headline workload through
     gg_coherent_run_ranks over a one-rank RCCL communicator against the
     device-driven single-context loop (gg_coherent_run); same results bit for
@@ -374,9 +374,11 @@ def exchange_section(args, dev):
                 "quanta": quanta, "single_context_seconds": res["single"], "rccl_one_rank_seconds": res["rccl"],
                 "exchange_us_per_quantum": 1e6 * (res["rccl"] - res["single"]) / max(1, quanta),
                 "bit_identical": same,
-                "note": "the one-rank round still runs every quantum's steps from the host (two syncs per quantum: "
-                        "the step batches' quiet flag and the exchange) where the single context runs the quantum "
-                        "loop on the device; the difference per quantum bounds the exchange's fixed cost"}
+                "note": "one host sync per quantum: the round enqueues the quantum's steps (a batch sized from "
+                        "the quanta before), the tail kernel (status + export), RCCL (peer slots, one all-gather "
+                        "of the status words), commit + import and the words' copy; the single context runs the "
+                        "quantum loop on the device with no sync, so the difference per quantum bounds the "
+                        "round's fixed cost"}
     finally:
         dist.destroy_process_group()
 

@@ -1697,7 +1697,7 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
     const uint32_t sent = (km == 0 ? rv[0] : km == 1 ? rv[1] : km == 2 ? rv[2] : rv[3]) +
                           (k == 1 ? ((Q & 1) ? rv[6] : rv[5]) : 0u);
     if (sent == 0) {                                 // the previous step sent nothing: the quantum is done
-      if (lt == 0 && ln == 0) { S.live[L & 3] = 0; if (!devloop) *S.quiet = 1; }
+      if (lt == 0 && ln == 0) { S.live[L & 3] = 0; if (!devloop) *S.quiet = k + 1; }   // (steps run + 1)
       if (devloop) quantum_end(P, S, L, q, Q);
       return;
     }
@@ -3068,41 +3068,97 @@ __global__ void k_c_export_scatter(CS S, const gg_cmsg* b, uint32_t n, const uin
   out[base[k] + atomicAdd(&cursor[k], 1u)] = b[i];
 }
 
-// gg_round_exchange's device side (gg_coh_export_slots / _round_status / _import_slots)
+// gg_round_exchange's device side (k_c_round_tail / _commit / _import, k_c_import_slots)
 __global__ void k_c_ri_quantum(CS S, uint64_t q)
 {
   S.ri[GG_RI_QUANTA]++;
   S.ri[GG_RI_FINAL_QUANTUM] = q;
 }
-__global__ void k_slot_clear(gg_cmsg* slots, uint32_t world, uint64_t region)
+// ---- one round of gg_round_exchange with one host sync (see there) --------
+// words of a rank's round status (gathered over the ranks, reduced by each)
+enum { RW_SENT = 0, RW_ACTIVE, RW_BLOCKED, RW_ERR, RW_MAXSLOT, RW_MINNEXT, RW_NOTDONE, RW_STEPS, RW_N };
+static_assert(RW_N == kRoundWords, "gg_internal.h kRoundWords");
+// before RCCL: if the quantum's steps have finished (quiet), the status of the
+// owned tiles and the held records scattered into the send slots by owning
+// rank; else empty slots and the not-done word.  Nothing here changes the
+// context's state: a round another rank has not finished is repeated.
+__global__ void __launch_bounds__(1024) k_c_round_tail(CP P, CS S, gg_cmsg* slots, uint32_t world, uint32_t per_rank,
+                                                      uint64_t region, const uint32_t* err, uint32_t host_err,
+                                                      uint64_t* dv)
 {
-  for (uint32_t r = threadIdx.x; r < world; r += blockDim.x) slots[(size_t)r * (region + 1)].addr = 0;
-}
-__global__ void k_c_export_slots(CS S, const gg_cmsg* b, const uint32_t* n_dev, uint32_t per_rank, uint64_t region,
-                                 gg_cmsg* slots)
-{
-  const uint32_t n = *n_dev;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint32_t r = rec_shard(S, b[i]) / per_rank;
-    gg_cmsg* sl = slots + (size_t)r * (region + 1);
-    const uint64_t j = atomicAdd((unsigned long long*)&sl[0].addr, 1ull);
-    if (j < region) sl[1 + j] = b[i];
-    else atomicOr(S.err, GG_DERR_CAP);
+  __shared__ unsigned long long st[3];                 // active, blocked, least next start
+  const uint32_t tid = threadIdx.x, nt = blockDim.x;
+  const uint32_t quiet = *(volatile uint32_t*)S.quiet;
+  for (uint32_t r = tid; r < world; r += nt) slots[(size_t)r * (region + 1)].addr = 0;
+  if (tid < 3) st[tid] = tid == 2 ? ~0ull : 0ull;
+  __syncthreads();
+  if (quiet) {
+    for (uint32_t lt = tid; lt < P.L; lt += nt) {      // k_c_status
+      const uint64_t r = S.rec[lt];
+      if (r >= S.rec_end[lt]) continue;
+      atomicAdd(&st[0], 1ull);
+      if (S.blocked[lt]) { atomicAdd(&st[1], 1ull); continue; }
+      atomicMin(&st[2], (unsigned long long)(S.clk[lt] + rec_gap(S.meta[r]) * P.gap_ps));
+    }
+    const uint32_t n = *(volatile uint32_t*)S.bnd_cnt;
+    for (uint32_t i = tid; i < n; i += nt) {           // the held records, by owning rank
+      const uint32_t r = rec_shard(S, S.bnd[i]) / per_rank;
+      gg_cmsg* sl = slots + (size_t)r * (region + 1);
+      const uint64_t j = atomicAdd((unsigned long long*)&sl[0].addr, 1ull);
+      if (j < region) sl[1 + j] = S.bnd[i];
+      else atomicOr(S.err, GG_DERR_CAP);
+    }
   }
-}
-__global__ void k_round_status(const uint64_t* st, const gg_cmsg* slots, uint32_t world, uint64_t region,
-                               const uint32_t* err, uint32_t host_err, uint64_t* dv)
-{
-  if (threadIdx.x != 0) return;
+  __threadfence();
+  __syncthreads();
+  if (tid != 0) return;
   uint64_t sent = 0, mx = 0;
   for (uint32_t r = 0; r < world; ++r) {
-    const uint64_t c = slots[(size_t)r * (region + 1)].addr;
+    const uint64_t c = __hip_atomic_load(&slots[(size_t)r * (region + 1)].addr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     sent += c; mx = c > mx ? c : mx;
   }
-  dv[0] = sent; dv[1] = st[0]; dv[2] = st[1];
-  dv[3] = (uint64_t)(*err | host_err); dv[4] = mx;
-  dv[5] = st[2];
+  dv[RW_SENT] = sent; dv[RW_ACTIVE] = st[0]; dv[RW_BLOCKED] = st[1];
+  dv[RW_ERR] = (uint64_t)(__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) | host_err);
+  dv[RW_MAXSLOT] = mx; dv[RW_MINNEXT] = st[2];
+  dv[RW_NOTDONE] = quiet ? 0ull : 1ull; dv[RW_STEPS] = quiet ? quiet - 1 : 0ull;
 }
+__device__ __forceinline__ bool round_go(const uint64_t* dv_all, uint32_t world)
+{
+  uint64_t bad = 0;
+  for (uint32_t r = 0; r < world; ++r) bad |= dv_all[(size_t)r * RW_N + RW_ERR] | dv_all[(size_t)r * RW_N + RW_NOTDONE];
+  return bad == 0;
+}
+// after RCCL, when every rank finished its quantum with no error: the
+// quantum's end on this rank (step counters, held list, run info, record
+// pools for the import)
+__global__ void k_c_round_commit(CP P, CS S, uint64_t q, const uint64_t* dv_all, uint32_t world)
+{
+  if (threadIdx.x != 0 || !round_go(dv_all, world)) return;
+  for (int i = 0; i < 7; ++i) S.ring[i] = 0;           // ring[4], quiet, imp[2]
+  *S.bnd_cnt = 0;
+  S.ri[GG_RI_QUANTA]++;
+  S.ri[GG_RI_FINAL_QUANTUM] = q;
+  S.npool[0] = S.npool[1] = P.L * kChunk;              // the next quantum's first step reads pool 1
+}
+// the received records [0, min(count, slot)) of every peer (nothing unless
+// round_go), and the send / receive slot counts for the host.  The rank's
+// own slot is read where the tail wrote it (its records never leave the GPU)
+__global__ void k_c_round_import(CP P, CS S, const gg_cmsg* send, const gg_cmsg* recv, uint32_t world, uint32_t self,
+                                 uint64_t region, uint64_t slot, const uint64_t* dv_all, uint64_t* counts)
+{
+  if (blockIdx.x == 0 && blockIdx.y == 0)
+    for (uint32_t r = threadIdx.x; r < world; r += blockDim.x) {
+      counts[r] = send[(size_t)r * (region + 1)].addr;
+      counts[world + r] = (r == self ? send : recv)[(size_t)r * (region + 1)].addr;
+    }
+  if (!round_go(dv_all, world)) return;
+  const gg_cmsg* sl = (blockIdx.y == self ? send : recv) + (size_t)blockIdx.y * (region + 1);
+  const uint64_t c = sl[0].addr;
+  const uint64_t e = c < slot ? c : slot;
+  for (uint64_t i = blockIdx.x * blockDim.x + threadIdx.x; i < e; i += (uint64_t)gridDim.x * blockDim.x)
+    import_one(P, S, sl[1 + i], &S.imp[0]);
+}
+
 __global__ void k_c_import_slots(CP P, CS S, const gg_cmsg* slots, uint64_t region, uint64_t lo, uint64_t hi,
                                  const uint64_t* skip)
 {
@@ -3661,32 +3717,52 @@ gg_status gg_coherent_quantum(gg_ctx* ctx, uint64_t q, gg_coherent_status* out)
 // the quantum boundary are scattered to the rank that owns their shard (export
 // order inside a slot does not matter: import lists them by atomics and every
 // consumer orders by the canonical keys).
-gg_status gg_coh_export_slots(gg_ctx* ctx, gg_cmsg* slots, uint32_t world, uint32_t per_rank, uint64_t region)
+// Steps [k0, k0 + n) of quantum q (host-indexed launches; the launches after
+// the quantum's quiet step return at once)
+gg_status gg_coh_steps_async(gg_ctx* ctx, uint64_t q, uint32_t k0, uint32_t n)
+{
+  gg_coh_state* C = ctx->coh;
+  if (!C || !C->begun) return gg_fail(GG_ERR_INVALID, "gg_coherent_begin first");
+  if (C->has_barrier)
+    return gg_fail(GG_ERR_UNSUPPORTED, "BARRIER records are released by gg_coherent_run only (one context)");
+  hipSetDevice(ctx->device);
+  hipStream_t s = ctx->last_stream;
+  const CP& P = C->P;
+  const uint64_t barrier = (q + 1) * (uint64_t)ctx->cfg.quantum_ns * 1000ull;
+  const bool hbh = P.net == GG_NET_EMESH_HOP_BY_HOP;
+  for (uint32_t k = k0; k < k0 + n; ++k) {
+    timed_launch(ctx, C, s, 0, [&] { hipLaunchKernelGGL(k_c_step, dim3(P.L), dim3(64), C->step_lds, s, P, C->S, k, 0u, barrier); });
+    if (hbh) {
+      if (P.nsx) timed_launch(ctx, C, s, 1, [&] { launch_walk(C, s, P.nsx, C->wtx, k, 0); });
+      if (P.nsy) timed_launch(ctx, C, s, 2, [&] { launch_walk(C, s, P.nsy, C->wty, k, 1); });
+    }
+  }
+  GG_HIP(hipGetLastError());
+  return GG_OK;
+}
+gg_status gg_coh_round_tail(gg_ctx* ctx, gg_cmsg* slots, uint32_t world, uint32_t per_rank, uint64_t region,
+                            uint32_t host_err, uint64_t* dv_own)
+{
+  gg_coh_state* C = ctx->coh;
+  if (!C || !C->begun) return gg_fail(GG_ERR_INVALID, "gg_coherent_begin first");
+  hipLaunchKernelGGL(k_c_round_tail, dim3(1), dim3(1024), 0, ctx->last_stream, C->P, C->S, slots, world, per_rank, region,
+                     (const uint32_t*)ctx->err_dev, host_err, dv_own);
+  GG_HIP(hipGetLastError());
+  return GG_OK;
+}
+gg_status gg_coh_round_import(gg_ctx* ctx, uint64_t q, const gg_cmsg* send, const gg_cmsg* recv, uint32_t world,
+                              uint32_t self, uint64_t region, uint64_t slot, const uint64_t* dv_all, uint64_t* counts)
 {
   gg_coh_state* C = ctx->coh;
   if (!C || !C->begun) return gg_fail(GG_ERR_INVALID, "gg_coherent_begin first");
   hipStream_t s = ctx->last_stream;
-  hipLaunchKernelGGL(k_slot_clear, dim3(1), dim3(64), 0, s, slots, world, region);
-  hipLaunchKernelGGL(k_c_export_slots, dim3(256), dim3(256), 0, s, C->S, (const gg_cmsg*)C->S.bnd,
-                     (const uint32_t*)C->S.bnd_cnt, per_rank, region, slots);
-  GG_HIP(hipMemsetAsync(C->S.bnd_cnt, 0, sizeof(uint32_t), s));
+  hipLaunchKernelGGL(k_c_round_commit, dim3(1), dim3(64), 0, s, C->P, C->S, q, dv_all, world);
+  hipLaunchKernelGGL(k_c_round_import, dim3(64, world), dim3(256), 0, s, C->P, C->S, send, recv, world, self, region,
+                     slot, dv_all, counts);
   GG_HIP(hipGetLastError());
   return GG_OK;
 }
-
-// the rank's status words for the all-reduces: dv = {records sent, active,
-// blocked | error flags, largest send-slot count | min next start}
-gg_status gg_coh_round_status(gg_ctx* ctx, const gg_cmsg* slots, uint32_t world, uint64_t region, uint32_t host_err,
-                              uint64_t* dv)
-{
-  gg_coh_state* C = ctx->coh;
-  if (!C || !C->begun) return gg_fail(GG_ERR_INVALID, "gg_coherent_begin first");
-  hipStream_t s = ctx->last_stream;
-  hipLaunchKernelGGL(k_round_status, dim3(1), dim3(64), 0, s, (const uint64_t*)C->status_dev, slots, world, region,
-                     (const uint32_t*)ctx->err_dev, host_err, dv);
-  GG_HIP(hipGetLastError());
-  return GG_OK;
-}
+void gg_coh_harvest(gg_ctx* ctx) { if (ctx->coh) timed_harvest(ctx->coh); }
 
 // import records [lo, min(count, hi)) of every received slot; `first`: the
 // quantum's first import (the record pools of its first step start empty);
@@ -3704,13 +3780,6 @@ gg_status gg_coh_import_slots(gg_ctx* ctx, const gg_cmsg* slots, uint32_t world,
 }
 
 gg_status gg_coh_check(gg_ctx* ctx) { return coh_check(ctx); }
-gg_status gg_coh_quantum_async(gg_ctx* ctx, uint64_t q)
-{
-  gg_coh_state* C = ctx->coh;
-  if (!C || !C->begun) return gg_fail(GG_ERR_INVALID, "gg_coherent_begin first");
-  hipSetDevice(ctx->device);
-  return coh_quantum_steps(ctx, q);
-}
 
 gg_status gg_coherent_export(gg_ctx* ctx, gg_cmsg* out_dev, uint64_t cap, uint64_t* per_shard_counts)
 {

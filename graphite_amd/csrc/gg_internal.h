@@ -148,10 +148,13 @@ gg_status gg_htree_run(gg_ctx* ctx, uint64_t min_proc, const uint64_t* t, const 
 gg_status gg_coh_kernel_stats(gg_ctx* ctx, const char* name, double* total_ms, uint64_t* launches);
 uint64_t  gg_coherent_msg_cap(gg_ctx* ctx);     // records a quantum boundary can hold (after gg_coherent_begin)
 // the quantum steps and the per-rank slot exchange of gg_round_exchange (gg_coherent.hip)
-gg_status gg_coh_quantum_async(gg_ctx* ctx, uint64_t q);
-gg_status gg_coh_export_slots(gg_ctx* ctx, gg_cmsg* slots, uint32_t world, uint32_t per_rank, uint64_t region);
-gg_status gg_coh_round_status(gg_ctx* ctx, const gg_cmsg* slots, uint32_t world, uint64_t region, uint32_t host_err,
-                              uint64_t* dv);
+gg_status gg_coh_steps_async(gg_ctx* ctx, uint64_t q, uint32_t k0, uint32_t n);
+gg_status gg_coh_round_tail(gg_ctx* ctx, gg_cmsg* slots, uint32_t world, uint32_t per_rank, uint64_t region,
+                            uint32_t host_err, uint64_t* dv_own);
+gg_status gg_coh_round_import(gg_ctx* ctx, uint64_t q, const gg_cmsg* send, const gg_cmsg* recv, uint32_t world,
+                              uint32_t self, uint64_t region, uint64_t slot, const uint64_t* dv_all, uint64_t* counts);
+void      gg_coh_harvest(gg_ctx* ctx);
+constexpr int kRoundWords = 8;          // a rank's round status words (RW_* in gg_coherent.hip)
 gg_status gg_coh_import_slots(gg_ctx* ctx, const gg_cmsg* slots, uint32_t world, uint64_t region, uint64_t lo,
                               uint64_t hi, bool first, const uint64_t* skip_if_dev);
 gg_status gg_coh_check(gg_ctx* ctx);
