@@ -2341,6 +2341,18 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
   return T.clk + rec_gap(S.meta[T.rec]) * P.gap_ps;
 }
 
+// The diagnostic hooks (GG_COH_PROFILE / GG_COH_TRACE: phase cycles, step and
+// walker traces) are compiled only into a diagnostics build (-DGG_COH_DIAG=1,
+// tools/build_variant.sh): in the product kernels their pointers are null
+// constants, so the hooks and the registers they would hold are gone.
+#ifndef GG_COH_DIAG
+#define GG_COH_DIAG 0
+#endif
+__device__ __forceinline__ void diag_off(CS& S)
+{
+  if (!GG_COH_DIAG) { S.prof = nullptr; S.trs = nullptr; S.trw = nullptr; S.tre = nullptr; }
+}
+
 // in-kernel launch timing (timing mode 2): the first workgroup start and the
 // last workgroup end of the launch on the 100 MHz s_memrealtime clock — the
 // kernel's execution span as rocprofv3's kernel trace sees it, without the
@@ -2358,6 +2370,7 @@ __device__ __forceinline__ void kt_end(const CS& S)
 
 __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t L, uint32_t devloop, uint64_t barrier_arg)
 {
+  diag_off(S);
   kt_begin(S);
   const uint64_t r0 = S.trs ? __builtin_amdgcn_s_memrealtime() : 0;
   TraceWin W{~0ull, 0, 0};
@@ -2863,6 +2876,7 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
 template <bool PIPE, bool RQ>
 __global__ void __launch_bounds__(PIPE ? 64 * kMaxWalkWaves : 64) k_c_walk(CP P, CS S, uint32_t L, int stage)
 {
+  diag_off(S);
   kt_begin(S);
   if (S.trs && L < S.tr_n && threadIdx.x == 0)
     S.trw[(((size_t)L * 2 + stage) * S.tr_wb + blockIdx.x) * 8] = __builtin_amdgcn_s_memrealtime();
@@ -2923,6 +2937,7 @@ __device__ __forceinline__ void cache_state_copy(const CP& P, const CS& S, uint3
 template <bool LC>
 __global__ void __launch_bounds__(64) k_c_persist(CP P, CS S, uint32_t L0, uint32_t L1)
 {
+  diag_off(S);
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const bool hbh = P.net == GG_NET_EMESH_HOP_BY_HOP;
   uint32_t gen = 0;
@@ -3543,6 +3558,9 @@ static gg_status coh_alloc(gg_ctx* ctx)
     S.kt = nullptr; S.kt_slot = 0;
   }
   S.trs = nullptr; S.trw = nullptr; S.tr_n = 0; S.tr_wb = std::max(std::max(P.nsx, P.nsy), 1u);
+  if (!GG_COH_DIAG && (getenv("GG_COH_TRACE") || getenv("GG_COH_TRACE_EV") || getenv("GG_COH_PROFILE")))
+    fprintf(stderr, "[gg_coh] GG_COH_TRACE / _EV / GG_COH_PROFILE need a diagnostics build "
+                    "(tools/build_variant.sh diag -DGG_COH_DIAG=1; GG_LIB=variants/diag/libgraphite_gpu.so)\n");
   if (getenv("GG_COH_TRACE") && atoi(getenv("GG_COH_TRACE")) > 0) {
     S.tr_n = (uint32_t)atoi(getenv("GG_COH_TRACE"));
     if ((st = dalloc(C, &S.trs, (size_t)S.tr_n * P.L * kTrStep))) return st;
