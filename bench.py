@@ -232,7 +232,10 @@ def coherent_run(args, T, N, H, K, net, world, rank, dev, steps, warmup, verify,
     nc = be.noc_counters()
     kern = {}
     if kernel_profile:
-        be.set_timing(True, every_launch=True)
+        # HIP event pairs on the launch stream around every 16th launch of each
+        # kernel (the pair also holds the launch's dispatch; in-kernel spans,
+        # every_launch=True, hold only its execution)
+        be.set_timing(True)
         c0 = time.perf_counter()
         step()
         torch.cuda.synchronize()
@@ -920,9 +923,8 @@ def main():
                          "traffic": None, "bytes_per_access": COH_BYTES_PER_ACCESS, "launch_accesses": lacc,
                          "kernel_avg_us": dk["avg_us"] if dk else None, "kernel_launches": dk["launches"] if dk else None,
                          "kernels": kern,
-                         "timing": "in-kernel launch spans (first workgroup start to last workgroup end, "
-                                   "s_memrealtime 100 MHz) of every launch, one extra untimed run; the timed runs "
-                                   "carry no instrumentation",
+                         "timing": "HIP event pairs on the launch stream around every 16th launch of each "
+                                   "kernel, one extra run; the timed runs carry no instrumentation",
                          "note": "Mode C is latency-bound: a step is a chain of dependent accesses per tile and each "
                                  "router port serves its packets one by one in the canonical order (DESIGN.md §4); "
                                  "the fraction measures how far that is from the HBM bound, not an HBM bottleneck"},

@@ -165,7 +165,7 @@ struct CS {
   uint32_t* gbar;                        // grid barrier counter of k_c_persist
   // in-kernel launch timing (gg_set_timing mode 2): per timed launch slot
   // {first workgroup start, last workgroup end} on the s_memrealtime clock
-  unsigned long long* kt; uint32_t kt_slot;
+  unsigned long long* kt; uint32_t kt_slot, kt_stride;   // timing mode 2: per block {start, end} of launch slot kt_slot
 };
 // profile slots: step phases 0..5 summed over tiles, 8 = sum over steps of the slowest tile;
 // walker: 16 staging+load, 17 event loop, 18 hand-off+write back, 19 events, 20 sum of slowest walker per launch (X),
@@ -2353,19 +2353,21 @@ __device__ __forceinline__ void diag_off(CS& S)
   if (!GG_COH_DIAG) { S.prof = nullptr; S.trs = nullptr; S.trw = nullptr; S.tre = nullptr; }
 }
 
-// in-kernel launch timing (timing mode 2): the first workgroup start and the
-// last workgroup end of the launch on the 100 MHz s_memrealtime clock — the
-// kernel's execution span as rocprofv3's kernel trace sees it, without the
-// dispatch gap an event pair around the launch adds
+// in-kernel launch timing (timing mode 2): every workgroup stamps its start
+// and end (100 MHz s_memrealtime) in its own words — plain stores, no atomic
+// on a shared word (1 024 blocks contending for one had added ~8 µs to the
+// step kernel) — and the host takes the first start and the last end: the
+// kernel's execution span as rocprofv3's kernel trace sees it
 __device__ __forceinline__ void kt_begin(const CS& S)
 {
-  if (S.kt && threadIdx.x == 0) atomicMin(&S.kt[2 * S.kt_slot], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  if (S.kt && threadIdx.x == 0)
+    S.kt[(size_t)S.kt_slot * S.kt_stride + 2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
 }
 __device__ __forceinline__ void kt_end(const CS& S)
 {
   if (!S.kt) return;
   __syncthreads();
-  if (threadIdx.x == 0) atomicMax(&S.kt[2 * S.kt_slot + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  if (threadIdx.x == 0) S.kt[(size_t)S.kt_slot * S.kt_stride + 2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
 }
 
 __global__ void __launch_bounds__(64) k_c_step(CP P, CS S, uint32_t L, uint32_t devloop, uint64_t barrier_arg)
@@ -3221,7 +3223,7 @@ struct gg_coh_state {
   uint64_t nlaunch[5] = {0, 0, 0, 0, 0};   // all launches
 };
 constexpr uint64_t kTimeSample = 16;
-constexpr uint32_t kKtRing = 4096;      // in-kernel timing slots between two harvests (a batch is <= 256 steps)
+constexpr uint32_t kKtRing = 1024;      // in-kernel timing slots between two harvests (a batch is <= 256 steps)
 static void launch_walk(gg_coh_state* C, hipStream_t s, uint32_t blocks, uint32_t threads, uint32_t L, int stage)
 {
   const bool rq = walk_regq(C->P);
@@ -3265,16 +3267,20 @@ template <class F> static void timed_launch(gg_ctx* ctx, gg_coh_state* C, hipStr
 static void timed_harvest(gg_coh_state* C)
 {
   if (!C->kt_kind.empty()) {
-    const size_t n = C->kt_kind.size();
-    C->kt_host.resize(2 * n);
-    if (hipMemcpy(C->kt_host.data(), C->kt_dev, 16 * n, hipMemcpyDeviceToHost) == hipSuccess) {
+    const size_t n = C->kt_kind.size(), st = C->S.kt_stride;
+    C->kt_host.resize(n * st);
+    if (hipMemcpy(C->kt_host.data(), C->kt_dev, 8 * n * st, hipMemcpyDeviceToHost) == hipSuccess) {
       for (size_t i = 0; i < n; ++i) {
-        const unsigned long long a = C->kt_host[2 * i], b = C->kt_host[2 * i + 1];
-        if (b >= a && a != ~0ull) { C->ksum[C->kt_kind[i]] += (double)(b - a) * C->kt_tick_ns * 1e-6; C->kcnt[C->kt_kind[i]]++; }
+        const int k = C->kt_kind[i];
+        const uint32_t nb = k == 0 ? C->P.L : k == 1 ? C->P.nsx : C->P.nsy;   // every block stamps both words
+        unsigned long long a = ~0ull, b = 0;
+        for (uint32_t j = 0; j < nb; ++j) {
+          a = std::min(a, C->kt_host[i * st + 2 * j]);
+          b = std::max(b, C->kt_host[i * st + 2 * j + 1]);
+        }
+        if (nb && b >= a) { C->ksum[k] += (double)(b - a) * C->kt_tick_ns * 1e-6; C->kcnt[k]++; }
       }
     }
-    for (size_t i = 0; i < n; ++i) { C->kt_host[2 * i] = ~0ull; C->kt_host[2 * i + 1] = 0; }
-    (void)hipMemcpy(C->kt_dev, C->kt_host.data(), 16 * n, hipMemcpyHostToDevice);
     C->kt_kind.clear();
   }
   for (uint32_t i = 0; i < C->tused; ++i) {
@@ -3551,10 +3557,8 @@ static gg_status coh_alloc(gg_ctx* ctx)
 #undef A
   {
     // in-kernel launch timing slots, reset to {~0, 0}
-    if ((st = dalloc(C, &C->kt_dev, 2ull * kKtRing))) return st;
-    std::vector<unsigned long long> init(2 * kKtRing);
-    for (uint32_t i = 0; i < kKtRing; ++i) { init[2 * i] = ~0ull; init[2 * i + 1] = 0; }
-    GG_HIP(hipMemcpy(C->kt_dev, init.data(), 16ull * kKtRing, hipMemcpyHostToDevice));
+    S.kt_stride = 2 * std::max(std::max(P.L, P.nsx), std::max(P.nsy, 1u));
+    if ((st = dalloc(C, &C->kt_dev, (size_t)S.kt_stride * kKtRing))) return st;
     S.kt = nullptr; S.kt_slot = 0;
   }
   S.trs = nullptr; S.trw = nullptr; S.tr_n = 0; S.tr_wb = std::max(std::max(P.nsx, P.nsy), 1u);

@@ -7,7 +7,7 @@
 # counts at 4 / 8 / 16-B widths: MI355X_MICROARCH.md §HBM "other access widths
 # are uncalibrated").  Per-launch means: tools/r03_pmc_agg.py.
 cd "$GRAFT_REPO_ROOT" || exit 1
-OUT="$GRAFT_REPO_ROOT/gpurun_out/r03/pmc"
+OUT="$GRAFT_REPO_ROOT/gpurun_out/${ROUND:-r03}/pmc"
 mkdir -p "$OUT"
 ARGS="--sections '' --steps 1 --warmup 0 --no-cpu-baseline --no-verify --no-kernel-profile ${PMC_ARGS:-}"
 cd /tmp && export TMPDIR=/tmp
