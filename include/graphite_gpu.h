@@ -448,10 +448,11 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* trace, uint64_t* access_o
 /* The coherent mode over ranks (one process per GPU), RCCL over xGMI.
  * nccl_comm is an ncclComm_t (RCCL) of W ranks; rank r's context must own
  * logical shards [r*K/W, (r+1)*K/W) (cfg.shard_begin / shard_end, K =
- * num_shards).  gg_round_exchange runs quantum q on the context
- * (gg_coherent_quantum), sends the held cross-shard records to the ranks that
- * own their shards and receives this rank's (grouped ncclSend / ncclRecv on
- * stream), imports them, and all-reduces the status; *next_q is the quantum
+ * num_shards).  gg_round_exchange runs quantum q's steps on the context,
+ * sends the held cross-shard records to the ranks that own their shards and
+ * receives this rank's (grouped ncclSend / ncclRecv on stream), all-gathers
+ * the ranks' status words and imports the records, with one host sync (a
+ * rank whose step batch was short repeats the round); *next_q is the quantum
  * every rank runs next and *done 1 when the run is over (GG_ERR_STATE on a
  * deadlock).  It replaces the reference's per-message transport
  * (common/transport/socktransport.cc) plus its lax barrier round
