@@ -2910,6 +2910,41 @@ __device__ __forceinline__ void grid_sync(const CS& S, uint32_t& gen)
   __syncthreads();
 }
 
+// The last barrier of a persistent step, with the run's stop vote: each block
+// reads the run-over and error flags after its own step (its writes are
+// visible to it) and ORs them into a vote word before arriving; after the
+// barrier every block reads the same OR, so all leave the loop at the same
+// step without a second barrier.  Three vote words rotate by generation:
+// block 0 clears the next one before arriving (no block votes in it before
+// passing this barrier), and the one it clears was last read before the
+// previous barrier.
+__device__ __forceinline__ uint32_t grid_sync_stop(const CS& S, uint32_t& gen)
+{
+  __shared__ uint32_t stop;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ++gen;
+    uint32_t* vw = S.gbar + 1;
+    const uint64_t done = __hip_atomic_load(&S.qs[QS_DONE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t e = __hip_atomic_load(S.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (done || e) __hip_atomic_fetch_or(&vw[gen % 3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (blockIdx.x == 0) __hip_atomic_store(&vw[(gen + 1) % 3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(S.gbar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t target = gen * gridDim.x;
+    for (uint32_t spin = 0; __hip_atomic_load(S.gbar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spin) {
+      if (spin > (1u << 24)) { atomicOr(S.err, GG_DERR_STATE); break; }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    stop = __hip_atomic_load(&vw[gen % 3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return stop;
+}
+
 // Small meshes (P.L <= kPersistTiles): the device-driven loop of
 // gg_coherent_run in ONE launch — launch indices [L0, L1) of step + X walk +
 // Y walk, separated by grid barriers instead of kernel boundaries.  Every
@@ -2947,21 +2982,17 @@ __global__ void __launch_bounds__(64) k_c_persist(CP P, CS S, uint32_t L0, uint3
   if (LC) cache_state_copy<LC>(P, S, blockIdx.x, smem + P.cache_lds_off, true);
   for (uint32_t L = L0; L < L1; ++L) {
     step_body<LC, true>(P, S, L, 1u, 0, W);
-    grid_sync(S, gen);
     if (hbh) {
+      grid_sync(S, gen);
       for (uint32_t b = blockIdx.x; b < P.nsx; b += gridDim.x)
         if (walk_regq(P)) walk_body<false, true>(P, S, L, 0, b); else walk_body<false, false>(P, S, L, 0, b);
       grid_sync(S, gen);
       for (uint32_t b = blockIdx.x; b < P.nsy; b += gridDim.x)
         if (walk_regq(P)) walk_body<false, true>(P, S, L, 1, b); else walk_body<false, false>(P, S, L, 1, b);
-      grid_sync(S, gen);
     }
-    const uint64_t done = __hip_atomic_load(&S.qs[QS_DONE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t e = __hip_atomic_load(S.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // every block has read this step's flags before any block starts the next
-    // step (which may set them): all blocks leave the loop at the same step
-    grid_sync(S, gen);
-    if (done || e) break;
+    // the step's last barrier, with the stop vote: all blocks leave the loop
+    // at the same step
+    if (grid_sync_stop(S, gen)) break;
   }
   if (LC) cache_state_copy<LC>(P, S, blockIdx.x, smem + P.cache_lds_off, false);
 }
@@ -3552,7 +3583,7 @@ static gg_status coh_alloc(gg_ctx* ctx)
   A(xl, (uint64_t)std::max(P.nsx, 1u) * P.seg_cap); A(nxl, std::max(P.nsx, 1u));
   A(yl, (uint64_t)std::max(P.nsy, 1u) * P.seg_cap); A(nyl, std::max(P.nsy, 1u));
   A(bnd, P.msg_cap); A(bnd_cnt, 1);
-  A(ring, 11); A(ri, GG_NUM_RUN_INFO); A(qs, QS_N); A(gbar, 1);
+  A(ring, 11); A(ri, GG_NUM_RUN_INFO); A(qs, QS_N); A(gbar, 4);
   A(gscr, L * 6 * P.IC);
 #undef A
   {
@@ -3888,7 +3919,7 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
       persist = false;
   }
   while (persist) {
-    GG_HIP(hipMemsetAsync(C->S.gbar, 0, sizeof(uint32_t), s));
+    GG_HIP(hipMemsetAsync(C->S.gbar, 0, 4 * sizeof(uint32_t), s));   // counter + the three stop-vote words
     if (plc) {
       const size_t lds = P.cache_lds_off + P.cache_lds_bytes;
       timed_launch(ctx, C, s, 3, [&] { hipLaunchKernelGGL(k_c_persist<true>, dim3(P.L), dim3(64), lds, s, P, C->S, L, L + kPersistLaunches); });
