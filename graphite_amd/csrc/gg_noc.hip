@@ -19,6 +19,12 @@
 
 #include <algorithm>
 
+// The diagnostic hooks (GG_NOC_PROFILE: phase cycles) are compiled only into
+// a diagnostics build (-DGG_NOC_DIAG=1): in the product kernels `prof` is a
+// null constant, so the hooks and the registers they hold are gone.
+#ifndef GG_NOC_DIAG
+#define GG_NOC_DIAG 0
+#endif
 namespace {
 using namespace gg;
 
@@ -611,6 +617,7 @@ __global__ __launch_bounds__(kSweepThreads) void k_chain_sweep(NocDev D, int sta
     const uint32_t* __restrict__ len, const uint64_t* __restrict__ bucket_off, uint32_t* __restrict__ bucket_ids,
     Ev* heap, PktState S, unsigned long long* prof)
 {
+  if (!GG_NOC_DIAG) prof = nullptr;
   chain_sweep(D, stage, dst, len, bucket_off, bucket_ids, heap, S, prof, blockIdx.x);
 }
 
@@ -648,6 +655,7 @@ __global__ __launch_bounds__(64 * kPipeWaves) void k_chain_pipe(NocDev D, int st
     const uint32_t* __restrict__ len, const uint64_t* __restrict__ bucket_off, uint32_t* __restrict__ bucket_ids,
     Ev* heap, PktState S, SK* pscr, uint64_t pstride, unsigned long long* prof)
 {
+  if (!GG_NOC_DIAG) prof = nullptr;
   extern __shared__ __attribute__((aligned(16))) uint8_t qlds[];
   const NocParams& P = D.P;
   const uint32_t c = blockIdx.x, line = c / 2, dir = c % 2, tid = threadIdx.x, ln = tid & 63, wv = tid >> 6;
@@ -1376,6 +1384,7 @@ __global__ __launch_bounds__(kTpThreads) void k_tree_pool(NocDev D, TreeIO IO, u
                                                          uint64_t hcap, uint32_t gcap, uint32_t ecap,
                                                          unsigned long long* prof)
 {
+  if (!GG_NOC_DIAG) prof = nullptr;
   extern __shared__ __align__(16) uint8_t tp_lds[];
   __shared__ uint32_t wsum[kTpThreads / 64 + 1];
   __shared__ unsigned long long s_tmin, s_pmin, s_pmin1;
@@ -1696,6 +1705,7 @@ __global__ __launch_bounds__(kTgThreads) void k_tree_grid(NocDev D, TreeIO IO, T
                                                          uint64_t bwg, uint32_t ecap, uint32_t gcap,
                                                          unsigned long long* prof)
 {
+  if (!GG_NOC_DIAG) prof = nullptr;
   // prof (GG_NOC_PROFILE=1, diagnostics): block 0's shader clocks per phase
   unsigned long long pc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pw = 0, pt = __builtin_amdgcn_s_memtime();
   auto lap = [&](int i) { if (prof) { const unsigned long long x = __builtin_amdgcn_s_memtime(); pc[i] += x - pt; pt = x; } };
@@ -2082,6 +2092,7 @@ gg_status gg_noc_alloc(gg_ctx* ctx)
   P.qaux = hq_aux(c.queue_model_type, c.basic_moving_avg, c.history_list_no_interleaving);
   if (gg_status e = gg_check_queue_model(c.queue_model_type, P.qaux, P.max_size)) return e;
   if (getenv("GG_NOC_PROFILE") && atoi(getenv("GG_NOC_PROFILE"))) {
+    if (!GG_NOC_DIAG) fprintf(stderr, "[gg_noc] GG_NOC_PROFILE needs a diagnostics build (-DGG_NOC_DIAG=1)\n");
     GG_HIP(hipMalloc((void**)&S->prof, 32 * sizeof(unsigned long long)));
     GG_HIP(hipMemset(S->prof, 0, 32 * sizeof(unsigned long long)));
     GG_HIP(hipMemset(S->prof + 25, 0xFF, sizeof(unsigned long long)));
