@@ -79,6 +79,10 @@ __device__ __forceinline__ bool has_data(uint32_t t)
 }
 
 struct DEnt { uint64_t addr; int32_t owner; uint16_t dstate; uint16_t nsh; };   // 16 B
+// a tile's step state (trace position, clock, pending access, blocking,
+// sequence, replaced entries, request FIFO length): one line, one pointer
+struct TileSt { uint64_t rec, rec_end, clk, pend_start, out_addr, out_time; uint32_t blocked, seq, nrep, nrq; };
+static_assert(sizeof(TileSt) == 64, "one 64-B line per tile");
 struct CReq { uint64_t addr, time; uint32_t type, requester; };                 // 24 B
 // address-space-typed pointers (a generic pointer whose origin the compiler
 // cannot see compiles to flat accesses)
@@ -130,11 +134,10 @@ struct CS {
   uint64_t* mtab;                        // [L][2][2^mt_log] address sets (line | E 1 I 2 F 4), ~0 empty; when tracking
   unsigned long long* mtc;               // [L][2][GG_NUM_MISS_TYPES] when tracking
   uint64_t* st;                          // [L][GG_NUM_TILE_STATS]
-  uint64_t *rec, *rec_end, *clk, *pend_start, *out_addr, *out_time;
-  uint32_t *blocked, *seq;
+  TileSt* ts;                            // [L] the tiles' step state (one 64-B line each)
   DEnt* dir; uint64_t* dsh;              // [L][E], [L][E][W]
-  DEnt* rep; uint64_t* rsh; uint32_t* nrep;   // [L][R], [L][R][W]
-  CReq* rq; uint32_t* nrq;               // [L][QC]
+  DEnt* rep; uint64_t* rsh;              // [L][R], [L][R][W]
+  CReq* rq;                              // [L][QC]
   HQueue* dq; HNode* dnd;                // DRAM queue per tile
   const uint32_t* gtile; const int32_t* ltile; const uint32_t* shard;   // local -> tile, tile -> local (-1), tile -> shard
   const uint64_t* addr; const uint32_t* meta; uint64_t* out;
@@ -577,9 +580,9 @@ struct TilePre {
   {
     tile = S.gtile[lt];
     segx = S.tseg[(size_t)tile * 2]; segy = S.tseg[(size_t)tile * 2 + 1];
-    rec = S.rec[lt]; rec_end = S.rec_end[lt]; clk = S.clk[lt]; pend_start = S.pend_start[lt];
-    out_addr = S.out_addr[lt]; out_time = S.out_time[lt];
-    blocked = S.blocked[lt]; seq = S.seq[lt]; nrep = S.nrep[lt]; nrq = S.nrq[lt];
+    rec = S.ts[lt].rec; rec_end = S.ts[lt].rec_end; clk = S.ts[lt].clk; pend_start = S.ts[lt].pend_start;
+    out_addr = S.ts[lt].out_addr; out_time = S.ts[lt].out_time;
+    blocked = S.ts[lt].blocked; seq = S.ts[lt].seq; nrep = S.ts[lt].nrep; nrq = S.ts[lt].nrq;
     ccv = ln < 2 * GG_NUM_CACHE_COUNTERS ? S.cc[(size_t)lt * 2 * GG_NUM_CACHE_COUNTERS + ln] : 0;
     stv = ln < GG_NUM_TILE_STATS ? S.st[(size_t)lt * GG_NUM_TILE_STATS + ln] : 0;
     narv0 = S.narv0[lt]; narv1 = S.narv1[lt]; ninb0 = S.ninb0[lt]; ninb1 = S.ninb1[lt];
@@ -1453,15 +1456,15 @@ struct Tile {
       else if (ln < GG_NUM_TILE_STATS && d) g[ln] = stv + d;
     }
     if (ln == 0) {
-      if (rec != p0.rec) S.rec[lt] = rec;
-      if (clk != p0.clk) S.clk[lt] = clk;
-      if (pend_start != p0.pend_start) S.pend_start[lt] = pend_start;
-      if (out_addr != p0.out_addr) S.out_addr[lt] = out_addr;
-      if (out_time != p0.out_time) S.out_time[lt] = out_time;
-      if (blocked != p0.blocked) S.blocked[lt] = blocked;
-      if (seq != p0.seq) S.seq[lt] = seq;
-      if (nrep != p0.nrep) S.nrep[lt] = nrep;
-      if (nrq != p0.nrq) S.nrq[lt] = nrq;
+      if (rec != p0.rec) S.ts[lt].rec = rec;
+      if (clk != p0.clk) S.ts[lt].clk = clk;
+      if (pend_start != p0.pend_start) S.ts[lt].pend_start = pend_start;
+      if (out_addr != p0.out_addr) S.ts[lt].out_addr = out_addr;
+      if (out_time != p0.out_time) S.ts[lt].out_time = out_time;
+      if (blocked != p0.blocked) S.ts[lt].blocked = blocked;
+      if (seq != p0.seq) S.ts[lt].seq = seq;
+      if (nrep != p0.nrep) S.ts[lt].nrep = nrep;
+      if (nrq != p0.nrq) S.ts[lt].nrq = nrq;
     }
   }
 };
@@ -1612,16 +1615,16 @@ __device__ __forceinline__ void quantum_end(const CP& P, const CS& S, uint32_t L
   const uint32_t ln = threadIdx.x, lt = blockIdx.x;
   volatile uint64_t* qs = S.qs;
   if (ln == 0) {
-    const uint64_t r = S.rec[lt];
-    if (r < S.rec_end[lt]) {
+    const uint64_t r = S.ts[lt].rec;
+    if (r < S.ts[lt].rec_end) {
       atomicAdd((unsigned long long*)&S.qs[QS_ACTIVE], 1ull);
-      const uint32_t b = S.blocked[lt];
+      const uint32_t b = S.ts[lt].blocked;
       if (b == kBarWait) {
         atomicAdd((unsigned long long*)&S.qs[QS_BWAIT], 1ull);
-        atomicMax((unsigned long long*)&S.qs[QS_BMAX], (unsigned long long)S.clk[lt]);
+        atomicMax((unsigned long long*)&S.qs[QS_BMAX], (unsigned long long)S.ts[lt].clk);
       } else if (b) atomicAdd((unsigned long long*)&S.qs[QS_BLOCKED], 1ull);
       else atomicMin((unsigned long long*)&S.qs[QS_MIN_NEXT],
-                     (unsigned long long)(S.clk[lt] + rec_gap(S.meta[r]) * P.gap_ps));
+                     (unsigned long long)(S.ts[lt].clk + rec_gap(S.meta[r]) * P.gap_ps));
     }
   }
   const uint32_t nb = *(volatile uint32_t*)S.bnd_cnt;
@@ -3053,11 +3056,11 @@ __global__ void k_c_status(CP P, CS S, uint64_t* out /* [active, blocked, min_ne
 {
   const uint32_t lt = blockIdx.x * blockDim.x + threadIdx.x;
   if (lt >= P.L) return;
-  const uint64_t r = S.rec[lt];
-  if (r >= S.rec_end[lt]) return;
+  const uint64_t r = S.ts[lt].rec;
+  if (r >= S.ts[lt].rec_end) return;
   atomicAdd((unsigned long long*)&out[0], 1ull);
-  if (S.blocked[lt]) { atomicAdd((unsigned long long*)&out[1], 1ull); return; }
-  const uint64_t s = S.clk[lt] + rec_gap(S.meta[r]) * P.gap_ps;
+  if (S.ts[lt].blocked) { atomicAdd((unsigned long long*)&out[1], 1ull); return; }
+  const uint64_t s = S.ts[lt].clk + rec_gap(S.meta[r]) * P.gap_ps;
   atomicMin((unsigned long long*)&out[2], (unsigned long long)s);
 }
 
@@ -3076,11 +3079,11 @@ __global__ void __launch_bounds__(256) k_c_reset(CP P, CS S, const uint64_t* off
   if (tid < 2 * GG_NUM_CACHE_COUNTERS) S.cc[(size_t)lt * 2 * GG_NUM_CACHE_COUNTERS + tid] = 0;
   if (tid < GG_NUM_TILE_STATS) S.st[(size_t)lt * GG_NUM_TILE_STATS + tid] = 0;
   if (tid == 0) {
-    S.nrep[lt] = 0; S.nrq[lt] = 0;
+    S.ts[lt].nrep = 0; S.ts[lt].nrq = 0;
     const uint32_t tile = S.gtile[lt];
-    S.rec[lt] = offs[tile]; S.rec_end[lt] = offs[tile + 1];
-    S.clk[lt] = 0; S.pend_start[lt] = 0; S.out_addr[lt] = INV_ADDR; S.out_time[lt] = 0;
-    S.blocked[lt] = 0; S.seq[lt] = 0;
+    S.ts[lt].rec = offs[tile]; S.ts[lt].rec_end = offs[tile + 1];
+    S.ts[lt].clk = 0; S.ts[lt].pend_start = 0; S.ts[lt].out_addr = INV_ADDR; S.ts[lt].out_time = 0;
+    S.ts[lt].blocked = 0; S.ts[lt].seq = 0;
     S.ninb0[lt] = 0; S.ninb1[lt] = 0; S.narv0[lt] = 0; S.narv1[lt] = 0;
     if (P.dram_qm)                                   // QueueModel::create(dram/queue_model/type, min_processing_time)
       hq_init(S.dq + lt, S.dnd + (size_t)lt * P.max_list, P.max_list, P.dram_qtype, P.dram_qaux);
@@ -3142,11 +3145,11 @@ __global__ void __launch_bounds__(1024) k_c_round_tail(CP P, CS S, gg_cmsg* slot
   __syncthreads();
   if (quiet) {
     for (uint32_t lt = tid; lt < P.L; lt += nt) {      // k_c_status
-      const uint64_t r = S.rec[lt];
-      if (r >= S.rec_end[lt]) continue;
+      const uint64_t r = S.ts[lt].rec;
+      if (r >= S.ts[lt].rec_end) continue;
       atomicAdd(&st[0], 1ull);
-      if (S.blocked[lt]) { atomicAdd(&st[1], 1ull); continue; }
-      atomicMin(&st[2], (unsigned long long)(S.clk[lt] + rec_gap(S.meta[r]) * P.gap_ps));
+      if (S.ts[lt].blocked) { atomicAdd(&st[1], 1ull); continue; }
+      atomicMin(&st[2], (unsigned long long)(S.ts[lt].clk + rec_gap(S.meta[r]) * P.gap_ps));
     }
     const uint32_t n = *(volatile uint32_t*)S.bnd_cnt;
     for (uint32_t i = tid; i < n; i += nt) {           // the held records, by owning rank
@@ -3570,11 +3573,10 @@ static gg_status coh_alloc(gg_ctx* ctx)
     P.mt_log = (uint32_t)__builtin_ctz(lines);
     A(mtab, (size_t)L * 2 << P.mt_log); A(mtc, L * 2 * GG_NUM_MISS_TYPES);
   }
-  A(rec, L); A(rec_end, L); A(clk, L); A(pend_start, L); A(out_addr, L); A(out_time, L);
-  A(blocked, L); A(seq, L);
+  A(ts, L);
   A(dir, L * P.E); A(dsh, L * P.E * P.W);
-  A(rep, L * P.R); A(rsh, L * P.R * P.W); A(nrep, L);
-  A(rq, L * P.QC); A(nrq, L);
+  A(rep, L * P.R); A(rsh, L * P.R * P.W);
+  A(rq, L * P.QC);
   A(dq, L); A(dnd, L * P.max_list);
   A(pool0, P.msg_cap); A(pool1, P.msg_cap); A(npool, 2);
   A(inb0, L * P.IC); A(inb1, L * P.IC); A(ninb0, L); A(ninb1, L);
