@@ -142,8 +142,9 @@ struct CS {
   const uint32_t* gtile; const int32_t* ltile; const uint32_t* shard;   // local -> tile, tile -> local (-1), tile -> shard
   const uint64_t* addr; const uint32_t* meta; uint64_t* out;
   gg_cmsg* pool0; gg_cmsg* pool1; uint32_t* npool;    // records of even / odd steps, alloc counters [2]
-  uint32_t* inb0; uint32_t* inb1; uint32_t* ninb0; uint32_t* ninb1;   // inbox record lists [L][IC], [L]
-  uint32_t* arv0; uint32_t* arv1; uint32_t* narv0; uint32_t* narv1;   // hop-by-hop SELF lists
+  uint32_t* inb0; uint32_t* inb1;       // inbox record lists [L][IC]
+  uint32_t* arv0; uint32_t* arv1;       // hop-by-hop SELF lists [L][IC]
+  uint32_t* cnt4;                       // [L][4]: the lists' lengths {inbox even, odd, SELF even, odd}
   uint32_t* xl; uint32_t* nxl; uint32_t* yl; uint32_t* nyl;           // segment lists [n][seg_cap], [n]
   const Seg* segx; const Seg* segy;
   const uint32_t* tseg;                  // [T][2]: X run, Y run of a tile (~0 if not owned)
@@ -189,9 +190,9 @@ __device__ __forceinline__ void prof_batch(const CS& S, int kind, uint32_t m, ui
 
 __device__ __forceinline__ gg_cmsg* pool(const CS& S, uint32_t p) { return p ? S.pool1 : S.pool0; }
 __device__ __forceinline__ uint32_t* inb(const CS& S, uint32_t p) { return p ? S.inb1 : S.inb0; }
-__device__ __forceinline__ uint32_t* ninb(const CS& S, uint32_t p) { return p ? S.ninb1 : S.ninb0; }
+__device__ __forceinline__ uint32_t* ninb_at(const CS& S, uint32_t p, size_t l) { return S.cnt4 + l * 4 + p; }
 __device__ __forceinline__ uint32_t* arv(const CS& S, uint32_t p) { return p ? S.arv1 : S.arv0; }
-__device__ __forceinline__ uint32_t* narv(const CS& S, uint32_t p) { return p ? S.narv1 : S.narv0; }
+__device__ __forceinline__ uint32_t* narv_at(const CS& S, uint32_t p, size_t l) { return S.cnt4 + l * 4 + 2 + p; }
 
 __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) { return (uint64_t)__shfl((long long)v, src); }
 // lane l's value for a wave-uniform l (v_readlane, no LDS permute)
@@ -534,12 +535,12 @@ struct GHooks {
   }
   __device__ __forceinline__ uint32_t inbox_slot(uint32_t pn, uint32_t ld) const
   {
-    const uint32_t j = atomicAdd(&(pn ? S.ninb1 : S.ninb0)[ld], 1u);
+    const uint32_t j = atomicAdd(ninb_at(S, pn, ld), 1u);
     return j < P.IC ? j : ~0u;
   }
   __device__ __forceinline__ uint32_t arv_slot(uint32_t pn, uint32_t ld) const
   {
-    const uint32_t j = atomicAdd(&(pn ? S.narv1 : S.narv0)[ld], 1u);
+    const uint32_t j = atomicAdd(narv_at(S, pn, ld), 1u);
     return j < P.IC ? j : ~0u;
   }
   __device__ __forceinline__ uint32_t seg_slot(bool is_x, uint32_t sg) const
@@ -555,8 +556,8 @@ struct GHooks {
     return true;
   }
   // the tile's delivery counts of parity p were consumed
-  __device__ __forceinline__ void clear_arv(uint32_t p, uint32_t lt) const { (p ? S.narv1 : S.narv0)[lt] = 0; }
-  __device__ __forceinline__ void clear_inb(uint32_t p, uint32_t lt) const { (p ? S.ninb1 : S.ninb0)[lt] = 0; }
+  __device__ __forceinline__ void clear_arv(uint32_t p, uint32_t lt) const { *narv_at(S, p, lt) = 0; }
+  __device__ __forceinline__ void clear_inb(uint32_t p, uint32_t lt) const { *ninb_at(S, p, lt) = 0; }
   // lane 0: the step's run-info counts
   __device__ __forceinline__ void step_counts(uint32_t k, uint32_t net, uint32_t self, uint32_t bnd, uint32_t sent) const
   {
@@ -585,7 +586,8 @@ struct TilePre {
     blocked = S.ts[lt].blocked; seq = S.ts[lt].seq; nrep = S.ts[lt].nrep; nrq = S.ts[lt].nrq;
     ccv = ln < 2 * GG_NUM_CACHE_COUNTERS ? S.cc[(size_t)lt * 2 * GG_NUM_CACHE_COUNTERS + ln] : 0;
     stv = ln < GG_NUM_TILE_STATS ? S.st[(size_t)lt * GG_NUM_TILE_STATS + ln] : 0;
-    narv0 = S.narv0[lt]; narv1 = S.narv1[lt]; ninb0 = S.ninb0[lt]; ninb1 = S.ninb1[lt];
+    const uint4 c = reinterpret_cast<const uint4*>(S.cnt4)[lt];      // one 16-B load
+    ninb0 = c.x; ninb1 = c.y; narv0 = c.z; narv1 = c.w;
   }
 };
 
@@ -2814,7 +2816,7 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
     const uint32_t dst = i == tid ? pdst : m->dst;
     if (h == dst) {                                            // the SELF port of the destination, next step
       const int32_t ld = i == tid ? (int32_t)pf : S.ltile[dst];
-      const uint32_t j = atomicAdd(&narv(S, p ^ 1u)[ld], 1u);
+      const uint32_t j = atomicAdd(narv_at(S, p ^ 1u, ld), 1u);
       if (j >= P.IC) { atomicOr(S.err, GG_DERR_CAP); continue; }
       arv(S, p ^ 1u)[(size_t)ld * P.IC + j] = r;
     } else {                                                   // X done: the Y segment of the destination column
@@ -3013,7 +3015,7 @@ __device__ __forceinline__ void import_one(const CP& P, const CS& S, const gg_cm
     if (r >= P.msg_cap) { atomicOr(S.err, GG_DERR_CAP); return; }
     S.pool1[r] = m;
     const int32_t ld = S.ltile[m.dst];
-    const uint32_t j = atomicAdd(&S.ninb0[ld], 1u);
+    const uint32_t j = atomicAdd(ninb_at(S, 0, ld), 1u);
     if (j >= P.IC) { atomicOr(S.err, GG_DERR_CAP); return; }
     S.inb0[(size_t)ld * P.IC + j] = r;
     return;
@@ -3024,7 +3026,7 @@ __device__ __forceinline__ void import_one(const CP& P, const CS& S, const gg_cm
   atomicAdd(resumed, 1u);
   if (m.hop == m.dst) {
     const int32_t ld = S.ltile[m.dst];
-    const uint32_t j = atomicAdd(&S.narv1[ld], 1u);
+    const uint32_t j = atomicAdd(narv_at(S, 1, ld), 1u);
     if (j >= P.IC) { atomicOr(S.err, GG_DERR_CAP); return; }
     S.arv1[(size_t)ld * P.IC + j] = r;
     return;
@@ -3084,7 +3086,7 @@ __global__ void __launch_bounds__(256) k_c_reset(CP P, CS S, const uint64_t* off
     S.ts[lt].rec = offs[tile]; S.ts[lt].rec_end = offs[tile + 1];
     S.ts[lt].clk = 0; S.ts[lt].pend_start = 0; S.ts[lt].out_addr = INV_ADDR; S.ts[lt].out_time = 0;
     S.ts[lt].blocked = 0; S.ts[lt].seq = 0;
-    S.ninb0[lt] = 0; S.ninb1[lt] = 0; S.narv0[lt] = 0; S.narv1[lt] = 0;
+    reinterpret_cast<uint4*>(S.cnt4)[lt] = make_uint4(0, 0, 0, 0);
     if (P.dram_qm)                                   // QueueModel::create(dram/queue_model/type, min_processing_time)
       hq_init(S.dq + lt, S.dnd + (size_t)lt * P.max_list, P.max_list, P.dram_qtype, P.dram_qaux);
   }
@@ -3579,9 +3581,9 @@ static gg_status coh_alloc(gg_ctx* ctx)
   A(rq, L * P.QC);
   A(dq, L); A(dnd, L * P.max_list);
   A(pool0, P.msg_cap); A(pool1, P.msg_cap); A(npool, 2);
-  A(inb0, L * P.IC); A(inb1, L * P.IC); A(ninb0, L); A(ninb1, L);
+  A(inb0, L * P.IC); A(inb1, L * P.IC); A(cnt4, L * 4);
   const uint64_t al = P.net == GG_NET_EMESH_HOP_BY_HOP ? L * P.IC : 1;
-  A(arv0, al); A(arv1, al); A(narv0, L); A(narv1, L);
+  A(arv0, al); A(arv1, al);
   A(xl, (uint64_t)std::max(P.nsx, 1u) * P.seg_cap); A(nxl, std::max(P.nsx, 1u));
   A(yl, (uint64_t)std::max(P.nsy, 1u) * P.seg_cap); A(nyl, std::max(P.nsy, 1u));
   A(bnd, P.msg_cap); A(bnd_cnt, 1);
