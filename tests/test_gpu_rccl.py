@@ -3,7 +3,7 @@
 torch.distributed "nccl" (= RCCL) process group (ProcessGroupNCCL._comm_ptr).
 A one-GPU box forms a one-rank communicator only (RCCL refuses two ranks on
 one device); the exchange logic over several ranks is the same as
-graphite_amd.coherent.run, covered by the gloo tests (tests/test_coherent_dist.py).
+graphite_amd.coherent.run, covered by the gloo tests (tests/test_dist_gloo.py).
 The run is repeated with one-record peer slots (GG_ROUND_SLOT=1) so that the
 sized overflow round of gg_round_exchange runs too."""
 import os
