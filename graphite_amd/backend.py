@@ -58,7 +58,21 @@ EXPORTS = ["gg_abi_version", "gg_last_error", "gg_config_default", "gg_create", 
            "gg_coherent_begin", "gg_coherent_quantum", "gg_coherent_export", "gg_coherent_import",
            "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace", "gg_shard_map",
            "gg_kernel_stats", "gg_round_exchange", "gg_coherent_run_ranks", "gg_gen_stress_trace",
-           "gg_split_accesses", "gg_combine_accesses", "gg_dump_summary", "gg_core_model_run", "gg_core_get_stats", "gg_coherent_get_miss_types"]
+           "gg_split_accesses", "gg_combine_accesses", "gg_dump_summary", "gg_core_model_run", "gg_core_get_stats", "gg_coherent_get_miss_types",
+           "gg_round_pack", "gg_round_unpack", "gg_round_finish"]
+
+
+class RoundIO(ctypes.Structure):
+    """gg_round_io: the device buffers of one rank's round (gg_round_pack)."""
+    _fields_ = [("send", ctypes.c_void_p), ("recv", ctypes.c_void_p), ("words_own", ctypes.c_void_p),
+                ("words_all", ctypes.c_void_p), ("stride", ctypes.c_uint64), ("slot", ctypes.c_uint64),
+                ("send_count", ctypes.POINTER(ctypes.c_uint64)), ("recv_count", ctypes.POINTER(ctypes.c_uint64)),
+                ("next_q", ctypes.c_uint64), ("done", ctypes.c_int32), ("state", ctypes.c_int32)]
+
+
+ROUND_WORDS = 8
+ROUND_DONE, ROUND_AGAIN, ROUND_OVERFLOW = 0, 1, 2
+CMSG_RECORD_BYTES = 64
 
 
 class _CStatus(ctypes.Structure):
@@ -119,11 +133,14 @@ def load():
     L.gg_core_model_run.argtypes = [vp, ctypes.POINTER(_Trace), vp, vp]
     L.gg_core_get_stats.argtypes = [vp, vp]
     L.gg_coherent_get_miss_types.argtypes = [vp, vp]
+    L.gg_round_pack.argtypes = [vp, u32, u32, u64, ctypes.POINTER(RoundIO)]
+    L.gg_round_unpack.argtypes = [vp, ctypes.POINTER(RoundIO)]
+    L.gg_round_finish.argtypes = [vp, ctypes.POINTER(RoundIO)]
     for name in ["gg_kernel_stats", "gg_shard_map", "gg_coherent_begin", "gg_coherent_quantum", "gg_coherent_export",
                  "gg_coherent_import", "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace",
                  "gg_round_exchange", "gg_coherent_run_ranks", "gg_gen_stress_trace", "gg_split_accesses",
                  "gg_combine_accesses", "gg_dump_summary", "gg_core_model_run", "gg_core_get_stats",
-                 "gg_coherent_get_miss_types"]:
+                 "gg_coherent_get_miss_types", "gg_round_pack", "gg_round_unpack", "gg_round_finish"]:
         getattr(L, name).restype = i32
     for name in ["gg_reset", "gg_cache_access_batch", "gg_cache_get_counters", "gg_cache_get_line_info",
                  "gg_cache_set_line_info", "gg_cache_access_line", "gg_cache_insert_line",
@@ -313,6 +330,21 @@ class Backend:
             _need_dev(out, torch.int64, addr.numel())
         tr = self._trace(addr, meta, tile_offsets)
         _check(load().gg_coherent_begin(self.h, ctypes.byref(tr), _ptr(out), _stream(stream)))
+
+    def round_pack(self, world, rank, q):
+        """gg_round_pack: quantum q's steps + the tail on the context's stream;
+        returns the RoundIO with the device slots / words to move."""
+        io = RoundIO()
+        _check(load().gg_round_pack(self.h, world, rank, q, ctypes.byref(io)))
+        return io
+
+    def round_unpack(self, io):
+        _check(load().gg_round_unpack(self.h, ctypes.byref(io)))
+        return io
+
+    def round_finish(self, io):
+        _check(load().gg_round_finish(self.h, ctypes.byref(io)))
+        return io
 
     def coherent_quantum(self, q):
         st = _CStatus()

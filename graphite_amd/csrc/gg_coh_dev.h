@@ -84,6 +84,7 @@ __device__ __forceinline__ bool has_data(uint32_t t)
 }
 
 struct DEnt { uint64_t addr; int32_t owner; uint16_t dstate; uint16_t nsh; };   // 16 B
+struct HMsg { uint64_t addr, arrival_ps; uint32_t type, src, requester; };        // the fields a handler reads
 // a tile's step state (trace position, clock, pending access, blocking,
 // sequence, replaced entries, request FIFO length): one line, one pointer
 struct TileSt { uint64_t rec, rec_end, clk, pend_start, out_addr, out_time; uint32_t blocked, seq, nrep, nrq; };
@@ -128,6 +129,7 @@ struct CP {
   uint32_t walk_wide;                      // pipelined walkers take the one-wave sweep (the > 128-packet path; GG_COH_WALK_WIDE=1)
   uint32_t no_hit_runs;                    // 1: every record through app_access (hit runs off; 0 in the build)
   uint32_t mt1, mt2, mt_log;               // miss-type tracking of the L1-D / L2 (cfg flags), log2 set capacity
+  uint32_t fast;                           // k_c_step<true> (Tile's F): register queues only, no miss types
   uint64_t lat_l1d, lat_l1t, lat_l2d, lat_l2t, lat_dir, gap_ps, dram_proc, dram_cost;
   NocParams np;
 };
@@ -145,6 +147,7 @@ struct CS {
   CReq* rq;                              // [L][QC]
   HQueue* dq; HNode* dnd;                // DRAM queue per tile
   const uint32_t* gtile; const int32_t* ltile; const uint32_t* shard;   // local -> tile, tile -> local (-1), tile -> shard
+  const uint4* tinfo;                    // [L] {tile, X run, Y run, 0} of a local tile: one load, no chain
   const uint64_t* addr; const uint32_t* meta; uint64_t* out;
   gg_cmsg* pool0; gg_cmsg* pool1; uint32_t* npool;    // records of even / odd steps, alloc counters [2]
   uint32_t* inb0; uint32_t* inb1;       // inbox record lists [L][IC]
@@ -202,30 +205,31 @@ __device__ __forceinline__ uint32_t* narv_at(const CS& S, uint32_t p, size_t l) 
 __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) { return (uint64_t)__shfl((long long)v, src); }
 // lane l's value for a wave-uniform l (v_readlane, no LDS permute)
 __device__ __forceinline__ uint32_t rl32(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
+// wave reductions on the VALU (DPP row shifts, then the row broadcasts; the
+// result read from lane 63 is uniform): no LDS permutes, whose dependent
+// chain of six costs ~300 cycles.  Called by the whole wave.
+template <class Op>
+__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v, uint32_t id, Op op)
 {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, 0x111, 0xf, 0xf, false));   // row_shr:1
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, 0x112, 0xf, 0xf, false));   // row_shr:2
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, 0x114, 0xf, 0xf, false));   // row_shr:4
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, 0x118, 0xf, 0xf, false));   // row_shr:8
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, 0x142, 0xa, 0xf, false));   // row_bcast:15
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, 0x143, 0xc, 0xf, false));   // row_bcast:31
   return v;
 }
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t v)
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += (uint64_t)__shfl_xor((long long)v, o);
-  return v;
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp(v, 0u, [](uint32_t a, uint32_t b) { return a + b; }), 63);
 }
 __device__ __forceinline__ uint32_t wave_min(uint32_t v)
 {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor(v, o));
-  return v;
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp(v, ~0u, [](uint32_t a, uint32_t b) { return a < b ? a : b; }), 63);
 }
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t ln)
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t)
 {
-  uint32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) { const uint32_t y = __shfl_up(x, o); if (ln >= (uint32_t)o) x += y; }
-  return x - v;
+  return wave_scan_dpp(v, 0u, [](uint32_t a, uint32_t b) { return a + b; }) - v;
 }
 // pick the element of a per-thread register array selected by a lane-varying index
 template <int N> __device__ __forceinline__ uint64_t pick(const uint64_t (&a)[N], uint32_t i)
@@ -286,7 +290,8 @@ __device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v)
   return v;
 }
 
-struct Cache {
+template <bool MT>
+struct CacheT {
   uint64_t* tag; uint8_t* meta; uint8_t* rr; uint64_t* cg;
   uint32_t sets, ways, log_line, pol, wb, ln;
   uint32_t cd;                         // this step's counter increments: lane k holds counter k
@@ -401,7 +406,7 @@ struct Cache {
     if (wr) cnt(GG_CC_WRITE_ACCESSES); else cnt(GG_CC_READ_ACCESSES);
     if (miss) {
       cnt(GG_CC_MISSES); if (wr) cnt(GG_CC_WRITE_MISSES); else cnt(GG_CC_READ_MISSES);
-      if (mtab) mt_classify(a, mt_err);
+      if (MT && mtab) mt_classify(a, mt_err);
     }
   }
   // getCacheLineInfo (cache.cc:187-215): state / loc of the line, I / 0 when absent
@@ -430,7 +435,7 @@ struct Cache {
     ld(s, tv, mv);
     const int w = way_of(tv, tag_of(a));
     if (w < 0) return false;
-    if (mtab && st == ST_I) mt_or(a, kMtI, mt_err);                  // cache.cc:228-230
+    if (MT && mtab && st == ST_I) mt_or(a, kMtI, mt_err);                  // cache.cc:228-230
     if ((int)ln == w) {
       st_meta(s, (mv & 0xF8u) | st | (loc << 2));
       if (st == ST_I) st_tag(s, INV_ADDR);
@@ -473,7 +478,7 @@ struct Cache {
     const uint32_t vm = rl32(mv, (uint32_t)w);
     ev = vt != INV_ADDR;
     if (ev) { ev_addr = vt << log_line; ev_st = vm & 3u; ev_loc = (vm >> 2) & 1u; }
-    if (mtab) mt_insert(a, ev, vt << log_line, mt_err);
+    if (MT && mtab) mt_insert(a, ev, vt << log_line, mt_err);
     if ((int)ln == w) {
       const uint32_t nm = (vm & 0xF8u) | st | (loc << 2);
       st_tag(s, tag_of(a));
@@ -516,7 +521,9 @@ using StepLds = StepLdsT<kInLds, kRqLds>;                 // one tile per workgr
 // The lanes of ONE wave exchange data through LDS / global memory between the
 // phases of a tile step; in a multi-wave workgroup the other waves run other
 // tiles, so this is a wave barrier with workgroup-scope fences (every wait a
-// __syncthreads would imply, no s_barrier).
+// __syncthreads would imply, no s_barrier).  With one wave per workgroup
+// (k_c_step, k_c_persist) the compiler emits these as wavefront-scope: no
+// wait for outstanding global accesses.
 __device__ __forceinline__ void tsync()
 {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -584,8 +591,8 @@ struct TilePre {
   uint32_t segx, segy;                   // the tile's X / Y run (hop-by-hop), ~0 otherwise
   __device__ __forceinline__ void load(const CS& S, uint32_t lt, uint32_t ln)
   {
-    tile = S.gtile[lt];
-    segx = S.tseg[(size_t)tile * 2]; segy = S.tseg[(size_t)tile * 2 + 1];
+    const uint4 ti = S.tinfo[lt];
+    tile = ti.x; segx = ti.y; segy = ti.z;
     rec = S.ts[lt].rec; rec_end = S.ts[lt].rec_end; clk = S.ts[lt].clk; pend_start = S.ts[lt].pend_start;
     out_addr = S.ts[lt].out_addr; out_time = S.ts[lt].out_time;
     blocked = S.ts[lt].blocked; seq = S.ts[lt].seq; nrep = S.ts[lt].nrep; nrq = S.ts[lt].nrq;
@@ -599,8 +606,16 @@ struct TilePre {
 // ---------------------------------------------------------------------------
 // one tile's controllers (every lane, identical values)
 // ---------------------------------------------------------------------------
-template <class SL, class H>
+// F: the fast instance (k_c_step<true>, chosen on the host by coh_fast):
+// every queue a step serves — the router ports and the DRAM queue — is a
+// history tree of <= kQMax intervals held in registers (RegQueue), and no
+// cache tracks miss types, so the other queue forms and the miss-type hooks
+// are compiled out of it (a smaller kernel: fewer instruction-cache misses
+// on a tile's path, fewer live values)
+template <class SL, class H, bool F = false>
 struct Tile {
+  static constexpr bool kF = F;
+  using Cache = CacheT<!F>;
   const CP& P; const CS& S;
   uint32_t lt, tile, ln, p;             // local index, tile id, lane, step parity
   SL& sl;
@@ -645,11 +660,11 @@ struct Tile {
       L2 = Cache{S.l2_tag + lt * n2, S.l2_meta + lt * n2, S.l2_rr + (size_t)lt * P.s2,
                  S.cc + ((size_t)lt * 2 + 1) * GG_NUM_CACHE_COUNTERS, P.s2, P.a2, P.log_line, P.pol2, 1, ln, 0, ~0u, 0, 0};
     }
-    if (P.mt1) {
+    if (!F && P.mt1) {
       L1.mtab = S.mtab + ((size_t)lt * 2 << P.mt_log); L1.mtc = S.mtc + (size_t)lt * 2 * GG_NUM_MISS_TYPES;
       L1.mt_log = P.mt_log;
     }
-    if (P.mt2) {
+    if (!F && P.mt2) {
       L2.mtab = S.mtab + (((size_t)lt * 2 + 1) << P.mt_log); L2.mtc = S.mtc + ((size_t)lt * 2 + 1) * GG_NUM_MISS_TYPES;
       L2.mt_log = P.mt_log;
     }
@@ -819,17 +834,55 @@ struct Tile {
     stat(GG_CT_DIR_ACCESSES, 1);
     const uint32_t base = dset(a) * P.dassoc;
     DEnt* d = S.dir + (size_t)lt * P.E;
-    const uint64_t v = ln < P.dassoc ? d[base + ln].addr : 0;
-    const uint64_t hit = __ballot(ln < P.dassoc && v == a);
-    if (hit) return (int32_t)(base + __builtin_ctzll(hit));
-    const uint64_t fr = __ballot(ln < P.dassoc && v == INV_ADDR);
+    // one round of loads: the set's entries (lane = way) and, when they fit
+    // four words per lane, the set's sharer words (word idx = way * W + k in
+    // lane idx & 63 of register idx >> 6): a hit opens its entry (eopen)
+    // without a dependent load
+    const bool spec = P.W * P.dassoc <= 256 && (P.W & (P.W - 1)) == 0;   // (W a power of two: an entry's words never straddle two registers)
+    DEnt e{INV_ADDR, -1, 0, 0};
+    if (ln < P.dassoc) e = d[base + ln];
+    uint64_t sw0 = 0, sw1 = 0, sw2 = 0, sw3 = 0;
+    if (spec) {
+      const uint64_t* g = S.dsh + ((size_t)lt * P.E + base) * P.W;
+      const uint32_t nw = P.W * P.dassoc;
+      if (ln < nw) sw0 = g[ln];
+      if (ln + 64 < nw) sw1 = g[ln + 64];
+      if (ln + 128 < nw) sw2 = g[ln + 128];
+      if (ln + 192 < nw) sw3 = g[ln + 192];
+    }
+    const uint64_t hit = __ballot(ln < P.dassoc && e.addr == a);
+    if (hit) {
+      const uint32_t w = (uint32_t)__builtin_ctzll(hit);
+      const int32_t h = (int32_t)(base + w);
+      if (spec && oh != h) {                       // an open entry is newer than HBM: keep it
+        eclose();
+        oaddr = a;
+        oown = (int32_t)rl32((uint32_t)e.owner, w);
+        ost = rl32((uint32_t)e.dstate, w);
+        onsh = rl32((uint32_t)e.nsh, w);
+        const uint32_t i0 = w * P.W, u = i0 >> 6;                    // the entry's words: one register
+        const uint64_t src = u == 0 ? sw0 : u == 1 ? sw1 : u == 2 ? sw2 : sw3;
+        const uint64_t x = shfl64(src, (int)((i0 + ln) & 63));
+        osh = ln < P.W ? x : 0ull;
+        oh = h; od = false;
+      }
+      return h;
+    }
+    const uint64_t fr = __ballot(ln < P.dassoc && e.addr == INV_ADDR);
     if (fr) {
       // a never-used slot: its sharer words are zeroed here, not at reset
-      // (full-map vectors of every entry are 2 GB at 1024 tiles)
-      const uint32_t i = base + (uint32_t)__builtin_ctzll(fr);
+      // (full-map vectors of every entry are 2 GB at 1024 tiles); opened
+      // with its reset fields (owner -1, UNCACHED, no sharers)
+      const uint32_t w = (uint32_t)__builtin_ctzll(fr);
+      const uint32_t i = base + w;
       if (oh == (int32_t)i) eclose();
       d[i].addr = a;
       if (ln < P.W) shw((int32_t)i)[ln] = 0;
+      if (spec) {
+        eclose();
+        oaddr = a; oown = (int32_t)rl32((uint32_t)e.owner, w); ost = rl32((uint32_t)e.dstate, w);
+        onsh = rl32((uint32_t)e.nsh, w); osh = 0; oh = (int32_t)i; od = false;
+      }
       return (int32_t)i;
     }
     const uint64_t rv = ln < nrep ? rep_ent(ln)->addr : 0;
@@ -919,9 +972,9 @@ struct Tile {
   }
   __device__ __forceinline__ uint32_t qcount(uint64_t a) const
   {
-    uint32_t c = 0;
-    for (uint32_t i = ln; i < nrq; i += 64) c += (rq_addr(i) == a);
-    return wave_sum(c);
+    uint32_t c = 0;                                  // a ballot per 64 entries (no cross-lane reduction)
+    for (uint32_t b = 0; b < nrq; b += 64) c += (uint32_t)__builtin_popcountll(__ballot(b + ln < nrq && rq_addr(b + ln) == a));
+    return c;
   }
   __device__ __forceinline__ int32_t qfront(uint64_t a) const
   {
@@ -986,24 +1039,26 @@ struct Tile {
     if (P.dram_qm) {
       // each side's queue pointers derived where they are used (LDS / HBM):
       // a pointer merged from the two would make every queue access flat
-      if (dq_lds && P.dram_qtype == GG_QM_HISTORY_TREE) {
+      if (F || (dq_lds && P.dram_qtype == GG_QM_HISTORY_TREE)) {
         // a history tree: the image into registers (RegQueue), one request,
         // back to the image — ~3x fewer cycles than the lane-parallel LDS form
         HQueue* lq = reinterpret_cast<HQueue*>(sl.dimg);
         HNode* lnd = reinterpret_cast<HNode*>(sl.dimg + sizeof(HQueue));
         RegQueue rq;
-        rq.load(lq, lnd, P.dram_proc, P.analytical != 0, ln);
+        rq.load_h0(lq, lnd, P.max_list, P.dram_proc, P.analytical != 0, ln);
         qd = rq.request(pkt_ns, P.dram_proc, S.err);
         wave_sync();
         rq.store(lq, lnd);
         wave_sync();
-      } else if (dq_lds) {
-        HTree tr{reinterpret_cast<HQueue*>(sl.dimg), reinterpret_cast<HNode*>(sl.dimg + sizeof(HQueue)), P.dram_proc,
-                 P.analytical != 0};
-        qd = tr.delay_w(pkt_ns, P.dram_proc, S.err, ln);
-      } else {
-        HTree tr{S.dq + lt, S.dnd + (size_t)lt * P.max_list, P.dram_proc, P.analytical != 0};
-        qd = tr.delay(pkt_ns, P.dram_proc, S.err);
+      } else if constexpr (!F) {
+        if (dq_lds) {
+          HTree tr{reinterpret_cast<HQueue*>(sl.dimg), reinterpret_cast<HNode*>(sl.dimg + sizeof(HQueue)), P.dram_proc,
+                   P.analytical != 0};
+          qd = tr.delay_w(pkt_ns, P.dram_proc, S.err, ln);
+        } else {
+          HTree tr{S.dq + lt, S.dnd + (size_t)lt * P.max_list, P.dram_proc, P.analytical != 0};
+          qd = tr.delay(pkt_ns, P.dram_proc, S.err);
+        }
       }
       stat(GG_CT_DRAM_QUEUE_REQUESTS, 1);
     }
@@ -1124,7 +1179,7 @@ struct Tile {
   }
 
   // handleMsgFromL2Cache (:43-96) + processInv/Flush/WbRepFromL2Cache (:410-543)
-  __device__ __forceinline__ void directory_msg(const gg_cmsg& m)
+  __device__ __forceinline__ void directory_msg(const HMsg& m)
   {
     uint64_t t = m.arrival_ps;           // __handleMsgFromNetwork: setCurrTime(packet.time)
     const uint64_t a = m.addr;
@@ -1388,7 +1443,7 @@ struct Tile {
     pend_start = s;
   }
   // L2CacheCntlr::handleMsgFromDramDirectory (l2:294-502) + the core's second attempt
-  __device__ __forceinline__ void l2_msg(const gg_cmsg& m)
+  __device__ __forceinline__ void l2_msg(const HMsg& m)
   {
     uint64_t t = m.arrival_ps;
     const uint64_t a = m.addr;
@@ -1485,9 +1540,9 @@ struct Tile {
 // (P, sender, seq) with P = the largest arrival up to the message in its
 // channel (a head can only leave after its channel's earlier messages, and
 // every head waiting behind a larger arrival inherits it).  a = arrival,
-// k = sender << 32 | seq, idx = record; out = records in processing order.
-__device__ __forceinline__ void order_inbox(uint32_t n, const uint64_t* a, const uint64_t* k, uint64_t* pm, const uint32_t* idx,
-                            uint32_t* out, uint32_t ln)
+// k = sender << 32 | seq; out = local indices in processing order.
+__device__ __forceinline__ void order_inbox(uint32_t n, const uint64_t* a, const uint64_t* k, uint64_t* pm, uint32_t* out,
+                                            uint32_t ln)
 {
   for (uint32_t i = ln; i < n; i += 64) {
     const uint64_t ki = k[i];
@@ -1503,7 +1558,7 @@ __device__ __forceinline__ void order_inbox(uint32_t n, const uint64_t* a, const
     const uint64_t pi = pm[i], ki = k[i];
     uint32_t r = 0;
     for (uint32_t j = 0; j < n; ++j) { const uint64_t pj = pm[j]; r += (pj < pi) || (pj == pi && k[j] < ki); }
-    out[r] = idx[i];
+    out[r] = i;                                   // the local index (its record: idx[i])
   }
   tsync();
 }
@@ -1671,14 +1726,14 @@ __device__ __forceinline__ void quantum_end(const CP& P, const CS& S, uint32_t L
 struct TraceWin { uint64_t wbase, wa; uint32_t wm; };
 constexpr uint64_t kNsFin = ~0ull, kNsBlk = ~0ull - 1;   // next start of a finished / blocked tile
 
-template <bool LC, bool HR, class SL, class H>
+template <bool LC, bool HR, bool F, class SL, class H>
 __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t lt, uint32_t k, uint32_t L, uint64_t barrier,
                                           TraceWin& W, SL& sl, uint8_t* clds, const TilePre& pre, const H& hk,
                                           uint32_t na, uint32_t ni, uint64_t rel);
 
 // LC: cache state in LDS; HR: L1 hit runs (persistent small meshes, where
 // long runs of hits between misses pay for the window look-up)
-template <bool LC, bool HR>
+template <bool LC, bool HR, bool F = false>
 __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, uint32_t devloop, uint64_t barrier_arg,
                                           TraceWin& W)
 {
@@ -1721,7 +1776,7 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
   const GHooks hk{P, S};
   const uint32_t na = P.net == GG_NET_EMESH_HOP_BY_HOP ? (p ? pre.narv1 : pre.narv0) : 0u;
   const uint32_t ni = p ? pre.ninb1 : pre.ninb0;
-  tile_step<LC, HR>(P, S, lt, k, L, barrier, W, sl, smem + P.cache_lds_off, pre, hk, na, ni,
+  tile_step<LC, HR, F>(P, S, lt, k, L, barrier, W, sl, smem + P.cache_lds_off, pre, hk, na, ni,
                     devloop && k == 0 ? qsv[QS_REL] : 0ull);
 }
 
@@ -1743,11 +1798,19 @@ __device__ __forceinline__ void publish_hbh_lds(TT& T, gg_cmsg* cur, uint32_t nl
   const uint64_t qi = (uint64_t)tile * 6 + P_INJ;
   HQueue* gq = S.nq + qi;
   HNode* gnd = S.nnd + qi * P.np.max_size;
-  const bool regq = P.np.qm && P.np.qtype == GG_QM_HISTORY_TREE && P.np.max_size <= kQMax;
-  const bool wave = P.np.qm && P.np.max_size <= kQMax && !regq;
+  constexpr bool F = TT::kF;
+  const bool regq = F ? P.np.qm != 0 : P.np.qm && P.np.qtype == GG_QM_HISTORY_TREE && P.np.max_size <= kQMax;
+  const bool wave = !F && P.np.qm && P.np.max_size <= kQMax && !regq;
   RegQueue rq;
   uint32_t nn = 0;
   bool rq_loaded = false;
+  // The list slots (inbox of the next step for self-sends, the X / Y run
+  // for the rest) do not depend on the port: the slot atomics of the first 64
+  // sends are issued here and their list words stored after the port's
+  // requests, so their round trip overlaps the ordering and the requests
+  // (a list's order is free: the walkers and the inbox order by the keys)
+  uint32_t* late_p = nullptr;
+  uint32_t late_j = ~0u, late_r = 0, late_cap = 0;   // the raw atomic result, checked at the store
   for (uint32_t i0 = 0; i0 < nloc; i0 += 64) {
     const uint32_t i = i0 + ln;
     uint64_t e = 0, ts = 0;
@@ -1755,29 +1818,40 @@ __device__ __forceinline__ void publish_hbh_lds(TT& T, gg_cmsg* cur, uint32_t nl
     if (i < nloc) { e = sl.x3[i]; ts = sl.x4[i]; self = (uint32_t)((e >> 32) & 0x7FFFFFFFu) == tile; net = !self; }
     const uint32_t r = (uint32_t)e;
     if (self) {
-      const uint32_t j = hk.inbox_slot(p ^ 1u, lt);
-      if (j == ~0u) atomicOr(S.err, GG_DERR_CAP);
-      else inb(S, p ^ 1u)[(size_t)lt * P.IC + j] = r;
+      uint32_t* lp = inb(S, p ^ 1u) + (size_t)lt * P.IC;
+      const uint32_t j = atomicAdd(ninb_at(S, p ^ 1u, lt), 1u);     // (hk.inbox_slot, checked at the store)
+      if (i0 == 0) { late_p = lp; late_j = j; late_r = r; late_cap = P.IC; }
+      else if (j >= P.IC) atomicOr(S.err, GG_DERR_CAP);
+      else lp[j] = r;
       ri_self++;
     }
     const uint64_t m = __ballot(net);
-    if (m && regq && !rq_loaded) { rq.load(gq, gnd, 1, P.np.analytical != 0, ln); rq_loaded = true; }
+    if (m && regq && !rq_loaded) { rq.load_h0(gq, gnd, P.np.max_size, 1, P.np.analytical != 0, ln); rq_loaded = true; }
     const uint32_t pos = nn + (uint32_t)__builtin_popcountll(m & ((1ull << ln) - 1));
     if (net) {
       const uint32_t d = (uint32_t)((e >> 32) & 0x7FFFFFFFu), dx = d % P.mw, dy = d / P.mw;
-      const uint32_t seg = cx != dx ? ((T.p0.segx * 2 + (dx > cx ? 1u : 0u)) | 0x80000000u)
-                                    : (T.p0.segy * 2 + (dy > cy ? 1u : 0u));
+      const bool is_x = cx != dx;
+      const uint32_t sg = is_x ? T.p0.segx * 2 + (dx > cx ? 1u : 0u) : T.p0.segy * 2 + (dy > cy ? 1u : 0u);
       const uint64_t hd = e >> 63;
       sl.x1[pos] = ts;
       sl.x2[pos] = ((uint64_t)(seq0 + i) << 1) | hd;      // the sender is this tile: its seq orders equal times
       sl.i1[pos] = r;
-      sl.x4[pos] = seg | (hd << 32);                      // (read above for slot i >= pos, in program order)
+      sl.x4[pos] = hd << 32;                              // (read above for slot i >= pos, in program order)
+      // onto the X (or Y) run the packet enters (hk.seg_slot, checked at the store)
+      const uint32_t j = atomicAdd(&(is_x ? S.nxl : S.nyl)[sg], 1u);
+      uint32_t* lp = (is_x ? S.xl : S.yl) + (size_t)sg * P.seg_cap;
+      if (i0 == 0) { late_p = lp; late_j = j; late_r = r; late_cap = P.seg_cap; }
+      else if (j >= P.seg_cap) atomicOr(S.err, GG_DERR_CAP);
+      else lp[j] = r;
       ri_net++;
     }
     nn += (uint32_t)__builtin_popcountll(m);
   }
   tsync();
-  if (!nn) return;
+  auto late_store = [&]() {                              // the list words of the first 64 sends
+    if (late_p) { if (late_j >= late_cap) atomicOr(S.err, GG_DERR_CAP); else late_p[late_j] = late_r; }
+  };
+  if (!nn) { late_store(); return; }
   if (S.trs) q1 = __builtin_amdgcn_s_memtime();
   order_port_local(nn, sl.x1, sl.x1, sl.x2, sl.i2, ln);
   if (S.trs) q2 = __builtin_amdgcn_s_memtime();
@@ -1809,7 +1883,7 @@ __device__ __forceinline__ void publish_hbh_lds(TT& T, gg_cmsg* cur, uint32_t nl
       uint64_t qd = 0;
       if (P.np.qm) {
         const uint64_t tc = time_to_cycles(rl64(sp, k), P.np.f);
-        qd = regq ? rq.request(tc, nf, S.err) : (wave ? trl.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
+        if constexpr (F) qd = rq.request(tc, nf, S.err); else qd = regq ? rq.request(tc, nf, S.err) : (wave ? trl.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
       }
       if (ln == k) oq = qd;
       fs += nf; bs += (uint32_t)__builtin_amdgcn_readlane((int)bits, (int)k);   // updateSendCounters (network_model.cc:228-251)
@@ -1829,16 +1903,7 @@ __device__ __forceinline__ void publish_hbh_lds(TT& T, gg_cmsg* cur, uint32_t nl
     cadd(S.ctr, tile, GG_NC_PACKETS_SENT, ps); cadd(S.ctr, tile, GG_NC_FLITS_SENT, fs);
     cadd(S.ctr, tile, GG_NC_BITS_SENT, bs);
   }
-  // onto the X (or Y) run the packet enters
-  for (uint32_t i = ln; i < nn; i += 64) {
-    const uint32_t e = sl.i2[i];
-    const uint32_t r = sl.i1[e], seg = (uint32_t)sl.x4[e];
-    const bool is_x = seg >> 31;
-    const uint32_t sg = seg & 0x7FFFFFFFu;
-    const uint32_t j = hk.seg_slot(is_x, sg);
-    if (j == ~0u) { atomicOr(S.err, GG_DERR_CAP); continue; }
-    (is_x ? S.xl : S.yl)[(size_t)sg * P.seg_cap + j] = r;
-  }
+  late_store();
   tsync();
 }
 
@@ -1846,14 +1911,14 @@ __device__ __forceinline__ void publish_hbh_lds(TT& T, gg_cmsg* cur, uint32_t nl
 // the calling wave: the SELF port + receive of the packets that
 // reached the tile (na), the inbox (ni records), the trace, publish, write
 // back.  Deliveries go through the hooks.
-template <bool LC, bool HR, class SL, class H>
+template <bool LC, bool HR, bool F, class SL, class H>
 __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t lt, uint32_t k, uint32_t L, uint64_t barrier,
                                           TraceWin& W, SL& sl, uint8_t* clds, const TilePre& pre, const H& hk,
                                           uint32_t na, uint32_t ni, uint64_t rel)
 {
   const uint32_t ln = lane_id(), p = k & 1u;
   PROF_T0();
-  Tile<SL, H> T(P, S, lt, p, sl, hk, clds, std::integral_constant<bool, LC>(), pre);
+  Tile<SL, H, F> T(P, S, lt, p, sl, hk, clds, std::integral_constant<bool, LC>(), pre);
   T.tr_on = S.trs != nullptr && L < S.tr_n;
   const gg_cmsg* prev = pool(S, p ^ 1u);     // records delivered to this step
   uint64_t* gscr = S.gscr + (size_t)lt * 6 * P.IC;
@@ -1895,6 +1960,8 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
   // inbox keys (new arrival, sender << 32 | seq, record) in LDS, so the inbox
   // is ordered without gathering its records again
   const bool self_keys = ni == 0 && na && na <= SL::kIn;
+  uint64_t h_addr = 0;                           // address and type | requester << 8 of the message at local index lane
+  uint32_t h_tr = 0;
   if (na) {
     if (S.prof || S.trs) _sb = __builtin_amdgcn_s_memtime();
     const uint32_t* al = arv(S, p) + (size_t)lt * P.IC;
@@ -1903,10 +1970,10 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
     const uint64_t qi = (uint64_t)T.tile * 6 + P_SELF;
     HQueue* gq = S.nq + qi;
     HNode* gnd = S.nnd + qi * P.np.max_size;
-    const bool regq = P.np.qm && P.np.qtype == GG_QM_HISTORY_TREE && P.np.max_size <= kQMax;
-    const bool wave = P.np.qm && P.np.max_size <= kQMax && !regq;
+    const bool regq = F ? P.np.qm != 0 : P.np.qm && P.np.qtype == GG_QM_HISTORY_TREE && P.np.max_size <= kQMax;
+    const bool wave = !F && P.np.qm && P.np.max_size <= kQMax && !regq;
     RegQueue rq;
-    if (regq) rq.load(gq, gnd, 1, P.np.analytical != 0, ln);
+    if (regq) rq.load_h0(gq, gnd, P.np.max_size, 1, P.np.analytical != 0, ln);
     const uint64_t zps = lat_to_ps((uint64_t)P.np.router_delay + P.np.link_delay, P.np.f);
     uint64_t cq = 0, cf = 0;                                   // uniform: contention cycles, flits
     uint64_t rf = 0, rb = 0, rl = 0, rc = 0;                   // uniform: received flits, bits, latency, contention
@@ -1934,6 +2001,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
         if (i0 + 64 * u < na) {
           const gg_cmsg& m = prev[rr[u]];
           ta[u] = m.arrival_ps; sa[u] = m.send_ps; za[u] = m.zero_load_ps; sr[u] = m.src; sq[u] = m.seq; ty[u] = m.type;
+          if (u == 0 && i0 == ln) { h_addr = m.addr; h_tr = m.type | (m.requester << 8); }   // the handler's fields
         }
 #pragma unroll
       for (uint32_t u = 0; u < 4; ++u) {
@@ -1979,7 +2047,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
         if (P.np.qm) {
           const uint64_t tc = time_to_cycles(t, P.np.f);
           ntail += tc >= x0;
-          qd = regq ? rq.request(tc, nf, S.err) : (wave ? trl.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
+          if constexpr (F) qd = rq.request(tc, nf, S.err); else qd = regq ? rq.request(tc, nf, S.err) : (wave ? trl.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
         }
         cq += qd; cf += nf;
         // serialization + receive (network_model.cc:118-150), uniform: the
@@ -2056,7 +2124,11 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
       uint32_t sr[4], sq[4];
 #pragma unroll
       for (uint32_t u = 0; u < 4; ++u)
-        if (i0 + 64 * u < n) { const gg_cmsg& m = prev[rr[u]]; ta[u] = m.arrival_ps; sr[u] = m.src; sq[u] = m.seq; }
+        if (i0 + 64 * u < n) {
+          const gg_cmsg& m = prev[rr[u]];
+          ta[u] = m.arrival_ps; sr[u] = m.src; sq[u] = m.seq;
+          if (u == 0 && i0 == ln) { h_addr = m.addr; h_tr = m.type | (m.requester << 8); }   // the handler's fields
+        }
 #pragma unroll
       for (uint32_t u = 0; u < 4; ++u) {
         const uint32_t i = i0 + 64 * u;
@@ -2065,15 +2137,34 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
     }
     tsync();
     hk.clear_inb(p, lt);
-    order_inbox(n, a_, k_, m_, i_, o_, ln);
+    order_inbox(n, a_, k_, m_, o_, ln);
     };
     if (lds) inbox_batch(std::true_type{}); else inbox_batch(std::false_type{});
     const uint32_t* go_ = (const uint32_t*)(gscr + 4 * P.IC);
+    const uint32_t* gi_ = (const uint32_t*)(gscr + 3 * P.IC);
     PROF_AT(_p1b);
     _q1b = _p1b;
     if (S.prof && ln == 0) atomicAdd(&S.prof[9], (unsigned long long)(_p1b - _p1));
     for (uint32_t j = 0; j < n && !T.failed; ++j) {
-      const gg_cmsg m = prev[lds ? sl.i2[j] : go_[j]];
+      // the message: arrival and sender from the ordering arrays, address /
+      // type / requester from the gather's registers (local index < 64: no
+      // reload of the record), else from the record
+      HMsg m;
+      if (lds) {
+        const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane((int)sl.i2[j]);
+        m.arrival_ps = sl.x1[e]; m.src = (uint32_t)(sl.x2[e] >> 32);
+        if (e < 64) {
+          m.addr = rl64(h_addr, e);
+          const uint32_t tr = rl32(h_tr, e);
+          m.type = tr & 0xFFu; m.requester = tr >> 8;
+        } else {
+          const gg_cmsg& g = prev[sl.i1[e]];
+          m.addr = g.addr; m.type = g.type; m.requester = g.requester;
+        }
+      } else {
+        const gg_cmsg& g = prev[gi_[go_[j]]];
+        m.arrival_ps = g.arrival_ps; m.src = g.src; m.addr = g.addr; m.type = g.type; m.requester = g.requester;
+      }
       T.stat(GG_CT_MSGS_RECEIVED, 1);
       const uint64_t h0 = S.trs ? __builtin_amdgcn_s_memtime() : 0;
       const bool dm = to_directory(m.type);
@@ -2220,8 +2311,8 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
         const uint64_t qi = (uint64_t)T.tile * 6 + P_INJ;
         HQueue* gq = S.nq + qi;
         HNode* gnd = S.nnd + qi * P.np.max_size;
-        const bool regq = P.np.qm && P.np.qtype == GG_QM_HISTORY_TREE && P.np.max_size <= kQMax;
-        const bool wave = P.np.qm && P.np.max_size <= kQMax && !regq;
+        const bool regq = F ? P.np.qm != 0 : P.np.qm && P.np.qtype == GG_QM_HISTORY_TREE && P.np.max_size <= kQMax;
+        const bool wave = !F && P.np.qm && P.np.max_size <= kQMax && !regq;
         // the port's queue: tr in HBM, trl the LDS image (one address space each:
         // a pointer merged from the two would make every queue access flat)
         HTree tr{gq, gnd, 1, P.np.analytical != 0};
@@ -2232,7 +2323,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
           tsync();
             }
         RegQueue rq;
-        if (regq) rq.load(gq, gnd, 1, P.np.analytical != 0, ln);
+        if (regq) rq.load_h0(gq, gnd, P.np.max_size, 1, P.np.analytical != 0, ln);
         if (S.trs) { (void)__builtin_amdgcn_readfirstlane((int)rq.a0); _q3 = __builtin_amdgcn_s_memtime(); }
         uint64_t ps = 0, fs = 0, bs = 0;
         for (uint32_t c0 = 0; c0 < nn; c0 += 64) {
@@ -2255,7 +2346,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
             if (P.np.qm) {
               const uint64_t tc = time_to_cycles(rl64(sp, k), P.np.f);
               ntail += tc >= x0;
-              qd = regq ? rq.request(tc, nf, S.err) : (wave ? trl.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
+              if constexpr (F) qd = rq.request(tc, nf, S.err); else qd = regq ? rq.request(tc, nf, S.err) : (wave ? trl.delay_w(tc, nf, S.err, ln) : tr.delay(tc, nf, S.err));
             }
             if (ln == k) oq = qd;
             fs += nf; bs += (uint32_t)__builtin_amdgcn_readlane((int)bits, (int)k);   // updateSendCounters, uniform
@@ -2504,7 +2595,7 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
   RegQueue rq;
   if (direct && wv < npos) {
     const uint64_t qi = (uint64_t)tile_at(dir ? sd.lo + wv : sd.hi - wv) * 6 + port;
-    rq.load(S.nq + qi, S.nnd + qi * P.np.max_size, 1, P.np.analytical != 0, ln);
+    rq.load_h0(S.nq + qi, S.nnd + qi * P.np.max_size, P.np.max_size, 1, P.np.analytical != 0, ln);
   }
   uint8_t* qimg = smem;
   uint64_t* lc = reinterpret_cast<uint64_t*>(smem + (size_t)npos * P.qimg);     // [npos][kNetCtr]
@@ -2996,6 +3087,8 @@ __device__ __forceinline__ void import_one(const CP& P, const CS& S, const gg_cm
 
 // ---- launchers (gg_coh_step.hip, gg_coh_persist.hip, gg_coh_walk.hip) ----
 void launch_step(const CP& P, const CS& S, size_t lds, hipStream_t s, uint32_t L, uint32_t devloop, uint64_t barrier);
+void launch_step_fast(const CP& P, const CS& S, size_t lds, hipStream_t s, uint32_t L, uint32_t devloop, uint64_t barrier);
+hipError_t step_fast_set_lds(size_t lds);
 void launch_persist(bool lc, const CP& P, const CS& S, size_t lds, hipStream_t s, uint32_t L0, uint32_t L1);
 hipError_t step_set_lds(size_t step_lds, size_t persist_lc_lds, size_t persist_lds);
 hipError_t persist_occupancy(bool lc, size_t lds, int* per_cu);

@@ -532,6 +532,15 @@ static gg_status coh_alloc(gg_ctx* ctx)
   // miss-type tracking (default off): one address table per (tile, cache)
   P.mt1 = ctx->cfg.l1i_track_miss_types ? 1u : 0u;
   P.mt2 = ctx->cfg.l2_track_miss_types ? 1u : 0u;
+  {
+    // the fast step instance: every queue it serves a history tree held in
+    // registers (or no queue model), no miss types; GG_COH_NO_FAST=1 forces
+    // the general instance (A/B)
+    const bool rq_net = !P.np.qm || (P.np.qtype == GG_QM_HISTORY_TREE && P.np.max_size <= kQMax);
+    const bool rq_dram = !P.dram_qm || (P.dram_qtype == GG_QM_HISTORY_TREE && P.max_list <= kQMax);
+    const char* nf = getenv("GG_COH_NO_FAST");
+    P.fast = rq_net && rq_dram && !P.mt1 && !P.mt2 && !(nf && atoi(nf)) ? 1u : 0u;
+  }
   if (P.mt1 || P.mt2) {
     const uint32_t lines = ctx->cfg.miss_track_lines ? ctx->cfg.miss_track_lines : 65536u;
     if (lines & (lines - 1) || lines < 64) return gg_fail(GG_ERR_INVALID, "miss_track_lines must be a power of two >= 64");
@@ -588,6 +597,12 @@ static gg_status coh_alloc(gg_ctx* ctx)
   if ((st = dupload(C, &S.segx, segx))) return st;
   if ((st = dupload(C, &S.segy, segy))) return st;
   if ((st = dupload(C, &S.tseg, tseg))) return st;
+  {
+    std::vector<uint4> ti(P.L);
+    for (uint32_t l = 0; l < P.L; ++l)
+      ti[l] = make_uint4(gtile[l], tseg[(size_t)gtile[l] * 2], tseg[(size_t)gtile[l] * 2 + 1], 0u);
+    if ((st = dupload(C, &S.tinfo, ti))) return st;
+  }
   if ((st = dalloc(C, &C->status_dev, 4))) return st;
   if ((st = dalloc(C, &C->ecount_dev, 2 * (uint64_t)P.K + 2))) return st;
   if ((st = dalloc(C, &C->offs_dev, (uint64_t)P.T + 1))) return st;

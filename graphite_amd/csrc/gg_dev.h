@@ -485,6 +485,29 @@ struct RegQueue {
     j = head + ln + 64; if (j >= cap) j -= cap; if (j >= cap) j -= cap;
     if (ln + 64 < sz) { const HNode x = nd[j]; a1 = x.first; b1 = x.second; }
   }
+  // load() with the node loads issued beside the header's instead of behind
+  // it: every store() writes the list back from slot 0 (head 0), so a queue
+  // only ever served through RegQueue (hq_init starts at head 0) has head 0 at
+  // every load, and nodes [0, max_size) are the list in order.  The header is
+  // checked when it arrives: a queue another form left at head != 0 takes the
+  // dependent load().  One memory round trip instead of two.
+  __device__ __forceinline__ void load_h0(const HQueue* q, const HNode* nd, uint32_t max_size, uint64_t mp, bool an,
+                                          uint32_t lane)
+  {
+    HNode x0{0, 0}, x1{0, 0};
+    if (lane < max_size) x0 = nd[lane];
+    if (lane + 64 < max_size) x1 = nd[lane + 64];
+    const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane((int)q->head);
+    if (h != 0) { load(q, nd, mp, an, lane); return; }
+    ln = lane; min_proc = mp; analytical = an; errs = 0; errp = nullptr;
+    sz = (uint32_t)__builtin_amdgcn_readfirstlane((int)q->size);
+    cap = (uint32_t)__builtin_amdgcn_readfirstlane((int)q->max_size);
+    sig_sq = rfl64(q->sig_sq); sig = rfl64(q->sig); nreq = rfl64(q->n); newest = rfl64(q->newest);
+    util = rfl64(q->util); last_req = rfl64(q->last_req); total_req = rfl64(q->total_req); anl = rfl64(q->analytical);
+    const bool v0 = ln < sz, v1 = ln + 64 < sz;
+    a0 = v0 ? x0.first : 0; b0 = v0 ? x0.second : 0;
+    a1 = v1 ? x1.first : 0; b1 = v1 ? x1.second : 0;
+  }
   __device__ __forceinline__ void store(HQueue* q, HNode* nd) const
   {
     if (errs && errp && ln == 0) atomicOr(errp, errs);

@@ -36,6 +36,7 @@ namespace {
 
 constexpr uint32_t kBatchMargin = 3;      // steps launched past the recent quanta's largest (see the round)
 constexpr uint64_t kSlotDefault = 1024;   // records per peer and quantum sent in the fixed round (64 KB)
+static_assert(GG_ROUND_WORDS == kRoundWords, "gg_internal.h kRoundWords");
 
 struct RoundBufs {
   gg_cmsg* send = nullptr; gg_cmsg* recv = nullptr;   // [world][1 + region] each
@@ -44,6 +45,13 @@ struct RoundBufs {
   uint64_t region = 0; int world = 0;
   uint32_t steps_hist[4] = {8, 8, 8, 8};              // steps of the last quanta (the batch predictor)
   uint32_t hist_i = 0;
+  // the round in progress (pack .. unpack / finish)
+  uint32_t rank = 0, per = 0, k0 = 0, nb = 0, attempt = 0;
+  uint64_t q = 0, slot = 0;
+  bool again = false;                                 // unpack said GG_ROUND_AGAIN: the next pack continues q
+  uint32_t herr = 0;                                  // this rank's local failure (its error flag in the words)
+  gg_status est = GG_OK;
+  std::string emsg;
   size_t dv_words() const { return (size_t)(1 + world) * kRoundWords + 2 * (size_t)world; }
 };
 
@@ -60,20 +68,28 @@ void bufs_free(void* p)
   delete b;
 }
 
-gg_status bufs_for(gg_ctx* ctx, RoundBufs*& B, int world, uint64_t region)
+gg_status bufs_for(gg_ctx* ctx, RoundBufs*& B, int world, uint32_t rank, uint64_t region)
 {
   B = static_cast<RoundBufs*>(gg_round_state(ctx));
   if (B && B->world == world && B->region >= region) return GG_OK;
   if (B) bufs_free(B);
   gg_round_state_set(ctx, nullptr, nullptr);
   B = new RoundBufs();
-  B->region = region; B->world = world;
+  B->region = region; B->world = world; B->rank = rank;
   gg_round_state_set(ctx, B, bufs_free);
   const size_t slots = (size_t)world * (region + 1);
   GG_HIP(hipMalloc((void**)&B->send, sizeof(gg_cmsg) * slots));
   GG_HIP(hipMalloc((void**)&B->recv, sizeof(gg_cmsg) * slots));
   GG_HIP(hipMalloc((void**)&B->dv, sizeof(uint64_t) * B->dv_words()));
   GG_HIP(hipHostMalloc((void**)&B->host, sizeof(uint64_t) * B->dv_words()));
+  // test knob: the first batches' step counts per rank ("n0,n1,...", rank r
+  // takes entry r mod the list): a short first batch on one rank makes the
+  // round repeat while the other ranks have finished the quantum
+  if (const char* e = getenv("GG_ROUND_BATCH0")) {
+    std::vector<uint32_t> v;
+    for (const char* c = e; *c;) { v.push_back((uint32_t)strtoul(c, (char**)&c, 10)); if (*c == ',') ++c; else break; }
+    if (!v.empty()) for (uint32_t& x : B->steps_hist) x = std::max<uint32_t>(1, v[(size_t)B->rank % v.size()]);
+  }
   return GG_OK;
 }
 
@@ -84,7 +100,155 @@ uint64_t slot_records(uint64_t region)
   return std::max<uint64_t>(1, std::min(v, region));
 }
 
+RoundBufs* bufs_of(gg_ctx* ctx) { return static_cast<RoundBufs*>(gg_round_state(ctx)); }
+
+void fill_io(const RoundBufs* B, gg_round_io* io)
+{
+  io->send = B->send; io->recv = B->recv;
+  io->words_own = B->dv; io->words_all = B->dv + kRoundWords;
+  io->stride = B->region + 1; io->slot = B->slot;
+  io->send_count = B->host + (size_t)B->world * kRoundWords;
+  io->recv_count = io->send_count + B->world;
+}
+
+// pack with an extra local failure (gg_round_exchange's wrong stream)
+gg_status round_pack(gg_ctx* ctx, uint32_t W, uint32_t R, uint64_t q, gg_round_io* io, gg_status xerr, const char* xmsg)
+{
+  if (!ctx || !io) return gg_fail(GG_ERR_INVALID, "NULL argument");
+  const gg_config& c = ctx->cfg;
+  const uint32_t K = c.num_shards ? c.num_shards : 1;
+  if (W == 0 || R >= W) return gg_fail(GG_ERR_INVALID, "rank %u of %u ranks", R, W);
+  if (K % W) return gg_fail(GG_ERR_INVALID, "%u logical shards do not split over %u ranks", K, W);
+  const uint32_t per = K / W;
+  const uint32_t k1 = c.shard_end ? c.shard_end : K;
+  if (c.shard_begin != R * per || k1 != (R + 1) * per)
+    return gg_fail(GG_ERR_INVALID, "rank %u must own shards [%u, %u), the context owns [%u, %u)", R, R * per,
+                   (R + 1) * per, c.shard_begin, k1);
+  hipSetDevice(ctx->device);
+  // These checks and the first round's buffers fail before anything is
+  // enqueued: they depend only on arguments and on gg_coherent_begin having
+  // run, which every rank of one program gets identically (the send buffer
+  // of the first round is the one rank-local failure that cannot become the
+  // round's error flag: there is no buffer).
+  const uint64_t region = gg_coherent_msg_cap(ctx);
+  if (!region) return gg_fail(GG_ERR_INVALID, "gg_coherent_begin first");
+  RoundBufs* B = nullptr;
+  if (gg_status st = bufs_for(ctx, B, (int)W, R, region)) return st;
+  B->rank = R; B->per = per;
+  if (B->again && B->q == q) { B->k0 += B->nb; ++B->attempt; }
+  else { B->k0 = 0; B->attempt = 0; B->herr = 0; B->est = GG_OK; B->emsg.clear(); }
+  B->again = false; B->q = q;
+  B->slot = slot_records(region);
+  // the batch: the largest of the last four quanta's steps + 3, doubling on a
+  // repeat.  A step past the quantum's end costs three empty launches (~8
+  // µs), a short batch a whole repeated round (~40 µs): margins 0 / 1 / 2 / 3
+  // measured 62 / 44 / 45 / 35 µs per quantum (bench exchange, one rank)
+  uint32_t nb = 0;
+  for (uint32_t x : B->steps_hist) nb = std::max(nb, x);
+  B->nb = std::min<uint32_t>(256, (nb + kBatchMargin) << std::min<uint32_t>(B->attempt, 4));
+  if (xerr && !B->herr) { B->herr = GG_DERR_STATE; B->est = gg_fail(xerr, "%s", xmsg); B->emsg = gg_last_error(); }
+  if (!B->herr) {
+    if (gg_status st = gg_coh_steps_async(ctx, q, B->k0, B->nb)) { B->herr = GG_DERR_STATE; B->est = st; B->emsg = gg_last_error(); }
+  }
+  if (gg_status st = gg_coh_round_tail(ctx, B->send, W, per, region, B->herr, B->dv)) {
+    // the tail did not run: the words say so (best effort), the transport still runs
+    if (!B->herr) { B->herr = GG_DERR_STATE; B->est = st; B->emsg = gg_last_error(); }
+    std::vector<uint64_t> w(kRoundWords, 0);
+    w[3] = GG_DERR_STATE;
+    hipMemcpyAsync(B->dv, w.data(), sizeof(uint64_t) * kRoundWords, hipMemcpyHostToDevice, ctx->last_stream);
+    for (uint32_t r = 0; r < W; ++r)
+      hipMemsetAsync(B->send + (size_t)r * (region + 1), 0, sizeof(gg_cmsg), ctx->last_stream);
+  }
+  fill_io(B, io);
+  io->state = GG_ROUND_AGAIN;
+  return GG_OK;
+}
+
+// the quantum's end after every slot is in: the reduced words decide
+gg_status round_decide(gg_ctx* ctx, RoundBufs* B, gg_round_io* io)
+{
+  const uint64_t* h = B->host;
+  const int W = B->world;
+  uint64_t msgs = 0, active = 0, blocked = 0, mn = ~0ull;
+  for (int r = 0; r < W; ++r) {
+    const uint64_t* w = h + (size_t)r * kRoundWords;
+    msgs += w[0]; active += w[1]; blocked += w[2]; mn = std::min(mn, w[5]);
+  }
+  const uint64_t q = B->q;
+  const uint64_t qps = (uint64_t)ctx->cfg.quantum_ns * 1000ull;
+  io->state = GG_ROUND_DONE;
+  io->done = 0;
+  if (active == 0 && msgs == 0) { io->done = 1; io->next_q = q; return gg_coh_check(ctx); }
+  if (msgs == 0 && blocked != 0) return gg_fail(GG_ERR_STATE, "coherent run deadlocked: tiles blocked with no message in flight");
+  io->next_q = (msgs == 0) ? std::max<uint64_t>(q + 1, mn / qps) : q + 1;
+  return GG_OK;
+}
+
 }  // namespace
+
+gg_status gg_round_pack(gg_ctx* ctx, uint32_t world, uint32_t rank, uint64_t q, gg_round_io* io)
+{
+  return round_pack(ctx, world, rank, q, io, GG_OK, "");
+}
+
+gg_status gg_round_unpack(gg_ctx* ctx, gg_round_io* io)
+{
+  if (!ctx || !io) return gg_fail(GG_ERR_INVALID, "NULL argument");
+  RoundBufs* B = bufs_of(ctx);
+  if (!B || !ctx->coh) return gg_fail(GG_ERR_INVALID, "gg_round_pack first");
+  hipSetDevice(ctx->device);
+  hipStream_t s = ctx->last_stream;
+  const int W = B->world;
+  uint64_t* dv_all = B->dv + kRoundWords;
+  uint64_t* counts = B->dv + (size_t)(1 + W) * kRoundWords;
+  // commit + import (nothing unless every rank's words are clean), then the
+  // words to the host; a local failure here still copies the words, so this
+  // rank decides like the others and reports its own error on top
+  gg_status lerr = gg_coh_round_import(ctx, B->q, B->send, B->recv, (uint32_t)W, B->rank, B->region, B->slot, dv_all, counts);
+  std::string lmsg = lerr ? gg_last_error() : "";
+  GG_HIP(hipMemcpyAsync(B->host, dv_all, sizeof(uint64_t) * ((size_t)W * kRoundWords + 2 * (size_t)W),
+                        hipMemcpyDeviceToHost, s));
+  GG_HIP(hipStreamSynchronize(s));
+  gg_coh_harvest(ctx);
+  fill_io(B, io);
+  const uint64_t* h = B->host;
+  uint64_t err = 0, notdone = 0, mx = 0;
+  for (int r = 0; r < W; ++r) {
+    err |= h[r * kRoundWords + 3]; notdone |= h[r * kRoundWords + 6]; mx = std::max(mx, h[r * kRoundWords + 4]);
+  }
+  if (err) {
+    io->state = GG_ROUND_DONE;
+    if (B->herr) return gg_fail(B->est ? B->est : GG_ERR_STATE, "%s", B->emsg.c_str());
+    if (gg_status st = gg_coh_check(ctx)) return st;
+    return gg_fail(GG_ERR_STATE, "quantum %llu failed on another rank", (unsigned long long)B->q);
+  }
+  if (lerr) { io->state = GG_ROUND_DONE; return gg_fail(lerr, "%s", lmsg.c_str()); }
+  if (notdone) { B->again = true; io->state = GG_ROUND_AGAIN; return GG_OK; }   // some rank's quantum is still running
+  B->steps_hist[B->hist_i++ & 3] = (uint32_t)std::max<uint64_t>(1, h[(size_t)B->rank * kRoundWords + 7]);
+  if (mx > B->slot) {
+    // a slot overflowed somewhere: every rank takes the sized round (the
+    // counts are known on both sides now); the own slot's tail is a local copy
+    const uint64_t* sc = h + (size_t)W * kRoundWords;
+    const size_t o = (size_t)B->rank * (B->region + 1);
+    GG_HIP(hipMemcpyAsync(B->recv + o, B->send + o, sizeof(gg_cmsg) * (1 + std::max(sc[B->rank], B->slot)),
+                          hipMemcpyDeviceToDevice, s));
+    io->state = GG_ROUND_OVERFLOW;
+    return GG_OK;
+  }
+  return round_decide(ctx, B, io);
+}
+
+gg_status gg_round_finish(gg_ctx* ctx, gg_round_io* io)
+{
+  if (!ctx || !io) return gg_fail(GG_ERR_INVALID, "NULL argument");
+  RoundBufs* B = bufs_of(ctx);
+  if (!B || !ctx->coh) return gg_fail(GG_ERR_INVALID, "gg_round_pack first");
+  hipSetDevice(ctx->device);
+  if (gg_status st = gg_coh_import_slots(ctx, B->recv, (uint32_t)B->world, B->region, B->slot, B->region, false, nullptr))
+    return st;
+  GG_HIP(hipStreamSynchronize(ctx->last_stream));
+  return round_decide(ctx, B, io);
+}
 
 gg_status gg_round_exchange(gg_ctx* ctx, void* nccl_comm, void* stream, uint64_t q, uint64_t* next_q, int* done)
 {
@@ -93,118 +257,51 @@ gg_status gg_round_exchange(gg_ctx* ctx, void* nccl_comm, void* stream, uint64_t
   int W = 0, R = 0;
   GG_NCCL(ncclCommCount(comm, &W));
   GG_NCCL(ncclCommUserRank(comm, &R));
-  const gg_config& c = ctx->cfg;
-  const uint32_t K = c.num_shards ? c.num_shards : 1;
-  if (K % (uint32_t)W) return gg_fail(GG_ERR_INVALID, "%u logical shards do not split over %d ranks", K, W);
-  const uint32_t per = K / (uint32_t)W;
-  const uint32_t k1 = c.shard_end ? c.shard_end : K;
-  if (c.shard_begin != (uint32_t)R * per || k1 != ((uint32_t)R + 1) * per)
-    return gg_fail(GG_ERR_INVALID, "rank %d must own shards [%u, %u), the context owns [%u, %u)", R, R * per,
-                   (R + 1) * per, c.shard_begin, k1);
-  hipSetDevice(ctx->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  // The checks above and these two return before any RCCL call: they depend
-  // only on arguments and on gg_coherent_begin having run, which every rank of
-  // one program gets identically, so they fail on every rank at once (the
-  // send-buffer allocation of the first round is the one rank-local failure
-  // that cannot be turned into the round's error flag: there is no buffer).
-  const uint64_t region = gg_coherent_msg_cap(ctx);
-  if (!region) return gg_fail(GG_ERR_INVALID, "gg_coherent_begin first");
-  RoundBufs* B = nullptr;
-  if (gg_status st = bufs_for(ctx, B, W, region)) return st;
-  const uint64_t slot = slot_records(region);
-  const size_t sbytes = sizeof(gg_cmsg) * (slot + 1);
-
-  // the quantum's steps, tail, RCCL, commit + import and the words' copy, one
-  // sync per attempt; a failure (a wrong stream included) turns into the
-  // error flag of the round, which every rank still takes part in
-  const bool wrong_stream = s != ctx->last_stream;        // the context's kernels run on last_stream
-  uint64_t* dv_own = B->dv;
-  uint64_t* dv_all = B->dv + kRoundWords;
-  uint64_t* counts = B->dv + (size_t)(1 + W) * kRoundWords;
-  const uint64_t* h = B->host;
-  uint32_t k0 = 0;
-  for (int attempt = 0;; ++attempt) {
-    uint32_t herr = 0;
-    std::string emsg;
-    gg_status est = GG_OK;
-    if (wrong_stream) est = gg_fail(GG_ERR_INVALID, "gg_round_exchange needs the stream of gg_coherent_begin");
-    // the batch: the largest of the last four quanta's steps + 3, doubling on a
-    // repeat.  A step past the quantum's end costs three empty launches (~8
-    // µs), a short batch a whole repeated round (~40 µs): margins 0 / 1 / 2 / 3
-    // measured 62 / 44 / 45 / 35 µs per quantum (bench exchange, one rank)
-    uint32_t nb = 0;
-    for (uint32_t x : B->steps_hist) nb = std::max(nb, x);
-    nb = std::min<uint32_t>(256, (nb + kBatchMargin) << std::min(attempt, 4));
-    if (!est) est = gg_coh_steps_async(ctx, q, k0, nb);
-    if (est) { herr = GG_DERR_STATE; emsg = gg_last_error(); }
-    if (gg_status st = gg_coh_round_tail(ctx, B->send, (uint32_t)W, per, region, herr, dv_own)) return st;
+  // the context's kernels run on last_stream; RCCL on `stream`.  A different
+  // stream is a local failure: it becomes the round's error flag, and the
+  // transport is still posted so that no peer is left blocked inside RCCL
+  const bool wrong_stream = s != ctx->last_stream;
+  gg_round_io io{};
+  for (;;) {
+    if (gg_status st = round_pack(ctx, (uint32_t)W, (uint32_t)R, q, &io, wrong_stream ? GG_ERR_INVALID : GG_OK,
+                                  "gg_round_exchange needs the stream of gg_coherent_begin"))
+      return st;
     if (wrong_stream) GG_HIP(hipStreamSynchronize(ctx->last_stream));   // the slots and words before RCCL reads them on s
+    const size_t sbytes = sizeof(gg_cmsg) * (io.slot + 1);
     if (W > 1) {                                           // the peers' slots (the own one is imported in place)
       GG_NCCL(ncclGroupStart());
       for (int r = 0; r < W; ++r) {
         if (r == R) continue;
-        GG_NCCL(ncclSend(B->send + (size_t)r * (region + 1), sbytes, ncclUint8, r, comm, s));
-        GG_NCCL(ncclRecv(B->recv + (size_t)r * (region + 1), sbytes, ncclUint8, r, comm, s));
+        GG_NCCL(ncclSend(io.send + (size_t)r * io.stride, sbytes, ncclUint8, r, comm, s));
+        GG_NCCL(ncclRecv(io.recv + (size_t)r * io.stride, sbytes, ncclUint8, r, comm, s));
       }
       GG_NCCL(ncclGroupEnd());
     }
-    GG_NCCL(ncclAllGather(dv_own, dv_all, kRoundWords, ncclUint64, comm, s));
-    if (wrong_stream) {                                    // this rank failed: nothing to import
-      GG_HIP(hipStreamSynchronize(s));
-      return gg_fail(est, "%s", emsg.c_str());
-    }
-    if (gg_status st = gg_coh_round_import(ctx, q, B->send, B->recv, (uint32_t)W, (uint32_t)R, region, slot, dv_all, counts))
-      return st;
-    GG_HIP(hipMemcpyAsync(B->host, dv_all, sizeof(uint64_t) * ((size_t)W * kRoundWords + 2 * (size_t)W),
-                          hipMemcpyDeviceToHost, s));
-    GG_HIP(hipStreamSynchronize(s));
-    gg_coh_harvest(ctx);
-    uint64_t err = 0, notdone = 0;
-    for (int r = 0; r < W; ++r) { err |= h[r * kRoundWords + 3]; notdone |= h[r * kRoundWords + 6]; }
-    if (err) {
-      if (herr) return gg_fail(est ? est : GG_ERR_STATE, "%s", emsg.c_str());
-      if (gg_status st = gg_coh_check(ctx)) return st;
-      return gg_fail(GG_ERR_STATE, "quantum %llu failed on another rank", (unsigned long long)q);
-    }
-    if (notdone) { k0 += nb; continue; }                  // some rank's quantum is still running
+    GG_NCCL(ncclAllGather(io.words_own, io.words_all, kRoundWords, ncclUint64, comm, s));
+    if (wrong_stream) GG_HIP(hipStreamSynchronize(s));     // RCCL's writes before the unpack reads them on last_stream
+    if (gg_status st = gg_round_unpack(ctx, &io)) return st;
+    if (io.state == GG_ROUND_AGAIN) continue;
     break;
   }
-  // the reduced words: sent, active, blocked (sums), largest slot count (max),
-  // least next start (min), the quantum's steps on this rank
-  uint64_t msgs = 0, active = 0, blocked = 0, mx = 0, mn = ~0ull;
-  for (int r = 0; r < W; ++r) {
-    const uint64_t* w = h + (size_t)r * kRoundWords;
-    msgs += w[0]; active += w[1]; blocked += w[2]; mx = std::max(mx, w[4]); mn = std::min(mn, w[5]);
-  }
-  B->steps_hist[B->hist_i++ & 3] = (uint32_t)std::max<uint64_t>(1, h[(size_t)R * kRoundWords + 7]);
-  // a slot overflowed somewhere: every rank takes the sized round (the counts are known on both sides now)
-  if (mx > slot) {
-    const uint64_t* sc = h + (size_t)W * kRoundWords;
-    const uint64_t* rc = sc + W;
-    {                                                      // the own slot's tail: a local copy into the receive slot
-      const size_t o = (size_t)R * (region + 1);
-      GG_HIP(hipMemcpyAsync(B->recv + o, B->send + o, sizeof(gg_cmsg) * (1 + std::max(sc[R], slot)),
-                            hipMemcpyDeviceToDevice, s));
-    }
+  if (io.state == GG_ROUND_OVERFLOW) {
+    const uint64_t* sc = io.send_count;
+    const uint64_t* rc = io.recv_count;
     if (W > 1) {
       GG_NCCL(ncclGroupStart());
       for (int r = 0; r < W; ++r) {
         if (r == R) continue;
-        const size_t o = (size_t)r * (region + 1) + 1 + slot;
-        if (sc[r] > slot) GG_NCCL(ncclSend(B->send + o, sizeof(gg_cmsg) * (sc[r] - slot), ncclUint8, r, comm, s));
-        if (rc[r] > slot) GG_NCCL(ncclRecv(B->recv + o, sizeof(gg_cmsg) * (rc[r] - slot), ncclUint8, r, comm, s));
+        const size_t o = (size_t)r * io.stride + 1 + io.slot;
+        if (sc[r] > io.slot) GG_NCCL(ncclSend(io.send + o, sizeof(gg_cmsg) * (sc[r] - io.slot), ncclUint8, r, comm, s));
+        if (rc[r] > io.slot) GG_NCCL(ncclRecv(io.recv + o, sizeof(gg_cmsg) * (rc[r] - io.slot), ncclUint8, r, comm, s));
       }
       GG_NCCL(ncclGroupEnd());
     }
-    if (gg_status st = gg_coh_import_slots(ctx, B->recv, (uint32_t)W, region, slot, region, false, nullptr)) return st;
-    GG_HIP(hipStreamSynchronize(s));
+    if (wrong_stream) GG_HIP(hipStreamSynchronize(s));
+    if (gg_status st = gg_round_finish(ctx, &io)) return st;
   }
-  const uint64_t qps = (uint64_t)c.quantum_ns * 1000ull;
-  *done = 0;
-  if (active == 0 && msgs == 0) { *done = 1; *next_q = q; return gg_coh_check(ctx); }
-  if (msgs == 0 && blocked != 0) return gg_fail(GG_ERR_STATE, "coherent run deadlocked: tiles blocked with no message in flight");
-  *next_q = (msgs == 0) ? std::max<uint64_t>(q + 1, mn / qps) : q + 1;
+  *next_q = io.next_q;
+  *done = io.done;
   return GG_OK;
 }
 

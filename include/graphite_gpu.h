@@ -461,6 +461,49 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* trace, uint64_t* access_o
 gg_status gg_round_exchange(gg_ctx* ctx, void* nccl_comm, void* stream, uint64_t q, uint64_t* next_q, int* done);
 gg_status gg_coherent_run_ranks(gg_ctx* ctx, void* nccl_comm, const gg_trace* trace, uint64_t* access_out_dev,
                                 void* stream);
+/* The round of gg_round_exchange split at its transport, for a caller that
+ * moves the bytes itself (another transport, or several contexts on one GPU
+ * with device copies).  gg_round_exchange is exactly: pack -> transport ->
+ * unpack, again while unpack says GG_ROUND_AGAIN, and on GG_ROUND_OVERFLOW a
+ * second transport of the remainder -> gg_round_finish.
+ *   gg_round_pack: quantum q's steps (a batch sized from the quanta before,
+ *     doubled on each repeat) and the tail kernel: the held cross-rank
+ *     records into per-peer send slots and this rank's status words; enqueued
+ *     on the context's stream (gg_coherent_begin's), not synced.  Fills io.
+ *     The checks of world / rank / shard ownership fail before anything is
+ *     enqueued (they fail alike on every rank); a failure of the steps or the
+ *     tail becomes the error flag of this rank's status words instead, so the
+ *     transport still runs and every rank's unpack returns the error.
+ *   transport 1: once the context's stream has finished the pack, for every
+ *     r != rank: records [0, 1 + slot) of send + r * stride into rank r's
+ *     recv + rank * stride; and words_own into words_all + rank *
+ *     GG_ROUND_WORDS of every rank (this rank's too: an all-gather).
+ *   gg_round_unpack: commit + import on the stream, the gathered words to the
+ *     host, one sync; io->state = GG_ROUND_AGAIN (some rank's quantum had not
+ *     finished: pack again with the same q), GG_ROUND_OVERFLOW (a slot held
+ *     more than `slot` records: send_count[r] / recv_count[r] records are in
+ *     send slot r / receive slot r; transport 2 moves records [1 + slot,
+ *     1 + send_count[r]) of send slot r into rank r's receive slot `rank`,
+ *     then gg_round_finish) or GG_ROUND_DONE (next_q / done as in
+ *     gg_round_exchange).  Record 0 of a slot is a header whose addr is the
+ *     slot's record count.                                                   */
+enum { GG_ROUND_WORDS = 8, GG_ROUND_DONE = 0, GG_ROUND_AGAIN = 1, GG_ROUND_OVERFLOW = 2 };
+typedef struct {
+  gg_cmsg* send;                 /* device: [world][stride] records, the slots this rank sends */
+  gg_cmsg* recv;                 /* device: [world][stride] records, the slots this rank receives */
+  uint64_t* words_own;           /* device: [GG_ROUND_WORDS] this rank's status words */
+  uint64_t* words_all;           /* device: [world][GG_ROUND_WORDS] every rank's (the all-gather's target) */
+  uint64_t stride;               /* records per slot region (1 + capacity) */
+  uint64_t slot;                 /* records of transport 1 per slot, header excluded */
+  const uint64_t* send_count;    /* host [world]: records in send slot r (GG_ROUND_OVERFLOW) */
+  const uint64_t* recv_count;    /* host [world]: records in receive slot r (GG_ROUND_OVERFLOW) */
+  uint64_t next_q;               /* GG_ROUND_DONE: the quantum every rank runs next */
+  int done;                      /* GG_ROUND_DONE: 1 when the run is over */
+  int state;                     /* GG_ROUND_* after unpack / finish */
+} gg_round_io;
+gg_status gg_round_pack(gg_ctx* ctx, uint32_t world, uint32_t rank, uint64_t q, gg_round_io* io);
+gg_status gg_round_unpack(gg_ctx* ctx, gg_round_io* io);
+gg_status gg_round_finish(gg_ctx* ctx, gg_round_io* io);
 /* tile_stats: [tiles][GG_NUM_TILE_STATS]; cache: [tiles][2][GG_NUM_CACHE_COUNTERS]
  * (either may be NULL); run_info: [GG_NUM_RUN_INFO] (may be NULL).  Tiles a
  * context does not own read 0.  Network counters: gg_noc_get_counters.      */

@@ -1,0 +1,14 @@
+#!/bin/bash
+# A/B of library variants on the headline (tools/coh_bench.py, warm run, no
+# oracle): VARIANTS="base variants/x/libgraphite_gpu.so ..." (base = the tree's build)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+OUT=${OUT:-gpurun_out/r05/ab}
+mkdir -p $OUT
+for rep in 1 2; do
+  for v in ${VARIANTS:-base}; do
+    if [ "$v" = base ]; then lib=""; else lib=$v; fi
+    GG_LIB=$lib timeout -k 10 300 python -u tools/coh_bench.py 1024 256 8 256 --hbh --warm --no-oracle $BENCH_ARGS > $OUT/ab.log 2>&1 || { tail $OUT/ab.log; exit 1; }
+    echo "$v: $(grep gpu $OUT/ab.log)"
+  done
+done
