@@ -51,11 +51,53 @@
 #include "directory_entry.h"
 #include "directory_entry_limitless.h"
 #include "network.h"
+#ifdef GG_PROTO_MOSI
+// pr_l1_pr_l2_dram_directory_mosi (coh_harness_mosi): the protocol's event
+// counters are private members of DramDirectoryCntlr / L2CacheCntlr; the
+// harness reads them after the run (access widened for this translation unit
+// only: the reference objects are compiled as they are)
+#include <fstream>
+#include <iostream>
+#include <sstream>
+#define private public
+#define protected public
+#include "pr_l1_pr_l2_dram_directory_mosi/memory_manager.h"
+#undef private
+#undef protected
+#else
 #include "pr_l1_pr_l2_dram_directory_msi/memory_manager.h"
+#endif
 #include "ref_htree.h"
 
 using namespace std;
+#ifdef GG_PROTO_MOSI
+namespace MSI = PrL1PrL2DramDirectoryMOSI;     // (the glue below is written once for both protocols)
+// DirectoryEntryFullMap::getOneSharer draws from a drand48 stream the entry
+// seeds with time(NULL) (misc/random.h:14-18): the canonical schedule fixes
+// that seed (GG_MOSI_RNG_SEED, include/graphite_gpu.h), so every entry starts
+// from the same drand48 state, as entries created in the same second do
+extern "C" time_t time(time_t* t) { if (t) *t = (time_t)1; return (time_t)1; }
+#else
 namespace MSI = PrL1PrL2DramDirectoryMSI;
+#endif
+
+// message types in the backend's numbering (GG_MSG_*, include/graphite_gpu.h):
+// the MSI enum is that numbering; MOSI's inserts INV_FLUSH_COMBINED_REQ after WB_REQ
+static UInt32 gg_type(UInt32 t)
+{
+#ifdef GG_PROTO_MOSI
+  switch (t) {
+  case MSI::ShmemMsg::EX_REQ: return 1; case MSI::ShmemMsg::SH_REQ: return 2; case MSI::ShmemMsg::INV_REQ: return 3;
+  case MSI::ShmemMsg::FLUSH_REQ: return 4; case MSI::ShmemMsg::WB_REQ: return 5; case MSI::ShmemMsg::EX_REP: return 6;
+  case MSI::ShmemMsg::SH_REP: return 7; case MSI::ShmemMsg::UPGRADE_REP: return 8; case MSI::ShmemMsg::INV_REP: return 9;
+  case MSI::ShmemMsg::FLUSH_REP: return 10; case MSI::ShmemMsg::WB_REP: return 11; case MSI::ShmemMsg::NULLIFY_REQ: return 12;
+  case MSI::ShmemMsg::INV_FLUSH_COMBINED_REQ: return 13;
+  default: CHECK(0); return 0;
+  }
+#else
+  return t;
+#endif
+}
 
 // ===========================================================================
 // harness configuration and per-tile harness state
@@ -72,7 +114,7 @@ static HCfg H;
 
 enum { NC_PS = 0, NC_PR, NC_LAT, NC_N };        // packets sent, received, total latency (ps)
 enum { S_CLOCK = 0, S_ACC, S_L1H, S_L2H, S_MISS, S_LAT, S_DACC, S_DEV, S_DBI, S_DRAM, S_DRAMLAT, S_DRAMQD,
-       S_DRAMQR, S_DRAMQA, S_SENT, S_RECV, S_BYTYPE, S_DRAMQU = S_BYTYPE + 11, S_DRAMQL, S_N = 32 };
+       S_DRAMQR, S_DRAMQA, S_SENT, S_RECV, S_BYTYPE, S_DRAMQU = S_BYTYPE + 11, S_DRAMQL, S_SENT_IFC = 29, S_N = 32 };
 
 struct HMsg {
   UInt32 src, dst, seq, type;
@@ -457,7 +499,12 @@ NetPacket::NetPacket() : time(0), type(INVALID_PACKET_TYPE), sender(INVALID_CORE
 // ===========================================================================
 // MemoryManager (memory_manager.cc) and the MSI MemoryManager (…msi/memory_manager.cc)
 // ===========================================================================
+#ifdef GG_PROTO_MOSI
+CachingProtocolType MemoryManager::_caching_protocol_type = PR_L1_PR_L2_DRAM_DIRECTORY_MOSI;
+ofstream MSI::MemoryManager::_cache_line_replication_file;
+#else
 CachingProtocolType MemoryManager::_caching_protocol_type = PR_L1_PR_L2_DRAM_DIRECTORY_MSI;
+#endif
 MemoryManager::MemoryManager(Tile* tile) : _tile(tile), _network(NULL), _enabled(false)
 {
   _shmem_perf_model = new ShmemPerfModel();
@@ -514,8 +561,13 @@ MSI::MemoryManager::MemoryManager(Tile* tile) : ::MemoryManager(tile), _dram_dir
   _dram_cntlr = new DramCntlr(tile, (float)g_dram_cost, g_dram_bw, true, "history_tree", 64);
   char ent[32], acc[8] = "auto";
   if (H.dir_entries) snprintf(ent, sizeof(ent), "%u", H.dir_entries); else snprintf(ent, sizeof(ent), "auto");
+#ifdef GG_PROTO_MOSI
+  _dram_directory_cntlr = new DramDirectoryCntlr(this, _dram_cntlr, ent, H.dir_assoc, 64,
+                                                 Config::getSingleton()->getTotalTiles(), 64, "full_map", H.T, acc);
+#else
   _dram_directory_cntlr = new DramDirectoryCntlr(this, _dram_cntlr, ent, H.dir_assoc, 64,
                                                  Config::getSingleton()->getTotalTiles(), 64, "full_map", acc, H.T);
+#endif
   _dram_directory_home_lookup = new AddressHomeLookup(ceilLog2(64), ctrl, 64);
   _L1_cache_cntlr = new L1CacheCntlr(this, 64, 16, 4, 1, "lru", 1, 1, "parallel", false,
                                      32, 4, 1, "lru", 1, 1, "parallel", false);
@@ -525,8 +577,12 @@ MSI::MemoryManager::MemoryManager(Tile* tile) : ::MemoryManager(tile), _dram_dir
 }
 MSI::MemoryManager::~MemoryManager() {}
 void MSI::MemoryManager::enableModels()                                    // …msi/memory_manager.cc:382-396
-{
+{                                                                           // (…mosi/memory_manager.cc:373-390)
   getL1ICache()->enable(); getL1DCache()->enable(); getL2Cache()->enable();
+#ifdef GG_PROTO_MOSI
+  _L2_cache_cntlr->enable();
+  _dram_directory_cntlr->enable();
+#endif
   _dram_directory_cntlr->getDramDirectoryCache()->enable();
   g_dram[_dram_cntlr].enabled = true;
   ::MemoryManager::enableModels();
@@ -590,13 +646,14 @@ void MSI::MemoryManager::sendMsg(tile_id_t receiver, ShmemMsg& msg)
   }
   HTile& S = g_t[src];
   HMsg m;
-  m.src = src; m.dst = (UInt32)receiver; m.seq = S.seq++; m.type = msg.getType();
+  m.src = src; m.dst = (UInt32)receiver; m.seq = S.seq++; m.type = gg_type(msg.getType());
   m.send = t.getTime(); m.arrival = m.send;
   m.buf.assign(buf, buf + msg.getMsgLen());
   delete[] buf;
   g_step.push_back(m);
   S.st[S_SENT]++;
-  S.st[S_BYTYPE + m.type - 1]++;
+  if (m.type == 13) S.st[S_SENT_IFC]++;                                      // INV_FLUSH_COMBINED_REQ (MOSI)
+  else S.st[S_BYTYPE + m.type - 1]++;
 }
 void MSI::MemoryManager::broadcastMsg(ShmemMsg&) { CHECK(0); }   // full_map never broadcasts
 
@@ -610,12 +667,11 @@ Tile::~Tile() { delete _memory_manager; }
 // ===========================================================================
 // the canonical schedule
 // ===========================================================================
-static UInt32 modeled_bits(UInt32 type)        // network_model.cc:185-200 + shmem_msg.cc:100-125
+static UInt32 modeled_bits(UInt32 type)        // network_model.cc:185-200 + shmem_msg.cc:100-125 (…mosi/shmem_msg.cc:122-151)
 {
   UInt32 idb = H.T > 1 ? ceilLog2(H.T) : 0;
-  bool data = type == MSI::ShmemMsg::EX_REP || type == MSI::ShmemMsg::SH_REP || type == MSI::ShmemMsg::FLUSH_REP ||
-              type == MSI::ShmemMsg::WB_REP;
-  return 2 * idb + 4 + 48 + (data ? 512 : 0);
+  bool data = type == 6 || type == 7 || type == 10 || type == 11;            // EX_REP, SH_REP, FLUSH_REP, WB_REP
+  return 2 * idb + 4 + 48 + (data ? 512 : 0) + (type == 13 ? idb : 0);   // INV_FLUSH_COMBINED_REQ: + single receiver
 }
 static UInt64 lat_ps(UInt64 cycles) { return (UInt64)ceil(((double)1000 * cycles) / 1.0); }
 // emesh_hop_counter (network_model_emesh_hop_counter.cc:143-157) / magic + serialization (network_model.cc:142-150)
@@ -889,6 +945,43 @@ static void run_case(FILE* man, bool first, const char* name, UInt32 T, UInt32 N
   write_bin("coh_" + n + "_stats.u64", &st[0], st.size() * 8);
   write_bin("coh_" + n + "_cache.u64", &cc[0], cc.size() * 8);
   write_bin("coh_" + n + "_net.u64", &nc[0], nc.size() * 8);
+#ifdef GG_PROTO_MOSI
+  {
+    // the MOSI controllers' event counters [T][32] (GG_PS_*, include/graphite_gpu.h)
+    // and their outputSummary text (l2_cache_cntlr.cc:638-649,
+    // dram_directory_cntlr.cc:1041-1142), one "Tile t:" block per tile
+    vector<UInt64> ps((size_t)T * 32, 0);
+    string txt;
+    for (UInt32 t = 0; t < T; ++t) {
+      MSI::DramDirectoryCntlr* d = g_t[t].mm->_dram_directory_cntlr;
+      MSI::L2CacheCntlr* l2 = g_t[t].mm->_L2_cache_cntlr;
+      UInt64* v = &ps[(size_t)t * 32];
+      v[0] = d->_total_exreq; v[1] = d->_total_exreq_in_modified_state; v[2] = d->_total_exreq_in_shared_state;
+      v[3] = d->_total_exreq_with_upgrade_replies; v[4] = d->_total_exreq_in_uncached_state;
+      v[5] = d->_total_exreq_serialization_time.getTime(); v[6] = d->_total_exreq_processing_time.getTime();
+      v[7] = d->_total_shreq; v[8] = d->_total_shreq_in_modified_state; v[9] = d->_total_shreq_in_shared_state;
+      v[10] = d->_total_shreq_in_uncached_state;
+      v[11] = d->_total_shreq_serialization_time.getTime(); v[12] = d->_total_shreq_processing_time.getTime();
+      v[13] = d->_total_nullifyreq; v[14] = d->_total_nullifyreq_in_modified_state; v[15] = d->_total_nullifyreq_in_shared_state;
+      v[16] = d->_total_nullifyreq_in_uncached_state;
+      v[17] = d->_total_nullifyreq_serialization_time.getTime(); v[18] = d->_total_nullifyreq_processing_time.getTime();
+      v[19] = d->_total_invalidations_unicast_mode; v[20] = d->_total_invalidations_broadcast_mode;
+      v[21] = d->_total_sharers_invalidated_unicast_mode; v[22] = d->_total_sharers_invalidated_broadcast_mode;
+      v[23] = d->_total_invalidation_processing_time_unicast_mode.getTime();
+      v[24] = d->_total_invalidation_processing_time_broadcast_mode.getTime();
+      v[25] = l2->_total_invalidations; v[26] = l2->_total_evictions;
+      v[27] = l2->_total_dirty_evictions_exreq; v[28] = l2->_total_clean_evictions_exreq;
+      v[29] = l2->_total_dirty_evictions_shreq; v[30] = l2->_total_clean_evictions_shreq;
+      std::ostringstream os;
+      os << "Tile " << t << ":\n";
+      l2->outputSummary(os);
+      d->outputSummary(os);
+      txt += os.str();
+    }
+    write_bin("coh_" + n + "_proto.u64", &ps[0], ps.size() * 8);
+    write_bin("coh_" + n + "_summary.txt", txt.data(), txt.size());
+  }
+#endif
   fprintf(man, "%s  \"%s\": {\"tiles\": %u, \"per_tile\": %u, \"hot_lines\": %u, \"num_shards\": %u, \"net\": %u, "
           "\"dir_entries\": %u, \"dir_assoc\": %u, \"l2_assoc\": %u, \"workload\": \"%s\", \"records\": %llu, "
           "\"quanta\": %llu, \"steps\": %llu}",
@@ -903,6 +996,32 @@ static void run_case(FILE* man, bool first, const char* name, UInt32 T, UInt32 N
 int main(int argc, char** argv)
 {
   g_dir = argc > 1 ? argv[1] : ".";
+#ifdef GG_PROTO_MOSI
+  // pr_l1_pr_l2_dram_directory_mosi: the hotspot / stress shapes of the MSI
+  // fixtures (OWNED lines, upgrade replies, combined invalidate-flush, the
+  // directory's cached data, NULLIFY of OWNED entries) and the reference's FFT
+  string mp = g_dir + "/coh_mosi_manifest.json";
+  FILE* man = fopen(mp.c_str(), "w");
+  CHECK(man);
+  fprintf(man, "{\n");
+  run_case(man, true, "mosi_hot16", 16, 1500, 64, 1, 1, 0, 16);
+  run_case(man, false, "mosi_hot16magic", 16, 1000, 8, 1, 0, 0, 16);
+  run_case(man, false, "mosi_dir16", 16, 1000, 32, 1, 1, 64, 4);
+  run_case(man, false, "mosi_shard64", 64, 400, 32, 8, 1, 0, 16);
+  run_case(man, false, "mosi_shard256", 256, 150, 64, 8, 1, 0, 16);
+  run_case(man, false, "mosi_stress256w16", 256, 96, 0, 8, 1, 0, 16, 16, 1);
+  run_case(man, false, "mosi_shard1024", 1024, 24, 256, 8, 1, 0, 16);
+  if (argc > 2) {
+    RawTrace fft;
+    read_raw(string(argv[2]) + ".addr", fft.addr);
+    read_raw(string(argv[2]) + ".meta", fft.meta);
+    read_raw(string(argv[2]) + ".offs", fft.offs);
+    run_case(man, false, "mosi_fft10", 16, 0, 0, 1, 1, 0, 16, 8, 2, &fft);
+  }
+  fprintf(man, "\n}\n");
+  fclose(man);
+  return 0;
+#else
   string mp = g_dir + "/coh_manifest.json";
   FILE* man = fopen(mp.c_str(), "w");
   CHECK(man);
@@ -933,4 +1052,5 @@ int main(int argc, char** argv)
   fprintf(man, "\n}\n");
   fclose(man);
   return 0;
+#endif
 }

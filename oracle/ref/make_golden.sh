@@ -12,3 +12,5 @@ mkdir -p "$GOLD"
 # (coh_harness.cc), plus configs[0]'s captured FFT trace (-m10 fixture)
 python3 "$HERE/export_trace.py" "$GOLD/fft_real_p16_m10.npz" "$HERE/../_ref/fft10"
 "$HERE/../_ref/coh_harness" "$GOLD" "$HERE/../_ref/fft10"
+# the same schedule over the reference's MOSI controllers (coh_harness_mosi)
+"$HERE/../_ref/coh_harness_mosi" "$GOLD" "$HERE/../_ref/fft10"
