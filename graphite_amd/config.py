@@ -27,7 +27,10 @@ L2 = 1
 
 CSTATE_INVALID = 0
 CSTATE_SHARED = 1
+CSTATE_OWNED = 2      # MOSI
 CSTATE_MODIFIED = 4
+PROTO_MSI, PROTO_MOSI = 0, 1          # GG_PROTO_* (caching_protocol/type)
+MOSI_RNG_SEED = 1                     # GG_MOSI_RNG_SEED
 LOC_INVALID = 0
 LOC_L1D = 3
 
@@ -60,6 +63,20 @@ NUM_CACHE_COUNTERS = len(CACHE_COUNTERS)
 MSG_TYPES = ["EX_REQ", "SH_REQ", "INV_REQ", "FLUSH_REQ", "WB_REQ", "EX_REP", "SH_REP",
              "UPGRADE_REP", "INV_REP", "FLUSH_REP", "WB_REP"]
 MSG = {n: i + 1 for i, n in enumerate(MSG_TYPES)}
+MSG["NULLIFY_REQ"], MSG["INV_FLUSH_COMBINED_REQ"] = 12, 13
+CT_SENT_INV_FLUSH_COMBINED = 29       # GG_CT_SENT_INV_FLUSH_COMBINED (MOSI)
+# MOSI event counters, [tile][NUM_PROTO_STATS] (GG_PS_*)
+PROTO_STATS = ["exreq", "exreq_modified", "exreq_shared", "exreq_upgrade", "exreq_uncached",
+               "exreq_serialization_ps", "exreq_processing_ps",
+               "shreq", "shreq_modified", "shreq_shared", "shreq_uncached",
+               "shreq_serialization_ps", "shreq_processing_ps",
+               "nullify", "nullify_modified", "nullify_shared", "nullify_uncached",
+               "nullify_serialization_ps", "nullify_processing_ps",
+               "inv_unicast", "inv_broadcast", "inv_sharers_unicast", "inv_sharers_broadcast",
+               "inv_processing_unicast_ps", "inv_processing_broadcast_ps",
+               "l2_invalidations", "l2_evictions", "l2_dirty_evictions_exreq", "l2_clean_evictions_exreq",
+               "l2_dirty_evictions_shreq", "l2_clean_evictions_shreq"]
+NUM_PROTO_STATS = 32
 LVL_L1, LVL_L2, LVL_DIR = 0, 1, 2
 TILE_STATS = ["clock_ps", "accesses", "l1_hits", "l2_hits", "l2_misses", "latency_ps",
               "dir_accesses", "dir_evictions", "dir_back_invalidations",
@@ -122,6 +139,8 @@ class GGConfig(ctypes.Structure):
         ("l1i_track_miss_types", ctypes.c_uint32),
         ("l2_track_miss_types", ctypes.c_uint32),
         ("miss_track_lines", ctypes.c_uint32),
+        ("protocol", ctypes.c_uint32),
+        ("l1d_track_miss_types", ctypes.c_uint32),
     ]
 
 
@@ -174,7 +193,7 @@ def _cmsg_dtype():
     import numpy as np
     return np.dtype([("addr", "<u8"), ("send_ps", "<u8"), ("arrival_ps", "<u8"), ("zero_load_ps", "<u8"),
                      ("src", "<u4"), ("dst", "<u4"), ("requester", "<u4"), ("seq", "<u4"), ("type", "<u4"),
-                     ("link", "<u4"), ("hop", "<u4"), ("pad", "<u4")])
+                     ("link", "<u4"), ("hop", "<u4"), ("single_rx", "<u4")])
 
 
 CMSG_DTYPE = _cmsg_dtype()

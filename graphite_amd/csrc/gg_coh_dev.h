@@ -717,7 +717,7 @@ struct Tile {
     gg_cmsg m;
     m.addr = addr; m.send_ps = t; m.arrival_ps = t; m.zero_load_ps = 0;
     m.src = tile; m.dst = dst; m.requester = requester; m.seq = sq; m.type = type; m.link = 0;
-    m.hop = GG_HOP_NONE; m.pad = 0;
+    m.hop = GG_HOP_NONE; m.single_rx = 0;
     pool(S, p)[i] = m;
     // the step's sent list in LDS (slot = send order = sq - the step's first
     // seq): publish reads its records' fields from here, not back from HBM

@@ -56,7 +56,7 @@
 extern "C" {
 #endif
 
-#define GG_ABI_VERSION 7
+#define GG_ABI_VERSION 8
 
 typedef int gg_status;
 enum {
@@ -78,7 +78,7 @@ enum { GG_NET_MAGIC = 0, GG_NET_EMESH_HOP_COUNTER = 1, GG_NET_EMESH_HOP_BY_HOP =
 enum { GG_L1D = 0, GG_L2 = 1 };
 
 /* Cache line states, numerically identical to CacheState::Type (cache_state.h:11-21) */
-enum { GG_CSTATE_INVALID = 0, GG_CSTATE_SHARED = 1, GG_CSTATE_MODIFIED = 4 };
+enum { GG_CSTATE_INVALID = 0, GG_CSTATE_SHARED = 1, GG_CSTATE_OWNED = 2 /* MOSI */, GG_CSTATE_MODIFIED = 4 };
 
 /* Cached-location values of a private L2 line, MemComponent::Type subset
  * (PrL2CacheLineInfo::_cached_loc, pr_l1_pr_l2_dram_directory_msi/cache_line_info.h) */
@@ -220,7 +220,21 @@ typedef struct gg_config {
                                     tiles x 2 x lines x 8 B (65536: 1 GiB at 1024 tiles,
                                     4 GiB at 4096).  A full table stops the run with
                                     GG_ERR_UNSUPPORTED (no set entry is overwritten). */
+  /* ---- caching protocol (caching_protocol/type, carbon_sim.cfg:184) ---- */
+  uint32_t protocol;             /* GG_PROTO_*: pr_l1_pr_l2_dram_directory_msi (0) / _mosi (1) */
+  uint32_t l1d_track_miss_types; /* l1_dcache/T1/track_miss_types (false): read by the MOSI
+                                    protocol only, whose L1CacheCntlr passes the L1-D flag to the
+                                    L1-D (…mosi/l1_cache_cntlr.cc:68; MSI passes the L1-I one) */
 } gg_config;
+
+/* Caching protocols of the coherent mode (MemoryManager::createMMU,
+ * memory_manager.cc:22-60).  MOSI's DramDirectoryCntlr picks "one sharer"
+ * with the directory entry's own drand48 stream (DirectoryEntryFullMap::
+ * getOneSharer, directory_entry_full_map.cc:67-74; misc/random.h), which the
+ * reference seeds with time(NULL) when the entry is created: the canonical
+ * schedule seeds every entry with GG_MOSI_RNG_SEED (one fixed second).      */
+enum { GG_PROTO_MSI = 0, GG_PROTO_MOSI = 1 };
+#define GG_MOSI_RNG_SEED 1
 
 /* Miss types (Cache::MissType, cache.h:45-52), counted per (tile, cache). */
 enum { GG_MT_COLD = 0, GG_MT_CAPACITY, GG_MT_SHARING, GG_NUM_MISS_TYPES = 3 };
@@ -278,11 +292,13 @@ typedef struct gg_line_info {    /* CacheLineInfo / PrL2CacheLineInfo           
  * canonical schedule of DESIGN.md §Mode C.
  * ------------------------------------------------------------------------ */
 
-/* ShmemMsg::Type (pr_l1_pr_l2_dram_directory_msi/shmem_msg.h:12-30) */
+/* ShmemMsg::Type (pr_l1_pr_l2_dram_directory_msi/shmem_msg.h:12-30); MOSI's
+ * INV_FLUSH_COMBINED_REQ (…mosi/shmem_msg.h:20, numbered after WB_REQ there)
+ * is 13 here so the MSI numbering stays as it is */
 enum {
   GG_MSG_EX_REQ = 1, GG_MSG_SH_REQ, GG_MSG_INV_REQ, GG_MSG_FLUSH_REQ, GG_MSG_WB_REQ,
   GG_MSG_EX_REP, GG_MSG_SH_REP, GG_MSG_UPGRADE_REP, GG_MSG_INV_REP, GG_MSG_FLUSH_REP,
-  GG_MSG_WB_REP, GG_MSG_NULLIFY_REQ
+  GG_MSG_WB_REP, GG_MSG_NULLIFY_REQ, GG_MSG_INV_FLUSH_COMBINED_REQ
 };
 
 /* One ShmemMsg in flight (64 bytes).  The per-sender sequence number keeps
@@ -305,7 +321,8 @@ typedef struct gg_cmsg {
   uint32_t type;         /* GG_MSG_*                                            */
   uint32_t link;         /* backend-private (ignored on import)                 */
   uint32_t hop;          /* GG_HOP_NONE, or the router tile of a held packet    */
-  uint32_t pad;
+  uint32_t single_rx;    /* ShmemMsg::_single_receiver of an INV_FLUSH_COMBINED_REQ
+                            (…mosi/shmem_msg.h), else 0                          */
 } gg_cmsg;
 
 /* Logical shards: on a full W x H mesh (W = floor(sqrt
@@ -339,7 +356,27 @@ enum {
    * for DramPerfModel::outputSummary's "Queue Utilization" (dram_perf_model.cc:141-163) */
   GG_CT_DRAM_QUEUE_UTILIZED_NS = GG_CT_SENT_BY_TYPE + 11, /* _total_utilized_cycles */
   GG_CT_DRAM_QUEUE_LAST_NS,                               /* _last_request_time     */
+  GG_CT_SENT_INV_FLUSH_COMBINED = 29,                     /* MOSI INV_FLUSH_COMBINED_REQs sent */
   GG_NUM_TILE_STATS = 32
+};
+
+/* Per-tile protocol event counters of the MOSI controllers, [tile][GG_NUM_PROTO_STATS]
+ * (DramDirectoryCntlr::updateShmemReqEventCounters / updateShmemReqLatencyCounters /
+ * updateInvalidationEventCounters, …mosi/dram_directory_cntlr.cc:842-1023;
+ * L2CacheCntlr::updateInvalidationCounters / updateEvictionCounters,
+ * …mosi/l2_cache_cntlr.cc:596-636).  Times in picoseconds.  MSI: zeros.       */
+enum {
+  GG_PS_EXREQ = 0, GG_PS_EXREQ_MODIFIED, GG_PS_EXREQ_SHARED, GG_PS_EXREQ_UPGRADE, GG_PS_EXREQ_UNCACHED,
+  GG_PS_EXREQ_SERIALIZATION_PS, GG_PS_EXREQ_PROCESSING_PS,
+  GG_PS_SHREQ, GG_PS_SHREQ_MODIFIED, GG_PS_SHREQ_SHARED, GG_PS_SHREQ_UNCACHED,
+  GG_PS_SHREQ_SERIALIZATION_PS, GG_PS_SHREQ_PROCESSING_PS,
+  GG_PS_NULLIFY, GG_PS_NULLIFY_MODIFIED, GG_PS_NULLIFY_SHARED, GG_PS_NULLIFY_UNCACHED,
+  GG_PS_NULLIFY_SERIALIZATION_PS, GG_PS_NULLIFY_PROCESSING_PS,
+  GG_PS_INV_UNICAST, GG_PS_INV_BROADCAST, GG_PS_INV_SHARERS_UNICAST, GG_PS_INV_SHARERS_BROADCAST,
+  GG_PS_INV_PROCESSING_UNICAST_PS, GG_PS_INV_PROCESSING_BROADCAST_PS,
+  GG_PS_L2_INVALIDATIONS, GG_PS_L2_EVICTIONS, GG_PS_L2_DIRTY_EVICTIONS_EXREQ, GG_PS_L2_CLEAN_EVICTIONS_EXREQ,
+  GG_PS_L2_DIRTY_EVICTIONS_SHREQ, GG_PS_L2_CLEAN_EVICTIONS_SHREQ,
+  GG_NUM_PROTO_STATS = 32
 };
 
 /* Whole-run information, [GG_NUM_RUN_INFO]. */
@@ -516,6 +553,9 @@ gg_status gg_coherent_get_stats(gg_ctx* ctx, uint64_t* tile_stats, uint64_t* cac
  * (Mode P) replay does not track them: gg_cache_access_batch returns
  * GG_ERR_UNSUPPORTED when either flag is set.                                */
 gg_status gg_coherent_get_miss_types(gg_ctx* ctx, uint64_t* out);
+/* The MOSI event counters of a coherent run: out [tiles][GG_NUM_PROTO_STATS]
+ * (zeros under MSI; tiles a context does not own read 0).                   */
+gg_status gg_coherent_get_protocol_stats(gg_ctx* ctx, uint64_t* out);
 
 /* The sim.out text of the context's statistics (replaces the per-tile
  * outputSummary chain: TileManager::outputSummary, tile_manager_summary.cc:

@@ -446,7 +446,7 @@ static int o_insert_line(o_cache* c, uint64_t addr, const o_line* in, int* evict
   if (*eviction) {
     c->c[GG_CC_TAG_READS]++; c->c[GG_CC_DATA_READS]++;
     c->c[GG_CC_EVICTIONS]++;
-    if (c->write_back && (evicted->cstate == CS_M))  /* CacheState::dirty(): M/O/DIRTY */
+    if (c->write_back && (evicted->cstate == CS_M || evicted->cstate == GG_CSTATE_OWNED))  /* CacheState::dirty(): M/O/DIRTY */
       c->c[GG_CC_DIRTY_EVICTIONS]++;
   } else {
     c->c[GG_CC_TAG_READS]++;

@@ -107,6 +107,7 @@ void oracle_coh_cache_counters(const oracle_coh* C, uint64_t* out);  /* [tile][2
 void oracle_coh_net_counters(const oracle_coh* C, uint64_t* out);    /* [tile][GG_NUM_NET_COUNTERS] */
 void oracle_coh_run_info(const oracle_coh* C, uint64_t* out);        /* [GG_NUM_RUN_INFO] */
 void oracle_coh_miss_types(const oracle_coh* C, uint64_t* out);      /* [tile][2][GG_NUM_MISS_TYPES] */
+void oracle_coh_proto_stats(const oracle_coh* C, uint64_t* out);     /* [tile][GG_NUM_PROTO_STATS] (MOSI) */
 void oracle_cache_miss_types(const oracle_cache* oc, uint64_t* out); /* [tile][2][GG_NUM_MISS_TYPES] */
 /* the whole run with one context per logical shard, `threads` OpenMP threads */
 /* tile-parallel steps on `threads` OpenMP threads (bit-identical results) */

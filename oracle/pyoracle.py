@@ -101,7 +101,7 @@ def lib():
         L.oracle_coh_run.restype = ctypes.c_int
         L.oracle_coh_run.argtypes = [vp, _u64p, _u32p, _u64p, vp]
         for n in ("oracle_coh_tile_stats", "oracle_coh_cache_counters", "oracle_coh_net_counters",
-                  "oracle_coh_run_info", "oracle_coh_miss_types", "oracle_cache_miss_types"):
+                  "oracle_coh_run_info", "oracle_coh_miss_types", "oracle_coh_proto_stats", "oracle_cache_miss_types"):
             getattr(L, n).argtypes = [vp, _u64p]
             getattr(L, n).restype = None
         _lib = L
@@ -258,6 +258,10 @@ class OracleCoherent:
 
     def miss_types(self):
         return self._get("oracle_coh_miss_types", (self.cfg.num_tiles, 2, 3))
+
+    def proto_stats(self):
+        """MOSI event counters [tile][NUM_PROTO_STATS] (zeros under MSI)."""
+        return self._get("oracle_coh_proto_stats", (self.cfg.num_tiles, 32))
 
 
 class OracleCache:

@@ -1011,6 +1011,10 @@ int main(int argc, char** argv)
   run_case(man, false, "mosi_shard256", 256, 150, 64, 8, 1, 0, 16);
   run_case(man, false, "mosi_stress256w16", 256, 96, 0, 8, 1, 0, 16, 16, 1);
   run_case(man, false, "mosi_shard1024", 1024, 24, 256, 8, 1, 0, 16);
+  // L2 evictions (private footprints past the 8192-line L2): FLUSH_REP of
+  // MODIFIED / OWNED lines, INV_REP of SHARED ones, "just an eviction" writes
+  run_case(man, false, "mosi_evict16", 16, 12000, 64, 1, 1, 0, 16);
+  run_case(man, false, "mosi_evict16s4", 16, 12000, 64, 4, 1, 0, 16);
   if (argc > 2) {
     RawTrace fft;
     read_raw(string(argv[2]) + ".addr", fft.addr);
@@ -1038,6 +1042,9 @@ int main(int argc, char** argv)
   run_case(man, false, "stress256w16", 256, 96, 0, 8, 1, 0, 16, 16, 1);
   // configs[3] scale: 1024 tiles x 8 logical shards, 256 hot lines, reduced length
   run_case(man, false, "shard1024", 1024, 24, 256, 8, 1, 0, 16);
+  // L2 evictions (private footprints past the 8192-line L2)
+  run_case(man, false, "evict16", 16, 12000, 64, 1, 1, 0, 16);
+  run_case(man, false, "evict16s4", 16, 12000, 64, 4, 1, 0, 16);
   // configs[0]: the reference's own fft.C (-p16 -m10) as captured by
   // tools/fft_trace (tests/golden/fft_real_p16_m10.npz, accesses only: the
   // BARRIER release is restated, not the reference's SyncServer), 16 tiles,

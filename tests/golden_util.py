@@ -43,9 +43,15 @@ def coh_manifest():
         return json.load(f)
 
 
+def coh_mosi_manifest():
+    with open(os.path.join(GOLDEN, "coh_mosi_manifest.json")) as f:
+        return json.load(f)
+
+
 def coh_case(name, m):
     """(cfg, addr, meta, offsets, expected dict) of a coherent-mode fixture written
-    by oracle/ref/coh_harness.cc (the reference's MSI controllers)."""
+    by oracle/ref/coh_harness.cc (the reference's MSI controllers; "mosi_*"
+    names: coh_harness_mosi, the MOSI controllers, plus their event counters)."""
     from graphite_amd import config as C
     from oracle import pyoracle as po
     T, N = m["tiles"], m["per_tile"]
@@ -53,6 +59,9 @@ def coh_case(name, m):
     if m["dir_entries"]:
         kw.update(dir_total_entries=m["dir_entries"], dir_assoc=m["dir_assoc"])
     kw.update(l2_assoc=m.get("l2_assoc", 8))
+    mosi = name.startswith("mosi_")
+    if mosi:
+        kw.update(protocol=C.PROTO_MOSI)
     cfg = C.default_config(T, **kw)
     wl = m.get("workload", "hotspot")
     if wl == "stress":
@@ -67,6 +76,8 @@ def coh_case(name, m):
            "cache": load("coh_%s_cache.u64" % name, np.uint64).reshape(T, 2, 12),
            "net": load("coh_%s_net.u64" % name, np.uint64).reshape(T, 3),
            "quanta": m["quanta"], "steps": m["steps"]}
+    if mosi:
+        exp["proto"] = load("coh_%s_proto.u64" % name, np.uint64).reshape(T, 32)
     return cfg, a, meta, o, exp
 
 

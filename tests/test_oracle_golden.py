@@ -199,3 +199,42 @@ def test_coherent_oracle_matches_reference_controllers(name):
     ri = oc.run_info()
     assert ri[C.RUN_INFO.index("quanta")] == exp["quanta"]
     assert ri[C.RUN_INFO.index("steps")] == exp["steps"]
+
+
+# ---- coherent mode, MOSI: pinned by the reference's own MOSI controllers ---
+@pytest.mark.parametrize("name", sorted(G.coh_mosi_manifest()))
+def test_coherent_mosi_oracle_matches_reference_controllers(name):
+    """The MOSI restatement (oracle/gg_coherent.inc, protocol = GG_PROTO_MOSI)
+    == pr_l1_pr_l2_dram_directory_mosi's L1CacheCntlr / L2CacheCntlr /
+    DramDirectoryCntlr compiled from /root/reference (coh_harness_mosi):
+    access words, tile statistics (INV_FLUSH_COMBINED_REQs in slot 29), cache
+    and NoC counters, quanta / steps and the controllers' event counters."""
+    from graphite_amd import config as C
+    cfg, a, m, o, exp = G.coh_case(name, G.coh_mosi_manifest()[name])
+    oc = po.OracleCoherent(cfg)
+    out = oc.run(a, m, o)
+    np.testing.assert_array_equal(out, exp["out"])
+    np.testing.assert_array_equal(oc.tile_stats(), exp["stats"])
+    np.testing.assert_array_equal(oc.cache_counters(), exp["cache"])
+    nc = oc.net_counters()[:, [C.NET_COUNTERS.index(k) for k in G.NET3]]
+    np.testing.assert_array_equal(nc, exp["net"])
+    np.testing.assert_array_equal(oc.proto_stats(), exp["proto"])
+    ri = oc.run_info()
+    assert ri[C.RUN_INFO.index("quanta")] == exp["quanta"]
+    assert ri[C.RUN_INFO.index("steps")] == exp["steps"]
+
+
+def test_mosi_fixtures_exercise_the_protocol():
+    """The MOSI fixtures reach what MSI lacks: upgrade replies, combined
+    invalidate-flush requests, OWNED write-backs (dirty evictions / shared
+    requests in OWNED state) and directory-entry nullifies."""
+    tot = {}
+    for name in G.coh_mosi_manifest():
+        cfg, a, m, o, exp = G.coh_case(name, G.coh_mosi_manifest()[name])
+        tot[name] = (exp["proto"].sum(0), exp["stats"][:, 29].sum())
+    from graphite_amd import config as C
+    P = {k: i for i, k in enumerate(C.PROTO_STATS)}
+    assert sum(int(p[P["exreq_upgrade"]]) for p, _ in tot.values()) > 0
+    assert sum(int(ifc) for _, ifc in tot.values()) > 0
+    assert int(tot["mosi_dir16"][0][P["nullify"]]) > 0
+    assert sum(int(p[P["shreq_shared"]]) for p, _ in tot.values()) > 0
