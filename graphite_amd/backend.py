@@ -59,6 +59,7 @@ EXPORTS = ["gg_abi_version", "gg_last_error", "gg_config_default", "gg_create", 
            "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace", "gg_shard_map",
            "gg_kernel_stats", "gg_round_exchange", "gg_coherent_run_ranks", "gg_gen_stress_trace",
            "gg_split_accesses", "gg_combine_accesses", "gg_dump_summary", "gg_core_model_run", "gg_core_get_stats", "gg_coherent_get_miss_types",
+           "gg_coherent_get_protocol_stats",
            "gg_round_pack", "gg_round_unpack", "gg_round_finish"]
 
 
@@ -133,6 +134,7 @@ def load():
     L.gg_core_model_run.argtypes = [vp, ctypes.POINTER(_Trace), vp, vp]
     L.gg_core_get_stats.argtypes = [vp, vp]
     L.gg_coherent_get_miss_types.argtypes = [vp, vp]
+    L.gg_coherent_get_protocol_stats.argtypes = [vp, vp]
     L.gg_round_pack.argtypes = [vp, u32, u32, u64, ctypes.POINTER(RoundIO)]
     L.gg_round_unpack.argtypes = [vp, ctypes.POINTER(RoundIO)]
     L.gg_round_finish.argtypes = [vp, ctypes.POINTER(RoundIO)]
@@ -140,7 +142,7 @@ def load():
                  "gg_coherent_import", "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace",
                  "gg_round_exchange", "gg_coherent_run_ranks", "gg_gen_stress_trace", "gg_split_accesses",
                  "gg_combine_accesses", "gg_dump_summary", "gg_core_model_run", "gg_core_get_stats",
-                 "gg_coherent_get_miss_types", "gg_round_pack", "gg_round_unpack", "gg_round_finish"]:
+                 "gg_coherent_get_miss_types", "gg_coherent_get_protocol_stats", "gg_round_pack", "gg_round_unpack", "gg_round_finish"]:
         getattr(L, name).restype = i32
     for name in ["gg_reset", "gg_cache_access_batch", "gg_cache_get_counters", "gg_cache_get_line_info",
                  "gg_cache_set_line_info", "gg_cache_access_line", "gg_cache_insert_line",
@@ -393,6 +395,13 @@ class Backend:
         out = np.zeros(T * 2 * 3, np.uint64)
         _check(load().gg_coherent_get_miss_types(self.h, out.ctypes.data_as(ctypes.c_void_p)))
         return out.reshape(T, 2, 3)
+
+    def protocol_stats(self):
+        """[tiles][NUM_PROTO_STATS] MOSI event counters (gg_coherent_get_protocol_stats; zeros under MSI)."""
+        T = self.cfg.num_tiles
+        out = np.zeros(T * 32, np.uint64)
+        _check(load().gg_coherent_get_protocol_stats(self.h, out.ctypes.data_as(ctypes.c_void_p)))
+        return out.reshape(T, 32)
 
     def core_stats(self):
         T = self.cfg.num_tiles

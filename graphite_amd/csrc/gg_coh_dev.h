@@ -68,8 +68,9 @@ enum { M_EX_REQ = GG_MSG_EX_REQ, M_SH_REQ = GG_MSG_SH_REQ, M_INV_REQ = GG_MSG_IN
        M_FLUSH_REQ = GG_MSG_FLUSH_REQ, M_WB_REQ = GG_MSG_WB_REQ, M_EX_REP = GG_MSG_EX_REP,
        M_SH_REP = GG_MSG_SH_REP, M_INV_REP = GG_MSG_INV_REP, M_FLUSH_REP = GG_MSG_FLUSH_REP,
        M_WB_REP = GG_MSG_WB_REP, M_NULLIFY_REQ = GG_MSG_NULLIFY_REQ };
-enum { DS_UNCACHED = 0, DS_SHARED = 1, DS_MODIFIED = 2 };
-enum { ST_I = 0, ST_S = 1, ST_M = 2 };           // meta byte bits 0-1
+enum { DS_UNCACHED = 0, DS_SHARED = 1, DS_MODIFIED = 2, DS_OWNED = 3 /* MOSI */ };
+enum { ST_I = 0, ST_S = 1, ST_M = 2, ST_O = 3 /* MOSI */ };   // meta byte bits 0-1
+enum { M_UPGRADE_REP = GG_MSG_UPGRADE_REP, M_IFC_REQ = GG_MSG_INV_FLUSH_COMBINED_REQ };
 enum { P_SELF = 0, P_LEFT, P_RIGHT, P_DOWN, P_UP, P_INJ };   // network_model_emesh_hop_by_hop.h:41-48 (+ injection)
 #define INV_ADDR (~0ull)
 #define NO_ENT (-0x7fffffff)
@@ -82,14 +83,25 @@ __device__ __forceinline__ bool has_data(uint32_t t)
 {
   return t == M_EX_REP || t == M_SH_REP || t == M_FLUSH_REP || t == M_WB_REP;
 }
+// modeled length class of a message (ShmemMsg::getModeledLength, shmem_msg.cc:100-125,
+// …mosi/shmem_msg.cc:122-151): 0 request, 1 with a cache line, 2 MOSI
+// INV_FLUSH_COMBINED_REQ (+ the single receiver's tile id)
+__device__ __forceinline__ uint32_t len_class(uint32_t t) { return has_data(t) ? 1u : t == M_IFC_REQ ? 2u : 0u; }
 
 struct DEnt { uint64_t addr; int32_t owner; uint16_t dstate; uint16_t nsh; };   // 16 B
-struct HMsg { uint64_t addr, arrival_ps; uint32_t type, src, requester; };        // the fields a handler reads
+struct HMsg { uint64_t addr, arrival_ps; uint32_t type, src, requester, single_rx; };   // the fields a handler reads
 // a tile's step state (trace position, clock, pending access, blocking,
 // sequence, replaced entries, request FIFO length): one line, one pointer
 struct TileSt { uint64_t rec, rec_end, clk, pend_start, out_addr, out_time; uint32_t blocked, seq, nrep, nrq; };
 static_assert(sizeof(TileSt) == 64, "one 64-B line per tile");
 struct CReq { uint64_t addr, time; uint32_t type, requester; };                 // 24 B
+// MOSI: the rest of a ShmemReq (…mosi/shmem_req.h:14-66) beside its FIFO slot
+// (CReq::time is its _processing_finish_time there)
+struct CReqX { uint64_t arrival, start; uint32_t ds0, upg; int32_t sharer; uint32_t pad; };   // 32 B
+constexpr uint32_t kCdl = 64;          // MOSI: the directory's cached data list, entries per tile
+// MOSI: a directory entry's Random (drand48_r state X) is stored XOR its seed
+// state, so zeroed memory is a freshly created entry (misc/random.h:14-23)
+constexpr uint64_t kRng0 = ((uint64_t)(uint32_t)GG_MOSI_RNG_SEED << 16) | 0x330Eu;
 // address-space-typed pointers (a generic pointer whose origin the compiler
 // cannot see compiles to flat accesses)
 #define GG_LDS __attribute__((address_space(3)))
@@ -120,7 +132,7 @@ struct CP {
   uint32_t T, K, L;                      // tiles, logical shards, owned tiles
   uint32_t s1, a1, s2, a2, log_line, pol1, pol2;
   uint32_t E, dassoc, log_dsets, log_slices, W, R, QC, IC;
-  uint32_t bits_req, bits_data, max_list, analytical, dram_qm, dram_qtype, dram_qaux;
+  uint32_t bits_req, bits_data, bits_ifc, max_list, analytical, dram_qm, dram_qtype, dram_qaux;
   uint32_t net, nsx, nsy, mw, mh, qimg;  // network model; X / Y segments; mesh; bytes of a queue image
   uint32_t msg_cap, seg_cap, walk_pk;    // pool records per parity; entries per segment list; walker LDS packets
   uint32_t seg_xcd;                      // > 0: runs interleaved by shard (seg_xcd shards), XCD-grouped walker blocks
@@ -130,9 +142,13 @@ struct CP {
   uint32_t no_hit_runs;                    // 1: every record through app_access (hit runs off; 0 in the build)
   uint32_t mt1, mt2, mt_log;               // miss-type tracking of the L1-D / L2 (cfg flags), log2 set capacity
   uint32_t fast;                           // k_c_step<true> (Tile's F): register queues only, no miss types
+  uint32_t mosi;                           // pr_l1_pr_l2_dram_directory_mosi: k_c_step<false, true> (Tile's MO)
   uint64_t lat_l1d, lat_l1t, lat_l2d, lat_l2t, lat_dir, gap_ps, dram_proc, dram_cost;
   NocParams np;
 };
+
+__device__ __forceinline__ uint32_t class_bits(const CP& P, uint32_t c) { return c == 1 ? P.bits_data : c == 2 ? P.bits_ifc : P.bits_req; }
+__device__ __forceinline__ uint32_t msg_bits(const CP& P, uint32_t t) { return class_bits(P, len_class(t)); }
 
 struct CS {
   uint64_t* l1_tag; uint8_t* l1_meta; uint8_t* l1_rr;
@@ -145,6 +161,12 @@ struct CS {
   DEnt* dir; uint64_t* dsh;              // [L][E], [L][E][W]
   DEnt* rep; uint64_t* rsh;              // [L][R], [L][R][W]
   CReq* rq;                              // [L][QC]
+  // MOSI: the FIFO's other request fields, the entries' Random states (XOR
+  // kRng0), the cached data list + length, the protocol event counters
+  CReqX* rqx;                            // [L][QC]
+  uint64_t* drng; uint64_t* rrng;        // [L][E], [L][R]
+  uint64_t* cdl; uint32_t* ncdl;         // [L][kCdl], [L]
+  uint64_t* ps;                          // [L][GG_NUM_PROTO_STATS]
   HQueue* dq; HNode* dnd;                // DRAM queue per tile
   const uint32_t* gtile; const int32_t* ltile; const uint32_t* shard;   // local -> tile, tile -> local (-1), tile -> shard
   const uint4* tinfo;                    // [L] {tile, X run, Y run, 0} of a local tile: one load, no chain
@@ -490,7 +512,7 @@ struct CacheT {
     if (ev) {
       cnt(GG_CC_DATA_READS);
       cnt(GG_CC_EVICTIONS);
-      if (wb && ev_st == ST_M) cnt(GG_CC_DIRTY_EVICTIONS);
+      if (wb && (ev_st == ST_M || ev_st == ST_O)) cnt(GG_CC_DIRTY_EVICTIONS);   // CacheState::dirty(): M / O
     }
     cnt(GG_CC_TAG_WRITES); cnt(GG_CC_DATA_WRITES);
     return true;
@@ -612,9 +634,14 @@ struct TilePre {
 // cache tracks miss types, so the other queue forms and the miss-type hooks
 // are compiled out of it (a smaller kernel: fewer instruction-cache misses
 // on a tile's path, fewer live values)
-template <class SL, class H, bool F = false>
+// MO: the MOSI controllers (pr_l1_pr_l2_dram_directory_mosi, k_c_step<false,
+// true>): OWNED lines and entries, upgrade replies, combined invalidate-flush
+// requests, sharer write-backs, the directory's cached data list and the
+// protocol event counters (directory_msg_mo / l2_msg_mo below)
+template <class SL, class H, bool F = false, bool MO = false>
 struct Tile {
   static constexpr bool kF = F;
+  static constexpr bool kMO = MO;
   using Cache = CacheT<!F>;
   const CP& P; const CS& S;
   uint32_t lt, tile, ln, p;             // local index, tile id, lane, step parity
@@ -635,6 +662,11 @@ struct Tile {
   uint64_t oaddr = 0, osh = 0; int32_t oown = -1; uint32_t ost = 0, onsh = 0;
   bool tr_on = false;                   // GG_COH_TRACE: cycles by handler part (dget, sharers, DRAM, send, FIFO, sharer words)
   uint64_t tra[6] = {0, 0, 0, 0, 0, 0};
+  // MOSI: event counter increments (lane k holds counter k), the cached data
+  // list's length (and at step start), the FIFO's MOSI fields
+  uint64_t pd = 0;
+  uint32_t ncdl = 0, ncdl0 = 0;
+  GG_GLB CReqX* rqx = nullptr;
 
   // LC: the tile's L1-D / L2 tags, meta bytes and RR counters live in LDS at
   // clds for the whole launch (k_c_persist; layout of cache_lds_bytes)
@@ -676,8 +708,13 @@ struct Tile {
     rqg = (GG_GLB CReq*)(S.rq + (size_t)lt * P.QC); rq_lds = false;
     nch = 0; cbase = 0; cused = 0; ccap = 0; nsent = 0; failed = false; ferr = 0;
     ccv = pre.ccv; stv = pre.stv;
+    if constexpr (MO) {
+      rqx = (GG_GLB CReqX*)(S.rqx + (size_t)lt * P.QC);
+      ncdl = ncdl0 = S.ncdl[lt];
+    }
   }
   __device__ __forceinline__ void stat(uint32_t k, uint64_t v) { if (ln == k) sd += v; }
+  __device__ __forceinline__ void pstat(uint32_t k, uint64_t v = 1) { if (ln == k) pd += v; }   // MOSI event counters
   // error flags are gathered in a register and reported once per step
   // (flush_err): one atomic site instead of one per inlined check
   __device__ __forceinline__ void fail(uint32_t e = GG_DERR_STATE)
@@ -712,19 +749,19 @@ struct Tile {
     return i;
   }
   __device__ __forceinline__ void put(uint32_t i, uint32_t dst, uint32_t type, uint32_t requester, uint64_t addr,
-                                      uint64_t t, uint32_t sq)
+                                      uint64_t t, uint32_t sq, uint32_t single_rx = 0)
   {
     gg_cmsg m;
     m.addr = addr; m.send_ps = t; m.arrival_ps = t; m.zero_load_ps = 0;
     m.src = tile; m.dst = dst; m.requester = requester; m.seq = sq; m.type = type; m.link = 0;
-    m.hop = GG_HOP_NONE; m.single_rx = 0;
+    m.hop = GG_HOP_NONE; m.single_rx = single_rx;
     pool(S, p)[i] = m;
     // the step's sent list in LDS (slot = send order = sq - the step's first
     // seq): publish reads its records' fields from here, not back from HBM
     // (x3 / x4 are free once the inbox is ordered; sends come after that)
     const uint32_t slot = sq - p0.seq;
     if (slot < SL::kIn) {
-      sl.x3[slot] = (uint64_t)i | ((uint64_t)dst << 32) | (has_data(type) ? (1ull << 63) : 0ull);
+      sl.x3[slot] = (uint64_t)i | ((uint64_t)dst << 32) | ((uint64_t)len_class(type) << 62);   // dst < 2^30
       sl.x4[slot] = t;
     }
   }
@@ -732,6 +769,7 @@ struct Tile {
   {
     stat(GG_CT_MSGS_SENT, n);
     if (type - 1u < 11u) stat(GG_CT_SENT_BY_TYPE + type - 1u, n);
+    else if (MO && type == M_IFC_REQ) stat(GG_CT_SENT_INV_FLUSH_COMBINED, n);
   }
   __device__ __forceinline__ void send(uint32_t dst, uint32_t type, uint32_t requester, uint64_t addr, uint64_t t)
   { const uint64_t c0 = tr_on ? __builtin_amdgcn_s_memtime() : 0; send_(dst, type, requester, addr, t); if (tr_on) tra[3] += __builtin_amdgcn_s_memtime() - c0; }
@@ -878,6 +916,7 @@ struct Tile {
       if (oh == (int32_t)i) eclose();
       d[i].addr = a;
       if (ln < P.W) shw((int32_t)i)[ln] = 0;
+      if constexpr (MO) S.drng[(size_t)lt * P.E + i] = 0;          // a fresh Random (seed state)
       if (spec) {
         eclose();
         oaddr = a; oown = (int32_t)rl32((uint32_t)e.owner, w); ost = rl32((uint32_t)e.dstate, w);
@@ -908,6 +947,10 @@ struct Tile {
     uint64_t* so = shw(slot); uint64_t* sr = shw(-(int32_t)r - 1);
     for (uint32_t w = 0; w < P.W; ++w) { sr[w] = so[w]; so[w] = 0; }
     d[slot] = DEnt{a, -1, DS_UNCACHED, 0};
+    if constexpr (MO) {                           // the old entry keeps its Random, the new one is fresh
+      S.rrng[(size_t)lt * P.R + r] = S.drng[(size_t)lt * P.E + slot];
+      S.drng[(size_t)lt * P.E + slot] = 0;
+    }
     t += P.lat_dir;
     stat(GG_CT_DIR_ACCESSES, 1);
     stat(GG_CT_DIR_EVICTIONS, 1);
@@ -926,14 +969,17 @@ struct Tile {
       *ent(-(int32_t)k - 1) = *ent(-(int32_t)k - 2);
       uint64_t* dst = shw(-(int32_t)k - 1); const uint64_t* src = shw(-(int32_t)k - 2);
       for (uint32_t w = 0; w < P.W; ++w) dst[w] = src[w];
+      if constexpr (MO) S.rrng[(size_t)lt * P.R + k] = S.rrng[(size_t)lt * P.R + k + 1];
     }
     nrep = nr - 1;
   }
   // getSharersList (ascending, full_map.cc:48-66): one message per sharer,
   // lane k writes the messages of sharer word k
-  __device__ __forceinline__ void send_sharers(int32_t h, uint32_t type, uint32_t requester, uint64_t a, uint64_t t)
-  { const uint64_t c0 = tr_on ? __builtin_amdgcn_s_memtime() : 0; send_sharers_(h, type, requester, a, t); if (tr_on) tra[1] += __builtin_amdgcn_s_memtime() - c0; }
-  __device__ __forceinline__ void send_sharers_(int32_t h, uint32_t type, uint32_t requester, uint64_t a, uint64_t t)
+  __device__ __forceinline__ void send_sharers(int32_t h, uint32_t type, uint32_t requester, uint64_t a, uint64_t t,
+                                               uint32_t single_rx = 0)
+  { const uint64_t c0 = tr_on ? __builtin_amdgcn_s_memtime() : 0; send_sharers_(h, type, requester, a, t, single_rx); if (tr_on) tra[1] += __builtin_amdgcn_s_memtime() - c0; }
+  __device__ __forceinline__ void send_sharers_(int32_t h, uint32_t type, uint32_t requester, uint64_t a, uint64_t t,
+                                                uint32_t single_rx)
   {
     eopen(h);
     uint64_t bits = ln < P.W ? osh : 0;
@@ -946,7 +992,7 @@ struct Tile {
     uint32_t k = pre;
     while (bits) {
       const uint32_t b = (uint32_t)__builtin_ctzll(bits); bits &= bits - 1;
-      put(base + k, ln * 64 + b, type, requester, a, t, seq + k);
+      put(base + k, ln * 64 + b, type, requester, a, t, seq + k, single_rx);
       ++k;
     }
     seq += tot;
@@ -970,6 +1016,17 @@ struct Tile {
     if (rq_lds) { GG_LDS CReq* x = lrq() + i; x->addr = v.addr; x->time = v.time; x->type = v.type; x->requester = v.requester; }
     else { GG_GLB CReq* x = rqg + i; x->addr = v.addr; x->time = v.time; x->type = v.type; x->requester = v.requester; }
   }
+  // MOSI: the FIFO's other request fields (HBM)
+  __device__ __forceinline__ CReqX rqx_get(uint32_t i) const
+  {
+    const GG_GLB CReqX* x = rqx + i;
+    return CReqX{x->arrival, x->start, x->ds0, x->upg, x->sharer, 0};
+  }
+  __device__ __forceinline__ void rqx_put(uint32_t i, const CReqX& v)
+  {
+    GG_GLB CReqX* x = rqx + i;
+    x->arrival = v.arrival; x->start = v.start; x->ds0 = v.ds0; x->upg = v.upg; x->sharer = v.sharer;
+  }
   __device__ __forceinline__ uint32_t qcount(uint64_t a) const
   {
     uint32_t c = 0;                                  // a ballot per 64 entries (no cross-lane reduction)
@@ -991,6 +1048,7 @@ struct Tile {
   {
     if (nrq >= (rq_lds ? SL::kRq : P.QC)) { fail(GG_DERR_CAP); return; }
     rq_put(nrq, CReq{a, t, type, req});
+    if constexpr (MO) rqx_put(nrq, CReqX{t, t, DS_UNCACHED, 0, -1, 0});   // ShmemReq(msg, time) (…mosi/shmem_req.cc:8-22)
     if (rq_lds) wave_sync();
     ++nrq;
   }
@@ -1011,6 +1069,14 @@ struct Tile {
       }
     } else {
       for (uint32_t k = (uint32_t)f; k + 1 < nrq; ++k) rq_put(k, rq_get(k + 1));
+    }
+    if constexpr (MO) {                             // the MOSI fields move with their entries
+      for (uint32_t b = (uint32_t)f + 1; b < nrq; b += 64) {
+        const uint32_t i = b + ln;
+        CReqX v{};
+        if (i < nrq) v = rqx_get(i);
+        if (i < nrq) rqx_put(i - 1, v);               // (the loads of the 64 complete before any store)
+      }
     }
     --nrq;
   }
@@ -1412,7 +1478,7 @@ struct Tile {
     L1.miss_counters(a, wr, !hit);
     if (hit) { t += P.lat_l1d; l1_access(a, wr); finish(s, t, GG_LVL_L1); return; }
     t += P.lat_l1t;
-    l1_invalidate(a);
+    if constexpr (!MO) l1_invalidate(a);                             // (MOSI keeps the line, …mosi/l1:127-135)
     uint32_t c2, l2;                                                 // processShmemRequestFromL1Cache (l2:180-224)
     L2.get(a, c2, l2);
     const bool hit2 = wr ? c2 == ST_M : c2 != ST_I;
@@ -1430,7 +1496,9 @@ struct Tile {
     if (out_addr != INV_ADDR) fail();                                // handleMsgFromL1Cache (l2:226-258)
     out_addr = a; out_time = t;
     const uint32_t h = home(a);
-    if (wr) {                                                        // processExReqFromL1Cache (l2:260-282)
+    if constexpr (MO) {                                              // …mosi/l2:266-285: the request as is
+      send(h, wr ? M_EX_REQ : M_SH_REQ, tile, a, t);
+    } else if (wr) {                                                 // processExReqFromL1Cache (l2:260-282)
       uint32_t x, xl;
       L2.get(a, x, xl);
       if (x == ST_S) { if (!L2.set(a, ST_I, 0)) fail(); send(h, M_INV_REP, tile, a, t); }
@@ -1500,6 +1568,460 @@ struct Tile {
     }
   }
 
+  // ==== MOSI (pr_l1_pr_l2_dram_directory_mosi) ================================
+  // The MOSI directory and L2 controllers on the same directory cache, request
+  // FIFO, DRAM, clock and network as the MSI ones above (Tile<..., MO = true>).
+  __device__ __forceinline__ uint64_t* rng_ptr(int32_t h) const
+  {
+    h = __builtin_amdgcn_readfirstlane(h);
+    return h >= 0 ? S.drng + (size_t)lt * P.E + h : S.rrng + (size_t)lt * P.R + (-h - 1);
+  }
+  // DirectoryEntryFullMap::getOneSharer (directory_entry_full_map.cc:67-74):
+  // Random<int>::next(#sharers) over drand48_r (misc/random.h:25-31) —
+  // X <- (0x5DEECE66D X + 0xB) mod 2^48, result X / 2^48 (exact in a double),
+  // index (int)(result * n) — into the ascending sharers list (lane w holds
+  // sharer word w: the index's word by a prefix count, its bit by clearing)
+  __device__ __forceinline__ int32_t one_sharer(int32_t h)
+  {
+    eopen(h);
+    uint64_t* rp = rng_ptr(h);
+    uint64_t x = *rp ^ kRng0;
+    x = (0x5DEECE66Dull * x + 0xBull) & 0xFFFFFFFFFFFFull;
+    *rp = x ^ kRng0;
+    const double r = (double)x * 0x1p-48;
+    const uint32_t n = onsh;
+    const uint32_t k = (uint32_t)(int)(r * (double)(int)n);
+    if (k >= n) { fail(); return 0; }
+    const uint64_t bits = ln < P.W ? osh : 0ull;
+    const uint32_t c = (uint32_t)__builtin_popcountll(bits);
+    const uint32_t pre = wave_excl_scan(c, ln);
+    const bool mine = k >= pre && k < pre + c;
+    uint32_t sh = 0;
+    if (mine) {
+      uint64_t b = bits;
+      for (uint32_t j = k - pre; j; --j) b &= b - 1;
+      sh = ln * 64 + (uint32_t)__builtin_ctzll(b);
+    }
+    const uint64_t who = __ballot(mine);
+    if (!who) { fail(); return 0; }
+    return (int32_t)rl32(sh, (uint32_t)__builtin_ctzll(who));
+  }
+  // DataList (…mosi/dram_directory_cntlr.cc:1196-1241): the line data is not modeled
+  __device__ __forceinline__ int32_t cdl_find(uint64_t a) const
+  {
+    if (!ncdl) return -1;
+    const uint64_t v = ln < ncdl ? S.cdl[(size_t)lt * kCdl + ln] : 0ull;
+    const uint64_t m = __ballot(ln < ncdl && v == a);
+    return m ? (int32_t)__builtin_ctzll(m) : -1;
+  }
+  __device__ __forceinline__ void cdl_insert(uint64_t a)
+  {
+    if (cdl_find(a) >= 0) return;                                 // already there: the same data
+    if (ncdl >= kCdl) { fail(GG_DERR_CAP); return; }
+    S.cdl[(size_t)lt * kCdl + ncdl] = a;
+    ++ncdl;
+  }
+  __device__ __forceinline__ void cdl_erase_at(int32_t i)
+  {
+    uint64_t* c = S.cdl + (size_t)lt * kCdl;
+    const uint64_t last = c[ncdl - 1];
+    c[i] = last;
+    --ncdl;
+  }
+  // updateShmemReqEventCounters (:879-965) of the request at FIFO slot f, with
+  // setInitialDState before it (first_call of process*Req)
+  __device__ __forceinline__ void mo_event(int32_t h, int32_t f, uint32_t type, uint32_t requester)
+  {
+    const uint32_t ds = e_state(h), n = e_nsh(h);
+    const bool shared = ds == DS_OWNED || ds == DS_SHARED;
+    rqx[f].ds0 = ds;
+    if (type == M_EX_REQ) {
+      pstat(GG_PS_EXREQ);
+      if (ds == DS_MODIFIED) pstat(GG_PS_EXREQ_MODIFIED);
+      else if (shared) {
+        pstat(GG_PS_EXREQ_SHARED);
+        if (n == 1 && one_sharer(h) == (int32_t)requester) { rqx[f].upg = 1; pstat(GG_PS_EXREQ_UPGRADE); }
+        else { pstat(GG_PS_INV_UNICAST); pstat(GG_PS_INV_SHARERS_UNICAST, n); }   // updateInvalidationEventCounters
+      } else pstat(GG_PS_EXREQ_UNCACHED);
+    } else if (type == M_SH_REQ) {
+      pstat(GG_PS_SHREQ);
+      pstat(ds == DS_MODIFIED ? GG_PS_SHREQ_MODIFIED : shared ? GG_PS_SHREQ_SHARED : GG_PS_SHREQ_UNCACHED);
+    } else {
+      pstat(GG_PS_NULLIFY);
+      if (ds == DS_MODIFIED) pstat(GG_PS_NULLIFY_MODIFIED);
+      else if (shared) { pstat(GG_PS_NULLIFY_SHARED); pstat(GG_PS_INV_UNICAST); pstat(GG_PS_INV_SHARERS_UNICAST, n); }
+      else pstat(GG_PS_NULLIFY_UNCACHED);
+    }
+  }
+  // the completed front of a FIFO: updateProcessingFinishTime + updateShmemReqLatencyCounters (:982-1014)
+  __device__ __forceinline__ void mo_retire(int32_t f, uint64_t t)
+  {
+    const CReq r = rq_get(f);
+    const CReqX x = rqx_get(f);
+    const uint64_t fin = r.time < t ? t : r.time;
+    const uint64_t ser = x.start - x.arrival, proc = fin - x.start;
+    const bool inv0 = x.ds0 == DS_OWNED || x.ds0 == DS_SHARED;
+    if (r.type == M_EX_REQ) {
+      pstat(GG_PS_EXREQ_SERIALIZATION_PS, ser); pstat(GG_PS_EXREQ_PROCESSING_PS, proc);
+      if (inv0 && !x.upg) pstat(GG_PS_INV_PROCESSING_UNICAST_PS, proc);
+    } else if (r.type == M_SH_REQ) {
+      pstat(GG_PS_SHREQ_SERIALIZATION_PS, ser); pstat(GG_PS_SHREQ_PROCESSING_PS, proc);
+    } else {
+      pstat(GG_PS_NULLIFY_SERIALIZATION_PS, ser); pstat(GG_PS_NULLIFY_PROCESSING_PS, proc);
+      if (inv0) pstat(GG_PS_INV_PROCESSING_UNICAST_PS, proc);
+    }
+  }
+  // retrieveDataAndSendToL2Cache (:563-595): the cached data, else DRAM
+  __device__ __forceinline__ void mo_retrieve(uint32_t type, uint32_t rx, uint64_t a, uint64_t& t)
+  {
+    const int32_t ci = cdl_find(a);
+    if (ci >= 0) { send(rx, type, rx, a, t); cdl_erase_at(ci); }
+    else { t += dram_ps(t); send(rx, type, rx, a, t); }
+  }
+  // restartShmemReq (:797-833): the work item it continues with (W_NONE if none)
+  __device__ __forceinline__ Work mo_restart(uint32_t sender, int32_t f, int32_t h, uint64_t a, uint64_t& t)
+  {
+    uint32_t type, req;
+    front_update(f, t, type, req);                                  // updateProcessingFinishTime + updateCurrTime(getTime())
+    const uint32_t ds = e_state(h);
+    if (type == M_EX_REQ) return ds == DS_UNCACHED ? Work{a, W_CONT, M_EX_REQ, req, 0, h} : Work{a, W_NONE, 0, 0, 0, NO_ENT};
+    if (type == M_SH_REQ) {
+      const int32_t sh = rqx[f].sharer;
+      if (sh < 0) { fail(); return Work{a, W_NONE, 0, 0, 0, NO_ENT}; }
+      if ((int32_t)sender != sh) return Work{a, W_NONE, 0, 0, 0, NO_ENT};
+      rqx[f].sharer = -1;
+      return Work{a, W_CONT, M_SH_REQ, req, 0, h};
+    }
+    return ds == DS_UNCACHED ? Work{a, W_NULLIFY, 0, req, 0, h} : Work{a, W_NONE, 0, 0, 0, NO_ENT};
+  }
+  // the MOSI call chains as a work loop (Work::cached = first_call, Work::h =
+  // the entry when the reference passes one, else NO_ENT)
+  __device__ __forceinline__ void directory_run_mo(Work w, uint64_t& t)
+  {
+    Work* stack = sl.wstack;
+    int sp = 0;
+    for (;;) {
+      if (failed) return;
+      switch (w.kind) {
+      case W_PROC: {                     // processEx/ShReqFromL2Cache (…mosi :299-533): no entry given
+        int32_t h = dget(w.addr, t);
+        if (h == NO_ENT) {               // processDirectoryEntryAllocationReq (:165-209)
+          const uint64_t msg_time = t;
+          if (dget(w.addr, t) != NO_ENT) fail();   // getReplacementCandidates' assert (directory_cache.cc:161)
+          const uint32_t base = dset(w.addr) * P.dassoc;
+          const DEnt* d = S.dir + (size_t)lt * P.E;
+          eflush();
+          uint32_t key = ~0u;
+          if (ln < P.dassoc) {
+            const DEnt e = d[base + ln];
+            uint32_t qc = 0;
+            for (uint32_t i = 0; i < nrq; ++i) qc += (rq_addr(i) == e.addr);
+            if (qc == 0) key = ((uint32_t)e.nsh << 8) | ln;
+          }
+          key = wave_min(key);
+          if (key == ~0u) { fail(); return; }
+          const uint64_t replaced = d[base + (key & 0xFFu)].addr;
+          h = dreplace(replaced, w.addr, t);
+          if (h == NO_ENT) return;
+          qpush(replaced, msg_time, M_NULLIFY_REQ, w.requester);
+          if (qcount(replaced) != 1) fail();
+          if (sp >= WSTACK) { fail(GG_DERR_CAP); return; }
+          Work c = w; c.kind = W_CONT; c.h = h;
+          stack[sp++] = c;
+          w = Work{replaced, W_NULLIFY, 0, w.requester, 1, NO_ENT};
+          continue;
+        }
+        w.kind = W_CONT; w.h = h;
+        continue;
+      }
+      case W_CONT: {                     // the directory-state switch
+        const int32_t f = qfront(w.addr);
+        if (f < 0) { fail(); return; }
+        if (w.cached) mo_event(w.h, f, w.type, w.requester);
+        const uint32_t ds = e_state(w.h), n = e_nsh(w.h);
+        w.kind = W_NONE;
+        if (w.type == M_EX_REQ) {
+          if (ds == DS_MODIFIED) {
+            send((uint32_t)e_owner(w.h), M_FLUSH_REQ, w.requester, w.addr, t);
+          } else if (ds == DS_OWNED) {
+            const int32_t o = e_owner(w.h);
+            if (o == (int32_t)w.requester && n == 1) {
+              set_state(w.h, DS_MODIFIED);
+              send(w.requester, M_UPGRADE_REP, w.requester, w.addr, t);
+              w.kind = W_NEXT;
+            } else {
+              send_sharers(w.h, M_IFC_REQ, w.requester, w.addr, t, (uint32_t)o);   // FLUSH to the owner, INV to the rest
+            }
+          } else if (ds == DS_SHARED) {
+            if (n == 0) fail();
+            if (n == 1 && has(w.h, w.requester)) {
+              set_owner(w.h, (int32_t)w.requester);
+              set_state(w.h, DS_MODIFIED);
+              send(w.requester, M_UPGRADE_REP, w.requester, w.addr, t);
+              w.kind = W_NEXT;
+            } else {
+              const int32_t one = one_sharer(w.h);
+              send_sharers(w.h, M_IFC_REQ, w.requester, w.addr, t, (uint32_t)one);
+            }
+          } else {
+            if (n != 0) fail();
+            add_sharer(w.h, w.requester);
+            set_owner(w.h, (int32_t)w.requester);
+            set_state(w.h, DS_MODIFIED);
+            mo_retrieve(M_EX_REP, w.requester, w.addr, t);
+            w.kind = W_NEXT;
+          }
+        } else {
+          if (ds == DS_MODIFIED) {
+            const int32_t o = e_owner(w.h);
+            send((uint32_t)o, M_WB_REQ, w.requester, w.addr, t);
+            rqx[f].sharer = o;
+          } else if (ds == DS_OWNED || ds == DS_SHARED) {
+            if (n == 0) fail();
+            const int32_t sh = one_sharer(w.h);            // the sharer can be the owner
+            add_sharer(w.h, w.requester);
+            if (cdl_find(w.addr) < 0) {
+              remove_sharer(w.h, w.requester);             // not complete yet: the data comes from the sharer
+              send((uint32_t)sh, M_WB_REQ, w.requester, w.addr, t);
+              rqx[f].sharer = sh;
+            } else {
+              mo_retrieve(M_SH_REP, w.requester, w.addr, t);
+              w.kind = W_NEXT;
+            }
+          } else {
+            add_sharer(w.h, w.requester);
+            set_state(w.h, DS_SHARED);
+            mo_retrieve(M_SH_REP, w.requester, w.addr, t);
+            w.kind = W_NEXT;
+          }
+        }
+        w.h = NO_ENT;
+        continue;
+      }
+      case W_NEXT: {                     // processNextReqFromL2Cache (…mosi :117-163)
+        if (qcount(w.addr) < 1) { fail(); return; }
+        mo_retire(qfront(w.addr), t);
+        qpop(w.addr);
+        if (cdl_find(w.addr) >= 0) fail();           // assert(_cached_data_list.lookup(address) == NULL)
+        const int32_t f = qfront(w.addr);
+        if (f < 0) { w.kind = W_NONE; continue; }
+        // updateProcessingStartTime + updateCurrTime(getTime())
+        CReq r = rq_get(f);
+        if (rqx[f].start < t) {
+          rqx[f].start = t; r.time = t;
+          if (rq_lds) wave_sync();
+          if (rq_lds) lrq()[f].time = t; else rqg[f].time = t;
+          if (rq_lds) wave_sync();
+        }
+        if (t < r.time) t = r.time;
+        if (r.type != M_EX_REQ && r.type != M_SH_REQ) { fail(); return; }
+        w = Work{w.addr, W_PROC, r.type, r.requester, 1, NO_ENT};
+        continue;
+      }
+      case W_NULLIFY: {                  // processNullifyReq (…mosi :211-297)
+        const int32_t h = w.h != NO_ENT ? w.h : dget(w.addr, t);
+        if (h == NO_ENT) { fail(); return; }
+        if (w.cached) {
+          const int32_t f = qfront(w.addr);
+          if (f < 0) { fail(); return; }
+          mo_event(h, f, M_NULLIFY_REQ, w.requester);
+        }
+        const uint32_t ds = e_state(h);
+        w.h = NO_ENT;
+        if (ds == DS_MODIFIED) {
+          send((uint32_t)e_owner(h), M_FLUSH_REQ, w.requester, w.addr, t);
+          w.kind = W_NONE;
+        } else if (ds == DS_OWNED) {
+          const int32_t o = e_owner(h);
+          if (o < 0) fail();
+          send_sharers(h, M_IFC_REQ, w.requester, w.addr, t, (uint32_t)o);
+          w.kind = W_NONE;
+        } else if (ds == DS_SHARED) {
+          if (e_owner(h) >= 0) fail();
+          send_sharers(h, M_INV_REQ, w.requester, w.addr, t);
+          w.kind = W_NONE;
+        } else {
+          const int32_t ci = cdl_find(w.addr);
+          if (ci >= 0) { (void)dram_ps(t); cdl_erase_at(ci); }      // sendDataToDram
+          dinvalidate(w.addr);
+          w.kind = W_NEXT;
+        }
+        continue;
+      }
+      default:
+        if (sp == 0) return;
+        w = stack[--sp];
+        continue;
+      }
+    }
+  }
+  // handleMsgFromL2Cache (…mosi :49-115) + processInv/Flush/WbRepFromL2Cache (:597-795)
+  __device__ __forceinline__ void directory_msg_mo(const HMsg& m)
+  {
+    uint64_t t = m.arrival_ps;
+    const uint64_t a = m.addr;
+    const uint32_t src = m.src;
+    Work w{a, W_NONE, 0, 0, 0, NO_ENT};
+    if (m.type == M_EX_REQ || m.type == M_SH_REQ) {
+      qpush(a, t, m.type, m.requester);
+      if (qcount(a) == 1) {
+        if (cdl_find(a) >= 0) fail();
+        w = Work{a, W_PROC, m.type, m.requester, 1, NO_ENT};
+      }
+    } else {
+      const int32_t h = dget(a, t);
+      if (h == NO_ENT) { fail(); return; }
+      const uint32_t ds = e_state(h);
+      if (m.type == M_INV_REP) {
+        if (ds == DS_OWNED) {
+          if ((int32_t)src == e_owner(h) || e_nsh(h) == 0) fail();
+          remove_sharer(h, src);
+          if (e_nsh(h) == 0) fail();
+        } else if (ds == DS_SHARED) {
+          if (e_owner(h) >= 0 || e_nsh(h) == 0) fail();
+          remove_sharer(h, src);
+          if (e_nsh(h) == 0) set_state(h, DS_UNCACHED);
+        } else { fail(); return; }
+        const int32_t f = qfront(a);
+        if (f >= 0) w = mo_restart(src, f, h, a, t);
+      } else if (m.type == M_FLUSH_REP) {
+        if (ds == DS_MODIFIED) {
+          if ((int32_t)src != e_owner(h)) fail();
+          remove_sharer(h, src);
+          set_owner(h, -1);
+          set_state(h, DS_UNCACHED);
+        } else if (ds == DS_OWNED) {
+          const int32_t o = e_owner(h);
+          if (o < 0 || e_nsh(h) == 0) fail();
+          remove_sharer(h, src);
+          if ((int32_t)src == o) { set_owner(h, -1); set_state(h, e_nsh(h) > 0 ? DS_SHARED : DS_UNCACHED); }
+        } else if (ds == DS_SHARED) {
+          if (e_owner(h) >= 0 || e_nsh(h) == 0) fail();
+          remove_sharer(h, src);
+          if (e_nsh(h) == 0) set_state(h, DS_UNCACHED);
+        } else { fail(); return; }
+        const int32_t f = qfront(a);
+        if (f >= 0) {
+          cdl_insert(a);
+          const uint32_t ds1 = e_state(h);
+          if (rq_get(f).type == M_SH_REQ && (ds == DS_MODIFIED || ds == DS_OWNED) && (ds1 == DS_SHARED || ds1 == DS_UNCACHED))
+            (void)dram_ps(t);                                        // sendDataToDram
+          w = mo_restart(src, f, h, a, t);
+        } else {
+          (void)dram_ps(t);                                          // just an eviction: to DRAM
+        }
+      } else if (m.type == M_WB_REP) {
+        if (ds == DS_MODIFIED) {
+          if ((int32_t)src != e_owner(h) || qcount(a) == 0) fail();
+          set_state(h, DS_OWNED);
+        } else if (ds == DS_OWNED) {
+          if (!has(h, src)) fail();
+        } else if (ds == DS_SHARED) {
+          if (e_owner(h) >= 0 || !has(h, src)) fail();
+        } else { fail(); return; }
+        const int32_t f = qfront(a);
+        if (f < 0) { fail(); return; }                                 // "WB_REP, NO requester"
+        cdl_insert(a);
+        w = mo_restart(src, f, h, a, t);
+      } else {
+        fail();
+        return;
+      }
+    }
+    if (w.kind != W_NONE) directory_run_mo(w, t);
+  }
+  // L2CacheCntlr::insertCacheLine (…mosi/l2_cache_cntlr.cc:95-149) + updateEvictionCounters (:605-636)
+  __device__ __forceinline__ void l2_insert_mo(uint64_t a, uint32_t cs, uint64_t t)
+  {
+    bool ev; uint64_t ea = 0; uint32_t es = 0, el = 0;
+    if (!L2.insert(a, cs, 1, ev, ea, es, el)) { fail(); return; }
+    if (!ev) return;
+    const bool dirty = es == ST_M || es == ST_O;
+    if (!dirty && es != ST_S) { fail(); return; }
+    pstat(GG_PS_L2_EVICTIONS);
+    pstat(cs == ST_M ? (dirty ? GG_PS_L2_DIRTY_EVICTIONS_EXREQ : GG_PS_L2_CLEAN_EVICTIONS_EXREQ)
+                     : (dirty ? GG_PS_L2_DIRTY_EVICTIONS_SHREQ : GG_PS_L2_CLEAN_EVICTIONS_SHREQ));
+    if (el) l1_invalidate(ea);
+    send(home(ea), dirty ? M_FLUSH_REP : M_INV_REP, tile, ea, t);
+  }
+  // L2CacheCntlr::handleMsgFromDramDirectory (…mosi :287-594) + the core's second attempt
+  __device__ __forceinline__ void l2_msg_mo(const HMsg& m)
+  {
+    uint64_t t = m.arrival_ps;
+    const uint64_t a = m.addr;
+    uint32_t type = m.type;
+    if (type == M_IFC_REQ) type = m.single_rx == tile ? M_FLUSH_REQ : M_INV_REQ;   // (:581-594)
+    if (type == M_EX_REP || type == M_SH_REP || type == M_UPGRADE_REP) {
+      if (!blocked || out_addr != a) { fail(); return; }
+      if (type != M_UPGRADE_REP) {                                   // insertCacheLineInHierarchy (:210-224)
+        const uint32_t cs = type == M_EX_REP ? ST_M : ST_S;
+        l2_insert_mo(a, cs, t);
+        insert_in_l1(a, cs);
+      } else {                                                       // processUpgradeRepFromDramDirectory (:370-412)
+        uint32_t c2, loc;
+        L2.get(a, c2, loc);
+        if (c2 != ST_S && c2 != ST_O) fail();
+        if (!loc) {
+          if (!L2.access(a, false)) fail();                          // readCacheLine
+          insert_in_l1(a, ST_M);
+          loc = 1;
+        } else {
+          uint32_t c1, l1;                                           // setCacheLineState (…mosi/l1:260-273)
+          L1.get(a, c1, l1);
+          if (c1 == ST_I) fail();
+          if (!L1.set(a, ST_M, 0)) fail();
+        }
+        if (!L2.set(a, ST_M, loc)) fail();
+      }
+      if (out_time > t) fail();
+      t += P.lat_l2d;
+      out_addr = INV_ADDR;
+      const bool wr = (S.meta[rec] & GG_META_WRITE) != 0;          // access_num == 2 (…mosi/l1:105-126)
+      uint32_t c1, l1;
+      L1.get(a, c1, l1);
+      const bool hit = wr ? c1 == ST_M : c1 != ST_I;
+      if (!hit) { fail(); return; }
+      t += P.lat_l1d;
+      l1_access(a, wr);
+      blocked = 0;
+      finish(pend_start, t, GG_LVL_DIR);
+      return;
+    }
+    uint32_t c2, loc;
+    L2.get(a, c2, loc);
+    if (c2 == ST_I) { t += P.lat_l2t; return; }                      // tags only; full map: no reply expected
+    if (type == M_INV_REQ) {                                         // (:414-468)
+      if (c2 != ST_S) { fail(); return; }
+      t += P.lat_l2t;
+      pstat(GG_PS_L2_INVALIDATIONS);
+      if (loc) { t += P.lat_l1t; l1_invalidate(a); }
+      if (!L2.set(a, ST_I, 0)) fail();
+      send(m.src, M_INV_REP, m.requester, a, t);
+    } else if (type == M_FLUSH_REQ) {                                // (MODIFIED, OWNED, SHARED) -> INVALID (:470-527)
+      t += P.lat_l2d;
+      pstat(GG_PS_L2_INVALIDATIONS);
+      if (loc) { t += P.lat_l1t; l1_invalidate(a); }
+      if (!L2.access(a, false)) fail();
+      if (!L2.set(a, ST_I, 0)) fail();
+      send(m.src, M_FLUSH_REP, m.requester, a, t);
+    } else if (type == M_WB_REQ) {                                   // M -> O, O -> O, S -> S (:529-579)
+      t += P.lat_l2d;
+      const uint32_t ns = c2 == ST_M ? ST_O : c2;
+      if (loc) {
+        t += P.lat_l1t;
+        uint32_t c1, l1;
+        L1.get(a, c1, l1);
+        if (c1 == ST_I) fail();
+        if (!L1.set(a, ns, 0)) fail();
+      }
+      if (!L2.access(a, false)) fail();
+      if (!L2.set(a, ns, loc)) fail();
+      send(m.src, M_WB_REP, m.requester, a, t);
+    } else {
+      fail();
+    }
+  }
+
   // store-only write back of what the step changed: the counters were
   // loaded with the tile, and an idle tile (most of them in a step) leaves
   // its lines clean, so the launch's end writes back only the active tiles'
@@ -1527,6 +2049,10 @@ struct Tile {
       if (seq != p0.seq) S.ts[lt].seq = seq;
       if (nrep != p0.nrep) S.ts[lt].nrep = nrep;
       if (nrq != p0.nrq) S.ts[lt].nrq = nrq;
+    }
+    if constexpr (MO) {
+      if (ln < GG_NUM_PROTO_STATS && pd) S.ps[(size_t)lt * GG_NUM_PROTO_STATS + ln] += pd;
+      if (ln == 0 && ncdl != ncdl0) S.ncdl[lt] = ncdl;
     }
   }
 };
@@ -1726,14 +2252,14 @@ __device__ __forceinline__ void quantum_end(const CP& P, const CS& S, uint32_t L
 struct TraceWin { uint64_t wbase, wa; uint32_t wm; };
 constexpr uint64_t kNsFin = ~0ull, kNsBlk = ~0ull - 1;   // next start of a finished / blocked tile
 
-template <bool LC, bool HR, bool F, class SL, class H>
+template <bool LC, bool HR, bool F, bool MO, class SL, class H>
 __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t lt, uint32_t k, uint32_t L, uint64_t barrier,
                                           TraceWin& W, SL& sl, uint8_t* clds, const TilePre& pre, const H& hk,
                                           uint32_t na, uint32_t ni, uint64_t rel);
 
 // LC: cache state in LDS; HR: L1 hit runs (persistent small meshes, where
 // long runs of hits between misses pay for the window look-up)
-template <bool LC, bool HR, bool F = false>
+template <bool LC, bool HR, bool F = false, bool MO = false>
 __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, uint32_t devloop, uint64_t barrier_arg,
                                           TraceWin& W)
 {
@@ -1776,7 +2302,7 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
   const GHooks hk{P, S};
   const uint32_t na = P.net == GG_NET_EMESH_HOP_BY_HOP ? (p ? pre.narv1 : pre.narv0) : 0u;
   const uint32_t ni = p ? pre.ninb1 : pre.ninb0;
-  tile_step<LC, HR, F>(P, S, lt, k, L, barrier, W, sl, smem + P.cache_lds_off, pre, hk, na, ni,
+  tile_step<LC, HR, F, MO>(P, S, lt, k, L, barrier, W, sl, smem + P.cache_lds_off, pre, hk, na, ni,
                     devloop && k == 0 ? qsv[QS_REL] : 0ull);
 }
 
@@ -1815,7 +2341,7 @@ __device__ __forceinline__ void publish_hbh_lds(TT& T, gg_cmsg* cur, uint32_t nl
     const uint32_t i = i0 + ln;
     uint64_t e = 0, ts = 0;
     bool self = false, net = false;
-    if (i < nloc) { e = sl.x3[i]; ts = sl.x4[i]; self = (uint32_t)((e >> 32) & 0x7FFFFFFFu) == tile; net = !self; }
+    if (i < nloc) { e = sl.x3[i]; ts = sl.x4[i]; self = (uint32_t)((e >> 32) & 0x3FFFFFFFu) == tile; net = !self; }
     const uint32_t r = (uint32_t)e;
     if (self) {
       uint32_t* lp = inb(S, p ^ 1u) + (size_t)lt * P.IC;
@@ -1829,14 +2355,14 @@ __device__ __forceinline__ void publish_hbh_lds(TT& T, gg_cmsg* cur, uint32_t nl
     if (m && regq && !rq_loaded) { rq.load_h0(gq, gnd, P.np.max_size, 1, P.np.analytical != 0, ln); rq_loaded = true; }
     const uint32_t pos = nn + (uint32_t)__builtin_popcountll(m & ((1ull << ln) - 1));
     if (net) {
-      const uint32_t d = (uint32_t)((e >> 32) & 0x7FFFFFFFu), dx = d % P.mw, dy = d / P.mw;
+      const uint32_t d = (uint32_t)((e >> 32) & 0x3FFFFFFFu), dx = d % P.mw, dy = d / P.mw;
       const bool is_x = cx != dx;
       const uint32_t sg = is_x ? T.p0.segx * 2 + (dx > cx ? 1u : 0u) : T.p0.segy * 2 + (dy > cy ? 1u : 0u);
-      const uint64_t hd = e >> 63;
+      const uint64_t lc = e >> 62;                        // length class
       sl.x1[pos] = ts;
-      sl.x2[pos] = ((uint64_t)(seq0 + i) << 1) | hd;      // the sender is this tile: its seq orders equal times
+      sl.x2[pos] = ((uint64_t)(seq0 + i) << 2) | lc;      // the sender is this tile: its seq orders equal times
       sl.i1[pos] = r;
-      sl.x4[pos] = hd << 32;                              // (read above for slot i >= pos, in program order)
+      sl.x4[pos] = lc << 32;                              // (read above for slot i >= pos, in program order)
       // onto the X (or Y) run the packet enters (hk.seg_slot, checked at the store)
       const uint32_t j = atomicAdd(&(is_x ? S.nxl : S.nyl)[sg], 1u);
       uint32_t* lp = (is_x ? S.xl : S.yl) + (size_t)sg * P.seg_cap;
@@ -1874,7 +2400,7 @@ __device__ __forceinline__ void publish_hbh_lds(TT& T, gg_cmsg* cur, uint32_t nl
       const uint32_t e = sl.i2[c0 + ln];
       r = sl.i1[e];
       sp = sl.x1[e];
-      bits = (sl.x4[e] >> 32) ? P.bits_data : P.bits_req;
+      bits = class_bits(P, (uint32_t)(sl.x4[e] >> 32));
       nf_ = (uint32_t)nflits(P.np, bits);
     }
     uint64_t oq = 0;
@@ -1911,14 +2437,14 @@ __device__ __forceinline__ void publish_hbh_lds(TT& T, gg_cmsg* cur, uint32_t nl
 // the calling wave: the SELF port + receive of the packets that
 // reached the tile (na), the inbox (ni records), the trace, publish, write
 // back.  Deliveries go through the hooks.
-template <bool LC, bool HR, bool F, class SL, class H>
+template <bool LC, bool HR, bool F, bool MO, class SL, class H>
 __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t lt, uint32_t k, uint32_t L, uint64_t barrier,
                                           TraceWin& W, SL& sl, uint8_t* clds, const TilePre& pre, const H& hk,
                                           uint32_t na, uint32_t ni, uint64_t rel)
 {
   const uint32_t ln = lane_id(), p = k & 1u;
   PROF_T0();
-  Tile<SL, H, F> T(P, S, lt, p, sl, hk, clds, std::integral_constant<bool, LC>(), pre);
+  Tile<SL, H, F, MO> T(P, S, lt, p, sl, hk, clds, std::integral_constant<bool, LC>(), pre);
   T.tr_on = S.trs != nullptr && L < S.tr_n;
   const gg_cmsg* prev = pool(S, p ^ 1u);     // records delivered to this step
   uint64_t* gscr = S.gscr + (size_t)lt * 6 * P.IC;
@@ -2008,7 +2534,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
         const uint32_t i = i0 + 64 * u;
         if (i < na) {
           t_[i] = ta[u]; s_[i] = sa[u]; z_a[i] = za[u]; i_[i] = rr[u];
-          k_[i] = ((uint64_t)sr[u] << 33) | ((uint64_t)sq[u] << 1) | (has_data(ty[u]) ? 1u : 0u);
+          k_[i] = ((uint64_t)sr[u] << 34) | ((uint64_t)sq[u] << 2) | len_class(ty[u]);
         }
       }
     }
@@ -2034,7 +2560,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
         e = o_[c0 + ln];                                         // local index of the packet of rank c0 + ln
         r = i_[e];
         tv = t_[e]; z_ = z_a[e]; sp = s_[e];
-        bits = (k_[e] & 1u) ? P.bits_data : P.bits_req;
+        bits = class_bits(P, (uint32_t)(k_[e] & 3u));
         nf_ = (uint32_t)nflits(P.np, bits);
       }
       uint64_t ot = tv, oz = z_;
@@ -2062,7 +2588,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
       if (S.trs) _sf = __builtin_amdgcn_s_memtime();
       if (ln < cnt) {
         pv[r].arrival_ps = ot; pv[r].zero_load_ps = oz;
-        if (LD && self_keys) { const uint64_t kk = k_[e]; t_[e] = ot; s_[e] = ((kk >> 33) << 32) | ((kk >> 1) & 0xFFFFFFFFull); }
+        if (LD && self_keys) { const uint64_t kk = k_[e]; t_[e] = ot; s_[e] = ((kk >> 34) << 32) | ((kk >> 2) & 0xFFFFFFFFull); }
       }
     }
     };
@@ -2161,14 +2687,17 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
           const gg_cmsg& g = prev[sl.i1[e]];
           m.addr = g.addr; m.type = g.type; m.requester = g.requester;
         }
+        m.single_rx = MO && m.type == M_IFC_REQ ? prev[sl.i1[e]].single_rx : 0u;
       } else {
         const gg_cmsg& g = prev[gi_[go_[j]]];
         m.arrival_ps = g.arrival_ps; m.src = g.src; m.addr = g.addr; m.type = g.type; m.requester = g.requester;
+        m.single_rx = MO ? g.single_rx : 0u;
       }
       T.stat(GG_CT_MSGS_RECEIVED, 1);
       const uint64_t h0 = S.trs ? __builtin_amdgcn_s_memtime() : 0;
       const bool dm = to_directory(m.type);
-      if (dm) T.directory_msg(m); else T.l2_msg(m);
+      if constexpr (MO) { if (dm) T.directory_msg_mo(m); else T.l2_msg_mo(m); }
+      else { if (dm) T.directory_msg(m); else T.l2_msg(m); }
       if (S.trs) {
         const uint64_t h1 = __builtin_amdgcn_s_memtime();
         if (dm) { _hd += h1 - h0; _hn += 1; } else { _hl += h1 - h0; _hn += 1ull << 32; }
@@ -2260,7 +2789,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
         const uint32_t r = i_[i];
         gg_cmsg m = cur[r];
         uint64_t zl;
-        m.arrival_ps = route_closed_form(P.np, m.src, m.dst, has_data(m.type) ? P.bits_data : P.bits_req, m.send_ps,
+        m.arrival_ps = route_closed_form(P.np, m.src, m.dst, msg_bits(P, m.type), m.send_ps,
                                          zl, S.ctr);
         m.zero_load_ps = zl;
         if (m.src == m.dst) ri_self++; else ri_net++;
@@ -2334,7 +2863,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
             r = o_[c0 + ln];
             const gg_cmsg& g = cur[r];
             sp = g.send_ps;
-            bits = has_data(g.type) ? P.bits_data : P.bits_req;
+            bits = msg_bits(P, g.type);
             nf_ = (uint32_t)nflits(P.np, bits);
           }
           uint64_t oq = 0;
@@ -2626,7 +3155,7 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
     W.Pt[i] = m.arrival_ps; W.Ph[i] = m.send_ps; W.Pk[i] = ((uint64_t)m.src << 32) | m.seq; W.Pz[i] = m.zero_load_ps;
     W.Pi[i] = r; W.Pp[i] = pos_of(m.hop); W.Pd[i] = pos_of(m.dst);
     if (m.arrival_ps >> 51) atomicOr(S.err, GG_DERR_CAP);        // batch keys are time << 12 | rank
-    W.Pf[i] = (uint32_t)nflits(P.np, has_data(m.type) ? P.bits_data : P.bits_req);
+    W.Pf[i] = (uint32_t)nflits(P.np, msg_bits(P, m.type));
   }
   if (!sweep)                     // the pipeline's moving state: one word per packet (W.Qt, unused by it)
     for (uint32_t i = tid; i < n; i += nthr) W.Qt[i] = pipe_word(W.Pt[i], W.Pp[i], 0u);
@@ -3089,6 +3618,8 @@ __device__ __forceinline__ void import_one(const CP& P, const CS& S, const gg_cm
 void launch_step(const CP& P, const CS& S, size_t lds, hipStream_t s, uint32_t L, uint32_t devloop, uint64_t barrier);
 void launch_step_fast(const CP& P, const CS& S, size_t lds, hipStream_t s, uint32_t L, uint32_t devloop, uint64_t barrier);
 hipError_t step_fast_set_lds(size_t lds);
+void launch_step_mosi(const CP& P, const CS& S, size_t lds, hipStream_t s, uint32_t L, uint32_t devloop, uint64_t barrier);
+hipError_t step_mosi_set_lds(size_t lds);
 void launch_persist(bool lc, const CP& P, const CS& S, size_t lds, hipStream_t s, uint32_t L0, uint32_t L1);
 hipError_t step_set_lds(size_t step_lds, size_t persist_lc_lds, size_t persist_lds);
 hipError_t persist_occupancy(bool lc, size_t lds, int* per_cu);

@@ -52,6 +52,8 @@ __global__ void __launch_bounds__(256) k_c_reset(CP P, CS S, const uint64_t* off
   for (size_t i = tid; i < P.E; i += nt) S.dir[(size_t)lt * P.E + i] = DEnt{INV_ADDR, -1, DS_UNCACHED, 0};
   if (tid < 2 * GG_NUM_CACHE_COUNTERS) S.cc[(size_t)lt * 2 * GG_NUM_CACHE_COUNTERS + tid] = 0;
   if (tid < GG_NUM_TILE_STATS) S.st[(size_t)lt * GG_NUM_TILE_STATS + tid] = 0;
+  if (P.mosi && tid < GG_NUM_PROTO_STATS) S.ps[(size_t)lt * GG_NUM_PROTO_STATS + tid] = 0;
+  if (P.mosi && tid == 0) S.ncdl[lt] = 0;
   if (tid == 0) {
     S.ts[lt].nrep = 0; S.ts[lt].nrq = 0;
     const uint32_t tile = S.gtile[lt];
@@ -427,6 +429,9 @@ static gg_status coh_alloc(gg_ctx* ctx)
   const uint32_t idb = P.T > 1 ? (uint32_t)clog2(P.T) : 0;
   P.bits_req = 2 * idb + 4 + 48;
   P.bits_data = P.bits_req + 8 * c.line_size;
+  P.bits_ifc = P.bits_req + idb;                 // …mosi/shmem_msg.cc:137-139: + the single receiver
+  if (c.protocol > GG_PROTO_MOSI) return gg_fail(GG_ERR_INVALID, "protocol must be GG_PROTO_MSI or GG_PROTO_MOSI");
+  P.mosi = c.protocol == GG_PROTO_MOSI ? 1u : 0u;
   P.dram_qm = c.dram_queue_model_enabled;
   P.dram_qtype = c.dram_queue_model_type;
   P.dram_qaux = hq_aux(c.dram_queue_model_type, c.basic_moving_avg, c.history_list_no_interleaving);
@@ -530,7 +535,8 @@ static gg_status coh_alloc(gg_ctx* ctx)
   A(l2_tag, L * P.s2 * P.a2); A(l2_meta, L * P.s2 * P.a2); A(l2_rr, L * P.s2);
   A(cc, L * 2 * GG_NUM_CACHE_COUNTERS); A(st, L * GG_NUM_TILE_STATS);
   // miss-type tracking (default off): one address table per (tile, cache)
-  P.mt1 = ctx->cfg.l1i_track_miss_types ? 1u : 0u;
+  // (MSI's L1CacheCntlr hands the L1-D the L1-I flag, l1_cache_cntlr.cc:69; MOSI its own, …mosi/l1:68)
+  P.mt1 = (P.mosi ? ctx->cfg.l1d_track_miss_types : ctx->cfg.l1i_track_miss_types) ? 1u : 0u;
   P.mt2 = ctx->cfg.l2_track_miss_types ? 1u : 0u;
   {
     // the fast step instance: every queue it serves a history tree held in
@@ -539,7 +545,7 @@ static gg_status coh_alloc(gg_ctx* ctx)
     const bool rq_net = !P.np.qm || (P.np.qtype == GG_QM_HISTORY_TREE && P.np.max_size <= kQMax);
     const bool rq_dram = !P.dram_qm || (P.dram_qtype == GG_QM_HISTORY_TREE && P.max_list <= kQMax);
     const char* nf = getenv("GG_COH_NO_FAST");
-    P.fast = rq_net && rq_dram && !P.mt1 && !P.mt2 && !(nf && atoi(nf)) ? 1u : 0u;
+    P.fast = rq_net && rq_dram && !P.mt1 && !P.mt2 && !P.mosi && !(nf && atoi(nf)) ? 1u : 0u;
   }
   if (P.mt1 || P.mt2) {
     const uint32_t lines = ctx->cfg.miss_track_lines ? ctx->cfg.miss_track_lines : 65536u;
@@ -551,6 +557,9 @@ static gg_status coh_alloc(gg_ctx* ctx)
   A(dir, L * P.E); A(dsh, L * P.E * P.W);
   A(rep, L * P.R); A(rsh, L * P.R * P.W);
   A(rq, L * P.QC);
+  if (P.mosi) {
+    A(rqx, L * P.QC); A(drng, L * P.E); A(rrng, L * P.R); A(cdl, L * kCdl); A(ncdl, L); A(ps, L * GG_NUM_PROTO_STATS);
+  }
   A(dq, L); A(dnd, L * P.max_list);
   A(pool0, P.msg_cap); A(pool1, P.msg_cap); A(npool, 2);
   A(inb0, L * P.IC); A(inb1, L * P.IC); A(cnt4, L * 4);
@@ -892,7 +901,7 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
   const char* np_env = getenv("GG_COH_NO_PERSIST");
   const char* nl_env = getenv("GG_COH_NO_LDS_CACHE");
   const bool plc = C->persist_lc && !(nl_env && atoi(nl_env));
-  bool persist = P.L <= kPersistTiles && !(np_env && atoi(np_env));
+  bool persist = P.L <= kPersistTiles && !P.mosi && !(np_env && atoi(np_env));   // (no persistent MOSI instance)
   if (persist) {
     // the grid barrier needs every workgroup resident at once (a partitioned
     // device has fewer CUs): else the per-step launches
@@ -1025,6 +1034,26 @@ gg_status gg_coherent_get_miss_types(gg_ctx* ctx, uint64_t* out)
   GG_HIP(hipMemcpy(gtile.data(), C->S.gtile, sizeof(uint32_t) * P.L, hipMemcpyDeviceToHost));
   for (uint32_t l = 0; l < P.L; ++l)
     std::memcpy(out + (size_t)gtile[l] * per, v.data() + (size_t)l * per, sizeof(uint64_t) * per);
+  return coh_check(ctx);
+}
+
+gg_status gg_coherent_get_protocol_stats(gg_ctx* ctx, uint64_t* out)
+{
+  if (!ctx || !out) return gg_fail(GG_ERR_INVALID, "NULL argument");
+  gg_coh_state* C = ctx->coh;
+  if (!C) return gg_fail(GG_ERR_INVALID, "no coherent run on this context");
+  hipSetDevice(ctx->device);
+  const CP& P = C->P;
+  std::memset(out, 0, sizeof(uint64_t) * P.T * GG_NUM_PROTO_STATS);
+  if (!C->S.ps) return GG_OK;                        // MSI: no MOSI counters
+  GG_HIP(hipStreamSynchronize(ctx->last_stream));
+  std::vector<uint64_t> v((size_t)P.L * GG_NUM_PROTO_STATS);
+  std::vector<uint32_t> gtile(P.L);
+  GG_HIP(hipMemcpy(v.data(), C->S.ps, sizeof(uint64_t) * v.size(), hipMemcpyDeviceToHost));
+  GG_HIP(hipMemcpy(gtile.data(), C->S.gtile, sizeof(uint32_t) * P.L, hipMemcpyDeviceToHost));
+  for (uint32_t l = 0; l < P.L; ++l)
+    std::memcpy(out + (size_t)gtile[l] * GG_NUM_PROTO_STATS, v.data() + (size_t)l * GG_NUM_PROTO_STATS,
+                sizeof(uint64_t) * GG_NUM_PROTO_STATS);
   return coh_check(ctx);
 }
 

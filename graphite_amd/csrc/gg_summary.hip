@@ -28,7 +28,13 @@ gg_status gg_dump_summary(gg_ctx* ctx, int format, char* buf, uint64_t cap, uint
   } else if (gg_status e = gg_cache_get_counters(ctx, cc.data())) return e;
   if (gg_status e = gg_noc_get_counters(ctx, nc.data())) return e;
   std::vector<uint64_t> mt;
-  if (coherent && (cfg.l1i_track_miss_types || cfg.l2_track_miss_types)) {
+  const bool mosi = cfg.protocol == GG_PROTO_MOSI;
+  std::vector<uint64_t> ps;
+  if (coherent && mosi) {
+    ps.resize((size_t)T * GG_NUM_PROTO_STATS);
+    if (gg_status e = gg_coherent_get_protocol_stats(ctx, ps.data())) return e;
+  }
+  if (coherent && ((mosi ? cfg.l1d_track_miss_types : cfg.l1i_track_miss_types) || cfg.l2_track_miss_types)) {
     mt.resize((size_t)T * 2 * GG_NUM_MISS_TYPES);
     if (gg_status e = gg_coherent_get_miss_types(ctx, mt.data())) return e;
   }
@@ -46,7 +52,8 @@ gg_status gg_dump_summary(gg_ctx* ctx, int format, char* buf, uint64_t cap, uint
       graphite_amd::writeTileSummary(os, cfg, coherent ? &st[(size_t)t * GG_NUM_TILE_STATS] : nullptr,
                                      &cc[(size_t)t * 2 * GG_NUM_CACHE_COUNTERS], &nc[(size_t)t * GG_NUM_NET_COUNTERS],
                                      core.empty() ? nullptr : &core[(size_t)t * GG_NUM_CORE_STATS],
-                                     mt.empty() ? nullptr : &mt[(size_t)t * 2 * GG_NUM_MISS_TYPES]);
+                                     mt.empty() ? nullptr : &mt[(size_t)t * 2 * GG_NUM_MISS_TYPES],
+                                     ps.empty() ? nullptr : &ps[(size_t)t * GG_NUM_PROTO_STATS]);
       if (format == GG_SUMMARY_TABLE) per_tile.push_back(os.str());
       else all << "Tile " << t << " Summary:" << std::endl << os.str();
     }

@@ -27,6 +27,9 @@
 //       hop-by-hop broadcast tree) on a packet file; hops + network summaries
 //   gg_replay --summary-selftest
 //       prints writeCacheSummary() for fixed counters (no GPU needed)
+//   gg_replay --mosi-summary FILE TILES
+//       prints "Tile t:" + the MOSI L2 / directory controller blocks of the
+//       [TILES][GG_NUM_PROTO_STATS] counters in FILE (no GPU needed)
 #include <rccl/rccl.h>
 
 #include <chrono>
@@ -125,7 +128,19 @@ int main(int argc, char** argv)
       else if (n == "magic") net = GG_NET_MAGIC;
       else { std::fprintf(stderr, "unknown network %s\n", n.c_str()); return 2; }
     }
-    else if (a == "--summary-selftest") {
+    else if (a == "--mosi-summary" && i + 2 < argc) {
+      std::ifstream f(argv[i + 1], std::ios::binary);
+      const uint32_t T = (uint32_t)atoi(argv[i + 2]);
+      std::vector<uint64_t> ps((size_t)T * GG_NUM_PROTO_STATS);
+      f.read(reinterpret_cast<char*>(ps.data()), (std::streamsize)(ps.size() * 8));
+      if (!f) { fprintf(stderr, "cannot read %s\n", argv[i + 1]); return 1; }
+      for (uint32_t t = 0; t < T; ++t) {
+        std::cout << "Tile " << t << ":\n";
+        writeMosiL2CntlrSummary(std::cout, &ps[(size_t)t * GG_NUM_PROTO_STATS]);
+        writeMosiDirectoryCntlrSummary(std::cout, &ps[(size_t)t * GG_NUM_PROTO_STATS]);
+      }
+      return 0;
+    } else if (a == "--summary-selftest") {
       const uint64_t c1[GG_NUM_CACHE_COUNTERS] = {1000, 250, 700, 150, 300, 100, 240, 0, 2600, 900, 760, 1250};
       const uint64_t c2[GG_NUM_CACHE_COUNTERS] = {250, 180, 150, 110, 100, 70, 120, 45, 700, 600, 190, 480};
       const uint64_t z[GG_NUM_CACHE_COUNTERS] = {0};

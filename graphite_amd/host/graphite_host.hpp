@@ -339,17 +339,116 @@ inline void writeDirectorySummary(std::ostream& out, const uint64_t* st, const D
   out << "    Total Back-Invalidations: " << st[GG_CT_DIR_BACK_INVALIDATIONS] << std::endl;
 }
 
+// MOSI: L2CacheCntlr::outputSummary (…mosi/l2_cache_cntlr.cc:638-649) for one
+// tile's GG_PS_* counters
+inline void writeMosiL2CntlrSummary(std::ostream& out, const uint64_t* ps)
+{
+  out << "    L2 Cache Cntlr: " << std::endl;
+  out << "      Total Invalidations: " << ps[GG_PS_L2_INVALIDATIONS] << std::endl;
+  out << "      Total Evictions: " << ps[GG_PS_L2_EVICTIONS] << std::endl;
+  out << "        Exclusive Request - Dirty Evictions: " << ps[GG_PS_L2_DIRTY_EVICTIONS_EXREQ] << std::endl;
+  out << "        Exclusive Request - Clean Evictions: " << ps[GG_PS_L2_CLEAN_EVICTIONS_EXREQ] << std::endl;
+  out << "        Shared Request - Dirty Evictions: " << ps[GG_PS_L2_DIRTY_EVICTIONS_SHREQ] << std::endl;
+  out << "        Shared Request - Clean Evictions: " << ps[GG_PS_L2_CLEAN_EVICTIONS_SHREQ] << std::endl;
+}
+
+// MOSI: DramDirectoryCntlr::outputSummary (…mosi/dram_directory_cntlr.cc:1041-1142).
+// The averages are (float) Time::toNanosec() (ceil of ps / 1000, time_types.h:111-114)
+// over (float) counts; a block with no requests prints its labels only.
+inline void writeMosiDirectoryCntlrSummary(std::ostream& out, const uint64_t* ps)
+{
+  auto ns = [](uint64_t p) { return (float)(uint64_t)ceil((double)p / 1.0e3); };
+  auto avg_ns = [&](uint64_t p, uint64_t n) { return ns(p) / (float)n; };
+  const uint64_t ex = ps[GG_PS_EXREQ], sh = ps[GG_PS_SHREQ], nu = ps[GG_PS_NULLIFY];
+  out << "Dram Directory Cntlr: " << std::endl;
+  out << "    Total Requests: " << ex + sh + nu << std::endl;
+  out << "    Exclusive Requests: " << ex << std::endl;
+  out << "    Shared Requests: " << sh << std::endl;
+  out << "    Nullify Requests: " << nu << std::endl;
+  if (ex > 0) {
+    out << "    Exclusive Request - MODIFIED State: " << ps[GG_PS_EXREQ_MODIFIED] << std::endl;
+    out << "    Exclusive Request - SHARED State: " << ps[GG_PS_EXREQ_SHARED] << std::endl;
+    out << "    Exclusive Request - UNCACHED State: " << ps[GG_PS_EXREQ_UNCACHED] << std::endl;
+    out << "    Exclusive Request - Upgrade Reply: " << ps[GG_PS_EXREQ_UPGRADE] << std::endl;
+    out << "    Average Exclusive Request Serialization Time (in nanoseconds): " << avg_ns(ps[GG_PS_EXREQ_SERIALIZATION_PS], ex) << std::endl;
+    out << "    Average Exclusive Request Processing Time (in nanoseconds): " << avg_ns(ps[GG_PS_EXREQ_PROCESSING_PS], ex) << std::endl;
+  } else {
+    out << "    Exclusive Request - MODIFIED State: " << std::endl;
+    out << "    Exclusive Request - SHARED State: " << std::endl;
+    out << "    Exclusive Request - UNCACHED State: " << std::endl;
+    out << "    Exclusive Request - Upgrade Reply: " << std::endl;
+    out << "    Average Exclusive Request Serialization Time (in nanoseconds): " << std::endl;
+    out << "    Average Exclusive Request Processing Time (in nanoseconds): " << std::endl;
+  }
+  if (sh > 0) {
+    out << "    Shared Request - MODIFIED State: " << ps[GG_PS_SHREQ_MODIFIED] << std::endl;
+    out << "    Shared Request - SHARED State: " << ps[GG_PS_SHREQ_SHARED] << std::endl;
+    out << "    Shared Request - UNCACHED State: " << ps[GG_PS_SHREQ_UNCACHED] << std::endl;
+    out << "    Average Shared Request Serialization Time (in nanoseconds): " << avg_ns(ps[GG_PS_SHREQ_SERIALIZATION_PS], sh) << std::endl;
+    out << "    Average Shared Request Processing Time (in nanoseconds): " << avg_ns(ps[GG_PS_SHREQ_PROCESSING_PS], sh) << std::endl;
+  } else {
+    out << "    Shared Request - MODIFIED State: " << std::endl;
+    out << "    Shared Request - SHARED State: " << std::endl;
+    out << "    Shared Request - UNCACHED State: " << std::endl;
+    out << "    Average Shared Request Serialization Time (in nanoseconds): " << std::endl;
+    out << "    Average Shared Request Processing Time (in nanoseconds): " << std::endl;
+  }
+  if (nu > 0) {
+    out << "    Nullify Request - MODIFIED State: " << ps[GG_PS_NULLIFY_MODIFIED] << std::endl;
+    out << "    Nullify Request - SHARED State: " << ps[GG_PS_NULLIFY_SHARED] << std::endl;
+    out << "    Nullify Request - UNCACHED State: " << ps[GG_PS_NULLIFY_UNCACHED] << std::endl;
+    out << "    Average Nullify Request Serialization Time (in nanoseconds): " << avg_ns(ps[GG_PS_NULLIFY_SERIALIZATION_PS], nu) << std::endl;
+    out << "    Average Nullify Request Processing Time (in nanoseconds): " << avg_ns(ps[GG_PS_NULLIFY_PROCESSING_PS], nu) << std::endl;
+  } else {
+    out << "    Nullify Request - MODIFIED State: " << std::endl;
+    out << "    Nullify Request - SHARED State: " << std::endl;
+    out << "    Nullify Request - UNCACHED State: " << std::endl;
+    out << "    Average Nullify Request Serialization Time (in nanoseconds): " << std::endl;
+    out << "    Average Nullify Request Processing Time (in nanoseconds): " << std::endl;
+  }
+  const uint64_t iu = ps[GG_PS_INV_UNICAST], ib = ps[GG_PS_INV_BROADCAST];
+  out << "    Total Invalidation Requests - Unicast Mode: " << iu << std::endl;
+  if (iu > 0) {
+    out << "    Average Sharers Invalidated - Unicast Mode: " << (float)ps[GG_PS_INV_SHARERS_UNICAST] / (float)iu << std::endl;
+    out << "    Average Invalidation Processing Time - Unicast Mode (in nanoseconds): " << avg_ns(ps[GG_PS_INV_PROCESSING_UNICAST_PS], iu) << std::endl;
+  } else {
+    out << "    Average Sharers Invalidated - Unicast Mode: " << std::endl;
+    out << "    Average Invalidation Processing Time - Unicast Mode (in nanoseconds): " << std::endl;
+  }
+  out << "    Total Invalidation Requests - Broadcast Mode: " << ib << std::endl;
+  if (ib > 0) {
+    out << "    Average Sharers Invalidated - Broadcast Mode: " << (float)ps[GG_PS_INV_SHARERS_BROADCAST] / (float)ib << std::endl;
+    out << "    Average Invalidation Processing Time - Broadcast Mode (in nanoseconds): " << avg_ns(ps[GG_PS_INV_PROCESSING_BROADCAST_PS], ib) << std::endl;
+  } else {
+    out << "    Average Sharers Invalidated - Broadcast Mode: " << std::endl;
+    out << "    Average Invalidation Processing Time - Broadcast Mode (in nanoseconds): " << std::endl;
+  }
+}
+
 // The memory part of one tile's sim.out block in the coherent mode
 // (msi/memory_manager.cc:415-430): Cache Summary (L1-D, L2; no L1-I is
-// modeled), then the DRAM and directory summaries.
+// modeled), then the DRAM and directory summaries.  MOSI
+// (…mosi/memory_manager.cc:412-436, proto = the tile's GG_PS_* counters): the
+// L2 and directory controllers' blocks after the caches, the directory cache
+// before the DRAM.
 inline void writeMemorySummary(std::ostream& out, const gg_config& c, const uint64_t* tile_stats,
-                               const uint64_t* cache_counters, const uint64_t* miss_types = nullptr)
+                               const uint64_t* cache_counters, const uint64_t* miss_types = nullptr,
+                               const uint64_t* proto = nullptr)
 {
+  const bool mosi = c.protocol == GG_PROTO_MOSI;
+  const bool l1_mt = mosi ? c.l1d_track_miss_types : c.l1i_track_miss_types;
   out << "Cache Summary:\n";
-  writeCacheSummary(out, "L1-D", cache_counters, false, false,
-                    miss_types && c.l1i_track_miss_types ? miss_types : nullptr);
+  writeCacheSummary(out, "L1-D", cache_counters, false, false, miss_types && l1_mt ? miss_types : nullptr);
   writeCacheSummary(out, "L2", cache_counters + GG_NUM_CACHE_COUNTERS, true, false,
                     miss_types && c.l2_track_miss_types ? miss_types + GG_NUM_MISS_TYPES : nullptr);
+  if (mosi) {
+    static const uint64_t zero_ps[GG_NUM_PROTO_STATS] = {0};
+    writeMosiL2CntlrSummary(out, proto ? proto : zero_ps);
+    writeMosiDirectoryCntlrSummary(out, proto ? proto : zero_ps);
+    writeDirectorySummary(out, tile_stats, directorySizing(c));
+    writeDramSummary(out, tile_stats, c.dram_queue_model_enabled != 0, c.dram_queue_model_type);
+    return;
+  }
   writeDramSummary(out, tile_stats, c.dram_queue_model_enabled != 0, c.dram_queue_model_type);
   writeDirectorySummary(out, tile_stats, directorySizing(c));
 }
@@ -362,11 +461,12 @@ inline void writeMemorySummary(std::ostream& out, const gg_config& c, const uint
 // then the networks.
 inline void writeTileSummary(std::ostream& os, const gg_config& cfg, const uint64_t* tile_stats,
                              const uint64_t* cache_counters, const uint64_t* net_counters,
-                             const uint64_t* core_stats = nullptr, const uint64_t* miss_types = nullptr)
+                             const uint64_t* core_stats = nullptr, const uint64_t* miss_types = nullptr,
+                             const uint64_t* proto = nullptr)
 {
   static const uint64_t zero_net[GG_NUM_NET_COUNTERS] = {0};
   if (core_stats) writeCoreSummary(os, core_stats, cfg.frequency_ghz);   // Tile::outputSummary (tile.cc:52-69)
-  if (tile_stats) writeMemorySummary(os, cfg, tile_stats, cache_counters, miss_types);
+  if (tile_stats) writeMemorySummary(os, cfg, tile_stats, cache_counters, miss_types, proto);
   else {
     os << "Cache Summary:\n";
     writeCacheSummary(os, "L1-D", cache_counters, false);

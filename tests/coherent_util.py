@@ -54,6 +54,7 @@ def check_invariants(stats, cache, out, offs, per_tile_expected=None):
     assert np.array_equal(cache[:, 1, C.CACHE_COUNTERS.index("misses")], S["l2_misses"])
     reqs = S["sent_ex_req"] + S["sent_sh_req"]
     assert np.array_equal(reqs, S["l2_misses"])
-    reps = S["sent_ex_rep"].sum() + S["sent_sh_rep"].sum()
+    # every request gets one reply (MOSI: an UPGRADE_REP for a lone sharer / owner)
+    reps = S["sent_ex_rep"].sum() + S["sent_sh_rep"].sum() + S["sent_upgrade_rep"].sum()
     assert reps == reqs.sum()
     assert S["msgs_sent"].sum() == S["msgs_received"].sum()

@@ -58,7 +58,7 @@ def test_two_rank_tile_sharding(tmp_path):
         assert float(open(tmp_path / ("r%d.txt" % r)).read()) == float(world)
 
 
-def _coherent_worker(rank, world, port, T, N, K, outdir):
+def _coherent_worker(rank, world, port, T, N, K, outdir, protocol=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
                       LOCAL_RANK=str(rank))
     import sys
@@ -70,7 +70,7 @@ def _coherent_worker(rank, world, port, T, N, K, outdir):
     from tests.coherent_util import OracleEngine
     D.init("gloo")
     k0, k1 = CO.shard_range(rank, world, K)
-    cfg = C.default_config(T, num_shards=K, shard_begin=k0, shard_end=k1)
+    cfg = C.default_config(T, num_shards=K, shard_begin=k0, shard_end=k1, protocol=protocol)
     a, m, o = po.gen_trace(T, N, hot_lines=16)
     eng = OracleEngine(cfg, a, m, o)
     CO.run(eng, cfg.quantum_ns * 1000, K, world, rank, "gloo", "cpu")
@@ -87,16 +87,19 @@ def _coherent_worker(rank, world, port, T, N, K, outdir):
     dist.destroy_process_group()
 
 
-def test_two_rank_coherent_exchange(tmp_path):
+@pytest.mark.parametrize("protocol", [0, 1])
+def test_two_rank_coherent_exchange(tmp_path, protocol):
     """Mode C over 2 ranks x 2 logical shards each (gloo all-to-all of the
     cross-shard ShmemMsgs at every quantum boundary) == one process owning all
-    4 shards: the schedule depends on the shard count, not the rank count."""
+    4 shards: the schedule depends on the shard count, not the rank count.
+    protocol 1: MOSI (INV_FLUSH_COMBINED_REQs carry their single receiver
+    across ranks)."""
     world, T, N, K = 2, 16, 1200, 4
-    mp.spawn(_coherent_worker, args=(world, _free_port(), T, N, K, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_coherent_worker, args=(world, _free_port(), T, N, K, str(tmp_path), protocol), nprocs=world, join=True)
     from graphite_amd import config as C
     from oracle import pyoracle as po
     a, m, o = po.gen_trace(T, N, hot_lines=16)
-    oc = po.OracleCoherent(C.default_config(T, num_shards=K))
+    oc = po.OracleCoherent(C.default_config(T, num_shards=K, protocol=protocol))
     out = oc.run(a, m, o)
     np.testing.assert_array_equal(np.load(tmp_path / "out.npy"), out)
     np.testing.assert_array_equal(np.load(tmp_path / "stats.npy"), oc.tile_stats())

@@ -49,7 +49,8 @@ def _run_ranks(torch, W, K, cfg_kw, a, m, o, stats):
     bes, outs = [], []
     for r in range(W):
         k0, k1 = CO.shard_range(r, W, K)
-        be = B.Backend(C.default_config(T, num_shards=K, shard_begin=k0, shard_end=k1, net_model=cfg_kw["net"]))
+        be = B.Backend(C.default_config(T, num_shards=K, shard_begin=k0, shard_end=k1, net_model=cfg_kw["net"],
+                                        protocol=cfg_kw.get("protocol", C.PROTO_MSI)))
         out = torch.zeros(len(a), dtype=torch.int64, device="cuda")
         be.coherent_begin(addr, meta, o, out)
         bes.append(be); outs.append(out)

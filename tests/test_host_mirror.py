@@ -247,3 +247,17 @@ def test_tile_summary_table_matches_reference(tmp_path):
     for sel in (files[:3], files):
         out = subprocess.run([REPLAY, "--format-table"] + sel, capture_output=True, text=True, check=True).stdout
         assert out == reference_table([open(f).read() for f in sel])
+
+
+@pytest.mark.parametrize("name", ["mosi_hot16", "mosi_hot16magic", "mosi_dir16", "mosi_fft10"])
+def test_mosi_controller_summaries_match_reference(name):
+    """The host mirror's MOSI blocks (writeMosiL2CntlrSummary /
+    writeMosiDirectoryCntlrSummary) print the reference's own
+    L2CacheCntlr::outputSummary + DramDirectoryCntlr::outputSummary text
+    (…mosi/l2_cache_cntlr.cc:638-649, dram_directory_cntlr.cc:1041-1142, written
+    by coh_harness_mosi) from the same event counters, byte for byte."""
+    g = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    out = subprocess.run([REPLAY, "--mosi-summary", os.path.join(g, "coh_%s_proto.u64" % name), "16"],
+                         capture_output=True, text=True, check=True).stdout
+    with open(os.path.join(g, "coh_%s_summary.txt" % name)) as f:
+        assert out == f.read()
