@@ -61,6 +61,13 @@
 #include <cstdlib>
 #include <vector>
 
+#ifndef GG_COH_DIAG
+#define GG_COH_DIAG 0
+#endif
+// a diagnostics pointer of CS: the pointer in a diagnostics build, a null
+// constant otherwise (the hooks compile out wherever S lives)
+#define DG(x) (GG_COH_DIAG ? (x) : nullptr)
+
 namespace ggc {
 using namespace gg;
 
@@ -206,16 +213,16 @@ struct CS {
 // 21 (Y), 22 launches
 constexpr uint32_t kTrStep = 32;       // GG_COH_TRACE words per (launch, tile)
 constexpr uint32_t kTrEv0 = 200, kTrEvMax = 128;
-#define PROF_T0() const uint64_t _p0 = (S.prof || S.trs) ? __builtin_amdgcn_s_memtime() : 0
-#define PROF_AT(var) const uint64_t var = (S.prof || S.trs) ? __builtin_amdgcn_s_memtime() : 0
+#define PROF_T0() const uint64_t _p0 = (DG(S.prof) || DG(S.trs)) ? __builtin_amdgcn_s_memtime() : 0
+#define PROF_AT(var) const uint64_t var = (DG(S.prof) || DG(S.trs)) ? __builtin_amdgcn_s_memtime() : 0
 // GG_COH_PROFILE batch shapes: per port kind (0 SELF, 1 injection, 2 walker),
 // requests by batch size bucket (1, 2-3, 4-7, ..., 64+), requests at or after
 // the last interval's start at the batch's start (a tail run)
 __device__ __forceinline__ void prof_batch(const CS& S, int kind, uint32_t m, uint32_t tail)
 {
   const int b = m <= 1 ? 0 : m <= 3 ? 1 : m <= 7 ? 2 : m <= 15 ? 3 : m <= 31 ? 4 : m <= 63 ? 5 : 6;
-  atomicAdd(&S.prof[50 + 8 * kind + b], (unsigned long long)m);
-  atomicAdd(&S.prof[80 + kind], (unsigned long long)tail);
+  atomicAdd(&DG(S.prof)[50 + 8 * kind + b], (unsigned long long)m);
+  atomicAdd(&DG(S.prof)[80 + kind], (unsigned long long)tail);
 }
 
 __device__ __forceinline__ gg_cmsg* pool(const CS& S, uint32_t p) { return p ? S.pool1 : S.pool0; }
@@ -1405,7 +1412,7 @@ struct Tile {
     const bool ok = mine && hit && l2ok && (e - P.lat_l1d < barrier || (wm & GG_META_CONT));
     const uint64_t m = __ballot(ok) >> o;
     const uint32_t n = ~m ? (uint32_t)__builtin_ctzll(~m) : 64u - o;
-    if (S.prof && ln == 0) { atomicAdd(&S.prof[37], (unsigned long long)__builtin_amdgcn_s_memtime()); atomicAdd(&S.prof[38], 1ull); }
+    if (DG(S.prof) && ln == 0) { atomicAdd(&DG(S.prof)[37], (unsigned long long)__builtin_amdgcn_s_memtime()); atomicAdd(&DG(S.prof)[38], 1ull); }
     if (!n) return 0;
     const uint64_t run = (n == 64 ? ~0ull : ((1ull << n) - 1)) << o;
     const bool inrun = (run >> ln) & 1;
@@ -1437,12 +1444,12 @@ struct Tile {
         }
       }
       PROF_AT(_q1);
-      if (S.prof && ln == 0) atomicAdd(&S.prof[40], (unsigned long long)_q1);
+      if (DG(S.prof) && ln == 0) atomicAdd(&DG(S.prof)[40], (unsigned long long)_q1);
       if (lru1 && inrun) lru_run_store(L1.meta + (size_t)s1 * L1.ways, L1.ways, r1a, r1b, w1, tm1, af1);
       if (lru2 && w2l) lru_run_store(L2.meta + (size_t)s2 * L2.ways, L2.ways, r2a, r2b, w2, tm2, af2);
       L1.cset = ~0u; L2.cset = ~0u;                                  // the one-row caches reload
       PROF_AT(_q2);
-      if (S.prof && ln == 0) { atomicAdd(&S.prof[41], (unsigned long long)_q2); atomicAdd(&S.prof[42], 1ull); }
+      if (DG(S.prof) && ln == 0) { atomicAdd(&DG(S.prof)[41], (unsigned long long)_q2); atomicAdd(&DG(S.prof)[42], 1ull); }
     } else if (lru1 || lru2) {                                       // > 16 ways: one touch at a time
       for (uint32_t k = 0; k < n; ++k) {
         const uint32_t l = o + k;
@@ -2378,9 +2385,9 @@ __device__ __forceinline__ void publish_hbh_lds(TT& T, gg_cmsg* cur, uint32_t nl
     if (late_p) { if (late_j >= late_cap) atomicOr(S.err, GG_DERR_CAP); else late_p[late_j] = late_r; }
   };
   if (!nn) { late_store(); return; }
-  if (S.trs) q1 = __builtin_amdgcn_s_memtime();
+  if (DG(S.trs)) q1 = __builtin_amdgcn_s_memtime();
   order_port_local(nn, sl.x1, sl.x1, sl.x2, sl.i2, ln);
-  if (S.trs) q2 = __builtin_amdgcn_s_memtime();
+  if (DG(S.trs)) q2 = __builtin_amdgcn_s_memtime();
   // the port's queue: tr in HBM, trl the LDS image (one address space each:
   // a pointer merged from the two would make every queue access flat)
   HTree tr{gq, gnd, 1, P.np.analytical != 0};
@@ -2390,7 +2397,7 @@ __device__ __forceinline__ void publish_hbh_lds(TT& T, gg_cmsg* cur, uint32_t nl
     img_in(sl.pimg, gq, gnd, P.np.max_size, ln);
     tsync();
   }
-  if (S.trs) { (void)__builtin_amdgcn_readfirstlane((int)rq.a0); q3 = __builtin_amdgcn_s_memtime(); }
+  if (DG(S.trs)) { (void)__builtin_amdgcn_readfirstlane((int)rq.a0); q3 = __builtin_amdgcn_s_memtime(); }
   uint64_t ps = 0, fs = 0, bs = 0;
   for (uint32_t c0 = 0; c0 < nn; c0 += 64) {
     const uint32_t cnt = min(64u, nn - c0);
@@ -2422,7 +2429,7 @@ __device__ __forceinline__ void publish_hbh_lds(TT& T, gg_cmsg* cur, uint32_t nl
       g->hop = tile;
     }
   }
-  if (S.trs) q4 = __builtin_amdgcn_s_memtime();
+  if (DG(S.trs)) q4 = __builtin_amdgcn_s_memtime();
   if (regq) rq.store(gq, gnd);
   if (wave) { tsync(); img_out(gq, gnd, sl.pimg, P.np.max_size, ln); }
   if (ln == 0) {
@@ -2445,7 +2452,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
   const uint32_t ln = lane_id(), p = k & 1u;
   PROF_T0();
   Tile<SL, H, F, MO> T(P, S, lt, p, sl, hk, clds, std::integral_constant<bool, LC>(), pre);
-  T.tr_on = S.trs != nullptr && L < S.tr_n;
+  T.tr_on = DG(S.trs) != nullptr && L < S.tr_n;
   const gg_cmsg* prev = pool(S, p ^ 1u);     // records delivered to this step
   uint64_t* gscr = S.gscr + (size_t)lt * 6 * P.IC;
   // NoC counters of the SELF port (lanes 0-6) and of the receiver
@@ -2489,7 +2496,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
   uint64_t h_addr = 0;                           // address and type | requester << 8 of the message at local index lane
   uint32_t h_tr = 0;
   if (na) {
-    if (S.prof || S.trs) _sb = __builtin_amdgcn_s_memtime();
+    if (DG(S.prof) || DG(S.trs)) _sb = __builtin_amdgcn_s_memtime();
     const uint32_t* al = arv(S, p) + (size_t)lt * P.IC;
     // the port's queue in registers for the batch (RegQueue, its loads in
     // flight beside the records'); other models on an LDS image
@@ -2539,9 +2546,9 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
       }
     }
     tsync();
-    if (S.prof || S.trs) _sc = __builtin_amdgcn_s_memtime();
+    if (DG(S.prof) || DG(S.trs)) _sc = __builtin_amdgcn_s_memtime();
     order_port_local(na, t_, s_, k_, o_, ln);
-    if (S.prof || S.trs) _sd = __builtin_amdgcn_s_memtime();
+    if (DG(S.prof) || DG(S.trs)) _sd = __builtin_amdgcn_s_memtime();
     // the port's queue: tr in HBM, trl the LDS image (one address space each:
     // a pointer merged from the two would make every queue access flat)
     HTree tr{gq, gnd, 1, P.np.analytical != 0};
@@ -2551,7 +2558,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
       img_in(sl.pimg, gq, gnd, P.np.max_size, ln);
       tsync();
     }
-    if (S.prof || S.trs) { (void)__builtin_amdgcn_readfirstlane((int)rq.a0); _se = __builtin_amdgcn_s_memtime(); }
+    if (DG(S.prof) || DG(S.trs)) { (void)__builtin_amdgcn_readfirstlane((int)rq.a0); _se = __builtin_amdgcn_s_memtime(); }
     for (uint32_t c0 = 0; c0 < na; c0 += 64) {
       const uint32_t cnt = min(64u, na - c0);
       uint32_t r = 0, nf_ = 0, bits = 0, e = 0;
@@ -2564,7 +2571,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
         nf_ = (uint32_t)nflits(P.np, bits);
       }
       uint64_t ot = tv, oz = z_;
-      const uint64_t x0 = S.prof && regq ? rq.A(rq.sz - 1) : 0;
+      const uint64_t x0 = DG(S.prof) && regq ? rq.A(rq.sz - 1) : 0;
       uint32_t ntail = 0;
       for (uint32_t k = 0; k < cnt; ++k) {
         const uint64_t t = rl64(tv, k);
@@ -2584,8 +2591,8 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
         rf += nf; rb += (uint32_t)__builtin_amdgcn_readlane((int)bits, (int)k); rl += z2 + ct; rc += ct;
         if (ln == k) { ot = t2; oz = z2; }
       }
-      if (S.prof && ln == 0) prof_batch(S, 0, cnt, ntail);
-      if (S.trs) _sf = __builtin_amdgcn_s_memtime();
+      if (DG(S.prof) && ln == 0) prof_batch(S, 0, cnt, ntail);
+      if (DG(S.trs)) _sf = __builtin_amdgcn_s_memtime();
       if (ln < cnt) {
         pv[r].arrival_ps = ot; pv[r].zero_load_ps = oz;
         if (LD && self_keys) { const uint64_t kk = k_[e]; t_[e] = ot; s_[e] = ((kk >> 34) << 32) | ((kk >> 2) & 0xFFFFFFFFull); }
@@ -2604,13 +2611,13 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
   }
 
   PROF_AT(_p1);
-  if (S.prof && ln == 0 && na) {
-    atomicAdd(&S.prof[90], (unsigned long long)(_sa - _p0)); atomicAdd(&S.prof[91], (unsigned long long)(_sb - _sa));
-    atomicAdd(&S.prof[92], (unsigned long long)(_sc - _sb)); atomicAdd(&S.prof[93], (unsigned long long)(_sd - _sc));
-    atomicAdd(&S.prof[94], (unsigned long long)(_se - _sd)); atomicAdd(&S.prof[95], (unsigned long long)(_p1 - _se));
-    atomicAdd(&S.prof[96], 1ull);
+  if (DG(S.prof) && ln == 0 && na) {
+    atomicAdd(&DG(S.prof)[90], (unsigned long long)(_sa - _p0)); atomicAdd(&DG(S.prof)[91], (unsigned long long)(_sb - _sa));
+    atomicAdd(&DG(S.prof)[92], (unsigned long long)(_sc - _sb)); atomicAdd(&DG(S.prof)[93], (unsigned long long)(_sd - _sc));
+    atomicAdd(&DG(S.prof)[94], (unsigned long long)(_se - _sd)); atomicAdd(&DG(S.prof)[95], (unsigned long long)(_p1 - _se));
+    atomicAdd(&DG(S.prof)[96], 1ull);
   }
-  if (S.prof && ln == 0 && !na) { atomicAdd(&S.prof[97], (unsigned long long)(_sa - _p0)); atomicAdd(&S.prof[98], 1ull); }
+  if (DG(S.prof) && ln == 0 && !na) { atomicAdd(&DG(S.prof)[97], (unsigned long long)(_sa - _p0)); atomicAdd(&DG(S.prof)[98], 1ull); }
   // directory request FIFO in LDS when it cannot outgrow it this step
   if (rq_fit) {
     if (pre_rq) {
@@ -2670,7 +2677,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
     const uint32_t* gi_ = (const uint32_t*)(gscr + 3 * P.IC);
     PROF_AT(_p1b);
     _q1b = _p1b;
-    if (S.prof && ln == 0) atomicAdd(&S.prof[9], (unsigned long long)(_p1b - _p1));
+    if (DG(S.prof) && ln == 0) atomicAdd(&DG(S.prof)[9], (unsigned long long)(_p1b - _p1));
     for (uint32_t j = 0; j < n && !T.failed; ++j) {
       // the message: arrival and sender from the ordering arrays, address /
       // type / requester from the gather's registers (local index < 64: no
@@ -2694,11 +2701,11 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
         m.single_rx = MO ? g.single_rx : 0u;
       }
       T.stat(GG_CT_MSGS_RECEIVED, 1);
-      const uint64_t h0 = S.trs ? __builtin_amdgcn_s_memtime() : 0;
+      const uint64_t h0 = DG(S.trs) ? __builtin_amdgcn_s_memtime() : 0;
       const bool dm = to_directory(m.type);
       if constexpr (MO) { if (dm) T.directory_msg_mo(m); else T.l2_msg_mo(m); }
       else { if (dm) T.directory_msg(m); else T.l2_msg(m); }
-      if (S.trs) {
+      if (DG(S.trs)) {
         const uint64_t h1 = __builtin_amdgcn_s_memtime();
         if (dm) { _hd += h1 - h0; _hn += 1; } else { _hl += h1 - h0; _hn += 1ull << 32; }
       }
@@ -2739,10 +2746,10 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
       }
       if (try_run) {
         PROF_AT(_h0);
-        if (S.prof && ln == 0) atomicAdd(&S.prof[39], (unsigned long long)_h0);
+        if (DG(S.prof) && ln == 0) atomicAdd(&DG(S.prof)[39], (unsigned long long)_h0);
         const uint32_t nh = T.l1_hit_run(wbase, (uint32_t)o, wa, wm, line_mask, barrier);
         PROF_AT(_h1);
-        if (S.prof && ln == 0) { atomicAdd(&S.prof[33], (unsigned long long)(_h1 - _h0)); atomicAdd(&S.prof[34], (unsigned long long)nh); }
+        if (DG(S.prof) && ln == 0) { atomicAdd(&DG(S.prof)[33], (unsigned long long)(_h1 - _h0)); atomicAdd(&DG(S.prof)[34], (unsigned long long)nh); }
         if (nh) { if (o + nh < 64) stop = T.rec; continue; }
       }
       PROF_AT(_ha);
@@ -2755,7 +2762,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
       if (s >= barrier && !(meta & GG_META_CONT)) break;             // a multi-line access is one instruction
       T.app_access(rl64(wa, (uint32_t)o) & line_mask, (meta & GG_META_WRITE) != 0, s);
       PROF_AT(_h2);
-      if (S.prof && ln == 0) { atomicAdd(&S.prof[35], (unsigned long long)(_h2 - _ha)); atomicAdd(&S.prof[36], 1ull); }
+      if (DG(S.prof) && ln == 0) { atomicAdd(&DG(S.prof)[35], (unsigned long long)(_h2 - _ha)); atomicAdd(&DG(S.prof)[36], 1ull); }
     }
     W.wbase = wbase; W.wa = wa; W.wm = wm;
   }
@@ -2834,9 +2841,9 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
         // the injection port (routePacket SEND_TILE, hop_by_hop.cc:151-159) in (time, key) order
         for (uint32_t i = ln; i < nn; i += 64) i_[i] = o_[i];
         tsync();
-        if (S.trs) _q1 = __builtin_amdgcn_s_memtime();
+        if (DG(S.trs)) _q1 = __builtin_amdgcn_s_memtime();
         order_port(nn, t_, s_, k_, i_, o_, ln);
-        if (S.trs) _q2 = __builtin_amdgcn_s_memtime();
+        if (DG(S.trs)) _q2 = __builtin_amdgcn_s_memtime();
         const uint64_t qi = (uint64_t)T.tile * 6 + P_INJ;
         HQueue* gq = S.nq + qi;
         HNode* gnd = S.nnd + qi * P.np.max_size;
@@ -2853,7 +2860,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
             }
         RegQueue rq;
         if (regq) rq.load_h0(gq, gnd, P.np.max_size, 1, P.np.analytical != 0, ln);
-        if (S.trs) { (void)__builtin_amdgcn_readfirstlane((int)rq.a0); _q3 = __builtin_amdgcn_s_memtime(); }
+        if (DG(S.trs)) { (void)__builtin_amdgcn_readfirstlane((int)rq.a0); _q3 = __builtin_amdgcn_s_memtime(); }
         uint64_t ps = 0, fs = 0, bs = 0;
         for (uint32_t c0 = 0; c0 < nn; c0 += 64) {
           const uint32_t cnt = min(64u, nn - c0);
@@ -2867,7 +2874,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
             nf_ = (uint32_t)nflits(P.np, bits);
           }
           uint64_t oq = 0;
-          const uint64_t x0 = S.prof && regq ? rq.A(rq.sz - 1) : 0;
+          const uint64_t x0 = DG(S.prof) && regq ? rq.A(rq.sz - 1) : 0;
           uint32_t ntail = 0;
           for (uint32_t k = 0; k < cnt; ++k) {
             const uint32_t nf = (uint32_t)__builtin_amdgcn_readlane((int)nf_, (int)k);
@@ -2881,7 +2888,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
             fs += nf; bs += (uint32_t)__builtin_amdgcn_readlane((int)bits, (int)k);   // updateSendCounters, uniform
           }
           ps += cnt;
-          if (S.prof && ln == 0) prof_batch(S, 1, cnt, ntail);
+          if (DG(S.prof) && ln == 0) prof_batch(S, 1, cnt, ntail);
           if (ln < cnt) {                                       // (network_model.cc:228-251)
             gg_cmsg* g = cur + r;
             g->arrival_ps = sp + lat_to_ps(0, P.np.f) + lat_to_ps(oq, P.np.f);
@@ -2889,7 +2896,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
             g->hop = T.tile;
           }
         }
-        if (S.trs) _q4 = __builtin_amdgcn_s_memtime();
+        if (DG(S.trs)) _q4 = __builtin_amdgcn_s_memtime();
         if (regq) rq.store(gq, gnd);
         if (wave) { tsync(); img_out(gq, gnd, sl.pimg, P.np.max_size, ln); }
         if (ln == 0) {
@@ -2937,27 +2944,27 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
     const uint32_t a = wave_sum((uint32_t)ri_net), b = wave_sum((uint32_t)ri_self), c = wave_sum((uint32_t)ri_bnd);
     if (ln == 0) hk.step_counts(k, a, b, c, np_);
   }
-  if (S.prof && ln == 0) {
+  if (DG(S.prof) && ln == 0) {
     const uint64_t e = __builtin_amdgcn_s_memtime();
-    atomicAdd(&S.prof[0], (unsigned long long)(_p1 - _p0)); atomicAdd(&S.prof[1], (unsigned long long)(_p2 - _p1));
-    atomicAdd(&S.prof[2], (unsigned long long)(_p3 - _p2)); atomicAdd(&S.prof[3], (unsigned long long)(_p4 - _p3));
-    atomicAdd(&S.prof[4], (unsigned long long)(e - _p4));
-    atomicMax(&S.prof[1024 + (L & 65535)], (unsigned long long)(e - _p0));
-    atomicMax(&S.prof[1024 + 3 * 65536 + (L & 65535)], (unsigned long long)(na + T.nsent));
+    atomicAdd(&DG(S.prof)[0], (unsigned long long)(_p1 - _p0)); atomicAdd(&DG(S.prof)[1], (unsigned long long)(_p2 - _p1));
+    atomicAdd(&DG(S.prof)[2], (unsigned long long)(_p3 - _p2)); atomicAdd(&DG(S.prof)[3], (unsigned long long)(_p4 - _p3));
+    atomicAdd(&DG(S.prof)[4], (unsigned long long)(e - _p4));
+    atomicMax(&DG(S.prof)[1024 + (L & 65535)], (unsigned long long)(e - _p0));
+    atomicMax(&DG(S.prof)[1024 + 3 * 65536 + (L & 65535)], (unsigned long long)(na + T.nsent));
     {
       // the slowest tile's shape: (total << 24) | payload, max per launch
       const uint64_t tot = (e - _p0) << 24;
       auto c8 = [](uint64_t v) { return v > 255 ? 255ull : v; };
       auto c24 = [](uint64_t v) { v >>= 8; return v > 0xFFFFFF ? 0xFFFFFFull : v; };
       const size_t b = 1024 + 6 * 65536 + 4 * (L & 16383);
-      atomicMax(&S.prof[b + 0], (unsigned long long)(tot | (c8(ni) << 16) | (c8(na) << 8) | c8(T.nsent)));
-      atomicMax(&S.prof[b + 1], (unsigned long long)(tot | c24(_p1 - _p0)));
-      atomicMax(&S.prof[b + 2], (unsigned long long)(tot | c24(_p2 - _p1)));
-      atomicMax(&S.prof[b + 3], (unsigned long long)(tot | c24(_p3 - _p2)));
+      atomicMax(&DG(S.prof)[b + 0], (unsigned long long)(tot | (c8(ni) << 16) | (c8(na) << 8) | c8(T.nsent)));
+      atomicMax(&DG(S.prof)[b + 1], (unsigned long long)(tot | c24(_p1 - _p0)));
+      atomicMax(&DG(S.prof)[b + 2], (unsigned long long)(tot | c24(_p2 - _p1)));
+      atomicMax(&DG(S.prof)[b + 3], (unsigned long long)(tot | c24(_p3 - _p2)));
     }
   }
-  if (S.trs && L < S.tr_n && ln == 0) {
-    unsigned long long* r = S.trs + ((size_t)L * P.L + lt) * kTrStep;
+  if (DG(S.trs) && L < S.tr_n && ln == 0) {
+    unsigned long long* r = DG(S.trs) + ((size_t)L * P.L + lt) * kTrStep;
     r[2] = _p0; r[3] = _sa; r[4] = _p1; r[5] = _p2; r[6] = _p3; r[7] = _p4; r[8] = __builtin_amdgcn_s_memtime();
     r[9] = (unsigned long long)na | ((unsigned long long)ni << 16) | ((unsigned long long)T.nsent << 32);
     r[10] = _sb; r[11] = _sc; r[12] = _sd; r[13] = _se; r[14] = _q1b; r[15] = _sf;
@@ -2975,9 +2982,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
 // walker traces) are compiled only into a diagnostics build (-DGG_COH_DIAG=1,
 // tools/build_variant.sh): in the product kernels their pointers are null
 // constants, so the hooks and the registers they would hold are gone.
-#ifndef GG_COH_DIAG
-#define GG_COH_DIAG 0
-#endif
+
 __device__ __forceinline__ void diag_off(CS& S)
 {
   if (!GG_COH_DIAG) { S.prof = nullptr; S.trs = nullptr; S.trw = nullptr; S.tre = nullptr; }
@@ -3275,8 +3280,8 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
     const uint32_t status_nx = (nx < sd.lo || nx > sd.hi) ? 2u : 0u;   // next router in another shard: held
     uint64_t cq = 0, cf = 0, m = 0;
     uint32_t spin = 0, polls = 0;
-    const bool tev = S.tre && L >= kTrEv0 && L < kTrEv0 + S.tre_n;
-    unsigned long long* tre = tev ? S.tre + (((size_t)(L - kTrEv0) * 2 + stage) * S.tr_wb + blk) * (kTrEvMax * 4 + 4) : nullptr;
+    const bool tev = DG(S.tre) && L >= kTrEv0 && L < kTrEv0 + S.tre_n;
+    unsigned long long* tre = tev ? DG(S.tre) + (((size_t)(L - kTrEv0) * 2 + stage) * S.tr_wb + blk) * (kTrEvMax * 4 + 4) : nullptr;
     auto crosses = [&](uint32_t i) {
       if (i >= n) return false;
       const uint32_t a = W.Pp[i], z = W.Pd[i];
@@ -3458,11 +3463,11 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
     }
   }
   if (tid == 0) *cntp = 0;
-  if (S.tre && L >= kTrEv0 && L < kTrEv0 + S.tre_n && tid == 0) {
-    unsigned long long* e = S.tre + (((size_t)(L - kTrEv0) * 2 + stage) * S.tr_wb + blk) * (kTrEvMax * 4 + 4);
+  if (DG(S.tre) && L >= kTrEv0 && L < kTrEv0 + S.tre_n && tid == 0) {
+    unsigned long long* e = DG(S.tre) + (((size_t)(L - kTrEv0) * 2 + stage) * S.tr_wb + blk) * (kTrEvMax * 4 + 4);
     e[0] = rlohi[2]; e[1] = _w1; e[2] = _w2; e[3] = n | ((unsigned long long)npos << 32);
   }
-  if (S.trs && L < S.tr_n) {
+  if (DG(S.trs) && L < S.tr_n) {
     nev = wave_sum(ln == 0 ? nev : 0u);
     __shared__ uint32_t tr_ev;
     if (tid == 0) tr_ev = 0;
@@ -3470,24 +3475,24 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
     if (ln == 0) atomicAdd(&tr_ev, nev);
     __syncthreads();
     if (tid == 0) {
-      unsigned long long* r = S.trw + (((size_t)L * 2 + stage) * S.tr_wb + blk) * 8;
+      unsigned long long* r = DG(S.trw) + (((size_t)L * 2 + stage) * S.tr_wb + blk) * 8;
       r[1] = __builtin_amdgcn_s_memrealtime();
       r[2] = _p0; r[3] = _w1; r[4] = _w2; r[5] = __builtin_amdgcn_s_memtime();
       r[6] = (unsigned long long)n | ((unsigned long long)npos << 32); r[7] = tr_ev;
     }
   }
-  if (S.prof) {
+  if (DG(S.prof)) {
     nev = wave_sum(ln == 0 ? nev : 0u);
     if (ln == 0) {
       const uint64_t e = __builtin_amdgcn_s_memtime();
-      atomicAdd(&S.prof[19], (unsigned long long)nev);
+      atomicAdd(&DG(S.prof)[19], (unsigned long long)nev);
       if (wv == 0) {
-        atomicAdd(&S.prof[16], (unsigned long long)(_w1 - _p0)); atomicAdd(&S.prof[17], (unsigned long long)(_w2 - _w1));
-        atomicAdd(&S.prof[18], (unsigned long long)(e - _w2));
-        atomicAdd(&S.prof[22], 1ull);
-        atomicMax(&S.prof[1024 + 65536 + 2 * (L & 65535) + stage], (unsigned long long)(e - _p0));
+        atomicAdd(&DG(S.prof)[16], (unsigned long long)(_w1 - _p0)); atomicAdd(&DG(S.prof)[17], (unsigned long long)(_w2 - _w1));
+        atomicAdd(&DG(S.prof)[18], (unsigned long long)(e - _w2));
+        atomicAdd(&DG(S.prof)[22], 1ull);
+        atomicMax(&DG(S.prof)[1024 + 65536 + 2 * (L & 65535) + stage], (unsigned long long)(e - _p0));
       }
-      atomicMax(&S.prof[24 + stage], (unsigned long long)nev);
+      atomicMax(&DG(S.prof)[24 + stage], (unsigned long long)nev);
     }
   }
 }
@@ -3615,10 +3620,12 @@ __device__ __forceinline__ void import_one(const CP& P, const CS& S, const gg_cm
 }
 
 // ---- launchers (gg_coh_step.hip, gg_coh_persist.hip, gg_coh_walk.hip) ----
-void launch_step(const CP& P, const CS& S, size_t lds, hipStream_t s, uint32_t L, uint32_t devloop, uint64_t barrier);
-void launch_step_fast(const CP& P, const CS& S, size_t lds, hipStream_t s, uint32_t L, uint32_t devloop, uint64_t barrier);
+// k_c_step's arguments: the device copies of the launch state and this launch's timing slot
+struct StepArgs { const CP* P; const CS* S; unsigned long long* kt; uint32_t kt_slot; };
+void launch_step(const CP& P, const StepArgs& a, size_t lds, hipStream_t s, uint32_t L, uint32_t devloop, uint64_t barrier);
+void launch_step_fast(const CP& P, const StepArgs& a, size_t lds, hipStream_t s, uint32_t L, uint32_t devloop, uint64_t barrier);
 hipError_t step_fast_set_lds(size_t lds);
-void launch_step_mosi(const CP& P, const CS& S, size_t lds, hipStream_t s, uint32_t L, uint32_t devloop, uint64_t barrier);
+void launch_step_mosi(const CP& P, const StepArgs& a, size_t lds, hipStream_t s, uint32_t L, uint32_t devloop, uint64_t barrier);
 hipError_t step_mosi_set_lds(size_t lds);
 void launch_persist(bool lc, const CP& P, const CS& S, size_t lds, hipStream_t s, uint32_t L0, uint32_t L1);
 hipError_t step_set_lds(size_t step_lds, size_t persist_lc_lds, size_t persist_lds);

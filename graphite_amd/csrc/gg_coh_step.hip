@@ -8,11 +8,11 @@ namespace ggc {
 
 #include "gg_coh_step.inc"
 
-void launch_step(const CP& P, const CS& S, size_t lds, hipStream_t s, uint32_t L, uint32_t devloop, uint64_t barrier)
+void launch_step(const CP& P, const StepArgs& a, size_t lds, hipStream_t s, uint32_t L, uint32_t devloop, uint64_t barrier)
 {
-  if (P.mosi) launch_step_mosi(P, S, lds, s, L, devloop, barrier);
-  else if (P.fast) launch_step_fast(P, S, lds, s, L, devloop, barrier);
-  else hipLaunchKernelGGL(k_c_step<false>, dim3(P.L), dim3(64), lds, s, P, S, L, devloop, barrier);
+  if (P.mosi) launch_step_mosi(P, a, lds, s, L, devloop, barrier);
+  else if (P.fast) launch_step_fast(P, a, lds, s, L, devloop, barrier);
+  else hipLaunchKernelGGL(k_c_step<false>, dim3(P.L), dim3(64), lds, s, a.P, a.S, L, devloop, barrier, a.kt, a.kt_slot);
 }
 hipError_t step_set_lds(size_t step_lds, size_t persist_lc_lds, size_t persist_lds)
 {

@@ -7,9 +7,9 @@ namespace ggc {
 
 #include "gg_coh_step.inc"
 
-void launch_step_fast(const CP& P, const CS& S, size_t lds, hipStream_t s, uint32_t L, uint32_t devloop, uint64_t barrier)
+void launch_step_fast(const CP& P, const StepArgs& a, size_t lds, hipStream_t s, uint32_t L, uint32_t devloop, uint64_t barrier)
 {
-  hipLaunchKernelGGL(k_c_step<true>, dim3(P.L), dim3(64), lds, s, P, S, L, devloop, barrier);
+  hipLaunchKernelGGL(k_c_step<true>, dim3(P.L), dim3(64), lds, s, a.P, a.S, L, devloop, barrier, a.kt, a.kt_slot);
 }
 hipError_t step_fast_set_lds(size_t lds)
 {

@@ -10,8 +10,8 @@ __global__ void __launch_bounds__(PIPE ? 64 * kMaxWalkWaves : 64) k_c_walk(CP P,
 {
   diag_off(S);
   kt_begin(S);
-  if (S.trs && L < S.tr_n && threadIdx.x == 0)
-    S.trw[(((size_t)L * 2 + stage) * S.tr_wb + blockIdx.x) * 8] = __builtin_amdgcn_s_memrealtime();
+  if (DG(S.trs) && L < S.tr_n && threadIdx.x == 0)
+    DG(S.trw)[(((size_t)L * 2 + stage) * S.tr_wb + blockIdx.x) * 8] = __builtin_amdgcn_s_memrealtime();
   walk_body<PIPE, RQ>(P, S, L, stage, blockIdx.x);
   kt_end(S);
 }

@@ -208,6 +208,8 @@ using namespace gg;
 struct gg_coh_state {
   CP P{};
   CS S{};
+  CP* Pd = nullptr;                  // device copies of P / S (k_c_step reads its launch state through them)
+  CS* Sd = nullptr;
   std::vector<void*> allocs;
   uint64_t* status_dev = nullptr;
   uint32_t* ecount_dev = nullptr;    // export counts + cursors
@@ -237,6 +239,7 @@ struct gg_coh_state {
 };
 constexpr uint64_t kTimeSample = 16;
 constexpr uint32_t kKtRing = 1024;      // in-kernel timing slots between two harvests (a batch is <= 256 steps)
+static StepArgs step_args(const gg_coh_state* C) { return StepArgs{C->Pd, C->Sd, C->S.kt, C->S.kt_slot}; }
 static void launch_walk(gg_coh_state* C, hipStream_t s, uint32_t blocks, uint32_t threads, uint32_t L, int stage)
 {
   ggc::launch_walk(threads > 64, walk_regq(C->P), blocks, threads, C->walk_lds, s, C->P, C->S, L, stage);
@@ -613,6 +616,8 @@ static gg_status coh_alloc(gg_ctx* ctx)
     if ((st = dupload(C, &S.tinfo, ti))) return st;
   }
   if ((st = dalloc(C, &C->status_dev, 4))) return st;
+  if ((st = dalloc(C, &C->Pd, 1))) return st;
+  if ((st = dalloc(C, &C->Sd, 1))) return st;
   if ((st = dalloc(C, &C->ecount_dev, 2 * (uint64_t)P.K + 2))) return st;
   if ((st = dalloc(C, &C->offs_dev, (uint64_t)P.T + 1))) return st;
   S.ctr = gg_noc_ctr(ctx);
@@ -647,6 +652,8 @@ gg_status gg_coherent_begin(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_ou
     if (tr->tile_offsets[t] > tr->tile_offsets[t + 1]) return gg_fail(GG_ERR_INVALID, "tile_offsets not monotone");
   if (tr->num_records && (!tr->addr_dev || !tr->meta_dev)) return gg_fail(GG_ERR_INVALID, "NULL trace pointers");
   C->S.addr = tr->addr_dev; C->S.meta = tr->meta_dev; C->S.out = access_out_dev;
+  GG_HIP(hipMemcpyAsync(C->Pd, &C->P, sizeof(CP), hipMemcpyHostToDevice, s));
+  GG_HIP(hipMemcpyAsync(C->Sd, &C->S, sizeof(CS), hipMemcpyHostToDevice, s));
   C->n_records = tr->num_records;
   for (int k = 0; k < 5; ++k) { C->ksum[k] = 0; C->kcnt[k] = 0; C->nlaunch[k] = 0; }
   C->tused = 0;
@@ -711,7 +718,7 @@ static gg_status coh_quantum_steps(gg_ctx* ctx, uint64_t q)
   uint32_t k = 0, batch = 8;
   for (;;) {
     for (uint32_t b = 0; b < batch; ++b, ++k) {
-      timed_launch(ctx, C, s, 0, [&] { launch_step(P, C->S, C->step_lds, s, k, 0u, barrier); });
+      timed_launch(ctx, C, s, 0, [&] { launch_step(P, step_args(C), C->step_lds, s, k, 0u, barrier); });
       if (hbh) {
         if (P.nsx) timed_launch(ctx, C, s, 1, [&] { launch_walk(C, s, P.nsx, C->wtx, k, 0); });
         if (P.nsy) timed_launch(ctx, C, s, 2, [&] { launch_walk(C, s, P.nsy, C->wty, k, 1); });
@@ -778,7 +785,7 @@ gg_status gg_coh_steps_async(gg_ctx* ctx, uint64_t q, uint32_t k0, uint32_t n)
   const uint64_t barrier = (q + 1) * (uint64_t)ctx->cfg.quantum_ns * 1000ull;
   const bool hbh = P.net == GG_NET_EMESH_HOP_BY_HOP;
   for (uint32_t k = k0; k < k0 + n; ++k) {
-    timed_launch(ctx, C, s, 0, [&] { launch_step(P, C->S, C->step_lds, s, k, 0u, barrier); });
+    timed_launch(ctx, C, s, 0, [&] { launch_step(P, step_args(C), C->step_lds, s, k, 0u, barrier); });
     if (hbh) {
       if (P.nsx) timed_launch(ctx, C, s, 1, [&] { launch_walk(C, s, P.nsx, C->wtx, k, 0); });
       if (P.nsy) timed_launch(ctx, C, s, 2, [&] { launch_walk(C, s, P.nsy, C->wty, k, 1); });
@@ -932,7 +939,7 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
   }
   for (; !persist;) {
     for (uint32_t b = 0; b < batch; ++b, ++L) {
-      timed_launch(ctx, C, s, 0, [&] { launch_step(P, C->S, C->step_lds, s, L, 1u, (uint64_t)0); });
+      timed_launch(ctx, C, s, 0, [&] { launch_step(P, step_args(C), C->step_lds, s, L, 1u, (uint64_t)0); });
       if (hbh) {
         if (P.nsx) timed_launch(ctx, C, s, 1, [&] { launch_walk(C, s, P.nsx, C->wtx, L, 0); });
         if (P.nsy) timed_launch(ctx, C, s, 2, [&] { launch_walk(C, s, P.nsy, C->wty, L, 1); });
