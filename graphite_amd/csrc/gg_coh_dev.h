@@ -3627,14 +3627,14 @@ void launch_step_fast(const CP& P, const StepArgs& a, size_t lds, hipStream_t s,
 hipError_t step_fast_set_lds(size_t lds);
 void launch_step_mosi(const CP& P, const StepArgs& a, size_t lds, hipStream_t s, uint32_t L, uint32_t devloop, uint64_t barrier);
 hipError_t step_mosi_set_lds(size_t lds);
-void launch_persist(bool lc, const CP& P, const CS& S, size_t lds, hipStream_t s, uint32_t L0, uint32_t L1);
+void launch_persist(bool lc, const CP& P, const StepArgs& a, size_t lds, hipStream_t s, uint32_t L0, uint32_t L1);
 hipError_t step_set_lds(size_t step_lds, size_t persist_lc_lds, size_t persist_lds);
 hipError_t persist_occupancy(bool lc, size_t lds, int* per_cu);
 hipError_t persist_set_lds(size_t persist_lc_lds, size_t persist_lds);
-void launch_persist_lc(const CP& P, const CS& S, size_t lds, hipStream_t s, uint32_t L0, uint32_t L1);
+void launch_persist_lc(const CP& P, const StepArgs& a, size_t lds, hipStream_t s, uint32_t L0, uint32_t L1);
 hipError_t persist_lc_set_lds(size_t lds);
 hipError_t persist_lc_occ(size_t lds, int* per_cu);
-void launch_walk(bool pipe, bool rq, uint32_t blocks, uint32_t threads, size_t lds, hipStream_t s, const CP& P, const CS& S,
+void launch_walk(bool pipe, bool rq, uint32_t blocks, uint32_t threads, size_t lds, hipStream_t s, const StepArgs& a,
                  uint32_t L, int stage);
 hipError_t walk_set_lds(size_t lds);
 

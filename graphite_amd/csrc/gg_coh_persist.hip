@@ -6,9 +6,9 @@ namespace ggc {
 
 #include "gg_coh_persist.inc"
 
-void launch_persist_plain(const CP& P, const CS& S, size_t lds, hipStream_t s, uint32_t L0, uint32_t L1)
+void launch_persist_plain(const CP& P, const StepArgs& a, size_t lds, hipStream_t s, uint32_t L0, uint32_t L1)
 {
-  hipLaunchKernelGGL(k_c_persist<false>, dim3(P.L), dim3(64), lds, s, P, S, L0, L1);
+  hipLaunchKernelGGL(k_c_persist<false>, dim3(P.L), dim3(64), lds, s, a.P, a.S, L0, L1);
 }
 hipError_t persist_plain_set_lds(size_t lds)
 {
@@ -19,9 +19,9 @@ hipError_t persist_plain_occ(size_t lds, int* per_cu)
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, (const void*)k_c_persist<false>, 64, lds);
 }
 
-void launch_persist(bool lc, const CP& P, const CS& S, size_t lds, hipStream_t s, uint32_t L0, uint32_t L1)
+void launch_persist(bool lc, const CP& P, const StepArgs& a, size_t lds, hipStream_t s, uint32_t L0, uint32_t L1)
 {
-  if (lc) launch_persist_lc(P, S, lds, s, L0, L1); else launch_persist_plain(P, S, lds, s, L0, L1);
+  if (lc) launch_persist_lc(P, a, lds, s, L0, L1); else launch_persist_plain(P, a, lds, s, L0, L1);
 }
 hipError_t persist_occupancy(bool lc, size_t lds, int* per_cu)
 {

@@ -6,9 +6,9 @@ namespace ggc {
 
 #include "gg_coh_persist.inc"
 
-void launch_persist_lc(const CP& P, const CS& S, size_t lds, hipStream_t s, uint32_t L0, uint32_t L1)
+void launch_persist_lc(const CP& P, const StepArgs& a, size_t lds, hipStream_t s, uint32_t L0, uint32_t L1)
 {
-  hipLaunchKernelGGL(k_c_persist<true>, dim3(P.L), dim3(64), lds, s, P, S, L0, L1);
+  hipLaunchKernelGGL(k_c_persist<true>, dim3(P.L), dim3(64), lds, s, a.P, a.S, L0, L1);
 }
 hipError_t persist_lc_set_lds(size_t lds)
 {

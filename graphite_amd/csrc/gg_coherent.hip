@@ -242,7 +242,7 @@ constexpr uint32_t kKtRing = 1024;      // in-kernel timing slots between two ha
 static StepArgs step_args(const gg_coh_state* C) { return StepArgs{C->Pd, C->Sd, C->S.kt, C->S.kt_slot}; }
 static void launch_walk(gg_coh_state* C, hipStream_t s, uint32_t blocks, uint32_t threads, uint32_t L, int stage)
 {
-  ggc::launch_walk(threads > 64, walk_regq(C->P), blocks, threads, C->walk_lds, s, C->P, C->S, L, stage);
+  ggc::launch_walk(threads > 64, walk_regq(C->P), blocks, threads, C->walk_lds, s, step_args(C), L, stage);
 }
 constexpr uint32_t kPersistTiles = 64;        // owned tiles up to which gg_coherent_run uses k_c_persist
 constexpr uint32_t kPersistLaunches = 16384;  // launch indices per k_c_persist launch
@@ -922,10 +922,10 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
     GG_HIP(hipMemsetAsync(C->S.gbar, 0, 4 * sizeof(uint32_t), s));   // counter + the three stop-vote words
     if (plc) {
       const size_t lds = P.cache_lds_off + P.cache_lds_bytes;
-      timed_launch(ctx, C, s, 3, [&] { launch_persist(true, P, C->S, lds, s, L, L + kPersistLaunches); });
+      timed_launch(ctx, C, s, 3, [&] { launch_persist(true, P, step_args(C), lds, s, L, L + kPersistLaunches); });
     } else {
       const size_t lds = std::max(C->walk_lds, C->step_lds);
-      timed_launch(ctx, C, s, 3, [&] { launch_persist(false, P, C->S, lds, s, L, L + kPersistLaunches); });
+      timed_launch(ctx, C, s, 3, [&] { launch_persist(false, P, step_args(C), lds, s, L, L + kPersistLaunches); });
     }
     GG_HIP(hipGetLastError());
     L += kPersistLaunches;
