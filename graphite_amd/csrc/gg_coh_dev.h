@@ -113,6 +113,17 @@ constexpr uint64_t kRng0 = ((uint64_t)(uint32_t)GG_MOSI_RNG_SEED << 16) | 0x330E
 // cannot see compiles to flat accesses)
 #define GG_LDS __attribute__((address_space(3)))
 #define GG_GLB __attribute__((address_space(1)))
+// CS's pointers are global in the device pass (GG_DP), so every access derived
+// from them compiles to global_* instead of flat_* (a flat access counts in
+// both vmcnt and lgkmcnt: each wait for a scalar or LDS result would also wait
+// for it).  The host pass sees plain pointers; the layout is the same.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GG_DP __attribute__((address_space(1)))
+#else
+#define GG_DP
+#endif
+// a host pointer into a CS field (host code is type-checked in the device pass too)
+template <class D, class Q> inline void cs_set(D& dst, Q src) { dst = (D)src; }
 struct Seg { uint32_t line, lo, hi, pad; };       // a run of row (X) / column (Y) `line`: positions [lo, hi]
 // device-driven quantum loop (gg_coherent_run): current quantum, launch index
 // of its step 0, run over, quantum-end arrivals, active / blocked tiles, least
@@ -158,55 +169,55 @@ __device__ __forceinline__ uint32_t class_bits(const CP& P, uint32_t c) { return
 __device__ __forceinline__ uint32_t msg_bits(const CP& P, uint32_t t) { return class_bits(P, len_class(t)); }
 
 struct CS {
-  uint64_t* l1_tag; uint8_t* l1_meta; uint8_t* l1_rr;
-  uint64_t* l2_tag; uint8_t* l2_meta; uint8_t* l2_rr;
-  uint64_t* cc;                          // [L][2][12]
-  uint64_t* mtab;                        // [L][2][2^mt_log] address sets (line | E 1 I 2 F 4), ~0 empty; when tracking
-  unsigned long long* mtc;               // [L][2][GG_NUM_MISS_TYPES] when tracking
-  uint64_t* st;                          // [L][GG_NUM_TILE_STATS]
-  TileSt* ts;                            // [L] the tiles' step state (one 64-B line each)
-  DEnt* dir; uint64_t* dsh;              // [L][E], [L][E][W]
-  DEnt* rep; uint64_t* rsh;              // [L][R], [L][R][W]
-  CReq* rq;                              // [L][QC]
+  GG_DP uint64_t* l1_tag; GG_DP uint8_t* l1_meta; GG_DP uint8_t* l1_rr;
+  GG_DP uint64_t* l2_tag; GG_DP uint8_t* l2_meta; GG_DP uint8_t* l2_rr;
+  GG_DP uint64_t* cc;                          // [L][2][12]
+  GG_DP uint64_t* mtab;                        // [L][2][2^mt_log] address sets (line | E 1 I 2 F 4), ~0 empty; when tracking
+  GG_DP unsigned long long* mtc;               // [L][2][GG_NUM_MISS_TYPES] when tracking
+  GG_DP uint64_t* st;                          // [L][GG_NUM_TILE_STATS]
+  GG_DP TileSt* ts;                            // [L] the tiles' step state (one 64-B line each)
+  GG_DP DEnt* dir; GG_DP uint64_t* dsh;              // [L][E], [L][E][W]
+  GG_DP DEnt* rep; GG_DP uint64_t* rsh;              // [L][R], [L][R][W]
+  GG_DP CReq* rq;                              // [L][QC]
   // MOSI: the FIFO's other request fields, the entries' Random states (XOR
   // kRng0), the cached data list + length, the protocol event counters
-  CReqX* rqx;                            // [L][QC]
-  uint64_t* drng; uint64_t* rrng;        // [L][E], [L][R]
-  uint64_t* cdl; uint32_t* ncdl;         // [L][kCdl], [L]
-  uint64_t* ps;                          // [L][GG_NUM_PROTO_STATS]
-  HQueue* dq; HNode* dnd;                // DRAM queue per tile
-  const uint32_t* gtile; const int32_t* ltile; const uint32_t* shard;   // local -> tile, tile -> local (-1), tile -> shard
-  const uint4* tinfo;                    // [L] {tile, X run, Y run, 0} of a local tile: one load, no chain
-  const uint64_t* addr; const uint32_t* meta; uint64_t* out;
-  gg_cmsg* pool0; gg_cmsg* pool1; uint32_t* npool;    // records of even / odd steps, alloc counters [2]
-  uint32_t* inb0; uint32_t* inb1;       // inbox record lists [L][IC]
-  uint32_t* arv0; uint32_t* arv1;       // hop-by-hop SELF lists [L][IC]
-  uint32_t* cnt4;                       // [L][4]: the lists' lengths {inbox even, odd, SELF even, odd}
-  uint32_t* xl; uint32_t* nxl; uint32_t* yl; uint32_t* nyl;           // segment lists [n][seg_cap], [n]
-  const Seg* segx; const Seg* segy;
-  const uint32_t* tseg;                  // [T][2]: X run, Y run of a tile (~0 if not owned)
-  gg_cmsg* bnd; uint32_t* bnd_cnt;       // held for the quantum boundary
-  uint32_t* ring; uint32_t* quiet;       // records sent per step (mod 4); quiet flag of the quantum
-  uint32_t* imp;                         // [2] held packets imported for the quantum of parity Q & 1
-  uint32_t* live;                        // [4] launch L & 3: step index + 1 of a step launch, 0 otherwise
-  uint64_t* qs;                          // device-driven run: QS_* below
-  uint64_t* ri; uint32_t* err;
-  HQueue* nq; HNode* nnd;                // router queues [tile * 6 + port]
-  uint64_t* ctr;                         // NoC counters [T][GG_NUM_NET_COUNTERS]
-  uint64_t* gscr;                        // [L][6 * IC] ordering scratch beyond kInLds
-  unsigned long long* prof;              // GG_COH_PROFILE=1: shader-clock cycles per phase (diagnostics)
+  GG_DP CReqX* rqx;                            // [L][QC]
+  GG_DP uint64_t* drng; GG_DP uint64_t* rrng;        // [L][E], [L][R]
+  GG_DP uint64_t* cdl; GG_DP uint32_t* ncdl;         // [L][kCdl], [L]
+  GG_DP uint64_t* ps;                          // [L][GG_NUM_PROTO_STATS]
+  GG_DP HQueue* dq; GG_DP HNode* dnd;                // DRAM queue per tile
+  GG_DP const uint32_t* gtile; GG_DP const int32_t* ltile; GG_DP const uint32_t* shard;   // local -> tile, tile -> local (-1), tile -> shard
+  GG_DP const uint4* tinfo;                    // [L] {tile, X run, Y run, 0} of a local tile: one load, no chain
+  GG_DP const uint64_t* addr; GG_DP const uint32_t* meta; GG_DP uint64_t* out;
+  GG_DP gg_cmsg* pool0; GG_DP gg_cmsg* pool1; GG_DP uint32_t* npool;    // records of even / odd steps, alloc counters [2]
+  GG_DP uint32_t* inb0; GG_DP uint32_t* inb1;       // inbox record lists [L][IC]
+  GG_DP uint32_t* arv0; GG_DP uint32_t* arv1;       // hop-by-hop SELF lists [L][IC]
+  GG_DP uint32_t* cnt4;                       // [L][4]: the lists' lengths {inbox even, odd, SELF even, odd}
+  GG_DP uint32_t* xl; GG_DP uint32_t* nxl; GG_DP uint32_t* yl; GG_DP uint32_t* nyl;           // segment lists [n][seg_cap], [n]
+  GG_DP const Seg* segx; GG_DP const Seg* segy;
+  GG_DP const uint32_t* tseg;                  // [T][2]: X run, Y run of a tile (~0 if not owned)
+  GG_DP gg_cmsg* bnd; GG_DP uint32_t* bnd_cnt;       // held for the quantum boundary
+  GG_DP uint32_t* ring; GG_DP uint32_t* quiet;       // records sent per step (mod 4); quiet flag of the quantum
+  GG_DP uint32_t* imp;                         // [2] held packets imported for the quantum of parity Q & 1
+  GG_DP uint32_t* live;                        // [4] launch L & 3: step index + 1 of a step launch, 0 otherwise
+  GG_DP uint64_t* qs;                          // device-driven run: QS_* below
+  GG_DP uint64_t* ri; GG_DP uint32_t* err;
+  GG_DP HQueue* nq; GG_DP HNode* nnd;                // router queues [tile * 6 + port]
+  GG_DP uint64_t* ctr;                         // NoC counters [T][GG_NUM_NET_COUNTERS]
+  GG_DP uint64_t* gscr;                        // [L][6 * IC] ordering scratch beyond kInLds
+  GG_DP unsigned long long* prof;              // GG_COH_PROFILE=1: shader-clock cycles per phase (diagnostics)
   // GG_COH_TRACE=n: per launch L < n, plain stores of every tile's / walker
   // block's phase clocks (trs [L][owned tile][16], trw [L][stage][block][8]);
   // no atomics, so the run's timing is barely disturbed (diagnostics)
-  unsigned long long* trs; unsigned long long* trw; uint32_t tr_n, tr_wb;
+  GG_DP unsigned long long* trs; GG_DP unsigned long long* trw; uint32_t tr_n, tr_wb;
   // GG_COH_TRACE_EV=n: walker events of launches [kTrEv0, kTrEv0 + n): per block
   // 128 x {memtime at the serve decision, after the request, after the
   // publish, packet | position << 16 | wave << 24 | poll count << 32} and a count
-  unsigned long long* tre; uint32_t tre_n;
-  uint32_t* gbar;                        // grid barrier counter of k_c_persist
+  GG_DP unsigned long long* tre; uint32_t tre_n;
+  GG_DP uint32_t* gbar;                        // grid barrier counter of k_c_persist
   // in-kernel launch timing (gg_set_timing mode 2): per timed launch slot
   // {first workgroup start, last workgroup end} on the s_memrealtime clock
-  unsigned long long* kt; uint32_t kt_slot, kt_stride;   // timing mode 2: per block {start, end} of launch slot kt_slot
+  GG_DP unsigned long long* kt; uint32_t kt_slot, kt_stride;   // timing mode 2: per block {start, end} of launch slot kt_slot
 };
 // profile slots: step phases 0..5 summed over tiles, 8 = sum over steps of the slowest tile;
 // walker: 16 staging+load, 17 event loop, 18 hand-off+write back, 19 events, 20 sum of slowest walker per launch (X),
@@ -668,7 +679,7 @@ struct Tile {
   int32_t oh = NO_ENT; bool od = false;  // the open directory entry (eopen) and whether it changed
   uint64_t oaddr = 0, osh = 0; int32_t oown = -1; uint32_t ost = 0, onsh = 0;
   bool tr_on = false;                   // GG_COH_TRACE: cycles by handler part (dget, sharers, DRAM, send, FIFO, sharer words)
-  uint64_t tra[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t tra[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};   // + directory_msg before the run, the run, entry opens
   // MOSI: event counter increments (lane k holds counter k), the cached data
   // list's length (and at step start), the FIFO's MOSI fields
   uint64_t pd = 0;
@@ -815,6 +826,12 @@ struct Tile {
   {
     h = __builtin_amdgcn_readfirstlane(h);
     if (h == oh) return;
+    const uint64_t c0 = tr_on ? __builtin_amdgcn_s_memtime() : 0;
+    eopen_(h);
+    if (tr_on) tra[8] += __builtin_amdgcn_s_memtime() - c0;
+  }
+  __device__ __forceinline__ void eopen_(int32_t h)
+  {
     eclose();
     const DEnt* e = ent(h);
     oaddr = e->addr; oown = e->owner; ost = e->dstate; onsh = e->nsh;
@@ -1254,6 +1271,7 @@ struct Tile {
   // handleMsgFromL2Cache (:43-96) + processInv/Flush/WbRepFromL2Cache (:410-543)
   __device__ __forceinline__ void directory_msg(const HMsg& m)
   {
+    const uint64_t c0 = tr_on ? __builtin_amdgcn_s_memtime() : 0;
     uint64_t t = m.arrival_ps;           // __handleMsgFromNetwork: setCurrTime(packet.time)
     const uint64_t a = m.addr;
     Work w{a, W_NONE, 0, 0, 0, 0};
@@ -1305,7 +1323,10 @@ struct Tile {
         return;
       }
     }
+    const uint64_t c1 = tr_on ? __builtin_amdgcn_s_memtime() : 0;
+    if (tr_on) tra[6] += c1 - c0;
     if (w.kind != W_NONE) directory_run(w, t);
+    if (tr_on) tra[7] += __builtin_amdgcn_s_memtime() - c1;
   }
 
   // ---- L1 / L2 controllers ---------------------------------------------------
@@ -2970,7 +2991,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
     r[10] = _sb; r[11] = _sc; r[12] = _sd; r[13] = _se; r[14] = _q1b; r[15] = _sf;
     r[16] = _q1; r[17] = _q2; r[18] = _q3; r[19] = _q4;
     r[20] = _hd; r[21] = _hl; r[22] = _hn;
-    for (int i = 0; i < 6; ++i) r[23 + i] = T.tra[i];
+    for (int i = 0; i < 9; ++i) r[23 + i] = T.tra[i];
   }
   // the tile's next start for the shard scheduler: finished, blocked, or clock + gap
   if (T.rec >= T.rec_end) return kNsFin;

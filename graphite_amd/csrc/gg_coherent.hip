@@ -256,7 +256,7 @@ template <class F> static void timed_launch(gg_ctx* ctx, gg_coh_state* C, hipStr
       C->allocs.push_back((void*)C->kt_dev);
   if (ctx->timing >= 2 && C->kt_dev && kind < 3 && C->kt_kind.size() < kKtRing) {
     C->nlaunch[kind]++;
-    C->S.kt = C->kt_dev;
+    cs_set(C->S.kt, C->kt_dev);
     C->S.kt_slot = (uint32_t)C->kt_kind.size();
     C->kt_kind.push_back(kind);
     fn();
@@ -333,17 +333,19 @@ static uint64_t lat_ps_host(uint64_t cycles, double f) { return (uint64_t)ceil((
 
 template <class T> static gg_status dalloc(gg_coh_state* C, T** p, uint64_t n)
 {
-  hipError_t e = hipMalloc((void**)p, sizeof(T) * (n ? n : 1));
+  void* v = nullptr;
+  hipError_t e = hipMalloc(&v, sizeof(T) * (n ? n : 1));
   if (e != hipSuccess) return gg_hip_check(e, "hipMalloc(coherent state)");
-  C->allocs.push_back((void*)*p);
+  *p = (T*)v;
+  C->allocs.push_back(v);
   return GG_OK;
 }
-template <class T> static gg_status dupload(gg_coh_state* C, const T** p, const std::vector<T>& v)
+template <class D, class T> static gg_status dupload(gg_coh_state* C, D* p, const std::vector<T>& v)
 {
   T* d = nullptr;
   if (gg_status st = dalloc(C, &d, v.size())) return st;
   if (!v.empty()) GG_HIP(hipMemcpy(d, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice));
-  *p = d;
+  cs_set(*p, d);
   return GG_OK;
 }
 
@@ -620,9 +622,13 @@ static gg_status coh_alloc(gg_ctx* ctx)
   if ((st = dalloc(C, &C->Sd, 1))) return st;
   if ((st = dalloc(C, &C->ecount_dev, 2 * (uint64_t)P.K + 2))) return st;
   if ((st = dalloc(C, &C->offs_dev, (uint64_t)P.T + 1))) return st;
-  S.ctr = gg_noc_ctr(ctx);
-  gg_noc_queues(ctx, &S.nq, &S.nnd);
-  S.err = ctx->err_dev;
+  cs_set(S.ctr, gg_noc_ctr(ctx));
+  {
+    gg::HQueue* q; gg::HNode* nd;
+    gg_noc_queues(ctx, &q, &nd);
+    cs_set(S.nq, q); cs_set(S.nnd, nd);
+  }
+  cs_set(S.err, ctx->err_dev);
   return GG_OK;
 }
 
@@ -651,7 +657,7 @@ gg_status gg_coherent_begin(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_ou
   for (uint32_t t = 0; t < P.T; ++t)
     if (tr->tile_offsets[t] > tr->tile_offsets[t + 1]) return gg_fail(GG_ERR_INVALID, "tile_offsets not monotone");
   if (tr->num_records && (!tr->addr_dev || !tr->meta_dev)) return gg_fail(GG_ERR_INVALID, "NULL trace pointers");
-  C->S.addr = tr->addr_dev; C->S.meta = tr->meta_dev; C->S.out = access_out_dev;
+  cs_set(C->S.addr, tr->addr_dev); cs_set(C->S.meta, tr->meta_dev); cs_set(C->S.out, access_out_dev);
   GG_HIP(hipMemcpyAsync(C->Pd, &C->P, sizeof(CP), hipMemcpyHostToDevice, s));
   GG_HIP(hipMemcpyAsync(C->Sd, &C->S, sizeof(CS), hipMemcpyHostToDevice, s));
   C->n_records = tr->num_records;

@@ -4,8 +4,9 @@
 // golden fixtures tests/golden/coh_*.  TEST INFRASTRUCTURE ONLY: never shipped,
 // never linked into graphite_amd/.
 //
-// Reference code exercised verbatim (-DNDEBUG: the logging back end needs
-// Boost, absent from this image; see oracle/ref/Makefile):
+// Reference code exercised verbatim, its own assert() calls active (only
+// log.h's LOG_* are compiled out: the logging back end needs Boost, absent
+// from this image; oracle/ref/assert_prelude.h):
 //   L1CacheCntlr          pr_l1_pr_l2_dram_directory_msi/l1_cache_cntlr.cc
 //   L2CacheCntlr          pr_l1_pr_l2_dram_directory_msi/l2_cache_cntlr.cc
 //   DramDirectoryCntlr    pr_l1_pr_l2_dram_directory_msi/dram_directory_cntlr.cc

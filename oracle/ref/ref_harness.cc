@@ -4,9 +4,10 @@
 //
 // TEST INFRASTRUCTURE ONLY: never shipped, never linked into graphite_amd/.
 //
-// Reference code exercised verbatim (compiled with -DNDEBUG because the
-// logging back end common/misc/log.cc needs Boost, which this image lacks; the
-// reference asserts in these files carry no side effects):
+// Reference code exercised verbatim, its own assert() calls active (only
+// log.h's LOG_* are compiled out, because the logging back end
+// common/misc/log.cc needs Boost, which this image lacks;
+// oracle/ref/assert_prelude.h):
 //   CacheSet                      common/tile/memory_subsystem/cache/cache_set.cc
 //   LRUReplacementPolicy          .../cache/lru_replacement_policy.cc
 //   RoundRobinReplacementPolicy   .../cache/round_robin_replacement_policy.cc

@@ -249,7 +249,7 @@ def test_tile_summary_table_matches_reference(tmp_path):
         assert out == reference_table([open(f).read() for f in sel])
 
 
-@pytest.mark.parametrize("name", ["mosi_hot16", "mosi_hot16magic", "mosi_dir16", "mosi_fft10"])
+@pytest.mark.parametrize("name", ["mosi_hot16", "mosi_hot16magic", "mosi_dir16", "mosi_fft10", "mosi_evict16", "mosi_evict16s4"])
 def test_mosi_controller_summaries_match_reference(name):
     """The host mirror's MOSI blocks (writeMosiL2CntlrSummary /
     writeMosiDirectoryCntlrSummary) print the reference's own

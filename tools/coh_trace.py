@@ -30,7 +30,7 @@ def main():
     keys = ["entry", "exit"] + phases + sum(sub.values(), []) + \
         ["span_step", "span_x", "span_y", "gap_sx", "gap_xy", "gap_ys", "crit_na", "crit_ni", "crit_sent",
          "dir_msg_ns", "l2_msg_ns", "crit_dir_msgs", "crit_l2_msgs",
-         "h_dget", "h_sharers", "h_dram", "h_send", "h_fifo", "h_shwords",
+         "h_dget", "h_sharers", "h_dram", "h_send", "h_fifo", "h_shwords", "h_pre", "h_run", "h_eopen",
          "tiles_working", "clock_ghz", "qend", "crit_has_self", "crit_has_inbox", "crit_has_pub"]
     acc = {k: [] for k in keys}
     wacc = {s: {k: [] for k in ("entry", "staging", "loop", "handoff", "exit", "events", "n", "npos", "blocks")}
@@ -72,7 +72,7 @@ def main():
                 hn = int(r[22]); nd, nl = hn & 0xFFFFFFFF, hn >> 32
                 acc["crit_dir_msgs"].append(nd); acc["crit_l2_msgs"].append(nl)
                 if nd: acc["dir_msg_ns"].append(r[20] * f / nd)
-                for i, k in enumerate(("h_dget", "h_sharers", "h_dram", "h_send", "h_fifo", "h_shwords")):
+                for i, k in enumerate(("h_dget", "h_sharers", "h_dram", "h_send", "h_fifo", "h_shwords", "h_pre", "h_run", "h_eopen")):
                     acc[k].append(r[23 + i] * f)
                 if nl: acc["l2_msg_ns"].append(r[21] * f / nl)
             if r[16] > 0:
