@@ -29,7 +29,7 @@ CSTATE_INVALID = 0
 CSTATE_SHARED = 1
 CSTATE_OWNED = 2      # MOSI
 CSTATE_MODIFIED = 4
-PROTO_MSI, PROTO_MOSI = 0, 1          # GG_PROTO_* (caching_protocol/type)
+PROTO_MSI, PROTO_MOSI, PROTO_SHL2_MSI = 0, 1, 2   # GG_PROTO_* (caching_protocol/type)
 MOSI_RNG_SEED = 1                     # GG_MOSI_RNG_SEED
 LOC_INVALID = 0
 LOC_L1D = 3
@@ -64,7 +64,9 @@ MSG_TYPES = ["EX_REQ", "SH_REQ", "INV_REQ", "FLUSH_REQ", "WB_REQ", "EX_REP", "SH
              "UPGRADE_REP", "INV_REP", "FLUSH_REP", "WB_REP"]
 MSG = {n: i + 1 for i, n in enumerate(MSG_TYPES)}
 MSG["NULLIFY_REQ"], MSG["INV_FLUSH_COMBINED_REQ"] = 12, 13
+MSG["DRAM_FETCH_REQ"], MSG["DRAM_STORE_REQ"], MSG["DRAM_FETCH_REP"] = 14, 15, 16   # pr_l1_sh_l2_msi
 CT_SENT_INV_FLUSH_COMBINED = 29       # GG_CT_SENT_INV_FLUSH_COMBINED (MOSI)
+CT_SENT_DRAM_FETCH_REQ, CT_SENT_DRAM_STORE_REQ, CT_SENT_DRAM_FETCH_REP = 29, 30, 31   # pr_l1_sh_l2_msi
 # MOSI event counters, [tile][NUM_PROTO_STATS] (GG_PS_*)
 PROTO_STATS = ["exreq", "exreq_modified", "exreq_shared", "exreq_upgrade", "exreq_uncached",
                "exreq_serialization_ps", "exreq_processing_ps",

@@ -56,7 +56,7 @@
 extern "C" {
 #endif
 
-#define GG_ABI_VERSION 8
+#define GG_ABI_VERSION 9
 
 typedef int gg_status;
 enum {
@@ -221,19 +221,24 @@ typedef struct gg_config {
                                     4 GiB at 4096).  A full table stops the run with
                                     GG_ERR_UNSUPPORTED (no set entry is overwritten). */
   /* ---- caching protocol (caching_protocol/type, carbon_sim.cfg:184) ---- */
-  uint32_t protocol;             /* GG_PROTO_*: pr_l1_pr_l2_dram_directory_msi (0) / _mosi (1) */
+  uint32_t protocol;             /* GG_PROTO_*: pr_l1_pr_l2_dram_directory_msi (0) / _mosi (1) /
+                                    pr_l1_sh_l2_msi (2)                                        */
   uint32_t l1d_track_miss_types; /* l1_dcache/T1/track_miss_types (false): read by the MOSI
                                     protocol only, whose L1CacheCntlr passes the L1-D flag to the
                                     L1-D (…mosi/l1_cache_cntlr.cc:68; MSI passes the L1-I one) */
 } gg_config;
 
 /* Caching protocols of the coherent mode (MemoryManager::createMMU,
- * memory_manager.cc:22-60).  MOSI's DramDirectoryCntlr picks "one sharer"
+ * memory_manager.cc:22-60).  pr_l1_sh_l2_msi: private L1s, the L2 a shared
+ * slice per tile (home = line % tiles) whose lines hold the full-map
+ * directory entries, a DRAM controller per tile reached by DRAM_FETCH /
+ * DRAM_STORE messages; the l2_* geometry is one slice's, the dir_* fields are
+ * not used.  MOSI's DramDirectoryCntlr picks "one sharer"
  * with the directory entry's own drand48 stream (DirectoryEntryFullMap::
  * getOneSharer, directory_entry_full_map.cc:67-74; misc/random.h), which the
  * reference seeds with time(NULL) when the entry is created: the canonical
  * schedule seeds every entry with GG_MOSI_RNG_SEED (one fixed second).      */
-enum { GG_PROTO_MSI = 0, GG_PROTO_MOSI = 1 };
+enum { GG_PROTO_MSI = 0, GG_PROTO_MOSI = 1, GG_PROTO_SHL2_MSI = 2 };
 #define GG_MOSI_RNG_SEED 1
 
 /* Miss types (Cache::MissType, cache.h:45-52), counted per (tile, cache). */
@@ -294,11 +299,13 @@ typedef struct gg_line_info {    /* CacheLineInfo / PrL2CacheLineInfo           
 
 /* ShmemMsg::Type (pr_l1_pr_l2_dram_directory_msi/shmem_msg.h:12-30); MOSI's
  * INV_FLUSH_COMBINED_REQ (…mosi/shmem_msg.h:20, numbered after WB_REQ there)
- * is 13 here so the MSI numbering stays as it is */
+ * is 13 here so the MSI numbering stays as it is; pr_l1_sh_l2_msi's DRAM
+ * messages (…sh_l2_msi/shmem_msg.h:26-30) follow it */
 enum {
   GG_MSG_EX_REQ = 1, GG_MSG_SH_REQ, GG_MSG_INV_REQ, GG_MSG_FLUSH_REQ, GG_MSG_WB_REQ,
   GG_MSG_EX_REP, GG_MSG_SH_REP, GG_MSG_UPGRADE_REP, GG_MSG_INV_REP, GG_MSG_FLUSH_REP,
-  GG_MSG_WB_REP, GG_MSG_NULLIFY_REQ, GG_MSG_INV_FLUSH_COMBINED_REQ
+  GG_MSG_WB_REP, GG_MSG_NULLIFY_REQ, GG_MSG_INV_FLUSH_COMBINED_REQ,
+  GG_MSG_DRAM_FETCH_REQ, GG_MSG_DRAM_STORE_REQ, GG_MSG_DRAM_FETCH_REP
 };
 
 /* One ShmemMsg in flight (64 bytes).  The per-sender sequence number keeps
@@ -357,6 +364,8 @@ enum {
   GG_CT_DRAM_QUEUE_UTILIZED_NS = GG_CT_SENT_BY_TYPE + 11, /* _total_utilized_cycles */
   GG_CT_DRAM_QUEUE_LAST_NS,                               /* _last_request_time     */
   GG_CT_SENT_INV_FLUSH_COMBINED = 29,                     /* MOSI INV_FLUSH_COMBINED_REQs sent */
+  /* pr_l1_sh_l2_msi (no INV_FLUSH_COMBINED_REQ there): its DRAM messages sent */
+  GG_CT_SENT_DRAM_FETCH_REQ = 29, GG_CT_SENT_DRAM_STORE_REQ = 30, GG_CT_SENT_DRAM_FETCH_REP = 31,
   GG_NUM_TILE_STATS = 32
 };
 

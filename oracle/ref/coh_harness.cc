@@ -65,6 +65,12 @@
 #include "pr_l1_pr_l2_dram_directory_mosi/memory_manager.h"
 #undef private
 #undef protected
+#elif defined(GG_PROTO_SHL2)
+// pr_l1_sh_l2_msi (coh_harness_shl2): private L1s, the L2 a shared slice per
+// tile holding each line's directory entry, a DRAM controller per tile
+#include "pr_l1_sh_l2_msi/memory_manager.h"
+#include "pr_l1_sh_l2_msi/l2_cache_hash_fn.h"
+#include "pr_l1_sh_l2_msi/l2_directory_cfg.h"
 #else
 #include "pr_l1_pr_l2_dram_directory_msi/memory_manager.h"
 #endif
@@ -78,6 +84,8 @@ namespace MSI = PrL1PrL2DramDirectoryMOSI;     // (the glue below is written onc
 // that seed (GG_MOSI_RNG_SEED, include/graphite_gpu.h), so every entry starts
 // from the same drand48 state, as entries created in the same second do
 extern "C" time_t time(time_t* t) { if (t) *t = (time_t)1; return (time_t)1; }
+#elif defined(GG_PROTO_SHL2)
+namespace MSI = PrL1ShL2MSI;
 #else
 namespace MSI = PrL1PrL2DramDirectoryMSI;
 #endif
@@ -94,6 +102,13 @@ static UInt32 gg_type(UInt32 t)
   case MSI::ShmemMsg::FLUSH_REP: return 10; case MSI::ShmemMsg::WB_REP: return 11; case MSI::ShmemMsg::NULLIFY_REQ: return 12;
   case MSI::ShmemMsg::INV_FLUSH_COMBINED_REQ: return 13;
   default: CHECK(0); return 0;
+  }
+#elif defined(GG_PROTO_SHL2)
+  // EX_REQ .. WB_REP share the numbering; the DRAM messages follow the MOSI type
+  switch (t) {
+  case MSI::ShmemMsg::DRAM_FETCH_REQ: return 14; case MSI::ShmemMsg::DRAM_STORE_REQ: return 15;
+  case MSI::ShmemMsg::DRAM_FETCH_REP: return 16; case MSI::ShmemMsg::NULLIFY_REQ: return 12;
+  default: CHECK(t >= 1 && t <= 11); return t;
   }
 #else
   return t;
@@ -503,6 +518,8 @@ NetPacket::NetPacket() : time(0), type(INVALID_PACKET_TYPE), sender(INVALID_CORE
 #ifdef GG_PROTO_MOSI
 CachingProtocolType MemoryManager::_caching_protocol_type = PR_L1_PR_L2_DRAM_DIRECTORY_MOSI;
 ofstream MSI::MemoryManager::_cache_line_replication_file;
+#elif defined(GG_PROTO_SHL2)
+CachingProtocolType MemoryManager::_caching_protocol_type = PR_L1_SH_L2_MSI;
 #else
 CachingProtocolType MemoryManager::_caching_protocol_type = PR_L1_PR_L2_DRAM_DIRECTORY_MSI;
 #endif
@@ -550,6 +567,89 @@ void MemoryManager::wakeUpAppThread()        // the reply handler hands control 
 void MemoryManager::waitForAppThread() {}    // ... which returns once its access has completed
 void MemoryManager::wakeUpSimThread() {}
 
+#ifdef GG_PROTO_SHL2
+// carbon_sim.cfg defaults (l1_icache/T1 :208-217, l1_dcache/T1 :219-228,
+// l2_cache/T1 :230-239, l2_directory :260-263, dram :265-273); the
+// constructor body follows â€¦sh_l2_msi/memory_manager.cc:116-185 (the config
+// reads are Boost's, so the values are given here)
+MSI::MemoryManager::MemoryManager(Tile* tile) : ::MemoryManager(tile), _dram_cntlr(NULL), _dram_cntlr_present(false)
+{
+  _cache_line_size = 64;
+  vector<tile_id_t> ctrl;
+  for (UInt32 i = 0; i < H.T; ++i) ctrl.push_back(i);
+  _dram_home_lookup = new AddressHomeLookup(ceilLog2(64), ctrl, 64);
+  _L2_cache_home_lookup = new AddressHomeLookup(ceilLog2(64), ctrl, 64);
+  _dram_cntlr_present = true;
+  _dram_cntlr = new DramCntlr(this, (float)g_dram_cost, g_dram_bw, true, "history_tree", 64);
+  L2DirectoryCfg::setDirectoryType(DirectoryEntry::parseDirectoryType("full_map"));
+  L2DirectoryCfg::setMaxHWSharers(64);
+  L2DirectoryCfg::setMaxNumSharers(Config::getSingleton()->getTotalTiles());
+  _L1_cache_cntlr = new L1CacheCntlr(this, _L2_cache_home_lookup, 64, 16, 4, 1, "lru", 1, 1, "parallel", false,
+                                     32, 4, 1, "lru", 1, 1, "parallel", false);
+  _L2_cache_cntlr = new L2CacheCntlr(this, _dram_home_lookup, 64, 512, H.l2_assoc, 1, "lru", 8, 3, "parallel", false);
+}
+MSI::MemoryManager::~MemoryManager() {}
+void MSI::MemoryManager::enableModels()                                    // â€¦sh_l2_msi/memory_manager.cc:378-393
+{
+  getL1ICache()->enable(); getL1DCache()->enable(); getL2Cache()->enable();
+  _L2_cache_cntlr->enable();
+  g_dram[_dram_cntlr].enabled = true;
+  ::MemoryManager::enableModels();
+}
+void MSI::MemoryManager::disableModels() { ::MemoryManager::disableModels(); }
+void MSI::MemoryManager::outputSummary(std::ostream&, const Time&) {}
+void MSI::MemoryManager::computeEnergy(const Time&) {}
+double MSI::MemoryManager::getDynamicEnergy() { return 0; }
+double MSI::MemoryManager::getLeakageEnergy() { return 0; }
+int MSI::MemoryManager::getDVFS(module_t, double&, double&) { return -1; }
+int MSI::MemoryManager::setDVFS(module_t, double, voltage_option_t, const Time&) { return -1; }
+bool MSI::MemoryManager::coreInitiateMemoryAccess(MemComponent::Type mc, Core::lock_signal_t ls, Core::mem_op_t op,
+                                                  IntPtr address, UInt32 offset, Byte* buf, UInt32 len, bool modeled)
+{                                                                           // â€¦sh_l2_msi/memory_manager.cc:202-213
+  return _L1_cache_cntlr->processMemOpFromCore(mc, ls, op, address, offset, buf, len, modeled);
+}
+void MSI::MemoryManager::handleMsgFromNetwork(NetPacket& packet)           // â€¦sh_l2_msi/memory_manager.cc:215-294
+{
+  core_id_t sender = packet.sender;
+  ShmemMsg* shmem_msg = ShmemMsg::getShmemMsg((Byte*)packet.data);
+  const MemComponent::Type snd = shmem_msg->getSenderMemComponent();
+  switch (shmem_msg->getReceiverMemComponent()) {
+  case MemComponent::L1_ICACHE:
+  case MemComponent::L1_DCACHE:
+    if (snd == MemComponent::CORE) { CHECK(sender.tile_id == getTile()->getId()); _L1_cache_cntlr->handleMsgFromCore(shmem_msg); }
+    else { CHECK(snd == MemComponent::L2_CACHE); _L1_cache_cntlr->handleMsgFromL2Cache(sender.tile_id, shmem_msg); }
+    break;
+  case MemComponent::L2_CACHE:
+    if (snd == MemComponent::L1_ICACHE || snd == MemComponent::L1_DCACHE) _L2_cache_cntlr->handleMsgFromL1Cache(sender.tile_id, shmem_msg);
+    else { CHECK(snd == MemComponent::DRAM_CNTLR); _L2_cache_cntlr->handleMsgFromDram(sender.tile_id, shmem_msg); }
+    break;
+  case MemComponent::DRAM_CNTLR:
+    CHECK(_dram_cntlr_present && snd == MemComponent::L2_CACHE);
+    _dram_cntlr->handleMsgFromL2Cache(sender.tile_id, shmem_msg);
+    break;
+  default: CHECK(0);
+  }
+  if (shmem_msg->getDataLength() > 0) delete[] shmem_msg->getDataBuf();
+  delete shmem_msg;
+}
+// L2CacheHashFn (â€¦sh_l2_msi/l2_cache_hash_fn.cc: its translation unit includes
+// simulator.h, which needs Boost): the XOR fold of the address' set-index fields
+MSI::L2CacheHashFn::L2CacheHashFn(UInt32 cache_size, UInt32 associativity, UInt32 cache_line_size)
+  : CacheHashFn(cache_size, associativity, cache_line_size)                  // :8-13
+{
+  _log_num_application_tiles = floorLog2(Config::getSingleton()->getApplicationTiles());
+  _log_num_sets = floorLog2(_num_sets);
+}
+MSI::L2CacheHashFn::~L2CacheHashFn() {}
+UInt32 MSI::L2CacheHashFn::compute(IntPtr address)                               // :18-34
+{
+  if (_log_num_sets == 0) return 0;
+  IntPtr set = 0;
+  for (UInt32 i = _log_cache_line_size; (i + _log_num_sets) <= (sizeof(IntPtr) * 8); i += _log_num_sets)
+    set = set ^ getBits<IntPtr>(address, i + _log_num_sets, i);
+  return (UInt32)set;
+}
+#else
 MSI::MemoryManager::MemoryManager(Tile* tile) : ::MemoryManager(tile), _dram_directory_cntlr(NULL), _dram_cntlr(NULL),
                                                 _dram_cntlr_present(false)
 {
@@ -619,6 +719,7 @@ void MSI::MemoryManager::handleMsgFromNetwork(NetPacket& packet)           // â€
   if (shmem_msg->getDataLength() > 0) delete[] shmem_msg->getDataBuf();
   delete shmem_msg;
 }
+#endif
 // the MSI incrCurrTime (â€¦msi/memory_manager.cc:356-380)
 void MSI::MemoryManager::incrCurrTime(MemComponent::Type mc, CachePerfModel::AccessType at)
 {
@@ -636,8 +737,14 @@ void MSI::MemoryManager::sendMsg(tile_id_t receiver, ShmemMsg& msg)
   const UInt32 src = getTile()->getId();
   Time t = getShmemPerfModel()->getCurrTime();
   Byte* buf = msg.makeMsgBuf();
-  if ((UInt32)receiver == src && msg.getReceiverMemComponent() == MemComponent::L2_CACHE &&
-      (msg.getSenderMemComponent() == MemComponent::L1_DCACHE || msg.getSenderMemComponent() == MemComponent::L1_ICACHE)) {
+#ifdef GG_PROTO_SHL2
+  // the core -> L1 request of a miss (â€¦sh_l2_msi/l1_cache_cntlr.cc:131-136) is handled at once
+  const bool at_once = (UInt32)receiver == src && msg.getSenderMemComponent() == MemComponent::CORE;
+#else
+  const bool at_once = (UInt32)receiver == src && msg.getReceiverMemComponent() == MemComponent::L2_CACHE &&
+      (msg.getSenderMemComponent() == MemComponent::L1_DCACHE || msg.getSenderMemComponent() == MemComponent::L1_ICACHE);
+#endif
+  if (at_once) {
     // the L1 -> L2 request of a miss is handled at once (DESIGN.md Â§Mode C)
     NetPacket p; p.time = t; p.sender = Tile::getMainCoreId(src); p.receiver = p.sender;
     p.length = msg.getMsgLen(); p.data = buf;
@@ -654,6 +761,7 @@ void MSI::MemoryManager::sendMsg(tile_id_t receiver, ShmemMsg& msg)
   g_step.push_back(m);
   S.st[S_SENT]++;
   if (m.type == 13) S.st[S_SENT_IFC]++;                                      // INV_FLUSH_COMBINED_REQ (MOSI)
+  else if (m.type >= 14) S.st[S_SENT_IFC + m.type - 14]++;                  // DRAM_FETCH_REQ / STORE_REQ / FETCH_REP (sh_l2)
   else S.st[S_BYTYPE + m.type - 1]++;
 }
 void MSI::MemoryManager::broadcastMsg(ShmemMsg&) { CHECK(0); }   // full_map never broadcasts
@@ -671,7 +779,7 @@ Tile::~Tile() { delete _memory_manager; }
 static UInt32 modeled_bits(UInt32 type)        // network_model.cc:185-200 + shmem_msg.cc:100-125 (â€¦mosi/shmem_msg.cc:122-151)
 {
   UInt32 idb = H.T > 1 ? ceilLog2(H.T) : 0;
-  bool data = type == 6 || type == 7 || type == 10 || type == 11;            // EX_REP, SH_REP, FLUSH_REP, WB_REP
+  bool data = type == 6 || type == 7 || type == 10 || type == 11 || type == 15 || type == 16;   // EX_REP, SH_REP, FLUSH_REP, WB_REP, DRAM_STORE_REQ, DRAM_FETCH_REP
   return 2 * idb + 4 + 48 + (data ? 512 : 0) + (type == 13 ? idb : 0);   // INV_FLUSH_COMBINED_REQ: + single receiver
 }
 static UInt64 lat_ps(UInt64 cycles) { return (UInt64)ceil(((double)1000 * cycles) / 1.0); }
@@ -930,8 +1038,10 @@ static void run_case(FILE* man, bool first, const char* name, UInt32 T, UInt32 N
     HTile& X = g_t[t];
     UInt64* s = &st[(size_t)t * S_N];
     memcpy(s, X.st, sizeof(X.st));
+#ifndef GG_PROTO_SHL2                                        // (sh_l2: the directory lives in the L2 lines)
     DirectoryCache* dc = X.mm->getDramDirectoryCache();
     s[S_DACC] = dcount(dc)[DC_ACC]; s[S_DEV] = dcount(dc)[DC_EV]; s[S_DBI] = dcount(dc)[DC_BI];
+#endif
     HDram& d = g_dram[X.mm->getDramCntlr()];
     s[S_DRAM] = d.n; s[S_DRAMLAT] = d.lat; s[S_DRAMQD] = d.qd; s[S_DRAMQR] = d.qreq;
     s[S_DRAMQA] = d.q ? d.q->analytical_requests : 0;
@@ -997,7 +1107,38 @@ static void run_case(FILE* man, bool first, const char* name, UInt32 T, UInt32 N
 int main(int argc, char** argv)
 {
   g_dir = argc > 1 ? argv[1] : ".";
-#ifdef GG_PROTO_MOSI
+#if defined(GG_PROTO_SHL2)
+  // pr_l1_sh_l2_msi: the hotspot / stress shapes of the MSI fixtures (shared
+  // L2 slices: remote L2 hits, DRAM fetches and stores through the DRAM
+  // controller, L2 evictions with NULLIFY of their sharers, upgrade replies)
+  // and the reference's FFT
+  string mp = g_dir + "/coh_shl2_manifest.json";
+  FILE* man = fopen(mp.c_str(), "w");
+  CHECK(man);
+  fprintf(man, "{\n");
+  run_case(man, true, "shl2_private16", 16, 1500, 0, 1, 1, 0, 16);
+  run_case(man, false, "shl2_hot16", 16, 1500, 64, 1, 1, 0, 16);
+  run_case(man, false, "shl2_hot16magic", 16, 1000, 8, 1, 0, 0, 16);
+  run_case(man, false, "shl2_shard64", 64, 400, 32, 8, 1, 0, 16);
+  run_case(man, false, "shl2_shard256", 256, 150, 64, 8, 1, 0, 16);
+  run_case(man, false, "shl2_stress256w16", 256, 96, 0, 8, 1, 0, 16, 16, 1);
+  run_case(man, false, "shl2_shard1024", 1024, 24, 256, 8, 1, 0, 16);
+  // L2 slice evictions (2-way slices; a 1-way slice whose one line waits on a
+  // request has no replacement candidate, l2_cache_replacement_policy.cc:55-66):
+  // NULLIFY of sharers and owners, DRAM stores
+  run_case(man, false, "shl2_evict16", 16, 12000, 64, 1, 1, 0, 16, 2);
+  run_case(man, false, "shl2_evict16s4", 16, 12000, 64, 4, 1, 0, 16, 2);
+  if (argc > 2) {
+    RawTrace fft;
+    read_raw(string(argv[2]) + ".addr", fft.addr);
+    read_raw(string(argv[2]) + ".meta", fft.meta);
+    read_raw(string(argv[2]) + ".offs", fft.offs);
+    run_case(man, false, "shl2_fft10", 16, 0, 0, 1, 1, 0, 16, 8, 2, &fft);
+  }
+  fprintf(man, "\n}\n");
+  fclose(man);
+  return 0;
+#elif defined(GG_PROTO_MOSI)
   // pr_l1_pr_l2_dram_directory_mosi: the hotspot / stress shapes of the MSI
   // fixtures (OWNED lines, upgrade replies, combined invalidate-flush, the
   // directory's cached data, NULLIFY of OWNED entries) and the reference's FFT

@@ -48,10 +48,16 @@ def coh_mosi_manifest():
         return json.load(f)
 
 
+def coh_shl2_manifest():
+    with open(os.path.join(GOLDEN, "coh_shl2_manifest.json")) as f:
+        return json.load(f)
+
+
 def coh_case(name, m):
     """(cfg, addr, meta, offsets, expected dict) of a coherent-mode fixture written
     by oracle/ref/coh_harness.cc (the reference's MSI controllers; "mosi_*"
-    names: coh_harness_mosi, the MOSI controllers, plus their event counters)."""
+    names: coh_harness_mosi, the MOSI controllers, plus their event counters;
+    "shl2_*": coh_harness_shl2, the shared-L2 MSI controllers)."""
     from graphite_amd import config as C
     from oracle import pyoracle as po
     T, N = m["tiles"], m["per_tile"]
@@ -62,6 +68,8 @@ def coh_case(name, m):
     mosi = name.startswith("mosi_")
     if mosi:
         kw.update(protocol=C.PROTO_MOSI)
+    if name.startswith("shl2_"):                     # coh_harness_shl2: pr_l1_sh_l2_msi
+        kw.update(protocol=C.PROTO_SHL2_MSI)
     cfg = C.default_config(T, **kw)
     wl = m.get("workload", "hotspot")
     if wl == "stress":

@@ -224,6 +224,45 @@ def test_coherent_mosi_oracle_matches_reference_controllers(name):
     assert ri[C.RUN_INFO.index("steps")] == exp["steps"]
 
 
+# ---- coherent mode, shared L2: pinned by the reference's pr_l1_sh_l2_msi ----
+@pytest.mark.parametrize("name", sorted(G.coh_shl2_manifest()))
+def test_coherent_shl2_oracle_matches_reference_controllers(name):
+    """The shared-L2 restatement (oracle/gg_coherent.inc, protocol =
+    GG_PROTO_SHL2_MSI) == pr_l1_sh_l2_msi's L1CacheCntlr / L2CacheCntlr /
+    DramCntlr compiled from /root/reference (coh_harness_shl2): access words,
+    tile statistics (DRAM_FETCH_REQ / STORE_REQ / FETCH_REP in slots 29-31),
+    L1-D and L2-slice counters, NoC counters, quanta / steps."""
+    from graphite_amd import config as C
+    cfg, a, m, o, exp = G.coh_case(name, G.coh_shl2_manifest()[name])
+    oc = po.OracleCoherent(cfg)
+    out = oc.run(a, m, o)
+    np.testing.assert_array_equal(out, exp["out"])
+    np.testing.assert_array_equal(oc.tile_stats(), exp["stats"])
+    np.testing.assert_array_equal(oc.cache_counters(), exp["cache"])
+    nc = oc.net_counters()[:, [C.NET_COUNTERS.index(k) for k in G.NET3]]
+    np.testing.assert_array_equal(nc, exp["net"])
+    ri = oc.run_info()
+    assert ri[C.RUN_INFO.index("quanta")] == exp["quanta"]
+    assert ri[C.RUN_INFO.index("steps")] == exp["steps"]
+
+
+def test_shl2_fixtures_exercise_the_protocol():
+    """The shared-L2 fixtures reach the slice's paths: remote L2 hits (SH_REPs
+    beyond the DRAM fetches), upgrade replies, slice evictions with NULLIFY
+    (invalidations of sharers, flushes of owners) and DRAM stores of dirty lines."""
+    tot = {}
+    for name in G.coh_shl2_manifest():
+        cfg, a, m, o, exp = G.coh_case(name, G.coh_shl2_manifest()[name])
+        tot[name] = (exp["stats"].sum(0), exp["cache"][:, 1].sum(0))
+    from graphite_amd import config as C
+    st = sum(t[0] for t in tot.values())
+    by = lambda k: int(st[C.TILE_STATS.index("sent_%s" % k.lower())])
+    assert by("UPGRADE_REP") > 0 and by("WB_REQ") > 0 and by("FLUSH_REQ") > 0
+    assert by("SH_REP") + by("EX_REP") > int(st[C.CT_SENT_DRAM_FETCH_REP])    # L2 hits at the home slice
+    assert int(tot["shl2_evict16"][1][C.CACHE_COUNTERS.index("evictions")]) > 0
+    assert int(st[C.CT_SENT_DRAM_STORE_REQ]) > 0
+
+
 def test_mosi_fixtures_exercise_the_protocol():
     """The MOSI fixtures reach what MSI lacks: upgrade replies, combined
     invalidate-flush requests, OWNED write-backs (dirty evictions / shared
