@@ -78,6 +78,8 @@ enum { M_EX_REQ = GG_MSG_EX_REQ, M_SH_REQ = GG_MSG_SH_REQ, M_INV_REQ = GG_MSG_IN
 enum { DS_UNCACHED = 0, DS_SHARED = 1, DS_MODIFIED = 2, DS_OWNED = 3 /* MOSI */ };
 enum { ST_I = 0, ST_S = 1, ST_M = 2, ST_O = 3 /* MOSI */ };   // meta byte bits 0-1
 enum { M_UPGRADE_REP = GG_MSG_UPGRADE_REP, M_IFC_REQ = GG_MSG_INV_FLUSH_COMBINED_REQ };
+enum { M_DRAM_FETCH_REQ = GG_MSG_DRAM_FETCH_REQ, M_DRAM_STORE_REQ = GG_MSG_DRAM_STORE_REQ,   // pr_l1_sh_l2_msi
+       M_DRAM_FETCH_REP = GG_MSG_DRAM_FETCH_REP };
 enum { P_SELF = 0, P_LEFT, P_RIGHT, P_DOWN, P_UP, P_INJ };   // network_model_emesh_hop_by_hop.h:41-48 (+ injection)
 #define INV_ADDR (~0ull)
 #define NO_ENT (-0x7fffffff)
@@ -88,7 +90,8 @@ __device__ __forceinline__ bool to_directory(uint32_t t)
 }
 __device__ __forceinline__ bool has_data(uint32_t t)
 {
-  return t == M_EX_REP || t == M_SH_REP || t == M_FLUSH_REP || t == M_WB_REP;
+  return t == M_EX_REP || t == M_SH_REP || t == M_FLUSH_REP || t == M_WB_REP ||
+         t == M_DRAM_STORE_REQ || t == M_DRAM_FETCH_REP;            // …sh_l2_msi/shmem_msg.cc:128-140
 }
 // modeled length class of a message (ShmemMsg::getModeledLength, shmem_msg.cc:100-125,
 // …mosi/shmem_msg.cc:122-151): 0 request, 1 with a cache line, 2 MOSI
@@ -160,7 +163,8 @@ struct CP {
   uint32_t no_hit_runs;                    // 1: every record through app_access (hit runs off; 0 in the build)
   uint32_t mt1, mt2, mt_log;               // miss-type tracking of the L1-D / L2 (cfg flags), log2 set capacity
   uint32_t fast;                           // k_c_step<true> (Tile's F): register queues only, no miss types
-  uint32_t mosi;                           // pr_l1_pr_l2_dram_directory_mosi: k_c_step<false, true> (Tile's MO)
+  uint32_t mosi;                           // pr_l1_pr_l2_dram_directory_mosi: k_c_step<false, 1> (Tile's PR = 1)
+  uint32_t shl2;                           // pr_l1_sh_l2_msi: k_c_step<false, 2> (Tile's PR = 2)
   uint64_t lat_l1d, lat_l1t, lat_l2d, lat_l2t, lat_dir, gap_ps, dram_proc, dram_cost;
   NocParams np;
 };
@@ -656,8 +660,12 @@ struct TilePre {
 // true>): OWNED lines and entries, upgrade replies, combined invalidate-flush
 // requests, sharer write-backs, the directory's cached data list and the
 // protocol event counters (directory_msg_mo / l2_msg_mo below)
-template <class SL, class H, bool F = false, bool MO = false>
+// PR: the caching protocol — 0 pr_l1_pr_l2_dram_directory_msi, 1 its MOSI
+// form (MO), 2 pr_l1_sh_l2_msi (SH: the L2 a shared slice per tile whose lines
+// carry the directory entries, sh_* below)
+template <class SL, class H, bool F = false, int PR = 0>
 struct Tile {
+  static constexpr bool MO = PR == 1, SH = PR == 2;
   static constexpr bool kF = F;
   static constexpr bool kMO = MO;
   using Cache = CacheT<!F>;
@@ -705,8 +713,9 @@ struct Tile {
       L2 = Cache{t2, m2, r2, S.cc + ((size_t)lt * 2 + 1) * GG_NUM_CACHE_COUNTERS, P.s2, P.a2, P.log_line, P.pol2, 1, ln, 0,
                  ~0u, 0, 0};
     } else {
+      // the L1-D is write-through under pr_l1_pr_l2 (l1_cache_cntlr.cc:59), write-back under sh_l2 (…sh_l2_msi/l1:57)
       L1 = Cache{S.l1_tag + lt * n1, S.l1_meta + lt * n1, S.l1_rr + (size_t)lt * P.s1,
-                 S.cc + (size_t)lt * 2 * GG_NUM_CACHE_COUNTERS, P.s1, P.a1, P.log_line, P.pol1, 0, ln, 0, ~0u, 0, 0};
+                 S.cc + (size_t)lt * 2 * GG_NUM_CACHE_COUNTERS, P.s1, P.a1, P.log_line, P.pol1, SH ? 1u : 0u, ln, 0, ~0u, 0, 0};
       L2 = Cache{S.l2_tag + lt * n2, S.l2_meta + lt * n2, S.l2_rr + (size_t)lt * P.s2,
                  S.cc + ((size_t)lt * 2 + 1) * GG_NUM_CACHE_COUNTERS, P.s2, P.a2, P.log_line, P.pol2, 1, ln, 0, ~0u, 0, 0};
     }
@@ -788,6 +797,7 @@ struct Tile {
     stat(GG_CT_MSGS_SENT, n);
     if (type - 1u < 11u) stat(GG_CT_SENT_BY_TYPE + type - 1u, n);
     else if (MO && type == M_IFC_REQ) stat(GG_CT_SENT_INV_FLUSH_COMBINED, n);
+    else if (SH && type >= M_DRAM_FETCH_REQ) stat(GG_CT_SENT_DRAM_FETCH_REQ + type - M_DRAM_FETCH_REQ, n);
   }
   __device__ __forceinline__ void send(uint32_t dst, uint32_t type, uint32_t requester, uint64_t addr, uint64_t t)
   { const uint64_t c0 = tr_on ? __builtin_amdgcn_s_memtime() : 0; send_(dst, type, requester, addr, t); if (tr_on) tra[3] += __builtin_amdgcn_s_memtime() - c0; }
@@ -1405,7 +1415,7 @@ struct Tile {
         hit = wr ? cs == ST_M : cs != ST_I;
         w1 = (uint32_t)fw;
       }
-      if (hit && wr) {                                               // the write-through L2 line (l2:66-70)
+      if (!SH && hit && wr) {                                        // the write-through L2 line (l2:66-70)
         s2 = L2.set_of(a);
         const uint64_t* t2 = L2.tag + (size_t)s2 * L2.ways;
         int f2 = -1;
@@ -1439,7 +1449,7 @@ struct Tile {
     const bool inrun = (run >> ln) & 1;
     const uint64_t wmask = __ballot(wr) & run;
     const uint32_t nw = (uint32_t)__builtin_popcountll(wmask);
-    const bool lru1 = L1.pol == GG_POLICY_LRU, lru2 = L2.pol == GG_POLICY_LRU && nw;
+    const bool lru1 = L1.pol == GG_POLICY_LRU, lru2 = !SH && L2.pol == GG_POLICY_LRU && nw;
     if ((lru1 || lru2) && rows) {
       // the run's LRU touches (lru:40-50) in closed form: ages are a
       // permutation of 0..ways-1 in every set (reset to the way index; touch
@@ -1487,7 +1497,7 @@ struct Tile {
     L1.cnt_add(GG_CC_WRITE_ACCESSES, nw);
     L1.cnt_add(GG_CC_DATA_READS, nr);
     L1.cnt_add(GG_CC_DATA_WRITES, nw);
-    L2.cnt_add(GG_CC_DATA_WRITES, nw);
+    if constexpr (!SH) L2.cnt_add(GG_CC_DATA_WRITES, nw);
     if (S.out && ln >= o && ln < o + n) S.out[wbase + ln] = ((uint64_t)P.lat_l1d << 2) | GG_LVL_L1;
     stat(GG_CT_ACCESSES, n);
     stat(GG_CT_LATENCY_PS, (uint64_t)n * P.lat_l1d);
@@ -1499,6 +1509,7 @@ struct Tile {
   // Core::initiateMemoryAccess -> L1CacheCntlr::processMemOpFromCore, first attempt (l1:89-180)
   __device__ __forceinline__ void app_access(uint64_t a, bool wr, uint64_t s)
   {
+    if constexpr (SH) { sh_app_access(a, wr, s); return; }
     uint64_t t = s;
     uint32_t cs, loc;
     L1.get(a, cs, loc);
@@ -2054,6 +2065,358 @@ struct Tile {
   // loaded with the tile, and an idle tile (most of them in a step) leaves
   // its lines clean, so the launch's end writes back only the active tiles'
   // state (the agent-scope release costs by the dirty bytes)
+  // ==== pr_l1_sh_l2_msi (Tile<..., PR = 2>) ====================================
+  // The tile's L2 slice is its directory-entry array: slot set * a2 + way
+  // holds one line (addr = its address, INV_ADDR while never used; dstate =
+  // directory state | cache state << 8: DATA_INVALID, CLEAN or DIRTY; owner,
+  // sharer count and words), set = L2CacheHashFn (the directory's XOR fold
+  // over log2(sets)-bit fields, no slice bits); the replaced list is
+  // L2CacheCntlr::_evicted_cache_line_map.  The slice's Cache operations count
+  // in L2.cd.  The controller's call chains run as a work loop (sh_run), as
+  // directory_run does for the private-L2 protocols.
+  static constexpr uint32_t CS_DINV = 5, CS_CLEAN = 6, CS_DIRTY = 7;          // CacheState::Type (cache_state.h:11-22)
+  enum { SW_NONE = 0, SW_PROC, SW_CONT, SW_NULL, SW_NEXT };
+  struct SWork { uint64_t addr; uint32_t kind, type, first, data, req; int32_t h; };
+  static_assert(sizeof(SWork) <= sizeof(Work), "SWork continuations live in the directory work stack");
+  __device__ __forceinline__ uint32_t sh_cs(int32_t h) { return e_state(h) >> 8; }
+  __device__ __forceinline__ uint32_t sh_ds(int32_t h) { return e_state(h) & 0xFFu; }
+  __device__ __forceinline__ void sh_set_ds(int32_t h, uint32_t ds) { eopen(h); ost = (ost & 0xFF00u) | ds; od = true; }
+  __device__ __forceinline__ void sh_set_cs(int32_t h, uint32_t cs) { eopen(h); ost = (ost & 0xFFu) | (cs << 8); od = true; }
+  // CacheSet::find in the slice (lane = way): the line's slot or NO_ENT
+  __device__ __forceinline__ int32_t sh_slot(uint64_t a)
+  {
+    const uint32_t base = dset(a) * P.dassoc;
+    const DEnt* d = S.dir + (size_t)lt * P.E;
+    const uint64_t v = ln < P.dassoc ? d[base + ln].addr : INV_ADDR;
+    const uint64_t m = __ballot(ln < P.dassoc && v == a);
+    return m ? (int32_t)(base + (uint32_t)__builtin_ctzll(m)) : NO_ENT;
+  }
+  // _evicted_cache_line_map.find (lane = entry)
+  __device__ __forceinline__ int32_t sh_evicted(uint64_t a)
+  {
+    const uint64_t rv = ln < nrep ? rep_ent(ln)->addr : INV_ADDR;
+    const uint64_t rh = __ballot(ln < nrep && rv == a);
+    return rh ? -(int32_t)__builtin_ctzll(rh) - 1 : NO_ENT;
+  }
+  // L2CacheCntlr::setCacheLineInfo (l2_cache_cntlr.cc:102-116): a line in the
+  // slice is a tag write (its fields go back with the open entry)
+  __device__ __forceinline__ void sh_setinfo(int32_t h) { if (h >= 0) L2.cnt(GG_CC_TAG_WRITES); }
+  // allocateCacheLine (l2_cache_cntlr.cc:130-189): a DATA_INVALID line with a
+  // fresh entry; the victim (L2CacheReplacementPolicy::getReplacementWay,
+  // l2_cache_replacement_policy.cc:20-67: the first INVALID way, else the
+  // fewest sharers among lines no request waits on, first wins) moves to the
+  // evicted map.  Returns the new line's slot; ev_addr = the victim's line or INV_ADDR.
+  __device__ __forceinline__ int32_t sh_allocate(uint64_t a, uint64_t& ev_addr)
+  {
+    eclose();                                     // the moves below work on HBM
+    ev_addr = INV_ADDR;
+    const uint32_t base = dset(a) * P.dassoc;
+    DEnt* d = S.dir + (size_t)lt * P.E;
+    DEnt e{INV_ADDR, -1, 0, 0};
+    if (ln < P.dassoc) e = d[base + ln];
+    const uint64_t inv = __ballot(ln < P.dassoc && e.addr == INV_ADDR);
+    uint32_t w;
+    if (inv) {
+      w = (uint32_t)__builtin_ctzll(inv);
+    } else {
+      uint32_t key = ~0u;
+      if (ln < P.dassoc) {
+        uint32_t qc = 0;
+        for (uint32_t i = 0; i < nrq; ++i) qc += (rq_addr(i) == e.addr);
+        if (qc == 0) key = ((uint32_t)e.nsh << 8) | ln;
+      }
+      key = wave_min(key);
+      if (key == ~0u) { fail(); return NO_ENT; }  // "Could not find a replacement candidate"
+      w = key & 0xFFu;
+    }
+    const int32_t slot = (int32_t)(base + w);
+    const uint64_t va = rl64(e.addr, w);
+    L2.cnt(GG_CC_TAG_READS);
+    if (va != INV_ADDR) {
+      const uint32_t r = nrep;
+      if (r >= P.R) { fail(GG_DERR_CAP); return NO_ENT; }
+      nrep = r + 1;
+      *ent(-(int32_t)r - 1) = d[slot];
+      uint64_t* so = shw(slot); uint64_t* sr = shw(-(int32_t)r - 1);
+      if (ln < P.W) sr[ln] = so[ln];
+      const uint32_t vcs = rl32((uint32_t)e.dstate, w) >> 8;
+      if (vcs != CS_CLEAN && vcs != CS_DIRTY) fail();
+      L2.cnt(GG_CC_DATA_READS); L2.cnt(GG_CC_EVICTIONS);
+      if (vcs == CS_DIRTY) L2.cnt(GG_CC_DIRTY_EVICTIONS);
+      ev_addr = va;
+    }
+    d[slot] = DEnt{a, -1, (uint16_t)((CS_DINV << 8) | DS_UNCACHED), 0};
+    if (ln < P.W) shw(slot)[ln] = 0;
+    L2.cnt(GG_CC_TAG_WRITES); L2.cnt(GG_CC_DATA_WRITES);
+    return slot;
+  }
+  // processNextReqFromL1Cache (l2_cache_cntlr.cc:305-336) / restartShmemReq (:813-847) helpers
+  // the L2 controller's call chains: processEx/ShReqFromL1Cache (:442-697),
+  // processNullifyReq (:358-440), processNextReqFromL1Cache, with the
+  // allocation's nullify run before the request continues (a stack of continuations)
+  __device__ __forceinline__ void sh_run(SWork w, uint64_t& t)
+  {
+    SWork* stack = reinterpret_cast<SWork*>(sl.wstack);
+    int sp = 0;
+    for (;;) {
+      if (failed) return;
+      switch (w.kind) {
+      case SW_PROC: {                             // getCacheLineInfo (:65-100)
+        int32_t h = sh_evicted(w.addr);
+        if (h != NO_ENT) { if (w.first) fail(); w.kind = SW_CONT; w.h = h; continue; }
+        h = sh_slot(w.addr);
+        L2.cnt(GG_CC_TAG_READS);
+        const bool miss = h == NO_ENT;
+        if (w.first) L2.miss_counters(w.addr, w.type == M_EX_REQ, miss);
+        if (miss) {
+          uint64_t ev = INV_ADDR;
+          h = sh_allocate(w.addr, ev);
+          if (h == NO_ENT) return;
+          if (ev != INV_ADDR) {                   // a NULLIFY_REQ for the victim, queued and processed now (:162-182)
+            qpush(ev, t, M_NULLIFY_REQ, tile);
+            if (sp >= WSTACK) { fail(GG_DERR_CAP); return; }
+            SWork c = w; c.kind = SW_CONT; c.h = h;
+            stack[sp++] = c;
+            w = SWork{ev, SW_NULL, 0, 0, 1, tile, 0};
+            continue;
+          }
+        }
+        w.kind = SW_CONT; w.h = h;
+        continue;
+      }
+      case SW_CONT: {
+        const int32_t h = w.h;
+        const uint64_t a = w.addr;
+        const uint32_t rq = w.req, cs = sh_cs(h), ds = sh_ds(h);
+        bool done = false;
+        if (cs == CS_DINV) {
+          send(home(a), M_DRAM_FETCH_REQ, rq, a, t);               // fetchDataFromDram (:907-914)
+        } else if (w.type == M_EX_REQ) {
+          if (ds == DS_MODIFIED) {
+            send((uint32_t)e_owner(h), M_FLUSH_REQ, rq, a, t);
+          } else if (ds == DS_SHARED) {
+            if (has(h, rq) && e_nsh(h) == 1) {                     // upgrade: the lone sharer
+              set_owner(h, (int32_t)rq);
+              sh_set_ds(h, DS_MODIFIED);
+              send(rq, M_UPGRADE_REP, rq, a, t);
+              done = true;
+            } else {
+              send_sharers(h, M_INV_REQ, rq, a, t);
+            }
+          } else {
+            if (e_nsh(h) != 0) fail();
+            add_sharer(h, rq);
+            set_owner(h, (int32_t)rq);
+            sh_set_ds(h, DS_MODIFIED);
+            if (!w.data) L2.cnt(GG_CC_DATA_READS);                 // readCacheLine (:878-905)
+            send(rq, M_EX_REP, rq, a, t);
+            done = true;
+          }
+        } else {
+          if (ds == DS_MODIFIED) {
+            send((uint32_t)e_owner(h), M_WB_REQ, rq, a, t);
+          } else {
+            if (ds == DS_UNCACHED) { if (e_nsh(h) != 0) fail(); sh_set_ds(h, DS_SHARED); }
+            add_sharer(h, rq);                                     // full map: always added
+            if (!w.data) L2.cnt(GG_CC_DATA_READS);
+            send(rq, M_SH_REP, rq, a, t);
+            done = true;
+          }
+        }
+        if (done) { sh_setinfo(h); w.kind = SW_NEXT; continue; }
+        w.kind = SW_NONE;
+        continue;
+      }
+      case SW_NULL: {                                              // the line in the evicted map
+        const uint64_t a = w.addr;
+        const int32_t h = sh_evicted(a);
+        if (h == NO_ENT) { fail(); return; }
+        const uint32_t cs = sh_cs(h), ds = sh_ds(h);
+        if (ds == DS_MODIFIED) {
+          send((uint32_t)e_owner(h), M_FLUSH_REQ, w.req, a, t);
+          w.kind = SW_NONE;
+        } else if (ds == DS_SHARED) {
+          send_sharers(h, M_INV_REQ, w.req, a, t);
+          if (cs == CS_DIRTY && w.data) send(home(a), M_DRAM_STORE_REQ, w.req, a, t);
+          w.kind = SW_NONE;
+        } else {
+          if (cs == CS_DIRTY && w.data) send(home(a), M_DRAM_STORE_REQ, w.req, a, t);
+          dinvalidate(a);                                          // the entry deleted, the line out of the map
+          w.kind = SW_NEXT;
+        }
+        continue;
+      }
+      case SW_NEXT: {
+        t += P.gap_ps;                                     // Latency(1, L2 frequency)
+        if (qcount(w.addr) < 1) { fail(); return; }
+        qpop(w.addr);
+        const int32_t f = qfront(w.addr);
+        if (f < 0) { w.kind = SW_NONE; continue; }
+        uint32_t type, req;
+        front_update(f, t, type, req);
+        if (type != M_EX_REQ && type != M_SH_REQ) { fail(); return; }
+        w = SWork{w.addr, SW_PROC, type, 1, 0, req, 0};            // processShmemReq (:338-356)
+        continue;
+      }
+      default:
+        if (sp == 0) return;
+        w = stack[--sp];
+        continue;
+      }
+    }
+  }
+  // restartShmemReq (l2_cache_cntlr.cc:813-847): the front request of a, after a reply
+  __device__ __forceinline__ void sh_restart(uint64_t a, int32_t f, int32_t h, uint32_t data, uint64_t& t)
+  {
+    t += P.gap_ps;                                     // Latency(1, L2 frequency)
+    uint32_t type, req;
+    front_update(f, t, type, req);
+    const uint32_t ds = sh_ds(h);
+    if (type == M_EX_REQ) { if (ds == DS_UNCACHED) sh_run(SWork{a, SW_PROC, type, 0, data, req, 0}, t); }
+    else if (type == M_SH_REQ) sh_run(SWork{a, SW_PROC, type, 0, data, req, 0}, t);
+    else if (type == M_NULLIFY_REQ) { if (ds == DS_UNCACHED) sh_run(SWork{a, SW_NULL, 0, 0, data, req, 0}, t); }
+    else fail();
+  }
+  // L1CacheCntlr::insertCacheLine (l1_cache_cntlr.cc:230-274): an evicted line goes home
+  __device__ __forceinline__ void sh_l1_insert(uint64_t a, uint32_t cs, uint64_t t)
+  {
+    bool ev; uint64_t ea = 0; uint32_t es = 0, el = 0;
+    if (!L1.insert(a, cs, 0, ev, ea, es, el)) { fail(); return; }
+    if (!ev) return;
+    if (es == ST_M) send(home(ea), M_FLUSH_REP, tile, ea, t);
+    else if (es == ST_S) send(home(ea), M_INV_REP, tile, ea, t);
+    else fail();
+  }
+  // invalidateCacheLine (:276-287)
+  __device__ __forceinline__ void sh_l1_invalidate(uint64_t a)
+  {
+    uint32_t c, l;
+    L1.get(a, c, l);
+    if (!L1.set(a, ST_I, 0)) fail();
+  }
+  // processMemOpFromCore (l1_cache_cntlr.cc:80-144): no invalidate before a
+  // miss; the request (handleMsgFromCore, :289-302, at once) to the line's home slice
+  __device__ __forceinline__ void sh_app_access(uint64_t a, bool wr, uint64_t s)
+  {
+    uint64_t t = s;
+    uint32_t cs, loc;
+    L1.get(a, cs, loc);
+    const bool hit = wr ? cs == ST_M : cs != ST_I;
+    L1.miss_counters(a, wr, !hit);
+    if (hit) { t += P.lat_l1d; if (!L1.access(a, wr)) fail(); finish(s, t, GG_LVL_L1); return; }
+    t += P.lat_l1t;
+    if (out_addr != INV_ADDR) fail();
+    out_addr = a; out_time = t;
+    send(home(a), wr ? M_EX_REQ : M_SH_REQ, tile, a, t);
+    blocked = 1;
+    pend_start = s;
+  }
+  // MemoryManager::handleMsgFromNetwork (…sh_l2_msi/memory_manager.cc:215-294)
+  __device__ __forceinline__ void sh_msg(const HMsg& m)
+  {
+    uint64_t t = m.arrival_ps;
+    const uint64_t a = m.addr;
+    const uint32_t ty = m.type;
+    if (ty == M_EX_REP || ty == M_SH_REP || ty == M_UPGRADE_REP) {   // L1CacheCntlr::handleMsgFromL2Cache (l1:304-409)
+      if (!blocked || out_addr != a) { fail(); return; }
+      if (ty == M_UPGRADE_REP) {
+        uint32_t c1, l1;
+        L1.get(a, c1, l1);
+        if (c1 != ST_S) fail();
+        if (!L1.set(a, ST_M, 0)) fail();
+      } else {
+        sh_l1_insert(a, ty == M_EX_REP ? ST_M : ST_S, t);
+      }
+      if (out_time > t) fail();
+      t += P.lat_l1d;
+      out_addr = INV_ADDR;
+      const bool wr = (S.meta[rec] & GG_META_WRITE) != 0;             // access_num == 2 (l1:97-119)
+      uint32_t c1, l1;
+      L1.get(a, c1, l1);
+      if (!(wr ? c1 == ST_M : c1 != ST_I)) { fail(); return; }
+      t += P.lat_l1d;
+      if (!L1.access(a, wr)) fail();
+      blocked = 0;
+      finish(pend_start, t, GG_LVL_DIR);
+    } else if (ty == M_INV_REQ) {                                     // processInvReqFromL2Cache (l1:411-448)
+      uint32_t c1, l1;
+      L1.get(a, c1, l1);
+      t += P.lat_l1t;
+      if (c1 != ST_I) {
+        if (c1 != ST_S) fail();
+        sh_l1_invalidate(a);
+        send(m.src, M_INV_REP, m.requester, a, t);
+      }
+    } else if (ty == M_FLUSH_REQ || ty == M_WB_REQ) {                 // l1:450-536
+      uint32_t c1, l1;
+      L1.get(a, c1, l1);
+      if (c1 != ST_I) {
+        if (c1 != ST_M) fail();
+        t += P.lat_l1d;
+        if (!L1.access(a, false)) fail();                               // readCacheLine
+        if (ty == M_FLUSH_REQ) { sh_l1_invalidate(a); send(m.src, M_FLUSH_REP, m.requester, a, t); }
+        else { if (!L1.set(a, ST_S, 0)) fail(); send(m.src, M_WB_REP, m.requester, a, t); }
+      } else {
+        t += P.lat_l1t;
+      }
+    } else if (ty == M_EX_REQ || ty == M_SH_REQ) {                    // L2CacheCntlr::handleMsgFromL1Cache (l2:191-220)
+      t += P.lat_l2d;
+      qpush(a, t, ty, m.requester);
+      if (qcount(a) == 1) sh_run(SWork{a, SW_PROC, ty, 1, 0, m.requester, 0}, t);
+    } else if (ty == M_INV_REP || ty == M_FLUSH_REP || ty == M_WB_REP) {   // l2:222-270
+      t += P.lat_l2d;
+      int32_t h = sh_evicted(a);
+      if (h == NO_ENT) { h = sh_slot(a); L2.cnt(GG_CC_TAG_READS); }
+      if (h == NO_ENT) { fail(); return; }
+      const uint32_t ds = sh_ds(h);
+      if (ty == M_INV_REP) {                                          // processInvRepFromL1Cache (:699-729)
+        if (ds == DS_SHARED) {
+          remove_sharer(h, m.src);
+          if (e_nsh(h) == 0) sh_set_ds(h, DS_UNCACHED);
+        }
+      } else if (ty == M_FLUSH_REP) {                                 // processFlushRepFromL1Cache (:731-773)
+        if (ds == DS_MODIFIED) {
+          const int32_t f = qfront(a);
+          if (f < 0 || rq_get(f).type == M_SH_REQ) { if (h < 0) fail(); L2.cnt(GG_CC_DATA_WRITES); }   // writeCacheLine
+          sh_set_cs(h, CS_DIRTY);
+          remove_sharer(h, m.src);
+          set_owner(h, -1);
+          sh_set_ds(h, DS_UNCACHED);
+        }
+      } else {                                                        // processWbRepFromL1Cache (:775-811)
+        if (ds == DS_MODIFIED) {
+          if (h < 0) fail();
+          L2.cnt(GG_CC_DATA_WRITES);
+          sh_set_cs(h, CS_DIRTY);
+          set_owner(h, -1);
+          sh_set_ds(h, DS_SHARED);
+        }
+      }
+      sh_setinfo(h);
+      const int32_t f = qfront(a);
+      if (f >= 0) sh_restart(a, f, h, ty != M_INV_REP, t);
+    } else if (ty == M_DRAM_FETCH_REP) {                              // L2CacheCntlr::handleMsgFromDram (l2:278-303)
+      t += P.lat_l2d;
+      const int32_t h = sh_slot(a);
+      L2.cnt(GG_CC_TAG_READS);
+      const int32_t f = qfront(a);
+      if (h == NO_ENT || f < 0) { fail(); return; }
+      const uint32_t ft = rq_get(f).type;
+      if (ft == M_SH_REQ) L2.cnt(GG_CC_DATA_WRITES);                 // writeCacheLine
+      else if (ft != M_EX_REQ) fail();
+      sh_set_cs(h, CS_CLEAN);
+      sh_setinfo(h);
+      sh_restart(a, f, h, 1, t);
+    } else if (ty == M_DRAM_FETCH_REQ) {                              // DramCntlr::handleMsgFromL2Cache (…sh_l2_msi/dram_cntlr.cc:19-52)
+      t += dram_ps(t);
+      send(m.src, M_DRAM_FETCH_REP, m.requester, a, t);
+    } else if (ty == M_DRAM_STORE_REQ) {
+      (void)dram_ps(t);
+    } else {
+      fail();
+    }
+  }
+
   __device__ __forceinline__ void flush()
   {
     {
@@ -2280,14 +2643,14 @@ __device__ __forceinline__ void quantum_end(const CP& P, const CS& S, uint32_t L
 struct TraceWin { uint64_t wbase, wa; uint32_t wm; };
 constexpr uint64_t kNsFin = ~0ull, kNsBlk = ~0ull - 1;   // next start of a finished / blocked tile
 
-template <bool LC, bool HR, bool F, bool MO, class SL, class H>
+template <bool LC, bool HR, bool F, int PR, class SL, class H>
 __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t lt, uint32_t k, uint32_t L, uint64_t barrier,
                                           TraceWin& W, SL& sl, uint8_t* clds, const TilePre& pre, const H& hk,
                                           uint32_t na, uint32_t ni, uint64_t rel);
 
 // LC: cache state in LDS; HR: L1 hit runs (persistent small meshes, where
 // long runs of hits between misses pay for the window look-up)
-template <bool LC, bool HR, bool F = false, bool MO = false>
+template <bool LC, bool HR, bool F = false, int PR = 0>
 __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, uint32_t devloop, uint64_t barrier_arg,
                                           TraceWin& W)
 {
@@ -2330,7 +2693,7 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
   const GHooks hk{P, S};
   const uint32_t na = P.net == GG_NET_EMESH_HOP_BY_HOP ? (p ? pre.narv1 : pre.narv0) : 0u;
   const uint32_t ni = p ? pre.ninb1 : pre.ninb0;
-  tile_step<LC, HR, F, MO>(P, S, lt, k, L, barrier, W, sl, smem + P.cache_lds_off, pre, hk, na, ni,
+  tile_step<LC, HR, F, PR>(P, S, lt, k, L, barrier, W, sl, smem + P.cache_lds_off, pre, hk, na, ni,
                     devloop && k == 0 ? qsv[QS_REL] : 0ull);
 }
 
@@ -2465,14 +2828,15 @@ __device__ __forceinline__ void publish_hbh_lds(TT& T, gg_cmsg* cur, uint32_t nl
 // the calling wave: the SELF port + receive of the packets that
 // reached the tile (na), the inbox (ni records), the trace, publish, write
 // back.  Deliveries go through the hooks.
-template <bool LC, bool HR, bool F, bool MO, class SL, class H>
+template <bool LC, bool HR, bool F, int PR, class SL, class H>
 __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t lt, uint32_t k, uint32_t L, uint64_t barrier,
                                           TraceWin& W, SL& sl, uint8_t* clds, const TilePre& pre, const H& hk,
                                           uint32_t na, uint32_t ni, uint64_t rel)
 {
   const uint32_t ln = lane_id(), p = k & 1u;
   PROF_T0();
-  Tile<SL, H, F, MO> T(P, S, lt, p, sl, hk, clds, std::integral_constant<bool, LC>(), pre);
+  constexpr bool MO = PR == 1, SH = PR == 2;
+  Tile<SL, H, F, PR> T(P, S, lt, p, sl, hk, clds, std::integral_constant<bool, LC>(), pre);
   T.tr_on = DG(S.trs) != nullptr && L < S.tr_n;
   const gg_cmsg* prev = pool(S, p ^ 1u);     // records delivered to this step
   uint64_t* gscr = S.gscr + (size_t)lt * 6 * P.IC;
@@ -2724,7 +3088,8 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
       T.stat(GG_CT_MSGS_RECEIVED, 1);
       const uint64_t h0 = DG(S.trs) ? __builtin_amdgcn_s_memtime() : 0;
       const bool dm = to_directory(m.type);
-      if constexpr (MO) { if (dm) T.directory_msg_mo(m); else T.l2_msg_mo(m); }
+      if constexpr (SH) T.sh_msg(m);
+      else if constexpr (MO) { if (dm) T.directory_msg_mo(m); else T.l2_msg_mo(m); }
       else { if (dm) T.directory_msg(m); else T.l2_msg(m); }
       if (DG(S.trs)) {
         const uint64_t h1 = __builtin_amdgcn_s_memtime();
@@ -3648,6 +4013,8 @@ void launch_step_fast(const CP& P, const StepArgs& a, size_t lds, hipStream_t s,
 hipError_t step_fast_set_lds(size_t lds);
 void launch_step_mosi(const CP& P, const StepArgs& a, size_t lds, hipStream_t s, uint32_t L, uint32_t devloop, uint64_t barrier);
 hipError_t step_mosi_set_lds(size_t lds);
+void launch_step_shl2(const CP& P, const StepArgs& a, size_t lds, hipStream_t s, uint32_t L, uint32_t devloop, uint64_t barrier);
+hipError_t step_shl2_set_lds(size_t lds);
 void launch_persist(bool lc, const CP& P, const StepArgs& a, size_t lds, hipStream_t s, uint32_t L0, uint32_t L1);
 hipError_t step_set_lds(size_t step_lds, size_t persist_lc_lds, size_t persist_lds);
 hipError_t persist_occupancy(bool lc, size_t lds, int* per_cu);

@@ -435,8 +435,19 @@ static gg_status coh_alloc(gg_ctx* ctx)
   P.bits_req = 2 * idb + 4 + 48;
   P.bits_data = P.bits_req + 8 * c.line_size;
   P.bits_ifc = P.bits_req + idb;                 // …mosi/shmem_msg.cc:137-139: + the single receiver
-  if (c.protocol > GG_PROTO_MOSI) return gg_fail(GG_ERR_INVALID, "protocol must be GG_PROTO_MSI or GG_PROTO_MOSI");
+  if (c.protocol > GG_PROTO_SHL2_MSI)
+    return gg_fail(GG_ERR_INVALID, "protocol must be GG_PROTO_MSI, GG_PROTO_MOSI or GG_PROTO_SHL2_MSI");
   P.mosi = c.protocol == GG_PROTO_MOSI ? 1u : 0u;
+  P.shl2 = c.protocol == GG_PROTO_SHL2_MSI ? 1u : 0u;
+  if (P.shl2) {
+    // pr_l1_sh_l2_msi: the directory entries are the L2 slice's lines
+    // (ShL2CacheLineInfo); set = L2CacheHashFn (l2_cache_hash_fn.cc:18-34),
+    // the directory's XOR fold with log2(L2 sets) bits and no slice bits
+    if (P.s2 < 2 || (P.s2 & (P.s2 - 1))) return gg_fail(GG_ERR_UNSUPPORTED, "pr_l1_sh_l2_msi: L2 sets must be a power of two >= 2");
+    if (P.a2 > 64) return gg_fail(GG_ERR_UNSUPPORTED, "pr_l1_sh_l2_msi: at most 64 L2 ways");
+    if (c.l2_track_miss_types) return gg_fail(GG_ERR_UNSUPPORTED, "pr_l1_sh_l2_msi: L2 miss types are not tracked");
+    P.E = P.s2 * P.a2; P.dassoc = P.a2; P.log_dsets = (uint32_t)ilog2(P.s2); P.log_slices = 0;
+  }
   P.dram_qm = c.dram_queue_model_enabled;
   P.dram_qtype = c.dram_queue_model_type;
   P.dram_qaux = hq_aux(c.dram_queue_model_type, c.basic_moving_avg, c.history_list_no_interleaving);
@@ -541,7 +552,7 @@ static gg_status coh_alloc(gg_ctx* ctx)
   A(cc, L * 2 * GG_NUM_CACHE_COUNTERS); A(st, L * GG_NUM_TILE_STATS);
   // miss-type tracking (default off): one address table per (tile, cache)
   // (MSI's L1CacheCntlr hands the L1-D the L1-I flag, l1_cache_cntlr.cc:69; MOSI its own, …mosi/l1:68)
-  P.mt1 = (P.mosi ? ctx->cfg.l1d_track_miss_types : ctx->cfg.l1i_track_miss_types) ? 1u : 0u;
+  P.mt1 = ((P.mosi || P.shl2) ? ctx->cfg.l1d_track_miss_types : ctx->cfg.l1i_track_miss_types) ? 1u : 0u;   // (sh_l2: its own flag, …sh_l2_msi/l1:67)
   P.mt2 = ctx->cfg.l2_track_miss_types ? 1u : 0u;
   {
     // the fast step instance: every queue it serves a history tree held in
@@ -550,7 +561,7 @@ static gg_status coh_alloc(gg_ctx* ctx)
     const bool rq_net = !P.np.qm || (P.np.qtype == GG_QM_HISTORY_TREE && P.np.max_size <= kQMax);
     const bool rq_dram = !P.dram_qm || (P.dram_qtype == GG_QM_HISTORY_TREE && P.max_list <= kQMax);
     const char* nf = getenv("GG_COH_NO_FAST");
-    P.fast = rq_net && rq_dram && !P.mt1 && !P.mt2 && !P.mosi && !(nf && atoi(nf)) ? 1u : 0u;
+    P.fast = rq_net && rq_dram && !P.mt1 && !P.mt2 && !P.mosi && !P.shl2 && !(nf && atoi(nf)) ? 1u : 0u;
   }
   if (P.mt1 || P.mt2) {
     const uint32_t lines = ctx->cfg.miss_track_lines ? ctx->cfg.miss_track_lines : 65536u;
@@ -914,7 +925,7 @@ gg_status gg_coherent_run(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_out_
   const char* np_env = getenv("GG_COH_NO_PERSIST");
   const char* nl_env = getenv("GG_COH_NO_LDS_CACHE");
   const bool plc = C->persist_lc && !(nl_env && atoi(nl_env));
-  bool persist = P.L <= kPersistTiles && !P.mosi && !(np_env && atoi(np_env));   // (no persistent MOSI instance)
+  bool persist = P.L <= kPersistTiles && !P.mosi && !P.shl2 && !(np_env && atoi(np_env));   // (no persistent MOSI / sh_l2 instance)
   if (persist) {
     // the grid barrier needs every workgroup resident at once (a partitioned
     // device has fewer CUs): else the per-step launches

@@ -427,7 +427,7 @@ inline void writeMosiDirectoryCntlrSummary(std::ostream& out, const uint64_t* ps
 
 // The memory part of one tile's sim.out block in the coherent mode
 // (msi/memory_manager.cc:415-430): Cache Summary (L1-D, L2; no L1-I is
-// modeled), then the DRAM and directory summaries.  MOSI
+// modeled), then the DRAM and directory summaries (sh_l2: no directory block).  MOSI
 // (…mosi/memory_manager.cc:412-436, proto = the tile's GG_PS_* counters): the
 // L2 and directory controllers' blocks after the caches, the directory cache
 // before the DRAM.
@@ -435,10 +435,11 @@ inline void writeMemorySummary(std::ostream& out, const gg_config& c, const uint
                                const uint64_t* cache_counters, const uint64_t* miss_types = nullptr,
                                const uint64_t* proto = nullptr)
 {
-  const bool mosi = c.protocol == GG_PROTO_MOSI;
-  const bool l1_mt = mosi ? c.l1d_track_miss_types : c.l1i_track_miss_types;
+  const bool mosi = c.protocol == GG_PROTO_MOSI, shl2 = c.protocol == GG_PROTO_SHL2_MSI;
+  const bool l1_mt = (mosi || shl2) ? c.l1d_track_miss_types : c.l1i_track_miss_types;
   out << "Cache Summary:\n";
-  writeCacheSummary(out, "L1-D", cache_counters, false, false, miss_types && l1_mt ? miss_types : nullptr);
+  // (the L1-D is write-back under pr_l1_sh_l2_msi, …sh_l2_msi/l1_cache_cntlr.cc:57)
+  writeCacheSummary(out, "L1-D", cache_counters, shl2, false, miss_types && l1_mt ? miss_types : nullptr);
   writeCacheSummary(out, "L2", cache_counters + GG_NUM_CACHE_COUNTERS, true, false,
                     miss_types && c.l2_track_miss_types ? miss_types + GG_NUM_MISS_TYPES : nullptr);
   if (mosi) {
@@ -450,7 +451,9 @@ inline void writeMemorySummary(std::ostream& out, const gg_config& c, const uint
     return;
   }
   writeDramSummary(out, tile_stats, c.dram_queue_model_enabled != 0, c.dram_queue_model_type);
-  writeDirectorySummary(out, tile_stats, directorySizing(c));
+  // pr_l1_sh_l2_msi (…sh_l2_msi/memory_manager.cc:411-429): the L2 slice is the
+  // directory, so no directory-cache block
+  if (!shl2) writeDirectorySummary(out, tile_stats, directorySizing(c));
 }
 
 // One tile's summary text in the coherent mode: the core part when the core

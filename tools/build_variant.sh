@@ -7,7 +7,7 @@ set -e
 cd "$(dirname "$0")/../graphite_amd/csrc"
 name=$1; shift
 mkdir -p ../../variants/$name
-units="gg_coherent gg_coh_step gg_coh_step_fast gg_coh_step_mosi gg_coh_persist gg_coh_persist_lc gg_coh_walk"
+units="gg_coherent gg_coh_step gg_coh_step_fast gg_coh_step_mosi gg_coh_step_shl2 gg_coh_persist gg_coh_persist_lc gg_coh_walk"
 for u in $units; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -w -I../../include "$@" \
     -c $u.hip -o ../../variants/$name/$u.o &
