@@ -28,8 +28,9 @@ L2 = 1
 CSTATE_INVALID = 0
 CSTATE_SHARED = 1
 CSTATE_OWNED = 2      # MOSI
+CSTATE_EXCLUSIVE = 3  # MESI
 CSTATE_MODIFIED = 4
-PROTO_MSI, PROTO_MOSI, PROTO_SHL2_MSI = 0, 1, 2   # GG_PROTO_* (caching_protocol/type)
+PROTO_MSI, PROTO_MOSI, PROTO_SHL2_MSI, PROTO_SHL2_MESI = 0, 1, 2, 3   # GG_PROTO_* (caching_protocol/type)
 MOSI_RNG_SEED = 1                     # GG_MOSI_RNG_SEED
 LOC_INVALID = 0
 LOC_L1D = 3
@@ -65,6 +66,7 @@ MSG_TYPES = ["EX_REQ", "SH_REQ", "INV_REQ", "FLUSH_REQ", "WB_REQ", "EX_REP", "SH
 MSG = {n: i + 1 for i, n in enumerate(MSG_TYPES)}
 MSG["NULLIFY_REQ"], MSG["INV_FLUSH_COMBINED_REQ"] = 12, 13
 MSG["DRAM_FETCH_REQ"], MSG["DRAM_STORE_REQ"], MSG["DRAM_FETCH_REP"] = 14, 15, 16   # pr_l1_sh_l2_msi
+MSG["DOWNGRADE_REQ"], MSG["SH_REP_EX"], MSG["DOWNGRADE_REP"] = 17, 18, 19            # pr_l1_sh_l2_mesi
 CT_SENT_INV_FLUSH_COMBINED = 29       # GG_CT_SENT_INV_FLUSH_COMBINED (MOSI)
 CT_SENT_DRAM_FETCH_REQ, CT_SENT_DRAM_STORE_REQ, CT_SENT_DRAM_FETCH_REP = 29, 30, 31   # pr_l1_sh_l2_msi
 # MOSI event counters, [tile][NUM_PROTO_STATS] (GG_PS_*)

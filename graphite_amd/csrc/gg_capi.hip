@@ -207,7 +207,7 @@ gg_ctx* gg_create(const gg_config* cfg, gg_status* status)
   gg_status st = gg_cache_state_alloc(ctx);
   if (st == GG_OK) st = gg_noc_alloc(ctx);
   if (st == GG_OK) {
-    he = hipMalloc((void**)&ctx->err_dev, sizeof(uint32_t));
+    he = hipMalloc((void**)&ctx->err_dev, 2 * sizeof(uint32_t));   // flags, first failing source line (coherent)
     if (he != hipSuccess) st = gg_hip_check(he, "hipMalloc(err)");
   }
   if (st == GG_OK) st = gg_reset(ctx);
@@ -238,7 +238,7 @@ gg_status gg_reset(gg_ctx* ctx)
   hipStream_t s = ctx->last_stream;
   if (gg_status st = gg_cache_state_reset(ctx, s)) return st;
   if (gg_status st = gg_noc_reset(ctx, s)) return st;
-  GG_HIP(hipMemsetAsync(ctx->err_dev, 0, sizeof(uint32_t), s));
+  GG_HIP(hipMemsetAsync(ctx->err_dev, 0, 2 * sizeof(uint32_t), s));
   GG_HIP(hipStreamSynchronize(s));
   return GG_OK;
 }
@@ -345,7 +345,7 @@ gg_status gg_queue_delay_batch(gg_ctx* ctx, uint64_t min_processing_time, const 
   // representation of gg_dev.h relies on it
   if (min_processing_time == 0) return gg_fail(GG_ERR_UNSUPPORTED, "min_processing_time 0");
   hipSetDevice(ctx->device);
-  GG_HIP(hipMemset(ctx->err_dev, 0, sizeof(uint32_t)));
+  GG_HIP(hipMemset(ctx->err_dev, 0, 2 * sizeof(uint32_t)));
   if (gg_status st = gg_htree_run(ctx, min_processing_time, pkt_time, proc_time, n, delay_out)) return st;
   uint32_t e = 0;
   GG_HIP(hipMemcpy(&e, ctx->err_dev, sizeof(e), hipMemcpyDeviceToHost));

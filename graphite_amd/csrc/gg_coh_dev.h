@@ -79,7 +79,10 @@ enum { DS_UNCACHED = 0, DS_SHARED = 1, DS_MODIFIED = 2, DS_OWNED = 3 /* MOSI */ 
 enum { ST_I = 0, ST_S = 1, ST_M = 2, ST_O = 3 /* MOSI */ };   // meta byte bits 0-1
 enum { M_UPGRADE_REP = GG_MSG_UPGRADE_REP, M_IFC_REQ = GG_MSG_INV_FLUSH_COMBINED_REQ };
 enum { M_DRAM_FETCH_REQ = GG_MSG_DRAM_FETCH_REQ, M_DRAM_STORE_REQ = GG_MSG_DRAM_STORE_REQ,   // pr_l1_sh_l2_msi
-       M_DRAM_FETCH_REP = GG_MSG_DRAM_FETCH_REP };
+       M_DRAM_FETCH_REP = GG_MSG_DRAM_FETCH_REP,
+       M_DOWNGRADE_REQ = GG_MSG_DOWNGRADE_REQ, M_SH_REP_EX = GG_MSG_SH_REP_EX,                  // pr_l1_sh_l2_mesi
+       M_DOWNGRADE_REP = GG_MSG_DOWNGRADE_REP };
+constexpr uint32_t ST_E = ST_O;           // MESI's EXCLUSIVE L1 lines take the MOSI OWNED code (protocols never mix)
 enum { P_SELF = 0, P_LEFT, P_RIGHT, P_DOWN, P_UP, P_INJ };   // network_model_emesh_hop_by_hop.h:41-48 (+ injection)
 #define INV_ADDR (~0ull)
 #define NO_ENT (-0x7fffffff)
@@ -91,7 +94,8 @@ __device__ __forceinline__ bool to_directory(uint32_t t)
 __device__ __forceinline__ bool has_data(uint32_t t)
 {
   return t == M_EX_REP || t == M_SH_REP || t == M_FLUSH_REP || t == M_WB_REP ||
-         t == M_DRAM_STORE_REQ || t == M_DRAM_FETCH_REP;            // …sh_l2_msi/shmem_msg.cc:128-140
+         t == M_DRAM_STORE_REQ || t == M_DRAM_FETCH_REP ||          // …sh_l2_msi/shmem_msg.cc:128-140
+         t == M_SH_REP_EX;                                          // (MESI's DOWNGRADE_REP carries no data buffer)
 }
 // modeled length class of a message (ShmemMsg::getModeledLength, shmem_msg.cc:100-125,
 // …mosi/shmem_msg.cc:122-151): 0 request, 1 with a cache line, 2 MOSI
@@ -164,7 +168,8 @@ struct CP {
   uint32_t mt1, mt2, mt_log;               // miss-type tracking of the L1-D / L2 (cfg flags), log2 set capacity
   uint32_t fast;                           // k_c_step<true> (Tile's F): register queues only, no miss types
   uint32_t mosi;                           // pr_l1_pr_l2_dram_directory_mosi: k_c_step<false, 1> (Tile's PR = 1)
-  uint32_t shl2;                           // pr_l1_sh_l2_msi: k_c_step<false, 2> (Tile's PR = 2)
+  uint32_t shl2;                           // pr_l1_sh_l2_msi / _mesi: k_c_step<false, 2 / 3> (Tile's PR = 2 / 3)
+  uint32_t mesi;                           // pr_l1_sh_l2_mesi
   uint64_t lat_l1d, lat_l1t, lat_l2d, lat_l2t, lat_dir, gap_ps, dram_proc, dram_cost;
   NocParams np;
 };
@@ -346,6 +351,7 @@ struct CacheT {
   // invalidated / fetched address sets as one open-addressing table owned by
   // the tile (line address | bits), probed 64 slots per wave load
   uint64_t* mtab = nullptr; unsigned long long* mtc = nullptr; uint32_t mt_log = 0;
+  uint32_t e3 = 0;                     // state code 3 is MESI's EXCLUSIVE (clean), not MOSI's OWNED
   static constexpr uint64_t kMtEmpty = ~0ull;
   static constexpr uint32_t kMtE = 1, kMtI = 2, kMtF = 4;
   __device__ __forceinline__ uint64_t mt_slot(uint64_t a, uint32_t& bits, uint32_t& err)
@@ -534,7 +540,7 @@ struct CacheT {
     if (ev) {
       cnt(GG_CC_DATA_READS);
       cnt(GG_CC_EVICTIONS);
-      if (wb && (ev_st == ST_M || ev_st == ST_O)) cnt(GG_CC_DIRTY_EVICTIONS);   // CacheState::dirty(): M / O
+      if (wb && (ev_st == ST_M || (ev_st == ST_O && !e3))) cnt(GG_CC_DIRTY_EVICTIONS);   // CacheState::dirty(): M / O
     }
     cnt(GG_CC_TAG_WRITES); cnt(GG_CC_DATA_WRITES);
     return true;
@@ -662,10 +668,11 @@ struct TilePre {
 // protocol event counters (directory_msg_mo / l2_msg_mo below)
 // PR: the caching protocol — 0 pr_l1_pr_l2_dram_directory_msi, 1 its MOSI
 // form (MO), 2 pr_l1_sh_l2_msi (SH: the L2 a shared slice per tile whose lines
-// carry the directory entries, sh_* below)
+// carry the directory entries, sh_* below), 3 pr_l1_sh_l2_mesi (SH and ME:
+// EXCLUSIVE L1 lines)
 template <class SL, class H, bool F = false, int PR = 0>
 struct Tile {
-  static constexpr bool MO = PR == 1, SH = PR == 2;
+  static constexpr bool MO = PR == 1, SH = PR >= 2, ME = PR == 3;
   static constexpr bool kF = F;
   static constexpr bool kMO = MO;
   using Cache = CacheT<!F>;
@@ -682,6 +689,7 @@ struct Tile {
   uint32_t nch, cbase, cused, ccap, nsent;
   bool failed;
   uint32_t ferr;                         // GG_DERR_* gathered by fail()
+  uint32_t fline = 0;                    // the source line of the first fail()
   uint64_t ccv, stv;                    // lane k's cache counter k (of 2 x 12) and statistic k, loaded at step start
   const TilePre& p0;                    // the state loaded at step start (flush stores only what changed)
   int32_t oh = NO_ENT; bool od = false;  // the open directory entry (eopen) and whether it changed
@@ -719,6 +727,7 @@ struct Tile {
       L2 = Cache{S.l2_tag + lt * n2, S.l2_meta + lt * n2, S.l2_rr + (size_t)lt * P.s2,
                  S.cc + ((size_t)lt * 2 + 1) * GG_NUM_CACHE_COUNTERS, P.s2, P.a2, P.log_line, P.pol2, 1, ln, 0, ~0u, 0, 0};
     }
+    if constexpr (ME) L1.e3 = 1;
     if (!F && P.mt1) {
       L1.mtab = S.mtab + ((size_t)lt * 2 << P.mt_log); L1.mtc = S.mtc + (size_t)lt * 2 * GG_NUM_MISS_TYPES;
       L1.mt_log = P.mt_log;
@@ -744,15 +753,17 @@ struct Tile {
   __device__ __forceinline__ void pstat(uint32_t k, uint64_t v = 1) { if (ln == k) pd += v; }   // MOSI event counters
   // error flags are gathered in a register and reported once per step
   // (flush_err): one atomic site instead of one per inlined check
-  __device__ __forceinline__ void fail(uint32_t e = GG_DERR_STATE)
+  // (line: the call site's line in this file, reported with the first failure)
+  __device__ __forceinline__ void fail(uint32_t e = GG_DERR_STATE, uint32_t line = __builtin_LINE())
   {
+    if (!failed) fline = line;
     failed = true;
     ferr |= e;
   }
   __device__ __forceinline__ void flush_err()
   {
     ferr |= L1.mt_err | L2.mt_err;
-    if (ferr && ln == 0) atomicOr(S.err, ferr);
+    if (ferr && ln == 0) { atomicOr(S.err, ferr); if (fline) atomicCAS(S.err + 1, 0u, fline); }
   }
 
   // ---- records (MemoryManager::sendMsg, …msi/memory_manager.cc:306-332) ------
@@ -797,7 +808,7 @@ struct Tile {
     stat(GG_CT_MSGS_SENT, n);
     if (type - 1u < 11u) stat(GG_CT_SENT_BY_TYPE + type - 1u, n);
     else if (MO && type == M_IFC_REQ) stat(GG_CT_SENT_INV_FLUSH_COMBINED, n);
-    else if (SH && type >= M_DRAM_FETCH_REQ) stat(GG_CT_SENT_DRAM_FETCH_REQ + type - M_DRAM_FETCH_REQ, n);
+    else if (SH && type >= M_DRAM_FETCH_REQ && type <= M_DRAM_FETCH_REP) stat(GG_CT_SENT_DRAM_FETCH_REQ + type - M_DRAM_FETCH_REQ, n);
   }
   __device__ __forceinline__ void send(uint32_t dst, uint32_t type, uint32_t requester, uint64_t addr, uint64_t t)
   { const uint64_t c0 = tr_on ? __builtin_amdgcn_s_memtime() : 0; send_(dst, type, requester, addr, t); if (tr_on) tra[3] += __builtin_amdgcn_s_memtime() - c0; }
@@ -2192,8 +2203,8 @@ struct Tile {
         if (cs == CS_DINV) {
           send(home(a), M_DRAM_FETCH_REQ, rq, a, t);               // fetchDataFromDram (:907-914)
         } else if (w.type == M_EX_REQ) {
-          if (ds == DS_MODIFIED) {
-            send((uint32_t)e_owner(h), M_FLUSH_REQ, rq, a, t);
+          if (ds == DS_MODIFIED) {                                 // (MESI: EXCLUSIVE, the owner invalidated)
+            send((uint32_t)e_owner(h), ME ? M_INV_REQ : M_FLUSH_REQ, rq, a, t);
           } else if (ds == DS_SHARED) {
             if (has(h, rq) && e_nsh(h) == 1) {                     // upgrade: the lone sharer
               set_owner(h, (int32_t)rq);
@@ -2213,13 +2224,25 @@ struct Tile {
             done = true;
           }
         } else {
-          if (ds == DS_MODIFIED) {
-            send((uint32_t)e_owner(h), M_WB_REQ, rq, a, t);
+          if (ds == DS_MODIFIED) {                                 // (MESI: DOWNGRADE_REQ to the exclusive owner)
+            send((uint32_t)e_owner(h), ME ? M_DOWNGRADE_REQ : M_WB_REQ, rq, a, t);
           } else {
-            if (ds == DS_UNCACHED) { if (e_nsh(h) != 0) fail(); sh_set_ds(h, DS_SHARED); }
-            add_sharer(h, rq);                                     // full map: always added
+            uint32_t rep_type = M_SH_REP;
+            if (ds == DS_UNCACHED) {
+              if (e_nsh(h) != 0) fail();
+              add_sharer(h, rq);
+              if constexpr (ME) {                                  // …sh_l2_mesi/l2:671-687: an L1-D reader owns it EXCLUSIVE
+                sh_set_ds(h, DS_MODIFIED);
+                set_owner(h, (int32_t)rq);
+                rep_type = M_SH_REP_EX;
+              } else {
+                sh_set_ds(h, DS_SHARED);
+              }
+            } else {
+              add_sharer(h, rq);                                   // full map: always added
+            }
             if (!w.data) L2.cnt(GG_CC_DATA_READS);
-            send(rq, M_SH_REP, rq, a, t);
+            send(rq, rep_type, rq, a, t);
             done = true;
           }
         }
@@ -2233,7 +2256,7 @@ struct Tile {
         if (h == NO_ENT) { fail(); return; }
         const uint32_t cs = sh_cs(h), ds = sh_ds(h);
         if (ds == DS_MODIFIED) {
-          send((uint32_t)e_owner(h), M_FLUSH_REQ, w.req, a, t);
+          send((uint32_t)e_owner(h), ME ? M_INV_REQ : M_FLUSH_REQ, w.req, a, t);
           w.kind = SW_NONE;
         } else if (ds == DS_SHARED) {
           send_sharers(h, M_INV_REQ, w.req, a, t);
@@ -2284,8 +2307,18 @@ struct Tile {
     if (!L1.insert(a, cs, 0, ev, ea, es, el)) { fail(); return; }
     if (!ev) return;
     if (es == ST_M) send(home(ea), M_FLUSH_REP, tile, ea, t);
-    else if (es == ST_S) send(home(ea), M_INV_REP, tile, ea, t);
+    else if (es == ST_S || (ME && es == ST_E)) send(home(ea), M_INV_REP, tile, ea, t);
     else fail();
+  }
+  // MESI: a hit rewrites the line's info, MODIFIED on a write
+  // (operationPermissibleinL1Cache, …sh_l2_mesi/l1_cache_cntlr.cc:168-211)
+  __device__ __forceinline__ void sh_mesi_hit(uint64_t a, bool wr, uint32_t cs)
+  {
+    if (!L1.set(a, wr ? (uint32_t)ST_M : cs, 0)) fail();
+  }
+  __device__ __forceinline__ bool sh_l1_ok(uint32_t cs, bool wr) const
+  {
+    return wr ? (cs == ST_M || (ME && cs == ST_E)) : cs != ST_I;
   }
   // invalidateCacheLine (:276-287)
   __device__ __forceinline__ void sh_l1_invalidate(uint64_t a)
@@ -2301,7 +2334,8 @@ struct Tile {
     uint64_t t = s;
     uint32_t cs, loc;
     L1.get(a, cs, loc);
-    const bool hit = wr ? cs == ST_M : cs != ST_I;
+    const bool hit = sh_l1_ok(cs, wr);
+    if (ME && hit) sh_mesi_hit(a, wr, cs);
     L1.miss_counters(a, wr, !hit);
     if (hit) { t += P.lat_l1d; if (!L1.access(a, wr)) fail(); finish(s, t, GG_LVL_L1); return; }
     t += P.lat_l1t;
@@ -2317,7 +2351,7 @@ struct Tile {
     uint64_t t = m.arrival_ps;
     const uint64_t a = m.addr;
     const uint32_t ty = m.type;
-    if (ty == M_EX_REP || ty == M_SH_REP || ty == M_UPGRADE_REP) {   // L1CacheCntlr::handleMsgFromL2Cache (l1:304-409)
+    if (ty == M_EX_REP || ty == M_SH_REP || ty == M_UPGRADE_REP || (ME && ty == M_SH_REP_EX)) {   // handleMsgFromL2Cache (l1:304-409)
       if (!blocked || out_addr != a) { fail(); return; }
       if (ty == M_UPGRADE_REP) {
         uint32_t c1, l1;
@@ -2325,7 +2359,7 @@ struct Tile {
         if (c1 != ST_S) fail();
         if (!L1.set(a, ST_M, 0)) fail();
       } else {
-        sh_l1_insert(a, ty == M_EX_REP ? ST_M : ST_S, t);
+        sh_l1_insert(a, ty == M_EX_REP ? (uint32_t)ST_M : ty == M_SH_REP_EX ? ST_E : (uint32_t)ST_S, t);
       }
       if (out_time > t) fail();
       t += P.lat_l1d;
@@ -2333,11 +2367,41 @@ struct Tile {
       const bool wr = (S.meta[rec] & GG_META_WRITE) != 0;             // access_num == 2 (l1:97-119)
       uint32_t c1, l1;
       L1.get(a, c1, l1);
-      if (!(wr ? c1 == ST_M : c1 != ST_I)) { fail(); return; }
+      if (!sh_l1_ok(c1, wr)) { fail(); return; }
+      if constexpr (ME) sh_mesi_hit(a, wr, c1);
       t += P.lat_l1d;
       if (!L1.access(a, wr)) fail();
       blocked = 0;
       finish(pend_start, t, GG_LVL_DIR);
+    } else if (ME && ty == M_INV_REQ) {                               // …sh_l2_mesi/l1:432-498: a MODIFIED line is flushed
+      uint32_t c1, l1;
+      L1.get(a, c1, l1);
+      if (c1 == ST_M) {
+        t += P.lat_l1d;
+        if (!L1.access(a, false)) fail();                               // readCacheLine
+        sh_l1_invalidate(a);
+        send(m.src, M_FLUSH_REP, m.requester, a, t);
+      } else {
+        t += P.lat_l1t;
+        if (c1 != ST_I) { sh_l1_invalidate(a); send(m.src, M_INV_REP, m.requester, a, t); }
+      }
+    } else if (ME && ty == M_DOWNGRADE_REQ) {                         // processDowngradeReqFromL2Cache (…sh_l2_mesi/l1:540-600)
+      uint32_t c1, l1;
+      L1.get(a, c1, l1);
+      if (c1 != ST_I) {
+        if (c1 == ST_M) {
+          t += P.lat_l1d;
+          if (!L1.access(a, false)) fail();
+          send(m.src, M_WB_REP, m.requester, a, t);
+        } else {
+          if (c1 != ST_E) fail();
+          t += P.lat_l1t;
+          send(m.src, M_DOWNGRADE_REP, m.requester, a, t);
+        }
+        if (!L1.set(a, ST_S, 0)) fail();
+      } else {
+        t += P.lat_l1t;
+      }
     } else if (ty == M_INV_REQ) {                                     // processInvReqFromL2Cache (l1:411-448)
       uint32_t c1, l1;
       L1.get(a, c1, l1);
@@ -2363,7 +2427,7 @@ struct Tile {
       t += P.lat_l2d;
       qpush(a, t, ty, m.requester);
       if (qcount(a) == 1) sh_run(SWork{a, SW_PROC, ty, 1, 0, m.requester, 0}, t);
-    } else if (ty == M_INV_REP || ty == M_FLUSH_REP || ty == M_WB_REP) {   // l2:222-270
+    } else if (ty == M_INV_REP || ty == M_FLUSH_REP || ty == M_WB_REP || (ME && ty == M_DOWNGRADE_REP)) {   // l2:222-270
       t += P.lat_l2d;
       int32_t h = sh_evicted(a);
       if (h == NO_ENT) { h = sh_slot(a); L2.cnt(GG_CC_TAG_READS); }
@@ -2373,7 +2437,14 @@ struct Tile {
         if (ds == DS_SHARED) {
           remove_sharer(h, m.src);
           if (e_nsh(h) == 0) sh_set_ds(h, DS_UNCACHED);
+        } else if (ME && ds == DS_MODIFIED) {                         // …sh_l2_mesi/l2:739-751: the exclusive owner
+          if (e_nsh(h) != 1) fail();
+          remove_sharer(h, m.src);
+          set_owner(h, -1);
+          sh_set_ds(h, DS_UNCACHED);
         }
+      } else if (ME && ty == M_DOWNGRADE_REP) {                       // processDowngradeRepFromL1Cache (…sh_l2_mesi/l2:804-836)
+        if (ds == DS_MODIFIED) { set_owner(h, -1); sh_set_ds(h, DS_SHARED); }
       } else if (ty == M_FLUSH_REP) {                                 // processFlushRepFromL1Cache (:731-773)
         if (ds == DS_MODIFIED) {
           const int32_t f = qfront(a);
@@ -2394,7 +2465,7 @@ struct Tile {
       }
       sh_setinfo(h);
       const int32_t f = qfront(a);
-      if (f >= 0) sh_restart(a, f, h, ty != M_INV_REP, t);
+      if (f >= 0) sh_restart(a, f, h, ty != M_INV_REP && ty != M_DOWNGRADE_REP, t);
     } else if (ty == M_DRAM_FETCH_REP) {                              // L2CacheCntlr::handleMsgFromDram (l2:278-303)
       t += P.lat_l2d;
       const int32_t h = sh_slot(a);
@@ -2835,7 +2906,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
 {
   const uint32_t ln = lane_id(), p = k & 1u;
   PROF_T0();
-  constexpr bool MO = PR == 1, SH = PR == 2;
+  constexpr bool MO = PR == 1, SH = PR >= 2;   // (PR 2 / 3: the shared-L2 MSI / MESI controllers)
   Tile<SL, H, F, PR> T(P, S, lt, p, sl, hk, clds, std::integral_constant<bool, LC>(), pre);
   T.tr_on = DG(S.trs) != nullptr && L < S.tr_n;
   const gg_cmsg* prev = pool(S, p ^ 1u);     // records delivered to this step

@@ -435,12 +435,13 @@ static gg_status coh_alloc(gg_ctx* ctx)
   P.bits_req = 2 * idb + 4 + 48;
   P.bits_data = P.bits_req + 8 * c.line_size;
   P.bits_ifc = P.bits_req + idb;                 // …mosi/shmem_msg.cc:137-139: + the single receiver
-  if (c.protocol > GG_PROTO_SHL2_MSI)
-    return gg_fail(GG_ERR_INVALID, "protocol must be GG_PROTO_MSI, GG_PROTO_MOSI or GG_PROTO_SHL2_MSI");
+  if (c.protocol > GG_PROTO_SHL2_MESI)
+    return gg_fail(GG_ERR_INVALID, "protocol must be GG_PROTO_MSI, _MOSI, _SHL2_MSI or _SHL2_MESI");
   P.mosi = c.protocol == GG_PROTO_MOSI ? 1u : 0u;
-  P.shl2 = c.protocol == GG_PROTO_SHL2_MSI ? 1u : 0u;
+  P.shl2 = c.protocol == GG_PROTO_SHL2_MSI || c.protocol == GG_PROTO_SHL2_MESI ? 1u : 0u;
+  P.mesi = c.protocol == GG_PROTO_SHL2_MESI ? 1u : 0u;
   if (P.shl2) {
-    // pr_l1_sh_l2_msi: the directory entries are the L2 slice's lines
+    // pr_l1_sh_l2_msi / _mesi: the directory entries are the L2 slice's lines
     // (ShL2CacheLineInfo); set = L2CacheHashFn (l2_cache_hash_fn.cc:18-34),
     // the directory's XOR fold with log2(L2 sets) bits and no slice bits
     if (P.s2 < 2 || (P.s2 & (P.s2 - 1))) return gg_fail(GG_ERR_UNSUPPORTED, "pr_l1_sh_l2_msi: L2 sets must be a power of two >= 2");
@@ -645,13 +646,14 @@ static gg_status coh_alloc(gg_ctx* ctx)
 
 static gg_status coh_check(gg_ctx* ctx)
 {
-  uint32_t e = 0;
-  GG_HIP(hipMemcpy(&e, ctx->err_dev, sizeof(e), hipMemcpyDeviceToHost));
+  uint32_t ew[2] = {0, 0};
+  GG_HIP(hipMemcpy(ew, ctx->err_dev, sizeof(ew), hipMemcpyDeviceToHost));
+  const uint32_t e = ew[0];
   if (e & GG_DERR_CAP) return gg_fail(GG_ERR_UNSUPPORTED, "coherent mode: a device capacity (records / inbox / "
                                       "request queue / replaced entries / call chain / segment, or with miss-type "
                                       "tracking the miss_track_lines address table of a tile) was exceeded");
   if (e & GG_DERR_STATE) return gg_fail(GG_ERR_STATE, "coherent mode: a state the reference would reject "
-                                        "(LOG_ASSERT_ERROR / assert)");
+                                        "(LOG_ASSERT_ERROR / assert; first at gg_coh_dev.h:%u)", ew[1]);
   return GG_OK;
 }
 
@@ -676,7 +678,7 @@ gg_status gg_coherent_begin(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_ou
   C->tused = 0;
   GG_HIP(hipMemcpyAsync(C->offs_dev, tr->tile_offsets, sizeof(uint64_t) * (P.T + 1), hipMemcpyHostToDevice, s));
   if (gg_status st = gg_noc_reset(ctx, s)) return st;
-  GG_HIP(hipMemsetAsync(ctx->err_dev, 0, sizeof(uint32_t), s));
+  GG_HIP(hipMemsetAsync(ctx->err_dev, 0, 2 * sizeof(uint32_t), s));
   GG_HIP(hipMemsetAsync(C->S.ri, 0, sizeof(uint64_t) * GG_NUM_RUN_INFO, s));
   GG_HIP(coh_pool_reset(C, s));
   GG_HIP(hipMemsetAsync(C->S.ring, 0, sizeof(uint32_t) * 11, s));

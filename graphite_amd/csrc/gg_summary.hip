@@ -34,7 +34,7 @@ gg_status gg_dump_summary(gg_ctx* ctx, int format, char* buf, uint64_t cap, uint
     ps.resize((size_t)T * GG_NUM_PROTO_STATS);
     if (gg_status e = gg_coherent_get_protocol_stats(ctx, ps.data())) return e;
   }
-  if (coherent && (((mosi || cfg.protocol == GG_PROTO_SHL2_MSI) ? cfg.l1d_track_miss_types : cfg.l1i_track_miss_types) ||
+  if (coherent && (((mosi || cfg.protocol >= GG_PROTO_SHL2_MSI) ? cfg.l1d_track_miss_types : cfg.l1i_track_miss_types) ||
                    cfg.l2_track_miss_types)) {
     mt.resize((size_t)T * 2 * GG_NUM_MISS_TYPES);
     if (gg_status e = gg_coherent_get_miss_types(ctx, mt.data())) return e;

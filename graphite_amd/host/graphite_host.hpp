@@ -435,7 +435,7 @@ inline void writeMemorySummary(std::ostream& out, const gg_config& c, const uint
                                const uint64_t* cache_counters, const uint64_t* miss_types = nullptr,
                                const uint64_t* proto = nullptr)
 {
-  const bool mosi = c.protocol == GG_PROTO_MOSI, shl2 = c.protocol == GG_PROTO_SHL2_MSI;
+  const bool mosi = c.protocol == GG_PROTO_MOSI, shl2 = c.protocol >= GG_PROTO_SHL2_MSI;   // (sh_l2 MSI or MESI)
   const bool l1_mt = (mosi || shl2) ? c.l1d_track_miss_types : c.l1i_track_miss_types;
   out << "Cache Summary:\n";
   // (the L1-D is write-back under pr_l1_sh_l2_msi, …sh_l2_msi/l1_cache_cntlr.cc:57)

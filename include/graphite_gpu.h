@@ -78,7 +78,8 @@ enum { GG_NET_MAGIC = 0, GG_NET_EMESH_HOP_COUNTER = 1, GG_NET_EMESH_HOP_BY_HOP =
 enum { GG_L1D = 0, GG_L2 = 1 };
 
 /* Cache line states, numerically identical to CacheState::Type (cache_state.h:11-21) */
-enum { GG_CSTATE_INVALID = 0, GG_CSTATE_SHARED = 1, GG_CSTATE_OWNED = 2 /* MOSI */, GG_CSTATE_MODIFIED = 4 };
+enum { GG_CSTATE_INVALID = 0, GG_CSTATE_SHARED = 1, GG_CSTATE_OWNED = 2 /* MOSI */, GG_CSTATE_EXCLUSIVE = 3 /* MESI */,
+       GG_CSTATE_MODIFIED = 4 };
 
 /* Cached-location values of a private L2 line, MemComponent::Type subset
  * (PrL2CacheLineInfo::_cached_loc, pr_l1_pr_l2_dram_directory_msi/cache_line_info.h) */
@@ -222,7 +223,7 @@ typedef struct gg_config {
                                     GG_ERR_UNSUPPORTED (no set entry is overwritten). */
   /* ---- caching protocol (caching_protocol/type, carbon_sim.cfg:184) ---- */
   uint32_t protocol;             /* GG_PROTO_*: pr_l1_pr_l2_dram_directory_msi (0) / _mosi (1) /
-                                    pr_l1_sh_l2_msi (2)                                        */
+                                    pr_l1_sh_l2_msi (2) / pr_l1_sh_l2_mesi (3)                */
   uint32_t l1d_track_miss_types; /* l1_dcache/T1/track_miss_types (false): read by the MOSI
                                     protocol only, whose L1CacheCntlr passes the L1-D flag to the
                                     L1-D (…mosi/l1_cache_cntlr.cc:68; MSI passes the L1-I one) */
@@ -233,12 +234,16 @@ typedef struct gg_config {
  * slice per tile (home = line % tiles) whose lines hold the full-map
  * directory entries, a DRAM controller per tile reached by DRAM_FETCH /
  * DRAM_STORE messages; the l2_* geometry is one slice's, the dir_* fields are
- * not used.  MOSI's DramDirectoryCntlr picks "one sharer"
+ * not used.  pr_l1_sh_l2_mesi adds EXCLUSIVE L1 lines: a read of an uncached
+ * line is answered SH_REP_EX, the exclusive owner is invalidated (INV_REQ,
+ * answered FLUSH_REP when modified) or downgraded (DOWNGRADE_REQ, answered
+ * WB_REP when modified, else DOWNGRADE_REP); its own message types count in
+ * GG_CT_MSGS_SENT only.  MOSI's DramDirectoryCntlr picks "one sharer"
  * with the directory entry's own drand48 stream (DirectoryEntryFullMap::
  * getOneSharer, directory_entry_full_map.cc:67-74; misc/random.h), which the
  * reference seeds with time(NULL) when the entry is created: the canonical
  * schedule seeds every entry with GG_MOSI_RNG_SEED (one fixed second).      */
-enum { GG_PROTO_MSI = 0, GG_PROTO_MOSI = 1, GG_PROTO_SHL2_MSI = 2 };
+enum { GG_PROTO_MSI = 0, GG_PROTO_MOSI = 1, GG_PROTO_SHL2_MSI = 2, GG_PROTO_SHL2_MESI = 3 };
 #define GG_MOSI_RNG_SEED 1
 
 /* Miss types (Cache::MissType, cache.h:45-52), counted per (tile, cache). */
@@ -305,7 +310,8 @@ enum {
   GG_MSG_EX_REQ = 1, GG_MSG_SH_REQ, GG_MSG_INV_REQ, GG_MSG_FLUSH_REQ, GG_MSG_WB_REQ,
   GG_MSG_EX_REP, GG_MSG_SH_REP, GG_MSG_UPGRADE_REP, GG_MSG_INV_REP, GG_MSG_FLUSH_REP,
   GG_MSG_WB_REP, GG_MSG_NULLIFY_REQ, GG_MSG_INV_FLUSH_COMBINED_REQ,
-  GG_MSG_DRAM_FETCH_REQ, GG_MSG_DRAM_STORE_REQ, GG_MSG_DRAM_FETCH_REP
+  GG_MSG_DRAM_FETCH_REQ, GG_MSG_DRAM_STORE_REQ, GG_MSG_DRAM_FETCH_REP,
+  GG_MSG_DOWNGRADE_REQ, GG_MSG_SH_REP_EX, GG_MSG_DOWNGRADE_REP   /* pr_l1_sh_l2_mesi (…sh_l2_mesi/shmem_msg.h:14-39) */
 };
 
 /* One ShmemMsg in flight (64 bytes).  The per-sender sequence number keeps

@@ -65,6 +65,12 @@
 #include "pr_l1_pr_l2_dram_directory_mosi/memory_manager.h"
 #undef private
 #undef protected
+#elif defined(GG_PROTO_SHL2) && defined(GG_SHL2_MESI)
+// pr_l1_sh_l2_mesi (coh_harness_shl2_mesi): the shared-L2 organisation with
+// EXCLUSIVE lines (SH_REP_EX, DOWNGRADE_REQ / _REP); the same glue as MSI's
+#include "pr_l1_sh_l2_mesi/memory_manager.h"
+#include "pr_l1_sh_l2_mesi/l2_cache_hash_fn.h"
+#include "pr_l1_sh_l2_mesi/l2_directory_cfg.h"
 #elif defined(GG_PROTO_SHL2)
 // pr_l1_sh_l2_msi (coh_harness_shl2): private L1s, the L2 a shared slice per
 // tile holding each line's directory entry, a DRAM controller per tile
@@ -84,6 +90,8 @@ namespace MSI = PrL1PrL2DramDirectoryMOSI;     // (the glue below is written onc
 // that seed (GG_MOSI_RNG_SEED, include/graphite_gpu.h), so every entry starts
 // from the same drand48 state, as entries created in the same second do
 extern "C" time_t time(time_t* t) { if (t) *t = (time_t)1; return (time_t)1; }
+#elif defined(GG_PROTO_SHL2) && defined(GG_SHL2_MESI)
+namespace MSI = PrL1ShL2MESI;
 #elif defined(GG_PROTO_SHL2)
 namespace MSI = PrL1ShL2MSI;
 #else
@@ -101,6 +109,18 @@ static UInt32 gg_type(UInt32 t)
   case MSI::ShmemMsg::SH_REP: return 7; case MSI::ShmemMsg::UPGRADE_REP: return 8; case MSI::ShmemMsg::INV_REP: return 9;
   case MSI::ShmemMsg::FLUSH_REP: return 10; case MSI::ShmemMsg::WB_REP: return 11; case MSI::ShmemMsg::NULLIFY_REQ: return 12;
   case MSI::ShmemMsg::INV_FLUSH_COMBINED_REQ: return 13;
+  default: CHECK(0); return 0;
+  }
+#elif defined(GG_PROTO_SHL2) && defined(GG_SHL2_MESI)
+  // MESI inserts DOWNGRADE_REQ, SH_REP_EX and DOWNGRADE_REP: they follow the DRAM messages here
+  switch (t) {
+  case MSI::ShmemMsg::EX_REQ: return 1; case MSI::ShmemMsg::SH_REQ: return 2; case MSI::ShmemMsg::INV_REQ: return 3;
+  case MSI::ShmemMsg::FLUSH_REQ: return 4; case MSI::ShmemMsg::WB_REQ: return 5; case MSI::ShmemMsg::EX_REP: return 6;
+  case MSI::ShmemMsg::SH_REP: return 7; case MSI::ShmemMsg::UPGRADE_REP: return 8; case MSI::ShmemMsg::INV_REP: return 9;
+  case MSI::ShmemMsg::FLUSH_REP: return 10; case MSI::ShmemMsg::WB_REP: return 11; case MSI::ShmemMsg::NULLIFY_REQ: return 12;
+  case MSI::ShmemMsg::DRAM_FETCH_REQ: return 14; case MSI::ShmemMsg::DRAM_STORE_REQ: return 15;
+  case MSI::ShmemMsg::DRAM_FETCH_REP: return 16; case MSI::ShmemMsg::DOWNGRADE_REQ: return 17;
+  case MSI::ShmemMsg::SH_REP_EX: return 18; case MSI::ShmemMsg::DOWNGRADE_REP: return 19;
   default: CHECK(0); return 0;
   }
 #elif defined(GG_PROTO_SHL2)
@@ -518,6 +538,8 @@ NetPacket::NetPacket() : time(0), type(INVALID_PACKET_TYPE), sender(INVALID_CORE
 #ifdef GG_PROTO_MOSI
 CachingProtocolType MemoryManager::_caching_protocol_type = PR_L1_PR_L2_DRAM_DIRECTORY_MOSI;
 ofstream MSI::MemoryManager::_cache_line_replication_file;
+#elif defined(GG_PROTO_SHL2) && defined(GG_SHL2_MESI)
+CachingProtocolType MemoryManager::_caching_protocol_type = PR_L1_SH_L2_MESI;
 #elif defined(GG_PROTO_SHL2)
 CachingProtocolType MemoryManager::_caching_protocol_type = PR_L1_SH_L2_MSI;
 #else
@@ -761,7 +783,8 @@ void MSI::MemoryManager::sendMsg(tile_id_t receiver, ShmemMsg& msg)
   g_step.push_back(m);
   S.st[S_SENT]++;
   if (m.type == 13) S.st[S_SENT_IFC]++;                                      // INV_FLUSH_COMBINED_REQ (MOSI)
-  else if (m.type >= 14) S.st[S_SENT_IFC + m.type - 14]++;                  // DRAM_FETCH_REQ / STORE_REQ / FETCH_REP (sh_l2)
+  else if (m.type >= 14 && m.type <= 16) S.st[S_SENT_IFC + m.type - 14]++;  // DRAM_FETCH_REQ / STORE_REQ / FETCH_REP (sh_l2)
+  else if (m.type >= 17) {}                                                 // MESI's own types: msgs_sent only
   else S.st[S_BYTYPE + m.type - 1]++;
 }
 void MSI::MemoryManager::broadcastMsg(ShmemMsg&) { CHECK(0); }   // full_map never broadcasts
@@ -779,7 +802,7 @@ Tile::~Tile() { delete _memory_manager; }
 static UInt32 modeled_bits(UInt32 type)        // network_model.cc:185-200 + shmem_msg.cc:100-125 (…mosi/shmem_msg.cc:122-151)
 {
   UInt32 idb = H.T > 1 ? ceilLog2(H.T) : 0;
-  bool data = type == 6 || type == 7 || type == 10 || type == 11 || type == 15 || type == 16;   // EX_REP, SH_REP, FLUSH_REP, WB_REP, DRAM_STORE_REQ, DRAM_FETCH_REP
+  bool data = type == 6 || type == 7 || type == 10 || type == 11 || type == 15 || type == 16 || type == 18;   // EX_REP, SH_REP, FLUSH_REP, WB_REP, DRAM_STORE_REQ, DRAM_FETCH_REP, SH_REP_EX (DOWNGRADE_REP: no data buffer)
   return 2 * idb + 4 + 48 + (data ? 512 : 0) + (type == 13 ? idb : 0);   // INV_FLUSH_COMBINED_REQ: + single receiver
 }
 static UInt64 lat_ps(UInt64 cycles) { return (UInt64)ceil(((double)1000 * cycles) / 1.0); }
@@ -1112,29 +1135,36 @@ int main(int argc, char** argv)
   // L2 slices: remote L2 hits, DRAM fetches and stores through the DRAM
   // controller, L2 evictions with NULLIFY of their sharers, upgrade replies)
   // and the reference's FFT
-  string mp = g_dir + "/coh_shl2_manifest.json";
+#ifdef GG_SHL2_MESI
+  const string pre = "mesi_";                                   // pr_l1_sh_l2_mesi
+#else
+  const string pre = "shl2_";
+#endif
+  string mp = g_dir + "/coh_" + pre + "manifest.json";
   FILE* man = fopen(mp.c_str(), "w");
   CHECK(man);
   fprintf(man, "{\n");
-  run_case(man, true, "shl2_private16", 16, 1500, 0, 1, 1, 0, 16);
-  run_case(man, false, "shl2_hot16", 16, 1500, 64, 1, 1, 0, 16);
-  run_case(man, false, "shl2_hot16magic", 16, 1000, 8, 1, 0, 0, 16);
-  run_case(man, false, "shl2_shard64", 64, 400, 32, 8, 1, 0, 16);
-  run_case(man, false, "shl2_shard256", 256, 150, 64, 8, 1, 0, 16);
-  run_case(man, false, "shl2_stress256w16", 256, 96, 0, 8, 1, 0, 16, 16, 1);
-  run_case(man, false, "shl2_shard1024", 1024, 24, 256, 8, 1, 0, 16);
+#define N(x) (pre + x).c_str()
+  run_case(man, true, N("private16"), 16, 1500, 0, 1, 1, 0, 16);
+  run_case(man, false, N("hot16"), 16, 1500, 64, 1, 1, 0, 16);
+  run_case(man, false, N("hot16magic"), 16, 1000, 8, 1, 0, 0, 16);
+  run_case(man, false, N("shard64"), 64, 400, 32, 8, 1, 0, 16);
+  run_case(man, false, N("shard256"), 256, 150, 64, 8, 1, 0, 16);
+  run_case(man, false, N("stress256w16"), 256, 96, 0, 8, 1, 0, 16, 16, 1);
+  run_case(man, false, N("shard1024"), 1024, 24, 256, 8, 1, 0, 16);
   // L2 slice evictions (2-way slices; a 1-way slice whose one line waits on a
   // request has no replacement candidate, l2_cache_replacement_policy.cc:55-66):
   // NULLIFY of sharers and owners, DRAM stores
-  run_case(man, false, "shl2_evict16", 16, 12000, 64, 1, 1, 0, 16, 2);
-  run_case(man, false, "shl2_evict16s4", 16, 12000, 64, 4, 1, 0, 16, 2);
+  run_case(man, false, N("evict16"), 16, 12000, 64, 1, 1, 0, 16, 2);
+  run_case(man, false, N("evict16s4"), 16, 12000, 64, 4, 1, 0, 16, 2);
   if (argc > 2) {
     RawTrace fft;
     read_raw(string(argv[2]) + ".addr", fft.addr);
     read_raw(string(argv[2]) + ".meta", fft.meta);
     read_raw(string(argv[2]) + ".offs", fft.offs);
-    run_case(man, false, "shl2_fft10", 16, 0, 0, 1, 1, 0, 16, 8, 2, &fft);
+    run_case(man, false, N("fft10"), 16, 0, 0, 1, 1, 0, 16, 8, 2, &fft);
   }
+#undef N
   fprintf(man, "\n}\n");
   fclose(man);
   return 0;

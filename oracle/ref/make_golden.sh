@@ -16,3 +16,5 @@ python3 "$HERE/export_trace.py" "$GOLD/fft_real_p16_m10.npz" "$HERE/../_ref/fft1
 "$HERE/../_ref/coh_harness_mosi" "$GOLD" "$HERE/../_ref/fft10"
 # the same schedule over the reference's shared-L2 MSI controllers (coh_harness_shl2)
 "$HERE/../_ref/coh_harness_shl2" "$GOLD" "$HERE/../_ref/fft10"
+# and over the shared-L2 MESI controllers (coh_harness_shl2_mesi)
+"$HERE/../_ref/coh_harness_shl2_mesi" "$GOLD" "$HERE/../_ref/fft10"

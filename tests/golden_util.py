@@ -53,11 +53,17 @@ def coh_shl2_manifest():
         return json.load(f)
 
 
+def coh_mesi_sh_manifest():
+    with open(os.path.join(GOLDEN, "coh_mesi_manifest.json")) as f:
+        return json.load(f)
+
+
 def coh_case(name, m):
     """(cfg, addr, meta, offsets, expected dict) of a coherent-mode fixture written
     by oracle/ref/coh_harness.cc (the reference's MSI controllers; "mosi_*"
     names: coh_harness_mosi, the MOSI controllers, plus their event counters;
-    "shl2_*": coh_harness_shl2, the shared-L2 MSI controllers)."""
+    "shl2_*": coh_harness_shl2, the shared-L2 MSI controllers; "mesi_*":
+    coh_harness_shl2_mesi, the shared-L2 MESI controllers)."""
     from graphite_amd import config as C
     from oracle import pyoracle as po
     T, N = m["tiles"], m["per_tile"]
@@ -70,6 +76,8 @@ def coh_case(name, m):
         kw.update(protocol=C.PROTO_MOSI)
     if name.startswith("shl2_"):                     # coh_harness_shl2: pr_l1_sh_l2_msi
         kw.update(protocol=C.PROTO_SHL2_MSI)
+    if name.startswith("mesi_"):                     # coh_harness_shl2_mesi: pr_l1_sh_l2_mesi
+        kw.update(protocol=C.PROTO_SHL2_MESI)
     cfg = C.default_config(T, **kw)
     wl = m.get("workload", "hotspot")
     if wl == "stress":

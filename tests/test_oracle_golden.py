@@ -232,8 +232,12 @@ def test_coherent_shl2_oracle_matches_reference_controllers(name):
     DramCntlr compiled from /root/reference (coh_harness_shl2): access words,
     tile statistics (DRAM_FETCH_REQ / STORE_REQ / FETCH_REP in slots 29-31),
     L1-D and L2-slice counters, NoC counters, quanta / steps."""
+    _shl2_oracle_case(name, G.coh_shl2_manifest())
+
+
+def _shl2_oracle_case(name, manifest):
     from graphite_amd import config as C
-    cfg, a, m, o, exp = G.coh_case(name, G.coh_shl2_manifest()[name])
+    cfg, a, m, o, exp = G.coh_case(name, manifest[name])
     oc = po.OracleCoherent(cfg)
     out = oc.run(a, m, o)
     np.testing.assert_array_equal(out, exp["out"])
@@ -246,7 +250,16 @@ def test_coherent_shl2_oracle_matches_reference_controllers(name):
     assert ri[C.RUN_INFO.index("steps")] == exp["steps"]
 
 
+@pytest.mark.parametrize("name", sorted(G.coh_mesi_sh_manifest()))
+def test_coherent_shl2_mesi_oracle_matches_reference_controllers(name):
+    """The shared-L2 MESI restatement (protocol = GG_PROTO_SHL2_MESI) ==
+    pr_l1_sh_l2_mesi's controllers compiled from /root/reference
+    (coh_harness_shl2_mesi): the same outputs as the MSI test above."""
+    _shl2_oracle_case(name, G.coh_mesi_sh_manifest())
+
+
 def test_shl2_fixtures_exercise_the_protocol():
+    from graphite_amd import config as C_
     """The shared-L2 fixtures reach the slice's paths: remote L2 hits (SH_REPs
     beyond the DRAM fetches), upgrade replies, slice evictions with NULLIFY
     (invalidations of sharers, flushes of owners) and DRAM stores of dirty lines."""
@@ -254,6 +267,10 @@ def test_shl2_fixtures_exercise_the_protocol():
     for name in G.coh_shl2_manifest():
         cfg, a, m, o, exp = G.coh_case(name, G.coh_shl2_manifest()[name])
         tot[name] = (exp["stats"].sum(0), exp["cache"][:, 1].sum(0))
+    mesi_sent = sum(int(G.coh_case(n, G.coh_mesi_sh_manifest()[n])[4]["stats"][:, C_.TILE_STATS.index("msgs_sent")].sum())
+                    for n in ("mesi_hot16", "mesi_shard64"))
+    msi_sent = sum(int(tot[n][0][C_.TILE_STATS.index("msgs_sent")]) for n in ("shl2_hot16", "shl2_shard64"))
+    assert mesi_sent != msi_sent                      # EXCLUSIVE lines change the traffic
     from graphite_amd import config as C
     st = sum(t[0] for t in tot.values())
     by = lambda k: int(st[C.TILE_STATS.index("sent_%s" % k.lower())])
