@@ -59,7 +59,7 @@ EXPORTS = ["gg_abi_version", "gg_last_error", "gg_config_default", "gg_create", 
            "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace", "gg_shard_map",
            "gg_kernel_stats", "gg_round_exchange", "gg_coherent_run_ranks", "gg_gen_stress_trace",
            "gg_split_accesses", "gg_combine_accesses", "gg_dump_summary", "gg_core_model_run", "gg_core_get_stats", "gg_coherent_get_miss_types",
-           "gg_coherent_get_protocol_stats",
+           "gg_coherent_get_protocol_stats", "gg_iocoom_run", "gg_iocoom_get_stats",
            "gg_round_pack", "gg_round_unpack", "gg_round_finish"]
 
 
@@ -133,6 +133,8 @@ def load():
     L.gg_dump_summary.argtypes = [vp, i32, ctypes.c_char_p, u64, ctypes.POINTER(u64)]
     L.gg_core_model_run.argtypes = [vp, ctypes.POINTER(_Trace), vp, vp]
     L.gg_core_get_stats.argtypes = [vp, vp]
+    L.gg_iocoom_run.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.gg_iocoom_get_stats.argtypes = [vp, vp]
     L.gg_coherent_get_miss_types.argtypes = [vp, vp]
     L.gg_coherent_get_protocol_stats.argtypes = [vp, vp]
     L.gg_round_pack.argtypes = [vp, u32, u32, u64, ctypes.POINTER(RoundIO)]
@@ -142,7 +144,8 @@ def load():
                  "gg_coherent_import", "gg_coherent_run", "gg_coherent_get_stats", "gg_gen_hotspot_trace",
                  "gg_round_exchange", "gg_coherent_run_ranks", "gg_gen_stress_trace", "gg_split_accesses",
                  "gg_combine_accesses", "gg_dump_summary", "gg_core_model_run", "gg_core_get_stats",
-                 "gg_coherent_get_miss_types", "gg_coherent_get_protocol_stats", "gg_round_pack", "gg_round_unpack", "gg_round_finish"]:
+                 "gg_coherent_get_miss_types", "gg_coherent_get_protocol_stats", "gg_iocoom_run",
+                 "gg_iocoom_get_stats", "gg_round_pack", "gg_round_unpack", "gg_round_finish"]:
         getattr(L, name).restype = i32
     for name in ["gg_reset", "gg_cache_access_batch", "gg_cache_get_counters", "gg_cache_get_line_info",
                  "gg_cache_set_line_info", "gg_cache_access_line", "gg_cache_insert_line",
@@ -387,6 +390,37 @@ class Backend:
         _need_dev(access_out, torch.int64, n)
         tr = _Trace(None, meta.data_ptr(), self._offs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), n)
         _check(load().gg_core_model_run(self.h, ctypes.byref(tr), access_out.data_ptr(), _stream(stream)))
+
+    def iocoom_run(self, params, ins, ins_offsets, addr, meta, lat, acc_offsets, stream=None):
+        """The iocoom core model (gg_iocoom_run): params (config.IocoomParams),
+        ins (device tensor holding the gg_ins records, 16 B each), host
+        instruction tile offsets, the access stream's addr (int64), meta
+        (int32) and latency (int64, ps) device tensors, host access tile
+        offsets."""
+        import torch
+        T = self.cfg.num_tiles
+        io = np.ascontiguousarray(ins_offsets, np.uint64)
+        ao = np.ascontiguousarray(acc_offsets, np.uint64)
+        if io.size != T + 1 or ao.size != T + 1:
+            raise ValueError("tile offsets need num_tiles + 1 entries")
+        if not ins.is_cuda or not ins.is_contiguous() or ins.numel() * ins.element_size() < 16 * int(io[-1]):
+            raise ValueError("ins: a contiguous device tensor of %d gg_ins records" % int(io[-1]))
+        n = int(ao[-1])
+        _need_dev(addr, torch.int64, n)
+        _need_dev(meta, torch.int32, n)
+        _need_dev(lat, torch.int64, n)
+        self._io_offs = (io, ao)
+        self._io_params = params
+        _check(load().gg_iocoom_run(self.h, ctypes.byref(params), ins.data_ptr(), io.ctypes.data, addr.data_ptr(),
+                                    meta.data_ptr(), lat.data_ptr(), ao.ctypes.data, _stream(stream)))
+
+    def iocoom_stats(self):
+        """[tiles][NUM_IOCOOM_STATS] (gg_iocoom_get_stats)."""
+        from graphite_amd.config import NUM_IOCOOM_STATS
+        T = self.cfg.num_tiles
+        out = np.zeros(T * NUM_IOCOOM_STATS, np.uint64)
+        _check(load().gg_iocoom_get_stats(self.h, out.ctypes.data_as(ctypes.c_void_p)))
+        return out.reshape(T, NUM_IOCOOM_STATS)
 
     def miss_types(self):
         """[tiles][2][3] cold / capacity / sharing misses of the L1-D and L2

@@ -8,6 +8,8 @@ l2_cache/T1 (:230-239), network/emesh_* (:290-313), queue_model/history_tree
 import ctypes
 import math
 
+import numpy as np
+
 POLICY_LRU = 0
 POLICY_ROUND_ROBIN = 1
 NET_MAGIC = 0
@@ -97,6 +99,27 @@ MISS_TYPES = ["cold", "capacity", "sharing"]   # GG_MT_* (Cache::MissType)
 META_BARRIER = 0xFFFFFFFF     # GG_META_BARRIER: a BARRIER record of the trace
 LVL_SYNC = 3                  # GG_LVL_SYNC: its access word (stall << 2) | 3
 NUM_CORE_STATS = 8
+# gg_iocoom_run (include/graphite_gpu.h gg_ins, GG_INS_*, GG_IOCOOM_*)
+INS_DTYPE = np.dtype([("cost", "<u2"), ("ops", "u1"), ("regs", "u1"), ("reg", "<u2", (6,))])
+INS_SIMPLE_MOV_LOAD, INS_ATOMIC, INS_FENCE_SHIFT, INS_SYNC = 0x10, 0x20, 6, 0x80
+IOCOOM_NUM_REGISTERS = 512
+IOCOOM_STATS = ["instructions", "time_ps", "memory_stall_ps", "execution_stall_ps", "sync_instructions",
+                "sync_stall_ps", "load_queue_stall_ps", "store_queue_stall_ps", "l1i_stall_ps",
+                "intra_l1d_stall_ps", "inter_l1d_stall_ps", "intra_exec_stall_ps", "inter_exec_stall_ps",
+                "explicit_fences", "implicit_mfences", "data_accesses", "data_latency_ps"]
+NUM_IOCOOM_STATS = 17
+
+
+class IocoomParams(ctypes.Structure):
+    """gg_iocoom_params; defaults = carbon_sim.cfg [core/iocoom]."""
+    _fields_ = [("num_load_queue_entries", ctypes.c_uint32), ("num_store_queue_entries", ctypes.c_uint32),
+                ("speculative_loads_enabled", ctypes.c_uint32),
+                ("multiple_outstanding_RFOs_enabled", ctypes.c_uint32)]
+
+    def __init__(self, lq=8, sq=8, spec=1, rfo=1):
+        super().__init__(lq, sq, spec, rfo)
+
+
 CMSG_DTYPE = None  # filled below (numpy view of gg_cmsg)
 NUM_NET_COUNTERS = len(NET_COUNTERS)
 

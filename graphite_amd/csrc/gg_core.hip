@@ -21,7 +21,7 @@
 // with a stall is the SyncInstruction of sync_client.cc:306-314 (dynamic:
 // curr_time += stall, CoreModel::updateDynamicInstructionCounters,
 // core_model.cc:237-250).
-#include "gg_internal.h"
+#include "gg_dev.h"
 
 namespace {
 
@@ -100,6 +100,230 @@ __global__ void __launch_bounds__(64 * kCoreWaves) k_core_model(const uint32_t* 
   }
 }
 
+// ---- IOCOOMCoreModel (common/tile/core/models/iocoom_core_model.cc) ---------
+// One wave per tile, every piece of the model's state in registers: the 512
+// register scoreboard entries as 8 per lane (register r in lane r & 63, slot
+// r >> 6) with their units as 2-bit fields, the load queue's and the store
+// buffer's entries one per lane (<= 64 each).  The instructions' fields are
+// wave-uniform (read lane by lane from a 64-instruction window loaded as one
+// 16-B record per lane), so the whole model runs as scalar control with
+// readlanes; the store buffer's address match (isAddressAvailable) is one
+// ballot.  Instructions of one tile are strictly serial (curr_time and the
+// scoreboard): the parallelism is across tiles.
+constexpr uint32_t kIoWaves = 4;
+enum : uint32_t { kUnitInvalid = 0, kUnitLoad = 1, kUnitExec = 3 };   // CoreUnit (iocoom_core_model.h:14-20)
+
+__device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l)
+{
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), (int)l) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
+}
+__device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+typedef uint64_t u64x8 __attribute__((ext_vector_type(8)));
+
+struct IoCore {
+  uint32_t ln;
+  u64x8 sb;                       // _register_scoreboard: register ln + 64 s in slot s (a vector
+                                  // value: a uniform slot index reads it by indirect register
+                                  // addressing, no memory)
+  uint32_t unit;                  // _register_dependency_list: slot s in bits 2s..2s+1
+  uint64_t lsb;                   // LoadQueue::_scoreboard[ln]
+  uint64_t ssb, sad;              // StoreQueue::_scoreboard[ln], _addresses[ln]
+  uint32_t ln_q, sn_q, lidx, sidx;
+  bool spec, rfo;
+  uint64_t one;
+
+  __device__ __forceinline__ uint64_t reg_time(uint32_t r) const
+  {
+    return rl64(sb[r >> 6], r & 63);
+  }
+  __device__ __forceinline__ uint32_t reg_unit(uint32_t r) const
+  {
+    return ((uint32_t)__builtin_amdgcn_readlane((int)unit, (int)(r & 63)) >> (2 * (r >> 6))) & 3u;
+  }
+  __device__ __forceinline__ void reg_write(uint32_t r, uint64_t t, uint32_t u)
+  {
+    const uint32_t s = r >> 6;
+    const bool mine = ln == (r & 63);
+    const uint64_t old = sb[s];
+    sb[s] = mine ? t : old;
+    if (mine) unit = (unit & ~(3u << (2 * s))) | (u << (2 * s));
+  }
+  // LoadQueue::execute (:182-208): the allocate time, *completion
+  __device__ __forceinline__ uint64_t lq_execute(uint64_t schedule, uint64_t lat, uint64_t& completion)
+  {
+    const uint32_t last = (lidx + ln_q - 1) % ln_q;
+    const uint64_t allocate = umax64(rl64(lsb, lidx), schedule), lastd = rl64(lsb, last);
+    uint64_t dealloc;
+    if (spec) { completion = allocate + lat; dealloc = umax64(completion, lastd + one); }
+    else { completion = umax64(lastd, schedule) + lat; dealloc = completion; }
+    if (ln == lidx) lsb = dealloc;
+    lidx = (lidx + 1) % ln_q;
+    return allocate;
+  }
+  // executeLoad (:140-153) with StoreQueue::isAddressAvailable (:296-309)
+  __device__ __forceinline__ uint64_t load(uint64_t schedule, uint64_t a, uint64_t latency, uint64_t& completion)
+  {
+    if (__ballot(ln < sn_q && sad == a && ssb >= schedule)) { completion = schedule + one; return schedule; }
+    return lq_execute(schedule, latency + one, completion);
+  }
+  // executeStore (:155-165) + StoreQueue::execute (:250-284)
+  __device__ __forceinline__ uint64_t store(uint64_t schedule, uint64_t a, uint64_t latency)
+  {
+    const uint64_t lat = latency + one;
+    const uint64_t last_load = rl64(lsb, (lidx + ln_q - 1) % ln_q);
+    const uint64_t allocate = umax64(rl64(ssb, sidx), schedule);
+    const uint64_t last_store = rl64(ssb, (sidx + sn_q - 1) % sn_q);
+    const uint64_t dealloc = rfo ? umax64(umax64(allocate + lat, last_store + one), last_load)
+                                 : umax64(umax64(schedule, last_store), last_load) + lat;
+    if (ln == sidx) { ssb = dealloc; sad = a; }
+    sidx = (sidx + 1) % sn_q;
+    return allocate;
+  }
+};
+
+// The access stream, 64 accesses per window (lane l holds access base + l)
+struct IoAcc {
+  uint64_t base = ~0ull, a = 0, l = 0;
+  uint32_t m = 0;
+  __device__ __forceinline__ void get(uint64_t k, uint64_t end, const uint64_t* __restrict__ addr,
+                                      const uint32_t* __restrict__ meta, const uint64_t* __restrict__ lat,
+                                      uint32_t ln, uint64_t& A, uint32_t& M, uint64_t& L)
+  {
+    if (base == ~0ull || k - base >= 64) {
+      base = k;
+      const uint64_t i = k + ln;
+      a = i < end ? addr[i] : 0; m = i < end ? meta[i] : 0; l = i < end ? lat[i] : 0;
+    }
+    const uint32_t j = (uint32_t)(k - base);
+    A = rl64(a, j); M = (uint32_t)__builtin_amdgcn_readlane((int)m, (int)j); L = rl64(l, j);
+  }
+};
+
+__global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restrict__ ins, const uint64_t* __restrict__ offs,
+                                                          const uint64_t* __restrict__ addr,
+                                                          const uint32_t* __restrict__ meta,
+                                                          const uint64_t* __restrict__ lat, uint32_t T,
+                                                          gg_iocoom_params p, double f, uint64_t* stats, uint32_t* err)
+{
+  const uint32_t t = blockIdx.x * kIoWaves + (threadIdx.x >> 6), ln = threadIdx.x & 63;
+  if (t >= T) return;
+  IoCore c;
+  c.ln = ln;
+  c.sb = u64x8{0, 0, 0, 0, 0, 0, 0, 0};
+  c.unit = 0; c.lsb = 0; c.ssb = 0; c.sad = ~0ull;                  // INVALID_ADDRESS (fixed_types.h:36)
+  c.ln_q = p.num_load_queue_entries; c.sn_q = p.num_store_queue_entries; c.lidx = 0; c.sidx = 0;
+  c.spec = p.speculative_loads_enabled != 0; c.rfo = p.multiple_outstanding_RFOs_enabled != 0;
+  c.one = gg::lat_to_ps(1, f);
+  IoAcc acc;
+  uint64_t st[GG_NUM_IOCOOM_STATS];
+#pragma unroll
+  for (int k = 0; k < GG_NUM_IOCOOM_STATS; ++k) st[k] = 0;
+  const uint64_t i0 = offs[t], i1 = offs[t + 1], k1 = offs[T + 1 + t + 1];
+  uint64_t k = offs[T + 1 + t], curr = 0;
+  bool bad = false;
+  for (uint64_t b = i0; b < i1 && !bad; b += 64) {
+    const uint4 w = b + ln < i1 ? ins[b + ln] : make_uint4(0, 0, 0, 0);
+    const uint32_t cnt = i1 - b < 64 ? (uint32_t)(i1 - b) : 64u;
+    for (uint32_t j = 0; j < cnt && !bad; ++j) {
+      const uint32_t w0 = (uint32_t)__builtin_amdgcn_readlane((int)w.x, (int)j);
+      const uint32_t wr[3] = {(uint32_t)__builtin_amdgcn_readlane((int)w.y, (int)j),
+                              (uint32_t)__builtin_amdgcn_readlane((int)w.z, (int)j),
+                              (uint32_t)__builtin_amdgcn_readlane((int)w.w, (int)j)};
+      auto reg = [&](uint32_t i) {                                  // (a select: no indexed register array)
+        const uint32_t x = (i >> 1) == 0 ? wr[0] : (i >> 1) == 1 ? wr[1] : wr[2];
+        return (x >> (16 * (i & 1))) & 0xFFFFu;
+      };
+      const uint32_t ops = (w0 >> 16) & 0xFFu, regs = w0 >> 24;
+      ++st[GG_IOCOOM_INSTRUCTIONS];                                   // :72
+      if (regs & GG_INS_SYNC) {                                       // dynamic (:74-79)
+        uint64_t A, L; uint32_t M;
+        if (k >= k1) { bad = true; break; }
+        acc.get(k++, k1, addr, meta, lat, ln, A, M, L);
+        if (M != GG_META_BARRIER) { bad = true; break; }
+        if (!L) { --st[GG_IOCOOM_INSTRUCTIONS]; continue; }
+        curr += L;
+        ++st[GG_IOCOOM_SYNC_INSTRUCTIONS];
+        st[GG_IOCOOM_SYNC_STALL_PS] += L;
+        continue;
+      }
+      const uint64_t cost = gg::lat_to_ps(w0 & 0xFFFFu, f);              // getCost (:70)
+      const uint64_t ready = curr;                                    // no L1-I (:78-87)
+      const uint32_t nr = regs & 7u, nw = (regs >> 3) & 7u;
+      if (nr + nw > 6) { bad = true; break; }
+      uint64_t rl = ready, re = ready;                                // :100-125
+      for (uint32_t i = 0; i < nr; ++i) {
+        const uint32_t r = reg(i);
+        if (r >= GG_IOCOOM_NUM_REGISTERS) { bad = true; break; }
+        const uint32_t u = c.reg_unit(r);
+        const uint64_t v = c.reg_time(r);
+        if (u == kUnitLoad) rl = umax64(rl, v);
+        else if (u == kUnitExec) re = umax64(re, v);
+        else if (v > ready) { bad = true; break; }
+      }
+      if (bad) break;
+      const uint64_t rr = umax64(rl, re);                             // :128-129
+      uint64_t lqr = rr, rmr = rr;                                    // :133-152
+      for (uint32_t i = 0; i < (ops & 3u); ++i) {
+        uint64_t A, L; uint32_t M;
+        if (k >= k1) { bad = true; break; }
+        acc.get(k++, k1, addr, meta, lat, ln, A, M, L);
+        if (M == GG_META_BARRIER || (M & GG_META_WRITE)) { bad = true; break; }
+        uint64_t comp;
+        const uint64_t alloc = c.load(rr, A, L, comp);
+        ++st[GG_IOCOOM_DATA_ACCESSES]; st[GG_IOCOOM_DATA_LATENCY_PS] += L;
+        lqr = umax64(lqr, alloc); rmr = umax64(rmr, comp);
+      }
+      if (bad) break;
+      const uint64_t wor = rmr + cost;                                // :158-166
+      const bool smov = (ops & GG_INS_SIMPLE_MOV_LOAD) != 0;
+      for (uint32_t i = 0; i < nw; ++i) {                             // :172-184
+        const uint32_t r = reg(nr + i);
+        if (r >= GG_IOCOOM_NUM_REGISTERS) { bad = true; break; }
+        c.reg_write(r, wor, smov ? kUnitLoad : kUnitExec);
+      }
+      if (bad) break;
+      uint64_t sqr = wor;                                             // :186-201
+      const uint32_t nwm = (ops >> 2) & 3u;
+      for (uint32_t i = 0; i < nwm; ++i) {
+        uint64_t A, L; uint32_t M;
+        if (k >= k1) { bad = true; break; }
+        acc.get(k++, k1, addr, meta, lat, ln, A, M, L);
+        if (M == GG_META_BARRIER || !(M & GG_META_WRITE)) { bad = true; break; }
+        sqr = umax64(sqr, c.store(wor, A, L));
+        ++st[GG_IOCOOM_DATA_ACCESSES]; st[GG_IOCOOM_DATA_LATENCY_PS] += L;
+      }
+      if (bad) break;
+      uint64_t mem = 0, ex = 0;                                       // :209-252
+      ex += re - ready;   st[GG_IOCOOM_INTER_EXEC_STALL_PS] += re - ready;
+      mem += rr - re;     st[GG_IOCOOM_INTER_L1D_STALL_PS] += rr - re;
+      mem += lqr - rr;    st[GG_IOCOOM_LOAD_QUEUE_STALL_PS] += lqr - rr;
+      curr = lqr;
+      if (!smov) {
+        mem += rmr - lqr; st[GG_IOCOOM_INTRA_L1D_STALL_PS] += rmr - lqr;
+        curr = rmr;
+        if (nwm) {
+          ex += wor - rmr;  st[GG_IOCOOM_INTRA_EXEC_STALL_PS] += wor - rmr;
+          mem += sqr - wor; st[GG_IOCOOM_STORE_QUEUE_STALL_PS] += sqr - wor;
+          curr = sqr;
+        }
+      }
+      if (ops & GG_INS_ATOMIC) ++st[GG_IOCOOM_IMPLICIT_MFENCES];     // core_model.cc:221-235
+      if (ops >> GG_INS_FENCE_SHIFT) ++st[GG_IOCOOM_EXPLICIT_FENCES];
+      st[GG_IOCOOM_MEMORY_STALL_PS] += mem;                           // core_model.cc:260-264
+      st[GG_IOCOOM_EXECUTION_STALL_PS] += ex;
+    }
+  }
+  if (k != k1) bad = true;
+  st[GG_IOCOOM_TIME_PS] = curr;
+  if (bad) { if (ln == 0) atomicOr(err, 1u); return; }
+  // lane s stores statistic s (one vector store)
+  uint64_t v = 0;
+#pragma unroll
+  for (int s = 0; s < GG_NUM_IOCOOM_STATS; ++s) v = ln == (uint32_t)s ? st[s] : v;
+  if (ln < GG_NUM_IOCOOM_STATS) stats[(size_t)t * GG_NUM_IOCOOM_STATS + ln] = v;
+}
+
 uint64_t cycle_ps(double f_ghz) { return (uint64_t)ceil(((double)1000 * 1) / f_ghz); }   // Latency(1, f).toPicosec
 
 }  // namespace
@@ -109,6 +333,10 @@ void gg_core_free(gg_ctx* ctx)
   if (ctx->core_dev) hipFree(ctx->core_dev);
   if (ctx->core_tasks) hipFree(ctx->core_tasks);
   ctx->core_dev = nullptr; ctx->core_tasks = nullptr; ctx->core_task_cap = 0; ctx->core_valid = false;
+  if (ctx->io_stats) hipFree(ctx->io_stats);
+  if (ctx->io_offs) hipFree(ctx->io_offs);
+  if (ctx->io_err) hipFree(ctx->io_err);
+  ctx->io_stats = nullptr; ctx->io_offs = nullptr; ctx->io_err = nullptr; ctx->io_valid = false;
 }
 
 extern "C" {
@@ -162,6 +390,64 @@ gg_status gg_core_get_stats(gg_ctx* ctx, uint64_t* out)
   hipSetDevice(ctx->device);
   GG_HIP(hipStreamSynchronize(ctx->last_stream));
   GG_HIP(hipMemcpy(out, ctx->core_dev, sizeof(uint64_t) * ctx->cfg.num_tiles * GG_NUM_CORE_STATS,
+                   hipMemcpyDeviceToHost));
+  return GG_OK;
+}
+
+gg_status gg_iocoom_run(gg_ctx* ctx, const gg_iocoom_params* params, const gg_ins* ins_dev,
+                        const uint64_t* ins_tile_offsets, const uint64_t* acc_addr_dev, const uint32_t* acc_meta_dev,
+                        const uint64_t* acc_lat_dev, const uint64_t* acc_tile_offsets, void* stream)
+{
+  if (!ctx || !params || !ins_tile_offsets || !acc_tile_offsets)
+    return gg_fail(GG_ERR_INVALID, "gg_iocoom_run: NULL argument");
+  const gg_iocoom_params p = *params;
+  if (p.num_load_queue_entries - 1u >= 64u || p.num_store_queue_entries - 1u >= 64u)
+    return gg_fail(GG_ERR_UNSUPPORTED, "gg_iocoom_run: queue entries %u / %u (1..64)", p.num_load_queue_entries,
+                   p.num_store_queue_entries);
+  const uint32_t T = ctx->cfg.num_tiles;
+  for (const uint64_t* o : {ins_tile_offsets, acc_tile_offsets})
+    for (uint32_t t = 0; t < T; ++t)
+      if (o[t + 1] < o[t]) return gg_fail(GG_ERR_INVALID, "gg_iocoom_run: tile offsets decrease");
+  if (ins_tile_offsets[T] > ins_tile_offsets[0] && !ins_dev) return gg_fail(GG_ERR_INVALID, "gg_iocoom_run: NULL instructions");
+  if (acc_tile_offsets[T] > acc_tile_offsets[0] && (!acc_addr_dev || !acc_meta_dev || !acc_lat_dev))
+    return gg_fail(GG_ERR_INVALID, "gg_iocoom_run: NULL access stream");
+  if (!(ctx->cfg.frequency_ghz > 0)) return gg_fail(GG_ERR_INVALID, "gg_iocoom_run: frequency %g", ctx->cfg.frequency_ghz);
+  hipSetDevice(ctx->device);
+  hipStream_t s = (hipStream_t)stream;
+  ctx->last_stream = s;
+  if (!ctx->io_stats) {
+    GG_HIP(hipMalloc((void**)&ctx->io_stats, sizeof(uint64_t) * T * GG_NUM_IOCOOM_STATS));
+    GG_HIP(hipMalloc((void**)&ctx->io_offs, sizeof(uint64_t) * 2 * (T + 1)));
+    GG_HIP(hipMalloc((void**)&ctx->io_err, sizeof(uint32_t)));
+  }
+  std::vector<uint64_t> offs(2 * (size_t)(T + 1));
+  std::copy(ins_tile_offsets, ins_tile_offsets + T + 1, offs.begin());
+  std::copy(acc_tile_offsets, acc_tile_offsets + T + 1, offs.begin() + T + 1);
+  GG_HIP(hipMemcpyAsync(ctx->io_offs, offs.data(), sizeof(uint64_t) * offs.size(), hipMemcpyHostToDevice, s));
+  GG_HIP(hipMemsetAsync(ctx->io_stats, 0, sizeof(uint64_t) * T * GG_NUM_IOCOOM_STATS, s));
+  GG_HIP(hipMemsetAsync(ctx->io_err, 0, sizeof(uint32_t), s));
+  if (T) {
+    gg_timer_begin(ctx, "iocoom", s);
+    hipLaunchKernelGGL(k_iocoom, dim3((T + kIoWaves - 1) / kIoWaves), dim3(64 * kIoWaves), 0, s,
+                       reinterpret_cast<const uint4*>(ins_dev), (const uint64_t*)ctx->io_offs, acc_addr_dev,
+                       acc_meta_dev, acc_lat_dev, T, p, ctx->cfg.frequency_ghz, ctx->io_stats, ctx->io_err);
+    GG_HIP(hipGetLastError());
+    gg_timer_end(ctx, "iocoom", s);
+  }
+  ctx->io_valid = true;
+  return GG_OK;
+}
+
+gg_status gg_iocoom_get_stats(gg_ctx* ctx, uint64_t* out)
+{
+  if (!ctx || !out) return gg_fail(GG_ERR_INVALID, "gg_iocoom_get_stats: NULL argument");
+  if (!ctx->io_valid) return gg_fail(GG_ERR_STATE, "gg_iocoom_get_stats: gg_iocoom_run has not run");
+  hipSetDevice(ctx->device);
+  GG_HIP(hipStreamSynchronize(ctx->last_stream));
+  uint32_t e = 0;
+  GG_HIP(hipMemcpy(&e, ctx->io_err, sizeof e, hipMemcpyDeviceToHost));
+  if (e) return gg_fail(GG_ERR_STATE, "gg_iocoom_run: the instruction and access streams disagree");
+  GG_HIP(hipMemcpy(out, ctx->io_stats, sizeof(uint64_t) * ctx->cfg.num_tiles * GG_NUM_IOCOOM_STATS,
                    hipMemcpyDeviceToHost));
   return GG_OK;
 }

@@ -108,6 +108,12 @@ struct gg_ctx {
   void* core_tasks = nullptr;
   uint64_t core_task_cap = 0;
   bool core_valid = false;
+  // the iocoom core model (gg_core.hip): [tiles][GG_NUM_IOCOOM_STATS], the
+  // two offset lists [2][tiles + 1] and the stream-check word
+  uint64_t* io_stats = nullptr;
+  uint64_t* io_offs = nullptr;
+  uint32_t* io_err = nullptr;
+  bool io_valid = false;
   // multi-rank round buffers (gg_round.hip), freed by gg_destroy
   void* round = nullptr;
   void (*round_free)(void*) = nullptr;

@@ -44,6 +44,11 @@ gg_status gg_dump_summary(gg_ctx* ctx, int format, char* buf, uint64_t cap, uint
     core.resize((size_t)T * GG_NUM_CORE_STATS);
     if (gg_status e = gg_core_get_stats(ctx, core.data())) return e;
   }
+  std::vector<uint64_t> io;
+  if (ctx->io_valid) {                         // gg_iocoom_run's statistics: the iocoom "Core Summary" blocks
+    io.resize((size_t)T * GG_NUM_IOCOOM_STATS);
+    if (gg_status e = gg_iocoom_get_stats(ctx, io.data())) return e;
+  }
   std::string text;
   try {
     std::vector<std::string> per_tile;
@@ -54,7 +59,8 @@ gg_status gg_dump_summary(gg_ctx* ctx, int format, char* buf, uint64_t cap, uint
                                      &cc[(size_t)t * 2 * GG_NUM_CACHE_COUNTERS], &nc[(size_t)t * GG_NUM_NET_COUNTERS],
                                      core.empty() ? nullptr : &core[(size_t)t * GG_NUM_CORE_STATS],
                                      mt.empty() ? nullptr : &mt[(size_t)t * 2 * GG_NUM_MISS_TYPES],
-                                     ps.empty() ? nullptr : &ps[(size_t)t * GG_NUM_PROTO_STATS]);
+                                     ps.empty() ? nullptr : &ps[(size_t)t * GG_NUM_PROTO_STATS],
+                                     io.empty() ? nullptr : &io[(size_t)t * GG_NUM_IOCOOM_STATS]);
       if (format == GG_SUMMARY_TABLE) per_tile.push_back(os.str());
       else all << "Tile " << t << " Summary:" << std::endl << os.str();
     }

@@ -158,34 +158,36 @@ inline uint64_t psToCycles(uint64_t ps, double f) { return (uint64_t)ceil(((doub
 // Core::outputSummary's shared-memory block (core.cc:283-310; no L1-I).
 // McPATCoreInterface's parameter and micro-op tables (mcpat_core_interface.cc:
 // 780-1020) are not written: McPAT is not part of this path.
-inline void writeCoreSummary(std::ostream& os, const uint64_t* core, double frequency_ghz)
+// CoreModel::outputSummary's lines (core_model.cc:90-115) for a model's
+// instruction count, completion time, sync / stall totals and fence counts
+inline void writeCoreModelSummary(std::ostream& os, uint64_t n, uint64_t t, uint64_t sync_n, uint64_t mem_ps,
+                                  uint64_t ex_ps, uint64_t sync_ps, uint64_t explicit_fences, uint64_t implicit_fences,
+                                  double frequency_ghz)
 {
-  const uint64_t n = core[GG_CORE_INSTRUCTIONS], t = core[GG_CORE_TIME_PS];
   const uint64_t zero = 0;
   const double avg_f = ((double)psToCycles(t, frequency_ghz)) / ((double)psToNanosec(t));
   os << "Core Summary:" << std::endl;
   os << "    Total Instructions: " << n << std::endl;
   os << "    Completion Time (in nanoseconds): " << psToNanosec(t) << std::endl;
   os << "    Average Frequency (in GHz): " << avg_f << std::endl;
-  os << "    Synchronization Stalls: " << core[GG_CORE_SYNC_INSTRUCTIONS] << std::endl;
+  os << "    Synchronization Stalls: " << sync_n << std::endl;
   os << "    Network Recv Stalls: " << zero << std::endl;
   os << "    Stall Time Breakdown (in nanoseconds): " << std::endl;
-  os << "      Memory: " << psToNanosec(core[GG_CORE_MEMORY_STALL_PS]) << std::endl;
-  os << "      Execution Unit: " << psToNanosec(core[GG_CORE_EXECUTION_STALL_PS]) << std::endl;
-  os << "      Synchronization: " << psToNanosec(core[GG_CORE_SYNC_STALL_PS]) << std::endl;
+  os << "      Memory: " << psToNanosec(mem_ps) << std::endl;
+  os << "      Execution Unit: " << psToNanosec(ex_ps) << std::endl;
+  os << "      Synchronization: " << psToNanosec(sync_ps) << std::endl;
   os << "      Network Recv: " << psToNanosec(0) << std::endl;
   os << "    Branch Predictor Statistics:" << std::endl
      << "      Num Correct: " << zero << std::endl
      << "      Num Incorrect: " << zero << std::endl;
   os << "    Fence Instructions: " << std::endl;
-  os << "      Explicit LFENCE, SFENCE, MFENCE: " << zero << std::endl;
-  os << "      Implicit MFENCE: " << zero << std::endl;
-  os << "    Detailed Stall Time Breakdown (in nanoseconds): " << std::endl;
-  os << "      L1-I Cache: " << psToNanosec(0) << std::endl;
-  os << "      L1-D Cache: "
-     << psToNanosec(core[GG_CORE_L1D_READ_STALL_PS]) + psToNanosec(core[GG_CORE_L1D_WRITE_STALL_PS]) << std::endl;
-  const uint64_t ni = 0, data_ns = psToNanosec(core[GG_CORE_MEMORY_STALL_PS]), instr_ns = psToNanosec(0);
-  const uint64_t nd = n - core[GG_CORE_SYNC_INSTRUCTIONS];          // data accesses (Core::_num_data_memory_accesses)
+  os << "      Explicit LFENCE, SFENCE, MFENCE: " << explicit_fences << std::endl;
+  os << "      Implicit MFENCE: " << implicit_fences << std::endl;
+}
+// Core::outputSummary's shared-memory block (core.cc:283-310; no L1-I)
+inline void writeCoreMemorySummary(std::ostream& os, uint64_t nd, uint64_t data_ps)
+{
+  const uint64_t zero = 0, ni = 0, data_ns = psToNanosec(data_ps), instr_ns = psToNanosec(0);
   os << "Shared Memory Model Summary: " << std::endl;
   os << "    Total Memory Accesses: " << ni + nd << std::endl;
   os << "    Average Memory Access Latency (in nanoseconds): " << (1.0 * (instr_ns + data_ns) / (ni + nd)) << std::endl;
@@ -194,6 +196,36 @@ inline void writeCoreSummary(std::ostream& os, const uint64_t* core, double freq
   os << "    Average Instruction Memory Access Latency (in nanoseconds): " << 1.0 * instr_ns / ni << std::endl;
   os << "    Total Data Memory Accesses: " << nd << std::endl;
   os << "    Average Data Memory Access Latency (in nanoseconds): " << 1.0 * data_ns / nd << std::endl;
+}
+inline void writeCoreSummary(std::ostream& os, const uint64_t* core, double frequency_ghz)
+{
+  const uint64_t n = core[GG_CORE_INSTRUCTIONS];
+  writeCoreModelSummary(os, n, core[GG_CORE_TIME_PS], core[GG_CORE_SYNC_INSTRUCTIONS], core[GG_CORE_MEMORY_STALL_PS],
+                        core[GG_CORE_EXECUTION_STALL_PS], core[GG_CORE_SYNC_STALL_PS], 0, 0, frequency_ghz);
+  os << "    Detailed Stall Time Breakdown (in nanoseconds): " << std::endl;
+  os << "      L1-I Cache: " << psToNanosec(0) << std::endl;
+  os << "      L1-D Cache: "
+     << psToNanosec(core[GG_CORE_L1D_READ_STALL_PS]) + psToNanosec(core[GG_CORE_L1D_WRITE_STALL_PS]) << std::endl;
+  // data accesses (Core::_num_data_memory_accesses): the instructions but the sync ones
+  writeCoreMemorySummary(os, n - core[GG_CORE_SYNC_INSTRUCTIONS], core[GG_CORE_MEMORY_STALL_PS]);
+}
+// The iocoom core model's part (GG_IOCOOM_* statistics of gg_iocoom_run):
+// CoreModel::outputSummary, IOCOOMCoreModel's detailed breakdown
+// (iocoom_core_model.cc:53-64), the shared-memory block.
+inline void writeIocoomSummary(std::ostream& os, const uint64_t* io, double frequency_ghz)
+{
+  writeCoreModelSummary(os, io[GG_IOCOOM_INSTRUCTIONS], io[GG_IOCOOM_TIME_PS], io[GG_IOCOOM_SYNC_INSTRUCTIONS],
+                        io[GG_IOCOOM_MEMORY_STALL_PS], io[GG_IOCOOM_EXECUTION_STALL_PS], io[GG_IOCOOM_SYNC_STALL_PS],
+                        io[GG_IOCOOM_EXPLICIT_FENCES], io[GG_IOCOOM_IMPLICIT_MFENCES], frequency_ghz);
+  os << "    Detailed Stall Time Breakdown (in nanoseconds): " << std::endl;
+  os << "      Load Queue: " << psToNanosec(io[GG_IOCOOM_LOAD_QUEUE_STALL_PS]) << std::endl;
+  os << "      Store Queue: " << psToNanosec(io[GG_IOCOOM_STORE_QUEUE_STALL_PS]) << std::endl;
+  os << "      L1-I Cache: " << psToNanosec(io[GG_IOCOOM_L1I_STALL_PS]) << std::endl;
+  os << "      L1-D Cache (Intra-Instruction): " << psToNanosec(io[GG_IOCOOM_INTRA_L1D_STALL_PS]) << std::endl;
+  os << "      L1-D Cache (Inter-Instruction): " << psToNanosec(io[GG_IOCOOM_INTER_L1D_STALL_PS]) << std::endl;
+  os << "      Execution Unit (Intra-Instruction): " << psToNanosec(io[GG_IOCOOM_INTRA_EXEC_STALL_PS]) << std::endl;
+  os << "      Execution Unit (Inter-Instruction): " << psToNanosec(io[GG_IOCOOM_INTER_EXEC_STALL_PS]) << std::endl;
+  writeCoreMemorySummary(os, io[GG_IOCOOM_DATA_ACCESSES], io[GG_IOCOOM_DATA_LATENCY_PS]);
 }
 
 // NetworkModel::outputSummary (network/network_model.cc:274-316) for one tile's
@@ -465,10 +497,12 @@ inline void writeMemorySummary(std::ostream& out, const gg_config& c, const uint
 inline void writeTileSummary(std::ostream& os, const gg_config& cfg, const uint64_t* tile_stats,
                              const uint64_t* cache_counters, const uint64_t* net_counters,
                              const uint64_t* core_stats = nullptr, const uint64_t* miss_types = nullptr,
-                             const uint64_t* proto = nullptr)
+                             const uint64_t* proto = nullptr, const uint64_t* iocoom_stats = nullptr)
 {
   static const uint64_t zero_net[GG_NUM_NET_COUNTERS] = {0};
-  if (core_stats) writeCoreSummary(os, core_stats, cfg.frequency_ghz);   // Tile::outputSummary (tile.cc:52-69)
+  // Tile::outputSummary (tile.cc:52-69): the tile's core model (iocoom when gg_iocoom_run ran)
+  if (iocoom_stats) writeIocoomSummary(os, iocoom_stats, cfg.frequency_ghz);
+  else if (core_stats) writeCoreSummary(os, core_stats, cfg.frequency_ghz);
   if (tile_stats) writeMemorySummary(os, cfg, tile_stats, cache_counters, miss_types, proto);
   else {
     os << "Cache Summary:\n";

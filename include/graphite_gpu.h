@@ -56,7 +56,7 @@
 extern "C" {
 #endif
 
-#define GG_ABI_VERSION 9
+#define GG_ABI_VERSION 10
 
 typedef int gg_status;
 enum {
@@ -677,6 +677,85 @@ gg_status gg_core_model_run(gg_ctx* ctx, const gg_trace* trace, const uint64_t* 
 /* out: num_tiles * GG_NUM_CORE_STATS (host).  Synchronizes.  GG_ERR_STATE if
  * gg_core_model_run has not run on the context.                              */
 gg_status gg_core_get_stats(gg_ctx* ctx, uint64_t* out);
+
+/* The iocoom core model (IOCOOMCoreModel, common/tile/core/models/
+ * iocoom_core_model.cc; carbon_sim.cfg's default core type): an in-order core
+ * with a register scoreboard and out-of-order memory through a load queue
+ * and a store buffer.  Its time depends on register dependences, so it runs
+ * over an INSTRUCTION stream, one gg_ins per instruction the core model
+ * handles (CoreModel::iterate, core_model.cc:290-297), whose memory operands
+ * take their DynamicMemoryInfo {address, read, latency} from an ACCESS
+ * stream in order (Core::initiateMemoryAccess pushes one per access,
+ * core.cc:258-263): per tile, the k-th memory operand of the instruction
+ * stream (each instruction's reads, then its writes) is the k-th access.
+ * The access stream's latencies are a coherent run's (gg_combine_accesses
+ * of its line words, or its access words >> 2 for an unsplit trace): the
+ * memory system is timed with the engine's issue times, and the core model
+ * retimes the core around them (the reference feeds iocoom's curr_time back
+ * as the next access's initial time; a trace carries no instructions between
+ * its accesses to do that with).                                            */
+typedef struct {
+  uint16_t cost;     /* static cost in core cycles (Instruction::getCost: the
+                        [core/static_instruction_costs] of its type, or a
+                        branch's resolved cost); unused by a SYNC instruction */
+  uint8_t  ops;      /* bits 0-1 memory read operands, bits 2-3 memory write
+                        operands, GG_INS_SIMPLE_MOV_LOAD, GG_INS_ATOMIC,
+                        GG_INS_FENCE_* in bits 6-7                             */
+  uint8_t  regs;     /* bits 0-2 read registers, bits 3-5 write registers
+                        (reads + writes <= 6), GG_INS_SYNC                     */
+  uint16_t reg[6];   /* the read registers, then the write registers (< 512)  */
+} gg_ins;
+#define GG_INS_SIMPLE_MOV_LOAD 0x10u   /* Instruction::isSimpleMovMemoryLoad            */
+#define GG_INS_ATOMIC          0x20u   /* Instruction::isAtomic (implicit MFENCE)        */
+#define GG_INS_FENCE_SHIFT     6       /* 1 LFENCE, 2 SFENCE, 3 MFENCE (INST_*FENCE)    */
+#define GG_INS_SYNC            0x80u   /* a SyncInstruction (dynamic): consumes the next
+                                          access, which must be a BARRIER record, and
+                                          costs its stall (sync_client.cc:306-314); a
+                                          released barrier without a stall is no
+                                          instruction, as in gg_core_model_run        */
+#define GG_IOCOOM_NUM_REGISTERS 512    /* IOCOOMCoreModel::_NUM_REGISTERS               */
+typedef struct {
+  uint32_t num_load_queue_entries;             /* [core/iocoom] (1..64; default 8)    */
+  uint32_t num_store_queue_entries;            /* (1..64; default 8)                   */
+  uint32_t speculative_loads_enabled;          /* (default true)                       */
+  uint32_t multiple_outstanding_RFOs_enabled;  /* (default true)                       */
+} gg_iocoom_params;
+/* Per-tile statistics, [tile][GG_NUM_IOCOOM_STATS]: */
+enum {
+  GG_IOCOOM_INSTRUCTIONS = 0,        /* CoreModel::_instruction_count                        */
+  GG_IOCOOM_TIME_PS,                 /* _curr_time                                           */
+  GG_IOCOOM_MEMORY_STALL_PS,         /* _total_memory_stall_time                             */
+  GG_IOCOOM_EXECUTION_STALL_PS,      /* _total_execution_unit_stall_time                     */
+  GG_IOCOOM_SYNC_INSTRUCTIONS,       /* _total_sync_instructions                             */
+  GG_IOCOOM_SYNC_STALL_PS,           /* _total_sync_instruction_stall_time                   */
+  GG_IOCOOM_LOAD_QUEUE_STALL_PS,     /* IOCOOMCoreModel::_total_load_queue_stall_time        */
+  GG_IOCOOM_STORE_QUEUE_STALL_PS,    /* _total_store_queue_stall_time                        */
+  GG_IOCOOM_L1I_STALL_PS,            /* _total_l1icache_stall_time (0: no L1-I)              */
+  GG_IOCOOM_INTRA_L1D_STALL_PS,      /* _total_intra_ins_l1dcache_stall_time                 */
+  GG_IOCOOM_INTER_L1D_STALL_PS,      /* _total_inter_ins_l1dcache_stall_time                 */
+  GG_IOCOOM_INTRA_EXEC_STALL_PS,     /* _total_intra_ins_execution_unit_stall_time           */
+  GG_IOCOOM_INTER_EXEC_STALL_PS,     /* _total_inter_ins_execution_unit_stall_time           */
+  GG_IOCOOM_EXPLICIT_FENCES,         /* lfence + sfence + explicit mfence instructions       */
+  GG_IOCOOM_IMPLICIT_MFENCES,        /* atomic instructions                                  */
+  GG_IOCOOM_DATA_ACCESSES,           /* memory operands (Core's data memory accesses)        */
+  GG_IOCOOM_DATA_LATENCY_PS,         /* their summed latency (Core::incrTotalMemoryAccessLatency) */
+  GG_NUM_IOCOOM_STATS = 17
+};
+/* Runs IOCOOMCoreModel::handleInstruction over each tile's instructions
+ * (ins_dev, host ins_tile_offsets[num_tiles + 1]) and accesses (acc_addr_dev
+ * u64 address, acc_meta_dev u32 meta word — GG_META_WRITE or GG_META_BARRIER
+ * — acc_lat_dev u64 latency in ps or a barrier's stall, host
+ * acc_tile_offsets[num_tiles + 1]) from the model's constructor state.  A
+ * memory read operand met by a write access (or the reverse), a SYNC met by
+ * a non-BARRIER access, a register >= 512, a tile whose instructions leave
+ * accesses unconsumed or run out of them: the run's error, reported by
+ * gg_iocoom_get_stats (GG_ERR_STATE).  Asynchronous on stream.               */
+gg_status gg_iocoom_run(gg_ctx* ctx, const gg_iocoom_params* params, const gg_ins* ins_dev,
+                        const uint64_t* ins_tile_offsets, const uint64_t* acc_addr_dev, const uint32_t* acc_meta_dev,
+                        const uint64_t* acc_lat_dev, const uint64_t* acc_tile_offsets, void* stream);
+/* out: num_tiles * GG_NUM_IOCOOM_STATS (host).  Synchronizes.  GG_ERR_STATE
+ * if gg_iocoom_run has not run on the context or its streams disagreed.    */
+gg_status gg_iocoom_get_stats(gg_ctx* ctx, uint64_t* out);
 
 /* Device time (ms) of the most recent launch of a named kernel
  * ("cache_hist", "cache_scatter", "cache_replay", "cache_unshard",

@@ -266,6 +266,183 @@ void oracle_core_model(const uint32_t* meta, const uint64_t* access_out, const u
 }
 
 /* ======================================================================== */
+/* Core timing: IOCOOMCoreModel (common/tile/core/models/iocoom_core_model.cc) */
+/* ======================================================================== */
+enum { IO_INVALID_UNIT = 0, IO_LOAD_UNIT = 1, IO_STORE_UNIT = 2, IO_EXECUTION_UNIT = 3 };   /* .h:14-20 */
+#define IO_MAXQ 64
+typedef struct {                     /* LoadQueue (:162-223) / StoreQueue (:225-322) */
+  uint64_t sb[IO_MAXQ];              /* _scoreboard (deallocate times)           */
+  uint64_t addr[IO_MAXQ];            /* _addresses (store queue)                 */
+  uint32_t n, idx, flag;             /* _num_entries, _allocate_idx, speculative / multiple RFOs */
+} o_ioq;
+typedef struct {
+  uint64_t sb[GG_IOCOOM_NUM_REGISTERS];      /* _register_scoreboard             */
+  uint8_t dep[GG_IOCOOM_NUM_REGISTERS];      /* _register_dependency_list        */
+  o_ioq lq, sq;
+  uint64_t one;                              /* _ONE_CYCLE                        */
+  uint64_t st[GG_NUM_IOCOOM_STATS];
+} o_iocoom;
+
+static inline uint64_t o_max(uint64_t a, uint64_t b) { return a > b ? a : b; }
+
+/* LoadQueue::execute (:182-208): returns allocate time, *completion */
+static uint64_t o_lq_execute(o_iocoom* c, uint64_t schedule, uint64_t lat, uint64_t* completion)
+{
+  o_ioq* q = &c->lq;
+  const uint64_t allocate = o_max(q->sb[q->idx], schedule);
+  const uint32_t last = (q->idx + q->n - 1) % q->n;
+  uint64_t dealloc;
+  if (q->flag) {                                   /* speculative loads */
+    *completion = allocate + lat;
+    dealloc = o_max(*completion, q->sb[last] + c->one);
+  } else {
+    *completion = o_max(q->sb[last], schedule) + lat;
+    dealloc = *completion;
+  }
+  q->sb[q->idx] = dealloc;
+  q->idx = (q->idx + 1) % q->n;
+  return allocate;
+}
+/* StoreQueue::isAddressAvailable (:296-309): every entry, never-used ones included */
+static int o_sq_available(const o_iocoom* c, uint64_t schedule, uint64_t a)
+{
+  for (uint32_t i = 0; i < c->sq.n; ++i)
+    if (c->sq.addr[i] == a && c->sq.sb[i] >= schedule) return 1;
+  return 0;
+}
+/* executeLoad (:140-153) */
+static uint64_t o_io_load(o_iocoom* c, uint64_t schedule, uint64_t a, uint64_t latency, uint64_t* completion)
+{
+  const uint64_t lat = latency + c->one;
+  if (o_sq_available(c, schedule, a)) { *completion = schedule + c->one; return schedule; }
+  return o_lq_execute(c, schedule, lat, completion);
+}
+/* executeStore (:155-165) + StoreQueue::execute (:250-284) */
+static uint64_t o_io_store(o_iocoom* c, uint64_t schedule, uint64_t a, uint64_t latency)
+{
+  const uint64_t lat = latency + c->one;
+  const uint64_t last_load = c->lq.sb[(c->lq.idx + c->lq.n - 1) % c->lq.n];   /* getLastDeallocateTime */
+  o_ioq* q = &c->sq;
+  const uint64_t allocate = o_max(q->sb[q->idx], schedule);
+  const uint32_t last = (q->idx + q->n - 1) % q->n;
+  const uint64_t last_store = q->sb[last];
+  uint64_t dealloc;
+  if (q->flag) dealloc = o_max(o_max(allocate + lat, last_store + c->one), last_load);   /* multiple RFOs */
+  else dealloc = o_max(o_max(schedule, last_store), last_load) + lat;
+  q->sb[q->idx] = dealloc;
+  q->addr[q->idx] = a;
+  q->idx = (q->idx + 1) % q->n;
+  return allocate;
+}
+
+/* IOCOOMCoreModel::handleInstruction (iocoom_core_model.cc:66-227) for one
+ * gg_ins; its memory operands take the tile's next accesses (*k).  No L1-I:
+ * modelICache contributes 0 (:78-81).  Returns 0, or -1 when the streams
+ * disagree (the reference's LOG_ASSERT_ERRORs at :93-118,:129,:175).      */
+static int o_io_handle(o_iocoom* c, uint64_t* curr, const gg_ins* in, const uint64_t* addr, const uint32_t* meta,
+                       const uint64_t* lat, uint64_t* k, uint64_t kend, double f)
+{
+  uint64_t* st = c->st;
+  st[GG_IOCOOM_INSTRUCTIONS]++;                                       /* :72 */
+  if (in->regs & GG_INS_SYNC) {                                       /* dynamic (:74-79) */
+    if (*k >= kend || meta[*k] != GG_META_BARRIER) return -1;
+    const uint64_t stall = lat[(*k)++];
+    if (!stall) { st[GG_IOCOOM_INSTRUCTIONS]--; return 0; }           /* released without a stall: no instruction */
+    *curr += stall;
+    st[GG_IOCOOM_SYNC_INSTRUCTIONS]++;                                /* core_model.cc:237-250 */
+    st[GG_IOCOOM_SYNC_STALL_PS] += stall;
+    return 0;
+  }
+  const uint64_t cost = lat_to_ps(in->cost, f);                       /* getCost (:70) */
+  const uint64_t ready = *curr;                                       /* instruction_ready (:82-87) */
+  const uint32_t nr = in->regs & 7u, nw = (in->regs >> 3) & 7u;
+  if (nr + nw > 6) return -1;
+  uint64_t rl = ready, re = ready;                                    /* :100-125 */
+  for (uint32_t i = 0; i < nr; ++i) {
+    const uint32_t r = in->reg[i];
+    if (r >= GG_IOCOOM_NUM_REGISTERS) return -1;
+    if (c->dep[r] == IO_LOAD_UNIT) rl = o_max(rl, c->sb[r]);
+    else if (c->dep[r] == IO_EXECUTION_UNIT) re = o_max(re, c->sb[r]);
+    else if (c->sb[r] > ready) return -1;
+  }
+  const uint64_t rr = o_max(rl, re);                                  /* :128-129 */
+  uint64_t lqr = rr, rmr = rr;                                        /* :133-152 */
+  for (uint32_t i = 0; i < (in->ops & 3u); ++i) {
+    if (*k >= kend || meta[*k] == GG_META_BARRIER || (meta[*k] & GG_META_WRITE)) return -1;
+    uint64_t comp;
+    const uint64_t alloc = o_io_load(c, rr, addr[*k], lat[*k], &comp);
+    st[GG_IOCOOM_DATA_ACCESSES]++; st[GG_IOCOOM_DATA_LATENCY_PS] += lat[*k];
+    ++*k;
+    lqr = o_max(lqr, alloc);
+    rmr = o_max(rmr, comp);
+  }
+  const uint64_t wor = rmr + cost;                                    /* :158-166 */
+  const int smov = (in->ops & GG_INS_SIMPLE_MOV_LOAD) != 0;
+  for (uint32_t i = 0; i < nw; ++i) {                                 /* :172-184 */
+    const uint32_t r = in->reg[nr + i];
+    if (r >= GG_IOCOOM_NUM_REGISTERS) return -1;
+    c->sb[r] = wor;
+    c->dep[r] = smov ? IO_LOAD_UNIT : IO_EXECUTION_UNIT;
+  }
+  uint64_t sqr = wor;                                                 /* :186-201 */
+  const uint32_t nwm = (in->ops >> 2) & 3u;
+  for (uint32_t i = 0; i < nwm; ++i) {
+    if (*k >= kend || meta[*k] == GG_META_BARRIER || !(meta[*k] & GG_META_WRITE)) return -1;
+    const uint64_t alloc = o_io_store(c, wor, addr[*k], lat[*k]);
+    st[GG_IOCOOM_DATA_ACCESSES]++; st[GG_IOCOOM_DATA_LATENCY_PS] += lat[*k];
+    ++*k;
+    sqr = o_max(sqr, alloc);
+  }
+  uint64_t mem = 0, ex = 0;                                           /* :209-252 */
+  ex += re - ready;                       st[GG_IOCOOM_INTER_EXEC_STALL_PS] += re - ready;
+  mem += rr - re;                         st[GG_IOCOOM_INTER_L1D_STALL_PS] += rr - re;
+  mem += lqr - rr;                        st[GG_IOCOOM_LOAD_QUEUE_STALL_PS] += lqr - rr;
+  *curr = lqr;
+  if (!smov) {
+    mem += rmr - lqr;                     st[GG_IOCOOM_INTRA_L1D_STALL_PS] += rmr - lqr;
+    *curr = rmr;
+    if (nwm > 0) {
+      ex += wor - rmr;                    st[GG_IOCOOM_INTRA_EXEC_STALL_PS] += wor - rmr;
+      mem += sqr - wor;                   st[GG_IOCOOM_STORE_QUEUE_STALL_PS] += sqr - wor;
+      *curr = sqr;
+    }
+  }
+  if (in->ops & GG_INS_ATOMIC) st[GG_IOCOOM_IMPLICIT_MFENCES]++;      /* updateMemoryFenceCounters (core_model.cc:221-235) */
+  if (in->ops >> GG_INS_FENCE_SHIFT) st[GG_IOCOOM_EXPLICIT_FENCES]++;
+  st[GG_IOCOOM_MEMORY_STALL_PS] += mem;                               /* core_model.cc:260-264 */
+  st[GG_IOCOOM_EXECUTION_STALL_PS] += ex;
+  return 0;
+}
+
+int oracle_iocoom(const gg_iocoom_params* p, const gg_ins* ins, const uint64_t* ins_offsets, const uint64_t* addr,
+                  const uint32_t* meta, const uint64_t* lat, const uint64_t* acc_offsets, uint32_t tiles,
+                  double frequency_ghz, uint64_t* stats)
+{
+  if (!p->num_load_queue_entries || p->num_load_queue_entries > IO_MAXQ || !p->num_store_queue_entries ||
+      p->num_store_queue_entries > IO_MAXQ)
+    return -1;
+  o_iocoom* c = (o_iocoom*)malloc(sizeof(o_iocoom));
+  if (!c) return -1;
+  int bad = 0;
+  for (uint32_t t = 0; t < tiles; ++t) {
+    memset(c, 0, sizeof *c);                                          /* constructor (:10-45) */
+    c->lq.n = p->num_load_queue_entries; c->lq.flag = p->speculative_loads_enabled != 0;
+    c->sq.n = p->num_store_queue_entries; c->sq.flag = p->multiple_outstanding_RFOs_enabled != 0;
+    for (uint32_t i = 0; i < IO_MAXQ; ++i) c->sq.addr[i] = ~0ull;     /* INVALID_ADDRESS (fixed_types.h:36) */
+    c->one = lat_to_ps(1, frequency_ghz);
+    uint64_t curr = 0, k = acc_offsets[t];
+    for (uint64_t i = ins_offsets[t]; i < ins_offsets[t + 1] && !bad; ++i)
+      bad = o_io_handle(c, &curr, &ins[i], addr, meta, lat, &k, acc_offsets[t + 1], frequency_ghz) != 0;
+    if (k != acc_offsets[t + 1]) bad = 1;
+    c->st[GG_IOCOOM_TIME_PS] = curr;
+    memcpy(stats + (size_t)t * GG_NUM_IOCOOM_STATS, c->st, sizeof c->st);
+    if (bad) break;
+  }
+  free(c);
+  return bad ? -1 : 0;
+}
+
+/* ======================================================================== */
 /* Cache (common/tile/memory_subsystem/cache/)                               */
 /* ======================================================================== */
 #define O_INVALID_TAG (~0ull)                        /* cache_line_info.h:21-22 */

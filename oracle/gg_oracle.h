@@ -133,6 +133,13 @@ void oracle_combine_accesses(const uint64_t* line_out, const uint64_t* first, ui
  * gg_oracle.c.  stats: [tiles][GG_NUM_CORE_STATS].                          */
 void oracle_core_model(const uint32_t* meta, const uint64_t* access_out, const uint64_t* tile_offsets,
                        uint32_t tiles, double frequency_ghz, uint64_t* stats);
+/* The iocoom core model over instruction and access streams (IOCOOMCoreModel::
+ * handleInstruction, iocoom_core_model.cc:66-322; the streams of
+ * gg_iocoom_run); stats: [tiles][GG_NUM_IOCOOM_STATS].  Returns -1 when the
+ * streams disagree (stats of the tiles before and including the bad one).   */
+int oracle_iocoom(const gg_iocoom_params* p, const gg_ins* ins, const uint64_t* ins_offsets, const uint64_t* addr,
+                  const uint32_t* meta, const uint64_t* lat, const uint64_t* acc_offsets, uint32_t tiles,
+                  double frequency_ghz, uint64_t* stats);
 
 #ifdef __cplusplus
 }

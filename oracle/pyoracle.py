@@ -76,6 +76,8 @@ def lib():
         L.oracle_combine_accesses.argtypes = [_u64p, _u64p, ctypes.c_uint64, _u64p, _u32p]
         L.oracle_core_model.argtypes = [_u32p, _u64p, _u64p, ctypes.c_uint32, ctypes.c_double, _u64p]
         L.oracle_core_model.restype = None
+        L.oracle_iocoom.argtypes = [vp, vp, _u64p, _u64p, _u32p, _u64p, _u64p, ctypes.c_uint32, ctypes.c_double, _u64p]
+        L.oracle_iocoom.restype = ctypes.c_int
         L.oracle_gen_hotspot.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u64p, _u32p]
         L.oracle_gen_stress.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
@@ -426,6 +428,23 @@ def core_model(meta, access_out, tile_offsets, frequency_ghz=1.0):
     lib().oracle_core_model(np.ascontiguousarray(meta, np.uint32), np.ascontiguousarray(access_out, np.uint64), offs,
                             T, float(frequency_ghz), out)
     return out[:T * 8].reshape(T, 8)
+
+
+def iocoom(params, ins, ins_offsets, addr, meta, lat, acc_offsets, frequency_ghz=1.0):
+    """[tiles][GG_NUM_IOCOOM_STATS] of the iocoom core model (oracle_iocoom);
+    raises ValueError when the instruction and access streams disagree."""
+    from graphite_amd.config import INS_DTYPE, NUM_IOCOOM_STATS
+    ins = np.ascontiguousarray(ins, INS_DTYPE)
+    io = np.ascontiguousarray(ins_offsets, np.uint64)
+    ao = np.ascontiguousarray(acc_offsets, np.uint64)
+    T = len(io) - 1
+    out = np.zeros(max(T, 1) * NUM_IOCOOM_STATS, np.uint64)
+    r = lib().oracle_iocoom(ctypes.byref(params), ins.ctypes.data_as(ctypes.c_void_p), io,
+                            np.ascontiguousarray(addr, np.uint64), np.ascontiguousarray(meta, np.uint32),
+                            np.ascontiguousarray(lat, np.uint64), ao, T, float(frequency_ghz), out)
+    if r:
+        raise ValueError("oracle_iocoom: the instruction and access streams disagree")
+    return out[:T * NUM_IOCOOM_STATS].reshape(T, NUM_IOCOOM_STATS)
 
 
 def split_lines(addr, size, line=64):

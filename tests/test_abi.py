@@ -23,7 +23,7 @@ def test_library_exports_every_symbol():
     lib = ctypes.CDLL(B.LIB_PATH)
     for name in declared_symbols():
         assert hasattr(lib, name), name
-    assert B.load().gg_abi_version() == 9
+    assert B.load().gg_abi_version() == 10
 
 
 def test_config_default_matches_python_mirror():
