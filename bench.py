@@ -134,7 +134,7 @@ def parse():
                    help="skip the extra instrumented run (for an external rocprofv3 trace of the timed runs alone)")
     p.add_argument("--sections",
                    default="coherent_long,exchange,hop_counter,hotspot256,stress,fft,private,private_16way,noc,"
-                           "core_model",
+                           "core_model,iocoom",
                    help="extra sections at N = 1 (comma list; '' = none)")
     p.add_argument("--hc-per-tile", type=int, default=1024, help="hop_counter section: accesses per tile")
     p.add_argument("--h256-per-tile", type=int, default=1024, help="hotspot256 section (configs[2]): accesses per tile")
@@ -148,6 +148,8 @@ def parse():
     p.add_argument("--noc-tiles", type=int, default=1024)
     p.add_argument("--core-tiles", type=int, default=1024, help="core_model section: tiles of the synthetic trace")
     p.add_argument("--core-per-tile", type=int, default=1 << 18, help="core_model section: records per tile")
+    p.add_argument("--iocoom-tiles", type=int, default=1024, help="iocoom section: tiles")
+    p.add_argument("--iocoom-per-tile", type=int, default=16384, help="iocoom section: instructions per tile")
     p.add_argument("--fft-m", type=int, default=20,
                    help="configs[0] section: the reference's FFT -p16 -m<m> (configs[0]: m=20; the trace build() "
                         "captures; m=14 is committed)")
@@ -738,6 +740,61 @@ def core_model_section(args, dev):
     return res
 
 
+def iocoom_section(args, dev):
+    """§8f-4 core timing, the iocoom model: gg_iocoom_run over synthetic
+    instruction streams (random register operands from 64 registers, 0-2
+    memory reads and 0-1 writes, simple-mov loads, SyncInstructions) of
+    args.iocoom_tiles x args.iocoom_per_tile instructions at carbon_sim.cfg's
+    [core/iocoom] defaults; HIP-event timed launch; every tile checked against
+    the oracle, whose time on 8 tiles is the 1-thread CPU baseline.  One wave
+    per tile walks its instructions serially (register scoreboard, load
+    queue, store buffer): the bound is that chain, not HBM (16 B per
+    instruction + 20 B per access streamed)."""
+    import torch
+    from graphite_amd import config as C
+    from graphite_amd import backend as B
+    from oracle import pyoracle as po
+    T, N = args.iocoom_tiles, args.iocoom_per_tile
+    ins, io, addr, meta, lat, ao = B.gen_iocoom_streams(T, N, 11, regs=64)
+    p = C.IocoomParams()
+    be = B.Backend(C.default_config(T))
+    be.set_timing(True)
+    d_ins = torch.from_numpy(ins.view(np.uint8)).to(dev)
+    d_addr = torch.from_numpy(addr.view(np.int64)).to(dev)
+    d_meta = torch.from_numpy(meta.view(np.int32)).to(dev)
+    d_lat = torch.from_numpy(lat.view(np.int64)).to(dev)
+    stream = torch.cuda.current_stream(dev)
+    times = []
+    for it in range(3):
+        torch.cuda.synchronize()
+        be.iocoom_run(p, d_ins, io, d_addr, d_meta, d_lat, ao, stream)
+        torch.cuda.synchronize()
+        times.append(be.kernel_time_ms("iocoom"))
+    kms = min(times[1:])
+    st = be.iocoom_stats()
+    c0 = time.perf_counter()
+    ref = po.iocoom(p, ins, io, addr, meta, lat, ao)
+    cdt = (time.perf_counter() - c0) * min(8, T) / T
+    ok = bool(np.array_equal(st, ref))
+    nbytes = 16 * len(ins) + 20 * len(addr)
+    gbs = nbytes / (kms / 1e3) / 1e9
+    res = {"workload": "gg_iocoom_run: synthetic %d tiles x %d instructions (%d accesses), [core/iocoom] defaults"
+                       % (T, N, len(addr)),
+           "value": len(ins) / (kms / 1e3), "unit": "instructions/s", "kernel_ms": kms,
+           "roofline": {"bound": "hbm", "kernel": "k_iocoom", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": gbs / HBM_PEAK_GBS, "note": "per-tile serial chain; bytes = 16/instruction + 20/access"},
+           "bit_exact_checked": ok,
+           "cpu_baseline": {"value": min(8, T) * N / cdt, "unit": "instructions/s", "cores": 1, "kind": "port",
+                            "sample": "oracle_iocoom -O3, 1 thread, all %d tiles timed, scaled to 8 tiles: %.2f s"
+                                      % (T, cdt)}}
+    if not ok:
+        print("bench.py: IOCOOM BIT-EXACT CHECK FAILED", file=sys.stderr)
+    be.close()
+    del d_ins, d_addr, d_meta, d_lat
+    torch.cuda.empty_cache()
+    return res
+
+
 def cpu_baseline(tiles, per_tile, threads):
     """Oracle (oracle/gg_oracle.c, -O3) on a bounded sample: `tiles` tile
     replays (fresh cache state each) cycling over 16 pre-generated tiles of
@@ -971,6 +1028,8 @@ def main():
                 r = private16_section(args, dev)
             elif name == "core_model" and args.core_per_tile:
                 r = core_model_section(args, dev)
+            elif name == "iocoom" and args.iocoom_per_tile:
+                r = iocoom_section(args, dev)
             else:
                 continue
         except Exception as e:            # a section failing must not hide the headline

@@ -527,6 +527,48 @@ def combine_accesses(line_out, first, stream=None):
     return lat, miss
 
 
+def gen_iocoom_streams(T, per_tile, seed, regs=24, addrs=24, p_sync=0.01, max_lat=300000):
+    """Tile-major instructions (random read / write registers from `regs`
+    registers, 0-2 memory reads and 0-1 memory writes, simple-mov loads,
+    atomics, fences, SyncInstructions) and the access stream their memory
+    operands consume in order (addresses from `addrs` per tile, so loads hit
+    the store buffer; 0xFFFFFFFF records with and without a stall)."""
+    from . import config as C_
+    rng = np.random.default_rng(seed)
+    n = T * per_tile
+    ins = np.zeros(n, C_.INS_DTYPE)
+    sync = rng.random(n) < p_sync
+    nr = rng.integers(0, 4, n)
+    nw = np.minimum(rng.integers(0, 3, n), 6 - nr)
+    nrd = rng.choice(3, n, p=[0.55, 0.35, 0.10])
+    nwm = (rng.random(n) < 0.25).astype(np.int64)
+    smov = (nrd == 1) & (nwm == 0) & (nw == 1) & (rng.random(n) < 0.6)
+    fence = np.where(rng.random(n) < 0.03, rng.integers(1, 4, n), 0)
+    atomic = rng.random(n) < 0.02
+    nr[sync] = 0; nw[sync] = 0; nrd[sync] = 0; nwm[sync] = 0; smov[sync] = False; fence[sync] = 0; atomic[sync] = False
+    ins["cost"] = rng.choice(np.array([0, 1, 1, 1, 3, 5, 6, 18]), n)
+    ins["ops"] = (nrd | (nwm << 2) | np.where(smov, C_.INS_SIMPLE_MOV_LOAD, 0) |
+                  np.where(atomic, C_.INS_ATOMIC, 0) | (fence << C_.INS_FENCE_SHIFT)).astype(np.uint8)
+    ins["regs"] = (nr | (nw << 3) | np.where(sync, C_.INS_SYNC, 0)).astype(np.uint8)
+    ins["reg"] = rng.integers(0, regs, (n, 6)).astype(np.uint16)
+    ins_offs = np.arange(T + 1, dtype=np.uint64) * np.uint64(per_tile)
+    cnt = np.where(sync, 1, nrd + nwm)
+    tot = int(cnt.sum())
+    owner = np.repeat(np.arange(n), cnt)
+    pos = np.arange(tot) - np.repeat(np.cumsum(cnt) - cnt, cnt)
+    is_bar = sync[owner]
+    is_wr = ~is_bar & (pos >= nrd[owner])
+    meta = np.where(is_bar, np.uint32(0xFFFFFFFF), np.where(is_wr, np.uint32(1), np.uint32(0))).astype(np.uint32)
+    meta[~is_bar] |= (rng.integers(0, 8, int((~is_bar).sum())) << 1).astype(np.uint32)   # gap bits: ignored
+    tile = owner // per_tile
+    addr = (tile.astype(np.uint64) << np.uint64(20)) + rng.integers(0, addrs, tot).astype(np.uint64) * np.uint64(8)
+    lat = rng.integers(1000, max_lat, tot).astype(np.uint64)
+    lat[is_bar & (rng.random(tot) < 0.3)] = 0
+    per = np.bincount(tile, minlength=T)
+    acc_offs = np.concatenate([[0], np.cumsum(per)]).astype(np.uint64)
+    return ins, ins_offs, addr, meta, lat, acc_offs
+
+
 class CoherentEngine:
     """A Backend context behind the engine surface of graphite_amd.coherent.run
     (one rank: the shards [cfg.shard_begin, cfg.shard_end))."""

@@ -1625,8 +1625,11 @@ __global__ __launch_bounds__((NCW + 1) * GG_WAVE) void k_cache_stream(gg_cache_s
       uint64_t ev = 0;
       const uint32_t rv = nostep ? kl : step(kl, (uint32_t)(key >> 32), &ev);
       st32(&headp[u], hn);
-      if (res_out) res_out[idx] = rv;
-      if (EV) ev_out[idx] = ev;
+      // a record index outside the tile is a broken hand-off: flagged, never stored
+      const bool inr = idx < n;
+      errv |= inr ? 0u : GG_DERR_CAP;
+      if (res_out && inr) res_out[idx] = rv;
+      if (EV && inr) ev_out[idx] = ev;
       count(rv, kl & 1u);
     }
     h = hn;

@@ -5,7 +5,7 @@
 # under its own time limit; the first failure ends the script.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
-OUT=gpurun_out/r05/final
+OUT=${OUT:-gpurun_out/r05/final}
 mkdir -p $OUT
 if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -30 $OUT/pytest_gpu.log; exit 1; }
