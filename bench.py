@@ -746,7 +746,7 @@ def iocoom_section(args, dev):
     memory reads and 0-1 writes, simple-mov loads, SyncInstructions) of
     args.iocoom_tiles x args.iocoom_per_tile instructions at carbon_sim.cfg's
     [core/iocoom] defaults; HIP-event timed launch; every tile checked against
-    the oracle, whose time on 8 tiles is the 1-thread CPU baseline.  One wave
+    the oracle, whose time on them is the 1-thread CPU baseline.  One wave
     per tile walks its instructions serially (register scoreboard, load
     queue, store buffer): the bound is that chain, not HBM (16 B per
     instruction + 20 B per access streamed)."""
@@ -774,7 +774,7 @@ def iocoom_section(args, dev):
     st = be.iocoom_stats()
     c0 = time.perf_counter()
     ref = po.iocoom(p, ins, io, addr, meta, lat, ao)
-    cdt = (time.perf_counter() - c0) * min(8, T) / T
+    cdt = time.perf_counter() - c0
     ok = bool(np.array_equal(st, ref))
     nbytes = 16 * len(ins) + 20 * len(addr)
     gbs = nbytes / (kms / 1e3) / 1e9
@@ -784,9 +784,9 @@ def iocoom_section(args, dev):
            "roofline": {"bound": "hbm", "kernel": "k_iocoom", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": gbs / HBM_PEAK_GBS, "note": "per-tile serial chain; bytes = 16/instruction + 20/access"},
            "bit_exact_checked": ok,
-           "cpu_baseline": {"value": min(8, T) * N / cdt, "unit": "instructions/s", "cores": 1, "kind": "port",
-                            "sample": "oracle_iocoom -O3, 1 thread, all %d tiles timed, scaled to 8 tiles: %.2f s"
-                                      % (T, cdt)}}
+           "cpu_baseline": {"value": len(ins) / cdt, "unit": "instructions/s", "cores": 1, "kind": "port",
+                            "sample": "the same %d tiles x %d instructions, oracle_iocoom -O3, 1 thread, %.2f s"
+                                      % (T, N, cdt)}}
     if not ok:
         print("bench.py: IOCOOM BIT-EXACT CHECK FAILED", file=sys.stderr)
     be.close()
