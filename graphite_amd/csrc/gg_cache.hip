@@ -1309,6 +1309,10 @@ __global__ __launch_bounds__((NCW + 1) * GG_WAVE) void k_cache_stream(gg_cache_s
     const uint64_t* ap = addr + base;
     const uint32_t* mp = meta + base;
     const uint64_t lt_mask = (1ull << lane) - 1;
+    // test knob (GG_STREAM_BAD_INDEX): the tile's first record is handed off
+    // with an index past the tile's end, as a broken hand-off would; the
+    // consumer must flag it (GG_DERR_CAP) and store nothing
+    const uint32_t bad_idx = (dbg && dbg[6] == 1) ? n : 0u;
     uint64_t pa[K], na[K], qa[K];
     uint32_t pm[K], nm[K], qm[K];
     uint32_t bad = 0;
@@ -1335,7 +1339,7 @@ __global__ __launch_bounds__((NCW + 1) * GG_WAVE) void k_cache_stream(gg_cache_s
         bad |= (valid && pm[k] == GG_META_BARRIER) ? 2u : 0u;      // coherent-mode records only
         const uint64_t line = pa[k] >> g.log_line;
         set[k] = valid ? (uint32_t)line & (U1 - 1) : U1;             // U1 = no record
-        key[k] = ((uint64_t)(uint32_t)(line >> g.log_l2) << 32) | (j << (1 + log_s2)) |
+        key[k] = ((uint64_t)(uint32_t)(line >> g.log_l2) << 32) | ((j + (j == 0 ? bad_idx : 0u)) << (1 + log_s2)) |
                  ((((uint32_t)line >> g.log_u1) & (S2 - 1)) << 1) | (pm[k] & GG_META_WRITE);
       }
 #pragma unroll
@@ -2003,13 +2007,18 @@ gg_status gg_cache_run_batch(gg_ctx* ctx, const gg_trace* tr, uint32_t* result, 
       stream_fn fn = evicted ? sk->ev : sk->plain;
       GG_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       gg_timer_begin(ctx, "cache_stream", s);
-      // GG_STREAM_DEBUG=1: hand-off counters of the launch on stderr (diagnostics)
+      // GG_STREAM_DEBUG=1: hand-off counters of the launch on stderr (diagnostics);
+      // GG_STREAM_BAD_INDEX=1 (test knob, read per batch): a broken hand-off
+      // of each tile's first record (the consumer's guard must flag it)
       static const int dbg_on = getenv("GG_STREAM_DEBUG") ? atoi(getenv("GG_STREAM_DEBUG")) : 0;
+      const char* bi = getenv("GG_STREAM_BAD_INDEX");
+      const bool bad_index = bi && atoi(bi) == 1;
       unsigned long long* dbg = nullptr;
-      if (dbg_on) {
+      if (dbg_on || bad_index) {
         GG_HIP(hipMalloc((void**)&dbg, 8 * sizeof(unsigned long long)));
         GG_HIP(hipMemsetAsync(dbg, 0, 8 * sizeof(unsigned long long), s));
         if (dbg_on == 2) GG_HIP(hipMemsetAsync(dbg + 7, 1, 1, s));   // GG_STREAM_DEBUG=2: skip the cache step (builds with -DGG_STREAM_NOSTEP)
+        if (bad_index) GG_HIP(hipMemsetAsync(dbg + 6, 1, 1, s));
       }
       hipLaunchKernelGGL(fn, dim3(g.tiles), dim3((sk->ncw + 1) * GG_WAVE), lds, s, ctx->cs, g, tr->addr_dev,
                          tr->meta_dev, (const uint64_t*)ctx->tile_off_dev, result, evicted,
@@ -2021,7 +2030,7 @@ gg_status gg_cache_run_batch(gg_ctx* ctx, const gg_trace* tr, uint32_t* result, 
         GG_HIP(hipMemcpyAsync(h, dbg, sizeof(h), hipMemcpyDeviceToHost, s));
         GG_HIP(hipStreamSynchronize(s));
         hipFree(dbg);
-        fprintf(stderr, "[gg_stream] batches %llu slow %llu producer-spins %llu | consumer wave-iters %llu "
+        if (dbg_on) fprintf(stderr, "[gg_stream] batches %llu slow %llu producer-spins %llu | consumer wave-iters %llu "
                 "idle-sleeps %llu records %llu (lane util %.3f)\n", h[0], h[1], h[2], h[3], h[4], h[5],
                 h[3] ? (double)h[5] / (64.0 * h[3]) : 0.0);
       }

@@ -219,6 +219,7 @@ struct gg_coh_state {
   uint32_t wtx = 64, wty = 64;          // threads of an X / Y walker workgroup
   bool persist_lc = false;
   bool begun = false;
+  uint64_t gen = 0;                     // gg_coherent_begin count: a round in progress belongs to one run
   bool has_barrier = false;             // the bound trace holds BARRIER records (gg_coherent_run only)
   uint32_t* bar_flag = nullptr;
   // live kernel timing (gg_set_timing): an event pair around every
@@ -674,6 +675,7 @@ gg_status gg_coherent_begin(gg_ctx* ctx, const gg_trace* tr, uint64_t* access_ou
   GG_HIP(hipMemcpyAsync(C->Pd, &C->P, sizeof(CP), hipMemcpyHostToDevice, s));
   GG_HIP(hipMemcpyAsync(C->Sd, &C->S, sizeof(CS), hipMemcpyHostToDevice, s));
   C->n_records = tr->num_records;
+  ++C->gen;
   for (int k = 0; k < 5; ++k) { C->ksum[k] = 0; C->kcnt[k] = 0; C->nlaunch[k] = 0; }
   C->tused = 0;
   GG_HIP(hipMemcpyAsync(C->offs_dev, tr->tile_offsets, sizeof(uint64_t) * (P.T + 1), hipMemcpyHostToDevice, s));
@@ -853,6 +855,7 @@ gg_status gg_coh_import_slots(gg_ctx* ctx, const gg_cmsg* slots, uint32_t world,
 }
 
 gg_status gg_coh_check(gg_ctx* ctx) { return coh_check(ctx); }
+uint64_t gg_coh_generation(gg_ctx* ctx) { return ctx->coh ? ctx->coh->gen : 0; }
 
 gg_status gg_coherent_export(gg_ctx* ctx, gg_cmsg* out_dev, uint64_t cap, uint64_t* per_shard_counts)
 {

@@ -164,3 +164,4 @@ constexpr int kRoundWords = 8;          // a rank's round status words (RW_* in 
 gg_status gg_coh_import_slots(gg_ctx* ctx, const gg_cmsg* slots, uint32_t world, uint64_t region, uint64_t lo,
                               uint64_t hi, bool first, const uint64_t* skip_if_dev);
 gg_status gg_coh_check(gg_ctx* ctx);
+uint64_t  gg_coh_generation(gg_ctx* ctx);    // bumped by every gg_coherent_begin (0: none yet)

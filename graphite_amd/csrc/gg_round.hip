@@ -22,7 +22,13 @@
 // posts every send / receive and the all-gather (with its error flag in its
 // status words), the commit and imports are skipped on the device when any
 // rank's flag is set, and every rank returns the error together — no peer is
-// left blocked inside RCCL.
+// left blocked inside RCCL.  A failure found after a round's collective (the
+// commit / import of unpack, the sized import of finish) cannot reach the
+// words its peers already hold: it is kept as the rank's pending failure, the
+// rank decides this round like its peers, and its next pack turns it into the
+// error flag of its words — every rank returns it from that round's unpack.
+// Only when this round ends the run (no peer will post another round) does
+// the rank return the pending failure alone.
 #include "gg_internal.h"
 
 #include <rccl/rccl.h>
@@ -52,6 +58,10 @@ struct RoundBufs {
   uint32_t herr = 0;                                  // this rank's local failure (its error flag in the words)
   gg_status est = GG_OK;
   std::string emsg;
+  gg_status pend = GG_OK;                             // a failure after the collective: the next round's flag
+  std::string pmsg;
+  uint64_t gen = 0;                                   // the coherent run (gg_coh_generation) the round belongs to
+  uint32_t nunpack = 0, nfinish = 0;                  // unpack / finish calls of this run (test knobs)
   size_t dv_words() const { return (size_t)(1 + world) * kRoundWords + 2 * (size_t)world; }
 };
 
@@ -102,6 +112,27 @@ uint64_t slot_records(uint64_t region)
 
 RoundBufs* bufs_of(gg_ctx* ctx) { return static_cast<RoundBufs*>(gg_round_state(ctx)); }
 
+// test knob: GG_ROUND_FAIL_IMPORT / GG_ROUND_FAIL_FINISH = "rank,n" makes the
+// n-th (0-based) unpack / finish of this run on that rank fail after the
+// collective, as a failed commit or import would
+bool knob_fail(const char* name, uint32_t rank, uint32_t n)
+{
+  const char* e = getenv(name);
+  if (!e || !*e) return false;
+  char* c = nullptr;
+  const unsigned long r = strtoul(e, &c, 10);
+  if (!c || *c != ',') return false;
+  return r == rank && strtoul(c + 1, nullptr, 10) == n;
+}
+
+// a local failure after the collective: kept for the next round (the first one wins)
+void set_pending(RoundBufs* B, gg_status st, const std::string& msg)
+{
+  if (B->pend) return;
+  B->pend = st ? st : GG_ERR_STATE;
+  B->pmsg = msg;
+}
+
 void fill_io(const RoundBufs* B, gg_round_io* io)
 {
   io->send = B->send; io->recv = B->recv;
@@ -135,9 +166,18 @@ gg_status round_pack(gg_ctx* ctx, uint32_t W, uint32_t R, uint64_t q, gg_round_i
   RoundBufs* B = nullptr;
   if (gg_status st = bufs_for(ctx, B, (int)W, R, region)) return st;
   B->rank = R; B->per = per;
+  const uint64_t gen = gg_coh_generation(ctx);
+  if (B->gen != gen) {
+    // a new run (gg_coherent_begin): nothing of an abandoned round carries over
+    B->gen = gen; B->again = false; B->pend = GG_OK; B->pmsg.clear(); B->nunpack = 0; B->nfinish = 0;
+  }
   if (B->again && B->q == q) { B->k0 += B->nb; ++B->attempt; }
   else { B->k0 = 0; B->attempt = 0; B->herr = 0; B->est = GG_OK; B->emsg.clear(); }
   B->again = false; B->q = q;
+  if (B->pend) {                                       // the last round's failure becomes this round's flag
+    if (!B->herr) { B->herr = GG_DERR_STATE; B->est = B->pend; B->emsg = B->pmsg; }
+    B->pend = GG_OK; B->pmsg.clear();
+  }
   B->slot = slot_records(region);
   // the batch: the largest of the last four quanta's steps + 3, doubling on a
   // repeat.  A step past the quantum's end costs three empty launches (~8
@@ -178,7 +218,12 @@ gg_status round_decide(gg_ctx* ctx, RoundBufs* B, gg_round_io* io)
   const uint64_t qps = (uint64_t)ctx->cfg.quantum_ns * 1000ull;
   io->state = GG_ROUND_DONE;
   io->done = 0;
-  if (active == 0 && msgs == 0) { io->done = 1; io->next_q = q; return gg_coh_check(ctx); }
+  if (active == 0 && msgs == 0) {
+    io->done = 1; io->next_q = q;
+    // the run ends here on every rank: a pending failure has no next round
+    if (B->pend) { const gg_status p = B->pend; B->pend = GG_OK; return gg_fail(p, "%s", B->pmsg.c_str()); }
+    return gg_coh_check(ctx);
+  }
   if (msgs == 0 && blocked != 0) return gg_fail(GG_ERR_STATE, "coherent run deadlocked: tiles blocked with no message in flight");
   io->next_q = (msgs == 0) ? std::max<uint64_t>(q + 1, mn / qps) : q + 1;
   return GG_OK;
@@ -206,6 +251,11 @@ gg_status gg_round_unpack(gg_ctx* ctx, gg_round_io* io)
   // rank decides like the others and reports its own error on top
   gg_status lerr = gg_coh_round_import(ctx, B->q, B->send, B->recv, (uint32_t)W, B->rank, B->region, B->slot, dv_all, counts);
   std::string lmsg = lerr ? gg_last_error() : "";
+  if (!lerr && knob_fail("GG_ROUND_FAIL_IMPORT", B->rank, B->nunpack)) {
+    lerr = GG_ERR_STATE;
+    lmsg = "commit / import failed on rank " + std::to_string(B->rank) + " (GG_ROUND_FAIL_IMPORT)";
+  }
+  ++B->nunpack;
   GG_HIP(hipMemcpyAsync(B->host, dv_all, sizeof(uint64_t) * ((size_t)W * kRoundWords + 2 * (size_t)W),
                         hipMemcpyDeviceToHost, s));
   GG_HIP(hipStreamSynchronize(s));
@@ -218,11 +268,14 @@ gg_status gg_round_unpack(gg_ctx* ctx, gg_round_io* io)
   }
   if (err) {
     io->state = GG_ROUND_DONE;
+    B->again = false; B->pend = GG_OK; B->pmsg.clear();
     if (B->herr) return gg_fail(B->est ? B->est : GG_ERR_STATE, "%s", B->emsg.c_str());
     if (gg_status st = gg_coh_check(ctx)) return st;
     return gg_fail(GG_ERR_STATE, "quantum %llu failed on another rank", (unsigned long long)B->q);
   }
-  if (lerr) { io->state = GG_ROUND_DONE; return gg_fail(lerr, "%s", lmsg.c_str()); }
+  // a failure after the collective: this round is decided like the peers'
+  // (they hold clean words), the next round carries it to every rank
+  if (lerr) set_pending(B, lerr, lmsg);
   if (notdone) { B->again = true; io->state = GG_ROUND_AGAIN; return GG_OK; }   // some rank's quantum is still running
   B->steps_hist[B->hist_i++ & 3] = (uint32_t)std::max<uint64_t>(1, h[(size_t)B->rank * kRoundWords + 7]);
   if (mx > B->slot) {
@@ -244,9 +297,18 @@ gg_status gg_round_finish(gg_ctx* ctx, gg_round_io* io)
   RoundBufs* B = bufs_of(ctx);
   if (!B || !ctx->coh) return gg_fail(GG_ERR_INVALID, "gg_round_pack first");
   hipSetDevice(ctx->device);
-  if (gg_status st = gg_coh_import_slots(ctx, B->recv, (uint32_t)B->world, B->region, B->slot, B->region, false, nullptr))
-    return st;
-  GG_HIP(hipStreamSynchronize(ctx->last_stream));
+  // a failed import is this rank's alone (its peers decide from the same
+  // words and go on): pending, as in unpack
+  gg_status st = gg_coh_import_slots(ctx, B->recv, (uint32_t)B->world, B->region, B->slot, B->region, false, nullptr);
+  std::string msg = st ? gg_last_error() : "";
+  if (!st && knob_fail("GG_ROUND_FAIL_FINISH", B->rank, B->nfinish)) {
+    st = GG_ERR_STATE;
+    msg = "sized import failed on rank " + std::to_string(B->rank) + " (GG_ROUND_FAIL_FINISH)";
+  }
+  ++B->nfinish;
+  if (st) set_pending(B, st, msg);
+  if (hipError_t e = hipStreamSynchronize(ctx->last_stream))
+    set_pending(B, GG_ERR_STATE, std::string("hipStreamSynchronize: ") + hipGetErrorString(e));
   return round_decide(ctx, B, io);
 }
 

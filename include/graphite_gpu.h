@@ -538,7 +538,15 @@ gg_status gg_coherent_run_ranks(gg_ctx* ctx, void* nccl_comm, const gg_trace* tr
  *     1 + send_count[r]) of send slot r into rank r's receive slot `rank`,
  *     then gg_round_finish) or GG_ROUND_DONE (next_q / done as in
  *     gg_round_exchange).  Record 0 of a slot is a header whose addr is the
- *     slot's record count.                                                   */
+ *     slot's record count.
+ *   A failure unpack or finish meets after the transport (commit / import)
+ *   cannot reach the words the peers already hold: the rank decides that
+ *   round like its peers (GG_OK, same state) and its next pack raises its
+ *   error flag, so every rank's unpack of the next round returns the error
+ *   (the failing rank its own message).  If that round ended the run there
+ *   is no next round: the failing rank alone returns its error.  A new
+ *   gg_coherent_begin drops a round left in progress (after AGAIN or an
+ *   error): the next pack starts at step 0 of its quantum.                  */
 enum { GG_ROUND_WORDS = 8, GG_ROUND_DONE = 0, GG_ROUND_AGAIN = 1, GG_ROUND_OVERFLOW = 2 };
 typedef struct {
   gg_cmsg* send;                 /* device: [world][stride] records, the slots this rank sends */

@@ -201,3 +201,39 @@ def test_stream_idle_waves_alternating_bursts():
     be, res, _ = run_gpu(cfg, addr, meta, offs, torch, want_ev=False)
     np.testing.assert_array_equal(res, ref)
     np.testing.assert_array_equal(be.cache_counters(), oc.counters())
+
+
+def test_stream_broken_handoff_is_flagged_not_stored(monkeypatch):
+    """The streaming replay's hand-off guard (the r05 pm0 fault: a broken
+    hand-off named a record outside its tile and the consumer stored there):
+    with GG_STREAM_BAD_INDEX=1 the producer hands each tile's first record
+    over with an index one past the tile's end.  The consumer must flag it
+    (GG_DERR_CAP -> gg_cache_get_counters fails with the hand-off message),
+    store no result outside the batch, and every other record's result must
+    still equal the oracle's (CacheSet::find / insert order, cache_set.cc:57-103)."""
+    torch = torch_dev()
+    T, N = 4, 3000
+    addr, meta, offs = ragged_trace(T, 11, 12, N)
+    cfg = C.default_config(T, replay_kernel=0)
+    oc = po.OracleCache(cfg)
+    ref, _ = oc.run(addr, meta, offs, want_evicted=True)
+    n = int(offs[-1])
+    be = B.Backend(cfg)
+    a, m = to_dev(torch, addr, torch.int64), to_dev(torch, meta, torch.int32)
+    # the batch's results sit inside a larger buffer: a store past the batch would land in the guard words
+    guard = 4096
+    big = torch.full((n + guard,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    monkeypatch.setenv("GG_STREAM_BAD_INDEX", "1")
+    be.cache_access_batch(a, m, offs, big[:n], None)
+    torch.cuda.synchronize()
+    monkeypatch.delenv("GG_STREAM_BAD_INDEX")
+    with pytest.raises(B.GGError) as ei:
+        be.cache_counters()
+    assert "hand-off" in str(ei.value)
+    got = to_np(big, np.uint32)
+    assert np.all(got[n:] == np.uint32(0x5A5A5A5A))              # nothing stored past the batch
+    first = {int(offs[t]) for t in range(T) if offs[t + 1] > offs[t]}
+    rest = np.array([i for i in range(n) if i not in first], dtype=np.int64)
+    np.testing.assert_array_equal(got[rest], ref[rest])
+    for i in first:                                              # the flagged records' words were not written
+        assert got[i] == np.uint32(0x5A5A5A5A)

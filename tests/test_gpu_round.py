@@ -147,3 +147,158 @@ def test_round_halves_over_contexts_equal_one_context(W, net, mode, monkeypatch)
         assert stats["overflow"] > 0, stats
     if mode == "short_batch":
         assert stats["again"] > 0, stats
+
+
+def _round_loop(torch, bes, W, max_rounds=100000):
+    """pack / device-copy transport / unpack (/ finish) over the contexts until
+    the run ends or fails; returns (rounds, failure) where failure is None or
+    (round, [message per rank]) — every rank must fail in the same call, or
+    none."""
+    from graphite_amd import backend as B
+    hip = _hip()
+    rb = B.CMSG_RECORD_BYTES
+    q, rounds = 0, 0
+
+    def every(fn):
+        res = []
+        for r, be in enumerate(bes):
+            try:
+                fn(r, be)
+                res.append(None)
+            except B.GGError as e:
+                res.append(str(e))
+        failed = [x is not None for x in res]
+        assert all(failed) or not any(failed), res       # collective: all or none
+        return res if all(failed) else None
+
+    while rounds < max_rounds:
+        ios = [be.round_pack(W, r, q) for r, be in enumerate(bes)]
+        torch.cuda.synchronize()
+        for r in range(W):
+            for p in range(W):
+                if p != r:
+                    _copy(hip, ios[p].recv + r * ios[p].stride * rb, ios[r].send + p * ios[r].stride * rb,
+                          (ios[r].slot + 1) * rb)
+                _copy(hip, ios[p].words_all + r * B.ROUND_WORDS * 8, ios[r].words_own, B.ROUND_WORDS * 8)
+        torch.cuda.synchronize()
+        f = every(lambda r, be: be.round_unpack(ios[r]))
+        rounds += 1
+        if f:
+            return rounds, (rounds, f)
+        state = {io.state for io in ios}
+        assert len(state) == 1, state
+        state = state.pop()
+        if state == B.ROUND_AGAIN:
+            continue
+        if state == B.ROUND_OVERFLOW:
+            for r in range(W):
+                for p in range(W):
+                    n = ios[r].send_count[p]
+                    if p != r and n > ios[r].slot:
+                        off = 1 + ios[r].slot
+                        _copy(hip, ios[p].recv + (r * ios[p].stride + off) * rb,
+                              ios[r].send + (p * ios[r].stride + off) * rb, (n - ios[r].slot) * rb)
+            torch.cuda.synchronize()
+            f = every(lambda r, be: be.round_finish(ios[r]))
+            if f:
+                return rounds, (rounds, f)
+        assert len({(io.next_q, io.done) for io in ios}) == 1
+        if ios[0].done:
+            return rounds, None
+        q = ios[0].next_q
+    raise AssertionError("the run did not end")
+
+
+def _contexts(torch, W, K, T, net, a, m, o):
+    from graphite_amd import backend as B
+    from graphite_amd import coherent as CO
+    addr, meta = to_dev(torch, a, torch.int64), to_dev(torch, m, torch.int32)
+    bes, outs = [], []
+    for r in range(W):
+        k0, k1 = CO.shard_range(r, W, K)
+        be = B.Backend(C.default_config(T, num_shards=K, shard_begin=k0, shard_end=k1, net_model=net))
+        out = torch.zeros(len(a), dtype=torch.int64, device="cuda")
+        be.coherent_begin(addr, meta, o, out)
+        bes.append(be); outs.append(out)
+    return bes, outs, addr, meta
+
+
+@pytest.mark.parametrize("W", [2, 4])
+@pytest.mark.parametrize("where", ["import", "finish"])
+def test_round_failure_after_collective_is_collective(W, where, monkeypatch):
+    """A failure a rank finds after the round's collective (its commit /
+    import in unpack, or the sized import of finish) is kept as that rank's
+    pending failure: every rank decides the round alike, and in the NEXT
+    round every rank's unpack returns the error — no rank continues into a
+    round its peer will not post (lax_barrier_sync_server.cc:57-160: the
+    barrier releases all or none).  The failing rank reports its own message,
+    its peers 'failed on another rank'."""
+    torch = torch_dev()
+    from oracle import pyoracle as po
+    T, N, K = 64, 300, 8
+    net = C.NET_EMESH_HOP_BY_HOP
+    monkeypatch.delenv("GG_ROUND_BATCH0", raising=False)
+    monkeypatch.setenv("GG_ROUND_SLOT", "1" if where == "finish" else "1024")
+    a, m, o = po.gen_trace(T, N, hot_lines=32)
+    bad, at = W - 1, 3                                   # the rank and its 0-based unpack / finish call
+    monkeypatch.setenv("GG_ROUND_FAIL_IMPORT" if where == "import" else "GG_ROUND_FAIL_FINISH", "%d,%d" % (bad, at))
+    bes, outs, _, _ = _contexts(torch, W, K, T, net, a, m, o)
+    try:
+        rounds, fail = _round_loop(torch, bes, W)
+    finally:
+        for be in bes:
+            be.close()
+    assert fail is not None, "the injected failure was lost"
+    rnd, msgs = fail
+    assert rnd >= at + 2                                  # reported by the round after the failing call
+    knob = "GG_ROUND_FAIL_IMPORT" if where == "import" else "GG_ROUND_FAIL_FINISH"
+    assert knob in msgs[bad], msgs
+    assert all("another rank" in x for r, x in enumerate(msgs) if r != bad), msgs
+
+
+def test_round_abandoned_after_again_then_fresh_run(monkeypatch):
+    """A run abandoned after unpack said GG_ROUND_AGAIN (the round in
+    progress: its step offset, attempt and repeat flag) leaves nothing behind:
+    gg_coherent_begin starts a new run, whose rounds start at step 0, and the
+    result equals one context and the oracle bit for bit."""
+    torch = torch_dev()
+    from graphite_amd import backend as B
+    from oracle import pyoracle as po
+    hip = _hip()
+    T, N, K, W = 64, 300, 8, 2
+    net = C.NET_EMESH_HOP_BY_HOP
+    monkeypatch.setenv("GG_ROUND_SLOT", "1024")
+    monkeypatch.setenv("GG_ROUND_BATCH0", "1,16")            # rank 0's first batch is one step: AGAIN
+    monkeypatch.delenv("GG_ROUND_FAIL_IMPORT", raising=False)
+    monkeypatch.delenv("GG_ROUND_FAIL_FINISH", raising=False)
+    a, m, o = po.gen_trace(T, N, hot_lines=32)
+    bes, outs, addr, meta = _contexts(torch, W, K, T, net, a, m, o)
+    rb = B.CMSG_RECORD_BYTES
+    ios = [be.round_pack(W, r, 0) for r, be in enumerate(bes)]
+    torch.cuda.synchronize()
+    for r in range(W):
+        for p in range(W):
+            if p != r:
+                _copy(hip, ios[p].recv + r * ios[p].stride * rb, ios[r].send + p * ios[r].stride * rb,
+                      (ios[r].slot + 1) * rb)
+            _copy(hip, ios[p].words_all + r * B.ROUND_WORDS * 8, ios[r].words_own, B.ROUND_WORDS * 8)
+    torch.cuda.synchronize()
+    for r, be in enumerate(bes):
+        be.round_unpack(ios[r])
+    assert {io.state for io in ios} == {B.ROUND_AGAIN}
+    # abandon: a new run on the same contexts
+    for be, out in zip(bes, outs):
+        out.zero_()
+        be.coherent_begin(addr, meta, o, out)
+    try:
+        _, fail = _round_loop(torch, bes, W)
+        assert fail is None, fail
+        torch.cuda.synchronize()
+        got = sum(to_np(x, np.uint64) for x in outs)
+        st = sum(be.coherent_stats()[0] for be in bes)
+    finally:
+        for be in bes:
+            be.close()
+    cfg = C.default_config(T, num_shards=K, net_model=net)
+    one = _single(torch, cfg, a, m, o)
+    assert np.array_equal(got, one[0]) and np.array_equal(st, one[1])
