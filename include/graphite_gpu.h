@@ -701,7 +701,13 @@ gg_status gg_core_get_stats(gg_ctx* ctx, uint64_t* out);
  * memory system is timed with the engine's issue times, and the core model
  * retimes the core around them (the reference feeds iocoom's curr_time back
  * as the next access's initial time; a trace carries no instructions between
- * its accesses to do that with).                                            */
+ * its accesses to do that with).  Barriers likewise: a SYNC instruction
+ * costs the stall the coherent engine measured (its release time minus the
+ * engine's arrival time), taken as it is.  The reference's SyncClient
+ * measures the stall on the core's own clock (sync_client.cc:308-313: time -
+ * start_time); iocoom overlaps loads, so its arrival can be earlier and that
+ * stall longer, and its clock after a barrier need not land on the common
+ * release time.  Not recomputed here (nor in the oracle): parity unpinned.  */
 typedef struct {
   uint16_t cost;     /* static cost in core cycles (Instruction::getCost: the
                         [core/static_instruction_costs] of its type, or a
