@@ -149,16 +149,20 @@ struct IoCore {
     sb[s] = mine ? t : old;
     if (mine) unit = (unit & ~(3u << (2 * s))) | (u << (2 * s));
   }
+  // the queues' ring indices wrap by a compare, not a modulo (a scalar
+  // division is a long VALU sequence on the instruction's chain)
+  __device__ __forceinline__ static uint32_t prev_of(uint32_t i, uint32_t n) { return i ? i - 1 : n - 1; }
+  __device__ __forceinline__ static uint32_t next_of(uint32_t i, uint32_t n) { return i + 1 == n ? 0u : i + 1; }
   // LoadQueue::execute (:182-208): the allocate time, *completion
   __device__ __forceinline__ uint64_t lq_execute(uint64_t schedule, uint64_t lat, uint64_t& completion)
   {
-    const uint32_t last = (lidx + ln_q - 1) % ln_q;
+    const uint32_t last = prev_of(lidx, ln_q);
     const uint64_t allocate = umax64(rl64(lsb, lidx), schedule), lastd = rl64(lsb, last);
     uint64_t dealloc;
     if (spec) { completion = allocate + lat; dealloc = umax64(completion, lastd + one); }
     else { completion = umax64(lastd, schedule) + lat; dealloc = completion; }
     if (ln == lidx) lsb = dealloc;
-    lidx = (lidx + 1) % ln_q;
+    lidx = next_of(lidx, ln_q);
     return allocate;
   }
   // executeLoad (:140-153) with StoreQueue::isAddressAvailable (:296-309)
@@ -171,13 +175,13 @@ struct IoCore {
   __device__ __forceinline__ uint64_t store(uint64_t schedule, uint64_t a, uint64_t latency)
   {
     const uint64_t lat = latency + one;
-    const uint64_t last_load = rl64(lsb, (lidx + ln_q - 1) % ln_q);
+    const uint64_t last_load = rl64(lsb, prev_of(lidx, ln_q));
     const uint64_t allocate = umax64(rl64(ssb, sidx), schedule);
-    const uint64_t last_store = rl64(ssb, (sidx + sn_q - 1) % sn_q);
+    const uint64_t last_store = rl64(ssb, prev_of(sidx, sn_q));
     const uint64_t dealloc = rfo ? umax64(umax64(allocate + lat, last_store + one), last_load)
                                  : umax64(umax64(schedule, last_store), last_load) + lat;
     if (ln == sidx) { ssb = dealloc; sad = a; }
-    sidx = (sidx + 1) % sn_q;
+    sidx = next_of(sidx, sn_q);
     return allocate;
   }
 };
@@ -206,7 +210,12 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
                                                           const uint64_t* __restrict__ lat, uint32_t T,
                                                           gg_iocoom_params p, double f, uint64_t* stats, uint32_t* err)
 {
-  const uint32_t t = blockIdx.x * kIoWaves + (threadIdx.x >> 6), ln = threadIdx.x & 63;
+  // the tile index is wave-uniform: readfirstlane'd, so its offsets load into
+  // SGPRs and every loop over its instructions is scalar control (from a
+  // thread-derived index the compiler had built exec-masked loops whose
+  // uniform state — curr, k, the counters — lived in VGPRs)
+  const uint32_t t = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * kIoWaves + (threadIdx.x >> 6)));
+  const uint32_t ln = threadIdx.x & 63;
   if (t >= T) return;
   IoCore c;
   c.ln = ln;
@@ -294,28 +303,30 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
         ++st[GG_IOCOOM_DATA_ACCESSES]; st[GG_IOCOOM_DATA_LATENCY_PS] += L;
       }
       if (bad) break;
-      uint64_t mem = 0, ex = 0;                                       // :209-252
-      ex += re - ready;   st[GG_IOCOOM_INTER_EXEC_STALL_PS] += re - ready;
-      mem += rr - re;     st[GG_IOCOOM_INTER_L1D_STALL_PS] += rr - re;
-      mem += lqr - rr;    st[GG_IOCOOM_LOAD_QUEUE_STALL_PS] += lqr - rr;
+      // :209-252; the memory / execution stall totals (core_model.cc:260-264)
+      // are the sums of these parts, formed once after the loop
+      st[GG_IOCOOM_INTER_EXEC_STALL_PS] += re - ready;
+      st[GG_IOCOOM_INTER_L1D_STALL_PS] += rr - re;
+      st[GG_IOCOOM_LOAD_QUEUE_STALL_PS] += lqr - rr;
       curr = lqr;
       if (!smov) {
-        mem += rmr - lqr; st[GG_IOCOOM_INTRA_L1D_STALL_PS] += rmr - lqr;
+        st[GG_IOCOOM_INTRA_L1D_STALL_PS] += rmr - lqr;
         curr = rmr;
         if (nwm) {
-          ex += wor - rmr;  st[GG_IOCOOM_INTRA_EXEC_STALL_PS] += wor - rmr;
-          mem += sqr - wor; st[GG_IOCOOM_STORE_QUEUE_STALL_PS] += sqr - wor;
+          st[GG_IOCOOM_INTRA_EXEC_STALL_PS] += wor - rmr;
+          st[GG_IOCOOM_STORE_QUEUE_STALL_PS] += sqr - wor;
           curr = sqr;
         }
       }
       if (ops & GG_INS_ATOMIC) ++st[GG_IOCOOM_IMPLICIT_MFENCES];     // core_model.cc:221-235
       if (ops >> GG_INS_FENCE_SHIFT) ++st[GG_IOCOOM_EXPLICIT_FENCES];
-      st[GG_IOCOOM_MEMORY_STALL_PS] += mem;                           // core_model.cc:260-264
-      st[GG_IOCOOM_EXECUTION_STALL_PS] += ex;
     }
   }
   if (k != k1) bad = true;
   st[GG_IOCOOM_TIME_PS] = curr;
+  st[GG_IOCOOM_MEMORY_STALL_PS] = st[GG_IOCOOM_INTER_L1D_STALL_PS] + st[GG_IOCOOM_LOAD_QUEUE_STALL_PS] +
+                                  st[GG_IOCOOM_INTRA_L1D_STALL_PS] + st[GG_IOCOOM_STORE_QUEUE_STALL_PS];
+  st[GG_IOCOOM_EXECUTION_STALL_PS] = st[GG_IOCOOM_INTER_EXEC_STALL_PS] + st[GG_IOCOOM_INTRA_EXEC_STALL_PS];
   if (bad) { if (ln == 0) atomicOr(err, 1u); return; }
   // lane s stores statistic s (one vector store)
   uint64_t v = 0;
