@@ -3445,6 +3445,33 @@ __device__ __forceinline__ void diag_off(CS& S)
   if (!GG_COH_DIAG) { S.prof = nullptr; S.trs = nullptr; S.trw = nullptr; S.tre = nullptr; }
 }
 
+// Scalar-cache warm-up of a launch-state block (CP / CS, read where used
+// through pointers): one load per 64-B line, all issued at
+// kernel entry, so the scalar-cache misses a wave would otherwise take one by
+// one along its dependent path (an L2 round trip each; PMC: ~1 300 scalar
+// misses per step launch) cost one latency.  The words are folded into a
+// value an empty asm consumes, so the loads are kept.
+#ifndef GG_KWARM
+#define GG_KWARM 1
+#endif
+template <class A, class B>
+__device__ __forceinline__ void kwarm(const A* __restrict__ a, const B* __restrict__ b)
+{
+  if (!GG_KWARM) return;
+  const uint32_t* wa = reinterpret_cast<const uint32_t*>(a);
+  const uint32_t* wb = reinterpret_cast<const uint32_t*>(b);
+  constexpr uint32_t kA = (uint32_t)((sizeof(A) + 63) / 64), kB = (uint32_t)((sizeof(B) + 63) / 64);
+  uint32_t x[kA + kB];
+#pragma unroll
+  for (uint32_t i = 0; i < kA; ++i) x[i] = wa[16 * i];
+#pragma unroll
+  for (uint32_t i = 0; i < kB; ++i) x[kA + i] = wb[16 * i];
+  uint32_t acc = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < kA + kB; ++i) acc ^= x[i];
+  asm volatile("; kwarm %0" ::"s"(acc));
+}
+
 // in-kernel launch timing (timing mode 2): every workgroup stamps its start
 // and end (100 MHz s_memrealtime) in its own words — plain stores, no atomic
 // on a shared word (1 024 blocks contending for one had added ~8 µs to the

@@ -9,6 +9,7 @@ template <bool PIPE, bool RQ>
 __global__ void __launch_bounds__(PIPE ? 64 * kMaxWalkWaves : 64) k_c_walk(const CP* __restrict__ Pp, const CS* __restrict__ Sp, uint32_t L, int stage,
                                                                          unsigned long long* kt, uint32_t kt_slot)
 {
+  kwarm(Pp, Sp);
   const CP& P = *Pp;                 // the launch state read on use (see k_c_step)
   const CS& S = *Sp;
   if (kt && threadIdx.x == 0) kt[(size_t)kt_slot * S.kt_stride + 2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
