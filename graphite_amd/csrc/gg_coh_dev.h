@@ -202,7 +202,10 @@ struct CS {
   GG_DP uint32_t* inb0; GG_DP uint32_t* inb1;       // inbox record lists [L][IC]
   GG_DP uint32_t* arv0; GG_DP uint32_t* arv1;       // hop-by-hop SELF lists [L][IC]
   GG_DP uint32_t* cnt4;                       // [L][4]: the lists' lengths {inbox even, odd, SELF even, odd}
-  GG_DP uint32_t* xl; GG_DP uint32_t* nxl; GG_DP uint32_t* yl; GG_DP uint32_t* nyl;           // segment lists [n][seg_cap], [n]
+  // segment (run) lists [n][seg_cap] of {record index | destination tile << 32} (the
+  // destination rides with the index so a walker's hand-off lookups start with
+  // the record loads), their counts [n]
+  GG_DP uint64_t* xl; GG_DP uint32_t* nxl; GG_DP uint64_t* yl; GG_DP uint32_t* nyl;
   GG_DP const Seg* segx; GG_DP const Seg* segy;
   GG_DP const uint32_t* tseg;                  // [T][2]: X run, Y run of a tile (~0 if not owned)
   GG_DP gg_cmsg* bnd; GG_DP uint32_t* bnd_cnt;       // held for the quantum boundary
@@ -2790,6 +2793,7 @@ __device__ __forceinline__ void publish_hbh_lds(TT& T, gg_cmsg* cur, uint32_t nl
   const bool regq = F ? P.np.qm != 0 : P.np.qm && P.np.qtype == GG_QM_HISTORY_TREE && P.np.max_size <= kQMax;
   const bool wave = !F && P.np.qm && P.np.max_size <= kQMax && !regq;
   RegQueue rq;
+  RegQueue::Raw rqr;                                  // (issued with the sends' list atomics, read after the order)
   uint32_t nn = 0;
   bool rq_loaded = false;
   // The list slots (inbox of the next step for self-sends, the X / Y run
@@ -2797,8 +2801,10 @@ __device__ __forceinline__ void publish_hbh_lds(TT& T, gg_cmsg* cur, uint32_t nl
   // sends are issued here and their list words stored after the port's
   // requests, so their round trip overlaps the ordering and the requests
   // (a list's order is free: the walkers and the inbox order by the keys)
-  uint32_t* late_p = nullptr;
+  uint32_t* late_p = nullptr;                        // an inbox list (self-send) ...
+  uint64_t* late_q = nullptr;                        // ... or a run list
   uint32_t late_j = ~0u, late_r = 0, late_cap = 0;   // the raw atomic result, checked at the store
+  uint64_t late_v = 0;
   for (uint32_t i0 = 0; i0 < nloc; i0 += 64) {
     const uint32_t i = i0 + ln;
     uint64_t e = 0, ts = 0;
@@ -2814,7 +2820,7 @@ __device__ __forceinline__ void publish_hbh_lds(TT& T, gg_cmsg* cur, uint32_t nl
       ri_self++;
     }
     const uint64_t m = __ballot(net);
-    if (m && regq && !rq_loaded) { rq.load_h0(gq, gnd, P.np.max_size, 1, P.np.analytical != 0, ln); rq_loaded = true; }
+    if (m && regq && !rq_loaded) { rqr = RegQueue::issue(gq, gnd, P.np.max_size, ln); rq_loaded = true; }
     const uint32_t pos = nn + (uint32_t)__builtin_popcountll(m & ((1ull << ln) - 1));
     if (net) {
       const uint32_t d = (uint32_t)((e >> 32) & 0x3FFFFFFFu), dx = d % P.mw, dy = d / P.mw;
@@ -2827,10 +2833,11 @@ __device__ __forceinline__ void publish_hbh_lds(TT& T, gg_cmsg* cur, uint32_t nl
       sl.x4[pos] = lc << 32;                              // (read above for slot i >= pos, in program order)
       // onto the X (or Y) run the packet enters (hk.seg_slot, checked at the store)
       const uint32_t j = atomicAdd(&(is_x ? S.nxl : S.nyl)[sg], 1u);
-      uint32_t* lp = (is_x ? S.xl : S.yl) + (size_t)sg * P.seg_cap;
-      if (i0 == 0) { late_p = lp; late_j = j; late_r = r; late_cap = P.seg_cap; }
+      uint64_t* lp = (is_x ? S.xl : S.yl) + (size_t)sg * P.seg_cap;
+      const uint64_t v = (uint64_t)r | ((uint64_t)d << 32);
+      if (i0 == 0) { late_q = lp; late_j = j; late_v = v; late_cap = P.seg_cap; }
       else if (j >= P.seg_cap) atomicOr(S.err, GG_DERR_CAP);
-      else lp[j] = r;
+      else lp[j] = v;
       ri_net++;
     }
     nn += (uint32_t)__builtin_popcountll(m);
@@ -2838,6 +2845,7 @@ __device__ __forceinline__ void publish_hbh_lds(TT& T, gg_cmsg* cur, uint32_t nl
   tsync();
   auto late_store = [&]() {                              // the list words of the first 64 sends
     if (late_p) { if (late_j >= late_cap) atomicOr(S.err, GG_DERR_CAP); else late_p[late_j] = late_r; }
+    if (late_q) { if (late_j >= late_cap) atomicOr(S.err, GG_DERR_CAP); else late_q[late_j] = late_v; }
   };
   if (!nn) { late_store(); return; }
   if (DG(S.trs)) q1 = __builtin_amdgcn_s_memtime();
@@ -2852,6 +2860,7 @@ __device__ __forceinline__ void publish_hbh_lds(TT& T, gg_cmsg* cur, uint32_t nl
     img_in(sl.pimg, gq, gnd, P.np.max_size, ln);
     tsync();
   }
+  if (regq) rq.finish(rqr, gq, gnd, 1, P.np.analytical != 0, ln);
   if (DG(S.trs)) { (void)__builtin_amdgcn_readfirstlane((int)rq.a0); q3 = __builtin_amdgcn_s_memtime(); }
   uint64_t ps = 0, fs = 0, bs = 0;
   for (uint32_t c0 = 0; c0 < nn; c0 += 64) {
@@ -2961,8 +2970,10 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
     HNode* gnd = S.nnd + qi * P.np.max_size;
     const bool regq = F ? P.np.qm != 0 : P.np.qm && P.np.qtype == GG_QM_HISTORY_TREE && P.np.max_size <= kQMax;
     const bool wave = !F && P.np.qm && P.np.max_size <= kQMax && !regq;
+    // (its loads issued now, beside the batch's list words; read after the order)
     RegQueue rq;
-    if (regq) rq.load_h0(gq, gnd, P.np.max_size, 1, P.np.analytical != 0, ln);
+    RegQueue::Raw rqr;
+    if (regq) rqr = RegQueue::issue(gq, gnd, P.np.max_size, ln);
     const uint64_t zps = lat_to_ps((uint64_t)P.np.router_delay + P.np.link_delay, P.np.f);
     uint64_t cq = 0, cf = 0;                                   // uniform: contention cycles, flits
     uint64_t rf = 0, rb = 0, rl = 0, rc = 0;                   // uniform: received flits, bits, latency, contention
@@ -3014,6 +3025,7 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
       img_in(sl.pimg, gq, gnd, P.np.max_size, ln);
       tsync();
     }
+    if (regq) rq.finish(rqr, gq, gnd, 1, P.np.analytical != 0, ln);
     if (DG(S.prof) || DG(S.trs)) { (void)__builtin_amdgcn_readfirstlane((int)rq.a0); _se = __builtin_amdgcn_s_memtime(); }
     for (uint32_t c0 = 0; c0 < na; c0 += 64) {
       const uint32_t cnt = min(64u, na - c0);
@@ -3365,10 +3377,11 @@ __device__ __forceinline__ uint64_t tile_step(const CP& P, const CS& S, uint32_t
         for (uint32_t i = ln; i < nn; i += 64) {
           const uint32_t r = o_[i];
           bool is_x;
-          const uint32_t sg = xy_stage_seg(P, S, T.tile, cur[r].dst, is_x);
+          const uint32_t d = cur[r].dst;
+          const uint32_t sg = xy_stage_seg(P, S, T.tile, d, is_x);
           const uint32_t j = hk.seg_slot(is_x, sg);
           if (j == ~0u) { atomicOr(S.err, GG_DERR_CAP); continue; }
-          (is_x ? S.xl : S.yl)[(size_t)sg * P.seg_cap + j] = r;
+          (is_x ? S.xl : S.yl)[(size_t)sg * P.seg_cap + j] = (uint64_t)r | ((uint64_t)d << 32);
         }
       }
     }
@@ -3586,11 +3599,11 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
   // one round of loads: the launch's live word, the run's count and bounds,
   // and (speculatively: in bounds whatever the count) its first list words
   uint32_t* cntp = (stage == 0 ? S.nxl : S.nyl) + sg;
-  const uint32_t* list = (stage == 0 ? S.xl : S.yl) + (size_t)sg * P.seg_cap;
+  const uint64_t* list = (stage == 0 ? S.xl : S.yl) + (size_t)sg * P.seg_cap;
   const uint32_t live = S.live[L & 3];
   const uint32_t n0 = *cntp;
   const Seg sd = (stage == 0 ? S.segx : S.segy)[sg >> 1];
-  const uint32_t lw = tid < P.seg_cap ? list[tid] : 0u;
+  const uint64_t lw = tid < P.seg_cap ? list[tid] : 0ull;
   if (!live) return;                                 // launch L was no step
   const uint32_t p = (live - 1) & 1u;
   PROF_T0();
@@ -3610,11 +3623,12 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
   // tree straight from HBM into registers now, beside the packet staging
   // (no LDS image copy in or out; written back only if the port served)
   const bool direct = PIPE && regq && !sweep;
+  // (issued right after the lane's packet record loads below, read after
+  // them: the queue's round trip and the records' overlap)
   RegQueue rq;
-  if (direct && wv < npos) {
-    const uint64_t qi = (uint64_t)tile_at(dir ? sd.lo + wv : sd.hi - wv) * 6 + port;
-    rq.load_h0(S.nq + qi, S.nnd + qi * P.np.max_size, P.np.max_size, 1, P.np.analytical != 0, ln);
-  }
+  RegQueue::Raw rqr;
+  const bool rq_direct = direct && wv < npos;
+  const uint64_t rq_qi = rq_direct ? (uint64_t)tile_at(dir ? sd.lo + wv : sd.hi - wv) * 6 + port : 0ull;
   uint8_t* qimg = smem;
   uint64_t* lc = reinterpret_cast<uint64_t*>(smem + (size_t)npos * P.qimg);     // [npos][kNetCtr]
   uint64_t* wlow = lc + (size_t)npos * kNetCtr;                                  // [kMaxWalkWaves] horizons (kInf: done)
@@ -3629,23 +3643,63 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
   W.Pr = W.Pf + P.walk_pk;                                       // rank in (send time, sender, seq) order
   W.Qt = reinterpret_cast<uint64_t*>(W.Pr + P.walk_pk);          // batch scratch of the one-wave sweep
   W.Qr = reinterpret_cast<uint32_t*>(W.Qt + P.walk_pk); W.Qs = W.Qr + P.walk_pk;
-  // the hand-off's lookups, issued now and consumed after the walk (lane i ==
-  // tid, the common case): the destination, and the receiver's local slot
-  // (the run ends at the destination) or the Y run the packet turns into
+  // The hand-off of lane i == tid's packet (the common case) is prepared
+  // here, beside the record loads: the destination comes with the list
+  // entry, so the receiver's local slot (the run ends at the destination) or
+  // the Y run the packet turns into is looked up in the same round as the
+  // records; where the packet leaves the run is known before the walk (at
+  // the destination's position, or held at the shard's edge when that lies
+  // beyond the run), so its slot in the next list is reserved right after
+  // staging and the walk hides that atomic's round trip; a held packet's
+  // other record fields are read now for its boundary copy.  The hand-off
+  // then only stores.
   uint32_t pdst = 0, pf = 0;
-  for (uint32_t i = tid; i < n; i += nthr) {
-    const uint32_t r = i == tid ? lw : list[i];
+  bool pheld = false;
+  uint64_t haddr = 0;
+  uint32_t hreq = 0, htype = 0, hlink = 0, hsrx = 0;
+  // lane tid's packet first, with no loop around it (so the waits for its
+  // record are counted, not drained): record fields and lookups, then the
+  // port queue's loads, then the record into LDS
+  // (unconditional loads — a lane without a packet reads record 0 and
+  // tile 0 — so no branch merges their registers before the queue's issue)
+  const bool has_p = tid < n;
+  const uint32_t orec = has_p ? (uint32_t)lw : 0u;
+  pdst = has_p ? (uint32_t)(lw >> 32) : 0u;
+  const gg_cmsg& om = cur[orec];
+  const uint64_t ot = om.arrival_ps, os = om.send_ps, oz = om.zero_load_ps;
+  const uint32_t osrc = om.src, oseq = om.seq, ohop = om.hop, otype = om.type;
+  haddr = om.addr; hreq = om.requester; hlink = om.link; hsrx = om.single_rx;
+  {
+    const uint32_t z = pos_of(pdst);
+    pheld = has_p && (z < sd.lo || z > sd.hi);
+    const uint32_t hx = tile_at(z);
+    pf = hx == pdst ? (uint32_t)S.ltile[pdst] : S.tseg[(size_t)hx * 2 + 1];
+  }
+  if (rq_direct) rqr = RegQueue::issue(S.nq + rq_qi, S.nnd + rq_qi * P.np.max_size, P.np.max_size, ln);
+  if (tid < n) {
+    const uint32_t i = tid;
+    htype = otype;
+    W.Pt[i] = ot; W.Ph[i] = os; W.Pk[i] = ((uint64_t)osrc << 32) | oseq; W.Pz[i] = oz;
+    W.Pi[i] = orec; W.Pp[i] = pos_of(ohop); W.Pd[i] = pos_of(pdst);
+    if (ot >> 51) atomicOr(S.err, GG_DERR_CAP);                  // batch keys are time << 12 | rank
+    W.Pf[i] = (uint32_t)nflits(P.np, msg_bits(P, otype));
+  }
+  for (uint32_t i = tid + nthr; i < n; i += nthr) {               // more packets than threads
+    const uint64_t le = list[i];
+    const uint32_t r = (uint32_t)le;
     const gg_cmsg& m = cur[r];
-    if (i == tid) {
-      pdst = m.dst;
-      const uint32_t hx = tile_at(pos_of(m.dst));
-      pf = hx == m.dst ? (uint32_t)S.ltile[m.dst] : S.tseg[(size_t)hx * 2 + 1];
-    }
     W.Pt[i] = m.arrival_ps; W.Ph[i] = m.send_ps; W.Pk[i] = ((uint64_t)m.src << 32) | m.seq; W.Pz[i] = m.zero_load_ps;
     W.Pi[i] = r; W.Pp[i] = pos_of(m.hop); W.Pd[i] = pos_of(m.dst);
-    if (m.arrival_ps >> 51) atomicOr(S.err, GG_DERR_CAP);        // batch keys are time << 12 | rank
+    if (m.arrival_ps >> 51) atomicOr(S.err, GG_DERR_CAP);
     W.Pf[i] = (uint32_t)nflits(P.np, msg_bits(P, m.type));
   }
+  if (rq_direct) rq.finish(rqr, S.nq + rq_qi, S.nnd + rq_qi * P.np.max_size, 1, P.np.analytical != 0, ln);
+  // lane tid's slot in the list its packet moves to (a held record, a SELF
+  // list, a Y run): reserved when the wave's walk is over, so the atomic's
+  // round trip overlaps the other waves' (the raw result is checked at the
+  // hand-off)
+  uint32_t jres = ~0u, s2res = 0;
+  bool pself = false;
   if (!sweep)                     // the pipeline's moving state: one word per packet (W.Qt, unused by it)
     for (uint32_t i = tid; i < n; i += nthr) W.Qt[i] = pipe_word(W.Pt[i], W.Pp[i], 0u);
   for (uint32_t i = tid; i < npos * kNetCtr; i += nthr) lc[i] = 0;
@@ -3888,6 +3942,13 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
     if (ln == 0 && visited) add_ctr(pos, cq, m, cf);
     nev = (uint32_t)m;
   }
+  if (tid < n) {
+    const uint32_t hx = tile_at(pos_of(pdst));
+    pself = !pheld && hx == pdst;
+    if (pheld) jres = atomicAdd(S.bnd_cnt, 1u);
+    else if (pself) jres = atomicAdd(narv_at(S, p ^ 1u, pf), 1u);
+    else { s2res = pf * 2 + (pdst / P.mw > hx / P.mw ? 1u : 0u); jres = atomicAdd(&S.nyl[s2res], 1u); }
+  }
   __syncthreads();
   PROF_AT(_w2);
   // hand-off
@@ -3905,27 +3966,37 @@ __device__ __forceinline__ void walk_body(const CP& P, const CS& S, uint32_t L, 
     }
     const uint32_t h = tile_at(p1);
     m->arrival_ps = ta; m->zero_load_ps = z; m->hop = h;
+    const bool own = i == tid;                                 // this lane's packet: its slot is reserved
     if (stt == 2) {                                            // held for the quantum boundary
-      const uint32_t j = atomicAdd(S.bnd_cnt, 1u);
+      if (own && !pheld) { atomicOr(S.err, GG_DERR_STATE); continue; }
+      const uint32_t j = own ? jres : atomicAdd(S.bnd_cnt, 1u);
       if (j >= P.msg_cap) { atomicOr(S.err, GG_DERR_CAP); continue; }
-      gg_cmsg g = *m;
+      gg_cmsg g;
+      if (own) {
+        const uint64_t kk = W.Pk[i];
+        g.addr = haddr; g.send_ps = W.Ph[i]; g.src = (uint32_t)(kk >> 32); g.dst = pdst; g.requester = hreq;
+        g.seq = (uint32_t)kk; g.type = htype; g.link = hlink; g.single_rx = hsrx;
+      } else {
+        g = *m;
+      }
       g.arrival_ps = ta; g.zero_load_ps = z; g.hop = h;
       S.bnd[j] = g;
       ++nb;
       continue;
     }
-    const uint32_t dst = i == tid ? pdst : m->dst;
+    const uint32_t dst = own ? pdst : m->dst;
+    if (own && (pheld || pself != (h == dst))) { atomicOr(S.err, GG_DERR_STATE); continue; }   // left where staging said
     if (h == dst) {                                            // the SELF port of the destination, next step
-      const int32_t ld = i == tid ? (int32_t)pf : S.ltile[dst];
-      const uint32_t j = atomicAdd(narv_at(S, p ^ 1u, ld), 1u);
+      const int32_t ld = own ? (int32_t)pf : S.ltile[dst];
+      const uint32_t j = own ? jres : atomicAdd(narv_at(S, p ^ 1u, ld), 1u);
       if (j >= P.IC) { atomicOr(S.err, GG_DERR_CAP); continue; }
       arv(S, p ^ 1u)[(size_t)ld * P.IC + j] = r;
     } else {                                                   // X done: the Y segment of the destination column
       bool is_x;
-      const uint32_t s2 = i == tid ? pf * 2 + (dst / P.mw > h / P.mw ? 1u : 0u) : xy_stage_seg(P, S, h, dst, is_x);
-      const uint32_t j = atomicAdd(&S.nyl[s2], 1u);
+      const uint32_t s2 = own ? s2res : xy_stage_seg(P, S, h, dst, is_x);
+      const uint32_t j = own ? jres : atomicAdd(&S.nyl[s2], 1u);
       if (j >= P.seg_cap) { atomicOr(S.err, GG_DERR_CAP); continue; }
-      S.yl[(size_t)s2 * P.seg_cap + j] = r;
+      S.yl[(size_t)s2 * P.seg_cap + j] = (uint64_t)r | ((uint64_t)dst << 32);
     }
   }
   nb = wave_sum(nb);
@@ -4100,7 +4171,7 @@ __device__ __forceinline__ void import_one(const CP& P, const CS& S, const gg_cm
   uint32_t* cnt = is_x ? S.nxl : S.nyl;
   const uint32_t j = atomicAdd(&cnt[sg], 1u);
   if (j >= P.seg_cap) { atomicOr(S.err, GG_DERR_CAP); return; }
-  (is_x ? S.xl : S.yl)[(size_t)sg * P.seg_cap + j] = r;
+  (is_x ? S.xl : S.yl)[(size_t)sg * P.seg_cap + j] = (uint64_t)r | ((uint64_t)m.dst << 32);
 }
 
 // ---- launchers (gg_coh_step.hip, gg_coh_persist.hip, gg_coh_walk.hip) ----

@@ -508,6 +508,50 @@ struct RegQueue {
     a0 = v0 ? x0.first : 0; b0 = v0 ? x0.second : 0;
     a1 = v1 ? x1.first : 0; b1 = v1 ? x1.second : 0;
   }
+  // load_h0 in two halves, so that a wave can issue other loads while the
+  // queue's are in flight: issue() starts the loads into registers and waits
+  // for nothing (the header spread over lanes, one 16-B chunk per lane k <
+  // sizeof(HQueue) / 16; the nodes as load_h0 reads them); finish() reads
+  // the header's fields out of the lanes, which waits for them, and takes
+  // the dependent load() when the list does not start at node 0.
+  struct Raw { uint4 hc; HNode x0, x1; };
+  __device__ __forceinline__ static Raw issue(const HQueue* q, const HNode* nd, uint32_t max_size, uint32_t lane)
+  {
+    Raw r;
+    r.x0 = HNode{0, 0}; r.x1 = HNode{0, 0}; r.hc = make_uint4(0, 0, 0, 0);
+    if (lane < max_size) r.x0 = nd[lane];
+    if (lane + 64 < max_size) r.x1 = nd[lane + 64];
+    if (lane < sizeof(HQueue) / 16) r.hc = reinterpret_cast<const uint4*>(q)[lane];
+    return r;
+  }
+  template <size_t OFF>
+  __device__ __forceinline__ static uint32_t hw32(const uint4& c)
+  {
+    static_assert(OFF % 4 == 0 && OFF < sizeof(HQueue), "a 32-bit header word");
+    constexpr uint32_t w = OFF / 4, k = w & 3u;
+    const uint32_t v = k == 0 ? c.x : k == 1 ? c.y : k == 2 ? c.z : c.w;
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)(w >> 2));
+  }
+  template <size_t OFF>
+  __device__ __forceinline__ static uint64_t hw64(const uint4& c)
+  {
+    return ((uint64_t)hw32<OFF + 4>(c) << 32) | hw32<OFF>(c);
+  }
+  __device__ __forceinline__ void finish(const Raw& r, const HQueue* q, const HNode* nd, uint64_t mp, bool an, uint32_t lane)
+  {
+    const uint32_t h = hw32<offsetof(HQueue, head)>(r.hc);
+    if (h != 0) { load(q, nd, mp, an, lane); return; }
+    ln = lane; min_proc = mp; analytical = an; errs = 0; errp = nullptr;
+    sz = hw32<offsetof(HQueue, size)>(r.hc);
+    cap = hw32<offsetof(HQueue, max_size)>(r.hc);
+    sig_sq = hw64<offsetof(HQueue, sig_sq)>(r.hc); sig = hw64<offsetof(HQueue, sig)>(r.hc);
+    nreq = hw64<offsetof(HQueue, n)>(r.hc); newest = hw64<offsetof(HQueue, newest)>(r.hc);
+    util = hw64<offsetof(HQueue, util)>(r.hc); last_req = hw64<offsetof(HQueue, last_req)>(r.hc);
+    total_req = hw64<offsetof(HQueue, total_req)>(r.hc); anl = hw64<offsetof(HQueue, analytical)>(r.hc);
+    const bool v0 = ln < sz, v1 = ln + 64 < sz;
+    a0 = v0 ? r.x0.first : 0; b0 = v0 ? r.x0.second : 0;
+    a1 = v1 ? r.x1.first : 0; b1 = v1 ? r.x1.second : 0;
+  }
   __device__ __forceinline__ void store(HQueue* q, HNode* nd) const
   {
     if (errs && errp && ln == 0) atomicOr(errp, errs);
