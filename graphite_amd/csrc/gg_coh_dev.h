@@ -2731,15 +2731,22 @@ __device__ __forceinline__ void step_body(const CP& P, const CS& S, uint32_t L, 
   const uint32_t ln = threadIdx.x, lt = blockIdx.x;
   uint32_t k = L;
   uint64_t barrier = barrier_arg, q = 0, Q = 0;
-  // one round trip: the launch state (written by earlier launches)
+  // one round trip: the launch state (written by earlier launches) spread
+  // over lanes — lane i loads word i of the quantum state and of the step
+  // ring, unconditionally, beside the tile's own state — then read out of
+  // the lanes (per-word loads behind the devloop selects had compiled to a
+  // chain of a load and a wait per word)
+  static_assert(QS_N <= 64, "the quantum state fits a wave");
+  const uint64_t qw = ln < QS_N ? S.qs[ln] : 0ull;
+  const uint32_t rw = ln < 11 ? S.ring[ln] : 0u;              // ring[4], quiet, imp[2], live[4]
+  TilePre pre;
+  pre.load(S, lt, ln);
   uint64_t qsv[QS_N];
   uint32_t rv[11];
 #pragma unroll
-  for (int i = 0; i < QS_N; ++i) qsv[i] = devloop ? S.qs[i] : 0;
+  for (int i = 0; i < QS_N; ++i) qsv[i] = devloop ? rl64(qw, (uint32_t)i) : 0ull;
 #pragma unroll
-  for (int i = 0; i < 11; ++i) rv[i] = S.ring[i];           // ring[4], quiet, imp[2], live[4]
-  TilePre pre;
-  pre.load(S, lt, ln);
+  for (int i = 0; i < 11; ++i) rv[i] = rl32(rw, (uint32_t)i);
   if (devloop) {
     if (qsv[QS_DONE]) { if (lt == 0 && ln == 0) S.live[L & 3] = 0; return; }
     q = qsv[QS_Q]; Q = qsv[QS_COUNT];

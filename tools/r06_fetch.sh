@@ -26,7 +26,7 @@ for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=T
         a = acc[k][r["Counter_Name"]]; a[0] += float(r["Counter_Value"]); a[1] += 1
 for k, c in sorted(acc.items()):
     n = max(x[1] for x in c.values())
-    if n < 100: continue
+    if n < int(os.environ.get("MINL", "100")): continue
     print(name, k, "launches~%d" % n, " ".join("%s=%.1f" % (m, s / max(cnt, 1)) for m, (s, cnt) in sorted(c.items())))
 PY
   find "$OUT/$name" -name "*counter_collection.csv" -delete
