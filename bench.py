@@ -83,7 +83,7 @@ def pmc_traffic(kernel, key):
             continue
         ks = d.get("kernels", {})
         # the summary keys are rocprof's names (template arguments included)
-        v = ks.get(kernel) or next((ks[k] for k in ks if k.split("<")[0] == kernel), None)
+        v = ks.get(kernel) or next((ks[k] for k in ks if k.split("<")[0].split("::")[-1] == kernel), None)
         if v and "hbm_bytes" in v:
             best = {"bytes": v["hbm_bytes"], "source": os.path.relpath(f, ROOT)}
             if "traffic_factors" in v:

@@ -704,6 +704,13 @@ struct Tile {
   uint64_t pd = 0;
   uint32_t ncdl = 0, ncdl0 = 0;
   GG_GLB CReqX* rqx = nullptr;
+  // the directory's per-tile arrays and sharer words per entry, formed once
+  // per step: ent / shw run on every handler's path, and formed there from
+  // CP / CS each call re-read those fields with scalar loads and waited
+  GG_DP DEnt* dirb; GG_DP DEnt* repb;
+  GG_DP uint64_t* dshb; GG_DP uint64_t* rshb;
+  uint32_t wd;
+  GG_DP gg_cmsg* cpool;                 // this step's record pool (put)
 
   // LC: the tile's L1-D / L2 tags, meta bytes and RR counters live in LDS at
   // clds for the whole launch (k_c_persist; layout of cache_lds_bytes)
@@ -740,6 +747,9 @@ struct Tile {
       L2.mt_log = P.mt_log;
     }
     sd = 0;
+    dirb = S.dir + (size_t)lt * P.E; repb = S.rep + (size_t)lt * P.R;
+    dshb = S.dsh + (size_t)lt * P.E * P.W; rshb = S.rsh + (size_t)lt * P.R * P.W; wd = P.W;
+    cpool = p ? S.pool1 : S.pool0;
     rec = pre.rec; rec_end = pre.rec_end; clk = pre.clk; pend_start = pre.pend_start;
     out_addr = pre.out_addr; out_time = pre.out_time;
     blocked = pre.blocked; seq = pre.seq; nrep = pre.nrep; nrq = pre.nrq;
@@ -796,7 +806,7 @@ struct Tile {
     m.addr = addr; m.send_ps = t; m.arrival_ps = t; m.zero_load_ps = 0;
     m.src = tile; m.dst = dst; m.requester = requester; m.seq = sq; m.type = type; m.link = 0;
     m.hop = GG_HOP_NONE; m.single_rx = single_rx;
-    pool(S, p)[i] = m;
+    cpool[i] = m;
     // the step's sent list in LDS (slot = send order = sq - the step's first
     // seq): publish reads its records' fields from here, not back from HBM
     // (x3 / x4 are free once the inbox is ordered; sends come after that)
@@ -832,14 +842,14 @@ struct Tile {
   __device__ __forceinline__ DEnt* ent(int32_t h) const
   {
     h = __builtin_amdgcn_readfirstlane(h);
-    return h >= 0 ? S.dir + (size_t)lt * P.E + h : S.rep + (size_t)lt * P.R + (-h - 1);
+    return h >= 0 ? dirb + h : repb + (-h - 1);
   }
   __device__ __forceinline__ uint64_t* shw(int32_t h) const
   {
     h = __builtin_amdgcn_readfirstlane(h);
-    return h >= 0 ? S.dsh + ((size_t)lt * P.E + h) * P.W : S.rsh + ((size_t)lt * P.R + (-h - 1)) * P.W;
+    return h >= 0 ? dshb + (size_t)h * wd : rshb + (size_t)(-h - 1) * wd;
   }
-  __device__ __forceinline__ const DEnt* rep_ent(uint32_t i) const { return S.rep + (size_t)lt * P.R + i; }
+  __device__ __forceinline__ const DEnt* rep_ent(uint32_t i) const { return repb + i; }
   // The open entry: the directory entry the current message works on, its
   // fields in scalars and its sharer words in lanes 0..W-1 (W <= 64), so a
   // handler's read-modify-writes of the entry are register operations (in
@@ -859,7 +869,7 @@ struct Tile {
     eclose();
     const DEnt* e = ent(h);
     oaddr = e->addr; oown = e->owner; ost = e->dstate; onsh = e->nsh;
-    osh = ln < P.W ? shw(h)[ln] : 0ull;
+    osh = ln < wd ? shw(h)[ln] : 0ull;
     oh = h; od = false;
   }
   __device__ __forceinline__ void eflush()
@@ -867,7 +877,7 @@ struct Tile {
     if (oh == NO_ENT || !od) return;
     DEnt* e = ent(oh);
     e->owner = oown; e->dstate = (uint16_t)ost; e->nsh = (uint16_t)onsh;
-    if (ln < P.W) shw(oh)[ln] = osh;
+    if (ln < wd) shw(oh)[ln] = osh;
     od = false;
   }
   __device__ __forceinline__ void eclose() { eflush(); oh = NO_ENT; }
@@ -919,18 +929,18 @@ struct Tile {
     t += P.lat_dir;
     stat(GG_CT_DIR_ACCESSES, 1);
     const uint32_t base = dset(a) * P.dassoc;
-    DEnt* d = S.dir + (size_t)lt * P.E;
+    DEnt* d = dirb;
     // one round of loads: the set's entries (lane = way) and, when they fit
     // four words per lane, the set's sharer words (word idx = way * W + k in
     // lane idx & 63 of register idx >> 6): a hit opens its entry (eopen)
     // without a dependent load
-    const bool spec = P.W * P.dassoc <= 256 && (P.W & (P.W - 1)) == 0;   // (W a power of two: an entry's words never straddle two registers)
+    const bool spec = wd * P.dassoc <= 256 && (wd & (wd - 1)) == 0;   // (W a power of two: an entry's words never straddle two registers)
     DEnt e{INV_ADDR, -1, 0, 0};
     if (ln < P.dassoc) e = d[base + ln];
     uint64_t sw0 = 0, sw1 = 0, sw2 = 0, sw3 = 0;
     if (spec) {
-      const uint64_t* g = S.dsh + ((size_t)lt * P.E + base) * P.W;
-      const uint32_t nw = P.W * P.dassoc;
+      const uint64_t* g = dshb + (size_t)base * wd;
+      const uint32_t nw = wd * P.dassoc;
       if (ln < nw) sw0 = g[ln];
       if (ln + 64 < nw) sw1 = g[ln + 64];
       if (ln + 128 < nw) sw2 = g[ln + 128];
@@ -946,10 +956,10 @@ struct Tile {
         oown = (int32_t)rl32((uint32_t)e.owner, w);
         ost = rl32((uint32_t)e.dstate, w);
         onsh = rl32((uint32_t)e.nsh, w);
-        const uint32_t i0 = w * P.W, u = i0 >> 6;                    // the entry's words: one register
+        const uint32_t i0 = w * wd, u = i0 >> 6;                    // the entry's words: one register
         const uint64_t src = u == 0 ? sw0 : u == 1 ? sw1 : u == 2 ? sw2 : sw3;
         const uint64_t x = shfl64(src, (int)((i0 + ln) & 63));
-        osh = ln < P.W ? x : 0ull;
+        osh = ln < wd ? x : 0ull;
         oh = h; od = false;
       }
       return h;
@@ -963,7 +973,7 @@ struct Tile {
       const uint32_t i = base + w;
       if (oh == (int32_t)i) eclose();
       d[i].addr = a;
-      if (ln < P.W) shw((int32_t)i)[ln] = 0;
+      if (ln < wd) shw((int32_t)i)[ln] = 0;
       if constexpr (MO) S.drng[(size_t)lt * P.E + i] = 0;          // a fresh Random (seed state)
       if (spec) {
         eclose();
@@ -983,7 +993,7 @@ struct Tile {
   {
     eclose();                                     // the moves below work on HBM
     const uint32_t base = dset(replaced) * P.dassoc;
-    DEnt* d = S.dir + (size_t)lt * P.E;
+    DEnt* d = dirb;
     const uint64_t v = ln < P.dassoc ? d[base + ln].addr : 0;
     const uint64_t m = __ballot(ln < P.dassoc && v == replaced);
     if (!m) { fail(); return NO_ENT; }
@@ -993,7 +1003,7 @@ struct Tile {
     nrep = r + 1;
     *ent(-(int32_t)r - 1) = d[slot];
     uint64_t* so = shw(slot); uint64_t* sr = shw(-(int32_t)r - 1);
-    for (uint32_t w = 0; w < P.W; ++w) { sr[w] = so[w]; so[w] = 0; }
+    for (uint32_t w = 0; w < wd; ++w) { sr[w] = so[w]; so[w] = 0; }
     d[slot] = DEnt{a, -1, DS_UNCACHED, 0};
     if constexpr (MO) {                           // the old entry keeps its Random, the new one is fresh
       S.rrng[(size_t)lt * P.R + r] = S.drng[(size_t)lt * P.E + slot];
@@ -1016,7 +1026,7 @@ struct Tile {
     for (uint32_t k = (uint32_t)__builtin_ctzll(rh); k + 1 < nr; ++k) {
       *ent(-(int32_t)k - 1) = *ent(-(int32_t)k - 2);
       uint64_t* dst = shw(-(int32_t)k - 1); const uint64_t* src = shw(-(int32_t)k - 2);
-      for (uint32_t w = 0; w < P.W; ++w) dst[w] = src[w];
+      for (uint32_t w = 0; w < wd; ++w) dst[w] = src[w];
       if constexpr (MO) S.rrng[(size_t)lt * P.R + k] = S.rrng[(size_t)lt * P.R + k + 1];
     }
     nrep = nr - 1;
@@ -1030,7 +1040,7 @@ struct Tile {
                                                 uint32_t single_rx)
   {
     eopen(h);
-    uint64_t bits = ln < P.W ? osh : 0;
+    uint64_t bits = ln < wd ? osh : 0;
     const uint32_t c = (uint32_t)__builtin_popcountll(bits);
     const uint32_t pre = wave_excl_scan(c, ln);
     const uint32_t tot = wave_sum(c);
@@ -1197,7 +1207,7 @@ struct Tile {
           const uint64_t msg_time = t;
           if (dget(w.addr, t) != NO_ENT) fail();   // the assert in getReplacementCandidates (directory_cache.cc:161)
           const uint32_t base = dset(w.addr) * P.dassoc;
-          const DEnt* d = S.dir + (size_t)lt * P.E;
+          const DEnt* d = dirb;
           eflush();                                 // the scan reads the ways' sharer counts from HBM
           // candidate (:138-149): fewest sharers among ways with no queued request, first wins
           uint32_t key = ~0u;
@@ -1645,7 +1655,7 @@ struct Tile {
     const uint32_t n = onsh;
     const uint32_t k = (uint32_t)(int)(r * (double)(int)n);
     if (k >= n) { fail(); return 0; }
-    const uint64_t bits = ln < P.W ? osh : 0ull;
+    const uint64_t bits = ln < wd ? osh : 0ull;
     const uint32_t c = (uint32_t)__builtin_popcountll(bits);
     const uint32_t pre = wave_excl_scan(c, ln);
     const bool mine = k >= pre && k < pre + c;
@@ -1762,7 +1772,7 @@ struct Tile {
           const uint64_t msg_time = t;
           if (dget(w.addr, t) != NO_ENT) fail();   // getReplacementCandidates' assert (directory_cache.cc:161)
           const uint32_t base = dset(w.addr) * P.dassoc;
-          const DEnt* d = S.dir + (size_t)lt * P.E;
+          const DEnt* d = dirb;
           eflush();
           uint32_t key = ~0u;
           if (ln < P.dassoc) {
@@ -2100,7 +2110,7 @@ struct Tile {
   __device__ __forceinline__ int32_t sh_slot(uint64_t a)
   {
     const uint32_t base = dset(a) * P.dassoc;
-    const DEnt* d = S.dir + (size_t)lt * P.E;
+    const DEnt* d = dirb;
     const uint64_t v = ln < P.dassoc ? d[base + ln].addr : INV_ADDR;
     const uint64_t m = __ballot(ln < P.dassoc && v == a);
     return m ? (int32_t)(base + (uint32_t)__builtin_ctzll(m)) : NO_ENT;
@@ -2125,7 +2135,7 @@ struct Tile {
     eclose();                                     // the moves below work on HBM
     ev_addr = INV_ADDR;
     const uint32_t base = dset(a) * P.dassoc;
-    DEnt* d = S.dir + (size_t)lt * P.E;
+    DEnt* d = dirb;
     DEnt e{INV_ADDR, -1, 0, 0};
     if (ln < P.dassoc) e = d[base + ln];
     const uint64_t inv = __ballot(ln < P.dassoc && e.addr == INV_ADDR);
@@ -2152,7 +2162,7 @@ struct Tile {
       nrep = r + 1;
       *ent(-(int32_t)r - 1) = d[slot];
       uint64_t* so = shw(slot); uint64_t* sr = shw(-(int32_t)r - 1);
-      if (ln < P.W) sr[ln] = so[ln];
+      if (ln < wd) sr[ln] = so[ln];
       const uint32_t vcs = rl32((uint32_t)e.dstate, w) >> 8;
       if (vcs != CS_CLEAN && vcs != CS_DIRTY) fail();
       L2.cnt(GG_CC_DATA_READS); L2.cnt(GG_CC_EVICTIONS);
@@ -2160,7 +2170,7 @@ struct Tile {
       ev_addr = va;
     }
     d[slot] = DEnt{a, -1, (uint16_t)((CS_DINV << 8) | DS_UNCACHED), 0};
-    if (ln < P.W) shw(slot)[ln] = 0;
+    if (ln < wd) shw(slot)[ln] = 0;
     L2.cnt(GG_CC_TAG_WRITES); L2.cnt(GG_CC_DATA_WRITES);
     return slot;
   }
