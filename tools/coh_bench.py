@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Coherent-mode (Mode C) timing experiment: GPU gg_coherent_run vs the C
-oracle on the same hotspot trace.  usage: coh_bench.py T N [K] [hot] [--no-oracle] [--hbh]"""
+oracle on the same hotspot trace.  usage: coh_bench.py T N [K] [hot] [--no-oracle] [--hbh] [--warm] [--no-timing] [--heartbeat]"""
 import os
 import sys
 import time
@@ -11,6 +11,15 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
+    if "--heartbeat" in sys.argv:            # long oracle runs: a line every 30 s (gpurun's idle watchdog)
+        import threading
+
+        def beat():
+            while True:
+                time.sleep(30)
+                print("... %.0f s" % (time.perf_counter() - t_start), flush=True)
+        t_start = time.perf_counter()
+        threading.Thread(target=beat, daemon=True).start()
     import torch
     from graphite_amd import config as C
     from graphite_amd import backend as B
