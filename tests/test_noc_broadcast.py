@@ -124,6 +124,8 @@ def oracle_tree(cfg, src, dst, bits, t, batches=1):
 @pytest.mark.parametrize("T,n,span,batches,frac,qm", [(16, 3000, 200000, 1, 0.1, 1), (64, 4000, 400000, 2, 0.05, 1),
                                                       (64, 3000, 100000, 1, 0.02, 1), (16, 2000, 100000, 1, 0.2, 0),
                                                       (256, 2000, 400000, 1, 0.01, 1), (256, 3000, 600000, 1, 0.03, 1),
+                                                      # the bench's mesh: 256 blocks x 4 routers
+                                                      (1024, 3000, 400000, 1, 0.01, 1),
                                                       # more routers than the workgroup's threads
                                                       (2116, 1500, 400000, 1, 0.004, 1),
                                                       (4096, 1500, 400000, 1, 0.004, 1),
