@@ -118,36 +118,48 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l)
   return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), (int)l) << 32) |
          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
 }
-__device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+// max of two wave-uniform u64: the subtract's borrow decides, all on the
+// scalar unit (the compiler forms a u64 compare of SGPRs with a VALU compare
+// through VCC, a VALU latency on the instruction's chain)
+__device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b)
+{
+  uint32_t rlo, rhi, t0, t1;
+  asm("s_sub_u32 %2, %4, %6\n\t"
+      "s_subb_u32 %3, %5, %7\n\t"
+      "s_cselect_b32 %0, %6, %4\n\t"
+      "s_cselect_b32 %1, %7, %5"
+      : "=&s"(rlo), "=&s"(rhi), "=&s"(t0), "=&s"(t1)
+      : "s"((uint32_t)a), "s"((uint32_t)(a >> 32)), "s"((uint32_t)b), "s"((uint32_t)(b >> 32))
+      : "scc");
+  return (uint64_t)rhi << 32 | rlo;
+}
 typedef uint64_t u64x8 __attribute__((ext_vector_type(8)));
+
+// A scoreboard entry is the register's time with its unit in the top two
+// bits (one indexed read gives both); times of 2^62 ps or more are flagged.
+constexpr uint64_t kTimeMask = (1ull << 62) - 1;
 
 struct IoCore {
   uint32_t ln;
-  u64x8 sb;                       // _register_scoreboard: register ln + 64 s in slot s (a vector
-                                  // value: a uniform slot index reads it by indirect register
+  u64x8 sb;                       // _register_scoreboard + _register_dependency_list: register
+                                  // ln + 64 s in slot s, unit << 62 | time (a vector value: a
+                                  // uniform slot index reads it by indirect register
                                   // addressing, no memory)
-  uint32_t unit;                  // _register_dependency_list: slot s in bits 2s..2s+1
   uint64_t lsb;                   // LoadQueue::_scoreboard[ln]
   uint64_t ssb, sad;              // StoreQueue::_scoreboard[ln], _addresses[ln]
   uint32_t ln_q, sn_q, lidx, sidx;
   bool spec, rfo;
   uint64_t one;
 
-  __device__ __forceinline__ uint64_t reg_time(uint32_t r) const
+  __device__ __forceinline__ uint64_t reg_entry(uint32_t r) const
   {
     return rl64(sb[r >> 6], r & 63);
   }
-  __device__ __forceinline__ uint32_t reg_unit(uint32_t r) const
-  {
-    return ((uint32_t)__builtin_amdgcn_readlane((int)unit, (int)(r & 63)) >> (2 * (r >> 6))) & 3u;
-  }
-  __device__ __forceinline__ void reg_write(uint32_t r, uint64_t t, uint32_t u)
+  __device__ __forceinline__ void reg_write(uint32_t r, uint64_t e)
   {
     const uint32_t s = r >> 6;
-    const bool mine = ln == (r & 63);
     const uint64_t old = sb[s];
-    sb[s] = mine ? t : old;
-    if (mine) unit = (unit & ~(3u << (2 * s))) | (u << (2 * s));
+    sb[s] = ln == (r & 63) ? e : old;
   }
   // the queues' ring indices wrap by a compare, not a modulo (a scalar
   // division is a long VALU sequence on the instruction's chain)
@@ -186,20 +198,26 @@ struct IoCore {
   }
 };
 
-// The access stream, 64 accesses per window (lane l holds access base + l)
+// The tile's access stream, 64 accesses per window (lane l holds access
+// base + l); indices are 32-bit and relative to the tile's first access
+// (gg_iocoom_run checks the per-tile counts), so the window tests are scalar
+// compares
 struct IoAcc {
-  uint64_t base = ~0ull, a = 0, l = 0;
-  uint32_t m = 0;
-  __device__ __forceinline__ void get(uint64_t k, uint64_t end, const uint64_t* __restrict__ addr,
-                                      const uint32_t* __restrict__ meta, const uint64_t* __restrict__ lat,
-                                      uint32_t ln, uint64_t& A, uint32_t& M, uint64_t& L)
+  const uint64_t* __restrict__ addr;
+  const uint32_t* __restrict__ meta;
+  const uint64_t* __restrict__ lat;
+  uint32_t n, ln, base = 0, m = 0;
+  uint64_t a = 0, l = 0;
+  __device__ __forceinline__ void load(uint32_t b)
   {
-    if (base == ~0ull || k - base >= 64) {
-      base = k;
-      const uint64_t i = k + ln;
-      a = i < end ? addr[i] : 0; m = i < end ? meta[i] : 0; l = i < end ? lat[i] : 0;
-    }
-    const uint32_t j = (uint32_t)(k - base);
+    base = b;
+    const uint32_t i = b + ln;
+    a = i < n ? addr[i] : 0; m = i < n ? meta[i] : 0; l = i < n ? lat[i] : 0;
+  }
+  __device__ __forceinline__ void get(uint32_t k, uint64_t& A, uint32_t& M, uint64_t& L)
+  {
+    if (k - base >= 64) load(k);
+    const uint32_t j = k - base;
     A = rl64(a, j); M = (uint32_t)__builtin_amdgcn_readlane((int)m, (int)j); L = rl64(l, j);
   }
 };
@@ -220,20 +238,25 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
   IoCore c;
   c.ln = ln;
   c.sb = u64x8{0, 0, 0, 0, 0, 0, 0, 0};
-  c.unit = 0; c.lsb = 0; c.ssb = 0; c.sad = ~0ull;                  // INVALID_ADDRESS (fixed_types.h:36)
+  c.lsb = 0; c.ssb = 0; c.sad = ~0ull;                              // INVALID_ADDRESS (fixed_types.h:36)
   c.ln_q = p.num_load_queue_entries; c.sn_q = p.num_store_queue_entries; c.lidx = 0; c.sidx = 0;
   c.spec = p.speculative_loads_enabled != 0; c.rfo = p.multiple_outstanding_RFOs_enabled != 0;
   c.one = gg::lat_to_ps(1, f);
-  IoAcc acc;
   uint64_t st[GG_NUM_IOCOOM_STATS];
 #pragma unroll
   for (int k = 0; k < GG_NUM_IOCOOM_STATS; ++k) st[k] = 0;
-  const uint64_t i0 = offs[t], i1 = offs[t + 1], k1 = offs[T + 1 + t + 1];
-  uint64_t k = offs[T + 1 + t], curr = 0;
+  const uint64_t i0 = offs[t], k0 = offs[T + 1 + t];
+  const uint32_t ni = (uint32_t)(offs[t + 1] - i0), k1 = (uint32_t)(offs[T + 1 + t + 1] - k0);
+  const uint4* __restrict__ tins = ins + i0;
+  IoAcc acc;
+  acc.addr = addr + k0; acc.meta = meta + k0; acc.lat = lat + k0; acc.n = k1; acc.ln = ln;
+  acc.load(0);
+  uint32_t k = 0;
+  uint64_t curr = 0;
   bool bad = false;
-  for (uint64_t b = i0; b < i1 && !bad; b += 64) {
-    const uint4 w = b + ln < i1 ? ins[b + ln] : make_uint4(0, 0, 0, 0);
-    const uint32_t cnt = i1 - b < 64 ? (uint32_t)(i1 - b) : 64u;
+  for (uint32_t b = 0; b < ni && !bad; b += 64) {
+    const uint4 w = b + ln < ni ? tins[b + ln] : make_uint4(0, 0, 0, 0);
+    const uint32_t cnt = ni - b < 64 ? ni - b : 64u;
     for (uint32_t j = 0; j < cnt && !bad; ++j) {
       const uint32_t w0 = (uint32_t)__builtin_amdgcn_readlane((int)w.x, (int)j);
       const uint32_t wr[3] = {(uint32_t)__builtin_amdgcn_readlane((int)w.y, (int)j),
@@ -248,7 +271,7 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
       if (regs & GG_INS_SYNC) {                                       // dynamic (:74-79)
         uint64_t A, L; uint32_t M;
         if (k >= k1) { bad = true; break; }
-        acc.get(k++, k1, addr, meta, lat, ln, A, M, L);
+        acc.get(k++, A, M, L);
         if (M != GG_META_BARRIER) { bad = true; break; }
         if (!L) { --st[GG_IOCOOM_INSTRUCTIONS]; continue; }
         curr += L;
@@ -261,14 +284,16 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
       const uint32_t nr = regs & 7u, nw = (regs >> 3) & 7u;
       if (nr + nw > 6) { bad = true; break; }
       uint64_t rl = ready, re = ready;                                // :100-125
-      for (uint32_t i = 0; i < nr; ++i) {
+      for (uint32_t i = 0; i < nr; ++i) {                             // (selects: no branch per operand)
         const uint32_t r = reg(i);
-        if (r >= GG_IOCOOM_NUM_REGISTERS) { bad = true; break; }
-        const uint32_t u = c.reg_unit(r);
-        const uint64_t v = c.reg_time(r);
-        if (u == kUnitLoad) rl = umax64(rl, v);
-        else if (u == kUnitExec) re = umax64(re, v);
-        else if (v > ready) { bad = true; break; }
+        bad |= r >= GG_IOCOOM_NUM_REGISTERS;
+        const uint64_t e = c.reg_entry(r & (GG_IOCOOM_NUM_REGISTERS - 1));
+        const uint32_t u = (uint32_t)(e >> 62);
+        const uint64_t v = e & kTimeMask;
+        const uint64_t mx = umax64(v, u == kUnitLoad ? rl : re);
+        rl = u == kUnitLoad ? mx : rl;
+        re = u == kUnitExec ? mx : re;
+        bad |= u != kUnitLoad && u != kUnitExec && umax64(v, ready) != ready;
       }
       if (bad) break;
       const uint64_t rr = umax64(rl, re);                             // :128-129
@@ -276,7 +301,7 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
       for (uint32_t i = 0; i < (ops & 3u); ++i) {
         uint64_t A, L; uint32_t M;
         if (k >= k1) { bad = true; break; }
-        acc.get(k++, k1, addr, meta, lat, ln, A, M, L);
+        acc.get(k++, A, M, L);
         if (M == GG_META_BARRIER || (M & GG_META_WRITE)) { bad = true; break; }
         uint64_t comp;
         const uint64_t alloc = c.load(rr, A, L, comp);
@@ -286,10 +311,12 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
       if (bad) break;
       const uint64_t wor = rmr + cost;                                // :158-166
       const bool smov = (ops & GG_INS_SIMPLE_MOV_LOAD) != 0;
+      const uint64_t went = wor | (uint64_t)(smov ? kUnitLoad : kUnitExec) << 62;
+      bad |= wor > kTimeMask;
       for (uint32_t i = 0; i < nw; ++i) {                             // :172-184
         const uint32_t r = reg(nr + i);
-        if (r >= GG_IOCOOM_NUM_REGISTERS) { bad = true; break; }
-        c.reg_write(r, wor, smov ? kUnitLoad : kUnitExec);
+        bad |= r >= GG_IOCOOM_NUM_REGISTERS;
+        c.reg_write(r & (GG_IOCOOM_NUM_REGISTERS - 1), went);
       }
       if (bad) break;
       uint64_t sqr = wor;                                             // :186-201
@@ -297,7 +324,7 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
       for (uint32_t i = 0; i < nwm; ++i) {
         uint64_t A, L; uint32_t M;
         if (k >= k1) { bad = true; break; }
-        acc.get(k++, k1, addr, meta, lat, ln, A, M, L);
+        acc.get(k++, A, M, L);
         if (M == GG_META_BARRIER || !(M & GG_META_WRITE)) { bad = true; break; }
         sqr = umax64(sqr, c.store(wor, A, L));
         ++st[GG_IOCOOM_DATA_ACCESSES]; st[GG_IOCOOM_DATA_LATENCY_PS] += L;
@@ -419,6 +446,9 @@ gg_status gg_iocoom_run(gg_ctx* ctx, const gg_iocoom_params* params, const gg_in
   for (const uint64_t* o : {ins_tile_offsets, acc_tile_offsets})
     for (uint32_t t = 0; t < T; ++t)
       if (o[t + 1] < o[t]) return gg_fail(GG_ERR_INVALID, "gg_iocoom_run: tile offsets decrease");
+      else if (o[t + 1] - o[t] > (1ull << 31))   // the kernel's tile-relative indices are 32-bit
+        return gg_fail(GG_ERR_RANGE, "gg_iocoom_run: tile %u has %llu instructions or accesses (at most 2^31)", t,
+                       (unsigned long long)(o[t + 1] - o[t]));
   if (ins_tile_offsets[T] > ins_tile_offsets[0] && !ins_dev) return gg_fail(GG_ERR_INVALID, "gg_iocoom_run: NULL instructions");
   if (acc_tile_offsets[T] > acc_tile_offsets[0] && (!acc_addr_dev || !acc_meta_dev || !acc_lat_dev))
     return gg_fail(GG_ERR_INVALID, "gg_iocoom_run: NULL access stream");
