@@ -151,9 +151,11 @@ struct IoCore {
   bool spec, rfo;
   uint64_t one;
 
-  __device__ __forceinline__ uint64_t reg_entry(uint32_t r) const
+  __device__ __forceinline__ void reg_entry(uint32_t r, uint32_t& hi, uint32_t& lo) const
   {
-    return rl64(sb[r >> 6], r & 63);
+    const uint64_t x = sb[r >> 6];
+    hi = (uint32_t)__builtin_amdgcn_readlane((int)(x >> 32), (int)(r & 63));
+    lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, (int)(r & 63));
   }
   __device__ __forceinline__ void reg_write(uint32_t r, uint64_t e)
   {
@@ -253,26 +255,28 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
   acc.load(0);
   uint32_t k = 0;
   uint64_t curr = 0;
-  bool bad = false;
+  uint32_t bad = 0;                 // (a word, not a bool: the compiler kept a bool in a VGPR)
   for (uint32_t b = 0; b < ni && !bad; b += 64) {
     const uint4 w = b + ln < ni ? tins[b + ln] : make_uint4(0, 0, 0, 0);
     const uint32_t cnt = ni - b < 64 ? ni - b : 64u;
     for (uint32_t j = 0; j < cnt && !bad; ++j) {
       const uint32_t w0 = (uint32_t)__builtin_amdgcn_readlane((int)w.x, (int)j);
-      const uint32_t wr[3] = {(uint32_t)__builtin_amdgcn_readlane((int)w.y, (int)j),
-                              (uint32_t)__builtin_amdgcn_readlane((int)w.z, (int)j),
-                              (uint32_t)__builtin_amdgcn_readlane((int)w.w, (int)j)};
-      auto reg = [&](uint32_t i) {                                  // (a select: no indexed register array)
-        const uint32_t x = (i >> 1) == 0 ? wr[0] : (i >> 1) == 1 ? wr[1] : wr[2];
-        return (x >> (16 * (i & 1))) & 0xFFFFu;
+      // the register operands as a queue: reads, then writes, 16 bits each
+      uint64_t rq = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)w.z, (int)j) << 32 |
+                    (uint32_t)__builtin_amdgcn_readlane((int)w.y, (int)j);
+      uint32_t rq2 = (uint32_t)__builtin_amdgcn_readlane((int)w.w, (int)j);
+      auto reg = [&]() {
+        const uint32_t r = (uint32_t)rq & 0xFFFFu;
+        rq = rq >> 16 | (uint64_t)rq2 << 48; rq2 >>= 16;
+        return r;
       };
       const uint32_t ops = (w0 >> 16) & 0xFFu, regs = w0 >> 24;
       ++st[GG_IOCOOM_INSTRUCTIONS];                                   // :72
       if (regs & GG_INS_SYNC) {                                       // dynamic (:74-79)
         uint64_t A, L; uint32_t M;
-        if (k >= k1) { bad = true; break; }
+        if (k >= k1) { bad = 1; break; }
         acc.get(k++, A, M, L);
-        if (M != GG_META_BARRIER) { bad = true; break; }
+        if (M != GG_META_BARRIER) { bad = 1; break; }
         if (!L) { --st[GG_IOCOOM_INSTRUCTIONS]; continue; }
         curr += L;
         ++st[GG_IOCOOM_SYNC_INSTRUCTIONS];
@@ -282,27 +286,32 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
       const uint64_t cost = gg::lat_to_ps(w0 & 0xFFFFu, f);              // getCost (:70)
       const uint64_t ready = curr;                                    // no L1-I (:78-87)
       const uint32_t nr = regs & 7u, nw = (regs >> 3) & 7u;
-      if (nr + nw > 6) { bad = true; break; }
-      uint64_t rl = ready, re = ready;                                // :100-125
-      for (uint32_t i = 0; i < nr; ++i) {                             // (selects: no branch per operand)
-        const uint32_t r = reg(i);
-        bad |= r >= GG_IOCOOM_NUM_REGISTERS;
-        const uint64_t e = c.reg_entry(r & (GG_IOCOOM_NUM_REGISTERS - 1));
-        const uint32_t u = (uint32_t)(e >> 62);
-        const uint64_t v = e & kTimeMask;
-        const uint64_t mx = umax64(v, u == kUnitLoad ? rl : re);
-        rl = u == kUnitLoad ? mx : rl;
-        re = u == kUnitExec ? mx : re;
-        bad |= u != kUnitLoad && u != kUnitExec && umax64(v, ready) != ready;
+      if (nr + nw > 6) { bad = 1; break; }
+      // :100-125, as selects (no branch per operand).  An entry's unit is
+      // LOAD (1) or EXECUTION (3) once written and INVALID (0) only with
+      // time 0, which no maximum below can take: the top bit picks the
+      // accumulator, and an INVALID entry's "time > ready" never holds.
+      uint64_t rl = ready, re = ready;
+      for (uint32_t i = 0; i < nr; ++i) {
+        const uint32_t r = reg();
+        bad |= r >> 9;                                                // >= GG_IOCOOM_NUM_REGISTERS
+        uint32_t hi, lo;
+        c.reg_entry(r & (GG_IOCOOM_NUM_REGISTERS - 1), hi, lo);
+        uint32_t hs = hi;
+        asm("" : "+s"(hs));                 // (opaque copy: else the test is folded into a VALU i64 compare)
+        const bool ex = (int32_t)hs < 0;
+        const uint64_t mx = umax64((uint64_t)(hi & 0x3FFFFFFFu) << 32 | lo, ex ? re : rl);
+        rl = ex ? rl : mx;
+        re = ex ? mx : re;
       }
       if (bad) break;
       const uint64_t rr = umax64(rl, re);                             // :128-129
       uint64_t lqr = rr, rmr = rr;                                    // :133-152
       for (uint32_t i = 0; i < (ops & 3u); ++i) {
         uint64_t A, L; uint32_t M;
-        if (k >= k1) { bad = true; break; }
+        if (k >= k1) { bad = 1; break; }
         acc.get(k++, A, M, L);
-        if (M == GG_META_BARRIER || (M & GG_META_WRITE)) { bad = true; break; }
+        if (M == GG_META_BARRIER || (M & GG_META_WRITE)) { bad = 1; break; }
         uint64_t comp;
         const uint64_t alloc = c.load(rr, A, L, comp);
         ++st[GG_IOCOOM_DATA_ACCESSES]; st[GG_IOCOOM_DATA_LATENCY_PS] += L;
@@ -312,10 +321,10 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
       const uint64_t wor = rmr + cost;                                // :158-166
       const bool smov = (ops & GG_INS_SIMPLE_MOV_LOAD) != 0;
       const uint64_t went = wor | (uint64_t)(smov ? kUnitLoad : kUnitExec) << 62;
-      bad |= wor > kTimeMask;
+      bad |= (uint32_t)(wor >> 62);
       for (uint32_t i = 0; i < nw; ++i) {                             // :172-184
-        const uint32_t r = reg(nr + i);
-        bad |= r >= GG_IOCOOM_NUM_REGISTERS;
+        const uint32_t r = reg();
+        bad |= r >> 9;
         c.reg_write(r & (GG_IOCOOM_NUM_REGISTERS - 1), went);
       }
       if (bad) break;
@@ -323,9 +332,9 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
       const uint32_t nwm = (ops >> 2) & 3u;
       for (uint32_t i = 0; i < nwm; ++i) {
         uint64_t A, L; uint32_t M;
-        if (k >= k1) { bad = true; break; }
+        if (k >= k1) { bad = 1; break; }
         acc.get(k++, A, M, L);
-        if (M == GG_META_BARRIER || !(M & GG_META_WRITE)) { bad = true; break; }
+        if (M == GG_META_BARRIER || !(M & GG_META_WRITE)) { bad = 1; break; }
         sqr = umax64(sqr, c.store(wor, A, L));
         ++st[GG_IOCOOM_DATA_ACCESSES]; st[GG_IOCOOM_DATA_LATENCY_PS] += L;
       }
@@ -349,7 +358,7 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
       if (ops >> GG_INS_FENCE_SHIFT) ++st[GG_IOCOOM_EXPLICIT_FENCES];
     }
   }
-  if (k != k1) bad = true;
+  if (k != k1) bad = 1;
   st[GG_IOCOOM_TIME_PS] = curr;
   st[GG_IOCOOM_MEMORY_STALL_PS] = st[GG_IOCOOM_INTER_L1D_STALL_PS] + st[GG_IOCOOM_LOAD_QUEUE_STALL_PS] +
                                   st[GG_IOCOOM_INTRA_L1D_STALL_PS] + st[GG_IOCOOM_STORE_QUEUE_STALL_PS];
