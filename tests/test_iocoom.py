@@ -309,6 +309,26 @@ def test_gpu_iocoom_errors():
                   to_dev(torch, addr, torch.int64), to_dev(torch, bad, torch.int32), to_dev(torch, lat, torch.int64), ao)
     with pytest.raises(B.GGError):
         be.iocoom_stats()                                    # the streams disagree
+
+    def run(i_, lat_):
+        be.iocoom_run(C.IocoomParams(), torch.from_numpy(i_.view(np.uint8).copy()).cuda(), io,
+                      to_dev(torch, addr, torch.int64), to_dev(torch, meta, torch.int32),
+                      to_dev(torch, lat_, torch.int64), ao)
+        return be.iocoom_stats()
+    run(ins, lat)                                            # clean
+    r = ins.copy()
+    i = int(np.nonzero(((r["regs"] & C.INS_SYNC) == 0) & ((r["ops"] & 0xF) == 0))[0][0])
+    r["regs"][i] = 1                                         # one read register, out of range
+    r["reg"][i, 0] = 512
+    with pytest.raises(B.GGError):
+        run(r, lat)
+    # a register time of 2^62 ps or more does not fit the scoreboard entry
+    # beside its unit (gg_core.hip, kTimeMask): flagged, not wrapped
+    big = lat.copy()
+    big[(meta != BARRIER) & ((meta & WRITE) == 0)] = np.uint64(1) << np.uint64(62)
+    with pytest.raises(B.GGError):
+        run(ins, big)
+    run(ins, lat)                                            # the context recovers
     with pytest.raises(B.GGError):
         be.iocoom_run(C.IocoomParams(65, 8), torch.from_numpy(ins.view(np.uint8).copy()).cuda(), io,
                       to_dev(torch, addr, torch.int64), to_dev(torch, meta, torch.int32),
