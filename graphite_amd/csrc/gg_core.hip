@@ -496,7 +496,7 @@ gg_status gg_iocoom_get_stats(gg_ctx* ctx, uint64_t* out)
   GG_HIP(hipStreamSynchronize(ctx->last_stream));
   uint32_t e = 0;
   GG_HIP(hipMemcpy(&e, ctx->io_err, sizeof e, hipMemcpyDeviceToHost));
-  if (e) return gg_fail(GG_ERR_STATE, "gg_iocoom_run: the instruction and access streams disagree");
+  if (e) return gg_fail(GG_ERR_STATE, "gg_iocoom_run: the instruction and access streams disagree, a register is out of range or a register time reached 2^62 ps");
   GG_HIP(hipMemcpy(out, ctx->io_stats, sizeof(uint64_t) * ctx->cfg.num_tiles * GG_NUM_IOCOOM_STATS,
                    hipMemcpyDeviceToHost));
   return GG_OK;
