@@ -259,7 +259,11 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
   for (uint32_t b = 0; b < ni && !bad; b += 64) {
     const uint4 w = b + ln < ni ? tins[b + ln] : make_uint4(0, 0, 0, 0);
     const uint32_t cnt = ni - b < 64 ? ni - b : 64u;
-    for (uint32_t j = 0; j < cnt && !bad; ++j) {
+    // No early exit inside a window: a failed check sets `bad` and the
+    // instruction runs on (register indices masked, accesses past the stream
+    // read as zeros, stream indices never wrap), so the body is straight-line
+    // scalar code; `bad` ends the walk at the window's end.
+    for (uint32_t j = 0; j < cnt; ++j) {
       const uint32_t w0 = (uint32_t)__builtin_amdgcn_readlane((int)w.x, (int)j);
       // the register operands as a queue: reads, then writes, 16 bits each
       uint64_t rq = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)w.z, (int)j) << 32 |
@@ -270,92 +274,91 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
         rq = rq >> 16 | (uint64_t)rq2 << 48; rq2 >>= 16;
         return r;
       };
+      auto next_access = [&](uint64_t& A, uint32_t& M, uint64_t& L) {
+        bad |= k >= k1 ? 1u : 0u;
+        acc.get(k, A, M, L);
+        k += k < k1 ? 1u : 0u;
+      };
       const uint32_t ops = (w0 >> 16) & 0xFFu, regs = w0 >> 24;
-      ++st[GG_IOCOOM_INSTRUCTIONS];                                   // :72
       if (regs & GG_INS_SYNC) {                                       // dynamic (:74-79)
         uint64_t A, L; uint32_t M;
-        if (k >= k1) { bad = 1; break; }
-        acc.get(k++, A, M, L);
-        if (M != GG_META_BARRIER) { bad = 1; break; }
-        if (!L) { --st[GG_IOCOOM_INSTRUCTIONS]; continue; }
+        next_access(A, M, L);
+        bad |= M != GG_META_BARRIER ? 1u : 0u;
+        const uint64_t one_if = L ? 1u : 0u;                          // a zero stall is no instruction
+        st[GG_IOCOOM_INSTRUCTIONS] += one_if;
+        st[GG_IOCOOM_SYNC_INSTRUCTIONS] += one_if;
         curr += L;
-        ++st[GG_IOCOOM_SYNC_INSTRUCTIONS];
         st[GG_IOCOOM_SYNC_STALL_PS] += L;
-        continue;
-      }
-      const uint64_t cost = gg::lat_to_ps(w0 & 0xFFFFu, f);              // getCost (:70)
-      const uint64_t ready = curr;                                    // no L1-I (:78-87)
-      const uint32_t nr = regs & 7u, nw = (regs >> 3) & 7u;
-      if (nr + nw > 6) { bad = 1; break; }
-      // :100-125, as selects (no branch per operand).  An entry's unit is
-      // LOAD (1) or EXECUTION (3) once written and INVALID (0) only with
-      // time 0, which no maximum below can take: the top bit picks the
-      // accumulator, and an INVALID entry's "time > ready" never holds.
-      uint64_t rl = ready, re = ready;
-      for (uint32_t i = 0; i < nr; ++i) {
-        const uint32_t r = reg();
-        bad |= r >> 9;                                                // >= GG_IOCOOM_NUM_REGISTERS
-        uint32_t hi, lo;
-        c.reg_entry(r & (GG_IOCOOM_NUM_REGISTERS - 1), hi, lo);
-        uint32_t hs = hi;
-        asm("" : "+s"(hs));                 // (opaque copy: else the test is folded into a VALU i64 compare)
-        const bool ex = (int32_t)hs < 0;
-        const uint64_t mx = umax64((uint64_t)(hi & 0x3FFFFFFFu) << 32 | lo, ex ? re : rl);
-        rl = ex ? rl : mx;
-        re = ex ? mx : re;
-      }
-      if (bad) break;
-      const uint64_t rr = umax64(rl, re);                             // :128-129
-      uint64_t lqr = rr, rmr = rr;                                    // :133-152
-      for (uint32_t i = 0; i < (ops & 3u); ++i) {
-        uint64_t A, L; uint32_t M;
-        if (k >= k1) { bad = 1; break; }
-        acc.get(k++, A, M, L);
-        if (M == GG_META_BARRIER || (M & GG_META_WRITE)) { bad = 1; break; }
-        uint64_t comp;
-        const uint64_t alloc = c.load(rr, A, L, comp);
-        ++st[GG_IOCOOM_DATA_ACCESSES]; st[GG_IOCOOM_DATA_LATENCY_PS] += L;
-        lqr = umax64(lqr, alloc); rmr = umax64(rmr, comp);
-      }
-      if (bad) break;
-      const uint64_t wor = rmr + cost;                                // :158-166
-      const bool smov = (ops & GG_INS_SIMPLE_MOV_LOAD) != 0;
-      const uint64_t went = wor | (uint64_t)(smov ? kUnitLoad : kUnitExec) << 62;
-      bad |= (uint32_t)(wor >> 62);
-      for (uint32_t i = 0; i < nw; ++i) {                             // :172-184
-        const uint32_t r = reg();
-        bad |= r >> 9;
-        c.reg_write(r & (GG_IOCOOM_NUM_REGISTERS - 1), went);
-      }
-      if (bad) break;
-      uint64_t sqr = wor;                                             // :186-201
-      const uint32_t nwm = (ops >> 2) & 3u;
-      for (uint32_t i = 0; i < nwm; ++i) {
-        uint64_t A, L; uint32_t M;
-        if (k >= k1) { bad = 1; break; }
-        acc.get(k++, A, M, L);
-        if (M == GG_META_BARRIER || !(M & GG_META_WRITE)) { bad = 1; break; }
-        sqr = umax64(sqr, c.store(wor, A, L));
-        ++st[GG_IOCOOM_DATA_ACCESSES]; st[GG_IOCOOM_DATA_LATENCY_PS] += L;
-      }
-      if (bad) break;
-      // :209-252; the memory / execution stall totals (core_model.cc:260-264)
-      // are the sums of these parts, formed once after the loop
-      st[GG_IOCOOM_INTER_EXEC_STALL_PS] += re - ready;
-      st[GG_IOCOOM_INTER_L1D_STALL_PS] += rr - re;
-      st[GG_IOCOOM_LOAD_QUEUE_STALL_PS] += lqr - rr;
-      curr = lqr;
-      if (!smov) {
-        st[GG_IOCOOM_INTRA_L1D_STALL_PS] += rmr - lqr;
-        curr = rmr;
-        if (nwm) {
-          st[GG_IOCOOM_INTRA_EXEC_STALL_PS] += wor - rmr;
-          st[GG_IOCOOM_STORE_QUEUE_STALL_PS] += sqr - wor;
-          curr = sqr;
+      } else {
+        ++st[GG_IOCOOM_INSTRUCTIONS];                                 // :72
+        const uint64_t cost = gg::lat_to_ps(w0 & 0xFFFFu, f);            // getCost (:70)
+        const uint64_t ready = curr;                                  // no L1-I (:78-87)
+        const uint32_t nr = regs & 7u, nw = (regs >> 3) & 7u;
+        bad |= nr + nw > 6 ? 1u : 0u;
+        // :100-125, as selects (no branch per operand).  An entry's unit is
+        // LOAD (1) or EXECUTION (3) once written and INVALID (0) only with
+        // time 0, which no maximum below can take: the top bit picks the
+        // accumulator, and an INVALID entry's "time > ready" never holds.
+        uint64_t rl = ready, re = ready;
+        for (uint32_t i = 0; i < nr; ++i) {
+          const uint32_t r = reg();
+          bad |= r >> 9;                                              // >= GG_IOCOOM_NUM_REGISTERS
+          uint32_t hi, lo;
+          c.reg_entry(r & (GG_IOCOOM_NUM_REGISTERS - 1), hi, lo);
+          uint32_t hs = hi;
+          asm("" : "+s"(hs));               // (opaque copy: else the test is folded into a VALU i64 compare)
+          const bool ex = (int32_t)hs < 0;
+          const uint64_t mx = umax64((uint64_t)(hi & 0x3FFFFFFFu) << 32 | lo, ex ? re : rl);
+          rl = ex ? rl : mx;
+          re = ex ? mx : re;
         }
+        const uint64_t rr = umax64(rl, re);                           // :128-129
+        uint64_t lqr = rr, rmr = rr;                                  // :133-152
+        for (uint32_t i = 0; i < (ops & 3u); ++i) {
+          uint64_t A, L; uint32_t M;
+          next_access(A, M, L);
+          bad |= M == GG_META_BARRIER || (M & GG_META_WRITE) ? 1u : 0u;
+          uint64_t comp;
+          const uint64_t alloc = c.load(rr, A, L, comp);
+          ++st[GG_IOCOOM_DATA_ACCESSES]; st[GG_IOCOOM_DATA_LATENCY_PS] += L;
+          lqr = umax64(lqr, alloc); rmr = umax64(rmr, comp);
+        }
+        const uint64_t wor = rmr + cost;                              // :158-166
+        const bool smov = (ops & GG_INS_SIMPLE_MOV_LOAD) != 0;
+        const uint64_t went = wor | (uint64_t)(smov ? kUnitLoad : kUnitExec) << 62;
+        bad |= (uint32_t)(wor >> 62);
+        for (uint32_t i = 0; i < nw; ++i) {                           // :172-184
+          const uint32_t r = reg();
+          bad |= r >> 9;
+          c.reg_write(r & (GG_IOCOOM_NUM_REGISTERS - 1), went);
+        }
+        uint64_t sqr = wor;                                           // :186-201
+        const uint32_t nwm = (ops >> 2) & 3u;
+        for (uint32_t i = 0; i < nwm; ++i) {
+          uint64_t A, L; uint32_t M;
+          next_access(A, M, L);
+          bad |= M == GG_META_BARRIER || !(M & GG_META_WRITE) ? 1u : 0u;
+          sqr = umax64(sqr, c.store(wor, A, L));
+          ++st[GG_IOCOOM_DATA_ACCESSES]; st[GG_IOCOOM_DATA_LATENCY_PS] += L;
+        }
+        // :209-252; the memory / execution stall totals (core_model.cc:260-264)
+        // are the sums of these parts, formed once after the loop
+        st[GG_IOCOOM_INTER_EXEC_STALL_PS] += re - ready;
+        st[GG_IOCOOM_INTER_L1D_STALL_PS] += rr - re;
+        st[GG_IOCOOM_LOAD_QUEUE_STALL_PS] += lqr - rr;
+        curr = lqr;
+        if (!smov) {
+          st[GG_IOCOOM_INTRA_L1D_STALL_PS] += rmr - lqr;
+          curr = rmr;
+          if (nwm) {
+            st[GG_IOCOOM_INTRA_EXEC_STALL_PS] += wor - rmr;
+            st[GG_IOCOOM_STORE_QUEUE_STALL_PS] += sqr - wor;
+            curr = sqr;
+          }
+        }
+        if (ops & GG_INS_ATOMIC) ++st[GG_IOCOOM_IMPLICIT_MFENCES];   // core_model.cc:221-235
+        if (ops >> GG_INS_FENCE_SHIFT) ++st[GG_IOCOOM_EXPLICIT_FENCES];
       }
-      if (ops & GG_INS_ATOMIC) ++st[GG_IOCOOM_IMPLICIT_MFENCES];     // core_model.cc:221-235
-      if (ops >> GG_INS_FENCE_SHIFT) ++st[GG_IOCOOM_EXPLICIT_FENCES];
     }
   }
   if (k != k1) bad = 1;
