@@ -121,6 +121,9 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l)
 // max of two wave-uniform u64: the subtract's borrow decides, all on the
 // scalar unit (the compiler forms a u64 compare of SGPRs with a VALU compare
 // through VCC, a VALU latency on the instruction's chain)
+// The error checks as arithmetic on words: a bool or-ed across checks is
+// kept as a lane mask and widened through a VALU select and a readfirstlane
+__device__ __forceinline__ uint32_t is_barrier(uint32_t m) { return (uint32_t)(((uint64_t)m + 1u) >> 32); }
 __device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b)
 {
   uint32_t rlo, rhi, t0, t1;
@@ -182,7 +185,7 @@ struct IoCore {
   // executeLoad (:140-153) with StoreQueue::isAddressAvailable (:296-309)
   __device__ __forceinline__ uint64_t load(uint64_t schedule, uint64_t a, uint64_t latency, uint64_t& completion)
   {
-    if (__ballot(ln < sn_q && sad == a && ssb >= schedule)) { completion = schedule + one; return schedule; }
+    if (__builtin_amdgcn_ballot_w64(ln < sn_q && sad == a && ssb >= schedule)) { completion = schedule + one; return schedule; }
     return lq_execute(schedule, latency + one, completion);
   }
   // executeStore (:155-165) + StoreQueue::execute (:250-284)
@@ -275,7 +278,7 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
         return r;
       };
       auto next_access = [&](uint64_t& A, uint32_t& M, uint64_t& L) {
-        bad |= k >= k1 ? 1u : 0u;
+        bad |= (uint32_t)(int32_t)(k1 - 1u - k) >> 31;                // k >= k1 (both < 2^31)
         acc.get(k, A, M, L);
         k += k < k1 ? 1u : 0u;
       };
@@ -283,7 +286,7 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
       if (regs & GG_INS_SYNC) {                                       // dynamic (:74-79)
         uint64_t A, L; uint32_t M;
         next_access(A, M, L);
-        bad |= M != GG_META_BARRIER ? 1u : 0u;
+        bad |= is_barrier(M) ^ 1u;
         const uint64_t one_if = L ? 1u : 0u;                          // a zero stall is no instruction
         st[GG_IOCOOM_INSTRUCTIONS] += one_if;
         st[GG_IOCOOM_SYNC_INSTRUCTIONS] += one_if;
@@ -294,7 +297,9 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
         const uint64_t cost = gg::lat_to_ps(w0 & 0xFFFFu, f);            // getCost (:70)
         const uint64_t ready = curr;                                  // no L1-I (:78-87)
         const uint32_t nr = regs & 7u, nw = (regs >> 3) & 7u;
-        bad |= nr + nw > 6 ? 1u : 0u;
+        uint32_t nrw = nr + nw;
+        asm("" : "+s"(nrw));                // (opaque: else folded back into a compare widened by the VALU)
+        bad |= (6u - nrw) >> 31;                                      // nr + nw > 6
         // :100-125, as selects (no branch per operand).  An entry's unit is
         // LOAD (1) or EXECUTION (3) once written and INVALID (0) only with
         // time 0, which no maximum below can take: the top bit picks the
@@ -317,7 +322,7 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
         for (uint32_t i = 0; i < (ops & 3u); ++i) {
           uint64_t A, L; uint32_t M;
           next_access(A, M, L);
-          bad |= M == GG_META_BARRIER || (M & GG_META_WRITE) ? 1u : 0u;
+          bad |= M & GG_META_WRITE;                                   // a write or a BARRIER (all ones)
           uint64_t comp;
           const uint64_t alloc = c.load(rr, A, L, comp);
           ++st[GG_IOCOOM_DATA_ACCESSES]; st[GG_IOCOOM_DATA_LATENCY_PS] += L;
@@ -337,27 +342,24 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
         for (uint32_t i = 0; i < nwm; ++i) {
           uint64_t A, L; uint32_t M;
           next_access(A, M, L);
-          bad |= M == GG_META_BARRIER || !(M & GG_META_WRITE) ? 1u : 0u;
+          bad |= ((M & GG_META_WRITE) ^ 1u) | is_barrier(M);
           sqr = umax64(sqr, c.store(wor, A, L));
           ++st[GG_IOCOOM_DATA_ACCESSES]; st[GG_IOCOOM_DATA_LATENCY_PS] += L;
         }
         // :209-252; the memory / execution stall totals (core_model.cc:260-264)
         // are the sums of these parts, formed once after the loop
+        // (selects: a simple-mov load stops at lqr, a store-free one at rmr)
+        const bool st_on = !smov && nwm;
+        const uint64_t rmr_e = smov ? lqr : rmr, wor_e = st_on ? wor : rmr_e, sqr_e = st_on ? sqr : wor_e;
         st[GG_IOCOOM_INTER_EXEC_STALL_PS] += re - ready;
         st[GG_IOCOOM_INTER_L1D_STALL_PS] += rr - re;
         st[GG_IOCOOM_LOAD_QUEUE_STALL_PS] += lqr - rr;
-        curr = lqr;
-        if (!smov) {
-          st[GG_IOCOOM_INTRA_L1D_STALL_PS] += rmr - lqr;
-          curr = rmr;
-          if (nwm) {
-            st[GG_IOCOOM_INTRA_EXEC_STALL_PS] += wor - rmr;
-            st[GG_IOCOOM_STORE_QUEUE_STALL_PS] += sqr - wor;
-            curr = sqr;
-          }
-        }
-        if (ops & GG_INS_ATOMIC) ++st[GG_IOCOOM_IMPLICIT_MFENCES];   // core_model.cc:221-235
-        if (ops >> GG_INS_FENCE_SHIFT) ++st[GG_IOCOOM_EXPLICIT_FENCES];
+        st[GG_IOCOOM_INTRA_L1D_STALL_PS] += rmr_e - lqr;
+        st[GG_IOCOOM_INTRA_EXEC_STALL_PS] += wor_e - rmr_e;
+        st[GG_IOCOOM_STORE_QUEUE_STALL_PS] += sqr_e - wor_e;
+        curr = sqr_e;
+        st[GG_IOCOOM_IMPLICIT_MFENCES] += (ops / GG_INS_ATOMIC) & 1u;   // core_model.cc:221-235
+        st[GG_IOCOOM_EXPLICIT_FENCES] += ((ops >> GG_INS_FENCE_SHIFT) + 3u) >> 2;   // kind 1-3 -> 1
       }
     }
   }
