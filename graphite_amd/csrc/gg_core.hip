@@ -151,6 +151,7 @@ struct IoCore {
   uint64_t lsb;                   // LoadQueue::_scoreboard[ln]
   uint64_t ssb, sad;              // StoreQueue::_scoreboard[ln], _addresses[ln]
   uint32_t ln_q, sn_q, lidx, sidx;
+  uint64_t sq_lanes;               // the store buffer's lanes (< sn_q) as a wave mask
   bool spec, rfo;
   uint64_t one;
 
@@ -185,7 +186,11 @@ struct IoCore {
   // executeLoad (:140-153) with StoreQueue::isAddressAvailable (:296-309)
   __device__ __forceinline__ uint64_t load(uint64_t schedule, uint64_t a, uint64_t latency, uint64_t& completion)
   {
-    if (__builtin_amdgcn_ballot_w64(ln < sn_q && sad == a && ssb >= schedule)) { completion = schedule + one; return schedule; }
+    // (one ballot per compare: their masks combine on the scalar unit)
+    if (__builtin_amdgcn_ballot_w64(sad == a) & __builtin_amdgcn_ballot_w64(ssb >= schedule) & sq_lanes) {
+      completion = schedule + one;
+      return schedule;
+    }
     return lq_execute(schedule, latency + one, completion);
   }
   // executeStore (:155-165) + StoreQueue::execute (:250-284)
@@ -245,6 +250,7 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
   c.sb = u64x8{0, 0, 0, 0, 0, 0, 0, 0};
   c.lsb = 0; c.ssb = 0; c.sad = ~0ull;                              // INVALID_ADDRESS (fixed_types.h:36)
   c.ln_q = p.num_load_queue_entries; c.sn_q = p.num_store_queue_entries; c.lidx = 0; c.sidx = 0;
+  c.sq_lanes = __builtin_amdgcn_ballot_w64(ln < c.sn_q);
   c.spec = p.speculative_loads_enabled != 0; c.rfo = p.multiple_outstanding_RFOs_enabled != 0;
   c.one = gg::lat_to_ps(1, f);
   uint64_t st[GG_NUM_IOCOOM_STATS];
