@@ -152,6 +152,8 @@ struct IoCore {
   uint64_t ssb, sad;              // StoreQueue::_scoreboard[ln], _addresses[ln]
   uint32_t ln_q, sn_q, lidx, sidx;
   uint64_t sq_lanes;               // the store buffer's lanes (< sn_q) as a wave mask
+  uint64_t l_last, s_last;        // the entries at prev(lidx) / prev(sidx): the last ones written
+                                  // (rings written in order), kept on the scalar unit
   bool spec, rfo;
   uint64_t one;
 
@@ -169,17 +171,16 @@ struct IoCore {
   }
   // the queues' ring indices wrap by a compare, not a modulo (a scalar
   // division is a long VALU sequence on the instruction's chain)
-  __device__ __forceinline__ static uint32_t prev_of(uint32_t i, uint32_t n) { return i ? i - 1 : n - 1; }
   __device__ __forceinline__ static uint32_t next_of(uint32_t i, uint32_t n) { return i + 1 == n ? 0u : i + 1; }
   // LoadQueue::execute (:182-208): the allocate time, *completion
   __device__ __forceinline__ uint64_t lq_execute(uint64_t schedule, uint64_t lat, uint64_t& completion)
   {
-    const uint32_t last = prev_of(lidx, ln_q);
-    const uint64_t allocate = umax64(rl64(lsb, lidx), schedule), lastd = rl64(lsb, last);
+    const uint64_t allocate = umax64(rl64(lsb, lidx), schedule), lastd = l_last;
     uint64_t dealloc;
     if (spec) { completion = allocate + lat; dealloc = umax64(completion, lastd + one); }
     else { completion = umax64(lastd, schedule) + lat; dealloc = completion; }
     if (ln == lidx) lsb = dealloc;
+    l_last = dealloc;
     lidx = next_of(lidx, ln_q);
     return allocate;
   }
@@ -197,12 +198,13 @@ struct IoCore {
   __device__ __forceinline__ uint64_t store(uint64_t schedule, uint64_t a, uint64_t latency)
   {
     const uint64_t lat = latency + one;
-    const uint64_t last_load = rl64(lsb, prev_of(lidx, ln_q));
+    const uint64_t last_load = l_last;
     const uint64_t allocate = umax64(rl64(ssb, sidx), schedule);
-    const uint64_t last_store = rl64(ssb, prev_of(sidx, sn_q));
+    const uint64_t last_store = s_last;
     const uint64_t dealloc = rfo ? umax64(umax64(allocate + lat, last_store + one), last_load)
                                  : umax64(umax64(schedule, last_store), last_load) + lat;
     if (ln == sidx) { ssb = dealloc; sad = a; }
+    s_last = dealloc;
     sidx = next_of(sidx, sn_q);
     return allocate;
   }
@@ -251,6 +253,7 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
   c.lsb = 0; c.ssb = 0; c.sad = ~0ull;                              // INVALID_ADDRESS (fixed_types.h:36)
   c.ln_q = p.num_load_queue_entries; c.sn_q = p.num_store_queue_entries; c.lidx = 0; c.sidx = 0;
   c.sq_lanes = __builtin_amdgcn_ballot_w64(ln < c.sn_q);
+  c.l_last = 0; c.s_last = 0;
   c.spec = p.speculative_loads_enabled != 0; c.rfo = p.multiple_outstanding_RFOs_enabled != 0;
   c.one = gg::lat_to_ps(1, f);
   uint64_t st[GG_NUM_IOCOOM_STATS];
