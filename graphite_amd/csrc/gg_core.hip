@@ -220,11 +220,21 @@ struct IoAcc {
   const uint64_t* __restrict__ lat;
   uint32_t n, ln, base = 0, m = 0;
   uint64_t a = 0, l = 0;
+  // Per-lane tallies of the windows, summed over the wave at the end: the
+  // windows tile [0, n) exactly (k advances by one per access) and a run
+  // with k == n at its end consumed every access, a BARRIER by a
+  // SyncInstruction and any other by a memory operand (else `bad`), so the
+  // access-side statistics need no scalar work per instruction.
+  uint64_t d_lat = 0, s_lat = 0;                  // data / SyncInstruction latency sums
+  uint32_t d_cnt = 0, s_cnt = 0, s_zero = 0;      // data accesses, stalls != 0, stalls == 0
   __device__ __forceinline__ void load(uint32_t b)
   {
     base = b;
     const uint32_t i = b + ln;
     a = i < n ? addr[i] : 0; m = i < n ? meta[i] : 0; l = i < n ? lat[i] : 0;
+    const bool bar = m == GG_META_BARRIER, in = i < n;
+    d_lat += in && !bar ? l : 0; d_cnt += in && !bar ? 1u : 0u;
+    s_lat += bar ? l : 0; s_cnt += bar && l ? 1u : 0u; s_zero += bar && !l ? 1u : 0u;
   }
   __device__ __forceinline__ void get(uint32_t k, uint64_t& A, uint32_t& M, uint64_t& L)
   {
@@ -296,13 +306,8 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
         uint64_t A, L; uint32_t M;
         next_access(A, M, L);
         bad |= is_barrier(M) ^ 1u;
-        const uint64_t one_if = L ? 1u : 0u;                          // a zero stall is no instruction
-        st[GG_IOCOOM_INSTRUCTIONS] += one_if;
-        st[GG_IOCOOM_SYNC_INSTRUCTIONS] += one_if;
-        curr += L;
-        st[GG_IOCOOM_SYNC_STALL_PS] += L;
+        curr += L;                                                    // (its counts: the window tallies)
       } else {
-        ++st[GG_IOCOOM_INSTRUCTIONS];                                 // :72
         const uint64_t cost = gg::lat_to_ps(w0 & 0xFFFFu, f);            // getCost (:70)
         const uint64_t ready = curr;                                  // no L1-I (:78-87)
         const uint32_t nr = regs & 7u, nw = (regs >> 3) & 7u;
@@ -334,7 +339,6 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
           bad |= M & GG_META_WRITE;                                   // a write or a BARRIER (all ones)
           uint64_t comp;
           const uint64_t alloc = c.load(rr, A, L, comp);
-          ++st[GG_IOCOOM_DATA_ACCESSES]; st[GG_IOCOOM_DATA_LATENCY_PS] += L;
           lqr = umax64(lqr, alloc); rmr = umax64(rmr, comp);
         }
         const uint64_t wor = rmr + cost;                              // :158-166
@@ -353,7 +357,6 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
           next_access(A, M, L);
           bad |= ((M & GG_META_WRITE) ^ 1u) | is_barrier(M);
           sqr = umax64(sqr, c.store(wor, A, L));
-          ++st[GG_IOCOOM_DATA_ACCESSES]; st[GG_IOCOOM_DATA_LATENCY_PS] += L;
         }
         // :209-252; the memory / execution stall totals (core_model.cc:260-264)
         // are the sums of these parts, formed once after the loop
@@ -373,6 +376,18 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
     }
   }
   if (k != k1) bad = 1;
+  // :72 (a SyncInstruction of zero stall is no instruction), :74-79, the
+  // data operands: the window tallies summed over the wave
+  auto wsum = [](uint64_t v) {
+#pragma unroll
+    for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+  };
+  st[GG_IOCOOM_INSTRUCTIONS] = ni - wsum(acc.s_zero);
+  st[GG_IOCOOM_SYNC_INSTRUCTIONS] = wsum(acc.s_cnt);
+  st[GG_IOCOOM_SYNC_STALL_PS] = wsum(acc.s_lat);
+  st[GG_IOCOOM_DATA_ACCESSES] = wsum(acc.d_cnt);
+  st[GG_IOCOOM_DATA_LATENCY_PS] = wsum(acc.d_lat);
   st[GG_IOCOOM_TIME_PS] = curr;
   st[GG_IOCOOM_MEMORY_STALL_PS] = st[GG_IOCOOM_INTER_L1D_STALL_PS] + st[GG_IOCOOM_LOAD_QUEUE_STALL_PS] +
                                   st[GG_IOCOOM_INTRA_L1D_STALL_PS] + st[GG_IOCOOM_STORE_QUEUE_STALL_PS];
