@@ -278,6 +278,7 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
   uint32_t k = 0;
   uint64_t curr = 0;
   uint32_t bad = 0;                 // (a word, not a bool: the compiler kept a bool in a VGPR)
+  uint64_t sum_ready = 0, sum_re = 0, sum_rr = 0, sum_lqr = 0, sum_rmr = 0, sum_wor = 0, n_atomic = 0, n_fence = 0;
   for (uint32_t b = 0; b < ni && !bad; b += 64) {
     const uint4 w = b + ln < ni ? tins[b + ln] : make_uint4(0, 0, 0, 0);
     const uint32_t cnt = ni - b < 64 ? ni - b : 64u;
@@ -285,6 +286,12 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
     // instruction runs on (register indices masked, accesses past the stream
     // read as zeros, stream indices never wrap), so the body is straight-line
     // scalar code; `bad` ends the walk at the window's end.
+    {                                       // the window's fences (core_model.cc:221-235), lane-parallel
+      const uint32_t ops = (w.x >> 16) & 0xFFu;
+      const bool real = b + ln < ni && !((w.x >> 24) & GG_INS_SYNC);
+      n_atomic += __builtin_popcountll(__builtin_amdgcn_ballot_w64(real && (ops & GG_INS_ATOMIC)));
+      n_fence += __builtin_popcountll(__builtin_amdgcn_ballot_w64(real && (ops >> GG_INS_FENCE_SHIFT)));
+    }
     for (uint32_t j = 0; j < cnt; ++j) {
       const uint32_t w0 = (uint32_t)__builtin_amdgcn_readlane((int)w.x, (int)j);
       // the register operands as a queue: reads, then writes, 16 bits each
@@ -363,15 +370,11 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
         // (selects: a simple-mov load stops at lqr, a store-free one at rmr)
         const bool st_on = !smov && nwm;
         const uint64_t rmr_e = smov ? lqr : rmr, wor_e = st_on ? wor : rmr_e, sqr_e = st_on ? sqr : wor_e;
-        st[GG_IOCOOM_INTER_EXEC_STALL_PS] += re - ready;
-        st[GG_IOCOOM_INTER_L1D_STALL_PS] += rr - re;
-        st[GG_IOCOOM_LOAD_QUEUE_STALL_PS] += lqr - rr;
-        st[GG_IOCOOM_INTRA_L1D_STALL_PS] += rmr_e - lqr;
-        st[GG_IOCOOM_INTRA_EXEC_STALL_PS] += wor_e - rmr_e;
-        st[GG_IOCOOM_STORE_QUEUE_STALL_PS] += sqr_e - wor_e;
+        // the six stall parts are differences of the chain ready <= re <=
+        // rr <= lqr <= rmr_e <= wor_e <= sqr_e: sums of its links (mod 2^64,
+        // exact for the differences), the last one from curr at the end
+        sum_ready += ready; sum_re += re; sum_rr += rr; sum_lqr += lqr; sum_rmr += rmr_e; sum_wor += wor_e;
         curr = sqr_e;
-        st[GG_IOCOOM_IMPLICIT_MFENCES] += (ops / GG_INS_ATOMIC) & 1u;   // core_model.cc:221-235
-        st[GG_IOCOOM_EXPLICIT_FENCES] += ((ops >> GG_INS_FENCE_SHIFT) + 3u) >> 2;   // kind 1-3 -> 1
       }
     }
   }
@@ -388,6 +391,15 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
   st[GG_IOCOOM_SYNC_STALL_PS] = wsum(acc.s_lat);
   st[GG_IOCOOM_DATA_ACCESSES] = wsum(acc.d_cnt);
   st[GG_IOCOOM_DATA_LATENCY_PS] = wsum(acc.d_lat);
+  const uint64_t sum_sqr = sum_ready + (curr - st[GG_IOCOOM_SYNC_STALL_PS]);   // curr = the links + the syncs' stalls
+  st[GG_IOCOOM_INTER_EXEC_STALL_PS] = sum_re - sum_ready;                    // :209-252
+  st[GG_IOCOOM_INTER_L1D_STALL_PS] = sum_rr - sum_re;
+  st[GG_IOCOOM_LOAD_QUEUE_STALL_PS] = sum_lqr - sum_rr;
+  st[GG_IOCOOM_INTRA_L1D_STALL_PS] = sum_rmr - sum_lqr;
+  st[GG_IOCOOM_INTRA_EXEC_STALL_PS] = sum_wor - sum_rmr;
+  st[GG_IOCOOM_STORE_QUEUE_STALL_PS] = sum_sqr - sum_wor;
+  st[GG_IOCOOM_IMPLICIT_MFENCES] = n_atomic;
+  st[GG_IOCOOM_EXPLICIT_FENCES] = n_fence;
   st[GG_IOCOOM_TIME_PS] = curr;
   st[GG_IOCOOM_MEMORY_STALL_PS] = st[GG_IOCOOM_INTER_L1D_STALL_PS] + st[GG_IOCOOM_LOAD_QUEUE_STALL_PS] +
                                   st[GG_IOCOOM_INTRA_L1D_STALL_PS] + st[GG_IOCOOM_STORE_QUEUE_STALL_PS];
