@@ -762,8 +762,11 @@ enum {
  * acc_tile_offsets[num_tiles + 1]) from the model's constructor state.  A
  * memory read operand met by a write access (or the reverse), a SYNC met by
  * a non-BARRIER access, a register >= 512, a tile whose instructions leave
- * accesses unconsumed or run out of them: the run's error, reported by
- * gg_iocoom_get_stats (GG_ERR_STATE).  Asynchronous on stream.               */
+ * accesses unconsumed or run out of them, a register time of 2^62 ps or more
+ * (the scoreboard keeps the unit in an entry's top two bits): the run's
+ * error, reported by gg_iocoom_get_stats (GG_ERR_STATE).  GG_ERR_RANGE up
+ * front for a tile of more than 2^31 instructions or accesses.
+ * Asynchronous on stream.                                                    */
 gg_status gg_iocoom_run(gg_ctx* ctx, const gg_iocoom_params* params, const gg_ins* ins_dev,
                         const uint64_t* ins_tile_offsets, const uint64_t* acc_addr_dev, const uint32_t* acc_meta_dev,
                         const uint64_t* acc_lat_dev, const uint64_t* acc_tile_offsets, void* stream);
