@@ -285,12 +285,19 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
     // No early exit inside a window: a failed check sets `bad` and the
     // instruction runs on (register indices masked, accesses past the stream
     // read as zeros, stream indices never wrap), so the body is straight-line
-    // scalar code; `bad` ends the walk at the window's end.
-    {                                       // the window's fences (core_model.cc:221-235), lane-parallel
-      const uint32_t ops = (w.x >> 16) & 0xFFu;
-      const bool real = b + ln < ni && !((w.x >> 24) & GG_INS_SYNC);
+    // scalar code; `bad` ends the walk at the window's end.  The operand
+    // checks run over the window's 64 instructions at once, before the walk.
+    {                                       // lane-parallel over the window: one instruction per lane
+      const uint32_t ops = (w.x >> 16) & 0xFFu, regs = w.x >> 24;
+      const bool real = b + ln < ni && !(regs & GG_INS_SYNC);
+      // the fences (core_model.cc:221-235)
       n_atomic += __builtin_popcountll(__builtin_amdgcn_ballot_w64(real && (ops & GG_INS_ATOMIC)));
       n_fence += __builtin_popcountll(__builtin_amdgcn_ballot_w64(real && (ops >> GG_INS_FENCE_SHIFT)));
+      // the operand checks: at most six register operands, each < 512
+      const uint32_t no = (regs & 7u) + ((regs >> 3) & 7u);
+      const bool badl = no > 6 || (no > 0 && (w.y & 0xFE00u)) || (no > 1 && (w.y >> 25)) || (no > 2 && (w.z & 0xFE00u)) ||
+                        (no > 3 && (w.z >> 25)) || (no > 4 && (w.w & 0xFE00u)) || (no > 5 && (w.w >> 25));
+      bad |= __builtin_amdgcn_ballot_w64(real && badl) ? 1u : 0u;
     }
     for (uint32_t j = 0; j < cnt; ++j) {
       const uint32_t w0 = (uint32_t)__builtin_amdgcn_readlane((int)w.x, (int)j);
@@ -304,10 +311,8 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
         return r;
       };
       auto next_access = [&](uint64_t& A, uint32_t& M, uint64_t& L) {
-        bad |= (uint32_t)(int32_t)(k1 - 1u - k) >> 31;                // k >= k1 (both < 2^31)
-        acc.get(k, A, M, L);
-        k += k < k1 ? 1u : 0u;
-      };
+        acc.get(k++, A, M, L);        // past the stream: zeros, and k != k1 at the end (k < 2^32:
+      };                              // at most 6 accesses per instruction, 2^28 instructions)
       const uint32_t ops = (w0 >> 16) & 0xFFu, regs = w0 >> 24;
       if (regs & GG_INS_SYNC) {                                       // dynamic (:74-79)
         uint64_t A, L; uint32_t M;
@@ -318,9 +323,6 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
         const uint64_t cost = gg::lat_to_ps(w0 & 0xFFFFu, f);            // getCost (:70)
         const uint64_t ready = curr;                                  // no L1-I (:78-87)
         const uint32_t nr = regs & 7u, nw = (regs >> 3) & 7u;
-        uint32_t nrw = nr + nw;
-        asm("" : "+s"(nrw));                // (opaque: else folded back into a compare widened by the VALU)
-        bad |= (6u - nrw) >> 31;                                      // nr + nw > 6
         // :100-125, as selects (no branch per operand).  An entry's unit is
         // LOAD (1) or EXECUTION (3) once written and INVALID (0) only with
         // time 0, which no maximum below can take: the top bit picks the
@@ -328,7 +330,6 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
         uint64_t rl = ready, re = ready;
         for (uint32_t i = 0; i < nr; ++i) {
           const uint32_t r = reg();
-          bad |= r >> 9;                                              // >= GG_IOCOOM_NUM_REGISTERS
           uint32_t hi, lo;
           c.reg_entry(r & (GG_IOCOOM_NUM_REGISTERS - 1), hi, lo);
           uint32_t hs = hi;
@@ -354,7 +355,6 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
         bad |= (uint32_t)(wor >> 62);
         for (uint32_t i = 0; i < nw; ++i) {                           // :172-184
           const uint32_t r = reg();
-          bad |= r >> 9;
           c.reg_write(r & (GG_IOCOOM_NUM_REGISTERS - 1), went);
         }
         uint64_t sqr = wor;                                           // :186-201
@@ -496,9 +496,10 @@ gg_status gg_iocoom_run(gg_ctx* ctx, const gg_iocoom_params* params, const gg_in
   for (const uint64_t* o : {ins_tile_offsets, acc_tile_offsets})
     for (uint32_t t = 0; t < T; ++t)
       if (o[t + 1] < o[t]) return gg_fail(GG_ERR_INVALID, "gg_iocoom_run: tile offsets decrease");
-      else if (o[t + 1] - o[t] > (1ull << 31))   // the kernel's tile-relative indices are 32-bit
-        return gg_fail(GG_ERR_RANGE, "gg_iocoom_run: tile %u has %llu instructions or accesses (at most 2^31)", t,
-                       (unsigned long long)(o[t + 1] - o[t]));
+      else if (o[t + 1] - o[t] > (o == ins_tile_offsets ? 1ull << 28 : 1ull << 31))   // 32-bit tile-relative indices
+        return gg_fail(GG_ERR_RANGE, "gg_iocoom_run: tile %u has %llu %s (at most 2^%d)", t,
+                       (unsigned long long)(o[t + 1] - o[t]), o == ins_tile_offsets ? "instructions" : "accesses",
+                       o == ins_tile_offsets ? 28 : 31);
   if (ins_tile_offsets[T] > ins_tile_offsets[0] && !ins_dev) return gg_fail(GG_ERR_INVALID, "gg_iocoom_run: NULL instructions");
   if (acc_tile_offsets[T] > acc_tile_offsets[0] && (!acc_addr_dev || !acc_meta_dev || !acc_lat_dev))
     return gg_fail(GG_ERR_INVALID, "gg_iocoom_run: NULL access stream");
