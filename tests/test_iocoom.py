@@ -329,6 +329,18 @@ def test_gpu_iocoom_errors():
     with pytest.raises(B.GGError):
         run(ins, big)
     run(ins, lat)                                            # the context recovers
+    for d in (-1, 1):                                        # the last tile runs out of accesses / leaves one
+        ao2 = ao.copy()
+        ao2[-1] = ao2[-1] + np.uint64(d) if d > 0 else ao2[-1] - np.uint64(1)
+        n2 = int(ao2[-1])
+        a2, m2, l2 = (np.resize(x, n2) for x in (addr, meta, lat))
+        if d > 0:
+            m2[-1] = 0                                       # an extra read access
+        be.iocoom_run(C.IocoomParams(), torch.from_numpy(ins.view(np.uint8).copy()).cuda(), io,
+                      to_dev(torch, a2, torch.int64), to_dev(torch, m2, torch.int32), to_dev(torch, l2, torch.int64), ao2)
+        with pytest.raises(B.GGError):
+            be.iocoom_stats()
+    run(ins, lat)
     with pytest.raises(B.GGError):
         be.iocoom_run(C.IocoomParams(65, 8), torch.from_numpy(ins.view(np.uint8).copy()).cuda(), io,
                       to_dev(torch, addr, torch.int64), to_dev(torch, meta, torch.int32),
