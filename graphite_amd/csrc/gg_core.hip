@@ -244,6 +244,9 @@ struct IoAcc {
   }
 };
 
+// F1: the clock is 1 GHz, an instruction's cost is 1000 ps per cycle (the
+// exact integer form of lat_to_ps, without its per-call test)
+template <bool F1>
 __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restrict__ ins, const uint64_t* __restrict__ offs,
                                                           const uint64_t* __restrict__ addr,
                                                           const uint32_t* __restrict__ meta,
@@ -320,7 +323,7 @@ __global__ void __launch_bounds__(64 * kIoWaves) k_iocoom(const uint4* __restric
         bad |= is_barrier(M) ^ 1u;
         curr += L;                                                    // (its counts: the window tallies)
       } else {
-        const uint64_t cost = gg::lat_to_ps(w0 & 0xFFFFu, f);            // getCost (:70)
+        const uint64_t cost = F1 ? 1000ull * (w0 & 0xFFFFu) : gg::lat_to_ps(w0 & 0xFFFFu, f);   // getCost (:70)
         const uint64_t ready = curr;                                  // no L1-I (:78-87)
         const uint32_t nr = regs & 7u, nw = (regs >> 3) & 7u;
         // :100-125, as selects (no branch per operand).  An entry's unit is
@@ -520,7 +523,8 @@ gg_status gg_iocoom_run(gg_ctx* ctx, const gg_iocoom_params* params, const gg_in
   GG_HIP(hipMemsetAsync(ctx->io_err, 0, sizeof(uint32_t), s));
   if (T) {
     gg_timer_begin(ctx, "iocoom", s);
-    hipLaunchKernelGGL(k_iocoom, dim3((T + kIoWaves - 1) / kIoWaves), dim3(64 * kIoWaves), 0, s,
+    hipLaunchKernelGGL(ctx->cfg.frequency_ghz == 1.0 ? k_iocoom<true> : k_iocoom<false>, dim3((T + kIoWaves - 1) / kIoWaves),
+                       dim3(64 * kIoWaves), 0, s,
                        reinterpret_cast<const uint4*>(ins_dev), (const uint64_t*)ctx->io_offs, acc_addr_dev,
                        acc_meta_dev, acc_lat_dev, T, p, ctx->cfg.frequency_ghz, ctx->io_stats, ctx->io_err);
     GG_HIP(hipGetLastError());
