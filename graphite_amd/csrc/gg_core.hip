@@ -110,7 +110,7 @@ __global__ void __launch_bounds__(64 * kCoreWaves) k_core_model(const uint32_t* 
 // readlanes; the store buffer's address match (isAddressAvailable) is one
 // ballot.  Instructions of one tile are strictly serial (curr_time and the
 // scoreboard): the parallelism is across tiles.
-constexpr uint32_t kIoWaves = 4;
+constexpr uint32_t kIoWaves = 1;   // one-wave blocks: 1.4 % faster than 4, 2 puts two tiles on some SIMDs (-25 %)
 enum : uint32_t { kUnitInvalid = 0, kUnitLoad = 1, kUnitExec = 3 };   // CoreUnit (iocoom_core_model.h:14-20)
 
 __device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l)
